@@ -1,0 +1,142 @@
+"""TEST INFRASTRUCTURE ONLY -- CPU oracle for the UCLA-ROMS hot path.
+
+ctypes binding of oracle/liboracle.so (plain-C restatement, see
+roms_oracle.h).  Only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg may import this package.  Parity pinned against the
+reference golden log tests/Filament/benchmark.result_github_gnu.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "liboracle.so")
+CASE_FILAMENT, CASE_BASIN = 0, 1
+
+
+class OrCfg(ctypes.Structure):
+    _fields_ = [("LLm", ctypes.c_int), ("MMm", ctypes.c_int), ("N", ctypes.c_int), ("NT", ctypes.c_int),
+                ("ew_periodic", ctypes.c_int), ("ns_periodic", ctypes.c_int),
+                ("salinity", ctypes.c_int), ("nonlin_eos", ctypes.c_int), ("lmd", ctypes.c_int),
+                ("case_id", ctypes.c_int), ("ntimes", ctypes.c_int),
+                ("dt", ctypes.c_double), ("ndtfast", ctypes.c_int),
+                ("theta_s", ctypes.c_double), ("theta_b", ctypes.c_double), ("hc", ctypes.c_double),
+                ("rho0", ctypes.c_double), ("visc2", ctypes.c_double), ("tnu2", ctypes.c_double),
+                ("rdrg", ctypes.c_double), ("rdrg2", ctypes.c_double), ("Zob", ctypes.c_double),
+                ("Akv_bak", ctypes.c_double), ("Akt_bak", ctypes.c_double * 2),
+                ("Tcoef", ctypes.c_double), ("T0", ctypes.c_double), ("Scoef", ctypes.c_double),
+                ("S0", ctypes.c_double), ("sizex", ctypes.c_double), ("sizey", ctypes.c_double),
+                ("diag_np_xi", ctypes.c_int), ("diag_np_eta", ctypes.c_int)]
+
+
+def build():
+    """Compile liboracle.so with the committed Makefile (gcc, -ffp-contract=off)."""
+    subprocess.run(["make", "-s", "-C", _HERE, "liboracle.so"], check=True)
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB):
+            build()
+        L = ctypes.CDLL(_LIB)
+        L.or_create.restype = ctypes.c_void_p
+        L.or_create.argtypes = [ctypes.POINTER(OrCfg)]
+        for fn in ("or_init", "or_step"):
+            getattr(L, fn).argtypes = [ctypes.c_void_p]
+            getattr(L, fn).restype = ctypes.c_int
+        L.or_norms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]
+        L.or_field.restype = ctypes.POINTER(ctypes.c_double)
+        L.or_field.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_size_t)]
+        L.or_iic.argtypes = [ctypes.c_void_p]
+        L.or_nfast.argtypes = [ctypes.c_void_p]
+        L.or_weights.argtypes = [ctypes.c_void_p]
+        L.or_weights.restype = ctypes.POINTER(ctypes.c_double)
+        L.or_tindex.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
+        L.or_set_tindex.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
+        L.or_destroy.argtypes = [ctypes.c_void_p]
+        for fn in ("or_set_HUV", "or_omega", "or_prsgrd", "or_pre_step3d", "or_set_HUV1", "or_step3d_uv1",
+                   "or_visc3d", "or_step2d", "or_step3d_uv2", "or_step3d_t", "or_t3dmix", "or_set_depth",
+                   "or_diag"):
+            getattr(L, fn).argtypes = [ctypes.c_void_p]
+        L.or_rho_eos.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.or_set_iif.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        _lib = L
+    return _lib
+
+
+def filament_cfg(LLm=64, MMm=64, N=32, NT=1, salinity=False, sizex=12.8e3, sizey=3.2e3, np_xi=3, np_eta=2):
+    """tests/Filament/{param.opt,benchmark.in,cppdefs.opt} of the reference."""
+    c = OrCfg()
+    c.LLm, c.MMm, c.N, c.NT = LLm, MMm, N, NT
+    c.ew_periodic = c.ns_periodic = 1
+    c.salinity = int(salinity)
+    c.case_id = CASE_FILAMENT
+    c.dt, c.ndtfast = 5.0, 60
+    c.theta_s, c.theta_b, c.hc, c.rho0 = 6.0, 2.0, 25.0, 1000.0
+    c.rdrg, c.rdrg2, c.Zob = 0.0, 1.0e-3, 1.0e-2
+    c.Tcoef, c.T0, c.Scoef, c.S0 = 0.20, 1.0, 0.822, 1.0
+    c.sizex, c.sizey = sizex, sizey
+    c.diag_np_xi, c.diag_np_eta = np_xi, np_eta
+    return c
+
+
+class Oracle:
+    """One CPU model instance; field() returns Fortran-ordered numpy views."""
+
+    def __init__(self, cfg):
+        self.cfg = cfg
+        self.L = lib()
+        self.h = self.L.or_create(ctypes.byref(cfg))
+        self.nx2, self.ny2 = cfg.LLm + 4, cfg.MMm + 4
+
+    def init(self):
+        self.L.or_init(self.h)
+
+    def step(self, n=1):
+        for _ in range(n):
+            self.L.or_step(self.h)
+
+    def norms(self):
+        out = (ctypes.c_double * 4)()
+        self.L.or_norms(self.h, out)
+        return list(out)
+
+    def field(self, name):
+        cnt = ctypes.c_size_t()
+        p = self.L.or_field(self.h, name.encode(), ctypes.byref(cnt))
+        if not p:
+            raise KeyError(name)
+        a = np.ctypeslib.as_array(p, shape=(cnt.value,))
+        n2 = self.nx2 * self.ny2
+        return a.reshape((cnt.value // n2, self.ny2, self.nx2)) if cnt.value % n2 == 0 else a
+
+    def tindex(self):
+        out = (ctypes.c_int * 6)()
+        self.L.or_tindex(self.h, out)
+        return list(out)
+
+    def set_tindex(self, t):
+        self.L.or_set_tindex(self.h, (ctypes.c_int * 6)(*t))
+
+    def nfast(self):
+        return self.L.or_nfast(self.h)
+
+    def weights(self):
+        p = self.L.or_weights(self.h)
+        w = np.ctypeslib.as_array(p, shape=(2 * 288,)).reshape(2, 288)
+        return w.copy()
+
+    def call(self, routine, *args):
+        getattr(self.L, "or_" + routine)(self.h, *args)
+
+    def __del__(self):
+        try:
+            self.L.or_destroy(self.h)
+        except Exception:
+            pass

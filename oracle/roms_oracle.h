@@ -1,0 +1,88 @@
+/*
+ * roms_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement (plain C99, FP64, no FMA contraction) of the UCLA-ROMS
+ * split-explicit time step, used exclusively as the parity checker for the
+ * MI355X HIP path (tests/, __graft_entry__.smoke(), bench.py cpu_baseline).
+ * Nothing in the product links or loads this library.
+ *
+ * Pinning: the restatement reproduces the reference's own golden log
+ * tests/Filament/benchmark.result_github_gnu (per-step KINETIC_ENRG,
+ * BAROTR_KE, MAX_ADV_CFL, MAX_VERT_CFL) -- see tests/test_oracle_golden.py.
+ *
+ * The state layout is the reference's Fortran layout: every horizontal
+ * array is (-1:Lm+2, -1:Mm+2), i fastest; rho-point 3-D arrays add (1:N),
+ * w-point arrays (0:N); u,v carry 3 time levels, zeta/ubar/vbar 4,
+ * t(:,:,:,3,NT).  (/root/reference/src/ocean_vars.F:68-116, tracers.F:327)
+ */
+#ifndef ROMS_ORACLE_H
+#define ROMS_ORACLE_H
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* analytic case selector */
+enum { OR_CASE_FILAMENT = 0, OR_CASE_BASIN = 1 };
+
+typedef struct or_cfg {
+  int LLm, MMm, N, NT;           /* interior dims, tracers (T[,S,passive]) */
+  int ew_periodic, ns_periodic;
+  int salinity, nonlin_eos;      /* nonlin_eos implies SPLIT_EOS */
+  int lmd;                       /* LMD_MIXING+KPP+BKPP+RIMIX+CONVEC+NONLOCAL */
+  int case_id;
+  int ntimes;
+  double dt; int ndtfast;
+  double theta_s, theta_b, hc, rho0;
+  double visc2, tnu2;
+  double rdrg, rdrg2, Zob;
+  double Akv_bak, Akt_bak[2];
+  double Tcoef, T0, Scoef, S0;
+  double sizex, sizey;           /* analytic domain size [m] */
+  int diag_np_xi, diag_np_eta;   /* rank layout emulated in diag sums */
+} or_cfg;
+
+typedef struct or_state or_state;
+
+or_state *or_create(const or_cfg *cfg);
+void      or_destroy(or_state *S);
+/* roms_init (main.F:85-321) : grid, ICs, set_depth, set_HUV, omega, rho_eos, diag */
+int       or_init(or_state *S);
+/* one roms_step (main.F:333-520); returns 0 */
+int       or_step(or_state *S);
+
+/* norms printed by diag (diag.F code_check line) for the last diag call */
+void      or_norms(const or_state *S, double out[4]);
+int       or_iic(const or_state *S);
+int       or_nfast(const or_state *S);
+const double *or_weights(const or_state *S); /* weight(2,nfast), column-major */
+
+/* field access: returns pointer + element count of a named array */
+double   *or_field(or_state *S, const char *name, size_t *count);
+/* scalar time indices: iic kstp knew nstp nrhs nnew */
+void      or_tindex(const or_state *S, int out[6]);
+
+/* individual routines (same names as the reference), for per-routine parity */
+void or_rho_eos(or_state *S, int tidx);
+void or_set_HUV(or_state *S);
+void or_omega(or_state *S);
+void or_prsgrd(or_state *S);
+void or_pre_step3d(or_state *S);
+void or_set_HUV1(or_state *S);
+void or_step3d_uv1(or_state *S);
+void or_visc3d(or_state *S);
+void or_step2d(or_state *S);
+void or_step3d_uv2(or_state *S);
+void or_step3d_t(or_state *S);
+void or_t3dmix(or_state *S);
+void or_set_depth(or_state *S);
+void or_lmd_vmix(or_state *S, int tind);
+void or_diag(or_state *S);
+void or_set_tindex(or_state *S, const int in[6]);
+void or_set_iif(or_state *S, int iif);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
