@@ -1,0 +1,149 @@
+/*
+ * roms_gpu.h -- C ABI of the MI355X-native UCLA-ROMS split-explicit hot path.
+ *
+ * Drop-in boundary: the reference's hot-path
+ * routines are argument-less / (tile) / (tidx) external Fortran subroutines
+ * that read and write module arrays (/root/reference/src/main.F:397-479).
+ * Each routine below replaces one of them; all state they touch lives in
+ * device memory owned by this library, in the reference's Fortran layout
+ * (-1:Lm+2, -1:Mm+2 [,levels] [,time] [,tracer]), i fastest.  Host arrays are
+ * borrowed only across roms_gpu_register .. roms_gpu_finalize and are copied
+ * explicitly with roms_gpu_upload / roms_gpu_download.
+ *
+ * One process drives one GPU (one MPI rank / one subdomain, like the
+ * reference's one rank per tile).  Every entry returns 0 on success and a
+ * negative code on failure; roms_gpu_last_error() gives the message (the
+ * reference's error_log%raise_* + abort_check, error_handling_mod.F90:144-365).
+ * Routine entries enqueue on the library's HIP stream and return immediately;
+ * roms_gpu_sync() waits.
+ */
+#ifndef ROMS_GPU_H
+#define ROMS_GPU_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ROMS_GPU_ABI_VERSION 1
+#define ROMS_MAX_FAST 288
+
+/* Subdomain geometry of this rank: param.F / dimensions.F / mpi_setup.F:39-210 */
+typedef struct roms_dims {
+  int Lm, Mm, N, NT;             /* local interior size, levels, tracers   */
+  int LLm, MMm;                  /* global interior size                   */
+  int np_xi, np_eta, inode, jnode;
+  int iSW_corn, jSW_corn;        /* offset of this subdomain (mpi_setup.F) */
+  int ew_periodic, ns_periodic;  /* EW_PERIODIC / NS_PERIODIC              */
+  int west_exchng, east_exchng, south_exchng, north_exchng; /* message edges */
+} roms_dims;
+
+/* cppdefs.opt switches and run scalars (scalars.F, read_inp_mod.F, set_weights.F) */
+typedef struct roms_cfg {
+  int nonlin_eos;                /* NONLIN_EOS (+SPLIT_EOS)                */
+  int salinity;                  /* SALINITY                               */
+  int lmd_mixing;                /* LMD_MIXING/KPP/BKPP/RIMIX/CONVEC/NONLOCAL */
+  int uv_vis2, ts_dif2;          /* UV_VIS2, TS_DIF2                        */
+  double dt;                     /* baroclinic step [s]                    */
+  int ndtfast, nfast;            /* mode splitting                         */
+  double weight[2][ROMS_MAX_FAST]; /* fast-time averaging weights (C order [2][288]) */
+  double g, rho0, rdrg, rdrg2, Zob, gamma2;
+  double Akv_bak, Akt_bak[2];
+  double Tcoef, T0, Scoef, S0;   /* linear EOS                              */
+  double theta_s, theta_b, hc;   /* S-coordinate                            */
+} roms_cfg;
+
+/* Time-step indices (scalars.F:32-36).  The step entry updates them. */
+typedef struct roms_tlev {
+  int iic, ntstart, forw_start, iif, nfast, kstp, knew, nstp, nrhs, nnew;
+} roms_tlev;
+
+/* Field identifiers: the reference's module arrays (names as in the source) */
+enum roms_field {
+  ROMS_ALL = -1,
+  /* grid.F */
+  ROMS_h = 0, ROMS_hinv, ROMS_f, ROMS_fomn, ROMS_pm, ROMS_pn, ROMS_dm_r, ROMS_dn_r, ROMS_dm_u, ROMS_dn_u,
+  ROMS_dm_v, ROMS_dn_v, ROMS_dm_p, ROMS_dn_p, ROMS_pmon_u, ROMS_pnom_v, ROMS_rmask, ROMS_pmask, ROMS_umask,
+  ROMS_vmask,
+  /* scoord.F (N+1 each) */
+  ROMS_Cs_w, ROMS_Cs_r,
+  /* ocean_vars.F, tracers.F */
+  ROMS_zeta, ROMS_ubar, ROMS_vbar, ROMS_u, ROMS_v, ROMS_t, ROMS_FlxU, ROMS_FlxV, ROMS_We, ROMS_Wi,
+  ROMS_Hz, ROMS_Hz_u, ROMS_Hz_v, ROMS_z_r, ROMS_z_w,
+  /* coupling.F */
+  ROMS_rufrc, ROMS_rvfrc, ROMS_rhoA, ROMS_rhoS, ROMS_r_D, ROMS_Zt_avg1, ROMS_DU_avg1, ROMS_DV_avg1,
+  ROMS_DU_avg2, ROMS_DV_avg2, ROMS_DU_avg_bak, ROMS_DV_avg_bak,
+  /* eos_vars.F, mixing.F */
+  ROMS_rho, ROMS_rho1, ROMS_qp1, ROMS_bvf, ROMS_Akv, ROMS_Akt, ROMS_visc2_r, ROMS_visc2_p, ROMS_diff2,
+  ROMS_hbls, ROMS_hbbl, ROMS_ghat, ROMS_swr_frac,
+  /* surf_flux.F */
+  ROMS_sustr, ROMS_svstr, ROMS_stflx, ROMS_srflx, ROMS_swflx,
+  /* private scratch carried between routines (prsgrd -> pre_step3d/step3d_uv1) */
+  ROMS_ru, ROMS_rv,
+  ROMS_NFIELDS
+};
+
+/* ---- lifecycle ---- */
+int  roms_gpu_abi_version(void);
+/* Allocates device state (the only allocating entry).  device: HIP device
+ * ordinal; comm: opaque RCCL communicator for multi-rank halo exchange (NULL
+ * for a single rank, whose periodic halos are wrapped on-device).           */
+int  roms_gpu_init(const roms_dims *dims, const roms_cfg *cfg, int device, void *comm);
+int  roms_gpu_finalize(void);
+const char *roms_gpu_last_error(void);
+/* element count of a field in the Fortran layout of this rank */
+long roms_gpu_field_size(int field_id);
+/* host mirror for upload/download (init_arrays.F; host keeps ownership)     */
+int  roms_gpu_register(int field_id, double *host_ptr, long count);
+int  roms_gpu_upload(int field_id);      /* host -> device, ROMS_ALL allowed */
+int  roms_gpu_download(int field_id);    /* device -> host, ROMS_ALL allowed */
+/* direct synchronous copies without registration                            */
+int  roms_gpu_copy_in(int field_id, const double *src, long count);
+int  roms_gpu_copy_out(int field_id, double *dst, long count);
+int  roms_gpu_sync(void);
+void *roms_gpu_stream(void);             /* hipStream_t the routines run on  */
+
+/* ---- hot-path routines (reference entry points they replace) ---- */
+int roms_gpu_rho_eos(int tidx, const roms_tlev *t);   /* rho_eos(tidx)   rho_eos.F:6      */
+int roms_gpu_set_huv(const roms_tlev *t);             /* set_HUV          set_depth.F:190  */
+int roms_gpu_omega(const roms_tlev *t);               /* omega            omega.F:4        */
+int roms_gpu_lmd_vmix(int tind, const roms_tlev *t);  /* lmd_vmix(tind)   lmd_vmix.F:5     */
+int roms_gpu_prsgrd(const roms_tlev *t);              /* prsgrd           prsgrd.F:4       */
+int roms_gpu_pre_step3d(const roms_tlev *t);          /* pre_step3d(tile) pre_step3d4S.F:4 */
+int roms_gpu_set_huv1(const roms_tlev *t);           /* set_HUV1(tile)   set_depth.F:239  */
+int roms_gpu_step3d_uv1(const roms_tlev *t);          /* step3d_uv1(tile) step3d_uv1.F:5   */
+int roms_gpu_visc3d(const roms_tlev *t);              /* visc3d           visc3d_S.F:4     */
+int roms_gpu_step2d(const roms_tlev *t);              /* step2d           step2d_FB.F:3    */
+int roms_gpu_step3d_uv2(const roms_tlev *t);          /* step3d_uv2(tile) step3d_uv2.F:6   */
+int roms_gpu_step3d_t(const roms_tlev *t);            /* step3d_t(tile)   step3d_t_ISO.F:20*/
+int roms_gpu_t3dmix(const roms_tlev *t);              /* t3dmix           t3dmix_S.F:4     */
+int roms_gpu_set_depth(const roms_tlev *t);           /* set_depth(tile)  set_depth.F:4    */
+
+/* One whole roms_step (main.F:333-520, forcing held fixed): advances t->iic
+ * and leaves nstp/nrhs/nnew/kstp/knew as the reference does.  Steady-state
+ * steps replay a captured HIP graph.                                        */
+int roms_gpu_step(roms_tlev *t);
+/* roms_init device sequence after the host uploaded grid + initial state:
+ * set_depth, set_HUV, omega, rho_eos(nrhs) (main.F:268-288).                 */
+int roms_gpu_init_sequence(roms_tlev *t);
+
+/* ---- analytic cases (host-side ana_grid/ana_init restatements) ---- */
+enum roms_case_id { ROMS_CASE_FILAMENT = 0, ROMS_CASE_BASIN = 1 };
+typedef struct roms_case {
+  int case_id, LLm, MMm, N, NT;
+  int salinity, nonlin_eos, lmd_mixing;
+  double dt; int ndtfast;
+  double sizex, sizey;
+} roms_case;
+/* Builds the analytic grid/ICs on the host (setup_grid1/2, set_scoord,
+ * set_weights, ana_init), initialises the device and runs roms_init.        */
+int roms_gpu_init_case(const roms_case *c, int device, roms_tlev *t);
+
+/* ---- diagnostics (diag.F code_check norms, device reduction) ---- */
+int roms_gpu_diag(const roms_tlev *t, double norms[4]);
+/* event-timed replay of n steps on the library stream: total milliseconds  */
+int roms_gpu_time_steps(roms_tlev *t, int n, double *ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ROMS_GPU_H */

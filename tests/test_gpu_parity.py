@@ -1,0 +1,200 @@
+"""GPU parity: the HIP path (libromsgpu.so through the C ABI) against the CPU
+oracle (oracle/, pinned bit-exactly to the reference golden log).
+
+Tolerances: FP64 throughout; kernels are built with -ffp-contract=off and
+keep the reference's operation order, so most routines agree to the last bit.
+The few transcendental calls (log in the bottom drag, sqrt) may differ by an
+ulp between ROCm's device libm and glibc, hence a per-routine relative bound
+of 1e-12 and the north_star bound for whole runs: field RMS error < 1e-10.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+import romsgpu
+
+pytestmark = pytest.mark.gpu
+
+RTOL_ROUTINE = 1e-12
+RMS_RUN = 1e-10
+
+
+def basin_cfg(LLm=48, MMm=40, N=12, NT=2, nonlin=False, dt=60.0, ndtfast=30, sizex=96e3, sizey=80e3):
+    c = oracle.OrCfg()
+    c.LLm, c.MMm, c.N, c.NT = LLm, MMm, N, NT
+    c.ew_periodic = c.ns_periodic = 0
+    c.salinity, c.nonlin_eos, c.lmd = 1, int(nonlin), 0
+    c.case_id = oracle.CASE_BASIN
+    c.dt, c.ndtfast = dt, ndtfast
+    c.theta_s, c.theta_b, c.hc, c.rho0 = 6.0, 2.0, 250.0, 1027.5
+    c.rdrg, c.rdrg2, c.Zob = 0.0, 1.0e-3, 1.0e-2
+    c.Akv_bak = 1.0e-4
+    c.Akt_bak[0] = c.Akt_bak[1] = 1.0e-5
+    c.Tcoef, c.T0, c.Scoef, c.S0 = 0.20, 1.0, 0.822, 1.0
+    c.sizex, c.sizey = sizex, sizey
+    c.diag_np_xi = c.diag_np_eta = 1
+    return c
+
+
+def make_pair(cfg):
+    o = oracle.Oracle(cfg)
+    o.init()
+    m = romsgpu.Model.from_case(cfg.case_id, cfg.LLm, cfg.MMm, cfg.N, cfg.NT, salinity=bool(cfg.salinity),
+                                nonlin_eos=bool(cfg.nonlin_eos), dt=cfg.dt, ndtfast=cfg.ndtfast,
+                                sizex=cfg.sizex, sizey=cfg.sizey)
+    return o, m
+
+
+def interior(a, Lm, Mm):
+    return a[..., 2:Mm + 2, 2:Lm + 2]
+
+
+def relerr(a, b):
+    d = np.max(np.abs(a - b))
+    s = max(np.max(np.abs(b)), 1e-300)
+    return d / s
+
+
+def rms(a, b):
+    return float(np.sqrt(np.mean((a - b) ** 2)))
+
+
+def copy_state(o, m):
+    for name in romsgpu.FIELDS:
+        m.put(name, o.field(name))
+
+
+PROGNOSTIC = ["zeta", "ubar", "vbar", "u", "v", "t", "Hz", "z_r", "z_w", "FlxU", "FlxV", "We", "Wi"]
+
+
+def check_fields(o, m, names, Lm, Mm, tol, kind="rel"):
+    bad = []
+    for n in names:
+        a, b = interior(m.get(n), Lm, Mm), interior(o.field(n), Lm, Mm)
+        e = relerr(a, b) if kind == "rel" else rms(a, b)
+        if not (e <= tol):
+            bad.append((n, e))
+    assert not bad, bad
+
+
+def test_filament_init_matches_oracle():
+    cfg = oracle.filament_cfg(LLm=32, MMm=24, N=16, np_xi=1, np_eta=1)
+    o, m = make_pair(cfg)
+    check_fields(o, m, PROGNOSTIC + ["rho", "rhoA", "rhoS", "DU_avg1", "DV_avg1"], 32, 24, RTOL_ROUTINE)
+    m.close()
+
+
+ROUTINE_CASES = [
+    # (name, tindex mutation, outputs)
+    ("rho_eos", None, ["rho", "rhoA", "rhoS"]),
+    ("set_HUV", None, ["FlxU", "FlxV", "Hz_u", "Hz_v"]),
+    ("omega", None, ["We", "Wi"]),
+    ("prsgrd", None, ["ru", "rv"]),
+    ("pre_step3d", None, ["t", "u", "v", "r_D"]),
+    ("set_HUV1", None, ["u", "v", "FlxU", "FlxV"]),
+    ("step3d_uv1", "corr", ["u", "v", "rufrc", "rvfrc"]),
+    ("visc3d", "corr", ["u", "v", "rufrc", "rvfrc"]),
+    ("step3d_uv2", "corr", ["u", "v", "ubar", "vbar", "FlxU", "FlxV"]),
+    ("step3d_t", "corr", ["t"]),
+    ("t3dmix", "corr", ["t"]),
+    ("set_depth", None, ["z_w", "z_r", "Hz"]),
+]
+
+
+@pytest.mark.parametrize("case", ["filament", "basin", "basin_nonlin"])
+@pytest.mark.parametrize("routine,mode,outs", ROUTINE_CASES, ids=[r[0] for r in ROUTINE_CASES])
+def test_routine_parity(case, routine, mode, outs):
+    if case == "filament":
+        cfg = oracle.filament_cfg(LLm=32, MMm=24, N=16, np_xi=1, np_eta=1)
+    else:
+        cfg = basin_cfg(nonlin=(case == "basin_nonlin"))
+    o, m = make_pair(cfg)
+    o.step(3)
+    iic, kstp, knew, nstp, nrhs, nnew = o.tindex()
+    if mode == "corr":
+        nrhs, nnew = 3, 3 - nstp
+    else:
+        nrhs, nnew = nstp, 3
+    o.set_tindex([iic, kstp, knew, nstp, nrhs, nnew])
+    copy_state(o, m)
+    m.set_tindex(iic, kstp, knew, nstp, nrhs, nnew, nfast=o.nfast())
+    if routine == "rho_eos":
+        o.call("rho_eos", nrhs)
+        m.rho_eos(nrhs)
+        if cfg.nonlin_eos:
+            outs = ["rho1", "qp1", "rhoA", "rhoS"]
+    else:
+        o.call(routine)
+        getattr(m, routine)()
+    m.sync()
+    check_fields(o, m, outs, cfg.LLm, cfg.MMm, RTOL_ROUTINE)
+    m.close()
+
+
+def test_step2d_fast_loop_parity():
+    cfg = oracle.filament_cfg(LLm=32, MMm=24, N=16, np_xi=1, np_eta=1)
+    o, m = make_pair(cfg)
+    o.step(2)
+    iic, kstp, knew, nstp, nrhs, nnew = o.tindex()
+    copy_state(o, m)
+    for iif in (1, 2, 3, 4):
+        kstp, knew = knew, knew % 4 + 1
+        o.set_tindex([iic, kstp, knew, nstp, 3, 3 - nstp])
+        o.L.or_set_iif(o.h, iif)
+        o.call("step2d")
+        m.set_tindex(iic, kstp, knew, nstp, 3, 3 - nstp, iif=iif, nfast=o.nfast())
+        m.step2d()
+    check_fields(o, m, ["zeta", "ubar", "vbar", "Zt_avg1", "DU_avg1", "DV_avg1", "DU_avg2", "DV_avg2", "rufrc"],
+                 32, 24, RTOL_ROUTINE)
+    m.close()
+
+
+def test_filament_20_steps_golden_and_fields():
+    """Reference Filament case (64x64x32, 20 steps) on the GPU: diag norms vs
+    the golden log within reduction-order noise, fields vs the oracle."""
+    import json
+    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "filament_github_gnu.json")))["rows"]
+    cfg = oracle.filament_cfg()
+    o, m = make_pair(cfg)
+    for s in range(1, 21):
+        o.step()
+        m.step()
+        g = m.diag()
+        r = gold[s]
+        for key, val in zip(("ke", "ke2b", "cu_adv"), g[:3]):
+            ref = float(r[key])
+            assert abs(val - ref) <= 1e-11 * abs(ref), (s, key, val, ref)
+    check_fields(o, m, PROGNOSTIC, 64, 64, RMS_RUN, kind="rms")
+    m.close()
+
+
+def test_basin_nonlin_100_steps_rms():
+    """Closed synthetic basin, nonlinear split EOS, T+S: 100 steps, field RMS
+    against the oracle below the north_star bound."""
+    cfg = basin_cfg(LLm=40, MMm=32, N=10, nonlin=True)
+    o, m = make_pair(cfg)
+    o.step(100)
+    m.step(100)
+    m.sync()
+    assert o.tindex() == m.t.as_list()
+    check_fields(o, m, PROGNOSTIC, 40, 32, RMS_RUN, kind="rms")
+    m.close()
+
+
+def test_graph_replay_bitwise_equals_eager():
+    cfg = oracle.filament_cfg(LLm=32, MMm=24, N=16, np_xi=1, np_eta=1)
+    m1 = romsgpu.Model.from_case(0, 32, 24, 16, sizex=cfg.sizex, sizey=cfg.sizey)
+    m1.step(6)
+    a = {n: m1.get(n) for n in ("zeta", "u", "v", "t")}
+    m1.close()
+    os.environ["ROMS_GPU_NO_GRAPH"] = "1"
+    try:
+        m2 = romsgpu.Model.from_case(0, 32, 24, 16, sizex=cfg.sizex, sizey=cfg.sizey)
+        m2.step(6)
+        for n, v in a.items():
+            assert np.array_equal(m2.get(n), v), n
+        m2.close()
+    finally:
+        os.environ.pop("ROMS_GPU_NO_GRAPH", None)

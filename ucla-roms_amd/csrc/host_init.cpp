@@ -1,0 +1,373 @@
+// host_init.cpp -- host-side model setup for the analytic cases: the parts
+// of roms_init (main.F:85-321) that the reference runs once on the CPU before
+// time stepping -- set_weights (set_weights.F:7-235), set_scoord
+// (set_scoord.F:4-66), ana_grid / ana_init (tests/Filament/ana_grid.h,
+// ana_init.h; synthetic basin of SURVEY.md 8(d)), setup_grid1 metrics and the
+// setup_grid2 area/volume sums.  Produces host arrays in the Fortran layout
+// that the shim uploads; the time-stepping itself never touches the host.
+#include "host_init.h"
+
+#include <cmath>
+#include <cstring>
+
+namespace roms {
+
+HostState::HostState(int Lm_, int Mm_, int N_, int NT_, int nTS_)
+    : Lm(Lm_), Mm(Mm_), N(N_), NT(NT_), nTS(nTS_), nx2(Lm_ + 4), n2((long)(Lm_ + 4) * (Mm_ + 4)) {}
+
+std::vector<double>& HostState::a(int id) { return arr[id]; }
+
+// ---- set_weights (p=2, q=4, r=0.25) ----
+int set_weights(int ndtfast, double w[2][kMaxFast]) {
+  for (int i = 0; i < kMaxFast; i++) { w[0][i] = 0.0; w[1][i] = 0.0; }
+  int nfast = 0;
+  const double p = 2.0, q = 4.0, r = 0.25;
+  double scale = (p + 1.0) * (p + q + 1.0) / ((p + 2.0) * (p + q + 2.0) * (double)ndtfast);
+  double sum, shft, cff;
+  for (int iter = 1; iter <= 16; iter++) {
+    nfast = 0;
+    for (int i = 1; i <= 2 * ndtfast; i++) {
+      cff = scale * (double)i;
+      w[0][i - 1] = std::pow(cff, p) - std::pow(cff, p + q) - r * cff;
+      if (w[0][i - 1] > 0.0) nfast = i;
+      if (nfast > 0 && w[0][i - 1] < 0.0) w[0][i - 1] = 0.0;
+    }
+    sum = 0.0; shft = 0.0;
+    for (int i = 1; i <= nfast; i++) { sum = sum + w[0][i - 1]; shft = shft + w[0][i - 1] * (double)i; }
+    scale = scale * shft / (sum * (double)ndtfast);
+  }
+  for (int iter = 1; iter <= ndtfast; iter++) {
+    sum = 0.0; shft = 0.0;
+    for (int i = 1; i <= nfast; i++) { sum = sum + w[0][i - 1]; shft = shft + (double)i * w[0][i - 1]; }
+    shft = shft / sum;
+    cff = (double)ndtfast - shft;
+    if (cff > 1.0) {
+      nfast = nfast + 1;
+      for (int i = nfast; i >= 2; i--) w[0][i - 1] = w[0][i - 2];
+      w[0][0] = 0.0;
+    } else if (cff > 0.0) {
+      sum = 1.0 - cff;
+      for (int i = nfast; i >= 2; i--) w[0][i - 1] = sum * w[0][i - 1] + cff * w[0][i - 2];
+      w[0][0] = sum * w[0][0];
+    } else if (cff < -1.0) {
+      nfast = nfast - 1;
+      for (int i = 1; i <= nfast; i++) w[0][i - 1] = w[0][i];
+      w[0][nfast] = 0.0;
+    } else if (cff < 0.0) {
+      sum = 1.0 + cff;
+      for (int i = 1; i <= nfast - 1; i++) w[0][i - 1] = sum * w[0][i - 1] - cff * w[0][i];
+      w[0][nfast - 1] = sum * w[0][nfast - 1];
+    }
+  }
+  for (int j = 1; j <= nfast; j++) {
+    cff = w[0][j - 1];
+    for (int i = 1; i <= j; i++) w[1][i - 1] = w[1][i - 1] + cff;
+  }
+  sum = 0.0; cff = 0.0;
+  for (int i = 1; i <= nfast; i++) { sum = sum + w[0][i - 1]; cff = cff + w[1][i - 1]; }
+  sum = 1.0 / sum; cff = 1.0 / cff;
+  for (int i = 1; i <= nfast; i++) { w[0][i - 1] = sum * w[0][i - 1]; w[1][i - 1] = cff * w[1][i - 1]; }
+  return nfast;
+}
+
+// ---- set_scoord: SM09 stretching ----
+static double CSF(double sc, double theta_s, double theta_b) {
+  double csrf;
+  if (theta_s > 0.0) csrf = (1.0 - std::cosh(theta_s * sc)) / (std::cosh(theta_s) - 1.0);
+  else csrf = -(sc * sc);
+  if (theta_b > 0.0) return (std::exp(theta_b * csrf) - 1.0) / (1.0 - std::exp(-theta_b));
+  return csrf;
+}
+void set_scoord(int N, double theta_s, double theta_b, double* Cs_w, double* Cs_r) {
+  const double ds = 1.0 / (double)N;
+  Cs_w[N] = 0.0;
+  for (int k = N - 1; k >= 1; k--) Cs_w[k] = CSF(ds * (double)(k - N), theta_s, theta_b);
+  Cs_w[0] = -1.0;
+  Cs_r[0] = 0.0;
+  for (int k = 1; k <= N; k++) Cs_r[k] = CSF(ds * ((double)(k - N) - 0.5), theta_s, theta_b);
+}
+
+// periodic halo wrap on the host (same semantics as the device exchange)
+static void wrap(const HostState& H, double* a, int nlev, bool ewp, bool nsp) {
+  const int Lm = H.Lm, Mm = H.Mm;
+  auto at = [&](int i, int j, int k) -> double& { return a[(i + 1) + (long)(j + 1) * H.nx2 + (long)k * H.n2]; };
+  for (int k = 0; k < nlev; k++) {
+    if (ewp)
+      for (int j = 0; j <= Mm + 1; j++) {
+        at(-1, j, k) = at(Lm - 1, j, k); at(0, j, k) = at(Lm, j, k);
+        at(Lm + 1, j, k) = at(1, j, k); at(Lm + 2, j, k) = at(2, j, k);
+      }
+    if (nsp)
+      for (int i = 0; i <= Lm + 1; i++) {
+        int is = i;
+        if (ewp) { if (i == 0) is = Lm; if (i == Lm + 1) is = 1; }
+        at(i, -1, k) = at(is, Mm - 1, k); at(i, 0, k) = at(is, Mm, k);
+        at(i, Mm + 1, k) = at(is, 1, k); at(i, Mm + 2, k) = at(is, 2, k);
+      }
+    if (ewp && nsp)
+      for (int dj = 0; dj < 2; dj++)
+        for (int di = 0; di < 2; di++) {
+          at(-1 + di, -1 + dj, k) = at(Lm - 1 + di, Mm - 1 + dj, k);
+          at(Lm + 1 + di, -1 + dj, k) = at(1 + di, Mm - 1 + dj, k);
+          at(-1 + di, Mm + 1 + dj, k) = at(Lm - 1 + di, 1 + dj, k);
+          at(Lm + 1 + di, Mm + 1 + dj, k) = at(1 + di, 1 + dj, k);
+        }
+  }
+}
+
+static double pair_reduce(const HostState& H, std::vector<double> A, int istr, int iend, int jstr, int jend) {
+  auto at = [&](int i, int j) -> double& { return A[(i + 1) + (long)(j + 1) * H.nx2]; };
+  int isize = iend - istr, jsize = jend - jstr;
+  while (isize > 0 || jsize > 0) {
+    if (jsize > 0) {
+      int js = (jsize + 1) / 2 - 1;
+      for (int j = 0; j <= js; j++) {
+        const int jtg = jstr + j;
+        for (int i = istr; i <= istr + isize; i++) at(i, jtg) = at(i, jtg + j) + at(i, jtg + j + 1);
+      }
+      if (2 * js + 1 < jsize) {
+        js = js + 1;
+        const int jtg = jstr + js;
+        for (int i = istr; i <= istr + isize; i++) at(i, jtg) = at(i, jtg + js);
+      }
+      jsize = js;
+    }
+    if (isize > 0) {
+      int is = (isize + 1) / 2 - 1;
+      for (int j = jstr; j <= jstr + jsize; j++)
+        for (int i = 0; i <= is; i++) {
+          const int itg = istr + i;
+          at(itg, j) = at(itg + i, j) + at(itg + i + 1, j);
+        }
+      if (2 * is + 1 < isize) {
+        is = is + 1;
+        const int itg = istr + is;
+        for (int j = jstr; j <= jstr + jsize; j++) at(itg, j) = at(itg + is, j);
+      }
+      isize = is;
+    }
+  }
+  return at(istr, jstr);
+}
+double pair_sum(const HostState& H, const std::vector<double>& A) { return pair_reduce(H, A, 1, H.Lm, 1, H.Mm); }
+
+// Build grid + initial state of an analytic case on the host.
+void build_case(const CaseSpec& cs, HostState& H, double& area, double& volume) {
+  const int Lm = H.Lm, Mm = H.Mm, N = H.N, NT = H.NT;
+  const long n2 = H.n2, n3 = n2 * N, n3w = n2 * (N + 1);
+  const bool ewp = cs.ew_periodic, nsp = cs.ns_periodic;
+  auto alloc = [&](int id, long n) { H.arr[id].assign(n, 0.0); };
+  for (int id : {kh, khinv, kf, kfomn, kpm, kpn, kdm_r, kdn_r, kdm_u, kdn_u, kdm_v, kdn_v, kdm_p, kdn_p, kpmon_u, kpnom_v,
+                 krmask, kpmask, kumask, kvmask, kxr, kyr, kvisc2_r, kvisc2_p, ksustr, ksvstr, ksrflx, kswflx})
+    alloc(id, n2);
+  alloc(kzeta, 4 * n2); alloc(kubar, 4 * n2); alloc(kvbar, 4 * n2);
+  alloc(ku, 3 * n3); alloc(kv, 3 * n3); alloc(kt, 3 * n3 * NT);
+  alloc(kAkv, n3w); alloc(kAkt, n3w * H.nTS); alloc(kdiff2, n2 * NT); alloc(kstflx, n2 * NT);
+  alloc(kz_r, n3); alloc(kz_w, n3w); alloc(kHz, n3);
+  alloc(kCs_w, N + 1); alloc(kCs_r, N + 1);
+  set_scoord(N, cs.theta_s, cs.theta_b, H.arr[kCs_w].data(), H.arr[kCs_r].data());
+  auto A = [&](int id, int i, int j) -> double& { return H.arr[id][(i + 1) + (long)(j + 1) * H.nx2]; };
+  auto A3 = [&](int id, int i, int j, int k) -> double& { return H.arr[id][(i + 1) + (long)(j + 1) * H.nx2 + (long)(k - 1) * n2]; };
+  auto W3 = [&](int id, int i, int j, int k) -> double& { return H.arr[id][(i + 1) + (long)(j + 1) * H.nx2 + (long)k * n2]; };
+  auto T = [&](int i, int j, int k, int l, int it) -> double& {
+    return H.arr[kt][(i + 1) + (long)(j + 1) * H.nx2 + (long)(k - 1) * n2 + (long)(l - 1) * n3 + (long)(it - 1) * 3 * n3];
+  };
+  // ---- ana_grid ----
+  if (cs.case_id == 0) {
+    const double SizeX = cs.sizex, SizeY = cs.sizey;
+    const double f0 = 2 * 7.81e-5, beta = 0;
+    const double dx = SizeX / cs.LLm, dy = SizeY / cs.MMm, x_mid = SizeX / 2.0;
+    const double x0 = dx * (double)cs.iSW_corn, y0 = dy * (double)cs.jSW_corn;
+    for (int j = -1; j <= Mm + 2; j++)
+      for (int i = -1; i <= Lm + 2; i++) {
+        A(kxr, i, j) = x0 + dx * ((double)i - 0.5) - x_mid;
+        A(kyr, i, j) = y0 + dy * ((double)j - 0.5);
+        A(kpm, i, j) = 1.0 / dx;
+        A(kpn, i, j) = 1.0 / dy;
+        A(kf, i, j) = f0 + beta * (A(kyr, i, j) - SizeY / 2.0);
+        A(kh, i, j) = 1000;
+        A(krmask, i, j) = 1;
+      }
+  } else {
+    const double dx = cs.sizex / cs.LLm, dy = cs.sizey / cs.MMm;
+    const double R = 0.5 * (cs.sizex < cs.sizey ? cs.sizex : cs.sizey);
+    for (int j = -1; j <= Mm + 2; j++)
+      for (int i = -1; i <= Lm + 2; i++) {
+        const double x = dx * ((double)(i + cs.iSW_corn) - 0.5), y = dy * ((double)(j + cs.jSW_corn) - 0.5);
+        A(kxr, i, j) = x; A(kyr, i, j) = y;
+        A(kpm, i, j) = 1.0 / dx; A(kpn, i, j) = 1.0 / dy;
+        A(kf, i, j) = 1.0e-4;
+        const double rx = x - 0.5 * cs.sizex, ry = y - 0.5 * cs.sizey;
+        double s = 1.0 - (rx * rx + ry * ry) / (R * R);
+        if (s < 0.0) s = 0.0;
+        A(kh, i, j) = 200.0 + 3800.0 * s;
+        A(krmask, i, j) = 1.0;
+      }
+  }
+  // ---- setup_grid1 (setup_grid1.F): metric combinations and masks ----
+  const int istr = 1, iend = Lm, jstr = 1, jend = Mm;
+  const bool we = !ewp && !cs.west_exchng, ee = !ewp && !cs.east_exchng;
+  const bool se = !nsp && !cs.south_exchng, ne = !nsp && !cs.north_exchng;
+  const int istrR = we ? istr - 1 : istr, iendR = ee ? iend + 1 : iend;
+  const int jstrR = se ? jstr - 1 : jstr, jendR = ne ? jend + 1 : jend;
+  const int istrE = (ewp || cs.west_exchng) ? istr - 2 : istr - 1, iendE = (ewp || cs.east_exchng) ? iend + 2 : iend + 1;
+  const int jstrE = (nsp || cs.south_exchng) ? jstr - 2 : jstr - 1, jendE = (nsp || cs.north_exchng) ? jend + 2 : jend + 1;
+  for (int j = jstrE; j <= jendE; j++)
+    for (int i = istrE; i <= iendE; i++) A(kfomn, i, j) = A(kf, i, j) / (A(kpm, i, j) * A(kpn, i, j));
+  for (int j = jstrR; j <= jendR; j++)
+    for (int i = istrR; i <= iendR; i++) { A(kdm_r, i, j) = 1.0 / A(kpm, i, j); A(kdn_r, i, j) = 1.0 / A(kpn, i, j); }
+  for (int j = jstrR; j <= jendR; j++)
+    for (int i = istr; i <= iendR; i++) {
+      A(kpmon_u, i, j) = (A(kpm, i, j) + A(kpm, i - 1, j)) / (A(kpn, i, j) + A(kpn, i - 1, j));
+      A(kdm_u, i, j) = 2.0 / (A(kpm, i, j) + A(kpm, i - 1, j));
+      A(kdn_u, i, j) = 2.0 / (A(kpn, i, j) + A(kpn, i - 1, j));
+      A(kumask, i, j) = A(krmask, i, j) * A(krmask, i - 1, j);
+    }
+  for (int j = jstr; j <= jendR; j++)
+    for (int i = istrR; i <= iendR; i++) {
+      A(kpnom_v, i, j) = (A(kpn, i, j) + A(kpn, i, j - 1)) / (A(kpm, i, j) + A(kpm, i, j - 1));
+      A(kdm_v, i, j) = 2.0 / (A(kpm, i, j) + A(kpm, i, j - 1));
+      A(kdn_v, i, j) = 2.0 / (A(kpn, i, j) + A(kpn, i, j - 1));
+      A(kvmask, i, j) = A(krmask, i, j) * A(krmask, i, j - 1);
+    }
+  for (int j = jstr; j <= jendR; j++)
+    for (int i = istr; i <= iendR; i++) {
+      A(kdm_p, i, j) = 4.0 / (A(kpm, i, j) + A(kpm, i, j - 1) + A(kpm, i - 1, j) + A(kpm, i - 1, j - 1));
+      A(kdn_p, i, j) = 4.0 / (A(kpn, i, j) + A(kpn, i, j - 1) + A(kpn, i - 1, j) + A(kpn, i - 1, j - 1));
+      const int a = A(krmask, i - 1, j) > 0.5, b = A(krmask, i, j) > 0.5, c = A(krmask, i - 1, j - 1) > 0.5,
+                d = A(krmask, i, j - 1) > 0.5;
+      const int n = a + b + c + d;
+      double pmk = 0.0;
+      if (n >= 3) pmk = 1.0;
+      else if (n == 2 && ((a && c) || (b && d) || (a && b) || (c && d))) pmk = 2.0;
+      A(kpmask, i, j) = pmk;
+    }
+  for (int id : {kdm_r, kdn_r, kdm_p, kdn_p, kdm_u, kdn_u, kdm_v, kdn_v, kpmon_u, kpnom_v, krmask, kumask, kvmask, kpmask})
+    wrap(H, H.arr[id].data(), 1, ewp, nsp);
+  // setup_grid2: area/volume (single-rank pairwise sums)
+  {
+    std::vector<double> dA(n2, 0.0), dV(n2, 0.0);
+    for (int j = 1; j <= Mm; j++)
+      for (int i = 1; i <= Lm; i++) {
+        const long o = (i + 1) + (long)(j + 1) * H.nx2;
+        dA[o] = A(krmask, i, j) / (A(kpm, i, j) * A(kpn, i, j));
+        dV[o] = dA[o] * A(kh, i, j);
+      }
+    area = pair_sum(H, dA);
+    volume = pair_sum(H, dV);
+  }
+  // mixing.F:156-162
+  for (long q = 0; q < n2; q++) { H.arr[kvisc2_r][q] = cs.visc2; H.arr[kvisc2_p][q] = cs.visc2; }
+  for (long q = 0; q < n2 * NT; q++) H.arr[kdiff2][q] = cs.tnu2;
+  // ---- set_depth at rest (zeta=0) for ana_init: set_depth.F:65-90 ----
+  const double hc = cs.hc, ds = 1.0 / (double)N;
+  const double* Cs_w = H.arr[kCs_w].data();
+  const double* Cs_r = H.arr[kCs_r].data();
+  for (int j = -1; j <= Mm + 2; j++)
+    for (int i = -1; i <= Lm + 2; i++) {
+      const double hh = A(kh, i, j), hi = 1.0 / (hh + hc), z = 0.0;
+      W3(kz_w, i, j, 0) = -hh;
+      for (int k = 1; k <= N; k++) {
+        const double cff_w = hc * ds * (double)(k - N), cff_r = hc * ds * ((double)(k - N) - 0.5);
+        W3(kz_w, i, j, k) = z + (z + hh) * (cff_w + Cs_w[k] * hh) * hi;
+        A3(kz_r, i, j, k) = z + (z + hh) * (cff_r + Cs_r[k] * hh) * hi;
+        A3(kHz, i, j, k) = W3(kz_w, i, j, k) - W3(kz_w, i, j, k - 1);
+      }
+    }
+  // ---- ana_init ----
+  const double g = 9.81;
+  if (cs.case_id == 0) {
+    const double b0 = 5.0e-2, B_cff = 0.025, lambda_inv = 8.0, Nb = 1.0e-7, N0 = 3.0e-5, h0 = 60.0, dh0 = 15.,
+                 L = 2000.0, HD = 1000;
+    const double alpha = cs.Tcoef / cs.rho0;
+    for (int j = -1; j <= Mm + 2; j++)
+      for (int i = -1; i <= Lm + 2; i++) {
+        const double xl = A(kxr, i, j) / L;
+        const double h_sbl = h0 + dh0 * std::exp(-(xl * xl));
+        for (int k = 1; k <= N; k++) {
+          const double zr = A3(kz_r, i, j, k);
+          const double b = b0 + Nb * (zr + HD) +
+                           0.5 * N0 * ((1 + B_cff) * zr - (1 - B_cff) * (h_sbl + lambda_inv * std::log(std::cosh((1. / lambda_inv) * (zr + h_sbl)))));
+          T(i, j, k, 1, 1) = b / (g * alpha);
+        }
+      }
+    double bf_int = 0;
+    for (int k = 1; k <= N; k++) {
+      const double zr = A3(kz_r, 1, 1, k);
+      bf_int = bf_int + A3(kHz, 1, 1, k) *
+                            (b0 + Nb * (zr + HD) +
+                             0.5 * N0 * ((1 + B_cff) * zr - (1 - B_cff) * (h0 + lambda_inv * std::log(std::cosh((1. / lambda_inv) * (zr + h0)))))) /
+                            g;
+    }
+    for (int k = 1; k <= N; k++)
+      for (int j = -1; j <= Mm + 2; j++)
+        for (int i = -1; i <= Lm + 2; i++) {
+          T(i, j, k, 2, 1) = T(i, j, k, 1, 1);
+          if (cs.salinity) { T(i, j, k, 1, 2) = 36.; T(i, j, k, 2, 2) = T(i, j, k, 1, 2); }
+        }
+    auto Z = [&](int i, int j, int l) -> double& { return H.arr[kzeta][(i + 1) + (long)(j + 1) * H.nx2 + (long)(l - 1) * n2]; };
+    auto VB = [&](int i, int j, int l) -> double& { return H.arr[kvbar][(i + 1) + (long)(j + 1) * H.nx2 + (long)(l - 1) * n2]; };
+    auto V = [&](int i, int j, int k, int l) -> double& {
+      return H.arr[kv][(i + 1) + (long)(j + 1) * H.nx2 + (long)(k - 1) * n2 + (long)(l - 1) * n3];
+    };
+    for (int k = 1; k <= N; k++)
+      for (int j = -1; j <= Mm + 2; j++)
+        for (int i = -1; i <= Lm + 2; i++) Z(i, j, 1) = Z(i, j, 1) + T(i, j, k, 1, 1) * alpha * A3(kHz, i, j, k);
+    for (int j = -1; j <= Mm + 2; j++)
+      for (int i = -1; i <= Lm + 2; i++) Z(i, j, 1) = (Z(i, j, 1) - bf_int);
+    for (int j = 0; j <= Mm + 1; j++)
+      for (int i = 0; i <= Lm + 1; i++) {
+        const double dzdx = 0.5 * A(kpm, i, j) * (Z(i + 1, j, 1) - Z(i - 1, j, 1));
+        V(i, j, N, 1) = g * dzdx / A(kf, i, j);
+      }
+    for (int k = N - 1; k >= 1; k--)
+      for (int j = 0; j <= Mm + 1; j++)
+        for (int i = 0; i <= Lm + 1; i++) {
+          const double dbdx = 0.25 * A(kpm, i, j) * g * alpha *
+                              (T(i + 1, j, k, 1, 1) - T(i - 1, j, k, 1, 1) + T(i + 1, j, k + 1, 1, 1) - T(i - 1, j, k + 1, 1, 1));
+          V(i, j, k, 1) = V(i, j, k + 1, 1) - dbdx * (A3(kz_r, i, j, k + 1) - A3(kz_r, i, j, k)) / A(kf, i, j);
+        }
+    for (int k = N - 1; k >= 1; k--)
+      for (int j = 0; j <= Mm + 1; j++)
+        for (int i = 0; i <= Lm + 1; i++) VB(i, j, 1) = VB(i, j, 1) + V(i, j, k, 1) * A3(kHz, i, j, k) / HD;
+    for (int j = 1; j <= Mm; j++)
+      for (int i = 1; i <= Lm; i++) {
+        VB(i, j, 2) = VB(i, j, 1);
+        Z(i, j, 2) = Z(i, j, 1);
+        for (int k = 1; k <= N; k++) V(i, j, k, 2) = V(i, j, k, 1);
+      }
+  } else {
+    const double Lx = cs.sizex, Ly = cs.sizey, pi = 3.14159265358979323;
+    for (int k = 1; k <= N; k++)
+      for (int j = -1; j <= Mm + 2; j++)
+        for (int i = -1; i <= Lm + 2; i++) {
+          const double x = A(kxr, i, j), y = A(kyr, i, j), ez = std::exp(A3(kz_r, i, j, k) / 500.0);
+          T(i, j, k, 1, 1) = 4.0 + 10.0 * ez + 0.5 * std::sin(2.0 * pi * x / Lx) * std::sin(2.0 * pi * y / Ly) * ez;
+          T(i, j, k, 2, 1) = T(i, j, k, 1, 1);
+          if (cs.salinity) {
+            T(i, j, k, 1, 2) = 35.0 + 0.25 * std::cos(2.0 * pi * x / Lx);
+            T(i, j, k, 2, 2) = T(i, j, k, 1, 2);
+          }
+          for (int it = 3; it <= NT; it++) {
+            const double rx = (x - 0.3 * Lx) / (0.1 * Lx), ry = (y - 0.5 * Ly) / (0.1 * Ly);
+            T(i, j, k, 1, it) = std::exp(-(rx * rx + ry * ry)) * ez * (double)(it - 2);
+            T(i, j, k, 2, it) = T(i, j, k, 1, it);
+          }
+        }
+    for (long q = 0; q < n3w; q++) H.arr[kAkv][q] = cs.Akv_bak;
+    for (int it = 1; it <= H.nTS; it++)
+      for (long q = 0; q < n3w; q++) H.arr[kAkt][q + (long)(it - 1) * n3w] = cs.Akt_bak[it - 1];
+    const double piy = 3.14159265358979323;
+    for (int j = -1; j <= Mm + 2; j++)
+      for (int i = -1; i <= Lm + 2; i++) A(ksustr, i, j) = 1.0e-4 * std::sin(piy * A(kyr, i, j) / cs.sizey);
+  }
+  // ana_init_generic exchanges
+  wrap(H, H.arr[kzeta].data(), 1, ewp, nsp);
+  wrap(H, H.arr[kubar].data(), 1, ewp, nsp);
+  wrap(H, H.arr[kvbar].data(), 1, ewp, nsp);
+  wrap(H, H.arr[ku].data(), N, ewp, nsp);
+  wrap(H, H.arr[kv].data(), N, ewp, nsp);
+  for (int it = 1; it <= NT; it++) wrap(H, H.arr[kt].data() + (long)(it - 1) * 3 * n3, N, ewp, nsp);
+}
+
+}  // namespace roms

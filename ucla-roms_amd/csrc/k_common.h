@@ -1,0 +1,309 @@
+// k_common.h -- device restatements of the reference's shared flux fragments:
+//   compute_horiz_tracer_fluxes.h  (4th-order centred / UPSTREAM_TS)
+//   compute_vert_tracer_fluxes.h   (SPLINE_TS, natural b.c.)
+//   compute_horiz_rhs_uv_terms.h   (UV_COR + UV_ADV, centred / UPSTREAM_UV)
+//   compute_vert_rhs_uv_terms.h    (SPLINE_UV, MASKING)
+// The reference evaluates these over extended index ranges into 2-D scratch;
+// here each lane recomputes the face values it needs from the inputs, which
+// keeps the arithmetic of every face identical and removes the scratch round
+// trip through HBM.  The one-sided edge extrapolations of the reference become
+// index clamps at closed (non-periodic) physical edges.
+#pragma once
+#include "roms_dev.h"
+
+namespace roms {
+
+// ---- pseudo-continuity of the predictor (pre_step3d4S.F:136-148) ----
+__device__ __forceinline__ void hz_bak_fwd(const Dev& d, int i, int j, int k, double cff, double& bak, double& fwd) {
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const long ij = IJ(b, i, j), o = ij + (long)(k - 1) * b.n2, w = ij + (long)k * b.n2;
+  const double FlxDiv = cff * F.pm[ij] * F.pn[ij] *
+                        (F.FlxU[o + 1] - F.FlxU[o] + F.FlxV[o + b.nx2] - F.FlxV[o] + F.We[w] + F.Wi[w] -
+                         F.We[w - b.n2] - F.Wi[w - b.n2]);
+  bak = F.Hz[o] + FlxDiv;
+  fwd = F.Hz[o] - FlxDiv;
+}
+
+// ---- horizontal tracer fluxes at one face ----
+// FX at u-point m (row j, level k): elementary differences FXel(q) for
+// q=m-1..m+1, clamped at closed edges (FX(istr-1)=FX(istr), FX(iend+2)=FX(iend+1)).
+__device__ __forceinline__ double tracer_fx(const Dev& d, const double* __restrict__ T, int m, int j, int k,
+                                            bool upstream) {
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const long row = (long)(j + 1) * b.nx2 + (long)(k - 1) * b.n2;
+  const int lo = b.west_edge ? b.istr : -1000000, hi = b.east_edge ? b.iend + 1 : 1000000;
+  double el[3];
+  for (int q = 0; q < 3; q++) {
+    const int p = iclamp(m - 1 + q, lo, hi);
+    const long o = row + p + 1;
+    el[q] = (T[o] - T[o - 1]) * F.umask[IJ(b, p, j)];
+  }
+  const long o = row + m + 1;
+  const double Fl = F.FlxU[o];
+  if (upstream) {
+    const double cm = el[1] - el[0], c0 = el[2] - el[1];   // curv(m-1), curv(m)
+    return 0.5 * (T[o] + T[o - 1]) * Fl - 0.1666666666666666 * (cm * fmax0(Fl) + c0 * fmin0(Fl));
+  }
+  const double gm = 0.5 * (el[1] + el[0]), g0 = 0.5 * (el[2] + el[1]);  // grad(m-1), grad(m)
+  return 0.5 * (T[o] + T[o - 1] - 0.3333333333333333 * (g0 - gm)) * Fl;
+}
+__device__ __forceinline__ double tracer_fe(const Dev& d, const double* __restrict__ T, int i, int m, int k,
+                                            bool upstream) {
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const long sj = b.nx2;
+  const long col = (long)(i + 1) + (long)(k - 1) * b.n2;
+  const int lo = b.south_edge ? b.jstr : -1000000, hi = b.north_edge ? b.jend + 1 : 1000000;
+  double el[3];
+  for (int q = 0; q < 3; q++) {
+    const int p = iclamp(m - 1 + q, lo, hi);
+    const long o = col + (long)(p + 1) * sj;
+    el[q] = (T[o] - T[o - sj]) * F.vmask[IJ(b, i, p)];
+  }
+  const long o = col + (long)(m + 1) * sj;
+  const double Fl = F.FlxV[o];
+  if (upstream) {
+    const double cm = el[1] - el[0], c0 = el[2] - el[1];
+    return 0.5 * (T[o] + T[o - sj]) * Fl - 0.1666666666666666 * (cm * fmax0(Fl) + c0 * fmin0(Fl));
+  }
+  const double gm = 0.5 * (el[1] + el[0]), g0 = 0.5 * (el[2] + el[1]);
+  return 0.5 * (T[o] + T[o - sj] - 0.3333333333333333 * (g0 - gm)) * Fl;
+}
+
+// ---- parabolic-spline vertical tracer fluxes, written as FC(0:N) into the
+// lane's column scratch (layout of a w-point array); CF uses a second column.
+__device__ __forceinline__ void tracer_spline_fc(const Dev& d, const double* __restrict__ T, long ij,
+                                                 double* __restrict__ FC, double* __restrict__ CF) {
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const int N = b.N;
+  const long n2 = b.n2;
+  double cfk = 1.0;                 // CF(1)
+  double fcm = 2.0 * T[ij];         // FC(0)
+  FC[ij] = fcm;
+  double hk = F.Hz[ij], tk = T[ij];
+  for (int k = 1; k <= N - 1; k++) {
+    const long o1 = ij + (long)k * n2;  // level k+1 (rho layout)
+    const double hk1 = F.Hz[o1], tk1 = T[o1];
+    const double cff = 1.0 / (2.0 * hk + hk1 * (2.0 - cfk));
+    const double cf1 = cff * hk;
+    const double fck = cff * (3.0 * (hk * tk1 + hk1 * tk) - hk1 * fcm);
+    CF[ij + (long)(k + 1) * n2] = cf1;
+    FC[ij + (long)k * n2] = fck;
+    cfk = cf1; fcm = fck; hk = hk1; tk = tk1;
+  }
+  double fc1 = (2.0 * tk - fcm) / (1.0 - cfk);   // FC(N)
+  for (int k = N - 1; k >= 0; k--) {
+    const double fck = FC[ij + (long)k * n2] - CF[ij + (long)(k + 1) * n2] * fc1;
+    FC[ij + (long)(k + 1) * n2] = fc1 * F.We[ij + (long)(k + 1) * n2];
+    FC[ij + (long)k * n2] = fck;
+    fc1 = fck;
+  }
+  FC[ij + (long)N * n2] = 0.0;
+  FC[ij] = 0.0;
+}
+
+// ---- horizontal momentum r.h.s. (Coriolis + advection) at (i,j,k) ----
+struct UVBounds {
+  int u_imin, u_imax, v_jmin, v_jmax;   // uxx / vee extrapolation ranges
+  int e_jmin, e_jmax, x_imin, x_imax;   // uee / vxx extrapolation ranges
+};
+__host__ inline UVBounds uv_bounds(const Bounds& b) {
+  UVBounds r;
+  if (!b.ew_periodic) {
+    r.u_imin = b.west_edge ? b.istrU : b.istrU - 1; r.u_imax = b.east_edge ? b.iend : b.iend + 1;
+    r.x_imin = b.west_edge ? b.istr : b.istr - 1;   r.x_imax = b.east_edge ? b.iend : b.iend + 1;
+  } else {
+    r.u_imin = r.x_imin = b.istr - 1; r.u_imax = r.x_imax = b.iend + 1;
+  }
+  if (!b.ns_periodic) {
+    r.v_jmin = b.south_edge ? b.jstrV : b.jstrV - 1; r.v_jmax = b.north_edge ? b.jend : b.jend + 1;
+    r.e_jmin = b.south_edge ? b.jstr : b.jstr - 1;   r.e_jmax = b.north_edge ? b.jend : b.jend + 1;
+  } else {
+    r.v_jmin = r.e_jmin = b.jstr - 1; r.v_jmax = r.e_jmax = b.jend + 1;
+  }
+  return r;
+}
+
+// u at (i,j,k) of level slab U (already offset to the time level)
+#define UU(ii, jj) U[IJ(b, ii, jj) + kk]
+#define VV(ii, jj) V[IJ(b, ii, jj) + kk]
+#define FU(ii, jj) F.FlxU[IJ(b, ii, jj) + kk]
+#define FV(ii, jj) F.FlxV[IJ(b, ii, jj) + kk]
+
+__device__ __forceinline__ double uxx_at(const Dev& d, const double* U, int m, int j, long kk, const UVBounds& r) {
+  const Bounds& b = d.b;
+  m = iclamp(m, r.u_imin, r.u_imax);
+  return UU(m - 1, j) - 2.0 * UU(m, j) + UU(m + 1, j);
+}
+__device__ __forceinline__ double Huxx_at(const Dev& d, int m, int j, long kk, const UVBounds& r) {
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  m = iclamp(m, r.u_imin, r.u_imax);
+  return FU(m - 1, j) - 2.0 * FU(m, j) + FU(m + 1, j);
+}
+__device__ __forceinline__ double vee_at(const Dev& d, const double* V, int i, int m, long kk, const UVBounds& r) {
+  const Bounds& b = d.b;
+  m = iclamp(m, r.v_jmin, r.v_jmax);
+  return VV(i, m - 1) - 2.0 * VV(i, m) + VV(i, m + 1);
+}
+__device__ __forceinline__ double Hvee_at(const Dev& d, int i, int m, long kk, const UVBounds& r) {
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  m = iclamp(m, r.v_jmin, r.v_jmax);
+  return FV(i, m - 1) - 2.0 * FV(i, m) + FV(i, m + 1);
+}
+__device__ __forceinline__ double uee_at(const Dev& d, const double* U, int i, int m, long kk, const UVBounds& r) {
+  const Bounds& b = d.b;
+  m = iclamp(m, r.e_jmin, r.e_jmax);
+  return UU(i, m - 1) - 2.0 * UU(i, m) + UU(i, m + 1);
+}
+__device__ __forceinline__ double vxx_at(const Dev& d, const double* V, int m, int j, long kk, const UVBounds& r) {
+  const Bounds& b = d.b;
+  m = iclamp(m, r.x_imin, r.x_imax);
+  return VV(m - 1, j) - 2.0 * VV(m, j) + VV(m + 1, j);
+}
+
+// UFx at rho-point (m,j): diagonal xi-flux of u-momentum
+__device__ __forceinline__ double adv_UFx(const Dev& d, const double* U, int m, int j, long kk, const UVBounds& r,
+                                          bool up) {
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const double delta = 0.1666666666666667, gamma = 0.3333333333333333;
+  const double ux0 = uxx_at(d, U, m, j, kk, r), ux1 = uxx_at(d, U, m + 1, j, kk, r);
+  const double Hx0 = Huxx_at(d, m, j, kk, r), Hx1 = Huxx_at(d, m + 1, j, kk, r);
+  if (up) {
+    const double cff = FU(m, j) + FU(m + 1, j) - delta * (Hx0 + Hx1);
+    return 0.25 * (cff * (UU(m, j) + UU(m + 1, j)) - gamma * (fmax0(cff) * ux0 + fmin0(cff) * ux1));
+  }
+  return 0.25 * (UU(m, j) + UU(m + 1, j) - delta * (ux0 + ux1)) * (FU(m, j) + FU(m + 1, j) - delta * (Hx0 + Hx1));
+}
+// VFe at rho-point (i,m)
+__device__ __forceinline__ double adv_VFe(const Dev& d, const double* V, int i, int m, long kk, const UVBounds& r,
+                                          bool up) {
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const double delta = 0.1666666666666667, gamma = 0.3333333333333333;
+  const double ve0 = vee_at(d, V, i, m, kk, r), ve1 = vee_at(d, V, i, m + 1, kk, r);
+  const double He0 = Hvee_at(d, i, m, kk, r), He1 = Hvee_at(d, i, m + 1, kk, r);
+  if (up) {
+    const double cff = FV(i, m) + FV(i, m + 1) - delta * (He0 + He1);
+    return 0.25 * (cff * (VV(i, m) + VV(i, m + 1)) - gamma * (fmax0(cff) * ve0 + fmin0(cff) * ve1));
+  }
+  return 0.25 * (VV(i, m) + VV(i, m + 1) - delta * (ve0 + ve1)) * (FV(i, m) + FV(i, m + 1) - delta * (He0 + He1));
+}
+// UFe at psi-point (i,m)
+__device__ __forceinline__ double adv_UFe(const Dev& d, const double* U, int i, int m, long kk, const UVBounds& r,
+                                          bool up) {
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const double delta = 0.1666666666666667, gamma = 0.3333333333333333;
+  const double Hv0 = FV(i - 1, m) - 2.0 * FV(i, m) + FV(i + 1, m);       // Hvxx(i,m)
+  const double Hvm = FV(i - 2, m) - 2.0 * FV(i - 1, m) + FV(i, m);       // Hvxx(i-1,m)
+  const double um1 = uee_at(d, U, i, m - 1, kk, r), u0 = uee_at(d, U, i, m, kk, r);
+  if (up) {
+    const double cff = FV(i, m) + FV(i - 1, m) - delta * (Hv0 + Hvm);
+    return 0.25 * (cff * (UU(i, m) + UU(i, m - 1)) - gamma * (fmax0(cff) * um1 + fmin0(cff) * u0));
+  }
+  return 0.25 * (UU(i, m) + UU(i, m - 1) - delta * (u0 + um1)) * (FV(i, m) + FV(i - 1, m) - delta * (Hv0 + Hvm));
+}
+// VFx at psi-point (m,j)
+__device__ __forceinline__ double adv_VFx(const Dev& d, const double* V, int m, int j, long kk, const UVBounds& r,
+                                          bool up) {
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const double delta = 0.1666666666666667, gamma = 0.3333333333333333;
+  const double Hu0 = FU(m, j - 1) - 2.0 * FU(m, j) + FU(m, j + 1);       // Huee(m,j)
+  const double Hum = FU(m, j - 2) - 2.0 * FU(m, j - 1) + FU(m, j);       // Huee(m,j-1)
+  const double vm1 = vxx_at(d, V, m - 1, j, kk, r), v0 = vxx_at(d, V, m, j, kk, r);
+  if (up) {
+    const double cff = FU(m, j) + FU(m, j - 1) - delta * (Hu0 + Hum);
+    return 0.25 * (cff * (VV(m, j) + VV(m - 1, j)) - gamma * (fmax0(cff) * vm1 + fmin0(cff) * v0));
+  }
+  return 0.25 * (VV(m, j) + VV(m - 1, j) - delta * (v0 + vm1)) * (FU(m, j) + FU(m, j - 1) - delta * (Hu0 + Hum));
+}
+
+// Full horizontal r.h.s. at (i,j,k): Coriolis first, then advection, with the
+// two accumulation steps into ru/rv kept in the reference's order.
+__device__ __forceinline__ void uv_horiz_rhs(const Dev& d, int i, int j, int k, int nrhs, const UVBounds& r,
+                                             bool up) {
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const long kk = (long)(k - 1) * b.n2;
+  const double* U = F.u + (long)(nrhs - 1) * b.n3;
+  const double* V = F.v + (long)(nrhs - 1) * b.n3;
+  const long o = IJ(b, i, j) + kk;
+  if (i >= b.istrU && i <= b.iend && j >= b.jstr && j <= b.jend) {
+    // Coriolis UFx at i and i-1: cff=0.5*Hz*fomn; UFx=cff*(v(j)+v(j+1))
+    const double c0 = 0.5 * F.Hz[o] * (F.fomn[IJ(b, i, j)]);
+    const double c1 = 0.5 * F.Hz[o - 1] * (F.fomn[IJ(b, i - 1, j)]);
+    const double U0 = c0 * (VV(i, j) + VV(i, j + 1)), U1 = c1 * (VV(i - 1, j) + VV(i - 1, j + 1));
+    double ru = F.ru[o] + 0.5 * (U0 + U1);
+    ru = ru - adv_UFx(d, U, i, j, kk, r, up) + adv_UFx(d, U, i - 1, j, kk, r, up) - adv_UFe(d, U, i, j + 1, kk, r, up) +
+         adv_UFe(d, U, i, j, kk, r, up);
+    F.ru[o] = ru;
+  }
+  if (i >= b.istr && i <= b.iend && j >= b.jstrV && j <= b.jend) {
+    const double c0 = 0.5 * F.Hz[o] * (F.fomn[IJ(b, i, j)]);
+    const double c1 = 0.5 * F.Hz[o - b.nx2] * (F.fomn[IJ(b, i, j - 1)]);
+    const double V0 = c0 * (UU(i, j) + UU(i + 1, j)), V1 = c1 * (UU(i, j - 1) + UU(i + 1, j - 1));
+    double rv = F.rv[o] - 0.5 * (V0 + V1);
+    rv = rv - adv_VFx(d, V, i + 1, j, kk, r, up) + adv_VFx(d, V, i, j, kk, r, up) - adv_VFe(d, V, i, j, kk, r, up) +
+         adv_VFe(d, V, i, j - 1, kk, r, up);
+    F.rv[o] = rv;
+  }
+}
+#undef UU
+#undef VV
+#undef FU
+#undef FV
+
+// ---- vertical momentum advection by parabolic splines (SPLINE_UV) ----
+// dir=0: u at (i,j) (Hz/We averaged over i-1,i; stencil i-2..i+1, umask)
+// dir=1: v at (i,j) (over j-1,j; vmask).  FC,CF: lane column scratch.
+__device__ __forceinline__ void uv_vert_rhs(const Dev& d, int i, int j, int nrhs, int dir, double* __restrict__ FC,
+                                            double* __restrict__ CF) {
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const int N = b.N;
+  const long n2 = b.n2, ij = IJ(b, i, j);
+  const long s = dir == 0 ? 1 : b.nx2;
+  const double* Uv = (dir == 0 ? F.u : F.v) + (long)(nrhs - 1) * b.n3;
+  double* rr = dir == 0 ? F.ru : F.rv;
+  const double* mask = dir == 0 ? F.umask : F.vmask;
+  auto DCk = [&](int k) {
+    const long o = ij + (long)(k - 1) * n2;
+    return 0.5625 * (F.Hz[o] + F.Hz[o - s]) - 0.0625 * (F.Hz[o + s] + F.Hz[o - 2 * s]);
+  };
+  double dck = DCk(1), cfk = 1.0, fcm = 2.0 * Uv[ij];
+  FC[ij] = fcm;
+  for (int k = 1; k <= N - 1; k++) {
+    const double dc1 = DCk(k + 1);
+    const double cff = 1.0 / (2.0 * dck + dc1 * (2.0 - cfk));
+    const double cf1 = cff * dck;
+    const long o = ij + (long)(k - 1) * n2;
+    const double fck = cff * (3.0 * (dck * Uv[o + n2] + dc1 * Uv[o]) - dc1 * fcm);
+    CF[ij + (long)(k + 1) * n2] = cf1;
+    FC[ij + (long)k * n2] = fck;
+    dck = dc1; cfk = cf1; fcm = fck;
+  }
+  double fc1 = (2.0 * Uv[ij + (long)(N - 1) * n2] - fcm) / (1.0 - cfk);  // FC(N)
+  double dc1 = 0.0;                                                      // DC(N)
+  const double m1 = mask[ij + s], m0 = mask[ij - s];
+  for (int k = N - 1; k >= 1; k--) {
+    const double fck = FC[ij + (long)k * n2] - CF[ij + (long)(k + 1) * n2] * fc1;
+    const long w = ij + (long)k * n2;
+    const double dck2 = fck * 0.5 *
+                        (F.We[w] + F.We[w - s] -
+                         0.125 * ((F.We[w + s] - F.We[w]) * m1 - (F.We[w - s] - F.We[w - 2 * s]) * m0));
+    const long o1 = ij + (long)k * n2;  // rho-level k+1
+    rr[o1] = rr[o1] - dc1 + dck2;
+    dc1 = dck2;
+    fc1 = fck;
+  }
+  rr[ij] = rr[ij] - dc1;
+}
+
+}  // namespace roms

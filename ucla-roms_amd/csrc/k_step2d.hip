@@ -1,0 +1,325 @@
+// k_step2d.hip -- step2d_FB_tile (step2d_FB.F:24-576): one generalized
+// forward-backward AB3-AM4 barotropic step with fast-time averaging and the
+// 3-D -> 2-D coupling at the first fast step.
+//
+// Kernel A (zeta range istrU-1..iend x jstrV-1..jend): free surface zeta_new,
+// Dnew and the backward-averaged zwrk/rzeta/rzeta2/rzetaSA into 2-D scratch;
+// the extrapolated fluxes DUon/DVom are rebuilt per lane from Drhs.
+// Kernel B (istrR..iendR x jstrR..jendR): zeta(knew), fast averages,
+// pressure-gradient rubar/rvbar (+ PGF_FB correction at iif=1) and the
+// momentum update ubar/vbar(knew), DU_avg1/DV_avg1.
+// Kernel C (closed edges only): u2dbc/v2dbc and the boundary flux averages.
+#include "roms_dev.h"
+
+namespace roms {
+
+struct FBCoef {
+  int kstp, kbak, kold, knew, iif, nfast;
+  double fwd, fwd1, fwd2, bkw_new, bkw, bkw1, bkw2;
+  double w1, w2;  // weight(1,iif), weight(2,iif)
+};
+
+__device__ __forceinline__ double s2d_Drhs(const Dev& d, const FBCoef& c, long ij) {
+  const Fields& F = d.f;
+  const long n2 = d.b.n2;
+  return F.h[ij] + c.fwd * F.zeta[ij + (long)(c.kstp - 1) * n2] + c.fwd1 * F.zeta[ij + (long)(c.kbak - 1) * n2] +
+         c.fwd2 * F.zeta[ij + (long)(c.kold - 1) * n2];
+}
+__device__ __forceinline__ double s2d_DUon(const Dev& d, const FBCoef& c, long ij) {
+  const Fields& F = d.f;
+  const long n2 = d.b.n2;
+  const double urhs = c.fwd * F.ubar[ij + (long)(c.kstp - 1) * n2] + c.fwd1 * F.ubar[ij + (long)(c.kbak - 1) * n2] +
+                      c.fwd2 * F.ubar[ij + (long)(c.kold - 1) * n2];
+  return 0.5 * (s2d_Drhs(d, c, ij) + s2d_Drhs(d, c, ij - 1)) * F.dn_u[ij] * (urhs);
+}
+__device__ __forceinline__ double s2d_DVom(const Dev& d, const FBCoef& c, long ij) {
+  const Fields& F = d.f;
+  const long n2 = d.b.n2, sj = d.b.nx2;
+  const double vrhs = c.fwd * F.vbar[ij + (long)(c.kstp - 1) * n2] + c.fwd1 * F.vbar[ij + (long)(c.kbak - 1) * n2] +
+                      c.fwd2 * F.vbar[ij + (long)(c.kold - 1) * n2];
+  return 0.5 * (s2d_Drhs(d, c, ij) + s2d_Drhs(d, c, ij - sj)) * F.dm_v[ij] * (vrhs);
+}
+
+__global__ void k_s2d_zeta(Dev d, Range R, FBCoef c) {
+  ROMS_IJ_OR_RETURN(R)
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const long ij = IJ(b, i, j), sj = b.nx2, n2 = b.n2;
+  const double zk = F.zeta[ij + (long)(c.kstp - 1) * n2];
+  double zn = zk + d.p.dtfast * F.pm[ij] * F.pn[ij] *
+                       (s2d_DUon(d, c, ij) - s2d_DUon(d, c, ij + 1) + s2d_DVom(d, c, ij) - s2d_DVom(d, c, ij + sj)) +
+              d.p.dtfast * F.swflx[ij];
+  zn = zn * F.rmask[ij];
+  F.s0[ij] = zn;
+  F.s1[ij] = zn + F.h[ij];
+  const double zwrk = c.bkw_new * zn + c.bkw * zk + c.bkw1 * F.zeta[ij + (long)(c.kbak - 1) * n2] +
+                      c.bkw2 * F.zeta[ij + (long)(c.kold - 1) * n2];
+  const double rzeta = (1.0 + F.rhoS[ij]) * zwrk;
+  F.s2[ij] = zwrk;
+  F.s3[ij] = rzeta;
+  F.s5[ij] = zwrk * (F.rhoS[ij] - F.rhoA[ij]);
+  F.s4[ij] = rzeta * zwrk;
+}
+
+// zetabc_tile (zetabc.F) for closed walls: zero-gradient, corners averaged
+__global__ void k_s2d_zetabc(Dev d, int phase) {
+  const Bounds& b = d.b;
+  double* zn = d.f.s0;
+  const double* rm = d.f.rmask;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (phase == 0) {
+    const int nj = b.jend - (b.jstrV - 1) + 1, ni = b.iend - (b.istrU - 1) + 1;
+    if (p < nj) {
+      const int j = b.jstrV - 1 + p;
+      if (b.west_edge) zn[IJ(b, b.istr - 1, j)] = zn[IJ(b, b.istr, j)] * rm[IJ(b, b.istr - 1, j)];
+      if (b.east_edge) zn[IJ(b, b.iend + 1, j)] = zn[IJ(b, b.iend, j)] * rm[IJ(b, b.iend + 1, j)];
+    } else if (p < nj + ni) {
+      const int i = b.istrU - 1 + p - nj;
+      if (b.south_edge) zn[IJ(b, i, b.jstr - 1)] = zn[IJ(b, i, b.jstr)] * rm[IJ(b, i, b.jstr - 1)];
+      if (b.north_edge) zn[IJ(b, i, b.jend + 1)] = zn[IJ(b, i, b.jend)] * rm[IJ(b, i, b.jend + 1)];
+    }
+  } else if (p == 0) {
+    const int is = b.istr, ie = b.iend, js = b.jstr, je = b.jend;
+    if (b.south_edge && b.west_edge) zn[IJ(b, is - 1, js - 1)] = 0.5 * (zn[IJ(b, is, js - 1)] + zn[IJ(b, is - 1, js)]);
+    if (b.south_edge && b.east_edge) zn[IJ(b, ie + 1, js - 1)] = 0.5 * (zn[IJ(b, ie, js - 1)] + zn[IJ(b, ie + 1, js)]);
+    if (b.north_edge && b.west_edge) zn[IJ(b, is - 1, je + 1)] = 0.5 * (zn[IJ(b, is, je + 1)] + zn[IJ(b, is - 1, je)]);
+    if (b.north_edge && b.east_edge) zn[IJ(b, ie + 1, je + 1)] = 0.5 * (zn[IJ(b, ie, je + 1)] + zn[IJ(b, ie + 1, je)]);
+  }
+}
+
+__device__ __forceinline__ double pgf_x(const Dev& d, long ij, long s, const double* rz, const double* rz2,
+                                        const double* rzSA, const double* zw, double dn) {
+  const Fields& F = d.f;
+  const double cff = 0.5 * d.p.g;
+  return cff * dn *
+         ((F.h[ij - s] + F.h[ij]) * (rz[ij - s] - rz[ij]) + rz2[ij - s] - rz2[ij] +
+          (F.h[ij - s] - F.h[ij]) * (rzSA[ij - s] + rzSA[ij] + 0.333333333333 * (F.rhoA[ij - s] - F.rhoA[ij]) * (zw[ij - s] - zw[ij])));
+}
+// PGF_FB correction terms at one point (iif==1)
+__device__ __forceinline__ void fb_corr(const Dev& d, const FBCoef& c, long ij, double& zwrk, double& rzeta,
+                                        double& rzeta2, double& rzetaSA) {
+  const Fields& F = d.f;
+  const double zn = F.s0[ij], zk = F.zeta[ij + (long)(c.kstp - 1) * d.b.n2];
+  zwrk = zn - zk;
+  rzeta = (1.0 + F.rhoS[ij]) * zwrk;
+  rzeta2 = rzeta * (zn + zk);
+  rzetaSA = zwrk * (F.rhoS[ij] - F.rhoA[ij]);
+}
+
+__global__ void k_s2d_mom(Dev d, Range R, FBCoef c) {
+  ROMS_IJ_OR_RETURN(R)
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const long ij = IJ(b, i, j), sj = b.nx2, n2 = b.n2;
+  const double* zn = F.s0;
+  const double* Dnew = F.s1;
+  const bool avg = i >= b.istrR && i <= b.iendR && j >= b.jstrR && j <= b.jendR;
+  if (avg) {
+    const double z = zn[ij];
+    F.zeta[ij + (long)(c.knew - 1) * n2] = z;
+    if (c.iif == 1) {
+      F.DU_avg_bak[ij] = F.DU_avg1[ij] - 0.1024390243902439 * F.DU_avg2[ij];
+      F.DV_avg_bak[ij] = F.DV_avg1[ij] - 0.1024390243902439 * F.DV_avg2[ij];
+      F.Zt_avg1[ij] = c.w1 * z;
+      F.DU_avg1[ij] = 0.0;
+      F.DV_avg1[ij] = 0.0;
+      F.DU_avg2[ij] = c.w2 * s2d_DUon(d, c, ij);
+      F.DV_avg2[ij] = c.w2 * s2d_DVom(d, c, ij);
+    } else {
+      F.Zt_avg1[ij] = F.Zt_avg1[ij] + c.w1 * z;
+      F.DU_avg2[ij] = F.DU_avg2[ij] + c.w2 * s2d_DUon(d, c, ij);
+      F.DV_avg2[ij] = F.DV_avg2[ij] + c.w2 * s2d_DVom(d, c, ij);
+    }
+  }
+  if (i < b.istr || i > b.iend || j < b.jstr || j > b.jend) return;
+  double rubar = pgf_x(d, ij, 1, F.s3, F.s4, F.s5, F.s2, F.dn_u[ij]);
+  double rvbar = pgf_x(d, ij, sj, F.s3, F.s4, F.s5, F.s2, F.dm_v[ij]);
+  double rufrc = F.rufrc[ij], rvfrc = F.rvfrc[ij];
+  if (c.iif == 1) {
+    rufrc = rufrc - rubar;
+    rvfrc = rvfrc - rvbar;
+    F.rufrc[ij] = rufrc;
+    F.rvfrc[ij] = rvfrc;
+    double zw0, rz0, rz20, sa0, zw1, rz1, rz21, sa1, zw2, rz2_, rz22, sa2;
+    fb_corr(d, c, ij, zw0, rz0, rz20, sa0);
+    fb_corr(d, c, ij - 1, zw1, rz1, rz21, sa1);
+    fb_corr(d, c, ij - sj, zw2, rz2_, rz22, sa2);
+    const double cff = 0.5 * d.p.g;
+    rubar = rubar + cff * F.dn_u[ij] *
+                        ((F.h[ij - 1] + F.h[ij]) * (rz1 - rz0) + rz21 - rz20 +
+                         (F.h[ij - 1] - F.h[ij]) * (sa1 + sa0 + 0.333333333333 * (F.rhoA[ij - 1] - F.rhoA[ij]) * (zw1 - zw0)));
+    rvbar = rvbar + cff * F.dm_v[ij] *
+                        ((F.h[ij - sj] + F.h[ij]) * (rz2_ - rz0) + rz22 - rz20 +
+                         (F.h[ij - sj] - F.h[ij]) * (sa2 + sa0 + 0.333333333333 * (F.rhoA[ij - sj] - F.rhoA[ij]) * (zw2 - zw0)));
+  }
+  const double cff = 0.5 * d.p.dtfast, cff1 = 0.5 * c.w1;
+  const long lk = (long)(c.kstp - 1) * n2;
+  const double Dstp0 = F.zeta[ij + lk] + F.h[ij];
+  if (i >= b.istrU) {
+    const double Dstpm = F.zeta[ij - 1 + lk] + F.h[ij - 1];
+    const double DUnew = ((Dstp0 + Dstpm) * F.ubar[ij + lk] +
+                          cff * (F.pm[ij] + F.pm[ij - 1]) * (F.pn[ij] + F.pn[ij - 1]) * (rubar + rufrc)) *
+                         F.umask[ij];
+    F.ubar[ij + (long)(c.knew - 1) * n2] = DUnew / (Dnew[ij] + Dnew[ij - 1]);
+    F.DU_avg1[ij] = F.DU_avg1[ij] + cff1 * F.dn_u[ij] * (DUnew);
+  }
+  if (j >= b.jstrV) {
+    const double Dstpm = F.zeta[ij - sj + lk] + F.h[ij - sj];
+    const double DVnew = ((Dstp0 + Dstpm) * F.vbar[ij + lk] +
+                          cff * (F.pm[ij] + F.pm[ij - sj]) * (F.pn[ij] + F.pn[ij - sj]) * (rvbar + rvfrc)) *
+                         F.vmask[ij];
+    F.vbar[ij + (long)(c.knew - 1) * n2] = DVnew / (Dnew[ij] + Dnew[ij - sj]);
+    F.DV_avg1[ij] = F.DV_avg1[ij] + cff1 * F.dm_v[ij] * (DVnew);
+  }
+}
+
+// u2dbc/v2dbc (closed), boundary Dnew, boundary flux averages (step2d_FB.F:444-529)
+__global__ void k_s2d_edges(Dev d, FBCoef c, int phase) {
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const long n2 = b.n2, kn = (long)(c.knew - 1) * n2;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  const int L = b.nx2 > b.Mm + 4 ? b.nx2 : b.Mm + 4;  // edge lanes per side
+  const int side = p / L, q = p - side * L;
+  if (side > 3) return;
+  double* ub = F.ubar + kn;
+  double* vb = F.vbar + kn;
+  double* Dn = F.s1;
+  const double g2 = d.p.gamma2;
+  if (phase == 0) {  // wall-normal components
+    if (side == 0 && b.west_edge && q <= b.jend - b.jstr) ub[IJ(b, b.istr, b.jstr + q)] = 0.0;
+    if (side == 1 && b.east_edge && q <= b.jend - b.jstr) ub[IJ(b, b.iend + 1, b.jstr + q)] = 0.0;
+    if (side == 2 && b.south_edge && q <= b.iend - b.istr) vb[IJ(b, b.istr + q, b.jstr)] = 0.0;
+    if (side == 3 && b.north_edge && q <= b.iend - b.istr) vb[IJ(b, b.istr + q, b.jend + 1)] = 0.0;
+  } else if (phase == 1) {  // tangential components + boundary Dnew
+    if (side == 2 && b.south_edge && q <= b.iendR - b.istr) {
+      const int i = b.istr + q;
+      ub[IJ(b, i, b.jstr - 1)] = g2 * ub[IJ(b, i, b.jstr)] * F.umask[IJ(b, i, b.jstr - 1)];
+    }
+    if (side == 3 && b.north_edge && q <= b.iendR - b.istr) {
+      const int i = b.istr + q;
+      ub[IJ(b, i, b.jend + 1)] = g2 * ub[IJ(b, i, b.jend)] * F.umask[IJ(b, i, b.jend + 1)];
+    }
+    if (side == 0 && b.west_edge && q <= b.jendR - b.jstr) {
+      const int j = b.jstr + q;
+      vb[IJ(b, b.istr - 1, j)] = g2 * vb[IJ(b, b.istr, j)] * F.vmask[IJ(b, b.istr - 1, j)];
+    }
+    if (side == 1 && b.east_edge && q <= b.jendR - b.jstr) {
+      const int j = b.jstr + q;
+      vb[IJ(b, b.iend + 1, j)] = g2 * vb[IJ(b, b.iend, j)] * F.vmask[IJ(b, b.iend + 1, j)];
+    }
+    if (side == 0 && b.west_edge && q <= b.jendR - (b.jstr - 1)) {
+      const long o = IJ(b, b.istr - 1, b.jstr - 1 + q);
+      Dn[o] = F.h[o] + F.s0[o];
+    }
+    if (side == 1 && b.east_edge && q <= b.jendR - (b.jstr - 1)) {
+      const long o = IJ(b, b.iend + 1, b.jstr - 1 + q);
+      Dn[o] = F.h[o] + F.s0[o];
+    }
+    if (side == 2 && b.south_edge && q <= b.iendR - (b.istr - 1)) {
+      const long o = IJ(b, b.istr - 1 + q, b.jstr - 1);
+      Dn[o] = F.h[o] + F.s0[o];
+    }
+    if (side == 3 && b.north_edge && q <= b.iendR - (b.istr - 1)) {
+      const long o = IJ(b, b.istr - 1 + q, b.jend + 1);
+      Dn[o] = F.h[o] + F.s0[o];
+    }
+  } else {  // boundary fast-time-averaged fluxes
+    const double cff1 = 0.5 * c.w1;
+    const long sj = b.nx2;
+    if (side == 0 && b.west_edge) {
+      const int iu = b.istrU - 1;
+      if (q <= b.jendR - b.jstrR) {
+        const long o = IJ(b, iu, b.jstrR + q);
+        F.DU_avg1[o] = F.DU_avg1[o] + cff1 * (Dn[o] + Dn[o - 1]) * (ub[o]) * F.dn_u[o];
+      }
+      if (q <= b.jend - b.jstrV) {
+        const long o = IJ(b, b.istr - 1, b.jstrV + q);
+        F.DV_avg1[o] = F.DV_avg1[o] + cff1 * (Dn[o] + Dn[o - sj]) * (vb[o]) * F.dm_v[o];
+      }
+    }
+    if (side == 1 && b.east_edge) {
+      if (q <= b.jendR - b.jstrR) {
+        const long o = IJ(b, b.iend + 1, b.jstrR + q);
+        F.DU_avg1[o] = F.DU_avg1[o] + cff1 * (Dn[o] + Dn[o - 1]) * (ub[o]) * F.dn_u[o];
+      }
+      if (q <= b.jend - b.jstrV) {
+        const long o = IJ(b, b.iend + 1, b.jstrV + q);
+        F.DV_avg1[o] = F.DV_avg1[o] + cff1 * (Dn[o] + Dn[o - sj]) * (vb[o]) * F.dm_v[o];
+      }
+    }
+    if (side == 2 && b.south_edge) {
+      if (q <= b.iend - b.istrU) {
+        const long o = IJ(b, b.istrU + q, b.jstr - 1);
+        F.DU_avg1[o] = F.DU_avg1[o] + cff1 * (Dn[o] + Dn[o - 1]) * (ub[o]) * F.dn_u[o];
+      }
+      if (q <= b.iendR - b.istrR) {
+        const long o = IJ(b, b.istrR + q, b.jstrV - 1);
+        F.DV_avg1[o] = F.DV_avg1[o] + cff1 * (Dn[o] + Dn[o - sj]) * (vb[o]) * F.dm_v[o];
+      }
+    }
+    if (side == 3 && b.north_edge) {
+      if (q <= b.iend - b.istrU) {
+        const long o = IJ(b, b.istrU + q, b.jend + 1);
+        F.DU_avg1[o] = F.DU_avg1[o] + cff1 * (Dn[o] + Dn[o - 1]) * (ub[o]) * F.dn_u[o];
+      }
+      if (q <= b.iendR - b.istrR) {
+        const long o = IJ(b, b.istrR + q, b.jend + 1);
+        F.DV_avg1[o] = F.DV_avg1[o] + cff1 * (Dn[o] + Dn[o - sj]) * (vb[o]) * F.dm_v[o];
+      }
+    }
+  }
+}
+
+__global__ void k_s2d_last(Dev d, Range R, int knew) {
+  ROMS_IJ_OR_RETURN(R)
+  const long ij = IJ(d.b, i, j);
+  d.f.zeta[ij + (long)(knew - 1) * d.b.n2] = d.f.Zt_avg1[ij];
+}
+
+void launch_step2d(const Dev& d, hipStream_t s, const Tlev& t, const double* w1, const double* w2) {
+  const Bounds& b = d.b;
+  FBCoef c;
+  c.kstp = t.kstp; c.knew = t.knew; c.iif = t.iif; c.nfast = t.nfast;
+  if (t.iif == 1) {
+    c.kbak = t.kstp; c.kold = t.kstp;
+    c.fwd = 1.0; c.fwd1 = 0.0; c.fwd2 = 0.0;
+    c.bkw_new = 0.0; c.bkw = 1.0; c.bkw1 = 0.0; c.bkw2 = 0.0;
+  } else if (t.iif == 2) {
+    c.kbak = t.kstp - 1; if (c.kbak < 1) c.kbak = 4;
+    c.kold = c.kbak;
+    c.fwd = 1.0; c.fwd1 = 0.0; c.fwd2 = 0.0;
+    c.bkw_new = 1.0833333333333; c.bkw = -0.1666666666666; c.bkw1 = 0.0833333333333; c.bkw2 = 0.0;
+  } else {
+    c.kbak = t.kstp - 1; if (c.kbak < 1) c.kbak = 4;
+    c.kold = c.kbak - 1; if (c.kold < 1) c.kold = 4;
+    c.fwd = 1.781105; c.fwd1 = -1.06221; c.fwd2 = 0.281105;
+    c.bkw_new = 0.614; c.bkw = 0.285; c.bkw1 = 0.088; c.bkw2 = 0.013;
+  }
+  c.w1 = w1[t.iif - 1];
+  c.w2 = w2[t.iif - 1];
+  Range RA{b.istrU - 1, b.iend, b.jstrV - 1, b.jend};
+  hipLaunchKernelGGL(k_s2d_zeta, grid_of(RA), dim3(kBX, kBY), 0, s, d, RA, c);
+  const bool closed = b.west_edge || b.east_edge || b.south_edge || b.north_edge;
+  if (closed) {
+    const int n = (b.jend - b.jstrV + 2) + (b.iend - b.istrU + 2);
+    hipLaunchKernelGGL(k_s2d_zetabc, dim3((n + 255) / 256), dim3(256), 0, s, d, 0);
+    hipLaunchKernelGGL(k_s2d_zetabc, dim3(1), dim3(64), 0, s, d, 1);
+  }
+  Range RB{b.istrR, b.iendR, b.jstrR, b.jendR};
+  hipLaunchKernelGGL(k_s2d_mom, grid_of(RB), dim3(kBX, kBY), 0, s, d, RB, c);
+  if (closed) {
+    const int L = b.nx2 > b.Mm + 4 ? b.nx2 : b.Mm + 4;
+    for (int ph = 0; ph < 3; ph++)
+      hipLaunchKernelGGL(k_s2d_edges, dim3((4 * L + 255) / 256), dim3(256), 0, s, d, c, ph);
+  }
+  if (t.iif == t.nfast) {
+    hipLaunchKernelGGL(k_s2d_last, grid_of(RB), dim3(kBX, kBY), 0, s, d, RB, t.knew);
+    launch_set_depth(d, s, t);
+  }
+  launch_exchange(d, s, d.f.zeta + (long)(t.knew - 1) * b.n2, 1);
+  launch_exchange(d, s, d.f.ubar + (long)(t.knew - 1) * b.n2, 1);
+  launch_exchange(d, s, d.f.vbar + (long)(t.knew - 1) * b.n2, 1);
+}
+
+}  // namespace roms

@@ -1,0 +1,270 @@
+// k_step3d_uv.hip -- corrector momentum: step3d_uv1 (step3d_uv1.F:23-534),
+// visc3d (visc3d_S.F:18-131) and the 2-D/3-D coupling step3d_uv2
+// (step3d_uv2.F:18-786, IMPLICIT_BOTTOM_DRAG branch).
+#include "k_common.h"
+
+namespace roms {
+
+void launch_uv_horiz(const Dev& d, hipStream_t s, int nrhs, int up);
+
+// ---- step3d_uv1: implicit viscosity with implicit bottom drag r_D, result
+// stored as Hz*u in u(nnew); rufrc = vertical integral of ru + stresses ----
+__device__ void uv1_solve(const Dev& d, int i, int j, int dir, int nnew) {
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const int N = b.N;
+  const double dt = d.p.dt;
+  const long n2 = b.n2, ij = IJ(b, i, j);
+  const long s = dir == 0 ? 1 : b.nx2;
+  double* Un = (dir == 0 ? F.u : F.v) + (long)(nnew - 1) * b.n3;
+  const double* rr = dir == 0 ? F.ru : F.rv;
+  const double sstr = dir == 0 ? F.sustr[ij] : F.svstr[ij];
+  double* CFs = F.c1;
+  double* DCs = F.c2;
+  const double* Hz = F.Hz;
+  const double* Akv = F.Akv;
+  const double DC0 = dt * 0.25 * (F.pm[ij] + F.pm[ij - s]) * (F.pn[ij] + F.pn[ij - s]);
+  auto hz = [&](int k) { return Hz[ij + (long)(k - 1) * n2]; };
+  auto hzm = [&](int k) { return Hz[ij - s + (long)(k - 1) * n2]; };
+  auto uk = [&](int k) { return Un[ij + (long)(k - 1) * n2] + DC0 * rr[ij + (long)(k - 1) * n2]; };
+  double FCk = 2.0 * dt * (Akv[ij + (long)(N - 1) * n2] + Akv[ij - s + (long)(N - 1) * n2]) /
+               (hz(N) + hzm(N) + hz(N - 1) + hzm(N - 1));
+  double WCk = DC0 * 0.5 * (F.Wi[ij + (long)(N - 1) * n2] + F.Wi[ij - s + (long)(N - 1) * n2]);
+  double cff = 1.0 / (0.5 * (hz(N) + hzm(N)) + FCk - fmin0(WCk));
+  double CFk = cff * (FCk + fmax0(WCk));
+  double DCk1 = cff * (Un[ij + (long)(N - 1) * n2] + DC0 * rr[ij + (long)(N - 1) * n2] + dt * sstr);
+  DCs[ij + (long)N * n2] = DCk1;
+  CFs[ij + (long)(N - 1) * n2] = CFk;
+  for (int k = N - 1; k >= 2; k--) {
+    const double FCl = 2.0 * dt * (Akv[ij + (long)(k - 1) * n2] + Akv[ij - s + (long)(k - 1) * n2]) /
+                       (hz(k) + hzm(k) + hz(k - 1) + hzm(k - 1));
+    const double WCl = DC0 * 0.5 * (F.Wi[ij + (long)(k - 1) * n2] + F.Wi[ij - s + (long)(k - 1) * n2]);
+    cff = 1.0 / (0.5 * (hz(k) + hzm(k)) + FCl - fmin0(WCl) + FCk + fmax0(WCk) - CFk * (FCk - fmin0(WCk)));
+    const double CFl = cff * (FCl + fmax0(WCl));
+    const double DCk = cff * (uk(k) + DCk1 * (FCk - fmin0(WCk)));
+    CFs[ij + (long)(k - 1) * n2] = CFl;
+    DCs[ij + (long)k * n2] = DCk;
+    DCk1 = DCk; FCk = FCl; WCk = WCl; CFk = CFl;
+  }
+  const double rD = F.r_D[ij], rDm = F.r_D[ij - s];
+  double dc = (uk(1) + DCk1 * (FCk - fmin0(WCk))) /
+              (0.5 * (hz(1) + hzm(1)) + 0.5 * dt * (rD + rDm) + FCk + fmax0(WCk) - CFk * (FCk - fmin0(WCk)));
+  Un[ij] = dc * 0.5 * (hz(1) + hzm(1));
+  const double dmdn = dir == 0 ? F.dm_u[ij] * F.dn_u[ij] : F.dm_v[ij] * F.dn_v[ij];
+  double frc = rr[ij] + dmdn * (sstr - 0.5 * (rDm + rD) * dc);
+  for (int k = 2; k <= N; k++) {
+    dc = DCs[ij + (long)k * n2] + CFs[ij + (long)(k - 1) * n2] * dc;
+    Un[ij + (long)(k - 1) * n2] = dc * 0.5 * (hz(k) + hzm(k));
+    frc = frc + rr[ij + (long)(k - 1) * n2];
+  }
+  if (dir == 0) F.rufrc[ij] = frc;
+  else F.rvfrc[ij] = frc;
+}
+
+__global__ void k_uv1(Dev d, Range R, int nnew, int nrhs) {
+  ROMS_IJ_OR_RETURN(R)
+  const Bounds& b = d.b;
+  if (i >= b.istrU && i <= b.iend) {
+    uv_vert_rhs(d, i, j, nrhs, 0, d.f.c0, d.f.c1);
+    uv1_solve(d, i, j, 0, nnew);
+  }
+  if (j >= b.jstrV) {
+    uv_vert_rhs(d, i, j, nrhs, 1, d.f.c0, d.f.c1);
+    uv1_solve(d, i, j, 1, nnew);
+  }
+}
+
+void launch_step3d_uv1(const Dev& d, hipStream_t s, const Tlev& t) {
+  const Bounds& b = d.b;
+  launch_uv_horiz(d, s, t.nrhs, 1);
+  Range R{b.istr, b.iend, b.jstr, b.jend};
+  hipLaunchKernelGGL(k_uv1, grid_of(R), dim3(kBX, kBY), 0, s, d, R, t.nnew, t.nrhs);
+}
+
+// ---- visc3d: harmonic viscosity along S; adds dt*cff to u,v(indx) (Hz*u)
+// and cff to rufrc,rvfrc.  Each lane forms the two rho-point and two
+// psi-point stress components around its u (v) point. ----
+__device__ __forceinline__ void visc_rho(const Dev& d, int i, int j, int k, int nstp, double& UFx, double& VFe) {
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const long ij = IJ(b, i, j), o = ij + (long)(k - 1) * b.n2, l = (long)(nstp - 1) * b.n3;
+  const double* pm = F.pm;
+  const double* pn = F.pn;
+  const long sj = b.nx2;
+  const double cff = 0.5 * F.Hz[o] * F.visc2_r[ij] *
+                     (F.dn_r[ij] * pm[ij] * ((pn[ij] + pn[ij + 1]) * F.u[o + 1 + l] - (pn[ij - 1] + pn[ij]) * F.u[o + l]) -
+                      F.dm_r[ij] * pn[ij] * ((pm[ij] + pm[ij + sj]) * F.v[o + sj + l] - (pm[ij - sj] + pm[ij]) * F.v[o + l]));
+  UFx = cff * F.dn_r[ij] * F.dn_r[ij];
+  VFe = -cff * F.dm_r[ij] * F.dm_r[ij];
+}
+__device__ __forceinline__ void visc_psi(const Dev& d, int i, int j, int k, int nstp, double& UFe, double& VFx) {
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const long sj = b.nx2;
+  const long ij = IJ(b, i, j), o = ij + (long)(k - 1) * b.n2, l = (long)(nstp - 1) * b.n3;
+  const double* pm = F.pm;
+  const double* pn = F.pn;
+  const double cff =
+      0.125 * (F.Hz[o - 1] + F.Hz[o] + F.Hz[o - 1 - sj] + F.Hz[o - sj]) * F.visc2_p[ij] *
+      (0.25 * (pm[ij - 1] + pm[ij] + pm[ij - 1 - sj] + pm[ij - sj]) * F.dn_p[ij] *
+           ((pn[ij - sj] + pn[ij]) * F.v[o + l] - (pn[ij - 1 - sj] + pn[ij - 1]) * F.v[o - 1 + l]) +
+       0.25 * (pn[ij - 1] + pn[ij] + pn[ij - 1 - sj] + pn[ij - sj]) * F.dm_p[ij] *
+           ((pm[ij - 1] + pm[ij]) * F.u[o + l] - (pm[ij - 1 - sj] + pm[ij - sj]) * F.u[o - sj + l])) *
+      F.pmask[ij];
+  UFe = cff * F.dm_p[ij] * F.dm_p[ij];
+  VFx = cff * F.dn_p[ij] * F.dn_p[ij];
+}
+
+__global__ void k_visc3d(Dev d, Range R, int nstp) {
+  ROMS_IJ_OR_RETURN(R)
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const int indx = 3 - nstp;
+  const long ij = IJ(b, i, j), sj = b.nx2;
+  const double* pm = F.pm;
+  const double* pn = F.pn;
+  const bool du = i >= b.istrU && i <= b.iend;
+  const bool dv = j >= b.jstrV && j <= b.jend;
+  double frcu = F.rufrc[ij], frcv = F.rvfrc[ij];
+  for (int k = 1; k <= b.N; k++) {
+    const long o = ij + (long)(k - 1) * b.n2;
+    if (du) {
+      double UFx0, UFx1, VFe_, UFe0, UFe1, VFx_;
+      visc_rho(d, i, j, k, nstp, UFx0, VFe_);
+      visc_rho(d, i - 1, j, k, nstp, UFx1, VFe_);
+      visc_psi(d, i, j, k, nstp, UFe0, VFx_);
+      visc_psi(d, i, j + 1, k, nstp, UFe1, VFx_);
+      const double cff = 0.125 * (pm[ij - 1] + pm[ij]) * (pn[ij - 1] + pn[ij]) *
+                         ((pn[ij - 1] + pn[ij]) * (UFx0 - UFx1) + (pm[ij - 1] + pm[ij]) * (UFe1 - UFe0));
+      frcu = frcu + cff;
+      F.u[o + (long)(indx - 1) * b.n3] = F.u[o + (long)(indx - 1) * b.n3] + d.p.dt * cff;
+    }
+    if (dv) {
+      double VFe0, VFe1, UFx_, VFx0, VFx1, UFe_;
+      visc_rho(d, i, j, k, nstp, UFx_, VFe0);
+      visc_rho(d, i, j - 1, k, nstp, UFx_, VFe1);
+      visc_psi(d, i, j, k, nstp, UFe_, VFx0);
+      visc_psi(d, i + 1, j, k, nstp, UFe_, VFx1);
+      const double cff = 0.125 * (pm[ij] + pm[ij - sj]) * (pn[ij] + pn[ij - sj]) *
+                         ((pn[ij - sj] + pn[ij]) * (VFx1 - VFx0) + (pm[ij - sj] + pm[ij]) * (VFe0 - VFe1));
+      frcv = frcv + cff;
+      F.v[o + (long)(indx - 1) * b.n3] = F.v[o + (long)(indx - 1) * b.n3] + d.p.dt * cff;
+    }
+  }
+  if (du) F.rufrc[ij] = frcu;
+  if (dv) F.rvfrc[ij] = frcv;
+}
+
+void launch_visc3d(const Dev& d, hipStream_t s, const Tlev& t) {
+  const Bounds& b = d.b;
+  Range R{b.istr, b.iend, b.jstr, b.jend};
+  hipLaunchKernelGGL(k_visc3d, grid_of(R), dim3(kBX, kBY), 0, s, d, R, t.nstp);
+}
+
+// ---- step3d_uv2 part 1: convert Hz*u to u and remove the mismatch against
+// the fast-time-averaged barotropic flux DU_avg1 (at n+1 depths) ----
+__global__ void k_uv2_couple(Dev d, Range R, int nnew) {
+  ROMS_IJ_OR_RETURN(R)
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const int N = b.N;
+  const long ij = IJ(b, i, j), n2 = b.n2;
+  for (int dir = 0; dir < 2; dir++) {
+    if (dir == 0 && !(i >= b.istrU)) continue;
+    if (dir == 1 && !(j >= b.jstrV)) continue;
+    const long s = dir == 0 ? 1 : b.nx2;
+    double* Un = (dir == 0 ? F.u : F.v) + (long)(nnew - 1) * b.n3;
+    const double dn = dir == 0 ? F.dn_u[ij] : F.dm_v[ij];
+    const double avg1 = dir == 0 ? F.DU_avg1[ij] : F.DV_avg1[ij];
+    const double msk = dir == 0 ? F.umask[ij] : F.vmask[ij];
+    long o = ij + (long)(N - 1) * n2;
+    double CF0 = 0.5 * (F.Hz[o] + F.Hz[o - s]);
+    double DC0 = Un[o];
+    Un[o] = Un[o] / CF0;
+    for (int k = N - 1; k >= 1; k--) {
+      o = ij + (long)(k - 1) * n2;
+      const double cff = 0.5 * (F.Hz[o] + F.Hz[o - s]);
+      CF0 = CF0 + cff;
+      DC0 = DC0 + Un[o];
+      Un[o] = Un[o] / cff;
+    }
+    DC0 = (DC0 * dn - avg1) / (CF0 * dn);
+    for (int k = 1; k <= N; k++) {
+      o = ij + (long)(k - 1) * n2;
+      Un[o] = (Un[o] - DC0) * msk;
+    }
+  }
+}
+
+// ---- step3d_uv2 part 2: ubar,vbar(knew) from DU_avg1; corrected fluxes
+// FlxU = DELTA*FlxU + EPSIL*Hz_u*dn_u*(u(nstp)+u(nnew)), mismatch vs DU_avg2 ----
+__global__ void k_uv2_flux(Dev d, Range R, int nnew, int nstp, int knew, int iu0, int iu1, int iv0, int iv1) {
+  ROMS_IJ_OR_RETURN(R)
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const int N = b.N;
+  const long ij = IJ(b, i, j), n2 = b.n2;
+  const double DELTA = 0.28, EPSIL = 0.36;
+  for (int dir = 0; dir < 2; dir++) {
+    if (dir == 0 && !(i >= iu0 && i <= iu1)) continue;
+    if (dir == 1 && !(i >= iv0 && i <= iv1 && j >= b.jstr)) continue;
+    const long s = dir == 0 ? 1 : b.nx2;
+    double* Un = (dir == 0 ? F.u : F.v) + (long)(nnew - 1) * b.n3;
+    const double* Us = (dir == 0 ? F.u : F.v) + (long)(nstp - 1) * b.n3;
+    double* Flx = dir == 0 ? F.FlxU : F.FlxV;
+    const double dn = dir == 0 ? F.dn_u[ij] : F.dm_v[ij];
+    const double avg1 = dir == 0 ? F.DU_avg1[ij] : F.DV_avg1[ij];
+    const double avg2 = dir == 0 ? F.DU_avg2[ij] : F.DV_avg2[ij];
+    const double msk = dir == 0 ? F.umask[ij] : F.vmask[ij];
+    auto DCk = [&](int k) { const long o = ij + (long)(k - 1) * n2; return 0.5 * (F.Hz[o] + F.Hz[o - s]) * dn; };
+    long o = ij + (long)(N - 1) * n2;
+    const double dcN = DCk(N);
+    double DC0 = dcN, FC0 = dcN * Un[o];
+    for (int k = N - 1; k >= 1; k--) {
+      o = ij + (long)(k - 1) * n2;
+      const double dck = DCk(k);
+      DC0 = DC0 + dck;
+      FC0 = FC0 + dck * Un[o];
+    }
+    DC0 = 1.0 / DC0;
+    if (dir == 0) F.ubar[IJL(b, i, j, knew)] = DC0 * avg1;
+    else F.vbar[IJL(b, i, j, knew)] = DC0 * avg1;
+    FC0 = DC0 * (FC0 - avg1);
+    double CF0 = 0.0;
+    double* CFs = F.c0;
+    for (int k = N; k >= 1; k--) {
+      o = ij + (long)(k - 1) * n2;
+      const double un = (Un[o] - FC0) * msk;
+      Un[o] = un;
+      const double cfk = DELTA * Flx[o] + EPSIL * DCk(k) * (Us[o] + un);
+      CFs[ij + (long)k * n2] = cfk;
+      CF0 = CF0 + cfk;
+    }
+    CF0 = DC0 * (CF0 - avg2);
+    for (int k = 1; k <= N; k++) {
+      o = ij + (long)(k - 1) * n2;
+      Flx[o] = CFs[ij + (long)k * n2] - DCk(k) * CF0;
+    }
+  }
+}
+
+void launch_step3d_uv2(const Dev& d, hipStream_t s, const Tlev& t) {
+  const Bounds& b = d.b;
+  Range R1{b.istr, b.iend, b.jstr, b.jend};
+  hipLaunchKernelGGL(k_uv2_couple, grid_of(R1), dim3(kBX, kBY), 0, s, d, R1, t.nnew);
+  launch_u3dbc(d, s, t);
+  launch_v3dbc(d, s, t);
+  const int iu0 = b.istr, iu1 = b.ew_periodic ? b.iend : b.iendR;
+  const int iv0 = b.ew_periodic ? b.istr : b.istrR, iv1 = b.ew_periodic ? b.iend : b.iendR;
+  const int j0 = b.ns_periodic ? b.jstr : b.jstrR, j1 = b.ns_periodic ? b.jend : b.jendR;
+  Range R2{iv0 < iu0 ? iv0 : iu0, iu1 > iv1 ? iu1 : iv1, j0, j1};
+  hipLaunchKernelGGL(k_uv2_flux, grid_of(R2), dim3(kBX, kBY), 0, s, d, R2, t.nnew, t.nstp, t.knew, iu0, iu1, iv0, iv1);
+  launch_exchange(d, s, d.f.FlxU, b.N);
+  launch_exchange(d, s, d.f.u + (long)(t.nnew - 1) * b.n3, b.N);
+  launch_exchange(d, s, d.f.ubar + (long)(t.knew - 1) * b.n2, 1);
+  launch_exchange(d, s, d.f.FlxV, b.N);
+  launch_exchange(d, s, d.f.v + (long)(t.nnew - 1) * b.n3, b.N);
+  launch_exchange(d, s, d.f.vbar + (long)(t.knew - 1) * b.n2, 1);
+}
+
+}  // namespace roms

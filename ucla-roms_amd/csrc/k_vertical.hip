@@ -1,0 +1,396 @@
+// k_vertical.hip -- column kernels: set_depth, set_HUV, set_HUV1, omega, rho_eos.
+//
+// One lane owns one (i,j) water column and walks k in registers; lanes of a
+// wavefront are 64 consecutive i, so every level access is one coalesced
+// 512-byte row.  Arithmetic order follows the reference statements so FP64
+// results match the CPU reference bit for bit (built with -ffp-contract=off).
+#include "roms_dev.h"
+
+namespace roms {
+
+// ---------------------------------------------------------------------------
+// set_depth_tile (set_depth.F:16-186): z_w, z_r, Hz from zeta(knew); at iic=0
+// also hinv and the initial fast-time fluxes DU_avg1/DV_avg1.
+// ---------------------------------------------------------------------------
+__global__ void k_set_depth(Dev d, Range R, int iic, int knew) {
+  ROMS_IJ_OR_RETURN(R)
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const long ij = IJ(b, i, j);
+  if (iic == 0) {
+    F.hinv[ij] = 1.0 / (F.h[ij] + d.p.hc);
+    if (i >= b.istr)
+      F.DU_avg1[ij] = 0.5 * (F.h[IJ(b, i - 1, j)] + F.h[ij] + F.zeta[IJL(b, i, j, 1)] + F.zeta[IJL(b, i - 1, j, 1)]) *
+                      F.dn_u[ij] * (F.ubar[IJL(b, i, j, 1)]);
+    if (j >= b.jstr)
+      F.DV_avg1[ij] = 0.5 * (F.h[ij] + F.h[IJ(b, i, j - 1)] + F.zeta[IJL(b, i, j, 1)] + F.zeta[IJL(b, i, j - 1, 1)]) *
+                      F.dm_v[ij] * (F.vbar[IJL(b, i, j, 1)]);
+  }
+  const int N = b.N;
+  const double hc = d.p.hc, ds = 1.0 / (double)N;
+  const double hh = F.h[ij];
+  const double hi = iic == 0 ? 1.0 / (hh + hc) : F.hinv[ij];
+  const double z = F.zeta[IJL(b, i, j, knew)];
+  double zw_prev = -hh;
+  F.z_w[ij] = zw_prev;
+  for (int k = 1; k <= N; k++) {
+    const double cff_w = hc * ds * (double)(k - N);
+    const double cff_r = hc * ds * ((double)(k - N) - 0.5);
+    const double zw = z + (z + hh) * (cff_w + F.Cs_w[k] * hh) * hi;
+    const double zr = z + (z + hh) * (cff_r + F.Cs_r[k] * hh) * hi;
+    F.z_w[ij + (long)k * b.n2] = zw;
+    F.z_r[ij + (long)(k - 1) * b.n2] = zr;
+    F.Hz[ij + (long)(k - 1) * b.n2] = zw - zw_prev;
+    zw_prev = zw;
+  }
+}
+
+void launch_set_depth(const Dev& d, hipStream_t s, const Tlev& t) {
+  const Bounds& b = d.b;
+  Range R{b.istrR, b.iendR, b.jstrR, b.jendR};
+  hipLaunchKernelGGL(k_set_depth, grid_of(R), dim3(kBX, kBY), 0, s, d, R, t.iic, t.knew);
+  if (t.iic == 0) launch_exchange(d, s, d.f.hinv, 1);
+  launch_exchange(d, s, d.f.z_w, b.N + 1);
+  launch_exchange(d, s, d.f.z_r, b.N);
+  launch_exchange(d, s, d.f.Hz, b.N);
+}
+
+// ---------------------------------------------------------------------------
+// set_HUV_tile (set_depth.F:190-234)
+// ---------------------------------------------------------------------------
+__global__ void k_set_huv(Dev d, Range R, int nrhs) {
+  ROMS_IJ_OR_RETURN(R)
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const bool du = i >= b.istr && i <= b.iendR && j >= b.jstrR && j <= b.jendR;
+  const bool dv = i >= b.istrR && i <= b.iendR && j >= b.jstr && j <= b.jendR;
+  const long ij = IJ(b, i, j);
+  for (int k = 1; k <= b.N; k++) {
+    const long o = ij + (long)(k - 1) * b.n2;
+    const double hz = F.Hz[o];
+    if (du) {
+      const double hzm = F.Hz[o - 1];
+      F.FlxU[o] = 0.5 * (hz + hzm) * F.dn_u[ij] * (F.u[o + (long)(nrhs - 1) * b.n3]);
+      F.Hz_u[o] = 0.5 * (hz + hzm);
+    }
+    if (dv) {
+      const double hzm = F.Hz[o - b.nx2];
+      F.FlxV[o] = 0.5 * (hz + hzm) * F.dm_v[ij] * (F.v[o + (long)(nrhs - 1) * b.n3]);
+      F.Hz_v[o] = 0.5 * (hz + hzm);
+    }
+  }
+}
+
+void launch_set_huv(const Dev& d, hipStream_t s, const Tlev& t) {
+  const Bounds& b = d.b;
+  Range R{b.istrR < b.istr ? b.istrR : b.istr, b.iendR, b.jstrR < b.jstr ? b.jstrR : b.jstr, b.jendR};
+  hipLaunchKernelGGL(k_set_huv, grid_of(R), dim3(kBX, kBY), 0, s, d, R, t.nrhs);
+  launch_exchange(d, s, d.f.FlxU, b.N);
+  launch_exchange(d, s, d.f.FlxV, b.N);
+}
+
+// ---------------------------------------------------------------------------
+// set_HUV1_tile (set_depth.F:239-422): remove the barotropic mismatch of
+// u,v(nnew) against NOW/MID/BAK-extrapolated DU_avg's, recompute FlxU,FlxV.
+// ---------------------------------------------------------------------------
+__global__ void k_set_huv1(Dev d, Range R, int nnew, int first) {
+  ROMS_IJ_OR_RETURN(R)
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const double NOW = 3.63, MID = 4.47, BAK = 2.05;
+  const int N = b.N;
+  const long ij = IJ(b, i, j);
+  if (i >= b.istr && i <= b.iendR && j >= b.jstrR && j <= b.jendR) {
+    const double dn = F.dn_u[ij];
+    double* u = F.u + (long)(nnew - 1) * b.n3;
+    long o = ij + (long)(N - 1) * b.n2;
+    double dcN = 0.5 * (F.Hz[o] + F.Hz[o - 1]) * dn;
+    double DC0 = dcN, FC0 = dcN * u[o];
+    for (int k = N - 1; k >= 1; k--) {
+      o = ij + (long)(k - 1) * b.n2;
+      const double dck = 0.5 * (F.Hz[o] + F.Hz[o - 1]) * dn;
+      DC0 = DC0 + dck;
+      FC0 = FC0 + dck * u[o];
+    }
+    if (first) FC0 = (FC0 - F.DU_avg1[ij]) / DC0;
+    else FC0 = (FC0 - NOW * F.DU_avg1[ij] + MID * F.DU_avg2[ij] - BAK * F.DU_avg_bak[ij]) / DC0;
+    const double um = F.umask[ij];
+    for (int k = 1; k <= N; k++) {
+      o = ij + (long)(k - 1) * b.n2;
+      const double dck = 0.5 * (F.Hz[o] + F.Hz[o - 1]) * dn;
+      const double un = (u[o] - FC0) * um;
+      u[o] = un;
+      F.FlxU[o] = dck * (un);
+    }
+  }
+  if (i >= b.istrR && i <= b.iendR && j >= b.jstr && j <= b.jendR) {
+    const double dm = F.dm_v[ij];
+    double* v = F.v + (long)(nnew - 1) * b.n3;
+    long o = ij + (long)(N - 1) * b.n2;
+    double dcN = 0.5 * (F.Hz[o] + F.Hz[o - b.nx2]) * dm;
+    double DC0 = dcN, FC0 = dcN * v[o];
+    for (int k = N - 1; k >= 1; k--) {
+      o = ij + (long)(k - 1) * b.n2;
+      const double dck = 0.5 * (F.Hz[o] + F.Hz[o - b.nx2]) * dm;
+      DC0 = DC0 + dck;
+      FC0 = FC0 + dck * v[o];
+    }
+    if (first) FC0 = (FC0 - F.DV_avg1[ij]) / DC0;
+    else FC0 = (FC0 - NOW * F.DV_avg1[ij] + MID * F.DV_avg2[ij] - BAK * F.DV_avg_bak[ij]) / DC0;
+    const double vm = F.vmask[ij];
+    for (int k = 1; k <= N; k++) {
+      o = ij + (long)(k - 1) * b.n2;
+      const double dck = 0.5 * (F.Hz[o] + F.Hz[o - b.nx2]) * dm;
+      const double vn = (v[o] - FC0) * vm;
+      v[o] = vn;
+      F.FlxV[o] = dck * (vn);
+    }
+  }
+}
+
+void launch_set_huv1(const Dev& d, hipStream_t s, const Tlev& t) {
+  const Bounds& b = d.b;
+  Range R{b.istrR < b.istr ? b.istrR : b.istr, b.iendR, b.jstrR < b.jstr ? b.jstrR : b.jstr, b.jendR};
+  hipLaunchKernelGGL(k_set_huv1, grid_of(R), dim3(kBX, kBY), 0, s, d, R, t.nnew, (int)(t.iic == t.forw_start));
+  launch_exchange(d, s, d.f.FlxU, b.N);
+  launch_exchange(d, s, d.f.FlxV, b.N);
+  launch_exchange(d, s, d.f.u + (long)(t.nnew - 1) * b.n3, b.N);
+  launch_exchange(d, s, d.f.v + (long)(t.nnew - 1) * b.n3, b.N);
+}
+
+// ---------------------------------------------------------------------------
+// omega_tile (omega.F:17-236): bottom-up continuity, grid-motion removal,
+// Courant-limited explicit/implicit split of the vertical flux (We/Wi).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double omega_cx(const Bounds& b, const Fields& F, long o) {
+  return fmax0(F.FlxU[o + 1]) - fmin0(F.FlxU[o]) + fmax0(F.FlxV[o + b.nx2]) - fmin0(F.FlxV[o]);
+}
+
+__global__ void k_omega(Dev d, Range R, double dtau) {
+  ROMS_IJ_OR_RETURN(R)
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const int N = b.N;
+  const double cu_min = 0.6, cu_max = 1.0, cmnx_ratio = cu_min / cu_max, cutoff = 2.0 - cmnx_ratio,
+               r4cmx = 0.25 / (1.0 - cmnx_ratio);
+  const long ij = IJ(b, i, j);
+  double wi = 0.0;
+  F.Wi[ij] = 0.0;
+  for (int k = 1; k <= N; k++) {
+    const long o = ij + (long)(k - 1) * b.n2;
+    wi = wi - F.FlxU[o + 1] + F.FlxU[o] - F.FlxV[o + b.nx2] + F.FlxV[o];
+    F.Wi[ij + (long)k * b.n2] = wi;
+  }
+  wi = wi + F.swflx[ij] * F.dm_r[ij] * F.dn_r[ij];
+  const double wrk = wi / (F.z_w[ij + (long)N * b.n2] - F.z_w[ij]);
+  F.Wi[ij + (long)N * b.n2] = 0.0;
+  F.We[ij + (long)N * b.n2] = 0.0;
+  F.We[ij] = 0.0;
+  const double CX0 = dtau * F.pm[ij] * F.pn[ij];
+  const double zw0 = F.z_w[ij];
+  double cx_up = omega_cx(b, F, ij + (long)(N - 1) * b.n2);  // CX(k+1)
+  double hz_up = F.Hz[ij + (long)(N - 1) * b.n2];
+  for (int k = N - 1; k >= 1; k--) {
+    const long o = ij + (long)(k - 1) * b.n2;
+    const long ow = ij + (long)k * b.n2;
+    double w = F.Wi[ow] - wrk * (F.z_w[ow] - zw0);
+    const double cx_k = omega_cx(b, F, o);
+    const double hz_k = F.Hz[o];
+    const double c2d = dmax(cx_k, cx_up);
+    const double dh = dmin(hz_k, hz_up);
+    const double cw_max = cu_max * dh - c2d * CX0;
+    double we;
+    if (cw_max > 0.0) {
+      const double cw_max2 = cw_max * cw_max;
+      const double cw_min = cw_max * cmnx_ratio;
+      const double cw = fabs(w) * CX0;
+      double cff;
+      if (cw < cw_min) cff = cw_max2;
+      else if (cw < cutoff * cw_max) cff = cw_max2 + r4cmx * ((cw - cw_min) * (cw - cw_min));
+      else cff = cw_max * cw;
+      we = cw_max2 * w / cff;
+      w = w - we;
+    } else {
+      we = 0.0;
+    }
+    F.We[ow] = we;
+    F.Wi[ow] = w;
+    cx_up = cx_k;
+    hz_up = hz_k;
+  }
+}
+
+// Closed-edge copies of We/Wi into the boundary ghost row (omega.F:171-232).
+__global__ void k_omega_edges(Dev d) {
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nj = b.jend - b.jstr + 1, ni = b.iend - b.istr + 1;
+  int di = 0, dj = 0, si = 0, sj = 0;
+  if (p < nj) {
+    if (!b.west_edge) return;
+    dj = sj = b.jstr + p; di = b.istr - 1; si = b.istr;
+  } else if (p < 2 * nj) {
+    if (!b.east_edge) return;
+    dj = sj = b.jstr + p - nj; di = b.iend + 1; si = b.iend;
+  } else if (p < 2 * nj + ni) {
+    if (!b.south_edge) return;
+    di = si = b.istr + p - 2 * nj; dj = b.jstr - 1; sj = b.jstr;
+  } else if (p < 2 * nj + 2 * ni) {
+    if (!b.north_edge) return;
+    di = si = b.istr + p - 2 * nj - ni; dj = b.jend + 1; sj = b.jend;
+  } else {
+    const int c = p - 2 * nj - 2 * ni;
+    if (c == 0 && b.west_edge && b.south_edge) { di = b.istr - 1; dj = b.jstr - 1; si = b.istr; sj = b.jstr; }
+    else if (c == 1 && b.west_edge && b.north_edge) { di = b.istr - 1; dj = b.jend + 1; si = b.istr; sj = b.jend; }
+    else if (c == 2 && b.east_edge && b.south_edge) { di = b.iend + 1; dj = b.jstr - 1; si = b.iend; sj = b.jstr; }
+    else if (c == 3 && b.east_edge && b.north_edge) { di = b.iend + 1; dj = b.jend + 1; si = b.iend; sj = b.jend; }
+    else return;
+  }
+  const long dst = IJ(b, di, dj), src = IJ(b, si, sj);
+  for (int k = 0; k <= b.N; k++) {
+    F.We[dst + (long)k * b.n2] = F.We[src + (long)k * b.n2];
+    F.Wi[dst + (long)k * b.n2] = F.Wi[src + (long)k * b.n2];
+  }
+}
+
+void launch_omega(const Dev& d, hipStream_t s, const Tlev& t) {
+  const Bounds& b = d.b;
+  double dtau;
+  if (t.nrhs == 3) dtau = d.p.dt;
+  else if (t.iic == t.forw_start) dtau = 0.5 * d.p.dt;
+  else dtau = 0.6 * d.p.dt;
+  Range R{b.istr, b.iend, b.jstr, b.jend};
+  hipLaunchKernelGGL(k_omega, grid_of(R), dim3(kBX, kBY), 0, s, d, R, dtau);
+  if (b.west_edge || b.east_edge || b.south_edge || b.north_edge) {
+    const int n = 2 * (b.jend - b.jstr + 1) + 2 * (b.iend - b.istr + 1) + 4;
+    hipLaunchKernelGGL(k_omega_edges, dim3((n + 255) / 256), dim3(256), 0, s, d);
+  }
+  launch_exchange(d, s, d.f.We, b.N + 1);
+  launch_exchange(d, s, d.f.Wi, b.N + 1);
+}
+
+// ---------------------------------------------------------------------------
+// rho_eos_tile (rho_eos.F:24-409) over the extended range incl. halos.
+// Linear EOS -> rho; NONLIN_EOS -> JM95 split form rho1,qp1 (DUKO_2001).
+// bvf for LMD; VAR_RHO_2D column integrals rhoA, rhoS.
+// ---------------------------------------------------------------------------
+__global__ void k_rho_eos_linear(Dev d, Range R, int tidx) {
+  ROMS_IJ_OR_RETURN(R)
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const Params& P = d.p;
+  const int N = b.N;
+  const long ij = IJ(b, i, j);
+  const double rm = F.rmask[ij];
+  const double cff0 = P.salinity ? (P.Tcoef * P.T0 - P.Scoef * P.S0) : (P.Tcoef * P.T0);
+  const double* T = F.t + (long)(tidx - 1) * b.n3;
+  const double* Sa = F.t + (long)(tidx - 1) * b.n3 + 3 * b.n3;
+  for (int k = 1; k <= N; k++) {
+    const long o = ij + (long)(k - 1) * b.n2;
+    double r = cff0 - P.Tcoef * T[o];
+    if (P.salinity) r = r + P.Scoef * Sa[o];
+    F.rho[o] = r * rm;
+  }
+  if (P.lmd) {
+    const double cff = P.g / P.rho0;
+    for (int k = 1; k <= N - 1; k++) {
+      const long o = ij + (long)(k - 1) * b.n2;
+      F.bvf[ij + (long)k * b.n2] = cff * (F.rho[o] - F.rho[o + b.n2]) / (F.z_r[o + b.n2] - F.z_r[o]);
+    }
+    F.bvf[ij + (long)N * b.n2] = F.bvf[ij + (long)(N - 1) * b.n2];
+    F.bvf[ij] = F.bvf[ij + b.n2];
+  }
+  long o = ij + (long)(N - 1) * b.n2;
+  double cff = F.Hz[o] * F.rho[o];
+  double rhoS = 0.5 * cff * F.Hz[o];
+  double rhoA = cff;
+  for (int k = N - 1; k >= 1; k--) {
+    o = ij + (long)(k - 1) * b.n2;
+    const double hz = F.Hz[o];
+    cff = hz * F.rho[o];
+    rhoS = rhoS + hz * (rhoA + 0.5 * cff);
+    rhoA = rhoA + cff;
+  }
+  const double cff1 = 1.0 / P.rho0;
+  cff = 1.0 / (F.z_w[ij + (long)N * b.n2] - F.z_w[ij]);
+  F.rhoA[ij] = cff * cff1 * rhoA;
+  F.rhoS[ij] = 2.0 * cff * cff * cff1 * rhoS;
+}
+
+__global__ void k_rho_eos_split(Dev d, Range R, int tidx) {
+  ROMS_IJ_OR_RETURN(R)
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const Params& P = d.p;
+  const int N = b.N;
+  const double rho0 = P.rho0, qp2 = P.qp2;
+  const double r00 = 999.842594, r01 = 6.793952E-2, r02 = -9.095290E-3, r03 = 1.001685E-4, r04 = -1.120083E-6,
+               r05 = 6.536332E-9, r10 = 0.824493, r11 = -4.08990E-3, r12 = 7.64380E-5, r13 = -8.24670E-7,
+               r14 = 5.38750E-9, rS0 = -5.72466E-3, rS1 = 1.02270E-4, rS2 = -1.65460E-6, r20 = 4.8314E-4,
+               K00 = 19092.56, K01 = 209.8925, K02 = -3.041638, K03 = -1.852732e-3, K04 = -1.361629e-5,
+               K10 = 104.4077, K11 = -6.500517, K12 = 0.1553190, K13 = 2.326469e-4, KS0 = -5.587545,
+               KS1 = +0.7390729, KS2 = -1.909078e-2;
+  double Tt = 3.8, Ts = 34.5, sqrtTs = sqrt(Ts);
+  const double K0_Duk = Tt * (K01 + Tt * (K02 + Tt * (K03 + Tt * K04))) +
+                        Ts * (K10 + Tt * (K11 + Tt * (K12 + Tt * K13)) + sqrtTs * (KS0 + Tt * (KS1 + Tt * KS2)));
+  const double dr00 = r00 - rho0;
+  const long ij = IJ(b, i, j);
+  const double rm = F.rmask[ij];
+  const double* T = F.t + (long)(tidx - 1) * b.n3;
+  const double* Sa = T + 3 * b.n3;
+  for (int k = 1; k <= N; k++) {
+    const long o = ij + (long)(k - 1) * b.n2;
+    Tt = T[o];
+    Ts = Sa[o];
+    sqrtTs = sqrt(dmax(0.0, Ts));
+    const double r1 = (dr00 + Tt * (r01 + Tt * (r02 + Tt * (r03 + Tt * (r04 + Tt * r05)))) +
+                       Ts * (r10 + Tt * (r11 + Tt * (r12 + Tt * (r13 + Tt * r14))) + sqrtTs * (rS0 + Tt * (rS1 + Tt * rS2)) +
+                             Ts * r20)) *
+                      rm;
+    F.rho1[o] = r1;
+    const double K0 = Tt * (K01 + Tt * (K02 + Tt * (K03 + Tt * K04))) +
+                      Ts * (K10 + Tt * (K11 + Tt * (K12 + Tt * K13)) + sqrtTs * (KS0 + Tt * (KS1 + Tt * KS2)));
+    F.qp1[o] = 0.1 * (rho0 + r1) * (K0_Duk - K0) / ((K00 + K0) * (K00 + K0_Duk)) * rm;
+  }
+  if (P.lmd) {
+    const double cff = P.g / rho0;
+    for (int k = 1; k <= N - 1; k++) {
+      const long o = ij + (long)(k - 1) * b.n2;
+      const double dpth = -0.5 * (F.z_r[o + b.n2] + F.z_r[o]);
+      F.bvf[ij + (long)k * b.n2] =
+          -cff * (F.rho1[o + b.n2] - F.rho1[o] + (F.qp1[o + b.n2] - F.qp1[o]) * dpth * (1.0 - qp2 * dpth)) /
+          (F.z_r[o + b.n2] - F.z_r[o]) * rm;
+    }
+    F.bvf[ij + (long)N * b.n2] = F.bvf[ij + (long)(N - 1) * b.n2];
+    F.bvf[ij] = F.bvf[ij + b.n2];
+  }
+  long o = ij + (long)(N - 1) * b.n2;
+  double dpth = -F.z_r[o];
+  double cff = F.Hz[o] * (F.rho1[o] + F.qp1[o] * dpth * (1.0 - qp2 * dpth));
+  double rhoS = 0.5 * cff * F.Hz[o];
+  double rhoA = cff;
+  for (int k = N - 1; k >= 1; k--) {
+    o = ij + (long)(k - 1) * b.n2;
+    dpth = -F.z_r[o];
+    const double hz = F.Hz[o];
+    cff = hz * (F.rho1[o] + F.qp1[o] * dpth * (1.0 - qp2 * dpth));
+    rhoS = rhoS + hz * (rhoA + 0.5 * cff);
+    rhoA = rhoA + cff;
+  }
+  const double cff1 = 1.0 / rho0;
+  cff = 1.0 / (F.z_w[ij + (long)N * b.n2] - F.z_w[ij]);
+  F.rhoA[ij] = cff * cff1 * rhoA;
+  F.rhoS[ij] = 2.0 * cff * cff * cff1 * rhoS;
+}
+
+void launch_rho_eos(const Dev& d, hipStream_t s, const Tlev& t, int tidx) {
+  const Bounds& b = d.b;
+  Range R{b.istrE, b.iendE, b.jstrE, b.jendE};
+  if (d.p.nonlin_eos)
+    hipLaunchKernelGGL(k_rho_eos_split, grid_of(R), dim3(kBX, kBY), 0, s, d, R, tidx);
+  else
+    hipLaunchKernelGGL(k_rho_eos_linear, grid_of(R), dim3(kBX, kBY), 0, s, d, R, tidx);
+}
+
+}  // namespace roms

@@ -1,0 +1,135 @@
+// roms_dev.h -- device-side state and index helpers of the MI355X ROMS hot path.
+//
+// Every array keeps the reference's Fortran layout (ocean_vars.F:68-116):
+// horizontal extent (-1:Lm+2, -1:Mm+2), i fastest, so element (i,j) sits at
+// (i+1) + (j+1)*(Lm+4); rho-point 3-D arrays stack N levels (1:N), w-point
+// arrays N+1 levels (0:N); u,v add 3 time levels, zeta/ubar/vbar 4, t(...,3,NT).
+// Bulk host<->device copies therefore need no transpose, and a wavefront of 64
+// consecutive i at fixed (j,k) reads one contiguous 512-byte run.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstddef>
+#include <cstdint>
+
+namespace roms {
+
+constexpr int kMaxFast = 288;  // coupling.F:19, weight(2,288)
+
+// Loop bounds of the single tile that covers one rank's subdomain
+// (compute_tile_bounds.h, compute_auxiliary_bounds.h, compute_extended_bounds.h).
+struct Bounds {
+  int Lm, Mm, N, NT, nTS, nx2;
+  long n2, n3, n3w;
+  int istr, iend, jstr, jend;
+  int istrU, istrR, iendR, jstrV, jstrR, jendR;   // auxiliary
+  int istrE, iendE, jstrE, jendE;                  // extended
+  int west_edge, east_edge, south_edge, north_edge;  // physical (closed) edges
+  int ew_periodic, ns_periodic;
+  int west_exch, east_exch, south_exch, north_exch;  // message edges (rank neighbours)
+};
+
+// Physics switches (cppdefs.opt) and scalars of the run.
+struct Params {
+  int nonlin_eos, salinity, lmd, uv_vis2, ts_dif2;
+  double dt, dtfast, g, rho0, vonKar, qp2, gamma2, hc;
+  double rdrg, Zob, Tcoef, T0, Scoef, S0;
+};
+
+// Device pointers of the model state (the "module arrays") plus scratch.
+struct Fields {
+  // grid (grid.F)
+  double *h, *hinv, *f, *fomn, *pm, *pn, *dm_r, *dn_r, *dm_u, *dn_u, *dm_v, *dn_v, *dm_p, *dn_p,
+      *pmon_u, *pnom_v, *rmask, *pmask, *umask, *vmask;
+  double *Cs_w, *Cs_r;  // scoord.F (N+1)
+  // ocean vars
+  double *zeta, *ubar, *vbar, *u, *v, *t;
+  double *FlxU, *FlxV, *We, *Wi, *Hz, *Hz_u, *Hz_v, *z_r, *z_w;
+  // coupling.F
+  double *rufrc, *rvfrc, *rhoA, *rhoS, *r_D, *Zt_avg1, *DU_avg1, *DV_avg1, *DU_avg2, *DV_avg2,
+      *DU_avg_bak, *DV_avg_bak;
+  // eos_vars.F / mixing.F
+  double *rho, *rho1, *qp1, *bvf, *Akv, *Akt, *visc2_r, *visc2_p, *diff2;
+  double *hbls, *hbbl, *ghat, *swr_frac;
+  // surf_flux.F
+  double *sustr, *svstr, *stflx, *srflx, *swflx;
+  // private scratch: A3d(:,1..4) and per-column work arrays
+  double *ru, *rv, *P, *rhos;
+  double *c0, *c1, *c2, *c3;   // (0:N) column scratch, w-point layout
+  double *s0, *s1, *s2, *s3, *s4, *s5, *s6, *s7, *s8, *s9;  // 2-D scratch (step2d, diag)
+};
+
+struct Dev {
+  Bounds b;
+  Params p;
+  Fields f;
+};
+
+// ---- index helpers (device + host) ----
+__host__ __device__ __forceinline__ long IJ(const Bounds& b, int i, int j) {
+  return (long)(i + 1) + (long)(j + 1) * b.nx2;
+}
+__host__ __device__ __forceinline__ long IJK(const Bounds& b, int i, int j, int k) {  // 1:N
+  return IJ(b, i, j) + (long)(k - 1) * b.n2;
+}
+__host__ __device__ __forceinline__ long IJW(const Bounds& b, int i, int j, int k) {  // 0:N
+  return IJ(b, i, j) + (long)k * b.n2;
+}
+__host__ __device__ __forceinline__ long IJL(const Bounds& b, int i, int j, int l) {  // (:,:,4)
+  return IJ(b, i, j) + (long)(l - 1) * b.n2;
+}
+__host__ __device__ __forceinline__ long IJKL(const Bounds& b, int i, int j, int k, int l) {  // (:,:,N,3)
+  return IJ(b, i, j) + (long)(k - 1) * b.n2 + (long)(l - 1) * b.n3;
+}
+__host__ __device__ __forceinline__ long TIDX(const Bounds& b, int i, int j, int k, int l, int itrc) {
+  return IJKL(b, i, j, k, l) + (long)(itrc - 1) * 3 * b.n3;
+}
+
+__device__ __forceinline__ double fmax0(double a) { return a > 0.0 ? a : 0.0; }
+__device__ __forceinline__ double fmin0(double a) { return a < 0.0 ? a : 0.0; }
+__device__ __forceinline__ double dmax(double a, double b) { return a > b ? a : b; }
+__device__ __forceinline__ double dmin(double a, double b) { return a < b ? a : b; }
+__device__ __forceinline__ int iclamp(int x, int lo, int hi) { return x < lo ? lo : (x > hi ? hi : x); }
+
+// 2-D launch over an inclusive index rectangle [i0,i1]x[j0,j1]: one lane per
+// (i,j) column, 64 consecutive i per wavefront (coalesced), 4 rows per block.
+struct Range {
+  int i0, i1, j0, j1;
+};
+constexpr int kBX = 64, kBY = 4;
+inline dim3 grid_of(const Range& r) {
+  int ni = r.i1 - r.i0 + 1, nj = r.j1 - r.j0 + 1;
+  if (ni < 1) ni = 1;
+  if (nj < 1) nj = 1;
+  return dim3((ni + kBX - 1) / kBX, (nj + kBY - 1) / kBY, 1);
+}
+#define ROMS_IJ_OR_RETURN(R)                                   \
+  const int i = (R).i0 + (int)(blockIdx.x * kBX + threadIdx.x); \
+  const int j = (R).j0 + (int)(blockIdx.y * kBY + threadIdx.y); \
+  if (i > (R).i1 || j > (R).j1) return;
+
+// ---- launcher declarations (one translation unit per routine family) ----
+// Each takes the rank's device state and a stream; all enqueue asynchronously.
+struct Tlev {
+  int iic, ntstart, forw_start, iif, nfast, kstp, knew, nstp, nrhs, nnew;
+};
+
+void launch_exchange(const Dev& d, hipStream_t s, double* a, int nlev);
+void launch_set_depth(const Dev& d, hipStream_t s, const Tlev& t);
+void launch_set_huv(const Dev& d, hipStream_t s, const Tlev& t);
+void launch_set_huv1(const Dev& d, hipStream_t s, const Tlev& t);
+void launch_omega(const Dev& d, hipStream_t s, const Tlev& t);
+void launch_rho_eos(const Dev& d, hipStream_t s, const Tlev& t, int tidx);
+void launch_prsgrd(const Dev& d, hipStream_t s, const Tlev& t);
+void launch_pre_step3d(const Dev& d, hipStream_t s, const Tlev& t);
+void launch_step3d_uv1(const Dev& d, hipStream_t s, const Tlev& t);
+void launch_visc3d(const Dev& d, hipStream_t s, const Tlev& t);
+void launch_step2d(const Dev& d, hipStream_t s, const Tlev& t, const double* w1, const double* w2);
+void launch_step3d_uv2(const Dev& d, hipStream_t s, const Tlev& t);
+void launch_step3d_t(const Dev& d, hipStream_t s, const Tlev& t);
+void launch_t3dmix(const Dev& d, hipStream_t s, const Tlev& t);
+void launch_u3dbc(const Dev& d, hipStream_t s, const Tlev& t);
+void launch_v3dbc(const Dev& d, hipStream_t s, const Tlev& t);
+void launch_t3dbc(const Dev& d, hipStream_t s, const Tlev& t, int itrc);
+void launch_diag(const Dev& d, hipStream_t s, const Tlev& t, double* partials);
+
+}  // namespace roms

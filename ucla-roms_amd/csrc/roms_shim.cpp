@@ -1,0 +1,505 @@
+// roms_shim.cpp -- C-ABI implementation (include/roms_gpu.h): device state
+// registry, host<->device transfers, per-routine entries mirroring the
+// reference's hot-path subroutines, the roms_step driver (main.F:333-520)
+// with per-phase HIP-graph replay, analytic-case setup and diag norms.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/roms_gpu.h"
+#include "host_init.h"
+#include "roms_dev.h"
+
+using namespace roms;
+
+namespace {
+
+struct FieldDesc {
+  double* d = nullptr;
+  long count = 0;
+  double* host = nullptr;
+  long host_count = 0;
+};
+
+struct Ctx {
+  bool inited = false;
+  Dev d{};
+  hipStream_t s = nullptr;
+  FieldDesc f[ROMS_NFIELDS];
+  std::vector<double*> scratch;
+  roms_dims dims{};
+  roms_cfg cfg{};
+  double w1[kMaxFast], w2[kMaxFast];
+  double area = 0.0, volume = 0.0;
+  std::string err;
+  // graph cache: key = (nstp, knew at step start)
+  std::map<long, hipGraphExec_t> graphs;
+  bool use_graphs = true;
+  double* h_diag = nullptr;
+};
+Ctx g;
+
+#define CHECK_HIP(x)                                                                  \
+  do {                                                                                \
+    hipError_t e_ = (x);                                                              \
+    if (e_ != hipSuccess) {                                                           \
+      g.err = std::string(#x) + ": " + hipGetErrorString(e_);                         \
+      return -2;                                                                      \
+    }                                                                                 \
+  } while (0)
+
+#define REQUIRE_INIT()                                  \
+  do {                                                  \
+    if (!g.inited) {                                    \
+      g.err = "roms_gpu: not initialised";              \
+      return -1;                                        \
+    }                                                   \
+  } while (0)
+
+int post_launch() {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    g.err = std::string("kernel launch: ") + hipGetErrorString(e);
+    return -3;
+  }
+  return 0;
+}
+
+Bounds make_bounds(const roms_dims& D) {
+  Bounds b{};
+  b.Lm = D.Lm; b.Mm = D.Mm; b.N = D.N; b.NT = D.NT;
+  b.nTS = 1;
+  b.nx2 = D.Lm + 4;
+  b.n2 = (long)(D.Lm + 4) * (D.Mm + 4);
+  b.n3 = b.n2 * D.N;
+  b.n3w = b.n2 * (D.N + 1);
+  b.istr = 1; b.iend = D.Lm; b.jstr = 1; b.jend = D.Mm;
+  b.ew_periodic = D.ew_periodic; b.ns_periodic = D.ns_periodic;
+  b.west_exch = D.west_exchng; b.east_exch = D.east_exchng;
+  b.south_exch = D.south_exchng; b.north_exch = D.north_exchng;
+  // WESTERN_EDGE etc. are only defined without periodicity (set_global_definitions.h:174-191)
+  b.west_edge = !D.ew_periodic && !D.west_exchng;
+  b.east_edge = !D.ew_periodic && !D.east_exchng;
+  b.south_edge = !D.ns_periodic && !D.south_exchng;
+  b.north_edge = !D.ns_periodic && !D.north_exchng;
+  b.istrR = b.west_edge ? b.istr - 1 : b.istr;
+  b.istrU = b.west_edge ? b.istr + 1 : b.istr;
+  b.iendR = b.east_edge ? b.iend + 1 : b.iend;
+  b.jstrR = b.south_edge ? b.jstr - 1 : b.jstr;
+  b.jstrV = b.south_edge ? b.jstr + 1 : b.jstr;
+  b.jendR = b.north_edge ? b.jend + 1 : b.jend;
+  b.istrE = (D.ew_periodic || D.west_exchng) ? b.istr - 2 : b.istr - 1;
+  b.iendE = (D.ew_periodic || D.east_exchng) ? b.iend + 2 : b.iend + 1;
+  b.jstrE = (D.ns_periodic || D.south_exchng) ? b.jstr - 2 : b.jstr - 1;
+  b.jendE = (D.ns_periodic || D.north_exchng) ? b.jend + 2 : b.jend + 1;
+  return b;
+}
+
+long field_count(int id, const Bounds& b) {
+  const long n2 = b.n2, n3 = b.n3, n3w = b.n3w;
+  switch (id) {
+    case ROMS_Cs_w: case ROMS_Cs_r: return b.N + 1;
+    case ROMS_zeta: case ROMS_ubar: case ROMS_vbar: return 4 * n2;
+    case ROMS_u: case ROMS_v: return 3 * n3;
+    case ROMS_t: return 3 * n3 * b.NT;
+    case ROMS_FlxU: case ROMS_FlxV: case ROMS_Hz: case ROMS_Hz_u: case ROMS_Hz_v: case ROMS_z_r: case ROMS_rho:
+    case ROMS_rho1: case ROMS_qp1: case ROMS_ru: case ROMS_rv: return n3;
+    case ROMS_We: case ROMS_Wi: case ROMS_z_w: case ROMS_bvf: case ROMS_Akv: case ROMS_ghat: case ROMS_swr_frac:
+      return n3w;
+    case ROMS_Akt: return n3w * b.nTS;
+    case ROMS_diff2: case ROMS_stflx: return n2 * b.NT;
+    default: return n2;
+  }
+}
+
+double** field_slot(Fields& F, int id) {
+  switch (id) {
+    case ROMS_h: return &F.h; case ROMS_hinv: return &F.hinv; case ROMS_f: return &F.f; case ROMS_fomn: return &F.fomn;
+    case ROMS_pm: return &F.pm; case ROMS_pn: return &F.pn; case ROMS_dm_r: return &F.dm_r; case ROMS_dn_r: return &F.dn_r;
+    case ROMS_dm_u: return &F.dm_u; case ROMS_dn_u: return &F.dn_u; case ROMS_dm_v: return &F.dm_v;
+    case ROMS_dn_v: return &F.dn_v; case ROMS_dm_p: return &F.dm_p; case ROMS_dn_p: return &F.dn_p;
+    case ROMS_pmon_u: return &F.pmon_u; case ROMS_pnom_v: return &F.pnom_v; case ROMS_rmask: return &F.rmask;
+    case ROMS_pmask: return &F.pmask; case ROMS_umask: return &F.umask; case ROMS_vmask: return &F.vmask;
+    case ROMS_Cs_w: return &F.Cs_w; case ROMS_Cs_r: return &F.Cs_r;
+    case ROMS_zeta: return &F.zeta; case ROMS_ubar: return &F.ubar; case ROMS_vbar: return &F.vbar;
+    case ROMS_u: return &F.u; case ROMS_v: return &F.v; case ROMS_t: return &F.t; case ROMS_FlxU: return &F.FlxU;
+    case ROMS_FlxV: return &F.FlxV; case ROMS_We: return &F.We; case ROMS_Wi: return &F.Wi; case ROMS_Hz: return &F.Hz;
+    case ROMS_Hz_u: return &F.Hz_u; case ROMS_Hz_v: return &F.Hz_v; case ROMS_z_r: return &F.z_r; case ROMS_z_w: return &F.z_w;
+    case ROMS_rufrc: return &F.rufrc; case ROMS_rvfrc: return &F.rvfrc; case ROMS_rhoA: return &F.rhoA;
+    case ROMS_rhoS: return &F.rhoS; case ROMS_r_D: return &F.r_D; case ROMS_Zt_avg1: return &F.Zt_avg1;
+    case ROMS_DU_avg1: return &F.DU_avg1; case ROMS_DV_avg1: return &F.DV_avg1; case ROMS_DU_avg2: return &F.DU_avg2;
+    case ROMS_DV_avg2: return &F.DV_avg2; case ROMS_DU_avg_bak: return &F.DU_avg_bak;
+    case ROMS_DV_avg_bak: return &F.DV_avg_bak; case ROMS_rho: return &F.rho; case ROMS_rho1: return &F.rho1;
+    case ROMS_qp1: return &F.qp1; case ROMS_bvf: return &F.bvf; case ROMS_Akv: return &F.Akv; case ROMS_Akt: return &F.Akt;
+    case ROMS_visc2_r: return &F.visc2_r; case ROMS_visc2_p: return &F.visc2_p; case ROMS_diff2: return &F.diff2;
+    case ROMS_hbls: return &F.hbls; case ROMS_hbbl: return &F.hbbl; case ROMS_ghat: return &F.ghat;
+    case ROMS_swr_frac: return &F.swr_frac; case ROMS_sustr: return &F.sustr; case ROMS_svstr: return &F.svstr;
+    case ROMS_stflx: return &F.stflx; case ROMS_srflx: return &F.srflx; case ROMS_swflx: return &F.swflx;
+    case ROMS_ru: return &F.ru; case ROMS_rv: return &F.rv;
+    default: return nullptr;
+  }
+}
+
+void free_all() {
+  for (auto& kv : g.graphs) (void)hipGraphExecDestroy(kv.second);
+  g.graphs.clear();
+  for (int id = 0; id < ROMS_NFIELDS; id++)
+    if (g.f[id].d) { (void)hipFree(g.f[id].d); g.f[id] = FieldDesc{}; }
+  for (double* p : g.scratch) (void)hipFree(p);
+  g.scratch.clear();
+  if (g.h_diag) { (void)hipHostFree(g.h_diag); g.h_diag = nullptr; }
+  if (g.s) { (void)hipStreamDestroy(g.s); g.s = nullptr; }
+  g.inited = false;
+}
+
+Tlev to_tlev(const roms_tlev* t) {
+  Tlev r;
+  r.iic = t->iic; r.ntstart = t->ntstart; r.forw_start = t->forw_start; r.iif = t->iif; r.nfast = t->nfast;
+  r.kstp = t->kstp; r.knew = t->knew; r.nstp = t->nstp; r.nrhs = t->nrhs; r.nnew = t->nnew;
+  return r;
+}
+
+// the roms_step sequence for one step whose indices are already set in *t
+// (nstp,nrhs=nstp,nnew=3 on entry); enqueues everything on g.s
+void enqueue_step(roms_tlev* t) {
+  const Dev& d = g.d;
+  hipStream_t s = g.s;
+  Tlev T = to_tlev(t);
+  launch_rho_eos(d, s, T, T.nrhs);
+  launch_set_huv(d, s, T);
+  launch_omega(d, s, T);
+  launch_prsgrd(d, s, T);
+  launch_pre_step3d(d, s, T);
+  launch_set_huv1(d, s, T);
+  t->nrhs = 3;
+  t->nnew = 3 - t->nstp;
+  T = to_tlev(t);
+  launch_omega(d, s, T);
+  launch_rho_eos(d, s, T, T.nrhs);
+  launch_prsgrd(d, s, T);
+  launch_step3d_uv1(d, s, T);
+  if (g.cfg.uv_vis2) launch_visc3d(d, s, T);
+  for (int iif = 1; iif <= t->nfast; iif++) {
+    t->iif = iif;
+    t->kstp = t->knew;
+    t->knew = t->kstp + 1;
+    if (t->knew > 4) t->knew = 1;
+    T = to_tlev(t);
+    launch_step2d(d, s, T, g.w1, g.w2);
+  }
+  launch_step3d_uv2(d, s, T);
+  launch_omega(d, s, T);
+  launch_step3d_t(d, s, T);
+  if (g.cfg.ts_dif2) launch_t3dmix(d, s, T);
+  launch_rho_eos(d, s, T, T.nnew);
+}
+
+}  // namespace
+
+extern "C" {
+
+int roms_gpu_abi_version(void) { return ROMS_GPU_ABI_VERSION; }
+const char* roms_gpu_last_error(void) { return g.err.c_str(); }
+void* roms_gpu_stream(void) { return (void*)g.s; }
+
+int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* comm) {
+  if (g.inited) free_all();
+  if (!dims || !cfg) { g.err = "roms_gpu_init: null argument"; return -1; }
+  if (dims->N < 2 || dims->Lm < 2 || dims->Mm < 2 || dims->NT < 1) { g.err = "roms_gpu_init: bad dims"; return -1; }
+  if (cfg->nfast < 1 || cfg->nfast > ROMS_MAX_FAST) { g.err = "roms_gpu_init: bad nfast"; return -1; }
+  if (cfg->lmd_mixing) { g.err = "roms_gpu_init: LMD_MIXING not available in this build"; return -4; }
+  if (comm != nullptr || dims->np_xi * dims->np_eta > 1) {
+    g.err = "roms_gpu_init: multi-rank halo exchange not available in this build";
+    return -4;
+  }
+  CHECK_HIP(hipSetDevice(device));
+  g.dims = *dims;
+  g.cfg = *cfg;
+  g.d = Dev{};
+  g.d.b = make_bounds(*dims);
+  g.d.b.nTS = cfg->salinity ? 2 : 1;
+  Params& P = g.d.p;
+  P.nonlin_eos = cfg->nonlin_eos; P.salinity = cfg->salinity; P.lmd = cfg->lmd_mixing;
+  P.uv_vis2 = cfg->uv_vis2; P.ts_dif2 = cfg->ts_dif2;
+  P.dt = cfg->dt; P.dtfast = cfg->dt / (double)cfg->ndtfast; P.g = cfg->g; P.rho0 = cfg->rho0;
+  P.vonKar = 0.41; P.qp2 = 0.0000172; P.gamma2 = cfg->gamma2; P.hc = cfg->hc;
+  P.rdrg = cfg->rdrg; P.Zob = cfg->Zob; P.Tcoef = cfg->Tcoef; P.T0 = cfg->T0; P.Scoef = cfg->Scoef; P.S0 = cfg->S0;
+  for (int i = 0; i < kMaxFast; i++) { g.w1[i] = cfg->weight[0][i]; g.w2[i] = cfg->weight[1][i]; }
+  CHECK_HIP(hipStreamCreateWithFlags(&g.s, hipStreamNonBlocking));
+  const Bounds& b = g.d.b;
+  for (int id = 0; id < ROMS_NFIELDS; id++) {
+    const long n = field_count(id, b);
+    double* p = nullptr;
+    CHECK_HIP(hipMalloc(&p, (size_t)n * sizeof(double)));
+    CHECK_HIP(hipMemset(p, 0, (size_t)n * sizeof(double)));
+    g.f[id].d = p;
+    g.f[id].count = n;
+    *field_slot(g.d.f, id) = p;
+  }
+  auto scratch = [&](double*& p, long n) -> int {
+    CHECK_HIP(hipMalloc(&p, (size_t)n * sizeof(double)));
+    CHECK_HIP(hipMemset(p, 0, (size_t)n * sizeof(double)));
+    g.scratch.push_back(p);
+    return 0;
+  };
+  Fields& F = g.d.f;
+  if (scratch(F.P, b.n3) || scratch(F.rhos, b.n3) || scratch(F.c0, b.n3w) || scratch(F.c1, b.n3w) ||
+      scratch(F.c2, b.n3w) || scratch(F.c3, b.n3w))
+    return -2;
+  double** s2[] = {&F.s0, &F.s1, &F.s2, &F.s3, &F.s4, &F.s5, &F.s6, &F.s7, &F.s8, &F.s9};
+  for (double** q : s2)
+    if (scratch(*q, b.n2)) return -2;
+  CHECK_HIP(hipHostMalloc(&g.h_diag, (size_t)8 * b.n2 * sizeof(double), hipHostMallocDefault));
+  const char* env = getenv("ROMS_GPU_NO_GRAPH");
+  g.use_graphs = !(env && env[0] == '1');
+  g.inited = true;
+  return 0;
+}
+
+int roms_gpu_finalize(void) {
+  if (g.inited) {
+    (void)hipStreamSynchronize(g.s);
+    free_all();
+  }
+  return 0;
+}
+
+long roms_gpu_field_size(int id) {
+  if (!g.inited || id < 0 || id >= ROMS_NFIELDS) return -1;
+  return g.f[id].count;
+}
+
+int roms_gpu_register(int id, double* host, long count) {
+  REQUIRE_INIT();
+  if (id < 0 || id >= ROMS_NFIELDS) { g.err = "roms_gpu_register: bad field id"; return -1; }
+  if (count != g.f[id].count) { g.err = "roms_gpu_register: size mismatch for field"; return -1; }
+  g.f[id].host = host;
+  g.f[id].host_count = count;
+  return 0;
+}
+
+static int xfer(int id, bool up) {
+  if (id == ROMS_ALL) {
+    for (int q = 0; q < ROMS_NFIELDS; q++)
+      if (g.f[q].host) {
+        const int r = xfer(q, up);
+        if (r) return r;
+      }
+    return 0;
+  }
+  if (id < 0 || id >= ROMS_NFIELDS) { g.err = "bad field id"; return -1; }
+  if (!g.f[id].host) { g.err = "field not registered"; return -1; }
+  const size_t nb = (size_t)g.f[id].count * sizeof(double);
+  if (up) CHECK_HIP(hipMemcpyAsync(g.f[id].d, g.f[id].host, nb, hipMemcpyHostToDevice, g.s));
+  else CHECK_HIP(hipMemcpyAsync(g.f[id].host, g.f[id].d, nb, hipMemcpyDeviceToHost, g.s));
+  CHECK_HIP(hipStreamSynchronize(g.s));
+  return 0;
+}
+int roms_gpu_upload(int id) { REQUIRE_INIT(); return xfer(id, true); }
+int roms_gpu_download(int id) { REQUIRE_INIT(); return xfer(id, false); }
+
+int roms_gpu_copy_in(int id, const double* src, long count) {
+  REQUIRE_INIT();
+  if (id < 0 || id >= ROMS_NFIELDS || count != g.f[id].count) { g.err = "roms_gpu_copy_in: bad field/size"; return -1; }
+  CHECK_HIP(hipMemcpyAsync(g.f[id].d, src, (size_t)count * sizeof(double), hipMemcpyHostToDevice, g.s));
+  CHECK_HIP(hipStreamSynchronize(g.s));
+  return 0;
+}
+int roms_gpu_copy_out(int id, double* dst, long count) {
+  REQUIRE_INIT();
+  if (id < 0 || id >= ROMS_NFIELDS || count != g.f[id].count) { g.err = "roms_gpu_copy_out: bad field/size"; return -1; }
+  CHECK_HIP(hipMemcpyAsync(dst, g.f[id].d, (size_t)count * sizeof(double), hipMemcpyDeviceToHost, g.s));
+  CHECK_HIP(hipStreamSynchronize(g.s));
+  return 0;
+}
+int roms_gpu_sync(void) {
+  REQUIRE_INIT();
+  CHECK_HIP(hipStreamSynchronize(g.s));
+  return post_launch();
+}
+
+#define ROUTINE(name, call)           \
+  int name(const roms_tlev* t) {      \
+    REQUIRE_INIT();                   \
+    const Tlev T = to_tlev(t);        \
+    call;                             \
+    return post_launch();             \
+  }
+ROUTINE(roms_gpu_set_huv, launch_set_huv(g.d, g.s, T))
+ROUTINE(roms_gpu_omega, launch_omega(g.d, g.s, T))
+ROUTINE(roms_gpu_prsgrd, launch_prsgrd(g.d, g.s, T))
+ROUTINE(roms_gpu_pre_step3d, launch_pre_step3d(g.d, g.s, T))
+ROUTINE(roms_gpu_set_huv1, launch_set_huv1(g.d, g.s, T))
+ROUTINE(roms_gpu_step3d_uv1, launch_step3d_uv1(g.d, g.s, T))
+ROUTINE(roms_gpu_visc3d, launch_visc3d(g.d, g.s, T))
+ROUTINE(roms_gpu_step2d, launch_step2d(g.d, g.s, T, g.w1, g.w2))
+ROUTINE(roms_gpu_step3d_uv2, launch_step3d_uv2(g.d, g.s, T))
+ROUTINE(roms_gpu_step3d_t, launch_step3d_t(g.d, g.s, T))
+ROUTINE(roms_gpu_t3dmix, launch_t3dmix(g.d, g.s, T))
+ROUTINE(roms_gpu_set_depth, launch_set_depth(g.d, g.s, T))
+#undef ROUTINE
+
+int roms_gpu_rho_eos(int tidx, const roms_tlev* t) {
+  REQUIRE_INIT();
+  launch_rho_eos(g.d, g.s, to_tlev(t), tidx);
+  return post_launch();
+}
+int roms_gpu_lmd_vmix(int tind, const roms_tlev* t) {
+  (void)tind; (void)t;
+  REQUIRE_INIT();
+  g.err = "roms_gpu_lmd_vmix: LMD_MIXING not available in this build";
+  return -4;
+}
+
+int roms_gpu_step(roms_tlev* t) {
+  REQUIRE_INIT();
+  t->iic = t->iic + 1;
+  t->nstp = 1 + (t->iic - t->ntstart) % 2;
+  t->nrhs = t->nstp;
+  t->nnew = 3;
+  t->nfast = g.cfg.nfast;
+  const bool first = (t->iic == t->forw_start);
+  if (!g.use_graphs || first) {
+    enqueue_step(t);
+    return post_launch();
+  }
+  const long key = (long)t->nstp * 16 + t->knew;
+  auto it = g.graphs.find(key);
+  roms_tlev t0 = *t;
+  if (it == g.graphs.end()) {
+    hipGraph_t graph;
+    CHECK_HIP(hipStreamBeginCapture(g.s, hipStreamCaptureModeThreadLocal));
+    enqueue_step(t);
+    CHECK_HIP(hipStreamEndCapture(g.s, &graph));
+    hipGraphExec_t exec;
+    CHECK_HIP(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+    CHECK_HIP(hipGraphDestroy(graph));
+    g.graphs[key] = exec;
+    it = g.graphs.find(key);
+    *t = t0;
+  }
+  // replay; advance the host-side indices exactly as enqueue_step would
+  CHECK_HIP(hipGraphLaunch(it->second, g.s));
+  t->nrhs = 3;
+  t->nnew = 3 - t->nstp;
+  for (int iif = 1; iif <= t->nfast; iif++) {
+    t->iif = iif;
+    t->kstp = t->knew;
+    t->knew = t->kstp + 1;
+    if (t->knew > 4) t->knew = 1;
+  }
+  return post_launch();
+}
+
+int roms_gpu_init_sequence(roms_tlev* t) {
+  REQUIRE_INIT();
+  const Tlev T = to_tlev(t);
+  launch_set_depth(g.d, g.s, T);
+  launch_set_huv(g.d, g.s, T);
+  launch_omega(g.d, g.s, T);
+  launch_rho_eos(g.d, g.s, T, T.nrhs);
+  return post_launch();
+}
+
+int roms_gpu_init_case(const roms_case* c, int device, roms_tlev* t) {
+  if (!c || !t) { g.err = "roms_gpu_init_case: null argument"; return -1; }
+  roms_dims D{};
+  D.Lm = c->LLm; D.Mm = c->MMm; D.N = c->N; D.NT = c->NT; D.LLm = c->LLm; D.MMm = c->MMm;
+  D.np_xi = D.np_eta = 1;
+  const bool fil = c->case_id == ROMS_CASE_FILAMENT;
+  D.ew_periodic = D.ns_periodic = fil ? 1 : 0;
+  roms_cfg C{};
+  C.nonlin_eos = c->nonlin_eos; C.salinity = c->salinity; C.lmd_mixing = c->lmd_mixing;
+  C.uv_vis2 = 1; C.ts_dif2 = 1;
+  C.dt = c->dt; C.ndtfast = c->ndtfast;
+  C.nfast = set_weights(c->ndtfast, C.weight);
+  C.g = 9.81; C.rho0 = fil ? 1000.0 : 1027.5; C.gamma2 = 1.0;
+  C.rdrg = 0.0; C.rdrg2 = 1.0e-3; C.Zob = 1.0e-2;
+  C.Tcoef = 0.20; C.T0 = 1.0; C.Scoef = 0.822; C.S0 = 1.0;
+  C.theta_s = 6.0; C.theta_b = 2.0; C.hc = fil ? 25.0 : 250.0;
+  C.Akv_bak = fil ? 0.0 : 1.0e-4; C.Akt_bak[0] = fil ? 0.0 : 1.0e-5; C.Akt_bak[1] = C.Akt_bak[0];
+  int r = roms_gpu_init(&D, &C, device, nullptr);
+  if (r) return r;
+  CaseSpec cs{};
+  cs.case_id = c->case_id; cs.LLm = c->LLm; cs.MMm = c->MMm;
+  cs.ew_periodic = D.ew_periodic; cs.ns_periodic = D.ns_periodic;
+  cs.salinity = c->salinity; cs.theta_s = C.theta_s; cs.theta_b = C.theta_b; cs.hc = C.hc; cs.rho0 = C.rho0;
+  cs.Tcoef = C.Tcoef; cs.visc2 = 0.0; cs.tnu2 = 0.0; cs.Akv_bak = C.Akv_bak;
+  cs.Akt_bak[0] = C.Akt_bak[0]; cs.Akt_bak[1] = C.Akt_bak[1];
+  cs.sizex = c->sizex; cs.sizey = c->sizey;
+  HostState H(D.Lm, D.Mm, D.N, D.NT, C.salinity ? 2 : 1);
+  build_case(cs, H, g.area, g.volume);
+  for (int id = 0; id < ROMS_NFIELDS; id++) {
+    if (H.arr[id].empty()) continue;
+    r = roms_gpu_copy_in(id, H.arr[id].data(), (long)H.arr[id].size());
+    if (r) return r;
+  }
+  *t = roms_tlev{};
+  t->iic = 0; t->ntstart = 1; t->forw_start = 1; t->iif = 1; t->nfast = C.nfast;
+  t->kstp = 1; t->knew = 1; t->nstp = 1; t->nrhs = 1; t->nnew = 1;
+  return roms_gpu_init_sequence(t);
+}
+
+int roms_gpu_time_steps(roms_tlev* t, int n, double* ms) {
+  REQUIRE_INIT();
+  hipEvent_t a, b;
+  CHECK_HIP(hipEventCreate(&a));
+  CHECK_HIP(hipEventCreate(&b));
+  CHECK_HIP(hipEventRecord(a, g.s));
+  for (int q = 0; q < n; q++) {
+    const int r = roms_gpu_step(t);
+    if (r) return r;
+  }
+  CHECK_HIP(hipEventRecord(b, g.s));
+  CHECK_HIP(hipEventSynchronize(b));
+  float f = 0.f;
+  CHECK_HIP(hipEventElapsedTime(&f, a, b));
+  *ms = (double)f;
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  return 0;
+}
+
+// diag.F code_check norms: per-column terms on the device (launch_diag),
+// reduction-by-pairs and the (j, k desc, i) first-maximum scan on the host.
+int roms_gpu_diag(const roms_tlev* t, double norms[4]) {
+  REQUIRE_INIT();
+  const Bounds& b = g.d.b;
+  launch_diag(g.d, g.s, to_tlev(t), nullptr);
+  const long n2 = b.n2;
+  CHECK_HIP(hipMemcpyAsync(g.h_diag, g.d.f.s0, (size_t)n2 * sizeof(double), hipMemcpyDeviceToHost, g.s));
+  CHECK_HIP(hipMemcpyAsync(g.h_diag + n2, g.d.f.s1, (size_t)n2 * sizeof(double), hipMemcpyDeviceToHost, g.s));
+  CHECK_HIP(hipMemcpyAsync(g.h_diag + 2 * n2, g.d.f.s2, (size_t)n2 * sizeof(double), hipMemcpyDeviceToHost, g.s));
+  CHECK_HIP(hipMemcpyAsync(g.h_diag + 3 * n2, g.d.f.s3, (size_t)n2 * sizeof(double), hipMemcpyDeviceToHost, g.s));
+  CHECK_HIP(hipMemcpyAsync(g.h_diag + 4 * n2, g.d.f.s4, (size_t)n2 * sizeof(double), hipMemcpyDeviceToHost, g.s));
+  CHECK_HIP(hipMemcpyAsync(g.h_diag + 5 * n2, g.d.f.s5, (size_t)n2 * sizeof(double), hipMemcpyDeviceToHost, g.s));
+  CHECK_HIP(hipStreamSynchronize(g.s));
+  HostState H(b.Lm, b.Mm, b.N, b.NT, b.nTS);
+  std::vector<double> dVol(g.h_diag, g.h_diag + n2), ke(g.h_diag + n2, g.h_diag + 2 * n2),
+      ke2b(g.h_diag + 2 * n2, g.h_diag + 3 * n2);
+  const double* cx = g.h_diag + 3 * n2;
+  const double* cw = g.h_diag + 4 * n2;
+  const double* kx = g.h_diag + 5 * n2;
+  const double avzeta = pair_sum(H, dVol), kes = pair_sum(H, ke), ke2 = pair_sum(H, ke2b);
+  double Cu = 0.0, Cw = 0.0;
+  for (int j = 1; j <= b.Mm; j++) {
+    double best = 0.0, bw = 0.0, bk = -1.0;
+    for (int i = 1; i <= b.Lm; i++) {
+      const long o = IJ(b, i, j);
+      if (cx[o] > best || (cx[o] == best && best > 0.0 && kx[o] > bk)) { best = cx[o]; bw = cw[o]; bk = kx[o]; }
+    }
+    if (best > Cu) { Cu = best; Cw = bw; }
+  }
+  norms[0] = kes / (g.volume + avzeta);
+  norms[1] = ke2 / (g.volume + avzeta);
+  norms[2] = Cu;
+  norms[3] = Cw;
+  return post_launch();
+}
+
+}  // extern "C"

@@ -1,0 +1,197 @@
+"""romsgpu -- host-side mirror of the UCLA-ROMS hot-path routines on MI355X.
+
+The reference drives its split-explicit step from Fortran (main.F:333-520)
+by calling argument-less / (tile) / (tidx) subroutines that operate on module
+arrays.  ``Model`` exposes the same routines with the same names and the same
+time-index bookkeeping (scalars.F: iic, kstp, knew, nstp, nrhs, nnew), backed
+by ``libromsgpu.so`` (HIP kernels for gfx950 behind the C ABI declared in
+include/roms_gpu.h).  There is no CPU fallback: constructing a Model without
+the built library or without a GPU raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_PKG = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(_PKG, "libromsgpu.so")
+MAX_FAST = 288
+
+FIELDS = ["h", "hinv", "f", "fomn", "pm", "pn", "dm_r", "dn_r", "dm_u", "dn_u", "dm_v", "dn_v", "dm_p", "dn_p",
+          "pmon_u", "pnom_v", "rmask", "pmask", "umask", "vmask", "Cs_w", "Cs_r",
+          "zeta", "ubar", "vbar", "u", "v", "t", "FlxU", "FlxV", "We", "Wi", "Hz", "Hz_u", "Hz_v", "z_r", "z_w",
+          "rufrc", "rvfrc", "rhoA", "rhoS", "r_D", "Zt_avg1", "DU_avg1", "DV_avg1", "DU_avg2", "DV_avg2",
+          "DU_avg_bak", "DV_avg_bak", "rho", "rho1", "qp1", "bvf", "Akv", "Akt", "visc2_r", "visc2_p", "diff2",
+          "hbls", "hbbl", "ghat", "swr_frac", "sustr", "svstr", "stflx", "srflx", "swflx", "ru", "rv"]
+FIELD_ID = {n: i for i, n in enumerate(FIELDS)}
+CASE_FILAMENT, CASE_BASIN = 0, 1
+
+
+class Dims(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in
+                ("Lm", "Mm", "N", "NT", "LLm", "MMm", "np_xi", "np_eta", "inode", "jnode", "iSW_corn", "jSW_corn",
+                 "ew_periodic", "ns_periodic", "west_exchng", "east_exchng", "south_exchng", "north_exchng")]
+
+
+class Cfg(ctypes.Structure):
+    _fields_ = [("nonlin_eos", ctypes.c_int), ("salinity", ctypes.c_int), ("lmd_mixing", ctypes.c_int),
+                ("uv_vis2", ctypes.c_int), ("ts_dif2", ctypes.c_int), ("dt", ctypes.c_double),
+                ("ndtfast", ctypes.c_int), ("nfast", ctypes.c_int), ("weight", (ctypes.c_double * MAX_FAST) * 2),
+                ("g", ctypes.c_double), ("rho0", ctypes.c_double), ("rdrg", ctypes.c_double),
+                ("rdrg2", ctypes.c_double), ("Zob", ctypes.c_double), ("gamma2", ctypes.c_double),
+                ("Akv_bak", ctypes.c_double), ("Akt_bak", ctypes.c_double * 2), ("Tcoef", ctypes.c_double),
+                ("T0", ctypes.c_double), ("Scoef", ctypes.c_double), ("S0", ctypes.c_double),
+                ("theta_s", ctypes.c_double), ("theta_b", ctypes.c_double), ("hc", ctypes.c_double)]
+
+
+class Tlev(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in
+                ("iic", "ntstart", "forw_start", "iif", "nfast", "kstp", "knew", "nstp", "nrhs", "nnew")]
+
+    def as_list(self):
+        return [self.iic, self.kstp, self.knew, self.nstp, self.nrhs, self.nnew]
+
+
+class Case(ctypes.Structure):
+    _fields_ = [("case_id", ctypes.c_int), ("LLm", ctypes.c_int), ("MMm", ctypes.c_int), ("N", ctypes.c_int),
+                ("NT", ctypes.c_int), ("salinity", ctypes.c_int), ("nonlin_eos", ctypes.c_int),
+                ("lmd_mixing", ctypes.c_int), ("dt", ctypes.c_double), ("ndtfast", ctypes.c_int),
+                ("sizex", ctypes.c_double), ("sizey", ctypes.c_double)]
+
+
+ROUTINES_T = ["set_huv", "omega", "prsgrd", "pre_step3d", "set_huv1", "step3d_uv1", "visc3d", "step2d",
+              "step3d_uv2", "step3d_t", "t3dmix", "set_depth", "step", "init_sequence"]
+
+_lib = None
+
+
+def load_library(path=LIB_PATH):
+    """Load libromsgpu.so; raises if it has not been built (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError("romsgpu: %s not built -- run __graft_entry__.build()" % path)
+    L = ctypes.CDLL(path)
+    P = ctypes.POINTER
+    L.roms_gpu_last_error.restype = ctypes.c_char_p
+    L.roms_gpu_init.argtypes = [P(Dims), P(Cfg), ctypes.c_int, ctypes.c_void_p]
+    L.roms_gpu_init_case.argtypes = [P(Case), ctypes.c_int, P(Tlev)]
+    L.roms_gpu_field_size.argtypes = [ctypes.c_int]
+    L.roms_gpu_field_size.restype = ctypes.c_long
+    for fn in ("roms_gpu_copy_in", "roms_gpu_copy_out", "roms_gpu_register"):
+        getattr(L, fn).argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_long]
+    for fn in ROUTINES_T:
+        getattr(L, "roms_gpu_" + fn).argtypes = [P(Tlev)]
+    L.roms_gpu_rho_eos.argtypes = [ctypes.c_int, P(Tlev)]
+    L.roms_gpu_lmd_vmix.argtypes = [ctypes.c_int, P(Tlev)]
+    L.roms_gpu_diag.argtypes = [P(Tlev), P(ctypes.c_double)]
+    L.roms_gpu_time_steps.argtypes = [P(Tlev), ctypes.c_int, P(ctypes.c_double)]
+    L.roms_gpu_stream.restype = ctypes.c_void_p
+    _lib = L
+    return L
+
+
+class RomsGpuError(RuntimeError):
+    pass
+
+
+class Model:
+    """One rank's device-resident model state and the reference's routines."""
+
+    def __init__(self):
+        self.L = load_library()
+        self.t = Tlev()
+        self.shape2 = None
+
+    def _chk(self, rc, what):
+        if rc != 0:
+            raise RomsGpuError("%s failed (%d): %s" % (what, rc, self.L.roms_gpu_last_error().decode()))
+
+    # ---- construction ----
+    @classmethod
+    def from_case(cls, case_id, LLm, MMm, N, NT=1, salinity=False, nonlin_eos=False, dt=5.0, ndtfast=60,
+                  sizex=12.8e3, sizey=3.2e3, device=0):
+        m = cls()
+        c = Case(case_id, LLm, MMm, N, NT, int(salinity), int(nonlin_eos), 0, dt, ndtfast, sizex, sizey)
+        m._chk(m.L.roms_gpu_init_case(ctypes.byref(c), device, ctypes.byref(m.t)), "roms_gpu_init_case")
+        m.LLm, m.MMm, m.N, m.NT = LLm, MMm, N, NT
+        m.shape2 = (MMm + 4, LLm + 4)
+        return m
+
+    @classmethod
+    def from_dims(cls, dims, cfg, device=0):
+        m = cls()
+        m._chk(m.L.roms_gpu_init(ctypes.byref(dims), ctypes.byref(cfg), device, None), "roms_gpu_init")
+        m.LLm, m.MMm, m.N, m.NT = dims.Lm, dims.Mm, dims.N, dims.NT
+        m.shape2 = (dims.Mm + 4, dims.Lm + 4)
+        return m
+
+    def close(self):
+        self.L.roms_gpu_finalize()
+
+    # ---- state access (Fortran layout, returned as (levels, j, i) C arrays) ----
+    def get(self, name):
+        fid = FIELD_ID[name]
+        n = self.L.roms_gpu_field_size(fid)
+        a = np.empty(n, dtype=np.float64)
+        self._chk(self.L.roms_gpu_copy_out(fid, a.ctypes.data, n), "copy_out " + name)
+        n2 = self.shape2[0] * self.shape2[1]
+        return a.reshape((n // n2,) + self.shape2) if n % n2 == 0 else a
+
+    def put(self, name, arr):
+        fid = FIELD_ID[name]
+        a = np.ascontiguousarray(arr, dtype=np.float64).ravel()
+        n = self.L.roms_gpu_field_size(fid)
+        if a.size != n:
+            raise ValueError("%s: expected %d elements, got %d" % (name, n, a.size))
+        self._chk(self.L.roms_gpu_copy_in(fid, a.ctypes.data, n), "copy_in " + name)
+
+    def set_tindex(self, iic, kstp, knew, nstp, nrhs, nnew, iif=1, forw_start=1, ntstart=1, nfast=None):
+        self.t.iic, self.t.kstp, self.t.knew, self.t.nstp, self.t.nrhs, self.t.nnew = iic, kstp, knew, nstp, nrhs, nnew
+        self.t.iif, self.t.forw_start, self.t.ntstart = iif, forw_start, ntstart
+        if nfast is not None:
+            self.t.nfast = nfast
+
+    def sync(self):
+        self._chk(self.L.roms_gpu_sync(), "sync")
+
+    # ---- reference routines ----
+    def rho_eos(self, tidx):
+        self._chk(self.L.roms_gpu_rho_eos(tidx, ctypes.byref(self.t)), "rho_eos")
+
+    def lmd_vmix(self, tind):
+        self._chk(self.L.roms_gpu_lmd_vmix(tind, ctypes.byref(self.t)), "lmd_vmix")
+
+    def _r(self, fn):
+        self._chk(getattr(self.L, "roms_gpu_" + fn)(ctypes.byref(self.t)), fn)
+
+    def set_HUV(self): self._r("set_huv")
+    def omega(self): self._r("omega")
+    def prsgrd(self): self._r("prsgrd")
+    def pre_step3d(self): self._r("pre_step3d")
+    def set_HUV1(self): self._r("set_huv1")
+    def step3d_uv1(self): self._r("step3d_uv1")
+    def visc3d(self): self._r("visc3d")
+    def step2d(self): self._r("step2d")
+    def step3d_uv2(self): self._r("step3d_uv2")
+    def step3d_t(self): self._r("step3d_t")
+    def t3dmix(self): self._r("t3dmix")
+    def set_depth(self): self._r("set_depth")
+    def init_sequence(self): self._r("init_sequence")
+
+    def step(self, n=1):
+        """roms_step (main.F:333-520) n times; updates the time indices."""
+        for _ in range(n):
+            self._r("step")
+
+    def diag(self):
+        out = (ctypes.c_double * 4)()
+        self._chk(self.L.roms_gpu_diag(ctypes.byref(self.t), out), "diag")
+        return list(out)
+
+    def time_steps(self, n):
+        ms = ctypes.c_double()
+        self._chk(self.L.roms_gpu_time_steps(ctypes.byref(self.t), n, ctypes.byref(ms)), "time_steps")
+        return ms.value
