@@ -11,7 +11,7 @@
 
 namespace roms {
 
-__global__ void k_periodic_wrap(Bounds b, double* __restrict__ a, int nlev) {
+__global__ void __launch_bounds__(256) k_periodic_wrap(Bounds b, ExchList L) {
   const int Lm = b.Lm, Mm = b.Mm;
   const int nrow = 4 * b.nx2;           // rows j=-1,0,Mm+1,Mm+2, all i
   const int ncol = 4 * Mm;              // columns i=-1,0,Lm+1,Lm+2, j=1..Mm
@@ -46,15 +46,39 @@ __global__ void k_periodic_wrap(Bounds b, double* __restrict__ a, int nlev) {
   } else {
     return;
   }
-  const long dst = IJ(b, i, j), src = IJ(b, si, sj);
-  for (int k = 0; k < nlev; k++) a[dst + k * b.n2] = a[src + k * b.n2];
+  // grid.y enumerates the (array, level) pairs of the list: one copy per thread
+  int lev = blockIdx.y, q = 0;
+  while (q < L.n - 1 && lev >= L.nlev[q]) { lev -= L.nlev[q]; q++; }
+  if (lev >= L.nlev[q]) return;
+  const long off = (long)lev * b.n2;
+  L.p[q][IJ(b, i, j) + off] = L.p[q][IJ(b, si, sj) + off];
 }
 
-void launch_exchange(const Dev& d, hipStream_t s, double* a, int nlev) {
+void launch_exchange_list(const Dev& d, hipStream_t s, const ExchList& L) {
   const Bounds& b = d.b;
   if (!b.ew_periodic && !b.ns_periodic) return;
   const int n = 4 * b.nx2 + 4 * b.Mm;
-  hipLaunchKernelGGL(k_periodic_wrap, dim3((n + 255) / 256), dim3(256), 0, s, b, a, nlev);
+  int nl = 0;
+  for (int q = 0; q < L.n; q++) nl += L.nlev[q];
+  if (nl == 0) return;
+  hipLaunchKernelGGL(k_periodic_wrap, dim3((n + 255) / 256, nl), dim3(256), 0, s, b, L);
+}
+void launch_exchange_tracers(const Dev& d, hipStream_t s, int tlev) {
+  const Bounds& b = d.b;
+  ExchList L{};
+  for (int itrc = 1; itrc <= b.NT; itrc++) {
+    L.p[L.n] = d.f.t + (long)(tlev - 1) * b.n3 + (long)(itrc - 1) * 3 * b.n3;
+    L.nlev[L.n++] = b.N;
+    if (L.n == 8 || itrc == b.NT) {
+      launch_exchange_list(d, s, L);
+      L.n = 0;
+    }
+  }
+}
+void launch_exchange(const Dev& d, hipStream_t s, double* a, int nlev) {
+  ExchList L{};
+  L.p[0] = a; L.nlev[0] = nlev; L.n = 1;
+  launch_exchange_list(d, s, L);
 }
 
 // ---- 3-D closed-wall BCs: one lane per edge point, loop over k ----

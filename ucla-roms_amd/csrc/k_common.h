@@ -13,6 +13,21 @@
 
 namespace roms {
 
+// A lane's column scratch (levels 0..N) in LDS: level k of lane l at
+// smem[k*kCX + l], so a wavefront touches 64 consecutive doubles per level
+// (conflict-free).  Sweeps that keep their forward-elimination results here
+// issue no global stores until the back-substitution, so the global loads of
+// the inputs carry no aliasing hazards and can be scheduled ahead of use.
+struct ColLds {
+  double* p;
+  __device__ __forceinline__ double& operator[](int k) const { return p[k * kCX]; }
+};
+extern __shared__ double roms_smem[];
+__device__ __forceinline__ ColLds col_lds(int slot, int N) {
+  return ColLds{roms_smem + (long)slot * (N + 1) * kCX + threadIdx.x};
+}
+inline size_t col_lds_bytes(int nslots, int N) { return (size_t)nslots * (N + 1) * kCX * sizeof(double); }
+
 // ---- pseudo-continuity of the predictor (pre_step3d4S.F:136-148) ----
 __device__ __forceinline__ void hz_bak_fwd(const Dev& d, int i, int j, int k, double cff, double& bak, double& fwd) {
   const Bounds& b = d.b;
@@ -304,6 +319,53 @@ __device__ __forceinline__ void uv_vert_rhs(const Dev& d, int i, int j, int nrhs
     fc1 = fck;
   }
   rr[ij] = rr[ij] - dc1;
+}
+
+// ---- SPLINE_UV with LDS column scratch: leaves the vertical advective flux
+// of u (dir 0) / v (dir 1) at w-levels in A[k], k=0..N, A[0]=A[N]=0
+// (compute_vert_rhs_uv_terms.h); the r.h.s. update is rr(k) = rr(k) - A[k] +
+// A[k-1] in that order (uv_rr_update).
+__device__ __forceinline__ void uv_vert_flux_lds(const Dev& d, long ij, int nrhs, int dir, const ColLds& A,
+                                                 const ColLds& B) {
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const int N = b.N;
+  const long n2 = b.n2;
+  const long s = dir == 0 ? 1 : b.nx2;
+  const double* __restrict__ Uv = (dir == 0 ? F.u : F.v) + (long)(nrhs - 1) * b.n3 + ij;
+  const double* __restrict__ Hz = F.Hz + ij;
+  const double* __restrict__ We = F.We + ij;
+  const double* mask = dir == 0 ? F.umask : F.vmask;
+  auto DCk = [&](int k) {
+    const long o = (long)(k - 1) * n2;
+    return 0.5625 * (Hz[o] + Hz[o - s]) - 0.0625 * (Hz[o + s] + Hz[o - 2 * s]);
+  };
+  double dck = DCk(1), cfk = 1.0, fcm = 2.0 * Uv[0];
+#pragma unroll 4
+  for (int k = 1; k <= N - 1; k++) {
+    const double dc1 = DCk(k + 1);
+    const double cff = 1.0 / (2.0 * dck + dc1 * (2.0 - cfk));
+    const double cf1 = cff * dck;
+    const long o = (long)(k - 1) * n2;
+    const double fck = cff * (3.0 * (dck * Uv[o + n2] + dc1 * Uv[o]) - dc1 * fcm);
+    B[k + 1] = cf1;
+    A[k] = fck;
+    dck = dc1; cfk = cf1; fcm = fck;
+  }
+  double fc1 = (2.0 * Uv[(long)(N - 1) * n2] - fcm) / (1.0 - cfk);  // FC(N)
+  const double m1 = mask[ij + s], m0 = mask[ij - s];
+#pragma unroll 4
+  for (int k = N - 1; k >= 1; k--) {
+    const double fck = A[k] - B[k + 1] * fc1;
+    const long w = (long)k * n2;
+    A[k] = fck * 0.5 * (We[w] + We[w - s] - 0.125 * ((We[w + s] - We[w]) * m1 - (We[w - s] - We[w - 2 * s]) * m0));
+    fc1 = fck;
+  }
+  A[0] = 0.0;
+  A[N] = 0.0;
+}
+__device__ __forceinline__ double uv_rr_update(double r, const ColLds& A, int k) {
+  return k == 1 ? r - A[1] : r - A[k] + A[k - 1];
 }
 
 }  // namespace roms

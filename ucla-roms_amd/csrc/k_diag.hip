@@ -29,7 +29,7 @@ __device__ __forceinline__ double diag_vb(const Dev& d, int i, int j, int nstp) 
          (F.z_w[ij + N * n2] + F.z_w[ij - sj + N * n2] - F.z_w[ij] - F.z_w[ij - sj]);
 }
 
-__global__ void k_diag(Dev d, Range R, int nstp) {
+__global__ void __launch_bounds__(256) k_diag(Dev d, Range R, int nstp) {
   ROMS_IJ_OR_RETURN(R)
   const Bounds& b = d.b;
   const Fields& F = d.f;

@@ -10,91 +10,127 @@ struct PreCoef {
   double dtau, cf_stp, cf_bak;
 };
 
-// ---- tracers: horizontal 4th-order fluxes, vertical spline advection and the
-// implicit vertical diffusion with Wi up-winding, one lane per column. ----
-__global__ void k_pre_tracer(Dev d, Range R, PreCoef c, int nstp, int nnew, int nrhs) {
+// ---- tracers, horizontal part: one thread per (i,j,k) cell, all tracers:
+// t(nnew) = Hz_bak*(cf_stp*t(nstp)+cf_bak*t(indx)) - dtau*pm*pn*div(FX,FE),
+// t(indx) = Hz*t(nstp). ----
+__global__ void __launch_bounds__(256) k_pre_tracer_h(Dev d, Range R, PreCoef c, int nstp, int nnew, int nrhs) {
   ROMS_IJ_OR_RETURN(R)
   const Bounds& b = d.b;
   const Fields& F = d.f;
-  const int N = b.N, indx = 3 - nstp;
-  const long n2 = b.n2, ij = IJ(b, i, j);
-  double* FCs = F.c0;  // spline interface values / fluxes
-  double* CFs = F.c1;
-  double* DCs = F.c2;
+  const int k = 1 + (int)blockIdx.z, indx = 3 - nstp;
+  const long ij = IJ(b, i, j), o = ij + (long)(k - 1) * b.n2;
+  double hb, hf;
+  hz_bak_fwd(d, i, j, k, 0.5 * c.dtau, hb, hf);
+  F.c2[o] = hf;  // Hz_fwd, Hz_bak kept for the column solves (range istr-1.., jstr-1..)
+  F.c3[o] = hb;
+  if (i < b.istr || j < b.jstr) return;
+  const double hz = F.Hz[o];
   for (int itrc = 1; itrc <= b.NT; itrc++) {
-    const double* Tr = F.t + (long)(nrhs - 1) * b.n3 + (long)(itrc - 1) * 3 * b.n3;
-    double* Tn = F.t + (long)(nnew - 1) * b.n3 + (long)(itrc - 1) * 3 * b.n3;
-    double* Ti = F.t + (long)(indx - 1) * b.n3 + (long)(itrc - 1) * 3 * b.n3;
-    const double* Ts = F.t + (long)(nstp - 1) * b.n3 + (long)(itrc - 1) * 3 * b.n3;
-    for (int k = 1; k <= N; k++) {
-      double hb, hf;
-      hz_bak_fwd(d, i, j, k, 0.5 * c.dtau, hb, hf);
-      const double FX0 = tracer_fx(d, Tr, i, j, k, false), FX1 = tracer_fx(d, Tr, i + 1, j, k, false);
-      const double FE0 = tracer_fe(d, Tr, i, j, k, false), FE1 = tracer_fe(d, Tr, i, j + 1, k, false);
-      const long o = ij + (long)(k - 1) * n2;
-      const double tsk = Ts[o];
-      Tn[o] = hb * (c.cf_stp * tsk + c.cf_bak * Ti[o]) - c.dtau * F.pm[ij] * F.pn[ij] * (FX1 - FX0 + FE1 - FE0);
-      Ti[o] = F.Hz[o] * tsk;
+    const long tb = (long)(itrc - 1) * 3 * b.n3;
+    const double* Tr = F.t + (long)(nrhs - 1) * b.n3 + tb;
+    double* Tn = F.t + (long)(nnew - 1) * b.n3 + tb;
+    double* Ti = F.t + (long)(indx - 1) * b.n3 + tb;
+    const double* Ts = F.t + (long)(nstp - 1) * b.n3 + tb;
+    const double FX0 = tracer_fx(d, Tr, i, j, k, false), FX1 = tracer_fx(d, Tr, i + 1, j, k, false);
+    const double FE0 = tracer_fe(d, Tr, i, j, k, false), FE1 = tracer_fe(d, Tr, i, j + 1, k, false);
+    const double tsk = Ts[o];
+    Tn[o] = hb * (c.cf_stp * tsk + c.cf_bak * Ti[o]) - c.dtau * F.pm[ij] * F.pn[ij] * (FX1 - FX0 + FE1 - FE0);
+    Ti[o] = hz * tsk;
+  }
+}
+
+// ---- tracers, vertical part per column: spline advection on t(nrhs), then
+// implicit diffusion with Wi up-winding on Hz_fwd (LDS slots A, B). ----
+__global__ void __launch_bounds__(64) k_pre_tracer_v(Dev d, Range R, PreCoef c, int nnew, int nrhs) {
+  ROMS_IJC_OR_RETURN(R)
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const int N = b.N;
+  const long n2 = b.n2, ij = IJ(b, i, j);
+  const double* __restrict__ Hz = F.Hz + ij;
+  const double* __restrict__ We = F.We + ij;
+  const double* __restrict__ Wi = F.Wi + ij;
+  const ColLds A = col_lds(0, N), B = col_lds(1, N);
+  const double* __restrict__ Hf = F.c2 + ij;
+  auto hfwd = [&](int k) { return Hf[(long)(k - 1) * n2]; };
+  {
+    const int itrc = 1 + (int)blockIdx.z;
+    const long tb = (long)(itrc - 1) * 3 * b.n3;
+    const double* __restrict__ Tr = F.t + (long)(nrhs - 1) * b.n3 + tb + ij;
+    double* __restrict__ Tn = F.t + (long)(nnew - 1) * b.n3 + tb + ij;
+    double cfk = 1.0, fcm = 2.0 * Tr[0], hk = Hz[0], tk = Tr[0];
+#pragma unroll 4
+    for (int k = 1; k <= N - 1; k++) {
+      const double hk1 = Hz[(long)k * n2], tk1 = Tr[(long)k * n2];
+      const double cff = 1.0 / (2.0 * hk + hk1 * (2.0 - cfk));
+      const double cf1 = cff * hk;
+      const double fck = cff * (3.0 * (hk * tk1 + hk1 * tk) - hk1 * fcm);
+      B[k + 1] = cf1;
+      A[k] = fck;
+      cfk = cf1; fcm = fck; hk = hk1; tk = tk1;
     }
-    // vertical advective fluxes (spline on t(nrhs)) -> Tn
-    tracer_spline_fc(d, Tr, ij, FCs, CFs);
-    for (int k = 1; k <= N; k++) {
-      const long o = ij + (long)(k - 1) * n2;
-      Tn[o] = Tn[o] - c.dtau * F.pm[ij] * F.pn[ij] * (FCs[ij + (long)k * n2] - FCs[ij + (long)(k - 1) * n2]);
+    double fc1 = (2.0 * tk - fcm) / (1.0 - cfk);
+#pragma unroll 4
+    for (int k = N - 1; k >= 0; k--) {
+      const double fck = A[k] - B[k + 1] * fc1;
+      A[k + 1] = fc1 * We[(long)(k + 1) * n2];
+      A[k] = fck;
+      fc1 = fck;
     }
-    // implicit vertical diffusion (Thomas, top-down elimination written bottom-up)
+    A[N] = 0.0;
+    A[0] = 0.0;
+    auto tval = [&](int k) {
+      return Tn[(long)(k - 1) * n2] - c.dtau * F.pm[ij] * F.pn[ij] * (A[k] - A[k - 1]);
+    };
     const int iAkt = itrc < b.nTS ? itrc : b.nTS;
-    const double* Akt = F.Akt + (long)(iAkt - 1) * b.n3w;
-    double hf1, hf2, dummy;
-    hz_bak_fwd(d, i, j, 1, 0.5 * c.dtau, dummy, hf1);
-    hz_bak_fwd(d, i, j, 2, 0.5 * c.dtau, dummy, hf2);
+    const double* __restrict__ Akt = F.Akt + (long)(iAkt - 1) * b.n3w + ij;
     const double DC0 = c.dtau * F.pm[ij] * F.pn[ij];
-    double FCk = 2.0 * c.dtau * Akt[ij + n2] / (hf2 + hf1);
-    double WCk = DC0 * F.Wi[ij + n2];
+    const double hf1 = hfwd(1);
+    double hfk = hfwd(2);
+    double FCk = 2.0 * c.dtau * Akt[n2] / (hfk + hf1);
+    double WCk = DC0 * Wi[n2];
     double cff = 1.0 / (hf1 + FCk + fmax0(WCk));
     double CFk = cff * (FCk - fmin0(WCk));
-    double DCk = cff * Tn[ij];
-    CFs[ij + n2] = CFk;
-    DCs[ij + n2] = DCk;
-    double hfk = hf2;
+    double DCk = cff * tval(1);
+    B[1] = CFk;
+    A[0] = DCk;
+#pragma unroll 2
     for (int k = 2; k <= N - 1; k++) {
-      double hfk1;
-      hz_bak_fwd(d, i, j, k + 1, 0.5 * c.dtau, dummy, hfk1);
-      const double FCn = 2.0 * c.dtau * Akt[ij + (long)k * n2] / (hfk1 + hfk);
-      const double WCn = DC0 * F.Wi[ij + (long)k * n2];
+      const double hfk1 = hfwd(k + 1);
+      const double FCn = 2.0 * c.dtau * Akt[(long)k * n2] / (hfk1 + hfk);
+      const double WCn = DC0 * Wi[(long)k * n2];
       cff = 1.0 / (hfk + FCn + fmax0(WCn) + FCk - fmin0(WCk) - CFk * (FCk + fmax0(WCk)));
       const double CFn = cff * (FCn - fmin0(WCn));
-      const double DCn = cff * (Tn[ij + (long)(k - 1) * n2] + DCk * (FCk + fmax0(WCk)));
-      CFs[ij + (long)k * n2] = CFn;
-      DCs[ij + (long)k * n2] = DCn;
+      const double DCn = cff * (tval(k) + DCk * (FCk + fmax0(WCk)));
+      B[k] = CFn;
+      A[k - 1] = DCn;
       FCk = FCn; WCk = WCn; CFk = CFn; DCk = DCn; hfk = hfk1;
     }
-    // hfk is Hz_fwd(N) here (N>=3); for N==2 it is hf2
-    const long oN = ij + (long)(N - 1) * n2;
-    double tk = (Tn[oN] + DCk * (FCk + fmax0(WCk))) / (hfk + FCk - fmin0(WCk) - CFk * (FCk + fmax0(WCk)));
-    Tn[oN] = tk;
+    const long oN = (long)(N - 1) * n2;
+    double tt = (tval(N) + DCk * (FCk + fmax0(WCk))) / (hfk + FCk - fmin0(WCk) - CFk * (FCk + fmax0(WCk)));
+    Tn[oN] = tt;
+#pragma unroll 4
     for (int k = N - 1; k >= 1; k--) {
-      const long o = ij + (long)(k - 1) * n2;
-      tk = DCs[ij + (long)k * n2] + CFs[ij + (long)k * n2] * tk;
-      Tn[o] = tk;
+      tt = A[k - 1] + B[k] * tt;
+      Tn[(long)(k - 1) * n2] = tt;
     }
   }
 }
 
 // ---- horizontal momentum r.h.s. for all levels (pre_step3d / step3d_uv1) ----
-__global__ void k_uv_horiz(Dev d, Range R, int nrhs, UVBounds ub, int up) {
+__global__ void __launch_bounds__(256) k_uv_horiz(Dev d, Range R, int nrhs, UVBounds ub, int up) {
   ROMS_IJ_OR_RETURN(R)
-  for (int k = 1; k <= d.b.N; k++) uv_horiz_rhs(d, i, j, k, nrhs, ub, up != 0);
+  uv_horiz_rhs(d, i, j, 1 + (int)blockIdx.z, nrhs, ub, up != 0);
 }
 
 void launch_uv_horiz(const Dev& d, hipStream_t s, int nrhs, int up) {
   const Bounds& b = d.b;
   Range R{b.istr, b.iend, b.jstr, b.jend};
-  hipLaunchKernelGGL(k_uv_horiz, grid_of(R), dim3(kBX, kBY), 0, s, d, R, nrhs, uv_bounds(b), up);
+  hipLaunchKernelGGL(k_uv_horiz, grid3_of(R, b.N), dim3(kBX, kBY), 0, s, d, R, nrhs, uv_bounds(b), up);
 }
 
 // ---- bottom drag r_D (compute_rd_bott_drag.h), log-layer with Zob ----
-__global__ void k_rd(Dev d, Range R, int nstp) {
+__global__ void __launch_bounds__(256) k_rd(Dev d, Range R, int nstp) {
   ROMS_IJ_OR_RETURN(R)
   const Bounds& b = d.b;
   const Fields& F = d.f;
@@ -112,78 +148,98 @@ __global__ void k_rd(Dev d, Range R, int nstp) {
   }
 }
 
-// ---- momentum: vertical spline advection into ru/rv, then implicit
-// viscosity with implicit no-slip bottom (IMPLCT_NO_SLIP_BTTM_BC) ----
-__device__ void pre_uv_solve(const Dev& d, int i, int j, int dir, const PreCoef& c, int nstp, int nnew) {
+// ---- momentum, per column: vertical spline advection into ru/rv, then
+// implicit viscosity with implicit no-slip bottom (IMPLCT_NO_SLIP_BTTM_BC).
+// LDS: A = spline FC -> flux -> DC(k); B = spline CF -> CF(k-1). ----
+__device__ __forceinline__ void pre_uv_col(const Dev& d, int i, int j, int dir, const PreCoef& c, int nstp, int nnew,
+                                           int nrhs, const ColLds& A, const ColLds& B) {
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const int N = b.N, indx = 3 - nstp;
   const long n2 = b.n2, ij = IJ(b, i, j);
   const long s = dir == 0 ? 1 : b.nx2;
+  uv_vert_flux_lds(d, ij, nrhs, dir, A, B);
   double* Uall = dir == 0 ? F.u : F.v;
-  const double* rr = dir == 0 ? F.ru : F.rv;
-  const double* Ustp = Uall + (long)(nstp - 1) * b.n3;
-  double* Uidx = Uall + (long)(indx - 1) * b.n3;
-  double* Unew = Uall + (long)(nnew - 1) * b.n3;
+  double* __restrict__ rr = (dir == 0 ? F.ru : F.rv) + ij;
+  const double* __restrict__ Ustp = Uall + (long)(nstp - 1) * b.n3 + ij;
+  double* __restrict__ Uidx = Uall + (long)(indx - 1) * b.n3 + ij;
+  double* __restrict__ Unew = Uall + (long)(nnew - 1) * b.n3 + ij;
+  const double* __restrict__ Hz = F.Hz + ij;
+  const double* __restrict__ Akv = F.Akv + ij;
+  const double* __restrict__ Wi = F.Wi + ij;
   const double sstr = dir == 0 ? F.sustr[ij] : F.svstr[ij];
-  double* CFs = F.c1;
-  double* DCs = F.c2;
-  const double hcf = 0.5 * c.dtau;
-  auto hf = [&](int ii, int jj, int k) { double bb, ff; hz_bak_fwd(d, ii, jj, k, hcf, bb, ff); return ff; };
-  auto hb = [&](int ii, int jj, int k) { double bb, ff; hz_bak_fwd(d, ii, jj, k, hcf, bb, ff); return bb; };
-  const int im = dir == 0 ? i - 1 : i, jm = dir == 0 ? j : j - 1;
   const double DC0 = c.dtau * 0.25 * (F.pm[ij] + F.pm[ij - s]) * (F.pn[ij] + F.pn[ij - s]);
-  // initial DC(k) (computed on the fly) and u(indx) = Hz*u(nstp)
-  auto DCinit = [&](int k) {
-    const long o = ij + (long)(k - 1) * n2;
-    const double r = 0.5 * (hb(i, j, k) + hb(im, jm, k)) * (c.cf_stp * Ustp[o] + c.cf_bak * Uidx[o]) + DC0 * rr[o];
-    Uidx[o] = 0.5 * (F.Hz[o] + F.Hz[o - s]) * Ustp[o];
-    return r;
+  // DC(k) before elimination; also stores u(indx) = Hz*u(nstp) and the final ru
+  auto DCinit = [&](int k, double hbk, double hbkm) {
+    const long o = (long)(k - 1) * n2;
+    const double r = uv_rr_update(rr[o], A, k);
+    rr[o] = r;
+    const double us = Ustp[o];
+    const double v = 0.5 * (hbk + hbkm) * (c.cf_stp * us + c.cf_bak * Uidx[o]) + DC0 * r;
+    Uidx[o] = 0.5 * (Hz[o] + Hz[o - s]) * us;
+    return v;
   };
-  const double* Akv = F.Akv;
-  double hfN = hf(i, j, N), hfNm = hf(im, jm, N);
-  double hfK = hf(i, j, N - 1), hfKm = hf(im, jm, N - 1);
-  double FCk = 2.0 * c.dtau * (Akv[ij + (long)(N - 1) * n2] + Akv[ij - s + (long)(N - 1) * n2]) / (hfN + hfNm + hfK + hfKm);
-  double WCk = DC0 * 0.5 * (F.Wi[ij + (long)(N - 1) * n2] + F.Wi[ij - s + (long)(N - 1) * n2]);
+  const double* __restrict__ Hf = F.c2 + ij;
+  const double* __restrict__ Hb = F.c3 + ij;
+  const long ms = dir == 0 ? -1 : -(long)b.nx2;   // offset of the (im,jm) column
+  auto lev = [&](int k) { return (long)(k - 1) * n2; };
+  const double hbN = Hb[lev(N)], hfN = Hf[lev(N)], hbNm = Hb[lev(N) + ms], hfNm = Hf[lev(N) + ms];
+  double hbK = Hb[lev(N - 1)], hfK = Hf[lev(N - 1)], hbKm = Hb[lev(N - 1) + ms], hfKm = Hf[lev(N - 1) + ms];
+  double FCk = 2.0 * c.dtau * (Akv[(long)(N - 1) * n2] + Akv[(long)(N - 1) * n2 - s]) / (hfN + hfNm + hfK + hfKm);
+  double WCk = DC0 * 0.5 * (Wi[(long)(N - 1) * n2] + Wi[(long)(N - 1) * n2 - s]);
   double cff = 1.0 / (0.5 * (hfN + hfNm) + FCk - fmin0(WCk));
-  double CFk = cff * (FCk + fmax0(WCk));   // CF(N-1)
-  double DCk1 = cff * (DCinit(N) + c.dtau * sstr);  // DC(N)
-  DCs[ij + (long)N * n2] = DCk1;
-  CFs[ij + (long)(N - 1) * n2] = CFk;
-  // level k quantities: FCk=FC(k), WCk=WC(k), CFk=CF(k); hfK/hfKm = Hz_fwd(k)
+  double CFk = cff * (FCk + fmax0(WCk));             // CF(N-1)
+  double DCk1 = cff * (DCinit(N, hbN, hbNm) + c.dtau * sstr);  // DC(N)
+  A[N] = DCk1;
+  B[N - 1] = CFk;
+#pragma unroll 2
   for (int k = N - 1; k >= 2; k--) {
-    const double hfL = hf(i, j, k - 1), hfLm = hf(im, jm, k - 1);
-    const double FCl = 2.0 * c.dtau * (Akv[ij + (long)(k - 1) * n2] + Akv[ij - s + (long)(k - 1) * n2]) / (hfK + hfKm + hfL + hfLm);
-    const double WCl = DC0 * 0.5 * (F.Wi[ij + (long)(k - 1) * n2] + F.Wi[ij - s + (long)(k - 1) * n2]);
+    const double hbL = Hb[lev(k - 1)], hfL = Hf[lev(k - 1)], hbLm = Hb[lev(k - 1) + ms], hfLm = Hf[lev(k - 1) + ms];
+    const double FCl =
+        2.0 * c.dtau * (Akv[(long)(k - 1) * n2] + Akv[(long)(k - 1) * n2 - s]) / (hfK + hfKm + hfL + hfLm);
+    const double WCl = DC0 * 0.5 * (Wi[(long)(k - 1) * n2] + Wi[(long)(k - 1) * n2 - s]);
     cff = 1.0 / (0.5 * (hfK + hfKm) + FCl - fmin0(WCl) + FCk + fmax0(WCk) - CFk * (FCk - fmin0(WCk)));
     const double CFl = cff * (FCl + fmax0(WCl));
-    const double DCk = cff * (DCinit(k) + DCk1 * (FCk - fmin0(WCk)));
-    CFs[ij + (long)(k - 1) * n2] = CFl;
-    DCs[ij + (long)k * n2] = DCk;
-    DCk1 = DCk; FCk = FCl; WCk = WCl; CFk = CFl; hfK = hfL; hfKm = hfLm;
+    const double DCk = cff * (DCinit(k, hbK, hbKm) + DCk1 * (FCk - fmin0(WCk)));
+    B[k - 1] = CFl;
+    A[k] = DCk;
+    DCk1 = DCk; FCk = FCl; WCk = WCl; CFk = CFl;
+    hbK = hbL; hfK = hfL; hbKm = hbLm; hfKm = hfLm;
   }
-  // bottom: FCk=FC(1), WCk=WC(1), CFk=CF(1), DCk1=DC(2); hfK=Hz_fwd(1)
   const double rd = F.r_D[ij], rdm = F.r_D[ij - s];
-  double un = (DCinit(1) + DCk1 * (FCk - fmin0(WCk))) /
+  double un = (DCinit(1, hbK, hbKm) + DCk1 * (FCk - fmin0(WCk))) /
               (0.5 * (hfK + hfKm) + 0.5 * c.dtau * (rd + rdm) + FCk + fmax0(WCk) - CFk * (FCk - fmin0(WCk)));
-  Unew[ij] = un;
+  Unew[0] = un;
+#pragma unroll 4
   for (int k = 2; k <= N; k++) {
-    un = DCs[ij + (long)k * n2] + CFs[ij + (long)(k - 1) * n2] * un;
-    Unew[ij + (long)(k - 1) * n2] = un;
+    un = A[k] + B[k - 1] * un;
+    Unew[(long)(k - 1) * n2] = un;
   }
 }
 
-__global__ void k_pre_uv(Dev d, Range R, PreCoef c, int nstp, int nnew, int nrhs) {
-  ROMS_IJ_OR_RETURN(R)
+__global__ void __launch_bounds__(64) k_pre_uv(Dev d, Range R, PreCoef c, int nstp, int nnew, int nrhs) {
+  ROMS_IJC_OR_RETURN(R)
   const Bounds& b = d.b;
-  if (i >= b.istrU && i <= b.iend && j >= b.jstr && j <= b.jend) {
-    uv_vert_rhs(d, i, j, nrhs, 0, d.f.c0, d.f.c1);
-    pre_uv_solve(d, i, j, 0, c, nstp, nnew);
+  const ColLds A = col_lds(0, b.N), B = col_lds(1, b.N);
+  if (blockIdx.z == 0) {
+    if (i >= b.istrU && i <= b.iend && j >= b.jstr && j <= b.jend) pre_uv_col(d, i, j, 0, c, nstp, nnew, nrhs, A, B);
+  } else {
+    if (i >= b.istr && i <= b.iend && j >= b.jstrV && j <= b.jend) pre_uv_col(d, i, j, 1, c, nstp, nnew, nrhs, A, B);
   }
-  if (i >= b.istr && i <= b.iend && j >= b.jstrV && j <= b.jend) {
-    uv_vert_rhs(d, i, j, nrhs, 1, d.f.c0, d.f.c1);
-    pre_uv_solve(d, i, j, 1, c, nstp, nnew);
+}
+
+void setup_column_kernels_t(size_t bytes);
+void setup_column_kernels_uv1(size_t bytes);
+bool setup_column_kernels(int N) {
+  const size_t bytes = col_lds_bytes(2, N);
+  if (bytes > 160 * 1024) return false;
+  if (bytes > 64 * 1024) {
+    (void)hipFuncSetAttribute((const void*)k_pre_tracer_v, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    (void)hipFuncSetAttribute((const void*)k_pre_uv, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    setup_column_kernels_t(bytes);
+    setup_column_kernels_uv1(bytes);
   }
+  return true;
 }
 
 void launch_pre_step3d(const Dev& d, hipStream_t s, const Tlev& t) {
@@ -193,17 +249,21 @@ void launch_pre_step3d(const Dev& d, hipStream_t s, const Tlev& t) {
   if (t.iic == t.forw_start) { c.dtau = 0.5 * d.p.dt; c.cf_stp = 1.0; c.cf_bak = 0.0; }
   else { c.dtau = d.p.dt * (1.0 - AM3_crv); c.cf_stp = 0.5 + AM3_crv; c.cf_bak = 0.5 - AM3_crv; }
   Range RI{b.istr, b.iend, b.jstr, b.jend};
-  hipLaunchKernelGGL(k_pre_tracer, grid_of(RI), dim3(kBX, kBY), 0, s, d, RI, c, t.nstp, t.nnew, t.nrhs);
+  Range RH{b.istr - 1, b.iend, b.jstr - 1, b.jend};
+  hipLaunchKernelGGL(k_pre_tracer_h, grid3_of(RH, b.N), dim3(kBX, kBY), 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs);
+  dim3 gt = gridc_of(RI);
+  gt.z = b.NT;
+  hipLaunchKernelGGL(k_pre_tracer_v, gt, dim3(kCX), col_lds_bytes(2, b.N), s, d, RI, c, t.nnew, t.nrhs);
   launch_uv_horiz(d, s, t.nrhs, 0);
   Range Rd{b.istrU - 1, b.iend, b.jstrV - 1, b.jend};
   hipLaunchKernelGGL(k_rd, grid_of(Rd), dim3(kBX, kBY), 0, s, d, Rd, t.nstp);
-  hipLaunchKernelGGL(k_pre_uv, grid_of(RI), dim3(kBX, kBY), 0, s, d, RI, c, t.nstp, t.nnew, t.nrhs);
+  dim3 gu = gridc_of(RI);
+  gu.z = 2;
+  hipLaunchKernelGGL(k_pre_uv, gu, dim3(kCX), col_lds_bytes(2, b.N), s, d, RI, c, t.nstp, t.nnew, t.nrhs);
   launch_u3dbc(d, s, t);
   launch_v3dbc(d, s, t);
-  for (int itrc = 1; itrc <= b.NT; itrc++) {
-    launch_t3dbc(d, s, t, itrc);
-    launch_exchange(d, s, d.f.t + (long)(t.nnew - 1) * b.n3 + (long)(itrc - 1) * 3 * b.n3, b.N);
-  }
+  for (int itrc = 1; itrc <= b.NT; itrc++) launch_t3dbc(d, s, t, itrc);
+  launch_exchange_tracers(d, s, t.nnew);
 }
 
 }  // namespace roms

@@ -17,7 +17,7 @@ __device__ __forceinline__ double harm(double a, double b) {
   return c > 0.0 ? c / (a + b) : 0.0;
 }
 
-__global__ void k_prsgrd_P(Dev d, Range R, int split) {
+__global__ void __launch_bounds__(256) k_prsgrd_P(Dev d, Range R, int split) {
   ROMS_IJ_OR_RETURN(R)
   const Bounds& b = d.b;
   const Fields& F = d.f;
@@ -81,7 +81,7 @@ __global__ void k_prsgrd_P(Dev d, Range R, int split) {
   }
 }
 
-__global__ void k_prsgrd_uv(Dev d, Range R, int split, int imin, int imax, int jmin, int jmax) {
+__global__ void __launch_bounds__(256) k_prsgrd_uv(Dev d, Range R, int split, int imin, int imax, int jmin, int jmax) {
   ROMS_IJ_OR_RETURN(R)
   const Bounds& b = d.b;
   const Fields& F = d.f;

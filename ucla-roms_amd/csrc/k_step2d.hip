@@ -40,7 +40,7 @@ __device__ __forceinline__ double s2d_DVom(const Dev& d, const FBCoef& c, long i
   return 0.5 * (s2d_Drhs(d, c, ij) + s2d_Drhs(d, c, ij - sj)) * F.dm_v[ij] * (vrhs);
 }
 
-__global__ void k_s2d_zeta(Dev d, Range R, FBCoef c) {
+__global__ void __launch_bounds__(256) k_s2d_zeta(Dev d, Range R, FBCoef c) {
   ROMS_IJ_OR_RETURN(R)
   const Bounds& b = d.b;
   const Fields& F = d.f;
@@ -106,7 +106,7 @@ __device__ __forceinline__ void fb_corr(const Dev& d, const FBCoef& c, long ij, 
   rzetaSA = zwrk * (F.rhoS[ij] - F.rhoA[ij]);
 }
 
-__global__ void k_s2d_mom(Dev d, Range R, FBCoef c) {
+__global__ void __launch_bounds__(256) k_s2d_mom(Dev d, Range R, FBCoef c) {
   ROMS_IJ_OR_RETURN(R)
   const Bounds& b = d.b;
   const Fields& F = d.f;
@@ -271,7 +271,7 @@ __global__ void k_s2d_edges(Dev d, FBCoef c, int phase) {
   }
 }
 
-__global__ void k_s2d_last(Dev d, Range R, int knew) {
+__global__ void __launch_bounds__(256) k_s2d_last(Dev d, Range R, int knew) {
   ROMS_IJ_OR_RETURN(R)
   const long ij = IJ(d.b, i, j);
   d.f.zeta[ij + (long)(knew - 1) * d.b.n2] = d.f.Zt_avg1[ij];
@@ -317,9 +317,8 @@ void launch_step2d(const Dev& d, hipStream_t s, const Tlev& t, const double* w1,
     hipLaunchKernelGGL(k_s2d_last, grid_of(RB), dim3(kBX, kBY), 0, s, d, RB, t.knew);
     launch_set_depth(d, s, t);
   }
-  launch_exchange(d, s, d.f.zeta + (long)(t.knew - 1) * b.n2, 1);
-  launch_exchange(d, s, d.f.ubar + (long)(t.knew - 1) * b.n2, 1);
-  launch_exchange(d, s, d.f.vbar + (long)(t.knew - 1) * b.n2, 1);
+  const long kn = (long)(t.knew - 1) * b.n2;
+  launch_exchange_list(d, s, ExchList{{d.f.zeta + kn, d.f.ubar + kn, d.f.vbar + kn}, {1, 1, 1}, 3});
 }
 
 }  // namespace roms

@@ -6,8 +6,27 @@
 
 namespace roms {
 
-__global__ void k_step3d_t(Dev d, Range R, int nnew, int nrhs) {
+// Horizontal advection, one thread per (i,j,k) cell, all tracers.
+__global__ void __launch_bounds__(256) k_step3d_t_h(Dev d, Range R, int nnew, int nrhs) {
   ROMS_IJ_OR_RETURN(R)
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const int k = 1 + (int)blockIdx.z;
+  const long ij = IJ(b, i, j), o = ij + (long)(k - 1) * b.n2;
+  for (int itrc = 1; itrc <= b.NT; itrc++) {
+    const double* Tr = F.t + (long)(nrhs - 1) * b.n3 + (long)(itrc - 1) * 3 * b.n3;
+    double* Tn = F.t + (long)(nnew - 1) * b.n3 + (long)(itrc - 1) * 3 * b.n3;
+    const double FX0 = tracer_fx(d, Tr, i, j, k, true), FX1 = tracer_fx(d, Tr, i + 1, j, k, true);
+    const double FE0 = tracer_fe(d, Tr, i, j, k, true), FE1 = tracer_fe(d, Tr, i, j + 1, k, true);
+    Tn[o] = Tn[o] - d.p.dt * F.pm[ij] * F.pn[ij] * (FX1 - FX0 + FE1 - FE0);
+  }
+}
+
+// Vertical part per column: spline advection on t(nrhs), surface fluxes
+// (+ KPP non-local and solar terms), implicit diffusion.  LDS slots: A holds
+// FC (spline) then DC(k) at A[k-1]; B holds the spline CF then Thomas CF.
+__global__ void __launch_bounds__(64) k_step3d_t_v(Dev d, Range R, int nnew, int nrhs) {
+  ROMS_IJC_OR_RETURN(R)
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const Params& P = d.p;
@@ -15,86 +34,106 @@ __global__ void k_step3d_t(Dev d, Range R, int nnew, int nrhs) {
   const double dt = P.dt;
   const long n2 = b.n2, ij = IJ(b, i, j);
   const double rm = F.rmask[ij];
-  double* FCs = F.c0;
-  double* CFs = F.c1;
-  double* DCs = F.c2;
-  for (int itrc = 1; itrc <= b.NT; itrc++) {
-    const double* Tr = F.t + (long)(nrhs - 1) * b.n3 + (long)(itrc - 1) * 3 * b.n3;
-    double* Tn = F.t + (long)(nnew - 1) * b.n3 + (long)(itrc - 1) * 3 * b.n3;
+  const double* __restrict__ Hz = F.Hz + ij;
+  const ColLds A = col_lds(0, N), B = col_lds(1, N);
+  {
+    const int itrc = 1 + (int)blockIdx.z;
+    const double* __restrict__ Tr = F.t + (long)(nrhs - 1) * b.n3 + (long)(itrc - 1) * 3 * b.n3 + ij;
+    double* __restrict__ Tn = F.t + (long)(nnew - 1) * b.n3 + (long)(itrc - 1) * 3 * b.n3 + ij;
     const double stf = F.stflx[ij + (long)(itrc - 1) * n2];
-    for (int k = 1; k <= N; k++) {
-      const double FX0 = tracer_fx(d, Tr, i, j, k, true), FX1 = tracer_fx(d, Tr, i + 1, j, k, true);
-      const double FE0 = tracer_fe(d, Tr, i, j, k, true), FE1 = tracer_fe(d, Tr, i, j + 1, k, true);
-      const long o = ij + (long)(k - 1) * n2;
-      Tn[o] = Tn[o] - dt * F.pm[ij] * F.pn[ij] * (FX1 - FX0 + FE1 - FE0);
+    // spline interface values FC(0:N) (compute_vert_tracer_fluxes.h)
+    double cfk = 1.0, fcm = 2.0 * Tr[0], hk = Hz[0], tk = Tr[0];
+    A[0] = fcm;
+#pragma unroll 4
+    for (int k = 1; k <= N - 1; k++) {
+      const double hk1 = Hz[(long)k * n2], tk1 = Tr[(long)k * n2];
+      const double cff = 1.0 / (2.0 * hk + hk1 * (2.0 - cfk));
+      const double cf1 = cff * hk;
+      const double fck = cff * (3.0 * (hk * tk1 + hk1 * tk) - hk1 * fcm);
+      B[k + 1] = cf1;
+      A[k] = fck;
+      cfk = cf1; fcm = fck; hk = hk1; tk = tk1;
     }
-    tracer_spline_fc(d, Tr, ij, FCs, CFs);
-    for (int k = 1; k <= N; k++) {
-      const long o = ij + (long)(k - 1) * n2;
-      Tn[o] = Tn[o] - dt * F.pm[ij] * F.pn[ij] * (FCs[ij + (long)k * n2] - FCs[ij + (long)(k - 1) * n2]);
+    double fc1 = (2.0 * tk - fcm) / (1.0 - cfk);
+#pragma unroll 4
+    for (int k = N - 1; k >= 0; k--) {
+      const double fck = A[k] - B[k + 1] * fc1;
+      A[k + 1] = fc1 * F.We[ij + (long)(k + 1) * n2];
+      A[k] = fck;
+      fc1 = fck;
     }
-    const long oN = ij + (long)(N - 1) * n2;
-    if (itrc == 1) Tn[oN] = Tn[oN] + dt * F.swflx[ij] * Tn[oN] / F.Hz[oN];
-    Tn[oN] = Tn[oN] + dt * stf;
-    if (P.lmd) {
-      if (itrc == 1) {
-        const double sr = F.srflx[ij];
-        for (int k = N - 1; k >= 1; k--) {
-          const long w = ij + (long)k * n2, o = ij + (long)(k - 1) * n2;
-          const double cff = sr * F.swr_frac[w] - F.ghat[w] * (stf - sr);
-          Tn[o + n2] = Tn[o + n2] - dt * cff;
-          Tn[o] = Tn[o] + dt * cff;
-        }
-      } else if (itrc == 2 && P.salinity) {
-        for (int k = N - 1; k >= 1; k--) {
-          const long w = ij + (long)k * n2, o = ij + (long)(k - 1) * n2;
-          const double cff = -dt * F.ghat[w] * stf;
-          Tn[o + n2] = Tn[o + n2] - cff;
-          Tn[o] = Tn[o] + cff;
-        }
-      }
-    }
+    A[N] = 0.0;
+    A[0] = 0.0;
+    // advective update + surface/KPP terms fused into the Thomas elimination
     const int iAkt = itrc < b.nTS ? itrc : b.nTS;
-    const double* Akt = F.Akt + (long)(iAkt - 1) * b.n3w;
+    const double* __restrict__ Akt = F.Akt + (long)(iAkt - 1) * b.n3w + ij;
+    const double* __restrict__ Wi = F.Wi + ij;
     const double DC0 = dt * F.pm[ij] * F.pn[ij];
-    double FCk = 2.0 * dt * Akt[ij + n2] / (F.Hz[ij] + F.Hz[ij + n2]);
-    double WCk = DC0 * F.Wi[ij + n2];
-    double cff = 1.0 / (F.Hz[ij] + FCk + fmax0(WCk));
+    const bool kppT = P.lmd && itrc == 1, kppS = P.lmd && itrc == 2 && P.salinity;
+    const double sr = F.srflx[ij];
+    auto tval = [&](int k) {
+      const long o = (long)(k - 1) * n2;
+      double t = Tn[o] - dt * F.pm[ij] * F.pn[ij] * (A[k] - A[k - 1]);
+      if (k == N) {
+        if (itrc == 1) t = t + dt * F.swflx[ij] * t / Hz[o];
+        t = t + dt * stf;
+      }
+      if (kppT) {
+        if (k <= N - 1) t = t + dt * (sr * F.swr_frac[ij + (long)k * n2] - F.ghat[ij + (long)k * n2] * (stf - sr));
+        if (k >= 2) t = t - dt * (sr * F.swr_frac[ij + o] - F.ghat[ij + o] * (stf - sr));
+      } else if (kppS) {
+        if (k <= N - 1) t = t + (-dt * F.ghat[ij + (long)k * n2] * stf);
+        if (k >= 2) t = t - (-dt * F.ghat[ij + o] * stf);
+      }
+      return t;
+    };
+    double FCk = 2.0 * dt * Akt[n2] / (Hz[0] + Hz[n2]);
+    double WCk = DC0 * Wi[n2];
+    double cff = 1.0 / (Hz[0] + FCk + fmax0(WCk));
     double CFk = cff * (FCk - fmin0(WCk));
-    double DCk = cff * Tn[ij];
-    CFs[ij + n2] = CFk;
-    DCs[ij + n2] = DCk;
+    double DCk = cff * tval(1);
+    B[1] = CFk;
+    A[0] = DCk;
+#pragma unroll 4
     for (int k = 2; k <= N - 1; k++) {
-      const long o = ij + (long)(k - 1) * n2;
-      const double FCn = 2.0 * dt * Akt[ij + (long)k * n2] / (F.Hz[o] + F.Hz[o + n2]);
-      const double WCn = F.Wi[ij + (long)k * n2] * DC0;
-      cff = 1.0 / (F.Hz[o] + FCn + fmax0(WCn) + FCk - fmin0(WCk) - CFk * (FCk + fmax0(WCk)));
+      const long o = (long)(k - 1) * n2;
+      const double FCn = 2.0 * dt * Akt[(long)k * n2] / (Hz[o] + Hz[o + n2]);
+      const double WCn = Wi[(long)k * n2] * DC0;
+      cff = 1.0 / (Hz[o] + FCn + fmax0(WCn) + FCk - fmin0(WCk) - CFk * (FCk + fmax0(WCk)));
       const double CFn = cff * (FCn - fmin0(WCn));
-      const double DCn = cff * (Tn[o] + DCk * (FCk + fmax0(WCk)));
-      CFs[ij + (long)k * n2] = CFn;
-      DCs[ij + (long)k * n2] = DCn;
+      const double DCn = cff * (tval(k) + DCk * (FCk + fmax0(WCk)));
+      B[k] = CFn;
+      A[k - 1] = DCn;
       FCk = FCn; WCk = WCn; CFk = CFn; DCk = DCn;
     }
-    double tk = (Tn[oN] + DCk * (FCk + fmax0(WCk))) / (F.Hz[oN] + FCk - fmin0(WCk) - CFk * (FCk + fmax0(WCk))) * rm;
-    Tn[oN] = tk;
+    const long oN = (long)(N - 1) * n2;
+    double tt = (tval(N) + DCk * (FCk + fmax0(WCk))) / (Hz[oN] + FCk - fmin0(WCk) - CFk * (FCk + fmax0(WCk))) * rm;
+    Tn[oN] = tt;
+#pragma unroll 4
     for (int k = N - 1; k >= 1; k--) {
-      tk = (DCs[ij + (long)k * n2] + CFs[ij + (long)k * n2] * tk) * rm;
-      Tn[ij + (long)(k - 1) * n2] = tk;
+      tt = (A[k - 1] + B[k] * tt) * rm;
+      Tn[(long)(k - 1) * n2] = tt;
     }
   }
+}
+
+void setup_column_kernels_t(size_t bytes) {
+  (void)hipFuncSetAttribute((const void*)k_step3d_t_v, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
 void launch_step3d_t(const Dev& d, hipStream_t s, const Tlev& t) {
   const Bounds& b = d.b;
   Range R{b.istr, b.iend, b.jstr, b.jend};
-  hipLaunchKernelGGL(k_step3d_t, grid_of(R), dim3(kBX, kBY), 0, s, d, R, t.nnew, t.nrhs);
+  hipLaunchKernelGGL(k_step3d_t_h, grid3_of(R, b.N), dim3(kBX, kBY), 0, s, d, R, t.nnew, t.nrhs);
+  dim3 gt = gridc_of(R);
+  gt.z = b.NT;
+  hipLaunchKernelGGL(k_step3d_t_v, gt, dim3(kCX), col_lds_bytes(2, b.N), s, d, R, t.nnew, t.nrhs);
   for (int itrc = 1; itrc <= b.NT; itrc++) launch_t3dbc(d, s, t, itrc);
-  for (int itrc = 1; itrc <= b.NT; itrc++)
-    launch_exchange(d, s, d.f.t + (long)(t.nnew - 1) * b.n3 + (long)(itrc - 1) * 3 * b.n3, b.N);
+  launch_exchange_tracers(d, s, t.nnew);
 }
 
 // ---- t3dmix: Laplacian diffusion along S, t(nnew) += dt*pm*pn*div(F)/Hz ----
-__global__ void k_t3dmix(Dev d, Range R, int nnew, int nrhs, int itrc) {
+__global__ void __launch_bounds__(256) k_t3dmix(Dev d, Range R, int nnew, int nrhs, int itrc) {
   ROMS_IJ_OR_RETURN(R)
   const Bounds& b = d.b;
   const Fields& F = d.f;
@@ -119,10 +158,9 @@ __global__ void k_t3dmix(Dev d, Range R, int nnew, int nrhs, int itrc) {
 void launch_t3dmix(const Dev& d, hipStream_t s, const Tlev& t) {
   const Bounds& b = d.b;
   Range R{b.istr, b.iend, b.jstr, b.jend};
-  for (int itrc = 1; itrc <= b.NT; itrc++) {
+  for (int itrc = 1; itrc <= b.NT; itrc++)
     hipLaunchKernelGGL(k_t3dmix, grid_of(R), dim3(kBX, kBY), 0, s, d, R, t.nnew, t.nrhs, itrc);
-    launch_exchange(d, s, d.f.t + (long)(t.nnew - 1) * b.n3 + (long)(itrc - 1) * 3 * b.n3, b.N);
-  }
+  launch_exchange_tracers(d, s, t.nnew);
 }
 
 }  // namespace roms

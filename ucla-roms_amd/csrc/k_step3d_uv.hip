@@ -9,76 +9,89 @@ void launch_uv_horiz(const Dev& d, hipStream_t s, int nrhs, int up);
 
 // ---- step3d_uv1: implicit viscosity with implicit bottom drag r_D, result
 // stored as Hz*u in u(nnew); rufrc = vertical integral of ru + stresses ----
-__device__ void uv1_solve(const Dev& d, int i, int j, int dir, int nnew) {
+__device__ __forceinline__ void uv1_col(const Dev& d, int i, int j, int dir, int nnew, int nrhs, const ColLds& A,
+                                        const ColLds& B) {
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const int N = b.N;
   const double dt = d.p.dt;
   const long n2 = b.n2, ij = IJ(b, i, j);
   const long s = dir == 0 ? 1 : b.nx2;
-  double* Un = (dir == 0 ? F.u : F.v) + (long)(nnew - 1) * b.n3;
-  const double* rr = dir == 0 ? F.ru : F.rv;
+  uv_vert_flux_lds(d, ij, nrhs, dir, A, B);
+  double* __restrict__ Un = (dir == 0 ? F.u : F.v) + (long)(nnew - 1) * b.n3 + ij;
+  double* __restrict__ rr = (dir == 0 ? F.ru : F.rv) + ij;
+  const double* __restrict__ Hz = F.Hz + ij;
+  const double* __restrict__ Akv = F.Akv + ij;
+  const double* __restrict__ Wi = F.Wi + ij;
   const double sstr = dir == 0 ? F.sustr[ij] : F.svstr[ij];
-  double* CFs = F.c1;
-  double* DCs = F.c2;
-  const double* Hz = F.Hz;
-  const double* Akv = F.Akv;
   const double DC0 = dt * 0.25 * (F.pm[ij] + F.pm[ij - s]) * (F.pn[ij] + F.pn[ij - s]);
-  auto hz = [&](int k) { return Hz[ij + (long)(k - 1) * n2]; };
-  auto hzm = [&](int k) { return Hz[ij - s + (long)(k - 1) * n2]; };
-  auto uk = [&](int k) { return Un[ij + (long)(k - 1) * n2] + DC0 * rr[ij + (long)(k - 1) * n2]; };
-  double FCk = 2.0 * dt * (Akv[ij + (long)(N - 1) * n2] + Akv[ij - s + (long)(N - 1) * n2]) /
+  auto hz = [&](int k) { return Hz[(long)(k - 1) * n2]; };
+  auto hzm = [&](int k) { return Hz[(long)(k - 1) * n2 - s]; };
+  auto rk = [&](int k) {  // final ru(k): vertical advection added, stored back
+    const long o = (long)(k - 1) * n2;
+    const double r = uv_rr_update(rr[o], A, k);
+    rr[o] = r;
+    return r;
+  };
+  double FCk = 2.0 * dt * (Akv[(long)(N - 1) * n2] + Akv[(long)(N - 1) * n2 - s]) /
                (hz(N) + hzm(N) + hz(N - 1) + hzm(N - 1));
-  double WCk = DC0 * 0.5 * (F.Wi[ij + (long)(N - 1) * n2] + F.Wi[ij - s + (long)(N - 1) * n2]);
+  double WCk = DC0 * 0.5 * (Wi[(long)(N - 1) * n2] + Wi[(long)(N - 1) * n2 - s]);
   double cff = 1.0 / (0.5 * (hz(N) + hzm(N)) + FCk - fmin0(WCk));
   double CFk = cff * (FCk + fmax0(WCk));
-  double DCk1 = cff * (Un[ij + (long)(N - 1) * n2] + DC0 * rr[ij + (long)(N - 1) * n2] + dt * sstr);
-  DCs[ij + (long)N * n2] = DCk1;
-  CFs[ij + (long)(N - 1) * n2] = CFk;
+  double DCk1 = cff * (Un[(long)(N - 1) * n2] + DC0 * rk(N) + dt * sstr);
+  A[N] = DCk1;
+  B[N - 1] = CFk;
+#pragma unroll 2
   for (int k = N - 1; k >= 2; k--) {
-    const double FCl = 2.0 * dt * (Akv[ij + (long)(k - 1) * n2] + Akv[ij - s + (long)(k - 1) * n2]) /
+    const double FCl = 2.0 * dt * (Akv[(long)(k - 1) * n2] + Akv[(long)(k - 1) * n2 - s]) /
                        (hz(k) + hzm(k) + hz(k - 1) + hzm(k - 1));
-    const double WCl = DC0 * 0.5 * (F.Wi[ij + (long)(k - 1) * n2] + F.Wi[ij - s + (long)(k - 1) * n2]);
+    const double WCl = DC0 * 0.5 * (Wi[(long)(k - 1) * n2] + Wi[(long)(k - 1) * n2 - s]);
     cff = 1.0 / (0.5 * (hz(k) + hzm(k)) + FCl - fmin0(WCl) + FCk + fmax0(WCk) - CFk * (FCk - fmin0(WCk)));
     const double CFl = cff * (FCl + fmax0(WCl));
-    const double DCk = cff * (uk(k) + DCk1 * (FCk - fmin0(WCk)));
-    CFs[ij + (long)(k - 1) * n2] = CFl;
-    DCs[ij + (long)k * n2] = DCk;
+    const double DCk = cff * (Un[(long)(k - 1) * n2] + DC0 * rk(k) + DCk1 * (FCk - fmin0(WCk)));
+    B[k - 1] = CFl;
+    A[k] = DCk;
     DCk1 = DCk; FCk = FCl; WCk = WCl; CFk = CFl;
   }
   const double rD = F.r_D[ij], rDm = F.r_D[ij - s];
-  double dc = (uk(1) + DCk1 * (FCk - fmin0(WCk))) /
+  const double r1 = rk(1);
+  double dc = (Un[0] + DC0 * r1 + DCk1 * (FCk - fmin0(WCk))) /
               (0.5 * (hz(1) + hzm(1)) + 0.5 * dt * (rD + rDm) + FCk + fmax0(WCk) - CFk * (FCk - fmin0(WCk)));
-  Un[ij] = dc * 0.5 * (hz(1) + hzm(1));
+  Un[0] = dc * 0.5 * (hz(1) + hzm(1));
   const double dmdn = dir == 0 ? F.dm_u[ij] * F.dn_u[ij] : F.dm_v[ij] * F.dn_v[ij];
-  double frc = rr[ij] + dmdn * (sstr - 0.5 * (rDm + rD) * dc);
+  double frc = r1 + dmdn * (sstr - 0.5 * (rDm + rD) * dc);
+#pragma unroll 4
   for (int k = 2; k <= N; k++) {
-    dc = DCs[ij + (long)k * n2] + CFs[ij + (long)(k - 1) * n2] * dc;
-    Un[ij + (long)(k - 1) * n2] = dc * 0.5 * (hz(k) + hzm(k));
-    frc = frc + rr[ij + (long)(k - 1) * n2];
+    dc = A[k] + B[k - 1] * dc;
+    Un[(long)(k - 1) * n2] = dc * 0.5 * (hz(k) + hzm(k));
+    frc = frc + rr[(long)(k - 1) * n2];
   }
   if (dir == 0) F.rufrc[ij] = frc;
   else F.rvfrc[ij] = frc;
 }
 
-__global__ void k_uv1(Dev d, Range R, int nnew, int nrhs) {
-  ROMS_IJ_OR_RETURN(R)
+__global__ void __launch_bounds__(64) k_uv1(Dev d, Range R, int nnew, int nrhs) {
+  ROMS_IJC_OR_RETURN(R)
   const Bounds& b = d.b;
-  if (i >= b.istrU && i <= b.iend) {
-    uv_vert_rhs(d, i, j, nrhs, 0, d.f.c0, d.f.c1);
-    uv1_solve(d, i, j, 0, nnew);
+  const ColLds A = col_lds(0, b.N), B = col_lds(1, b.N);
+  if (blockIdx.z == 0) {
+    if (i >= b.istrU && i <= b.iend) uv1_col(d, i, j, 0, nnew, nrhs, A, B);
+  } else {
+    if (j >= b.jstrV) uv1_col(d, i, j, 1, nnew, nrhs, A, B);
   }
-  if (j >= b.jstrV) {
-    uv_vert_rhs(d, i, j, nrhs, 1, d.f.c0, d.f.c1);
-    uv1_solve(d, i, j, 1, nnew);
-  }
+}
+
+void setup_column_kernels_uv1(size_t bytes) {
+  (void)hipFuncSetAttribute((const void*)k_uv1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
 void launch_step3d_uv1(const Dev& d, hipStream_t s, const Tlev& t) {
   const Bounds& b = d.b;
   launch_uv_horiz(d, s, t.nrhs, 1);
   Range R{b.istr, b.iend, b.jstr, b.jend};
-  hipLaunchKernelGGL(k_uv1, grid_of(R), dim3(kBX, kBY), 0, s, d, R, t.nnew, t.nrhs);
+  dim3 g = gridc_of(R);
+  g.z = 2;
+  hipLaunchKernelGGL(k_uv1, g, dim3(kCX), col_lds_bytes(2, b.N), s, d, R, t.nnew, t.nrhs);
 }
 
 // ---- visc3d: harmonic viscosity along S; adds dt*cff to u,v(indx) (Hz*u)
@@ -115,7 +128,7 @@ __device__ __forceinline__ void visc_psi(const Dev& d, int i, int j, int k, int 
   VFx = cff * F.dn_p[ij] * F.dn_p[ij];
 }
 
-__global__ void k_visc3d(Dev d, Range R, int nstp) {
+__global__ void __launch_bounds__(256) k_visc3d(Dev d, Range R, int nstp) {
   ROMS_IJ_OR_RETURN(R)
   const Bounds& b = d.b;
   const Fields& F = d.f;
@@ -163,7 +176,7 @@ void launch_visc3d(const Dev& d, hipStream_t s, const Tlev& t) {
 
 // ---- step3d_uv2 part 1: convert Hz*u to u and remove the mismatch against
 // the fast-time-averaged barotropic flux DU_avg1 (at n+1 depths) ----
-__global__ void k_uv2_couple(Dev d, Range R, int nnew) {
+__global__ void __launch_bounds__(256) k_uv2_couple(Dev d, Range R, int nnew) {
   ROMS_IJ_OR_RETURN(R)
   const Bounds& b = d.b;
   const Fields& F = d.f;
@@ -198,7 +211,7 @@ __global__ void k_uv2_couple(Dev d, Range R, int nnew) {
 
 // ---- step3d_uv2 part 2: ubar,vbar(knew) from DU_avg1; corrected fluxes
 // FlxU = DELTA*FlxU + EPSIL*Hz_u*dn_u*(u(nstp)+u(nnew)), mismatch vs DU_avg2 ----
-__global__ void k_uv2_flux(Dev d, Range R, int nnew, int nstp, int knew, int iu0, int iu1, int iv0, int iv1) {
+__global__ void __launch_bounds__(256) k_uv2_flux(Dev d, Range R, int nnew, int nstp, int knew, int iu0, int iu1, int iv0, int iv1) {
   ROMS_IJ_OR_RETURN(R)
   const Bounds& b = d.b;
   const Fields& F = d.f;
@@ -259,12 +272,9 @@ void launch_step3d_uv2(const Dev& d, hipStream_t s, const Tlev& t) {
   const int j0 = b.ns_periodic ? b.jstr : b.jstrR, j1 = b.ns_periodic ? b.jend : b.jendR;
   Range R2{iv0 < iu0 ? iv0 : iu0, iu1 > iv1 ? iu1 : iv1, j0, j1};
   hipLaunchKernelGGL(k_uv2_flux, grid_of(R2), dim3(kBX, kBY), 0, s, d, R2, t.nnew, t.nstp, t.knew, iu0, iu1, iv0, iv1);
-  launch_exchange(d, s, d.f.FlxU, b.N);
-  launch_exchange(d, s, d.f.u + (long)(t.nnew - 1) * b.n3, b.N);
-  launch_exchange(d, s, d.f.ubar + (long)(t.knew - 1) * b.n2, 1);
-  launch_exchange(d, s, d.f.FlxV, b.N);
-  launch_exchange(d, s, d.f.v + (long)(t.nnew - 1) * b.n3, b.N);
-  launch_exchange(d, s, d.f.vbar + (long)(t.knew - 1) * b.n2, 1);
+  launch_exchange_list(d, s, ExchList{{d.f.FlxU, d.f.u + (long)(t.nnew - 1) * b.n3, d.f.ubar + (long)(t.knew - 1) * b.n2,
+                                        d.f.FlxV, d.f.v + (long)(t.nnew - 1) * b.n3, d.f.vbar + (long)(t.knew - 1) * b.n2},
+                                       {b.N, b.N, 1, b.N, b.N, 1}, 6});
 }
 
 }  // namespace roms

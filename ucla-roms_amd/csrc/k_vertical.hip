@@ -12,7 +12,7 @@ namespace roms {
 // set_depth_tile (set_depth.F:16-186): z_w, z_r, Hz from zeta(knew); at iic=0
 // also hinv and the initial fast-time fluxes DU_avg1/DV_avg1.
 // ---------------------------------------------------------------------------
-__global__ void k_set_depth(Dev d, Range R, int iic, int knew) {
+__global__ void __launch_bounds__(256) k_set_depth(Dev d, Range R, int iic, int knew) {
   ROMS_IJ_OR_RETURN(R)
   const Bounds& b = d.b;
   const Fields& F = d.f;
@@ -50,15 +50,13 @@ void launch_set_depth(const Dev& d, hipStream_t s, const Tlev& t) {
   Range R{b.istrR, b.iendR, b.jstrR, b.jendR};
   hipLaunchKernelGGL(k_set_depth, grid_of(R), dim3(kBX, kBY), 0, s, d, R, t.iic, t.knew);
   if (t.iic == 0) launch_exchange(d, s, d.f.hinv, 1);
-  launch_exchange(d, s, d.f.z_w, b.N + 1);
-  launch_exchange(d, s, d.f.z_r, b.N);
-  launch_exchange(d, s, d.f.Hz, b.N);
+  launch_exchange_list(d, s, ExchList{{d.f.z_w, d.f.z_r, d.f.Hz}, {b.N + 1, b.N, b.N}, 3});
 }
 
 // ---------------------------------------------------------------------------
 // set_HUV_tile (set_depth.F:190-234)
 // ---------------------------------------------------------------------------
-__global__ void k_set_huv(Dev d, Range R, int nrhs) {
+__global__ void __launch_bounds__(256) k_set_huv(Dev d, Range R, int nrhs) {
   ROMS_IJ_OR_RETURN(R)
   const Bounds& b = d.b;
   const Fields& F = d.f;
@@ -85,15 +83,14 @@ void launch_set_huv(const Dev& d, hipStream_t s, const Tlev& t) {
   const Bounds& b = d.b;
   Range R{b.istrR < b.istr ? b.istrR : b.istr, b.iendR, b.jstrR < b.jstr ? b.jstrR : b.jstr, b.jendR};
   hipLaunchKernelGGL(k_set_huv, grid_of(R), dim3(kBX, kBY), 0, s, d, R, t.nrhs);
-  launch_exchange(d, s, d.f.FlxU, b.N);
-  launch_exchange(d, s, d.f.FlxV, b.N);
+  launch_exchange_list(d, s, ExchList{{d.f.FlxU, d.f.FlxV}, {b.N, b.N}, 2});
 }
 
 // ---------------------------------------------------------------------------
 // set_HUV1_tile (set_depth.F:239-422): remove the barotropic mismatch of
 // u,v(nnew) against NOW/MID/BAK-extrapolated DU_avg's, recompute FlxU,FlxV.
 // ---------------------------------------------------------------------------
-__global__ void k_set_huv1(Dev d, Range R, int nnew, int first) {
+__global__ void __launch_bounds__(256) k_set_huv1(Dev d, Range R, int nnew, int first) {
   ROMS_IJ_OR_RETURN(R)
   const Bounds& b = d.b;
   const Fields& F = d.f;
@@ -152,10 +149,8 @@ void launch_set_huv1(const Dev& d, hipStream_t s, const Tlev& t) {
   const Bounds& b = d.b;
   Range R{b.istrR < b.istr ? b.istrR : b.istr, b.iendR, b.jstrR < b.jstr ? b.jstrR : b.jstr, b.jendR};
   hipLaunchKernelGGL(k_set_huv1, grid_of(R), dim3(kBX, kBY), 0, s, d, R, t.nnew, (int)(t.iic == t.forw_start));
-  launch_exchange(d, s, d.f.FlxU, b.N);
-  launch_exchange(d, s, d.f.FlxV, b.N);
-  launch_exchange(d, s, d.f.u + (long)(t.nnew - 1) * b.n3, b.N);
-  launch_exchange(d, s, d.f.v + (long)(t.nnew - 1) * b.n3, b.N);
+  launch_exchange_list(d, s, ExchList{{d.f.FlxU, d.f.FlxV, d.f.u + (long)(t.nnew - 1) * b.n3,
+                                        d.f.v + (long)(t.nnew - 1) * b.n3}, {b.N, b.N, b.N, b.N}, 4});
 }
 
 // ---------------------------------------------------------------------------
@@ -166,7 +161,7 @@ __device__ __forceinline__ double omega_cx(const Bounds& b, const Fields& F, lon
   return fmax0(F.FlxU[o + 1]) - fmin0(F.FlxU[o]) + fmax0(F.FlxV[o + b.nx2]) - fmin0(F.FlxV[o]);
 }
 
-__global__ void k_omega(Dev d, Range R, double dtau) {
+__global__ void __launch_bounds__(256) k_omega(Dev d, Range R, double dtau) {
   ROMS_IJ_OR_RETURN(R)
   const Bounds& b = d.b;
   const Fields& F = d.f;
@@ -266,8 +261,7 @@ void launch_omega(const Dev& d, hipStream_t s, const Tlev& t) {
     const int n = 2 * (b.jend - b.jstr + 1) + 2 * (b.iend - b.istr + 1) + 4;
     hipLaunchKernelGGL(k_omega_edges, dim3((n + 255) / 256), dim3(256), 0, s, d);
   }
-  launch_exchange(d, s, d.f.We, b.N + 1);
-  launch_exchange(d, s, d.f.Wi, b.N + 1);
+  launch_exchange_list(d, s, ExchList{{d.f.We, d.f.Wi}, {b.N + 1, b.N + 1}, 2});
 }
 
 // ---------------------------------------------------------------------------
@@ -275,7 +269,7 @@ void launch_omega(const Dev& d, hipStream_t s, const Tlev& t) {
 // Linear EOS -> rho; NONLIN_EOS -> JM95 split form rho1,qp1 (DUKO_2001).
 // bvf for LMD; VAR_RHO_2D column integrals rhoA, rhoS.
 // ---------------------------------------------------------------------------
-__global__ void k_rho_eos_linear(Dev d, Range R, int tidx) {
+__global__ void __launch_bounds__(256) k_rho_eos_linear(Dev d, Range R, int tidx) {
   ROMS_IJ_OR_RETURN(R)
   const Bounds& b = d.b;
   const Fields& F = d.f;
@@ -318,7 +312,7 @@ __global__ void k_rho_eos_linear(Dev d, Range R, int tidx) {
   F.rhoS[ij] = 2.0 * cff * cff * cff1 * rhoS;
 }
 
-__global__ void k_rho_eos_split(Dev d, Range R, int tidx) {
+__global__ void __launch_bounds__(256) k_rho_eos_split(Dev d, Range R, int tidx) {
   ROMS_IJ_OR_RETURN(R)
   const Bounds& b = d.b;
   const Fields& F = d.f;

@@ -102,6 +102,25 @@ inline dim3 grid_of(const Range& r) {
   if (nj < 1) nj = 1;
   return dim3((ni + kBX - 1) / kBX, (nj + kBY - 1) / kBY, 1);
 }
+// 3-D launch: same (i,j) tiling with one grid z-slice per level k=1..nk
+inline dim3 grid3_of(const Range& r, int nk) {
+  dim3 g = grid_of(r);
+  g.z = nk;
+  return g;
+}
+// Column launch: one wavefront of 64 consecutive i per block, one row j per
+// block row; column scratch lives in LDS (see ColLds in k_common.h).
+constexpr int kCX = 64;
+inline dim3 gridc_of(const Range& r) {
+  int ni = r.i1 - r.i0 + 1, nj = r.j1 - r.j0 + 1;
+  if (ni < 1) ni = 1;
+  if (nj < 1) nj = 1;
+  return dim3((ni + kCX - 1) / kCX, nj, 1);
+}
+#define ROMS_IJC_OR_RETURN(R)                                   \
+  const int i = (R).i0 + (int)(blockIdx.x * kCX + threadIdx.x); \
+  const int j = (R).j0 + (int)blockIdx.y;                       \
+  if (i > (R).i1 || j > (R).j1) return;
 #define ROMS_IJ_OR_RETURN(R)                                   \
   const int i = (R).i0 + (int)(blockIdx.x * kBX + threadIdx.x); \
   const int j = (R).j0 + (int)(blockIdx.y * kBY + threadIdx.y); \
@@ -114,6 +133,18 @@ struct Tlev {
 };
 
 void launch_exchange(const Dev& d, hipStream_t s, double* a, int nlev);
+// several arrays in one launch (one reference exchange_xxx(A,B,C,D) call)
+struct ExchList {
+  double* p[8];
+  int nlev[8];
+  int n;
+};
+void launch_exchange_list(const Dev& d, hipStream_t s, const ExchList& L);
+void launch_exchange_tracers(const Dev& d, hipStream_t s, int tlev);  // t(:,:,:,tlev,1:NT)
+// Column kernels keep 2 (N+1)-level scratch columns per lane in LDS; opt in to
+// the full 160 KB when N needs more than the default 64 KB.  Returns false if
+// N is too deep for one wavefront's columns to fit.
+bool setup_column_kernels(int N);
 void launch_set_depth(const Dev& d, hipStream_t s, const Tlev& t);
 void launch_set_huv(const Dev& d, hipStream_t s, const Tlev& t);
 void launch_set_huv1(const Dev& d, hipStream_t s, const Tlev& t);

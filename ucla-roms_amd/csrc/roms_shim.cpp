@@ -230,6 +230,10 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
   P.vonKar = 0.41; P.qp2 = 0.0000172; P.gamma2 = cfg->gamma2; P.hc = cfg->hc;
   P.rdrg = cfg->rdrg; P.Zob = cfg->Zob; P.Tcoef = cfg->Tcoef; P.T0 = cfg->T0; P.Scoef = cfg->Scoef; P.S0 = cfg->S0;
   for (int i = 0; i < kMaxFast; i++) { g.w1[i] = cfg->weight[0][i]; g.w2[i] = cfg->weight[1][i]; }
+  if (!setup_column_kernels(dims->N)) {
+    g.err = "roms_gpu_init: N too large for the LDS column kernels (2*(N+1)*512 B > 160 KB)";
+    return -2;
+  }
   CHECK_HIP(hipStreamCreateWithFlags(&g.s, hipStreamNonBlocking));
   const Bounds& b = g.d.b;
   for (int id = 0; id < ROMS_NFIELDS; id++) {
