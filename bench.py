@@ -1,17 +1,22 @@
 """Benchmark of the MI355X split-explicit ROMS step (BASELINE.json metric).
 
 Workload (BASELINE.json configs[1]): Filament physics +
-salinity (linear EOS, T and S), 512x512x50, dt=5 s, ndtfast=60 -> nfast=82,
-domain 51.2 km x 12.8 km (dx=100 m, dy=25 m), doubly periodic, synthetic
-analytic initial state.  One "step" = one full roms_step (main.F:333-520):
-2 rho_eos, 3 omega, 2 prsgrd, pre_step3d, set_HUV/HUV1, step3d_uv1, visc3d,
-82 barotropic step2d_FB, step3d_uv2, step3d_t, t3dmix.  State is resident
-in HBM before the timed region; steady steps replay captured HIP graphs.
+salinity (linear EOS, T and S), 512x512x50 per GPU, dt=5 s, ndtfast=60 ->
+nfast=82, dx=100 m, dy=25 m, doubly periodic, synthetic analytic initial
+state.  One "step" = one full roms_step (main.F:333-520): 3 rho_eos, 3 omega,
+2 prsgrd, pre_step3d, set_HUV/HUV1, step3d_uv1, visc3d, 82 barotropic
+step2d_FB, step3d_uv2, step3d_t, t3dmix.  State is resident in HBM before
+the timed region; steady steps replay captured HIP graphs.
 
-value = grid-cell updates per second summed over ranks (weak scaling: each
-rank advances its own 512x512x50 subdomain); model seconds per wall second
-reported beside it, with the HBM roofline of the step and of its dominant
-kernel (algorithmic bytes, SURVEY.md 8(d) pass counts, / measured time).
+N GPUs (one process each, torchrun): weak scaling on an npx x npe processor
+grid (1x1, 2x1, 2x2, 4x2, ...) of 512x512 subdomains of one periodic domain;
+halo exchanges go over RCCL (xGMI) inside the step graphs.
+
+value = grid-cell updates per second summed over ranks; model seconds per
+wall second beside it.  roofline: per-routine algorithmic bytes (SURVEY.md
+8(d) pass counts) / mean launch duration measured with HIP events on the
+library stream; the dominant routine (largest time per step) is reported,
+the full table under "routines".
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
 """
@@ -27,17 +32,35 @@ sys.path.insert(0, os.path.join(ROOT, "ucla-roms_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
-# C2 workload
+# C2 workload, per GPU
 LLM, MMM, NZ, NT = 512, 512, 50, 2
 DT, NDTFAST = 5.0, 60
 SIZEX, SIZEY = 51.2e3, 12.8e3
+NT_TS = 2
 
 
-def step_bytes(I, J, N, NT_, NT_TS, nfast):
-    """B_step = 8*(P3D*I*J*N + 35*nfast*I*J), linear EOS, no LMD:
-    P3D = 105 + 5*NT_TS + 10*NT."""
-    P3D = 105 + 5 * NT_TS + 10 * NT_
+def routine_passes(NT_, NT_TS_):
+    """SURVEY.md 8(d): unique 3-D array passes per call (linear EOS, no LMD);
+    step2d counts 35 2-D passes per fast step (flagged with None)."""
+    return {"rho_eos": 2 + NT_TS_, "set_HUV": 7, "omega": 6, "prsgrd": 5, "pre_step3d": 16 + NT_TS_ + 4 * NT_,
+            "set_HUV1": 7, "step3d_uv1": 14, "visc3d": 7, "step2d": None, "step3d_uv2": 11,
+            "step3d_t": 5 + NT_TS_ + 3 * NT_, "t3dmix": 1 + 3 * NT_}
+
+
+def step_bytes(I, J, N, NT_, NT_TS_, nfast):
+    """B_step = 8*(P3D*I*J*N + 35*nfast*I*J), P3D = 105+5*NT_TS+10*NT."""
+    P3D = 105 + 5 * NT_TS_ + 10 * NT_
     return 8.0 * (P3D * I * J * N + 35.0 * nfast * I * J)
+
+
+def proc_grid(n):
+    npx = 1
+    while npx * npx < n:
+        npx *= 2
+    npx = min(npx, n)
+    while n % npx:
+        npx -= 1
+    return npx, n // npx
 
 
 def cpu_baseline(nsteps=3):
@@ -57,27 +80,64 @@ def cpu_baseline(nsteps=3):
             "model_seconds_per_wallclock_sec": nsteps * DT / dt_wall}
 
 
+def pmc_traffic(routine):
+    """HBM bytes per launch of `routine` from the committed rocprofv3 PMC
+    summary (profiles/pmc_traffic.json, FETCH_SIZE*2 + WRITE_SIZE per
+    MI355X_MICROARCH.md), or None when absent."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        d = json.load(open(p))
+        r = d.get("routines", {}).get(routine)
+        return None if r is None else float(r["bytes_per_launch"])
+    except (ValueError, KeyError, TypeError):
+        return None
+
+
 def main():
+    # the JSON line is the only thing on stdout: libraries (RCCL prints a
+    # version banner at init) write to fd 1, so point it at stderr for the run
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=4)
+    ap.add_argument("--timing-steps", type=int, default=3, help="eager steps per routine for the event timings")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import romsgpu
+
     dist = None
-    if world > 1:
+    comm = None
+    npx, npe = proc_grid(world)
+    # ROMS_BENCH_FORCE_COMM=1: take the multi-rank path even at world size 1
+    # (RCCL comm + self-addressed exchanges; rehearses the N>1 plumbing)
+    force = os.environ.get("ROMS_BENCH_FORCE_COMM") == "1"
+    if world > 1 or force:
+        if force:
+            os.environ.setdefault("ROMS_GPU_RCCL_SELF", "1")
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", init_method="env://")
+        # bootstrap the library's own RCCL communicator through torch.distributed
+        uid = torch.zeros(128, dtype=torch.uint8, device="cuda")
+        if rank == 0:
+            uid.copy_(torch.frombuffer(bytearray(romsgpu.comm_unique_id()), dtype=torch.uint8))
+        dist.broadcast(uid, src=0)
+        comm = romsgpu.comm_create(bytes(uid.cpu().numpy().tobytes()), world, rank, local_rank)
 
-    import romsgpu
-    m = romsgpu.Model.from_case(romsgpu.CASE_FILAMENT, LLM, MMM, NZ, NT, salinity=True, dt=DT, ndtfast=NDTFAST,
-                                sizex=SIZEX, sizey=SIZEY, device=local_rank)
+    m = romsgpu.Model.from_case(romsgpu.CASE_FILAMENT, LLM * npx, MMM * npe, NZ, NT, salinity=True, dt=DT,
+                                ndtfast=NDTFAST, sizex=SIZEX * npx, sizey=SIZEY * npe, device=local_rank,
+                                np_xi=npx, np_eta=npe, comm=comm, rank=rank)
+    assert (m.Lm, m.Mm) == (LLM, MMM)
     nfast = m.t.nfast
     m.step(args.warmup)
     m.sync()
@@ -102,22 +162,33 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
+    # per-routine rooflines: HIP events around each routine's launches
+    cells3 = LLM * MMM * NZ
+    passes = routine_passes(NT, NT_TS)
+    routines = {}
+    for r in romsgpu.ROUTINES:
+        avg, n = m.time_routine(r, args.timing_steps)
+        per_step = n / args.timing_steps
+        nbytes = 35.0 * 8 * LLM * MMM if passes[r] is None else 8.0 * passes[r] * cells3
+        gbs = nbytes / (avg * 1e-3) / 1e9 if avg > 0 else 0.0
+        routines[r] = {"ms_per_call": avg, "calls_per_step": per_step, "ms_per_step": avg * per_step,
+                       "bytes_per_call": nbytes, "achieved_GBs": gbs, "frac": gbs / HBM_PEAK_GBS}
+    dom = max(routines, key=lambda k: routines[k]["ms_per_step"])
+    D = routines[dom]
+
     # sanity: the run must stay finite (blow-up check as diag.F does)
     norms = m.diag()
     if not all(map(lambda x: x == x and abs(x) < 1e30, norms)):
         raise SystemExit("bench: non-finite diag norms %r" % norms)
 
     ms_step = 1e3 * elapsed / args.steps
-    cells = LLM * MMM * NZ
-    B = step_bytes(LLM, MMM, NZ, NT, 2, nfast)
+    B = step_bytes(LLM, MMM, NZ, NT, NT_TS, nfast)
     step_gbs = B / (ms_step * 1e-3) / 1e9
-
-    # dominant kernel: time it in isolation with HIP events on the library stream
-    dom = m.kernel_roofline() if hasattr(m, "kernel_roofline") else None
+    traffic = pmc_traffic(dom)
 
     out = {
         "metric": "grid-cell-updates/sec",
-        "value": world * cells * args.steps / elapsed,
+        "value": world * cells3 * args.steps / elapsed,
         "unit": "cell-updates/s",
         "n_gpus": world,
         "steps": args.steps,
@@ -129,20 +200,25 @@ def main():
         "dtype": "f64",
         "data": "synthetic (analytic Filament+S initial state, ana_grid/ana_init of tests/Filament)",
         "config": {"workload": "C2: Filament+S 512x512x50 per GPU, NT=2, dt=5s, ndtfast=60 (nfast=%d)" % nfast,
-                   "grid": [LLM, MMM, NZ], "NT": NT, "dt": DT, "nfast": nfast, "parallelism": "%d GPU" % world},
+                   "grid_per_gpu": [LLM, MMM, NZ], "proc_grid": [npx, npe], "NT": NT, "dt": DT, "nfast": nfast,
+                   "parallelism": "domain decomposition %dx%d, RCCL halo exchange" % (npx, npe)},
         "model_seconds_per_wallclock_sec": args.steps * DT / elapsed,
+        "roofline": {"bound": "hbm", "achieved": D["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": D["frac"], "traffic": traffic,
+                     "kernel": dom + (" (one fast step: k_s2d_zeta + k_s2d_mom + halo)" if dom == "step2d" else ""),
+                     "bytes_per_launch": D["bytes_per_call"], "ms_per_launch": D["ms_per_call"]},
         "roofline_step": {"bound": "hbm", "achieved": step_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                           "frac": step_gbs / HBM_PEAK_GBS, "bytes_per_step": B},
+        "routines": routines,
     }
-    if dom is not None:
-        out["roofline"] = dom
-    else:
-        out["roofline"] = dict(out["roofline_step"], kernel="whole roms_step (graph)", traffic=None)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline()
     m.close()
+    if comm is not None:
+        romsgpu.comm_destroy(comm)
     if rank == 0:
-        print(json.dumps(out))
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     if dist is not None:
         dist.destroy_process_group()
 

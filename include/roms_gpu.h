@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define ROMS_GPU_ABI_VERSION 1
+#define ROMS_GPU_ABI_VERSION 2
 #define ROMS_MAX_FAST 288
 
 /* Subdomain geometry of this rank: param.F / dimensions.F / mpi_setup.F:39-210 */
@@ -85,8 +85,10 @@ enum roms_field {
 /* ---- lifecycle ---- */
 int  roms_gpu_abi_version(void);
 /* Allocates device state (the only allocating entry).  device: HIP device
- * ordinal; comm: opaque RCCL communicator for multi-rank halo exchange (NULL
- * for a single rank, whose periodic halos are wrapped on-device).           */
+ * ordinal; comm: handle from roms_gpu_comm_create / _create_local for a
+ * processor grid np_xi*np_eta > 1 (rank = inode + jnode*np_xi, as
+ * mpi_setup.F:60-61), NULL for a single rank, whose periodic halos are
+ * wrapped on-device.                                                        */
 int  roms_gpu_init(const roms_dims *dims, const roms_cfg *cfg, int device, void *comm);
 int  roms_gpu_finalize(void);
 const char *roms_gpu_last_error(void);
@@ -137,11 +139,42 @@ typedef struct roms_case {
 /* Builds the analytic grid/ICs on the host (setup_grid1/2, set_scoord,
  * set_weights, ana_init), initialises the device and runs roms_init.        */
 int roms_gpu_init_case(const roms_case *c, int device, roms_tlev *t);
+/* Same on this rank's subdomain of an np_xi x np_eta processor grid
+ * (mpi_setup.F:39-154 bounds); comm's rank selects inode,jnode.             */
+int roms_gpu_init_case_comm(const roms_case *c, int np_xi, int np_eta, void *comm, int device, roms_tlev *t);
+
+/* ---- communicators for the halo exchange (mpi_exchanges.F) ----
+ * RCCL: rank 0 calls roms_gpu_comm_unique_id, the 128-byte id is broadcast
+ * by the host's own means (MPI_Bcast in a Fortran driver, torch.distributed
+ * in the Python one), then every rank calls roms_gpu_comm_create.
+ * _create_local: subdomains driven by threads of ONE process (testing).     */
+int roms_gpu_comm_unique_id(void *id128);
+int roms_gpu_comm_create(const void *id128, int nranks, int rank, int device, void **comm);
+int roms_gpu_comm_create_local(int group, int nranks, int rank, void **comm);
+int roms_gpu_comm_destroy(void *comm);
+/* Host-only: neighbour ranks (-1 none), per-level message sizes for the 8
+ * directions W,E,S,N,SW,SE,NW,NE, and the strip extents {i0,i1,j0,j1}.      */
+int roms_gpu_halo_plan(int Lm, int Mm, int np_xi, int np_eta, int inode, int jnode, int ew_periodic,
+                       int ns_periodic, int peer[8], long count[8], int strip[4]);
+/* Host-only: the (i,j) cells, in message order, that direction dir packs
+ * (unpack=0, from this rank's interior) or unpacks into (unpack=1, halo).
+ * Returns the per-level count (<= cap) or -1.                               */
+long roms_gpu_halo_map(int Lm, int Mm, int np_xi, int np_eta, int inode, int jnode, int ew_periodic,
+                       int ns_periodic, int dir, int unpack, int *i, int *j, long cap);
 
 /* ---- diagnostics (diag.F code_check norms, device reduction) ---- */
 int roms_gpu_diag(const roms_tlev *t, double norms[4]);
 /* event-timed replay of n steps on the library stream: total milliseconds  */
 int roms_gpu_time_steps(roms_tlev *t, int n, double *ms);
+/* Runs nsteps steps eagerly with HIP events on the library stream around
+ * every launch of one routine; returns the mean duration of one launch
+ * (one call of the routine, incl. its boundary/exchange kernels).            */
+enum roms_routine {
+  ROMS_R_RHO_EOS = 0, ROMS_R_SET_HUV, ROMS_R_OMEGA, ROMS_R_PRSGRD, ROMS_R_PRE_STEP3D, ROMS_R_SET_HUV1,
+  ROMS_R_STEP3D_UV1, ROMS_R_VISC3D, ROMS_R_STEP2D, ROMS_R_STEP3D_UV2, ROMS_R_STEP3D_T, ROMS_R_T3DMIX,
+  ROMS_R_COUNT
+};
+int roms_gpu_time_routine(int routine, int nsteps, roms_tlev *t, double *avg_ms, long *launches);
 
 #ifdef __cplusplus
 }

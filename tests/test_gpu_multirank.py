@@ -1,0 +1,157 @@
+"""Domain decomposition on the GPU (mpi_setup.F + mpi_exchanges.F semantics).
+
+Subdomains of one processor grid are driven by threads of this process
+(roms_gpu_comm_create_local: the library's pack/unpack kernels with device
+copies as transport), so one GPU checks the decomposition end to end:
+  * every subdomain's fields equal the single-domain run's window bitwise,
+    for the periodic Filament and the closed basin, on 2x1, 1x2, 2x2, 3x2;
+  * Filament on the reference's own 3x2 grid reproduces the golden diag log
+    digit for digit (per-rank pairwise sums + the tree over ranks);
+  * the RCCL transport (self-addressed send/recv on one GPU, captured in the
+    step graph) gives the same fields as the single-rank wrap.
+"""
+import json
+import os
+import subprocess
+import sys
+import threading
+
+import numpy as np
+import pytest
+
+import romsgpu
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FIELDS = ("zeta", "ubar", "vbar", "u", "v", "t", "FlxU", "FlxV", "We", "Wi", "Hz", "z_r", "z_w", "rho", "rufrc",
+          "rvfrc", "DU_avg1", "DV_avg1", "DU_avg2", "DV_avg2", "Zt_avg1")
+_group = [100]
+
+
+def _case(kind):
+    if kind == "filament":
+        return dict(case_id=0, LLm=40, MMm=30, N=12, NT=1, salinity=False, nonlin_eos=False, dt=5.0, ndtfast=60,
+                    sizex=8.0e3, sizey=1.5e3)
+    return dict(case_id=1, LLm=36, MMm=28, N=10, NT=2, salinity=True, nonlin_eos=True, dt=60.0, ndtfast=30,
+                sizex=72e3, sizey=56e3)
+
+
+def run_decomposed(case, npx, npe, nsteps, fields=FIELDS, diag=False):
+    """Run every subdomain in its own thread; returns per-rank field dicts
+    (and per-step diag norms of rank 0 when diag=True)."""
+    n = npx * npe
+    _group[0] += 1
+    grp = _group[0]
+    out, errs, norms = [None] * n, [], []
+
+    def work(rank):
+        try:
+            h = romsgpu.comm_create_local(grp, n, rank)
+            m = romsgpu.Model.from_case(np_xi=npx, np_eta=npe, comm=h, rank=rank, **case)
+            if diag:   # diag is collective: every rank calls it
+                d = m.diag()
+                if rank == 0:
+                    norms.append(d)
+            for _ in range(nsteps):
+                m.step()
+                d = m.diag() if diag else None
+                if diag and rank == 0:
+                    norms.append(d)
+            m.sync()
+            out[rank] = (m.iSW, m.jSW, m.Lm, m.Mm, {f: m.get(f) for f in fields})
+            m.close()
+            romsgpu.comm_destroy(h)
+        except Exception as e:  # surfaced in the main thread
+            errs.append((rank, repr(e)))
+
+    th = [threading.Thread(target=work, args=(r,)) for r in range(n)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=240)
+    assert not errs, errs
+    return out, norms
+
+
+def window(a, iSW, jSW, Lm, Mm):
+    return a[..., jSW:jSW + Mm + 4, iSW:iSW + Lm + 4]
+
+
+EXCHANGED = ("zeta", "ubar", "vbar", "u", "v", "t", "FlxU", "FlxV", "We", "Wi", "Hz", "z_r", "z_w")
+
+
+@pytest.mark.parametrize("kind", ["filament", "basin"])
+@pytest.mark.parametrize("npx,npe", [(2, 1), (1, 2), (2, 2), (3, 2)])
+def test_decomposition_bitwise_equals_single_domain(kind, npx, npe):
+    case = _case(kind)
+    per = case["case_id"] == 0
+    m = romsgpu.Model.from_case(**case)
+    m.step(5)
+    ref = {f: m.get(f) for f in FIELDS}
+    m.close()
+    parts, _ = run_decomposed(case, npx, npe, 5)
+    bad = []
+    for rank, (iSW, jSW, Lm, Mm, got) in enumerate(parts):
+        jn, inn = divmod(rank, npx)
+        # owned cells: interior + the closed-edge ghost row/column the BC code sets
+        i_lo = 0 if (not per and inn == 0) else 1
+        i_hi = Lm + 1 if (not per and inn == npx - 1) else Lm
+        j_lo = 0 if (not per and jn == 0) else 1
+        j_hi = Mm + 1 if (not per and jn == npe - 1) else Mm
+        own = (Ellipsis, slice(j_lo + 1, j_hi + 2), slice(i_lo + 1, i_hi + 2))
+        for f in FIELDS:
+            w = window(ref[f], iSW, jSW, Lm, Mm)
+            g = got[f]
+            if not np.array_equal(g[own], w[own]):
+                bad.append((rank, f, "owned", float(np.max(np.abs(g[own] - w[own])))))
+            elif f in EXCHANGED and not np.array_equal(g, w):
+                bad.append((rank, f, "halo", float(np.max(np.abs(g - w)))))
+    assert not bad, (kind, npx, npe, bad[:6])
+
+
+def test_filament_3x2_matches_golden_digits():
+    """The reference's Filament benchmark runs on a 3x2 MPI grid; with the
+    same per-rank pairwise sums and tree over ranks the GPU run prints the
+    golden log's ES23.16 digits."""
+    gold = json.load(open(os.path.join(ROOT, "tests", "golden", "filament_github_gnu.json")))["rows"]
+    case = dict(case_id=0, LLm=64, MMm=64, N=32, NT=1, salinity=False, nonlin_eos=False, dt=5.0, ndtfast=60,
+                sizex=12.8e3, sizey=3.2e3)
+    _, norms = run_decomposed(case, 3, 2, 20, fields=("zeta",), diag=True)
+    assert len(norms) == 21
+    bad = []
+    for s, (r, g) in enumerate(zip(gold, norms)):
+        want = [r["ke"], r["ke2b"], r["cu_adv"], r["cu_w"]]
+        have = [("%23.16E" % v).strip() for v in g]
+        if want != have:
+            bad.append((s, want, have))
+    assert not bad, bad[:3]
+
+
+RCCL_SCRIPT = r"""
+import os, sys
+sys.path.insert(0, os.path.join(sys.argv[1], "ucla-roms_amd"))
+import numpy as np, romsgpu
+case = dict(case_id=0, LLm=32, MMm=24, N=8, NT=1, dt=5.0, ndtfast=60, sizex=6.4e3, sizey=1.2e3)
+m = romsgpu.Model.from_case(**case)
+m.step(4)
+ref = {f: m.get(f) for f in ("zeta", "u", "v", "t", "FlxU", "We")}
+m.close()
+uid = romsgpu.comm_unique_id()
+h = romsgpu.comm_create(uid, 1, 0, 0)
+m = romsgpu.Model.from_case(np_xi=1, np_eta=1, comm=h, rank=0, **case)
+m.step(4)
+for f, v in ref.items():
+    g = m.get(f)
+    assert np.array_equal(g[..., 1:-1, 1:-1], v[..., 1:-1, 1:-1]), f
+m.close()
+romsgpu.comm_destroy(h)
+print("RCCL_OK")
+"""
+
+
+def test_rccl_transport_self_routed_equals_wrap():
+    env = dict(os.environ, ROMS_GPU_RCCL_SELF="1")
+    r = subprocess.run([sys.executable, "-c", RCCL_SCRIPT, ROOT], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0 and "RCCL_OK" in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])

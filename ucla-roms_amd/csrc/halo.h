@@ -1,0 +1,50 @@
+// halo.h -- multi-rank halo exchange and cross-rank gathers (halo.hip).
+#pragma once
+#include <string>
+
+#include "roms_dev.h"
+
+namespace roms {
+
+enum HaloDir : int { kW = 0, kE, kS, kN, kSW, kSE, kNW, kNE };
+
+// message geometry of one rank; passed to the pack/unpack kernels by value
+struct HaloGeom {
+  int Lm, Mm, nx2;
+  long n2;
+  int j0, j1;      // rows of the W/E strips
+  int i0, i1;      // columns of the S/N strips
+  int active[8];   // neighbour present in direction d
+  long cnt[8];     // elements per level of the message to/from direction d
+};
+struct HaloPlan {
+  HaloGeom g;
+  int peer[8];     // rank of the neighbour in direction d (-1: none)
+};
+
+struct RomsComm;  // opaque communicator handle of the C ABI
+struct Halo {
+  RomsComm* comm = nullptr;
+  HaloPlan plan{};
+  double* sbuf = nullptr;  // 8 x cap send messages
+  double* rbuf = nullptr;  // 8 x cap receive messages
+  double* dred = nullptr;  // gather staging
+  long cap = 0;
+};
+
+int comm_unique_id(void* out128);
+RomsComm* comm_create_rccl(const void* id128, int nranks, int rank, std::string& err);
+RomsComm* comm_create_local(int group, int nranks, int rank);
+void comm_destroy(RomsComm* c);
+int comm_rank(const RomsComm* c);
+int comm_size(const RomsComm* c);
+
+HaloPlan halo_plan(int Lm, int Mm, int npx, int npe, int inode, int jnode, int ewp, int nsp);
+int halo_setup(Halo& H, RomsComm* comm, const HaloPlan& plan, int maxlev, std::string& err);
+void halo_free(Halo& H);
+bool halo_graph_safe(const Halo* H);
+long halo_map(const HaloPlan& P, int dir, int unpack, int* iv, int* jv);
+void halo_exchange(const Halo& H, hipStream_t s, const ExchList& L);
+int halo_allgather(const Halo& H, hipStream_t s, const double* in, int n, double* out);
+
+}  // namespace roms

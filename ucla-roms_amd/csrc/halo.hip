@@ -1,0 +1,304 @@
+// halo.hip -- multi-rank halo exchange (mpi_exchanges.F:1-760 restated for
+// one GPU per subdomain).
+//
+// An exchange of a list of arrays (one reference exchange_xxx(A,B,..) call)
+// is pack -> transport -> unpack:
+//   k_halo_pack   gathers, for each of the 8 neighbours (W,E,S,N,SW,SE,NW,NE),
+//                 the 2-wide strip / 2x2 corner of every level of every array
+//                 into one contiguous message (mpi_exchanges.F:533-598);
+//   transport     RCCL group send/recv on the library stream (capturable in a
+//                 HIP graph), or, for several subdomains driven by threads of
+//                 one process, device copies between their buffers;
+//   k_halo_unpack scatters the received messages into the halo
+//                 (mpi_exchanges.F:601-668).
+// Every halo cell that has a neighbour receives that neighbour's current
+// value (corners always travel), which is the superset of what the
+// reference fills and equals the single-domain run's interior there.  Strips
+// along a closed physical edge also carry the boundary ghost row/column, as
+// the reference's jl0=0 / jl1=nyl+1 extension at the first/last jnode does.
+#include <rccl/rccl.h>
+
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <vector>
+
+#include "halo.h"
+
+namespace roms {
+
+namespace {
+constexpr int kOpp[8] = {kE, kW, kN, kS, kNE, kNW, kSE, kSW};
+
+__host__ __device__ __forceinline__ void halo_src(const HaloGeom& g, int dir, long e, int& i, int& j) {
+  const int nxs = g.i1 - g.i0 + 1;
+  switch (dir) {
+    case kW: i = 1 + (int)(e % 2); j = g.j0 + (int)(e / 2); break;
+    case kE: i = g.Lm - 1 + (int)(e % 2); j = g.j0 + (int)(e / 2); break;
+    case kS: i = g.i0 + (int)(e % nxs); j = 1 + (int)(e / nxs); break;
+    case kN: i = g.i0 + (int)(e % nxs); j = g.Mm - 1 + (int)(e / nxs); break;
+    case kSW: i = 1 + (int)(e % 2); j = 1 + (int)(e / 2); break;
+    case kSE: i = g.Lm - 1 + (int)(e % 2); j = 1 + (int)(e / 2); break;
+    case kNW: i = 1 + (int)(e % 2); j = g.Mm - 1 + (int)(e / 2); break;
+    default: i = g.Lm - 1 + (int)(e % 2); j = g.Mm - 1 + (int)(e / 2); break;
+  }
+}
+__host__ __device__ __forceinline__ void halo_dst(const HaloGeom& g, int h, long e, int& i, int& j) {
+  const int nxs = g.i1 - g.i0 + 1;
+  switch (h) {
+    case kW: i = -1 + (int)(e % 2); j = g.j0 + (int)(e / 2); break;
+    case kE: i = g.Lm + 1 + (int)(e % 2); j = g.j0 + (int)(e / 2); break;
+    case kS: i = g.i0 + (int)(e % nxs); j = -1 + (int)(e / nxs); break;
+    case kN: i = g.i0 + (int)(e % nxs); j = g.Mm + 1 + (int)(e / nxs); break;
+    case kSW: i = -1 + (int)(e % 2); j = -1 + (int)(e / 2); break;
+    case kSE: i = g.Lm + 1 + (int)(e % 2); j = -1 + (int)(e / 2); break;
+    case kNW: i = -1 + (int)(e % 2); j = g.Mm + 1 + (int)(e / 2); break;
+    default: i = g.Lm + 1 + (int)(e % 2); j = g.Mm + 1 + (int)(e / 2); break;
+  }
+}
+// (array, level) of list-level index lev
+__device__ __forceinline__ int list_slot(const ExchList& L, int& lev) {
+  int q = 0;
+  while (q < L.n - 1 && lev >= L.nlev[q]) { lev -= L.nlev[q]; q++; }
+  return q;
+}
+
+// grid: x = element of the strip, y = list level, z = direction
+__global__ void __launch_bounds__(256) k_halo_pack(HaloGeom g, ExchList L, double* __restrict__ sbuf, long cap) {
+  const int dir = blockIdx.z;
+  if (!g.active[dir]) return;
+  const long cnt = g.cnt[dir];
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= cnt) return;
+  int lev = blockIdx.y;
+  const int q = list_slot(L, lev);
+  if (lev >= L.nlev[q]) return;
+  int i, j;
+  halo_src(g, dir, e, i, j);
+  sbuf[dir * cap + (long)blockIdx.y * cnt + e] = L.p[q][(long)(i + 1) + (long)(j + 1) * g.nx2 + (long)lev * g.n2];
+}
+__global__ void __launch_bounds__(256) k_halo_unpack(HaloGeom g, ExchList L, const double* __restrict__ rbuf, long cap) {
+  const int h = blockIdx.z;
+  if (!g.active[h]) return;
+  const long cnt = g.cnt[h];
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= cnt) return;
+  int lev = blockIdx.y;
+  const int q = list_slot(L, lev);
+  if (lev >= L.nlev[q]) return;
+  int i, j;
+  halo_dst(g, h, e, i, j);
+  L.p[q][(long)(i + 1) + (long)(j + 1) * g.nx2 + (long)lev * g.n2] = rbuf[h * cap + (long)blockIdx.y * cnt + e];
+}
+
+// ---- in-process transport: subdomains driven by threads of one process ----
+struct LocalGroup {
+  int n = 0;
+  std::mutex m;
+  std::condition_variable cv;
+  int waiting = 0;
+  long gen = 0;
+  std::vector<double*> sbuf;
+  std::vector<std::vector<double>> red;
+  long cap = 0;
+  void barrier() {
+    std::unique_lock<std::mutex> lk(m);
+    const long my = gen;
+    if (++waiting == n) {
+      waiting = 0;
+      gen++;
+      cv.notify_all();
+    } else if (!cv.wait_for(lk, std::chrono::seconds(120), [&] { return gen != my; })) {
+      // a rank never reached this collective: fail loudly rather than hang
+      fprintf(stderr, "roms_gpu: in-process halo barrier timed out (mismatched collective calls)\n");
+      std::abort();
+    }
+  }
+};
+std::mutex g_groups_m;
+std::map<int, LocalGroup*> g_groups;
+}  // namespace
+
+struct RomsComm {
+  int kind;  // 1 = RCCL, 2 = threads of one process
+  int rank, nranks;
+  ncclComm_t nccl;
+  LocalGroup* grp;
+  int route_self;  // test hook: send self-messages through RCCL as well
+};
+
+int comm_unique_id(void* out) {
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return -1;
+  std::memcpy(out, &id, sizeof(id));
+  return 0;
+}
+RomsComm* comm_create_rccl(const void* id, int nranks, int rank, std::string& err) {
+  ncclUniqueId u;
+  std::memcpy(&u, id, sizeof(u));
+  ncclComm_t c;
+  const ncclResult_t r = ncclCommInitRank(&c, nranks, u, rank);
+  if (r != ncclSuccess) {
+    err = std::string("ncclCommInitRank: ") + ncclGetErrorString(r);
+    return nullptr;
+  }
+  RomsComm* rc = new RomsComm{1, rank, nranks, c, nullptr, 0};
+  const char* env = getenv("ROMS_GPU_RCCL_SELF");
+  rc->route_self = env && env[0] == '1';
+  return rc;
+}
+RomsComm* comm_create_local(int group, int nranks, int rank) {
+  std::lock_guard<std::mutex> lk(g_groups_m);
+  LocalGroup*& gp = g_groups[group];
+  if (!gp) {
+    gp = new LocalGroup;
+    gp->n = nranks;
+    gp->sbuf.assign(nranks, nullptr);
+    gp->red.assign(nranks, {});
+  }
+  return new RomsComm{2, rank, nranks, nullptr, gp, 0};
+}
+void comm_destroy(RomsComm* c) {
+  if (!c) return;
+  if (c->kind == 1) (void)ncclCommDestroy(c->nccl);
+  delete c;
+}
+int comm_rank(const RomsComm* c) { return c ? c->rank : 0; }
+int comm_size(const RomsComm* c) { return c ? c->nranks : 1; }
+
+// neighbour table and message geometry from the processor grid (mpi_setup.F:59-139)
+HaloPlan halo_plan(int Lm, int Mm, int npx, int npe, int inode, int jnode, int ewp, int nsp) {
+  HaloPlan P{};
+  HaloGeom& g = P.g;
+  g.Lm = Lm; g.Mm = Mm; g.nx2 = Lm + 4; g.n2 = (long)(Lm + 4) * (Mm + 4);
+  const bool w = ewp || inode > 0, e = ewp || inode < npx - 1;
+  const bool s = nsp || jnode > 0, n = nsp || jnode < npe - 1;
+  g.j0 = s ? 1 : 0; g.j1 = n ? Mm : Mm + 1;
+  g.i0 = w ? 1 : 0; g.i1 = e ? Lm : Lm + 1;
+  const bool act[8] = {w, e, s, n, s && w, s && e, n && w, n && e};
+  const int di[8] = {-1, 1, 0, 0, -1, 1, -1, 1}, dj[8] = {0, 0, -1, 1, -1, -1, 1, 1};
+  for (int d = 0; d < 8; d++) {
+    g.active[d] = act[d];
+    const int in = (inode + di[d] + npx) % npx, jn = (jnode + dj[d] + npe) % npe;
+    P.peer[d] = act[d] ? in + jn * npx : -1;
+    if (d < 2) g.cnt[d] = 2L * (g.j1 - g.j0 + 1);
+    else if (d < 4) g.cnt[d] = 2L * (g.i1 - g.i0 + 1);
+    else g.cnt[d] = 4;
+    if (!act[d]) g.cnt[d] = 0;
+  }
+  return P;
+}
+
+int halo_setup(Halo& H, RomsComm* comm, const HaloPlan& plan, int maxlev, std::string& err) {
+  H.comm = comm;
+  H.plan = plan;
+  long mx = 0;
+  for (int d = 0; d < 8; d++) mx = plan.g.cnt[d] > mx ? plan.g.cnt[d] : mx;
+  H.cap = mx * (long)maxlev;
+  if (hipMalloc(&H.sbuf, (size_t)8 * H.cap * sizeof(double)) != hipSuccess ||
+      hipMalloc(&H.rbuf, (size_t)8 * H.cap * sizeof(double)) != hipSuccess ||
+      hipMalloc(&H.dred, (size_t)64 * (1 + (comm ? comm->nranks : 1)) * sizeof(double)) != hipSuccess) {
+    err = "halo_setup: hipMalloc failed";
+    return -2;
+  }
+  if (comm && comm->kind == 2) {
+    std::lock_guard<std::mutex> lk(comm->grp->m);
+    comm->grp->sbuf[comm->rank] = H.sbuf;
+    comm->grp->cap = H.cap;
+  }
+  return 0;
+}
+void halo_free(Halo& H) {
+  if (H.sbuf) (void)hipFree(H.sbuf);
+  if (H.rbuf) (void)hipFree(H.rbuf);
+  if (H.dred) (void)hipFree(H.dred);
+  H.sbuf = H.rbuf = H.dred = nullptr;
+}
+
+// host copy of the pack (unpack=0) or unpack (unpack=1) index map of one direction
+long halo_map(const HaloPlan& P, int dir, int unpack, int* iv, int* jv) {
+  const long n = P.g.cnt[dir];
+  for (long e = 0; e < n; e++) {
+    if (unpack) halo_dst(P.g, dir, e, iv[e], jv[e]);
+    else halo_src(P.g, dir, e, iv[e], jv[e]);
+  }
+  return n;
+}
+
+bool halo_graph_safe(const Halo* H) { return !H || !H->comm || H->comm->kind == 1; }
+
+void halo_exchange(const Halo& H, hipStream_t s, const ExchList& L) {
+  const HaloGeom& g = H.plan.g;
+  int nl = 0;
+  for (int q = 0; q < L.n; q++) nl += L.nlev[q];
+  if (nl == 0) return;
+  long mx = 0;
+  for (int d = 0; d < 8; d++) mx = g.cnt[d] > mx ? g.cnt[d] : mx;
+  const dim3 grid((unsigned)((mx + 255) / 256), (unsigned)nl, 8);
+  hipLaunchKernelGGL(k_halo_pack, grid, dim3(256), 0, s, g, L, H.sbuf, H.cap);
+  RomsComm* c = H.comm;
+  const int me = c->rank;
+  if (c->kind == 1) {
+    (void)ncclGroupStart();
+    for (int d = 0; d < 8; d++)
+      if (g.active[d] && (H.plan.peer[d] != me || c->route_self))
+        (void)ncclSend(H.sbuf + d * H.cap, (size_t)(nl * g.cnt[d]), ncclDouble, H.plan.peer[d], c->nccl, s);
+    // the k-th message to a peer lands in the k-th receive posted for it:
+    // receive halo opp(d) in the order the peer sent direction d
+    for (int d = 0; d < 8; d++) {
+      const int h = kOpp[d];
+      if (g.active[h] && (H.plan.peer[h] != me || c->route_self))
+        (void)ncclRecv(H.rbuf + h * H.cap, (size_t)(nl * g.cnt[h]), ncclDouble, H.plan.peer[h], c->nccl, s);
+    }
+    (void)ncclGroupEnd();
+    for (int h = 0; h < 8; h++)
+      if (g.active[h] && H.plan.peer[h] == me && !c->route_self)
+        (void)hipMemcpyAsync(H.rbuf + h * H.cap, H.sbuf + kOpp[h] * H.cap, (size_t)(nl * g.cnt[h]) * sizeof(double),
+                             hipMemcpyDeviceToDevice, s);
+  } else {
+    LocalGroup* G = c->grp;
+    (void)hipStreamSynchronize(s);
+    G->barrier();
+    for (int h = 0; h < 8; h++)
+      if (g.active[h])
+        (void)hipMemcpyAsync(H.rbuf + h * H.cap, G->sbuf[H.plan.peer[h]] + kOpp[h] * G->cap,
+                             (size_t)(nl * g.cnt[h]) * sizeof(double), hipMemcpyDeviceToDevice, s);
+    (void)hipStreamSynchronize(s);
+    G->barrier();
+  }
+  hipLaunchKernelGGL(k_halo_unpack, grid, dim3(256), 0, s, g, L, H.rbuf, H.cap);
+}
+
+// out[r*n + q] = in_r[q] for every rank r (blocking)
+int halo_allgather(const Halo& H, hipStream_t s, const double* in, int n, double* out) {
+  RomsComm* c = H.comm;
+  if (!c) {
+    std::memcpy(out, in, (size_t)n * sizeof(double));
+    return 0;
+  }
+  if (n > 64) return -1;
+  if (c->kind == 1) {
+    double* dsend = H.dred;        // 64 doubles
+    double* dall = H.dred + 64;    // 64 * nranks doubles
+    if (hipMemcpyAsync(dsend, in, (size_t)n * sizeof(double), hipMemcpyHostToDevice, s) != hipSuccess) return -2;
+    if (ncclAllGather(dsend, dall, (size_t)n, ncclDouble, c->nccl, s) != ncclSuccess) return -3;
+    if (hipMemcpyAsync(out, dall, (size_t)n * c->nranks * sizeof(double), hipMemcpyDeviceToHost, s) != hipSuccess)
+      return -2;
+    return hipStreamSynchronize(s) == hipSuccess ? 0 : -2;
+  }
+  LocalGroup* G = c->grp;
+  {
+    std::lock_guard<std::mutex> lk(G->m);
+    G->red[c->rank].assign(in, in + n);
+  }
+  G->barrier();
+  for (int r = 0; r < c->nranks; r++) std::memcpy(out + (long)r * n, G->red[r].data(), (size_t)n * sizeof(double));
+  G->barrier();
+  return 0;
+}
+
+}  // namespace roms

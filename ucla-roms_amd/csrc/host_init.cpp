@@ -89,6 +89,7 @@ void set_scoord(int N, double theta_s, double theta_b, double* Cs_w, double* Cs_
 
 // periodic halo wrap on the host (same semantics as the device exchange)
 static void wrap(const HostState& H, double* a, int nlev, bool ewp, bool nsp) {
+  if (!H.wrap_on) return;
   const int Lm = H.Lm, Mm = H.Mm;
   auto at = [&](int i, int j, int k) -> double& { return a[(i + 1) + (long)(j + 1) * H.nx2 + (long)k * H.n2]; };
   for (int k = 0; k < nlev; k++) {
@@ -172,6 +173,7 @@ void build_case(const CaseSpec& cs, HostState& H, double& area, double& volume) 
   auto T = [&](int i, int j, int k, int l, int it) -> double& {
     return H.arr[kt][(i + 1) + (long)(j + 1) * H.nx2 + (long)(k - 1) * n2 + (long)(l - 1) * n3 + (long)(it - 1) * 3 * n3];
   };
+  H.wrap_on = cs.host_wrap != 0;
   // ---- ana_grid ----
   if (cs.case_id == 0) {
     const double SizeX = cs.sizex, SizeY = cs.sizey;

@@ -23,6 +23,7 @@ struct HostState {
   int Lm, Mm, N, NT, nTS, nx2;
   long n2;
   std::vector<double> arr[kNHost];
+  bool wrap_on = true;
   HostState(int Lm_, int Mm_, int N_, int NT_, int nTS_);
   std::vector<double>& a(int id);
 };
@@ -32,6 +33,7 @@ struct CaseSpec {
   int iSW_corn, jSW_corn;
   int ew_periodic, ns_periodic, west_exchng, east_exchng, south_exchng, north_exchng;
   int salinity;
+  int host_wrap;  // apply periodic halo wraps on the host (single rank)
   double theta_s, theta_b, hc, rho0, Tcoef, visc2, tnu2, Akv_bak, Akt_bak[2];
   double sizex, sizey;
 };

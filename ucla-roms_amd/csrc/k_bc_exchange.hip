@@ -7,6 +7,7 @@
 // separately; since every message is packed from the pre-exchange array the
 // final halo is the periodic wrap of the interior.  Closed-wall BCs restate
 // u3dbc_im.F:4, v3dbc_im.F:4, t3dbc_im.F:4 with no OBC_* switch defined.
+#include "halo.h"
 #include "roms_dev.h"
 
 namespace roms {
@@ -56,6 +57,10 @@ __global__ void __launch_bounds__(256) k_periodic_wrap(Bounds b, ExchList L) {
 
 void launch_exchange_list(const Dev& d, hipStream_t s, const ExchList& L) {
   const Bounds& b = d.b;
+  if (d.halo && d.halo->comm) {
+    halo_exchange(*d.halo, s, L);
+    return;
+  }
   if (!b.ew_periodic && !b.ns_periodic) return;
   const int n = 4 * b.nx2 + 4 * b.Mm;
   int nl = 0;

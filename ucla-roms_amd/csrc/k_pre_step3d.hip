@@ -59,7 +59,7 @@ __global__ void __launch_bounds__(64) k_pre_tracer_v(Dev d, Range R, PreCoef c, 
     const double* __restrict__ Tr = F.t + (long)(nrhs - 1) * b.n3 + tb + ij;
     double* __restrict__ Tn = F.t + (long)(nnew - 1) * b.n3 + tb + ij;
     double cfk = 1.0, fcm = 2.0 * Tr[0], hk = Hz[0], tk = Tr[0];
-#pragma unroll 4
+#pragma unroll 8
     for (int k = 1; k <= N - 1; k++) {
       const double hk1 = Hz[(long)k * n2], tk1 = Tr[(long)k * n2];
       const double cff = 1.0 / (2.0 * hk + hk1 * (2.0 - cfk));
@@ -70,7 +70,7 @@ __global__ void __launch_bounds__(64) k_pre_tracer_v(Dev d, Range R, PreCoef c, 
       cfk = cf1; fcm = fck; hk = hk1; tk = tk1;
     }
     double fc1 = (2.0 * tk - fcm) / (1.0 - cfk);
-#pragma unroll 4
+#pragma unroll 8
     for (int k = N - 1; k >= 0; k--) {
       const double fck = A[k] - B[k + 1] * fc1;
       A[k + 1] = fc1 * We[(long)(k + 1) * n2];
@@ -94,7 +94,7 @@ __global__ void __launch_bounds__(64) k_pre_tracer_v(Dev d, Range R, PreCoef c, 
     double DCk = cff * tval(1);
     B[1] = CFk;
     A[0] = DCk;
-#pragma unroll 2
+#pragma unroll 8
     for (int k = 2; k <= N - 1; k++) {
       const double hfk1 = hfwd(k + 1);
       const double FCn = 2.0 * c.dtau * Akt[(long)k * n2] / (hfk1 + hfk);
@@ -109,7 +109,7 @@ __global__ void __launch_bounds__(64) k_pre_tracer_v(Dev d, Range R, PreCoef c, 
     const long oN = (long)(N - 1) * n2;
     double tt = (tval(N) + DCk * (FCk + fmax0(WCk))) / (hfk + FCk - fmin0(WCk) - CFk * (FCk + fmax0(WCk)));
     Tn[oN] = tt;
-#pragma unroll 4
+#pragma unroll 8
     for (int k = N - 1; k >= 1; k--) {
       tt = A[k - 1] + B[k] * tt;
       Tn[(long)(k - 1) * n2] = tt;
@@ -192,7 +192,7 @@ __device__ __forceinline__ void pre_uv_col(const Dev& d, int i, int j, int dir, 
   double DCk1 = cff * (DCinit(N, hbN, hbNm) + c.dtau * sstr);  // DC(N)
   A[N] = DCk1;
   B[N - 1] = CFk;
-#pragma unroll 2
+#pragma unroll 8
   for (int k = N - 1; k >= 2; k--) {
     const double hbL = Hb[lev(k - 1)], hfL = Hf[lev(k - 1)], hbLm = Hb[lev(k - 1) + ms], hfLm = Hf[lev(k - 1) + ms];
     const double FCl =
@@ -210,7 +210,7 @@ __device__ __forceinline__ void pre_uv_col(const Dev& d, int i, int j, int dir, 
   double un = (DCinit(1, hbK, hbKm) + DCk1 * (FCk - fmin0(WCk))) /
               (0.5 * (hfK + hfKm) + 0.5 * c.dtau * (rd + rdm) + FCk + fmax0(WCk) - CFk * (FCk - fmin0(WCk)));
   Unew[0] = un;
-#pragma unroll 4
+#pragma unroll 8
   for (int k = 2; k <= N; k++) {
     un = A[k] + B[k - 1] * un;
     Unew[(long)(k - 1) * n2] = un;

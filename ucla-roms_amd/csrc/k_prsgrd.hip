@@ -25,55 +25,62 @@ __global__ void __launch_bounds__(256) k_prsgrd_P(Dev d, Range R, int split) {
   const double g = d.p.g, rho0 = d.p.rho0, qp2 = d.p.qp2;
   const double OneFifth = 0.2, OneTwelfth = 1.0 / 12.0;
   const double grho = g / rho0, HalfGRho = 0.5 * grho;
-  const long ij = IJ(b, i, j);
+  const long ij = IJ(b, i, j), n2 = b.n2;
+  const double* __restrict__ zr = F.z_r + ij;
+  const double* __restrict__ rho = F.rho + ij;
+  const double* __restrict__ rho1 = F.rho1 + ij;
+  const double* __restrict__ qp1 = F.qp1 + ij;
+  double* __restrict__ rhos = F.rhos + ij;
+  double* __restrict__ Pp = F.P + ij;
   // in-situ density at rho-level k (SPLIT_EOS: rho1 + qp1*dpth*(1-qp2*dpth))
   auto rhoval = [&](long o) {
     if (split) {
-      const double dpth = -F.z_r[o];
-      return F.rho1[o] + F.qp1[o] * dpth * (1.0 - qp2 * dpth);
+      const double dpth = -zr[o];
+      return rho1[o] + qp1[o] * dpth * (1.0 - qp2 * dpth);
     }
-    return F.rho[o];
+    return rho[o];
   };
   // elementary difference at w-level k in 1..N-1
-  auto eZ = [&](int k) { const long o = ij + (long)(k - 1) * b.n2; return F.z_r[o + b.n2] - F.z_r[o]; };
+  auto eZ = [&](int k) { const long o = (long)(k - 1) * n2; return zr[o + n2] - zr[o]; };
   auto eR = [&](int k) {
-    const long o = ij + (long)(k - 1) * b.n2;
+    const long o = (long)(k - 1) * n2;
     if (split) {
-      const double dpth = -0.5 * (F.z_r[o + b.n2] + F.z_r[o]);
-      return F.rho1[o + b.n2] - F.rho1[o] + (F.qp1[o + b.n2] - F.qp1[o]) * dpth * (1.0 - qp2 * dpth);
+      const double dpth = -0.5 * (zr[o + n2] + zr[o]);
+      return rho1[o + n2] - rho1[o] + (qp1[o + n2] - qp1[o]) * dpth * (1.0 - qp2 * dpth);
     }
-    return F.rho[o + b.n2] - F.rho[o];
+    return rho[o + n2] - rho[o];
   };
   const bool doP = i >= b.istrU - 1 && i <= b.iend;
   // rolling: e(k), e(k-1) elementary; dZ/dR harmonic at k+1 (previous)
   double eZk = eZ(N - 1), eRk = eR(N - 1);   // e(N) = e(N-1)
   double dZ1 = 0.0, dR1 = 0.0, P1 = 0.0;       // values at k+1
+#pragma unroll 8
   for (int k = N; k >= 1; k--) {
     const int km = k - 1;
     const double eZm = km >= 1 ? eZ(km) : eZ(1);   // e(0) = e(1)
     const double eRm = km >= 1 ? eR(km) : eR(1);
     const double dZk = [&] { const double c = 2.0 * eZk * eZm; return c / (eZk + eZm); }();
     double dRk = harm(eRk, eRm);
-    const long o = ij + (long)(k - 1) * b.n2;
+    const long o = (long)(k - 1) * n2;
     if (split) {
-      const double dpth = -F.z_r[o];
-      dRk = dRk - F.qp1[o] * dZk * (1.0 - 2.0 * qp2 * dpth);
-      F.rhos[o] = rhoval(o);
+      const double dpth = -zr[o];
+      dRk = dRk - qp1[o] * dZk * (1.0 - 2.0 * qp2 * dpth);
+      rhos[o] = rhoval(o);
     }
     if (doP) {
       double Pk;
       if (k == N) {
-        const double zw = F.z_w[ij + (long)N * b.n2], zr = F.z_r[o], zrm = F.z_r[o - b.n2];
-        const double rN = rhoval(o), rNm = rhoval(o - b.n2);
-        Pk = g * zw + grho * (rN + 0.5 * (rN - rNm) * (zw - zr) / (zr - zrm)) * (zw - zr);
+        const double zw = F.z_w[ij + (long)N * n2], zr0 = zr[o], zrm = zr[o - n2];
+        const double rN = rhoval(o), rNm = rhoval(o - n2);
+        Pk = g * zw + grho * (rN + 0.5 * (rN - rNm) * (zw - zr0) / (zr0 - zrm)) * (zw - zr0);
       } else {
-        const double zr1 = F.z_r[o + b.n2], zr = F.z_r[o];
-        const double r1 = rhoval(o + b.n2), r0 = rhoval(o);
-        Pk = P1 + HalfGRho * ((r1 + r0) * (zr1 - zr) -
-                              OneFifth * ((dR1 - dRk) * (zr1 - zr - OneTwelfth * (dZ1 + dZk)) -
+        const double zr1 = zr[o + n2], zr0 = zr[o];
+        const double r1 = rhoval(o + n2), r0 = rhoval(o);
+        Pk = P1 + HalfGRho * ((r1 + r0) * (zr1 - zr0) -
+                              OneFifth * ((dR1 - dRk) * (zr1 - zr0 - OneTwelfth * (dZ1 + dZk)) -
                                           (dZ1 - dZk) * (r1 - r0 - OneTwelfth * (dR1 + dRk))));
       }
-      F.P[o] = Pk;
+      Pp[o] = Pk;
       P1 = Pk;
     }
     dZ1 = dZk; dR1 = dRk;

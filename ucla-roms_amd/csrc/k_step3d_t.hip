@@ -44,7 +44,7 @@ __global__ void __launch_bounds__(64) k_step3d_t_v(Dev d, Range R, int nnew, int
     // spline interface values FC(0:N) (compute_vert_tracer_fluxes.h)
     double cfk = 1.0, fcm = 2.0 * Tr[0], hk = Hz[0], tk = Tr[0];
     A[0] = fcm;
-#pragma unroll 4
+#pragma unroll 8
     for (int k = 1; k <= N - 1; k++) {
       const double hk1 = Hz[(long)k * n2], tk1 = Tr[(long)k * n2];
       const double cff = 1.0 / (2.0 * hk + hk1 * (2.0 - cfk));
@@ -55,7 +55,7 @@ __global__ void __launch_bounds__(64) k_step3d_t_v(Dev d, Range R, int nnew, int
       cfk = cf1; fcm = fck; hk = hk1; tk = tk1;
     }
     double fc1 = (2.0 * tk - fcm) / (1.0 - cfk);
-#pragma unroll 4
+#pragma unroll 8
     for (int k = N - 1; k >= 0; k--) {
       const double fck = A[k] - B[k + 1] * fc1;
       A[k + 1] = fc1 * F.We[ij + (long)(k + 1) * n2];
@@ -94,7 +94,7 @@ __global__ void __launch_bounds__(64) k_step3d_t_v(Dev d, Range R, int nnew, int
     double DCk = cff * tval(1);
     B[1] = CFk;
     A[0] = DCk;
-#pragma unroll 4
+#pragma unroll 8
     for (int k = 2; k <= N - 1; k++) {
       const long o = (long)(k - 1) * n2;
       const double FCn = 2.0 * dt * Akt[(long)k * n2] / (Hz[o] + Hz[o + n2]);
@@ -109,7 +109,7 @@ __global__ void __launch_bounds__(64) k_step3d_t_v(Dev d, Range R, int nnew, int
     const long oN = (long)(N - 1) * n2;
     double tt = (tval(N) + DCk * (FCk + fmax0(WCk))) / (Hz[oN] + FCk - fmin0(WCk) - CFk * (FCk + fmax0(WCk))) * rm;
     Tn[oN] = tt;
-#pragma unroll 4
+#pragma unroll 8
     for (int k = N - 1; k >= 1; k--) {
       tt = (A[k - 1] + B[k] * tt) * rm;
       Tn[(long)(k - 1) * n2] = tt;

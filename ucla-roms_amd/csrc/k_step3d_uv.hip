@@ -41,7 +41,7 @@ __device__ __forceinline__ void uv1_col(const Dev& d, int i, int j, int dir, int
   double DCk1 = cff * (Un[(long)(N - 1) * n2] + DC0 * rk(N) + dt * sstr);
   A[N] = DCk1;
   B[N - 1] = CFk;
-#pragma unroll 2
+#pragma unroll 8
   for (int k = N - 1; k >= 2; k--) {
     const double FCl = 2.0 * dt * (Akv[(long)(k - 1) * n2] + Akv[(long)(k - 1) * n2 - s]) /
                        (hz(k) + hzm(k) + hz(k - 1) + hzm(k - 1));
@@ -60,7 +60,7 @@ __device__ __forceinline__ void uv1_col(const Dev& d, int i, int j, int dir, int
   Un[0] = dc * 0.5 * (hz(1) + hzm(1));
   const double dmdn = dir == 0 ? F.dm_u[ij] * F.dn_u[ij] : F.dm_v[ij] * F.dn_v[ij];
   double frc = r1 + dmdn * (sstr - 0.5 * (rDm + rD) * dc);
-#pragma unroll 4
+#pragma unroll 8
   for (int k = 2; k <= N; k++) {
     dc = A[k] + B[k - 1] * dc;
     Un[(long)(k - 1) * n2] = dc * 0.5 * (hz(k) + hzm(k));
@@ -186,24 +186,28 @@ __global__ void __launch_bounds__(256) k_uv2_couple(Dev d, Range R, int nnew) {
     if (dir == 0 && !(i >= b.istrU)) continue;
     if (dir == 1 && !(j >= b.jstrV)) continue;
     const long s = dir == 0 ? 1 : b.nx2;
-    double* Un = (dir == 0 ? F.u : F.v) + (long)(nnew - 1) * b.n3;
+    double* __restrict__ Un = (dir == 0 ? F.u : F.v) + (long)(nnew - 1) * b.n3 + ij;
+    const double* __restrict__ Hz = F.Hz + ij;
     const double dn = dir == 0 ? F.dn_u[ij] : F.dm_v[ij];
     const double avg1 = dir == 0 ? F.DU_avg1[ij] : F.DV_avg1[ij];
     const double msk = dir == 0 ? F.umask[ij] : F.vmask[ij];
-    long o = ij + (long)(N - 1) * n2;
-    double CF0 = 0.5 * (F.Hz[o] + F.Hz[o - s]);
+    long o = (long)(N - 1) * n2;
+    double CF0 = 0.5 * (Hz[o] + Hz[o - s]);
     double DC0 = Un[o];
     Un[o] = Un[o] / CF0;
+#pragma unroll 8
     for (int k = N - 1; k >= 1; k--) {
-      o = ij + (long)(k - 1) * n2;
-      const double cff = 0.5 * (F.Hz[o] + F.Hz[o - s]);
+      o = (long)(k - 1) * n2;
+      const double cff = 0.5 * (Hz[o] + Hz[o - s]);
+      const double un = Un[o];
       CF0 = CF0 + cff;
-      DC0 = DC0 + Un[o];
-      Un[o] = Un[o] / cff;
+      DC0 = DC0 + un;
+      Un[o] = un / cff;
     }
     DC0 = (DC0 * dn - avg1) / (CF0 * dn);
+#pragma unroll 8
     for (int k = 1; k <= N; k++) {
-      o = ij + (long)(k - 1) * n2;
+      o = (long)(k - 1) * n2;
       Un[o] = (Un[o] - DC0) * msk;
     }
   }
@@ -222,19 +226,22 @@ __global__ void __launch_bounds__(256) k_uv2_flux(Dev d, Range R, int nnew, int 
     if (dir == 0 && !(i >= iu0 && i <= iu1)) continue;
     if (dir == 1 && !(i >= iv0 && i <= iv1 && j >= b.jstr)) continue;
     const long s = dir == 0 ? 1 : b.nx2;
-    double* Un = (dir == 0 ? F.u : F.v) + (long)(nnew - 1) * b.n3;
-    const double* Us = (dir == 0 ? F.u : F.v) + (long)(nstp - 1) * b.n3;
-    double* Flx = dir == 0 ? F.FlxU : F.FlxV;
+    double* __restrict__ Un = (dir == 0 ? F.u : F.v) + (long)(nnew - 1) * b.n3 + ij;
+    const double* __restrict__ Us = (dir == 0 ? F.u : F.v) + (long)(nstp - 1) * b.n3 + ij;
+    double* __restrict__ Flx = (dir == 0 ? F.FlxU : F.FlxV) + ij;
+    const double* __restrict__ Hz = F.Hz + ij;
+    double* __restrict__ CFs = F.c0 + ij;
     const double dn = dir == 0 ? F.dn_u[ij] : F.dm_v[ij];
     const double avg1 = dir == 0 ? F.DU_avg1[ij] : F.DV_avg1[ij];
     const double avg2 = dir == 0 ? F.DU_avg2[ij] : F.DV_avg2[ij];
     const double msk = dir == 0 ? F.umask[ij] : F.vmask[ij];
-    auto DCk = [&](int k) { const long o = ij + (long)(k - 1) * n2; return 0.5 * (F.Hz[o] + F.Hz[o - s]) * dn; };
-    long o = ij + (long)(N - 1) * n2;
+    auto DCk = [&](int k) { const long o = (long)(k - 1) * n2; return 0.5 * (Hz[o] + Hz[o - s]) * dn; };
+    long o = (long)(N - 1) * n2;
     const double dcN = DCk(N);
     double DC0 = dcN, FC0 = dcN * Un[o];
+#pragma unroll 8
     for (int k = N - 1; k >= 1; k--) {
-      o = ij + (long)(k - 1) * n2;
+      o = (long)(k - 1) * n2;
       const double dck = DCk(k);
       DC0 = DC0 + dck;
       FC0 = FC0 + dck * Un[o];
@@ -244,19 +251,20 @@ __global__ void __launch_bounds__(256) k_uv2_flux(Dev d, Range R, int nnew, int 
     else F.vbar[IJL(b, i, j, knew)] = DC0 * avg1;
     FC0 = DC0 * (FC0 - avg1);
     double CF0 = 0.0;
-    double* CFs = F.c0;
+#pragma unroll 8
     for (int k = N; k >= 1; k--) {
-      o = ij + (long)(k - 1) * n2;
+      o = (long)(k - 1) * n2;
       const double un = (Un[o] - FC0) * msk;
       Un[o] = un;
       const double cfk = DELTA * Flx[o] + EPSIL * DCk(k) * (Us[o] + un);
-      CFs[ij + (long)k * n2] = cfk;
+      CFs[(long)k * n2] = cfk;
       CF0 = CF0 + cfk;
     }
     CF0 = DC0 * (CF0 - avg2);
+#pragma unroll 8
     for (int k = 1; k <= N; k++) {
-      o = ij + (long)(k - 1) * n2;
-      Flx[o] = CFs[ij + (long)k * n2] - DCk(k) * CF0;
+      o = (long)(k - 1) * n2;
+      Flx[o] = CFs[(long)k * n2] - DCk(k) * CF0;
     }
   }
 }

@@ -96,51 +96,40 @@ __global__ void __launch_bounds__(256) k_set_huv1(Dev d, Range R, int nnew, int 
   const Fields& F = d.f;
   const double NOW = 3.63, MID = 4.47, BAK = 2.05;
   const int N = b.N;
-  const long ij = IJ(b, i, j);
-  if (i >= b.istr && i <= b.iendR && j >= b.jstrR && j <= b.jendR) {
-    const double dn = F.dn_u[ij];
-    double* u = F.u + (long)(nnew - 1) * b.n3;
-    long o = ij + (long)(N - 1) * b.n2;
-    double dcN = 0.5 * (F.Hz[o] + F.Hz[o - 1]) * dn;
+  const long ij = IJ(b, i, j), n2 = b.n2;
+  for (int dir = 0; dir < 2; dir++) {
+    if (dir == 0 && !(i >= b.istr && i <= b.iendR && j >= b.jstrR && j <= b.jendR)) continue;
+    if (dir == 1 && !(i >= b.istrR && i <= b.iendR && j >= b.jstr && j <= b.jendR)) continue;
+    const long s = dir == 0 ? 1 : b.nx2;
+    const double dn = dir == 0 ? F.dn_u[ij] : F.dm_v[ij];
+    double* __restrict__ u = (dir == 0 ? F.u : F.v) + (long)(nnew - 1) * b.n3 + ij;
+    double* __restrict__ Flx = (dir == 0 ? F.FlxU : F.FlxV) + ij;
+    const double* __restrict__ Hz = F.Hz + ij;
+    long o = (long)(N - 1) * n2;
+    double dcN = 0.5 * (Hz[o] + Hz[o - s]) * dn;
     double DC0 = dcN, FC0 = dcN * u[o];
+#pragma unroll 8
     for (int k = N - 1; k >= 1; k--) {
-      o = ij + (long)(k - 1) * b.n2;
-      const double dck = 0.5 * (F.Hz[o] + F.Hz[o - 1]) * dn;
+      o = (long)(k - 1) * n2;
+      const double dck = 0.5 * (Hz[o] + Hz[o - s]) * dn;
       DC0 = DC0 + dck;
       FC0 = FC0 + dck * u[o];
     }
-    if (first) FC0 = (FC0 - F.DU_avg1[ij]) / DC0;
-    else FC0 = (FC0 - NOW * F.DU_avg1[ij] + MID * F.DU_avg2[ij] - BAK * F.DU_avg_bak[ij]) / DC0;
-    const double um = F.umask[ij];
+    const double a1 = dir == 0 ? F.DU_avg1[ij] : F.DV_avg1[ij];
+    if (first) FC0 = (FC0 - a1) / DC0;
+    else {
+      const double a2 = dir == 0 ? F.DU_avg2[ij] : F.DV_avg2[ij];
+      const double ab = dir == 0 ? F.DU_avg_bak[ij] : F.DV_avg_bak[ij];
+      FC0 = (FC0 - NOW * a1 + MID * a2 - BAK * ab) / DC0;
+    }
+    const double um = dir == 0 ? F.umask[ij] : F.vmask[ij];
+#pragma unroll 8
     for (int k = 1; k <= N; k++) {
-      o = ij + (long)(k - 1) * b.n2;
-      const double dck = 0.5 * (F.Hz[o] + F.Hz[o - 1]) * dn;
+      o = (long)(k - 1) * n2;
+      const double dck = 0.5 * (Hz[o] + Hz[o - s]) * dn;
       const double un = (u[o] - FC0) * um;
       u[o] = un;
-      F.FlxU[o] = dck * (un);
-    }
-  }
-  if (i >= b.istrR && i <= b.iendR && j >= b.jstr && j <= b.jendR) {
-    const double dm = F.dm_v[ij];
-    double* v = F.v + (long)(nnew - 1) * b.n3;
-    long o = ij + (long)(N - 1) * b.n2;
-    double dcN = 0.5 * (F.Hz[o] + F.Hz[o - b.nx2]) * dm;
-    double DC0 = dcN, FC0 = dcN * v[o];
-    for (int k = N - 1; k >= 1; k--) {
-      o = ij + (long)(k - 1) * b.n2;
-      const double dck = 0.5 * (F.Hz[o] + F.Hz[o - b.nx2]) * dm;
-      DC0 = DC0 + dck;
-      FC0 = FC0 + dck * v[o];
-    }
-    if (first) FC0 = (FC0 - F.DV_avg1[ij]) / DC0;
-    else FC0 = (FC0 - NOW * F.DV_avg1[ij] + MID * F.DV_avg2[ij] - BAK * F.DV_avg_bak[ij]) / DC0;
-    const double vm = F.vmask[ij];
-    for (int k = 1; k <= N; k++) {
-      o = ij + (long)(k - 1) * b.n2;
-      const double dck = 0.5 * (F.Hz[o] + F.Hz[o - b.nx2]) * dm;
-      const double vn = (v[o] - FC0) * vm;
-      v[o] = vn;
-      F.FlxV[o] = dck * (vn);
+      Flx[o] = dck * (un);
     }
   }
 }
@@ -157,10 +146,6 @@ void launch_set_huv1(const Dev& d, hipStream_t s, const Tlev& t) {
 // omega_tile (omega.F:17-236): bottom-up continuity, grid-motion removal,
 // Courant-limited explicit/implicit split of the vertical flux (We/Wi).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ double omega_cx(const Bounds& b, const Fields& F, long o) {
-  return fmax0(F.FlxU[o + 1]) - fmin0(F.FlxU[o]) + fmax0(F.FlxV[o + b.nx2]) - fmin0(F.FlxV[o]);
-}
-
 __global__ void __launch_bounds__(256) k_omega(Dev d, Range R, double dtau) {
   ROMS_IJ_OR_RETURN(R)
   const Bounds& b = d.b;
@@ -168,29 +153,38 @@ __global__ void __launch_bounds__(256) k_omega(Dev d, Range R, double dtau) {
   const int N = b.N;
   const double cu_min = 0.6, cu_max = 1.0, cmnx_ratio = cu_min / cu_max, cutoff = 2.0 - cmnx_ratio,
                r4cmx = 0.25 / (1.0 - cmnx_ratio);
-  const long ij = IJ(b, i, j);
+  const long ij = IJ(b, i, j), n2 = b.n2, sj = b.nx2;
+  const double* __restrict__ FU = F.FlxU + ij;
+  const double* __restrict__ FV = F.FlxV + ij;
+  const double* __restrict__ Hz = F.Hz + ij;
+  const double* __restrict__ zw = F.z_w + ij;
+  double* __restrict__ Wi = F.Wi + ij;
+  double* __restrict__ We = F.We + ij;
+  auto cx = [&](long o) { return fmax0(FU[o + 1]) - fmin0(FU[o]) + fmax0(FV[o + sj]) - fmin0(FV[o]); };
   double wi = 0.0;
-  F.Wi[ij] = 0.0;
+  Wi[0] = 0.0;
+#pragma unroll 8
   for (int k = 1; k <= N; k++) {
-    const long o = ij + (long)(k - 1) * b.n2;
-    wi = wi - F.FlxU[o + 1] + F.FlxU[o] - F.FlxV[o + b.nx2] + F.FlxV[o];
-    F.Wi[ij + (long)k * b.n2] = wi;
+    const long o = (long)(k - 1) * n2;
+    wi = wi - FU[o + 1] + FU[o] - FV[o + sj] + FV[o];
+    Wi[(long)k * n2] = wi;
   }
   wi = wi + F.swflx[ij] * F.dm_r[ij] * F.dn_r[ij];
-  const double wrk = wi / (F.z_w[ij + (long)N * b.n2] - F.z_w[ij]);
-  F.Wi[ij + (long)N * b.n2] = 0.0;
-  F.We[ij + (long)N * b.n2] = 0.0;
-  F.We[ij] = 0.0;
+  const double zw0 = zw[0];
+  const double wrk = wi / (zw[(long)N * n2] - zw0);
+  Wi[(long)N * n2] = 0.0;
+  We[(long)N * n2] = 0.0;
+  We[0] = 0.0;
   const double CX0 = dtau * F.pm[ij] * F.pn[ij];
-  const double zw0 = F.z_w[ij];
-  double cx_up = omega_cx(b, F, ij + (long)(N - 1) * b.n2);  // CX(k+1)
-  double hz_up = F.Hz[ij + (long)(N - 1) * b.n2];
+  double cx_up = cx((long)(N - 1) * n2);  // CX(k+1)
+  double hz_up = Hz[(long)(N - 1) * n2];
+#pragma unroll 8
   for (int k = N - 1; k >= 1; k--) {
-    const long o = ij + (long)(k - 1) * b.n2;
-    const long ow = ij + (long)k * b.n2;
-    double w = F.Wi[ow] - wrk * (F.z_w[ow] - zw0);
-    const double cx_k = omega_cx(b, F, o);
-    const double hz_k = F.Hz[o];
+    const long o = (long)(k - 1) * n2;
+    const long ow = (long)k * n2;
+    double w = Wi[ow] - wrk * (zw[ow] - zw0);
+    const double cx_k = cx(o);
+    const double hz_k = Hz[o];
     const double c2d = dmax(cx_k, cx_up);
     const double dh = dmin(hz_k, hz_up);
     const double cw_max = cu_max * dh - c2d * CX0;
@@ -208,8 +202,8 @@ __global__ void __launch_bounds__(256) k_omega(Dev d, Range R, double dtau) {
     } else {
       we = 0.0;
     }
-    F.We[ow] = we;
-    F.Wi[ow] = w;
+    We[ow] = we;
+    Wi[ow] = w;
     cx_up = cx_k;
     hz_up = hz_k;
   }
@@ -275,39 +269,49 @@ __global__ void __launch_bounds__(256) k_rho_eos_linear(Dev d, Range R, int tidx
   const Fields& F = d.f;
   const Params& P = d.p;
   const int N = b.N;
-  const long ij = IJ(b, i, j);
+  const long ij = IJ(b, i, j), n2 = b.n2;
   const double rm = F.rmask[ij];
   const double cff0 = P.salinity ? (P.Tcoef * P.T0 - P.Scoef * P.S0) : (P.Tcoef * P.T0);
-  const double* T = F.t + (long)(tidx - 1) * b.n3;
-  const double* Sa = F.t + (long)(tidx - 1) * b.n3 + 3 * b.n3;
-  for (int k = 1; k <= N; k++) {
-    const long o = ij + (long)(k - 1) * b.n2;
+  const double* __restrict__ T = F.t + (long)(tidx - 1) * b.n3 + ij;
+  const double* __restrict__ Sa = T + 3 * b.n3;
+  const double* __restrict__ Hz = F.Hz + ij;
+  double* __restrict__ rho = F.rho + ij;
+  const bool salt = P.salinity;
+  auto rhok = [&](long o) {
     double r = cff0 - P.Tcoef * T[o];
-    if (P.salinity) r = r + P.Scoef * Sa[o];
-    F.rho[o] = r * rm;
-  }
-  if (P.lmd) {
-    const double cff = P.g / P.rho0;
-    for (int k = 1; k <= N - 1; k++) {
-      const long o = ij + (long)(k - 1) * b.n2;
-      F.bvf[ij + (long)k * b.n2] = cff * (F.rho[o] - F.rho[o + b.n2]) / (F.z_r[o + b.n2] - F.z_r[o]);
-    }
-    F.bvf[ij + (long)N * b.n2] = F.bvf[ij + (long)(N - 1) * b.n2];
-    F.bvf[ij] = F.bvf[ij + b.n2];
-  }
-  long o = ij + (long)(N - 1) * b.n2;
-  double cff = F.Hz[o] * F.rho[o];
-  double rhoS = 0.5 * cff * F.Hz[o];
+    if (salt) r = r + P.Scoef * Sa[o];
+    return r * rm;
+  };
+  // rho(k) and the VAR_RHO_2D integrals from the top down in one pass
+  long o = (long)(N - 1) * n2;
+  double rk = rhok(o);
+  rho[o] = rk;
+  double cff = Hz[o] * rk;
+  double rhoS = 0.5 * cff * Hz[o];
   double rhoA = cff;
+#pragma unroll 8
   for (int k = N - 1; k >= 1; k--) {
-    o = ij + (long)(k - 1) * b.n2;
-    const double hz = F.Hz[o];
-    cff = hz * F.rho[o];
+    o = (long)(k - 1) * n2;
+    rk = rhok(o);
+    rho[o] = rk;
+    const double hz = Hz[o];
+    cff = hz * rk;
     rhoS = rhoS + hz * (rhoA + 0.5 * cff);
     rhoA = rhoA + cff;
   }
+  if (P.lmd) {
+    const double c = P.g / P.rho0;
+    const double* __restrict__ zr = F.z_r + ij;
+    double* __restrict__ bvf = F.bvf + ij;
+    for (int k = 1; k <= N - 1; k++) {
+      const long q = (long)(k - 1) * n2;
+      bvf[(long)k * n2] = c * (rho[q] - rho[q + n2]) / (zr[q + n2] - zr[q]);
+    }
+    bvf[(long)N * n2] = bvf[(long)(N - 1) * n2];
+    bvf[0] = bvf[n2];
+  }
   const double cff1 = 1.0 / P.rho0;
-  cff = 1.0 / (F.z_w[ij + (long)N * b.n2] - F.z_w[ij]);
+  cff = 1.0 / (F.z_w[ij + (long)N * n2] - F.z_w[ij]);
   F.rhoA[ij] = cff * cff1 * rhoA;
   F.rhoS[ij] = 2.0 * cff * cff * cff1 * rhoS;
 }

@@ -58,10 +58,12 @@ struct Fields {
   double *s0, *s1, *s2, *s3, *s4, *s5, *s6, *s7, *s8, *s9;  // 2-D scratch (step2d, diag)
 };
 
+struct Halo;  // halo.h: multi-rank exchange state (host object; nullptr = single rank)
 struct Dev {
   Bounds b;
   Params p;
   Fields f;
+  const Halo* halo;
 };
 
 // ---- index helpers (device + host) ----

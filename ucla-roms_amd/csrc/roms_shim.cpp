@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "../../include/roms_gpu.h"
+#include "halo.h"
 #include "host_init.h"
 #include "roms_dev.h"
 
@@ -41,8 +42,34 @@ struct Ctx {
   std::map<long, hipGraphExec_t> graphs;
   bool use_graphs = true;
   double* h_diag = nullptr;
+  Halo halo;               // multi-rank exchange (halo.comm == nullptr: single rank)
+  // per-routine timing (roms_gpu_time_routine): events around every launch
+  int timed = -1;
+  std::vector<hipEvent_t> ev;
+  size_t nev = 0;
 };
-Ctx g;
+// One context per host thread: a process normally drives one GPU/subdomain
+// from one thread; tests drive several subdomains from threads of one process.
+thread_local Ctx g;
+
+// reference tree reduction over ranks (diag.F:488-535): receiver r adds r+step
+double tree_sum(std::vector<double> v) {
+  int size = (int)v.size();
+  while (size > 1) {
+    const int step = (size + 1) / 2;
+    for (int r = 0; r < size - step; r++) v[r] = v[r] + v[r + step];
+    size = step;
+  }
+  return v.empty() ? 0.0 : v[0];
+}
+// local sub-domain extent along one direction (mpi_setup.F:110-154)
+void rank_extent(int LL, int np, int node, int& len, int& sw) {
+  const int base = (LL + np - 1) / np, off = np * base - LL;
+  sw = node == 0 ? 0 : node * base - off / 2;
+  len = base;
+  if (node == 0) len -= off / 2;
+  if (node == np - 1) len -= (off + 1) / 2;
+}
 
 #define CHECK_HIP(x)                                                                  \
   do {                                                                                \
@@ -146,6 +173,11 @@ double** field_slot(Fields& F, int id) {
 }
 
 void free_all() {
+  for (hipEvent_t e : g.ev) (void)hipEventDestroy(e);
+  g.ev.clear();
+  halo_free(g.halo);
+  g.halo = Halo{};
+  g.d.halo = nullptr;
   for (auto& kv : g.graphs) (void)hipGraphExecDestroy(kv.second);
   g.graphs.clear();
   for (int id = 0; id < ROMS_NFIELDS; id++)
@@ -164,39 +196,48 @@ Tlev to_tlev(const roms_tlev* t) {
   return r;
 }
 
+// bracket one routine's launches with HIP events when it is the timed one
+#define TIMED(id, stmt)                                                     \
+  do {                                                                      \
+    const bool on_ = g.timed == (id) && g.nev + 2 <= g.ev.size();           \
+    if (on_) (void)hipEventRecord(g.ev[g.nev], s);                          \
+    stmt;                                                                   \
+    if (on_) { (void)hipEventRecord(g.ev[g.nev + 1], s); g.nev += 2; }      \
+  } while (0)
+
 // the roms_step sequence for one step whose indices are already set in *t
 // (nstp,nrhs=nstp,nnew=3 on entry); enqueues everything on g.s
 void enqueue_step(roms_tlev* t) {
   const Dev& d = g.d;
   hipStream_t s = g.s;
   Tlev T = to_tlev(t);
-  launch_rho_eos(d, s, T, T.nrhs);
-  launch_set_huv(d, s, T);
-  launch_omega(d, s, T);
-  launch_prsgrd(d, s, T);
-  launch_pre_step3d(d, s, T);
-  launch_set_huv1(d, s, T);
+  TIMED(ROMS_R_RHO_EOS, launch_rho_eos(d, s, T, T.nrhs));
+  TIMED(ROMS_R_SET_HUV, launch_set_huv(d, s, T));
+  TIMED(ROMS_R_OMEGA, launch_omega(d, s, T));
+  TIMED(ROMS_R_PRSGRD, launch_prsgrd(d, s, T));
+  TIMED(ROMS_R_PRE_STEP3D, launch_pre_step3d(d, s, T));
+  TIMED(ROMS_R_SET_HUV1, launch_set_huv1(d, s, T));
   t->nrhs = 3;
   t->nnew = 3 - t->nstp;
   T = to_tlev(t);
-  launch_omega(d, s, T);
-  launch_rho_eos(d, s, T, T.nrhs);
-  launch_prsgrd(d, s, T);
-  launch_step3d_uv1(d, s, T);
-  if (g.cfg.uv_vis2) launch_visc3d(d, s, T);
+  TIMED(ROMS_R_OMEGA, launch_omega(d, s, T));
+  TIMED(ROMS_R_RHO_EOS, launch_rho_eos(d, s, T, T.nrhs));
+  TIMED(ROMS_R_PRSGRD, launch_prsgrd(d, s, T));
+  TIMED(ROMS_R_STEP3D_UV1, launch_step3d_uv1(d, s, T));
+  if (g.cfg.uv_vis2) TIMED(ROMS_R_VISC3D, launch_visc3d(d, s, T));
   for (int iif = 1; iif <= t->nfast; iif++) {
     t->iif = iif;
     t->kstp = t->knew;
     t->knew = t->kstp + 1;
     if (t->knew > 4) t->knew = 1;
     T = to_tlev(t);
-    launch_step2d(d, s, T, g.w1, g.w2);
+    TIMED(ROMS_R_STEP2D, launch_step2d(d, s, T, g.w1, g.w2));
   }
-  launch_step3d_uv2(d, s, T);
-  launch_omega(d, s, T);
-  launch_step3d_t(d, s, T);
-  if (g.cfg.ts_dif2) launch_t3dmix(d, s, T);
-  launch_rho_eos(d, s, T, T.nnew);
+  TIMED(ROMS_R_STEP3D_UV2, launch_step3d_uv2(d, s, T));
+  TIMED(ROMS_R_OMEGA, launch_omega(d, s, T));
+  TIMED(ROMS_R_STEP3D_T, launch_step3d_t(d, s, T));
+  if (g.cfg.ts_dif2) TIMED(ROMS_R_T3DMIX, launch_t3dmix(d, s, T));
+  TIMED(ROMS_R_RHO_EOS, launch_rho_eos(d, s, T, T.nnew));
 }
 
 }  // namespace
@@ -213,9 +254,15 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
   if (dims->N < 2 || dims->Lm < 2 || dims->Mm < 2 || dims->NT < 1) { g.err = "roms_gpu_init: bad dims"; return -1; }
   if (cfg->nfast < 1 || cfg->nfast > ROMS_MAX_FAST) { g.err = "roms_gpu_init: bad nfast"; return -1; }
   if (cfg->lmd_mixing) { g.err = "roms_gpu_init: LMD_MIXING not available in this build"; return -4; }
-  if (comm != nullptr || dims->np_xi * dims->np_eta > 1) {
-    g.err = "roms_gpu_init: multi-rank halo exchange not available in this build";
-    return -4;
+  const int nranks = dims->np_xi * dims->np_eta;
+  if (nranks < 1) { g.err = "roms_gpu_init: bad processor grid"; return -1; }
+  if (nranks > 1 && comm == nullptr) { g.err = "roms_gpu_init: np_xi*np_eta > 1 needs a communicator"; return -1; }
+  if (comm != nullptr) {
+    RomsComm* c = (RomsComm*)comm;
+    if (comm_size(c) != nranks || comm_rank(c) != dims->inode + dims->jnode * dims->np_xi) {
+      g.err = "roms_gpu_init: communicator size/rank does not match np_xi*np_eta / inode+jnode*np_xi";
+      return -1;
+    }
   }
   CHECK_HIP(hipSetDevice(device));
   g.dims = *dims;
@@ -259,8 +306,15 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
   for (double** q : s2)
     if (scratch(*q, b.n2)) return -2;
   CHECK_HIP(hipHostMalloc(&g.h_diag, (size_t)8 * b.n2 * sizeof(double), hipHostMallocDefault));
+  if (comm != nullptr) {
+    const HaloPlan plan = halo_plan(dims->Lm, dims->Mm, dims->np_xi, dims->np_eta, dims->inode, dims->jnode,
+                                    dims->ew_periodic, dims->ns_periodic);
+    const int r = halo_setup(g.halo, (RomsComm*)comm, plan, 8 * (dims->N + 1), g.err);
+    if (r) return r;
+    g.d.halo = &g.halo;
+  }
   const char* env = getenv("ROMS_GPU_NO_GRAPH");
-  g.use_graphs = !(env && env[0] == '1');
+  g.use_graphs = !(env && env[0] == '1') && halo_graph_safe(g.d.halo);
   g.inited = true;
   return 0;
 }
@@ -410,13 +464,21 @@ int roms_gpu_init_sequence(roms_tlev* t) {
   return post_launch();
 }
 
-int roms_gpu_init_case(const roms_case* c, int device, roms_tlev* t) {
+static int init_case_impl(const roms_case* c, int np_xi, int np_eta, void* comm, int device, roms_tlev* t) {
   if (!c || !t) { g.err = "roms_gpu_init_case: null argument"; return -1; }
+  if (np_xi < 1 || np_eta < 1) { g.err = "roms_gpu_init_case: bad processor grid"; return -1; }
+  const int rank = comm ? comm_rank((RomsComm*)comm) : 0;
   roms_dims D{};
-  D.Lm = c->LLm; D.Mm = c->MMm; D.N = c->N; D.NT = c->NT; D.LLm = c->LLm; D.MMm = c->MMm;
-  D.np_xi = D.np_eta = 1;
+  D.N = c->N; D.NT = c->NT; D.LLm = c->LLm; D.MMm = c->MMm;
+  D.np_xi = np_xi; D.np_eta = np_eta;
+  D.jnode = rank / np_xi;              // mpi_setup.F:60-61
+  D.inode = rank - D.jnode * np_xi;
+  rank_extent(c->LLm, np_xi, D.inode, D.Lm, D.iSW_corn);
+  rank_extent(c->MMm, np_eta, D.jnode, D.Mm, D.jSW_corn);
   const bool fil = c->case_id == ROMS_CASE_FILAMENT;
   D.ew_periodic = D.ns_periodic = fil ? 1 : 0;
+  if (!D.ew_periodic) { D.west_exchng = D.inode > 0; D.east_exchng = D.inode < np_xi - 1; }
+  if (!D.ns_periodic) { D.south_exchng = D.jnode > 0; D.north_exchng = D.jnode < np_eta - 1; }
   roms_cfg C{};
   C.nonlin_eos = c->nonlin_eos; C.salinity = c->salinity; C.lmd_mixing = c->lmd_mixing;
   C.uv_vis2 = 1; C.ts_dif2 = 1;
@@ -427,26 +489,136 @@ int roms_gpu_init_case(const roms_case* c, int device, roms_tlev* t) {
   C.Tcoef = 0.20; C.T0 = 1.0; C.Scoef = 0.822; C.S0 = 1.0;
   C.theta_s = 6.0; C.theta_b = 2.0; C.hc = fil ? 25.0 : 250.0;
   C.Akv_bak = fil ? 0.0 : 1.0e-4; C.Akt_bak[0] = fil ? 0.0 : 1.0e-5; C.Akt_bak[1] = C.Akt_bak[0];
-  int r = roms_gpu_init(&D, &C, device, nullptr);
+  int r = roms_gpu_init(&D, &C, device, comm);
   if (r) return r;
   CaseSpec cs{};
   cs.case_id = c->case_id; cs.LLm = c->LLm; cs.MMm = c->MMm;
+  cs.iSW_corn = D.iSW_corn; cs.jSW_corn = D.jSW_corn;
   cs.ew_periodic = D.ew_periodic; cs.ns_periodic = D.ns_periodic;
+  cs.west_exchng = D.west_exchng; cs.east_exchng = D.east_exchng;
+  cs.south_exchng = D.south_exchng; cs.north_exchng = D.north_exchng;
+  cs.host_wrap = comm == nullptr;   // with a communicator the device exchange fills halos
   cs.salinity = c->salinity; cs.theta_s = C.theta_s; cs.theta_b = C.theta_b; cs.hc = C.hc; cs.rho0 = C.rho0;
   cs.Tcoef = C.Tcoef; cs.visc2 = 0.0; cs.tnu2 = 0.0; cs.Akv_bak = C.Akv_bak;
   cs.Akt_bak[0] = C.Akt_bak[0]; cs.Akt_bak[1] = C.Akt_bak[1];
   cs.sizex = c->sizex; cs.sizey = c->sizey;
   HostState H(D.Lm, D.Mm, D.N, D.NT, C.salinity ? 2 : 1);
-  build_case(cs, H, g.area, g.volume);
+  double area = 0.0, volume = 0.0;
+  build_case(cs, H, area, volume);
+  // setup_grid2.F: per-rank pairwise sums, then the tree over ranks
+  {
+    const double loc[2] = {area, volume};
+    std::vector<double> all(2 * (size_t)(np_xi * np_eta));
+    if (halo_allgather(g.halo, g.s, loc, 2, all.data())) { g.err = "init_case: area/volume gather failed"; return -2; }
+    std::vector<double> va, vv;
+    for (int q = 0; q < np_xi * np_eta; q++) { va.push_back(all[2 * q]); vv.push_back(all[2 * q + 1]); }
+    g.area = tree_sum(va);
+    g.volume = tree_sum(vv);
+  }
   for (int id = 0; id < ROMS_NFIELDS; id++) {
     if (H.arr[id].empty()) continue;
     r = roms_gpu_copy_in(id, H.arr[id].data(), (long)H.arr[id].size());
     if (r) return r;
   }
+  if (comm != nullptr) {
+    // the exchanges of setup_grid1.F and ana_init (host wrap in the single-rank build)
+    const Fields& F = g.d.f;
+    const ExchList grid1{{F.dm_r, F.dn_r, F.dm_p, F.dn_p, F.dm_u, F.dn_u, F.dm_v, F.dn_v}, {1, 1, 1, 1, 1, 1, 1, 1}, 8};
+    const ExchList grid2{{F.pmon_u, F.pnom_v, F.rmask, F.umask, F.vmask, F.pmask}, {1, 1, 1, 1, 1, 1}, 6};
+    const ExchList st{{F.zeta, F.ubar, F.vbar, F.u, F.v}, {1, 1, 1, D.N, D.N}, 5};
+    launch_exchange_list(g.d, g.s, grid1);
+    launch_exchange_list(g.d, g.s, grid2);
+    launch_exchange_list(g.d, g.s, st);
+    launch_exchange_tracers(g.d, g.s, 1);
+    CHECK_HIP(hipStreamSynchronize(g.s));
+  }
   *t = roms_tlev{};
   t->iic = 0; t->ntstart = 1; t->forw_start = 1; t->iif = 1; t->nfast = C.nfast;
   t->kstp = 1; t->knew = 1; t->nstp = 1; t->nrhs = 1; t->nnew = 1;
   return roms_gpu_init_sequence(t);
+}
+
+int roms_gpu_init_case(const roms_case* c, int device, roms_tlev* t) { return init_case_impl(c, 1, 1, nullptr, device, t); }
+int roms_gpu_init_case_comm(const roms_case* c, int np_xi, int np_eta, void* comm, int device, roms_tlev* t) {
+  if (np_xi * np_eta > 1 && !comm) { g.err = "roms_gpu_init_case_comm: communicator required"; return -1; }
+  return init_case_impl(c, np_xi, np_eta, comm, device, t);
+}
+
+// ---- communicators ----
+int roms_gpu_comm_unique_id(void* id128) {
+  if (!id128) return -1;
+  if (comm_unique_id(id128)) { g.err = "ncclGetUniqueId failed"; return -5; }
+  return 0;
+}
+int roms_gpu_comm_create(const void* id128, int nranks, int rank, int device, void** comm) {
+  if (!id128 || !comm || nranks < 1 || rank < 0 || rank >= nranks) { g.err = "roms_gpu_comm_create: bad argument"; return -1; }
+  CHECK_HIP(hipSetDevice(device));
+  RomsComm* c = comm_create_rccl(id128, nranks, rank, g.err);
+  if (!c) return -5;
+  *comm = c;
+  return 0;
+}
+int roms_gpu_comm_create_local(int group, int nranks, int rank, void** comm) {
+  if (!comm || nranks < 1 || rank < 0 || rank >= nranks) { g.err = "roms_gpu_comm_create_local: bad argument"; return -1; }
+  *comm = comm_create_local(group, nranks, rank);
+  return 0;
+}
+int roms_gpu_comm_destroy(void* comm) {
+  comm_destroy((RomsComm*)comm);
+  return 0;
+}
+long roms_gpu_halo_map(int Lm, int Mm, int np_xi, int np_eta, int inode, int jnode, int ew_periodic, int ns_periodic,
+                       int dir, int unpack, int* iv, int* jv, long cap) {
+  if (Lm < 2 || Mm < 2 || np_xi < 1 || np_eta < 1 || inode < 0 || inode >= np_xi || jnode < 0 || jnode >= np_eta ||
+      dir < 0 || dir > 7)
+    return -1;
+  const HaloPlan P = halo_plan(Lm, Mm, np_xi, np_eta, inode, jnode, ew_periodic, ns_periodic);
+  if (P.g.cnt[dir] > cap) return -1;
+  return halo_map(P, dir, unpack, iv, jv);
+}
+int roms_gpu_halo_plan(int Lm, int Mm, int np_xi, int np_eta, int inode, int jnode, int ew_periodic, int ns_periodic,
+                       int peer[8], long count[8], int strip[4]) {
+  if (Lm < 2 || Mm < 2 || np_xi < 1 || np_eta < 1 || inode < 0 || inode >= np_xi || jnode < 0 || jnode >= np_eta) return -1;
+  const HaloPlan P = halo_plan(Lm, Mm, np_xi, np_eta, inode, jnode, ew_periodic, ns_periodic);
+  for (int d = 0; d < 8; d++) { peer[d] = P.peer[d]; count[d] = P.g.cnt[d]; }
+  strip[0] = P.g.i0; strip[1] = P.g.i1; strip[2] = P.g.j0; strip[3] = P.g.j1;
+  return 0;
+}
+
+int roms_gpu_time_routine(int routine, int nsteps, roms_tlev* t, double* avg_ms, long* launches) {
+  REQUIRE_INIT();
+  if (routine < 0 || routine >= ROMS_R_COUNT || nsteps < 1 || !avg_ms || !launches) {
+    g.err = "roms_gpu_time_routine: bad argument";
+    return -1;
+  }
+  const size_t need = (size_t)2 * (size_t)nsteps * (size_t)(g.cfg.nfast + 4);
+  while (g.ev.size() < need) {
+    hipEvent_t e;
+    CHECK_HIP(hipEventCreate(&e));
+    g.ev.push_back(e);
+  }
+  g.timed = routine;
+  g.nev = 0;
+  // eager steps (no graph), same launches and stream as the graph replays
+  for (int q = 0; q < nsteps; q++) {
+    t->iic = t->iic + 1;
+    t->nstp = 1 + (t->iic - t->ntstart) % 2;
+    t->nrhs = t->nstp;
+    t->nnew = 3;
+    t->nfast = g.cfg.nfast;
+    enqueue_step(t);
+  }
+  g.timed = -1;
+  CHECK_HIP(hipStreamSynchronize(g.s));
+  double tot = 0.0;
+  for (size_t q = 0; q + 1 < g.nev; q += 2) {
+    float f = 0.f;
+    CHECK_HIP(hipEventElapsedTime(&f, g.ev[q], g.ev[q + 1]));
+    tot += (double)f;
+  }
+  *launches = (long)(g.nev / 2);
+  *avg_ms = g.nev ? tot / (double)(g.nev / 2) : 0.0;
+  return post_launch();
 }
 
 int roms_gpu_time_steps(roms_tlev* t, int n, double* ms) {
@@ -498,6 +670,27 @@ int roms_gpu_diag(const roms_tlev* t, double norms[4]) {
       if (cx[o] > best || (cx[o] == best && best > 0.0 && kx[o] > bk)) { best = cx[o]; bw = cw[o]; bk = kx[o]; }
     }
     if (best > Cu) { Cu = best; Cw = bw; }
+  }
+  if (g.halo.comm) {
+    // per-rank partial sums / maxima combined in the reference's tree order (diag.F:488-535)
+    const double loc[5] = {avzeta, kes, ke2, Cu, Cw};
+    const int nr = comm_size(g.halo.comm);
+    std::vector<double> all(5 * (size_t)nr);
+    if (halo_allgather(g.halo, g.s, loc, 5, all.data())) { g.err = "roms_gpu_diag: gather failed"; return -2; }
+    std::vector<double> a(nr), k1(nr), k2(nr), cu(nr), cw(nr);
+    for (int q = 0; q < nr; q++) { a[q] = all[5 * q]; k1[q] = all[5 * q + 1]; k2[q] = all[5 * q + 2]; cu[q] = all[5 * q + 3]; cw[q] = all[5 * q + 4]; }
+    int size = nr;
+    while (size > 1) {
+      const int step = (size + 1) / 2;
+      for (int r = 0; r < size - step; r++)
+        if (cu[r + step] > cu[r]) { cu[r] = cu[r + step]; cw[r] = cw[r + step]; }
+      size = step;
+    }
+    norms[0] = tree_sum(k1) / (g.volume + tree_sum(a));
+    norms[1] = tree_sum(k2) / (g.volume + tree_sum(a));
+    norms[2] = cu[0];
+    norms[3] = cw[0];
+    return post_launch();
   }
   norms[0] = kes / (g.volume + avzeta);
   norms[1] = ke2 / (g.volume + avzeta);

@@ -89,12 +89,103 @@ def load_library(path=LIB_PATH):
     L.roms_gpu_diag.argtypes = [P(Tlev), P(ctypes.c_double)]
     L.roms_gpu_time_steps.argtypes = [P(Tlev), ctypes.c_int, P(ctypes.c_double)]
     L.roms_gpu_stream.restype = ctypes.c_void_p
+    L.roms_gpu_time_routine.argtypes = [ctypes.c_int, ctypes.c_int, P(Tlev), P(ctypes.c_double), P(ctypes.c_long)]
+    L.roms_gpu_init_case_comm.argtypes = [P(Case), ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, P(Tlev)]
+    L.roms_gpu_comm_unique_id.argtypes = [ctypes.c_void_p]
+    L.roms_gpu_comm_create.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       P(ctypes.c_void_p)]
+    L.roms_gpu_comm_create_local.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, P(ctypes.c_void_p)]
+    L.roms_gpu_comm_destroy.argtypes = [ctypes.c_void_p]
+    L.roms_gpu_halo_plan.argtypes = [ctypes.c_int] * 8 + [P(ctypes.c_int), P(ctypes.c_long), P(ctypes.c_int)]
+    L.roms_gpu_halo_map.argtypes = [ctypes.c_int] * 10 + [P(ctypes.c_int), P(ctypes.c_int), ctypes.c_long]
+    L.roms_gpu_halo_map.restype = ctypes.c_long
     _lib = L
     return L
 
 
 class RomsGpuError(RuntimeError):
     pass
+
+
+def _check(L, rc, what):
+    if rc != 0:
+        raise RomsGpuError("%s failed (%d): %s" % (what, rc, L.roms_gpu_last_error().decode()))
+
+
+def rank_extent(LL, np_, node):
+    """(length, SW-corner offset) of a subdomain along one direction (mpi_setup.F:110-154)."""
+    base = (LL + np_ - 1) // np_
+    off = np_ * base - LL
+    sw = 0 if node == 0 else node * base - off // 2
+    n = base
+    if node == 0:
+        n -= off // 2
+    if node == np_ - 1:
+        n -= (off + 1) // 2
+    return n, sw
+
+
+def halo_plan(Lm, Mm, np_xi, np_eta, inode, jnode, ew_periodic, ns_periodic):
+    """Neighbour ranks, per-level message sizes (W,E,S,N,SW,SE,NW,NE) and strip
+    extents (i0,i1,j0,j1) of the library's halo exchange (host-only call)."""
+    L = load_library()
+    peer = (ctypes.c_int * 8)()
+    cnt = (ctypes.c_long * 8)()
+    strip = (ctypes.c_int * 4)()
+    rc = L.roms_gpu_halo_plan(Lm, Mm, np_xi, np_eta, inode, jnode, int(ew_periodic), int(ns_periodic), peer, cnt, strip)
+    if rc != 0:
+        raise ValueError("bad halo plan arguments")
+    return list(peer), list(cnt), tuple(strip)
+
+
+def halo_map(Lm, Mm, np_xi, np_eta, inode, jnode, ew_periodic, ns_periodic, direction, unpack):
+    """(i, j) arrays of the cells direction `direction` packs (unpack=False) or
+    fills (unpack=True), in message order (host-only call)."""
+    L = load_library()
+    cap = 4 * (max(Lm, Mm) + 4)
+    iv = (ctypes.c_int * cap)()
+    jv = (ctypes.c_int * cap)()
+    n = L.roms_gpu_halo_map(Lm, Mm, np_xi, np_eta, inode, jnode, int(ew_periodic), int(ns_periodic), direction,
+                            int(unpack), iv, jv, cap)
+    if n < 0:
+        raise ValueError("bad halo map arguments")
+    return np.array(iv[:n]), np.array(jv[:n])
+
+
+HALO_DIRS = ("W", "E", "S", "N", "SW", "SE", "NW", "NE")
+# enum roms_routine of include/roms_gpu.h
+ROUTINES = ("rho_eos", "set_HUV", "omega", "prsgrd", "pre_step3d", "set_HUV1", "step3d_uv1", "visc3d", "step2d",
+            "step3d_uv2", "step3d_t", "t3dmix")
+HALO_OPP = (1, 0, 3, 2, 7, 6, 5, 4)
+
+
+def comm_unique_id():
+    """128-byte RCCL id (rank 0); broadcast it with the host's own collective."""
+    L = load_library()
+    buf = ctypes.create_string_buffer(128)
+    _check(L, L.roms_gpu_comm_unique_id(buf), "roms_gpu_comm_unique_id")
+    return buf.raw
+
+
+def comm_create(uid, nranks, rank, device=0):
+    """RCCL communicator handle for roms_gpu_init / init_case_comm."""
+    L = load_library()
+    h = ctypes.c_void_p()
+    buf = ctypes.create_string_buffer(bytes(uid), 128)
+    _check(L, L.roms_gpu_comm_create(buf, nranks, rank, device, ctypes.byref(h)), "roms_gpu_comm_create")
+    return h
+
+
+def comm_create_local(group, nranks, rank):
+    """Handle for subdomains driven by threads of this process (one per thread)."""
+    L = load_library()
+    h = ctypes.c_void_p()
+    _check(L, L.roms_gpu_comm_create_local(group, nranks, rank, ctypes.byref(h)), "roms_gpu_comm_create_local")
+    return h
+
+
+def comm_destroy(h):
+    load_library().roms_gpu_comm_destroy(h)
 
 
 class Model:
@@ -112,12 +203,21 @@ class Model:
     # ---- construction ----
     @classmethod
     def from_case(cls, case_id, LLm, MMm, N, NT=1, salinity=False, nonlin_eos=False, dt=5.0, ndtfast=60,
-                  sizex=12.8e3, sizey=3.2e3, device=0):
+                  sizex=12.8e3, sizey=3.2e3, device=0, np_xi=1, np_eta=1, comm=None, rank=0):
+        """Analytic case on the whole grid, or on subdomain `rank` of an
+        np_xi x np_eta processor grid when a communicator is given."""
         m = cls()
         c = Case(case_id, LLm, MMm, N, NT, int(salinity), int(nonlin_eos), 0, dt, ndtfast, sizex, sizey)
-        m._chk(m.L.roms_gpu_init_case(ctypes.byref(c), device, ctypes.byref(m.t)), "roms_gpu_init_case")
+        if comm is None and np_xi * np_eta == 1:
+            m._chk(m.L.roms_gpu_init_case(ctypes.byref(c), device, ctypes.byref(m.t)), "roms_gpu_init_case")
+        else:
+            m._chk(m.L.roms_gpu_init_case_comm(ctypes.byref(c), np_xi, np_eta, comm, device, ctypes.byref(m.t)),
+                   "roms_gpu_init_case_comm")
         m.LLm, m.MMm, m.N, m.NT = LLm, MMm, N, NT
-        m.shape2 = (MMm + 4, LLm + 4)
+        m.jnode, m.inode = divmod(rank, np_xi)
+        m.Lm, m.iSW = rank_extent(LLm, np_xi, m.inode)
+        m.Mm, m.jSW = rank_extent(MMm, np_eta, m.jnode)
+        m.shape2 = (m.Mm + 4, m.Lm + 4)
         return m
 
     @classmethod
@@ -185,6 +285,16 @@ class Model:
         """roms_step (main.F:333-520) n times; updates the time indices."""
         for _ in range(n):
             self._r("step")
+
+    def time_routine(self, routine, nsteps):
+        """Mean duration [ms] of one call of `routine` (name in ROUTINES) and
+        the number of calls, from HIP events around its launches over
+        `nsteps` eager steps (the model advances by nsteps)."""
+        ms = ctypes.c_double()
+        n = ctypes.c_long()
+        self._chk(self.L.roms_gpu_time_routine(ROUTINES.index(routine), nsteps, ctypes.byref(self.t), ctypes.byref(ms),
+                                               ctypes.byref(n)), "time_routine")
+        return ms.value, n.value
 
     def diag(self):
         out = (ctypes.c_double * 4)()
