@@ -173,6 +173,173 @@ __global__ void __launch_bounds__(256) k_s2d_mom(Dev d, Range R, FBCoef c) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Fused fast step: one block owns a 64x4 tile of the averaging range RB and
+// first evaluates the free-surface part (k_s2d_zeta's formulas) on the tile
+// plus one row/column on its low side into LDS, applies the closed-wall
+// zetabc to ghost cells inside that window, then runs the averaging and
+// momentum part (k_s2d_mom's formulas) reading its i-1 / j-1 neighbours from
+// LDS.  zeta_new/Dnew also go to global scratch when closed-edge kernels
+// need them afterwards.
+// ---------------------------------------------------------------------------
+constexpr int kFX = kBX + 1, kFY = kBY + 1, kFN = kFX * kFY;
+struct FBTile {
+  double zn[kFN], Dn[kFN], zw[kFN], rz[kFN], rz2[kFN], rzSA[kFN];
+  unsigned char st[kFN];  // 0: outside, 1: computed, 2: set by zetabc
+};
+
+__global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int closed) {
+  __shared__ FBTile T;
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const long sj = b.nx2, n2 = b.n2;
+  const int i0 = R.i0 + (int)blockIdx.x * kBX, j0 = R.j0 + (int)blockIdx.y * kBY;
+  const int tid = threadIdx.x + kBX * threadIdx.y;
+  // zeta range of the reference kernel (istrU-1..iend, jstrV-1..jend)
+  const int za = b.istrU - 1, zb = b.iend, zc = b.jstrV - 1, zd = b.jend;
+  for (int q = tid; q < kFN; q += kBX * kBY) {
+    const int li = q % kFX, lj = q / kFX;
+    const int i = i0 - 1 + li, j = j0 - 1 + lj;
+    if (i < za || i > zb || j < zc || j > zd) {  // outside the reference's zeta range: never consumed
+      T.zn[q] = T.Dn[q] = T.zw[q] = T.rz[q] = T.rz2[q] = T.rzSA[q] = 0.0;
+      T.st[q] = 0;
+      continue;
+    }
+    T.st[q] = 1;
+    const long ij = IJ(b, i, j);
+    const double zk = F.zeta[ij + (long)(c.kstp - 1) * n2];
+    double zn = zk + d.p.dtfast * F.pm[ij] * F.pn[ij] *
+                         (s2d_DUon(d, c, ij) - s2d_DUon(d, c, ij + 1) + s2d_DVom(d, c, ij) - s2d_DVom(d, c, ij + sj)) +
+                d.p.dtfast * F.swflx[ij];
+    zn = zn * F.rmask[ij];
+    const double zwrk = c.bkw_new * zn + c.bkw * zk + c.bkw1 * F.zeta[ij + (long)(c.kbak - 1) * n2] +
+                        c.bkw2 * F.zeta[ij + (long)(c.kold - 1) * n2];
+    const double rzeta = (1.0 + F.rhoS[ij]) * zwrk;
+    T.zn[q] = zn;
+    T.Dn[q] = zn + F.h[ij];
+    T.zw[q] = zwrk;
+    T.rz[q] = rzeta;
+    T.rzSA[q] = zwrk * (F.rhoS[ij] - F.rhoA[ij]);
+    T.rz2[q] = rzeta * zwrk;
+  }
+  __syncthreads();
+  if (closed) {
+    // zetabc_tile (zetabc.F), closed walls: edges, then corners
+    auto L = [&](int i, int j) { return (i - (i0 - 1)) + (j - (j0 - 1)) * kFX; };
+    auto in = [&](int i, int j) { return i >= i0 - 1 && i <= i0 + kBX - 1 && j >= j0 - 1 && j <= j0 + kBY - 1; };
+    for (int q = tid; q < kFN; q += kBX * kBY) {
+      const int i = i0 - 1 + q % kFX, j = j0 - 1 + q / kFX;
+      const long ij = IJ(b, i, j);
+      if (j >= b.jstrV - 1 && j <= b.jend) {
+        if (b.west_edge && i == b.istr - 1 && in(b.istr, j)) { T.zn[q] = T.zn[L(b.istr, j)] * F.rmask[ij]; T.st[q] = 2; }
+        if (b.east_edge && i == b.iend + 1 && in(b.iend, j)) { T.zn[q] = T.zn[L(b.iend, j)] * F.rmask[ij]; T.st[q] = 2; }
+      }
+      if (i >= b.istrU - 1 && i <= b.iend) {
+        if (b.south_edge && j == b.jstr - 1 && in(i, b.jstr)) { T.zn[q] = T.zn[L(i, b.jstr)] * F.rmask[ij]; T.st[q] = 2; }
+        if (b.north_edge && j == b.jend + 1 && in(i, b.jend)) { T.zn[q] = T.zn[L(i, b.jend)] * F.rmask[ij]; T.st[q] = 2; }
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      const int is = b.istr, ie = b.iend, js = b.jstr, je = b.jend;
+      if (b.south_edge && b.west_edge && in(is - 1, js - 1) && in(is, js - 1) && in(is - 1, js))
+        { T.zn[L(is - 1, js - 1)] = 0.5 * (T.zn[L(is, js - 1)] + T.zn[L(is - 1, js)]); T.st[L(is - 1, js - 1)] = 2; }
+      if (b.south_edge && b.east_edge && in(ie + 1, js - 1) && in(ie, js - 1) && in(ie + 1, js))
+        { T.zn[L(ie + 1, js - 1)] = 0.5 * (T.zn[L(ie, js - 1)] + T.zn[L(ie + 1, js)]); T.st[L(ie + 1, js - 1)] = 2; }
+      if (b.north_edge && b.west_edge && in(is - 1, je + 1) && in(is, je + 1) && in(is - 1, je))
+        { T.zn[L(is - 1, je + 1)] = 0.5 * (T.zn[L(is, je + 1)] + T.zn[L(is - 1, je)]); T.st[L(is - 1, je + 1)] = 2; }
+      if (b.north_edge && b.east_edge && in(ie + 1, je + 1) && in(ie, je + 1) && in(ie + 1, je))
+        { T.zn[L(ie + 1, je + 1)] = 0.5 * (T.zn[L(ie, je + 1)] + T.zn[L(ie + 1, je)]); T.st[L(ie + 1, je + 1)] = 2; }
+    }
+    __syncthreads();
+    // the edge kernels read zeta_new / Dnew from global scratch: every block
+    // stores the window cells it computed or set (identical values where
+    // windows overlap)
+    for (int q = tid; q < kFN; q += kBX * kBY) {
+      if (!T.st[q]) continue;
+      const long o = IJ(b, i0 - 1 + q % kFX, j0 - 1 + q / kFX);
+      F.s0[o] = T.zn[q];
+      if (T.st[q] == 1) F.s1[o] = T.Dn[q];
+    }
+  }
+  const int i = i0 + (int)threadIdx.x, j = j0 + (int)threadIdx.y;
+  if (i > R.i1 || j > R.j1) return;
+  const int q = (threadIdx.x + 1) + (threadIdx.y + 1) * kFX;  // (i,j); q-1 = (i-1,j); q-kFX = (i,j-1)
+  const long ij = IJ(b, i, j);
+  {
+    const double z = T.zn[q];
+    F.zeta[ij + (long)(c.knew - 1) * n2] = z;
+    if (c.iif == 1) {
+      F.DU_avg_bak[ij] = F.DU_avg1[ij] - 0.1024390243902439 * F.DU_avg2[ij];
+      F.DV_avg_bak[ij] = F.DV_avg1[ij] - 0.1024390243902439 * F.DV_avg2[ij];
+      F.Zt_avg1[ij] = c.w1 * z;
+      F.DU_avg1[ij] = 0.0;
+      F.DV_avg1[ij] = 0.0;
+      F.DU_avg2[ij] = c.w2 * s2d_DUon(d, c, ij);
+      F.DV_avg2[ij] = c.w2 * s2d_DVom(d, c, ij);
+    } else {
+      F.Zt_avg1[ij] = F.Zt_avg1[ij] + c.w1 * z;
+      F.DU_avg2[ij] = F.DU_avg2[ij] + c.w2 * s2d_DUon(d, c, ij);
+      F.DV_avg2[ij] = F.DV_avg2[ij] + c.w2 * s2d_DVom(d, c, ij);
+    }
+  }
+  if (i < b.istr || i > b.iend || j < b.jstr || j > b.jend) return;
+  const double gh = 0.5 * d.p.g;
+  // pressure gradient at u (neighbour q-1) and v (neighbour q-kFX) points
+  auto pgf = [&](long s, int qm, double dn) {
+    return gh * dn *
+           ((F.h[ij - s] + F.h[ij]) * (T.rz[qm] - T.rz[q]) + T.rz2[qm] - T.rz2[q] +
+            (F.h[ij - s] - F.h[ij]) *
+                (T.rzSA[qm] + T.rzSA[q] + 0.333333333333 * (F.rhoA[ij - s] - F.rhoA[ij]) * (T.zw[qm] - T.zw[q])));
+  };
+  double rubar = pgf(1, q - 1, F.dn_u[ij]);
+  double rvbar = pgf(sj, q - kFX, F.dm_v[ij]);
+  double rufrc = F.rufrc[ij], rvfrc = F.rvfrc[ij];
+  if (c.iif == 1) {
+    rufrc = rufrc - rubar;
+    rvfrc = rvfrc - rvbar;
+    F.rufrc[ij] = rufrc;
+    F.rvfrc[ij] = rvfrc;
+    const long lk = (long)(c.kstp - 1) * n2;
+    auto corr = [&](int qq, long o, double& zwrk, double& rzeta, double& rzeta2, double& rzetaSA) {
+      const double zn = T.zn[qq], zk = F.zeta[o + lk];
+      zwrk = zn - zk;
+      rzeta = (1.0 + F.rhoS[o]) * zwrk;
+      rzeta2 = rzeta * (zn + zk);
+      rzetaSA = zwrk * (F.rhoS[o] - F.rhoA[o]);
+    };
+    double zw0, rz0, rz20, sa0, zw1, rz1, rz21, sa1, zw2, rz2_, rz22, sa2;
+    corr(q, ij, zw0, rz0, rz20, sa0);
+    corr(q - 1, ij - 1, zw1, rz1, rz21, sa1);
+    corr(q - kFX, ij - sj, zw2, rz2_, rz22, sa2);
+    rubar = rubar + gh * F.dn_u[ij] *
+                        ((F.h[ij - 1] + F.h[ij]) * (rz1 - rz0) + rz21 - rz20 +
+                         (F.h[ij - 1] - F.h[ij]) * (sa1 + sa0 + 0.333333333333 * (F.rhoA[ij - 1] - F.rhoA[ij]) * (zw1 - zw0)));
+    rvbar = rvbar + gh * F.dm_v[ij] *
+                        ((F.h[ij - sj] + F.h[ij]) * (rz2_ - rz0) + rz22 - rz20 +
+                         (F.h[ij - sj] - F.h[ij]) * (sa2 + sa0 + 0.333333333333 * (F.rhoA[ij - sj] - F.rhoA[ij]) * (zw2 - zw0)));
+  }
+  const double cff = 0.5 * d.p.dtfast, cff1 = 0.5 * c.w1;
+  const long lk = (long)(c.kstp - 1) * n2;
+  const double Dstp0 = F.zeta[ij + lk] + F.h[ij];
+  if (i >= b.istrU) {
+    const double Dstpm = F.zeta[ij - 1 + lk] + F.h[ij - 1];
+    const double DUnew = ((Dstp0 + Dstpm) * F.ubar[ij + lk] +
+                          cff * (F.pm[ij] + F.pm[ij - 1]) * (F.pn[ij] + F.pn[ij - 1]) * (rubar + rufrc)) *
+                         F.umask[ij];
+    F.ubar[ij + (long)(c.knew - 1) * n2] = DUnew / (T.Dn[q] + T.Dn[q - 1]);
+    F.DU_avg1[ij] = F.DU_avg1[ij] + cff1 * F.dn_u[ij] * (DUnew);
+  }
+  if (j >= b.jstrV) {
+    const double Dstpm = F.zeta[ij - sj + lk] + F.h[ij - sj];
+    const double DVnew = ((Dstp0 + Dstpm) * F.vbar[ij + lk] +
+                          cff * (F.pm[ij] + F.pm[ij - sj]) * (F.pn[ij] + F.pn[ij - sj]) * (rvbar + rvfrc)) *
+                         F.vmask[ij];
+    F.vbar[ij + (long)(c.knew - 1) * n2] = DVnew / (T.Dn[q] + T.Dn[q - kFX]);
+    F.DV_avg1[ij] = F.DV_avg1[ij] + cff1 * F.dm_v[ij] * (DVnew);
+  }
+}
+
 // u2dbc/v2dbc (closed), boundary Dnew, boundary flux averages (step2d_FB.F:444-529)
 __global__ void k_s2d_edges(Dev d, FBCoef c, int phase) {
   const Bounds& b = d.b;
@@ -298,16 +465,20 @@ void launch_step2d(const Dev& d, hipStream_t s, const Tlev& t, const double* w1,
   }
   c.w1 = w1[t.iif - 1];
   c.w2 = w2[t.iif - 1];
-  Range RA{b.istrU - 1, b.iend, b.jstrV - 1, b.jend};
-  hipLaunchKernelGGL(k_s2d_zeta, grid_of(RA), dim3(kBX, kBY), 0, s, d, RA, c);
   const bool closed = b.west_edge || b.east_edge || b.south_edge || b.north_edge;
-  if (closed) {
-    const int n = (b.jend - b.jstrV + 2) + (b.iend - b.istrU + 2);
-    hipLaunchKernelGGL(k_s2d_zetabc, dim3((n + 255) / 256), dim3(256), 0, s, d, 0);
-    hipLaunchKernelGGL(k_s2d_zetabc, dim3(1), dim3(64), 0, s, d, 1);
-  }
   Range RB{b.istrR, b.iendR, b.jstrR, b.jendR};
-  hipLaunchKernelGGL(k_s2d_mom, grid_of(RB), dim3(kBX, kBY), 0, s, d, RB, c);
+  if (d.p.s2d_split) {  // two-kernel form (kept for A/B timing)
+    Range RA{b.istrU - 1, b.iend, b.jstrV - 1, b.jend};
+    hipLaunchKernelGGL(k_s2d_zeta, grid_of(RA), dim3(kBX, kBY), 0, s, d, RA, c);
+    if (closed) {
+      const int n = (b.jend - b.jstrV + 2) + (b.iend - b.istrU + 2);
+      hipLaunchKernelGGL(k_s2d_zetabc, dim3((n + 255) / 256), dim3(256), 0, s, d, 0);
+      hipLaunchKernelGGL(k_s2d_zetabc, dim3(1), dim3(64), 0, s, d, 1);
+    }
+    hipLaunchKernelGGL(k_s2d_mom, grid_of(RB), dim3(kBX, kBY), 0, s, d, RB, c);
+  } else {
+    hipLaunchKernelGGL(k_s2d_fb, grid_of(RB), dim3(kBX, kBY), 0, s, d, RB, c, (int)closed);
+  }
   if (closed) {
     const int L = b.nx2 > b.Mm + 4 ? b.nx2 : b.Mm + 4;
     for (int ph = 0; ph < 3; ph++)

@@ -31,6 +31,7 @@ struct Bounds {
 // Physics switches (cppdefs.opt) and scalars of the run.
 struct Params {
   int nonlin_eos, salinity, lmd, uv_vis2, ts_dif2;
+  int s2d_split;  // 1: step2d as separate zeta / momentum kernels (ROMS_GPU_S2D_SPLIT=1)
   double dt, dtfast, g, rho0, vonKar, qp2, gamma2, hc;
   double rdrg, Zob, Tcoef, T0, Scoef, S0;
 };

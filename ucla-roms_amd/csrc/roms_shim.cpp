@@ -273,6 +273,10 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
   Params& P = g.d.p;
   P.nonlin_eos = cfg->nonlin_eos; P.salinity = cfg->salinity; P.lmd = cfg->lmd_mixing;
   P.uv_vis2 = cfg->uv_vis2; P.ts_dif2 = cfg->ts_dif2;
+  {
+    const char* e = getenv("ROMS_GPU_S2D_SPLIT");
+    P.s2d_split = e && e[0] == '1';
+  }
   P.dt = cfg->dt; P.dtfast = cfg->dt / (double)cfg->ndtfast; P.g = cfg->g; P.rho0 = cfg->rho0;
   P.vonKar = 0.41; P.qp2 = 0.0000172; P.gamma2 = cfg->gamma2; P.hc = cfg->hc;
   P.rdrg = cfg->rdrg; P.Zob = cfg->Zob; P.Tcoef = cfg->Tcoef; P.T0 = cfg->T0; P.Scoef = cfg->Scoef; P.S0 = cfg->S0;
