@@ -99,7 +99,8 @@ __global__ void __launch_bounds__(256) k_prsgrd_uv(Dev d, Range R, int split, in
   const bool du = i >= b.istrU && i <= b.iend && j >= b.jstr && j <= b.jend;
   const bool dv = i >= b.istr && i <= b.iend && j >= b.jstrV && j <= b.jend;
   const long ij = IJ(b, i, j);
-  for (int k = b.N; k >= 1; k--) {
+  {
+    const int k = 1 + (int)blockIdx.z;
     const long kk = (long)(k - 1) * b.n2;
     if (du) {
       // FC(m), rx(m) at u-points m=i-1,i,i+1 (clamped = edge extrapolation)
@@ -181,7 +182,7 @@ void launch_prsgrd(const Dev& d, hipStream_t s, const Tlev& t) {
   Range R1{0, b.Lm, 0, b.Mm};
   hipLaunchKernelGGL(k_prsgrd_P, grid_of(R1), dim3(kBX, kBY), 0, s, d, R1, split);
   Range R2{b.istr, b.iend, b.jstr, b.jend};
-  hipLaunchKernelGGL(k_prsgrd_uv, grid_of(R2), dim3(kBX, kBY), 0, s, d, R2, split, imin, imax, jmin, jmax);
+  hipLaunchKernelGGL(k_prsgrd_uv, grid3_of(R2, b.N), dim3(kBX, kBY), 0, s, d, R2, split, imin, imax, jmin, jmax);
 }
 
 }  // namespace roms

@@ -149,7 +149,8 @@ __global__ void __launch_bounds__(256) k_t3dmix(Dev d, Range R, int nnew, int nr
     return 0.25 * (d2[p] + d2[p - sj]) * F.pnom_v[p] * (F.Hz[p + kk] + F.Hz[p - sj + kk]) *
            (Tr[p + kk] - Tr[p - sj + kk]) * F.vmask[p];
   };
-  for (int k = 1; k <= b.N; k++) {
+  {
+    const int k = 1 + (int)blockIdx.z;
     const long kk = (long)(k - 1) * n2, o = ij + kk;
     Tn[o] = Tn[o] + d.p.dt * F.pm[ij] * F.pn[ij] * (FX(ij + 1, kk) - FX(ij, kk) + FE(ij + sj, kk) - FE(ij, kk)) / F.Hz[o];
   }
@@ -159,7 +160,7 @@ void launch_t3dmix(const Dev& d, hipStream_t s, const Tlev& t) {
   const Bounds& b = d.b;
   Range R{b.istr, b.iend, b.jstr, b.jend};
   for (int itrc = 1; itrc <= b.NT; itrc++)
-    hipLaunchKernelGGL(k_t3dmix, grid_of(R), dim3(kBX, kBY), 0, s, d, R, t.nnew, t.nrhs, itrc);
+    hipLaunchKernelGGL(k_t3dmix, grid3_of(R, b.N), dim3(kBX, kBY), 0, s, d, R, t.nnew, t.nrhs, itrc);
   launch_exchange_tracers(d, s, t.nnew);
 }
 

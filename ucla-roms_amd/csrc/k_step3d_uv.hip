@@ -128,50 +128,69 @@ __device__ __forceinline__ void visc_psi(const Dev& d, int i, int j, int k, int 
   VFx = cff * F.dn_p[ij] * F.dn_p[ij];
 }
 
+// per cell (i,j,k): stress divergence cff added as dt*cff to u,v(indx); cff
+// kept in column scratch (c0: u, c1: v) for the vertical sums below
 __global__ void __launch_bounds__(256) k_visc3d(Dev d, Range R, int nstp) {
   ROMS_IJ_OR_RETURN(R)
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const int indx = 3 - nstp;
+  const int k = 1 + (int)blockIdx.z;
   const long ij = IJ(b, i, j), sj = b.nx2;
   const double* pm = F.pm;
   const double* pn = F.pn;
-  const bool du = i >= b.istrU && i <= b.iend;
-  const bool dv = j >= b.jstrV && j <= b.jend;
-  double frcu = F.rufrc[ij], frcv = F.rvfrc[ij];
-  for (int k = 1; k <= b.N; k++) {
-    const long o = ij + (long)(k - 1) * b.n2;
-    if (du) {
-      double UFx0, UFx1, VFe_, UFe0, UFe1, VFx_;
-      visc_rho(d, i, j, k, nstp, UFx0, VFe_);
-      visc_rho(d, i - 1, j, k, nstp, UFx1, VFe_);
-      visc_psi(d, i, j, k, nstp, UFe0, VFx_);
-      visc_psi(d, i, j + 1, k, nstp, UFe1, VFx_);
-      const double cff = 0.125 * (pm[ij - 1] + pm[ij]) * (pn[ij - 1] + pn[ij]) *
-                         ((pn[ij - 1] + pn[ij]) * (UFx0 - UFx1) + (pm[ij - 1] + pm[ij]) * (UFe1 - UFe0));
-      frcu = frcu + cff;
-      F.u[o + (long)(indx - 1) * b.n3] = F.u[o + (long)(indx - 1) * b.n3] + d.p.dt * cff;
-    }
-    if (dv) {
-      double VFe0, VFe1, UFx_, VFx0, VFx1, UFe_;
-      visc_rho(d, i, j, k, nstp, UFx_, VFe0);
-      visc_rho(d, i, j - 1, k, nstp, UFx_, VFe1);
-      visc_psi(d, i, j, k, nstp, UFe_, VFx0);
-      visc_psi(d, i + 1, j, k, nstp, UFe_, VFx1);
-      const double cff = 0.125 * (pm[ij] + pm[ij - sj]) * (pn[ij] + pn[ij - sj]) *
-                         ((pn[ij - sj] + pn[ij]) * (VFx1 - VFx0) + (pm[ij - sj] + pm[ij]) * (VFe0 - VFe1));
-      frcv = frcv + cff;
-      F.v[o + (long)(indx - 1) * b.n3] = F.v[o + (long)(indx - 1) * b.n3] + d.p.dt * cff;
-    }
+  const long o = ij + (long)(k - 1) * b.n2;
+  if (i >= b.istrU && i <= b.iend) {
+    double UFx0, UFx1, VFe_, UFe0, UFe1, VFx_;
+    visc_rho(d, i, j, k, nstp, UFx0, VFe_);
+    visc_rho(d, i - 1, j, k, nstp, UFx1, VFe_);
+    visc_psi(d, i, j, k, nstp, UFe0, VFx_);
+    visc_psi(d, i, j + 1, k, nstp, UFe1, VFx_);
+    const double cff = 0.125 * (pm[ij - 1] + pm[ij]) * (pn[ij - 1] + pn[ij]) *
+                       ((pn[ij - 1] + pn[ij]) * (UFx0 - UFx1) + (pm[ij - 1] + pm[ij]) * (UFe1 - UFe0));
+    F.c0[o] = cff;
+    F.u[o + (long)(indx - 1) * b.n3] = F.u[o + (long)(indx - 1) * b.n3] + d.p.dt * cff;
   }
-  if (du) F.rufrc[ij] = frcu;
-  if (dv) F.rvfrc[ij] = frcv;
+  if (j >= b.jstrV && j <= b.jend) {
+    double VFe0, VFe1, UFx_, VFx0, VFx1, UFe_;
+    visc_rho(d, i, j, k, nstp, UFx_, VFe0);
+    visc_rho(d, i, j - 1, k, nstp, UFx_, VFe1);
+    visc_psi(d, i, j, k, nstp, UFe_, VFx0);
+    visc_psi(d, i + 1, j, k, nstp, UFe_, VFx1);
+    const double cff = 0.125 * (pm[ij] + pm[ij - sj]) * (pn[ij] + pn[ij - sj]) *
+                       ((pn[ij - sj] + pn[ij]) * (VFx1 - VFx0) + (pm[ij - sj] + pm[ij]) * (VFe0 - VFe1));
+    F.c1[o] = cff;
+    F.v[o + (long)(indx - 1) * b.n3] = F.v[o + (long)(indx - 1) * b.n3] + d.p.dt * cff;
+  }
+}
+
+// rufrc/rvfrc += sum_k cff(k), summed in the reference's k = 1..N order
+__global__ void __launch_bounds__(256) k_visc3d_frc(Dev d, Range R) {
+  ROMS_IJ_OR_RETURN(R)
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const long ij = IJ(b, i, j), n2 = b.n2;
+  if (i >= b.istrU && i <= b.iend) {
+    const double* __restrict__ cu = F.c0 + ij;
+    double frc = F.rufrc[ij];
+#pragma unroll 8
+    for (int k = 1; k <= b.N; k++) frc = frc + cu[(long)(k - 1) * n2];
+    F.rufrc[ij] = frc;
+  }
+  if (j >= b.jstrV && j <= b.jend) {
+    const double* __restrict__ cv = F.c1 + ij;
+    double frc = F.rvfrc[ij];
+#pragma unroll 8
+    for (int k = 1; k <= b.N; k++) frc = frc + cv[(long)(k - 1) * n2];
+    F.rvfrc[ij] = frc;
+  }
 }
 
 void launch_visc3d(const Dev& d, hipStream_t s, const Tlev& t) {
   const Bounds& b = d.b;
   Range R{b.istr, b.iend, b.jstr, b.jend};
-  hipLaunchKernelGGL(k_visc3d, grid_of(R), dim3(kBX, kBY), 0, s, d, R, t.nstp);
+  hipLaunchKernelGGL(k_visc3d, grid3_of(R, b.N), dim3(kBX, kBY), 0, s, d, R, t.nstp);
+  hipLaunchKernelGGL(k_visc3d_frc, grid_of(R), dim3(kBX, kBY), 0, s, d, R);
 }
 
 // ---- step3d_uv2 part 1: convert Hz*u to u and remove the mismatch against

@@ -63,7 +63,8 @@ __global__ void __launch_bounds__(256) k_set_huv(Dev d, Range R, int nrhs) {
   const bool du = i >= b.istr && i <= b.iendR && j >= b.jstrR && j <= b.jendR;
   const bool dv = i >= b.istrR && i <= b.iendR && j >= b.jstr && j <= b.jendR;
   const long ij = IJ(b, i, j);
-  for (int k = 1; k <= b.N; k++) {
+  {
+    const int k = 1 + (int)blockIdx.z;
     const long o = ij + (long)(k - 1) * b.n2;
     const double hz = F.Hz[o];
     if (du) {
@@ -82,7 +83,7 @@ __global__ void __launch_bounds__(256) k_set_huv(Dev d, Range R, int nrhs) {
 void launch_set_huv(const Dev& d, hipStream_t s, const Tlev& t) {
   const Bounds& b = d.b;
   Range R{b.istrR < b.istr ? b.istrR : b.istr, b.iendR, b.jstrR < b.jstr ? b.jstrR : b.jstr, b.jendR};
-  hipLaunchKernelGGL(k_set_huv, grid_of(R), dim3(kBX, kBY), 0, s, d, R, t.nrhs);
+  hipLaunchKernelGGL(k_set_huv, grid3_of(R, b.N), dim3(kBX, kBY), 0, s, d, R, t.nrhs);
   launch_exchange_list(d, s, ExchList{{d.f.FlxU, d.f.FlxV}, {b.N, b.N}, 2});
 }
 
