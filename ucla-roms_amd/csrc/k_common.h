@@ -142,138 +142,141 @@ __host__ inline UVBounds uv_bounds(const Bounds& b) {
   return r;
 }
 
-// u at (i,j,k) of level slab U (already offset to the time level)
-#define UU(ii, jj) U[IJ(b, ii, jj) + kk]
-#define VV(ii, jj) V[IJ(b, ii, jj) + kk]
-#define FU(ii, jj) F.FlxU[IJ(b, ii, jj) + kk]
-#define FV(ii, jj) F.FlxV[IJ(b, ii, jj) + kk]
+// The UV advection fragments are written once over an accessor A giving
+// u, v (time level nrhs) and FlxU, FlxV at level k: AccG reads HBM, AccL a
+// block's LDS window (k_uv_horiz).  Identical arithmetic either way.
+struct AccG {
+  const double *U, *V, *FU, *FV;
+  long kk;
+  int nx2;
+  __device__ __forceinline__ long at(int i, int j) const { return (long)(i + 1) + (long)(j + 1) * nx2 + kk; }
+  __device__ __forceinline__ double u(int i, int j) const { return U[at(i, j)]; }
+  __device__ __forceinline__ double v(int i, int j) const { return V[at(i, j)]; }
+  __device__ __forceinline__ double fu(int i, int j) const { return FU[at(i, j)]; }
+  __device__ __forceinline__ double fv(int i, int j) const { return FV[at(i, j)]; }
+};
+constexpr int kUVW = kBX + 4, kUVH = kBY + 4, kUVN = kUVW * kUVH;  // LDS window (i0-2.., j0-2..)
+struct AccL {
+  const double *U, *V, *FU, *FV;   // LDS windows, row-major kUVW
+  int ib, jb;                      // global (i,j) of window element 0
+  __device__ __forceinline__ int at(int i, int j) const { return (i - ib) + (j - jb) * kUVW; }
+  __device__ __forceinline__ double u(int i, int j) const { return U[at(i, j)]; }
+  __device__ __forceinline__ double v(int i, int j) const { return V[at(i, j)]; }
+  __device__ __forceinline__ double fu(int i, int j) const { return FU[at(i, j)]; }
+  __device__ __forceinline__ double fv(int i, int j) const { return FV[at(i, j)]; }
+};
 
-__device__ __forceinline__ double uxx_at(const Dev& d, const double* U, int m, int j, long kk, const UVBounds& r) {
-  const Bounds& b = d.b;
+template <class A>
+__device__ __forceinline__ double uxx_at(const A& a, int m, int j, const UVBounds& r) {
   m = iclamp(m, r.u_imin, r.u_imax);
-  return UU(m - 1, j) - 2.0 * UU(m, j) + UU(m + 1, j);
+  return a.u(m - 1, j) - 2.0 * a.u(m, j) + a.u(m + 1, j);
 }
-__device__ __forceinline__ double Huxx_at(const Dev& d, int m, int j, long kk, const UVBounds& r) {
-  const Bounds& b = d.b;
-  const Fields& F = d.f;
+template <class A>
+__device__ __forceinline__ double Huxx_at(const A& a, int m, int j, const UVBounds& r) {
   m = iclamp(m, r.u_imin, r.u_imax);
-  return FU(m - 1, j) - 2.0 * FU(m, j) + FU(m + 1, j);
+  return a.fu(m - 1, j) - 2.0 * a.fu(m, j) + a.fu(m + 1, j);
 }
-__device__ __forceinline__ double vee_at(const Dev& d, const double* V, int i, int m, long kk, const UVBounds& r) {
-  const Bounds& b = d.b;
+template <class A>
+__device__ __forceinline__ double vee_at(const A& a, int i, int m, const UVBounds& r) {
   m = iclamp(m, r.v_jmin, r.v_jmax);
-  return VV(i, m - 1) - 2.0 * VV(i, m) + VV(i, m + 1);
+  return a.v(i, m - 1) - 2.0 * a.v(i, m) + a.v(i, m + 1);
 }
-__device__ __forceinline__ double Hvee_at(const Dev& d, int i, int m, long kk, const UVBounds& r) {
-  const Bounds& b = d.b;
-  const Fields& F = d.f;
+template <class A>
+__device__ __forceinline__ double Hvee_at(const A& a, int i, int m, const UVBounds& r) {
   m = iclamp(m, r.v_jmin, r.v_jmax);
-  return FV(i, m - 1) - 2.0 * FV(i, m) + FV(i, m + 1);
+  return a.fv(i, m - 1) - 2.0 * a.fv(i, m) + a.fv(i, m + 1);
 }
-__device__ __forceinline__ double uee_at(const Dev& d, const double* U, int i, int m, long kk, const UVBounds& r) {
-  const Bounds& b = d.b;
+template <class A>
+__device__ __forceinline__ double uee_at(const A& a, int i, int m, const UVBounds& r) {
   m = iclamp(m, r.e_jmin, r.e_jmax);
-  return UU(i, m - 1) - 2.0 * UU(i, m) + UU(i, m + 1);
+  return a.u(i, m - 1) - 2.0 * a.u(i, m) + a.u(i, m + 1);
 }
-__device__ __forceinline__ double vxx_at(const Dev& d, const double* V, int m, int j, long kk, const UVBounds& r) {
-  const Bounds& b = d.b;
+template <class A>
+__device__ __forceinline__ double vxx_at(const A& a, int m, int j, const UVBounds& r) {
   m = iclamp(m, r.x_imin, r.x_imax);
-  return VV(m - 1, j) - 2.0 * VV(m, j) + VV(m + 1, j);
+  return a.v(m - 1, j) - 2.0 * a.v(m, j) + a.v(m + 1, j);
 }
 
 // UFx at rho-point (m,j): diagonal xi-flux of u-momentum
-__device__ __forceinline__ double adv_UFx(const Dev& d, const double* U, int m, int j, long kk, const UVBounds& r,
-                                          bool up) {
-  const Bounds& b = d.b;
-  const Fields& F = d.f;
+template <class A>
+__device__ __forceinline__ double adv_UFx(const A& a, int m, int j, const UVBounds& r, bool up) {
   const double delta = 0.1666666666666667, gamma = 0.3333333333333333;
-  const double ux0 = uxx_at(d, U, m, j, kk, r), ux1 = uxx_at(d, U, m + 1, j, kk, r);
-  const double Hx0 = Huxx_at(d, m, j, kk, r), Hx1 = Huxx_at(d, m + 1, j, kk, r);
+  const double ux0 = uxx_at(a, m, j, r), ux1 = uxx_at(a, m + 1, j, r);
+  const double Hx0 = Huxx_at(a, m, j, r), Hx1 = Huxx_at(a, m + 1, j, r);
   if (up) {
-    const double cff = FU(m, j) + FU(m + 1, j) - delta * (Hx0 + Hx1);
-    return 0.25 * (cff * (UU(m, j) + UU(m + 1, j)) - gamma * (fmax0(cff) * ux0 + fmin0(cff) * ux1));
+    const double cff = a.fu(m, j) + a.fu(m + 1, j) - delta * (Hx0 + Hx1);
+    return 0.25 * (cff * (a.u(m, j) + a.u(m + 1, j)) - gamma * (fmax0(cff) * ux0 + fmin0(cff) * ux1));
   }
-  return 0.25 * (UU(m, j) + UU(m + 1, j) - delta * (ux0 + ux1)) * (FU(m, j) + FU(m + 1, j) - delta * (Hx0 + Hx1));
+  return 0.25 * (a.u(m, j) + a.u(m + 1, j) - delta * (ux0 + ux1)) * (a.fu(m, j) + a.fu(m + 1, j) - delta * (Hx0 + Hx1));
 }
 // VFe at rho-point (i,m)
-__device__ __forceinline__ double adv_VFe(const Dev& d, const double* V, int i, int m, long kk, const UVBounds& r,
-                                          bool up) {
-  const Bounds& b = d.b;
-  const Fields& F = d.f;
+template <class A>
+__device__ __forceinline__ double adv_VFe(const A& a, int i, int m, const UVBounds& r, bool up) {
   const double delta = 0.1666666666666667, gamma = 0.3333333333333333;
-  const double ve0 = vee_at(d, V, i, m, kk, r), ve1 = vee_at(d, V, i, m + 1, kk, r);
-  const double He0 = Hvee_at(d, i, m, kk, r), He1 = Hvee_at(d, i, m + 1, kk, r);
+  const double ve0 = vee_at(a, i, m, r), ve1 = vee_at(a, i, m + 1, r);
+  const double He0 = Hvee_at(a, i, m, r), He1 = Hvee_at(a, i, m + 1, r);
   if (up) {
-    const double cff = FV(i, m) + FV(i, m + 1) - delta * (He0 + He1);
-    return 0.25 * (cff * (VV(i, m) + VV(i, m + 1)) - gamma * (fmax0(cff) * ve0 + fmin0(cff) * ve1));
+    const double cff = a.fv(i, m) + a.fv(i, m + 1) - delta * (He0 + He1);
+    return 0.25 * (cff * (a.v(i, m) + a.v(i, m + 1)) - gamma * (fmax0(cff) * ve0 + fmin0(cff) * ve1));
   }
-  return 0.25 * (VV(i, m) + VV(i, m + 1) - delta * (ve0 + ve1)) * (FV(i, m) + FV(i, m + 1) - delta * (He0 + He1));
+  return 0.25 * (a.v(i, m) + a.v(i, m + 1) - delta * (ve0 + ve1)) * (a.fv(i, m) + a.fv(i, m + 1) - delta * (He0 + He1));
 }
 // UFe at psi-point (i,m)
-__device__ __forceinline__ double adv_UFe(const Dev& d, const double* U, int i, int m, long kk, const UVBounds& r,
-                                          bool up) {
-  const Bounds& b = d.b;
-  const Fields& F = d.f;
+template <class A>
+__device__ __forceinline__ double adv_UFe(const A& a, int i, int m, const UVBounds& r, bool up) {
   const double delta = 0.1666666666666667, gamma = 0.3333333333333333;
-  const double Hv0 = FV(i - 1, m) - 2.0 * FV(i, m) + FV(i + 1, m);       // Hvxx(i,m)
-  const double Hvm = FV(i - 2, m) - 2.0 * FV(i - 1, m) + FV(i, m);       // Hvxx(i-1,m)
-  const double um1 = uee_at(d, U, i, m - 1, kk, r), u0 = uee_at(d, U, i, m, kk, r);
+  const double Hv0 = a.fv(i - 1, m) - 2.0 * a.fv(i, m) + a.fv(i + 1, m);       // Hvxx(i,m)
+  const double Hvm = a.fv(i - 2, m) - 2.0 * a.fv(i - 1, m) + a.fv(i, m);       // Hvxx(i-1,m)
+  const double um1 = uee_at(a, i, m - 1, r), u0 = uee_at(a, i, m, r);
   if (up) {
-    const double cff = FV(i, m) + FV(i - 1, m) - delta * (Hv0 + Hvm);
-    return 0.25 * (cff * (UU(i, m) + UU(i, m - 1)) - gamma * (fmax0(cff) * um1 + fmin0(cff) * u0));
+    const double cff = a.fv(i, m) + a.fv(i - 1, m) - delta * (Hv0 + Hvm);
+    return 0.25 * (cff * (a.u(i, m) + a.u(i, m - 1)) - gamma * (fmax0(cff) * um1 + fmin0(cff) * u0));
   }
-  return 0.25 * (UU(i, m) + UU(i, m - 1) - delta * (u0 + um1)) * (FV(i, m) + FV(i - 1, m) - delta * (Hv0 + Hvm));
+  return 0.25 * (a.u(i, m) + a.u(i, m - 1) - delta * (u0 + um1)) * (a.fv(i, m) + a.fv(i - 1, m) - delta * (Hv0 + Hvm));
 }
 // VFx at psi-point (m,j)
-__device__ __forceinline__ double adv_VFx(const Dev& d, const double* V, int m, int j, long kk, const UVBounds& r,
-                                          bool up) {
-  const Bounds& b = d.b;
-  const Fields& F = d.f;
+template <class A>
+__device__ __forceinline__ double adv_VFx(const A& a, int m, int j, const UVBounds& r, bool up) {
   const double delta = 0.1666666666666667, gamma = 0.3333333333333333;
-  const double Hu0 = FU(m, j - 1) - 2.0 * FU(m, j) + FU(m, j + 1);       // Huee(m,j)
-  const double Hum = FU(m, j - 2) - 2.0 * FU(m, j - 1) + FU(m, j);       // Huee(m,j-1)
-  const double vm1 = vxx_at(d, V, m - 1, j, kk, r), v0 = vxx_at(d, V, m, j, kk, r);
+  const double Hu0 = a.fu(m, j - 1) - 2.0 * a.fu(m, j) + a.fu(m, j + 1);       // Huee(m,j)
+  const double Hum = a.fu(m, j - 2) - 2.0 * a.fu(m, j - 1) + a.fu(m, j);       // Huee(m,j-1)
+  const double vm1 = vxx_at(a, m - 1, j, r), v0 = vxx_at(a, m, j, r);
   if (up) {
-    const double cff = FU(m, j) + FU(m, j - 1) - delta * (Hu0 + Hum);
-    return 0.25 * (cff * (VV(m, j) + VV(m - 1, j)) - gamma * (fmax0(cff) * vm1 + fmin0(cff) * v0));
+    const double cff = a.fu(m, j) + a.fu(m, j - 1) - delta * (Hu0 + Hum);
+    return 0.25 * (cff * (a.v(m, j) + a.v(m - 1, j)) - gamma * (fmax0(cff) * vm1 + fmin0(cff) * v0));
   }
-  return 0.25 * (VV(m, j) + VV(m - 1, j) - delta * (v0 + vm1)) * (FU(m, j) + FU(m, j - 1) - delta * (Hu0 + Hum));
+  return 0.25 * (a.v(m, j) + a.v(m - 1, j) - delta * (v0 + vm1)) * (a.fu(m, j) + a.fu(m, j - 1) - delta * (Hu0 + Hum));
 }
 
 // Full horizontal r.h.s. at (i,j,k): Coriolis first, then advection, with the
 // two accumulation steps into ru/rv kept in the reference's order.
-__device__ __forceinline__ void uv_horiz_rhs(const Dev& d, int i, int j, int k, int nrhs, const UVBounds& r,
+template <class A>
+__device__ __forceinline__ void uv_horiz_rhs(const Dev& d, const A& a, int i, int j, int k, const UVBounds& r,
                                              bool up) {
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const long kk = (long)(k - 1) * b.n2;
-  const double* U = F.u + (long)(nrhs - 1) * b.n3;
-  const double* V = F.v + (long)(nrhs - 1) * b.n3;
   const long o = IJ(b, i, j) + kk;
   if (i >= b.istrU && i <= b.iend && j >= b.jstr && j <= b.jend) {
     // Coriolis UFx at i and i-1: cff=0.5*Hz*fomn; UFx=cff*(v(j)+v(j+1))
     const double c0 = 0.5 * F.Hz[o] * (F.fomn[IJ(b, i, j)]);
     const double c1 = 0.5 * F.Hz[o - 1] * (F.fomn[IJ(b, i - 1, j)]);
-    const double U0 = c0 * (VV(i, j) + VV(i, j + 1)), U1 = c1 * (VV(i - 1, j) + VV(i - 1, j + 1));
+    const double U0 = c0 * (a.v(i, j) + a.v(i, j + 1)), U1 = c1 * (a.v(i - 1, j) + a.v(i - 1, j + 1));
     double ru = F.ru[o] + 0.5 * (U0 + U1);
-    ru = ru - adv_UFx(d, U, i, j, kk, r, up) + adv_UFx(d, U, i - 1, j, kk, r, up) - adv_UFe(d, U, i, j + 1, kk, r, up) +
-         adv_UFe(d, U, i, j, kk, r, up);
+    ru = ru - adv_UFx(a, i, j, r, up) + adv_UFx(a, i - 1, j, r, up) - adv_UFe(a, i, j + 1, r, up) +
+         adv_UFe(a, i, j, r, up);
     F.ru[o] = ru;
   }
   if (i >= b.istr && i <= b.iend && j >= b.jstrV && j <= b.jend) {
     const double c0 = 0.5 * F.Hz[o] * (F.fomn[IJ(b, i, j)]);
     const double c1 = 0.5 * F.Hz[o - b.nx2] * (F.fomn[IJ(b, i, j - 1)]);
-    const double V0 = c0 * (UU(i, j) + UU(i + 1, j)), V1 = c1 * (UU(i, j - 1) + UU(i + 1, j - 1));
+    const double V0 = c0 * (a.u(i, j) + a.u(i + 1, j)), V1 = c1 * (a.u(i, j - 1) + a.u(i + 1, j - 1));
     double rv = F.rv[o] - 0.5 * (V0 + V1);
-    rv = rv - adv_VFx(d, V, i + 1, j, kk, r, up) + adv_VFx(d, V, i, j, kk, r, up) - adv_VFe(d, V, i, j, kk, r, up) +
-         adv_VFe(d, V, i, j - 1, kk, r, up);
+    rv = rv - adv_VFx(a, i + 1, j, r, up) + adv_VFx(a, i, j, r, up) - adv_VFe(a, i, j, r, up) +
+         adv_VFe(a, i, j - 1, r, up);
     F.rv[o] = rv;
   }
 }
-#undef UU
-#undef VV
-#undef FU
-#undef FV
 
 // ---- vertical momentum advection by parabolic splines (SPLINE_UV) ----
 // dir=0: u at (i,j) (Hz/We averaged over i-1,i; stencil i-2..i+1, umask)

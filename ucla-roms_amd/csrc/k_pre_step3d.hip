@@ -117,10 +117,34 @@ __global__ void __launch_bounds__(64) k_pre_tracer_v(Dev d, Range R, PreCoef c, 
   }
 }
 
-// ---- horizontal momentum r.h.s. for all levels (pre_step3d / step3d_uv1) ----
+// ---- horizontal momentum r.h.s., one (i,j,k) cell per thread; u, v,
+// FlxU, FlxV of the block's 64x4 tile plus a 2-cell halo staged in LDS ----
 __global__ void __launch_bounds__(256) k_uv_horiz(Dev d, Range R, int nrhs, UVBounds ub, int up) {
-  ROMS_IJ_OR_RETURN(R)
-  uv_horiz_rhs(d, i, j, 1 + (int)blockIdx.z, nrhs, ub, up != 0);
+  __shared__ double sU[kUVN], sV[kUVN], sFU[kUVN], sFV[kUVN];
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const int k = 1 + (int)blockIdx.z;
+  const int i0 = R.i0 + (int)blockIdx.x * kBX, j0 = R.j0 + (int)blockIdx.y * kBY;
+  const int ib = i0 - 2, jb = j0 - 2;
+  const long kk = (long)(k - 1) * b.n2;
+  const double* U = F.u + (long)(nrhs - 1) * b.n3 + kk;
+  const double* V = F.v + (long)(nrhs - 1) * b.n3 + kk;
+  const double* FU = F.FlxU + kk;
+  const double* FV = F.FlxV + kk;
+  for (int q = threadIdx.x + kBX * threadIdx.y; q < kUVN; q += kBX * kBY) {
+    const int i = ib + q % kUVW, j = jb + q / kUVW;
+    if (i < -1 || i > b.Lm + 2 || j < -1 || j > b.Mm + 2) continue;  // never read
+    const long o = IJ(b, i, j);
+    sU[q] = U[o];
+    sV[q] = V[o];
+    sFU[q] = FU[o];
+    sFV[q] = FV[o];
+  }
+  __syncthreads();
+  const int i = i0 + (int)threadIdx.x, j = j0 + (int)threadIdx.y;
+  if (i > R.i1 || j > R.j1) return;
+  const AccL a{sU, sV, sFU, sFV, ib, jb};
+  uv_horiz_rhs(d, a, i, j, k, ub, up != 0);
 }
 
 void launch_uv_horiz(const Dev& d, hipStream_t s, int nrhs, int up) {
