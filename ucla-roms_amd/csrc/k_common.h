@@ -13,6 +13,9 @@
 
 namespace roms {
 
+// LDS window of a 64x4 tile with a 2-cell halo on every side (i0-2.., j0-2..)
+constexpr int kUVW = kBX + 4, kUVH = kBY + 4, kUVN = kUVW * kUVH;
+
 // A lane's column scratch (levels 0..N) in LDS: level k of lane l at
 // smem[k*kCX + l], so a wavefront touches 64 consecutive doubles per level
 // (conflict-free).  Sweeps that keep their forward-elimination results here
@@ -41,50 +44,73 @@ __device__ __forceinline__ void hz_bak_fwd(const Dev& d, int i, int j, int k, do
 }
 
 // ---- horizontal tracer fluxes at one face ----
-// FX at u-point m (row j, level k): elementary differences FXel(q) for
-// q=m-1..m+1, clamped at closed edges (FX(istr-1)=FX(istr), FX(iend+2)=FX(iend+1)).
-__device__ __forceinline__ double tracer_fx(const Dev& d, const double* __restrict__ T, int m, int j, int k,
-                                            bool upstream) {
-  const Bounds& b = d.b;
-  const Fields& F = d.f;
-  const long row = (long)(j + 1) * b.nx2 + (long)(k - 1) * b.n2;
+// Written over an accessor (t, umask, vmask, FlxU, FlxV at one level); the
+// kernels stage the block's window in LDS (AccTL).  FX at u-point m (row j):
+// elementary differences FXel(q) for q=m-1..m+1, clamped at closed edges
+// (FX(istr-1)=FX(istr), FX(iend+2)=FX(iend+1)).
+struct AccTL {
+  const double *T, *UM, *VM, *FU, *FV;  // LDS windows, row-major kUVW, origin (ib, jb)
+  int ib, jb;
+  __device__ __forceinline__ int at(int i, int j) const { return (i - ib) + (j - jb) * kUVW; }
+  __device__ __forceinline__ double t(int i, int j) const { return T[at(i, j)]; }
+  __device__ __forceinline__ double um(int i, int j) const { return UM[at(i, j)]; }
+  __device__ __forceinline__ double vm(int i, int j) const { return VM[at(i, j)]; }
+  __device__ __forceinline__ double fu(int i, int j) const { return FU[at(i, j)]; }
+  __device__ __forceinline__ double fv(int i, int j) const { return FV[at(i, j)]; }
+};
+template <class A>
+__device__ __forceinline__ double tracer_fx(const Bounds& b, const A& a, int m, int j, bool upstream) {
   const int lo = b.west_edge ? b.istr : -1000000, hi = b.east_edge ? b.iend + 1 : 1000000;
   double el[3];
   for (int q = 0; q < 3; q++) {
     const int p = iclamp(m - 1 + q, lo, hi);
-    const long o = row + p + 1;
-    el[q] = (T[o] - T[o - 1]) * F.umask[IJ(b, p, j)];
+    el[q] = (a.t(p, j) - a.t(p - 1, j)) * a.um(p, j);
   }
-  const long o = row + m + 1;
-  const double Fl = F.FlxU[o];
+  const double Fl = a.fu(m, j);
   if (upstream) {
     const double cm = el[1] - el[0], c0 = el[2] - el[1];   // curv(m-1), curv(m)
-    return 0.5 * (T[o] + T[o - 1]) * Fl - 0.1666666666666666 * (cm * fmax0(Fl) + c0 * fmin0(Fl));
+    return 0.5 * (a.t(m, j) + a.t(m - 1, j)) * Fl - 0.1666666666666666 * (cm * fmax0(Fl) + c0 * fmin0(Fl));
   }
   const double gm = 0.5 * (el[1] + el[0]), g0 = 0.5 * (el[2] + el[1]);  // grad(m-1), grad(m)
-  return 0.5 * (T[o] + T[o - 1] - 0.3333333333333333 * (g0 - gm)) * Fl;
+  return 0.5 * (a.t(m, j) + a.t(m - 1, j) - 0.3333333333333333 * (g0 - gm)) * Fl;
 }
-__device__ __forceinline__ double tracer_fe(const Dev& d, const double* __restrict__ T, int i, int m, int k,
-                                            bool upstream) {
-  const Bounds& b = d.b;
-  const Fields& F = d.f;
-  const long sj = b.nx2;
-  const long col = (long)(i + 1) + (long)(k - 1) * b.n2;
+template <class A>
+__device__ __forceinline__ double tracer_fe(const Bounds& b, const A& a, int i, int m, bool upstream) {
   const int lo = b.south_edge ? b.jstr : -1000000, hi = b.north_edge ? b.jend + 1 : 1000000;
   double el[3];
   for (int q = 0; q < 3; q++) {
     const int p = iclamp(m - 1 + q, lo, hi);
-    const long o = col + (long)(p + 1) * sj;
-    el[q] = (T[o] - T[o - sj]) * F.vmask[IJ(b, i, p)];
+    el[q] = (a.t(i, p) - a.t(i, p - 1)) * a.vm(i, p);
   }
-  const long o = col + (long)(m + 1) * sj;
-  const double Fl = F.FlxV[o];
+  const double Fl = a.fv(i, m);
   if (upstream) {
     const double cm = el[1] - el[0], c0 = el[2] - el[1];
-    return 0.5 * (T[o] + T[o - sj]) * Fl - 0.1666666666666666 * (cm * fmax0(Fl) + c0 * fmin0(Fl));
+    return 0.5 * (a.t(i, m) + a.t(i, m - 1)) * Fl - 0.1666666666666666 * (cm * fmax0(Fl) + c0 * fmin0(Fl));
   }
   const double gm = 0.5 * (el[1] + el[0]), g0 = 0.5 * (el[2] + el[1]);
-  return 0.5 * (T[o] + T[o - sj] - 0.3333333333333333 * (g0 - gm)) * Fl;
+  return 0.5 * (a.t(i, m) + a.t(i, m - 1) - 0.3333333333333333 * (g0 - gm)) * Fl;
+}
+
+// Stage the (kUVW x kUVH) window around a block's 64x4 tile: the level-k
+// fluxes and the masks (once), then per tracer the tracer field.
+struct TracerWin {
+  double T[kUVN], UM[kUVN], VM[kUVN], FU[kUVN], FV[kUVN];
+};
+__device__ __forceinline__ void tracer_win_fill(const Bounds& b, const Fields& F, TracerWin& W, int ib, int jb,
+                                                long kk, const double* T) {
+  for (int q = threadIdx.x + kBX * threadIdx.y; q < kUVN; q += kBX * kBY) {
+    const int i = ib + q % kUVW, j = jb + q / kUVW;
+    if (i < -1 || i > b.Lm + 2 || j < -1 || j > b.Mm + 2) continue;  // never read
+    const long o = IJ(b, i, j);
+    if (T) {
+      W.T[q] = T[o + kk];
+    } else {
+      W.UM[q] = F.umask[o];
+      W.VM[q] = F.vmask[o];
+      W.FU[q] = F.FlxU[o + kk];
+      W.FV[q] = F.FlxV[o + kk];
+    }
+  }
 }
 
 // ---- parabolic-spline vertical tracer fluxes, written as FC(0:N) into the
@@ -155,7 +181,6 @@ struct AccG {
   __device__ __forceinline__ double fu(int i, int j) const { return FU[at(i, j)]; }
   __device__ __forceinline__ double fv(int i, int j) const { return FV[at(i, j)]; }
 };
-constexpr int kUVW = kBX + 4, kUVH = kBY + 4, kUVN = kUVW * kUVH;  // LDS window (i0-2.., j0-2..)
 struct AccL {
   const double *U, *V, *FU, *FV;   // LDS windows, row-major kUVW
   int ib, jb;                      // global (i,j) of window element 0

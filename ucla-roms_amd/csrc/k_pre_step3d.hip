@@ -14,25 +14,39 @@ struct PreCoef {
 // t(nnew) = Hz_bak*(cf_stp*t(nstp)+cf_bak*t(indx)) - dtau*pm*pn*div(FX,FE),
 // t(indx) = Hz*t(nstp). ----
 __global__ void __launch_bounds__(256) k_pre_tracer_h(Dev d, Range R, PreCoef c, int nstp, int nnew, int nrhs) {
-  ROMS_IJ_OR_RETURN(R)
+  __shared__ TracerWin W;
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const int k = 1 + (int)blockIdx.z, indx = 3 - nstp;
-  const long ij = IJ(b, i, j), o = ij + (long)(k - 1) * b.n2;
-  double hb, hf;
-  hz_bak_fwd(d, i, j, k, 0.5 * c.dtau, hb, hf);
-  F.c2[o] = hf;  // Hz_fwd, Hz_bak kept for the column solves (range istr-1.., jstr-1..)
-  F.c3[o] = hb;
-  if (i < b.istr || j < b.jstr) return;
-  const double hz = F.Hz[o];
+  const int i0 = R.i0 + (int)blockIdx.x * kBX, j0 = R.j0 + (int)blockIdx.y * kBY;
+  const int ib = i0 - 2, jb = j0 - 2;
+  const long kk = (long)(k - 1) * b.n2;
+  tracer_win_fill(b, F, W, ib, jb, kk, nullptr);
+  const int i = i0 + (int)threadIdx.x, j = j0 + (int)threadIdx.y;
+  const bool act = i <= R.i1 && j <= R.j1;
+  const long ij = IJ(b, i, j), o = ij + kk;
+  double hb = 0.0;
+  if (act) {
+    double hf;
+    hz_bak_fwd(d, i, j, k, 0.5 * c.dtau, hb, hf);
+    F.c2[o] = hf;  // Hz_fwd, Hz_bak kept for the column solves (range istr-1.., jstr-1..)
+    F.c3[o] = hb;
+  }
+  const bool in = act && i >= b.istr && j >= b.jstr;
+  const double hz = in ? F.Hz[o] : 0.0;
+  const AccTL a{W.T, W.UM, W.VM, W.FU, W.FV, ib, jb};
   for (int itrc = 1; itrc <= b.NT; itrc++) {
     const long tb = (long)(itrc - 1) * 3 * b.n3;
     const double* Tr = F.t + (long)(nrhs - 1) * b.n3 + tb;
+    __syncthreads();  // previous tracer's window fully consumed
+    tracer_win_fill(b, F, W, ib, jb, kk, Tr);
+    __syncthreads();
+    if (!in) continue;
     double* Tn = F.t + (long)(nnew - 1) * b.n3 + tb;
     double* Ti = F.t + (long)(indx - 1) * b.n3 + tb;
     const double* Ts = F.t + (long)(nstp - 1) * b.n3 + tb;
-    const double FX0 = tracer_fx(d, Tr, i, j, k, false), FX1 = tracer_fx(d, Tr, i + 1, j, k, false);
-    const double FE0 = tracer_fe(d, Tr, i, j, k, false), FE1 = tracer_fe(d, Tr, i, j + 1, k, false);
+    const double FX0 = tracer_fx(b, a, i, j, false), FX1 = tracer_fx(b, a, i + 1, j, false);
+    const double FE0 = tracer_fe(b, a, i, j, false), FE1 = tracer_fe(b, a, i, j + 1, false);
     const double tsk = Ts[o];
     Tn[o] = hb * (c.cf_stp * tsk + c.cf_bak * Ti[o]) - c.dtau * F.pm[ij] * F.pn[ij] * (FX1 - FX0 + FE1 - FE0);
     Ti[o] = hz * tsk;

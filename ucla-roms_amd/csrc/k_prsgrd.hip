@@ -88,82 +88,107 @@ __global__ void __launch_bounds__(256) k_prsgrd_P(Dev d, Range R, int split) {
   }
 }
 
+// ---- per cell (i,j,k): XI and ETA components ru, rv.  The block evaluates
+// the clamped elementary differences FC, rx at the u-points (v-points) of its
+// tile row (column) plus one on each side, then their harmonic averages
+// dZ, dR (with the SPLIT_EOS compressibility term), once each, in LDS. ----
+constexpr int kPXW = kBX + 2, kPXN = kPXW * kBY;          // u-points m = i0-1 .. i0+64, tile rows
+constexpr int kPYH = kBY + 2, kPYN = kBX * kPYH;          // v-points m = j0-1 .. j0+4, tile columns
 __global__ void __launch_bounds__(256) k_prsgrd_uv(Dev d, Range R, int split, int imin, int imax, int jmin, int jmax) {
-  ROMS_IJ_OR_RETURN(R)
+  __shared__ double sFCx[kPXN], sRx[kPXN], sFCy[kPYN], sRy[kPYN];
+  __shared__ double sdZx[kPXN], sdRx[kPXN], sdZy[kPYN], sdRy[kPYN];
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const double g = d.p.g, rho0 = d.p.rho0, qp2 = d.p.qp2;
   const double OneFifth = 0.2, OneTwelfth = 1.0 / 12.0;
   const double HalfGRho = 0.5 * (g / rho0);
   const double* rho = split ? F.rhos : F.rho;
-  const bool du = i >= b.istrU && i <= b.iend && j >= b.jstr && j <= b.jend;
-  const bool dv = i >= b.istr && i <= b.iend && j >= b.jstrV && j <= b.jend;
-  const long ij = IJ(b, i, j);
-  {
-    const int k = 1 + (int)blockIdx.z;
-    const long kk = (long)(k - 1) * b.n2;
-    if (du) {
-      // FC(m), rx(m) at u-points m=i-1,i,i+1 (clamped = edge extrapolation)
-      double FC[3], rx[3];
-      for (int q = 0; q < 3; q++) {
-        const int m = iclamp(i - 1 + q, imin, imax);
-        const long om = IJ(b, m, j) + kk;
-        const double um = F.umask[IJ(b, m, j)];
-        FC[q] = (F.z_r[om] - F.z_r[om - 1]) * um;
-        if (split) {
-          const double dpth = -0.5 * (F.z_r[om] + F.z_r[om - 1]);
-          rx[q] = (F.rho1[om] - F.rho1[om - 1] + (F.qp1[om] - F.qp1[om - 1]) * dpth * (1.0 - qp2 * dpth)) * um;
-        } else {
-          rx[q] = (F.rho[om] - F.rho[om - 1]) * um;
-        }
+  const int k = 1 + (int)blockIdx.z;
+  const long kk = (long)(k - 1) * b.n2, sj = b.nx2;
+  const int i0 = R.i0 + (int)blockIdx.x * kBX, j0 = R.j0 + (int)blockIdx.y * kBY;
+  const int tid = threadIdx.x + kBX * threadIdx.y;
+  // elementary differences at clamped u-points (xi) and v-points (eta)
+  for (int q = tid; q < kPXN + kPYN; q += kBX * kBY) {
+    if (q < kPXN) {
+      const int j = j0 + q / kPXW;
+      int m = i0 - 1 + q % kPXW;
+      if (j > b.Mm + 1 || m > b.Lm + 2) { sFCx[q] = sRx[q] = 0.0; continue; }
+      m = iclamp(m, imin, imax);
+      const long om = IJ(b, m, j) + kk;
+      const double um = F.umask[IJ(b, m, j)];
+      sFCx[q] = (F.z_r[om] - F.z_r[om - 1]) * um;
+      if (split) {
+        const double dpth = -0.5 * (F.z_r[om] + F.z_r[om - 1]);
+        sRx[q] = (F.rho1[om] - F.rho1[om - 1] + (F.qp1[om] - F.qp1[om - 1]) * dpth * (1.0 - qp2 * dpth)) * um;
+      } else {
+        sRx[q] = (F.rho[om] - F.rho[om - 1]) * um;
       }
-      double dZx[2], dRx[2];  // at i-1, i
-      for (int q = 0; q < 2; q++) {
-        dZx[q] = harm(FC[q], FC[q + 1]);
-        dRx[q] = harm(rx[q], rx[q + 1]);
-        if (split) {
-          const long om = ij - 1 + q + kk;
-          dRx[q] = dRx[q] - F.qp1[om] * dZx[q] * (1.0 + 2.0 * qp2 * F.z_r[om]);
-        }
+    } else {
+      const int qq = q - kPXN;
+      const int i = i0 + qq % kBX;
+      int m = j0 - 1 + qq / kBX;
+      if (i > b.Lm + 1 || m > b.Mm + 2) { sFCy[qq] = sRy[qq] = 0.0; continue; }
+      m = iclamp(m, jmin, jmax);
+      const long om = IJ(b, i, m) + kk;
+      const double vm = F.vmask[IJ(b, i, m)];
+      sFCy[qq] = (F.z_r[om] - F.z_r[om - sj]) * vm;
+      if (split) {
+        const double dpth = -0.5 * (F.z_r[om] + F.z_r[om - sj]);
+        sRy[qq] = (F.rho1[om] - F.rho1[om - sj] + (F.qp1[om] - F.qp1[om - sj]) * dpth * (1.0 - qp2 * dpth)) * vm;
+      } else {
+        sRy[qq] = (F.rho[om] - F.rho[om - sj]) * vm;
       }
-      const long o = ij + kk;
-      F.ru[o] = 0.5 * (F.Hz[o] + F.Hz[o - 1]) * F.dn_u[ij] *
-                (F.P[o - 1] - F.P[o] -
-                 HalfGRho * ((rho[o] + rho[o - 1]) * (F.z_r[o] - F.z_r[o - 1]) -
-                             OneFifth * ((dRx[1] - dRx[0]) * (F.z_r[o] - F.z_r[o - 1] - OneTwelfth * (dZx[1] + dZx[0])) -
-                                         (dZx[1] - dZx[0]) * (rho[o] - rho[o - 1] - OneTwelfth * (dRx[1] + dRx[0])))));
     }
-    if (dv) {
-      const long sj = b.nx2;
-      double FC[3], rx[3];
-      for (int q = 0; q < 3; q++) {
-        const int m = iclamp(j - 1 + q, jmin, jmax);
-        const long om = IJ(b, i, m) + kk;
-        const double vm = F.vmask[IJ(b, i, m)];
-        FC[q] = (F.z_r[om] - F.z_r[om - sj]) * vm;
-        if (split) {
-          const double dpth = -0.5 * (F.z_r[om] + F.z_r[om - sj]);
-          rx[q] = (F.rho1[om] - F.rho1[om - sj] + (F.qp1[om] - F.qp1[om - sj]) * dpth * (1.0 - qp2 * dpth)) * vm;
-        } else {
-          rx[q] = (F.rho[om] - F.rho[om - sj]) * vm;
-        }
+  }
+  __syncthreads();
+  // harmonic averages at rho points p = i-1, i (xi) and j-1, j (eta)
+  for (int q = tid; q < kPXN + kPYN; q += kBX * kBY) {
+    if (q < kPXN) {
+      const int li = q % kPXW;
+      if (li == kPXW - 1) continue;
+      const int j = j0 + q / kPXW, p = i0 - 1 + li;
+      double dz = harm(sFCx[q], sFCx[q + 1]), dr = harm(sRx[q], sRx[q + 1]);
+      if (split && j <= b.Mm + 1 && p <= b.Lm + 1) {
+        const long om = IJ(b, p, j) + kk;
+        dr = dr - F.qp1[om] * dz * (1.0 + 2.0 * qp2 * F.z_r[om]);
       }
-      double dZx[2], dRx[2];
-      for (int q = 0; q < 2; q++) {
-        dZx[q] = harm(FC[q], FC[q + 1]);
-        dRx[q] = harm(rx[q], rx[q + 1]);
-        if (split) {
-          const long om = ij + (long)(q - 1) * sj + kk;
-          dRx[q] = dRx[q] - F.qp1[om] * dZx[q] * (1.0 + 2.0 * qp2 * F.z_r[om]);
-        }
+      sdZx[q] = dz;
+      sdRx[q] = dr;
+    } else {
+      const int qq = q - kPXN;
+      const int lj = qq / kBX;
+      if (lj == kPYH - 1) continue;
+      const int i = i0 + qq % kBX, p = j0 - 1 + lj;
+      double dz = harm(sFCy[qq], sFCy[qq + kBX]), dr = harm(sRy[qq], sRy[qq + kBX]);
+      if (split && i <= b.Lm + 1 && p <= b.Mm + 1) {
+        const long om = IJ(b, i, p) + kk;
+        dr = dr - F.qp1[om] * dz * (1.0 + 2.0 * qp2 * F.z_r[om]);
       }
-      const long o = ij + kk;
-      F.rv[o] = 0.5 * (F.Hz[o] + F.Hz[o - sj]) * F.dm_v[ij] *
-                (F.P[o - sj] - F.P[o] -
-                 HalfGRho * ((rho[o] + rho[o - sj]) * (F.z_r[o] - F.z_r[o - sj]) -
-                             OneFifth * ((dRx[1] - dRx[0]) * (F.z_r[o] - F.z_r[o - sj] - OneTwelfth * (dZx[1] + dZx[0])) -
-                                         (dZx[1] - dZx[0]) * (rho[o] - rho[o - sj] - OneTwelfth * (dRx[1] + dRx[0])))));
+      sdZy[qq] = dz;
+      sdRy[qq] = dr;
     }
+  }
+  __syncthreads();
+  const int i = i0 + (int)threadIdx.x, j = j0 + (int)threadIdx.y;
+  if (i > R.i1 || j > R.j1) return;
+  const long ij = IJ(b, i, j), o = ij + kk;
+  if (i >= b.istrU && i <= b.iend && j >= b.jstr && j <= b.jend) {
+    const int q = threadIdx.x + threadIdx.y * kPXW;   // p = i-1 ; q+1: p = i
+    const double dZ0 = sdZx[q], dZ1 = sdZx[q + 1], dR0 = sdRx[q], dR1 = sdRx[q + 1];
+    F.ru[o] = 0.5 * (F.Hz[o] + F.Hz[o - 1]) * F.dn_u[ij] *
+              (F.P[o - 1] - F.P[o] -
+               HalfGRho * ((rho[o] + rho[o - 1]) * (F.z_r[o] - F.z_r[o - 1]) -
+                           OneFifth * ((dR1 - dR0) * (F.z_r[o] - F.z_r[o - 1] - OneTwelfth * (dZ1 + dZ0)) -
+                                       (dZ1 - dZ0) * (rho[o] - rho[o - 1] - OneTwelfth * (dR1 + dR0)))));
+  }
+  if (i >= b.istr && i <= b.iend && j >= b.jstrV && j <= b.jend) {
+    const int q = threadIdx.x + threadIdx.y * kBX;    // p = j-1 ; q+kBX: p = j
+    const double dZ0 = sdZy[q], dZ1 = sdZy[q + kBX], dR0 = sdRy[q], dR1 = sdRy[q + kBX];
+    F.rv[o] = 0.5 * (F.Hz[o] + F.Hz[o - sj]) * F.dm_v[ij] *
+              (F.P[o - sj] - F.P[o] -
+               HalfGRho * ((rho[o] + rho[o - sj]) * (F.z_r[o] - F.z_r[o - sj]) -
+                           OneFifth * ((dR1 - dR0) * (F.z_r[o] - F.z_r[o - sj] - OneTwelfth * (dZ1 + dZ0)) -
+                                       (dZ1 - dZ0) * (rho[o] - rho[o - sj] - OneTwelfth * (dR1 + dR0)))));
   }
 }
 

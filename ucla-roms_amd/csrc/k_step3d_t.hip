@@ -8,16 +8,28 @@ namespace roms {
 
 // Horizontal advection, one thread per (i,j,k) cell, all tracers.
 __global__ void __launch_bounds__(256) k_step3d_t_h(Dev d, Range R, int nnew, int nrhs) {
-  ROMS_IJ_OR_RETURN(R)
+  __shared__ TracerWin W;
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const int k = 1 + (int)blockIdx.z;
-  const long ij = IJ(b, i, j), o = ij + (long)(k - 1) * b.n2;
+  const int i0 = R.i0 + (int)blockIdx.x * kBX, j0 = R.j0 + (int)blockIdx.y * kBY;
+  const int ib = i0 - 2, jb = j0 - 2;
+  const long kk = (long)(k - 1) * b.n2;
+  tracer_win_fill(b, F, W, ib, jb, kk, nullptr);
+  const int i = i0 + (int)threadIdx.x, j = j0 + (int)threadIdx.y;
+  const bool act = i <= R.i1 && j <= R.j1;
+  const long ij = IJ(b, i, j), o = ij + kk;
+  const AccTL a{W.T, W.UM, W.VM, W.FU, W.FV, ib, jb};
   for (int itrc = 1; itrc <= b.NT; itrc++) {
-    const double* Tr = F.t + (long)(nrhs - 1) * b.n3 + (long)(itrc - 1) * 3 * b.n3;
-    double* Tn = F.t + (long)(nnew - 1) * b.n3 + (long)(itrc - 1) * 3 * b.n3;
-    const double FX0 = tracer_fx(d, Tr, i, j, k, true), FX1 = tracer_fx(d, Tr, i + 1, j, k, true);
-    const double FE0 = tracer_fe(d, Tr, i, j, k, true), FE1 = tracer_fe(d, Tr, i, j + 1, k, true);
+    const long tb = (long)(itrc - 1) * 3 * b.n3;
+    const double* Tr = F.t + (long)(nrhs - 1) * b.n3 + tb;
+    __syncthreads();
+    tracer_win_fill(b, F, W, ib, jb, kk, Tr);
+    __syncthreads();
+    if (!act) continue;
+    double* Tn = F.t + (long)(nnew - 1) * b.n3 + tb;
+    const double FX0 = tracer_fx(b, a, i, j, true), FX1 = tracer_fx(b, a, i + 1, j, true);
+    const double FE0 = tracer_fe(b, a, i, j, true), FE1 = tracer_fe(b, a, i, j + 1, true);
     Tn[o] = Tn[o] - d.p.dt * F.pm[ij] * F.pn[ij] * (FX1 - FX0 + FE1 - FE0);
   }
 }

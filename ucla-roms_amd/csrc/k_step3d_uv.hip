@@ -129,34 +129,45 @@ __device__ __forceinline__ void visc_psi(const Dev& d, int i, int j, int k, int 
 }
 
 // per cell (i,j,k): stress divergence cff added as dt*cff to u,v(indx); cff
-// kept in column scratch (c0: u, c1: v) for the vertical sums below
+// kept in column scratch (c0: u, c1: v) for the vertical sums below.  The
+// block first evaluates each rho-point (UFx,VFe) and psi-point (UFe,VFx)
+// stress of its 64x4 tile once into LDS (rho points with a low-side, psi
+// points with a high-side halo), then forms the divergences.
+constexpr int kVW = kBX + 1, kVN = kVW * (kBY + 1);
 __global__ void __launch_bounds__(256) k_visc3d(Dev d, Range R, int nstp) {
-  ROMS_IJ_OR_RETURN(R)
+  __shared__ double sUFx[kVN], sVFe[kVN], sUFe[kVN], sVFx[kVN];
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const int indx = 3 - nstp;
   const int k = 1 + (int)blockIdx.z;
+  const int i0 = R.i0 + (int)blockIdx.x * kBX, j0 = R.j0 + (int)blockIdx.y * kBY;
+  for (int q = threadIdx.x + kBX * threadIdx.y; q < kVN; q += kBX * kBY) {
+    const int li = q % kVW, lj = q / kVW;
+    const int ir = i0 - 1 + li, jr = j0 - 1 + lj;  // rho point
+    double ufx = 0.0, vfe = 0.0, ufe = 0.0, vfx = 0.0;
+    if (ir >= 0 && ir <= b.Lm + 1 && jr >= 0 && jr <= b.Mm + 1) visc_rho(d, ir, jr, k, nstp, ufx, vfe);
+    const int ip = i0 + li, jp = j0 + lj;          // psi point
+    if (ip >= 0 && ip <= b.Lm + 2 && jp >= 0 && jp <= b.Mm + 2) visc_psi(d, ip, jp, k, nstp, ufe, vfx);
+    sUFx[q] = ufx; sVFe[q] = vfe; sUFe[q] = ufe; sVFx[q] = vfx;
+  }
+  __syncthreads();
+  const int i = i0 + (int)threadIdx.x, j = j0 + (int)threadIdx.y;
+  if (i > R.i1 || j > R.j1) return;
+  const int qr = (threadIdx.x + 1) + (threadIdx.y + 1) * kVW;  // rho (i,j); -1: (i-1,j); -kVW: (i,j-1)
+  const int qp = threadIdx.x + threadIdx.y * kVW;              // psi (i,j); +1: (i+1,j); +kVW: (i,j+1)
   const long ij = IJ(b, i, j), sj = b.nx2;
   const double* pm = F.pm;
   const double* pn = F.pn;
   const long o = ij + (long)(k - 1) * b.n2;
   if (i >= b.istrU && i <= b.iend) {
-    double UFx0, UFx1, VFe_, UFe0, UFe1, VFx_;
-    visc_rho(d, i, j, k, nstp, UFx0, VFe_);
-    visc_rho(d, i - 1, j, k, nstp, UFx1, VFe_);
-    visc_psi(d, i, j, k, nstp, UFe0, VFx_);
-    visc_psi(d, i, j + 1, k, nstp, UFe1, VFx_);
+    const double UFx0 = sUFx[qr], UFx1 = sUFx[qr - 1], UFe0 = sUFe[qp], UFe1 = sUFe[qp + kVW];
     const double cff = 0.125 * (pm[ij - 1] + pm[ij]) * (pn[ij - 1] + pn[ij]) *
                        ((pn[ij - 1] + pn[ij]) * (UFx0 - UFx1) + (pm[ij - 1] + pm[ij]) * (UFe1 - UFe0));
     F.c0[o] = cff;
     F.u[o + (long)(indx - 1) * b.n3] = F.u[o + (long)(indx - 1) * b.n3] + d.p.dt * cff;
   }
   if (j >= b.jstrV && j <= b.jend) {
-    double VFe0, VFe1, UFx_, VFx0, VFx1, UFe_;
-    visc_rho(d, i, j, k, nstp, UFx_, VFe0);
-    visc_rho(d, i, j - 1, k, nstp, UFx_, VFe1);
-    visc_psi(d, i, j, k, nstp, UFe_, VFx0);
-    visc_psi(d, i + 1, j, k, nstp, UFe_, VFx1);
+    const double VFe0 = sVFe[qr], VFe1 = sVFe[qr - kVW], VFx0 = sVFx[qp], VFx1 = sVFx[qp + 1];
     const double cff = 0.125 * (pm[ij] + pm[ij - sj]) * (pn[ij] + pn[ij - sj]) *
                        ((pn[ij - sj] + pn[ij]) * (VFx1 - VFx0) + (pm[ij - sj] + pm[ij]) * (VFe0 - VFe1));
     F.c1[o] = cff;
