@@ -43,6 +43,73 @@ __device__ __forceinline__ void hz_bak_fwd(const Dev& d, int i, int j, int k, do
   fwd = F.Hz[o] - FlxDiv;
 }
 
+// ---- SPLINE_TS vertical advective flux of one tracer column in LDS
+// (compute_vert_tracer_fluxes.h): FC(0:N) by the spline elimination, then
+// A[k] = FC(k)*We(k), A[0] = A[N] = 0.  Per-level inputs come through a
+// register ring kPF levels ahead of use (whole unrolled groups, then a
+// direct remainder), so the loads overlap the division chain.
+constexpr int kPF = 8;
+__device__ __forceinline__ void tracer_spline_lds(int N, long n2, const double* __restrict__ Hz,
+                                                  const double* __restrict__ Tr, const double* __restrict__ We,
+                                                  const ColLds& A, const ColLds& B) {
+    double cfk = 1.0, fcm = 2.0 * Tr[0], hk = Hz[0], tk = Tr[0];
+    A[0] = fcm;
+    // inputs of the next kPF levels stay in flight in a register ring (slot q
+    // of an unrolled group of kPF levels holds level k0+q+kPF after use);
+    // whole groups first, the remaining < kPF levels load directly
+    auto spl_fwd = [&](int k, double hk1, double tk1) {
+      const double cff = 1.0 / (2.0 * hk + hk1 * (2.0 - cfk));
+      const double cf1 = cff * hk;
+      const double fck = cff * (3.0 * (hk * tk1 + hk1 * tk) - hk1 * fcm);
+      B[k + 1] = cf1;
+      A[k] = fck;
+      cfk = cf1; fcm = fck; hk = hk1; tk = tk1;
+    };
+    int k0 = 1;
+    {
+      double rh[kPF], rt[kPF];
+#pragma unroll
+      for (int q = 0; q < kPF; q++) {
+        const long L = (long)min(1 + q, N - 1) * n2;
+        rh[q] = Hz[L]; rt[q] = Tr[L];
+      }
+      for (; k0 + kPF - 1 <= N - 1; k0 += kPF) {
+#pragma unroll
+        for (int q = 0; q < kPF; q++) {
+          const double hk1 = rh[q], tk1 = rt[q];
+          const long L = (long)min(k0 + q + kPF, N - 1) * n2;
+          rh[q] = Hz[L]; rt[q] = Tr[L];
+          spl_fwd(k0 + q, hk1, tk1);
+        }
+      }
+    }
+    for (int k = k0; k <= N - 1; k++) spl_fwd(k, Hz[(long)k * n2], Tr[(long)k * n2]);
+    double fc1 = (2.0 * tk - fcm) / (1.0 - cfk);
+    {
+      auto spl_bwd = [&](int k, double we) {
+        const double fck = A[k] - B[k + 1] * fc1;
+        A[k + 1] = fc1 * we;
+        A[k] = fck;
+        fc1 = fck;
+      };
+      int k1 = N - 1;
+      double rw[kPF];
+#pragma unroll
+      for (int q = 0; q < kPF; q++) rw[q] = We[(long)max(N - q, 1) * n2];
+      for (; k1 - kPF + 1 >= 0; k1 -= kPF) {
+#pragma unroll
+        for (int q = 0; q < kPF; q++) {
+          const double we = rw[q];
+          rw[q] = We[(long)max(k1 - q + 1 - kPF, 1) * n2];
+          spl_bwd(k1 - q, we);
+        }
+      }
+      for (int k = k1; k >= 0; k--) spl_bwd(k, We[(long)(k + 1) * n2]);
+    }
+  A[N] = 0.0;
+  A[0] = 0.0;
+}
+
 // ---- horizontal tracer fluxes at one face ----
 // Written over an accessor (t, umask, vmask, FlxU, FlxV at one level); the
 // kernels stage the block's window in LDS (AccTL).  FX at u-point m (row j):
@@ -353,6 +420,7 @@ __device__ __forceinline__ void uv_vert_rhs(const Dev& d, int i, int j, int nrhs
 // of u (dir 0) / v (dir 1) at w-levels in A[k], k=0..N, A[0]=A[N]=0
 // (compute_vert_rhs_uv_terms.h); the r.h.s. update is rr(k) = rr(k) - A[k] +
 // A[k-1] in that order (uv_rr_update).
+template <bool kRing>
 __device__ __forceinline__ void uv_vert_flux_lds(const Dev& d, long ij, int nrhs, int dir, const ColLds& A,
                                                  const ColLds& B) {
   const Bounds& b = d.b;
@@ -364,31 +432,76 @@ __device__ __forceinline__ void uv_vert_flux_lds(const Dev& d, long ij, int nrhs
   const double* __restrict__ Hz = F.Hz + ij;
   const double* __restrict__ We = F.We + ij;
   const double* mask = dir == 0 ? F.umask : F.vmask;
+  // DC(k) from the four Hz columns of rho level k (kept for the remainder loops)
   auto DCk = [&](int k) {
     const long o = (long)(k - 1) * n2;
     return 0.5625 * (Hz[o] + Hz[o - s]) - 0.0625 * (Hz[o + s] + Hz[o - 2 * s]);
   };
-  double dck = DCk(1), cfk = 1.0, fcm = 2.0 * Uv[0];
-#pragma unroll 4
-  for (int k = 1; k <= N - 1; k++) {
-    const double dc1 = DCk(k + 1);
+  double dck = DCk(1), cfk = 1.0, fcm = 2.0 * Uv[0], uk = Uv[0];
+  auto fwd = [&](int k, double dc1, double uk1) {   // level k -> k+1
     const double cff = 1.0 / (2.0 * dck + dc1 * (2.0 - cfk));
     const double cf1 = cff * dck;
-    const long o = (long)(k - 1) * n2;
-    const double fck = cff * (3.0 * (dck * Uv[o + n2] + dc1 * Uv[o]) - dc1 * fcm);
+    const double fck = cff * (3.0 * (dck * uk1 + dc1 * uk) - dc1 * fcm);
     B[k + 1] = cf1;
     A[k] = fck;
-    dck = dc1; cfk = cf1; fcm = fck;
+    dck = dc1; cfk = cf1; fcm = fck; uk = uk1;
+  };
+  // rings hold raw loads (derived values would force the wait at prefetch)
+  auto dc_of = [&](double h0, double hm, double hp, double hmm) { return 0.5625 * (h0 + hm) - 0.0625 * (hp + hmm); };
+  int k0 = 1;
+  if (kRing) {
+    double r0[kPF], r1[kPF], r2[kPF], r3[kPF], ru[kPF];  // Hz(i), Hz(i-s), Hz(i+s), Hz(i-2s), u at level k+1
+#pragma unroll
+    for (int q = 0; q < kPF; q++) {
+      const long o = (long)(min(2 + q, N) - 1) * n2;
+      r0[q] = Hz[o]; r1[q] = Hz[o - s]; r2[q] = Hz[o + s]; r3[q] = Hz[o - 2 * s]; ru[q] = Uv[o];
+    }
+    for (; k0 + kPF - 1 <= N - 1; k0 += kPF) {
+#pragma unroll
+      for (int q = 0; q < kPF; q++) {
+        const double dc1 = dc_of(r0[q], r1[q], r2[q], r3[q]), uk1 = ru[q];
+        const long o = (long)(min(k0 + q + 1 + kPF, N) - 1) * n2;
+        r0[q] = Hz[o]; r1[q] = Hz[o - s]; r2[q] = Hz[o + s]; r3[q] = Hz[o - 2 * s]; ru[q] = Uv[o];
+        fwd(k0 + q, dc1, uk1);
+      }
+    }
   }
+#pragma unroll 4
+  for (int k = k0; k <= N - 1; k++) fwd(k, DCk(k + 1), Uv[(long)k * n2]);
   double fc1 = (2.0 * Uv[(long)(N - 1) * n2] - fcm) / (1.0 - cfk);  // FC(N)
   const double m1 = mask[ij + s], m0 = mask[ij - s];
-#pragma unroll 4
-  for (int k = N - 1; k >= 1; k--) {
-    const double fck = A[k] - B[k + 1] * fc1;
+  auto wbr = [&](double w0, double wm, double wp, double wmm) {
+    return w0 + wm - 0.125 * ((wp - w0) * m1 - (wm - wmm) * m0);
+  };
+  auto wflux = [&](int k) {
     const long w = (long)k * n2;
-    A[k] = fck * 0.5 * (We[w] + We[w - s] - 0.125 * ((We[w + s] - We[w]) * m1 - (We[w - s] - We[w - 2 * s]) * m0));
+    return wbr(We[w], We[w - s], We[w + s], We[w - 2 * s]);
+  };
+  auto bwd = [&](int k, double wf) {
+    const double fck = A[k] - B[k + 1] * fc1;
+    A[k] = fck * 0.5 * wf;
     fc1 = fck;
+  };
+  int k1 = N - 1;
+  if (kRing) {
+    double w0[kPF], w1[kPF], w2[kPF], w3[kPF];
+#pragma unroll
+    for (int q = 0; q < kPF; q++) {
+      const long w = (long)max(N - 1 - q, 1) * n2;
+      w0[q] = We[w]; w1[q] = We[w - s]; w2[q] = We[w + s]; w3[q] = We[w - 2 * s];
+    }
+    for (; k1 - kPF + 1 >= 1; k1 -= kPF) {
+#pragma unroll
+      for (int q = 0; q < kPF; q++) {
+        const double wf = wbr(w0[q], w1[q], w2[q], w3[q]);
+        const long w = (long)max(k1 - q - kPF, 1) * n2;
+        w0[q] = We[w]; w1[q] = We[w - s]; w2[q] = We[w + s]; w3[q] = We[w - 2 * s];
+        bwd(k1 - q, wf);
+      }
+    }
   }
+#pragma unroll 4
+  for (int k = k1; k >= 1; k--) bwd(k, wflux(k));
   A[0] = 0.0;
   A[N] = 0.0;
 }

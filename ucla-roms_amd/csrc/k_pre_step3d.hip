@@ -72,30 +72,11 @@ __global__ void __launch_bounds__(64) k_pre_tracer_v(Dev d, Range R, PreCoef c, 
     const long tb = (long)(itrc - 1) * 3 * b.n3;
     const double* __restrict__ Tr = F.t + (long)(nrhs - 1) * b.n3 + tb + ij;
     double* __restrict__ Tn = F.t + (long)(nnew - 1) * b.n3 + tb + ij;
-    double cfk = 1.0, fcm = 2.0 * Tr[0], hk = Hz[0], tk = Tr[0];
-#pragma unroll 8
-    for (int k = 1; k <= N - 1; k++) {
-      const double hk1 = Hz[(long)k * n2], tk1 = Tr[(long)k * n2];
-      const double cff = 1.0 / (2.0 * hk + hk1 * (2.0 - cfk));
-      const double cf1 = cff * hk;
-      const double fck = cff * (3.0 * (hk * tk1 + hk1 * tk) - hk1 * fcm);
-      B[k + 1] = cf1;
-      A[k] = fck;
-      cfk = cf1; fcm = fck; hk = hk1; tk = tk1;
-    }
-    double fc1 = (2.0 * tk - fcm) / (1.0 - cfk);
-#pragma unroll 8
-    for (int k = N - 1; k >= 0; k--) {
-      const double fck = A[k] - B[k + 1] * fc1;
-      A[k + 1] = fc1 * We[(long)(k + 1) * n2];
-      A[k] = fck;
-      fc1 = fck;
-    }
-    A[N] = 0.0;
-    A[0] = 0.0;
-    auto tval = [&](int k) {
-      return Tn[(long)(k - 1) * n2] - c.dtau * F.pm[ij] * F.pn[ij] * (A[k] - A[k - 1]);
+    tracer_spline_lds(N, n2, Hz, Tr, We, A, B);
+    auto tval_of = [&](int k, double tnk) {
+      return tnk - c.dtau * F.pm[ij] * F.pn[ij] * (A[k] - A[k - 1]);
     };
+    auto tval = [&](int k) { return tval_of(k, Tn[(long)(k - 1) * n2]); };
     const int iAkt = itrc < b.nTS ? itrc : b.nTS;
     const double* __restrict__ Akt = F.Akt + (long)(iAkt - 1) * b.n3w + ij;
     const double DC0 = c.dtau * F.pm[ij] * F.pn[ij];
@@ -108,17 +89,36 @@ __global__ void __launch_bounds__(64) k_pre_tracer_v(Dev d, Range R, PreCoef c, 
     double DCk = cff * tval(1);
     B[1] = CFk;
     A[0] = DCk;
-#pragma unroll 8
-    for (int k = 2; k <= N - 1; k++) {
-      const double hfk1 = hfwd(k + 1);
-      const double FCn = 2.0 * c.dtau * Akt[(long)k * n2] / (hfk1 + hfk);
-      const double WCn = DC0 * Wi[(long)k * n2];
-      cff = 1.0 / (hfk + FCn + fmax0(WCn) + FCk - fmin0(WCk) - CFk * (FCk + fmax0(WCk)));
-      const double CFn = cff * (FCn - fmin0(WCn));
-      const double DCn = cff * (tval(k) + DCk * (FCk + fmax0(WCk)));
-      B[k] = CFn;
-      A[k - 1] = DCn;
-      FCk = FCn; WCk = WCn; CFk = CFn; DCk = DCn; hfk = hfk1;
+    {
+      auto thomas = [&](int k, double hfk1, double akt, double wi, double tn) {
+        const double FCn = 2.0 * c.dtau * akt / (hfk1 + hfk);
+        const double WCn = DC0 * wi;
+        cff = 1.0 / (hfk + FCn + fmax0(WCn) + FCk - fmin0(WCk) - CFk * (FCk + fmax0(WCk)));
+        const double CFn = cff * (FCn - fmin0(WCn));
+        const double DCn = cff * (tval_of(k, tn) + DCk * (FCk + fmax0(WCk)));
+        B[k] = CFn;
+        A[k - 1] = DCn;
+        FCk = FCn; WCk = WCn; CFk = CFn; DCk = DCn; hfk = hfk1;
+      };
+      double rhf[kPF], ra[kPF], rwi[kPF], rtn[kPF];  // Hz_fwd(k+1), Akt(k), Wi(k), Tn(k) of level k
+#pragma unroll
+      for (int q = 0; q < kPF; q++) {
+        const int k = min(2 + q, N - 1);
+        rhf[q] = Hf[(long)k * n2]; ra[q] = Akt[(long)k * n2]; rwi[q] = Wi[(long)k * n2];
+        rtn[q] = Tn[(long)(k - 1) * n2];
+      }
+      int k2 = 2;
+      for (; k2 + kPF - 1 <= N - 1; k2 += kPF) {
+#pragma unroll
+        for (int q = 0; q < kPF; q++) {
+          const double hf1 = rhf[q], akt = ra[q], wi = rwi[q], tn = rtn[q];
+          const int kn = min(k2 + q + kPF, N - 1);
+          rhf[q] = Hf[(long)kn * n2]; ra[q] = Akt[(long)kn * n2]; rwi[q] = Wi[(long)kn * n2];
+          rtn[q] = Tn[(long)(kn - 1) * n2];
+          thomas(k2 + q, hf1, akt, wi, tn);
+        }
+      }
+      for (int k = k2; k <= N - 1; k++) thomas(k, Hf[(long)k * n2], Akt[(long)k * n2], Wi[(long)k * n2], Tn[(long)(k - 1) * n2]);
     }
     const long oN = (long)(N - 1) * n2;
     double tt = (tval(N) + DCk * (FCk + fmax0(WCk))) / (hfk + FCk - fmin0(WCk) - CFk * (FCk + fmax0(WCk)));
@@ -196,7 +196,7 @@ __device__ __forceinline__ void pre_uv_col(const Dev& d, int i, int j, int dir, 
   const int N = b.N, indx = 3 - nstp;
   const long n2 = b.n2, ij = IJ(b, i, j);
   const long s = dir == 0 ? 1 : b.nx2;
-  uv_vert_flux_lds(d, ij, nrhs, dir, A, B);
+  uv_vert_flux_lds<true>(d, ij, nrhs, dir, A, B);
   double* Uall = dir == 0 ? F.u : F.v;
   double* __restrict__ rr = (dir == 0 ? F.ru : F.rv) + ij;
   const double* __restrict__ Ustp = Uall + (long)(nstp - 1) * b.n3 + ij;

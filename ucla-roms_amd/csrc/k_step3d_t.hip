@@ -54,26 +54,7 @@ __global__ void __launch_bounds__(64) k_step3d_t_v(Dev d, Range R, int nnew, int
     double* __restrict__ Tn = F.t + (long)(nnew - 1) * b.n3 + (long)(itrc - 1) * 3 * b.n3 + ij;
     const double stf = F.stflx[ij + (long)(itrc - 1) * n2];
     // spline interface values FC(0:N) (compute_vert_tracer_fluxes.h)
-    double cfk = 1.0, fcm = 2.0 * Tr[0], hk = Hz[0], tk = Tr[0];
-    A[0] = fcm;
-#pragma unroll 8
-    for (int k = 1; k <= N - 1; k++) {
-      const double hk1 = Hz[(long)k * n2], tk1 = Tr[(long)k * n2];
-      const double cff = 1.0 / (2.0 * hk + hk1 * (2.0 - cfk));
-      const double cf1 = cff * hk;
-      const double fck = cff * (3.0 * (hk * tk1 + hk1 * tk) - hk1 * fcm);
-      B[k + 1] = cf1;
-      A[k] = fck;
-      cfk = cf1; fcm = fck; hk = hk1; tk = tk1;
-    }
-    double fc1 = (2.0 * tk - fcm) / (1.0 - cfk);
-#pragma unroll 8
-    for (int k = N - 1; k >= 0; k--) {
-      const double fck = A[k] - B[k + 1] * fc1;
-      A[k + 1] = fc1 * F.We[ij + (long)(k + 1) * n2];
-      A[k] = fck;
-      fc1 = fck;
-    }
+    tracer_spline_lds(N, n2, Hz, Tr, F.We + ij, A, B);
     A[N] = 0.0;
     A[0] = 0.0;
     // advective update + surface/KPP terms fused into the Thomas elimination
@@ -83,9 +64,9 @@ __global__ void __launch_bounds__(64) k_step3d_t_v(Dev d, Range R, int nnew, int
     const double DC0 = dt * F.pm[ij] * F.pn[ij];
     const bool kppT = P.lmd && itrc == 1, kppS = P.lmd && itrc == 2 && P.salinity;
     const double sr = F.srflx[ij];
-    auto tval = [&](int k) {
+    auto tval_of = [&](int k, double tnk) {
       const long o = (long)(k - 1) * n2;
-      double t = Tn[o] - dt * F.pm[ij] * F.pn[ij] * (A[k] - A[k - 1]);
+      double t = tnk - dt * F.pm[ij] * F.pn[ij] * (A[k] - A[k - 1]);
       if (k == N) {
         if (itrc == 1) t = t + dt * F.swflx[ij] * t / Hz[o];
         t = t + dt * stf;
@@ -99,6 +80,7 @@ __global__ void __launch_bounds__(64) k_step3d_t_v(Dev d, Range R, int nnew, int
       }
       return t;
     };
+    auto tval = [&](int k) { return tval_of(k, Tn[(long)(k - 1) * n2]); };
     double FCk = 2.0 * dt * Akt[n2] / (Hz[0] + Hz[n2]);
     double WCk = DC0 * Wi[n2];
     double cff = 1.0 / (Hz[0] + FCk + fmax0(WCk));
@@ -106,17 +88,40 @@ __global__ void __launch_bounds__(64) k_step3d_t_v(Dev d, Range R, int nnew, int
     double DCk = cff * tval(1);
     B[1] = CFk;
     A[0] = DCk;
-#pragma unroll 8
-    for (int k = 2; k <= N - 1; k++) {
-      const long o = (long)(k - 1) * n2;
-      const double FCn = 2.0 * dt * Akt[(long)k * n2] / (Hz[o] + Hz[o + n2]);
-      const double WCn = Wi[(long)k * n2] * DC0;
-      cff = 1.0 / (Hz[o] + FCn + fmax0(WCn) + FCk - fmin0(WCk) - CFk * (FCk + fmax0(WCk)));
-      const double CFn = cff * (FCn - fmin0(WCn));
-      const double DCn = cff * (tval(k) + DCk * (FCk + fmax0(WCk)));
-      B[k] = CFn;
-      A[k - 1] = DCn;
-      FCk = FCn; WCk = WCn; CFk = CFn; DCk = DCn;
+    {
+      double hzk = Hz[n2];  // Hz of rho level k (starts at k=2)
+      auto thomas = [&](int k, double akt, double hz1, double wi, double tn) {
+        const double hz0 = hzk;
+        const double FCn = 2.0 * dt * akt / (hz0 + hz1);
+        const double WCn = wi * DC0;
+        cff = 1.0 / (hz0 + FCn + fmax0(WCn) + FCk - fmin0(WCk) - CFk * (FCk + fmax0(WCk)));
+        const double CFn = cff * (FCn - fmin0(WCn));
+        const double DCn = cff * (tval_of(k, tn) + DCk * (FCk + fmax0(WCk)));
+        B[k] = CFn;
+        A[k - 1] = DCn;
+        FCk = FCn; WCk = WCn; CFk = CFn; DCk = DCn;
+        hzk = hz1;
+      };
+      double ra[kPF], rhz[kPF], rwi[kPF], rtn[kPF];   // Akt(k), Hz(k+1), Wi(k), Tn(k) of level k
+#pragma unroll
+      for (int q = 0; q < kPF; q++) {
+        const int k = min(2 + q, N - 1);
+        ra[q] = Akt[(long)k * n2]; rhz[q] = Hz[(long)k * n2]; rwi[q] = Wi[(long)k * n2];
+        rtn[q] = Tn[(long)(k - 1) * n2];
+      }
+      int k2 = 2;
+      for (; k2 + kPF - 1 <= N - 1; k2 += kPF) {
+#pragma unroll
+        for (int q = 0; q < kPF; q++) {
+          const double akt = ra[q], hz1 = rhz[q], wi = rwi[q], tn = rtn[q];
+          const int kn = min(k2 + q + kPF, N - 1);
+          ra[q] = Akt[(long)kn * n2]; rhz[q] = Hz[(long)kn * n2]; rwi[q] = Wi[(long)kn * n2];
+          rtn[q] = Tn[(long)(kn - 1) * n2];
+          thomas(k2 + q, akt, hz1, wi, tn);
+        }
+      }
+      for (int k = k2; k <= N - 1; k++)
+        thomas(k, Akt[(long)k * n2], Hz[(long)k * n2], Wi[(long)k * n2], Tn[(long)(k - 1) * n2]);
     }
     const long oN = (long)(N - 1) * n2;
     double tt = (tval(N) + DCk * (FCk + fmax0(WCk))) / (Hz[oN] + FCk - fmin0(WCk) - CFk * (FCk + fmax0(WCk))) * rm;
