@@ -182,8 +182,13 @@ __global__ void __launch_bounds__(256) k_s2d_mom(Dev d, Range R, FBCoef c) {
 // LDS.  zeta_new/Dnew also go to global scratch when closed-edge kernels
 // need them afterwards.
 // ---------------------------------------------------------------------------
-constexpr int kFX = kBX + 1, kFY = kBY + 1, kFN = kFX * kFY;
+constexpr int kFX = kBX + 1, kFY = kBY + 1, kFN = kFX * kFY;  // zeta-part window (i0-1.., j0-1..)
+constexpr int kGX = kBX + 3, kGY = kBY + 3, kGN = kGX * kGY;  // input window (i0-2.., j0-2..)
+constexpr int kUX = kBX + 2, kUN = kUX * kFY;                 // DUon faces i0-1..i0+64, rows j0-1..j0+3
+constexpr int kVN = kFX * (kBY + 2);                          // DVom faces i0-1..i0+63, rows j0-1..j0+4
 struct FBTile {
+  double z0[kGN], z1[kGN], z2[kGN], h[kGN], Dr[kGN];   // zeta(kstp,kbak,kold), h, Drhs
+  double DU[kUN], DV[kVN];                              // DUon, DVom
   double zn[kFN], Dn[kFN], zw[kFN], rz[kFN], rz2[kFN], rzSA[kFN];
   unsigned char st[kFN];  // 0: outside, 1: computed, 2: set by zetabc
 };
@@ -195,31 +200,73 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int cl
   const long sj = b.nx2, n2 = b.n2;
   const int i0 = R.i0 + (int)blockIdx.x * kBX, j0 = R.j0 + (int)blockIdx.y * kBY;
   const int tid = threadIdx.x + kBX * threadIdx.y;
-  // zeta range of the reference kernel (istrU-1..iend, jstrV-1..jend)
+  constexpr int NT = kBX * kBY;
+  auto G = [&](int i, int j) { return (i - (i0 - 2)) + (j - (j0 - 2)) * kGX; };
+  auto inarr = [&](int i, int j) { return i >= -1 && i <= b.Lm + 2 && j >= -1 && j <= b.Mm + 2; };
+  // P0: time levels of zeta, h and Drhs = h + fwd*z(kstp) + fwd1*z(kbak) + fwd2*z(kold)
+  for (int q = tid; q < kGN; q += NT) {
+    const int i = i0 - 2 + q % kGX, j = j0 - 2 + q / kGX;
+    if (!inarr(i, j)) { T.z0[q] = T.z1[q] = T.z2[q] = T.h[q] = T.Dr[q] = 0.0; continue; }
+    const long ij = IJ(b, i, j);
+    const double z0 = F.zeta[ij + (long)(c.kstp - 1) * n2], z1 = F.zeta[ij + (long)(c.kbak - 1) * n2],
+                 z2 = F.zeta[ij + (long)(c.kold - 1) * n2], h = F.h[ij];
+    T.z0[q] = z0; T.z1[q] = z1; T.z2[q] = z2; T.h[q] = h;
+    T.Dr[q] = h + c.fwd * z0 + c.fwd1 * z1 + c.fwd2 * z2;
+  }
+  __syncthreads();
+  // P1: barotropic fluxes DUon (u faces) and DVom (v faces), once each
+  for (int q = tid; q < kUN + kVN; q += NT) {
+    if (q < kUN) {
+      const int i = i0 - 1 + q % kUX, j = j0 - 1 + q / kUX;
+      double v = 0.0;
+      if (i >= 0 && inarr(i, j)) {
+        const long ij = IJ(b, i, j);
+        const double urhs = c.fwd * F.ubar[ij + (long)(c.kstp - 1) * n2] + c.fwd1 * F.ubar[ij + (long)(c.kbak - 1) * n2] +
+                            c.fwd2 * F.ubar[ij + (long)(c.kold - 1) * n2];
+        v = 0.5 * (T.Dr[G(i, j)] + T.Dr[G(i - 1, j)]) * F.dn_u[ij] * (urhs);
+      }
+      T.DU[q] = v;
+    } else {
+      const int qq = q - kUN;
+      const int i = i0 - 1 + qq % kFX, j = j0 - 1 + qq / kFX;
+      double v = 0.0;
+      if (j >= 0 && inarr(i, j)) {
+        const long ij = IJ(b, i, j);
+        const double vrhs = c.fwd * F.vbar[ij + (long)(c.kstp - 1) * n2] + c.fwd1 * F.vbar[ij + (long)(c.kbak - 1) * n2] +
+                            c.fwd2 * F.vbar[ij + (long)(c.kold - 1) * n2];
+        v = 0.5 * (T.Dr[G(i, j)] + T.Dr[G(i, j - 1)]) * F.dm_v[ij] * (vrhs);
+      }
+      T.DV[qq] = v;
+    }
+  }
+  __syncthreads();
+  auto DU = [&](int i, int j) { return T.DU[(i - (i0 - 1)) + (j - (j0 - 1)) * kUX]; };
+  auto DV = [&](int i, int j) { return T.DV[(i - (i0 - 1)) + (j - (j0 - 1)) * kFX]; };
+  // P2: free surface and the backward-averaged terms of the reference's
+  // zeta range (istrU-1..iend, jstrV-1..jend) inside the window
   const int za = b.istrU - 1, zb = b.iend, zc = b.jstrV - 1, zd = b.jend;
-  for (int q = tid; q < kFN; q += kBX * kBY) {
-    const int li = q % kFX, lj = q / kFX;
-    const int i = i0 - 1 + li, j = j0 - 1 + lj;
-    if (i < za || i > zb || j < zc || j > zd) {  // outside the reference's zeta range: never consumed
+  for (int q = tid; q < kFN; q += NT) {
+    const int i = i0 - 1 + q % kFX, j = j0 - 1 + q / kFX;
+    if (i < za || i > zb || j < zc || j > zd) {  // never consumed
       T.zn[q] = T.Dn[q] = T.zw[q] = T.rz[q] = T.rz2[q] = T.rzSA[q] = 0.0;
       T.st[q] = 0;
       continue;
     }
     T.st[q] = 1;
     const long ij = IJ(b, i, j);
-    const double zk = F.zeta[ij + (long)(c.kstp - 1) * n2];
-    double zn = zk + d.p.dtfast * F.pm[ij] * F.pn[ij] *
-                         (s2d_DUon(d, c, ij) - s2d_DUon(d, c, ij + 1) + s2d_DVom(d, c, ij) - s2d_DVom(d, c, ij + sj)) +
+    const int g = G(i, j);
+    const double zk = T.z0[g];
+    double zn = zk + d.p.dtfast * F.pm[ij] * F.pn[ij] * (DU(i, j) - DU(i + 1, j) + DV(i, j) - DV(i, j + 1)) +
                 d.p.dtfast * F.swflx[ij];
     zn = zn * F.rmask[ij];
-    const double zwrk = c.bkw_new * zn + c.bkw * zk + c.bkw1 * F.zeta[ij + (long)(c.kbak - 1) * n2] +
-                        c.bkw2 * F.zeta[ij + (long)(c.kold - 1) * n2];
-    const double rzeta = (1.0 + F.rhoS[ij]) * zwrk;
+    const double zwrk = c.bkw_new * zn + c.bkw * zk + c.bkw1 * T.z1[g] + c.bkw2 * T.z2[g];
+    const double rhoS = F.rhoS[ij];
+    const double rzeta = (1.0 + rhoS) * zwrk;
     T.zn[q] = zn;
-    T.Dn[q] = zn + F.h[ij];
+    T.Dn[q] = zn + T.h[g];
     T.zw[q] = zwrk;
     T.rz[q] = rzeta;
-    T.rzSA[q] = zwrk * (F.rhoS[ij] - F.rhoA[ij]);
+    T.rzSA[q] = zwrk * (rhoS - F.rhoA[ij]);
     T.rz2[q] = rzeta * zwrk;
   }
   __syncthreads();
@@ -227,7 +274,7 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int cl
     // zetabc_tile (zetabc.F), closed walls: edges, then corners
     auto L = [&](int i, int j) { return (i - (i0 - 1)) + (j - (j0 - 1)) * kFX; };
     auto in = [&](int i, int j) { return i >= i0 - 1 && i <= i0 + kBX - 1 && j >= j0 - 1 && j <= j0 + kBY - 1; };
-    for (int q = tid; q < kFN; q += kBX * kBY) {
+    for (int q = tid; q < kFN; q += NT) {
       const int i = i0 - 1 + q % kFX, j = j0 - 1 + q / kFX;
       const long ij = IJ(b, i, j);
       if (j >= b.jstrV - 1 && j <= b.jend) {
@@ -242,101 +289,102 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int cl
     __syncthreads();
     if (tid == 0) {
       const int is = b.istr, ie = b.iend, js = b.jstr, je = b.jend;
-      if (b.south_edge && b.west_edge && in(is - 1, js - 1) && in(is, js - 1) && in(is - 1, js))
-        { T.zn[L(is - 1, js - 1)] = 0.5 * (T.zn[L(is, js - 1)] + T.zn[L(is - 1, js)]); T.st[L(is - 1, js - 1)] = 2; }
-      if (b.south_edge && b.east_edge && in(ie + 1, js - 1) && in(ie, js - 1) && in(ie + 1, js))
-        { T.zn[L(ie + 1, js - 1)] = 0.5 * (T.zn[L(ie, js - 1)] + T.zn[L(ie + 1, js)]); T.st[L(ie + 1, js - 1)] = 2; }
-      if (b.north_edge && b.west_edge && in(is - 1, je + 1) && in(is, je + 1) && in(is - 1, je))
-        { T.zn[L(is - 1, je + 1)] = 0.5 * (T.zn[L(is, je + 1)] + T.zn[L(is - 1, je)]); T.st[L(is - 1, je + 1)] = 2; }
-      if (b.north_edge && b.east_edge && in(ie + 1, je + 1) && in(ie, je + 1) && in(ie + 1, je))
-        { T.zn[L(ie + 1, je + 1)] = 0.5 * (T.zn[L(ie, je + 1)] + T.zn[L(ie + 1, je)]); T.st[L(ie + 1, je + 1)] = 2; }
+      if (b.south_edge && b.west_edge && in(is - 1, js - 1) && in(is, js - 1) && in(is - 1, js)) { T.zn[L(is - 1, js - 1)] = 0.5 * (T.zn[L(is, js - 1)] + T.zn[L(is - 1, js)]); T.st[L(is - 1, js - 1)] = 2; }
+      if (b.south_edge && b.east_edge && in(ie + 1, js - 1) && in(ie, js - 1) && in(ie + 1, js)) { T.zn[L(ie + 1, js - 1)] = 0.5 * (T.zn[L(ie, js - 1)] + T.zn[L(ie + 1, js)]); T.st[L(ie + 1, js - 1)] = 2; }
+      if (b.north_edge && b.west_edge && in(is - 1, je + 1) && in(is, je + 1) && in(is - 1, je)) { T.zn[L(is - 1, je + 1)] = 0.5 * (T.zn[L(is, je + 1)] + T.zn[L(is - 1, je)]); T.st[L(is - 1, je + 1)] = 2; }
+      if (b.north_edge && b.east_edge && in(ie + 1, je + 1) && in(ie, je + 1) && in(ie + 1, je)) { T.zn[L(ie + 1, je + 1)] = 0.5 * (T.zn[L(ie, je + 1)] + T.zn[L(ie + 1, je)]); T.st[L(ie + 1, je + 1)] = 2; }
     }
     __syncthreads();
     // the edge kernels read zeta_new / Dnew from global scratch: every block
     // stores the window cells it computed or set (identical values where
     // windows overlap)
-    for (int q = tid; q < kFN; q += kBX * kBY) {
+    for (int q = tid; q < kFN; q += NT) {
       if (!T.st[q]) continue;
       const long o = IJ(b, i0 - 1 + q % kFX, j0 - 1 + q / kFX);
       F.s0[o] = T.zn[q];
       if (T.st[q] == 1) F.s1[o] = T.Dn[q];
     }
   }
+  // P3: zeta(knew), fast averages, pressure gradient, momentum
   const int i = i0 + (int)threadIdx.x, j = j0 + (int)threadIdx.y;
   if (i > R.i1 || j > R.j1) return;
   const int q = (threadIdx.x + 1) + (threadIdx.y + 1) * kFX;  // (i,j); q-1 = (i-1,j); q-kFX = (i,j-1)
+  const int g = G(i, j);                                        // g-1: (i-1,j); g-kGX: (i,j-1)
   const long ij = IJ(b, i, j);
   {
     const double z = T.zn[q];
     F.zeta[ij + (long)(c.knew - 1) * n2] = z;
+    const double du = DU(i, j), dv = DV(i, j);
     if (c.iif == 1) {
       F.DU_avg_bak[ij] = F.DU_avg1[ij] - 0.1024390243902439 * F.DU_avg2[ij];
       F.DV_avg_bak[ij] = F.DV_avg1[ij] - 0.1024390243902439 * F.DV_avg2[ij];
       F.Zt_avg1[ij] = c.w1 * z;
       F.DU_avg1[ij] = 0.0;
       F.DV_avg1[ij] = 0.0;
-      F.DU_avg2[ij] = c.w2 * s2d_DUon(d, c, ij);
-      F.DV_avg2[ij] = c.w2 * s2d_DVom(d, c, ij);
+      F.DU_avg2[ij] = c.w2 * du;
+      F.DV_avg2[ij] = c.w2 * dv;
     } else {
       F.Zt_avg1[ij] = F.Zt_avg1[ij] + c.w1 * z;
-      F.DU_avg2[ij] = F.DU_avg2[ij] + c.w2 * s2d_DUon(d, c, ij);
-      F.DV_avg2[ij] = F.DV_avg2[ij] + c.w2 * s2d_DVom(d, c, ij);
+      F.DU_avg2[ij] = F.DU_avg2[ij] + c.w2 * du;
+      F.DV_avg2[ij] = F.DV_avg2[ij] + c.w2 * dv;
     }
   }
   if (i < b.istr || i > b.iend || j < b.jstr || j > b.jend) return;
   const double gh = 0.5 * d.p.g;
+  const double h0 = T.h[g], hxm = T.h[g - 1], hym = T.h[g - kGX];
+  const double rA0 = F.rhoA[ij], rAx = F.rhoA[ij - 1], rAy = F.rhoA[ij - sj];
   // pressure gradient at u (neighbour q-1) and v (neighbour q-kFX) points
-  auto pgf = [&](long s, int qm, double dn) {
+  auto pgf = [&](int qm, double hm, double rAm, double dn) {
     return gh * dn *
-           ((F.h[ij - s] + F.h[ij]) * (T.rz[qm] - T.rz[q]) + T.rz2[qm] - T.rz2[q] +
-            (F.h[ij - s] - F.h[ij]) *
-                (T.rzSA[qm] + T.rzSA[q] + 0.333333333333 * (F.rhoA[ij - s] - F.rhoA[ij]) * (T.zw[qm] - T.zw[q])));
+           ((hm + h0) * (T.rz[qm] - T.rz[q]) + T.rz2[qm] - T.rz2[q] +
+            (hm - h0) * (T.rzSA[qm] + T.rzSA[q] + 0.333333333333 * (rAm - rA0) * (T.zw[qm] - T.zw[q])));
   };
-  double rubar = pgf(1, q - 1, F.dn_u[ij]);
-  double rvbar = pgf(sj, q - kFX, F.dm_v[ij]);
+  const double dn_u = F.dn_u[ij], dm_v = F.dm_v[ij];
+  double rubar = pgf(q - 1, hxm, rAx, dn_u);
+  double rvbar = pgf(q - kFX, hym, rAy, dm_v);
   double rufrc = F.rufrc[ij], rvfrc = F.rvfrc[ij];
   if (c.iif == 1) {
     rufrc = rufrc - rubar;
     rvfrc = rvfrc - rvbar;
     F.rufrc[ij] = rufrc;
     F.rvfrc[ij] = rvfrc;
-    const long lk = (long)(c.kstp - 1) * n2;
-    auto corr = [&](int qq, long o, double& zwrk, double& rzeta, double& rzeta2, double& rzetaSA) {
-      const double zn = T.zn[qq], zk = F.zeta[o + lk];
+    auto corr = [&](int qq, int gg, long o, double& zwrk, double& rzeta, double& rzeta2, double& rzetaSA) {
+      const double zn = T.zn[qq], zk = T.z0[gg];
       zwrk = zn - zk;
       rzeta = (1.0 + F.rhoS[o]) * zwrk;
       rzeta2 = rzeta * (zn + zk);
       rzetaSA = zwrk * (F.rhoS[o] - F.rhoA[o]);
     };
     double zw0, rz0, rz20, sa0, zw1, rz1, rz21, sa1, zw2, rz2_, rz22, sa2;
-    corr(q, ij, zw0, rz0, rz20, sa0);
-    corr(q - 1, ij - 1, zw1, rz1, rz21, sa1);
-    corr(q - kFX, ij - sj, zw2, rz2_, rz22, sa2);
-    rubar = rubar + gh * F.dn_u[ij] *
-                        ((F.h[ij - 1] + F.h[ij]) * (rz1 - rz0) + rz21 - rz20 +
-                         (F.h[ij - 1] - F.h[ij]) * (sa1 + sa0 + 0.333333333333 * (F.rhoA[ij - 1] - F.rhoA[ij]) * (zw1 - zw0)));
-    rvbar = rvbar + gh * F.dm_v[ij] *
-                        ((F.h[ij - sj] + F.h[ij]) * (rz2_ - rz0) + rz22 - rz20 +
-                         (F.h[ij - sj] - F.h[ij]) * (sa2 + sa0 + 0.333333333333 * (F.rhoA[ij - sj] - F.rhoA[ij]) * (zw2 - zw0)));
+    corr(q, g, ij, zw0, rz0, rz20, sa0);
+    corr(q - 1, g - 1, ij - 1, zw1, rz1, rz21, sa1);
+    corr(q - kFX, g - kGX, ij - sj, zw2, rz2_, rz22, sa2);
+    rubar = rubar + gh * dn_u *
+                        ((hxm + h0) * (rz1 - rz0) + rz21 - rz20 +
+                         (hxm - h0) * (sa1 + sa0 + 0.333333333333 * (rAx - rA0) * (zw1 - zw0)));
+    rvbar = rvbar + gh * dm_v *
+                        ((hym + h0) * (rz2_ - rz0) + rz22 - rz20 +
+                         (hym - h0) * (sa2 + sa0 + 0.333333333333 * (rAy - rA0) * (zw2 - zw0)));
   }
   const double cff = 0.5 * d.p.dtfast, cff1 = 0.5 * c.w1;
   const long lk = (long)(c.kstp - 1) * n2;
-  const double Dstp0 = F.zeta[ij + lk] + F.h[ij];
+  const double Dstp0 = T.z0[g] + h0;
+  const double pm0 = F.pm[ij], pn0 = F.pn[ij];
   if (i >= b.istrU) {
-    const double Dstpm = F.zeta[ij - 1 + lk] + F.h[ij - 1];
+    const double Dstpm = T.z0[g - 1] + hxm;
     const double DUnew = ((Dstp0 + Dstpm) * F.ubar[ij + lk] +
-                          cff * (F.pm[ij] + F.pm[ij - 1]) * (F.pn[ij] + F.pn[ij - 1]) * (rubar + rufrc)) *
+                          cff * (pm0 + F.pm[ij - 1]) * (pn0 + F.pn[ij - 1]) * (rubar + rufrc)) *
                          F.umask[ij];
     F.ubar[ij + (long)(c.knew - 1) * n2] = DUnew / (T.Dn[q] + T.Dn[q - 1]);
-    F.DU_avg1[ij] = F.DU_avg1[ij] + cff1 * F.dn_u[ij] * (DUnew);
+    F.DU_avg1[ij] = F.DU_avg1[ij] + cff1 * dn_u * (DUnew);
   }
   if (j >= b.jstrV) {
-    const double Dstpm = F.zeta[ij - sj + lk] + F.h[ij - sj];
+    const double Dstpm = T.z0[g - kGX] + hym;
     const double DVnew = ((Dstp0 + Dstpm) * F.vbar[ij + lk] +
-                          cff * (F.pm[ij] + F.pm[ij - sj]) * (F.pn[ij] + F.pn[ij - sj]) * (rvbar + rvfrc)) *
+                          cff * (pm0 + F.pm[ij - sj]) * (pn0 + F.pn[ij - sj]) * (rvbar + rvfrc)) *
                          F.vmask[ij];
     F.vbar[ij + (long)(c.knew - 1) * n2] = DVnew / (T.Dn[q] + T.Dn[q - kFX]);
-    F.DV_avg1[ij] = F.DV_avg1[ij] + cff1 * F.dm_v[ij] * (DVnew);
+    F.DV_avg1[ij] = F.DV_avg1[ij] + cff1 * dm_v * (DVnew);
   }
 }
 
