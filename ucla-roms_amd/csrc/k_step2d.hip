@@ -203,6 +203,42 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int cl
   constexpr int NT = kBX * kBY;
   auto G = [&](int i, int j) { return (i - (i0 - 2)) + (j - (j0 - 2)) * kGX; };
   auto inarr = [&](int i, int j) { return i >= -1 && i <= b.Lm + 2 && j >= -1 && j <= b.Mm + 2; };
+  // Independent global loads of the later phases are issued first, so their
+  // latency overlaps the staging phases (the grid is one wave of blocks: each
+  // block's critical path is the kernel time).
+  const int za = b.istrU - 1, zb = b.iend, zc = b.jstrV - 1, zd = b.jend;
+  double e_pm[2], e_pn[2], e_sw[2], e_rm[2], e_rS[2], e_rA[2];
+#pragma unroll
+  for (int r = 0; r < 2; r++) {
+    const int q = tid + r * NT;
+    const int i = i0 - 1 + q % kFX, j = j0 - 1 + q / kFX;
+    e_pm[r] = e_pn[r] = e_sw[r] = e_rm[r] = e_rS[r] = e_rA[r] = 0.0;
+    if (q < kFN && i >= za && i <= zb && j >= zc && j <= zd) {
+      const long ij = IJ(b, i, j);
+      e_pm[r] = F.pm[ij];
+      e_pn[r] = F.pn[ij];
+      e_sw[r] = F.swflx[ij]; e_rm[r] = F.rmask[ij]; e_rS[r] = F.rhoS[ij]; e_rA[r] = F.rhoA[ij];
+    }
+  }
+  const int pi = i0 + (int)threadIdx.x, pj = j0 + (int)threadIdx.y;
+  const bool pact = pi <= R.i1 && pj <= R.j1;
+  const bool pint = pact && pi >= b.istr && pi <= b.iend && pj >= b.jstr && pj <= b.jend;
+  const long pij = pact ? IJ(b, pi, pj) : 0;
+  double x_rA0 = 0, x_rAx = 0, x_rAy = 0, x_dnu = 0, x_dmv = 0, x_rufrc = 0, x_rvfrc = 0, x_ub = 0, x_vb = 0;
+  double x_pmx = 0, x_pnx = 0, x_pmy = 0, x_pny = 0, x_pm0 = 0, x_pn0 = 0, x_um = 0, x_vm = 0, x_DU1 = 0, x_DV1 = 0;
+  double x_rS0 = 0, x_rSx = 0, x_rSy = 0;
+  if (pint) {
+    const long lk = (long)(c.kstp - 1) * n2;
+    x_rA0 = F.rhoA[pij]; x_rAx = F.rhoA[pij - 1]; x_rAy = F.rhoA[pij - sj];
+    x_dnu = F.dn_u[pij]; x_dmv = F.dm_v[pij];
+    x_rufrc = F.rufrc[pij]; x_rvfrc = F.rvfrc[pij];
+    x_ub = F.ubar[pij + lk]; x_vb = F.vbar[pij + lk];
+    x_pm0 = F.pm[pij]; x_pn0 = F.pn[pij]; x_pmx = F.pm[pij - 1]; x_pnx = F.pn[pij - 1];
+    x_pmy = F.pm[pij - sj]; x_pny = F.pn[pij - sj];
+    x_um = F.umask[pij]; x_vm = F.vmask[pij];
+    x_DU1 = F.DU_avg1[pij]; x_DV1 = F.DV_avg1[pij];
+    if (c.iif == 1) { x_rS0 = F.rhoS[pij]; x_rSx = F.rhoS[pij - 1]; x_rSy = F.rhoS[pij - sj]; }
+  }
   // P0: time levels of zeta, h and Drhs = h + fwd*z(kstp) + fwd1*z(kbak) + fwd2*z(kold)
   for (int q = tid; q < kGN; q += NT) {
     const int i = i0 - 2 + q % kGX, j = j0 - 2 + q / kGX;
@@ -244,8 +280,10 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int cl
   auto DV = [&](int i, int j) { return T.DV[(i - (i0 - 1)) + (j - (j0 - 1)) * kFX]; };
   // P2: free surface and the backward-averaged terms of the reference's
   // zeta range (istrU-1..iend, jstrV-1..jend) inside the window
-  const int za = b.istrU - 1, zb = b.iend, zc = b.jstrV - 1, zd = b.jend;
-  for (int q = tid; q < kFN; q += NT) {
+#pragma unroll
+  for (int r = 0; r < 2; r++) {
+    const int q = tid + r * NT;
+    if (q >= kFN) break;
     const int i = i0 - 1 + q % kFX, j = j0 - 1 + q / kFX;
     if (i < za || i > zb || j < zc || j > zd) {  // never consumed
       T.zn[q] = T.Dn[q] = T.zw[q] = T.rz[q] = T.rz2[q] = T.rzSA[q] = 0.0;
@@ -253,20 +291,19 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int cl
       continue;
     }
     T.st[q] = 1;
-    const long ij = IJ(b, i, j);
     const int g = G(i, j);
     const double zk = T.z0[g];
-    double zn = zk + d.p.dtfast * F.pm[ij] * F.pn[ij] * (DU(i, j) - DU(i + 1, j) + DV(i, j) - DV(i, j + 1)) +
-                d.p.dtfast * F.swflx[ij];
-    zn = zn * F.rmask[ij];
+    double zn = zk + d.p.dtfast * e_pm[r] * e_pn[r] * (DU(i, j) - DU(i + 1, j) + DV(i, j) - DV(i, j + 1)) +
+                d.p.dtfast * e_sw[r];
+    zn = zn * e_rm[r];
     const double zwrk = c.bkw_new * zn + c.bkw * zk + c.bkw1 * T.z1[g] + c.bkw2 * T.z2[g];
-    const double rhoS = F.rhoS[ij];
+    const double rhoS = e_rS[r];
     const double rzeta = (1.0 + rhoS) * zwrk;
     T.zn[q] = zn;
     T.Dn[q] = zn + T.h[g];
     T.zw[q] = zwrk;
     T.rz[q] = rzeta;
-    T.rzSA[q] = zwrk * (rhoS - F.rhoA[ij]);
+    T.rzSA[q] = zwrk * (rhoS - e_rA[r]);
     T.rz2[q] = rzeta * zwrk;
   }
   __syncthreads();
@@ -329,36 +366,37 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int cl
       F.DV_avg2[ij] = F.DV_avg2[ij] + c.w2 * dv;
     }
   }
-  if (i < b.istr || i > b.iend || j < b.jstr || j > b.jend) return;
+  if (!pint) return;
   const double gh = 0.5 * d.p.g;
   const double h0 = T.h[g], hxm = T.h[g - 1], hym = T.h[g - kGX];
-  const double rA0 = F.rhoA[ij], rAx = F.rhoA[ij - 1], rAy = F.rhoA[ij - sj];
+  const double rA0 = x_rA0, rAx = x_rAx, rAy = x_rAy;
   // pressure gradient at u (neighbour q-1) and v (neighbour q-kFX) points
   auto pgf = [&](int qm, double hm, double rAm, double dn) {
     return gh * dn *
            ((hm + h0) * (T.rz[qm] - T.rz[q]) + T.rz2[qm] - T.rz2[q] +
             (hm - h0) * (T.rzSA[qm] + T.rzSA[q] + 0.333333333333 * (rAm - rA0) * (T.zw[qm] - T.zw[q])));
   };
-  const double dn_u = F.dn_u[ij], dm_v = F.dm_v[ij];
+  const double dn_u = x_dnu, dm_v = x_dmv;
   double rubar = pgf(q - 1, hxm, rAx, dn_u);
   double rvbar = pgf(q - kFX, hym, rAy, dm_v);
-  double rufrc = F.rufrc[ij], rvfrc = F.rvfrc[ij];
+  double rufrc = x_rufrc, rvfrc = x_rvfrc;
   if (c.iif == 1) {
     rufrc = rufrc - rubar;
     rvfrc = rvfrc - rvbar;
     F.rufrc[ij] = rufrc;
     F.rvfrc[ij] = rvfrc;
-    auto corr = [&](int qq, int gg, long o, double& zwrk, double& rzeta, double& rzeta2, double& rzetaSA) {
+    auto corr = [&](int qq, int gg, double rS, double rA, double& zwrk, double& rzeta, double& rzeta2,
+                    double& rzetaSA) {
       const double zn = T.zn[qq], zk = T.z0[gg];
       zwrk = zn - zk;
-      rzeta = (1.0 + F.rhoS[o]) * zwrk;
+      rzeta = (1.0 + rS) * zwrk;
       rzeta2 = rzeta * (zn + zk);
-      rzetaSA = zwrk * (F.rhoS[o] - F.rhoA[o]);
+      rzetaSA = zwrk * (rS - rA);
     };
     double zw0, rz0, rz20, sa0, zw1, rz1, rz21, sa1, zw2, rz2_, rz22, sa2;
-    corr(q, g, ij, zw0, rz0, rz20, sa0);
-    corr(q - 1, g - 1, ij - 1, zw1, rz1, rz21, sa1);
-    corr(q - kFX, g - kGX, ij - sj, zw2, rz2_, rz22, sa2);
+    corr(q, g, x_rS0, rA0, zw0, rz0, rz20, sa0);
+    corr(q - 1, g - 1, x_rSx, rAx, zw1, rz1, rz21, sa1);
+    corr(q - kFX, g - kGX, x_rSy, rAy, zw2, rz2_, rz22, sa2);
     rubar = rubar + gh * dn_u *
                         ((hxm + h0) * (rz1 - rz0) + rz21 - rz20 +
                          (hxm - h0) * (sa1 + sa0 + 0.333333333333 * (rAx - rA0) * (zw1 - zw0)));
@@ -367,24 +405,18 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int cl
                          (hym - h0) * (sa2 + sa0 + 0.333333333333 * (rAy - rA0) * (zw2 - zw0)));
   }
   const double cff = 0.5 * d.p.dtfast, cff1 = 0.5 * c.w1;
-  const long lk = (long)(c.kstp - 1) * n2;
   const double Dstp0 = T.z0[g] + h0;
-  const double pm0 = F.pm[ij], pn0 = F.pn[ij];
   if (i >= b.istrU) {
     const double Dstpm = T.z0[g - 1] + hxm;
-    const double DUnew = ((Dstp0 + Dstpm) * F.ubar[ij + lk] +
-                          cff * (pm0 + F.pm[ij - 1]) * (pn0 + F.pn[ij - 1]) * (rubar + rufrc)) *
-                         F.umask[ij];
+    const double DUnew = ((Dstp0 + Dstpm) * x_ub + cff * (x_pm0 + x_pmx) * (x_pn0 + x_pnx) * (rubar + rufrc)) * x_um;
     F.ubar[ij + (long)(c.knew - 1) * n2] = DUnew / (T.Dn[q] + T.Dn[q - 1]);
-    F.DU_avg1[ij] = F.DU_avg1[ij] + cff1 * dn_u * (DUnew);
+    F.DU_avg1[ij] = (c.iif == 1 ? 0.0 : x_DU1) + cff1 * dn_u * (DUnew);
   }
   if (j >= b.jstrV) {
     const double Dstpm = T.z0[g - kGX] + hym;
-    const double DVnew = ((Dstp0 + Dstpm) * F.vbar[ij + lk] +
-                          cff * (pm0 + F.pm[ij - sj]) * (pn0 + F.pn[ij - sj]) * (rvbar + rvfrc)) *
-                         F.vmask[ij];
+    const double DVnew = ((Dstp0 + Dstpm) * x_vb + cff * (x_pm0 + x_pmy) * (x_pn0 + x_pny) * (rvbar + rvfrc)) * x_vm;
     F.vbar[ij + (long)(c.knew - 1) * n2] = DVnew / (T.Dn[q] + T.Dn[q - kFX]);
-    F.DV_avg1[ij] = F.DV_avg1[ij] + cff1 * dm_v * (DVnew);
+    F.DV_avg1[ij] = (c.iif == 1 ? 0.0 : x_DV1) + cff1 * dm_v * (DVnew);
   }
 }
 
