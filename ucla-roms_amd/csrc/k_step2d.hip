@@ -193,7 +193,7 @@ struct FBTile {
   unsigned char st[kFN];  // 0: outside, 1: computed, 2: set by zetabc
 };
 
-__global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int closed) {
+__global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int closed, int vwrap) {
   __shared__ FBTile T;
   const Bounds& b = d.b;
   const Fields& F = d.f;
@@ -203,6 +203,14 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int cl
   constexpr int NT = kBX * kBY;
   auto G = [&](int i, int j) { return (i - (i0 - 2)) + (j - (j0 - 2)) * kGX; };
   auto inarr = [&](int i, int j) { return i >= -1 && i <= b.Lm + 2 && j >= -1 && j <= b.Mm + 2; };
+  // vwrap: single-rank periodic directions read the fast-time fields' halo
+  // cells from their periodic images (the per-step wrap is deferred to the
+  // end of the fast loop, see launch_step2d)
+  auto FT = [&](int i, int j) -> long {
+    if (vwrap & 1) i = i < 1 ? i + b.Lm : (i > b.Lm ? i - b.Lm : i);
+    if (vwrap & 2) j = j < 1 ? j + b.Mm : (j > b.Mm ? j - b.Mm : j);
+    return IJ(b, i, j);
+  };
   // Independent global loads of the later phases are issued first, so their
   // latency overlaps the staging phases (the grid is one wave of blocks: each
   // block's critical path is the kernel time).
@@ -243,9 +251,9 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int cl
   for (int q = tid; q < kGN; q += NT) {
     const int i = i0 - 2 + q % kGX, j = j0 - 2 + q / kGX;
     if (!inarr(i, j)) { T.z0[q] = T.z1[q] = T.z2[q] = T.h[q] = T.Dr[q] = 0.0; continue; }
-    const long ij = IJ(b, i, j);
-    const double z0 = F.zeta[ij + (long)(c.kstp - 1) * n2], z1 = F.zeta[ij + (long)(c.kbak - 1) * n2],
-                 z2 = F.zeta[ij + (long)(c.kold - 1) * n2], h = F.h[ij];
+    const long ij = IJ(b, i, j), ft = FT(i, j);
+    const double z0 = F.zeta[ft + (long)(c.kstp - 1) * n2], z1 = F.zeta[ft + (long)(c.kbak - 1) * n2],
+                 z2 = F.zeta[ft + (long)(c.kold - 1) * n2], h = F.h[ij];
     T.z0[q] = z0; T.z1[q] = z1; T.z2[q] = z2; T.h[q] = h;
     T.Dr[q] = h + c.fwd * z0 + c.fwd1 * z1 + c.fwd2 * z2;
   }
@@ -256,9 +264,9 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int cl
       const int i = i0 - 1 + q % kUX, j = j0 - 1 + q / kUX;
       double v = 0.0;
       if (i >= 0 && inarr(i, j)) {
-        const long ij = IJ(b, i, j);
-        const double urhs = c.fwd * F.ubar[ij + (long)(c.kstp - 1) * n2] + c.fwd1 * F.ubar[ij + (long)(c.kbak - 1) * n2] +
-                            c.fwd2 * F.ubar[ij + (long)(c.kold - 1) * n2];
+        const long ij = IJ(b, i, j), ft = FT(i, j);
+        const double urhs = c.fwd * F.ubar[ft + (long)(c.kstp - 1) * n2] + c.fwd1 * F.ubar[ft + (long)(c.kbak - 1) * n2] +
+                            c.fwd2 * F.ubar[ft + (long)(c.kold - 1) * n2];
         v = 0.5 * (T.Dr[G(i, j)] + T.Dr[G(i - 1, j)]) * F.dn_u[ij] * (urhs);
       }
       T.DU[q] = v;
@@ -267,9 +275,9 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int cl
       const int i = i0 - 1 + qq % kFX, j = j0 - 1 + qq / kFX;
       double v = 0.0;
       if (j >= 0 && inarr(i, j)) {
-        const long ij = IJ(b, i, j);
-        const double vrhs = c.fwd * F.vbar[ij + (long)(c.kstp - 1) * n2] + c.fwd1 * F.vbar[ij + (long)(c.kbak - 1) * n2] +
-                            c.fwd2 * F.vbar[ij + (long)(c.kold - 1) * n2];
+        const long ij = IJ(b, i, j), ft = FT(i, j);
+        const double vrhs = c.fwd * F.vbar[ft + (long)(c.kstp - 1) * n2] + c.fwd1 * F.vbar[ft + (long)(c.kbak - 1) * n2] +
+                            c.fwd2 * F.vbar[ft + (long)(c.kold - 1) * n2];
         v = 0.5 * (T.Dr[G(i, j)] + T.Dr[G(i, j - 1)]) * F.dm_v[ij] * (vrhs);
       }
       T.DV[qq] = v;
@@ -547,6 +555,9 @@ void launch_step2d(const Dev& d, hipStream_t s, const Tlev& t, const double* w1,
   c.w2 = w2[t.iif - 1];
   const bool closed = b.west_edge || b.east_edge || b.south_edge || b.north_edge;
   Range RB{b.istrR, b.iendR, b.jstrR, b.jendR};
+  // single rank (no halo exchange object) with the fused kernel: periodic
+  // halos of the fast-time fields are read through their images
+  const int vwrap = (d.halo == nullptr && !d.p.s2d_split) ? (b.ew_periodic ? 1 : 0) | (b.ns_periodic ? 2 : 0) : 0;
   if (d.p.s2d_split) {  // two-kernel form (kept for A/B timing)
     Range RA{b.istrU - 1, b.iend, b.jstrV - 1, b.jend};
     hipLaunchKernelGGL(k_s2d_zeta, grid_of(RA), dim3(kBX, kBY), 0, s, d, RA, c);
@@ -557,7 +568,7 @@ void launch_step2d(const Dev& d, hipStream_t s, const Tlev& t, const double* w1,
     }
     hipLaunchKernelGGL(k_s2d_mom, grid_of(RB), dim3(kBX, kBY), 0, s, d, RB, c);
   } else {
-    hipLaunchKernelGGL(k_s2d_fb, grid_of(RB), dim3(kBX, kBY), 0, s, d, RB, c, (int)closed);
+    hipLaunchKernelGGL(k_s2d_fb, grid_of(RB), dim3(kBX, kBY), 0, s, d, RB, c, (int)closed, vwrap);
   }
   if (closed) {
     const int L = b.nx2 > b.Mm + 4 ? b.nx2 : b.Mm + 4;
@@ -567,6 +578,12 @@ void launch_step2d(const Dev& d, hipStream_t s, const Tlev& t, const double* w1,
   if (t.iif == t.nfast) {
     hipLaunchKernelGGL(k_s2d_last, grid_of(RB), dim3(kBX, kBY), 0, s, d, RB, t.knew);
     launch_set_depth(d, s, t);
+  }
+  if (vwrap) {
+    // halos were read from periodic images during the loop; refresh all four
+    // time slots once at its end (the same values the per-step wraps give)
+    if (t.iif == t.nfast) launch_exchange_list(d, s, ExchList{{d.f.zeta, d.f.ubar, d.f.vbar}, {4, 4, 4}, 3});
+    return;
   }
   const long kn = (long)(t.knew - 1) * b.n2;
   launch_exchange_list(d, s, ExchList{{d.f.zeta + kn, d.f.ubar + kn, d.f.vbar + kn}, {1, 1, 1}, 3});
