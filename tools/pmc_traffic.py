@@ -20,7 +20,7 @@ ROUTINE_OF = {
     "k_omega_edges": "omega", "k_prsgrd_P": "prsgrd", "k_prsgrd_uv": "prsgrd", "k_pre_tracer_h": "pre_step3d",
     "k_pre_tracer_v": "pre_step3d", "k_rd": "pre_step3d", "k_pre_uv": "pre_step3d", "k_set_huv1": "set_HUV1",
     "k_uv1": "step3d_uv1", "k_visc3d": "visc3d", "k_s2d_zeta": "step2d", "k_s2d_mom": "step2d",
-    "k_s2d_zetabc": "step2d", "k_s2d_edges": "step2d", "k_s2d_last": "step2d", "k_set_depth": "step2d",
+    "k_s2d_zetabc": "step2d", "k_s2d_fb": "step2d", "k_visc3d_frc": "visc3d", "k_s2d_edges": "step2d", "k_s2d_last": "step2d", "k_set_depth": "step2d",
     "k_uv2_couple": "step3d_uv2", "k_uv2_flux": "step3d_uv2", "k_step3d_t_h": "step3d_t", "k_step3d_t_v": "step3d_t",
     "k_t3dmix": "t3dmix", "k_periodic_wrap": "halo", "k_halo_pack": "halo", "k_halo_unpack": "halo",
 }
