@@ -211,9 +211,46 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int cl
     if (vwrap & 2) j = j < 1 ? j + b.Mm : (j > b.Mm ? j - b.Mm : j);
     return IJ(b, i, j);
   };
-  // Independent global loads of the later phases are issued first, so their
-  // latency overlaps the staging phases (the grid is one wave of blocks: each
-  // block's critical path is the kernel time).
+  // All global loads are issued at entry -- the staging window first, then
+  // the face fluxes, then the later phases -- so each block waits for memory
+  // once (the grid is one wave of blocks: a block's critical path is the
+  // kernel time) and the window stores start as soon as their data lands.
+  double g_z0[2], g_z1[2], g_z2[2], g_h[2];
+#pragma unroll
+  for (int r = 0; r < 2; r++) {
+    const int q = tid + r * NT;
+    const int i = i0 - 2 + q % kGX, j = j0 - 2 + q / kGX;
+    g_z0[r] = g_z1[r] = g_z2[r] = g_h[r] = 0.0;
+    if (q < kGN && inarr(i, j)) {
+      const long ij = IJ(b, i, j), ft = FT(i, j);
+      g_z0[r] = F.zeta[ft + (long)(c.kstp - 1) * n2];
+      g_z1[r] = F.zeta[ft + (long)(c.kbak - 1) * n2];
+      g_z2[r] = F.zeta[ft + (long)(c.kold - 1) * n2];
+      g_h[r] = F.h[ij];
+    }
+  }
+  double f_a[3], f_b[3], f_c[3], f_d[3];  // 3 time levels of ubar/vbar and dn_u/dm_v at the thread's faces
+#pragma unroll
+  for (int r = 0; r < 3; r++) {
+    const int q = tid + r * NT;
+    f_a[r] = f_b[r] = f_c[r] = f_d[r] = 0.0;
+    if (q < kUN) {
+      const int i = i0 - 1 + q % kUX, j = j0 - 1 + q / kUX;
+      if (i >= 0 && inarr(i, j)) {
+        const long ij = IJ(b, i, j), ft = FT(i, j);
+        f_a[r] = F.ubar[ft + (long)(c.kstp - 1) * n2]; f_b[r] = F.ubar[ft + (long)(c.kbak - 1) * n2];
+        f_c[r] = F.ubar[ft + (long)(c.kold - 1) * n2]; f_d[r] = F.dn_u[ij];
+      }
+    } else if (q < kUN + kVN) {
+      const int qq = q - kUN;
+      const int i = i0 - 1 + qq % kFX, j = j0 - 1 + qq / kFX;
+      if (j >= 0 && inarr(i, j)) {
+        const long ij = IJ(b, i, j), ft = FT(i, j);
+        f_a[r] = F.vbar[ft + (long)(c.kstp - 1) * n2]; f_b[r] = F.vbar[ft + (long)(c.kbak - 1) * n2];
+        f_c[r] = F.vbar[ft + (long)(c.kold - 1) * n2]; f_d[r] = F.dm_v[ij];
+      }
+    }
+  }
   const int za = b.istrU - 1, zb = b.iend, zc = b.jstrV - 1, zd = b.jend;
   double e_pm[2], e_pn[2], e_sw[2], e_rm[2], e_rS[2], e_rA[2];
 #pragma unroll
@@ -234,7 +271,7 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int cl
   const long pij = pact ? IJ(b, pi, pj) : 0;
   double x_rA0 = 0, x_rAx = 0, x_rAy = 0, x_dnu = 0, x_dmv = 0, x_rufrc = 0, x_rvfrc = 0, x_ub = 0, x_vb = 0;
   double x_pmx = 0, x_pnx = 0, x_pmy = 0, x_pny = 0, x_pm0 = 0, x_pn0 = 0, x_um = 0, x_vm = 0, x_DU1 = 0, x_DV1 = 0;
-  double x_rS0 = 0, x_rSx = 0, x_rSy = 0;
+  double x_rS0 = 0, x_rSx = 0, x_rSy = 0, x_DU2 = 0, x_DV2 = 0, x_Zt = 0;
   if (pint) {
     const long lk = (long)(c.kstp - 1) * n2;
     x_rA0 = F.rhoA[pij]; x_rAx = F.rhoA[pij - 1]; x_rAy = F.rhoA[pij - sj];
@@ -245,40 +282,37 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int cl
     x_pmy = F.pm[pij - sj]; x_pny = F.pn[pij - sj];
     x_um = F.umask[pij]; x_vm = F.vmask[pij];
     x_DU1 = F.DU_avg1[pij]; x_DV1 = F.DV_avg1[pij];
+    x_DU2 = F.DU_avg2[pij]; x_DV2 = F.DV_avg2[pij]; x_Zt = F.Zt_avg1[pij];
     if (c.iif == 1) { x_rS0 = F.rhoS[pij]; x_rSx = F.rhoS[pij - 1]; x_rSy = F.rhoS[pij - sj]; }
   }
   // P0: time levels of zeta, h and Drhs = h + fwd*z(kstp) + fwd1*z(kbak) + fwd2*z(kold)
-  for (int q = tid; q < kGN; q += NT) {
-    const int i = i0 - 2 + q % kGX, j = j0 - 2 + q / kGX;
-    if (!inarr(i, j)) { T.z0[q] = T.z1[q] = T.z2[q] = T.h[q] = T.Dr[q] = 0.0; continue; }
-    const long ij = IJ(b, i, j), ft = FT(i, j);
-    const double z0 = F.zeta[ft + (long)(c.kstp - 1) * n2], z1 = F.zeta[ft + (long)(c.kbak - 1) * n2],
-                 z2 = F.zeta[ft + (long)(c.kold - 1) * n2], h = F.h[ij];
-    T.z0[q] = z0; T.z1[q] = z1; T.z2[q] = z2; T.h[q] = h;
-    T.Dr[q] = h + c.fwd * z0 + c.fwd1 * z1 + c.fwd2 * z2;
+#pragma unroll
+  for (int r = 0; r < 2; r++) {
+    const int q = tid + r * NT;
+    if (q >= kGN) break;
+    T.z0[q] = g_z0[r]; T.z1[q] = g_z1[r]; T.z2[q] = g_z2[r]; T.h[q] = g_h[r];
+    T.Dr[q] = g_h[r] + c.fwd * g_z0[r] + c.fwd1 * g_z1[r] + c.fwd2 * g_z2[r];
   }
   __syncthreads();
   // P1: barotropic fluxes DUon (u faces) and DVom (v faces), once each
-  for (int q = tid; q < kUN + kVN; q += NT) {
+#pragma unroll
+  for (int r = 0; r < 3; r++) {
+    const int q = tid + r * NT;
     if (q < kUN) {
       const int i = i0 - 1 + q % kUX, j = j0 - 1 + q / kUX;
       double v = 0.0;
       if (i >= 0 && inarr(i, j)) {
-        const long ij = IJ(b, i, j), ft = FT(i, j);
-        const double urhs = c.fwd * F.ubar[ft + (long)(c.kstp - 1) * n2] + c.fwd1 * F.ubar[ft + (long)(c.kbak - 1) * n2] +
-                            c.fwd2 * F.ubar[ft + (long)(c.kold - 1) * n2];
-        v = 0.5 * (T.Dr[G(i, j)] + T.Dr[G(i - 1, j)]) * F.dn_u[ij] * (urhs);
+        const double urhs = c.fwd * f_a[r] + c.fwd1 * f_b[r] + c.fwd2 * f_c[r];
+        v = 0.5 * (T.Dr[G(i, j)] + T.Dr[G(i - 1, j)]) * f_d[r] * (urhs);
       }
       T.DU[q] = v;
-    } else {
+    } else if (q < kUN + kVN) {
       const int qq = q - kUN;
       const int i = i0 - 1 + qq % kFX, j = j0 - 1 + qq / kFX;
       double v = 0.0;
       if (j >= 0 && inarr(i, j)) {
-        const long ij = IJ(b, i, j), ft = FT(i, j);
-        const double vrhs = c.fwd * F.vbar[ft + (long)(c.kstp - 1) * n2] + c.fwd1 * F.vbar[ft + (long)(c.kbak - 1) * n2] +
-                            c.fwd2 * F.vbar[ft + (long)(c.kold - 1) * n2];
-        v = 0.5 * (T.Dr[G(i, j)] + T.Dr[G(i, j - 1)]) * F.dm_v[ij] * (vrhs);
+        const double vrhs = c.fwd * f_a[r] + c.fwd1 * f_b[r] + c.fwd2 * f_c[r];
+        v = 0.5 * (T.Dr[G(i, j)] + T.Dr[G(i, j - 1)]) * f_d[r] * (vrhs);
       }
       T.DV[qq] = v;
     }
@@ -361,17 +395,17 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int cl
     F.zeta[ij + (long)(c.knew - 1) * n2] = z;
     const double du = DU(i, j), dv = DV(i, j);
     if (c.iif == 1) {
-      F.DU_avg_bak[ij] = F.DU_avg1[ij] - 0.1024390243902439 * F.DU_avg2[ij];
-      F.DV_avg_bak[ij] = F.DV_avg1[ij] - 0.1024390243902439 * F.DV_avg2[ij];
+      F.DU_avg_bak[ij] = (pint ? x_DU1 : F.DU_avg1[ij]) - 0.1024390243902439 * (pint ? x_DU2 : F.DU_avg2[ij]);
+      F.DV_avg_bak[ij] = (pint ? x_DV1 : F.DV_avg1[ij]) - 0.1024390243902439 * (pint ? x_DV2 : F.DV_avg2[ij]);
       F.Zt_avg1[ij] = c.w1 * z;
       F.DU_avg1[ij] = 0.0;
       F.DV_avg1[ij] = 0.0;
       F.DU_avg2[ij] = c.w2 * du;
       F.DV_avg2[ij] = c.w2 * dv;
     } else {
-      F.Zt_avg1[ij] = F.Zt_avg1[ij] + c.w1 * z;
-      F.DU_avg2[ij] = F.DU_avg2[ij] + c.w2 * du;
-      F.DV_avg2[ij] = F.DV_avg2[ij] + c.w2 * dv;
+      F.Zt_avg1[ij] = (pint ? x_Zt : F.Zt_avg1[ij]) + c.w1 * z;
+      F.DU_avg2[ij] = (pint ? x_DU2 : F.DU_avg2[ij]) + c.w2 * du;
+      F.DV_avg2[ij] = (pint ? x_DV2 : F.DV_avg2[ij]) + c.w2 * dv;
     }
   }
   if (!pint) return;
