@@ -13,7 +13,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB = os.path.join(_HERE, "liboracle.so")
-CASE_FILAMENT, CASE_BASIN = 0, 1
+CASE_FILAMENT, CASE_BASIN, CASE_PIPES = 0, 1, 2
 
 
 class OrCfg(ctypes.Structure):
@@ -82,6 +82,26 @@ def filament_cfg(LLm=64, MMm=64, N=32, NT=1, salinity=False, sizex=12.8e3, sizey
     c.rdrg, c.rdrg2, c.Zob = 0.0, 1.0e-3, 1.0e-2
     c.Tcoef, c.T0, c.Scoef, c.S0 = 0.20, 1.0, 0.822, 1.0
     c.sizex, c.sizey = sizex, sizey
+    c.diag_np_xi, c.diag_np_eta = np_xi, np_eta
+    return c
+
+
+def pipes_cfg(LLm=100, MMm=100, N=10, np_xi=3, np_eta=2):
+    """tests/Pipes_ana/{param.opt,benchmark.in,cppdefs.opt,ana_grid.h,ana_init.h,ana_pipe_frc.h}:
+    KPP/BKPP/RIMIX/CONVEC/NONLOCAL, NONLIN+SPLIT EOS, T+S, land mask, one pipe.
+    benchmark.in has no vertical_mixing line, so Akv_bak = Akt_bak = 0."""
+    c = OrCfg()
+    c.LLm, c.MMm, c.N, c.NT = LLm, MMm, N, 2
+    c.ew_periodic = c.ns_periodic = 0
+    c.salinity, c.nonlin_eos, c.lmd = 1, 1, 1
+    c.case_id = CASE_PIPES
+    c.dt, c.ndtfast = 60.0, 30
+    c.theta_s, c.theta_b, c.hc, c.rho0 = 6.0, 6.0, 25.0, 1027.5
+    c.visc2, c.tnu2 = 0.0, 0.0
+    c.rdrg, c.rdrg2, c.Zob = 0.0, 1.0e-3, 1.0e-2
+    c.Akv_bak = 0.0
+    c.Akt_bak[0] = c.Akt_bak[1] = 0.0
+    c.sizex, c.sizey = 30.0e3, 30.0e3
     c.diag_np_xi, c.diag_np_eta = np_xi, np_eta
     return c
 

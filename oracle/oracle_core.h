@@ -39,6 +39,11 @@ struct or_state {
   double *rho, *rho1, *qp1, *bvf;
   double *Akv, *Akt, *visc2_r, *visc2_p, *diff2;
   double *hbls, *hbbl, *ghat, *swr_frac;
+  double *lmdKv, *lmdKt, *lmdKs, *lmdRig;  /* lmd_vmix A3d scratch (0:N) */
+  double *lmd2[9];                         /* lmd_kpp A2d scratch */
+  /* pipe_frc.F (npip = 1, analytic): pipe_idx>0 cells carry pipe_flx */
+  int pipe_source;
+  double *pipe_flx, *pipe_idx, pipe_prf[1024], pipe_trc[2];
   /* forcing */
   double *sustr, *svstr, *stflx, *srflx, *swflx;
   /* private scratch (A3d(:,1..4), A2d(:,1..)) */
@@ -100,4 +105,5 @@ void or_ana_forces(or_state *S);
 /* LMD/KPP (oracle_lmd.c) */
 void or_lmd_vmix_impl(or_state *S, int tind);
 void or_lmd_alloc(or_state *S);
+void or_swr_frac(or_state *S);
 #endif

@@ -61,6 +61,7 @@ or_state *or_create(const or_cfg *cfg) {
   for (int q = 0; q < 14; q++) S->s2[q] = zalloc(n2);
   for (int q = 0; q < 6; q++) S->c1[q] = zalloc((size_t)S->nx2 * (S->N + 1));
   if (cfg->lmd) or_lmd_alloc(S);
+  S->pipe_flx = zalloc(n2); S->pipe_idx = zalloc(n2);
   return S;
 }
 
@@ -388,6 +389,51 @@ void or_ana_grid(or_state *S) {
       for (int i = -1; i <= nx + 2; i++) A2(S->f, i, j) = f0 + beta * (A2(S->yr, i, j) - y0);
     for (int j = -1; j <= ny + 2; j++)
       for (int i = -1; i <= nx + 2; i++) { A2(S->h, i, j) = 1000; A2(S->rmask, i, j) = 1; }
+  } else if (S->c.case_id == OR_CASE_PIPES) {
+    /* tests/Pipes_ana/ana_grid.h:19-131 (single rank: iSW_corn = jSW_corn = 0) */
+    const double SizeX = S->c.sizex, SizeY = S->c.sizey, f0 = 1.0e-4, beta = 0;
+    const double dx = SizeX / S->c.LLm, dy = SizeY / S->c.MMm;
+    double x0 = 0., y0 = 0.;
+    for (int j = -1; j <= ny + 2; j++)
+      for (int i = -1; i <= nx + 2; i++) {
+        A2(S->xr, i, j) = x0 + dx * ((double)i - 0.5);
+        A2(S->yr, i, j) = y0 + dy * ((double)j - 0.5);
+        A2(S->pm, i, j) = 1. / dx;
+        A2(S->pn, i, j) = 1. / dy;
+      }
+    x0 = SizeX / 2.; y0 = SizeY / 2.;
+    for (int j = -1; j <= ny + 2; j++)
+      for (int i = -1; i <= nx + 2; i++) A2(S->f, i, j) = f0 + beta * (A2(S->yr, i, j) - y0);
+    const double depth = 10, max_depth = 100;
+    const double shelf = SizeY / 5, slope = (max_depth - depth) / (SizeY * 4 / 5);
+    for (int j = -1; j <= ny + 2; j++)
+      for (int i = -1; i <= nx + 2; i++) {
+        if (A2(S->yr, i, j) < shelf) A2(S->h, i, j) = depth;
+        else A2(S->h, i, j) = depth + (A2(S->yr, i, j) - shelf) * slope;
+      }
+    const double land = SizeY * 0.1, coast = SizeY * 0.02, riv_west = SizeX * 0.4, riv_east = SizeX * 0.6;
+    for (int j = -1; j <= ny + 2; j++)
+      for (int i = -1; i <= nx + 2; i++) {
+        A2(S->rmask, i, j) = 1;
+        if (A2(S->yr, i, j) < land)
+          if (A2(S->xr, i, j) < riv_west || A2(S->xr, i, j) > riv_east) A2(S->rmask, i, j) = 0.0;
+        if (A2(S->yr, i, j) < coast) A2(S->rmask, i, j) = 0.0;
+      }
+    /* pipe location; ana_pipe_frc.h: pipe_vol = 5e2, pipe_trc = (24, 1), pipe_prf(1:2) = 0.5 */
+    const double psz = SizeX * 0.02, px = SizeX * .5, py = SizeY * .5;
+    const double pipe_cells = (double)(lround(psz / dx) * lround(psz / dx));
+    S->pipe_source = 1;
+    for (int k = 0; k < S->N; k++) S->pipe_prf[k] = 0.0;
+    S->pipe_prf[0] = 0.5; S->pipe_prf[1] = 0.5;
+    S->pipe_trc[0] = 24.0; S->pipe_trc[1] = 1.0;
+    for (int j = -1; j <= ny + 2; j++)
+      for (int i = -1; i <= nx + 2; i++) {
+        double frac = 0.0, idx = 0.0;
+        if (A2(S->xr, i, j) > px - 0.5 * psz && A2(S->xr, i, j) < px + 0.5 * psz)
+          if (A2(S->yr, i, j) > py - 0.5 * psz && A2(S->yr, i, j) < py + 0.5 * psz) { frac = 1.0 / pipe_cells; idx = 1; }
+        A2(S->pipe_idx, i, j) = idx;
+        A2(S->pipe_flx, i, j) = frac * 5e2;
+      }
   } else {
     /* synthetic closed basin (C3 stand-in) */
     const double dx = S->c.sizex / S->c.LLm, dy = S->c.sizey / S->c.MMm;
@@ -469,6 +515,16 @@ void or_ana_init(or_state *S) {
         ZETA(i, j, 2) = ZETA(i, j, 1);
         for (int k = 1; k <= nz; k++) { U(i, j, k, 1) = 0.; U(i, j, k, 2) = U(i, j, k, 1); V(i, j, k, 2) = V(i, j, k, 1); }
       }
+  } else if (S->c.case_id == OR_CASE_PIPES) {
+    /* tests/Pipes_ana/ana_init.h:14-52: rest state, T = 4 + 10 e^{z/50}, S = 36 */
+    for (int k = 1; k <= nz; k++)
+      for (int j = 0; j <= ny + 1; j++)
+        for (int i = 0; i <= nx + 1; i++) {
+          TT(i, j, k, 1, 1) = 4. + 10. * exp(ZR(i, j, k) / 50.);
+          TT(i, j, k, 1, 2) = 36.;
+          TT(i, j, k, 2, 1) = TT(i, j, k, 1, 1);
+          TT(i, j, k, 2, 2) = TT(i, j, k, 1, 2);
+        }
   } else {
     /* synthetic basin: stratified T, weak S gradient, at rest */
     const double Lx = S->c.sizex, Ly = S->c.sizey, pi = 3.14159265358979323;
@@ -522,10 +578,12 @@ int or_init(or_state *S) {
   for (size_t q = 0; q < S->n2; q++) { S->visc2_r[q] = S->c.visc2; S->visc2_p[q] = S->c.visc2; }
   for (size_t q = 0; q < S->n2 * S->NT; q++) S->diff2[q] = S->c.tnu2;
   or_set_depth(S);
+  if (S->c.lmd) or_swr_frac(S);  /* main.F:217-220 */
   or_ana_forces(S);
   or_ana_init(S);
-  /* ana_vmix: only active when iic==forw_start, i.e. never at init (main.F:257) */
-  if (S->c.case_id != OR_CASE_FILAMENT) {
+  /* ana_vmix: only active when iic==forw_start, i.e. never at init (main.F:257);
+     with LMD_MIXING mixing.F:163-181 leaves Akv = Akt = 0 */
+  if (S->c.case_id != OR_CASE_FILAMENT && !S->c.lmd) {
     for (size_t q = 0; q < S->n3w; q++) S->Akv[q] = S->c.Akv_bak;
     for (int it = 1; it <= S->nTS; it++)
       for (size_t q = 0; q < S->n3w; q++) S->Akt[q + (size_t)(it - 1) * S->n3w] = S->c.Akt_bak[it - 1];

@@ -291,6 +291,8 @@ void or_omega(or_state *S) {
     for (int k = 1; k <= N; k++)
       for (int i = S->istr; i <= S->iend; i++) {
         WI(i, j, k) = WI(i, j, k - 1) - FLXU(i + 1, j, k) + FLXU(i, j, k) - FLXV(i, j + 1, k) + FLXV(i, j, k);
+        if (S->pipe_source && A2(S->pipe_idx, i, j) > 0)  /* omega.F:102-108 */
+          WI(i, j, k) = WI(i, j, k) + A2(S->pipe_flx, i, j) * S->pipe_prf[k - 1];
         C1(CX, i, k) = fmax0(FLXU(i + 1, j, k)) - fmin0(FLXU(i, j, k)) + fmax0(FLXV(i, j + 1, k)) -
                        fmin0(FLXV(i, j, k));
       }
@@ -1250,6 +1252,8 @@ void or_step2d(or_state *S) {
       A2(zeta_new, i, j) = ZETA(i, j, kstp) + S->dtfast * A2(S->pm, i, j) * A2(S->pn, i, j) *
                                                   (A2(DUon, i, j) - A2(DUon, i + 1, j) + A2(DVom, i, j) - A2(DVom, i, j + 1)) +
                            S->dtfast * A2(S->swflx, i, j);
+      if (S->pipe_source && A2(S->pipe_idx, i, j) > 0.)  /* step2d_FB.F:155-159 */
+        A2(zeta_new, i, j) = A2(zeta_new, i, j) + S->dtfast * A2(S->pm, i, j) * A2(S->pn, i, j) * A2(S->pipe_flx, i, j);
       A2(zeta_new, i, j) = A2(zeta_new, i, j) * A2(S->rmask, i, j);
       A2(Dnew, i, j) = A2(zeta_new, i, j) + A2(h, i, j);
       A2(zwrk, i, j) = bkw_new * A2(zeta_new, i, j) + bkw * ZETA(i, j, kstp) + bkw1 * ZETA(i, j, kbak) + bkw2 * ZETA(i, j, kold);
@@ -1539,9 +1543,14 @@ void or_step3d_t(or_state *S) {
     for (int j = S->jstr; j <= S->jend; j++) {
       vert_tracer_fluxes(S, j, itrc, nrhs, FC, CF, S->Hz);
       for (int k = 1; k <= N; k++)
-        for (int i = S->istr; i <= S->iend; i++)
+        for (int i = S->istr; i <= S->iend; i++) {
           TT(i, j, k, nnew, itrc) =
               TT(i, j, k, nnew, itrc) - dt * A2(S->pm, i, j) * A2(S->pn, i, j) * (C1(FC, i, k) - C1(FC, i, k - 1));
+          if (S->pipe_source && A2(S->pipe_idx, i, j) > 0.)  /* step3d_t_ISO.F:927-934 */
+            TT(i, j, k, nnew, itrc) = TT(i, j, k, nnew, itrc) + dt * A2(S->pm, i, j) * A2(S->pn, i, j) *
+                                                                    A2(S->pipe_flx, i, j) * S->pipe_prf[k - 1] *
+                                                                    S->pipe_trc[itrc - 1];
+        }
       if (itrc == 1)
         for (int i = S->istr; i <= S->iend; i++)
           TT(i, j, N, nnew, itrc) = TT(i, j, N, nnew, itrc) + dt * A2(S->swflx, i, j) * TT(i, j, N, nnew, itrc) / HZ(i, j, N);

@@ -24,7 +24,7 @@ extern "C" {
 #endif
 
 /* analytic case selector */
-enum { OR_CASE_FILAMENT = 0, OR_CASE_BASIN = 1 };
+enum { OR_CASE_FILAMENT = 0, OR_CASE_BASIN = 1, OR_CASE_PIPES = 2 };
 
 typedef struct or_cfg {
   int LLm, MMm, N, NT;           /* interior dims, tracers (T[,S,passive]) */

@@ -15,7 +15,9 @@ CASES = {
     "filament_github_gnu": ("Filament/benchmark.result_github_gnu", 20),
     "filament_github_ifx": ("Filament/benchmark.result_github_ifx", 20),
     "pipes_ana_github_gnu": ("Pipes_ana/benchmark.result_github_gnu", 20),
+    "pipes_ana_github_ifx": ("Pipes_ana/benchmark.result_github_ifx", 20),
     "rivers_ana_github_gnu": ("Rivers_ana/benchmark.result_github_gnu", 20),
+    "rivers_ana_github_ifx": ("Rivers_ana/benchmark.result_github_ifx", 20),
 }
 
 
