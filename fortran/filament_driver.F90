@@ -19,8 +19,8 @@ program filament_driver
   end if
   c%case_id = 0; c%LLm = 64; c%MMm = 64; c%N = 32; c%NT = 1
   c%salinity = 0; c%nonlin_eos = 0; c%lmd_mixing = 0
-  c%dt = 5.0d0; c%ndtfast = 60; c%sizex = 12.8d3; c%sizey = 3.2d3
-  if (roms_gpu_abi_version() /= 2) error stop 'ABI version mismatch'
+  c%dt = 5.0d0; c%ndtfast = 60; c%sizex = 12.8d3; c%sizey = 3.2d3; c%surf_flux = 0
+  if (roms_gpu_abi_version() /= ROMS_GPU_ABI) error stop 'ABI version mismatch'
   call roms_gpu_check(roms_gpu_init_case(c, 0_c_int, t), 'init_case')
   call roms_gpu_check(roms_gpu_diag(t, norms), 'diag')
   write(*, '(i6,4es24.16)') 0, norms

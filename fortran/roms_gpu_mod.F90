@@ -38,7 +38,10 @@ module roms_gpu_mod
     real(c_double) :: dt
     integer(c_int) :: ndtfast
     real(c_double) :: sizex, sizey
+    integer(c_int) :: surf_flux
   end type
+
+  integer(c_int), parameter :: ROMS_GPU_ABI = 3   ! ROMS_GPU_ABI_VERSION, include/roms_gpu.h
 
   ! field ids (enum roms_field) used by the drivers below
   integer(c_int), parameter :: ROMS_zeta = 22, ROMS_ubar = 23, ROMS_vbar = 24, ROMS_u = 25, ROMS_v = 26, &
@@ -146,6 +149,18 @@ module roms_gpu_mod
     integer(c_int) function roms_gpu_set_depth(t) bind(c)
       import :: c_int, roms_tlev
       type(roms_tlev), intent(in) :: t
+    end function
+    integer(c_int) function roms_gpu_swr_frac(t) bind(c)
+      import :: c_int, roms_tlev
+      type(roms_tlev), intent(in) :: t
+    end function
+    ! after set_forces' set_pipe_frc (pipe_frc.F:33): pipe_idx(GLOBAL_2D_ARRAY) integer,
+    ! pipe_flx(GLOBAL_2D_ARRAY), pipe_prf(npip,N), pipe_trc(npip,nt)
+    integer(c_int) function roms_gpu_set_pipe_frc(npip, pipe_idx, pipe_flx, pipe_prf, pipe_trc) bind(c)
+      import :: c_int, c_double
+      integer(c_int), value :: npip
+      integer(c_int), intent(in) :: pipe_idx(*)
+      real(c_double), intent(in) :: pipe_flx(*), pipe_prf(*), pipe_trc(*)
     end function
     integer(c_int) function roms_gpu_step(t) bind(c)
       import :: c_int, roms_tlev

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define ROMS_GPU_ABI_VERSION 2
+#define ROMS_GPU_ABI_VERSION 3
 #define ROMS_MAX_FAST 288
 
 /* Subdomain geometry of this rank: param.F / dimensions.F / mpi_setup.F:39-210 */
@@ -118,6 +118,13 @@ int roms_gpu_step2d(const roms_tlev *t);              /* step2d           step2d
 int roms_gpu_step3d_uv2(const roms_tlev *t);          /* step3d_uv2(tile) step3d_uv2.F:6   */
 int roms_gpu_step3d_t(const roms_tlev *t);            /* step3d_t(tile)   step3d_t_ISO.F:20*/
 int roms_gpu_t3dmix(const roms_tlev *t);              /* t3dmix           t3dmix_S.F:4     */
+int roms_gpu_swr_frac(const roms_tlev *t);            /* swr_frac(tile)   lmd_swr_frac.F:4 */
+/* set_pipe_frc (pipe_frc.F:33-80): the host's pipe_idx (0 = no pipe) and
+ * pipe_flx on the (-1:Lm+2,-1:Mm+2) grid, pipe_prf(npip,N) and
+ * pipe_trc(npip,NT) column-major.  npip = 0 switches pipe sources off.
+ * Call again whenever set_forces updates them; the next step uses them.      */
+int roms_gpu_set_pipe_frc(int npip, const int *pipe_idx, const double *pipe_flx, const double *pipe_prf,
+                          const double *pipe_trc);
 int roms_gpu_set_depth(const roms_tlev *t);           /* set_depth(tile)  set_depth.F:4    */
 
 /* One whole roms_step (main.F:333-520, forcing held fixed): advances t->iic
@@ -129,12 +136,13 @@ int roms_gpu_step(roms_tlev *t);
 int roms_gpu_init_sequence(roms_tlev *t);
 
 /* ---- analytic cases (host-side ana_grid/ana_init restatements) ---- */
-enum roms_case_id { ROMS_CASE_FILAMENT = 0, ROMS_CASE_BASIN = 1 };
+enum roms_case_id { ROMS_CASE_FILAMENT = 0, ROMS_CASE_BASIN = 1, ROMS_CASE_PIPES = 2 };
 typedef struct roms_case {
   int case_id, LLm, MMm, N, NT;
   int salinity, nonlin_eos, lmd_mixing;
   double dt; int ndtfast;
   double sizex, sizey;
+  int surf_flux;  /* basin only: analytic cooling, short-wave and salt fluxes (else 0) */
 } roms_case;
 /* Builds the analytic grid/ICs on the host (setup_grid1/2, set_scoord,
  * set_weights, ana_init), initialises the device and runs roms_init.        */
@@ -172,7 +180,7 @@ int roms_gpu_time_steps(roms_tlev *t, int n, double *ms);
 enum roms_routine {
   ROMS_R_RHO_EOS = 0, ROMS_R_SET_HUV, ROMS_R_OMEGA, ROMS_R_PRSGRD, ROMS_R_PRE_STEP3D, ROMS_R_SET_HUV1,
   ROMS_R_STEP3D_UV1, ROMS_R_VISC3D, ROMS_R_STEP2D, ROMS_R_STEP3D_UV2, ROMS_R_STEP3D_T, ROMS_R_T3DMIX,
-  ROMS_R_COUNT
+  ROMS_R_LMD_VMIX, ROMS_R_COUNT
 };
 int roms_gpu_time_routine(int routine, int nsteps, roms_tlev *t, double *avg_ms, long *launches);
 

@@ -28,7 +28,7 @@ class OrCfg(ctypes.Structure):
                 ("Akv_bak", ctypes.c_double), ("Akt_bak", ctypes.c_double * 2),
                 ("Tcoef", ctypes.c_double), ("T0", ctypes.c_double), ("Scoef", ctypes.c_double),
                 ("S0", ctypes.c_double), ("sizex", ctypes.c_double), ("sizey", ctypes.c_double),
-                ("diag_np_xi", ctypes.c_int), ("diag_np_eta", ctypes.c_int)]
+                ("diag_np_xi", ctypes.c_int), ("diag_np_eta", ctypes.c_int), ("surf_flux", ctypes.c_int)]
 
 
 def build():
@@ -62,9 +62,10 @@ def lib():
         L.or_destroy.argtypes = [ctypes.c_void_p]
         for fn in ("or_set_HUV", "or_omega", "or_prsgrd", "or_pre_step3d", "or_set_HUV1", "or_step3d_uv1",
                    "or_visc3d", "or_step2d", "or_step3d_uv2", "or_step3d_t", "or_t3dmix", "or_set_depth",
-                   "or_diag"):
+                   "or_diag", "or_swr_frac"):
             getattr(L, fn).argtypes = [ctypes.c_void_p]
         L.or_rho_eos.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.or_lmd_vmix.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.or_set_iif.argtypes = [ctypes.c_void_p, ctypes.c_int]
         _lib = L
     return _lib

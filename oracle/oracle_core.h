@@ -105,5 +105,4 @@ void or_ana_forces(or_state *S);
 /* LMD/KPP (oracle_lmd.c) */
 void or_lmd_vmix_impl(or_state *S, int tind);
 void or_lmd_alloc(or_state *S);
-void or_swr_frac(or_state *S);
 #endif

@@ -559,6 +559,12 @@ void or_ana_forces(or_state *S) {
       for (int i = -1; i <= S->Lm + 2; i++) {
         A2(S->sustr, i, j) = 1.0e-4 * sin(pi * A2(S->yr, i, j) / S->c.sizey);
         A2(S->svstr, i, j) = 0.0;
+        if (S->c.surf_flux) {  /* synthetic ana_stflux/ana_srflux: cooling, short-wave, evaporation */
+          const double x = A2(S->xr, i, j), y = A2(S->yr, i, j);
+          A2(S->stflx, i, j) = -1.0e-4 * (1.0 + 0.5 * cos(2.0 * pi * x / S->c.sizex));
+          A2(S->srflx, i, j) = 4.0e-5 * (1.0 + 0.5 * sin(pi * y / S->c.sizey));
+          if (S->c.salinity) S->stflx[O2(i, j) + S->n2] = 1.0e-7 * cos(pi * y / S->c.sizey);
+        }
       }
   }
 }

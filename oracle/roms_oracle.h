@@ -41,6 +41,7 @@ typedef struct or_cfg {
   double Tcoef, T0, Scoef, S0;
   double sizex, sizey;           /* analytic domain size [m] */
   int diag_np_xi, diag_np_eta;   /* rank layout emulated in diag sums */
+  int surf_flux;                 /* basin: analytic cooling/short-wave/salt fluxes */
 } or_cfg;
 
 typedef struct or_state or_state;
@@ -78,6 +79,7 @@ void or_step3d_t(or_state *S);
 void or_t3dmix(or_state *S);
 void or_set_depth(or_state *S);
 void or_lmd_vmix(or_state *S, int tind);
+void or_swr_frac(or_state *S);
 void or_diag(or_state *S);
 void or_set_tindex(or_state *S, const int in[6]);
 void or_set_iif(or_state *S, int iif);

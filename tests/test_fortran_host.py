@@ -23,7 +23,8 @@ def test_dropins_keep_reference_signatures():
     argument list (no-arg / tile / tidx / tind)."""
     want = {"step2d": "", "prsgrd": "", "omega": "", "set_HUV": "", "visc3d": "", "t3dmix": "",
             "pre_step3d": "tile", "set_HUV1": "tile", "step3d_uv1": "tile", "step3d_uv2": "tile",
-            "step3d_t": "tile", "set_depth": "tile", "rho_eos": "tidx", "lmd_vmix": "tind"}
+            "step3d_t": "tile", "set_depth": "tile", "rho_eos": "tidx", "lmd_vmix": "tind",
+            "swr_frac": "tile"}
     for name, arg in want.items():
         src = open(os.path.join(FDIR, "dropin", name + ".F")).read()
         head = "subroutine %s%s" % (name, "(%s)" % arg if arg else "")

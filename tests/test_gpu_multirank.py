@@ -33,8 +33,14 @@ def _case(kind):
     if kind == "filament":
         return dict(case_id=0, LLm=40, MMm=30, N=12, NT=1, salinity=False, nonlin_eos=False, dt=5.0, ndtfast=60,
                     sizex=8.0e3, sizey=1.5e3)
+    if kind == "pipes":   # tests/Pipes_ana: KPP/BKPP, land mask, pipe sources
+        return dict(case_id=2, LLm=50, MMm=50, N=10, NT=2, salinity=True, nonlin_eos=True, dt=60.0, ndtfast=30,
+                    sizex=30e3, sizey=30e3, lmd=True)
+    if kind == "basin_flux":   # LMD with surface cooling/short-wave (convective KPP branches)
+        return dict(case_id=1, LLm=36, MMm=28, N=20, NT=2, salinity=True, nonlin_eos=True, dt=60.0, ndtfast=30,
+                    sizex=72e3, sizey=56e3, lmd=True, surf_flux=True)
     return dict(case_id=1, LLm=36, MMm=28, N=10, NT=2, salinity=True, nonlin_eos=True, dt=60.0, ndtfast=30,
-                sizex=72e3, sizey=56e3)
+                sizex=72e3, sizey=56e3, lmd=(kind == "basin_lmd"))
 
 
 def run_decomposed(case, npx, npe, nsteps, fields=FIELDS, diag=False):
@@ -78,19 +84,22 @@ def window(a, iSW, jSW, Lm, Mm):
     return a[..., jSW:jSW + Mm + 4, iSW:iSW + Lm + 4]
 
 
-EXCHANGED = ("zeta", "ubar", "vbar", "u", "v", "t", "FlxU", "FlxV", "We", "Wi", "Hz", "z_r", "z_w")
+EXCHANGED = ("zeta", "ubar", "vbar", "u", "v", "t", "FlxU", "FlxV", "We", "Wi", "Hz", "z_r", "z_w",
+             "Akv", "Akt", "hbls", "hbbl")
+LMD_FIELDS = ("Akv", "Akt", "hbls", "hbbl", "ghat", "swr_frac")
 
 
-@pytest.mark.parametrize("kind", ["filament", "basin"])
+@pytest.mark.parametrize("kind", ["filament", "basin", "basin_lmd", "basin_flux", "pipes"])
 @pytest.mark.parametrize("npx,npe", [(2, 1), (1, 2), (2, 2), (3, 2)])
 def test_decomposition_bitwise_equals_single_domain(kind, npx, npe):
     case = _case(kind)
     per = case["case_id"] == 0
+    fields = FIELDS + (LMD_FIELDS if case.get("lmd") else ())
     m = romsgpu.Model.from_case(**case)
     m.step(5)
-    ref = {f: m.get(f) for f in FIELDS}
+    ref = {f: m.get(f) for f in fields}
     m.close()
-    parts, _ = run_decomposed(case, npx, npe, 5)
+    parts, _ = run_decomposed(case, npx, npe, 5, fields=fields)
     bad = []
     for rank, (iSW, jSW, Lm, Mm, got) in enumerate(parts):
         jn, inn = divmod(rank, npx)
@@ -100,7 +109,7 @@ def test_decomposition_bitwise_equals_single_domain(kind, npx, npe):
         j_lo = 0 if (not per and jn == 0) else 1
         j_hi = Mm + 1 if (not per and jn == npe - 1) else Mm
         own = (Ellipsis, slice(j_lo + 1, j_hi + 2), slice(i_lo + 1, i_hi + 2))
-        for f in FIELDS:
+        for f in fields:
             w = window(ref[f], iSW, jSW, Lm, Mm)
             g = got[f]
             if not np.array_equal(g[own], w[own]):
@@ -126,6 +135,24 @@ def test_filament_3x2_matches_golden_digits():
         if want != have:
             bad.append((s, want, have))
     assert not bad, bad[:3]
+
+
+def test_pipes_ana_3x2_within_compiler_spread():
+    """Pipes_ana (KPP, land mask, pipe) on the reference's 3x2 grid: every
+    printed norm within the gfortran/ifx spread of the golden logs."""
+    keys = ("ke", "ke2b", "cu_adv", "cu_w")
+    gnu = json.load(open(os.path.join(ROOT, "tests", "golden", "pipes_ana_github_gnu.json")))["rows"]
+    ifx = json.load(open(os.path.join(ROOT, "tests", "golden", "pipes_ana_github_ifx.json")))["rows"]
+    spread = max(abs(float(x[k]) - float(g[k])) / abs(float(g[k])) for g, x in zip(gnu, ifx) for k in keys
+                 if float(g[k]) != 0.0)
+    case = dict(case_id=2, LLm=100, MMm=100, N=10, NT=2, salinity=True, nonlin_eos=True, dt=60.0, ndtfast=30,
+                sizex=30e3, sizey=30e3, lmd=True)
+    _, norms = run_decomposed(case, 3, 2, 20, fields=("zeta",), diag=True)
+    assert len(norms) == 21
+    assert [("%23.16E" % v).strip() for v in norms[0]] == [gnu[0][k] for k in keys]
+    worst = max(abs(v - float(g[k])) / abs(float(g[k])) for g, n in zip(gnu, norms) for k, v in zip(keys, n)
+                if float(g[k]) != 0.0)
+    assert worst <= spread, (worst, spread)
 
 
 RCCL_SCRIPT = r"""

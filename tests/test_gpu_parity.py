@@ -58,7 +58,11 @@ def relerr(a, b):
 
 
 def rms(a, b):
-    return float(np.sqrt(np.mean((a - b) ** 2)))
+    """Field RMS error, in the field's units for O(1) fields (zeta, u, t ...)
+    and relative to the field's own RMS when that exceeds 1 (FlxU, FlxV, We,
+    Wi in m^3/s, depths and layer thicknesses in m)."""
+    scale = max(1.0, float(np.sqrt(np.mean(b ** 2))))
+    return float(np.sqrt(np.mean((a - b) ** 2))) / scale
 
 
 def copy_state(o, m):

@@ -190,6 +190,40 @@ void build_case(const CaseSpec& cs, HostState& H, double& area, double& volume) 
         A(kh, i, j) = 1000;
         A(krmask, i, j) = 1;
       }
+  } else if (cs.case_id == ROMS_CASE_PIPES) {
+    // tests/Pipes_ana/ana_grid.h:19-131: shelf + slope, land strip with a river gap, one pipe
+    const double SizeX = cs.sizex, SizeY = cs.sizey, f0 = 1.0e-4, beta = 0;
+    const double dx = SizeX / cs.LLm, dy = SizeY / cs.MMm;
+    const double x0 = dx * (double)cs.iSW_corn, y0 = dy * (double)cs.jSW_corn;
+    const double depth = 10, max_depth = 100, shelf = SizeY / 5, slope = (max_depth - depth) / (SizeY * 4 / 5);
+    const double land = SizeY * 0.1, coast = SizeY * 0.02, riv_west = SizeX * 0.4, riv_east = SizeX * 0.6;
+    const double psz = SizeX * 0.02, px = SizeX * .5, py = SizeY * .5;
+    const long pc = std::lround(psz / dx);
+    const double pipe_cells = (double)(pc * pc);
+    H.npip = 1;
+    H.pipe_idx.assign(n2, 0);
+    H.pipe_flx.assign(n2, 0.0);
+    H.pipe_prf.assign((size_t)N, 0.0);
+    H.pipe_prf[0] = 0.5; H.pipe_prf[1] = 0.5;             // ana_pipe_frc.h: pipe_prf(1,1:2)
+    H.pipe_trc.assign((size_t)NT, 0.0);
+    H.pipe_trc[0] = 24.0; if (NT > 1) H.pipe_trc[1] = 1.0;  // pipe_trc(1,1:2)
+    for (int j = -1; j <= Mm + 2; j++)
+      for (int i = -1; i <= Lm + 2; i++) {
+        const double x = x0 + dx * ((double)i - 0.5), y = y0 + dy * ((double)j - 0.5);
+        A(kxr, i, j) = x; A(kyr, i, j) = y;
+        A(kpm, i, j) = 1. / dx; A(kpn, i, j) = 1. / dy;
+        A(kf, i, j) = f0 + beta * (y - SizeY / 2.);
+        A(kh, i, j) = y < shelf ? depth : depth + (y - shelf) * slope;
+        double rm = 1;
+        if (y < land && (x < riv_west || x > riv_east)) rm = 0.0;
+        if (y < coast) rm = 0.0;
+        A(krmask, i, j) = rm;
+        if (x > px - 0.5 * psz && x < px + 0.5 * psz && y > py - 0.5 * psz && y < py + 0.5 * psz) {
+          const long o = (i + 1) + (long)(j + 1) * H.nx2;
+          H.pipe_idx[o] = 1;
+          H.pipe_flx[o] = 1.0 / pipe_cells * 5e2;  // pipe_fraction * pipe_vol(1)
+        }
+      }
   } else {
     const double dx = cs.sizex / cs.LLm, dy = cs.sizey / cs.MMm;
     const double R = 0.5 * (cs.sizex < cs.sizey ? cs.sizex : cs.sizey);
@@ -338,6 +372,15 @@ void build_case(const CaseSpec& cs, HostState& H, double& area, double& volume) 
         Z(i, j, 2) = Z(i, j, 1);
         for (int k = 1; k <= N; k++) V(i, j, k, 2) = V(i, j, k, 1);
       }
+  } else if (cs.case_id == ROMS_CASE_PIPES) {
+    // tests/Pipes_ana/ana_init.h:14-52: at rest, T = 4 + 10 e^{z/50}, S = 36 (LMD: Akv = Akt = 0)
+    for (int k = 1; k <= N; k++)
+      for (int j = 0; j <= Mm + 1; j++)
+        for (int i = 0; i <= Lm + 1; i++) {
+          T(i, j, k, 1, 1) = 4. + 10. * std::exp(A3(kz_r, i, j, k) / 50.);
+          T(i, j, k, 2, 1) = T(i, j, k, 1, 1);
+          if (cs.salinity) { T(i, j, k, 1, 2) = 36.; T(i, j, k, 2, 2) = T(i, j, k, 1, 2); }
+        }
   } else {
     const double Lx = cs.sizex, Ly = cs.sizey, pi = 3.14159265358979323;
     for (int k = 1; k <= N; k++)
@@ -356,12 +399,22 @@ void build_case(const CaseSpec& cs, HostState& H, double& area, double& volume) 
             T(i, j, k, 2, it) = T(i, j, k, 1, it);
           }
         }
-    for (long q = 0; q < n3w; q++) H.arr[kAkv][q] = cs.Akv_bak;
-    for (int it = 1; it <= H.nTS; it++)
-      for (long q = 0; q < n3w; q++) H.arr[kAkt][q + (long)(it - 1) * n3w] = cs.Akt_bak[it - 1];
+    if (!cs.lmd) {  // mixing.F:163-181: LMD_MIXING starts from Akv = Akt = 0
+      for (long q = 0; q < n3w; q++) H.arr[kAkv][q] = cs.Akv_bak;
+      for (int it = 1; it <= H.nTS; it++)
+        for (long q = 0; q < n3w; q++) H.arr[kAkt][q + (long)(it - 1) * n3w] = cs.Akt_bak[it - 1];
+    }
     const double piy = 3.14159265358979323;
     for (int j = -1; j <= Mm + 2; j++)
-      for (int i = -1; i <= Lm + 2; i++) A(ksustr, i, j) = 1.0e-4 * std::sin(piy * A(kyr, i, j) / cs.sizey);
+      for (int i = -1; i <= Lm + 2; i++) {
+        A(ksustr, i, j) = 1.0e-4 * std::sin(piy * A(kyr, i, j) / cs.sizey);
+        if (cs.surf_flux) {  // synthetic ana_stflux/ana_srflux (oracle_main.c or_ana_forces)
+          const double x = A(kxr, i, j), y = A(kyr, i, j);
+          H.arr[kstflx][(i + 1) + (long)(j + 1) * H.nx2] = -1.0e-4 * (1.0 + 0.5 * std::cos(2.0 * piy * x / cs.sizex));
+          A(ksrflx, i, j) = 4.0e-5 * (1.0 + 0.5 * std::sin(piy * y / cs.sizey));
+          if (cs.salinity) H.arr[kstflx][(i + 1) + (long)(j + 1) * H.nx2 + n2] = 1.0e-7 * std::cos(piy * y / cs.sizey);
+        }
+      }
   }
   // ana_init_generic exchanges
   wrap(H, H.arr[kzeta].data(), 1, ewp, nsp);

@@ -24,6 +24,10 @@ struct HostState {
   long n2;
   std::vector<double> arr[kNHost];
   bool wrap_on = true;
+  // pipe_frc.F (analytic pipes): npip = 0 when pipe_source is off
+  int npip = 0;
+  std::vector<int> pipe_idx;
+  std::vector<double> pipe_flx, pipe_prf, pipe_trc;
   HostState(int Lm_, int Mm_, int N_, int NT_, int nTS_);
   std::vector<double>& a(int id);
 };
@@ -32,7 +36,7 @@ struct CaseSpec {
   int case_id, LLm, MMm;
   int iSW_corn, jSW_corn;
   int ew_periodic, ns_periodic, west_exchng, east_exchng, south_exchng, north_exchng;
-  int salinity;
+  int salinity, lmd, surf_flux;
   int host_wrap;  // apply periodic halo wraps on the host (single rank)
   double theta_s, theta_b, hc, rho0, Tcoef, visc2, tnu2, Akv_bak, Akt_bak[2];
   double sizex, sizey;

@@ -1,0 +1,500 @@
+// k_lmd.hip -- LMD/KPP vertical mixing on gfx950: lmd_vmix(tind)
+// (lmd_vmix.F:5-433 + lmd_kpp.F:7-651, alfabeta.F:4-79) and the Jerlov
+// short-wave fractions of lmd_swr_frac.F:13-88.
+//
+// Switch set: LMD_RIMIX, LMD_CONVEC, LMD_KPP, LMD_BKPP, LMD_NONLOCAL,
+// SMOOTH_RIG, SMOOTH_HBL, INT_AT_RHO_POINTS, MASKING (no LMD_DDMIX, no
+// MERGE_OVERLAP, no LIMIT_UNSTABLE_ONLY, no BULK_FRC) -- the reference's
+// Pipes_ana / Rivers_ana / Iceland configuration.
+//
+// Two column passes replace the reference's four j-sweeps:
+//   k_kpp_ext  over the extended range (I_EXT_RANGE x J_EXT_RANGE): one
+//              descending sweep produces the raw gradient Richardson number
+//              Rig(1:N-1) (lmd_vmix.F:155-168), the bulk-Richardson integral
+//              FC(0:N) kept in LDS, the surface layer search kbls and hbl
+//              (lmd_kpp.F:200-275), then the bottom layer bbl (:276-305);
+//              alpha/beta, Bo, Bosol and ustar are stored for the second pass.
+//   k_kpp_int  over the interior: the masked isotropic smoothing of hbl/bbl
+//              (lmd_kpp_smooth_hbl.h) and of Rig at every level
+//              (lmd_vmix.F:206-241) are evaluated per column from the 3x3
+//              neighbourhood (closed-wall ghost copies become clamped
+//              indices); Kv/Kt/Ks stream bottom-up through the Rig mixing,
+//              the Lturb taper, the 1-2-1 vertical filter, the KPP shape
+//              functions, the BKPP layer and the masked copy to Akv/Akt, with
+//              no level-sized scratch at all.
+// Every expression keeps the reference's operation order (FP64, no FMA
+// contraction); integer powers are products, real powers pow().
+#include <cmath>
+
+#include "k_common.h"
+
+namespace roms {
+namespace {
+
+// lmd_kpp.F:70-95
+constexpr double kRicr = 0.15, kEpssfc = 0.1, kC_Ek = 258.;
+constexpr double kZeta_m = -0.2, kA_m = 1.257, kC_m = 8.360, kZeta_s = -1.0, kA_s = -28.86, kC_s = 98.96;
+constexpr double kEPS = 1.E-20;
+// lmd_vmix.F:58-70
+constexpr double kRi0 = 0.7, kNu0m = 1.e-2, kNu0s = 1.e-2, kNuwm = 1.0e-4, kNuws = 0.1e-4, kNu0c = 0.1, kLturb = 10.;
+constexpr double kPi = 3.14159265358979323;  // scalars.F:126
+
+struct KppConst {
+  double Cg, Vtc;  // lmd_kpp.F:137-138 (power functions: evaluated on the host)
+};
+
+// lmd_wscale_ws_only.h
+__device__ __forceinline__ double wscale_ws(double zscale, double Bfsfc, double hbl, double ustar, double rmask,
+                                            double vonKar) {
+  zscale = dmin(zscale, hbl * kEpssfc);
+  zscale = zscale * rmask;
+  const double zetahat = vonKar * zscale * Bfsfc;
+  const double ustar3 = ustar * ustar * ustar;
+  if (zetahat >= 0.) return vonKar * ustar * ustar3 / dmax(ustar3 + 5. * zetahat, 1.E-20);
+  if (zetahat > kZeta_s * ustar3) return vonKar * sqrt((ustar3 - 16. * zetahat) / ustar);  // **r2
+  return vonKar * pow(kA_s * ustar3 - kC_s * zetahat, 1. / 3.);
+}
+// lmd_wscale_wm_and_ws.h
+__device__ __forceinline__ void wscale_wm_ws(double zscale, double Bfsfc, double hbl, double ustar, double rmask,
+                                             double vonKar, double& wm, double& ws) {
+  zscale = dmin(zscale, hbl * kEpssfc);
+  zscale = zscale * rmask;
+  const double zetahat = vonKar * zscale * Bfsfc;
+  const double ustar3 = ustar * ustar * ustar;
+  if (zetahat >= 0.) {
+    wm = vonKar * ustar * ustar3 / dmax(ustar3 + 5. * zetahat, 1.E-20);
+    ws = wm;
+  } else {
+    if (zetahat > kZeta_m * ustar3) wm = vonKar * pow(ustar * (ustar3 - 16. * zetahat), 0.25);
+    else wm = vonKar * pow(kA_m * ustar3 - kC_m * zetahat, 1. / 3.);
+    if (zetahat > kZeta_s * ustar3) ws = vonKar * sqrt((ustar3 - 16. * zetahat) / ustar);
+    else ws = vonKar * pow(kA_s * ustar3 - kC_s * zetahat, 1. / 3.);
+  }
+}
+
+// Closed-wall ghost copies of the smoothing stencils (lmd_vmix.F:170-204,
+// lmd_kpp_smooth_hbl.h:13-50) as index clamps: a copied ghost cell reads the
+// interior cell it was copied from, corners included.
+struct EdgeClamp {
+  int ilo, ihi, jlo, jhi;
+  __device__ __forceinline__ long at(const Bounds& b, int i, int j) const {
+    return IJ(b, i < ilo ? ilo : (i > ihi ? ihi : i), j < jlo ? jlo : (j > jhi ? jhi : j));
+  }
+};
+EdgeClamp edge_clamp(const Bounds& b) {
+  EdgeClamp c;
+  c.ilo = (!b.ew_periodic && b.west_edge) ? b.istr : -1;
+  c.ihi = (!b.ew_periodic && b.east_edge) ? b.iend : b.Lm + 2;
+  c.jlo = (!b.ns_periodic && b.south_edge) ? b.jstr : -1;
+  c.jhi = (!b.ns_periodic && b.north_edge) ? b.jend : b.Mm + 2;
+  return c;
+}
+
+// Masks of the 3x3 smoothing stencil around (i,j): umask at (i..i+1, j-1..j+1),
+// vmask at (i-1..i+1, j..j+1).
+struct SmoothMasks {
+  double um[3][2];  // [j-1..j+1][i..i+1]
+  double vm[2][3];  // [j..j+1][i-1..i+1]
+};
+__device__ __forceinline__ SmoothMasks smooth_masks(const Bounds& b, const Fields& F, int i, int j) {
+  SmoothMasks m;
+#pragma unroll
+  for (int dj = 0; dj < 3; dj++)
+#pragma unroll
+    for (int di = 0; di < 2; di++) m.um[dj][di] = F.umask[IJ(b, i + di, j - 1 + dj)];
+#pragma unroll
+  for (int dj = 0; dj < 2; dj++)
+#pragma unroll
+    for (int di = 0; di < 3; di++) m.vm[dj][di] = F.vmask[IJ(b, i - 1 + di, j + dj)];
+  return m;
+}
+
+// Isotropic masked smoother evaluated at one point from w[dj][di] = wrk(i-1+di, j-1+dj)
+// (lmd_vmix.F:206-241 == lmd_kpp_smooth_hbl.h:63-102 before the final rmask).
+__device__ __forceinline__ double smooth_point(const double (&w)[3][3], const SmoothMasks& m) {
+  const double cff = 1. / 12., cff1 = 3. / 16.;
+  // FX(a,b) = (wrk(a,b)-wrk(a-1,b))*umask(a,b), a = i,i+1, b = j-1..j+1
+  double FX[3][2];
+#pragma unroll
+  for (int dj = 0; dj < 3; dj++)
+#pragma unroll
+    for (int di = 0; di < 2; di++) FX[dj][di] = (w[dj][di + 1] - w[dj][di]) * m.um[dj][di];
+  // FE1(a,b) = (wrk(a,b)-wrk(a,b-1))*vmask(a,b), a = i-1..i+1, b = j,j+1
+  double FE1[2][3];
+#pragma unroll
+  for (int dj = 0; dj < 2; dj++)
+#pragma unroll
+    for (int di = 0; di < 3; di++) FE1[dj][di] = (w[dj + 1][di] - w[dj][di]) * m.vm[dj][di];
+  // FE(i,b) for b = j, j+1 (raw FX), then FX(a,j) for a = i, i+1 updated with FE1
+  const double FEj = FE1[0][1] + cff * (FX[1][1] + FX[0][0] - FX[1][0] - FX[0][1]);
+  const double FEjp = FE1[1][1] + cff * (FX[2][1] + FX[1][0] - FX[2][0] - FX[1][1]);
+  const double FXi = FX[1][0] + cff * (FE1[1][1] + FE1[0][0] - FE1[0][1] - FE1[1][0]);
+  const double FXip = FX[1][1] + cff * (FE1[1][2] + FE1[0][1] - FE1[0][2] - FE1[1][1]);
+  return w[1][1] + cff1 * (FXip - FXi + FEjp - FEj);
+}
+
+__device__ __forceinline__ void load3x3(const Bounds& b, const EdgeClamp& ec, const double* a, int i, int j,
+                                        double (&w)[3][3]) {
+#pragma unroll
+  for (int dj = 0; dj < 3; dj++)
+#pragma unroll
+    for (int di = 0; di < 3; di++) w[dj][di] = a[ec.at(b, i - 1 + di, j - 1 + dj)];
+}
+
+// ---- lmd_swr_frac.F:31-85 (Jwt = 1) ----
+__global__ void __launch_bounds__(256) k_swr_frac(Dev d, Range R) {
+  ROMS_IJ_OR_RETURN(R)
+  const Bounds& b = d.b;
+  const long ij = IJ(b, i, j), n2 = b.n2;
+  const int N = b.N;
+  const double mu1 = 0.35, mu2 = 23.0, r1 = 0.58;
+  const double attn1 = -1. / mu1, attn2 = -1. / mu2;
+  double swdk1 = r1, swdk2 = 1. - swdk1;
+  double* __restrict__ sw = d.f.swr_frac + ij;
+  const double* __restrict__ Hz = d.f.Hz + ij;
+  sw[(long)N * n2] = 1.;
+  for (int k = N; k >= 1; k--) {
+    const double hz = Hz[(long)(k - 1) * n2];
+    const double xi1 = attn1 * hz;
+    if (xi1 > -20.) swdk1 = swdk1 * exp(xi1);
+    else swdk1 = 0.;
+    const double xi2 = attn2 * hz;
+    if (xi2 > -20.) swdk2 = swdk2 * exp(xi2);
+    else swdk2 = 0.;
+    sw[(long)(k - 1) * n2] = swdk1 + swdk2;
+  }
+}
+
+// ---- pass 1: extended range ----
+__global__ void __launch_bounds__(64) k_kpp_ext(Dev d, Range E, int tind, int nstp, KppConst kc) {
+  ROMS_IJC_OR_RETURN(E)
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const Params& P = d.p;
+  const int N = b.N;
+  const long n2 = b.n2, ij = IJ(b, i, j), sj = b.nx2;
+  const double g = P.g, vonKar = P.vonKar, Ri_inv = 1. / kRicr;
+  const ColLds FC = col_lds(0, N);
+  // alfabeta.F:46-78 at t(N,nstp); Bo, Bosol, ustar (lmd_kpp.F:154-181)
+  double alpha, beta;
+  const double Tt = F.t[ij + (long)(N - 1) * n2 + (long)(nstp - 1) * b.n3];
+  if (P.nonlin_eos) {
+    const double r01 = 6.793952E-2, r02 = -9.095290E-3, r03 = +1.001685E-4, r04 = -1.120083E-6,
+                 r05 = +6.536332E-9, r10 = +0.824493, r11 = -4.08990E-3, r12 = +7.64380E-5,
+                 r13 = -8.24670E-7, r14 = +5.38750E-9, rS0 = -5.72466E-3, rS1 = +1.02270E-4,
+                 rS2 = -1.65460E-6, r20 = +4.8314E-4;
+    const double cff = 1. / P.rho0;
+    if (P.salinity) {
+      const double Ts = F.t[ij + (long)(N - 1) * n2 + (long)(nstp - 1) * b.n3 + 3 * b.n3], sqrtTs = sqrt(dmax(0., Ts));
+      alpha = -cff * (r01 + Tt * (2. * r02 + Tt * (3. * r03 + Tt * (4. * r04 + Tt * 5. * r05))) +
+                      Ts * (r11 + Tt * (2. * r12 + Tt * (3. * r13 + Tt * 4. * r14)) + sqrtTs * (rS1 + Tt * 2. * rS2)));
+      beta = cff * (r10 + Tt * (r11 + Tt * (r12 + Tt * (r13 + Tt * r14))) + 1.5 * (rS0 + Tt * (rS1 + Tt * rS2)) * sqrtTs +
+                    2. * r20 * Ts);
+    } else {
+      alpha = -cff * (r01 + Tt * (2. * r02 + Tt * (3. * r03 + Tt * (4. * r04 + Tt * 5. * r05))));
+      beta = 0.;
+    }
+  } else {
+    alpha = fabs(P.Tcoef);
+    beta = P.salinity ? fabs(P.Scoef) : 0.;
+  }
+  const double sr = F.srflx[ij];
+  const double Bo = P.salinity ? g * (alpha * (F.stflx[ij] - sr) - beta * F.stflx[ij + n2]) : g * (alpha * (F.stflx[ij] - sr));
+  const double Bosol = g * alpha * sr;
+  const double su0 = F.sustr[ij], su1 = F.sustr[ij + 1], sv0 = F.svstr[ij], sv1 = F.svstr[ij + sj];
+  const double ustar = sqrt(sqrt(0.333333333333 * (su0 * su0 + su1 * su1 + su0 * su1 + sv0 * sv0 + sv1 * sv1 + sv0 * sv1)));
+  const double hbl0 = F.hbls[ij], bbl0 = F.hbbl[ij];
+  const double rm = F.rmask[ij], ff = F.f[ij];
+  F.lmd_Bo[ij] = Bo;
+  F.lmd_Bosol[ij] = Bosol;
+  F.lmd_ustar[ij] = ustar;
+
+  const double* __restrict__ U = F.u + (long)(tind - 1) * b.n3 + ij;
+  const double* __restrict__ V = F.v + (long)(tind - 1) * b.n3 + ij;
+  const double* __restrict__ Hz = F.Hz + ij;
+  const double* __restrict__ zr = F.z_r + ij;
+  const double* __restrict__ zw = F.z_w + ij;
+  const double* __restrict__ bvf = F.bvf + ij;
+  const double* __restrict__ sw = F.swr_frac + ij;
+  double* __restrict__ rig = F.lmd_rig + ij;
+  const double zwN = zw[(long)N * n2], zw0 = zw[0];
+  const double eh = kEpssfc * hbl0, eb = kEpssfc * bbl0;
+  const double eh2 = eh * eh, eb2 = eb * eb;
+
+  // k = N: FC(N) = 0, Cr(N) = Vtsq(N)
+  auto vtsq = [&](int k, double zrk) {
+    const double swk = sw[(long)k * n2], swm = sw[(long)(k - 1) * n2];
+    const double swdk_r = sqrt(swk * swm);
+    const double zscale = zwN - zrk;
+    const double Bfsfc = Bo + Bosol * (1. - swdk_r);
+    const double ws = wscale_ws(zscale, Bfsfc, hbl0, ustar, rm, vonKar);
+    return 1.8 * kc.Vtc * ws * sqrt(dmax(1.e-5, bvf[(long)(k - 1) * n2]));
+  };
+  double u0p = U[(long)(N - 1) * n2], u1p = U[(long)(N - 1) * n2 + 1];  // level k+1
+  double v0p = V[(long)(N - 1) * n2], v1p = V[(long)(N - 1) * n2 + sj];
+  double hzp = Hz[(long)(N - 1) * n2], zrp = zr[(long)(N - 1) * n2];
+  double FCk = 0.;
+  FC[N] = 0.;
+  double Crp = FCk + vtsq(N, zrp);
+  int kbls = Crp < 0. ? N : 0;
+  double cr_k = Crp, cr_kp = 0., zr_k = zrp, zr_kp = 0.;
+  for (int k = N - 1; k >= 1; k--) {
+    const long o = (long)(k - 1) * n2;
+    const double u0 = U[o], u1 = U[o + 1], v0 = V[o], v1 = V[o + sj];
+    const double hz = Hz[o], zrk = zr[o], zwk = zw[(long)k * n2], bk = bvf[(long)k * n2];
+    // raw gradient Richardson number (lmd_vmix.F:157-165)
+    {
+      const double cff = 0.5 / (zrp - zrk);
+      const double dudz = cff * (u0p - u0 + u1p - u1);
+      const double dvdz = cff * (v0p - v0 + v1p - v1);
+      rig[(long)k * n2] = bk / (kRi0 * dmax(dudz * dudz + dvdz * dvdz, 1.E-10));
+    }
+    // bulk Richardson integral (lmd_kpp.F:200-215)
+    {
+      const double cu = zwN - zwk, cd = zwk - zw0;
+      const double cff_up = cu * cu, cff_dn = cd * cd;
+      const double Kern = cff_up * cff_dn / ((cff_up + eh2) * (cff_dn + eb2));
+      const double du = u0p + u1p - u0 - u1;
+      const double dv = v0p + v1p - v0 - v1;
+      const double hh = hz + hzp;
+      FCk = FCk + Kern * (0.5 * (du * du + dv * dv) / hh - 0.5 * hh * (Ri_inv * bk + kC_Ek * ff * ff));
+      FC[k] = FCk;
+    }
+    const double Cr = FCk + vtsq(k, zrk);
+    if (kbls == 0 && Cr < 0.) {
+      kbls = k;
+      cr_k = Cr; cr_kp = Crp; zr_k = zrk; zr_kp = zrp;
+    }
+    Crp = Cr;
+    u0p = u0; u1p = u1; v0p = v0; v1p = v1; hzp = hz; zrp = zrk;
+  }
+  // FC(0) (lmd_kpp.F:216-229): level-1 values are the carried ones
+  {
+    const double hz1 = hzp;
+    const double z_bl = zw0 + 0.25 * hz1;
+    const double cu = zwN - z_bl, cd = z_bl - zw0;
+    const double cff_up = cu * cu, cff_dn = cd * cd;
+    const double Kern = cff_up * cff_dn / ((cff_up + eh2) * (cff_dn + eb2));
+    const double su = u0p + u1p, sv = v0p + v1p;
+    FC[0] = FC[1] + Kern * (0.5 * (su * su + sv * sv) / hz1 - 0.5 * hz1 * (Ri_inv * bvf[n2] + kC_Ek * ff * ff));
+  }
+  double hbl;
+  if (kbls > 0) {
+    if (kbls == N) hbl = zwN - zr[(long)(N - 1) * n2];
+    else hbl = zwN - (zr_k * cr_kp - zr_kp * cr_k) / (cr_kp - cr_k);
+  } else {
+    hbl = zwN - zw0;
+  }
+  F.lmd_hbl[ij] = hbl * rm;
+  // bottom layer (lmd_kpp.F:276-305): Cr(k) = FC(k) - FC(0), first k upward with Cr > 0
+  const double FC0 = FC[0];
+  double bbl = zwN - zw0;
+  double crm = 0.;
+  for (int k = 1; k <= N; k++) {
+    const double cr = FC[k] - FC0;
+    if (cr > 0.) {
+      if (k == 1) bbl = zr[0] - zw0;
+      else {
+        const double zrm = zr[(long)(k - 2) * n2], zrk = zr[(long)(k - 1) * n2];
+        bbl = (zrm * cr - zrk * crm) / (cr - crm) - zw0;
+      }
+      break;
+    }
+    crm = cr;
+  }
+  F.lmd_bbl[ij] = bbl * rm;
+}
+
+// ---- pass 2: interior ----
+__global__ void __launch_bounds__(64) k_kpp_int(Dev d, Range R, EdgeClamp ec, int tind, int nstp, int first,
+                                                KppConst kc) {
+  ROMS_IJC_OR_RETURN(R)
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const Params& P = d.p;
+  const int N = b.N;
+  const long n2 = b.n2, ij = IJ(b, i, j), sj = b.nx2;
+  const double vonKar = P.vonKar, Zob = P.Zob;
+  const double akv = P.Akv_bak, akt = P.Akt_bak[0], aks = P.Akt_bak[b.nTS - 1];
+  const double rm = F.rmask[ij];
+  const SmoothMasks m = smooth_masks(b, F, i, j);
+  // SMOOTH_HBL (lmd_kpp_smooth_hbl.h), then the two-step average (lmd_kpp.F:327-338)
+  double w[3][3];
+  load3x3(b, ec, F.lmd_hbl, i, j, w);
+  double hbl = smooth_point(w, m) * rm;
+  load3x3(b, ec, F.lmd_bbl, i, j, w);
+  double bbl = smooth_point(w, m) * rm;
+  if (!first) {
+    hbl = 0.5 * (hbl + F.hbls[ij]);
+    bbl = 0.5 * (bbl + F.hbbl[ij]);
+  }
+  const double* __restrict__ zw = F.z_w + ij;
+  const double* __restrict__ sw = F.swr_frac + ij;
+  const double zwN = zw[(long)N * n2], zw0 = zw[0];
+  // kbls and the buoyancy forcing at the boundary-layer depth (lmd_kpp.F:348-372)
+  int kbls = N;
+  for (int k = N - 1; k >= 1; k--)
+    if (zw[(long)k * n2] > zwN - hbl) kbls = k;
+  const double Bo = F.lmd_Bo[ij], Bosol = F.lmd_Bosol[ij], ustar = F.lmd_ustar[ij];
+  double Bfsfc;
+  {
+    const double z_bl = zwN - hbl;
+    const double swm = sw[(long)(kbls - 1) * n2], swk = sw[(long)kbls * n2];
+    const double zwk = zw[(long)kbls * n2], zwm = zw[(long)(kbls - 1) * n2];
+    if (swm > 0.)
+      Bfsfc = Bo + Bosol * (1. - swm * swk * (zwk - zwm) / (swk * (zwk - z_bl) + swm * (z_bl - zwm)));
+    else
+      Bfsfc = Bo + Bosol;
+  }
+  // BKPP friction velocity (lmd_kpp.F:472-480)
+  double wmb;
+  {
+    const long o = (long)(nstp - 1) * b.n3 + ij;
+    const double u0 = F.u[o], u1 = F.u[o + 1], v0 = F.v[o], v1 = F.v[o + sj];
+    wmb = vonKar * vonKar * sqrt(0.333333333333 * (u0 * u0 + u1 * u1 + u0 * u1 + v0 * v0 + v1 * v1 + v0 * v1)) /
+          log(1. + 0.5 * F.Hz[ij] / Zob);
+  }
+  const double wsb = wmb;
+
+  // raw interior Kv, Kt (= Ks) at level k from the smoothed Rig (lmd_vmix.F:249-272, 338-353)
+  const double* __restrict__ rig = F.lmd_rig;
+  auto raw_k = [&](int k, double& kv, double& kt) {
+    double r[3][3];
+    load3x3(b, ec, rig + (long)k * n2, i, j, r);
+    const double Rig = smooth_point(r, m);
+    const double cff = dmin(1., dmax(0., Rig));
+    double nu_sx = 1. - cff * cff;
+    nu_sx = nu_sx * nu_sx * nu_sx;
+    kv = kNuwm + kNu0m * nu_sx;
+    kt = kNuws + kNu0s * nu_sx;
+    if (Rig < 0.) {
+      kv = kv + kNu0c;
+      kt = kt + kNu0c;
+    }
+    const double zwk = zw[(long)k * n2];
+    const double dist = zwk - zw0;
+    if (dist < kLturb) {
+      const double mult = sin(0.5 * kPi * (zwk - zw0) / kLturb);
+      kv = kv * mult;
+      kt = kt * mult;
+    }
+  };
+  double* __restrict__ Akv = F.Akv + ij;
+  double* __restrict__ AktT = F.Akt + ij;
+  double* __restrict__ AktS = F.Akt + b.n3w + ij;
+  double* __restrict__ ghat = F.ghat + ij;
+  const bool wet = rm > 0.5;
+  // KPP shape functions (lmd_kpp.F:374-446), BKPP (:447-495), masked copy (:496-528)
+  auto finish = [&](int k, double Kv, double Kt, double Ks) {
+    const double zwk = zw[(long)k * n2];
+    double wm, ws;
+    wscale_wm_ws(zwN - zwk, Bfsfc, hbl, ustar, rm, vonKar, wm, ws);
+    const double ssgm = (zwN - zwk) / dmax(hbl, kEPS);
+    double gh = 0.;
+    if (ssgm < 1.) {
+      double cff;
+      if (ssgm < 0.07) cff = 0.5 * ((ssgm - 0.07) * (ssgm - 0.07)) / 0.07;
+      else cff = 0.;
+      cff = cff + ssgm * ((1. - ssgm) * (1. - ssgm));
+      const double amp = ssgm * ssgm;
+      double a, q;
+      a = amp * Kv; q = wm * hbl * cff;
+      Kv = sqrt(a * a + q * q);
+      a = amp * Kt; q = ws * hbl * cff;
+      Kt = sqrt(a * a + q * q);
+      a = amp * Ks;
+      Ks = sqrt(a * a + q * q);
+      if (Bfsfc < 0.) gh = -(kc.Cg * ssgm * ((1. - ssgm) * (1. - ssgm)));
+    }
+    ghat[(long)k * n2] = gh;
+    const double sgmb = (zwk - zw0 + Zob) / (bbl + Zob);
+    if (sgmb < 1.) {
+      const double cff1 = sgmb * ((1. - sgmb) * (1. - sgmb));
+      double q = wmb * bbl * cff1;
+      Kv = sqrt(Kv * Kv + q * q);
+      q = wsb * bbl * cff1;
+      Kt = sqrt(Kt * Kt + q * q);
+      Ks = sqrt(Ks * Ks + q * q);
+    }
+    Akv[(long)k * n2] = wet ? Kv : 0.;
+    AktT[(long)k * n2] = wet ? Kt : 0.;
+    if (b.nTS > 1) AktS[(long)k * n2] = wet ? Ks : 0.;
+  };
+  // bottom-up stream: padding (lmd_vmix.F:359-370) and the in-place ascending
+  // 1-2-1 filter Kv(k) = 0.5 Kv(k) + 0.25 Kv(k-1)[filtered] + 0.25 Kv(k+1)[raw] + bak
+  double rv, rt;      // raw level k
+  raw_k(1, rv, rt);
+  double rvN = rv, rtN = rt;  // raw level N-1 (known once reached)
+  double sv = rv + akv, st = rt + akt, ss = rt + aks;  // level 0 (padded)
+  finish(0, sv, st, ss);
+  for (int k = 1; k <= N - 1; k++) {
+    double nv, nt, ns;  // level k+1 before filtering
+    double rvn = 0., rtn = 0.;
+    if (k + 1 <= N - 1) {
+      raw_k(k + 1, rvn, rtn);
+      nv = rvn; nt = rtn; ns = rtn;
+    } else {
+      rvN = rv; rtN = rt;
+      nv = rv + akv; nt = rt + akt; ns = rt + aks;
+    }
+    sv = 0.5 * rv + 0.25 * sv + 0.25 * nv + akv;
+    st = 0.5 * rt + 0.25 * st + 0.25 * nt + akt;
+    ss = 0.5 * rt + 0.25 * ss + 0.25 * ns + aks;
+    finish(k, sv, st, ss);
+    rv = rvn; rt = rtn;
+  }
+  finish(N, rvN + akv, rtN + akt, rtN + aks);
+  // hbls/hbbl and their closed-wall ghost copies (lmd_kpp.F:530-620)
+  F.hbls[ij] = hbl;
+  F.hbbl[ij] = bbl;
+  const bool W = !b.ew_periodic && b.west_edge && i == b.istr, E = !b.ew_periodic && b.east_edge && i == b.iend;
+  const bool S = !b.ns_periodic && b.south_edge && j == b.jstr, Nn = !b.ns_periodic && b.north_edge && j == b.jend;
+  if (W) { F.hbls[ij - 1] = hbl; F.hbbl[ij - 1] = bbl; }
+  if (E) { F.hbls[ij + 1] = hbl; F.hbbl[ij + 1] = bbl; }
+  if (S) { F.hbls[ij - sj] = hbl; F.hbbl[ij - sj] = bbl; }
+  if (Nn) { F.hbls[ij + sj] = hbl; F.hbbl[ij + sj] = bbl; }
+  if (W && S) { F.hbls[ij - 1 - sj] = hbl; F.hbbl[ij - 1 - sj] = bbl; }
+  if (W && Nn) { F.hbls[ij - 1 + sj] = hbl; F.hbbl[ij - 1 + sj] = bbl; }
+  if (E && S) { F.hbls[ij + 1 - sj] = hbl; F.hbbl[ij + 1 - sj] = bbl; }
+  if (E && Nn) { F.hbls[ij + 1 + sj] = hbl; F.hbbl[ij + 1 + sj] = bbl; }
+}
+
+}  // namespace
+
+void launch_swr_frac(const Dev& d, hipStream_t s) {
+  const Bounds& b = d.b;
+  const Range R{b.istr, b.iend, b.jstr, b.jend};
+  hipLaunchKernelGGL(k_swr_frac, grid_of(R), dim3(kBX, kBY), 0, s, d, R);
+  ExchList L{};
+  L.p[0] = d.f.swr_frac; L.nlev[0] = b.N + 1; L.n = 1;
+  launch_exchange_list(d, s, L);
+}
+
+void launch_lmd_vmix(const Dev& d, hipStream_t s, const Tlev& t, int tind) {
+  const Bounds& b = d.b;
+  // lmd_kpp.F:97-123 (== lmd_vmix.F:105-141): I_EXT_RANGE x J_EXT_RANGE
+  Range E;
+  E.i0 = (b.ew_periodic || !b.west_edge) ? b.istr - 1 : b.istr;
+  E.i1 = (b.ew_periodic || !b.east_edge) ? b.iend + 1 : b.iend;
+  E.j0 = (b.ns_periodic || !b.south_edge) ? b.jstr - 1 : b.jstr;
+  E.j1 = (b.ns_periodic || !b.north_edge) ? b.jend + 1 : b.jend;
+  const Range R{b.istr, b.iend, b.jstr, b.jend};
+  // Cg, Vtc (lmd_kpp.F:137-138) with host libm, like the reference's own runtime pow
+  const double vonKar = d.p.vonKar, Cstar = 10., c_s = kC_s, epssfc = kEpssfc, Cv = 1.8, betaT = -0.2;
+  KppConst kc;
+  kc.Cg = Cstar * vonKar * std::pow(c_s * vonKar * epssfc, 1. / 3.);
+  kc.Vtc = Cv * std::sqrt(-betaT / (c_s * epssfc)) / (kRicr * (vonKar * vonKar));
+  const int first = t.iic == t.forw_start;  // FIRST_TIME_STEP with EXACT_RESTART
+  hipLaunchKernelGGL(k_kpp_ext, gridc_of(E), dim3(kCX), col_lds_bytes(1, b.N), s, d, E, tind, t.nstp, kc);
+  hipLaunchKernelGGL(k_kpp_int, gridc_of(R), dim3(kCX), 0, s, d, R, edge_clamp(b), tind, t.nstp, first, kc);
+  // lmd_kpp.F:631-649: Akv, hbls, hbbl, Akt(itemp), Akt(isalt)
+  ExchList L{};
+  L.p[0] = d.f.Akv; L.nlev[0] = b.N + 1;
+  L.p[1] = d.f.hbls; L.nlev[1] = 1;
+  L.p[2] = d.f.hbbl; L.nlev[2] = 1;
+  L.p[3] = d.f.Akt; L.nlev[3] = (b.N + 1) * b.nTS;
+  L.n = 4;
+  launch_exchange_list(d, s, L);
+}
+
+}  // namespace roms

@@ -49,6 +49,7 @@ __global__ void __launch_bounds__(256) k_s2d_zeta(Dev d, Range R, FBCoef c) {
   double zn = zk + d.p.dtfast * F.pm[ij] * F.pn[ij] *
                        (s2d_DUon(d, c, ij) - s2d_DUon(d, c, ij + 1) + s2d_DVom(d, c, ij) - s2d_DVom(d, c, ij + sj)) +
               d.p.dtfast * F.swflx[ij];
+  if (d.p.npip > 0 && F.pipe_idx[ij] > 0) zn = zn + d.p.dtfast * F.pm[ij] * F.pn[ij] * F.pipe_flx[ij];  // step2d_FB.F:155-159
   zn = zn * F.rmask[ij];
   F.s0[ij] = zn;
   F.s1[ij] = zn + F.h[ij];
@@ -193,6 +194,7 @@ struct FBTile {
   unsigned char st[kFN];  // 0: outside, 1: computed, 2: set by zetabc
 };
 
+template <bool kPipe>
 __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int closed, int vwrap) {
   __shared__ FBTile T;
   const Bounds& b = d.b;
@@ -252,17 +254,20 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int cl
     }
   }
   const int za = b.istrU - 1, zb = b.iend, zc = b.jstrV - 1, zd = b.jend;
-  double e_pm[2], e_pn[2], e_sw[2], e_rm[2], e_rS[2], e_rA[2];
+  double e_pm[2], e_pn[2], e_sw[2], e_rm[2], e_rS[2], e_rA[2], e_pf[2];
+  bool e_pp[2];
 #pragma unroll
   for (int r = 0; r < 2; r++) {
     const int q = tid + r * NT;
     const int i = i0 - 1 + q % kFX, j = j0 - 1 + q / kFX;
-    e_pm[r] = e_pn[r] = e_sw[r] = e_rm[r] = e_rS[r] = e_rA[r] = 0.0;
+    e_pm[r] = e_pn[r] = e_sw[r] = e_rm[r] = e_rS[r] = e_rA[r] = e_pf[r] = 0.0;
+    e_pp[r] = false;
     if (q < kFN && i >= za && i <= zb && j >= zc && j <= zd) {
       const long ij = IJ(b, i, j);
       e_pm[r] = F.pm[ij];
       e_pn[r] = F.pn[ij];
       e_sw[r] = F.swflx[ij]; e_rm[r] = F.rmask[ij]; e_rS[r] = F.rhoS[ij]; e_rA[r] = F.rhoA[ij];
+      if (kPipe) { e_pp[r] = F.pipe_idx[ij] > 0; e_pf[r] = F.pipe_flx[ij]; }
     }
   }
   const int pi = i0 + (int)threadIdx.x, pj = j0 + (int)threadIdx.y;
@@ -337,6 +342,7 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int cl
     const double zk = T.z0[g];
     double zn = zk + d.p.dtfast * e_pm[r] * e_pn[r] * (DU(i, j) - DU(i + 1, j) + DV(i, j) - DV(i, j + 1)) +
                 d.p.dtfast * e_sw[r];
+    if (kPipe && e_pp[r]) zn = zn + d.p.dtfast * e_pm[r] * e_pn[r] * e_pf[r];  // step2d_FB.F:155-159
     zn = zn * e_rm[r];
     const double zwrk = c.bkw_new * zn + c.bkw * zk + c.bkw1 * T.z1[g] + c.bkw2 * T.z2[g];
     const double rhoS = e_rS[r];
@@ -602,7 +608,10 @@ void launch_step2d(const Dev& d, hipStream_t s, const Tlev& t, const double* w1,
     }
     hipLaunchKernelGGL(k_s2d_mom, grid_of(RB), dim3(kBX, kBY), 0, s, d, RB, c);
   } else {
-    hipLaunchKernelGGL(k_s2d_fb, grid_of(RB), dim3(kBX, kBY), 0, s, d, RB, c, (int)closed, vwrap);
+    if (d.p.npip > 0)
+      hipLaunchKernelGGL(k_s2d_fb<true>, grid_of(RB), dim3(kBX, kBY), 0, s, d, RB, c, (int)closed, vwrap);
+    else
+      hipLaunchKernelGGL(k_s2d_fb<false>, grid_of(RB), dim3(kBX, kBY), 0, s, d, RB, c, (int)closed, vwrap);
   }
   if (closed) {
     const int L = b.nx2 > b.Mm + 4 ? b.nx2 : b.Mm + 4;

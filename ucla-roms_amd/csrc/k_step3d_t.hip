@@ -64,9 +64,14 @@ __global__ void __launch_bounds__(64) k_step3d_t_v(Dev d, Range R, int nnew, int
     const double DC0 = dt * F.pm[ij] * F.pn[ij];
     const bool kppT = P.lmd && itrc == 1, kppS = P.lmd && itrc == 2 && P.salinity;
     const double sr = F.srflx[ij];
+    // pipe_frc.F sources (step3d_t_ISO.F:927-934)
+    const int pidx = P.npip > 0 ? F.pipe_idx[ij] : 0;
+    const double pflx = pidx > 0 ? F.pipe_flx[ij] : 0.0;
+    const double ptrc = pidx > 0 ? F.pipe_trc[(pidx - 1) + (itrc - 1) * P.npip] : 0.0;
     auto tval_of = [&](int k, double tnk) {
       const long o = (long)(k - 1) * n2;
       double t = tnk - dt * F.pm[ij] * F.pn[ij] * (A[k] - A[k - 1]);
+      if (pidx > 0) t = t + dt * F.pm[ij] * F.pn[ij] * pflx * F.pipe_prf[(pidx - 1) + (k - 1) * P.npip] * ptrc;
       if (k == N) {
         if (itrc == 1) t = t + dt * F.swflx[ij] * t / Hz[o];
         t = t + dt * stf;

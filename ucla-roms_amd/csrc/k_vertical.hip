@@ -164,11 +164,24 @@ __global__ void __launch_bounds__(256) k_omega(Dev d, Range R, double dtau) {
   auto cx = [&](long o) { return fmax0(FU[o + 1]) - fmin0(FU[o]) + fmax0(FV[o + sj]) - fmin0(FV[o]); };
   double wi = 0.0;
   Wi[0] = 0.0;
+  // pipe sources enter Wi level by level (omega.F:102-108)
+  const int pidx = d.p.npip > 0 ? F.pipe_idx[ij] : 0;
+  if (pidx > 0) {
+    const double pflx = F.pipe_flx[ij];
+    const double* __restrict__ prf = F.pipe_prf + (pidx - 1);
+    for (int k = 1; k <= N; k++) {
+      const long o = (long)(k - 1) * n2;
+      wi = wi - FU[o + 1] + FU[o] - FV[o + sj] + FV[o];
+      wi = wi + pflx * prf[(long)(k - 1) * d.p.npip];
+      Wi[(long)k * n2] = wi;
+    }
+  } else {
 #pragma unroll 8
-  for (int k = 1; k <= N; k++) {
-    const long o = (long)(k - 1) * n2;
-    wi = wi - FU[o + 1] + FU[o] - FV[o + sj] + FV[o];
-    Wi[(long)k * n2] = wi;
+    for (int k = 1; k <= N; k++) {
+      const long o = (long)(k - 1) * n2;
+      wi = wi - FU[o + 1] + FU[o] - FV[o + sj] + FV[o];
+      Wi[(long)k * n2] = wi;
+    }
   }
   wi = wi + F.swflx[ij] * F.dm_r[ij] * F.dn_r[ij];
   const double zw0 = zw[0];

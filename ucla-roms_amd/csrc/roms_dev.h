@@ -32,8 +32,10 @@ struct Bounds {
 struct Params {
   int nonlin_eos, salinity, lmd, uv_vis2, ts_dif2;
   int s2d_split;  // 1: step2d as separate zeta / momentum kernels (ROMS_GPU_S2D_SPLIT=1)
+  int npip;       // pipe_frc.F: number of pipes (0: pipe_source off)
   double dt, dtfast, g, rho0, vonKar, qp2, gamma2, hc;
   double rdrg, Zob, Tcoef, T0, Scoef, S0;
+  double Akv_bak, Akt_bak[2];  // scalars.F:83
 };
 
 // Device pointers of the model state (the "module arrays") plus scratch.
@@ -57,6 +59,12 @@ struct Fields {
   double *ru, *rv, *P, *rhos;
   double *c0, *c1, *c2, *c3;   // (0:N) column scratch, w-point layout
   double *s0, *s1, *s2, *s3, *s4, *s5, *s6, *s7, *s8, *s9;  // 2-D scratch (step2d, diag)
+  // lmd_vmix / lmd_kpp private work arrays: raw Richardson number (0:N) and
+  // the 2-D boundary-layer fields carried from the extended-range pass
+  double *lmd_rig, *lmd_hbl, *lmd_bbl, *lmd_Bo, *lmd_Bosol, *lmd_ustar;
+  // pipe_frc.F: pipe_idx (0: none), pipe_flx, pipe_prf(npip,N), pipe_trc(npip,NT)
+  int* pipe_idx;
+  double *pipe_flx, *pipe_prf, *pipe_trc;
 };
 
 struct Halo;  // halo.h: multi-rank exchange state (host object; nullptr = single rank)
@@ -165,5 +173,7 @@ void launch_u3dbc(const Dev& d, hipStream_t s, const Tlev& t);
 void launch_v3dbc(const Dev& d, hipStream_t s, const Tlev& t);
 void launch_t3dbc(const Dev& d, hipStream_t s, const Tlev& t, int itrc);
 void launch_diag(const Dev& d, hipStream_t s, const Tlev& t, double* partials);
+void launch_swr_frac(const Dev& d, hipStream_t s);
+void launch_lmd_vmix(const Dev& d, hipStream_t s, const Tlev& t, int tind);
 
 }  // namespace roms

@@ -184,6 +184,7 @@ void free_all() {
     if (g.f[id].d) { (void)hipFree(g.f[id].d); g.f[id] = FieldDesc{}; }
   for (double* p : g.scratch) (void)hipFree(p);
   g.scratch.clear();
+  if (g.d.f.pipe_idx) { (void)hipFree(g.d.f.pipe_idx); g.d.f.pipe_idx = nullptr; }
   if (g.h_diag) { (void)hipHostFree(g.h_diag); g.h_diag = nullptr; }
   if (g.s) { (void)hipStreamDestroy(g.s); g.s = nullptr; }
   g.inited = false;
@@ -214,6 +215,7 @@ void enqueue_step(roms_tlev* t) {
   TIMED(ROMS_R_RHO_EOS, launch_rho_eos(d, s, T, T.nrhs));
   TIMED(ROMS_R_SET_HUV, launch_set_huv(d, s, T));
   TIMED(ROMS_R_OMEGA, launch_omega(d, s, T));
+  if (g.cfg.lmd_mixing) TIMED(ROMS_R_LMD_VMIX, launch_lmd_vmix(d, s, T, T.nstp));
   TIMED(ROMS_R_PRSGRD, launch_prsgrd(d, s, T));
   TIMED(ROMS_R_PRE_STEP3D, launch_pre_step3d(d, s, T));
   TIMED(ROMS_R_SET_HUV1, launch_set_huv1(d, s, T));
@@ -222,6 +224,7 @@ void enqueue_step(roms_tlev* t) {
   T = to_tlev(t);
   TIMED(ROMS_R_OMEGA, launch_omega(d, s, T));
   TIMED(ROMS_R_RHO_EOS, launch_rho_eos(d, s, T, T.nrhs));
+  if (g.cfg.lmd_mixing) TIMED(ROMS_R_LMD_VMIX, launch_lmd_vmix(d, s, T, T.nrhs));
   TIMED(ROMS_R_PRSGRD, launch_prsgrd(d, s, T));
   TIMED(ROMS_R_STEP3D_UV1, launch_step3d_uv1(d, s, T));
   if (g.cfg.uv_vis2) TIMED(ROMS_R_VISC3D, launch_visc3d(d, s, T));
@@ -253,7 +256,6 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
   if (!dims || !cfg) { g.err = "roms_gpu_init: null argument"; return -1; }
   if (dims->N < 2 || dims->Lm < 2 || dims->Mm < 2 || dims->NT < 1) { g.err = "roms_gpu_init: bad dims"; return -1; }
   if (cfg->nfast < 1 || cfg->nfast > ROMS_MAX_FAST) { g.err = "roms_gpu_init: bad nfast"; return -1; }
-  if (cfg->lmd_mixing) { g.err = "roms_gpu_init: LMD_MIXING not available in this build"; return -4; }
   const int nranks = dims->np_xi * dims->np_eta;
   if (nranks < 1) { g.err = "roms_gpu_init: bad processor grid"; return -1; }
   if (nranks > 1 && comm == nullptr) { g.err = "roms_gpu_init: np_xi*np_eta > 1 needs a communicator"; return -1; }
@@ -280,6 +282,8 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
   P.dt = cfg->dt; P.dtfast = cfg->dt / (double)cfg->ndtfast; P.g = cfg->g; P.rho0 = cfg->rho0;
   P.vonKar = 0.41; P.qp2 = 0.0000172; P.gamma2 = cfg->gamma2; P.hc = cfg->hc;
   P.rdrg = cfg->rdrg; P.Zob = cfg->Zob; P.Tcoef = cfg->Tcoef; P.T0 = cfg->T0; P.Scoef = cfg->Scoef; P.S0 = cfg->S0;
+  P.Akv_bak = cfg->Akv_bak; P.Akt_bak[0] = cfg->Akt_bak[0]; P.Akt_bak[1] = cfg->Akt_bak[1];
+  P.npip = 0;
   for (int i = 0; i < kMaxFast; i++) { g.w1[i] = cfg->weight[0][i]; g.w2[i] = cfg->weight[1][i]; }
   if (!setup_column_kernels(dims->N)) {
     g.err = "roms_gpu_init: N too large for the LDS column kernels (2*(N+1)*512 B > 160 KB)";
@@ -309,6 +313,12 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
   double** s2[] = {&F.s0, &F.s1, &F.s2, &F.s3, &F.s4, &F.s5, &F.s6, &F.s7, &F.s8, &F.s9};
   for (double** q : s2)
     if (scratch(*q, b.n2)) return -2;
+  if (P.lmd) {
+    if (scratch(F.lmd_rig, b.n3w)) return -2;
+    double** l2[] = {&F.lmd_hbl, &F.lmd_bbl, &F.lmd_Bo, &F.lmd_Bosol, &F.lmd_ustar};
+    for (double** q : l2)
+      if (scratch(*q, b.n2)) return -2;
+  }
   CHECK_HIP(hipHostMalloc(&g.h_diag, (size_t)8 * b.n2 * sizeof(double), hipHostMallocDefault));
   if (comm != nullptr) {
     const HaloPlan plan = halo_plan(dims->Lm, dims->Mm, dims->np_xi, dims->np_eta, dims->inode, dims->jnode,
@@ -412,10 +422,51 @@ int roms_gpu_rho_eos(int tidx, const roms_tlev* t) {
   return post_launch();
 }
 int roms_gpu_lmd_vmix(int tind, const roms_tlev* t) {
-  (void)tind; (void)t;
   REQUIRE_INIT();
-  g.err = "roms_gpu_lmd_vmix: LMD_MIXING not available in this build";
-  return -4;
+  if (!g.cfg.lmd_mixing) { g.err = "roms_gpu_lmd_vmix: library initialised without lmd_mixing"; return -4; }
+  if (tind < 1 || tind > 3) { g.err = "roms_gpu_lmd_vmix: bad time index"; return -1; }
+  launch_lmd_vmix(g.d, g.s, to_tlev(t), tind);
+  return post_launch();
+}
+int roms_gpu_swr_frac(const roms_tlev* t) {
+  (void)t;
+  REQUIRE_INIT();
+  launch_swr_frac(g.d, g.s);
+  return post_launch();
+}
+int roms_gpu_set_pipe_frc(int npip, const int* pipe_idx, const double* pipe_flx, const double* pipe_prf,
+                          const double* pipe_trc) {
+  REQUIRE_INIT();
+  const Bounds& b = g.d.b;
+  Fields& F = g.d.f;
+  if (npip < 0 || (npip > 0 && (!pipe_idx || !pipe_flx || !pipe_prf || !pipe_trc))) {
+    g.err = "roms_gpu_set_pipe_frc: bad argument";
+    return -1;
+  }
+  if (npip == 0) { g.d.p.npip = 0; return 0; }
+  for (long q = 0; q < b.n2; q++)
+    if (pipe_idx[q] < 0 || pipe_idx[q] > npip) { g.err = "roms_gpu_set_pipe_frc: pipe_idx out of 0..npip"; return -1; }
+  CHECK_HIP(hipStreamSynchronize(g.s));
+  if (npip != g.d.p.npip || !F.pipe_idx) {
+    // (re)allocate; captured graphs hold the old pointers
+    for (auto& kv : g.graphs) (void)hipGraphExecDestroy(kv.second);
+    g.graphs.clear();
+    if (F.pipe_idx) (void)hipFree(F.pipe_idx);
+    CHECK_HIP(hipMalloc(&F.pipe_idx, (size_t)b.n2 * sizeof(int)));
+    auto scratch = [&](double*& p, long n) -> int {
+      CHECK_HIP(hipMalloc(&p, (size_t)n * sizeof(double)));
+      g.scratch.push_back(p);
+      return 0;
+    };
+    if (scratch(F.pipe_flx, b.n2) || scratch(F.pipe_prf, (long)npip * b.N) || scratch(F.pipe_trc, (long)npip * b.NT))
+      return -2;
+    g.d.p.npip = npip;
+  }
+  CHECK_HIP(hipMemcpy(F.pipe_idx, pipe_idx, (size_t)b.n2 * sizeof(int), hipMemcpyHostToDevice));
+  CHECK_HIP(hipMemcpy(F.pipe_flx, pipe_flx, (size_t)b.n2 * sizeof(double), hipMemcpyHostToDevice));
+  CHECK_HIP(hipMemcpy(F.pipe_prf, pipe_prf, (size_t)npip * b.N * sizeof(double), hipMemcpyHostToDevice));
+  CHECK_HIP(hipMemcpy(F.pipe_trc, pipe_trc, (size_t)npip * b.NT * sizeof(double), hipMemcpyHostToDevice));
+  return 0;
 }
 
 int roms_gpu_step(roms_tlev* t) {
@@ -462,6 +513,7 @@ int roms_gpu_init_sequence(roms_tlev* t) {
   REQUIRE_INIT();
   const Tlev T = to_tlev(t);
   launch_set_depth(g.d, g.s, T);
+  if (g.cfg.lmd_mixing) launch_swr_frac(g.d, g.s);  // main.F:217-220 (zeta at rest)
   launch_set_huv(g.d, g.s, T);
   launch_omega(g.d, g.s, T);
   launch_rho_eos(g.d, g.s, T, T.nrhs);
@@ -479,7 +531,8 @@ static int init_case_impl(const roms_case* c, int np_xi, int np_eta, void* comm,
   D.inode = rank - D.jnode * np_xi;
   rank_extent(c->LLm, np_xi, D.inode, D.Lm, D.iSW_corn);
   rank_extent(c->MMm, np_eta, D.jnode, D.Mm, D.jSW_corn);
-  const bool fil = c->case_id == ROMS_CASE_FILAMENT;
+  if (c->case_id < ROMS_CASE_FILAMENT || c->case_id > ROMS_CASE_PIPES) { g.err = "roms_gpu_init_case: unknown case"; return -1; }
+  const bool fil = c->case_id == ROMS_CASE_FILAMENT, pipes = c->case_id == ROMS_CASE_PIPES;
   D.ew_periodic = D.ns_periodic = fil ? 1 : 0;
   if (!D.ew_periodic) { D.west_exchng = D.inode > 0; D.east_exchng = D.inode < np_xi - 1; }
   if (!D.ns_periodic) { D.south_exchng = D.jnode > 0; D.north_exchng = D.jnode < np_eta - 1; }
@@ -491,8 +544,9 @@ static int init_case_impl(const roms_case* c, int np_xi, int np_eta, void* comm,
   C.g = 9.81; C.rho0 = fil ? 1000.0 : 1027.5; C.gamma2 = 1.0;
   C.rdrg = 0.0; C.rdrg2 = 1.0e-3; C.Zob = 1.0e-2;
   C.Tcoef = 0.20; C.T0 = 1.0; C.Scoef = 0.822; C.S0 = 1.0;
-  C.theta_s = 6.0; C.theta_b = 2.0; C.hc = fil ? 25.0 : 250.0;
-  C.Akv_bak = fil ? 0.0 : 1.0e-4; C.Akt_bak[0] = fil ? 0.0 : 1.0e-5; C.Akt_bak[1] = C.Akt_bak[0];
+  C.theta_s = 6.0; C.theta_b = pipes ? 6.0 : 2.0; C.hc = (fil || pipes) ? 25.0 : 250.0;
+  // tests/Pipes_ana/benchmark.in has no vertical_mixing line: Akv_bak = Akt_bak = 0
+  C.Akv_bak = (fil || pipes) ? 0.0 : 1.0e-4; C.Akt_bak[0] = (fil || pipes) ? 0.0 : 1.0e-5; C.Akt_bak[1] = C.Akt_bak[0];
   int r = roms_gpu_init(&D, &C, device, comm);
   if (r) return r;
   CaseSpec cs{};
@@ -502,7 +556,7 @@ static int init_case_impl(const roms_case* c, int np_xi, int np_eta, void* comm,
   cs.west_exchng = D.west_exchng; cs.east_exchng = D.east_exchng;
   cs.south_exchng = D.south_exchng; cs.north_exchng = D.north_exchng;
   cs.host_wrap = comm == nullptr;   // with a communicator the device exchange fills halos
-  cs.salinity = c->salinity; cs.theta_s = C.theta_s; cs.theta_b = C.theta_b; cs.hc = C.hc; cs.rho0 = C.rho0;
+  cs.salinity = c->salinity; cs.lmd = c->lmd_mixing; cs.surf_flux = c->case_id == ROMS_CASE_BASIN ? c->surf_flux : 0; cs.theta_s = C.theta_s; cs.theta_b = C.theta_b; cs.hc = C.hc; cs.rho0 = C.rho0;
   cs.Tcoef = C.Tcoef; cs.visc2 = 0.0; cs.tnu2 = 0.0; cs.Akv_bak = C.Akv_bak;
   cs.Akt_bak[0] = C.Akt_bak[0]; cs.Akt_bak[1] = C.Akt_bak[1];
   cs.sizex = c->sizex; cs.sizey = c->sizey;
@@ -522,6 +576,10 @@ static int init_case_impl(const roms_case* c, int np_xi, int np_eta, void* comm,
   for (int id = 0; id < ROMS_NFIELDS; id++) {
     if (H.arr[id].empty()) continue;
     r = roms_gpu_copy_in(id, H.arr[id].data(), (long)H.arr[id].size());
+    if (r) return r;
+  }
+  if (H.npip > 0) {
+    r = roms_gpu_set_pipe_frc(H.npip, H.pipe_idx.data(), H.pipe_flx.data(), H.pipe_prf.data(), H.pipe_trc.data());
     if (r) return r;
   }
   if (comm != nullptr) {

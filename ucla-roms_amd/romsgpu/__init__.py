@@ -25,7 +25,7 @@ FIELDS = ["h", "hinv", "f", "fomn", "pm", "pn", "dm_r", "dn_r", "dm_u", "dn_u", 
           "DU_avg_bak", "DV_avg_bak", "rho", "rho1", "qp1", "bvf", "Akv", "Akt", "visc2_r", "visc2_p", "diff2",
           "hbls", "hbbl", "ghat", "swr_frac", "sustr", "svstr", "stflx", "srflx", "swflx", "ru", "rv"]
 FIELD_ID = {n: i for i, n in enumerate(FIELDS)}
-CASE_FILAMENT, CASE_BASIN = 0, 1
+CASE_FILAMENT, CASE_BASIN, CASE_PIPES = 0, 1, 2
 
 
 class Dims(ctypes.Structure):
@@ -57,11 +57,11 @@ class Case(ctypes.Structure):
     _fields_ = [("case_id", ctypes.c_int), ("LLm", ctypes.c_int), ("MMm", ctypes.c_int), ("N", ctypes.c_int),
                 ("NT", ctypes.c_int), ("salinity", ctypes.c_int), ("nonlin_eos", ctypes.c_int),
                 ("lmd_mixing", ctypes.c_int), ("dt", ctypes.c_double), ("ndtfast", ctypes.c_int),
-                ("sizex", ctypes.c_double), ("sizey", ctypes.c_double)]
+                ("sizex", ctypes.c_double), ("sizey", ctypes.c_double), ("surf_flux", ctypes.c_int)]
 
 
 ROUTINES_T = ["set_huv", "omega", "prsgrd", "pre_step3d", "set_huv1", "step3d_uv1", "visc3d", "step2d",
-              "step3d_uv2", "step3d_t", "t3dmix", "set_depth", "step", "init_sequence"]
+              "step3d_uv2", "step3d_t", "t3dmix", "set_depth", "swr_frac", "step", "init_sequence"]
 
 _lib = None
 
@@ -86,6 +86,8 @@ def load_library(path=LIB_PATH):
         getattr(L, "roms_gpu_" + fn).argtypes = [P(Tlev)]
     L.roms_gpu_rho_eos.argtypes = [ctypes.c_int, P(Tlev)]
     L.roms_gpu_lmd_vmix.argtypes = [ctypes.c_int, P(Tlev)]
+    L.roms_gpu_set_pipe_frc.argtypes = [ctypes.c_int, P(ctypes.c_int), P(ctypes.c_double), P(ctypes.c_double),
+                                        P(ctypes.c_double)]
     L.roms_gpu_diag.argtypes = [P(Tlev), P(ctypes.c_double)]
     L.roms_gpu_time_steps.argtypes = [P(Tlev), ctypes.c_int, P(ctypes.c_double)]
     L.roms_gpu_stream.restype = ctypes.c_void_p
@@ -155,7 +157,7 @@ def halo_map(Lm, Mm, np_xi, np_eta, inode, jnode, ew_periodic, ns_periodic, dire
 HALO_DIRS = ("W", "E", "S", "N", "SW", "SE", "NW", "NE")
 # enum roms_routine of include/roms_gpu.h
 ROUTINES = ("rho_eos", "set_HUV", "omega", "prsgrd", "pre_step3d", "set_HUV1", "step3d_uv1", "visc3d", "step2d",
-            "step3d_uv2", "step3d_t", "t3dmix")
+            "step3d_uv2", "step3d_t", "t3dmix", "lmd_vmix")
 HALO_OPP = (1, 0, 3, 2, 7, 6, 5, 4)
 
 
@@ -203,11 +205,13 @@ class Model:
     # ---- construction ----
     @classmethod
     def from_case(cls, case_id, LLm, MMm, N, NT=1, salinity=False, nonlin_eos=False, dt=5.0, ndtfast=60,
-                  sizex=12.8e3, sizey=3.2e3, device=0, np_xi=1, np_eta=1, comm=None, rank=0):
+                  sizex=12.8e3, sizey=3.2e3, device=0, np_xi=1, np_eta=1, comm=None, rank=0, lmd=False,
+                  surf_flux=False):
         """Analytic case on the whole grid, or on subdomain `rank` of an
         np_xi x np_eta processor grid when a communicator is given."""
         m = cls()
-        c = Case(case_id, LLm, MMm, N, NT, int(salinity), int(nonlin_eos), 0, dt, ndtfast, sizex, sizey)
+        c = Case(case_id, LLm, MMm, N, NT, int(salinity), int(nonlin_eos), int(lmd), dt, ndtfast, sizex, sizey,
+                 int(surf_flux))
         if comm is None and np_xi * np_eta == 1:
             m._chk(m.L.roms_gpu_init_case(ctypes.byref(c), device, ctypes.byref(m.t)), "roms_gpu_init_case")
         else:
@@ -264,6 +268,20 @@ class Model:
     def lmd_vmix(self, tind):
         self._chk(self.L.roms_gpu_lmd_vmix(tind, ctypes.byref(self.t)), "lmd_vmix")
 
+    def set_pipe_frc(self, pipe_idx, pipe_flx, pipe_prf, pipe_trc):
+        """pipe_frc.F:set_pipe_frc: pipe_idx/pipe_flx on the (Mm+4, Lm+4) grid,
+        pipe_prf (npip, N) and pipe_trc (npip, NT)."""
+        prf = np.asarray(pipe_prf, dtype=np.float64)
+        npip = prf.shape[0]
+        idx = np.ascontiguousarray(pipe_idx, dtype=np.int32).ravel()
+        flx = np.ascontiguousarray(pipe_flx, dtype=np.float64).ravel()
+        prf = np.asfortranarray(prf).ravel(order="F")
+        trc = np.asarray(pipe_trc, dtype=np.float64).ravel(order="F")
+        P = ctypes.POINTER
+        self._chk(self.L.roms_gpu_set_pipe_frc(npip, idx.ctypes.data_as(P(ctypes.c_int)), flx.ctypes.data_as(P(ctypes.c_double)),
+                                               prf.ctypes.data_as(P(ctypes.c_double)), trc.ctypes.data_as(P(ctypes.c_double))),
+                  "set_pipe_frc")
+
     def _r(self, fn):
         self._chk(getattr(self.L, "roms_gpu_" + fn)(ctypes.byref(self.t)), fn)
 
@@ -279,6 +297,7 @@ class Model:
     def step3d_t(self): self._r("step3d_t")
     def t3dmix(self): self._r("t3dmix")
     def set_depth(self): self._r("set_depth")
+    def swr_frac(self): self._r("swr_frac")
     def init_sequence(self): self._r("init_sequence")
 
     def step(self, n=1):
