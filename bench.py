@@ -18,7 +18,11 @@ wall second beside it.  roofline: per-routine algorithmic bytes (SURVEY.md
 library stream; the dominant routine (largest time per step) is reported,
 the full table under "routines".
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+--workload c3 (not the default): SURVEY.md 8(d) C3, the 1024x1024x100 closed
+basin with NONLIN+SPLIT EOS, T+S and LMD/KPP/BKPP mixing (dt=300 s, nfast=82),
+strong-scaled over the processor grid (the north_star's roofline target).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3]
 """
 import argparse
 import json
@@ -37,19 +41,27 @@ LLM, MMM, NZ, NT = 512, 512, 50, 2
 DT, NDTFAST = 5.0, 60
 SIZEX, SIZEY = 51.2e3, 12.8e3
 NT_TS = 2
+# C3 workload, whole domain (strong scaling)
+C3_L, C3_N, C3_DT, C3_DX = 1024, 100, 300.0, 2.0e3
 
 
-def routine_passes(NT_, NT_TS_):
-    """SURVEY.md 8(d): unique 3-D array passes per call (linear EOS, no LMD);
-    step2d counts 35 2-D passes per fast step (flagged with None)."""
+def routine_passes(NT_, NT_TS_, lmd=False):
+    """unique 3-D array passes per call; step2d counts 35 2-D
+    passes per fast step (flagged with None).  lmd: the C3 switch set
+    (NONLIN+SPLIT EOS, SALINITY, LMD/KPP), P3D = 150 + 10*NT."""
+    if lmd:
+        return {"rho_eos": 7, "set_HUV": 7, "omega": 6, "prsgrd": 6, "pre_step3d": 18 + 4 * NT_, "set_HUV1": 7,
+                "step3d_uv1": 14, "visc3d": 7, "step2d": None, "step3d_uv2": 11, "step3d_t": 9 + 3 * NT_,
+                "t3dmix": 1 + 3 * NT_, "lmd_vmix": 11}
     return {"rho_eos": 2 + NT_TS_, "set_HUV": 7, "omega": 6, "prsgrd": 5, "pre_step3d": 16 + NT_TS_ + 4 * NT_,
             "set_HUV1": 7, "step3d_uv1": 14, "visc3d": 7, "step2d": None, "step3d_uv2": 11,
-            "step3d_t": 5 + NT_TS_ + 3 * NT_, "t3dmix": 1 + 3 * NT_}
+            "step3d_t": 5 + NT_TS_ + 3 * NT_, "t3dmix": 1 + 3 * NT_, "lmd_vmix": 0}
 
 
-def step_bytes(I, J, N, NT_, NT_TS_, nfast):
-    """B_step = 8*(P3D*I*J*N + 35*nfast*I*J), P3D = 105+5*NT_TS+10*NT."""
-    P3D = 105 + 5 * NT_TS_ + 10 * NT_
+def step_bytes(I, J, N, NT_, NT_TS_, nfast, lmd=False):
+    """B_step = 8*(P3D*I*J*N + 35*nfast*I*J),
+    P3D = 105+5*NT_TS+10*NT (Filament) or 150+10*NT (C3 switches)."""
+    P3D = (150 + 10 * NT_) if lmd else (105 + 5 * NT_TS_ + 10 * NT_)
     return 8.0 * (P3D * I * J * N + 35.0 * nfast * I * J)
 
 
@@ -61,6 +73,34 @@ def proc_grid(n):
     while n % npx:
         npx -= 1
     return npx, n // npx
+
+
+def cpu_baseline_c3(nsteps=2, L=128):
+    """Oracle on a bounded LxLx100 cut of the C3 basin (same switches, dx)."""
+    import oracle
+    c = oracle.OrCfg()
+    c.LLm, c.MMm, c.N, c.NT = L, L, C3_N, 2
+    c.ew_periodic = c.ns_periodic = 0
+    c.salinity, c.nonlin_eos, c.lmd = 1, 1, 1
+    c.case_id = oracle.CASE_BASIN
+    c.dt, c.ndtfast = C3_DT, NDTFAST
+    c.theta_s, c.theta_b, c.hc, c.rho0 = 6.0, 2.0, 250.0, 1027.5
+    c.rdrg, c.rdrg2, c.Zob = 0.0, 1.0e-3, 1.0e-2
+    c.Akv_bak = 1.0e-4
+    c.Akt_bak[0] = c.Akt_bak[1] = 1.0e-5
+    c.Tcoef, c.T0, c.Scoef, c.S0 = 0.20, 1.0, 0.822, 1.0
+    c.sizex = c.sizey = C3_DX * L
+    c.diag_np_xi = c.diag_np_eta = 1
+    o = oracle.Oracle(c)
+    o.init()
+    t0 = time.perf_counter()
+    o.step(nsteps)
+    dt_wall = time.perf_counter() - t0
+    cells = L * L * C3_N
+    return {"value": nsteps * cells / dt_wall, "unit": "cell-updates/s", "cores": 1, "kind": "port",
+            "sample": "%d roms_step of a %dx%dx%d cut of the C3 basin (LMD/KPP, nonlinear EOS) on the oracle "
+                      "(oracle/, gcc -O2, 1 thread), %.1f s" % (nsteps, L, L, C3_N, dt_wall),
+            "model_seconds_per_wallclock_sec": nsteps * C3_DT / dt_wall * cells / (C3_L * C3_L * C3_N)}
 
 
 def cpu_baseline(nsteps=3):
@@ -107,7 +147,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--timing-steps", type=int, default=3, help="eager steps per routine for the event timings")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", choices=("c2", "c3"), default="c2")
     args = ap.parse_args()
+    c3 = args.workload == "c3"
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -134,10 +176,17 @@ def main():
         dist.broadcast(uid, src=0)
         comm = romsgpu.comm_create(bytes(uid.cpu().numpy().tobytes()), world, rank, local_rank)
 
-    m = romsgpu.Model.from_case(romsgpu.CASE_FILAMENT, LLM * npx, MMM * npe, NZ, NT, salinity=True, dt=DT,
-                                ndtfast=NDTFAST, sizex=SIZEX * npx, sizey=SIZEY * npe, device=local_rank,
-                                np_xi=npx, np_eta=npe, comm=comm, rank=rank)
-    assert (m.Lm, m.Mm) == (LLM, MMM)
+    if c3:
+        m = romsgpu.Model.from_case(romsgpu.CASE_BASIN, C3_L, C3_L, C3_N, NT, salinity=True, nonlin_eos=True,
+                                    lmd=True, dt=C3_DT, ndtfast=NDTFAST, sizex=C3_DX * C3_L, sizey=C3_DX * C3_L,
+                                    device=local_rank, np_xi=npx, np_eta=npe, comm=comm, rank=rank)
+        Lr, Mr, Nz, dt_step = m.Lm, m.Mm, C3_N, C3_DT
+    else:
+        m = romsgpu.Model.from_case(romsgpu.CASE_FILAMENT, LLM * npx, MMM * npe, NZ, NT, salinity=True, dt=DT,
+                                    ndtfast=NDTFAST, sizex=SIZEX * npx, sizey=SIZEY * npe, device=local_rank,
+                                    np_xi=npx, np_eta=npe, comm=comm, rank=rank)
+        assert (m.Lm, m.Mm) == (LLM, MMM)
+        Lr, Mr, Nz, dt_step = LLM, MMM, NZ, DT
     nfast = m.t.nfast
     m.step(args.warmup)
     m.sync()
@@ -163,13 +212,15 @@ def main():
         elapsed = float(tt.item())
 
     # per-routine rooflines: HIP events around each routine's launches
-    cells3 = LLM * MMM * NZ
-    passes = routine_passes(NT, NT_TS)
+    cells3 = Lr * Mr * Nz
+    passes = routine_passes(NT, NT_TS, lmd=c3)
     routines = {}
     for r in romsgpu.ROUTINES:
+        if passes[r] == 0:
+            continue
         avg, n = m.time_routine(r, args.timing_steps)
         per_step = n / args.timing_steps
-        nbytes = 35.0 * 8 * LLM * MMM if passes[r] is None else 8.0 * passes[r] * cells3
+        nbytes = 35.0 * 8 * Lr * Mr if passes[r] is None else 8.0 * passes[r] * cells3
         gbs = nbytes / (avg * 1e-3) / 1e9 if avg > 0 else 0.0
         routines[r] = {"ms_per_call": avg, "calls_per_step": per_step, "ms_per_step": avg * per_step,
                        "bytes_per_call": nbytes, "achieved_GBs": gbs, "frac": gbs / HBM_PEAK_GBS}
@@ -182,27 +233,30 @@ def main():
         raise SystemExit("bench: non-finite diag norms %r" % norms)
 
     ms_step = 1e3 * elapsed / args.steps
-    B = step_bytes(LLM, MMM, NZ, NT, NT_TS, nfast)
+    B = step_bytes(Lr, Mr, Nz, NT, NT_TS, nfast, lmd=c3)
     step_gbs = B / (ms_step * 1e-3) / 1e9
-    traffic = pmc_traffic(dom)
+    traffic = None if c3 else pmc_traffic(dom)   # profiles/pmc_traffic.json is measured on C2
 
     out = {
         "metric": "grid-cell-updates/sec",
-        "value": world * cells3 * args.steps / elapsed,
+        "value": (C3_L * C3_L * C3_N if c3 else world * cells3) * args.steps / elapsed,
         "unit": "cell-updates/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": ms_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if c3 else "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (analytic Filament+S initial state, ana_grid/ana_init of tests/Filament)",
-        "config": {"workload": "C2: Filament+S 512x512x50 per GPU, NT=2, dt=5s, ndtfast=60 (nfast=%d)" % nfast,
-                   "grid_per_gpu": [LLM, MMM, NZ], "proc_grid": [npx, npe], "NT": NT, "dt": DT, "nfast": nfast,
+        "data": ("synthetic (analytic closed basin, SURVEY.md 8(d) C3)" if c3 else
+                 "synthetic (analytic Filament+S initial state, ana_grid/ana_init of tests/Filament)"),
+        "config": {"workload": ("C3: basin 1024x1024x100, NONLIN+SPLIT EOS, T+S, LMD/KPP/BKPP, dt=300s, ndtfast=60 "
+                                "(nfast=%d)" % nfast) if c3 else
+                               "C2: Filament+S 512x512x50 per GPU, NT=2, dt=5s, ndtfast=60 (nfast=%d)" % nfast,
+                   "grid_per_gpu": [Lr, Mr, Nz], "proc_grid": [npx, npe], "NT": NT, "dt": dt_step, "nfast": nfast,
                    "parallelism": "domain decomposition %dx%d, RCCL halo exchange" % (npx, npe)},
-        "model_seconds_per_wallclock_sec": args.steps * DT / elapsed,
+        "model_seconds_per_wallclock_sec": args.steps * dt_step / elapsed,
         "roofline": {"bound": "hbm", "achieved": D["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": D["frac"], "traffic": traffic,
                      "kernel": dom + (" (one fast step: k_s2d_zeta + k_s2d_mom + halo)" if dom == "step2d" else ""),
@@ -212,7 +266,7 @@ def main():
         "routines": routines,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline()
+        out["cpu_baseline"] = cpu_baseline_c3() if c3 else cpu_baseline()
     m.close()
     if comm is not None:
         romsgpu.comm_destroy(comm)

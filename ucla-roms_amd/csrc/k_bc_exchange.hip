@@ -86,109 +86,102 @@ void launch_exchange(const Dev& d, hipStream_t s, double* a, int nlev) {
   launch_exchange_list(d, s, L);
 }
 
-// ---- 3-D closed-wall BCs: one lane per edge point, loop over k ----
+// ---- 3-D closed-wall BCs: one lane per (edge point, level k = 1 + blockIdx.y) ----
 // phase 0 sets the wall-normal component, phase 1 the tangential one (which
 // reads the former, as the sequential reference loop order implies)
 __global__ void k_u3dbc(Bounds b, double gamma2, const double* __restrict__ umask, double* __restrict__ u,
                         int nnew, int phase) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x, k = 1 + (int)blockIdx.y;
   const int nj = b.jend - b.jstr + 1, ni = b.iendR - b.istr + 1;
   if (phase == 0) {
     if (p >= nj) return;
     const int j = b.jstr + p;
-    for (int k = 1; k <= b.N; k++) {
-      if (b.west_edge) u[IJKL(b, b.istr, j, k, nnew)] = 0.0;
-      if (b.east_edge) u[IJKL(b, b.iend + 1, j, k, nnew)] = 0.0;
-    }
+    if (b.west_edge) u[IJKL(b, b.istr, j, k, nnew)] = 0.0;
+    if (b.east_edge) u[IJKL(b, b.iend + 1, j, k, nnew)] = 0.0;
   } else if (p < ni) {
     const int i = b.istr + p;
-    for (int k = 1; k <= b.N; k++) {
-      if (b.south_edge)
-        u[IJKL(b, i, b.jstr - 1, k, nnew)] = gamma2 * u[IJKL(b, i, b.jstr, k, nnew)] * umask[IJ(b, i, b.jstr - 1)];
-      if (b.north_edge)
-        u[IJKL(b, i, b.jend + 1, k, nnew)] = gamma2 * u[IJKL(b, i, b.jend, k, nnew)] * umask[IJ(b, i, b.jend + 1)];
-    }
+    if (b.south_edge)
+      u[IJKL(b, i, b.jstr - 1, k, nnew)] = gamma2 * u[IJKL(b, i, b.jstr, k, nnew)] * umask[IJ(b, i, b.jstr - 1)];
+    if (b.north_edge)
+      u[IJKL(b, i, b.jend + 1, k, nnew)] = gamma2 * u[IJKL(b, i, b.jend, k, nnew)] * umask[IJ(b, i, b.jend + 1)];
   }
 }
 __global__ void k_v3dbc(Bounds b, double gamma2, const double* __restrict__ vmask, double* __restrict__ v,
                         int nnew, int phase) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x, k = 1 + (int)blockIdx.y;
   const int ni = b.iend - b.istr + 1, nj = b.jendR - b.jstr + 1;
   if (phase == 0) {
     if (p >= ni) return;
     const int i = b.istr + p;
-    for (int k = 1; k <= b.N; k++) {
-      if (b.south_edge) v[IJKL(b, i, b.jstr, k, nnew)] = 0.0;
-      if (b.north_edge) v[IJKL(b, i, b.jend + 1, k, nnew)] = 0.0;
-    }
+    if (b.south_edge) v[IJKL(b, i, b.jstr, k, nnew)] = 0.0;
+    if (b.north_edge) v[IJKL(b, i, b.jend + 1, k, nnew)] = 0.0;
   } else if (p < nj) {
     const int j = b.jstr + p;
-    for (int k = 1; k <= b.N; k++) {
-      if (b.west_edge)
-        v[IJKL(b, b.istr - 1, j, k, nnew)] = gamma2 * v[IJKL(b, b.istr, j, k, nnew)] * vmask[IJ(b, b.istr - 1, j)];
-      if (b.east_edge)
-        v[IJKL(b, b.iend + 1, j, k, nnew)] = gamma2 * v[IJKL(b, b.iend, j, k, nnew)] * vmask[IJ(b, b.iend + 1, j)];
-    }
+    if (b.west_edge)
+      v[IJKL(b, b.istr - 1, j, k, nnew)] = gamma2 * v[IJKL(b, b.istr, j, k, nnew)] * vmask[IJ(b, b.istr - 1, j)];
+    if (b.east_edge)
+      v[IJKL(b, b.iend + 1, j, k, nnew)] = gamma2 * v[IJKL(b, b.iend, j, k, nnew)] * vmask[IJ(b, b.iend + 1, j)];
   }
 }
 // t3dbc: edges first, corners in a second launch (they read edge values)
 __global__ void k_t3dbc_edges(Bounds b, const double* __restrict__ rmask, double* __restrict__ t, int nnew, int itrc) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x, k = 1 + (int)blockIdx.y;
   const int nj = b.jend - b.jstr + 1, ni = b.iend - b.istr + 1;
   if (p < nj) {
     const int j = b.jstr + p;
-    for (int k = 1; k <= b.N; k++) {
-      if (b.west_edge) t[TIDX(b, b.istr - 1, j, k, nnew, itrc)] = t[TIDX(b, b.istr, j, k, nnew, itrc)] * rmask[IJ(b, b.istr - 1, j)];
-      if (b.east_edge) t[TIDX(b, b.iend + 1, j, k, nnew, itrc)] = t[TIDX(b, b.iend, j, k, nnew, itrc)] * rmask[IJ(b, b.iend + 1, j)];
-    }
+    if (b.west_edge) t[TIDX(b, b.istr - 1, j, k, nnew, itrc)] = t[TIDX(b, b.istr, j, k, nnew, itrc)] * rmask[IJ(b, b.istr - 1, j)];
+    if (b.east_edge) t[TIDX(b, b.iend + 1, j, k, nnew, itrc)] = t[TIDX(b, b.iend, j, k, nnew, itrc)] * rmask[IJ(b, b.iend + 1, j)];
   } else if (p < nj + ni) {
     const int i = b.istr + (p - nj);
-    for (int k = 1; k <= b.N; k++) {
-      if (b.south_edge) t[TIDX(b, i, b.jstr - 1, k, nnew, itrc)] = t[TIDX(b, i, b.jstr, k, nnew, itrc)] * rmask[IJ(b, i, b.jstr - 1)];
-      if (b.north_edge) t[TIDX(b, i, b.jend + 1, k, nnew, itrc)] = t[TIDX(b, i, b.jend, k, nnew, itrc)] * rmask[IJ(b, i, b.jend + 1)];
-    }
+    if (b.south_edge) t[TIDX(b, i, b.jstr - 1, k, nnew, itrc)] = t[TIDX(b, i, b.jstr, k, nnew, itrc)] * rmask[IJ(b, i, b.jstr - 1)];
+    if (b.north_edge) t[TIDX(b, i, b.jend + 1, k, nnew, itrc)] = t[TIDX(b, i, b.jend, k, nnew, itrc)] * rmask[IJ(b, i, b.jend + 1)];
   }
 }
-__device__ void t_corner(const Bounds& b, const double* rm, double* t, int nnew, int itrc, int ic, int jc, int ia,
-                         int ja, int ib, int jb) {
+__device__ void t_corner(const Bounds& b, const double* rm, double* t, int nnew, int itrc, int k, int ic, int jc,
+                         int ia, int ja, int ib, int jb) {
   double cff = rm[IJ(b, ia, ja)] + rm[IJ(b, ib, jb)];
   if (cff > 0.0) {
     cff = 1.0 / cff;
-    for (int k = 1; k <= b.N; k++)
-      t[TIDX(b, ic, jc, k, nnew, itrc)] = cff * (rm[IJ(b, ia, ja)] * t[TIDX(b, ia, ja, k, nnew, itrc)] +
-                                                 rm[IJ(b, ib, jb)] * t[TIDX(b, ib, jb, k, nnew, itrc)]);
+    t[TIDX(b, ic, jc, k, nnew, itrc)] = cff * (rm[IJ(b, ia, ja)] * t[TIDX(b, ia, ja, k, nnew, itrc)] +
+                                               rm[IJ(b, ib, jb)] * t[TIDX(b, ib, jb, k, nnew, itrc)]);
   } else {
-    for (int k = 1; k <= b.N; k++) t[TIDX(b, ic, jc, k, nnew, itrc)] = 0.0;
+    t[TIDX(b, ic, jc, k, nnew, itrc)] = 0.0;
   }
 }
+// one lane per (corner, level): corner c = lane & 3, k = 1 + lane / 4
 __global__ void k_t3dbc_corners(Bounds b, const double* __restrict__ rm, double* __restrict__ t, int nnew, int itrc) {
-  const int c = threadIdx.x;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = p & 3, k = 1 + (p >> 2);
+  if (k > b.N) return;
   const int is = b.istr, ie = b.iend, js = b.jstr, je = b.jend;
-  if (c == 0 && b.south_edge && b.west_edge) t_corner(b, rm, t, nnew, itrc, is - 1, js - 1, is, js - 1, is - 1, js);
-  if (c == 1 && b.south_edge && b.east_edge) t_corner(b, rm, t, nnew, itrc, ie + 1, js - 1, ie, js - 1, ie + 1, js);
-  if (c == 2 && b.north_edge && b.west_edge) t_corner(b, rm, t, nnew, itrc, is - 1, je + 1, is, je + 1, is - 1, je);
-  if (c == 3 && b.north_edge && b.east_edge) t_corner(b, rm, t, nnew, itrc, ie + 1, je + 1, ie, je + 1, ie + 1, je);
+  if (c == 0 && b.south_edge && b.west_edge) t_corner(b, rm, t, nnew, itrc, k, is - 1, js - 1, is, js - 1, is - 1, js);
+  if (c == 1 && b.south_edge && b.east_edge) t_corner(b, rm, t, nnew, itrc, k, ie + 1, js - 1, ie, js - 1, ie + 1, js);
+  if (c == 2 && b.north_edge && b.west_edge) t_corner(b, rm, t, nnew, itrc, k, is - 1, je + 1, is, je + 1, is - 1, je);
+  if (c == 3 && b.north_edge && b.east_edge) t_corner(b, rm, t, nnew, itrc, k, ie + 1, je + 1, ie, je + 1, ie + 1, je);
 }
 
 static inline bool closed_any(const Bounds& b) { return b.west_edge || b.east_edge || b.south_edge || b.north_edge; }
 
 void launch_u3dbc(const Dev& d, hipStream_t s, const Tlev& t) {
   if (!closed_any(d.b)) return;
-  const int n = (d.b.jend - d.b.jstr + 1) + (d.b.iendR - d.b.istr + 1);
+  const int n = (d.b.jend - d.b.jstr + 1) > (d.b.iendR - d.b.istr + 1) ? (d.b.jend - d.b.jstr + 1) : (d.b.iendR - d.b.istr + 1);
   for (int ph = 0; ph < 2; ph++)
-    hipLaunchKernelGGL(k_u3dbc, dim3((n + 255) / 256), dim3(256), 0, s, d.b, d.p.gamma2, d.f.umask, d.f.u, t.nnew, ph);
+    hipLaunchKernelGGL(k_u3dbc, dim3((n + 255) / 256, d.b.N), dim3(256), 0, s, d.b, d.p.gamma2, d.f.umask, d.f.u,
+                       t.nnew, ph);
 }
 void launch_v3dbc(const Dev& d, hipStream_t s, const Tlev& t) {
   if (!closed_any(d.b)) return;
-  const int n = (d.b.iend - d.b.istr + 1) + (d.b.jendR - d.b.jstr + 1);
+  const int n = (d.b.iend - d.b.istr + 1) > (d.b.jendR - d.b.jstr + 1) ? (d.b.iend - d.b.istr + 1) : (d.b.jendR - d.b.jstr + 1);
   for (int ph = 0; ph < 2; ph++)
-    hipLaunchKernelGGL(k_v3dbc, dim3((n + 255) / 256), dim3(256), 0, s, d.b, d.p.gamma2, d.f.vmask, d.f.v, t.nnew, ph);
+    hipLaunchKernelGGL(k_v3dbc, dim3((n + 255) / 256, d.b.N), dim3(256), 0, s, d.b, d.p.gamma2, d.f.vmask, d.f.v,
+                       t.nnew, ph);
 }
 void launch_t3dbc(const Dev& d, hipStream_t s, const Tlev& t, int itrc) {
   if (!closed_any(d.b)) return;
   const int n = (d.b.jend - d.b.jstr + 1) + (d.b.iend - d.b.istr + 1);
-  hipLaunchKernelGGL(k_t3dbc_edges, dim3((n + 255) / 256), dim3(256), 0, s, d.b, d.f.rmask, d.f.t, t.nnew, itrc);
-  hipLaunchKernelGGL(k_t3dbc_corners, dim3(1), dim3(64), 0, s, d.b, d.f.rmask, d.f.t, t.nnew, itrc);
+  hipLaunchKernelGGL(k_t3dbc_edges, dim3((n + 255) / 256, d.b.N), dim3(256), 0, s, d.b, d.f.rmask, d.f.t, t.nnew, itrc);
+  hipLaunchKernelGGL(k_t3dbc_corners, dim3((4 * d.b.N + 255) / 256), dim3(256), 0, s, d.b, d.f.rmask, d.f.t, t.nnew,
+                     itrc);
 }
 
 }  // namespace roms

@@ -31,6 +31,30 @@ __device__ __forceinline__ ColLds col_lds(int slot, int N) {
 }
 inline size_t col_lds_bytes(int nslots, int N) { return (size_t)nslots * (N + 1) * kCX * sizeof(double); }
 
+// The same column scratch in global memory (w-point layout, level k of column
+// ij at p[k*n2]: a wavefront still touches 64 consecutive doubles per level).
+// Deep columns use it: two LDS slots of N=100 levels are 103 KB per wave,
+// which leaves one wave per CU; in HBM (caught by L2 / Infinity Cache) the
+// solvers keep full occupancy.  Slot (z, s) of a kernel whose grid z indexes
+// tracers or directions lives at colscr + (2z + s)*n3w.
+struct ColGlb {
+  double* p;
+  long s;
+  __device__ __forceinline__ double& operator[](int k) const { return p[(long)k * s]; }
+};
+template <class C>
+struct ColMake;
+template <>
+struct ColMake<ColLds> {
+  __device__ static ColLds at(const Dev& d, int slot, int z, long ij) { return col_lds(slot, d.b.N); }
+};
+template <>
+struct ColMake<ColGlb> {
+  __device__ static ColGlb at(const Dev& d, int slot, int z, long ij) {
+    return ColGlb{d.f.colscr + ((long)z * 2 + slot) * d.b.n3w + ij, d.b.n2};
+  }
+};
+
 // ---- pseudo-continuity of the predictor (pre_step3d4S.F:136-148) ----
 __device__ __forceinline__ void hz_bak_fwd(const Dev& d, int i, int j, int k, double cff, double& bak, double& fwd) {
   const Bounds& b = d.b;
@@ -49,9 +73,10 @@ __device__ __forceinline__ void hz_bak_fwd(const Dev& d, int i, int j, int k, do
 // register ring kPF levels ahead of use (whole unrolled groups, then a
 // direct remainder), so the loads overlap the division chain.
 constexpr int kPF = 8;
+template <class C>
 __device__ __forceinline__ void tracer_spline_lds(int N, long n2, const double* __restrict__ Hz,
                                                   const double* __restrict__ Tr, const double* __restrict__ We,
-                                                  const ColLds& A, const ColLds& B) {
+                                                  const C& A, const C& B) {
     double cfk = 1.0, fcm = 2.0 * Tr[0], hk = Hz[0], tk = Tr[0];
     A[0] = fcm;
     // inputs of the next kPF levels stay in flight in a register ring (slot q
@@ -420,9 +445,9 @@ __device__ __forceinline__ void uv_vert_rhs(const Dev& d, int i, int j, int nrhs
 // of u (dir 0) / v (dir 1) at w-levels in A[k], k=0..N, A[0]=A[N]=0
 // (compute_vert_rhs_uv_terms.h); the r.h.s. update is rr(k) = rr(k) - A[k] +
 // A[k-1] in that order (uv_rr_update).
-template <bool kRing>
-__device__ __forceinline__ void uv_vert_flux_lds(const Dev& d, long ij, int nrhs, int dir, const ColLds& A,
-                                                 const ColLds& B) {
+template <bool kRing, class C>
+__device__ __forceinline__ void uv_vert_flux_lds(const Dev& d, long ij, int nrhs, int dir, const C& A,
+                                                 const C& B) {
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const int N = b.N;
@@ -505,7 +530,8 @@ __device__ __forceinline__ void uv_vert_flux_lds(const Dev& d, long ij, int nrhs
   A[0] = 0.0;
   A[N] = 0.0;
 }
-__device__ __forceinline__ double uv_rr_update(double r, const ColLds& A, int k) {
+template <class C>
+__device__ __forceinline__ double uv_rr_update(double r, const C& A, int k) {
   return k == 1 ? r - A[1] : r - A[k] + A[k - 1];
 }
 

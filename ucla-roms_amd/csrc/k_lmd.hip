@@ -166,6 +166,7 @@ __global__ void __launch_bounds__(256) k_swr_frac(Dev d, Range R) {
 }
 
 // ---- pass 1: extended range ----
+template <class C>
 __global__ void __launch_bounds__(64) k_kpp_ext(Dev d, Range E, int tind, int nstp, KppConst kc) {
   ROMS_IJC_OR_RETURN(E)
   const Bounds& b = d.b;
@@ -174,7 +175,7 @@ __global__ void __launch_bounds__(64) k_kpp_ext(Dev d, Range E, int tind, int ns
   const int N = b.N;
   const long n2 = b.n2, ij = IJ(b, i, j), sj = b.nx2;
   const double g = P.g, vonKar = P.vonKar, Ri_inv = 1. / kRicr;
-  const ColLds FC = col_lds(0, N);
+  const C FC = ColMake<C>::at(d, 0, 0, ij);
   // alfabeta.F:46-78 at t(N,nstp); Bo, Bosol, ustar (lmd_kpp.F:154-181)
   double alpha, beta;
   const double Tt = F.t[ij + (long)(N - 1) * n2 + (long)(nstp - 1) * b.n3];
@@ -485,7 +486,10 @@ void launch_lmd_vmix(const Dev& d, hipStream_t s, const Tlev& t, int tind) {
   kc.Cg = Cstar * vonKar * std::pow(c_s * vonKar * epssfc, 1. / 3.);
   kc.Vtc = Cv * std::sqrt(-betaT / (c_s * epssfc)) / (kRicr * (vonKar * vonKar));
   const int first = t.iic == t.forw_start;  // FIRST_TIME_STEP with EXACT_RESTART
-  hipLaunchKernelGGL(k_kpp_ext, gridc_of(E), dim3(kCX), col_lds_bytes(1, b.N), s, d, E, tind, t.nstp, kc);
+  if (d.f.colscr)
+    hipLaunchKernelGGL(k_kpp_ext<ColGlb>, gridc_of(E), dim3(kCX), 0, s, d, E, tind, t.nstp, kc);
+  else
+    hipLaunchKernelGGL(k_kpp_ext<ColLds>, gridc_of(E), dim3(kCX), col_lds_bytes(1, b.N), s, d, E, tind, t.nstp, kc);
   hipLaunchKernelGGL(k_kpp_int, gridc_of(R), dim3(kCX), 0, s, d, R, edge_clamp(b), tind, t.nstp, first, kc);
   // lmd_kpp.F:631-649: Akv, hbls, hbbl, Akt(itemp), Akt(isalt)
   ExchList L{};

@@ -55,6 +55,7 @@ __global__ void __launch_bounds__(256) k_pre_tracer_h(Dev d, Range R, PreCoef c,
 
 // ---- tracers, vertical part per column: spline advection on t(nrhs), then
 // implicit diffusion with Wi up-winding on Hz_fwd (LDS slots A, B). ----
+template <class C>
 __global__ void __launch_bounds__(64) k_pre_tracer_v(Dev d, Range R, PreCoef c, int nnew, int nrhs) {
   ROMS_IJC_OR_RETURN(R)
   const Bounds& b = d.b;
@@ -64,7 +65,7 @@ __global__ void __launch_bounds__(64) k_pre_tracer_v(Dev d, Range R, PreCoef c, 
   const double* __restrict__ Hz = F.Hz + ij;
   const double* __restrict__ We = F.We + ij;
   const double* __restrict__ Wi = F.Wi + ij;
-  const ColLds A = col_lds(0, N), B = col_lds(1, N);
+  const C A = ColMake<C>::at(d, 0, (int)blockIdx.z, ij), B = ColMake<C>::at(d, 1, (int)blockIdx.z, ij);
   const double* __restrict__ Hf = F.c2 + ij;
   auto hfwd = [&](int k) { return Hf[(long)(k - 1) * n2]; };
   {
@@ -189,8 +190,9 @@ __global__ void __launch_bounds__(256) k_rd(Dev d, Range R, int nstp) {
 // ---- momentum, per column: vertical spline advection into ru/rv, then
 // implicit viscosity with implicit no-slip bottom (IMPLCT_NO_SLIP_BTTM_BC).
 // LDS: A = spline FC -> flux -> DC(k); B = spline CF -> CF(k-1). ----
+template <class C>
 __device__ __forceinline__ void pre_uv_col(const Dev& d, int i, int j, int dir, const PreCoef& c, int nstp, int nnew,
-                                           int nrhs, const ColLds& A, const ColLds& B) {
+                                           int nrhs, const C& A, const C& B) {
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const int N = b.N, indx = 3 - nstp;
@@ -255,10 +257,12 @@ __device__ __forceinline__ void pre_uv_col(const Dev& d, int i, int j, int dir, 
   }
 }
 
+template <class C>
 __global__ void __launch_bounds__(64) k_pre_uv(Dev d, Range R, PreCoef c, int nstp, int nnew, int nrhs) {
   ROMS_IJC_OR_RETURN(R)
   const Bounds& b = d.b;
-  const ColLds A = col_lds(0, b.N), B = col_lds(1, b.N);
+  const long ij = IJ(b, i, j);
+  const C A = ColMake<C>::at(d, 0, (int)blockIdx.z, ij), B = ColMake<C>::at(d, 1, (int)blockIdx.z, ij);
   if (blockIdx.z == 0) {
     if (i >= b.istrU && i <= b.iend && j >= b.jstr && j <= b.jend) pre_uv_col(d, i, j, 0, c, nstp, nnew, nrhs, A, B);
   } else {
@@ -272,8 +276,9 @@ bool setup_column_kernels(int N) {
   const size_t bytes = col_lds_bytes(2, N);
   if (bytes > 160 * 1024) return false;
   if (bytes > 64 * 1024) {
-    (void)hipFuncSetAttribute((const void*)k_pre_tracer_v, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-    (void)hipFuncSetAttribute((const void*)k_pre_uv, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    (void)hipFuncSetAttribute((const void*)k_pre_tracer_v<ColLds>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)bytes);
+    (void)hipFuncSetAttribute((const void*)k_pre_uv<ColLds>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     setup_column_kernels_t(bytes);
     setup_column_kernels_uv1(bytes);
   }
@@ -291,13 +296,19 @@ void launch_pre_step3d(const Dev& d, hipStream_t s, const Tlev& t) {
   hipLaunchKernelGGL(k_pre_tracer_h, grid3_of(RH, b.N), dim3(kBX, kBY), 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs);
   dim3 gt = gridc_of(RI);
   gt.z = b.NT;
-  hipLaunchKernelGGL(k_pre_tracer_v, gt, dim3(kCX), col_lds_bytes(2, b.N), s, d, RI, c, t.nnew, t.nrhs);
+  if (d.f.colscr)
+    hipLaunchKernelGGL(k_pre_tracer_v<ColGlb>, gt, dim3(kCX), 0, s, d, RI, c, t.nnew, t.nrhs);
+  else
+    hipLaunchKernelGGL(k_pre_tracer_v<ColLds>, gt, dim3(kCX), col_lds_bytes(2, b.N), s, d, RI, c, t.nnew, t.nrhs);
   launch_uv_horiz(d, s, t.nrhs, 0);
   Range Rd{b.istrU - 1, b.iend, b.jstrV - 1, b.jend};
   hipLaunchKernelGGL(k_rd, grid_of(Rd), dim3(kBX, kBY), 0, s, d, Rd, t.nstp);
   dim3 gu = gridc_of(RI);
   gu.z = 2;
-  hipLaunchKernelGGL(k_pre_uv, gu, dim3(kCX), col_lds_bytes(2, b.N), s, d, RI, c, t.nstp, t.nnew, t.nrhs);
+  if (d.f.colscr)
+    hipLaunchKernelGGL(k_pre_uv<ColGlb>, gu, dim3(kCX), 0, s, d, RI, c, t.nstp, t.nnew, t.nrhs);
+  else
+    hipLaunchKernelGGL(k_pre_uv<ColLds>, gu, dim3(kCX), col_lds_bytes(2, b.N), s, d, RI, c, t.nstp, t.nnew, t.nrhs);
   launch_u3dbc(d, s, t);
   launch_v3dbc(d, s, t);
   for (int itrc = 1; itrc <= b.NT; itrc++) launch_t3dbc(d, s, t, itrc);

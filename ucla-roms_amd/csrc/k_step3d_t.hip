@@ -37,6 +37,7 @@ __global__ void __launch_bounds__(256) k_step3d_t_h(Dev d, Range R, int nnew, in
 // Vertical part per column: spline advection on t(nrhs), surface fluxes
 // (+ KPP non-local and solar terms), implicit diffusion.  LDS slots: A holds
 // FC (spline) then DC(k) at A[k-1]; B holds the spline CF then Thomas CF.
+template <class C>
 __global__ void __launch_bounds__(64) k_step3d_t_v(Dev d, Range R, int nnew, int nrhs) {
   ROMS_IJC_OR_RETURN(R)
   const Bounds& b = d.b;
@@ -47,7 +48,7 @@ __global__ void __launch_bounds__(64) k_step3d_t_v(Dev d, Range R, int nnew, int
   const long n2 = b.n2, ij = IJ(b, i, j);
   const double rm = F.rmask[ij];
   const double* __restrict__ Hz = F.Hz + ij;
-  const ColLds A = col_lds(0, N), B = col_lds(1, N);
+  const C A = ColMake<C>::at(d, 0, (int)blockIdx.z, ij), B = ColMake<C>::at(d, 1, (int)blockIdx.z, ij);
   {
     const int itrc = 1 + (int)blockIdx.z;
     const double* __restrict__ Tr = F.t + (long)(nrhs - 1) * b.n3 + (long)(itrc - 1) * 3 * b.n3 + ij;
@@ -140,7 +141,8 @@ __global__ void __launch_bounds__(64) k_step3d_t_v(Dev d, Range R, int nnew, int
 }
 
 void setup_column_kernels_t(size_t bytes) {
-  (void)hipFuncSetAttribute((const void*)k_step3d_t_v, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  (void)hipFuncSetAttribute((const void*)k_step3d_t_v<ColLds>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)bytes);
 }
 
 void launch_step3d_t(const Dev& d, hipStream_t s, const Tlev& t) {
@@ -149,7 +151,10 @@ void launch_step3d_t(const Dev& d, hipStream_t s, const Tlev& t) {
   hipLaunchKernelGGL(k_step3d_t_h, grid3_of(R, b.N), dim3(kBX, kBY), 0, s, d, R, t.nnew, t.nrhs);
   dim3 gt = gridc_of(R);
   gt.z = b.NT;
-  hipLaunchKernelGGL(k_step3d_t_v, gt, dim3(kCX), col_lds_bytes(2, b.N), s, d, R, t.nnew, t.nrhs);
+  if (d.f.colscr)
+    hipLaunchKernelGGL(k_step3d_t_v<ColGlb>, gt, dim3(kCX), 0, s, d, R, t.nnew, t.nrhs);
+  else
+    hipLaunchKernelGGL(k_step3d_t_v<ColLds>, gt, dim3(kCX), col_lds_bytes(2, b.N), s, d, R, t.nnew, t.nrhs);
   for (int itrc = 1; itrc <= b.NT; itrc++) launch_t3dbc(d, s, t, itrc);
   launch_exchange_tracers(d, s, t.nnew);
 }

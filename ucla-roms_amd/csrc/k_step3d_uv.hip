@@ -9,8 +9,9 @@ void launch_uv_horiz(const Dev& d, hipStream_t s, int nrhs, int up);
 
 // ---- step3d_uv1: implicit viscosity with implicit bottom drag r_D, result
 // stored as Hz*u in u(nnew); rufrc = vertical integral of ru + stresses ----
-__device__ __forceinline__ void uv1_col(const Dev& d, int i, int j, int dir, int nnew, int nrhs, const ColLds& A,
-                                        const ColLds& B) {
+template <class C>
+__device__ __forceinline__ void uv1_col(const Dev& d, int i, int j, int dir, int nnew, int nrhs, const C& A,
+                                        const C& B) {
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const int N = b.N;
@@ -70,10 +71,12 @@ __device__ __forceinline__ void uv1_col(const Dev& d, int i, int j, int dir, int
   else F.rvfrc[ij] = frc;
 }
 
+template <class C>
 __global__ void __launch_bounds__(64) k_uv1(Dev d, Range R, int nnew, int nrhs) {
   ROMS_IJC_OR_RETURN(R)
   const Bounds& b = d.b;
-  const ColLds A = col_lds(0, b.N), B = col_lds(1, b.N);
+  const long ij = IJ(b, i, j);
+  const C A = ColMake<C>::at(d, 0, (int)blockIdx.z, ij), B = ColMake<C>::at(d, 1, (int)blockIdx.z, ij);
   if (blockIdx.z == 0) {
     if (i >= b.istrU && i <= b.iend) uv1_col(d, i, j, 0, nnew, nrhs, A, B);
   } else {
@@ -82,7 +85,7 @@ __global__ void __launch_bounds__(64) k_uv1(Dev d, Range R, int nnew, int nrhs) 
 }
 
 void setup_column_kernels_uv1(size_t bytes) {
-  (void)hipFuncSetAttribute((const void*)k_uv1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  (void)hipFuncSetAttribute((const void*)k_uv1<ColLds>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
 void launch_step3d_uv1(const Dev& d, hipStream_t s, const Tlev& t) {
@@ -91,7 +94,10 @@ void launch_step3d_uv1(const Dev& d, hipStream_t s, const Tlev& t) {
   Range R{b.istr, b.iend, b.jstr, b.jend};
   dim3 g = gridc_of(R);
   g.z = 2;
-  hipLaunchKernelGGL(k_uv1, g, dim3(kCX), col_lds_bytes(2, b.N), s, d, R, t.nnew, t.nrhs);
+  if (d.f.colscr)
+    hipLaunchKernelGGL(k_uv1<ColGlb>, g, dim3(kCX), 0, s, d, R, t.nnew, t.nrhs);
+  else
+    hipLaunchKernelGGL(k_uv1<ColLds>, g, dim3(kCX), col_lds_bytes(2, b.N), s, d, R, t.nnew, t.nrhs);
 }
 
 // ---- visc3d: harmonic viscosity along S; adds dt*cff to u,v(indx) (Hz*u)

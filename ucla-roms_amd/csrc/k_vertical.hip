@@ -227,7 +227,7 @@ __global__ void __launch_bounds__(256) k_omega(Dev d, Range R, double dtau) {
 __global__ void k_omega_edges(Dev d) {
   const Bounds& b = d.b;
   const Fields& F = d.f;
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x, k = (int)blockIdx.y;  // k = 0..N
   const int nj = b.jend - b.jstr + 1, ni = b.iend - b.istr + 1;
   int di = 0, dj = 0, si = 0, sj = 0;
   if (p < nj) {
@@ -250,11 +250,9 @@ __global__ void k_omega_edges(Dev d) {
     else if (c == 3 && b.east_edge && b.north_edge) { di = b.iend + 1; dj = b.jend + 1; si = b.iend; sj = b.jend; }
     else return;
   }
-  const long dst = IJ(b, di, dj), src = IJ(b, si, sj);
-  for (int k = 0; k <= b.N; k++) {
-    F.We[dst + (long)k * b.n2] = F.We[src + (long)k * b.n2];
-    F.Wi[dst + (long)k * b.n2] = F.Wi[src + (long)k * b.n2];
-  }
+  const long dst = IJ(b, di, dj) + (long)k * b.n2, src = IJ(b, si, sj) + (long)k * b.n2;
+  F.We[dst] = F.We[src];
+  F.Wi[dst] = F.Wi[src];
 }
 
 void launch_omega(const Dev& d, hipStream_t s, const Tlev& t) {
@@ -267,7 +265,7 @@ void launch_omega(const Dev& d, hipStream_t s, const Tlev& t) {
   hipLaunchKernelGGL(k_omega, grid_of(R), dim3(kBX, kBY), 0, s, d, R, dtau);
   if (b.west_edge || b.east_edge || b.south_edge || b.north_edge) {
     const int n = 2 * (b.jend - b.jstr + 1) + 2 * (b.iend - b.istr + 1) + 4;
-    hipLaunchKernelGGL(k_omega_edges, dim3((n + 255) / 256), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_omega_edges, dim3((n + 255) / 256, b.N + 1), dim3(256), 0, s, d);
   }
   launch_exchange_list(d, s, ExchList{{d.f.We, d.f.Wi}, {b.N + 1, b.N + 1}, 2});
 }
@@ -347,12 +345,26 @@ __global__ void __launch_bounds__(256) k_rho_eos_split(Dev d, Range R, int tidx)
   const double K0_Duk = Tt * (K01 + Tt * (K02 + Tt * (K03 + Tt * K04))) +
                         Ts * (K10 + Tt * (K11 + Tt * (K12 + Tt * K13)) + sqrtTs * (KS0 + Tt * (KS1 + Tt * KS2)));
   const double dr00 = r00 - rho0;
-  const long ij = IJ(b, i, j);
+  const long ij = IJ(b, i, j), n2 = b.n2;
   const double rm = F.rmask[ij];
-  const double* T = F.t + (long)(tidx - 1) * b.n3;
-  const double* Sa = T + 3 * b.n3;
-  for (int k = 1; k <= N; k++) {
-    const long o = ij + (long)(k - 1) * b.n2;
+  // one top-down sweep: rho1, qp1 (rho_eos.F:208-262), bvf(k) from levels k
+  // and k+1 (:270-300) and the rhoA/rhoS column integrals (:365-395), each
+  // expression in the reference's order; restrict pointers let the loads of
+  // the next levels issue ahead of this level's stores
+  const double* __restrict__ T = F.t + (long)(tidx - 1) * b.n3 + ij;
+  const double* __restrict__ Sa = T + 3 * b.n3;
+  const double* __restrict__ zr = F.z_r + ij;
+  const double* __restrict__ Hz = F.Hz + ij;
+  double* __restrict__ rho1 = F.rho1 + ij;
+  double* __restrict__ qp1 = F.qp1 + ij;
+  double* __restrict__ bvf = F.bvf + ij;
+  const bool lmd = P.lmd;
+  const double gr = P.g / rho0;
+  double r1p = 0.0, q1p = 0.0, zrp = 0.0;  // level k+1
+  double rhoA = 0.0, rhoS = 0.0;
+#pragma unroll 4
+  for (int k = N; k >= 1; k--) {
+    const long o = (long)(k - 1) * n2;
     Tt = T[o];
     Ts = Sa[o];
     sqrtTs = sqrt(dmax(0.0, Ts));
@@ -360,38 +372,33 @@ __global__ void __launch_bounds__(256) k_rho_eos_split(Dev d, Range R, int tidx)
                        Ts * (r10 + Tt * (r11 + Tt * (r12 + Tt * (r13 + Tt * r14))) + sqrtTs * (rS0 + Tt * (rS1 + Tt * rS2)) +
                              Ts * r20)) *
                       rm;
-    F.rho1[o] = r1;
+    rho1[o] = r1;
     const double K0 = Tt * (K01 + Tt * (K02 + Tt * (K03 + Tt * K04))) +
                       Ts * (K10 + Tt * (K11 + Tt * (K12 + Tt * K13)) + sqrtTs * (KS0 + Tt * (KS1 + Tt * KS2)));
-    F.qp1[o] = 0.1 * (rho0 + r1) * (K0_Duk - K0) / ((K00 + K0) * (K00 + K0_Duk)) * rm;
-  }
-  if (P.lmd) {
-    const double cff = P.g / rho0;
-    for (int k = 1; k <= N - 1; k++) {
-      const long o = ij + (long)(k - 1) * b.n2;
-      const double dpth = -0.5 * (F.z_r[o + b.n2] + F.z_r[o]);
-      F.bvf[ij + (long)k * b.n2] =
-          -cff * (F.rho1[o + b.n2] - F.rho1[o] + (F.qp1[o + b.n2] - F.qp1[o]) * dpth * (1.0 - qp2 * dpth)) /
-          (F.z_r[o + b.n2] - F.z_r[o]) * rm;
+    const double q1 = 0.1 * (rho0 + r1) * (K0_Duk - K0) / ((K00 + K0) * (K00 + K0_Duk)) * rm;
+    qp1[o] = q1;
+    const double zrk = zr[o], hz = Hz[o];
+    if (lmd && k < N) {
+      const double dpth = -0.5 * (zrp + zrk);
+      bvf[(long)k * n2] = -gr * (r1p - r1 + (q1p - q1) * dpth * (1.0 - qp2 * dpth)) / (zrp - zrk) * rm;
     }
-    F.bvf[ij + (long)N * b.n2] = F.bvf[ij + (long)(N - 1) * b.n2];
-    F.bvf[ij] = F.bvf[ij + b.n2];
+    const double dpth = -zrk;
+    const double cff = hz * (r1 + q1 * dpth * (1.0 - qp2 * dpth));
+    if (k == N) {
+      rhoS = 0.5 * cff * hz;
+      rhoA = cff;
+    } else {
+      rhoS = rhoS + hz * (rhoA + 0.5 * cff);
+      rhoA = rhoA + cff;
+    }
+    r1p = r1; q1p = q1; zrp = zrk;
   }
-  long o = ij + (long)(N - 1) * b.n2;
-  double dpth = -F.z_r[o];
-  double cff = F.Hz[o] * (F.rho1[o] + F.qp1[o] * dpth * (1.0 - qp2 * dpth));
-  double rhoS = 0.5 * cff * F.Hz[o];
-  double rhoA = cff;
-  for (int k = N - 1; k >= 1; k--) {
-    o = ij + (long)(k - 1) * b.n2;
-    dpth = -F.z_r[o];
-    const double hz = F.Hz[o];
-    cff = hz * (F.rho1[o] + F.qp1[o] * dpth * (1.0 - qp2 * dpth));
-    rhoS = rhoS + hz * (rhoA + 0.5 * cff);
-    rhoA = rhoA + cff;
+  if (lmd) {
+    bvf[(long)N * n2] = bvf[(long)(N - 1) * n2];
+    bvf[0] = bvf[n2];
   }
   const double cff1 = 1.0 / rho0;
-  cff = 1.0 / (F.z_w[ij + (long)N * b.n2] - F.z_w[ij]);
+  const double cff = 1.0 / (F.z_w[ij + (long)N * n2] - F.z_w[ij]);
   F.rhoA[ij] = cff * cff1 * rhoA;
   F.rhoS[ij] = 2.0 * cff * cff * cff1 * rhoS;
 }

@@ -65,6 +65,9 @@ struct Fields {
   // pipe_frc.F: pipe_idx (0: none), pipe_flx, pipe_prf(npip,N), pipe_trc(npip,NT)
   int* pipe_idx;
   double *pipe_flx, *pipe_prf, *pipe_trc;
+  // column-solver scratch in global memory, 2*max(NT,2) slots of (0:N) levels
+  // (nullptr: the solvers keep their columns in LDS; see ColGlb in k_common.h)
+  double* colscr;
 };
 
 struct Halo;  // halo.h: multi-rank exchange state (host object; nullptr = single rank)
@@ -156,6 +159,9 @@ void launch_exchange_tracers(const Dev& d, hipStream_t s, int tlev);  // t(:,:,:
 // the full 160 KB when N needs more than the default 64 KB.  Returns false if
 // N is too deep for one wavefront's columns to fit.
 bool setup_column_kernels(int N);
+inline size_t col_smem_bytes(const Dev& d, int nslots) {
+  return d.f.colscr ? 0 : (size_t)nslots * (d.b.N + 1) * 64 * sizeof(double);
+}
 void launch_set_depth(const Dev& d, hipStream_t s, const Tlev& t);
 void launch_set_huv(const Dev& d, hipStream_t s, const Tlev& t);
 void launch_set_huv1(const Dev& d, hipStream_t s, const Tlev& t);

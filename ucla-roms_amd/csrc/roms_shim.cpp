@@ -285,7 +285,16 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
   P.Akv_bak = cfg->Akv_bak; P.Akt_bak[0] = cfg->Akt_bak[0]; P.Akt_bak[1] = cfg->Akt_bak[1];
   P.npip = 0;
   for (int i = 0; i < kMaxFast; i++) { g.w1[i] = cfg->weight[0][i]; g.w2[i] = cfg->weight[1][i]; }
-  if (!setup_column_kernels(dims->N)) {
+  // column-solver scratch: LDS while two (N+1)-level slots per wave fit the
+  // default 64 KB (N < 63), global memory for deeper grids;
+  // ROMS_GPU_COL_GLOBAL=1/0 forces either (A/B runs)
+  bool col_global = (size_t)2 * (dims->N + 1) * kCX * sizeof(double) > 64 * 1024;
+  {
+    const char* e = getenv("ROMS_GPU_COL_GLOBAL");
+    if (e && e[0] == '1') col_global = true;
+    if (e && e[0] == '0') col_global = false;
+  }
+  if (!col_global && !setup_column_kernels(dims->N)) {
     g.err = "roms_gpu_init: N too large for the LDS column kernels (2*(N+1)*512 B > 160 KB)";
     return -2;
   }
@@ -313,6 +322,7 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
   double** s2[] = {&F.s0, &F.s1, &F.s2, &F.s3, &F.s4, &F.s5, &F.s6, &F.s7, &F.s8, &F.s9};
   for (double** q : s2)
     if (scratch(*q, b.n2)) return -2;
+  if (col_global && scratch(F.colscr, 2L * (b.NT > 2 ? b.NT : 2) * b.n3w)) return -2;
   if (P.lmd) {
     if (scratch(F.lmd_rig, b.n3w)) return -2;
     double** l2[] = {&F.lmd_hbl, &F.lmd_bbl, &F.lmd_Bo, &F.lmd_Bosol, &F.lmd_ustar};
