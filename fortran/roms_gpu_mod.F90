@@ -27,6 +27,8 @@ module roms_gpu_mod
     real(c_double) :: Akv_bak, Akt_bak(2)
     real(c_double) :: Tcoef, T0, Scoef, S0
     real(c_double) :: theta_s, theta_b, hc
+    integer(c_int) :: obc                        ! OBC_WEST 1, OBC_EAST 2, OBC_SOUTH 4, OBC_NORTH 8
+    real(c_double) :: ubind
   end type
 
   type, bind(c) :: roms_tlev
@@ -39,9 +41,12 @@ module roms_gpu_mod
     integer(c_int) :: ndtfast
     real(c_double) :: sizex, sizey
     integer(c_int) :: surf_flux
+    integer(c_int) :: obc
+    real(c_double) :: v_sponge
+    integer(c_int) :: island
   end type
 
-  integer(c_int), parameter :: ROMS_GPU_ABI = 3   ! ROMS_GPU_ABI_VERSION, include/roms_gpu.h
+  integer(c_int), parameter :: ROMS_GPU_ABI = 4   ! ROMS_GPU_ABI_VERSION, include/roms_gpu.h
 
   ! field ids (enum roms_field) used by the drivers below
   integer(c_int), parameter :: ROMS_zeta = 22, ROMS_ubar = 23, ROMS_vbar = 24, ROMS_u = 25, ROMS_v = 26, &

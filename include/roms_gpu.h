@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define ROMS_GPU_ABI_VERSION 3
+#define ROMS_GPU_ABI_VERSION 4
 #define ROMS_MAX_FAST 288
 
 /* Subdomain geometry of this rank: param.F / dimensions.F / mpi_setup.F:39-210 */
@@ -50,6 +50,10 @@ typedef struct roms_cfg {
   double Akv_bak, Akt_bak[2];
   double Tcoef, T0, Scoef, S0;   /* linear EOS                              */
   double theta_s, theta_b, hc;   /* S-coordinate                            */
+  int obc;                       /* open edges (OBC_WEST 1, OBC_EAST 2, OBC_SOUTH 4, OBC_NORTH 8) with
+                                    OBC_M2FLATHER, OBC_M3ORLANSKI, OBC_TORLANSKI and Z/M2/M3/T_FRC_BRY;
+                                    closed walls elsewhere (zetabc.F, u2dbc_im.F ... t3dbc_im.F)  */
+  double ubind;                  /* OBC binding velocity [m/s] (scalars.F, read_inp_mod.F:809)    */
 } roms_cfg;
 
 /* Time-step indices (scalars.F:32-36).  The step entry updates them. */
@@ -79,6 +83,14 @@ enum roms_field {
   ROMS_sustr, ROMS_svstr, ROMS_stflx, ROMS_srflx, ROMS_swflx,
   /* private scratch carried between routines (prsgrd -> pre_step3d/step3d_uv1) */
   ROMS_ru, ROMS_rv,
+  /* boundary.F:21-39 open-boundary data: *_west/_east indexed j=0:Mm+1, *_south/_north i=0:Lm+1;
+     u,v (.,N); t (.,N,NT) -- column-major like the reference allocations (boundary.F:111-129) */
+  ROMS_zeta_west, ROMS_zeta_east, ROMS_zeta_south, ROMS_zeta_north,
+  ROMS_ubar_west, ROMS_ubar_east, ROMS_ubar_south, ROMS_ubar_north,
+  ROMS_vbar_west, ROMS_vbar_east, ROMS_vbar_south, ROMS_vbar_north,
+  ROMS_u_west, ROMS_u_east, ROMS_u_south, ROMS_u_north,
+  ROMS_v_west, ROMS_v_east, ROMS_v_south, ROMS_v_north,
+  ROMS_t_west, ROMS_t_east, ROMS_t_south, ROMS_t_north,
   ROMS_NFIELDS
 };
 
@@ -143,6 +155,9 @@ typedef struct roms_case {
   double dt; int ndtfast;
   double sizex, sizey;
   int surf_flux;  /* basin only: analytic cooling, short-wave and salt fluxes (else 0) */
+  int obc;        /* basin only: open edges (roms_cfg.obc) with analytic boundary data, ubind 0.1 */
+  double v_sponge;/* basin only: SPONGE band viscosity/diffusivity [m2/s] (set_nudgcof.F)      */
+  int island;     /* basin only: circular land mask (MASKING)                                   */
 } roms_case;
 /* Builds the analytic grid/ICs on the host (setup_grid1/2, set_scoord,
  * set_weights, ana_init), initialises the device and runs roms_init.        */

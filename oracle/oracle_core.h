@@ -44,6 +44,10 @@ struct or_state {
   /* pipe_frc.F (npip = 1, analytic): pipe_idx>0 cells carry pipe_flx */
   int pipe_source;
   double *pipe_flx, *pipe_idx, pipe_prf[1024], pipe_trc[2];
+  /* open-boundary data (boundary.F:21-39): [0] west, [1] east (index j, 0:Mm+1),
+     [2] south, [3] north (index i, 0:Lm+1); u,v (.,N), t (.,N,NT) */
+  int nbry[4];
+  double *bry_zeta[4], *bry_ubar[4], *bry_vbar[4], *bry_u[4], *bry_v[4], *bry_t[4];
   /* forcing */
   double *sustr, *svstr, *stflx, *srflx, *swflx;
   /* private scratch (A3d(:,1..4), A2d(:,1..)) */
@@ -98,6 +102,9 @@ void or_v2dbc(or_state *S);
 void or_u3dbc(or_state *S);
 void or_v3dbc(or_state *S);
 void or_t3dbc(or_state *S, int itrc);
+/* open boundaries: sponge (set_nudgcof.F) and analytic boundary data */
+void or_set_nudgcof(or_state *S);
+void or_ana_bry(or_state *S);
 /* analytic cases */
 void or_ana_grid(or_state *S);
 void or_ana_init(or_state *S);

@@ -62,6 +62,15 @@ or_state *or_create(const or_cfg *cfg) {
   for (int q = 0; q < 6; q++) S->c1[q] = zalloc((size_t)S->nx2 * (S->N + 1));
   if (cfg->lmd) or_lmd_alloc(S);
   S->pipe_flx = zalloc(n2); S->pipe_idx = zalloc(n2);
+  /* boundary.F:111-129: zeta_west(0:Mm+1), u_west(0:Mm+1,N), t_west(0:Mm+1,N,NT), ... */
+  S->nbry[0] = S->nbry[1] = S->Mm + 2;
+  S->nbry[2] = S->nbry[3] = S->Lm + 2;
+  for (int q = 0; q < 4; q++) {
+    const size_t nb = (size_t)S->nbry[q];
+    S->bry_zeta[q] = zalloc(nb); S->bry_ubar[q] = zalloc(nb); S->bry_vbar[q] = zalloc(nb);
+    S->bry_u[q] = zalloc(nb * S->N); S->bry_v[q] = zalloc(nb * S->N); S->bry_t[q] = zalloc(nb * S->N * S->NT);
+  }
+  if (cfg->obc && (S->Lm + 4 > 4200 || S->Mm + 4 > 4200)) { fprintf(stderr, "oracle: OBC strips limited to 4196 points\n"); return NULL; }
   return S;
 }
 
@@ -449,6 +458,10 @@ void or_ana_grid(or_state *S) {
         if (s < 0.0) s = 0.0;
         A2(S->h, i, j) = 200.0 + 3800.0 * s;
         A2(S->rmask, i, j) = 1.0;
+        if (S->c.island) {  /* circular island of radius 0.1 min(Lx,Ly) at (0.35 Lx, 0.6 Ly) */
+          const double ix = x - 0.35 * S->c.sizex, iy = y - 0.6 * S->c.sizey, ir = 0.2 * R;
+          if (ix * ix + iy * iy < ir * ir) A2(S->rmask, i, j) = 0.0;
+        }
       }
   }
 }
@@ -569,6 +582,63 @@ void or_ana_forces(or_state *S) {
   }
 }
 
+/* set_nudgcof_tile (set_nudgcof.F:17-111): sponge bands along the open
+ * edges add v_sponge*wrk to visc2_r, visc2_p and diff2 on the tile's
+ * own points (no exchange follows in the reference, main.F:299) */
+void or_set_nudgcof(or_state *S) {
+  const int isp = 15 + 1;
+  double *wrk = S->s2[0];
+  for (int j = (S->jstrR - 1 > -1 ? S->jstrR - 1 : -1); j <= S->jendR; j++)
+    for (int i = (S->istrR - 1 > -1 ? S->istrR - 1 : -1); i <= S->iendR; i++) {
+      int ibnd = isp;
+      if (S->c.obc & 1) ibnd = ibnd < i ? ibnd : i;
+      if (S->c.obc & 2) ibnd = ibnd < S->c.LLm + 1 - i ? ibnd : S->c.LLm + 1 - i;
+      if (S->c.obc & 4) ibnd = ibnd < j ? ibnd : j;
+      if (S->c.obc & 8) ibnd = ibnd < S->c.MMm + 1 - j ? ibnd : S->c.MMm + 1 - j;
+      A2(wrk, i, j) = (double)(isp - ibnd) / (double)isp;
+    }
+  const double vs = S->c.v_sponge;
+  for (int j = S->jstrR; j <= S->jendR; j++)
+    for (int i = S->istrR; i <= S->iendR; i++) A2(S->visc2_r, i, j) = A2(S->visc2_r, i, j) + vs * A2(wrk, i, j);
+  for (int j = S->jstr; j <= S->jendR; j++)
+    for (int i = S->istr; i <= S->iendR; i++)
+      A2(S->visc2_p, i, j) = A2(S->visc2_p, i, j) +
+                             0.25 * vs * (A2(wrk, i, j) + A2(wrk, i - 1, j) + A2(wrk, i, j - 1) + A2(wrk, i - 1, j - 1));
+  for (int it = 1; it <= S->NT; it++)
+    for (int j = S->jstrR; j <= S->jendR; j++)
+      for (int i = S->istrR; i <= S->iendR; i++) {
+        double *d2 = S->diff2 + (size_t)(it - 1) * S->n2;
+        A2(d2, i, j) = A2(d2, i, j) + vs * A2(wrk, i, j);
+      }
+  memset(wrk, 0, S->n2 * sizeof(double));
+}
+
+/* Analytic open-boundary data (stands in for set_bry_all / boundary.F:227,
+ * which read netCDF): smooth along-edge profiles, time independent.
+ * zeta/ubar/vbar/u/v from closed-form expressions, tracers = initial edge
+ * state + 0.05.  sj = (j-0.5)/MMm, si = (i-0.5)/LLm (global indices). */
+void or_ana_bry(or_state *S) {
+  const double pi = 3.14159265358979323;
+  const int N = S->N;
+  for (int q = 0; q < 4; q++)
+    for (int m = 0; m < S->nbry[q]; m++) {
+      const double s = q < 2 ? ((double)m - 0.5) / (double)S->c.MMm : ((double)m - 0.5) / (double)S->c.LLm;
+      const double sgn = (q == 0 || q == 2) ? 1.0 : -1.0;
+      S->bry_zeta[q][m] = sgn * (q < 2 ? 0.05 : 0.03) * sin(pi * s);
+      S->bry_ubar[q][m] = q < 2 ? 0.02 * sin(pi * s) : 0.01;
+      S->bry_vbar[q][m] = q < 2 ? -0.01 : 0.015 * sin(pi * s);
+      for (int k = 1; k <= N; k++) {
+        const double fk = 1.0 + 0.2 * ((double)k - 0.5) / (double)N;
+        S->bry_u[q][m + (size_t)S->nbry[q] * (k - 1)] = S->bry_ubar[q][m] * fk;
+        S->bry_v[q][m + (size_t)S->nbry[q] * (k - 1)] = S->bry_vbar[q][m] * fk;
+        for (int it = 1; it <= S->NT; it++) {
+          const int i = q == 0 ? 0 : q == 1 ? S->Lm + 1 : m, j = q == 2 ? 0 : q == 3 ? S->Mm + 1 : m;
+          S->bry_t[q][m + (size_t)S->nbry[q] * ((k - 1) + (size_t)N * (it - 1))] = TT(i, j, k, 1, it) + 0.05;
+        }
+      }
+    }
+}
+
 /* ---------------------------------------------------------------------- */
 /* roms_init (main.F:85-321)                                               */
 /* ---------------------------------------------------------------------- */
@@ -595,6 +665,7 @@ int or_init(or_state *S) {
       for (size_t q = 0; q < S->n3w; q++) S->Akt[q + (size_t)(it - 1) * S->n3w] = S->c.Akt_bak[it - 1];
   }
   or_ana_forces(S);
+  if (S->c.obc) { or_set_nudgcof(S); or_ana_bry(S); }
   or_set_depth(S);
   or_set_HUV(S);
   or_omega(S);
@@ -683,6 +754,18 @@ double *or_field(or_state *S, const char *name, size_t *count) {
   };
   for (size_t q = 0; q < sizeof(tab) / sizeof(tab[0]); q++)
     if (strcmp(tab[q].n, name) == 0) { if (count) *count = tab[q].c; return tab[q].p; }
+  static const char *side[4] = {"west", "east", "south", "north"};
+  for (int q = 0; q < 4; q++) {
+    char nm[32];
+    const size_t nb = (size_t)S->nbry[q];
+    struct { const char *k; double *p; size_t c; } bt[] = {
+        {"zeta", S->bry_zeta[q], nb}, {"ubar", S->bry_ubar[q], nb}, {"vbar", S->bry_vbar[q], nb},
+        {"u", S->bry_u[q], nb * S->N}, {"v", S->bry_v[q], nb * S->N}, {"t", S->bry_t[q], nb * S->N * S->NT}};
+    for (size_t r = 0; r < 6; r++) {
+      snprintf(nm, sizeof nm, "%s_%s", bt[r].k, side[q]);
+      if (strcmp(nm, name) == 0) { if (count) *count = bt[r].c; return bt[r].p; }
+    }
+  }
   if (count) *count = 0;
   return NULL;
 }

@@ -51,104 +51,6 @@ void or_exch3(or_state *S, double *a, int nlev) {
 }
 
 /* ---------------------------------------------------------------------- */
-/* closed-wall lateral BCs (no OBC_* defined): zetabc.F:3, u2dbc_im.F:3,    */
-/* v2dbc_im.F:3, u3dbc_im.F:4, v3dbc_im.F:4, t3dbc_im.F:4.  Periodic: no-op */
-/* ---------------------------------------------------------------------- */
-void or_zetabc(or_state *S, double *zn) {
-  const int istr = S->istr, iend = S->iend, jstr = S->jstr, jend = S->jend;
-  if (S->west_edge)
-    for (int j = S->jstrV - 1; j <= jend; j++) A2(zn, istr - 1, j) = A2(zn, istr, j) * A2(S->rmask, istr - 1, j);
-  if (S->east_edge)
-    for (int j = S->jstrV - 1; j <= jend; j++) A2(zn, iend + 1, j) = A2(zn, iend, j) * A2(S->rmask, iend + 1, j);
-  if (S->south_edge)
-    for (int i = S->istrU - 1; i <= iend; i++) A2(zn, i, jstr - 1) = A2(zn, i, jstr) * A2(S->rmask, i, jstr - 1);
-  if (S->north_edge)
-    for (int i = S->istrU - 1; i <= iend; i++) A2(zn, i, jend + 1) = A2(zn, i, jend) * A2(S->rmask, i, jend + 1);
-  if (S->south_edge && S->west_edge)
-    A2(zn, istr - 1, jstr - 1) = 0.5 * (A2(zn, istr, jstr - 1) + A2(zn, istr - 1, jstr));
-  if (S->south_edge && S->east_edge)
-    A2(zn, iend + 1, jstr - 1) = 0.5 * (A2(zn, iend, jstr - 1) + A2(zn, iend + 1, jstr));
-  if (S->north_edge && S->west_edge)
-    A2(zn, istr - 1, jend + 1) = 0.5 * (A2(zn, istr, jend + 1) + A2(zn, istr - 1, jend));
-  if (S->north_edge && S->east_edge)
-    A2(zn, iend + 1, jend + 1) = 0.5 * (A2(zn, iend, jend + 1) + A2(zn, iend + 1, jend));
-}
-void or_u2dbc(or_state *S) {
-  const int kn = S->knew;
-  if (S->west_edge) for (int j = S->jstr; j <= S->jend; j++) UBAR(S->istr, j, kn) = 0.0;
-  if (S->east_edge) for (int j = S->jstr; j <= S->jend; j++) UBAR(S->iend + 1, j, kn) = 0.0;
-  if (S->south_edge)
-    for (int i = S->istr; i <= S->iendR; i++)
-      UBAR(i, S->jstr - 1, kn) = S->gamma2 * UBAR(i, S->jstr, kn) * A2(S->umask, i, S->jstr - 1);
-  if (S->north_edge)
-    for (int i = S->istr; i <= S->iendR; i++)
-      UBAR(i, S->jend + 1, kn) = S->gamma2 * UBAR(i, S->jend, kn) * A2(S->umask, i, S->jend + 1);
-}
-void or_v2dbc(or_state *S) {
-  const int kn = S->knew;
-  if (S->south_edge) for (int i = S->istr; i <= S->iend; i++) VBAR(i, S->jstr, kn) = 0.0;
-  if (S->north_edge) for (int i = S->istr; i <= S->iend; i++) VBAR(i, S->jend + 1, kn) = 0.0;
-  if (S->west_edge)
-    for (int j = S->jstr; j <= S->jendR; j++)
-      VBAR(S->istr - 1, j, kn) = S->gamma2 * VBAR(S->istr, j, kn) * A2(S->vmask, S->istr - 1, j);
-  if (S->east_edge)
-    for (int j = S->jstr; j <= S->jendR; j++)
-      VBAR(S->iend + 1, j, kn) = S->gamma2 * VBAR(S->iend, j, kn) * A2(S->vmask, S->iend + 1, j);
-}
-void or_u3dbc(or_state *S) {
-  const int nn = S->nnew, N = S->N;
-  for (int k = 1; k <= N; k++) {
-    if (S->west_edge) for (int j = S->jstr; j <= S->jend; j++) U(S->istr, j, k, nn) = 0.0;
-    if (S->east_edge) for (int j = S->jstr; j <= S->jend; j++) U(S->iend + 1, j, k, nn) = 0.0;
-    if (S->south_edge)
-      for (int i = S->istr; i <= S->iendR; i++)
-        U(i, S->jstr - 1, k, nn) = S->gamma2 * U(i, S->jstr, k, nn) * A2(S->umask, i, S->jstr - 1);
-    if (S->north_edge)
-      for (int i = S->istr; i <= S->iendR; i++)
-        U(i, S->jend + 1, k, nn) = S->gamma2 * U(i, S->jend, k, nn) * A2(S->umask, i, S->jend + 1);
-  }
-}
-void or_v3dbc(or_state *S) {
-  const int nn = S->nnew, N = S->N;
-  for (int k = 1; k <= N; k++) {
-    if (S->south_edge) for (int i = S->istr; i <= S->iend; i++) V(i, S->jstr, k, nn) = 0.0;
-    if (S->north_edge) for (int i = S->istr; i <= S->iend; i++) V(i, S->jend + 1, k, nn) = 0.0;
-    if (S->west_edge)
-      for (int j = S->jstr; j <= S->jendR; j++)
-        V(S->istr - 1, j, k, nn) = S->gamma2 * V(S->istr, j, k, nn) * A2(S->vmask, S->istr - 1, j);
-    if (S->east_edge)
-      for (int j = S->jstr; j <= S->jendR; j++)
-        V(S->iend + 1, j, k, nn) = S->gamma2 * V(S->iend, j, k, nn) * A2(S->vmask, S->iend + 1, j);
-  }
-}
-void or_t3dbc(or_state *S, int it) {
-  const int nn = S->nnew, N = S->N, istr = S->istr, iend = S->iend, jstr = S->jstr, jend = S->jend;
-  const double *rm = S->rmask;
-  for (int k = 1; k <= N; k++) {
-    if (S->west_edge) for (int j = jstr; j <= jend; j++) TT(istr - 1, j, k, nn, it) = TT(istr, j, k, nn, it) * A2(rm, istr - 1, j);
-    if (S->east_edge) for (int j = jstr; j <= jend; j++) TT(iend + 1, j, k, nn, it) = TT(iend, j, k, nn, it) * A2(rm, iend + 1, j);
-    if (S->south_edge) for (int i = istr; i <= iend; i++) TT(i, jstr - 1, k, nn, it) = TT(i, jstr, k, nn, it) * A2(rm, i, jstr - 1);
-    if (S->north_edge) for (int i = istr; i <= iend; i++) TT(i, jend + 1, k, nn, it) = TT(i, jend, k, nn, it) * A2(rm, i, jend + 1);
-  }
-#define TCORNER(ic, jc, ia, ja, ib, jb)                                         \
-  {                                                                            \
-    double cff = A2(rm, ia, ja) + A2(rm, ib, jb);                              \
-    if (cff > 0.0) {                                                           \
-      cff = 1.0 / cff;                                                         \
-      for (int k = 1; k <= N; k++)                                             \
-        TT(ic, jc, k, nn, it) = cff * (A2(rm, ia, ja) * TT(ia, ja, k, nn, it) + \
-                                       A2(rm, ib, jb) * TT(ib, jb, k, nn, it)); \
-    } else                                                                     \
-      for (int k = 1; k <= N; k++) TT(ic, jc, k, nn, it) = 0.0;               \
-  }
-  if (S->south_edge && S->west_edge) TCORNER(istr - 1, jstr - 1, istr, jstr - 1, istr - 1, jstr);
-  if (S->south_edge && S->east_edge) TCORNER(iend + 1, jstr - 1, iend, jstr - 1, iend + 1, jstr);
-  if (S->north_edge && S->west_edge) TCORNER(istr - 1, jend + 1, istr, jend + 1, istr - 1, jend);
-  if (S->north_edge && S->east_edge) TCORNER(iend + 1, jend + 1, iend, jend + 1, iend + 1, jend);
-#undef TCORNER
-}
-
-/* ---------------------------------------------------------------------- */
 /* set_depth_tile (set_depth.F:16-186)                                     */
 /* ---------------------------------------------------------------------- */
 static void set_depth_tile(or_state *S) {

@@ -42,6 +42,10 @@ typedef struct or_cfg {
   double sizex, sizey;           /* analytic domain size [m] */
   int diag_np_xi, diag_np_eta;   /* rank layout emulated in diag sums */
   int surf_flux;                 /* basin: analytic cooling/short-wave/salt fluxes */
+  int obc;                       /* open edges: 1 W, 2 E, 4 S, 8 N (OBC_WEST..; Flather/Orlanski + *_FRC_BRY) */
+  double ubind;                  /* OBC binding velocity [m/s] (read_inp_mod.F:809) */
+  double v_sponge;               /* SPONGE viscosity/diffusivity [m2/s] (set_nudgcof.F:25-111) */
+  int island;                    /* basin: circular land mask (MASKING) */
 } or_cfg;
 
 typedef struct or_state or_state;

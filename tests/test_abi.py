@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
     missing = [n for n in _declared() if n not in exported]
     assert not missing, missing
     L = ctypes.CDLL(LIB)
-    assert L.roms_gpu_abi_version() == 3
+    assert L.roms_gpu_abi_version() == 4
 
 
 @pytest.mark.skipif(not os.path.exists(LIB), reason="libromsgpu.so not built")

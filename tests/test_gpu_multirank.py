@@ -39,6 +39,11 @@ def _case(kind):
     if kind == "basin_flux":   # LMD with surface cooling/short-wave (convective KPP branches)
         return dict(case_id=1, LLm=36, MMm=28, N=20, NT=2, salinity=True, nonlin_eos=True, dt=60.0, ndtfast=30,
                     sizex=72e3, sizey=56e3, lmd=True, surf_flux=True)
+    if kind == "basin_obc":   # open edges (Flather/Orlanski + boundary data) and an island; no sponge, whose
+        # bands the reference sets on each rank's own points only (set_nudgcof.F, no exchange), so a
+        # sponge run is decomposition dependent in the reference itself
+        return dict(case_id=1, LLm=36, MMm=28, N=10, NT=2, salinity=True, nonlin_eos=True, dt=60.0, ndtfast=30,
+                    sizex=72e3, sizey=56e3, lmd=True, obc=15, island=True)
     return dict(case_id=1, LLm=36, MMm=28, N=10, NT=2, salinity=True, nonlin_eos=True, dt=60.0, ndtfast=30,
                 sizex=72e3, sizey=56e3, lmd=(kind == "basin_lmd"))
 
@@ -89,7 +94,7 @@ EXCHANGED = ("zeta", "ubar", "vbar", "u", "v", "t", "FlxU", "FlxV", "We", "Wi", 
 LMD_FIELDS = ("Akv", "Akt", "hbls", "hbbl", "ghat", "swr_frac")
 
 
-@pytest.mark.parametrize("kind", ["filament", "basin", "basin_lmd", "basin_flux", "pipes"])
+@pytest.mark.parametrize("kind", ["filament", "basin", "basin_lmd", "basin_flux", "pipes", "basin_obc"])
 @pytest.mark.parametrize("npx,npe", [(2, 1), (1, 2), (2, 2), (3, 2)])
 def test_decomposition_bitwise_equals_single_domain(kind, npx, npe):
     case = _case(kind)

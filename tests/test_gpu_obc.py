@@ -1,0 +1,108 @@
+"""GPU parity of the open lateral boundaries:
+zetabc / u2dbc / v2dbc with OBC_M2FLATHER (tangential components through the
+OBC_M2ORLANSKI branch, u2dbc_im.F:270-273), u3dbc / v3dbc with OBC_M3ORLANSKI,
+t3dbc with OBC_TORLANSKI, all with *_FRC_BRY boundary data and the ubind
+binding velocity; plus the SPONGE bands (set_nudgcof.F) and a land mask.
+
+The case is the synthetic basin with all four edges open, an island and
+analytic time-independent boundary data (Iceland switch set,
+Examples/Iceland/Iceland_parent/cppdefs.opt; the real Iceland inputs are not
+available offline).  The oracle's open-boundary restatement
+(oracle/oracle_obc.c) has no golden log of its own -- the reference's OBC
+tests need netCDF inputs fetched from GitHub -- so this parity is GPU vs
+oracle only ("parity unpinned" for the OBC branches; the closed-wall branches
+of the same routines stay pinned by the Filament / Pipes_ana goldens).
+Tolerances as in test_gpu_parity: 1e-12 relative per routine (sqrt in
+Flather's phase speed may differ by an ulp), field RMS < 1e-10 per run.
+"""
+import numpy as np
+import pytest
+
+import oracle
+import romsgpu
+from test_gpu_parity import PROGNOSTIC, RMS_RUN, RTOL_ROUTINE, basin_cfg, check_fields, copy_state
+
+pytestmark = pytest.mark.gpu
+
+BRY = ["%s_%s" % (v, e) for v in ("zeta", "ubar", "vbar", "u", "v", "t") for e in ("west", "east", "south", "north")]
+
+
+def obc_cfg(obc=15, sponge=1.0, island=1, lmd=0, **kw):
+    c = basin_cfg(nonlin=True, **kw)
+    c.obc, c.ubind, c.v_sponge, c.island, c.lmd = obc, 0.1, sponge, island, lmd
+    return c
+
+
+def make_pair(cfg):
+    o = oracle.Oracle(cfg)
+    o.init()
+    m = romsgpu.Model.from_case(cfg.case_id, cfg.LLm, cfg.MMm, cfg.N, cfg.NT, salinity=bool(cfg.salinity),
+                                nonlin_eos=bool(cfg.nonlin_eos), dt=cfg.dt, ndtfast=cfg.ndtfast, sizex=cfg.sizex,
+                                sizey=cfg.sizey, lmd=bool(cfg.lmd), obc=cfg.obc, v_sponge=cfg.v_sponge,
+                                island=bool(cfg.island))
+    return o, m
+
+
+def full(a, b):
+    """Whole arrays incl. ghost rows (the boundary values are the point here)."""
+    d = float(np.max(np.abs(a - b)))
+    return d / max(float(np.max(np.abs(b))), 1e-300)
+
+
+def test_init_boundary_data_sponge_and_masks_match_oracle():
+    cfg = obc_cfg()
+    o, m = make_pair(cfg)
+    bad = [(n, full(m.get(n), o.field(n))) for n in BRY + ["visc2_r", "visc2_p", "diff2", "rmask", "umask", "vmask",
+                                                          "pmask"]]
+    bad = [x for x in bad if not x[1] == 0.0]
+    assert not bad, bad
+    assert float(np.max(o.field("visc2_r"))) > 0.9 and float(np.min(o.field("rmask"))) == 0.0
+    m.close()
+
+
+@pytest.mark.parametrize("routine", ["step2d", "pre_step3d", "step3d_uv2", "step3d_t"])
+@pytest.mark.parametrize("obc", [15, 5, 10])
+def test_open_boundary_routine_parity(routine, obc):
+    """One routine on identical mid-run states, ghost rows included.  obc=5:
+    west+south open (east/north closed, so closed-open corners), 10: east+north."""
+    cfg = obc_cfg(obc=obc)
+    o, m = make_pair(cfg)
+    o.step(3)
+    iic, kstp, knew, nstp, nrhs, nnew = o.tindex()
+    if routine == "step2d":
+        kstp, knew = knew, knew % 4 + 1
+        nrhs, nnew = 3, 3 - nstp
+        o.L.or_set_iif(o.h, 2)
+    elif routine == "pre_step3d":
+        nrhs, nnew = nstp, 3
+    else:
+        nrhs, nnew = 3, 3 - nstp
+    o.set_tindex([iic, kstp, knew, nstp, nrhs, nnew])
+    copy_state(o, m)
+    m.set_tindex(iic, kstp, knew, nstp, nrhs, nnew, iif=2, nfast=o.nfast())
+    o.call(routine)
+    getattr(m, routine)()
+    m.sync()
+    outs = {"step2d": ["zeta", "ubar", "vbar", "DU_avg1", "DV_avg1", "Zt_avg1"],
+            "pre_step3d": ["u", "v", "t"], "step3d_uv2": ["u", "v", "ubar", "vbar", "FlxU", "FlxV"],
+            "step3d_t": ["t"]}[routine]
+    bad = [(n, full(m.get(n), o.field(n))) for n in outs]
+    bad = [x for x in bad if not x[1] <= RTOL_ROUTINE]
+    assert not bad, (routine, obc, bad)
+    m.close()
+
+
+@pytest.mark.parametrize("lmd", [0, 1])
+def test_open_basin_30_steps_rms(lmd):
+    cfg = obc_cfg(lmd=lmd)
+    o, m = make_pair(cfg)
+    o.step(30)
+    m.step(30)
+    check_fields(o, m, PROGNOSTIC, cfg.LLm, cfg.MMm, RMS_RUN, kind="rms")
+    # the open edges carried flow: the western ghost column moved off its initial state
+    ub = o.field("ubar")
+    assert float(np.max(np.abs(ub[:, 2:-2, 2]))) > 1e-4
+    for n in ("zeta", "ubar", "vbar", "u", "v", "t"):   # ghost rows too
+        a, b = m.get(n), o.field(n)
+        assert float(np.sqrt(np.mean((a - b) ** 2))) / max(1.0, float(np.sqrt(np.mean(b ** 2)))) < RMS_RUN, n
+    m.close()

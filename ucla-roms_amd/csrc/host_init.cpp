@@ -7,6 +7,7 @@
 // that the shim uploads; the time-stepping itself never touches the host.
 #include "host_init.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 
@@ -238,6 +239,10 @@ void build_case(const CaseSpec& cs, HostState& H, double& area, double& volume) 
         if (s < 0.0) s = 0.0;
         A(kh, i, j) = 200.0 + 3800.0 * s;
         A(krmask, i, j) = 1.0;
+        if (cs.island) {  // circular island of radius 0.1 min(Lx,Ly) at (0.35 Lx, 0.6 Ly)
+          const double ix = x - 0.35 * cs.sizex, iy = y - 0.6 * cs.sizey, ir = 0.2 * R;
+          if (ix * ix + iy * iy < ir * ir) A(krmask, i, j) = 0.0;
+        }
       }
   }
   // ---- setup_grid1 (setup_grid1.F): metric combinations and masks ----
@@ -295,6 +300,35 @@ void build_case(const CaseSpec& cs, HostState& H, double& area, double& volume) 
   // mixing.F:156-162
   for (long q = 0; q < n2; q++) { H.arr[kvisc2_r][q] = cs.visc2; H.arr[kvisc2_p][q] = cs.visc2; }
   for (long q = 0; q < n2 * NT; q++) H.arr[kdiff2][q] = cs.tnu2;
+  // set_nudgcof.F:42-111 sponge bands along open edges, on this rank's own
+  // points only (the reference exchanges nothing afterwards, main.F:299)
+  if (cs.obc) {
+    const int isp = 15 + 1;
+    std::vector<double> wrk(n2, 0.0);
+    auto Wk = [&](int i, int j) -> double& { return wrk[(i + 1) + (long)(j + 1) * H.nx2]; };
+    for (int j = std::max(-1, jstrR - 1); j <= jendR; j++)
+      for (int i = std::max(-1, istrR - 1); i <= iendR; i++) {
+        const int ig = i + cs.iSW_corn, jg = j + cs.jSW_corn;
+        int ibnd = isp;
+        if (cs.obc & 1) ibnd = std::min(ibnd, ig);
+        if (cs.obc & 2) ibnd = std::min(ibnd, cs.LLm + 1 - ig);
+        if (cs.obc & 4) ibnd = std::min(ibnd, jg);
+        if (cs.obc & 8) ibnd = std::min(ibnd, cs.MMm + 1 - jg);
+        Wk(i, j) = (double)(isp - ibnd) / (double)isp;
+      }
+    const double vs = cs.v_sponge;
+    for (int j = jstrR; j <= jendR; j++)
+      for (int i = istrR; i <= iendR; i++) A(kvisc2_r, i, j) = A(kvisc2_r, i, j) + vs * Wk(i, j);
+    for (int j = jstr; j <= jendR; j++)
+      for (int i = istr; i <= iendR; i++)
+        A(kvisc2_p, i, j) = A(kvisc2_p, i, j) + 0.25 * vs * (Wk(i, j) + Wk(i - 1, j) + Wk(i, j - 1) + Wk(i - 1, j - 1));
+    for (int it = 1; it <= NT; it++)
+      for (int j = jstrR; j <= jendR; j++)
+        for (int i = istrR; i <= iendR; i++) {
+          double& d2 = H.arr[kdiff2][(i + 1) + (long)(j + 1) * H.nx2 + (long)(it - 1) * n2];
+          d2 = d2 + vs * Wk(i, j);
+        }
+  }
   // ---- set_depth at rest (zeta=0) for ana_init: set_depth.F:65-90 ----
   const double hc = cs.hc, ds = 1.0 / (double)N;
   const double* Cs_w = H.arr[kCs_w].data();
@@ -423,6 +457,38 @@ void build_case(const CaseSpec& cs, HostState& H, double& area, double& volume) 
   wrap(H, H.arr[ku].data(), N, ewp, nsp);
   wrap(H, H.arr[kv].data(), N, ewp, nsp);
   for (int it = 1; it <= NT; it++) wrap(H, H.arr[kt].data() + (long)(it - 1) * 3 * n3, N, ewp, nsp);
+  // analytic open-boundary data (oracle_main.c or_ana_bry): smooth along-edge
+  // profiles of zeta/ubar/vbar/u/v, tracers = initial edge state + 0.05
+  if (cs.obc) {
+    const double pi = 3.14159265358979323;
+    for (int q = 0; q < 4; q++) {
+      const int nb = q < 2 ? Mm + 2 : Lm + 2;
+      const int off = q < 2 ? cs.jSW_corn : cs.iSW_corn;
+      std::vector<double>& bz = H.arr[ROMS_zeta_west + q];
+      std::vector<double>& bub = H.arr[ROMS_ubar_west + q];
+      std::vector<double>& bvb = H.arr[ROMS_vbar_west + q];
+      std::vector<double>& bu = H.arr[ROMS_u_west + q];
+      std::vector<double>& bv = H.arr[ROMS_v_west + q];
+      std::vector<double>& bt = H.arr[ROMS_t_west + q];
+      bz.assign(nb, 0.0); bub.assign(nb, 0.0); bvb.assign(nb, 0.0);
+      bu.assign((size_t)nb * N, 0.0); bv.assign((size_t)nb * N, 0.0); bt.assign((size_t)nb * N * NT, 0.0);
+      for (int m = 0; m < nb; m++) {
+        const int mg = m + off;
+        const double s = q < 2 ? ((double)mg - 0.5) / (double)cs.MMm : ((double)mg - 0.5) / (double)cs.LLm;
+        const double sgn = (q == 0 || q == 2) ? 1.0 : -1.0;
+        bz[m] = sgn * (q < 2 ? 0.05 : 0.03) * std::sin(pi * s);
+        bub[m] = q < 2 ? 0.02 * std::sin(pi * s) : 0.01;
+        bvb[m] = q < 2 ? -0.01 : 0.015 * std::sin(pi * s);
+        for (int k = 1; k <= N; k++) {
+          const double fk = 1.0 + 0.2 * ((double)k - 0.5) / (double)N;
+          bu[m + (size_t)nb * (k - 1)] = bub[m] * fk;
+          bv[m + (size_t)nb * (k - 1)] = bvb[m] * fk;
+          const int i = q == 0 ? 0 : q == 1 ? Lm + 1 : m, j = q == 2 ? 0 : q == 3 ? Mm + 1 : m;
+          for (int it = 1; it <= NT; it++) bt[m + (size_t)nb * ((k - 1) + (size_t)N * (it - 1))] = T(i, j, k, 1, it) + 0.05;
+        }
+      }
+    }
+  }
 }
 
 }  // namespace roms

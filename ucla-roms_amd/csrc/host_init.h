@@ -37,6 +37,8 @@ struct CaseSpec {
   int iSW_corn, jSW_corn;
   int ew_periodic, ns_periodic, west_exchng, east_exchng, south_exchng, north_exchng;
   int salinity, lmd, surf_flux;
+  int obc, island;   // open edges (bitmask), circular land mask
+  double v_sponge;   // set_nudgcof.F sponge
   int host_wrap;  // apply periodic halo wraps on the host (single rank)
   double theta_s, theta_b, hc, rho0, Tcoef, visc2, tnu2, Akv_bak, Akt_bak[2];
   double sizex, sizey;

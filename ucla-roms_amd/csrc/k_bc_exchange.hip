@@ -162,8 +162,13 @@ __global__ void k_t3dbc_corners(Bounds b, const double* __restrict__ rm, double*
 
 static inline bool closed_any(const Bounds& b) { return b.west_edge || b.east_edge || b.south_edge || b.north_edge; }
 
+void launch_u3dbc_obc(const Dev& d, hipStream_t s, const Tlev& t);
+void launch_v3dbc_obc(const Dev& d, hipStream_t s, const Tlev& t);
+void launch_t3dbc_obc_edges(const Dev& d, hipStream_t s, const Tlev& t, int itrc);
+
 void launch_u3dbc(const Dev& d, hipStream_t s, const Tlev& t) {
   if (!closed_any(d.b)) return;
+  if (d.p.obc) { launch_u3dbc_obc(d, s, t); return; }
   const int n = (d.b.jend - d.b.jstr + 1) > (d.b.iendR - d.b.istr + 1) ? (d.b.jend - d.b.jstr + 1) : (d.b.iendR - d.b.istr + 1);
   for (int ph = 0; ph < 2; ph++)
     hipLaunchKernelGGL(k_u3dbc, dim3((n + 255) / 256, d.b.N), dim3(256), 0, s, d.b, d.p.gamma2, d.f.umask, d.f.u,
@@ -171,6 +176,7 @@ void launch_u3dbc(const Dev& d, hipStream_t s, const Tlev& t) {
 }
 void launch_v3dbc(const Dev& d, hipStream_t s, const Tlev& t) {
   if (!closed_any(d.b)) return;
+  if (d.p.obc) { launch_v3dbc_obc(d, s, t); return; }
   const int n = (d.b.iend - d.b.istr + 1) > (d.b.jendR - d.b.jstr + 1) ? (d.b.iend - d.b.istr + 1) : (d.b.jendR - d.b.jstr + 1);
   for (int ph = 0; ph < 2; ph++)
     hipLaunchKernelGGL(k_v3dbc, dim3((n + 255) / 256, d.b.N), dim3(256), 0, s, d.b, d.p.gamma2, d.f.vmask, d.f.v,
@@ -179,7 +185,8 @@ void launch_v3dbc(const Dev& d, hipStream_t s, const Tlev& t) {
 void launch_t3dbc(const Dev& d, hipStream_t s, const Tlev& t, int itrc) {
   if (!closed_any(d.b)) return;
   const int n = (d.b.jend - d.b.jstr + 1) + (d.b.iend - d.b.istr + 1);
-  hipLaunchKernelGGL(k_t3dbc_edges, dim3((n + 255) / 256, d.b.N), dim3(256), 0, s, d.b, d.f.rmask, d.f.t, t.nnew, itrc);
+  if (d.p.obc) launch_t3dbc_obc_edges(d, s, t, itrc);
+  else hipLaunchKernelGGL(k_t3dbc_edges, dim3((n + 255) / 256, d.b.N), dim3(256), 0, s, d.b, d.f.rmask, d.f.t, t.nnew, itrc);
   hipLaunchKernelGGL(k_t3dbc_corners, dim3((4 * d.b.N + 255) / 256), dim3(256), 0, s, d.b, d.f.rmask, d.f.t, t.nnew,
                      itrc);
 }

@@ -62,22 +62,57 @@ __global__ void __launch_bounds__(256) k_s2d_zeta(Dev d, Range R, FBCoef c) {
   F.s4[ij] = rzeta * zwrk;
 }
 
-// zetabc_tile (zetabc.F) for closed walls: zero-gradient, corners averaged
-__global__ void k_s2d_zetabc(Dev d, int phase) {
+// zetabc_tile (zetabc.F:3-224): zero-gradient on closed edges, OBC_M2FLATHER
+// on open ones (from zeta(kstp)), corners averaged
+__global__ void k_s2d_zetabc(Dev d, int phase, int kstp) {
   const Bounds& b = d.b;
   double* zn = d.f.s0;
   const double* rm = d.f.rmask;
+  const double* zk = d.f.zeta + (long)(kstp - 1) * b.n2;
+  const double dtf = d.p.dtfast, g = d.p.g;
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (phase == 0) {
     const int nj = b.jend - (b.jstrV - 1) + 1, ni = b.iend - (b.istrU - 1) + 1;
     if (p < nj) {
       const int j = b.jstrV - 1 + p;
-      if (b.west_edge) zn[IJ(b, b.istr - 1, j)] = zn[IJ(b, b.istr, j)] * rm[IJ(b, b.istr - 1, j)];
-      if (b.east_edge) zn[IJ(b, b.iend + 1, j)] = zn[IJ(b, b.iend, j)] * rm[IJ(b, b.iend + 1, j)];
+      if (b.west_edge) {
+        const int i = b.istr;
+        if (d.p.obc & 1) {
+          const double cx = dtf * d.f.pm[IJ(b, i, j)] * sqrt(g * d.f.h[IJ(b, i, j)]);
+          zn[IJ(b, i - 1, j)] = ((1. - cx) * zk[IJ(b, i - 1, j)] + cx * zk[IJ(b, i, j)]) * rm[IJ(b, i - 1, j)];
+        } else {
+          zn[IJ(b, i - 1, j)] = zn[IJ(b, i, j)] * rm[IJ(b, i - 1, j)];
+        }
+      }
+      if (b.east_edge) {
+        const int i = b.iend;
+        if (d.p.obc & 2) {
+          const double cx = dtf * d.f.pm[IJ(b, i, j)] * sqrt(g * d.f.h[IJ(b, i, j)]);
+          zn[IJ(b, i + 1, j)] = ((1. - cx) * zk[IJ(b, i + 1, j)] + cx * zk[IJ(b, i, j)]) * rm[IJ(b, i + 1, j)];
+        } else {
+          zn[IJ(b, i + 1, j)] = zn[IJ(b, i, j)] * rm[IJ(b, i + 1, j)];
+        }
+      }
     } else if (p < nj + ni) {
       const int i = b.istrU - 1 + p - nj;
-      if (b.south_edge) zn[IJ(b, i, b.jstr - 1)] = zn[IJ(b, i, b.jstr)] * rm[IJ(b, i, b.jstr - 1)];
-      if (b.north_edge) zn[IJ(b, i, b.jend + 1)] = zn[IJ(b, i, b.jend)] * rm[IJ(b, i, b.jend + 1)];
+      if (b.south_edge) {
+        const int j = b.jstr;
+        if (d.p.obc & 4) {
+          const double cx = dtf * d.f.pn[IJ(b, i, j)] * sqrt(g * d.f.h[IJ(b, i, j)]);
+          zn[IJ(b, i, j - 1)] = ((1. - cx) * zk[IJ(b, i, j - 1)] + cx * zk[IJ(b, i, j)]) * rm[IJ(b, i, j - 1)];
+        } else {
+          zn[IJ(b, i, j - 1)] = zn[IJ(b, i, j)] * rm[IJ(b, i, j - 1)];
+        }
+      }
+      if (b.north_edge) {
+        const int j = b.jend;
+        if (d.p.obc & 8) {
+          const double cx = dtf * d.f.pn[IJ(b, i, j)] * sqrt(g * d.f.h[IJ(b, i, j)]);
+          zn[IJ(b, i, j + 1)] = ((1. - cx) * zk[IJ(b, i, j + 1)] + cx * zk[IJ(b, i, j)]) * rm[IJ(b, i, j + 1)];
+        } else {
+          zn[IJ(b, i, j + 1)] = zn[IJ(b, i, j)] * rm[IJ(b, i, j + 1)];
+        }
+      }
     }
   } else if (p == 0) {
     const int is = b.istr, ie = b.iend, js = b.jstr, je = b.jend;
@@ -468,40 +503,171 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int cl
   }
 }
 
-// u2dbc/v2dbc (closed), boundary Dnew, boundary flux averages (step2d_FB.F:444-529)
+// u2dbc/v2dbc (u2dbc_im.F:3-481, v2dbc_im.F:3-472), boundary Dnew and the
+// boundary flux averages (step2d_FB.F:444-529).  Phase 0: wall-normal
+// components (closed: 0; open: OBC_M2FLATHER with zeta/ubar_west...),
+// 1: tangential components (closed: gamma2; open: the OBC_M2ORLANSKI branch
+// the reference switches to under OBC_M2FLATHER, u2dbc_im.F:270-273) and the
+// boundary Dnew, 2: corners between adjacent open edges, 3: flux averages.
+__device__ __forceinline__ double flather_zx(double cx, double zi, double zb, double zin) {
+  double zx = (0.5 + cx) * zi + (0.5 - cx) * zb;
+  if (cx > 0.292893218813452) {
+    const double q = 1. - 0.292893218813452 / cx;
+    zx = zx + (zin + cx * zb - (1. + cx) * zi) * (q * q);
+  }
+  return zx;
+}
+__device__ __forceinline__ double orl_tan2(double cx, double cy, double bs, double is, double gb0, double gb1,
+                                           double gi0, double gi1, double bry) {
+  double cext;
+  if (cx > 0.) cext = 0.;
+  else { cext = -cx; cx = 0.; }
+  double r = (1. - cx) * (bs - fmax0(cy) * gb0 - fmin0(cy) * gb1) + cx * (is - fmax0(cy) * gi0 - fmin0(cy) * gi1);
+  return (1. - cext) * r + cext * bry;
+}
 __global__ void k_s2d_edges(Dev d, FBCoef c, int phase) {
   const Bounds& b = d.b;
   const Fields& F = d.f;
-  const long n2 = b.n2, kn = (long)(c.knew - 1) * n2;
+  const long n2 = b.n2, kn = (long)(c.knew - 1) * n2, ksl = (long)(c.kstp - 1) * n2;
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   const int L = b.nx2 > b.Mm + 4 ? b.nx2 : b.Mm + 4;  // edge lanes per side
   const int side = p / L, q = p - side * L;
   if (side > 3) return;
   double* ub = F.ubar + kn;
   double* vb = F.vbar + kn;
+  const double* ubs = F.ubar + ksl;
+  const double* vbs = F.vbar + ksl;
+  const double* zs = F.zeta + ksl;
+  const double* zn = F.zeta + kn;
   double* Dn = F.s1;
-  const double g2 = d.p.gamma2;
+  const double g2 = d.p.gamma2, dtf = d.p.dtfast, g = d.p.g;
+  const int is = b.istr, ie = b.iend, js = b.jstr, je = b.jend;
+  const bool oW = d.p.obc & 1, oE = d.p.obc & 2, oS = d.p.obc & 4, oN = d.p.obc & 8;
+  auto pm = [&](int i, int j) { return F.pm[IJ(b, i, j)]; };
+  auto pn = [&](int i, int j) { return F.pn[IJ(b, i, j)]; };
+  auto hh = [&](int i, int j) { return F.h[IJ(b, i, j)]; };
+  auto U = [&](const double* a, int i, int j) { return a[IJ(b, i, j)]; };
   if (phase == 0) {  // wall-normal components
-    if (side == 0 && b.west_edge && q <= b.jend - b.jstr) ub[IJ(b, b.istr, b.jstr + q)] = 0.0;
-    if (side == 1 && b.east_edge && q <= b.jend - b.jstr) ub[IJ(b, b.iend + 1, b.jstr + q)] = 0.0;
-    if (side == 2 && b.south_edge && q <= b.iend - b.istr) vb[IJ(b, b.istr + q, b.jstr)] = 0.0;
-    if (side == 3 && b.north_edge && q <= b.iend - b.istr) vb[IJ(b, b.istr + q, b.jend + 1)] = 0.0;
+    if (side == 0 && b.west_edge && q <= je - js) {
+      const int j = js + q;
+      double val = 0.0;
+      if (oW) {
+        const double cff = 0.5 * (hh(is - 1, j) + hh(is, j));
+        const double hx = sqrt(g / cff);
+        const double cx = dtf * cff * hx * 0.5 * (pm(is - 1, j) + pm(is, j));
+        const double zx = flather_zx(cx, U(zs, is, j), U(zs, is - 1, j), U(zn, is, j));
+        val = 0.5 * ((1. - cx) * U(ubs, is, j) + cx * U(ubs, is + 1, j) + F.bubar[0][j] - hx * (zx - F.bzeta[0][j])) *
+              F.umask[IJ(b, is, j)];
+      }
+      ub[IJ(b, is, j)] = val;
+    }
+    if (side == 1 && b.east_edge && q <= je - js) {
+      const int j = js + q;
+      double val = 0.0;
+      if (oE) {
+        const double cff = 0.5 * (hh(ie, j) + hh(ie + 1, j));
+        const double hx = sqrt(g / cff);
+        const double cx = dtf * cff * hx * 0.5 * (pm(ie, j) + pm(ie + 1, j));
+        const double zx = flather_zx(cx, U(zs, ie, j), U(zs, ie + 1, j), U(zn, ie, j));
+        val = 0.5 * ((1. - cx) * U(ubs, ie + 1, j) + cx * U(ubs, ie, j) + F.bubar[1][j] + hx * (zx - F.bzeta[1][j])) *
+              F.umask[IJ(b, ie + 1, j)];
+      }
+      ub[IJ(b, ie + 1, j)] = val;
+    }
+    if (side == 2 && b.south_edge && q <= ie - is) {
+      const int i = is + q;
+      double val = 0.0;
+      if (oS) {
+        const double cff = 0.5 * (hh(i, js - 1) + hh(i, js));
+        const double hx = sqrt(g / cff);
+        const double cx = dtf * cff * hx * 0.5 * (pn(i, js - 1) + pn(i, js));
+        const double zx = flather_zx(cx, U(zs, i, js), U(zs, i, js - 1), U(zn, i, js));
+        val = 0.5 * ((1. - cx) * U(vbs, i, js) + cx * U(vbs, i, js + 1) + F.bvbar[2][i] - hx * (zx - F.bzeta[2][i])) *
+              F.vmask[IJ(b, i, js)];
+      }
+      vb[IJ(b, i, js)] = val;
+    }
+    if (side == 3 && b.north_edge && q <= ie - is) {
+      const int i = is + q;
+      double val = 0.0;
+      if (oN) {
+        const double cff = 0.5 * (hh(i, je) + hh(i, je + 1));
+        const double hx = sqrt(g / cff);
+        const double cx = dtf * cff * hx * 0.5 * (pn(i, je) + pn(i, je + 1));
+        const double zx = flather_zx(cx, U(zs, i, je), U(zs, i, je + 1), U(zn, i, je));
+        val = 0.5 * ((1. - cx) * U(vbs, i, je + 1) + cx * U(vbs, i, je) + F.bvbar[3][i] + hx * (zx - F.bzeta[3][i])) *
+              F.vmask[IJ(b, i, je + 1)];
+      }
+      vb[IJ(b, i, je + 1)] = val;
+    }
   } else if (phase == 1) {  // tangential components + boundary Dnew
-    if (side == 2 && b.south_edge && q <= b.iendR - b.istr) {
-      const int i = b.istr + q;
-      ub[IJ(b, i, b.jstr - 1)] = g2 * ub[IJ(b, i, b.jstr)] * F.umask[IJ(b, i, b.jstr - 1)];
+    if (side == 2 && b.south_edge) {
+      if (oS) {
+        const int i = b.istrU + q;
+        if (i <= ie) {
+          auto gr = [&](int ii, int jj) { return U(ubs, ii + 1, jj) - U(ubs, ii, jj); };
+          const double cx = -0.125 * dtf * (U(vbs, i, js) + U(vbs, i - 1, js)) * (pn(i, js - 1) + pn(i - 1, js - 1) + pn(i, js) + pn(i - 1, js));
+          const double cy = 0.125 * dtf * (U(ubs, i, js - 1) + U(ubs, i, js)) * (pm(i, js - 1) + pm(i - 1, js - 1) + pm(i, js) + pm(i - 1, js));
+          const double r = orl_tan2(cx, cy, U(ubs, i, js - 1), U(ubs, i, js), gr(i - 1, js - 1), gr(i, js - 1),
+                                    gr(i - 1, js), gr(i, js), F.bubar[2][i]);
+          ub[IJ(b, i, js - 1)] = r * F.umask[IJ(b, i, js - 1)];
+        }
+      } else if (q <= b.iendR - is) {
+        const int i0 = b.ew_periodic ? b.istrU : is, i1 = b.ew_periodic ? ie : b.iendR;
+        const int i = i0 + q;
+        if (i <= i1) ub[IJ(b, i, js - 1)] = g2 * ub[IJ(b, i, js)] * F.umask[IJ(b, i, js - 1)];
+      }
     }
-    if (side == 3 && b.north_edge && q <= b.iendR - b.istr) {
-      const int i = b.istr + q;
-      ub[IJ(b, i, b.jend + 1)] = g2 * ub[IJ(b, i, b.jend)] * F.umask[IJ(b, i, b.jend + 1)];
+    if (side == 3 && b.north_edge) {
+      if (oN) {
+        const int i = b.istrU + q;
+        if (i <= ie) {
+          auto gr = [&](int ii, int jj) { return U(ubs, ii + 1, jj) - U(ubs, ii, jj); };
+          const double cx = 0.125 * dtf * (U(vbs, i, je + 1) + U(vbs, i - 1, je + 1)) * (pn(i, je) + pn(i - 1, je) + pn(i, je + 1) + pn(i - 1, je + 1));
+          const double cy = 0.125 * dtf * (U(ubs, i, je) + U(ubs, i, je + 1)) * (pm(i, je) + pm(i - 1, je) + pm(i, je + 1) + pm(i - 1, je + 1));
+          const double r = orl_tan2(cx, cy, U(ubs, i, je + 1), U(ubs, i, je), gr(i - 1, je + 1), gr(i, je + 1),
+                                    gr(i - 1, je), gr(i, je), F.bubar[3][i]);
+          ub[IJ(b, i, je + 1)] = r * F.umask[IJ(b, i, je + 1)];
+        }
+      } else if (q <= b.iendR - is) {
+        const int i0 = b.ew_periodic ? b.istrU : is, i1 = b.ew_periodic ? ie : b.iendR;
+        const int i = i0 + q;
+        if (i <= i1) ub[IJ(b, i, je + 1)] = g2 * ub[IJ(b, i, je)] * F.umask[IJ(b, i, je + 1)];
+      }
     }
-    if (side == 0 && b.west_edge && q <= b.jendR - b.jstr) {
-      const int j = b.jstr + q;
-      vb[IJ(b, b.istr - 1, j)] = g2 * vb[IJ(b, b.istr, j)] * F.vmask[IJ(b, b.istr - 1, j)];
+    if (side == 0 && b.west_edge) {
+      if (oW) {
+        const int j = b.jstrV + q;
+        if (j <= je) {
+          auto gr = [&](int ii, int jj) { return U(vbs, ii, jj + 1) - U(vbs, ii, jj); };
+          const double cx = -0.125 * dtf * (U(ubs, is, j) + U(ubs, is, j - 1)) * (pm(is - 1, j) + pm(is - 1, j - 1) + pm(is, j) + pm(is, j - 1));
+          const double cy = 0.125 * dtf * (U(vbs, is - 1, j) + U(vbs, is, j)) * (pn(is - 1, j) + pn(is - 1, j - 1) + pn(is, j) + pn(is, j - 1));
+          const double r = orl_tan2(cx, cy, U(vbs, is - 1, j), U(vbs, is, j), gr(is - 1, j - 1), gr(is - 1, j),
+                                    gr(is, j - 1), gr(is, j), F.bvbar[0][j]);
+          vb[IJ(b, is - 1, j)] = r * F.vmask[IJ(b, is - 1, j)];
+        }
+      } else {
+        const int j0 = b.ns_periodic ? b.jstrV : js, j1 = b.ns_periodic ? je : b.jendR;
+        const int j = j0 + q;
+        if (j <= j1) vb[IJ(b, is - 1, j)] = g2 * vb[IJ(b, is, j)] * F.vmask[IJ(b, is - 1, j)];
+      }
     }
-    if (side == 1 && b.east_edge && q <= b.jendR - b.jstr) {
-      const int j = b.jstr + q;
-      vb[IJ(b, b.iend + 1, j)] = g2 * vb[IJ(b, b.iend, j)] * F.vmask[IJ(b, b.iend + 1, j)];
+    if (side == 1 && b.east_edge) {
+      if (oE) {
+        const int j = b.jstrV + q;
+        if (j <= je) {
+          auto gr = [&](int ii, int jj) { return U(vbs, ii, jj + 1) - U(vbs, ii, jj); };
+          const double cx = 0.125 * dtf * (U(ubs, ie + 1, j) + U(ubs, ie + 1, j - 1)) * (pm(ie, j) + pm(ie, j - 1) + pm(ie + 1, j) + pm(ie + 1, j - 1));
+          const double cy = 0.125 * dtf * (U(vbs, ie, j) + U(vbs, ie + 1, j)) * (pn(ie, j) + pn(ie, j - 1) + pn(ie + 1, j) + pn(ie + 1, j - 1));
+          const double r = orl_tan2(cx, cy, U(vbs, ie + 1, j), U(vbs, ie, j), gr(ie + 1, j - 1), gr(ie + 1, j),
+                                    gr(ie, j - 1), gr(ie, j), F.bvbar[1][j]);
+          vb[IJ(b, ie + 1, j)] = r * F.vmask[IJ(b, ie + 1, j)];
+        }
+      } else {
+        const int j0 = b.ns_periodic ? b.jstrV : js, j1 = b.ns_periodic ? je : b.jendR;
+        const int j = j0 + q;
+        if (j <= j1) vb[IJ(b, ie + 1, j)] = g2 * vb[IJ(b, ie, j)] * F.vmask[IJ(b, ie + 1, j)];
+      }
     }
     if (side == 0 && b.west_edge && q <= b.jendR - (b.jstr - 1)) {
       const long o = IJ(b, b.istr - 1, b.jstr - 1 + q);
@@ -519,6 +685,17 @@ __global__ void k_s2d_edges(Dev d, FBCoef c, int phase) {
       const long o = IJ(b, b.istr - 1 + q, b.jend + 1);
       Dn[o] = F.h[o] + F.s0[o];
     }
+  } else if (phase == 2) {  // corners between adjacent open edges (u2dbc_im.F:445-478, v2dbc_im.F:440-469)
+    if (p != 0) return;
+    const bool W = b.west_edge && oW, E = b.east_edge && oE, S = b.south_edge && oS, N = b.north_edge && oN;
+    if (S && W) ub[IJ(b, is, js - 1)] = 0.5 * (ub[IJ(b, is + 1, js - 1)] + ub[IJ(b, is, js)]);
+    if (S && E) ub[IJ(b, ie + 1, js - 1)] = 0.5 * (ub[IJ(b, ie, js - 1)] + ub[IJ(b, ie + 1, js)]);
+    if (N && W) ub[IJ(b, is, je + 1)] = 0.5 * (ub[IJ(b, is + 1, je + 1)] + ub[IJ(b, is, je)]);
+    if (N && E) ub[IJ(b, ie + 1, je + 1)] = 0.5 * (ub[IJ(b, ie, je + 1)] + ub[IJ(b, ie + 1, je)]);
+    if (S && W) vb[IJ(b, is - 1, js)] = 0.5 * (vb[IJ(b, is - 1, js + 1)] + vb[IJ(b, is, js)]);
+    if (S && E) vb[IJ(b, ie + 1, js)] = 0.5 * (vb[IJ(b, ie + 1, js + 1)] + vb[IJ(b, ie, js)]);
+    if (N && W) vb[IJ(b, is - 1, je + 1)] = 0.5 * (vb[IJ(b, is - 1, je)] + vb[IJ(b, is, je + 1)]);
+    if (N && E) vb[IJ(b, ie + 1, je + 1)] = 0.5 * (vb[IJ(b, ie + 1, je)] + vb[IJ(b, ie, je + 1)]);
   } else {  // boundary fast-time-averaged fluxes
     const double cff1 = 0.5 * c.w1;
     const long sj = b.nx2;
@@ -603,8 +780,8 @@ void launch_step2d(const Dev& d, hipStream_t s, const Tlev& t, const double* w1,
     hipLaunchKernelGGL(k_s2d_zeta, grid_of(RA), dim3(kBX, kBY), 0, s, d, RA, c);
     if (closed) {
       const int n = (b.jend - b.jstrV + 2) + (b.iend - b.istrU + 2);
-      hipLaunchKernelGGL(k_s2d_zetabc, dim3((n + 255) / 256), dim3(256), 0, s, d, 0);
-      hipLaunchKernelGGL(k_s2d_zetabc, dim3(1), dim3(64), 0, s, d, 1);
+      hipLaunchKernelGGL(k_s2d_zetabc, dim3((n + 255) / 256), dim3(256), 0, s, d, 0, c.kstp);
+      hipLaunchKernelGGL(k_s2d_zetabc, dim3(1), dim3(64), 0, s, d, 1, c.kstp);
     }
     hipLaunchKernelGGL(k_s2d_mom, grid_of(RB), dim3(kBX, kBY), 0, s, d, RB, c);
   } else {
@@ -615,8 +792,10 @@ void launch_step2d(const Dev& d, hipStream_t s, const Tlev& t, const double* w1,
   }
   if (closed) {
     const int L = b.nx2 > b.Mm + 4 ? b.nx2 : b.Mm + 4;
-    for (int ph = 0; ph < 3; ph++)
-      hipLaunchKernelGGL(k_s2d_edges, dim3((4 * L + 255) / 256), dim3(256), 0, s, d, c, ph);
+    for (int ph = 0; ph < 4; ph++) {
+      if (ph == 2 && !d.p.obc) continue;
+      hipLaunchKernelGGL(k_s2d_edges, dim3(ph == 2 ? 1 : (4 * L + 255) / 256), dim3(ph == 2 ? 64 : 256), 0, s, d, c, ph);
+    }
   }
   if (t.iif == t.nfast) {
     hipLaunchKernelGGL(k_s2d_last, grid_of(RB), dim3(kBX, kBY), 0, s, d, RB, t.knew);

@@ -33,6 +33,8 @@ struct Params {
   int nonlin_eos, salinity, lmd, uv_vis2, ts_dif2;
   int s2d_split;  // 1: step2d as separate zeta / momentum kernels (ROMS_GPU_S2D_SPLIT=1)
   int npip;       // pipe_frc.F: number of pipes (0: pipe_source off)
+  int obc;        // open edges: 1 W, 2 E, 4 S, 8 N (Flather / Orlanski + *_FRC_BRY)
+  double ubind;   // OBC binding velocity
   double dt, dtfast, g, rho0, vonKar, qp2, gamma2, hc;
   double rdrg, Zob, Tcoef, T0, Scoef, S0;
   double Akv_bak, Akt_bak[2];  // scalars.F:83
@@ -65,6 +67,9 @@ struct Fields {
   // pipe_frc.F: pipe_idx (0: none), pipe_flx, pipe_prf(npip,N), pipe_trc(npip,NT)
   int* pipe_idx;
   double *pipe_flx, *pipe_prf, *pipe_trc;
+  // boundary.F open-boundary data, [0] west, [1] east (index j, 0:Mm+1),
+  // [2] south, [3] north (index i, 0:Lm+1); u, v (.,N); t (.,N,NT)
+  double *bzeta[4], *bubar[4], *bvbar[4], *bu[4], *bv[4], *bt[4];
   // column-solver scratch in global memory, 2*max(NT,2) slots of (0:N) levels
   // (nullptr: the solvers keep their columns in LDS; see ColGlb in k_common.h)
   double* colscr;

@@ -140,8 +140,14 @@ long field_count(int id, const Bounds& b) {
       return n3w;
     case ROMS_Akt: return n3w * b.nTS;
     case ROMS_diff2: case ROMS_stflx: return n2 * b.NT;
-    default: return n2;
+    default: break;
   }
+  if (id >= ROMS_zeta_west && id <= ROMS_t_north) {
+    const int side = (id - ROMS_zeta_west) % 4, var = (id - ROMS_zeta_west) / 4;
+    const long nb = side < 2 ? b.Mm + 2 : b.Lm + 2;
+    return var < 3 ? nb : var < 5 ? nb * b.N : nb * b.N * b.NT;
+  }
+  return n2;
 }
 
 double** field_slot(Fields& F, int id) {
@@ -168,8 +174,14 @@ double** field_slot(Fields& F, int id) {
     case ROMS_swr_frac: return &F.swr_frac; case ROMS_sustr: return &F.sustr; case ROMS_svstr: return &F.svstr;
     case ROMS_stflx: return &F.stflx; case ROMS_srflx: return &F.srflx; case ROMS_swflx: return &F.swflx;
     case ROMS_ru: return &F.ru; case ROMS_rv: return &F.rv;
-    default: return nullptr;
+    default: break;
   }
+  if (id >= ROMS_zeta_west && id <= ROMS_t_north) {
+    const int side = (id - ROMS_zeta_west) % 4, var = (id - ROMS_zeta_west) / 4;
+    double** tab[6] = {F.bzeta, F.bubar, F.bvbar, F.bu, F.bv, F.bt};
+    return &tab[var][side];
+  }
+  return nullptr;
 }
 
 void free_all() {
@@ -284,6 +296,10 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
   P.rdrg = cfg->rdrg; P.Zob = cfg->Zob; P.Tcoef = cfg->Tcoef; P.T0 = cfg->T0; P.Scoef = cfg->Scoef; P.S0 = cfg->S0;
   P.Akv_bak = cfg->Akv_bak; P.Akt_bak[0] = cfg->Akt_bak[0]; P.Akt_bak[1] = cfg->Akt_bak[1];
   P.npip = 0;
+  if (cfg->obc < 0 || cfg->obc > 15) { g.err = "roms_gpu_init: obc must be a 4-bit edge mask"; return -1; }
+  P.obc = cfg->obc & ((dims->ew_periodic ? 0 : 3) | (dims->ns_periodic ? 0 : 12));
+  P.ubind = cfg->ubind;
+  if (P.obc) P.s2d_split = 1;  // open edges: separate zeta / zetabc / momentum kernels (step2d)
   for (int i = 0; i < kMaxFast; i++) { g.w1[i] = cfg->weight[0][i]; g.w2[i] = cfg->weight[1][i]; }
   // column-solver scratch: LDS while two (N+1)-level slots per wave fit the
   // default 64 KB (N < 63), global memory for deeper grids;
@@ -556,6 +572,8 @@ static int init_case_impl(const roms_case* c, int np_xi, int np_eta, void* comm,
   C.Tcoef = 0.20; C.T0 = 1.0; C.Scoef = 0.822; C.S0 = 1.0;
   C.theta_s = 6.0; C.theta_b = pipes ? 6.0 : 2.0; C.hc = (fil || pipes) ? 25.0 : 250.0;
   // tests/Pipes_ana/benchmark.in has no vertical_mixing line: Akv_bak = Akt_bak = 0
+  C.obc = c->case_id == ROMS_CASE_BASIN ? c->obc : 0;
+  C.ubind = 0.1;  // Examples/Iceland/Iceland_parent/roms.in: ubind
   C.Akv_bak = (fil || pipes) ? 0.0 : 1.0e-4; C.Akt_bak[0] = (fil || pipes) ? 0.0 : 1.0e-5; C.Akt_bak[1] = C.Akt_bak[0];
   int r = roms_gpu_init(&D, &C, device, comm);
   if (r) return r;
@@ -570,6 +588,8 @@ static int init_case_impl(const roms_case* c, int np_xi, int np_eta, void* comm,
   cs.Tcoef = C.Tcoef; cs.visc2 = 0.0; cs.tnu2 = 0.0; cs.Akv_bak = C.Akv_bak;
   cs.Akt_bak[0] = C.Akt_bak[0]; cs.Akt_bak[1] = C.Akt_bak[1];
   cs.sizex = c->sizex; cs.sizey = c->sizey;
+  cs.obc = C.obc; cs.island = c->case_id == ROMS_CASE_BASIN ? c->island : 0;
+  cs.v_sponge = C.obc ? c->v_sponge : 0.0;
   HostState H(D.Lm, D.Mm, D.N, D.NT, C.salinity ? 2 : 1);
   double area = 0.0, volume = 0.0;
   build_case(cs, H, area, volume);
