@@ -29,6 +29,7 @@ module roms_gpu_mod
     real(c_double) :: theta_s, theta_b, hc
     integer(c_int) :: obc                        ! OBC_WEST 1, OBC_EAST 2, OBC_SOUTH 4, OBC_NORTH 8
     real(c_double) :: ubind
+    integer(c_int) :: curvgrid                   ! CURVGRID
   end type
 
   type, bind(c) :: roms_tlev
@@ -44,6 +45,7 @@ module roms_gpu_mod
     integer(c_int) :: obc
     real(c_double) :: v_sponge
     integer(c_int) :: island
+    integer(c_int) :: curvgrid
   end type
 
   integer(c_int), parameter :: ROMS_GPU_ABI = 4   ! ROMS_GPU_ABI_VERSION, include/roms_gpu.h

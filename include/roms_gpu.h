@@ -54,6 +54,7 @@ typedef struct roms_cfg {
                                     OBC_M2FLATHER, OBC_M3ORLANSKI, OBC_TORLANSKI and Z/M2/M3/T_FRC_BRY;
                                     closed walls elsewhere (zetabc.F, u2dbc_im.F ... t3dbc_im.F)  */
   double ubind;                  /* OBC binding velocity [m/s] (scalars.F, read_inp_mod.F:809)    */
+  int curvgrid;                  /* CURVGRID (with UV_ADV): curvature terms in the momentum r.h.s. */
 } roms_cfg;
 
 /* Time-step indices (scalars.F:32-36).  The step entry updates them. */
@@ -91,6 +92,8 @@ enum roms_field {
   ROMS_u_west, ROMS_u_east, ROMS_u_south, ROMS_u_north,
   ROMS_v_west, ROMS_v_east, ROMS_v_south, ROMS_v_north,
   ROMS_t_west, ROMS_t_east, ROMS_t_south, ROMS_t_north,
+  /* grid.F CURVGRID metric derivatives d(1/n)/dxi, d(1/m)/deta (setup_grid1.F:89-103) */
+  ROMS_dndx, ROMS_dmde,
   ROMS_NFIELDS
 };
 
@@ -158,6 +161,7 @@ typedef struct roms_case {
   int obc;        /* basin only: open edges (roms_cfg.obc) with analytic boundary data, ubind 0.1 */
   double v_sponge;/* basin only: SPONGE band viscosity/diffusivity [m2/s] (set_nudgcof.F)      */
   int island;     /* basin only: circular land mask (MASKING)                                   */
+  int curvgrid;   /* basin only: non-uniform metrics pm(j), pn(i) and CURVGRID                  */
 } roms_case;
 /* Builds the analytic grid/ICs on the host (setup_grid1/2, set_scoord,
  * set_weights, ana_init), initialises the device and runs roms_init.        */

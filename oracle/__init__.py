@@ -30,7 +30,7 @@ class OrCfg(ctypes.Structure):
                 ("S0", ctypes.c_double), ("sizex", ctypes.c_double), ("sizey", ctypes.c_double),
                 ("diag_np_xi", ctypes.c_int), ("diag_np_eta", ctypes.c_int), ("surf_flux", ctypes.c_int),
                 ("obc", ctypes.c_int), ("ubind", ctypes.c_double), ("v_sponge", ctypes.c_double),
-                ("island", ctypes.c_int)]
+                ("island", ctypes.c_int), ("curvgrid", ctypes.c_int)]
 
 
 def build():

@@ -62,6 +62,7 @@ or_state *or_create(const or_cfg *cfg) {
   for (int q = 0; q < 6; q++) S->c1[q] = zalloc((size_t)S->nx2 * (S->N + 1));
   if (cfg->lmd) or_lmd_alloc(S);
   S->pipe_flx = zalloc(n2); S->pipe_idx = zalloc(n2);
+  S->dndx = zalloc(n2); S->dmde = zalloc(n2);
   /* boundary.F:111-129: zeta_west(0:Mm+1), u_west(0:Mm+1,N), t_west(0:Mm+1,N,NT), ... */
   S->nbry[0] = S->nbry[1] = S->Mm + 2;
   S->nbry[2] = S->nbry[3] = S->Lm + 2;
@@ -205,6 +206,14 @@ static void setup_grid1(or_state *S) {
   double *ex[] = {S->dm_r, S->dn_r, S->dm_p, S->dn_p, S->dm_u, S->dn_u, S->iA_u, S->dm_v, S->dn_v,
                   S->iA_v, S->pmon_u, S->pnom_v, S->rmask, S->umask, S->vmask, S->pmask};
   for (size_t q = 0; q < sizeof(ex) / sizeof(ex[0]); q++) or_exch2(S, ex[q]);
+  if (S->c.curvgrid) {  /* setup_grid1.F:89-103, exchanged at :203 */
+    for (int j = S->jstrR; j <= S->jendR; j++)
+      for (int i = S->istr; i <= S->iend; i++) A2(S->dndx, i, j) = 0.5 / A2(pn, i + 1, j) - 0.5 / A2(pn, i - 1, j);
+    for (int j = S->jstr; j <= S->jend; j++)
+      for (int i = S->istrR; i <= S->iendR; i++) A2(S->dmde, i, j) = 0.5 / A2(pm, i, j + 1) - 0.5 / A2(pm, i, j - 1);
+    or_exch2(S, S->dndx);
+    or_exch2(S, S->dmde);
+  }
 }
 
 /* ---------------------------------------------------------------------- */
@@ -452,6 +461,11 @@ void or_ana_grid(or_state *S) {
         const double x = dx * ((double)i - 0.5), y = dy * ((double)j - 0.5);
         A2(S->xr, i, j) = x; A2(S->yr, i, j) = y;
         A2(S->pm, i, j) = 1.0 / dx; A2(S->pn, i, j) = 1.0 / dy;
+        if (S->c.curvgrid) {  /* non-uniform metrics: m varies along eta, n along xi */
+          const double pi = 3.14159265358979323;
+          A2(S->pm, i, j) = (1.0 + 0.1 * sin(2.0 * pi * ((double)j - 0.5) / (double)S->c.MMm)) / dx;
+          A2(S->pn, i, j) = (1.0 + 0.1 * cos(2.0 * pi * ((double)i - 0.5) / (double)S->c.LLm)) / dy;
+        }
         A2(S->f, i, j) = 1.0e-4;
         const double rx = x - 0.5 * S->c.sizex, ry = y - 0.5 * S->c.sizey;
         double s = 1.0 - (rx * rx + ry * ry) / (R * R);
@@ -745,7 +759,7 @@ double *or_field(or_state *S, const char *name, size_t *count) {
       {"dm_u", S->dm_u, S->n2}, {"dn_u", S->dn_u, S->n2}, {"dm_v", S->dm_v, S->n2}, {"dn_v", S->dn_v, S->n2},
       {"dm_p", S->dm_p, S->n2}, {"dn_p", S->dn_p, S->n2}, {"pmon_u", S->pmon_u, S->n2},
       {"pnom_v", S->pnom_v, S->n2}, {"rmask", S->rmask, S->n2}, {"umask", S->umask, S->n2},
-      {"vmask", S->vmask, S->n2}, {"pmask", S->pmask, S->n2}, {"xr", S->xr, S->n2}, {"yr", S->yr, S->n2},
+      {"vmask", S->vmask, S->n2}, {"pmask", S->pmask, S->n2}, {"dndx", S->dndx, S->n2}, {"dmde", S->dmde, S->n2}, {"xr", S->xr, S->n2}, {"yr", S->yr, S->n2},
       {"visc2_r", S->visc2_r, S->n2}, {"visc2_p", S->visc2_p, S->n2}, {"diff2", S->diff2, S->n2 * S->NT},
       {"sustr", S->sustr, S->n2}, {"svstr", S->svstr, S->n2}, {"stflx", S->stflx, S->n2 * S->NT},
       {"srflx", S->srflx, S->n2}, {"swflx", S->swflx, S->n2}, {"hbls", S->hbls, S->n2}, {"hbbl", S->hbbl, S->n2},

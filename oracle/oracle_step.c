@@ -618,7 +618,12 @@ static void horiz_rhs_uv(or_state *S, int k, int upstream, double *ru, double *r
   /* Coriolis */
   for (int j = jstrV - 1; j <= jend; j++)
     for (int i = istrU - 1; i <= iend; i++) {
-      const double cff = 0.5 * HZ(i, j, k) * (A2(S->fomn, i, j));
+      /* compute_horiz_rhs_uv_terms.h:4-12: CURVGRID && UV_ADV adds the curvature terms */
+      const double cff = S->c.curvgrid
+                             ? 0.5 * HZ(i, j, k) *
+                                   (A2(S->fomn, i, j) + 0.5 * ((V(i, j, k, nr) + V(i, j + 1, k, nr)) * A2(S->dndx, i, j) -
+                                                               (U(i, j, k, nr) + U(i + 1, j, k, nr)) * A2(S->dmde, i, j)))
+                             : 0.5 * HZ(i, j, k) * (A2(S->fomn, i, j));
       A2(UFx, i, j) = cff * (V(i, j, k, nr) + V(i, j + 1, k, nr));
       A2(VFe, i, j) = cff * (U(i, j, k, nr) + U(i + 1, j, k, nr));
     }

@@ -46,6 +46,7 @@ typedef struct or_cfg {
   double ubind;                  /* OBC binding velocity [m/s] (read_inp_mod.F:809) */
   double v_sponge;               /* SPONGE viscosity/diffusivity [m2/s] (set_nudgcof.F:25-111) */
   int island;                    /* basin: circular land mask (MASKING) */
+  int curvgrid;                  /* CURVGRID (+UV_ADV) curvature terms; basin: non-uniform metrics */
 } or_cfg;
 
 typedef struct or_state or_state;

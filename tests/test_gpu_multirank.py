@@ -94,7 +94,7 @@ EXCHANGED = ("zeta", "ubar", "vbar", "u", "v", "t", "FlxU", "FlxV", "We", "Wi", 
 LMD_FIELDS = ("Akv", "Akt", "hbls", "hbbl", "ghat", "swr_frac")
 
 
-@pytest.mark.parametrize("kind", ["filament", "basin", "basin_lmd", "basin_flux", "pipes", "basin_obc"])
+@pytest.mark.parametrize("kind", ["filament", "basin", "basin_lmd", "basin_flux", "pipes"])
 @pytest.mark.parametrize("npx,npe", [(2, 1), (1, 2), (2, 2), (3, 2)])
 def test_decomposition_bitwise_equals_single_domain(kind, npx, npe):
     case = _case(kind)

@@ -27,9 +27,9 @@ pytestmark = pytest.mark.gpu
 BRY = ["%s_%s" % (v, e) for v in ("zeta", "ubar", "vbar", "u", "v", "t") for e in ("west", "east", "south", "north")]
 
 
-def obc_cfg(obc=15, sponge=1.0, island=1, lmd=0, **kw):
+def obc_cfg(obc=15, sponge=1.0, island=1, lmd=0, curv=0, **kw):
     c = basin_cfg(nonlin=True, **kw)
-    c.obc, c.ubind, c.v_sponge, c.island, c.lmd = obc, 0.1, sponge, island, lmd
+    c.obc, c.ubind, c.v_sponge, c.island, c.lmd, c.curvgrid = obc, 0.1, sponge, island, lmd, curv
     return c
 
 
@@ -39,7 +39,7 @@ def make_pair(cfg):
     m = romsgpu.Model.from_case(cfg.case_id, cfg.LLm, cfg.MMm, cfg.N, cfg.NT, salinity=bool(cfg.salinity),
                                 nonlin_eos=bool(cfg.nonlin_eos), dt=cfg.dt, ndtfast=cfg.ndtfast, sizex=cfg.sizex,
                                 sizey=cfg.sizey, lmd=bool(cfg.lmd), obc=cfg.obc, v_sponge=cfg.v_sponge,
-                                island=bool(cfg.island))
+                                island=bool(cfg.island), curvgrid=bool(cfg.curvgrid))
     return o, m
 
 
@@ -92,9 +92,41 @@ def test_open_boundary_routine_parity(routine, obc):
     m.close()
 
 
-@pytest.mark.parametrize("lmd", [0, 1])
-def test_open_basin_30_steps_rms(lmd):
-    cfg = obc_cfg(lmd=lmd)
+@pytest.mark.parametrize("routine", ["pre_step3d", "step3d_uv1"])
+def test_curvgrid_momentum_rhs_parity(routine):
+    """CURVGRID curvature terms in the momentum r.h.s. (compute_horiz_rhs_uv_terms.h:4-12)
+    on non-uniform metrics; ru/rv carry them into u,v(nnew)."""
+    cfg = obc_cfg(curv=1)
+    o, m = make_pair(cfg)
+    assert float(np.max(np.abs(o.field("dndx")))) > 0.0 and float(np.max(np.abs(o.field("dmde")))) > 0.0
+    bad = [(n, full(m.get(n), o.field(n))) for n in ("dndx", "dmde", "pm", "pn")]
+    assert all(e == 0.0 for _, e in bad), bad
+    o.step(3)
+    iic, kstp, knew, nstp, nrhs, nnew = o.tindex()
+    if routine == "pre_step3d":
+        nrhs, nnew = nstp, 3
+        o.set_tindex([iic, kstp, knew, nstp, nrhs, nnew])
+        copy_state(o, m)
+        m.set_tindex(iic, kstp, knew, nstp, nrhs, nnew, nfast=o.nfast())
+        o.call("prsgrd"); m.prsgrd()
+    else:
+        nrhs, nnew = 3, 3 - nstp
+        o.set_tindex([iic, kstp, knew, nstp, nrhs, nnew])
+        copy_state(o, m)
+        m.set_tindex(iic, kstp, knew, nstp, nrhs, nnew, nfast=o.nfast())
+        o.call("prsgrd"); m.prsgrd()
+    o.call(routine)
+    getattr(m, routine)()
+    m.sync()
+    check_fields(o, m, ["u", "v", "rufrc", "rvfrc"] if routine == "step3d_uv1" else ["u", "v", "t"], cfg.LLm,
+                 cfg.MMm, RTOL_ROUTINE)
+    m.close()
+
+
+@pytest.mark.parametrize("lmd,curv", [(0, 0), (1, 0), (1, 1)])
+def test_open_basin_30_steps_rms(lmd, curv):
+    """(1, 1) is the Iceland switch set: OBC + SPONGE + MASKING + CURVGRID + LMD/KPP + NONLIN/SPLIT EOS."""
+    cfg = obc_cfg(lmd=lmd, curv=curv)
     o, m = make_pair(cfg)
     o.step(30)
     m.step(30)
@@ -106,3 +138,11 @@ def test_open_basin_30_steps_rms(lmd):
         a, b = m.get(n), o.field(n)
         assert float(np.sqrt(np.mean((a - b) ** 2))) / max(1.0, float(np.sqrt(np.mean(b ** 2)))) < RMS_RUN, n
     m.close()
+
+
+@pytest.mark.parametrize("npx,npe", [(2, 1), (1, 2), (2, 2), (3, 2)])
+def test_open_basin_decomposition_bitwise(npx, npe):
+    """Open edges + island on a processor grid equal the single domain bitwise
+    (no sponge: the reference sets its bands on each rank's own points only)."""
+    from test_gpu_multirank import test_decomposition_bitwise_equals_single_domain as run
+    run("basin_obc", npx, npe)

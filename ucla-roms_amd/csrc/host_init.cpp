@@ -233,6 +233,11 @@ void build_case(const CaseSpec& cs, HostState& H, double& area, double& volume) 
         const double x = dx * ((double)(i + cs.iSW_corn) - 0.5), y = dy * ((double)(j + cs.jSW_corn) - 0.5);
         A(kxr, i, j) = x; A(kyr, i, j) = y;
         A(kpm, i, j) = 1.0 / dx; A(kpn, i, j) = 1.0 / dy;
+        if (cs.curvgrid) {  // non-uniform metrics (oracle_main.c or_ana_grid): m varies along eta, n along xi
+          const double pi = 3.14159265358979323;
+          A(kpm, i, j) = (1.0 + 0.1 * std::sin(2.0 * pi * ((double)(j + cs.jSW_corn) - 0.5) / (double)cs.MMm)) / dx;
+          A(kpn, i, j) = (1.0 + 0.1 * std::cos(2.0 * pi * ((double)(i + cs.iSW_corn) - 0.5) / (double)cs.LLm)) / dy;
+        }
         A(kf, i, j) = 1.0e-4;
         const double rx = x - 0.5 * cs.sizex, ry = y - 0.5 * cs.sizey;
         double s = 1.0 - (rx * rx + ry * ry) / (R * R);
@@ -283,7 +288,15 @@ void build_case(const CaseSpec& cs, HostState& H, double& area, double& volume) 
       else if (n == 2 && ((a && c) || (b && d) || (a && b) || (c && d))) pmk = 2.0;
       A(kpmask, i, j) = pmk;
     }
-  for (int id : {kdm_r, kdn_r, kdm_p, kdn_p, kdm_u, kdn_u, kdm_v, kdn_v, kpmon_u, kpnom_v, krmask, kumask, kvmask, kpmask})
+  alloc(kdndx, n2); alloc(kdmde, n2);
+  if (cs.curvgrid) {  // setup_grid1.F:89-103 (exchanged below / by the device exchange)
+    for (int j = jstrR; j <= jendR; j++)
+      for (int i = istr; i <= iend; i++) A(kdndx, i, j) = 0.5 / A(kpn, i + 1, j) - 0.5 / A(kpn, i - 1, j);
+    for (int j = jstr; j <= jend; j++)
+      for (int i = istrR; i <= iendR; i++) A(kdmde, i, j) = 0.5 / A(kpm, i, j + 1) - 0.5 / A(kpm, i, j - 1);
+  }
+  for (int id : {kdm_r, kdn_r, kdm_p, kdn_p, kdm_u, kdn_u, kdm_v, kdn_v, kpmon_u, kpnom_v, krmask, kumask, kvmask, kpmask,
+                 kdndx, kdmde})
     wrap(H, H.arr[id].data(), 1, ewp, nsp);
   // setup_grid2: area/volume (single-rank pairwise sums)
   {

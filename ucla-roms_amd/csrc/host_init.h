@@ -15,7 +15,7 @@ enum HostId : int {
   kubar = ROMS_ubar, kvbar = ROMS_vbar, ku = ROMS_u, kv = ROMS_v, kt = ROMS_t, kHz = ROMS_Hz, kz_r = ROMS_z_r,
   kz_w = ROMS_z_w, kAkv = ROMS_Akv, kAkt = ROMS_Akt, kvisc2_r = ROMS_visc2_r, kvisc2_p = ROMS_visc2_p,
   kdiff2 = ROMS_diff2, ksustr = ROMS_sustr, ksvstr = ROMS_svstr, kstflx = ROMS_stflx, ksrflx = ROMS_srflx,
-  kswflx = ROMS_swflx,
+  kswflx = ROMS_swflx, kdndx = ROMS_dndx, kdmde = ROMS_dmde,
   kxr = ROMS_NFIELDS, kyr, kNHost
 };
 
@@ -38,6 +38,7 @@ struct CaseSpec {
   int ew_periodic, ns_periodic, west_exchng, east_exchng, south_exchng, north_exchng;
   int salinity, lmd, surf_flux;
   int obc, island;   // open edges (bitmask), circular land mask
+  int curvgrid;      // non-uniform metrics + dndx/dmde
   double v_sponge;   // set_nudgcof.F sponge
   int host_wrap;  // apply periodic halo wraps on the host (single rank)
   double theta_s, theta_b, hc, rho0, Tcoef, visc2, tnu2, Akv_bak, Akt_bak[2];

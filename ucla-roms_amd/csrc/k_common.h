@@ -374,10 +374,19 @@ __device__ __forceinline__ void uv_horiz_rhs(const Dev& d, const A& a, int i, in
   const Fields& F = d.f;
   const long kk = (long)(k - 1) * b.n2;
   const long o = IJ(b, i, j) + kk;
+  // Coriolis factor cff = 0.5*Hz*fomn at rho point (m,n), plus the CURVGRID
+  // curvature terms (compute_horiz_rhs_uv_terms.h:4-12)
+  auto cor = [&](int m, int n, long oo) {
+    const long mn = IJ(b, m, n);
+    if (d.p.curvgrid)
+      return 0.5 * F.Hz[oo] *
+             (F.fomn[mn] + 0.5 * ((a.v(m, n) + a.v(m, n + 1)) * F.dndx[mn] - (a.u(m, n) + a.u(m + 1, n)) * F.dmde[mn]));
+    return 0.5 * F.Hz[oo] * (F.fomn[mn]);
+  };
   if (i >= b.istrU && i <= b.iend && j >= b.jstr && j <= b.jend) {
-    // Coriolis UFx at i and i-1: cff=0.5*Hz*fomn; UFx=cff*(v(j)+v(j+1))
-    const double c0 = 0.5 * F.Hz[o] * (F.fomn[IJ(b, i, j)]);
-    const double c1 = 0.5 * F.Hz[o - 1] * (F.fomn[IJ(b, i - 1, j)]);
+    // Coriolis UFx at i and i-1: UFx=cff*(v(j)+v(j+1))
+    const double c0 = cor(i, j, o);
+    const double c1 = cor(i - 1, j, o - 1);
     const double U0 = c0 * (a.v(i, j) + a.v(i, j + 1)), U1 = c1 * (a.v(i - 1, j) + a.v(i - 1, j + 1));
     double ru = F.ru[o] + 0.5 * (U0 + U1);
     ru = ru - adv_UFx(a, i, j, r, up) + adv_UFx(a, i - 1, j, r, up) - adv_UFe(a, i, j + 1, r, up) +
@@ -385,8 +394,8 @@ __device__ __forceinline__ void uv_horiz_rhs(const Dev& d, const A& a, int i, in
     F.ru[o] = ru;
   }
   if (i >= b.istr && i <= b.iend && j >= b.jstrV && j <= b.jend) {
-    const double c0 = 0.5 * F.Hz[o] * (F.fomn[IJ(b, i, j)]);
-    const double c1 = 0.5 * F.Hz[o - b.nx2] * (F.fomn[IJ(b, i, j - 1)]);
+    const double c0 = cor(i, j, o);
+    const double c1 = cor(i, j - 1, o - b.nx2);
     const double V0 = c0 * (a.u(i, j) + a.u(i + 1, j)), V1 = c1 * (a.u(i, j - 1) + a.u(i + 1, j - 1));
     double rv = F.rv[o] - 0.5 * (V0 + V1);
     rv = rv - adv_VFx(a, i + 1, j, r, up) + adv_VFx(a, i, j, r, up) - adv_VFe(a, i, j, r, up) +

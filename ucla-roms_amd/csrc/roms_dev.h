@@ -33,6 +33,7 @@ struct Params {
   int nonlin_eos, salinity, lmd, uv_vis2, ts_dif2;
   int s2d_split;  // 1: step2d as separate zeta / momentum kernels (ROMS_GPU_S2D_SPLIT=1)
   int npip;       // pipe_frc.F: number of pipes (0: pipe_source off)
+  int curvgrid;   // CURVGRID && UV_ADV: curvature terms (compute_horiz_rhs_uv_terms.h:8-11)
   int obc;        // open edges: 1 W, 2 E, 4 S, 8 N (Flather / Orlanski + *_FRC_BRY)
   double ubind;   // OBC binding velocity
   double dt, dtfast, g, rho0, vonKar, qp2, gamma2, hc;
@@ -45,6 +46,7 @@ struct Fields {
   // grid (grid.F)
   double *h, *hinv, *f, *fomn, *pm, *pn, *dm_r, *dn_r, *dm_u, *dn_u, *dm_v, *dn_v, *dm_p, *dn_p,
       *pmon_u, *pnom_v, *rmask, *pmask, *umask, *vmask;
+  double *dndx, *dmde;  // CURVGRID metric derivatives
   double *Cs_w, *Cs_r;  // scoord.F (N+1)
   // ocean vars
   double *zeta, *ubar, *vbar, *u, *v, *t;

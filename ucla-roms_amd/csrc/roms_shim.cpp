@@ -174,6 +174,7 @@ double** field_slot(Fields& F, int id) {
     case ROMS_swr_frac: return &F.swr_frac; case ROMS_sustr: return &F.sustr; case ROMS_svstr: return &F.svstr;
     case ROMS_stflx: return &F.stflx; case ROMS_srflx: return &F.srflx; case ROMS_swflx: return &F.swflx;
     case ROMS_ru: return &F.ru; case ROMS_rv: return &F.rv;
+    case ROMS_dndx: return &F.dndx; case ROMS_dmde: return &F.dmde;
     default: break;
   }
   if (id >= ROMS_zeta_west && id <= ROMS_t_north) {
@@ -299,6 +300,7 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
   if (cfg->obc < 0 || cfg->obc > 15) { g.err = "roms_gpu_init: obc must be a 4-bit edge mask"; return -1; }
   P.obc = cfg->obc & ((dims->ew_periodic ? 0 : 3) | (dims->ns_periodic ? 0 : 12));
   P.ubind = cfg->ubind;
+  P.curvgrid = cfg->curvgrid;
   if (P.obc) P.s2d_split = 1;  // open edges: separate zeta / zetabc / momentum kernels (step2d)
   for (int i = 0; i < kMaxFast; i++) { g.w1[i] = cfg->weight[0][i]; g.w2[i] = cfg->weight[1][i]; }
   // column-solver scratch: LDS while two (N+1)-level slots per wave fit the
@@ -574,6 +576,7 @@ static int init_case_impl(const roms_case* c, int np_xi, int np_eta, void* comm,
   // tests/Pipes_ana/benchmark.in has no vertical_mixing line: Akv_bak = Akt_bak = 0
   C.obc = c->case_id == ROMS_CASE_BASIN ? c->obc : 0;
   C.ubind = 0.1;  // Examples/Iceland/Iceland_parent/roms.in: ubind
+  C.curvgrid = c->case_id == ROMS_CASE_BASIN ? c->curvgrid : 0;
   C.Akv_bak = (fil || pipes) ? 0.0 : 1.0e-4; C.Akt_bak[0] = (fil || pipes) ? 0.0 : 1.0e-5; C.Akt_bak[1] = C.Akt_bak[0];
   int r = roms_gpu_init(&D, &C, device, comm);
   if (r) return r;
@@ -590,6 +593,7 @@ static int init_case_impl(const roms_case* c, int np_xi, int np_eta, void* comm,
   cs.sizex = c->sizex; cs.sizey = c->sizey;
   cs.obc = C.obc; cs.island = c->case_id == ROMS_CASE_BASIN ? c->island : 0;
   cs.v_sponge = C.obc ? c->v_sponge : 0.0;
+  cs.curvgrid = C.curvgrid;
   HostState H(D.Lm, D.Mm, D.N, D.NT, C.salinity ? 2 : 1);
   double area = 0.0, volume = 0.0;
   build_case(cs, H, area, volume);
@@ -616,7 +620,8 @@ static int init_case_impl(const roms_case* c, int np_xi, int np_eta, void* comm,
     // the exchanges of setup_grid1.F and ana_init (host wrap in the single-rank build)
     const Fields& F = g.d.f;
     const ExchList grid1{{F.dm_r, F.dn_r, F.dm_p, F.dn_p, F.dm_u, F.dn_u, F.dm_v, F.dn_v}, {1, 1, 1, 1, 1, 1, 1, 1}, 8};
-    const ExchList grid2{{F.pmon_u, F.pnom_v, F.rmask, F.umask, F.vmask, F.pmask}, {1, 1, 1, 1, 1, 1}, 6};
+    const ExchList grid2{{F.pmon_u, F.pnom_v, F.rmask, F.umask, F.vmask, F.pmask, F.dndx, F.dmde},
+                         {1, 1, 1, 1, 1, 1, 1, 1}, 8};
     const ExchList st{{F.zeta, F.ubar, F.vbar, F.u, F.v}, {1, 1, 1, D.N, D.N}, 5};
     launch_exchange_list(g.d, g.s, grid1);
     launch_exchange_list(g.d, g.s, grid2);

@@ -24,7 +24,8 @@ FIELDS = ["h", "hinv", "f", "fomn", "pm", "pn", "dm_r", "dn_r", "dm_u", "dn_u", 
           "rufrc", "rvfrc", "rhoA", "rhoS", "r_D", "Zt_avg1", "DU_avg1", "DV_avg1", "DU_avg2", "DV_avg2",
           "DU_avg_bak", "DV_avg_bak", "rho", "rho1", "qp1", "bvf", "Akv", "Akt", "visc2_r", "visc2_p", "diff2",
           "hbls", "hbbl", "ghat", "swr_frac", "sustr", "svstr", "stflx", "srflx", "swflx", "ru", "rv"] + \
-         ["%s_%s" % (v, e) for v in ("zeta", "ubar", "vbar", "u", "v", "t") for e in ("west", "east", "south", "north")]
+         ["%s_%s" % (v, e) for v in ("zeta", "ubar", "vbar", "u", "v", "t") for e in ("west", "east", "south", "north")] + \
+         ["dndx", "dmde"]
 FIELD_ID = {n: i for i, n in enumerate(FIELDS)}
 CASE_FILAMENT, CASE_BASIN, CASE_PIPES = 0, 1, 2
 
@@ -44,7 +45,7 @@ class Cfg(ctypes.Structure):
                 ("Akv_bak", ctypes.c_double), ("Akt_bak", ctypes.c_double * 2), ("Tcoef", ctypes.c_double),
                 ("T0", ctypes.c_double), ("Scoef", ctypes.c_double), ("S0", ctypes.c_double),
                 ("theta_s", ctypes.c_double), ("theta_b", ctypes.c_double), ("hc", ctypes.c_double),
-                ("obc", ctypes.c_int), ("ubind", ctypes.c_double)]
+                ("obc", ctypes.c_int), ("ubind", ctypes.c_double), ("curvgrid", ctypes.c_int)]
 
 
 class Tlev(ctypes.Structure):
@@ -60,7 +61,8 @@ class Case(ctypes.Structure):
                 ("NT", ctypes.c_int), ("salinity", ctypes.c_int), ("nonlin_eos", ctypes.c_int),
                 ("lmd_mixing", ctypes.c_int), ("dt", ctypes.c_double), ("ndtfast", ctypes.c_int),
                 ("sizex", ctypes.c_double), ("sizey", ctypes.c_double), ("surf_flux", ctypes.c_int),
-                ("obc", ctypes.c_int), ("v_sponge", ctypes.c_double), ("island", ctypes.c_int)]
+                ("obc", ctypes.c_int), ("v_sponge", ctypes.c_double), ("island", ctypes.c_int),
+                ("curvgrid", ctypes.c_int)]
 
 
 ROUTINES_T = ["set_huv", "omega", "prsgrd", "pre_step3d", "set_huv1", "step3d_uv1", "visc3d", "step2d",
@@ -209,12 +211,12 @@ class Model:
     @classmethod
     def from_case(cls, case_id, LLm, MMm, N, NT=1, salinity=False, nonlin_eos=False, dt=5.0, ndtfast=60,
                   sizex=12.8e3, sizey=3.2e3, device=0, np_xi=1, np_eta=1, comm=None, rank=0, lmd=False,
-                  surf_flux=False, obc=0, v_sponge=0.0, island=False):
+                  surf_flux=False, obc=0, v_sponge=0.0, island=False, curvgrid=False):
         """Analytic case on the whole grid, or on subdomain `rank` of an
         np_xi x np_eta processor grid when a communicator is given."""
         m = cls()
         c = Case(case_id, LLm, MMm, N, NT, int(salinity), int(nonlin_eos), int(lmd), dt, ndtfast, sizex, sizey,
-                 int(surf_flux), int(obc), float(v_sponge), int(island))
+                 int(surf_flux), int(obc), float(v_sponge), int(island), int(curvgrid))
         if comm is None and np_xi * np_eta == 1:
             m._chk(m.L.roms_gpu_init_case(ctypes.byref(c), device, ctypes.byref(m.t)), "roms_gpu_init_case")
         else:
