@@ -346,8 +346,10 @@ void build_case(const CaseSpec& cs, HostState& H, double& area, double& volume) 
   const double hc = cs.hc, ds = 1.0 / (double)N;
   const double* Cs_w = H.arr[kCs_w].data();
   const double* Cs_r = H.arr[kCs_r].data();
-  for (int j = -1; j <= Mm + 2; j++)
-    for (int i = -1; i <= Lm + 2; i++) {
+  // istrR..iendR plus the halo the exchange fills (set_depth.F:72-90 and its
+  // exchange): on a physical non-periodic edge the outer ghost stays zero
+  for (int j = se ? jstrR : -1; j <= (ne ? jendR : Mm + 2); j++)
+    for (int i = we ? istrR : -1; i <= (ee ? iendR : Lm + 2); i++) {
       const double hh = A(kh, i, j), hi = 1.0 / (hh + hc), z = 0.0;
       W3(kz_w, i, j, 0) = -hh;
       for (int k = 1; k <= N; k++) {
