@@ -134,80 +134,133 @@ __device__ __forceinline__ void visc_psi(const Dev& d, int i, int j, int k, int 
   VFx = cff * F.dn_p[ij] * F.dn_p[ij];
 }
 
-// per cell (i,j,k): stress divergence cff added as dt*cff to u,v(indx); cff
-// kept in column scratch (c0: u, c1: v) for the vertical sums below.  The
-// block first evaluates each rho-point (UFx,VFe) and psi-point (UFe,VFx)
-// stress of its 64x4 tile once into LDS (rho points with a low-side, psi
-// points with a high-side halo), then forms the divergences.
-constexpr int kVW = kBX + 1, kVN = kVW * (kBY + 1);
+// Whole-column tiles: a block owns a 64x4 tile of (i,j) for all levels
+// k = 1..N.  The 2-D metric factors of every stress point and divergence
+// point are formed once per block (registers) instead of once per level,
+// and each lane sums its own stress divergence over k in the reference's
+// k = 1..N order, so rufrc/rvfrc need no column scratch or second kernel.
+// Per level, the rho-point (UFx,VFe) and psi-point (UFe,VFx) stresses of
+// the tile (rho points with a low-side, psi points with a high-side halo)
+// are evaluated once into LDS, then each lane forms its divergences.
+// Operation order is the reference's (visc3d_S.F:60-136), so results are
+// bit-identical to the per-level form.
+constexpr int kVW = kBX + 1, kVN = kVW * (kBY + 1), kVQ = (kVN + kBX * kBY - 1) / (kBX * kBY);
+struct ViscRho {  // metric factors of one rho point
+  double v2, X, sx1, sx0, Y, sy1, sy0, dn, dm;
+  long ij;
+  bool on;
+};
+struct ViscPsi {  // metric factors of one psi point
+  double v2, P1, P2, a1, a0, b1, b0, msk, dm, dn;
+  long ij;
+  bool on;
+};
 __global__ void __launch_bounds__(256) k_visc3d(Dev d, Range R, int nstp) {
   __shared__ double sUFx[kVN], sVFe[kVN], sUFe[kVN], sVFx[kVN];
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const int indx = 3 - nstp;
-  const int k = 1 + (int)blockIdx.z;
   const int i0 = R.i0 + (int)blockIdx.x * kBX, j0 = R.j0 + (int)blockIdx.y * kBY;
-  for (int q = threadIdx.x + kBX * threadIdx.y; q < kVN; q += kBX * kBY) {
-    const int li = q % kVW, lj = q / kVW;
-    const int ir = i0 - 1 + li, jr = j0 - 1 + lj;  // rho point
-    double ufx = 0.0, vfe = 0.0, ufe = 0.0, vfx = 0.0;
-    if (ir >= 0 && ir <= b.Lm + 1 && jr >= 0 && jr <= b.Mm + 1) visc_rho(d, ir, jr, k, nstp, ufx, vfe);
-    const int ip = i0 + li, jp = j0 + lj;          // psi point
-    if (ip >= 0 && ip <= b.Lm + 2 && jp >= 0 && jp <= b.Mm + 2) visc_psi(d, ip, jp, k, nstp, ufe, vfx);
-    sUFx[q] = ufx; sVFe[q] = vfe; sUFe[q] = ufe; sVFx[q] = vfx;
-  }
-  __syncthreads();
-  const int i = i0 + (int)threadIdx.x, j = j0 + (int)threadIdx.y;
-  if (i > R.i1 || j > R.j1) return;
-  const int qr = (threadIdx.x + 1) + (threadIdx.y + 1) * kVW;  // rho (i,j); -1: (i-1,j); -kVW: (i,j-1)
-  const int qp = threadIdx.x + threadIdx.y * kVW;              // psi (i,j); +1: (i+1,j); +kVW: (i,j+1)
-  const long ij = IJ(b, i, j), sj = b.nx2;
+  const long sj = b.nx2;
   const double* pm = F.pm;
   const double* pn = F.pn;
-  const long o = ij + (long)(k - 1) * b.n2;
-  if (i >= b.istrU && i <= b.iend) {
-    const double UFx0 = sUFx[qr], UFx1 = sUFx[qr - 1], UFe0 = sUFe[qp], UFe1 = sUFe[qp + kVW];
-    const double cff = 0.125 * (pm[ij - 1] + pm[ij]) * (pn[ij - 1] + pn[ij]) *
-                       ((pn[ij - 1] + pn[ij]) * (UFx0 - UFx1) + (pm[ij - 1] + pm[ij]) * (UFe1 - UFe0));
-    F.c0[o] = cff;
-    F.u[o + (long)(indx - 1) * b.n3] = F.u[o + (long)(indx - 1) * b.n3] + d.p.dt * cff;
+  const int tid = threadIdx.x + kBX * threadIdx.y;
+  ViscRho gr[kVQ];
+  ViscPsi gp[kVQ];
+#pragma unroll
+  for (int m = 0; m < kVQ; m++) {
+    const int q = tid + m * kBX * kBY;
+    const int li = q % kVW, lj = q / kVW;
+    const int ir = i0 - 1 + li, jr = j0 - 1 + lj;  // rho point
+    ViscRho& r = gr[m];
+    r.on = q < kVN && ir >= 0 && ir <= b.Lm + 1 && jr >= 0 && jr <= b.Mm + 1;
+    r.ij = IJ(b, ir, jr);
+    if (r.on) {
+      const long ij = r.ij;
+      r.v2 = F.visc2_r[ij];
+      r.X = F.dn_r[ij] * pm[ij]; r.sx1 = pn[ij] + pn[ij + 1]; r.sx0 = pn[ij - 1] + pn[ij];
+      r.Y = F.dm_r[ij] * pn[ij]; r.sy1 = pm[ij] + pm[ij + sj]; r.sy0 = pm[ij - sj] + pm[ij];
+      r.dn = F.dn_r[ij]; r.dm = F.dm_r[ij];
+    }
+    const int ip = i0 + li, jp = j0 + lj;  // psi point
+    ViscPsi& p = gp[m];
+    p.on = q < kVN && ip >= 0 && ip <= b.Lm + 2 && jp >= 0 && jp <= b.Mm + 2;
+    p.ij = IJ(b, ip, jp);
+    if (p.on) {
+      const long ij = p.ij;
+      p.v2 = F.visc2_p[ij];
+      p.P1 = 0.25 * (pm[ij - 1] + pm[ij] + pm[ij - 1 - sj] + pm[ij - sj]) * F.dn_p[ij];
+      p.a1 = pn[ij - sj] + pn[ij]; p.a0 = pn[ij - 1 - sj] + pn[ij - 1];
+      p.P2 = 0.25 * (pn[ij - 1] + pn[ij] + pn[ij - 1 - sj] + pn[ij - sj]) * F.dm_p[ij];
+      p.b1 = pm[ij - 1] + pm[ij]; p.b0 = pm[ij - 1 - sj] + pm[ij - sj];
+      p.msk = F.pmask[ij]; p.dm = F.dm_p[ij]; p.dn = F.dn_p[ij];
+    }
   }
-  if (j >= b.jstrV && j <= b.jend) {
-    const double VFe0 = sVFe[qr], VFe1 = sVFe[qr - kVW], VFx0 = sVFx[qp], VFx1 = sVFx[qp + 1];
-    const double cff = 0.125 * (pm[ij] + pm[ij - sj]) * (pn[ij] + pn[ij - sj]) *
-                       ((pn[ij - sj] + pn[ij]) * (VFx1 - VFx0) + (pm[ij - sj] + pm[ij]) * (VFe0 - VFe1));
-    F.c1[o] = cff;
-    F.v[o + (long)(indx - 1) * b.n3] = F.v[o + (long)(indx - 1) * b.n3] + d.p.dt * cff;
+  const int i = i0 + (int)threadIdx.x, j = j0 + (int)threadIdx.y;
+  const bool act = i <= R.i1 && j <= R.j1;
+  const long ij = IJ(b, i, j);
+  const bool du = act && i >= b.istrU && i <= b.iend, dv = act && j >= b.jstrV && j <= b.jend;
+  double cum = 0.0, cun = 0.0, cvm = 0.0, cvn = 0.0, fu = 0.0, fv = 0.0;
+  if (du) { cum = pm[ij - 1] + pm[ij]; cun = pn[ij - 1] + pn[ij]; fu = F.rufrc[ij]; }
+  if (dv) { cvm = pm[ij] + pm[ij - sj]; cvn = pn[ij] + pn[ij - sj]; fv = F.rvfrc[ij]; }
+  const double cu0 = 0.125 * cum * cun, cv0 = 0.125 * cvm * cvn;
+  const double* U = F.u + (long)(nstp - 1) * b.n3;
+  const double* V = F.v + (long)(nstp - 1) * b.n3;
+  double* Ui = F.u + (long)(indx - 1) * b.n3;
+  double* Vi = F.v + (long)(indx - 1) * b.n3;
+  const int qr = (threadIdx.x + 1) + (threadIdx.y + 1) * kVW;  // rho (i,j); -1: (i-1,j); -kVW: (i,j-1)
+  const int qp = threadIdx.x + threadIdx.y * kVW;              // psi (i,j); +1: (i+1,j); +kVW: (i,j+1)
+  for (int k = 1; k <= b.N; k++) {
+    const long kk = (long)(k - 1) * b.n2;
+    const double* Hk = F.Hz + kk;
+    const double* Uk = U + kk;
+    const double* Vk = V + kk;
+    if (k > 1) __syncthreads();  // previous level's stresses consumed
+#pragma unroll
+    for (int m = 0; m < kVQ; m++) {
+      const int q = tid + m * kBX * kBY;
+      if (q >= kVN) break;
+      double ufx = 0.0, vfe = 0.0, ufe = 0.0, vfx = 0.0;
+      const ViscRho& r = gr[m];
+      if (r.on) {
+        const long o = r.ij;
+        const double cff = 0.5 * Hk[o] * r.v2 * (r.X * (r.sx1 * Uk[o + 1] - r.sx0 * Uk[o]) -
+                                                 r.Y * (r.sy1 * Vk[o + sj] - r.sy0 * Vk[o]));
+        ufx = cff * r.dn * r.dn;
+        vfe = -cff * r.dm * r.dm;
+      }
+      const ViscPsi& p = gp[m];
+      if (p.on) {
+        const long o = p.ij;
+        const double cff = 0.125 * (Hk[o - 1] + Hk[o] + Hk[o - 1 - sj] + Hk[o - sj]) * p.v2 *
+                           (p.P1 * (p.a1 * Vk[o] - p.a0 * Vk[o - 1]) + p.P2 * (p.b1 * Uk[o] - p.b0 * Uk[o - sj])) *
+                           p.msk;
+        ufe = cff * p.dm * p.dm;
+        vfx = cff * p.dn * p.dn;
+      }
+      sUFx[q] = ufx; sVFe[q] = vfe; sUFe[q] = ufe; sVFx[q] = vfx;
+    }
+    __syncthreads();
+    const long o = ij + kk;
+    if (du) {
+      const double cff = cu0 * (cun * (sUFx[qr] - sUFx[qr - 1]) + cum * (sUFe[qp + kVW] - sUFe[qp]));
+      Ui[o] = Ui[o] + d.p.dt * cff;
+      fu = fu + cff;
+    }
+    if (dv) {
+      const double cff = cv0 * (cvn * (sVFx[qp + 1] - sVFx[qp]) + cvm * (sVFe[qr] - sVFe[qr - kVW]));
+      Vi[o] = Vi[o] + d.p.dt * cff;
+      fv = fv + cff;
+    }
   }
-}
-
-// rufrc/rvfrc += sum_k cff(k), summed in the reference's k = 1..N order
-__global__ void __launch_bounds__(256) k_visc3d_frc(Dev d, Range R) {
-  ROMS_IJ_OR_RETURN(R)
-  const Bounds& b = d.b;
-  const Fields& F = d.f;
-  const long ij = IJ(b, i, j), n2 = b.n2;
-  if (i >= b.istrU && i <= b.iend) {
-    const double* __restrict__ cu = F.c0 + ij;
-    double frc = F.rufrc[ij];
-#pragma unroll 8
-    for (int k = 1; k <= b.N; k++) frc = frc + cu[(long)(k - 1) * n2];
-    F.rufrc[ij] = frc;
-  }
-  if (j >= b.jstrV && j <= b.jend) {
-    const double* __restrict__ cv = F.c1 + ij;
-    double frc = F.rvfrc[ij];
-#pragma unroll 8
-    for (int k = 1; k <= b.N; k++) frc = frc + cv[(long)(k - 1) * n2];
-    F.rvfrc[ij] = frc;
-  }
+  if (du) F.rufrc[ij] = fu;
+  if (dv) F.rvfrc[ij] = fv;
 }
 
 void launch_visc3d(const Dev& d, hipStream_t s, const Tlev& t) {
   const Bounds& b = d.b;
   Range R{b.istr, b.iend, b.jstr, b.jend};
-  hipLaunchKernelGGL(k_visc3d, grid3_of(R, b.N), dim3(kBX, kBY), 0, s, d, R, t.nstp);
-  hipLaunchKernelGGL(k_visc3d_frc, grid_of(R), dim3(kBX, kBY), 0, s, d, R);
+  hipLaunchKernelGGL(k_visc3d, grid_of(R), dim3(kBX, kBY), 0, s, d, R, t.nstp);
 }
 
 // ---- step3d_uv2 part 1: convert Hz*u to u and remove the mismatch against
