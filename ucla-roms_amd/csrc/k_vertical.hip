@@ -162,43 +162,41 @@ __global__ void __launch_bounds__(256) k_omega(Dev d, Range R, double dtau) {
   double* __restrict__ Wi = F.Wi + ij;
   double* __restrict__ We = F.We + ij;
   auto cx = [&](long o) { return fmax0(FU[o + 1]) - fmin0(FU[o]) + fmax0(FV[o + sj]) - fmin0(FV[o]); };
-  double wi = 0.0;
-  Wi[0] = 0.0;
-  // pipe sources enter Wi level by level (omega.F:102-108)
+  // Two bottom-up passes over the column.  Pass 1 only forms the column
+  // total of the divergence (omega.F:95-110) for the grid-motion term; pass 2
+  // re-accumulates the same partial sums in the same order (bit-identical
+  // Wi(k)) and applies the Courant split level by level (omega.F:120-165),
+  // so Wi is never stored and re-read.  The split at level k needs
+  // CX(k), CX(k+1), Hz(k), Hz(k+1): one level of look-ahead.
   const int pidx = d.p.npip > 0 ? F.pipe_idx[ij] : 0;
-  if (pidx > 0) {
-    const double pflx = F.pipe_flx[ij];
-    const double* __restrict__ prf = F.pipe_prf + (pidx - 1);
-    for (int k = 1; k <= N; k++) {
-      const long o = (long)(k - 1) * n2;
-      wi = wi - FU[o + 1] + FU[o] - FV[o + sj] + FV[o];
-      wi = wi + pflx * prf[(long)(k - 1) * d.p.npip];
-      Wi[(long)k * n2] = wi;
-    }
-  } else {
+  const double pflx = pidx > 0 ? F.pipe_flx[ij] : 0.0;
+  const double* __restrict__ prf = pidx > 0 ? F.pipe_prf + (pidx - 1) : nullptr;
+  auto div = [&](int k, double wi) {  // wi - div(k) (+ pipe source), omega.F:102-108
+    const long o = (long)(k - 1) * n2;
+    wi = wi - FU[o + 1] + FU[o] - FV[o + sj] + FV[o];
+    if (pidx > 0) wi = wi + pflx * prf[(long)(k - 1) * d.p.npip];
+    return wi;
+  };
+  double wi = 0.0;
 #pragma unroll 8
-    for (int k = 1; k <= N; k++) {
-      const long o = (long)(k - 1) * n2;
-      wi = wi - FU[o + 1] + FU[o] - FV[o + sj] + FV[o];
-      Wi[(long)k * n2] = wi;
-    }
-  }
+  for (int k = 1; k <= N; k++) wi = div(k, wi);
   wi = wi + F.swflx[ij] * F.dm_r[ij] * F.dn_r[ij];
   const double zw0 = zw[0];
   const double wrk = wi / (zw[(long)N * n2] - zw0);
+  Wi[0] = 0.0;
+  We[0] = 0.0;
   Wi[(long)N * n2] = 0.0;
   We[(long)N * n2] = 0.0;
-  We[0] = 0.0;
   const double CX0 = dtau * F.pm[ij] * F.pn[ij];
-  double cx_up = cx((long)(N - 1) * n2);  // CX(k+1)
-  double hz_up = Hz[(long)(N - 1) * n2];
+  double cx_k = cx(0), hz_k = Hz[0];
+  wi = 0.0;
 #pragma unroll 8
-  for (int k = N - 1; k >= 1; k--) {
-    const long o = (long)(k - 1) * n2;
-    const long ow = (long)k * n2;
-    double w = Wi[ow] - wrk * (zw[ow] - zw0);
-    const double cx_k = cx(o);
-    const double hz_k = Hz[o];
+  for (int k = 1; k <= N - 1; k++) {
+    const long o1 = (long)k * n2;  // level k+1 (rho layout) == w-level k
+    wi = div(k, wi);
+    double w = wi - wrk * (zw[o1] - zw0);
+    const double cx_up = cx(o1);
+    const double hz_up = Hz[o1];
     const double c2d = dmax(cx_k, cx_up);
     const double dh = dmin(hz_k, hz_up);
     const double cw_max = cu_max * dh - c2d * CX0;
@@ -216,10 +214,10 @@ __global__ void __launch_bounds__(256) k_omega(Dev d, Range R, double dtau) {
     } else {
       we = 0.0;
     }
-    We[ow] = we;
-    Wi[ow] = w;
-    cx_up = cx_k;
-    hz_up = hz_k;
+    We[o1] = we;
+    Wi[o1] = w;
+    cx_k = cx_up;
+    hz_k = hz_up;
   }
 }
 
