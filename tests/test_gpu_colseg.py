@@ -1,0 +1,90 @@
+"""GPU parity of the segment-partitioned column solvers (k_colseg.h), which
+replace the sequential Thomas sweeps for deep grids (N > 32: the C2 and C3
+workloads).  Their elimination order differs from the reference's, so the
+bound is the north_star floating-point tolerance rather than bit equality:
+1e-12 relative per routine call, field RMS < 1e-10 over a run.
+
+Cases: the closed basin with nonlinear EOS at N = 50 (C2 depth) and with
+LMD/KPP + surface fluxes at N = 100 (C3 depth), on small horizontal grids so
+the oracle finishes in seconds.  Each routine is also compared with the
+library's own sequential path (ROMS_GPU_COLSEG=0) on the same state.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+import romsgpu
+from test_gpu_parity import PROGNOSTIC, RMS_RUN, RTOL_ROUTINE, basin_cfg, check_fields, copy_state, interior, relerr
+
+pytestmark = pytest.mark.gpu
+
+
+def seg_cfg(case):
+    if case == "n50":
+        return basin_cfg(nonlin=True, LLm=40, MMm=24, N=50)
+    c = basin_cfg(nonlin=True, LLm=24, MMm=20, N=100)
+    c.lmd, c.surf_flux = 1, 1
+    return c
+
+
+def make_model(cfg, colseg):
+    old = os.environ.get("ROMS_GPU_COLSEG")
+    os.environ["ROMS_GPU_COLSEG"] = str(colseg)
+    try:
+        return romsgpu.Model.from_case(cfg.case_id, cfg.LLm, cfg.MMm, cfg.N, cfg.NT, salinity=bool(cfg.salinity),
+                                       nonlin_eos=bool(cfg.nonlin_eos), dt=cfg.dt, ndtfast=cfg.ndtfast,
+                                       sizex=cfg.sizex, sizey=cfg.sizey, lmd=bool(cfg.lmd),
+                                       surf_flux=bool(cfg.surf_flux))
+    finally:
+        if old is None:
+            del os.environ["ROMS_GPU_COLSEG"]
+        else:
+            os.environ["ROMS_GPU_COLSEG"] = old
+
+
+ROUTINES = [("step3d_t", "corr", ["t"])]
+
+
+@pytest.mark.parametrize("case", ["n50", "n100"])
+@pytest.mark.parametrize("routine,mode,outs", ROUTINES, ids=[r[0] for r in ROUTINES])
+def test_seg_routine_parity(case, routine, mode, outs):
+    cfg = seg_cfg(case)
+    o = oracle.Oracle(cfg)
+    o.init()
+    o.step(3)
+    iic, kstp, knew, nstp, nrhs, nnew = o.tindex()
+    if mode == "corr":
+        nrhs, nnew = 3, 3 - nstp
+    else:
+        nrhs, nnew = nstp, 3
+    o.set_tindex([iic, kstp, knew, nstp, nrhs, nnew])
+    res = {}
+    for colseg in (1, 0):
+        m = make_model(cfg, colseg)
+        copy_state(o, m)
+        m.set_tindex(iic, kstp, knew, nstp, nrhs, nnew, nfast=o.nfast())
+        getattr(m, routine)()
+        m.sync()
+        res[colseg] = {n: interior(m.get(n), cfg.LLm, cfg.MMm) for n in outs}
+        m.close()
+    o.call(routine)
+    for n in outs:
+        ref = interior(o.field(n), cfg.LLm, cfg.MMm)
+        assert relerr(res[0][n], ref) <= RTOL_ROUTINE, (n, "sequential")
+        e = relerr(res[1][n], ref)
+        assert e <= RTOL_ROUTINE, (n, e)
+        assert e > 0.0 or np.array_equal(res[1][n], ref)
+
+
+@pytest.mark.parametrize("case", ["n50", "n100"])
+def test_seg_run_rms(case):
+    cfg = seg_cfg(case)
+    o = oracle.Oracle(cfg)
+    o.init()
+    m = make_model(cfg, 1)
+    o.step(30)
+    m.step(30)
+    check_fields(o, m, PROGNOSTIC, cfg.LLm, cfg.MMm, RMS_RUN, kind="rms")
+    m.close()

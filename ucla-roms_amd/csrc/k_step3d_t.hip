@@ -2,7 +2,7 @@
 // non-isoneutral branch: UPSTREAM_TS + SPLINE_TS) and the Laplacian tracer
 // diffusion t3dmix_tile (t3dmix_S.F).  One lane per water column; all levels
 // and the tridiagonal solve stay in the lane.
-#include "k_common.h"
+#include "k_colseg.h"
 
 namespace roms {
 
@@ -140,6 +140,121 @@ __global__ void __launch_bounds__(64) k_step3d_t_v(Dev d, Range R, int nnew, int
   }
 }
 
+// ---- segment-partitioned variant of k_step3d_t_v (k_colseg.h): block =
+// 64 columns x S segment wavefronts, one tracer per grid z.  The spline
+// interface values FC(0:N) and the implicit diffusion are each solved as one
+// partitioned tridiagonal system; the surface, KPP and pipe terms of the
+// diffusion r.h.s. are those of k_step3d_t_v (step3d_t_ISO.F:913-1100). ----
+__global__ void __launch_bounds__(128) k_step3d_t_seg(Dev d, Range R, int nnew, int nrhs) {
+  __shared__ SegXchg X;
+  constexpr int KR = kSegRows + 1;
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const Params& P = d.p;
+  const int N = b.N;
+  const double dt = P.dt;
+  const SegSpan sg = seg_span(N);
+  const int iu = R.i0 + (int)blockIdx.x * kSegCW + sg.col;
+  const bool act = iu <= R.i1;
+  const int i = act ? iu : R.i1, j = R.j0 + (int)blockIdx.y;
+  const int itrc = 1 + (int)blockIdx.z;
+  const long n2 = b.n2, ij = IJ(b, i, j);
+  const int c0 = sg.c0, n = sg.n;
+  const bool last = sg.s == sg.S - 1;
+  const double* __restrict__ Hz = F.Hz + ij;
+  const double* __restrict__ Tr = F.t + (long)(nrhs - 1) * b.n3 + (long)(itrc - 1) * 3 * b.n3 + ij;
+  double* __restrict__ Tn = F.t + (long)(nnew - 1) * b.n3 + (long)(itrc - 1) * 3 * b.n3 + ij;
+  const double* __restrict__ We = F.We + ij;
+  auto cell = [&](int k) { return (long)(k - 1) * n2; };   // rho level k
+  // hz[q] = Hz(c0-1+q), q = 0..n+1 (clamped to 1..N); tt[q] = t(nrhs)(c0-1+q), q = 0..n
+  double hz[KR + 1], tt[KR];
+#pragma unroll
+  for (int q = 0; q < KR + 1; q++) {
+    if (q <= n + 1) hz[q] = Hz[cell(min(max(c0 - 1 + q, 1), N))];
+    if (q <= n && q < KR) tt[q] = Tr[cell(min(max(c0 - 1 + q, 1), N))];
+  }
+  // spline rows: interfaces r = c0-1+q, q = 0..n-1 (+ r = N in the last segment)
+  SegTri<KR> T;
+  const int ns = n + (last ? 1 : 0);
+  T.eliminate(ns, [&](int q, double& a, double& bb, double& c, double& dd) {
+    const int r = c0 - 1 + q;
+    if (r == 0) { a = 0.0; bb = 1.0; c = 1.0; dd = 2.0 * tt[1]; }
+    else if (r == N) { a = 1.0; bb = 1.0; c = 0.0; dd = 2.0 * tt[q]; }
+    else {
+      a = hz[q + 1]; bb = 2.0 * (hz[q] + hz[q + 1]); c = hz[q];
+      dd = 3.0 * (hz[q] * tt[q + 1] + hz[q + 1] * tt[q]);
+    }
+  });
+  double xL, xR;
+  T.couple(sg, ns, X, xL, xR);
+  T.solve(ns, xL, xR);
+  // vertical advective fluxes FC(r)*We(r) at interfaces r = c0-1+q, q = 0..n (into tt)
+#pragma unroll
+  for (int q = 0; q < KR; q++) {
+    if (q <= n) {
+      const int r = c0 - 1 + q;
+      const double fc = q < ns ? T.D[q] : xR;
+      tt[q] = (r == 0 || r == N) ? 0.0 : fc * We[(long)r * n2];
+    }
+  }
+  // implicit diffusion rows, cells k = c0+p, p = 0..n-1
+  const int iAkt = itrc < b.nTS ? itrc : b.nTS;
+  const double* __restrict__ Akt = F.Akt + (long)(iAkt - 1) * b.n3w + ij;
+  const double* __restrict__ Wi = F.Wi + ij;
+  const double DC0 = dt * F.pm[ij] * F.pn[ij];
+  const bool kppT = P.lmd && itrc == 1, kppS = P.lmd && itrc == 2 && P.salinity;
+  const double sr = F.srflx[ij];
+  const double stf = F.stflx[ij + (long)(itrc - 1) * n2];
+  const int pidx = P.npip > 0 ? F.pipe_idx[ij] : 0;
+  const double pflx = pidx > 0 ? F.pipe_flx[ij] : 0.0;
+  const double ptrc = pidx > 0 ? F.pipe_trc[(pidx - 1) + (itrc - 1) * P.npip] : 0.0;
+  auto tval = [&](int k, double t, double dfl) {
+    const long o = cell(k);
+    t = t - dt * F.pm[ij] * F.pn[ij] * dfl;
+    if (pidx > 0) t = t + dt * F.pm[ij] * F.pn[ij] * pflx * F.pipe_prf[(pidx - 1) + (k - 1) * P.npip] * ptrc;
+    if (k == N) {
+      if (itrc == 1) t = t + dt * F.swflx[ij] * t / Hz[o];
+      t = t + dt * stf;
+    }
+    if (kppT) {
+      if (k <= N - 1) t = t + dt * (sr * F.swr_frac[ij + (long)k * n2] - F.ghat[ij + (long)k * n2] * (stf - sr));
+      if (k >= 2) t = t - dt * (sr * F.swr_frac[ij + o] - F.ghat[ij + o] * (stf - sr));
+    } else if (kppS) {
+      if (k <= N - 1) t = t + (-dt * F.ghat[ij + (long)k * n2] * stf);
+      if (k >= 2) t = t - (-dt * F.ghat[ij + o] * stf);
+    }
+    return t;
+  };
+  // FC, WC at interface r (0 at the bottom and the surface)
+  auto fcw = [&](int q, double& fc, double& wc) {   // interface c0-1+q
+    const int r = c0 - 1 + q;
+    if (r <= 0 || r >= N) { fc = 0.0; wc = 0.0; return; }
+    fc = 2.0 * dt * Akt[(long)r * n2] / (hz[q] + hz[q + 1]);
+    wc = DC0 * Wi[(long)r * n2];
+  };
+  double fcl, wcl;
+  fcw(0, fcl, wcl);
+  __syncthreads();  // X reused by the second coupling
+  T.eliminate(n, [&](int p, double& a, double& bb, double& c, double& dd) {
+    double fcu, wcu;
+    fcw(p + 1, fcu, wcu);
+    const int k = c0 + p;
+    a = -(fcl + fmax0(wcl));
+    bb = hz[p + 1] + fcu + fmax0(wcu) + fcl - fmin0(wcl);
+    c = -(fcu - fmin0(wcu));
+    dd = tval(k, Tn[cell(k)], tt[p + 1] - tt[p]);
+    fcl = fcu; wcl = wcu;
+  });
+  T.couple(sg, n, X, xL, xR);
+  T.solve(n, xL, xR);
+  if (act) {
+    const double rm = F.rmask[ij];
+#pragma unroll
+    for (int p = 0; p < KR; p++)
+      if (p < n) Tn[cell(c0 + p)] = T.D[p] * rm;
+  }
+}
+
 void setup_column_kernels_t(size_t bytes) {
   (void)hipFuncSetAttribute((const void*)k_step3d_t_v<ColLds>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)bytes);
@@ -151,7 +266,11 @@ void launch_step3d_t(const Dev& d, hipStream_t s, const Tlev& t) {
   hipLaunchKernelGGL(k_step3d_t_h, grid3_of(R, b.N), dim3(kBX, kBY), 0, s, d, R, t.nnew, t.nrhs);
   dim3 gt = gridc_of(R);
   gt.z = b.NT;
-  if (d.f.colscr)
+  if (d.p.colseg) {
+    dim3 gs((R.i1 - R.i0 + kSegCW) / kSegCW, R.j1 - R.j0 + 1, b.NT);
+    hipLaunchKernelGGL(k_step3d_t_seg, gs, dim3(kCX, seg_waves(b.N)), 0, s, d, R, t.nnew, t.nrhs);
+  }
+  else if (d.f.colscr)
     hipLaunchKernelGGL(k_step3d_t_v<ColGlb>, gt, dim3(kCX), 0, s, d, R, t.nnew, t.nrhs);
   else
     hipLaunchKernelGGL(k_step3d_t_v<ColLds>, gt, dim3(kCX), col_lds_bytes(2, b.N), s, d, R, t.nnew, t.nrhs);

@@ -32,6 +32,7 @@ struct Bounds {
 struct Params {
   int nonlin_eos, salinity, lmd, uv_vis2, ts_dif2;
   int s2d_split;  // 1: step2d as separate zeta / momentum kernels (ROMS_GPU_S2D_SPLIT=1)
+  int colseg;     // 1: segment-partitioned column solvers (k_colseg.h; N > 32, ROMS_GPU_COLSEG=0/1)
   int npip;       // pipe_frc.F: number of pipes (0: pipe_source off)
   int curvgrid;   // CURVGRID && UV_ADV: curvature terms (compute_horiz_rhs_uv_terms.h:8-11)
   int obc;        // open edges: 1 W, 2 E, 4 S, 8 N (Flather / Orlanski + *_FRC_BRY)
@@ -132,6 +133,9 @@ inline dim3 grid3_of(const Range& r, int nk) {
 // Column launch: one wavefront of 64 consecutive i per block, one row j per
 // block row; column scratch lives in LDS (see ColLds in k_common.h).
 constexpr int kCX = 64;
+// segment-partitioned column solvers (k_colseg.h)
+constexpr int kSegRows = 13;   // cells per segment (register arrays of kSegRows + 2)
+constexpr int kSegMaxS = 8;    // segments (wavefronts) per block: N <= 104
 inline dim3 gridc_of(const Range& r) {
   int ni = r.i1 - r.i0 + 1, nj = r.j1 - r.j0 + 1;
   if (ni < 1) ni = 1;

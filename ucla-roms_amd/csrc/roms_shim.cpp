@@ -303,6 +303,18 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
   P.curvgrid = cfg->curvgrid;
   if (P.obc) P.s2d_split = 1;  // open edges: separate zeta / zetabc / momentum kernels (step2d)
   for (int i = 0; i < kMaxFast; i++) { g.w1[i] = cfg->weight[0][i]; g.w2[i] = cfg->weight[1][i]; }
+  // segment-partitioned column solvers (k_colseg.h) where the sequential
+  // solvers' two LDS coefficient columns no longer fit (N > 63, up to 8
+  // segments of 13 levels); the bit-exact sequential LDS solvers otherwise
+  // (measured: at N = 50 the LDS sweep is faster, the partitioned solve
+  // costs ~3x the VALU instructions per level).
+  // ROMS_GPU_COLSEG=0/1 forces either (A/B and parity runs).
+  P.colseg = (size_t)2 * (dims->N + 1) * kCX * sizeof(double) > 64 * 1024 && dims->N <= kSegRows * kSegMaxS;
+  {
+    const char* e = getenv("ROMS_GPU_COLSEG");
+    if (e && e[0] == '0') P.colseg = 0;
+    if (e && e[0] == '1') P.colseg = dims->N <= kSegRows * kSegMaxS;
+  }
   // column-solver scratch: LDS while two (N+1)-level slots per wave fit the
   // default 64 KB (N < 63), global memory for deeper grids;
   // ROMS_GPU_COL_GLOBAL=1/0 forces either (A/B runs)
