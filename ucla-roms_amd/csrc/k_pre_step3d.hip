@@ -14,11 +14,12 @@ struct PreCoef {
 // t(nnew) = Hz_bak*(cf_stp*t(nstp)+cf_bak*t(indx)) - dtau*pm*pn*div(FX,FE),
 // t(indx) = Hz*t(nstp). ----
 __global__ void __launch_bounds__(256) k_pre_tracer_h(Dev d, Range R, PreCoef c, int nstp, int nnew, int nrhs) {
+  const uint3 bI = xcd_tile();
   __shared__ TracerWin W;
   const Bounds& b = d.b;
   const Fields& F = d.f;
-  const int k = 1 + (int)blockIdx.z, indx = 3 - nstp;
-  const int i0 = R.i0 + (int)blockIdx.x * kBX, j0 = R.j0 + (int)blockIdx.y * kBY;
+  const int k = 1 + (int)bI.z, indx = 3 - nstp;
+  const int i0 = R.i0 + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * kBY;
   const int ib = i0 - 2, jb = j0 - 2;
   const long kk = (long)(k - 1) * b.n2;
   tracer_win_fill(b, F, W, ib, jb, kk, nullptr);
@@ -65,11 +66,11 @@ __global__ void __launch_bounds__(64) k_pre_tracer_v(Dev d, Range R, PreCoef c, 
   const double* __restrict__ Hz = F.Hz + ij;
   const double* __restrict__ We = F.We + ij;
   const double* __restrict__ Wi = F.Wi + ij;
-  const C A = ColMake<C>::at(d, 0, (int)blockIdx.z, ij), B = ColMake<C>::at(d, 1, (int)blockIdx.z, ij);
+  const C A = ColMake<C>::at(d, 0, (int)bI.z, ij), B = ColMake<C>::at(d, 1, (int)bI.z, ij);
   const double* __restrict__ Hf = F.c2 + ij;
   auto hfwd = [&](int k) { return Hf[(long)(k - 1) * n2]; };
   {
-    const int itrc = 1 + (int)blockIdx.z;
+    const int itrc = 1 + (int)bI.z;
     const long tb = (long)(itrc - 1) * 3 * b.n3;
     const double* __restrict__ Tr = F.t + (long)(nrhs - 1) * b.n3 + tb + ij;
     double* __restrict__ Tn = F.t + (long)(nnew - 1) * b.n3 + tb + ij;
@@ -135,11 +136,12 @@ __global__ void __launch_bounds__(64) k_pre_tracer_v(Dev d, Range R, PreCoef c, 
 // ---- horizontal momentum r.h.s., one (i,j,k) cell per thread; u, v,
 // FlxU, FlxV of the block's 64x4 tile plus a 2-cell halo staged in LDS ----
 __global__ void __launch_bounds__(256) k_uv_horiz(Dev d, Range R, int nrhs, UVBounds ub, int up) {
+  const uint3 bI = xcd_tile();
   __shared__ double sU[kUVN], sV[kUVN], sFU[kUVN], sFV[kUVN];
   const Bounds& b = d.b;
   const Fields& F = d.f;
-  const int k = 1 + (int)blockIdx.z;
-  const int i0 = R.i0 + (int)blockIdx.x * kBX, j0 = R.j0 + (int)blockIdx.y * kBY;
+  const int k = 1 + (int)bI.z;
+  const int i0 = R.i0 + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * kBY;
   const int ib = i0 - 2, jb = j0 - 2;
   const long kk = (long)(k - 1) * b.n2;
   const double* U = F.u + (long)(nrhs - 1) * b.n3 + kk;
@@ -262,8 +264,8 @@ __global__ void __launch_bounds__(64) k_pre_uv(Dev d, Range R, PreCoef c, int ns
   ROMS_IJC_OR_RETURN(R)
   const Bounds& b = d.b;
   const long ij = IJ(b, i, j);
-  const C A = ColMake<C>::at(d, 0, (int)blockIdx.z, ij), B = ColMake<C>::at(d, 1, (int)blockIdx.z, ij);
-  if (blockIdx.z == 0) {
+  const C A = ColMake<C>::at(d, 0, (int)bI.z, ij), B = ColMake<C>::at(d, 1, (int)bI.z, ij);
+  if (bI.z == 0) {
     if (i >= b.istrU && i <= b.iend && j >= b.jstr && j <= b.jend) pre_uv_col(d, i, j, 0, c, nstp, nnew, nrhs, A, B);
   } else {
     if (i >= b.istr && i <= b.iend && j >= b.jstrV && j <= b.jend) pre_uv_col(d, i, j, 1, c, nstp, nnew, nrhs, A, B);

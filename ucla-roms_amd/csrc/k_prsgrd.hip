@@ -95,6 +95,7 @@ __global__ void __launch_bounds__(256) k_prsgrd_P(Dev d, Range R, int split) {
 constexpr int kPXW = kBX + 2, kPXN = kPXW * kBY;          // u-points m = i0-1 .. i0+64, tile rows
 constexpr int kPYH = kBY + 2, kPYN = kBX * kPYH;          // v-points m = j0-1 .. j0+4, tile columns
 __global__ void __launch_bounds__(256) k_prsgrd_uv(Dev d, Range R, int split, int imin, int imax, int jmin, int jmax) {
+  const uint3 bI = xcd_tile();
   __shared__ double sFCx[kPXN], sRx[kPXN], sFCy[kPYN], sRy[kPYN];
   __shared__ double sdZx[kPXN], sdRx[kPXN], sdZy[kPYN], sdRy[kPYN];
   const Bounds& b = d.b;
@@ -103,9 +104,9 @@ __global__ void __launch_bounds__(256) k_prsgrd_uv(Dev d, Range R, int split, in
   const double OneFifth = 0.2, OneTwelfth = 1.0 / 12.0;
   const double HalfGRho = 0.5 * (g / rho0);
   const double* rho = split ? F.rhos : F.rho;
-  const int k = 1 + (int)blockIdx.z;
+  const int k = 1 + (int)bI.z;
   const long kk = (long)(k - 1) * b.n2, sj = b.nx2;
-  const int i0 = R.i0 + (int)blockIdx.x * kBX, j0 = R.j0 + (int)blockIdx.y * kBY;
+  const int i0 = R.i0 + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * kBY;
   const int tid = threadIdx.x + kBX * threadIdx.y;
   // elementary differences at clamped u-points (xi) and v-points (eta)
   for (int q = tid; q < kPXN + kPYN; q += kBX * kBY) {

@@ -231,11 +231,12 @@ struct FBTile {
 
 template <bool kPipe>
 __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int closed, int vwrap) {
+  const uint3 bI = xcd_tile();
   __shared__ FBTile T;
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const long sj = b.nx2, n2 = b.n2;
-  const int i0 = R.i0 + (int)blockIdx.x * kBX, j0 = R.j0 + (int)blockIdx.y * kBY;
+  const int i0 = R.i0 + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * kBY;
   const int tid = threadIdx.x + kBX * threadIdx.y;
   constexpr int NT = kBX * kBY;
   auto G = [&](int i, int j) { return (i - (i0 - 2)) + (j - (j0 - 2)) * kGX; };

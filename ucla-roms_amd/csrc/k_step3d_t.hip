@@ -8,11 +8,12 @@ namespace roms {
 
 // Horizontal advection, one thread per (i,j,k) cell, all tracers.
 __global__ void __launch_bounds__(256) k_step3d_t_h(Dev d, Range R, int nnew, int nrhs) {
+  const uint3 bI = xcd_tile();
   __shared__ TracerWin W;
   const Bounds& b = d.b;
   const Fields& F = d.f;
-  const int k = 1 + (int)blockIdx.z;
-  const int i0 = R.i0 + (int)blockIdx.x * kBX, j0 = R.j0 + (int)blockIdx.y * kBY;
+  const int k = 1 + (int)bI.z;
+  const int i0 = R.i0 + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * kBY;
   const int ib = i0 - 2, jb = j0 - 2;
   const long kk = (long)(k - 1) * b.n2;
   tracer_win_fill(b, F, W, ib, jb, kk, nullptr);
@@ -48,9 +49,9 @@ __global__ void __launch_bounds__(64) k_step3d_t_v(Dev d, Range R, int nnew, int
   const long n2 = b.n2, ij = IJ(b, i, j);
   const double rm = F.rmask[ij];
   const double* __restrict__ Hz = F.Hz + ij;
-  const C A = ColMake<C>::at(d, 0, (int)blockIdx.z, ij), B = ColMake<C>::at(d, 1, (int)blockIdx.z, ij);
+  const C A = ColMake<C>::at(d, 0, (int)bI.z, ij), B = ColMake<C>::at(d, 1, (int)bI.z, ij);
   {
-    const int itrc = 1 + (int)blockIdx.z;
+    const int itrc = 1 + (int)bI.z;
     const double* __restrict__ Tr = F.t + (long)(nrhs - 1) * b.n3 + (long)(itrc - 1) * 3 * b.n3 + ij;
     double* __restrict__ Tn = F.t + (long)(nnew - 1) * b.n3 + (long)(itrc - 1) * 3 * b.n3 + ij;
     const double stf = F.stflx[ij + (long)(itrc - 1) * n2];
@@ -146,6 +147,7 @@ __global__ void __launch_bounds__(64) k_step3d_t_v(Dev d, Range R, int nnew, int
 // partitioned tridiagonal system; the surface, KPP and pipe terms of the
 // diffusion r.h.s. are those of k_step3d_t_v (step3d_t_ISO.F:913-1100). ----
 __global__ void __launch_bounds__(128) k_step3d_t_seg(Dev d, Range R, int nnew, int nrhs) {
+  const uint3 bI = xcd_tile();
   __shared__ SegXchg X;
   constexpr int KR = kSegRows + 1;
   const Bounds& b = d.b;
@@ -154,10 +156,10 @@ __global__ void __launch_bounds__(128) k_step3d_t_seg(Dev d, Range R, int nnew, 
   const int N = b.N;
   const double dt = P.dt;
   const SegSpan sg = seg_span(N);
-  const int iu = R.i0 + (int)blockIdx.x * kSegCW + sg.col;
+  const int iu = R.i0 + (int)bI.x * kSegCW + sg.col;
   const bool act = iu <= R.i1;
-  const int i = act ? iu : R.i1, j = R.j0 + (int)blockIdx.y;
-  const int itrc = 1 + (int)blockIdx.z;
+  const int i = act ? iu : R.i1, j = R.j0 + (int)bI.y;
+  const int itrc = 1 + (int)bI.z;
   const long n2 = b.n2, ij = IJ(b, i, j);
   const int c0 = sg.c0, n = sg.n;
   const bool last = sg.s == sg.S - 1;
@@ -278,35 +280,40 @@ void launch_step3d_t(const Dev& d, hipStream_t s, const Tlev& t) {
   launch_exchange_tracers(d, s, t.nnew);
 }
 
-// ---- t3dmix: Laplacian diffusion along S, t(nnew) += dt*pm*pn*div(F)/Hz ----
-__global__ void __launch_bounds__(256) k_t3dmix(Dev d, Range R, int nnew, int nrhs, int itrc) {
+// ---- t3dmix: Laplacian diffusion along S, t(nnew) += dt*pm*pn*div(F)/Hz.
+// One lane per column walking all levels, every tracer in one launch: the
+// column's 2-D metric factors are read once (t3dmix_S.F:60-259). ----
+__global__ void __launch_bounds__(256) k_t3dmix(Dev d, Range R, int nnew, int nrhs) {
   ROMS_IJ_OR_RETURN(R)
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const long ij = IJ(b, i, j), sj = b.nx2, n2 = b.n2;
-  const double* d2 = F.diff2 + (long)(itrc - 1) * n2;
-  const double* Tr = F.t + (long)(nrhs - 1) * b.n3 + (long)(itrc - 1) * 3 * b.n3;
-  double* Tn = F.t + (long)(nnew - 1) * b.n3 + (long)(itrc - 1) * 3 * b.n3;
-  auto FX = [&](long p, long kk) {
-    return 0.25 * (d2[p] + d2[p - 1]) * F.pmon_u[p] * (F.Hz[p + kk] + F.Hz[p - 1 + kk]) * (Tr[p + kk] - Tr[p - 1 + kk]) *
-           F.umask[p];
-  };
-  auto FE = [&](long p, long kk) {
-    return 0.25 * (d2[p] + d2[p - sj]) * F.pnom_v[p] * (F.Hz[p + kk] + F.Hz[p - sj + kk]) *
-           (Tr[p + kk] - Tr[p - sj + kk]) * F.vmask[p];
-  };
-  {
-    const int k = 1 + (int)blockIdx.z;
-    const long kk = (long)(k - 1) * n2, o = ij + kk;
-    Tn[o] = Tn[o] + d.p.dt * F.pm[ij] * F.pn[ij] * (FX(ij + 1, kk) - FX(ij, kk) + FE(ij + sj, kk) - FE(ij, kk)) / F.Hz[o];
+  const double* __restrict__ Hz = F.Hz;
+  const double pmn = d.p.dt * F.pm[ij] * F.pn[ij];
+  for (int itrc = 1; itrc <= b.NT; itrc++) {
+    const double* d2 = F.diff2 + (long)(itrc - 1) * n2;
+    const double* __restrict__ Tr = F.t + (long)(nrhs - 1) * b.n3 + (long)(itrc - 1) * 3 * b.n3;
+    double* __restrict__ Tn = F.t + (long)(nnew - 1) * b.n3 + (long)(itrc - 1) * 3 * b.n3;
+    // 0.25*(diff2+diff2)*pmon_u per face (the first factors of the reference product)
+    const double ax0 = 0.25 * (d2[ij] + d2[ij - 1]) * F.pmon_u[ij], ax1 = 0.25 * (d2[ij + 1] + d2[ij]) * F.pmon_u[ij + 1];
+    const double ay0 = 0.25 * (d2[ij] + d2[ij - sj]) * F.pnom_v[ij], ay1 = 0.25 * (d2[ij + sj] + d2[ij]) * F.pnom_v[ij + sj];
+    const double um0 = F.umask[ij], um1 = F.umask[ij + 1], vm0 = F.vmask[ij], vm1 = F.vmask[ij + sj];
+#pragma unroll 2
+    for (int k = 1; k <= b.N; k++) {
+      const long o = ij + (long)(k - 1) * n2;
+      const double FX1 = ax1 * (Hz[o + 1] + Hz[o]) * (Tr[o + 1] - Tr[o]) * um1;
+      const double FX0 = ax0 * (Hz[o] + Hz[o - 1]) * (Tr[o] - Tr[o - 1]) * um0;
+      const double FE1 = ay1 * (Hz[o + sj] + Hz[o]) * (Tr[o + sj] - Tr[o]) * vm1;
+      const double FE0 = ay0 * (Hz[o] + Hz[o - sj]) * (Tr[o] - Tr[o - sj]) * vm0;
+      Tn[o] = Tn[o] + pmn * (FX1 - FX0 + FE1 - FE0) / Hz[o];
+    }
   }
 }
 
 void launch_t3dmix(const Dev& d, hipStream_t s, const Tlev& t) {
   const Bounds& b = d.b;
   Range R{b.istr, b.iend, b.jstr, b.jend};
-  for (int itrc = 1; itrc <= b.NT; itrc++)
-    hipLaunchKernelGGL(k_t3dmix, grid3_of(R, b.N), dim3(kBX, kBY), 0, s, d, R, t.nnew, t.nrhs, itrc);
+  hipLaunchKernelGGL(k_t3dmix, grid_of(R), dim3(kBX, kBY), 0, s, d, R, t.nnew, t.nrhs);
   launch_exchange_tracers(d, s, t.nnew);
 }
 

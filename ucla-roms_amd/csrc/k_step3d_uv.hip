@@ -76,8 +76,8 @@ __global__ void __launch_bounds__(64) k_uv1(Dev d, Range R, int nnew, int nrhs) 
   ROMS_IJC_OR_RETURN(R)
   const Bounds& b = d.b;
   const long ij = IJ(b, i, j);
-  const C A = ColMake<C>::at(d, 0, (int)blockIdx.z, ij), B = ColMake<C>::at(d, 1, (int)blockIdx.z, ij);
-  if (blockIdx.z == 0) {
+  const C A = ColMake<C>::at(d, 0, (int)bI.z, ij), B = ColMake<C>::at(d, 1, (int)bI.z, ij);
+  if (bI.z == 0) {
     if (i >= b.istrU && i <= b.iend) uv1_col(d, i, j, 0, nnew, nrhs, A, B);
   } else {
     if (j >= b.jstrV) uv1_col(d, i, j, 1, nnew, nrhs, A, B);
@@ -156,11 +156,12 @@ struct ViscPsi {  // metric factors of one psi point
   bool on;
 };
 __global__ void __launch_bounds__(256) k_visc3d(Dev d, Range R, int nstp) {
+  const uint3 bI = xcd_tile();
   __shared__ double sUFx[kVN], sVFe[kVN], sUFe[kVN], sVFx[kVN];
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const int indx = 3 - nstp;
-  const int i0 = R.i0 + (int)blockIdx.x * kBX, j0 = R.j0 + (int)blockIdx.y * kBY;
+  const int i0 = R.i0 + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * kBY;
   const long sj = b.nx2;
   const double* pm = F.pm;
   const double* pn = F.pn;

@@ -62,20 +62,29 @@ __global__ void __launch_bounds__(256) k_set_huv(Dev d, Range R, int nrhs) {
   const Fields& F = d.f;
   const bool du = i >= b.istr && i <= b.iendR && j >= b.jstrR && j <= b.jendR;
   const bool dv = i >= b.istrR && i <= b.iendR && j >= b.jstr && j <= b.jendR;
-  const long ij = IJ(b, i, j);
-  {
-    const int k = 1 + (int)blockIdx.z;
-    const long o = ij + (long)(k - 1) * b.n2;
-    const double hz = F.Hz[o];
+  const long ij = IJ(b, i, j), n2 = b.n2;
+  // one lane per column, all levels: dn_u/dm_v read once per column
+  const double dnu = du ? F.dn_u[ij] : 0.0, dmv = dv ? F.dm_v[ij] : 0.0;
+  const double* __restrict__ Hz = F.Hz + ij;
+  const double* __restrict__ U = F.u + (long)(nrhs - 1) * b.n3 + ij;
+  const double* __restrict__ V = F.v + (long)(nrhs - 1) * b.n3 + ij;
+  double* __restrict__ FU = F.FlxU + ij;
+  double* __restrict__ FV = F.FlxV + ij;
+  double* __restrict__ HU = F.Hz_u + ij;
+  double* __restrict__ HV = F.Hz_v + ij;
+#pragma unroll 4
+  for (int k = 1; k <= b.N; k++) {
+    const long o = (long)(k - 1) * n2;
+    const double hz = Hz[o];
     if (du) {
-      const double hzm = F.Hz[o - 1];
-      F.FlxU[o] = 0.5 * (hz + hzm) * F.dn_u[ij] * (F.u[o + (long)(nrhs - 1) * b.n3]);
-      F.Hz_u[o] = 0.5 * (hz + hzm);
+      const double hzm = Hz[o - 1];
+      FU[o] = 0.5 * (hz + hzm) * dnu * (U[o]);
+      HU[o] = 0.5 * (hz + hzm);
     }
     if (dv) {
-      const double hzm = F.Hz[o - b.nx2];
-      F.FlxV[o] = 0.5 * (hz + hzm) * F.dm_v[ij] * (F.v[o + (long)(nrhs - 1) * b.n3]);
-      F.Hz_v[o] = 0.5 * (hz + hzm);
+      const double hzm = Hz[o - b.nx2];
+      FV[o] = 0.5 * (hz + hzm) * dmv * (V[o]);
+      HV[o] = 0.5 * (hz + hzm);
     }
   }
 }
@@ -83,7 +92,7 @@ __global__ void __launch_bounds__(256) k_set_huv(Dev d, Range R, int nrhs) {
 void launch_set_huv(const Dev& d, hipStream_t s, const Tlev& t) {
   const Bounds& b = d.b;
   Range R{b.istrR < b.istr ? b.istrR : b.istr, b.iendR, b.jstrR < b.jstr ? b.jstrR : b.jstr, b.jendR};
-  hipLaunchKernelGGL(k_set_huv, grid3_of(R, b.N), dim3(kBX, kBY), 0, s, d, R, t.nrhs);
+  hipLaunchKernelGGL(k_set_huv, grid_of(R), dim3(kBX, kBY), 0, s, d, R, t.nrhs);
   launch_exchange_list(d, s, ExchList{{d.f.FlxU, d.f.FlxV}, {b.N, b.N}, 2});
 }
 

@@ -112,6 +112,26 @@ __device__ __forceinline__ double dmax(double a, double b) { return a > b ? a : 
 __device__ __forceinline__ double dmin(double a, double b) { return a < b ? a : b; }
 __device__ __forceinline__ int iclamp(int x, int lo, int hi) { return x < lo ? lo : (x > hi ? hi : x); }
 
+// XCD-aware tile order.  Workgroups are dealt round-robin to the 8 XCDs
+// (MI355X_MICROARCH.md: blocks b and b+8 share an XCD and its L2), so with
+// the plain grid order the four neighbours of a tile live in other XCDs' L2s
+// and every halo row is fetched from HBM twice.  xcd_tile() maps the
+// physical block id to a logical tile so that each XCD walks one contiguous
+// 1/8 of the (x fastest, then y, then z) tile sequence: neighbouring tiles of
+// a level are processed by the same XCD at about the same time.
+__device__ __forceinline__ uint3 xcd_tile() {
+  const unsigned gx = gridDim.x, gy = gridDim.y;
+  const unsigned total = gx * gy * gridDim.z;
+  const unsigned phys = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  const unsigned q = total >> 3, r = total & 7u, x = phys & 7u, slot = phys >> 3;
+  const unsigned logical = x * q + (x < r ? x : r) + slot;
+  uint3 t;
+  t.x = logical % gx;
+  t.y = (logical / gx) % gy;
+  t.z = logical / (gx * gy);
+  return t;
+}
+
 // 2-D launch over an inclusive index rectangle [i0,i1]x[j0,j1]: one lane per
 // (i,j) column, 64 consecutive i per wavefront (coalesced), 4 rows per block.
 struct Range {
@@ -143,12 +163,14 @@ inline dim3 gridc_of(const Range& r) {
   return dim3((ni + kCX - 1) / kCX, nj, 1);
 }
 #define ROMS_IJC_OR_RETURN(R)                                   \
-  const int i = (R).i0 + (int)(blockIdx.x * kCX + threadIdx.x); \
-  const int j = (R).j0 + (int)blockIdx.y;                       \
+  const uint3 bI = xcd_tile();                                  \
+  const int i = (R).i0 + (int)(bI.x * kCX + threadIdx.x);       \
+  const int j = (R).j0 + (int)bI.y;                             \
   if (i > (R).i1 || j > (R).j1) return;
 #define ROMS_IJ_OR_RETURN(R)                                   \
-  const int i = (R).i0 + (int)(blockIdx.x * kBX + threadIdx.x); \
-  const int j = (R).j0 + (int)(blockIdx.y * kBY + threadIdx.y); \
+  const uint3 bI = xcd_tile();                                 \
+  const int i = (R).i0 + (int)(bI.x * kBX + threadIdx.x);      \
+  const int j = (R).j0 + (int)(bI.y * kBY + threadIdx.y);      \
   if (i > (R).i1 || j > (R).j1) return;
 
 // ---- launcher declarations (one translation unit per routine family) ----
