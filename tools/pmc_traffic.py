@@ -22,15 +22,15 @@ ROUTINE_OF = {
     "k_uv1": "step3d_uv1", "k_visc3d": "visc3d", "k_s2d_zeta": "step2d", "k_s2d_mom": "step2d",
     "k_s2d_zetabc": "step2d", "k_s2d_fb": "step2d", "k_visc3d_frc": "visc3d", "k_s2d_edges": "step2d", "k_s2d_last": "step2d", "k_set_depth": "step2d",
     "k_uv2_couple": "step3d_uv2", "k_uv2_flux": "step3d_uv2", "k_step3d_t_h": "step3d_t", "k_step3d_t_v": "step3d_t",
-    "k_t3dmix": "t3dmix", "k_periodic_wrap": "halo", "k_halo_pack": "halo", "k_halo_unpack": "halo",
+    "k_t3dmix": "t3dmix", "k_step3d_t_seg": "step3d_t", "k_periodic_wrap": "halo", "k_halo_pack": "halo", "k_halo_unpack": "halo",
 }
 CALLS_PER_STEP = {"rho_eos": 3, "set_HUV": 1, "omega": 3, "prsgrd": 2, "pre_step3d": 1, "set_HUV1": 1,
                   "step3d_uv1": 1, "visc3d": 1, "step2d": None, "step3d_uv2": 1, "step3d_t": 1, "t3dmix": 1}
 
 
 def short(name):
-    n = name.split("(")[0]
-    return n.split("::")[-1]
+    n = name.split("(")[0].replace("void ", "")
+    return n.split("<")[0].split("::")[-1]
 
 
 def read(path, counter):

@@ -32,59 +32,66 @@ __global__ void __launch_bounds__(256) k_prsgrd_P(Dev d, Range R, int split) {
   const double* __restrict__ qp1 = F.qp1 + ij;
   double* __restrict__ rhos = F.rhos + ij;
   double* __restrict__ Pp = F.P + ij;
-  // in-situ density at rho-level k (SPLIT_EOS: rho1 + qp1*dpth*(1-qp2*dpth))
-  auto rhoval = [&](long o) {
+  // Top-down walk with a rolling register window: z_r, rho1, qp1 (or rho) of
+  // each level are loaded once; the elementary differences, harmonic
+  // averages and P keep the reference's expressions (prsgrd.F:200-330).
+  auto rhov = [&](double r1, double q1, double z) {  // in-situ density at a rho level
     if (split) {
-      const double dpth = -zr[o];
-      return rho1[o] + qp1[o] * dpth * (1.0 - qp2 * dpth);
+      const double dpth = -z;
+      return r1 + q1 * dpth * (1.0 - qp2 * dpth);
     }
-    return rho[o];
+    return r1;
   };
-  // elementary difference at w-level k in 1..N-1
-  auto eZ = [&](int k) { const long o = (long)(k - 1) * n2; return zr[o + n2] - zr[o]; };
-  auto eR = [&](int k) {
-    const long o = (long)(k - 1) * n2;
+  auto eRof = [&](double ru, double rl, double qu, double ql, double zu, double zl) {  // levels l+1 (u), l
     if (split) {
-      const double dpth = -0.5 * (zr[o + n2] + zr[o]);
-      return rho1[o + n2] - rho1[o] + (qp1[o + n2] - qp1[o]) * dpth * (1.0 - qp2 * dpth);
+      const double dpth = -0.5 * (zu + zl);
+      return ru - rl + (qu - ql) * dpth * (1.0 - qp2 * dpth);
     }
-    return rho[o + n2] - rho[o];
+    return ru - rl;
   };
+  const double* __restrict__ R1 = split ? rho1 : rho;
+  auto ldz = [&](int k) { return zr[(long)(k - 1) * n2]; };
+  auto ldr = [&](int k) { return R1[(long)(k - 1) * n2]; };
+  auto ldq = [&](int k) { return split ? qp1[(long)(k - 1) * n2] : 0.0; };
   const bool doP = i >= b.istrU - 1 && i <= b.iend;
-  // rolling: e(k), e(k-1) elementary; dZ/dR harmonic at k+1 (previous)
-  double eZk = eZ(N - 1), eRk = eR(N - 1);   // e(N) = e(N-1)
-  double dZ1 = 0.0, dR1 = 0.0, P1 = 0.0;       // values at k+1
-#pragma unroll 8
+  double zC = ldz(N), rC = ldr(N), qC = ldq(N);              // level k
+  double zM = ldz(N - 1), rM = ldr(N - 1), qM = ldq(N - 1);  // level k-1
+  double eZk = zC - zM, eRk = eRof(rC, rM, qC, qM, zC, zM);  // e(N) = e(N-1)
+  double dZ1 = 0.0, dR1 = 0.0, P1 = 0.0;                     // values at k+1
+  double z1 = 0.0, v1 = 0.0;                                 // z_r, in-situ rho at k+1
+#pragma unroll 4
   for (int k = N; k >= 1; k--) {
-    const int km = k - 1;
-    const double eZm = km >= 1 ? eZ(km) : eZ(1);   // e(0) = e(1)
-    const double eRm = km >= 1 ? eR(km) : eR(1);
+    double eZm, eRm;
+    if (k >= 2) { eZm = zC - zM; eRm = eRof(rC, rM, qC, qM, zC, zM); }
+    else { eZm = eZk; eRm = eRk; }                           // e(0) = e(1)
     const double dZk = [&] { const double c = 2.0 * eZk * eZm; return c / (eZk + eZm); }();
     double dRk = harm(eRk, eRm);
     const long o = (long)(k - 1) * n2;
+    const double v0 = rhov(rC, qC, zC);
     if (split) {
-      const double dpth = -zr[o];
-      dRk = dRk - qp1[o] * dZk * (1.0 - 2.0 * qp2 * dpth);
-      rhos[o] = rhoval(o);
+      const double dpth = -zC;
+      dRk = dRk - qC * dZk * (1.0 - 2.0 * qp2 * dpth);
+      rhos[o] = v0;
     }
     if (doP) {
       double Pk;
       if (k == N) {
-        const double zw = F.z_w[ij + (long)N * n2], zr0 = zr[o], zrm = zr[o - n2];
-        const double rN = rhoval(o), rNm = rhoval(o - n2);
-        Pk = g * zw + grho * (rN + 0.5 * (rN - rNm) * (zw - zr0) / (zr0 - zrm)) * (zw - zr0);
+        const double zw = F.z_w[ij + (long)N * n2];
+        const double rNm = rhov(rM, qM, zM);
+        Pk = g * zw + grho * (v0 + 0.5 * (v0 - rNm) * (zw - zC) / (zC - zM)) * (zw - zC);
       } else {
-        const double zr1 = zr[o + n2], zr0 = zr[o];
-        const double r1 = rhoval(o + n2), r0 = rhoval(o);
-        Pk = P1 + HalfGRho * ((r1 + r0) * (zr1 - zr0) -
-                              OneFifth * ((dR1 - dRk) * (zr1 - zr0 - OneTwelfth * (dZ1 + dZk)) -
-                                          (dZ1 - dZk) * (r1 - r0 - OneTwelfth * (dR1 + dRk))));
+        Pk = P1 + HalfGRho * ((v1 + v0) * (z1 - zC) -
+                              OneFifth * ((dR1 - dRk) * (z1 - zC - OneTwelfth * (dZ1 + dZk)) -
+                                          (dZ1 - dZk) * (v1 - v0 - OneTwelfth * (dR1 + dRk))));
       }
       Pp[o] = Pk;
       P1 = Pk;
     }
     dZ1 = dZk; dR1 = dRk;
     eZk = eZm; eRk = eRm;
+    z1 = zC; v1 = v0;
+    zC = zM; rC = rM; qC = qM;
+    if (k >= 3) { zM = ldz(k - 2); rM = ldr(k - 2); qM = ldq(k - 2); }
   }
 }
 
