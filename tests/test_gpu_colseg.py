@@ -1,6 +1,8 @@
 """GPU parity of the segment-partitioned column solvers (k_colseg.h), which
-replace the sequential Thomas sweeps for deep grids (N > 32: the C2 and C3
-workloads).  Their elimination order differs from the reference's, so the
+replace the sequential Thomas sweeps for deep grids (N > 63: the C3 workload;
+forced on at N = 50 here): the predictor's tracer and momentum columns
+(pre_step3d), the corrector's momentum columns (step3d_uv1) and the tracer
+corrector (step3d_t).  Their elimination order differs from the reference's, so the
 bound is the north_star floating-point tolerance rather than bit equality:
 1e-12 relative per routine call, field RMS < 1e-10 over a run.
 
@@ -44,7 +46,9 @@ def make_model(cfg, colseg):
             os.environ["ROMS_GPU_COLSEG"] = old
 
 
-ROUTINES = [("step3d_t", "corr", ["t"])]
+ROUTINES = [("pre_step3d", "pred", ["t", "u", "v", "ru", "rv"]),
+            ("step3d_uv1", "corr", ["u", "v", "ru", "rv", "rufrc", "rvfrc"]),
+            ("step3d_t", "corr", ["t"])]
 
 
 @pytest.mark.parametrize("case", ["n50", "n100"])

@@ -136,4 +136,110 @@ struct SegTri {
   }
 };
 
+// ---- parabolic-spline interface values FC(0:N) of one column, segment form
+// (compute_vert_tracer_fluxes.h, compute_vert_rhs_uv_terms.h; sequential forms
+// tracer_spline_lds / uv_vert_flux_lds).  Rows: FC(0)+FC(1) = 2 f(1);
+// w(r+1) FC(r-1) + 2(w(r)+w(r+1)) FC(r) + w(r) FC(r+1) = 3(w(r) f(r+1) + w(r+1) f(r));
+// FC(N-1)+FC(N) = 2 f(N).  On entry w[q], f[q] hold the layer weights (Hz, or
+// the 4-point u/v average) and values at cell c0-1+q (clamped to 1..N),
+// q = 0..n+1 and 0..n.  On exit fc[q] = FC(c0-1+q), q = 0..n. ----
+template <int KR>
+__device__ __forceinline__ void spline_fc_seg(const SegSpan& sg, int N, SegXchg& X, const double (&w)[KR + 1],
+                                              const double (&f)[KR], double (&fc)[KR]) {
+  const int c0 = sg.c0, n = sg.n;
+  const int ns = n + (sg.s == sg.S - 1 ? 1 : 0);   // the last segment also owns interface N
+  SegTri<KR> T;
+  T.eliminate(ns, [&](int q, double& a, double& bb, double& c, double& dd) {
+    const int r = c0 - 1 + q;
+    if (r == 0) { a = 0.0; bb = 1.0; c = 1.0; dd = 2.0 * f[1]; }
+    else if (r == N) { a = 1.0; bb = 1.0; c = 0.0; dd = 2.0 * f[q]; }
+    else {
+      a = w[q + 1]; bb = 2.0 * (w[q] + w[q + 1]); c = w[q];
+      dd = 3.0 * (w[q] * f[q + 1] + w[q + 1] * f[q]);
+    }
+  });
+  double xL, xR;
+  T.couple(sg, ns, X, xL, xR);
+  T.solve(ns, xL, xR);
+#pragma unroll
+  for (int q = 0; q < KR; q++)
+    if (q <= n) fc[q] = q < ns ? T.D[q] : xR;
+}
+
+// SPLINE_UV advective flux of a u (dir 0) / v (dir 1) column at interfaces
+// r = c0-1+q, q = 0..n (0 at the bottom and the surface): FC(r) * 0.5 * the
+// 4-point We average with the reference's masked curvature correction.
+template <int KR>
+__device__ __forceinline__ void uv_spline_seg(const Dev& d, const SegSpan& sg, SegXchg& X, long ij, int nrhs, int dir,
+                                              double (&fl)[KR]) {
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const int N = b.N, c0 = sg.c0, n = sg.n;
+  const long n2 = b.n2, s = dir == 0 ? 1 : b.nx2;
+  const double* __restrict__ Uv = (dir == 0 ? F.u : F.v) + (long)(nrhs - 1) * b.n3 + ij;
+  const double* __restrict__ Hz = F.Hz + ij;
+  const double* __restrict__ We = F.We + ij;
+  const double* mask = dir == 0 ? F.umask : F.vmask;
+  double dc[KR + 1], uu[KR];
+#pragma unroll
+  for (int q = 0; q < KR + 1; q++) {
+    const long L = (long)(min(max(c0 - 1 + q, 1), N) - 1) * n2;
+    if (q <= n + 1) dc[q] = 0.5625 * (Hz[L] + Hz[L - s]) - 0.0625 * (Hz[L + s] + Hz[L - 2 * s]);
+    if (q <= n && q < KR) uu[q] = Uv[L];
+  }
+  spline_fc_seg<KR>(sg, N, X, dc, uu, fl);
+  const double m1 = mask[ij + s], m0 = mask[ij - s];
+#pragma unroll
+  for (int q = 0; q < KR; q++) {
+    if (q <= n) {
+      const int r = c0 - 1 + q;
+      if (r == 0 || r == N) { fl[q] = 0.0; continue; }
+      const long w = (long)r * n2;
+      const double wf = We[w] + We[w - s] - 0.125 * ((We[w + s] - We[w]) * m1 - (We[w - s] - We[w - 2 * s]) * m0);
+      fl[q] = fl[q] * 0.5 * wf;
+    }
+  }
+}
+
+// SPLINE_TS advective flux FC(r)*We(r) of a tracer column at interfaces
+// r = c0-1+q, q = 0..n (0 at the bottom and the surface); hz, tt as w, f of
+// spline_fc_seg.
+template <int KR>
+__device__ __forceinline__ void tracer_spline_seg(const SegSpan& sg, int N, long n2, SegXchg& X,
+                                                  const double (&hz)[KR + 1], const double (&tt)[KR],
+                                                  const double* __restrict__ We, double (&fl)[KR]) {
+  spline_fc_seg<KR>(sg, N, X, hz, tt, fl);
+#pragma unroll
+  for (int q = 0; q < KR; q++) {
+    if (q <= sg.n) {
+      const int r = sg.c0 - 1 + q;
+      fl[q] = (r == 0 || r == N) ? 0.0 : fl[q] * We[(long)r * n2];
+    }
+  }
+}
+
+// Block prologue of the momentum column kernels: grid z = direction (0: u at
+// i >= istrU, 1: v at j >= jstrV), 16 columns per block row.  Lanes past the
+// column range solve a clamped duplicate column (they take part in the
+// barriers) and store nothing.  Returns false for a block with no v column.
+struct SegCol {
+  int i, j, dir;
+  bool act;
+};
+__device__ __forceinline__ bool seg_uv_col(const Dev& d, const Range& R, const uint3& bI, const SegSpan& sg,
+                                           SegCol& c) {
+  const Bounds& b = d.b;
+  c.dir = (int)bI.z;
+  c.j = R.j0 + (int)bI.y;
+  if (c.dir == 1 && c.j < b.jstrV) return false;   // uniform over the block
+  const int ilo = c.dir == 0 ? b.istrU : b.istr;
+  const int iu = R.i0 + (int)bI.x * kSegCW + sg.col;
+  c.act = iu >= ilo && iu <= R.i1;
+  c.i = iu < ilo ? ilo : (iu > R.i1 ? R.i1 : iu);
+  return true;
+}
+inline dim3 seg_grid_of(const Range& R, int nz) {
+  return dim3((R.i1 - R.i0 + kSegCW) / kSegCW, R.j1 - R.j0 + 1, nz);
+}
+
 }  // namespace roms

@@ -2,7 +2,7 @@
 // predictor for tracers and momentum to n+1/2, and the bottom-drag
 // coefficient r_D (compute_rd_bott_drag.h).  Also hosts the horizontal
 // momentum r.h.s. kernel shared with step3d_uv1 (UPSTREAM_UV flag).
-#include "k_common.h"
+#include "k_colseg.h"
 
 namespace roms {
 
@@ -272,6 +272,156 @@ __global__ void __launch_bounds__(64) k_pre_uv(Dev d, Range R, PreCoef c, int ns
   }
 }
 
+// ---- segment-partitioned variants (k_colseg.h) for deep grids: block =
+// 16 columns x S segments.  The spline reconstruction and the implicit
+// diffusion / viscosity are each one partitioned tridiagonal system whose
+// rows are those of k_pre_tracer_v / pre_uv_col (pre_step3d4S.F:198-489). ----
+__global__ void __launch_bounds__(128) k_pre_tracer_seg(Dev d, Range R, PreCoef c, int nnew, int nrhs) {
+  const uint3 bI = xcd_tile();
+  __shared__ SegXchg X;
+  constexpr int KR = kSegRows + 1;
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const int N = b.N;
+  const SegSpan sg = seg_span(N);
+  const int iu = R.i0 + (int)bI.x * kSegCW + sg.col;
+  const bool act = iu <= R.i1;
+  const int i = act ? iu : R.i1, j = R.j0 + (int)bI.y;
+  const int itrc = 1 + (int)bI.z;
+  const long n2 = b.n2, ij = IJ(b, i, j);
+  const int c0 = sg.c0, n = sg.n;
+  auto cell = [&](int k) { return (long)(k - 1) * n2; };
+  const double* __restrict__ Hz = F.Hz + ij;
+  const double* __restrict__ Hf = F.c2 + ij;   // Hz_fwd (k_pre_tracer_h)
+  const long tb = (long)(itrc - 1) * 3 * b.n3;
+  const double* __restrict__ Tr = F.t + (long)(nrhs - 1) * b.n3 + tb + ij;
+  double* __restrict__ Tn = F.t + (long)(nnew - 1) * b.n3 + tb + ij;
+  double hz[KR + 1], tt[KR], fl[KR];
+#pragma unroll
+  for (int q = 0; q < KR + 1; q++) {
+    const long L = cell(min(max(c0 - 1 + q, 1), N));
+    if (q <= n + 1) hz[q] = Hz[L];
+    if (q <= n && q < KR) tt[q] = Tr[L];
+  }
+  tracer_spline_seg<KR>(sg, N, n2, X, hz, tt, F.We + ij, fl);
+  // implicit diffusion on Hz_fwd, cells k = c0+p
+#pragma unroll
+  for (int q = 0; q < KR + 1; q++)
+    if (q <= n + 1) hz[q] = Hf[cell(min(max(c0 - 1 + q, 1), N))];
+  const int iAkt = itrc < b.nTS ? itrc : b.nTS;
+  const double* __restrict__ Akt = F.Akt + (long)(iAkt - 1) * b.n3w + ij;
+  const double* __restrict__ Wi = F.Wi + ij;
+  const double DC0 = c.dtau * F.pm[ij] * F.pn[ij];
+  auto fcw = [&](int q, double& fc, double& wc) {   // interface c0-1+q
+    const int r = c0 - 1 + q;
+    if (r <= 0 || r >= N) { fc = 0.0; wc = 0.0; return; }
+    fc = 2.0 * c.dtau * Akt[(long)r * n2] / (hz[q + 1] + hz[q]);
+    wc = DC0 * Wi[(long)r * n2];
+  };
+  double fcl, wcl;
+  fcw(0, fcl, wcl);
+  __syncthreads();  // X reused by the second coupling
+  SegTri<KR> T;
+  T.eliminate(n, [&](int p, double& a, double& bb, double& cc, double& dd) {
+    double fcu, wcu;
+    fcw(p + 1, fcu, wcu);
+    a = -(fcl + fmax0(wcl));
+    bb = hz[p + 1] + fcu + fmax0(wcu) + fcl - fmin0(wcl);
+    cc = -(fcu - fmin0(wcu));
+    dd = Tn[cell(c0 + p)] - c.dtau * F.pm[ij] * F.pn[ij] * (fl[p + 1] - fl[p]);
+    fcl = fcu; wcl = wcu;
+  });
+  double xL, xR;
+  T.couple(sg, n, X, xL, xR);
+  T.solve(n, xL, xR);
+  if (act) {
+#pragma unroll
+    for (int p = 0; p < KR; p++)
+      if (p < n) Tn[cell(c0 + p)] = T.D[p];
+  }
+}
+
+__global__ void __launch_bounds__(128) k_pre_uv_seg(Dev d, Range R, PreCoef c, int nstp, int nnew, int nrhs) {
+  const uint3 bI = xcd_tile();
+  __shared__ SegXchg X;
+  constexpr int KR = kSegRows + 1;
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const int N = b.N, indx = 3 - nstp;
+  const SegSpan sg = seg_span(N);
+  SegCol col;
+  if (!seg_uv_col(d, R, bI, sg, col)) return;
+  const int dir = col.dir;
+  const bool act = col.act;
+  const long n2 = b.n2, ij = IJ(b, col.i, col.j), s = dir == 0 ? 1 : b.nx2;
+  const int c0 = sg.c0, n = sg.n;
+  auto cell = [&](int k) { return (long)(k - 1) * n2; };
+  double fl[KR];
+  uv_spline_seg<KR>(d, sg, X, ij, nrhs, dir, fl);
+  double* Uall = dir == 0 ? F.u : F.v;
+  double* __restrict__ rr = (dir == 0 ? F.ru : F.rv) + ij;
+  const double* __restrict__ Ustp = Uall + (long)(nstp - 1) * b.n3 + ij;
+  double* __restrict__ Uidx = Uall + (long)(indx - 1) * b.n3 + ij;
+  double* __restrict__ Unew = Uall + (long)(nnew - 1) * b.n3 + ij;
+  const double* __restrict__ Hz = F.Hz + ij;
+  const double* __restrict__ Akv = F.Akv + ij;
+  const double* __restrict__ Wi = F.Wi + ij;
+  const double* __restrict__ Hf = F.c2 + ij;   // Hz_fwd, Hz_bak (k_pre_tracer_h)
+  const double* __restrict__ Hb = F.c3 + ij;
+  const double sstr = dir == 0 ? F.sustr[ij] : F.svstr[ij];
+  const double DC0 = c.dtau * 0.25 * (F.pm[ij] + F.pm[ij - s]) * (F.pn[ij] + F.pn[ij - s]);
+  double hf[KR + 1], hfm[KR + 1];   // Hz_fwd(c0-1+q) of the column and of its (i-1) / (j-1) neighbour
+#pragma unroll
+  for (int q = 0; q < KR + 1; q++) {
+    if (q <= n + 1) {
+      const long L = cell(min(max(c0 - 1 + q, 1), N));
+      hf[q] = Hf[L];
+      hfm[q] = Hf[L - s];
+    }
+  }
+  auto fcw = [&](int q, double& fc, double& wc) {   // interface c0-1+q
+    const int r = c0 - 1 + q;
+    if (r <= 0 || r >= N) { fc = 0.0; wc = 0.0; return; }
+    const long w = (long)r * n2;
+    fc = 2.0 * c.dtau * (Akv[w] + Akv[w - s]) / (hf[q + 1] + hfm[q + 1] + hf[q] + hfm[q]);
+    wc = DC0 * 0.5 * (Wi[w] + Wi[w - s]);
+  };
+  const double rd = F.r_D[ij], rdm = F.r_D[ij - s];
+  double fcl, wcl;
+  fcw(0, fcl, wcl);
+  __syncthreads();  // X reused by the second coupling
+  SegTri<KR> T;
+  T.eliminate(n, [&](int p, double& a, double& bb, double& cc, double& dd) {
+    double fcu, wcu;
+    fcw(p + 1, fcu, wcu);
+    const int k = c0 + p;
+    const long o = cell(k);
+    a = -(fcl + fmax0(wcl));
+    cc = -(fcu - fmin0(wcu));
+    if (k == 1) bb = 0.5 * (hf[p + 1] + hfm[p + 1]) + 0.5 * c.dtau * (rd + rdm) + fcu + fmax0(wcu);
+    else bb = 0.5 * (hf[p + 1] + hfm[p + 1]) + fcl - fmin0(wcl) + fcu + fmax0(wcu);
+    // ru(k) with the vertical advection (uv_rr_update), u(indx) = Hz*u(nstp)
+    const double r = k == 1 ? rr[o] - fl[1] : rr[o] - fl[p + 1] + fl[p];
+    const double us = Ustp[o];
+    double v = 0.5 * (Hb[o] + Hb[o - s]) * (c.cf_stp * us + c.cf_bak * Uidx[o]) + DC0 * r;
+    if (act) {
+      rr[o] = r;
+      Uidx[o] = 0.5 * (Hz[o] + Hz[o - s]) * us;
+    }
+    if (k == N) v = v + c.dtau * sstr;
+    dd = v;
+    fcl = fcu; wcl = wcu;
+  });
+  double xL, xR;
+  T.couple(sg, n, X, xL, xR);
+  T.solve(n, xL, xR);
+  if (act) {
+#pragma unroll
+    for (int p = 0; p < KR; p++)
+      if (p < n) Unew[cell(c0 + p)] = T.D[p];
+  }
+}
+
 void setup_column_kernels_t(size_t bytes);
 void setup_column_kernels_uv1(size_t bytes);
 bool setup_column_kernels(int N) {
@@ -298,7 +448,10 @@ void launch_pre_step3d(const Dev& d, hipStream_t s, const Tlev& t) {
   hipLaunchKernelGGL(k_pre_tracer_h, grid3_of(RH, b.N), dim3(kBX, kBY), 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs);
   dim3 gt = gridc_of(RI);
   gt.z = b.NT;
-  if (d.f.colscr)
+  if (d.p.colseg)
+    hipLaunchKernelGGL(k_pre_tracer_seg, seg_grid_of(RI, b.NT), dim3(kCX, seg_waves(b.N)), 0, s, d, RI, c, t.nnew,
+                       t.nrhs);
+  else if (d.f.colscr)
     hipLaunchKernelGGL(k_pre_tracer_v<ColGlb>, gt, dim3(kCX), 0, s, d, RI, c, t.nnew, t.nrhs);
   else
     hipLaunchKernelGGL(k_pre_tracer_v<ColLds>, gt, dim3(kCX), col_lds_bytes(2, b.N), s, d, RI, c, t.nnew, t.nrhs);
@@ -307,7 +460,10 @@ void launch_pre_step3d(const Dev& d, hipStream_t s, const Tlev& t) {
   hipLaunchKernelGGL(k_rd, grid_of(Rd), dim3(kBX, kBY), 0, s, d, Rd, t.nstp);
   dim3 gu = gridc_of(RI);
   gu.z = 2;
-  if (d.f.colscr)
+  if (d.p.colseg)
+    hipLaunchKernelGGL(k_pre_uv_seg, seg_grid_of(RI, 2), dim3(kCX, seg_waves(b.N)), 0, s, d, RI, c, t.nstp, t.nnew,
+                       t.nrhs);
+  else if (d.f.colscr)
     hipLaunchKernelGGL(k_pre_uv<ColGlb>, gu, dim3(kCX), 0, s, d, RI, c, t.nstp, t.nnew, t.nrhs);
   else
     hipLaunchKernelGGL(k_pre_uv<ColLds>, gu, dim3(kCX), col_lds_bytes(2, b.N), s, d, RI, c, t.nstp, t.nnew, t.nrhs);

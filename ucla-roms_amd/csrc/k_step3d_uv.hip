@@ -1,7 +1,7 @@
 // k_step3d_uv.hip -- corrector momentum: step3d_uv1 (step3d_uv1.F:23-534),
 // visc3d (visc3d_S.F:18-131) and the 2-D/3-D coupling step3d_uv2
 // (step3d_uv2.F:18-786, IMPLICIT_BOTTOM_DRAG branch).
-#include "k_common.h"
+#include "k_colseg.h"
 
 namespace roms {
 
@@ -84,6 +84,93 @@ __global__ void __launch_bounds__(64) k_uv1(Dev d, Range R, int nnew, int nrhs) 
   }
 }
 
+// ---- segment-partitioned variant of k_uv1 (k_colseg.h) for deep grids:
+// block = 16 columns x S segments, grid z = direction.  Spline advection and
+// the implicit viscosity are each one partitioned tridiagonal system with the
+// rows of uv1_col; the final ru(k) of every level go to LDS, from where the
+// first segment forms rufrc/rvfrc in the reference's k = 1..N order. ----
+struct SegRu {
+  double r[kSegRows * kSegMaxS][kSegCW];
+};
+__global__ void __launch_bounds__(128) k_uv1_seg(Dev d, Range R, int nnew, int nrhs) {
+  const uint3 bI = xcd_tile();
+  __shared__ SegXchg X;
+  __shared__ SegRu Sr;
+  constexpr int KR = kSegRows + 1;
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const int N = b.N;
+  const double dt = d.p.dt;
+  const SegSpan sg = seg_span(N);
+  SegCol col;
+  if (!seg_uv_col(d, R, bI, sg, col)) return;
+  const int dir = col.dir;
+  const bool act = col.act;
+  const long n2 = b.n2, ij = IJ(b, col.i, col.j), s = dir == 0 ? 1 : b.nx2;
+  const int c0 = sg.c0, n = sg.n;
+  auto cell = [&](int k) { return (long)(k - 1) * n2; };
+  double fl[KR];
+  uv_spline_seg<KR>(d, sg, X, ij, nrhs, dir, fl);
+  double* __restrict__ Un = (dir == 0 ? F.u : F.v) + (long)(nnew - 1) * b.n3 + ij;
+  double* __restrict__ rr = (dir == 0 ? F.ru : F.rv) + ij;
+  const double* __restrict__ Hz = F.Hz + ij;
+  const double* __restrict__ Akv = F.Akv + ij;
+  const double* __restrict__ Wi = F.Wi + ij;
+  const double sstr = dir == 0 ? F.sustr[ij] : F.svstr[ij];
+  const double DC0 = dt * 0.25 * (F.pm[ij] + F.pm[ij - s]) * (F.pn[ij] + F.pn[ij - s]);
+  double hz[KR + 1], hzm[KR + 1];   // Hz(c0-1+q) of the column and of its (i-1) / (j-1) neighbour
+#pragma unroll
+  for (int q = 0; q < KR + 1; q++) {
+    if (q <= n + 1) {
+      const long L = cell(min(max(c0 - 1 + q, 1), N));
+      hz[q] = Hz[L];
+      hzm[q] = Hz[L - s];
+    }
+  }
+  auto fcw = [&](int q, double& fc, double& wc) {   // interface c0-1+q
+    const int r = c0 - 1 + q;
+    if (r <= 0 || r >= N) { fc = 0.0; wc = 0.0; return; }
+    const long w = (long)r * n2;
+    fc = 2.0 * dt * (Akv[w] + Akv[w - s]) / (hz[q + 1] + hzm[q + 1] + hz[q] + hzm[q]);
+    wc = DC0 * 0.5 * (Wi[w] + Wi[w - s]);
+  };
+  const double rD = F.r_D[ij], rDm = F.r_D[ij - s];
+  double fcl, wcl;
+  fcw(0, fcl, wcl);
+  __syncthreads();  // X reused by the second coupling
+  SegTri<KR> T;
+  T.eliminate(n, [&](int p, double& a, double& bb, double& cc, double& dd) {
+    double fcu, wcu;
+    fcw(p + 1, fcu, wcu);
+    const int k = c0 + p;
+    const long o = cell(k);
+    a = -(fcl + fmax0(wcl));
+    cc = -(fcu - fmin0(wcu));
+    if (k == 1) bb = 0.5 * (hz[p + 1] + hzm[p + 1]) + 0.5 * dt * (rD + rDm) + fcu + fmax0(wcu);
+    else bb = 0.5 * (hz[p + 1] + hzm[p + 1]) + fcl - fmin0(wcl) + fcu + fmax0(wcu);
+    const double r = k == 1 ? rr[o] - fl[1] : rr[o] - fl[p + 1] + fl[p];   // uv_rr_update
+    if (act) rr[o] = r;
+    Sr.r[k - 1][sg.col] = r;
+    dd = Un[o] + DC0 * r;
+    if (k == N) dd = dd + dt * sstr;
+    fcl = fcu; wcl = wcu;
+  });
+  double xL, xR;
+  T.couple(sg, n, X, xL, xR);   // its barrier also publishes Sr
+  T.solve(n, xL, xR);
+  if (!act) return;
+#pragma unroll
+  for (int p = 0; p < KR; p++)
+    if (p < n) Un[cell(c0 + p)] = T.D[p] * 0.5 * (hz[p + 1] + hzm[p + 1]);
+  if (sg.s == 0) {
+    const double dmdn = dir == 0 ? F.dm_u[ij] * F.dn_u[ij] : F.dm_v[ij] * F.dn_v[ij];
+    double frc = Sr.r[0][sg.col] + dmdn * (sstr - 0.5 * (rDm + rD) * T.D[0]);
+    for (int k = 2; k <= N; k++) frc = frc + Sr.r[k - 1][sg.col];
+    if (dir == 0) F.rufrc[ij] = frc;
+    else F.rvfrc[ij] = frc;
+  }
+}
+
 void setup_column_kernels_uv1(size_t bytes) {
   (void)hipFuncSetAttribute((const void*)k_uv1<ColLds>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
@@ -94,7 +181,9 @@ void launch_step3d_uv1(const Dev& d, hipStream_t s, const Tlev& t) {
   Range R{b.istr, b.iend, b.jstr, b.jend};
   dim3 g = gridc_of(R);
   g.z = 2;
-  if (d.f.colscr)
+  if (d.p.colseg)
+    hipLaunchKernelGGL(k_uv1_seg, seg_grid_of(R, 2), dim3(kCX, seg_waves(b.N)), 0, s, d, R, t.nnew, t.nrhs);
+  else if (d.f.colscr)
     hipLaunchKernelGGL(k_uv1<ColGlb>, g, dim3(kCX), 0, s, d, R, t.nnew, t.nrhs);
   else
     hipLaunchKernelGGL(k_uv1<ColLds>, g, dim3(kCX), col_lds_bytes(2, b.N), s, d, R, t.nnew, t.nrhs);
