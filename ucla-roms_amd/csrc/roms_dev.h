@@ -32,7 +32,8 @@ struct Bounds {
 struct Params {
   int nonlin_eos, salinity, lmd, uv_vis2, ts_dif2;
   int s2d_split;  // 1: step2d as separate zeta / momentum kernels (ROMS_GPU_S2D_SPLIT=1)
-  int colseg;     // 1: segment-partitioned column solvers (k_colseg.h; N > 32, ROMS_GPU_COLSEG=0/1)
+  int colseg;     // 1: segment-partitioned column solvers (k_colseg.h; N > 63, ROMS_GPU_COLSEG=0/1)
+  int colreg;     // 1: register-resident column solvers where compiled for N (ROMS_GPU_COLREG=0 disables)
   int npip;       // pipe_frc.F: number of pipes (0: pipe_source off)
   int curvgrid;   // CURVGRID && UV_ADV: curvature terms (compute_horiz_rhs_uv_terms.h:8-11)
   int obc;        // open edges: 1 W, 2 E, 4 S, 8 N (Flather / Orlanski + *_FRC_BRY)
@@ -131,6 +132,16 @@ __device__ __forceinline__ uint3 xcd_tile() {
   t.z = logical / (gx * gy);
   return t;
 }
+
+// Compiler fence between the levels of a fully unrolled column walk: memory
+// operations are not moved across it, so the scheduler cannot hoist the loads
+// of all N levels to the top (which would need N x (loads per level)
+// registers and spill); a few levels of look-ahead remain within a chunk.
+#define ROMS_LEVEL_FENCE() __asm__ volatile("" ::: "memory")
+#ifndef ROMS_FENCE_EVERY
+#define ROMS_FENCE_EVERY 1000
+#endif
+#define ROMS_LEVEL_FENCE_AT(k) do { if ((k) % ROMS_FENCE_EVERY == 0) ROMS_LEVEL_FENCE(); } while (0)
 
 // 2-D launch over an inclusive index rectangle [i0,i1]x[j0,j1]: one lane per
 // (i,j) column, 64 consecutive i per wavefront (coalesced), 4 rows per block.

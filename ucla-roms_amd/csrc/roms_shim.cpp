@@ -315,6 +315,13 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     if (e && e[0] == '0') P.colseg = 0;
     if (e && e[0] == '1') P.colseg = dims->N <= kSegRows * kSegMaxS;
   }
+  // register-resident sequential solvers (bit-exact) for the depths they are
+  // compiled for; ROMS_GPU_COLREG=0 falls back to the LDS form (A/B runs)
+  P.colreg = 1;
+  {
+    const char* e = getenv("ROMS_GPU_COLREG");
+    if (e && e[0] == '0') P.colreg = 0;
+  }
   // column-solver scratch: LDS while two (N+1)-level slots per wave fit the
   // default 64 KB (N < 63), global memory for deeper grids;
   // ROMS_GPU_COL_GLOBAL=1/0 forces either (A/B runs)
