@@ -124,6 +124,16 @@ def test_decomposition_bitwise_equals_single_domain(kind, npx, npe):
     assert not bad, (kind, npx, npe, bad[:6])
 
 
+@pytest.mark.parametrize("kind", ["filament", "basin"])
+def test_fast_loop_overlap_bitwise(kind, monkeypatch):
+    """Opt-in fast-loop overlap (ROMS_GPU_S2D_OVERLAP=1): each fast step's
+    zeta/ubar/vbar exchange runs on a second stream while the next fast step's
+    interior tiles compute; the rim tiles join it.  The subdomains must still
+    equal the single-domain run bitwise."""
+    monkeypatch.setenv("ROMS_GPU_S2D_OVERLAP", "1")
+    test_decomposition_bitwise_equals_single_domain(kind, 2, 2)
+
+
 def test_filament_3x2_matches_golden_digits():
     """The reference's Filament benchmark runs on a 3x2 MPI grid; with the
     same per-rank pairwise sums and tree over ranks the GPU run prints the
@@ -182,8 +192,9 @@ print("RCCL_OK")
 """
 
 
-def test_rccl_transport_self_routed_equals_wrap():
-    env = dict(os.environ, ROMS_GPU_RCCL_SELF="1")
+@pytest.mark.parametrize("overlap", ["0", "1"])
+def test_rccl_transport_self_routed_equals_wrap(overlap):
+    env = dict(os.environ, ROMS_GPU_RCCL_SELF="1", ROMS_GPU_S2D_OVERLAP=overlap)
     r = subprocess.run([sys.executable, "-c", RCCL_SCRIPT, ROOT], env=env, capture_output=True, text=True,
                        timeout=300)
     assert r.returncode == 0 and "RCCL_OK" in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])

@@ -30,6 +30,13 @@ struct Halo {
   double* rbuf = nullptr;  // 8 x cap receive messages
   double* dred = nullptr;  // gather staging
   long cap = 0;
+  // fast-loop overlap (launch_step2d): exchange on a second stream while the
+  // next fast step's interior tiles run; `pending` = an exchange not yet
+  // joined back into the library stream
+  hipStream_t cs = nullptr;
+  hipEvent_t efork = nullptr, ejoin = nullptr;
+  int pending = 0;
+  int overlap = 0;  // 1: enabled (ROMS_GPU_S2D_OVERLAP=1; off by default, see halo_setup)
 };
 
 int comm_unique_id(void* out128);
@@ -45,6 +52,10 @@ void halo_free(Halo& H);
 bool halo_graph_safe(const Halo* H);
 long halo_map(const HaloPlan& P, int dir, int unpack, int* iv, int* jv);
 void halo_exchange(const Halo& H, hipStream_t s, const ExchList& L);
+// exchange L on H.cs after the work already queued on s (fork); halo_join
+// makes s wait for it.  Both are no-ops without a pending exchange.
+void halo_fork_exchange(Halo& H, hipStream_t s, const ExchList& L);
+void halo_join(Halo& H, hipStream_t s);
 int halo_allgather(const Halo& H, hipStream_t s, const double* in, int n, double* out);
 
 }  // namespace roms

@@ -205,6 +205,21 @@ int halo_setup(Halo& H, RomsComm* comm, const HaloPlan& plan, int maxlev, std::s
     err = "halo_setup: hipMalloc failed";
     return -2;
   }
+  if (hipStreamCreateWithFlags(&H.cs, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&H.efork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&H.ejoin, hipEventDisableTiming) != hipSuccess) {
+    err = "halo_setup: stream/event creation failed";
+    return -2;
+  }
+  H.pending = 0;
+  {
+    // measured on one MI355X with every exchange routed through RCCL: the
+    // overlap costs more than it hides (13.8 vs 12.9 ms/step at C2: the RCCL
+    // kernel competes with the interior tiles for CUs, and the fast step
+    // becomes two launches), so it is opt-in: ROMS_GPU_S2D_OVERLAP=1
+    const char* e = getenv("ROMS_GPU_S2D_OVERLAP");
+    H.overlap = e && e[0] == '1';
+  }
   if (comm && comm->kind == 2) {
     std::lock_guard<std::mutex> lk(comm->grp->m);
     comm->grp->sbuf[comm->rank] = H.sbuf;
@@ -217,6 +232,12 @@ void halo_free(Halo& H) {
   if (H.rbuf) (void)hipFree(H.rbuf);
   if (H.dred) (void)hipFree(H.dred);
   H.sbuf = H.rbuf = H.dred = nullptr;
+  if (H.efork) (void)hipEventDestroy(H.efork);
+  if (H.ejoin) (void)hipEventDestroy(H.ejoin);
+  if (H.cs) (void)hipStreamDestroy(H.cs);
+  H.efork = H.ejoin = nullptr;
+  H.cs = nullptr;
+  H.pending = 0;
 }
 
 // host copy of the pack (unpack=0) or unpack (unpack=1) index map of one direction
@@ -271,6 +292,20 @@ void halo_exchange(const Halo& H, hipStream_t s, const ExchList& L) {
     G->barrier();
   }
   hipLaunchKernelGGL(k_halo_unpack, grid, dim3(256), 0, s, g, L, H.rbuf, H.cap);
+}
+
+void halo_fork_exchange(Halo& H, hipStream_t s, const ExchList& L) {
+  halo_join(H, s);  // at most one exchange in flight
+  (void)hipEventRecord(H.efork, s);
+  (void)hipStreamWaitEvent(H.cs, H.efork, 0);
+  halo_exchange(H, H.cs, L);
+  (void)hipEventRecord(H.ejoin, H.cs);
+  H.pending = 1;
+}
+void halo_join(Halo& H, hipStream_t s) {
+  if (!H.pending) return;
+  (void)hipStreamWaitEvent(s, H.ejoin, 0);
+  H.pending = 0;
 }
 
 // out[r*n + q] = in_r[q] for every rank r (blocking)

@@ -10,6 +10,7 @@
 // momentum update ubar/vbar(knew), DU_avg1/DV_avg1.
 // Kernel C (closed edges only): u2dbc/v2dbc and the boundary flux averages.
 #include "roms_dev.h"
+#include "halo.h"
 
 namespace roms {
 
@@ -230,8 +231,14 @@ struct FBTile {
 };
 
 template <bool kPipe>
-__global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int closed, int vwrap) {
+__global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int closed, int vwrap, int part) {
   const uint3 bI = xcd_tile();
+  // part 1: interior tiles only (their windows hold no halo cell), 2: the rim
+  // tiles, 0: all (see the fast-loop overlap in launch_step2d)
+  if (part) {
+    const bool rim = bI.x == 0 || bI.x + 1 == gridDim.x || bI.y == 0 || bI.y + 1 == gridDim.y;
+    if (rim != (part == 2)) return;
+  }
   __shared__ FBTile T;
   const Bounds& b = d.b;
   const Fields& F = d.f;
@@ -773,6 +780,7 @@ void launch_step2d(const Dev& d, hipStream_t s, const Tlev& t, const double* w1,
   c.w2 = w2[t.iif - 1];
   const bool closed = b.west_edge || b.east_edge || b.south_edge || b.north_edge;
   Range RB{b.istrR, b.iendR, b.jstrR, b.jendR};
+  Halo* H = const_cast<Halo*>(d.halo);   // multi-rank exchange state (host bookkeeping)
   // single rank (no halo exchange object) with the fused kernel: periodic
   // halos of the fast-time fields are read through their images
   const int vwrap = (d.halo == nullptr && !d.p.s2d_split) ? (b.ew_periodic ? 1 : 0) | (b.ns_periodic ? 2 : 0) : 0;
@@ -786,10 +794,21 @@ void launch_step2d(const Dev& d, hipStream_t s, const Tlev& t, const double* w1,
     }
     hipLaunchKernelGGL(k_s2d_mom, grid_of(RB), dim3(kBX, kBY), 0, s, d, RB, c);
   } else {
-    if (d.p.npip > 0)
-      hipLaunchKernelGGL(k_s2d_fb<true>, grid_of(RB), dim3(kBX, kBY), 0, s, d, RB, c, (int)closed, vwrap);
-    else
-      hipLaunchKernelGGL(k_s2d_fb<false>, grid_of(RB), dim3(kBX, kBY), 0, s, d, RB, c, (int)closed, vwrap);
+    auto fb = [&](int part) {
+      if (d.p.npip > 0)
+        hipLaunchKernelGGL(k_s2d_fb<true>, grid_of(RB), dim3(kBX, kBY), 0, s, d, RB, c, (int)closed, vwrap, part);
+      else
+        hipLaunchKernelGGL(k_s2d_fb<false>, grid_of(RB), dim3(kBX, kBY), 0, s, d, RB, c, (int)closed, vwrap, part);
+    };
+    if (H && H->pending) {
+      // the previous fast step's zeta/ubar/vbar(knew) exchange is still in
+      // flight on the halo stream: interior tiles first, the rim after it
+      fb(1);
+      halo_join(*H, s);
+      fb(2);
+    } else {
+      fb(0);
+    }
   }
   if (closed) {
     const int L = b.nx2 > b.Mm + 4 ? b.nx2 : b.Mm + 4;
@@ -809,7 +828,14 @@ void launch_step2d(const Dev& d, hipStream_t s, const Tlev& t, const double* w1,
     return;
   }
   const long kn = (long)(t.knew - 1) * b.n2;
-  launch_exchange_list(d, s, ExchList{{d.f.zeta + kn, d.f.ubar + kn, d.f.vbar + kn}, {1, 1, 1}, 3});
+  const ExchList L{{d.f.zeta + kn, d.f.ubar + kn, d.f.vbar + kn}, {1, 1, 1}, 3};
+  if (H && H->overlap && t.iif < t.nfast && !d.p.s2d_split) {
+    // overlap the exchange with the next fast step's interior tiles; that
+    // step joins it before its rim tiles (the last fast step never forks)
+    halo_fork_exchange(*H, s, L);
+    return;
+  }
+  launch_exchange_list(d, s, L);
 }
 
 }  // namespace roms

@@ -80,12 +80,19 @@ void rank_extent(int LL, int np, int node, int& len, int& sw) {
     }                                                                                 \
   } while (0)
 
-#define REQUIRE_INIT()                                  \
+#define REQUIRE_INIT_NOJOIN()                           \
   do {                                                  \
     if (!g.inited) {                                    \
       g.err = "roms_gpu: not initialised";              \
       return -1;                                        \
     }                                                   \
+  } while (0)
+// every entry but step2d first joins a fast-loop exchange still in flight on
+// the halo stream (launch_step2d overlaps it with the next fast step)
+#define REQUIRE_INIT()                                  \
+  do {                                                  \
+    REQUIRE_INIT_NOJOIN();                              \
+    if (g.d.halo) halo_join(g.halo, g.s);               \
   } while (0)
 
 int post_launch() {
@@ -456,12 +463,18 @@ ROUTINE(roms_gpu_pre_step3d, launch_pre_step3d(g.d, g.s, T))
 ROUTINE(roms_gpu_set_huv1, launch_set_huv1(g.d, g.s, T))
 ROUTINE(roms_gpu_step3d_uv1, launch_step3d_uv1(g.d, g.s, T))
 ROUTINE(roms_gpu_visc3d, launch_visc3d(g.d, g.s, T))
-ROUTINE(roms_gpu_step2d, launch_step2d(g.d, g.s, T, g.w1, g.w2))
 ROUTINE(roms_gpu_step3d_uv2, launch_step3d_uv2(g.d, g.s, T))
 ROUTINE(roms_gpu_step3d_t, launch_step3d_t(g.d, g.s, T))
 ROUTINE(roms_gpu_t3dmix, launch_t3dmix(g.d, g.s, T))
 ROUTINE(roms_gpu_set_depth, launch_set_depth(g.d, g.s, T))
 #undef ROUTINE
+
+int roms_gpu_step2d(const roms_tlev* t) {
+  REQUIRE_INIT_NOJOIN();   // keeps the previous fast step's exchange in flight
+  const Tlev T = to_tlev(t);
+  launch_step2d(g.d, g.s, T, g.w1, g.w2);
+  return post_launch();
+}
 
 int roms_gpu_rho_eos(int tidx, const roms_tlev* t) {
   REQUIRE_INIT();
