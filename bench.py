@@ -13,10 +13,11 @@ grid (1x1, 2x1, 2x2, 4x2, ...) of 512x512 subdomains of one periodic domain;
 halo exchanges go over RCCL (xGMI) inside the step graphs.
 
 value = grid-cell updates per second summed over ranks; model seconds per
-wall second beside it.  roofline: per-routine algorithmic bytes (SURVEY.md
-8(d) pass counts) / mean launch duration measured with HIP events on the
-library stream; the dominant routine (largest time per step) is reported,
-the full table under "routines".
+wall second beside it.  roofline: algorithmic bytes (SURVEY.md 8(d) pass
+counts) / mean launch duration measured with HIP events on the library
+stream, for the dominant kernel (C2: k_s2d_fb, one fast step, 35 2-D passes;
+C3: its routine pre_step3d); "roofline_routine" is the dominant routine and
+"routines" the full per-routine table.
 
 --workload c3 (not the default): SURVEY.md 8(d) C3, the 1024x1024x100 closed
 basin with NONLIN+SPLIT EOS, T+S and LMD/KPP/BKPP mixing (dt=300 s, nfast=82),
@@ -120,6 +121,19 @@ def cpu_baseline(nsteps=3):
             "model_seconds_per_wallclock_sec": nsteps * DT / dt_wall}
 
 
+def pmc_kernel_traffic(kernel):
+    """HBM bytes per dispatch of one kernel from profiles/pmc_traffic.json
+    (2*FETCH_SIZE + WRITE_SIZE), or None when absent."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        k = json.load(open(p)).get("kernels", {}).get(kernel)
+        return None if k is None else float(k["traffic_bytes"]) / float(k["dispatches"])
+    except (ValueError, KeyError, TypeError, ZeroDivisionError):
+        return None
+
+
 def pmc_traffic(routine):
     """HBM bytes per launch of `routine` from the committed rocprofv3 PMC
     summary (profiles/pmc_traffic.json, FETCH_SIZE*2 + WRITE_SIZE per
@@ -216,7 +230,7 @@ def main():
     passes = routine_passes(NT, NT_TS, lmd=c3)
     routines = {}
     for r in romsgpu.ROUTINES:
-        if passes[r] == 0:
+        if passes.get(r, 0) == 0:   # kernel-level ids and routines off in this workload
             continue
         avg, n = m.time_routine(r, args.timing_steps)
         per_step = n / args.timing_steps
@@ -226,6 +240,15 @@ def main():
                        "bytes_per_call": nbytes, "achieved_GBs": gbs, "frac": gbs / HBM_PEAK_GBS}
     dom = max(routines, key=lambda k: routines[k]["ms_per_step"])
     D = routines[dom]
+    # the fused barotropic kernel alone (HIP events around its launches only):
+    # 35 2-D passes per fast step over its launch time
+    # (one event interval per fast loop on a single rank: 82 back-to-back launches)
+    fb_ms, fb_n = m.time_routine("k_s2d_fb", args.timing_steps)
+    fb_bytes = 35.0 * 8 * Lr * Mr
+    fb_gbs = fb_bytes / (fb_ms * 1e-3) / 1e9 if fb_ms > 0 else 0.0
+    kernel_fb = {"kernel": "k_s2d_fb", "ms_per_launch": fb_ms, "launches_per_step": fb_n / args.timing_steps,
+                 "ms_per_step": fb_ms * fb_n / args.timing_steps, "bytes_per_launch": fb_bytes,
+                 "achieved_GBs": fb_gbs, "frac": fb_gbs / HBM_PEAK_GBS}
 
     # sanity: the run must stay finite (blow-up check as diag.F does)
     norms = m.diag()
@@ -237,6 +260,18 @@ def main():
     step_gbs = B / (ms_step * 1e-3) / 1e9
     traffic = None if c3 else pmc_traffic(dom)   # profiles/pmc_traffic.json is measured on C2
 
+    if not c3:
+        # C2: the dominant kernel (largest time per step in the kernel-trace
+        # table, profiles/r1_p4_c2_per_step.txt) is the fused barotropic kernel
+        roofline = {"bound": "hbm", "achieved": fb_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": fb_gbs / HBM_PEAK_GBS, "traffic": pmc_kernel_traffic("k_s2d_fb"),
+                    "kernel": "k_s2d_fb", "bytes_per_launch": fb_bytes, "ms_per_launch": fb_ms}
+    else:
+        # C3: the dominant kernel is k_pre_uv_seg (profiles/r1_p4_c3_per_step.txt),
+        # timed with the rest of its routine (pre_step3d)
+        roofline = {"bound": "hbm", "achieved": D["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": D["frac"], "traffic": None, "kernel": dom + " (routine)",
+                    "bytes_per_launch": D["bytes_per_call"], "ms_per_launch": D["ms_per_call"]}
     out = {
         "metric": "grid-cell-updates/sec",
         "value": (C3_L * C3_L * C3_N if c3 else world * cells3) * args.steps / elapsed,
@@ -257,13 +292,15 @@ def main():
                    "grid_per_gpu": [Lr, Mr, Nz], "proc_grid": [npx, npe], "NT": NT, "dt": dt_step, "nfast": nfast,
                    "parallelism": "domain decomposition %dx%d, RCCL halo exchange" % (npx, npe)},
         "model_seconds_per_wallclock_sec": args.steps * dt_step / elapsed,
-        "roofline": {"bound": "hbm", "achieved": D["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": D["frac"], "traffic": traffic,
-                     "kernel": dom + (" (one fast step: k_s2d_zeta + k_s2d_mom + halo)" if dom == "step2d" else ""),
-                     "bytes_per_launch": D["bytes_per_call"], "ms_per_launch": D["ms_per_call"]},
+        "roofline": roofline,
+        "roofline_routine": {"bound": "hbm", "achieved": D["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": D["frac"], "traffic": traffic,
+                             "routine": dom + (" (one fast step: k_s2d_fb + edges + halo)" if dom == "step2d" else ""),
+                             "bytes_per_launch": D["bytes_per_call"], "ms_per_launch": D["ms_per_call"]},
         "roofline_step": {"bound": "hbm", "achieved": step_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                           "frac": step_gbs / HBM_PEAK_GBS, "bytes_per_step": B},
         "routines": routines,
+        "kernel_s2d_fb": kernel_fb,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_c3() if c3 else cpu_baseline()

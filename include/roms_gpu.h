@@ -199,7 +199,9 @@ int roms_gpu_time_steps(roms_tlev *t, int n, double *ms);
 enum roms_routine {
   ROMS_R_RHO_EOS = 0, ROMS_R_SET_HUV, ROMS_R_OMEGA, ROMS_R_PRSGRD, ROMS_R_PRE_STEP3D, ROMS_R_SET_HUV1,
   ROMS_R_STEP3D_UV1, ROMS_R_VISC3D, ROMS_R_STEP2D, ROMS_R_STEP3D_UV2, ROMS_R_STEP3D_T, ROMS_R_T3DMIX,
-  ROMS_R_LMD_VMIX, ROMS_R_COUNT
+  ROMS_R_LMD_VMIX,
+  ROMS_R_K_S2D_FB,  /* kernel level: the fused barotropic kernel k_s2d_fb alone (one fast step) */
+  ROMS_R_COUNT
 };
 int roms_gpu_time_routine(int routine, int nsteps, roms_tlev *t, double *avg_ms, long *launches);
 

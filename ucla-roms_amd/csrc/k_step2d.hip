@@ -800,6 +800,10 @@ void launch_step2d(const Dev& d, hipStream_t s, const Tlev& t, const double* w1,
       else
         hipLaunchKernelGGL(k_s2d_fb<false>, grid_of(RB), dim3(kBX, kBY), 0, s, d, RB, c, (int)closed, vwrap, part);
     };
+    // kernel-level timing: one interval per fast loop when nothing else runs
+    // between the fused kernels (single rank, no closed edges), else one per launch
+    const bool span = d.halo == nullptr && !closed;
+    if (!span || t.iif == 1) ktimer_mark(s, kTimedS2dFb, 0);
     if (H && H->pending) {
       // the previous fast step's zeta/ubar/vbar(knew) exchange is still in
       // flight on the halo stream: interior tiles first, the rim after it
@@ -809,6 +813,8 @@ void launch_step2d(const Dev& d, hipStream_t s, const Tlev& t, const double* w1,
     } else {
       fb(0);
     }
+    if (!span) ktimer_mark(s, kTimedS2dFb, 1, 1);
+    else if (t.iif == t.nfast) ktimer_mark(s, kTimedS2dFb, 1, t.nfast);
   }
   if (closed) {
     const int L = b.nx2 > b.Mm + 4 ? b.nx2 : b.Mm + 4;

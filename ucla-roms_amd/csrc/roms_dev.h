@@ -190,6 +190,12 @@ struct Tlev {
   int iic, ntstart, forw_start, iif, nfast, kstp, knew, nstp, nrhs, nnew;
 };
 
+// kernel-level timing hook (roms_gpu_time_routine with a kernel id): HIP
+// events on the launch stream opening (end = 0) and closing (end = 1) an
+// interval that covers `count` launches of one kernel
+constexpr int kTimedS2dFb = 13;   // ROMS_R_K_S2D_FB
+void ktimer_mark(hipStream_t s, int kernel_id, int end, int count = 0);
+
 void launch_exchange(const Dev& d, hipStream_t s, double* a, int nlev);
 // several arrays in one launch (one reference exchange_xxx(A,B,C,D) call)
 struct ExchList {

@@ -47,6 +47,7 @@ struct Ctx {
   int timed = -1;
   std::vector<hipEvent_t> ev;
   size_t nev = 0;
+  long kcount = 0;   // kernel-level timing: launches covered by the intervals
 };
 // One context per host thread: a process normally drives one GPU/subdomain
 // from one thread; tests drive several subdomains from threads of one process.
@@ -225,6 +226,19 @@ Tlev to_tlev(const roms_tlev* t) {
     stmt;                                                                   \
     if (on_) { (void)hipEventRecord(g.ev[g.nev + 1], s); g.nev += 2; }      \
   } while (0)
+
+}  // namespace
+void roms::ktimer_mark(hipStream_t s, int id, int end, int count) {
+  if (g.timed != id) return;
+  if (!end) {
+    if (g.nev + 2 <= g.ev.size()) (void)hipEventRecord(g.ev[g.nev], s);
+  } else if (g.nev + 2 <= g.ev.size()) {
+    (void)hipEventRecord(g.ev[g.nev + 1], s);
+    g.nev += 2;
+    g.kcount += count;
+  }
+}
+namespace {
 
 // the roms_step sequence for one step whose indices are already set in *t
 // (nstp,nrhs=nstp,nnew=3 on entry); enqueues everything on g.s
@@ -728,6 +742,7 @@ int roms_gpu_time_routine(int routine, int nsteps, roms_tlev* t, double* avg_ms,
   }
   g.timed = routine;
   g.nev = 0;
+  g.kcount = 0;
   // eager steps (no graph), same launches and stream as the graph replays
   for (int q = 0; q < nsteps; q++) {
     t->iic = t->iic + 1;
@@ -747,6 +762,10 @@ int roms_gpu_time_routine(int routine, int nsteps, roms_tlev* t, double* avg_ms,
   }
   *launches = (long)(g.nev / 2);
   *avg_ms = g.nev ? tot / (double)(g.nev / 2) : 0.0;
+  if (g.kcount > 0) {   // kernel level: intervals span several launches
+    *launches = g.kcount;
+    *avg_ms = tot / (double)g.kcount;
+  }
   return post_launch();
 }
 

@@ -162,7 +162,8 @@ def halo_map(Lm, Mm, np_xi, np_eta, inode, jnode, ew_periodic, ns_periodic, dire
 HALO_DIRS = ("W", "E", "S", "N", "SW", "SE", "NW", "NE")
 # enum roms_routine of include/roms_gpu.h
 ROUTINES = ("rho_eos", "set_HUV", "omega", "prsgrd", "pre_step3d", "set_HUV1", "step3d_uv1", "visc3d", "step2d",
-            "step3d_uv2", "step3d_t", "t3dmix", "lmd_vmix")
+            "step3d_uv2", "step3d_t", "t3dmix", "lmd_vmix",
+            "k_s2d_fb")  # kernel level: the fused barotropic kernel alone
 HALO_OPP = (1, 0, 3, 2, 7, 6, 5, 4)
 
 
