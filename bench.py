@@ -250,6 +250,7 @@ def main():
                  "ms_per_step": fb_ms * fb_n / args.timing_steps, "bytes_per_launch": fb_bytes,
                  "achieved_GBs": fb_gbs, "frac": fb_gbs / HBM_PEAK_GBS}
 
+    transport = m.halo_transport() if comm is not None else "none (single rank)"
     # sanity: the run must stay finite (blow-up check as diag.F does)
     norms = m.diag()
     if not all(map(lambda x: x == x and abs(x) < 1e30, norms)):
@@ -290,7 +291,7 @@ def main():
                                 "(nfast=%d)" % nfast) if c3 else
                                "C2: Filament+S 512x512x50 per GPU, NT=2, dt=5s, ndtfast=60 (nfast=%d)" % nfast,
                    "grid_per_gpu": [Lr, Mr, Nz], "proc_grid": [npx, npe], "NT": NT, "dt": dt_step, "nfast": nfast,
-                   "parallelism": "domain decomposition %dx%d, RCCL halo exchange" % (npx, npe)},
+                   "parallelism": "domain decomposition %dx%d" % (npx, npe), "halo_transport": transport},
         "model_seconds_per_wallclock_sec": args.steps * dt_step / elapsed,
         "roofline": roofline,
         "roofline_routine": {"bound": "hbm", "achieved": D["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -179,6 +179,11 @@ int roms_gpu_comm_unique_id(void *id128);
 int roms_gpu_comm_create(const void *id128, int nranks, int rank, int device, void **comm);
 int roms_gpu_comm_create_local(int group, int nranks, int rank, void **comm);
 int roms_gpu_comm_destroy(void *comm);
+/* Halo transport of this rank after roms_gpu_init: 0 = RCCL send/recv (or
+ * single rank / in-process), 1 = IPC peer writes (enabled after a start-up
+ * self-test against RCCL; ROMS_GPU_HALO_IPC=0 disables), -1 = IPC with a
+ * timed-out arrival wait since init.                                        */
+int roms_gpu_halo_transport(void);
 /* Host-only: neighbour ranks (-1 none), per-level message sizes for the 8
  * directions W,E,S,N,SW,SE,NW,NE, and the strip extents {i0,i1,j0,j1}.      */
 int roms_gpu_halo_plan(int Lm, int Mm, int np_xi, int np_eta, int inode, int jnode, int ew_periodic,

@@ -1,6 +1,7 @@
 // halo.h -- multi-rank halo exchange and cross-rank gathers (halo.hip).
 #pragma once
 #include <string>
+#include <vector>
 
 #include "roms_dev.h"
 
@@ -23,6 +24,28 @@ struct HaloPlan {
 };
 
 struct RomsComm;  // opaque communicator handle of the C ABI
+
+// IPC transport (one process per GPU over an RCCL communicator): the pack
+// kernel writes each message straight into the neighbour's receive buffer
+// (IPC-mapped, uncached, double-buffered by exchange parity) and its last
+// block raises the neighbour's arrival counter (system-scope release); a
+// one-block kernel waits for the counters of this rank's receive slots
+// (acquire, bounded spin), then unpack.  Enabled only after a start-up
+// self-test reproduced the RCCL exchange bitwise on every rank.
+struct HaloIpc {
+  double* rbuf2 = nullptr;              // [2 parities][8 slots][cap], written by the neighbours
+  unsigned long long* flags = nullptr;  // [8] messages received per slot
+  unsigned int* cnt = nullptr;          // [8] pack-block counters (last block signals), [8]: receive blocks
+  unsigned long long* seq = nullptr;    // exchanges completed by this rank
+  int* err = nullptr;                   // set when a wait timed out
+  double* prbuf[8] = {};                // direction d's neighbour: its rbuf2
+  unsigned long long* pflags[8] = {};   // ... and its flags
+  std::vector<void*> opened;            // IPC mappings to close
+  long long timeout_ticks = 0;          // wall_clock64 ticks before a wait gives up
+  int fused_recv = 0;                   // wait + unpack in one kernel (k_halo_recv_ipc, opt-in)
+  int ok = 0;
+};
+
 struct Halo {
   RomsComm* comm = nullptr;
   HaloPlan plan{};
@@ -36,6 +59,7 @@ struct Halo {
   hipStream_t cs = nullptr;
   hipEvent_t efork = nullptr, ejoin = nullptr;
   int pending = 0;
+  HaloIpc ipc;
   int overlap = 0;  // 1: enabled (ROMS_GPU_S2D_OVERLAP=1; off by default, see halo_setup)
 };
 
@@ -57,5 +81,7 @@ void halo_exchange(const Halo& H, hipStream_t s, const ExchList& L);
 void halo_fork_exchange(Halo& H, hipStream_t s, const ExchList& L);
 void halo_join(Halo& H, hipStream_t s);
 int halo_allgather(const Halo& H, hipStream_t s, const double* in, int n, double* out);
+// 1 if the IPC transport is in use, 0 if RCCL; -1 if a wait timed out since setup
+int halo_transport(const Halo& H);
 
 }  // namespace roms

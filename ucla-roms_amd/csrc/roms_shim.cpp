@@ -483,6 +483,11 @@ ROUTINE(roms_gpu_t3dmix, launch_t3dmix(g.d, g.s, T))
 ROUTINE(roms_gpu_set_depth, launch_set_depth(g.d, g.s, T))
 #undef ROUTINE
 
+int roms_gpu_halo_transport(void) {
+  REQUIRE_INIT();
+  return g.d.halo ? halo_transport(g.halo) : 0;
+}
+
 int roms_gpu_step2d(const roms_tlev* t) {
   REQUIRE_INIT_NOJOIN();   // keeps the previous fast step's exchange in flight
   const Tlev T = to_tlev(t);

@@ -321,6 +321,11 @@ class Model:
                                                ctypes.byref(n)), "time_routine")
         return ms.value, n.value
 
+    def halo_transport(self):
+        """'ipc', 'rccl' (or single rank / in-process), or 'ipc-timeout'."""
+        r = self.L.roms_gpu_halo_transport()
+        return {1: "ipc", 0: "rccl", -1: "ipc-timeout"}.get(r, "error")
+
     def diag(self):
         out = (ctypes.c_double * 4)()
         self._chk(self.L.roms_gpu_diag(ctypes.byref(self.t), out), "diag")
