@@ -210,7 +210,7 @@ __global__ void __launch_bounds__(64, 2) k_uv1_reg(Dev d, Range R, int nnew, int
 struct SegRu {
   double r[kSegRows * kSegMaxS][kSegCW];
 };
-__global__ void __launch_bounds__(128) k_uv1_seg(Dev d, Range R, int nnew, int nrhs) {
+__global__ void __launch_bounds__(kSegBlock) k_uv1_seg(Dev d, Range R, int nnew, int nrhs) {
   const uint3 bI = xcd_tile();
   __shared__ SegXchg X;
   __shared__ SegRu Sr;

@@ -165,8 +165,15 @@ inline dim3 grid3_of(const Range& r, int nk) {
 // block row; column scratch lives in LDS (see ColLds in k_common.h).
 constexpr int kCX = 64;
 // segment-partitioned column solvers (k_colseg.h)
-constexpr int kSegRows = 13;   // cells per segment (register arrays of kSegRows + 2)
-constexpr int kSegMaxS = 8;    // segments (wavefronts) per block: N <= 104
+#ifndef ROMS_SEG_ROWS
+#define ROMS_SEG_ROWS 13
+#endif
+#ifndef ROMS_SEG_MAXS
+#define ROMS_SEG_MAXS 8
+#endif
+constexpr int kSegRows = ROMS_SEG_ROWS;   // cells per segment (register arrays of kSegRows + 2)
+constexpr int kSegMaxS = ROMS_SEG_MAXS;   // segments per block (16 columns each): N <= kSegRows * kSegMaxS
+constexpr int kSegBlock = ((kSegMaxS * 16 + 63) / 64) * 64;   // threads of a segment-solver block (max)
 inline dim3 gridc_of(const Range& r) {
   int ni = r.i1 - r.i0 + 1, nj = r.j1 - r.j0 + 1;
   if (ni < 1) ni = 1;
