@@ -108,30 +108,46 @@ struct IpcPtrs {
   int* err;
   long long timeout;
 };
-// pack straight into the neighbour's slot opp(d) of parity seq&1; the last
-// block of direction d raises that neighbour's counter for the slot
+// pack straight into the neighbour's slot opp(d) of parity seq&1
+#ifndef ROMS_IPC_SYSFENCE
+#define ROMS_IPC_SYSFENCE 0
+#endif
+// The messages are uncached stores (no L2 copy to write back), so ordering
+// them before the arrival counters needs no cache maintenance: each block
+// waits for its own stores to complete, counts itself, and the last block of
+// the grid raises the neighbours' counters.  (With a system-scope fence per
+// block -- an L2 write-back each -- a pack launch measured 54 us.)
 __global__ void __launch_bounds__(256) k_halo_pack_ipc(HaloGeom g, ExchList L, IpcPtrs P, long cap) {
   const int dir = blockIdx.z;
-  if (!g.active[dir]) return;   // uniform over the direction's blocks
-  const long cnt = g.cnt[dir];
-  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const unsigned long long par = *P.seq & 1ull;
-  int lev = blockIdx.y;
-  const int q = list_slot(L, lev);
-  if (e < cnt && lev < L.nlev[q]) {
-    int i, j;
-    halo_src(g, dir, e, i, j);
-    P.prbuf[dir][((long)par * 8 + kOpp[dir]) * cap + (long)blockIdx.y * cnt + e] =
-        L.p[q][(long)(i + 1) + (long)(j + 1) * g.nx2 + (long)lev * g.n2];
+  if (g.active[dir]) {
+    const long cnt = g.cnt[dir];
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const unsigned long long par = *P.seq & 1ull;
+    int lev = blockIdx.y;
+    const int q = list_slot(L, lev);
+    if (e < cnt && lev < L.nlev[q]) {
+      int i, j;
+      halo_src(g, dir, e, i, j);
+      P.prbuf[dir][((long)par * 8 + kOpp[dir]) * cap + (long)blockIdx.y * cnt + e] =
+          L.p[q][(long)(i + 1) + (long)(j + 1) * g.nx2 + (long)lev * g.n2];
+    }
   }
-  __threadfence_system();   // this block's remote writes before its count
+  // this block's (uncached) stores complete before its count: a wait on the
+  // store counter only -- an agent/system fence would also write back and
+  // invalidate the L2 (buffer_wbl2/buffer_inv), which the payload never uses
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   if (threadIdx.x == 0) {
-    const unsigned nb = gridDim.x * gridDim.y;
-    if (atomicAdd(&P.cnt[dir], 1u) == nb - 1) {   // every block of direction dir is done
-      P.cnt[dir] = 0;
+    const unsigned nb = gridDim.x * gridDim.y * gridDim.z;
+    if (atomicAdd(&P.cnt[0], 1u) == nb - 1) {   // every block of the grid is done
+      P.cnt[0] = 0;
+#if ROMS_IPC_SYSFENCE
       __threadfence_system();
-      __hip_atomic_fetch_add(P.pflags[dir] + kOpp[dir], 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+#endif
+      for (int d = 0; d < 8; d++)
+        if (g.active[d])
+          __hip_atomic_fetch_add(P.pflags[d] + kOpp[d], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }
