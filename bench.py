@@ -263,12 +263,12 @@ def main():
 
     if not c3:
         # C2: the dominant kernel (largest time per step in the kernel-trace
-        # table, profiles/r1_p4_c2_per_step.txt) is the fused barotropic kernel
+        # table, profiles/r1_p5_c2_per_step.txt) is the fused barotropic kernel
         roofline = {"bound": "hbm", "achieved": fb_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": fb_gbs / HBM_PEAK_GBS, "traffic": pmc_kernel_traffic("k_s2d_fb"),
                     "kernel": "k_s2d_fb", "bytes_per_launch": fb_bytes, "ms_per_launch": fb_ms}
     else:
-        # C3: the dominant kernel is k_pre_uv_seg (profiles/r1_p4_c3_per_step.txt),
+        # C3: the dominant kernel is k_pre_uv_seg (profiles/r1_p5_c3_per_step.txt),
         # timed with the rest of its routine (pre_step3d)
         roofline = {"bound": "hbm", "achieved": D["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": D["frac"], "traffic": None, "kernel": dom + " (routine)",
