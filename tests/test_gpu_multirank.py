@@ -182,7 +182,12 @@ m.close()
 uid = romsgpu.comm_unique_id()
 h = romsgpu.comm_create(uid, 1, 0, 0)
 m = romsgpu.Model.from_case(np_xi=1, np_eta=1, comm=h, rank=0, **case)
+want = os.environ.get("ROMS_EXPECT_TRANSPORT")
+if want:
+    assert m.halo_transport() == want, m.halo_transport()
 m.step(4)
+if want:
+    assert m.halo_transport() == want, m.halo_transport()   # no timed-out wait during the run
 for f, v in ref.items():
     g = m.get(f)
     assert np.array_equal(g[..., 1:-1, 1:-1], v[..., 1:-1, 1:-1]), f
@@ -192,9 +197,14 @@ print("RCCL_OK")
 """
 
 
-@pytest.mark.parametrize("overlap", ["0", "1"])
-def test_rccl_transport_self_routed_equals_wrap(overlap):
-    env = dict(os.environ, ROMS_GPU_RCCL_SELF="1", ROMS_GPU_S2D_OVERLAP=overlap)
+@pytest.mark.parametrize("overlap,transport", [("0", "ipc"), ("1", "ipc"), ("0", "rccl")])
+def test_rccl_transport_self_routed_equals_wrap(overlap, transport):
+    """Single rank with a communicator: every exchange goes through the
+    multi-rank transport (IPC peer writes to itself after the init self-test,
+    or RCCL self-sends with ROMS_GPU_HALO_IPC=0), graph-captured; fields equal
+    the on-device periodic wrap bitwise."""
+    env = dict(os.environ, ROMS_GPU_RCCL_SELF="1", ROMS_GPU_S2D_OVERLAP=overlap, ROMS_EXPECT_TRANSPORT=transport,
+               ROMS_GPU_HALO_IPC="1" if transport == "ipc" else "0")
     r = subprocess.run([sys.executable, "-c", RCCL_SCRIPT, ROOT], env=env, capture_output=True, text=True,
                        timeout=300)
     assert r.returncode == 0 and "RCCL_OK" in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
