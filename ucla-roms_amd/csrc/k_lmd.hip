@@ -167,7 +167,7 @@ __global__ void __launch_bounds__(256) k_swr_frac(Dev d, Range R) {
 
 // ---- pass 1: extended range ----
 template <class C>
-__global__ void __launch_bounds__(64) k_kpp_ext(Dev d, Range E, int tind, int nstp, KppConst kc) {
+__global__ void __launch_bounds__(64, 4) k_kpp_ext(Dev d, Range E, int tind, int nstp, KppConst kc) {
   ROMS_IJC_OR_RETURN(E)
   const Bounds& b = d.b;
   const Fields& F = d.f;
