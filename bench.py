@@ -82,7 +82,7 @@ def cpu_baseline_c3(nsteps=2, L=128):
     c = oracle.OrCfg()
     c.LLm, c.MMm, c.N, c.NT = L, L, C3_N, 2
     c.ew_periodic = c.ns_periodic = 0
-    c.salinity, c.nonlin_eos, c.lmd = 1, 1, 1
+    c.salinity, c.nonlin_eos, c.lmd = 1, 1, oracle.LMD_ICELAND
     c.case_id = oracle.CASE_BASIN
     c.dt, c.ndtfast = C3_DT, NDTFAST
     c.theta_s, c.theta_b, c.hc, c.rho0 = 6.0, 2.0, 250.0, 1027.5
@@ -192,7 +192,7 @@ def main():
 
     if c3:
         m = romsgpu.Model.from_case(romsgpu.CASE_BASIN, C3_L, C3_L, C3_N, NT, salinity=True, nonlin_eos=True,
-                                    lmd=True, dt=C3_DT, ndtfast=NDTFAST, sizex=C3_DX * C3_L, sizey=C3_DX * C3_L,
+                                    lmd=romsgpu.LMD_ICELAND, dt=C3_DT, ndtfast=NDTFAST, sizex=C3_DX * C3_L, sizey=C3_DX * C3_L,
                                     device=local_rank, np_xi=npx, np_eta=npe, comm=comm, rank=rank)
         Lr, Mr, Nz, dt_step = m.Lm, m.Mm, C3_N, C3_DT
     else:

@@ -20,6 +20,8 @@ program filament_driver
   c%case_id = 0; c%LLm = 64; c%MMm = 64; c%N = 32; c%NT = 1
   c%salinity = 0; c%nonlin_eos = 0; c%lmd_mixing = 0
   c%dt = 5.0d0; c%ndtfast = 60; c%sizex = 12.8d3; c%sizey = 3.2d3; c%surf_flux = 0
+  c%obc = 0; c%v_sponge = 0.0d0; c%island = 0; c%curvgrid = 0
+  c%uv_adv = 1; c%uv_cor = 1             ! tests/Filament/cppdefs.opt: UV_ADV, UV_COR
   if (roms_gpu_abi_version() /= ROMS_GPU_ABI) error stop 'ABI version mismatch'
   call roms_gpu_check(roms_gpu_init_case(c, 0_c_int, t), 'init_case')
   call roms_gpu_check(roms_gpu_diag(t, norms), 'diag')

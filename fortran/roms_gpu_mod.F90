@@ -30,6 +30,7 @@ module roms_gpu_mod
     integer(c_int) :: obc                        ! OBC_WEST 1, OBC_EAST 2, OBC_SOUTH 4, OBC_NORTH 8
     real(c_double) :: ubind
     integer(c_int) :: curvgrid                   ! CURVGRID
+    integer(c_int) :: uv_adv, uv_cor             ! UV_ADV, UV_COR
   end type
 
   type, bind(c) :: roms_tlev
@@ -46,9 +47,13 @@ module roms_gpu_mod
     real(c_double) :: v_sponge
     integer(c_int) :: island
     integer(c_int) :: curvgrid
+    integer(c_int) :: uv_adv, uv_cor
   end type
 
-  integer(c_int), parameter :: ROMS_GPU_ABI = 4   ! ROMS_GPU_ABI_VERSION, include/roms_gpu.h
+  ! LMD switch bits of lmd_mixing (ROMS_LMD_*)
+  integer(c_int), parameter :: ROMS_LMD_MIXING = 1, ROMS_LMD_KPP = 2, ROMS_LMD_BKPP = 4, ROMS_LMD_RIMIX = 8, &
+                               ROMS_LMD_CONVEC = 16, ROMS_LMD_NONLOCAL = 32
+  integer(c_int), parameter :: ROMS_GPU_ABI = 5   ! ROMS_GPU_ABI_VERSION, include/roms_gpu.h
 
   ! field ids (enum roms_field) used by the drivers below
   integer(c_int), parameter :: ROMS_zeta = 22, ROMS_ubar = 23, ROMS_vbar = 24, ROMS_u = 25, ROMS_v = 26, &

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define ROMS_GPU_ABI_VERSION 4
+#define ROMS_GPU_ABI_VERSION 5
 #define ROMS_MAX_FAST 288
 
 /* Subdomain geometry of this rank: param.F / dimensions.F / mpi_setup.F:39-210 */
@@ -37,11 +37,34 @@ typedef struct roms_dims {
   int west_exchng, east_exchng, south_exchng, north_exchng; /* message edges */
 } roms_dims;
 
-/* cppdefs.opt switches and run scalars (scalars.F, read_inp_mod.F, set_weights.F) */
+/* LMD switch bits of roms_cfg.lmd_mixing / roms_case.lmd_mixing (cppdefs.opt).
+ * Accepted sets are the ones the reference builds and runs correctly:
+ *   0 (no LMD_MIXING), or MIXING|KPP|BKPP plus any of RIMIX, NONLOCAL and
+ *   CONVEC (CONVEC needs RIMIX).  KPP without BKPP does not compile in the
+ *   reference (lmd_kpp.F:178 reads hbbl, imported only under LMD_BKPP,
+ *   lmd_kpp.F:37-39); MIXING without KPP/BKPP filters Kv(0), Kv(N) that are
+ *   never set (lmd_vmix.F:405-420); CONVEC without RIMIX tests an unset Rig
+ *   (lmd_vmix.F:269-274).  The Pipes_ana set is ROMS_LMD_ALL, the Iceland
+ *   set (Examples/Iceland/Iceland_parent/cppdefs.opt:41-46) ROMS_LMD_ICELAND. */
+#define ROMS_LMD_MIXING   1
+#define ROMS_LMD_KPP      2
+#define ROMS_LMD_BKPP     4
+#define ROMS_LMD_RIMIX    8
+#define ROMS_LMD_CONVEC   16
+#define ROMS_LMD_NONLOCAL 32
+#define ROMS_LMD_ALL      63
+#define ROMS_LMD_ICELAND  47   /* all but LMD_CONVEC */
+
+/* cppdefs.opt switches and run scalars (scalars.F, read_inp_mod.F, set_weights.F).
+ * Switches that need no flag here: MASKING is carried by the mask arrays
+ * (all-ones masks reproduce a build without it); IMPLICIT_BOTTOM_DRAG is
+ * forced on inside step3d_uv1.F:138 / step3d_uv2.F:82 and its only other use
+ * (compute_rd_bott_drag.h:41) is masked by IMPLCT_NO_SLIP_BTTM_BC, always
+ * defined (set_global_definitions.h:73). */
 typedef struct roms_cfg {
   int nonlin_eos;                /* NONLIN_EOS (+SPLIT_EOS)                */
   int salinity;                  /* SALINITY                               */
-  int lmd_mixing;                /* LMD_MIXING/KPP/BKPP/RIMIX/CONVEC/NONLOCAL */
+  int lmd_mixing;                /* 0 or ROMS_LMD_* bits (see above)       */
   int uv_vis2, ts_dif2;          /* UV_VIS2, TS_DIF2                        */
   double dt;                     /* baroclinic step [s]                    */
   int ndtfast, nfast;            /* mode splitting                         */
@@ -55,6 +78,9 @@ typedef struct roms_cfg {
                                     closed walls elsewhere (zetabc.F, u2dbc_im.F ... t3dbc_im.F)  */
   double ubind;                  /* OBC binding velocity [m/s] (scalars.F, read_inp_mod.F:809)    */
   int curvgrid;                  /* CURVGRID (with UV_ADV): curvature terms in the momentum r.h.s. */
+  int uv_adv, uv_cor;            /* UV_ADV (horizontal + vertical momentum advection,
+                                    compute_horiz_rhs_uv_terms.h:42-291, compute_vert_rhs_uv_terms.h),
+                                    UV_COR (Coriolis, compute_horiz_rhs_uv_terms.h:1-38)              */
 } roms_cfg;
 
 /* Time-step indices (scalars.F:32-36).  The step entry updates them. */
@@ -154,7 +180,7 @@ int roms_gpu_init_sequence(roms_tlev *t);
 enum roms_case_id { ROMS_CASE_FILAMENT = 0, ROMS_CASE_BASIN = 1, ROMS_CASE_PIPES = 2 };
 typedef struct roms_case {
   int case_id, LLm, MMm, N, NT;
-  int salinity, nonlin_eos, lmd_mixing;
+  int salinity, nonlin_eos, lmd_mixing;  /* lmd_mixing: 0 or ROMS_LMD_* bits */
   double dt; int ndtfast;
   double sizex, sizey;
   int surf_flux;  /* basin only: analytic cooling, short-wave and salt fluxes (else 0) */
@@ -162,6 +188,7 @@ typedef struct roms_case {
   double v_sponge;/* basin only: SPONGE band viscosity/diffusivity [m2/s] (set_nudgcof.F)      */
   int island;     /* basin only: circular land mask (MASKING)                                   */
   int curvgrid;   /* basin only: non-uniform metrics pm(j), pn(i) and CURVGRID                  */
+  int uv_adv, uv_cor;  /* UV_ADV, UV_COR (every reference case defines both: set 1, 1)          */
 } roms_case;
 /* Builds the analytic grid/ICs on the host (setup_grid1/2, set_scoord,
  * set_weights, ana_init), initialises the device and runs roms_init.        */

@@ -14,6 +14,9 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB = os.path.join(_HERE, "liboracle.so")
 CASE_FILAMENT, CASE_BASIN, CASE_PIPES = 0, 1, 2
+LMD_RIMIX, LMD_CONVEC, LMD_NONLOCAL = 8, 16, 32
+LMD_ALL = 63       # LMD_MIXING+KPP+BKPP+RIMIX+CONVEC+NONLOCAL (tests/Pipes_ana/cppdefs.opt)
+LMD_ICELAND = 47   # all but LMD_CONVEC (Examples/Iceland/Iceland_parent/cppdefs.opt:41-46)
 
 
 class OrCfg(ctypes.Structure):
@@ -30,7 +33,16 @@ class OrCfg(ctypes.Structure):
                 ("S0", ctypes.c_double), ("sizex", ctypes.c_double), ("sizey", ctypes.c_double),
                 ("diag_np_xi", ctypes.c_int), ("diag_np_eta", ctypes.c_int), ("surf_flux", ctypes.c_int),
                 ("obc", ctypes.c_int), ("ubind", ctypes.c_double), ("v_sponge", ctypes.c_double),
-                ("island", ctypes.c_int), ("curvgrid", ctypes.c_int)]
+                ("island", ctypes.c_int), ("curvgrid", ctypes.c_int), ("uv_adv", ctypes.c_int),
+                ("uv_cor", ctypes.c_int)]
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        # every reference case defines UV_ADV and UV_COR
+        if "uv_adv" not in k:
+            self.uv_adv = 1
+        if "uv_cor" not in k:
+            self.uv_cor = 1
 
 
 def build():
@@ -96,7 +108,7 @@ def pipes_cfg(LLm=100, MMm=100, N=10, np_xi=3, np_eta=2):
     c = OrCfg()
     c.LLm, c.MMm, c.N, c.NT = LLm, MMm, N, 2
     c.ew_periodic = c.ns_periodic = 0
-    c.salinity, c.nonlin_eos, c.lmd = 1, 1, 1
+    c.salinity, c.nonlin_eos, c.lmd = 1, 1, LMD_ALL
     c.case_id = CASE_PIPES
     c.dt, c.ndtfast = 60.0, 30
     c.theta_s, c.theta_b, c.hc, c.rho0 = 6.0, 6.0, 25.0, 1027.5

@@ -114,7 +114,17 @@ static void lmd_vmix_tile(or_state *S, int tind) {
   int imin, imax, jmin, jmax;
   ext_range(S, &imin, &imax, &jmin, &jmax);
   double *Rk = S->lmd2[3];
+  const int rimix = (S->c.lmd & OR_LMD_RIMIX) != 0, convec = (S->c.lmd & OR_LMD_CONVEC) != 0;
   for (int k = 1; k <= N - 1; k++) {
+    if (!rimix) {  /* internal waves only (lmd_vmix.F:262-264) */
+      for (int j = S->jstr; j <= S->jend; j++)
+        for (int i = S->istr; i <= S->iend; i++) {
+          KV(i, j, k) = nuwm;
+          KT(i, j, k) = nuws;
+          KS(i, j, k) = nuws;
+        }
+      continue;
+    }
     for (int j = jmin; j <= jmax; j++)
       for (int i = imin; i <= imax; i++) {
         const double cff = 0.5 / (ZR(i, j, k + 1) - ZR(i, j, k));
@@ -132,7 +142,7 @@ static void lmd_vmix_tile(or_state *S, int tind) {
         double nu_sx = 1. - cff * cff;
         nu_sx = nu_sx * nu_sx * nu_sx;
         double kv = nuwm + nu0m * nu_sx, kt = nuws + nu0s * nu_sx;
-        if (rig < 0.) { kv = kv + nu0c; kt = kt + nu0c; }  /* LMD_CONVEC */
+        if (convec && rig < 0.) { kv = kv + nu0c; kt = kt + nu0c; }  /* LMD_CONVEC (lmd_vmix.F:269-274) */
         KV(i, j, k) = kv;
         KT(i, j, k) = kt;
         KS(i, j, k) = kt;
@@ -230,6 +240,7 @@ static void lmd_kpp_tile(or_state *S, int tind) {
 #define KI(i) ((i) + 1)
   const int nstp = S->nstp;
   const double rho0 = S->rho0;
+  const int nonlocal = (S->c.lmd & OR_LMD_NONLOCAL) != 0;
   for (int j = jmin; j <= jmax; j++) {
     for (int i = imin; i <= imax; i++) {
       /* alfabeta.F:46-78 (NONLIN_EOS, SALINITY) at t(N,nstp) */
@@ -392,10 +403,12 @@ static void lmd_kpp_tile(or_state *S, int tind) {
           KT(i, j, k) = sqrt(a * a + w * w);
           a = amp * KS(i, j, k);
           KS(i, j, k) = sqrt(a * a + w * w);
-          if (Bfsfc < 0.) GHAT(i, j, k) = -(Cg * ssgm * ((1. - ssgm) * (1. - ssgm)));
-          else GHAT(i, j, k) = 0.;
+          if (nonlocal) {  /* LMD_NONLOCAL (lmd_kpp.F:436-442) */
+            if (Bfsfc < 0.) GHAT(i, j, k) = -(Cg * ssgm * ((1. - ssgm) * (1. - ssgm)));
+            else GHAT(i, j, k) = 0.;
+          }
         } else {
-          GHAT(i, j, k) = 0.;
+          if (nonlocal) GHAT(i, j, k) = 0.;
         }
       }
     /* LMD_BKPP bottom layer */

@@ -615,22 +615,29 @@ static void horiz_rhs_uv(or_state *S, int k, int upstream, double *ru, double *r
   const double delta = 0.1666666666666667, gamma = 0.3333333333333333;
   double *UFx = S->s2[4], *UFe = S->s2[5], *VFx = S->s2[6], *VFe = S->s2[7], *wrk1 = S->s2[8], *wrk2 = S->s2[9];
   int imin, imax, jmin, jmax;
-  /* Coriolis */
-  for (int j = jstrV - 1; j <= jend; j++)
-    for (int i = istrU - 1; i <= iend; i++) {
-      /* compute_horiz_rhs_uv_terms.h:4-12: CURVGRID && UV_ADV adds the curvature terms */
-      const double cff = S->c.curvgrid
-                             ? 0.5 * HZ(i, j, k) *
-                                   (A2(S->fomn, i, j) + 0.5 * ((V(i, j, k, nr) + V(i, j + 1, k, nr)) * A2(S->dndx, i, j) -
-                                                               (U(i, j, k, nr) + U(i + 1, j, k, nr)) * A2(S->dmde, i, j)))
-                             : 0.5 * HZ(i, j, k) * (A2(S->fomn, i, j));
-      A2(UFx, i, j) = cff * (V(i, j, k, nr) + V(i, j + 1, k, nr));
-      A2(VFe, i, j) = cff * (U(i, j, k, nr) + U(i + 1, j, k, nr));
-    }
-  for (int j = jstr; j <= jend; j++)
-    for (int i = istrU; i <= iend; i++) R3(ru, i, j, k) = R3(ru, i, j, k) + 0.5 * (A2(UFx, i, j) + A2(UFx, i - 1, j));
-  for (int j = jstrV; j <= jend; j++)
-    for (int i = istr; i <= iend; i++) R3(rv, i, j, k) = R3(rv, i, j, k) - 0.5 * (A2(VFe, i, j) + A2(VFe, i, j - 1));
+  const int ucor = S->c.uv_cor, curv = S->c.curvgrid && S->c.uv_adv;
+  /* Coriolis (UV_COR) and/or the CURVGRID && UV_ADV curvature terms */
+  if (ucor || curv) {
+    for (int j = jstrV - 1; j <= jend; j++)
+      for (int i = istrU - 1; i <= iend; i++) {
+        /* compute_horiz_rhs_uv_terms.h:4-12 */
+        double cff;
+        if (curv) {
+          const double ct = 0.5 * ((V(i, j, k, nr) + V(i, j + 1, k, nr)) * A2(S->dndx, i, j) -
+                                   (U(i, j, k, nr) + U(i + 1, j, k, nr)) * A2(S->dmde, i, j));
+          cff = 0.5 * HZ(i, j, k) * (ucor ? A2(S->fomn, i, j) + ct : ct);
+        } else {
+          cff = 0.5 * HZ(i, j, k) * (A2(S->fomn, i, j));
+        }
+        A2(UFx, i, j) = cff * (V(i, j, k, nr) + V(i, j + 1, k, nr));
+        A2(VFe, i, j) = cff * (U(i, j, k, nr) + U(i + 1, j, k, nr));
+      }
+    for (int j = jstr; j <= jend; j++)
+      for (int i = istrU; i <= iend; i++) R3(ru, i, j, k) = R3(ru, i, j, k) + 0.5 * (A2(UFx, i, j) + A2(UFx, i - 1, j));
+    for (int j = jstrV; j <= jend; j++)
+      for (int i = istr; i <= iend; i++) R3(rv, i, j, k) = R3(rv, i, j, k) - 0.5 * (A2(VFe, i, j) + A2(VFe, i, j - 1));
+  }
+  if (!S->c.uv_adv) return;  /* compute_horiz_rhs_uv_terms.h:42 */
   /* advection: UFx */
   if (!S->c.ew_periodic) {
     imin = S->west_edge ? istrU : istrU - 1;
@@ -748,6 +755,7 @@ static void horiz_rhs_uv(or_state *S, int k, int upstream, double *ru, double *r
 /* compute_vert_rhs_uv_terms.h, SPLINE_UV, MASKING                         */
 static void vert_rhs_uv(or_state *S, int j, double *ru, double *rv) {
   const int N = S->N, nr = S->nrhs;
+  if (!S->c.uv_adv) return;  /* compute_vert_rhs_uv_terms.h:1 */
   double *DC = S->c1[3], *CF = S->c1[2], *FC = S->c1[1];
   for (int i = S->istrU; i <= S->iend; i++) {
     C1(DC, i, 1) = 0.5625 * (HZ(i, j, 1) + HZ(i - 1, j, 1)) - 0.0625 * (HZ(i + 1, j, 1) + HZ(i - 2, j, 1));
@@ -1469,12 +1477,12 @@ void or_step3d_t(or_state *S) {
         if (itrc == 1) {
           for (int k = N - 1; k >= 1; k--)
             for (int i = S->istr; i <= S->iend; i++) {
-              const double cff = A2(S->srflx, i, j) * W3(S->swr_frac, i, j, k) -
-                                 W3(S->ghat, i, j, k) * (stf[O2(i, j)] - A2(S->srflx, i, j));
+              double cff = A2(S->srflx, i, j) * W3(S->swr_frac, i, j, k);
+              if (S->c.lmd & OR_LMD_NONLOCAL) cff = cff - W3(S->ghat, i, j, k) * (stf[O2(i, j)] - A2(S->srflx, i, j));
               TT(i, j, k + 1, nnew, 1) = TT(i, j, k + 1, nnew, 1) - dt * cff;
               TT(i, j, k, nnew, 1) = TT(i, j, k, nnew, 1) + dt * cff;
             }
-        } else if (itrc == 2 && S->c.salinity) {
+        } else if (itrc == 2 && S->c.salinity && (S->c.lmd & OR_LMD_NONLOCAL)) {
           for (int k = N - 1; k >= 1; k--)
             for (int i = S->istr; i <= S->iend; i++) {
               const double cff = -dt * W3(S->ghat, i, j, k) * stf[O2(i, j) + S->n2];

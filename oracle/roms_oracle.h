@@ -25,12 +25,15 @@ extern "C" {
 
 /* analytic case selector */
 enum { OR_CASE_FILAMENT = 0, OR_CASE_BASIN = 1, OR_CASE_PIPES = 2 };
+enum { OR_LMD_RIMIX = 8, OR_LMD_CONVEC = 16, OR_LMD_NONLOCAL = 32 };
 
 typedef struct or_cfg {
   int LLm, MMm, N, NT;           /* interior dims, tracers (T[,S,passive]) */
   int ew_periodic, ns_periodic;
   int salinity, nonlin_eos;      /* nonlin_eos implies SPLIT_EOS */
-  int lmd;                       /* LMD_MIXING+KPP+BKPP+RIMIX+CONVEC+NONLOCAL */
+  int lmd;                       /* 0 or LMD switch bits (as ROMS_LMD_* of include/roms_gpu.h):
+                                    1 MIXING, 2 KPP, 4 BKPP (MIXING|KPP|BKPP always together),
+                                    8 RIMIX, 16 CONVEC, 32 NONLOCAL */
   int case_id;
   int ntimes;
   double dt; int ndtfast;
@@ -47,6 +50,7 @@ typedef struct or_cfg {
   double v_sponge;               /* SPONGE viscosity/diffusivity [m2/s] (set_nudgcof.F:25-111) */
   int island;                    /* basin: circular land mask (MASKING) */
   int curvgrid;                  /* CURVGRID (+UV_ADV) curvature terms; basin: non-uniform metrics */
+  int uv_adv, uv_cor;            /* UV_ADV, UV_COR */
 } or_cfg;
 
 typedef struct or_state or_state;

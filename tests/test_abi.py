@@ -33,7 +33,33 @@ def test_library_exports_every_declared_symbol():
     missing = [n for n in _declared() if n not in exported]
     assert not missing, missing
     L = ctypes.CDLL(LIB)
-    assert L.roms_gpu_abi_version() == 4
+    want = int(re.search(r"#define ROMS_GPU_ABI_VERSION (\d+)", open(HDR).read()).group(1))
+    assert L.roms_gpu_abi_version() == want
+
+
+def test_ctypes_structs_match_header_layout(tmp_path):
+    """The Python mirrors (romsgpu.Dims/Cfg/Tlev/Case) have the C structs'
+    size and field offsets (compiled against include/roms_gpu.h here)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "ucla-roms_amd"))
+    import romsgpu
+    structs = {"roms_dims": romsgpu.Dims, "roms_cfg": romsgpu.Cfg, "roms_tlev": romsgpu.Tlev,
+               "roms_case": romsgpu.Case}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "roms_gpu.h"', "int main(void) {"]
+    for cname, py in structs.items():
+        lines.append('  printf("%s %%zu\\n", sizeof(%s));' % (cname, cname))
+        for fname, _ in py._fields_:
+            lines.append('  printf("%s.%s %%zu\\n", offsetof(%s, %s));' % (cname, fname, cname, fname))
+    lines.append("  return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines) + "\n")
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = dict(l.split() for l in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split("\n") if l)
+    for cname, py in structs.items():
+        assert int(got[cname]) == ctypes.sizeof(py), cname
+        for fname, _ in py._fields_:
+            assert int(got["%s.%s" % (cname, fname)]) == getattr(py, fname).offset, (cname, fname)
 
 
 @pytest.mark.skipif(not os.path.exists(LIB), reason="libromsgpu.so not built")

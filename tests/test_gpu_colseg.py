@@ -27,7 +27,7 @@ def seg_cfg(case):
     if case == "n50":
         return basin_cfg(nonlin=True, LLm=40, MMm=24, N=50)
     c = basin_cfg(nonlin=True, LLm=24, MMm=20, N=100)
-    c.lmd, c.surf_flux = 1, 1
+    c.lmd, c.surf_flux = oracle.LMD_ALL, 1
     return c
 
 
@@ -37,7 +37,7 @@ def make_model(cfg, colseg):
     try:
         return romsgpu.Model.from_case(cfg.case_id, cfg.LLm, cfg.MMm, cfg.N, cfg.NT, salinity=bool(cfg.salinity),
                                        nonlin_eos=bool(cfg.nonlin_eos), dt=cfg.dt, ndtfast=cfg.ndtfast,
-                                       sizex=cfg.sizex, sizey=cfg.sizey, lmd=bool(cfg.lmd),
+                                       sizex=cfg.sizex, sizey=cfg.sizey, lmd=cfg.lmd,
                                        surf_flux=bool(cfg.surf_flux))
     finally:
         if old is None:

@@ -1,0 +1,155 @@
+"""The BASELINE.json configurations against the oracle, and the cppdefs.opt
+switch variants.
+
+  C2  Filament + SALINITY (linear EOS, T and S, NT = 2), doubly periodic,
+      dx = 100 m, dy = 25 m: 64x64x50 for 100 steps (field RMS < 1e-10, the
+      north_star bound) and the full 512x512x50 bench grid for 2 steps.
+  C4  Iceland-size stand-in (the real Iceland inputs are offline-unavailable,
+      SURVEY.md 8(c)): 192x192x20 synthetic basin with the Iceland switch set
+      of Examples/Iceland/Iceland_parent/cppdefs.opt -- OBC_M2FLATHER /
+      M3ORLANSKI / TORLANSKI with *_FRC_BRY data, SPONGE, MASKING (island),
+      CURVGRID, NONLIN+SPLIT EOS, LMD_MIXING+KPP+BKPP+RIMIX+NONLOCAL without
+      LMD_CONVEC -- dt = 900 s, ndtfast = 30 (nfast 41, .../roms.in).
+      Single domain vs the oracle; 4x2 processor grid (8 subdomains, one
+      thread each) vs the single domain bitwise.  The 4x2 check runs without
+      the sponge: the reference sets the sponge bands on each rank's own
+      points only (set_nudgcof.F:89-111, no exchange after it) while
+      visc3d_S.F / t3dmix_S.F:55 read them across the halo, so a sponge run is
+      decomposition dependent in the reference itself.
+  C5  C4 + 8 passive tracers (NT = 10, param.opt nt_passive): passive
+      tracers take Akt(min(itrc, iTandS)) (step3d_t_ISO.F:1044), no EOS or
+      KPP surface terms; initial Gaussian blobs.
+  Switch variants: LMD_RIMIX / LMD_CONVEC / LMD_NONLOCAL individually off,
+  UV_ADV and UV_COR off (compute_horiz_rhs_uv_terms.h, compute_vert_rhs_uv_terms.h).
+
+The OBC/SPONGE/CURVGRID branches of the oracle have no runnable golden log
+offline (test_gpu_obc.py): "parity unpinned" there; everything else is
+pinned through the Filament / Pipes_ana goldens (test_oracle_golden.py).
+"""
+import numpy as np
+import pytest
+
+import oracle
+import romsgpu
+from test_gpu_multirank import check_decomposition
+from test_gpu_parity import PROGNOSTIC, RMS_RUN, basin_cfg, check_fields, rms
+
+pytestmark = pytest.mark.gpu
+
+
+def pair(cfg):
+    o = oracle.Oracle(cfg)
+    o.init()
+    m = romsgpu.Model.from_case(cfg.case_id, cfg.LLm, cfg.MMm, cfg.N, cfg.NT, salinity=bool(cfg.salinity),
+                                nonlin_eos=bool(cfg.nonlin_eos), dt=cfg.dt, ndtfast=cfg.ndtfast, sizex=cfg.sizex,
+                                sizey=cfg.sizey, lmd=cfg.lmd, surf_flux=bool(cfg.surf_flux), obc=cfg.obc,
+                                v_sponge=cfg.v_sponge, island=bool(cfg.island), curvgrid=bool(cfg.curvgrid),
+                                uv_adv=bool(cfg.uv_adv), uv_cor=bool(cfg.uv_cor))
+    return o, m
+
+
+def c2_cfg(L, M, N=50):
+    """C2: Filament physics + SALINITY at dx = 100 m, dy = 25 m."""
+    return oracle.filament_cfg(LLm=L, MMm=M, N=N, NT=2, salinity=True, sizex=100.0 * L, sizey=25.0 * M,
+                               np_xi=1, np_eta=1)
+
+
+def test_c2_filament_salinity_100_steps():
+    cfg = c2_cfg(64, 64)
+    o, m = pair(cfg)
+    o.step(100)
+    m.step(100)
+    m.sync()
+    assert o.tindex() == m.t.as_list()
+    check_fields(o, m, PROGNOSTIC, 64, 64, RMS_RUN, kind="rms")
+    # both tracers moved and stayed distinct (S is really advected)
+    t = m.get("t")
+    assert t.shape[0] == 3 * 2 * 50
+    m.close()
+
+
+def test_c2_full_grid_2_steps():
+    """The bench workload itself (512x512x50, NT = 2) for 2 steps."""
+    cfg = c2_cfg(512, 512)
+    o, m = pair(cfg)
+    o.step(2)
+    m.step(2)
+    m.sync()
+    check_fields(o, m, ["zeta", "ubar", "vbar", "u", "v", "t", "We", "Hz"], 512, 512, RMS_RUN, kind="rms")
+    m.close()
+
+
+def c4_cfg(NT=2, L=192, sponge=1.0e3, island=1):
+    """C4 stand-in: Iceland switches on a 192x192x20 synthetic open basin."""
+    c = basin_cfg(LLm=L, MMm=L, N=20, NT=NT, nonlin=True, dt=900.0, ndtfast=30, sizex=15.0e3 * L,
+                  sizey=15.0e3 * L)
+    c.obc, c.ubind, c.v_sponge, c.island, c.curvgrid = 15, 0.1, sponge, island, 1
+    c.lmd, c.surf_flux = oracle.LMD_ICELAND, 1
+    return c
+
+
+def _case(cfg):
+    return dict(case_id=cfg.case_id, LLm=cfg.LLm, MMm=cfg.MMm, N=cfg.N, NT=cfg.NT, salinity=bool(cfg.salinity),
+                nonlin_eos=bool(cfg.nonlin_eos), dt=cfg.dt, ndtfast=cfg.ndtfast, sizex=cfg.sizex, sizey=cfg.sizey,
+                lmd=cfg.lmd, surf_flux=bool(cfg.surf_flux), obc=cfg.obc, v_sponge=cfg.v_sponge,
+                island=bool(cfg.island), curvgrid=bool(cfg.curvgrid))
+
+
+@pytest.mark.parametrize("NT", [2, 10], ids=["C4", "C5"])
+def test_c4_c5_single_domain_vs_oracle(NT):
+    cfg = c4_cfg(NT=NT)
+    o, m = pair(cfg)
+    assert m.t.nfast == 41
+    o.step(40)
+    m.step(40)
+    m.sync()
+    check_fields(o, m, PROGNOSTIC + ["Akv", "Akt", "hbls", "hbbl"], cfg.LLm, cfg.MMm, RMS_RUN, kind="rms")
+    if NT == 10:   # every passive tracer separately (each carries its own blob)
+        a, b = m.get("t"), o.field("t")
+        n3 = cfg.N
+        for it in range(NT):
+            sl = slice(it * 3 * n3, (it + 1) * 3 * n3)
+            e = rms(a[sl][..., 2:-2, 2:-2], b[sl][..., 2:-2, 2:-2])
+            assert e < RMS_RUN, (it + 1, e)
+        assert float(np.max(np.abs(b[9 * 3 * n3:]))) > 0.1   # tracer 10 is not empty
+    m.close()
+
+
+@pytest.mark.parametrize("NT", [2, 10], ids=["C4", "C5"])
+def test_c4_c5_4x2_bitwise_equals_single_domain(NT):
+    check_decomposition(_case(c4_cfg(NT=NT, sponge=0.0)), 4, 2, nsteps=4)
+
+
+SWITCHES = [
+    ("no_rimix", dict(lmd=oracle.LMD_ICELAND & ~oracle.LMD_RIMIX)),
+    ("no_nonlocal", dict(lmd=oracle.LMD_ALL & ~oracle.LMD_NONLOCAL)),
+    ("convec", dict(lmd=oracle.LMD_ALL)),
+    ("no_uv_adv", dict(uv_adv=0)),
+    ("no_uv_cor", dict(uv_cor=0)),
+    ("no_uv_adv_cor", dict(uv_adv=0, uv_cor=0)),
+    ("curv_no_uv_cor", dict(uv_cor=0, curvgrid=1)),
+]
+
+
+@pytest.mark.parametrize("name,sw", SWITCHES, ids=[s[0] for s in SWITCHES])
+def test_switch_variants_30_steps(name, sw):
+    c = basin_cfg(LLm=40, MMm=32, N=16, nonlin=True)
+    c.surf_flux = 1
+    c.lmd = oracle.LMD_ICELAND
+    for k, v in sw.items():
+        setattr(c, k, v)
+    o, m = pair(c)
+    o.step(30)
+    m.step(30)
+    m.sync()
+    names = PROGNOSTIC + (["Akv", "Akt", "ghat"] if c.lmd else [])
+    check_fields(o, m, names, c.LLm, c.MMm, RMS_RUN, kind="rms")
+    m.close()
+
+
+def test_invalid_lmd_sets_are_rejected():
+    """Sets the reference cannot build or run correctly fail loudly."""
+    for bad in (1, 1 | 2, 1 | 2 | 4 | 16, 128):
+        with pytest.raises(romsgpu.RomsGpuError):
+            romsgpu.Model.from_case(1, 16, 16, 8, 2, salinity=True, nonlin_eos=True, lmd=bad, dt=60.0, ndtfast=30,
+                                    sizex=32e3, sizey=32e3)

@@ -30,7 +30,7 @@ LMD_OUT = ["Akv", "Akt", "hbls", "hbbl", "ghat"]
 
 def lmd_basin_cfg(surf_flux=0, **kw):
     c = basin_cfg(nonlin=True, **kw)
-    c.lmd = 1
+    c.lmd = oracle.LMD_ALL
     c.surf_flux = surf_flux
     return c
 
@@ -40,7 +40,7 @@ def make_pair(cfg):
     o.init()
     m = romsgpu.Model.from_case(cfg.case_id, cfg.LLm, cfg.MMm, cfg.N, cfg.NT, salinity=bool(cfg.salinity),
                                 nonlin_eos=bool(cfg.nonlin_eos), dt=cfg.dt, ndtfast=cfg.ndtfast,
-                                sizex=cfg.sizex, sizey=cfg.sizey, lmd=bool(cfg.lmd), surf_flux=bool(cfg.surf_flux))
+                                sizex=cfg.sizex, sizey=cfg.sizey, lmd=cfg.lmd, surf_flux=bool(cfg.surf_flux))
     return o, m
 
 

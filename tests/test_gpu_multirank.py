@@ -94,17 +94,17 @@ EXCHANGED = ("zeta", "ubar", "vbar", "u", "v", "t", "FlxU", "FlxV", "We", "Wi", 
 LMD_FIELDS = ("Akv", "Akt", "hbls", "hbbl", "ghat", "swr_frac")
 
 
-@pytest.mark.parametrize("kind", ["filament", "basin", "basin_lmd", "basin_flux", "pipes"])
-@pytest.mark.parametrize("npx,npe", [(2, 1), (1, 2), (2, 2), (3, 2)])
-def test_decomposition_bitwise_equals_single_domain(kind, npx, npe):
-    case = _case(kind)
+def check_decomposition(case, npx, npe, nsteps=5, fields=None):
+    """Every subdomain of an npx x npe run equals the single-domain run's
+    window bitwise (owned cells, and halos of the exchanged fields)."""
     per = case["case_id"] == 0
-    fields = FIELDS + (LMD_FIELDS if case.get("lmd") else ())
+    if fields is None:
+        fields = FIELDS + (LMD_FIELDS if case.get("lmd") else ())
     m = romsgpu.Model.from_case(**case)
-    m.step(5)
+    m.step(nsteps)
     ref = {f: m.get(f) for f in fields}
     m.close()
-    parts, _ = run_decomposed(case, npx, npe, 5, fields=fields)
+    parts, _ = run_decomposed(case, npx, npe, nsteps, fields=fields)
     bad = []
     for rank, (iSW, jSW, Lm, Mm, got) in enumerate(parts):
         jn, inn = divmod(rank, npx)
@@ -121,7 +121,13 @@ def test_decomposition_bitwise_equals_single_domain(kind, npx, npe):
                 bad.append((rank, f, "owned", float(np.max(np.abs(g[own] - w[own])))))
             elif f in EXCHANGED and not np.array_equal(g, w):
                 bad.append((rank, f, "halo", float(np.max(np.abs(g - w)))))
-    assert not bad, (kind, npx, npe, bad[:6])
+    assert not bad, (npx, npe, bad[:6])
+
+
+@pytest.mark.parametrize("kind", ["filament", "basin", "basin_lmd", "basin_flux", "pipes"])
+@pytest.mark.parametrize("npx,npe", [(2, 1), (1, 2), (2, 2), (3, 2)])
+def test_decomposition_bitwise_equals_single_domain(kind, npx, npe):
+    check_decomposition(_case(kind), npx, npe)
 
 
 @pytest.mark.parametrize("kind", ["filament", "basin"])

@@ -38,7 +38,7 @@ def make_pair(cfg):
     o.init()
     m = romsgpu.Model.from_case(cfg.case_id, cfg.LLm, cfg.MMm, cfg.N, cfg.NT, salinity=bool(cfg.salinity),
                                 nonlin_eos=bool(cfg.nonlin_eos), dt=cfg.dt, ndtfast=cfg.ndtfast, sizex=cfg.sizex,
-                                sizey=cfg.sizey, lmd=bool(cfg.lmd), obc=cfg.obc, v_sponge=cfg.v_sponge,
+                                sizey=cfg.sizey, lmd=cfg.lmd, obc=cfg.obc, v_sponge=cfg.v_sponge,
                                 island=bool(cfg.island), curvgrid=bool(cfg.curvgrid))
     return o, m
 
@@ -123,7 +123,7 @@ def test_curvgrid_momentum_rhs_parity(routine):
     m.close()
 
 
-@pytest.mark.parametrize("lmd,curv", [(0, 0), (1, 0), (1, 1)])
+@pytest.mark.parametrize("lmd,curv", [(0, 0), (oracle.LMD_ALL, 0), (oracle.LMD_ICELAND, 1)])
 def test_open_basin_30_steps_rms(lmd, curv):
     """(1, 1) is the Iceland switch set: OBC + SPONGE + MASKING + CURVGRID + LMD/KPP + NONLIN/SPLIT EOS."""
     cfg = obc_cfg(lmd=lmd, curv=curv)

@@ -175,6 +175,11 @@ __device__ __forceinline__ void uv_spline_seg(const Dev& d, const SegSpan& sg, S
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const int N = b.N, c0 = sg.c0, n = sg.n;
+  if (!d.p.uv_adv) {  // no UV_ADV (uniform over the grid: the skipped coupling barrier is too)
+#pragma unroll
+    for (int q = 0; q < KR; q++) fl[q] = 0.0;
+    return;
+  }
   const long n2 = b.n2, s = dir == 0 ? 1 : b.nx2;
   const double* __restrict__ Uv = (dir == 0 ? F.u : F.v) + (long)(nrhs - 1) * b.n3 + ij;
   const double* __restrict__ Hz = F.Hz + ij;

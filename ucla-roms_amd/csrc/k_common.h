@@ -205,39 +205,6 @@ __device__ __forceinline__ void tracer_win_fill(const Bounds& b, const Fields& F
   }
 }
 
-// ---- parabolic-spline vertical tracer fluxes, written as FC(0:N) into the
-// lane's column scratch (layout of a w-point array); CF uses a second column.
-__device__ __forceinline__ void tracer_spline_fc(const Dev& d, const double* __restrict__ T, long ij,
-                                                 double* __restrict__ FC, double* __restrict__ CF) {
-  const Bounds& b = d.b;
-  const Fields& F = d.f;
-  const int N = b.N;
-  const long n2 = b.n2;
-  double cfk = 1.0;                 // CF(1)
-  double fcm = 2.0 * T[ij];         // FC(0)
-  FC[ij] = fcm;
-  double hk = F.Hz[ij], tk = T[ij];
-  for (int k = 1; k <= N - 1; k++) {
-    const long o1 = ij + (long)k * n2;  // level k+1 (rho layout)
-    const double hk1 = F.Hz[o1], tk1 = T[o1];
-    const double cff = 1.0 / (2.0 * hk + hk1 * (2.0 - cfk));
-    const double cf1 = cff * hk;
-    const double fck = cff * (3.0 * (hk * tk1 + hk1 * tk) - hk1 * fcm);
-    CF[ij + (long)(k + 1) * n2] = cf1;
-    FC[ij + (long)k * n2] = fck;
-    cfk = cf1; fcm = fck; hk = hk1; tk = tk1;
-  }
-  double fc1 = (2.0 * tk - fcm) / (1.0 - cfk);   // FC(N)
-  for (int k = N - 1; k >= 0; k--) {
-    const double fck = FC[ij + (long)k * n2] - CF[ij + (long)(k + 1) * n2] * fc1;
-    FC[ij + (long)(k + 1) * n2] = fc1 * F.We[ij + (long)(k + 1) * n2];
-    FC[ij + (long)k * n2] = fck;
-    fc1 = fck;
-  }
-  FC[ij + (long)N * n2] = 0.0;
-  FC[ij] = 0.0;
-}
-
 // ---- horizontal momentum r.h.s. (Coriolis + advection) at (i,j,k) ----
 struct UVBounds {
   int u_imin, u_imax, v_jmin, v_jmax;   // uxx / vee extrapolation ranges
@@ -376,78 +343,42 @@ __device__ __forceinline__ void uv_horiz_rhs(const Dev& d, const A& a, int i, in
   const long o = IJ(b, i, j) + kk;
   // Coriolis factor cff = 0.5*Hz*fomn at rho point (m,n), plus the CURVGRID
   // curvature terms (compute_horiz_rhs_uv_terms.h:4-12)
+  // (UV_COR: fomn; CURVGRID && UV_ADV: curvature; either alone is allowed)
+  const bool ucor = d.p.uv_cor, curv = d.p.curvgrid, adv = d.p.uv_adv, corb = ucor || curv;
   auto cor = [&](int m, int n, long oo) {
     const long mn = IJ(b, m, n);
-    if (d.p.curvgrid)
-      return 0.5 * F.Hz[oo] *
-             (F.fomn[mn] + 0.5 * ((a.v(m, n) + a.v(m, n + 1)) * F.dndx[mn] - (a.u(m, n) + a.u(m + 1, n)) * F.dmde[mn]));
+    if (curv) {
+      const double ct = 0.5 * ((a.v(m, n) + a.v(m, n + 1)) * F.dndx[mn] - (a.u(m, n) + a.u(m + 1, n)) * F.dmde[mn]);
+      return 0.5 * F.Hz[oo] * (ucor ? F.fomn[mn] + ct : ct);
+    }
     return 0.5 * F.Hz[oo] * (F.fomn[mn]);
   };
   if (i >= b.istrU && i <= b.iend && j >= b.jstr && j <= b.jend) {
-    // Coriolis UFx at i and i-1: UFx=cff*(v(j)+v(j+1))
-    const double c0 = cor(i, j, o);
-    const double c1 = cor(i - 1, j, o - 1);
-    const double U0 = c0 * (a.v(i, j) + a.v(i, j + 1)), U1 = c1 * (a.v(i - 1, j) + a.v(i - 1, j + 1));
-    double ru = F.ru[o] + 0.5 * (U0 + U1);
-    ru = ru - adv_UFx(a, i, j, r, up) + adv_UFx(a, i - 1, j, r, up) - adv_UFe(a, i, j + 1, r, up) +
-         adv_UFe(a, i, j, r, up);
+    double ru = F.ru[o];
+    if (corb) {  // Coriolis UFx at i and i-1: UFx=cff*(v(j)+v(j+1))
+      const double c0 = cor(i, j, o);
+      const double c1 = cor(i - 1, j, o - 1);
+      const double U0 = c0 * (a.v(i, j) + a.v(i, j + 1)), U1 = c1 * (a.v(i - 1, j) + a.v(i - 1, j + 1));
+      ru = ru + 0.5 * (U0 + U1);
+    }
+    if (adv)
+      ru = ru - adv_UFx(a, i, j, r, up) + adv_UFx(a, i - 1, j, r, up) - adv_UFe(a, i, j + 1, r, up) +
+           adv_UFe(a, i, j, r, up);
     F.ru[o] = ru;
   }
   if (i >= b.istr && i <= b.iend && j >= b.jstrV && j <= b.jend) {
-    const double c0 = cor(i, j, o);
-    const double c1 = cor(i, j - 1, o - b.nx2);
-    const double V0 = c0 * (a.u(i, j) + a.u(i + 1, j)), V1 = c1 * (a.u(i, j - 1) + a.u(i + 1, j - 1));
-    double rv = F.rv[o] - 0.5 * (V0 + V1);
-    rv = rv - adv_VFx(a, i + 1, j, r, up) + adv_VFx(a, i, j, r, up) - adv_VFe(a, i, j, r, up) +
-         adv_VFe(a, i, j - 1, r, up);
+    double rv = F.rv[o];
+    if (corb) {
+      const double c0 = cor(i, j, o);
+      const double c1 = cor(i, j - 1, o - b.nx2);
+      const double V0 = c0 * (a.u(i, j) + a.u(i + 1, j)), V1 = c1 * (a.u(i, j - 1) + a.u(i + 1, j - 1));
+      rv = rv - 0.5 * (V0 + V1);
+    }
+    if (adv)
+      rv = rv - adv_VFx(a, i + 1, j, r, up) + adv_VFx(a, i, j, r, up) - adv_VFe(a, i, j, r, up) +
+           adv_VFe(a, i, j - 1, r, up);
     F.rv[o] = rv;
   }
-}
-
-// ---- vertical momentum advection by parabolic splines (SPLINE_UV) ----
-// dir=0: u at (i,j) (Hz/We averaged over i-1,i; stencil i-2..i+1, umask)
-// dir=1: v at (i,j) (over j-1,j; vmask).  FC,CF: lane column scratch.
-__device__ __forceinline__ void uv_vert_rhs(const Dev& d, int i, int j, int nrhs, int dir, double* __restrict__ FC,
-                                            double* __restrict__ CF) {
-  const Bounds& b = d.b;
-  const Fields& F = d.f;
-  const int N = b.N;
-  const long n2 = b.n2, ij = IJ(b, i, j);
-  const long s = dir == 0 ? 1 : b.nx2;
-  const double* Uv = (dir == 0 ? F.u : F.v) + (long)(nrhs - 1) * b.n3;
-  double* rr = dir == 0 ? F.ru : F.rv;
-  const double* mask = dir == 0 ? F.umask : F.vmask;
-  auto DCk = [&](int k) {
-    const long o = ij + (long)(k - 1) * n2;
-    return 0.5625 * (F.Hz[o] + F.Hz[o - s]) - 0.0625 * (F.Hz[o + s] + F.Hz[o - 2 * s]);
-  };
-  double dck = DCk(1), cfk = 1.0, fcm = 2.0 * Uv[ij];
-  FC[ij] = fcm;
-  for (int k = 1; k <= N - 1; k++) {
-    const double dc1 = DCk(k + 1);
-    const double cff = 1.0 / (2.0 * dck + dc1 * (2.0 - cfk));
-    const double cf1 = cff * dck;
-    const long o = ij + (long)(k - 1) * n2;
-    const double fck = cff * (3.0 * (dck * Uv[o + n2] + dc1 * Uv[o]) - dc1 * fcm);
-    CF[ij + (long)(k + 1) * n2] = cf1;
-    FC[ij + (long)k * n2] = fck;
-    dck = dc1; cfk = cf1; fcm = fck;
-  }
-  double fc1 = (2.0 * Uv[ij + (long)(N - 1) * n2] - fcm) / (1.0 - cfk);  // FC(N)
-  double dc1 = 0.0;                                                      // DC(N)
-  const double m1 = mask[ij + s], m0 = mask[ij - s];
-  for (int k = N - 1; k >= 1; k--) {
-    const double fck = FC[ij + (long)k * n2] - CF[ij + (long)(k + 1) * n2] * fc1;
-    const long w = ij + (long)k * n2;
-    const double dck2 = fck * 0.5 *
-                        (F.We[w] + F.We[w - s] -
-                         0.125 * ((F.We[w + s] - F.We[w]) * m1 - (F.We[w - s] - F.We[w - 2 * s]) * m0));
-    const long o1 = ij + (long)k * n2;  // rho-level k+1
-    rr[o1] = rr[o1] - dc1 + dck2;
-    dc1 = dck2;
-    fc1 = fck;
-  }
-  rr[ij] = rr[ij] - dc1;
 }
 
 // ---- SPLINE_UV with LDS column scratch: leaves the vertical advective flux
@@ -460,6 +391,10 @@ __device__ __forceinline__ void uv_vert_flux_lds(const Dev& d, long ij, int nrhs
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const int N = b.N;
+  if (!d.p.uv_adv) {  // no UV_ADV: no vertical advective flux (compute_vert_rhs_uv_terms.h:1)
+    for (int k = 0; k <= N; k++) A[k] = 0.0;
+    return;
+  }
   const long n2 = b.n2;
   const long s = dir == 0 ? 1 : b.nx2;
   const double* __restrict__ Uv = (dir == 0 ? F.u : F.v) + (long)(nrhs - 1) * b.n3 + ij;

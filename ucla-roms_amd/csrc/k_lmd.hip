@@ -2,10 +2,11 @@
 // (lmd_vmix.F:5-433 + lmd_kpp.F:7-651, alfabeta.F:4-79) and the Jerlov
 // short-wave fractions of lmd_swr_frac.F:13-88.
 //
-// Switch set: LMD_RIMIX, LMD_CONVEC, LMD_KPP, LMD_BKPP, LMD_NONLOCAL,
-// SMOOTH_RIG, SMOOTH_HBL, INT_AT_RHO_POINTS, MASKING (no LMD_DDMIX, no
-// MERGE_OVERLAP, no LIMIT_UNSTABLE_ONLY, no BULK_FRC) -- the reference's
-// Pipes_ana / Rivers_ana / Iceland configuration.
+// Switch set: LMD_KPP + LMD_BKPP (always together: roms_gpu.h), LMD_RIMIX,
+// LMD_CONVEC and LMD_NONLOCAL each switchable (Params), SMOOTH_RIG,
+// SMOOTH_HBL, INT_AT_RHO_POINTS, MASKING (no LMD_DDMIX, no MERGE_OVERLAP, no
+// LIMIT_UNSTABLE_ONLY, no BULK_FRC) -- Pipes_ana / Rivers_ana set all five,
+// Iceland all but LMD_CONVEC.
 //
 // Two column passes replace the reference's four j-sweeps:
 //   k_kpp_ext  over the extended range (I_EXT_RANGE x J_EXT_RANGE): one
@@ -243,8 +244,8 @@ __global__ void __launch_bounds__(64, 4) k_kpp_ext(Dev d, Range E, int tind, int
     const long o = (long)(k - 1) * n2;
     const double u0 = U[o], u1 = U[o + 1], v0 = V[o], v1 = V[o + sj];
     const double hz = Hz[o], zrk = zr[o], zwk = zw[(long)k * n2], bk = bvf[(long)k * n2];
-    // raw gradient Richardson number (lmd_vmix.F:157-165)
-    {
+    // raw gradient Richardson number (lmd_vmix.F:157-165), LMD_RIMIX only
+    if (P.lmd_rimix) {
       const double cff = 0.5 / (zrp - zrk);
       const double dudz = cff * (u0p - u0 + u1p - u1);
       const double dvdz = cff * (v0p - v0 + v1p - v1);
@@ -359,18 +360,24 @@ __global__ void __launch_bounds__(64) k_kpp_int(Dev d, Range R, EdgeClamp ec, in
 
   // raw interior Kv, Kt (= Ks) at level k from the smoothed Rig (lmd_vmix.F:249-272, 338-353)
   const double* __restrict__ rig = F.lmd_rig;
+  const bool rimix = P.lmd_rimix, convec = P.lmd_convec, nonlocal = P.lmd_nonlocal;
   auto raw_k = [&](int k, double& kv, double& kt) {
-    double r[3][3];
-    load3x3(b, ec, rig + (long)k * n2, i, j, r);
-    const double Rig = smooth_point(r, m);
-    const double cff = dmin(1., dmax(0., Rig));
-    double nu_sx = 1. - cff * cff;
-    nu_sx = nu_sx * nu_sx * nu_sx;
-    kv = kNuwm + kNu0m * nu_sx;
-    kt = kNuws + kNu0s * nu_sx;
-    if (Rig < 0.) {
-      kv = kv + kNu0c;
-      kt = kt + kNu0c;
+    if (rimix) {
+      double r[3][3];
+      load3x3(b, ec, rig + (long)k * n2, i, j, r);
+      const double Rig = smooth_point(r, m);
+      const double cff = dmin(1., dmax(0., Rig));
+      double nu_sx = 1. - cff * cff;
+      nu_sx = nu_sx * nu_sx * nu_sx;
+      kv = kNuwm + kNu0m * nu_sx;
+      kt = kNuws + kNu0s * nu_sx;
+      if (convec && Rig < 0.) {   // LMD_CONVEC (lmd_vmix.F:269-274)
+        kv = kv + kNu0c;
+        kt = kt + kNu0c;
+      }
+    } else {                      // internal waves only (lmd_vmix.F:262-264)
+      kv = kNuwm;
+      kt = kNuws;
     }
     const double zwk = zw[(long)k * n2];
     const double dist = zwk - zw0;
@@ -407,7 +414,7 @@ __global__ void __launch_bounds__(64) k_kpp_int(Dev d, Range R, EdgeClamp ec, in
       Ks = sqrt(a * a + q * q);
       if (Bfsfc < 0.) gh = -(kc.Cg * ssgm * ((1. - ssgm) * (1. - ssgm)));
     }
-    ghat[(long)k * n2] = gh;
+    if (nonlocal) ghat[(long)k * n2] = gh;   // LMD_NONLOCAL (lmd_kpp.F:436-446)
     const double sgmb = (zwk - zw0 + Zob) / (bbl + Zob);
     if (sgmb < 1.) {
       const double cff1 = sgmb * ((1. - sgmb) * (1. - sgmb));

@@ -166,6 +166,7 @@ __global__ void __launch_bounds__(256) k_uv_horiz(Dev d, Range R, int nrhs, UVBo
 
 void launch_uv_horiz(const Dev& d, hipStream_t s, int nrhs, int up) {
   const Bounds& b = d.b;
+  if (!d.p.uv_cor && !d.p.uv_adv) return;   // compute_horiz_rhs_uv_terms.h adds nothing
   Range R{b.istr, b.iend, b.jstr, b.jend};
   hipLaunchKernelGGL(k_uv_horiz, grid3_of(R, b.N), dim3(kBX, kBY), 0, s, d, R, nrhs, uv_bounds(b), up);
 }

@@ -64,7 +64,8 @@ __global__ void __launch_bounds__(64) k_step3d_t_v(Dev d, Range R, int nnew, int
     const double* __restrict__ Akt = F.Akt + (long)(iAkt - 1) * b.n3w + ij;
     const double* __restrict__ Wi = F.Wi + ij;
     const double DC0 = dt * F.pm[ij] * F.pn[ij];
-    const bool kppT = P.lmd && itrc == 1, kppS = P.lmd && itrc == 2 && P.salinity;
+    const bool kppT = P.lmd && itrc == 1, kppS = P.lmd_nonlocal && itrc == 2 && P.salinity;
+  auto gh = [&](long o) { return P.lmd_nonlocal ? F.ghat[ij + o] : 0.0; };
     const double sr = F.srflx[ij];
     // pipe_frc.F sources (step3d_t_ISO.F:927-934)
     const int pidx = P.npip > 0 ? F.pipe_idx[ij] : 0;
@@ -79,8 +80,9 @@ __global__ void __launch_bounds__(64) k_step3d_t_v(Dev d, Range R, int nnew, int
         t = t + dt * stf;
       }
       if (kppT) {
-        if (k <= N - 1) t = t + dt * (sr * F.swr_frac[ij + (long)k * n2] - F.ghat[ij + (long)k * n2] * (stf - sr));
-        if (k >= 2) t = t - dt * (sr * F.swr_frac[ij + o] - F.ghat[ij + o] * (stf - sr));
+        // without LMD_NONLOCAL the ghat term is absent: gh() = 0 leaves sr*swr_frac exact
+        if (k <= N - 1) t = t + dt * (sr * F.swr_frac[ij + (long)k * n2] - gh((long)k * n2) * (stf - sr));
+        if (k >= 2) t = t - dt * (sr * F.swr_frac[ij + o] - gh(o) * (stf - sr));
       } else if (kppS) {
         if (k <= N - 1) t = t + (-dt * F.ghat[ij + (long)k * n2] * stf);
         if (k >= 2) t = t - (-dt * F.ghat[ij + o] * stf);
@@ -204,7 +206,8 @@ __global__ void __launch_bounds__(kSegBlock) k_step3d_t_seg(Dev d, Range R, int 
   const double* __restrict__ Akt = F.Akt + (long)(iAkt - 1) * b.n3w + ij;
   const double* __restrict__ Wi = F.Wi + ij;
   const double DC0 = dt * F.pm[ij] * F.pn[ij];
-  const bool kppT = P.lmd && itrc == 1, kppS = P.lmd && itrc == 2 && P.salinity;
+  const bool kppT = P.lmd && itrc == 1, kppS = P.lmd_nonlocal && itrc == 2 && P.salinity;
+  auto gh = [&](long o) { return P.lmd_nonlocal ? F.ghat[ij + o] : 0.0; };
   const double sr = F.srflx[ij];
   const double stf = F.stflx[ij + (long)(itrc - 1) * n2];
   const int pidx = P.npip > 0 ? F.pipe_idx[ij] : 0;
@@ -219,8 +222,8 @@ __global__ void __launch_bounds__(kSegBlock) k_step3d_t_seg(Dev d, Range R, int 
       t = t + dt * stf;
     }
     if (kppT) {
-      if (k <= N - 1) t = t + dt * (sr * F.swr_frac[ij + (long)k * n2] - F.ghat[ij + (long)k * n2] * (stf - sr));
-      if (k >= 2) t = t - dt * (sr * F.swr_frac[ij + o] - F.ghat[ij + o] * (stf - sr));
+      if (k <= N - 1) t = t + dt * (sr * F.swr_frac[ij + (long)k * n2] - gh((long)k * n2) * (stf - sr));
+      if (k >= 2) t = t - dt * (sr * F.swr_frac[ij + o] - gh(o) * (stf - sr));
     } else if (kppS) {
       if (k <= N - 1) t = t + (-dt * F.ghat[ij + (long)k * n2] * stf);
       if (k >= 2) t = t - (-dt * F.ghat[ij + o] * stf);

@@ -105,7 +105,10 @@ __global__ void __launch_bounds__(64, 2) k_uv1_reg(Dev d, Range R, int nnew, int
   double A[N + 1];               // registers
   const ColLds B = col_lds(0, N);  // LDS: 26 KB per wave at N = 50
   // SPLINE_UV vertical flux (compute_vert_rhs_uv_terms.h), as uv_vert_flux_lds
-  {
+  if (!d.p.uv_adv) {
+#pragma unroll
+    for (int k = 0; k <= N; k++) A[k] = 0.0;
+  } else {
     const double* __restrict__ Uv = (dir == 0 ? F.u : F.v) + (long)(nrhs - 1) * b.n3 + ij;
     const double* __restrict__ Hz = F.Hz + ij;
     const double* __restrict__ We = F.We + ij;

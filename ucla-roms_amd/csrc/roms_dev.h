@@ -31,6 +31,8 @@ struct Bounds {
 // Physics switches (cppdefs.opt) and scalars of the run.
 struct Params {
   int nonlin_eos, salinity, lmd, uv_vis2, ts_dif2;
+  int lmd_rimix, lmd_convec, lmd_nonlocal;  // LMD_RIMIX, LMD_CONVEC, LMD_NONLOCAL (lmd != 0: MIXING+KPP+BKPP)
+  int uv_adv, uv_cor;                       // UV_ADV, UV_COR
   int s2d_split;  // 1: step2d as separate zeta / momentum kernels (ROMS_GPU_S2D_SPLIT=1)
   int colseg;     // 1: segment-partitioned column solvers (k_colseg.h; N > 63, ROMS_GPU_COLSEG=0/1)
   int colreg;     // 1: register-resident column solvers where compiled for N (ROMS_GPU_COLREG=0 disables)

@@ -307,7 +307,18 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
   g.d.b = make_bounds(*dims);
   g.d.b.nTS = cfg->salinity ? 2 : 1;
   Params& P = g.d.p;
-  P.nonlin_eos = cfg->nonlin_eos; P.salinity = cfg->salinity; P.lmd = cfg->lmd_mixing;
+  {
+    const int m = cfg->lmd_mixing, base = ROMS_LMD_MIXING | ROMS_LMD_KPP | ROMS_LMD_BKPP;
+    if (m != 0 && ((m & ~ROMS_LMD_ALL) || (m & base) != base || ((m & ROMS_LMD_CONVEC) && !(m & ROMS_LMD_RIMIX)))) {
+      g.err = "roms_gpu_init: lmd_mixing must be 0 or LMD_MIXING|LMD_KPP|LMD_BKPP [|RIMIX|NONLOCAL|CONVEC(needs RIMIX)]";
+      return -1;
+    }
+  }
+  P.nonlin_eos = cfg->nonlin_eos; P.salinity = cfg->salinity; P.lmd = cfg->lmd_mixing != 0;
+  P.lmd_rimix = (cfg->lmd_mixing & ROMS_LMD_RIMIX) != 0;
+  P.lmd_convec = (cfg->lmd_mixing & ROMS_LMD_CONVEC) != 0;
+  P.lmd_nonlocal = (cfg->lmd_mixing & ROMS_LMD_NONLOCAL) != 0;
+  P.uv_adv = cfg->uv_adv != 0; P.uv_cor = cfg->uv_cor != 0;
   P.uv_vis2 = cfg->uv_vis2; P.ts_dif2 = cfg->ts_dif2;
   {
     const char* e = getenv("ROMS_GPU_S2D_SPLIT");
@@ -321,7 +332,7 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
   if (cfg->obc < 0 || cfg->obc > 15) { g.err = "roms_gpu_init: obc must be a 4-bit edge mask"; return -1; }
   P.obc = cfg->obc & ((dims->ew_periodic ? 0 : 3) | (dims->ns_periodic ? 0 : 12));
   P.ubind = cfg->ubind;
-  P.curvgrid = cfg->curvgrid;
+  P.curvgrid = cfg->curvgrid && cfg->uv_adv;   // the curvature terms are part of UV_ADV
   if (P.obc) P.s2d_split = 1;  // open edges: separate zeta / zetabc / momentum kernels (step2d)
   for (int i = 0; i < kMaxFast; i++) { g.w1[i] = cfg->weight[0][i]; g.w2[i] = cfg->weight[1][i]; }
   // segment-partitioned column solvers (k_colseg.h) where the sequential
@@ -628,6 +639,7 @@ static int init_case_impl(const roms_case* c, int np_xi, int np_eta, void* comm,
   C.obc = c->case_id == ROMS_CASE_BASIN ? c->obc : 0;
   C.ubind = 0.1;  // Examples/Iceland/Iceland_parent/roms.in: ubind
   C.curvgrid = c->case_id == ROMS_CASE_BASIN ? c->curvgrid : 0;
+  C.uv_adv = c->uv_adv; C.uv_cor = c->uv_cor;
   C.Akv_bak = (fil || pipes) ? 0.0 : 1.0e-4; C.Akt_bak[0] = (fil || pipes) ? 0.0 : 1.0e-5; C.Akt_bak[1] = C.Akt_bak[0];
   int r = roms_gpu_init(&D, &C, device, comm);
   if (r) return r;
@@ -638,7 +650,7 @@ static int init_case_impl(const roms_case* c, int np_xi, int np_eta, void* comm,
   cs.west_exchng = D.west_exchng; cs.east_exchng = D.east_exchng;
   cs.south_exchng = D.south_exchng; cs.north_exchng = D.north_exchng;
   cs.host_wrap = comm == nullptr;   // with a communicator the device exchange fills halos
-  cs.salinity = c->salinity; cs.lmd = c->lmd_mixing; cs.surf_flux = c->case_id == ROMS_CASE_BASIN ? c->surf_flux : 0; cs.theta_s = C.theta_s; cs.theta_b = C.theta_b; cs.hc = C.hc; cs.rho0 = C.rho0;
+  cs.salinity = c->salinity; cs.lmd = c->lmd_mixing != 0; cs.surf_flux = c->case_id == ROMS_CASE_BASIN ? c->surf_flux : 0; cs.theta_s = C.theta_s; cs.theta_b = C.theta_b; cs.hc = C.hc; cs.rho0 = C.rho0;
   cs.Tcoef = C.Tcoef; cs.visc2 = 0.0; cs.tnu2 = 0.0; cs.Akv_bak = C.Akv_bak;
   cs.Akt_bak[0] = C.Akt_bak[0]; cs.Akt_bak[1] = C.Akt_bak[1];
   cs.sizex = c->sizex; cs.sizey = c->sizey;

@@ -28,6 +28,17 @@ FIELDS = ["h", "hinv", "f", "fomn", "pm", "pn", "dm_r", "dn_r", "dm_u", "dn_u", 
          ["dndx", "dmde"]
 FIELD_ID = {n: i for i, n in enumerate(FIELDS)}
 CASE_FILAMENT, CASE_BASIN, CASE_PIPES = 0, 1, 2
+# LMD switch bits (ROMS_LMD_* of include/roms_gpu.h)
+LMD_MIXING, LMD_KPP, LMD_BKPP, LMD_RIMIX, LMD_CONVEC, LMD_NONLOCAL = 1, 2, 4, 8, 16, 32
+LMD_ALL = 63       # tests/Pipes_ana/cppdefs.opt
+LMD_ICELAND = 47   # Examples/Iceland/Iceland_parent/cppdefs.opt: no LMD_CONVEC
+
+
+def lmd_bits(lmd):
+    """True -> every LMD switch (the Pipes_ana set), False -> 0, else the bits."""
+    if lmd is True:
+        return LMD_ALL
+    return int(lmd)
 
 
 class Dims(ctypes.Structure):
@@ -45,7 +56,8 @@ class Cfg(ctypes.Structure):
                 ("Akv_bak", ctypes.c_double), ("Akt_bak", ctypes.c_double * 2), ("Tcoef", ctypes.c_double),
                 ("T0", ctypes.c_double), ("Scoef", ctypes.c_double), ("S0", ctypes.c_double),
                 ("theta_s", ctypes.c_double), ("theta_b", ctypes.c_double), ("hc", ctypes.c_double),
-                ("obc", ctypes.c_int), ("ubind", ctypes.c_double), ("curvgrid", ctypes.c_int)]
+                ("obc", ctypes.c_int), ("ubind", ctypes.c_double), ("curvgrid", ctypes.c_int),
+                ("uv_adv", ctypes.c_int), ("uv_cor", ctypes.c_int)]
 
 
 class Tlev(ctypes.Structure):
@@ -62,7 +74,7 @@ class Case(ctypes.Structure):
                 ("lmd_mixing", ctypes.c_int), ("dt", ctypes.c_double), ("ndtfast", ctypes.c_int),
                 ("sizex", ctypes.c_double), ("sizey", ctypes.c_double), ("surf_flux", ctypes.c_int),
                 ("obc", ctypes.c_int), ("v_sponge", ctypes.c_double), ("island", ctypes.c_int),
-                ("curvgrid", ctypes.c_int)]
+                ("curvgrid", ctypes.c_int), ("uv_adv", ctypes.c_int), ("uv_cor", ctypes.c_int)]
 
 
 ROUTINES_T = ["set_huv", "omega", "prsgrd", "pre_step3d", "set_huv1", "step3d_uv1", "visc3d", "step2d",
@@ -212,12 +224,13 @@ class Model:
     @classmethod
     def from_case(cls, case_id, LLm, MMm, N, NT=1, salinity=False, nonlin_eos=False, dt=5.0, ndtfast=60,
                   sizex=12.8e3, sizey=3.2e3, device=0, np_xi=1, np_eta=1, comm=None, rank=0, lmd=False,
-                  surf_flux=False, obc=0, v_sponge=0.0, island=False, curvgrid=False):
+                  surf_flux=False, obc=0, v_sponge=0.0, island=False, curvgrid=False, uv_adv=True, uv_cor=True):
         """Analytic case on the whole grid, or on subdomain `rank` of an
-        np_xi x np_eta processor grid when a communicator is given."""
+        np_xi x np_eta processor grid when a communicator is given.
+        lmd: False, True (all LMD switches) or ROMS_LMD_* bits."""
         m = cls()
-        c = Case(case_id, LLm, MMm, N, NT, int(salinity), int(nonlin_eos), int(lmd), dt, ndtfast, sizex, sizey,
-                 int(surf_flux), int(obc), float(v_sponge), int(island), int(curvgrid))
+        c = Case(case_id, LLm, MMm, N, NT, int(salinity), int(nonlin_eos), lmd_bits(lmd), dt, ndtfast, sizex, sizey,
+                 int(surf_flux), int(obc), float(v_sponge), int(island), int(curvgrid), int(uv_adv), int(uv_cor))
         if comm is None and np_xi * np_eta == 1:
             m._chk(m.L.roms_gpu_init_case(ctypes.byref(c), device, ctypes.byref(m.t)), "roms_gpu_init_case")
         else:
