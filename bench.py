@@ -1,33 +1,43 @@
-"""Benchmark of the MI355X split-explicit ROMS step (BASELINE.json metric).
+"""Benchmark of the MI355X split-explicit ROMS step (BASELINE.json metric:
+model-seconds/wallclock-sec + grid-cell-updates/sec at 1/2/4/8 GPU; % HBM
+roofline).
 
-Workload (BASELINE.json configs[1]): Filament physics +
-salinity (linear EOS, T and S), 512x512x50 per GPU, dt=5 s, ndtfast=60 ->
-nfast=82, dx=100 m, dy=25 m, doubly periodic, synthetic analytic initial
-state.  One "step" = one full roms_step (main.F:333-520): 3 rho_eos, 3 omega,
-2 prsgrd, pre_step3d, set_HUV/HUV1, step3d_uv1, visc3d, 82 barotropic
-step2d_FB, step3d_uv2, step3d_t, t3dmix.  State is resident in HBM before
-the timed region; steady steps replay captured HIP graphs.
+Primary workload (BASELINE.json configs[1]): Filament
+physics + salinity (linear EOS, T and S), 512x512x50 per GPU, dt=5 s,
+ndtfast=60 -> nfast=82, dx=100 m, dy=25 m, doubly periodic, synthetic
+analytic initial state.  One "step" = one full roms_step (main.F:333-520):
+3 rho_eos, 3 omega, 2 prsgrd, pre_step3d, set_HUV/HUV1, step3d_uv1, visc3d,
+82 barotropic step2d_FB, step3d_uv2, step3d_t, t3dmix.  State is resident in
+HBM before the timed region; steady steps replay captured HIP graphs.  N GPUs:
+weak scaling on an npx x npe processor grid (1x1, 2x1, 2x2, 4x2) of 512x512
+subdomains of one periodic domain, halo exchanges inside the step graphs.
 
-N GPUs (one process each, torchrun): weak scaling on an npx x npe processor
-grid (1x1, 2x1, 2x2, 4x2, ...) of 512x512 subdomains of one periodic domain;
-halo exchanges go over RCCL (xGMI) inside the step graphs.
+Secondary workload, reported in the same JSON line as "c3" (SURVEY.md 8(d)
+C3, the north_star's roofline target): the 1024x1024x100 closed basin with
+NONLIN+SPLIT EOS, T+S and LMD_MIXING+KPP+BKPP+RIMIX+NONLOCAL (dt=300 s,
+nfast=82), strong-scaled over the same processor grid.
 
-value = grid-cell updates per second summed over ranks; model seconds per
-wall second beside it.  roofline: algorithmic bytes (SURVEY.md 8(d) pass
-counts) / mean launch duration measured with HIP events on the library
-stream, for the dominant kernel (C2: k_s2d_fb, one fast step, 35 2-D passes;
-C3: its routine pre_step3d); "roofline_routine" is the dominant routine and
-"routines" the full per-routine table.
+value = grid-cell updates per second summed over ranks (interior I*J*N per
+baroclinic step); model seconds per wall second beside it.  roofline: the
+dominant kernel's algorithmic bytes (SURVEY.md 8(d) pass counts) over its
+mean launch duration, measured with HIP events on the library stream;
+"routines" has every routine; "roofline_step" the whole step.
 
---workload c3 (not the default): SURVEY.md 8(d) C3, the 1024x1024x100 closed
-basin with NONLIN+SPLIT EOS, T+S and LMD/KPP/BKPP mixing (dt=300 s, nfast=82),
-strong-scaled over the processor grid (the north_star's roofline target).
+cpu_baseline (rank 0, N=1): the plain-C oracle (oracle/, the CPU restatement,
+"port") on a bounded sample of the same workloads, one process per available
+host core (P processes x 1 thread, each on its own cut of the grid, started
+together), run before the GPU is touched.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3] [--no-c3]
+With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py starts the N
+ranks itself (one process per GPU, RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set
+before any GPU call) and relays rank 0's line; under torchrun it is one rank.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -38,9 +48,8 @@ sys.path.insert(0, os.path.join(ROOT, "ucla-roms_amd"))
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 # C2 workload, per GPU
-LLM, MMM, NZ, NT = 512, 512, 50, 2
-DT, NDTFAST = 5.0, 60
-SIZEX, SIZEY = 51.2e3, 12.8e3
+C2_L, C2_N, NT, C2_DT, NDTFAST = 512, 50, 2, 5.0, 60
+C2_DX, C2_DY = 100.0, 25.0
 NT_TS = 2
 # C3 workload, whole domain (strong scaling)
 C3_L, C3_N, C3_DT, C3_DX = 1024, 100, 300.0, 2.0e3
@@ -76,103 +85,278 @@ def proc_grid(n):
     return npx, n // npx
 
 
-def cpu_baseline_c3(nsteps=2, L=128):
-    """Oracle on a bounded LxLx100 cut of the C3 basin (same switches, dx)."""
+# ---------------------------------------------------------------------------
+# CPU baseline: P oracle processes, one per core
+# ---------------------------------------------------------------------------
+def _cpu_worker(kind, L, M, nsteps):
+    """Child process: one oracle instance on an LxM cut; waits for GO on stdin
+    after init so all P processes step together; prints the step time."""
     import oracle
-    c = oracle.OrCfg()
-    c.LLm, c.MMm, c.N, c.NT = L, L, C3_N, 2
-    c.ew_periodic = c.ns_periodic = 0
-    c.salinity, c.nonlin_eos, c.lmd = 1, 1, oracle.LMD_ICELAND
-    c.case_id = oracle.CASE_BASIN
-    c.dt, c.ndtfast = C3_DT, NDTFAST
-    c.theta_s, c.theta_b, c.hc, c.rho0 = 6.0, 2.0, 250.0, 1027.5
-    c.rdrg, c.rdrg2, c.Zob = 0.0, 1.0e-3, 1.0e-2
-    c.Akv_bak = 1.0e-4
-    c.Akt_bak[0] = c.Akt_bak[1] = 1.0e-5
-    c.Tcoef, c.T0, c.Scoef, c.S0 = 0.20, 1.0, 0.822, 1.0
-    c.sizex = c.sizey = C3_DX * L
-    c.diag_np_xi = c.diag_np_eta = 1
-    o = oracle.Oracle(c)
-    o.init()
-    t0 = time.perf_counter()
-    o.step(nsteps)
-    dt_wall = time.perf_counter() - t0
-    cells = L * L * C3_N
-    return {"value": nsteps * cells / dt_wall, "unit": "cell-updates/s", "cores": 1, "kind": "port",
-            "sample": "%d roms_step of a %dx%dx%d cut of the C3 basin (LMD/KPP, nonlinear EOS) on the oracle "
-                      "(oracle/, gcc -O2, 1 thread), %.1f s" % (nsteps, L, L, C3_N, dt_wall),
-            "model_seconds_per_wallclock_sec": nsteps * C3_DT / dt_wall * cells / (C3_L * C3_L * C3_N)}
-
-
-def cpu_baseline(nsteps=3):
-    """Oracle (plain-C restatement, 1 thread) on the same 512x512x50 workload,
-    a bounded sample of `nsteps` steps after init."""
-    import oracle
-    cfg = oracle.filament_cfg(LLm=LLM, MMm=MMM, N=NZ, NT=NT, salinity=True, sizex=SIZEX, sizey=SIZEY,
-                              np_xi=1, np_eta=1)
+    if kind == "c2":
+        cfg = oracle.filament_cfg(LLm=L, MMm=M, N=C2_N, NT=NT, salinity=True, sizex=C2_DX * L, sizey=C2_DY * M,
+                                  np_xi=1, np_eta=1)
+    else:
+        cfg = oracle.OrCfg()
+        cfg.LLm, cfg.MMm, cfg.N, cfg.NT = L, M, C3_N, 2
+        cfg.ew_periodic = cfg.ns_periodic = 0
+        cfg.salinity, cfg.nonlin_eos, cfg.lmd = 1, 1, oracle.LMD_ICELAND
+        cfg.case_id = oracle.CASE_BASIN
+        cfg.dt, cfg.ndtfast = C3_DT, NDTFAST
+        cfg.theta_s, cfg.theta_b, cfg.hc, cfg.rho0 = 6.0, 2.0, 250.0, 1027.5
+        cfg.rdrg, cfg.rdrg2, cfg.Zob = 0.0, 1.0e-3, 1.0e-2
+        cfg.Akv_bak = 1.0e-4
+        cfg.Akt_bak[0] = cfg.Akt_bak[1] = 1.0e-5
+        cfg.Tcoef, cfg.T0, cfg.Scoef, cfg.S0 = 0.20, 1.0, 0.822, 1.0
+        cfg.sizex, cfg.sizey = C3_DX * L, C3_DX * M
+        cfg.diag_np_xi = cfg.diag_np_eta = 1
     o = oracle.Oracle(cfg)
     o.init()
+    print("READY", flush=True)
+    sys.stdin.readline()
     t0 = time.perf_counter()
     o.step(nsteps)
-    dt_wall = time.perf_counter() - t0
-    return {"value": nsteps * LLM * MMM * NZ / dt_wall, "unit": "cell-updates/s", "cores": 1, "kind": "port",
-            "sample": "%d roms_step of the 512x512x50 C2 workload on the oracle (oracle/, gcc -O2, 1 thread), %.1f s"
-                      % (nsteps, dt_wall),
-            "model_seconds_per_wallclock_sec": nsteps * DT / dt_wall}
+    print(json.dumps({"wall": time.perf_counter() - t0}), flush=True)
+
+
+def host_cores():
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    cap = os.environ.get("OMP_NUM_THREADS")   # the GPU box exports its CPU share (16) here
+    if cap and cap.isdigit() and int(cap) > 0:
+        n = min(n, int(cap))
+    return max(1, min(n, 16))
+
+
+def cpu_baseline(kind):
+    """P = host cores oracle processes, each stepping its own cut of the
+    workload grid (independent subdomains: no halo exchange between them),
+    started together; value = all cell updates / the slowest process's time."""
+    P = host_cores()
+    if kind == "c2":
+        L, M, nsteps, N, dt, full = C2_L, max(8, C2_L // P), 5, C2_N, C2_DT, C2_L * C2_L * C2_N
+    else:
+        L, M, nsteps, N, dt, full = C3_L, 32, 2, C3_N, C3_DT, C3_L * C3_L * C3_N
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    ps = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-worker", kind, str(L), str(M),
+                            str(nsteps)], stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, env=env)
+          for _ in range(P)]
+    try:
+        for p in ps:
+            if p.stdout.readline().strip() != "READY":
+                raise RuntimeError("cpu baseline worker failed")
+        for p in ps:
+            p.stdin.write("GO\n")
+            p.stdin.flush()
+        walls = [json.loads(p.stdout.readline())["wall"] for p in ps]
+    finally:
+        for p in ps:
+            try:
+                p.wait(timeout=120)
+            except subprocess.TimeoutExpired:
+                p.kill()
+    wall = max(walls)
+    cells = P * L * M * N * nsteps
+    v = cells / wall
+    what = ("C2 Filament+S, %d periodic %dx%dx%d cuts" % (P, L, M, N) if kind == "c2" else
+            "C3 basin (NONLIN+SPLIT EOS, LMD/KPP), %d closed %dx%dx%d cuts" % (P, L, M, N))
+    return {"value": v, "unit": "cell-updates/s", "cores": P, "kind": "port",
+            "layout": "%d processes x 1 thread (nproc %d)" % (P, os.cpu_count() or 0),
+            "sample": "%d roms_step of %s on the oracle (oracle/, gcc -O2 plain-C restatement), one process per core, "
+                      "no halo exchange between the cuts; slowest process %.1f s" % (nsteps, what, wall),
+            "model_seconds_per_wallclock_sec": v / full * dt}
+
+
+# ---------------------------------------------------------------------------
+# multi-rank launch
+# ---------------------------------------------------------------------------
+def launch_ranks(args, argv):
+    """Start args.gpus ranks of this script (one process per GPU) and relay
+    rank 0's JSON line.  Runs before anything touches the GPU."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ps = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_WORLD_SIZE=str(args.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        ps.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
+                                   stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    out = ps[0].stdout.read().decode()
+    rcs = [p.wait() for p in ps]
+    sys.stdout.write(out)
+    sys.stdout.flush()
+    return max(abs(rc) for rc in rcs)
+
+
+# ---------------------------------------------------------------------------
+# one workload on this rank
+# ---------------------------------------------------------------------------
+def run_workload(kind, romsgpu, comm, rank, world, local_rank, steps, warmup, timing_steps, barrier, allmax):
+    npx, npe = proc_grid(world)
+    c3 = kind == "c3"
+    if c3:
+        m = romsgpu.Model.from_case(romsgpu.CASE_BASIN, C3_L, C3_L, C3_N, NT, salinity=True, nonlin_eos=True,
+                                    lmd=romsgpu.LMD_ICELAND, dt=C3_DT, ndtfast=NDTFAST, sizex=C3_DX * C3_L,
+                                    sizey=C3_DX * C3_L, device=local_rank, np_xi=npx, np_eta=npe, comm=comm, rank=rank)
+        Lr, Mr, Nz, dt_step = m.Lm, m.Mm, C3_N, C3_DT
+        total_cells = C3_L * C3_L * C3_N
+    else:
+        m = romsgpu.Model.from_case(romsgpu.CASE_FILAMENT, C2_L * npx, C2_L * npe, C2_N, NT, salinity=True, dt=C2_DT,
+                                    ndtfast=NDTFAST, sizex=C2_DX * C2_L * npx, sizey=C2_DY * C2_L * npe,
+                                    device=local_rank, np_xi=npx, np_eta=npe, comm=comm, rank=rank)
+        assert (m.Lm, m.Mm) == (C2_L, C2_L)
+        Lr, Mr, Nz, dt_step = C2_L, C2_L, C2_N, C2_DT
+        total_cells = world * C2_L * C2_L * C2_N
+    nfast = m.t.nfast
+    m.step(warmup)
+    m.sync()
+    barrier()
+    t0 = time.perf_counter()
+    ev_ms = m.time_steps(steps)  # HIP events on the library stream around K steps
+    m.sync()
+    wall = time.perf_counter() - t0
+    barrier()
+    elapsed = allmax(max(wall, ev_ms / 1e3))
+
+    # per-routine rooflines: HIP events around each routine's launches
+    cells3 = Lr * Mr * Nz
+    passes = routine_passes(NT, NT_TS, lmd=c3)
+    routines = {}
+    for r in romsgpu.ROUTINES:
+        if passes.get(r, 0) == 0:   # kernel-level ids and routines off in this workload
+            continue
+        avg, n = m.time_routine(r, timing_steps)
+        per_step = n / timing_steps
+        nbytes = 35.0 * 8 * Lr * Mr if passes[r] is None else 8.0 * passes[r] * cells3
+        gbs = nbytes / (avg * 1e-3) / 1e9 if avg > 0 else 0.0
+        routines[r] = {"ms_per_call": avg, "calls_per_step": per_step, "ms_per_step": avg * per_step,
+                       "bytes_per_call": nbytes, "achieved_GBs": gbs, "frac": gbs / HBM_PEAK_GBS}
+    dom = max(routines, key=lambda k: routines[k]["ms_per_step"])
+    D = routines[dom]
+    # the fused barotropic kernel alone: 35 2-D passes per fast step over its
+    # launch time (one event interval per fast loop on a single rank)
+    fb_ms, fb_n = m.time_routine("k_s2d_fb", timing_steps)
+    fb_bytes = 35.0 * 8 * Lr * Mr
+    fb_gbs = fb_bytes / (fb_ms * 1e-3) / 1e9 if fb_ms > 0 else 0.0
+    kernel_fb = {"kernel": "k_s2d_fb", "ms_per_launch": fb_ms, "launches_per_step": fb_n / timing_steps,
+                 "ms_per_step": fb_ms * fb_n / timing_steps, "bytes_per_launch": fb_bytes,
+                 "achieved_GBs": fb_gbs, "frac": fb_gbs / HBM_PEAK_GBS}
+    transport = m.halo_transport() if comm is not None else "none (single rank)"
+    norms = m.diag()   # blow-up check as diag.F does (collective)
+    if not all(x == x and abs(x) < 1e30 for x in norms):
+        raise SystemExit("bench: non-finite diag norms %r" % norms)
+    ms_step = 1e3 * elapsed / steps
+    B = step_bytes(Lr, Mr, Nz, NT, NT_TS, nfast, lmd=c3)
+    step_gbs = B / (ms_step * 1e-3) / 1e9
+    m.close()
+    if not c3:
+        # dominant kernel by time per step in the C2 kernel trace
+        # (profiles/r2_*_c2_per_step.txt): the fused barotropic kernel
+        roofline = {"bound": "hbm", "achieved": fb_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": fb_gbs / HBM_PEAK_GBS, "traffic": pmc_kernel_traffic("k_s2d_fb"),
+                    "kernel": "k_s2d_fb", "bytes_per_launch": fb_bytes, "ms_per_launch": fb_ms}
+    else:
+        roofline = {"bound": "hbm", "achieved": D["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": D["frac"], "traffic": None, "kernel": dom + " (routine)",
+                    "bytes_per_launch": D["bytes_per_call"], "ms_per_launch": D["ms_per_call"]}
+    return {
+        "value": total_cells * steps / elapsed,
+        "ms_per_step": ms_step,
+        "model_seconds_per_wallclock_sec": steps * dt_step / elapsed,
+        "config": {"workload": ("C3: basin 1024x1024x100, NONLIN+SPLIT EOS, T+S, LMD KPP/BKPP/RIMIX/NONLOCAL, "
+                                "dt=300s, ndtfast=60 (nfast=%d)" % nfast) if c3 else
+                               "C2: Filament+S 512x512x50 per GPU, NT=2, dt=5s, ndtfast=60 (nfast=%d)" % nfast,
+                   "grid_per_gpu": [Lr, Mr, Nz], "proc_grid": [npx, npe], "NT": NT, "dt": dt_step, "nfast": nfast,
+                   "parallelism": "domain decomposition %dx%d" % (npx, npe), "halo_transport": transport},
+        "scaling": "strong" if c3 else "weak",
+        "steps": steps, "warmup": warmup,
+        "roofline": roofline,
+        "roofline_routine": {"bound": "hbm", "achieved": D["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": D["frac"], "traffic": None if c3 else pmc_traffic(dom),
+                             "routine": dom + (" (one fast step: k_s2d_fb + edges + halo)" if dom == "step2d" else ""),
+                             "bytes_per_launch": D["bytes_per_call"], "ms_per_launch": D["ms_per_call"]},
+        "roofline_step": {"bound": "hbm", "achieved": step_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": step_gbs / HBM_PEAK_GBS, "bytes_per_step": B},
+        "routines": routines,
+        "kernel_s2d_fb": kernel_fb,
+    }
+
+
+def _pmc():
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return {}
+    try:
+        return json.load(open(p))
+    except ValueError:
+        return {}
 
 
 def pmc_kernel_traffic(kernel):
-    """HBM bytes per dispatch of one kernel from profiles/pmc_traffic.json
-    (2*FETCH_SIZE + WRITE_SIZE), or None when absent."""
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if not os.path.exists(p):
-        return None
+    """HBM bytes per dispatch of one kernel (C2) from profiles/pmc_traffic.json
+    (2*FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md), or None when absent."""
     try:
-        k = json.load(open(p)).get("kernels", {}).get(kernel)
+        k = _pmc().get("kernels", {}).get(kernel)
         return None if k is None else float(k["traffic_bytes"]) / float(k["dispatches"])
-    except (ValueError, KeyError, TypeError, ZeroDivisionError):
+    except (KeyError, TypeError, ZeroDivisionError, ValueError):
         return None
 
 
 def pmc_traffic(routine):
-    """HBM bytes per launch of `routine` from the committed rocprofv3 PMC
-    summary (profiles/pmc_traffic.json, FETCH_SIZE*2 + WRITE_SIZE per
-    MI355X_MICROARCH.md), or None when absent."""
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if not os.path.exists(p):
-        return None
     try:
-        d = json.load(open(p))
-        r = d.get("routines", {}).get(routine)
+        r = _pmc().get("routines", {}).get(routine)
         return None if r is None else float(r["bytes_per_launch"])
-    except (ValueError, KeyError, TypeError):
+    except (KeyError, TypeError, ValueError):
         return None
 
 
 def main():
-    # the JSON line is the only thing on stdout: libraries (RCCL prints a
-    # version banner at init) write to fd 1, so point it at stderr for the run
-    sys.stdout.flush()
-    json_fd = os.dup(1)
-    os.dup2(2, 1)
+    if len(sys.argv) > 1 and sys.argv[1] == "--cpu-worker":
+        _cpu_worker(sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5]))
+        return 0
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--timing-steps", type=int, default=3, help="eager steps per routine for the event timings")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", choices=("c2", "c3"), default="c2")
+    ap.add_argument("--workload", choices=("c2", "c3"), default="c2", help="the workload of the primary line")
+    ap.add_argument("--no-c3", action="store_true", help="skip the secondary C3 object")
     args = ap.parse_args()
-    c3 = args.workload == "c3"
-
+    world_env = os.environ.get("WORLD_SIZE")
+    if args.gpus > 1 and world_env is None:
+        return launch_ranks(args, sys.argv[1:])
+    world = int(world_env or "1")
+    if world != args.gpus:
+        raise SystemExit("bench: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        # more ranks than GPUs (a rehearsal on a smaller box): ranks share devices
+        import torch
+        ndev = torch.cuda.device_count()   # does not initialise the GPU
+        if ndev > 0:
+            local_rank = local_rank % ndev
+
+    # CPU baseline first, before this process touches the GPU
+    cpu = {}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu[args.workload] = cpu_baseline(args.workload)
+        if args.workload == "c2" and not args.no_c3:
+            cpu["c3"] = cpu_baseline("c3")
+
+    # the JSON line is the only thing on stdout: libraries (RCCL prints a
+    # version banner at init) write to fd 1, so point it at stderr for the run
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     import romsgpu
 
     dist = None
     comm = None
-    npx, npe = proc_grid(world)
     # ROMS_BENCH_FORCE_COMM=1: take the multi-rank path even at world size 1
     # (RCCL comm + self-addressed exchanges; rehearses the N>1 plumbing)
     force = os.environ.get("ROMS_BENCH_FORCE_COMM") == "1"
@@ -190,122 +374,53 @@ def main():
         dist.broadcast(uid, src=0)
         comm = romsgpu.comm_create(bytes(uid.cpu().numpy().tobytes()), world, rank, local_rank)
 
-    if c3:
-        m = romsgpu.Model.from_case(romsgpu.CASE_BASIN, C3_L, C3_L, C3_N, NT, salinity=True, nonlin_eos=True,
-                                    lmd=romsgpu.LMD_ICELAND, dt=C3_DT, ndtfast=NDTFAST, sizex=C3_DX * C3_L, sizey=C3_DX * C3_L,
-                                    device=local_rank, np_xi=npx, np_eta=npe, comm=comm, rank=rank)
-        Lr, Mr, Nz, dt_step = m.Lm, m.Mm, C3_N, C3_DT
-    else:
-        m = romsgpu.Model.from_case(romsgpu.CASE_FILAMENT, LLM * npx, MMM * npe, NZ, NT, salinity=True, dt=DT,
-                                    ndtfast=NDTFAST, sizex=SIZEX * npx, sizey=SIZEY * npe, device=local_rank,
-                                    np_xi=npx, np_eta=npe, comm=comm, rank=rank)
-        assert (m.Lm, m.Mm) == (LLM, MMM)
-        Lr, Mr, Nz, dt_step = LLM, MMM, NZ, DT
-    nfast = m.t.nfast
-    m.step(args.warmup)
-    m.sync()
-
     def barrier():
         if dist is not None:
             import torch
             torch.cuda.synchronize()
             dist.barrier()
 
-    barrier()
-    m.sync()
-    t0 = time.perf_counter()
-    ev_ms = m.time_steps(args.steps)  # HIP events on the library stream around K steps
-    m.sync()
-    wall = time.perf_counter() - t0
-    barrier()
-    elapsed = max(wall, ev_ms / 1e3)
-    if dist is not None:
+    def allmax(x):
+        if dist is None:
+            return x
         import torch
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([x], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+        return float(tt.item())
 
-    # per-routine rooflines: HIP events around each routine's launches
-    cells3 = Lr * Mr * Nz
-    passes = routine_passes(NT, NT_TS, lmd=c3)
-    routines = {}
-    for r in romsgpu.ROUTINES:
-        if passes.get(r, 0) == 0:   # kernel-level ids and routines off in this workload
-            continue
-        avg, n = m.time_routine(r, args.timing_steps)
-        per_step = n / args.timing_steps
-        nbytes = 35.0 * 8 * Lr * Mr if passes[r] is None else 8.0 * passes[r] * cells3
-        gbs = nbytes / (avg * 1e-3) / 1e9 if avg > 0 else 0.0
-        routines[r] = {"ms_per_call": avg, "calls_per_step": per_step, "ms_per_step": avg * per_step,
-                       "bytes_per_call": nbytes, "achieved_GBs": gbs, "frac": gbs / HBM_PEAK_GBS}
-    dom = max(routines, key=lambda k: routines[k]["ms_per_step"])
-    D = routines[dom]
-    # the fused barotropic kernel alone (HIP events around its launches only):
-    # 35 2-D passes per fast step over its launch time
-    # (one event interval per fast loop on a single rank: 82 back-to-back launches)
-    fb_ms, fb_n = m.time_routine("k_s2d_fb", args.timing_steps)
-    fb_bytes = 35.0 * 8 * Lr * Mr
-    fb_gbs = fb_bytes / (fb_ms * 1e-3) / 1e9 if fb_ms > 0 else 0.0
-    kernel_fb = {"kernel": "k_s2d_fb", "ms_per_launch": fb_ms, "launches_per_step": fb_n / args.timing_steps,
-                 "ms_per_step": fb_ms * fb_n / args.timing_steps, "bytes_per_launch": fb_bytes,
-                 "achieved_GBs": fb_gbs, "frac": fb_gbs / HBM_PEAK_GBS}
-
-    transport = m.halo_transport() if comm is not None else "none (single rank)"
-    # sanity: the run must stay finite (blow-up check as diag.F does)
-    norms = m.diag()
-    if not all(map(lambda x: x == x and abs(x) < 1e30, norms)):
-        raise SystemExit("bench: non-finite diag norms %r" % norms)
-
-    ms_step = 1e3 * elapsed / args.steps
-    B = step_bytes(Lr, Mr, Nz, NT, NT_TS, nfast, lmd=c3)
-    step_gbs = B / (ms_step * 1e-3) / 1e9
-    traffic = None if c3 else pmc_traffic(dom)   # profiles/pmc_traffic.json is measured on C2
-
-    if not c3:
-        # C2: the dominant kernel (largest time per step in the kernel-trace
-        # table, profiles/r1_p5_c2_per_step.txt) is the fused barotropic kernel
-        roofline = {"bound": "hbm", "achieved": fb_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": fb_gbs / HBM_PEAK_GBS, "traffic": pmc_kernel_traffic("k_s2d_fb"),
-                    "kernel": "k_s2d_fb", "bytes_per_launch": fb_bytes, "ms_per_launch": fb_ms}
-    else:
-        # C3: the dominant kernel is k_pre_uv_seg (profiles/r1_p5_c3_per_step.txt),
-        # timed with the rest of its routine (pre_step3d)
-        roofline = {"bound": "hbm", "achieved": D["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": D["frac"], "traffic": None, "kernel": dom + " (routine)",
-                    "bytes_per_launch": D["bytes_per_call"], "ms_per_launch": D["ms_per_call"]}
+    prim = run_workload(args.workload, romsgpu, comm, rank, world, local_rank, args.steps, args.warmup,
+                        args.timing_steps, barrier, allmax)
     out = {
         "metric": "grid-cell-updates/sec",
-        "value": (C3_L * C3_L * C3_N if c3 else world * cells3) * args.steps / elapsed,
+        "value": prim["value"],
         "unit": "cell-updates/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": ms_step,
+        "ms_per_step": prim["ms_per_step"],
         "higher_is_better": True,
-        "scaling": "strong" if c3 else "weak",
+        "scaling": prim["scaling"],
         "vs_baseline": None,
         "dtype": "f64",
-        "data": ("synthetic (analytic closed basin, SURVEY.md 8(d) C3)" if c3 else
+        "data": ("synthetic (analytic closed basin, SURVEY.md 8(d) C3)" if args.workload == "c3" else
                  "synthetic (analytic Filament+S initial state, ana_grid/ana_init of tests/Filament)"),
-        "config": {"workload": ("C3: basin 1024x1024x100, NONLIN+SPLIT EOS, T+S, LMD/KPP/BKPP, dt=300s, ndtfast=60 "
-                                "(nfast=%d)" % nfast) if c3 else
-                               "C2: Filament+S 512x512x50 per GPU, NT=2, dt=5s, ndtfast=60 (nfast=%d)" % nfast,
-                   "grid_per_gpu": [Lr, Mr, Nz], "proc_grid": [npx, npe], "NT": NT, "dt": dt_step, "nfast": nfast,
-                   "parallelism": "domain decomposition %dx%d" % (npx, npe), "halo_transport": transport},
-        "model_seconds_per_wallclock_sec": args.steps * dt_step / elapsed,
-        "roofline": roofline,
-        "roofline_routine": {"bound": "hbm", "achieved": D["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                             "frac": D["frac"], "traffic": traffic,
-                             "routine": dom + (" (one fast step: k_s2d_fb + edges + halo)" if dom == "step2d" else ""),
-                             "bytes_per_launch": D["bytes_per_call"], "ms_per_launch": D["ms_per_call"]},
-        "roofline_step": {"bound": "hbm", "achieved": step_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                          "frac": step_gbs / HBM_PEAK_GBS, "bytes_per_step": B},
-        "routines": routines,
-        "kernel_s2d_fb": kernel_fb,
+        "config": prim["config"],
+        "model_seconds_per_wallclock_sec": prim["model_seconds_per_wallclock_sec"],
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline_c3() if c3 else cpu_baseline()
-    m.close()
+    for k in ("roofline", "roofline_routine", "roofline_step", "routines", "kernel_s2d_fb"):
+        out[k] = prim[k]
+    if args.workload in cpu:
+        out["cpu_baseline"] = cpu[args.workload]
+    if args.workload == "c2" and not args.no_c3:
+        # the north_star's target configuration, fewer steps (84 ms each on one GPU)
+        sec = run_workload("c3", romsgpu, comm, rank, world, local_rank, min(args.steps, 10), min(args.warmup, 2),
+                           min(args.timing_steps, 2), barrier, allmax)
+        sec["metric"] = "grid-cell-updates/sec"
+        sec["unit"] = "cell-updates/s"
+        sec["data"] = "synthetic (analytic closed basin, SURVEY.md 8(d) C3)"
+        if "c3" in cpu:
+            sec["cpu_baseline"] = cpu["c3"]
+        out["c3"] = sec
     if comm is not None:
         romsgpu.comm_destroy(comm)
     if rank == 0:
@@ -313,7 +428,8 @@ def main():
         os.write(json_fd, (json.dumps(out) + "\n").encode())
     if dist is not None:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

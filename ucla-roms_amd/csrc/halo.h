@@ -27,22 +27,26 @@ struct RomsComm;  // opaque communicator handle of the C ABI
 
 // IPC transport (one process per GPU over an RCCL communicator): the pack
 // kernel writes each message straight into the neighbour's receive buffer
-// (IPC-mapped, uncached, double-buffered by exchange parity) and its last
-// block raises the neighbour's arrival counter (system-scope release); a
-// one-block kernel waits for the counters of this rank's receive slots
-// (acquire, bounded spin), then unpack.  Enabled only after a start-up
-// self-test reproduced the RCCL exchange bitwise on every rank.
+// (IPC-mapped, uncached, double-buffered by exchange parity); a one-block
+// kernel, ordered after the pack by the kernel boundary, raises the
+// neighbours' arrival counters (system-scope release) and waits for the
+// counters of this rank's receive slots (acquire; a timeout is fatal); then
+// unpack.  Enabled only after a start-up self-test reproduced the RCCL
+// exchange bitwise on every rank.
 struct HaloIpc {
   double* rbuf2 = nullptr;              // [2 parities][8 slots][cap], written by the neighbours
   unsigned long long* flags = nullptr;  // [8] messages received per slot
-  unsigned int* cnt = nullptr;          // [8] pack-block counters (last block signals), [8]: receive blocks
   unsigned long long* seq = nullptr;    // exchanges completed by this rank
-  int* err = nullptr;                   // set when a wait timed out
+  int* err_dev = nullptr;               // set when a wait timed out (device copy)
+  int* err_host = nullptr;              // same, host-mapped (host entries poll it)
   double* prbuf[8] = {};                // direction d's neighbour: its rbuf2
   unsigned long long* pflags[8] = {};   // ... and its flags
   std::vector<void*> opened;            // IPC mappings to close
   long long timeout_ticks = 0;          // wall_clock64 ticks before a wait gives up
-  int fused_recv = 0;                   // wait + unpack in one kernel (k_halo_recv_ipc, opt-in)
+  // test hook (ROMS_GPU_IPC_TEST_DROP=n): the n-th exchange after setup does
+  // not signal its neighbours, so their waits time out (eager steps only)
+  mutable long nexch = 0;
+  long drop_at = -1;
   int ok = 0;
 };
 
@@ -83,5 +87,7 @@ void halo_join(Halo& H, hipStream_t s);
 int halo_allgather(const Halo& H, hipStream_t s, const double* in, int n, double* out);
 // 1 if the IPC transport is in use, 0 if RCCL; -1 if a wait timed out since setup
 int halo_transport(const Halo& H);
+// true once an IPC wait timed out: the exchanges since are invalid (fatal)
+bool halo_failed(const Halo& H);
 
 }  // namespace roms

@@ -103,65 +103,52 @@ struct IpcPtrs {
   unsigned long long* pflags[8];
   double* rbuf2;
   unsigned long long* flags;
-  unsigned int* cnt;
   unsigned long long* seq;
-  int* err;
+  int* err_dev;     // device copy of the error state (read by every pack block)
+  int* err_host;    // host-mapped copy (polled by the host entries without a sync)
   long long timeout;
 };
-// pack straight into the neighbour's slot opp(d) of parity seq&1
-#ifndef ROMS_IPC_SYSFENCE
-#define ROMS_IPC_SYSFENCE 0
-#endif
-// The messages are uncached stores (no L2 copy to write back), so ordering
-// them before the arrival counters needs no cache maintenance: each block
-// waits for its own stores to complete, counts itself, and the last block of
-// the grid raises the neighbours' counters.  (With a system-scope fence per
-// block -- an L2 write-back each -- a pack launch measured 54 us.)
+// pack straight into the neighbour's slot opp(d) of parity seq&1.  After a
+// failed wait (err_dev set) nothing more is written into a neighbour's
+// buffers: a rank that gave up must not overwrite a slot the neighbour has
+// not unpacked yet.
 __global__ void __launch_bounds__(256) k_halo_pack_ipc(HaloGeom g, ExchList L, IpcPtrs P, long cap) {
   const int dir = blockIdx.z;
-  if (g.active[dir]) {
-    const long cnt = g.cnt[dir];
-    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    const unsigned long long par = *P.seq & 1ull;
-    int lev = blockIdx.y;
-    const int q = list_slot(L, lev);
-    if (e < cnt && lev < L.nlev[q]) {
-      int i, j;
-      halo_src(g, dir, e, i, j);
-      P.prbuf[dir][((long)par * 8 + kOpp[dir]) * cap + (long)blockIdx.y * cnt + e] =
-          L.p[q][(long)(i + 1) + (long)(j + 1) * g.nx2 + (long)lev * g.n2];
-    }
-  }
-  // this block's (uncached) stores complete before its count: a wait on the
-  // store counter only -- an agent/system fence would also write back and
-  // invalidate the L2 (buffer_wbl2/buffer_inv), which the payload never uses
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned nb = gridDim.x * gridDim.y * gridDim.z;
-    if (atomicAdd(&P.cnt[0], 1u) == nb - 1) {   // every block of the grid is done
-      P.cnt[0] = 0;
-#if ROMS_IPC_SYSFENCE
-      __threadfence_system();
-#endif
-      for (int d = 0; d < 8; d++)
-        if (g.active[d])
-          __hip_atomic_fetch_add(P.pflags[d] + kOpp[d], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+  if (!g.active[dir] || *P.err_dev) return;
+  const long cnt = g.cnt[dir];
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned long long par = *P.seq & 1ull;
+  int lev = blockIdx.y;
+  const int q = list_slot(L, lev);
+  if (e < cnt && lev < L.nlev[q]) {
+    int i, j;
+    halo_src(g, dir, e, i, j);
+    P.prbuf[dir][((long)par * 8 + kOpp[dir]) * cap + (long)blockIdx.y * cnt + e] =
+        L.p[q][(long)(i + 1) + (long)(j + 1) * g.nx2 + (long)lev * g.n2];
   }
 }
-// wait until every active receive slot holds this exchange's message
-// (bounded: a timeout sets *err instead of hanging), then count the exchange
-__global__ void __launch_bounds__(64) k_halo_wait_ipc(HaloGeom g, IpcPtrs P) {
+// Signal + wait, one block.  The kernel boundary after k_halo_pack_ipc
+// orders every block's payload stores (uncached, written through to the
+// neighbour's memory) before this kernel runs; each active direction's
+// neighbour then sees its arrival counter raised with a system-scope
+// release.  Next, wait (acquire) until every active receive slot holds this
+// exchange's message.  The wait is bounded (P.timeout; ROMS_GPU_IPC_TIMEOUT
+// seconds): a timeout is fatal -- it sets the error state, which every later
+// pack skips on and every host entry reports (roms_gpu_last_error) -- so a
+// missing message never turns into silently stale halos.
+__global__ void __launch_bounds__(64) k_halo_wait_ipc(HaloGeom g, IpcPtrs P, int nosignal) {
   const int h = threadIdx.x;
   const unsigned long long want = *P.seq + 1ull;
-  if (h < 8 && g.active[h]) {
+  const bool dead = *P.err_dev != 0;
+  if (h < 8 && g.active[h] && !dead && !nosignal)
+    __hip_atomic_fetch_add(P.pflags[h] + kOpp[h], 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (h < 8 && g.active[h] && !dead) {
     const long long t0 = wall_clock64();
     while (__hip_atomic_load(P.flags + h, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < want) {
       __builtin_amdgcn_s_sleep(2);
       if (wall_clock64() - t0 > P.timeout) {
-        atomicExch(P.err, 1);
+        atomicExch(P.err_dev, 1);
+        __hip_atomic_store(P.err_host, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
     }
@@ -171,7 +158,7 @@ __global__ void __launch_bounds__(64) k_halo_wait_ipc(HaloGeom g, IpcPtrs P) {
 }
 __global__ void __launch_bounds__(256) k_halo_unpack_ipc(HaloGeom g, ExchList L, IpcPtrs P, long cap) {
   const int h = blockIdx.z;
-  if (!g.active[h]) return;
+  if (!g.active[h] || *P.err_dev) return;
   const long cnt = g.cnt[h];
   const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= cnt) return;
@@ -183,46 +170,6 @@ __global__ void __launch_bounds__(256) k_halo_unpack_ipc(HaloGeom g, ExchList L,
   halo_dst(g, h, e, i, j);
   L.p[q][(long)(i + 1) + (long)(j + 1) * g.nx2 + (long)lev * g.n2] =
       P.rbuf2[((long)par * 8 + h) * cap + (long)blockIdx.y * cnt + e];
-}
-// wait + unpack in one launch: each block waits (thread 0, bounded spin) for
-// its slot's counter, then scatters; the last block to finish counts the
-// exchange (cnt[8] is the block counter)
-__global__ void __launch_bounds__(256) k_halo_recv_ipc(HaloGeom g, ExchList L, IpcPtrs P, long cap) {
-  const int h = blockIdx.z;
-  const unsigned long long s0 = *P.seq, par = s0 & 1ull;
-  if (g.active[h]) {
-    __shared__ int ready;
-    if (threadIdx.x == 0) {
-      const long long t0 = wall_clock64();
-      while (__hip_atomic_load(P.flags + h, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < s0 + 1ull) {
-        __builtin_amdgcn_s_sleep(2);
-        if (wall_clock64() - t0 > P.timeout) {
-          atomicExch(P.err, 1);
-          break;
-        }
-      }
-      ready = 1;
-    }
-    __syncthreads();
-    const long cnt = g.cnt[h];
-    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    int lev = blockIdx.y;
-    const int q = list_slot(L, lev);
-    if (ready && e < cnt && lev < L.nlev[q]) {
-      int i, j;
-      halo_dst(g, h, e, i, j);
-      L.p[q][(long)(i + 1) + (long)(j + 1) * g.nx2 + (long)lev * g.n2] =
-          P.rbuf2[((long)par * 8 + h) * cap + (long)blockIdx.y * cnt + e];
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned nb = gridDim.x * gridDim.y * gridDim.z;
-    if (atomicAdd(&P.cnt[8], 1u) == nb - 1) {   // every block has read *seq
-      P.cnt[8] = 0;
-      *P.seq = s0 + 1ull;
-    }
-  }
 }
 
 // ---- in-process transport: subdomains driven by threads of one process ----
@@ -327,41 +274,41 @@ static void ipc_release(Halo& H);
 
 // IPC transport setup: buffers, handle exchange (allgather over the RCCL
 // communicator), mapping of the neighbours' buffers, then a self-test that
-// must reproduce the RCCL exchange bitwise on every rank (three exchanges of
-// a two-level test field, both buffer parities) before the transport is used.
-// Any failure anywhere leaves every rank on RCCL.
+// must reproduce the RCCL exchange bitwise on every rank (kSelfTestRounds
+// exchanges of a two-level test field, alternating buffer parities, several
+// exchanges queued back to back) before the transport is used.  Any failure
+// anywhere leaves every rank on RCCL; every rank takes part in every
+// collective whatever happened locally.
 static void ipc_setup(Halo& H) {
+  constexpr int kSelfTestRounds = 6;
   HaloIpc& I = H.ipc;
   RomsComm* c = H.comm;
   const int me = c->rank, nr = c->nranks;
-  hipStream_t s;
-  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return;
+  hipStream_t s = H.cs;   // created by halo_setup before this call
   double ok = 1.0;
   const size_t rbytes = (size_t)16 * H.cap * sizeof(double);
   if (hipExtMallocWithFlags((void**)&I.rbuf2, rbytes, hipDeviceMallocUncached) != hipSuccess ||
       hipExtMallocWithFlags((void**)&I.flags, 8 * sizeof(unsigned long long), hipDeviceMallocUncached) != hipSuccess ||
-      hipMalloc(&I.cnt, 9 * sizeof(unsigned int)) != hipSuccess ||
-      hipMalloc(&I.seq, sizeof(unsigned long long)) != hipSuccess || hipMalloc(&I.err, sizeof(int)) != hipSuccess)
+      hipMalloc(&I.seq, sizeof(unsigned long long)) != hipSuccess || hipMalloc(&I.err_dev, sizeof(int)) != hipSuccess ||
+      hipHostMalloc((void**)&I.err_host, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
     ok = 0.0;
   hipIpcMemHandle_t hr{}, hf{};
   if (ok != 0.0 && (hipMemset(I.rbuf2, 0, rbytes) != hipSuccess ||
                     hipMemset(I.flags, 0, 8 * sizeof(unsigned long long)) != hipSuccess ||
-                    hipMemset(I.cnt, 0, 9 * sizeof(unsigned int)) != hipSuccess ||
                     hipMemset(I.seq, 0, sizeof(unsigned long long)) != hipSuccess ||
-                    hipMemset(I.err, 0, sizeof(int)) != hipSuccess || hipIpcGetMemHandle(&hr, I.rbuf2) != hipSuccess ||
+                    hipMemset(I.err_dev, 0, sizeof(int)) != hipSuccess || hipIpcGetMemHandle(&hr, I.rbuf2) != hipSuccess ||
                     hipIpcGetMemHandle(&hf, I.flags) != hipSuccess))
     ok = 0.0;
+  if (I.err_host) *I.err_host = 0;
   int dev = 0, khz = 0;
   (void)hipGetDevice(&dev);
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) ok = 0.0;
-  I.timeout_ticks = (long long)khz * 1000LL * 2;   // 2 s
+  double tsec = 60.0;   // ROMS_GPU_IPC_TIMEOUT: seconds a wait may take before the run fails
   {
-    // wait + unpack fused into one launch measured no faster than the two
-    // kernels (12.7 vs 12.3 ms/step, one GPU, all exchanges through the
-    // transport): opt-in, ROMS_GPU_HALO_IPC_FUSED=1
-    const char* e = getenv("ROMS_GPU_HALO_IPC_FUSED");
-    I.fused_recv = e && e[0] == '1';
+    const char* e = getenv("ROMS_GPU_IPC_TIMEOUT");
+    if (e && atof(e) > 0.0) tsec = atof(e);
   }
+  I.timeout_ticks = (long long)((double)khz * 1000.0 * tsec);
   // handles of every rank: 2 x 64 B = 16 doubles, bit patterns carried as is
   static_assert(sizeof(hipIpcMemHandle_t) == 64, "IPC handle size");
   std::vector<double> mine(17), all((size_t)17 * nr);
@@ -398,43 +345,57 @@ static void ipc_setup(Halo& H) {
   for (int r = 0; r < nr; r++) ok = ok != 0.0 && all[r] != 0.0 ? 1.0 : 0.0;
   if (ok != 0.0) {
     const long n2 = H.plan.g.n2, n = 2 * n2;
-    double *A = nullptr, *B = nullptr;
+    std::vector<double*> A(kSelfTestRounds, nullptr), B(kSelfTestRounds, nullptr);
     std::vector<double> h(n), ha(n), hb(n);
-    if (hipMalloc(&A, n * sizeof(double)) != hipSuccess || hipMalloc(&B, n * sizeof(double)) != hipSuccess) ok = 0.0;
-    const ExchList LA{{A}, {2}, 1}, LB{{B}, {2}, 1};
-    for (int round = 0; round < 3 && ok != 0.0; round++) {
-      for (long q = 0; q < n; q++) h[q] = 1.0e7 * (me + 1) + 1.0e3 * round + (double)q + 0.25;
-      if (hipMemcpy(A, h.data(), n * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
-          hipMemcpy(B, h.data(), n * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) { ok = 0.0; break; }
-      I.ok = 0;
-      halo_exchange(H, s, LA);      // RCCL
-      I.ok = 1;
-      halo_exchange(H, s, LB);      // IPC
-      I.ok = 0;
-      int e = 0;
-      if (hipStreamSynchronize(s) != hipSuccess || hipMemcpy(ha.data(), A, n * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess ||
-          hipMemcpy(hb.data(), B, n * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess ||
-          hipMemcpy(&e, I.err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+    for (int r = 0; r < kSelfTestRounds; r++)
+      if (hipMalloc(&A[r], n * sizeof(double)) != hipSuccess || hipMalloc(&B[r], n * sizeof(double)) != hipSuccess)
         ok = 0.0;
-      if (e != 0 || std::memcmp(ha.data(), hb.data(), n * sizeof(double)) != 0) ok = 0.0;
+    for (int r = 0; r < kSelfTestRounds && ok != 0.0; r++) {
+      for (long q = 0; q < n; q++) h[q] = 1.0e7 * (me + 1) + 1.0e3 * r + (double)q + 0.25;
+      if (hipMemcpy(A[r], h.data(), n * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
+          hipMemcpy(B[r], h.data(), n * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) ok = 0.0;
     }
-    if (A) (void)hipFree(A);
-    if (B) (void)hipFree(B);
+    if (ok != 0.0) {
+      // the reference result: RCCL; then the IPC exchanges queued back to
+      // back on the stream (both parities, no host sync in between)
+      I.ok = 0;
+      for (int r = 0; r < kSelfTestRounds; r++) halo_exchange(H, s, ExchList{{A[r]}, {2}, 1});
+      I.ok = 1;
+      for (int r = 0; r < kSelfTestRounds; r++) halo_exchange(H, s, ExchList{{B[r]}, {2}, 1});
+      I.ok = 0;
+      if (hipStreamSynchronize(s) != hipSuccess || *I.err_host != 0) ok = 0.0;
+      for (int r = 0; r < kSelfTestRounds && ok != 0.0; r++) {
+        if (hipMemcpy(ha.data(), A[r], n * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess ||
+            hipMemcpy(hb.data(), B[r], n * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess ||
+            std::memcmp(ha.data(), hb.data(), n * sizeof(double)) != 0)
+          ok = 0.0;
+      }
+    }
+    for (int r = 0; r < kSelfTestRounds; r++) {
+      if (A[r]) (void)hipFree(A[r]);
+      if (B[r]) (void)hipFree(B[r]);
+    }
     v = ok;
     if (halo_allgather(H, s, &v, 1, all.data()) != 0) ok = 0.0;
     for (int r = 0; r < nr; r++) ok = ok != 0.0 && all[r] != 0.0 ? 1.0 : 0.0;
   }
   (void)hipStreamSynchronize(s);
-  (void)hipStreamDestroy(s);
-  if (ok != 0.0) I.ok = 1;
-  else ipc_release(H);
+  if (ok != 0.0) {
+    I.ok = 1;
+    const char* e = getenv("ROMS_GPU_IPC_TEST_DROP");
+    I.drop_at = e ? atol(e) : -1;
+    I.nexch = 0;
+  } else {
+    ipc_release(H);
+  }
 }
 
 int halo_transport(const Halo& H) {
   if (!H.ipc.ok) return 0;
-  int e = 0;
-  if (hipMemcpy(&e, H.ipc.err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess || e != 0) return -1;
-  return 1;
+  return halo_failed(H) ? -1 : 1;
+}
+bool halo_failed(const Halo& H) {
+  return H.ipc.ok && H.ipc.err_host && __atomic_load_n(H.ipc.err_host, __ATOMIC_ACQUIRE) != 0;
 }
 
 int halo_setup(Halo& H, RomsComm* comm, const HaloPlan& plan, int maxlev, std::string& err) {
@@ -481,9 +442,9 @@ static void ipc_release(Halo& H) {
   I.opened.clear();
   if (I.rbuf2) (void)hipFree(I.rbuf2);
   if (I.flags) (void)hipFree(I.flags);
-  if (I.cnt) (void)hipFree(I.cnt);
   if (I.seq) (void)hipFree(I.seq);
-  if (I.err) (void)hipFree(I.err);
+  if (I.err_dev) (void)hipFree(I.err_dev);
+  if (I.err_host) (void)hipHostFree(I.err_host);
   I = HaloIpc{};
 }
 void halo_free(Halo& H) {
@@ -516,19 +477,17 @@ namespace {
 IpcPtrs ipc_ptrs(const Halo& H) {
   IpcPtrs P;
   for (int d = 0; d < 8; d++) { P.prbuf[d] = H.ipc.prbuf[d]; P.pflags[d] = H.ipc.pflags[d]; }
-  P.rbuf2 = H.ipc.rbuf2; P.flags = H.ipc.flags; P.cnt = H.ipc.cnt; P.seq = H.ipc.seq; P.err = H.ipc.err;
+  P.rbuf2 = H.ipc.rbuf2; P.flags = H.ipc.flags; P.seq = H.ipc.seq;
+  P.err_dev = H.ipc.err_dev; P.err_host = H.ipc.err_host;
   P.timeout = H.ipc.timeout_ticks;
   return P;
 }
 void exchange_ipc(const Halo& H, hipStream_t s, const ExchList& L, const dim3& grid) {
   const IpcPtrs P = ipc_ptrs(H);
   hipLaunchKernelGGL(k_halo_pack_ipc, grid, dim3(256), 0, s, H.plan.g, L, P, H.cap);
-  if (H.ipc.fused_recv) {
-    hipLaunchKernelGGL(k_halo_recv_ipc, grid, dim3(256), 0, s, H.plan.g, L, P, H.cap);
-  } else {
-    hipLaunchKernelGGL(k_halo_wait_ipc, dim3(1), dim3(64), 0, s, H.plan.g, P);
-    hipLaunchKernelGGL(k_halo_unpack_ipc, grid, dim3(256), 0, s, H.plan.g, L, P, H.cap);
-  }
+  const int drop = H.ipc.drop_at >= 0 && H.ipc.nexch++ == H.ipc.drop_at;
+  hipLaunchKernelGGL(k_halo_wait_ipc, dim3(1), dim3(64), 0, s, H.plan.g, P, drop);
+  hipLaunchKernelGGL(k_halo_unpack_ipc, grid, dim3(256), 0, s, H.plan.g, L, P, H.cap);
 }
 }  // namespace
 

@@ -88,11 +88,23 @@ void rank_extent(int LL, int np, int node, int& len, int& sw) {
       return -1;                                        \
     }                                                   \
   } while (0)
+// A timed-out IPC halo wait is fatal (the reference's MPI_Waitall never
+// gives up; here the wait is bounded so a lost peer cannot hang the GPU):
+// every later entry reports it instead of computing on stale halos.
+#define REQUIRE_HALO_OK()                                                                    \
+  do {                                                                                       \
+    if (g.d.halo && halo_failed(g.halo)) {                                                   \
+      g.err = "roms_gpu: a halo exchange wait timed out (IPC transport, ROMS_GPU_IPC_TIMEOUT);" \
+              " the state since is invalid";                                                 \
+      return -6;                                                                             \
+    }                                                                                        \
+  } while (0)
 // every entry but step2d first joins a fast-loop exchange still in flight on
 // the halo stream (launch_step2d overlaps it with the next fast step)
 #define REQUIRE_INIT()                                  \
   do {                                                  \
     REQUIRE_INIT_NOJOIN();                              \
+    REQUIRE_HALO_OK();                                  \
     if (g.d.halo) halo_join(g.halo, g.s);               \
   } while (0)
 
@@ -466,11 +478,13 @@ int roms_gpu_copy_out(int id, double* dst, long count) {
   if (id < 0 || id >= ROMS_NFIELDS || count != g.f[id].count) { g.err = "roms_gpu_copy_out: bad field/size"; return -1; }
   CHECK_HIP(hipMemcpyAsync(dst, g.f[id].d, (size_t)count * sizeof(double), hipMemcpyDeviceToHost, g.s));
   CHECK_HIP(hipStreamSynchronize(g.s));
+  REQUIRE_HALO_OK();
   return 0;
 }
 int roms_gpu_sync(void) {
   REQUIRE_INIT();
   CHECK_HIP(hipStreamSynchronize(g.s));
+  REQUIRE_HALO_OK();
   return post_launch();
 }
 
@@ -495,12 +509,13 @@ ROUTINE(roms_gpu_set_depth, launch_set_depth(g.d, g.s, T))
 #undef ROUTINE
 
 int roms_gpu_halo_transport(void) {
-  REQUIRE_INIT();
+  REQUIRE_INIT_NOJOIN();
   return g.d.halo ? halo_transport(g.halo) : 0;
 }
 
 int roms_gpu_step2d(const roms_tlev* t) {
   REQUIRE_INIT_NOJOIN();   // keeps the previous fast step's exchange in flight
+  REQUIRE_HALO_OK();
   const Tlev T = to_tlev(t);
   launch_step2d(g.d, g.s, T, g.w1, g.w2);
   return post_launch();
@@ -542,6 +557,16 @@ int roms_gpu_set_pipe_frc(int npip, const int* pipe_idx, const double* pipe_flx,
     for (auto& kv : g.graphs) (void)hipGraphExecDestroy(kv.second);
     g.graphs.clear();
     if (F.pipe_idx) (void)hipFree(F.pipe_idx);
+    F.pipe_idx = nullptr;
+    // free the previous pipe arrays (they are tracked in g.scratch)
+    for (double** q : {&F.pipe_flx, &F.pipe_prf, &F.pipe_trc}) {
+      if (!*q) continue;
+      for (size_t k = 0; k < g.scratch.size(); k++)
+        if (g.scratch[k] == *q) { g.scratch.erase(g.scratch.begin() + (long)k); break; }
+      (void)hipFree(*q);
+      *q = nullptr;
+    }
+    g.d.p.npip = 0;
     CHECK_HIP(hipMalloc(&F.pipe_idx, (size_t)b.n2 * sizeof(int)));
     auto scratch = [&](double*& p, long n) -> int {
       CHECK_HIP(hipMalloc(&p, (size_t)n * sizeof(double)));
