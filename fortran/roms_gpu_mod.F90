@@ -31,6 +31,7 @@ module roms_gpu_mod
     real(c_double) :: ubind
     integer(c_int) :: curvgrid                   ! CURVGRID
     integer(c_int) :: uv_adv, uv_cor             ! UV_ADV, UV_COR
+    integer(c_int) :: pot_tides                  ! TIDES pot_tides
   end type
 
   type, bind(c) :: roms_tlev

@@ -81,6 +81,8 @@ typedef struct roms_cfg {
   int uv_adv, uv_cor;            /* UV_ADV (horizontal + vertical momentum advection,
                                     compute_horiz_rhs_uv_terms.h:42-291, compute_vert_rhs_uv_terms.h),
                                     UV_COR (Coriolis, compute_horiz_rhs_uv_terms.h:1-38)              */
+  int pot_tides;                 /* TIDES with pot_tides (tides.opt): the surface tidal potential
+                                    ptide enters the pressure gradient (prsgrd.F:209-211)             */
 } roms_cfg;
 
 /* Time-step indices (scalars.F:32-36).  The step entry updates them. */
@@ -120,6 +122,8 @@ enum roms_field {
   ROMS_t_west, ROMS_t_east, ROMS_t_south, ROMS_t_north,
   /* grid.F CURVGRID metric derivatives d(1/n)/dxi, d(1/m)/deta (setup_grid1.F:89-103) */
   ROMS_dndx, ROMS_dmde,
+  /* tides.F:26 surface tidal potential [m] (TIDES, pot_tides) */
+  ROMS_ptide,
   ROMS_NFIELDS
 };
 

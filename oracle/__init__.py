@@ -34,7 +34,7 @@ class OrCfg(ctypes.Structure):
                 ("diag_np_xi", ctypes.c_int), ("diag_np_eta", ctypes.c_int), ("surf_flux", ctypes.c_int),
                 ("obc", ctypes.c_int), ("ubind", ctypes.c_double), ("v_sponge", ctypes.c_double),
                 ("island", ctypes.c_int), ("curvgrid", ctypes.c_int), ("uv_adv", ctypes.c_int),
-                ("uv_cor", ctypes.c_int)]
+                ("uv_cor", ctypes.c_int), ("pot_tides", ctypes.c_int)]
 
     def __init__(self, *a, **k):
         super().__init__(*a, **k)

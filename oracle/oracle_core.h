@@ -29,6 +29,7 @@ struct or_state {
          *dn_u, *dm_v, *pm_v, *dn_v, *dm_p, *dn_p, *iA_u, *iA_v, *pmon_u,
          *pnom_v, *rmask, *pmask, *umask, *vmask;
   double *dndx, *dmde;             /* CURVGRID: d(1/n)/dxi, d(1/m)/deta (setup_grid1.F:89-103) */
+  double *ptide;                   /* tides.F:26 surface tidal potential (TIDES) */
   double area, volume;
   /* ocean vars */
   double *zeta, *ubar, *vbar, *u, *v, *t;

@@ -62,7 +62,7 @@ or_state *or_create(const or_cfg *cfg) {
   for (int q = 0; q < 6; q++) S->c1[q] = zalloc((size_t)S->nx2 * (S->N + 1));
   if (cfg->lmd) or_lmd_alloc(S);
   S->pipe_flx = zalloc(n2); S->pipe_idx = zalloc(n2);
-  S->dndx = zalloc(n2); S->dmde = zalloc(n2);
+  S->dndx = zalloc(n2); S->dmde = zalloc(n2); S->ptide = zalloc(n2);
   /* boundary.F:111-129: zeta_west(0:Mm+1), u_west(0:Mm+1,N), t_west(0:Mm+1,N,NT), ... */
   S->nbry[0] = S->nbry[1] = S->Mm + 2;
   S->nbry[2] = S->nbry[3] = S->Lm + 2;
@@ -759,7 +759,7 @@ double *or_field(or_state *S, const char *name, size_t *count) {
       {"dm_u", S->dm_u, S->n2}, {"dn_u", S->dn_u, S->n2}, {"dm_v", S->dm_v, S->n2}, {"dn_v", S->dn_v, S->n2},
       {"dm_p", S->dm_p, S->n2}, {"dn_p", S->dn_p, S->n2}, {"pmon_u", S->pmon_u, S->n2},
       {"pnom_v", S->pnom_v, S->n2}, {"rmask", S->rmask, S->n2}, {"umask", S->umask, S->n2},
-      {"vmask", S->vmask, S->n2}, {"pmask", S->pmask, S->n2}, {"dndx", S->dndx, S->n2}, {"dmde", S->dmde, S->n2}, {"xr", S->xr, S->n2}, {"yr", S->yr, S->n2},
+      {"vmask", S->vmask, S->n2}, {"pmask", S->pmask, S->n2}, {"dndx", S->dndx, S->n2}, {"dmde", S->dmde, S->n2}, {"ptide", S->ptide, S->n2}, {"xr", S->xr, S->n2}, {"yr", S->yr, S->n2},
       {"visc2_r", S->visc2_r, S->n2}, {"visc2_p", S->visc2_p, S->n2}, {"diff2", S->diff2, S->n2 * S->NT},
       {"sustr", S->sustr, S->n2}, {"svstr", S->svstr, S->n2}, {"stflx", S->stflx, S->n2 * S->NT},
       {"srflx", S->srflx, S->n2}, {"swflx", S->swflx, S->n2}, {"hbls", S->hbls, S->n2}, {"hbbl", S->hbbl, S->n2},

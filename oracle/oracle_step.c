@@ -424,6 +424,7 @@ void or_prsgrd(or_state *S) {
                        grho * (R3(rho, i, j, N) + 0.5 * (R3(rho, i, j, N) - R3(rho, i, j, N - 1)) *
                                                        (ZW(i, j, N) - ZR(i, j, N)) / (ZR(i, j, N) - ZR(i, j, N - 1))) *
                            (ZW(i, j, N) - ZR(i, j, N));
+      if (S->c.pot_tides) R3(P, i, j, N) = R3(P, i, j, N) - g * A2(S->ptide, i, j);  /* prsgrd.F:209-211 */
     }
     for (int k = N - 1; k >= 1; k--)
       for (int i = S->istrU - 1; i <= S->iend; i++) {

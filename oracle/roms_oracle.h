@@ -51,6 +51,7 @@ typedef struct or_cfg {
   int island;                    /* basin: circular land mask (MASKING) */
   int curvgrid;                  /* CURVGRID (+UV_ADV) curvature terms; basin: non-uniform metrics */
   int uv_adv, uv_cor;            /* UV_ADV, UV_COR */
+  int pot_tides;                 /* TIDES pot_tides: ptide in prsgrd (prsgrd.F:209-211) */
 } or_cfg;
 
 typedef struct or_state or_state;

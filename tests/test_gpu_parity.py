@@ -137,6 +137,13 @@ def test_routine_parity(case, routine, mode, outs):
     m.close()
 
 
+@pytest.mark.parametrize("case", ["filament", "basin", "basin_nonlin"])
+def test_prsgrd_fused_variant_parity(case, monkeypatch):
+    """The opt-in one-kernel prsgrd (ROMS_GPU_PRSGRD_FUSED=1) is bit-identical."""
+    monkeypatch.setenv("ROMS_GPU_PRSGRD_FUSED", "1")
+    test_routine_parity(case, "prsgrd", None, ["ru", "rv"])
+
+
 def test_step2d_fast_loop_parity():
     cfg = oracle.filament_cfg(LLm=32, MMm=24, N=16, np_xi=1, np_eta=1)
     o, m = make_pair(cfg)

@@ -17,7 +17,7 @@ __device__ __forceinline__ double harm(double a, double b) {
   return c > 0.0 ? c / (a + b) : 0.0;
 }
 
-__global__ void __launch_bounds__(256) k_prsgrd_P(Dev d, Range R, int split) {
+__global__ void __launch_bounds__(256) k_prsgrd_P(Dev d, Range R, int split, int tides) {
   ROMS_IJ_OR_RETURN(R)
   const Bounds& b = d.b;
   const Fields& F = d.f;
@@ -79,6 +79,7 @@ __global__ void __launch_bounds__(256) k_prsgrd_P(Dev d, Range R, int split) {
         const double zw = F.z_w[ij + (long)N * n2];
         const double rNm = rhov(rM, qM, zM);
         Pk = g * zw + grho * (v0 + 0.5 * (v0 - rNm) * (zw - zC) / (zC - zM)) * (zw - zC);
+        if (tides) Pk = Pk - g * F.ptide[ij];   // TIDES: pot_tides (prsgrd.F:209-211)
       } else {
         Pk = P1 + HalfGRho * ((v1 + v0) * (z1 - zC) -
                               OneFifth * ((dR1 - dRk) * (z1 - zC - OneTwelfth * (dZ1 + dZk)) -
@@ -200,6 +201,245 @@ __global__ void __launch_bounds__(256) k_prsgrd_uv(Dev d, Range R, int split, in
   }
 }
 
+// ---- fused form: one block per 64x4 tile walks the levels top-down.  Its
+// 325 "P columns" (the tile plus one column to the west and one row to the
+// south, where ru/rv read P and the in-situ density) run the vertical
+// recurrences of k_prsgrd_P in registers.  The level-k slice of z_r, rho1
+// (rho) and qp1 over the tile's stencil window (i0-2..i0+64 x j0-2..j0+4)
+// sits in LDS, three levels deep (k and k-1 for the recurrences, k-2 being
+// stored), fed from registers loaded two levels earlier.  Each tile lane then
+// forms the three clamped elementary differences per direction it needs,
+// their harmonic means and ru, rv, with the expressions of k_prsgrd_uv.  P
+// and the in-situ density never leave the CU, z_r / rho1 / qp1 are read from
+// HBM once per cell (window halo re-reads hit the neighbouring tiles' lines
+// in L2), two barriers per level.  Bit-identical to the two-kernel form. ----
+constexpr int kFW = kBX + 3, kFH = kBY + 3, kFN = kFW * kFH;   // window (i0-2..i0+64) x (j0-2..j0+4)
+constexpr int kFPW = kBX + 1, kFPH = kBY + 1, kFPN = kFPW * kFPH;   // P columns (i0-1..i0+63) x (j0-1..j0+3)
+constexpr int kFT = 384;                                         // threads: 6 wavefronts >= kFPN
+constexpr int kFQ = (kFN + kFT - 1) / kFT;                       // window entries per thread
+struct PrsWin {
+  double z[3][kFN], r[3][kFN], q[3][kFN];
+  double P[kFPN], V[kFPN];   // P and in-situ density of the P columns at level k
+};
+struct PrsPre {              // one level of this thread's window entries, in flight
+  double z[kFQ], r[kFQ], q[kFQ];
+};
+__global__ void __launch_bounds__(kFT) k_prsgrd_fused(Dev d, Range R, int split, int imin, int imax, int jmin,
+                                                       int jmax, int tides) {
+  const uint3 bI = xcd_tile();
+  __shared__ PrsWin W;
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const int N = b.N;
+  const double g = d.p.g, rho0 = d.p.rho0, qp2 = d.p.qp2;
+  const double OneFifth = 0.2, OneTwelfth = 1.0 / 12.0;
+  const double grho = g / rho0, HalfGRho = 0.5 * grho;
+  const long n2 = b.n2, sj = b.nx2;
+  const int i0 = R.i0 + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * kBY;
+  const int tid = threadIdx.x;
+  const double* R1 = split ? F.rho1 : F.rho;
+  // window entries owned by this thread
+  long wo[kFQ];
+  bool won[kFQ];
+#pragma unroll
+  for (int m = 0; m < kFQ; m++) {
+    const int e = tid + m * kFT;
+    const int i = i0 - 2 + e % kFW, j = j0 - 2 + e / kFW;
+    won[m] = e < kFN && i <= b.Lm + 2 && j <= b.Mm + 2;
+    wo[m] = IJ(b, i, j);
+  }
+  auto load = [&](int k, PrsPre& X) {
+    if (k < 1) return;
+    const long kk = (long)(k - 1) * n2;
+#pragma unroll
+    for (int m = 0; m < kFQ; m++) {
+      X.z[m] = X.r[m] = X.q[m] = 0.0;
+      if (won[m]) {
+        X.z[m] = F.z_r[wo[m] + kk];
+        X.r[m] = R1[wo[m] + kk];
+        if (split) X.q[m] = F.qp1[wo[m] + kk];
+      }
+    }
+  };
+  auto store = [&](int k, const PrsPre& X) {
+    if (k < 1) return;
+    const int sl = k % 3;
+#pragma unroll
+    for (int m = 0; m < kFQ; m++) {
+      const int e = tid + m * kFT;
+      if (e < kFN) { W.z[sl][e] = X.z[m]; W.r[sl][e] = X.r[m]; W.q[sl][e] = X.q[m]; }
+    }
+  };
+  // P column of this thread
+  const bool pcol = tid < kFPN;
+  const int pci = tid % kFPW, pcj = tid / kFPW;
+  const int pi = i0 - 1 + pci, pj = j0 - 1 + pcj;
+  const bool pon = pcol && pi <= b.Lm + 1 && pj <= b.Mm + 1;
+  const int pw = (pci + 1) + (pcj + 1) * kFW;   // its window position
+  const long pij = IJ(b, pi, pj);
+  auto rhov = [&](double r1, double q1, double z) {
+    if (split) {
+      const double dpth = -z;
+      return r1 + q1 * dpth * (1.0 - qp2 * dpth);
+    }
+    return r1;
+  };
+  auto eRof = [&](double ru, double rl, double qu, double ql, double zu, double zl) {
+    if (split) {
+      const double dpth = -0.5 * (zu + zl);
+      return ru - rl + (qu - ql) * dpth * (1.0 - qp2 * dpth);
+    }
+    return ru - rl;
+  };
+  // tile lane: clamped u-/v-point window offsets and masks (level independent)
+  const int ti = tid % kBX, tj = tid / kBX;
+  const int i = i0 + ti, j = j0 + tj;
+  const bool tile = tid < kBX * kBY && i <= R.i1 && j <= R.j1;
+  const long ij = IJ(b, i, j);
+  const bool du = tile && i >= b.istrU && i <= b.iend && j >= b.jstr && j <= b.jend;
+  const bool dv = tile && i >= b.istr && i <= b.iend && j >= b.jstrV && j <= b.jend;
+  const int wc = (ti + 2) + (tj + 2) * kFW;   // window (i, j)
+  const int pc = (ti + 1) + (tj + 1) * kFPW;  // P column (i, j)
+  int wux[3], wvy[3];                         // window of the clamped u-points i-1..i+1 / v-points j-1..j+1
+  double umx[3], vmy[3], dnu = 0.0, dmv = 0.0;
+#pragma unroll
+  for (int c = 0; c < 3; c++) {
+    wux[c] = wvy[c] = wc;
+    umx[c] = vmy[c] = 0.0;
+    if (du) {
+      const int m = iclamp(i - 1 + c, imin, imax);
+      wux[c] = (m - i0 + 2) + (tj + 2) * kFW;
+      umx[c] = F.umask[IJ(b, m, j)];
+    }
+    if (dv) {
+      const int m = iclamp(j - 1 + c, jmin, jmax);
+      wvy[c] = (ti + 2) + (m - j0 + 2) * kFW;
+      vmy[c] = F.vmask[IJ(b, i, m)];
+    }
+  }
+  if (du) dnu = F.dn_u[ij];
+  if (dv) dmv = F.dm_v[ij];
+  // prologue: levels N and N-1 in LDS, N-2 and N-3 in flight
+  {
+    PrsPre X;
+    load(N, X); store(N, X);
+    load(N - 1, X); store(N - 1, X);
+  }
+  PrsPre A, B;
+  load(N - 2, A);
+  load(N - 3, B);
+  __syncthreads();
+  double eZk = 0.0, eRk = 0.0, dZ1 = 0.0, dR1 = 0.0, P1 = 0.0, z1 = 0.0, v1 = 0.0;
+  if (pon) {
+    const int sN = N % 3, sM = (N - 1) % 3;
+    eZk = W.z[sN][pw] - W.z[sM][pw];
+    eRk = eRof(W.r[sN][pw], W.r[sM][pw], W.q[sN][pw], W.q[sM][pw], W.z[sN][pw], W.z[sM][pw]);
+  }
+  auto level = [&](int k, PrsPre& X) {   // X holds level k-2 on entry, k-4 on exit
+    const int sk = k % 3, sm = (k + 2) % 3;
+    const long o = ij + (long)(k - 1) * n2;
+    double hz0 = 0.0, hzu = 0.0, hzv = 0.0;
+    if (du) { hz0 = F.Hz[o]; hzu = F.Hz[o - 1]; }
+    if (dv) { hz0 = F.Hz[o]; hzv = F.Hz[o - sj]; }
+    // (1) P columns: vertical harmonic means and the hydrostatic integral
+    if (pon) {
+      const double zC = W.z[sk][pw], rC = W.r[sk][pw], qC = W.q[sk][pw];
+      double eZm, eRm;
+      if (k >= 2) {
+        const double zM = W.z[sm][pw], rM = W.r[sm][pw], qM = W.q[sm][pw];
+        eZm = zC - zM;
+        eRm = eRof(rC, rM, qC, qM, zC, zM);
+      } else {
+        eZm = eZk; eRm = eRk;
+      }
+      const double dZk = [&] { const double c = 2.0 * eZk * eZm; return c / (eZk + eZm); }();
+      double dRk = harm(eRk, eRm);
+      const double v0 = rhov(rC, qC, zC);
+      if (split) {
+        const double dpth = -zC;
+        dRk = dRk - qC * dZk * (1.0 - 2.0 * qp2 * dpth);
+      }
+      double Pk;
+      if (k == N) {
+        const double zw = F.z_w[pij + (long)N * n2];
+        const double zM = W.z[sm][pw];
+        const double rNm = rhov(W.r[sm][pw], W.q[sm][pw], zM);
+        Pk = g * zw + grho * (v0 + 0.5 * (v0 - rNm) * (zw - zC) / (zC - zM)) * (zw - zC);
+        if (tides) Pk = Pk - g * F.ptide[pij];   // TIDES: pot_tides (prsgrd.F:209-211)
+      } else {
+        Pk = P1 + HalfGRho * ((v1 + v0) * (z1 - zC) -
+                              OneFifth * ((dR1 - dRk) * (z1 - zC - OneTwelfth * (dZ1 + dZk)) -
+                                          (dZ1 - dZk) * (v1 - v0 - OneTwelfth * (dR1 + dRk))));
+      }
+      W.P[tid] = Pk;
+      W.V[tid] = v0;
+      P1 = Pk;
+      dZ1 = dZk; dR1 = dRk;
+      eZk = eZm; eRk = eRm;
+      z1 = zC; v1 = v0;
+    }
+    __syncthreads();
+    // (2) ru, rv of the tile: clamped elementary differences at the three
+    // u-points (v-points), harmonic means at p = i-1, i (j-1, j), then the
+    // density-Jacobian pressure gradient (k_prsgrd_uv expressions)
+    const double* Z = W.z[sk];
+    const double* Rr = W.r[sk];
+    const double* Qq = W.q[sk];
+    auto diffs = [&](const int (&w)[3], const double (&mk)[3], int st, double (&fc)[3], double (&rx)[3]) {
+#pragma unroll
+      for (int c = 0; c < 3; c++) {
+        const int w1 = w[c], w0 = w1 - st;
+        fc[c] = (Z[w1] - Z[w0]) * mk[c];
+        if (split) {
+          const double dpth = -0.5 * (Z[w1] + Z[w0]);
+          rx[c] = (Rr[w1] - Rr[w0] + (Qq[w1] - Qq[w0]) * dpth * (1.0 - qp2 * dpth)) * mk[c];
+        } else {
+          rx[c] = (Rr[w1] - Rr[w0]) * mk[c];
+        }
+      }
+    };
+    auto means = [&](const double (&fc)[3], const double (&rx)[3], int wp0, int wp1, double& dZ0, double& dZ1o,
+                     double& dR0, double& dR1o) {
+      dZ0 = harm(fc[0], fc[1]); dR0 = harm(rx[0], rx[1]);
+      dZ1o = harm(fc[1], fc[2]); dR1o = harm(rx[1], rx[2]);
+      if (split) {
+        dR0 = dR0 - Qq[wp0] * dZ0 * (1.0 + 2.0 * qp2 * Z[wp0]);
+        dR1o = dR1o - Qq[wp1] * dZ1o * (1.0 + 2.0 * qp2 * Z[wp1]);
+      }
+    };
+    if (du) {
+      double fc[3], rx[3], dZ0, dZ1x, dR0, dR1x;
+      diffs(wux, umx, 1, fc, rx);
+      means(fc, rx, wc - 1, wc, dZ0, dZ1x, dR0, dR1x);
+      const double zr0 = Z[wc], zrm = Z[wc - 1], r0 = W.V[pc], rm = W.V[pc - 1];
+      F.ru[o] = 0.5 * (hz0 + hzu) * dnu *
+                (W.P[pc - 1] - W.P[pc] -
+                 HalfGRho * ((r0 + rm) * (zr0 - zrm) -
+                             OneFifth * ((dR1x - dR0) * (zr0 - zrm - OneTwelfth * (dZ1x + dZ0)) -
+                                         (dZ1x - dZ0) * (r0 - rm - OneTwelfth * (dR1x + dR0)))));
+    }
+    if (dv) {
+      double fc[3], rx[3], dZ0, dZ1y, dR0, dR1y;
+      diffs(wvy, vmy, kFW, fc, rx);
+      means(fc, rx, wc - kFW, wc, dZ0, dZ1y, dR0, dR1y);
+      const double zr0 = Z[wc], zrm = Z[wc - kFW], r0 = W.V[pc], rm = W.V[pc - kFPW];
+      F.rv[o] = 0.5 * (hz0 + hzv) * dmv *
+                (W.P[pc - kFPW] - W.P[pc] -
+                 HalfGRho * ((r0 + rm) * (zr0 - zrm) -
+                             OneFifth * ((dR1y - dR0) * (zr0 - zrm - OneTwelfth * (dZ1y + dZ0)) -
+                                         (dZ1y - dZ0) * (r0 - rm - OneTwelfth * (dR1y + dR0)))));
+    }
+    // (3) level k-2 into the slot of k+1 (free), then the loads of k-4
+    store(k - 2, X);
+    load(k - 4, X);
+    __syncthreads();
+  };
+  for (int k = N; k >= 1; k -= 2) {
+    level(k, A);
+    if (k - 1 >= 1) level(k - 1, B);
+  }
+}
+
 void launch_prsgrd(const Dev& d, hipStream_t s, const Tlev& t) {
   const Bounds& b = d.b;
   const int split = d.p.nonlin_eos;
@@ -212,9 +452,14 @@ void launch_prsgrd(const Dev& d, hipStream_t s, const Tlev& t) {
     jmin = b.south_edge ? b.jstrV : b.jstrV - 1;
     jmax = b.north_edge ? b.jend : b.jend + 1;
   } else { jmin = b.jstr - 1; jmax = b.jend + 1; }
-  Range R1{0, b.Lm, 0, b.Mm};
-  hipLaunchKernelGGL(k_prsgrd_P, grid_of(R1), dim3(kBX, kBY), 0, s, d, R1, split);
   Range R2{b.istr, b.iend, b.jstr, b.jend};
+  if (!d.p.prs_split) {
+    hipLaunchKernelGGL(k_prsgrd_fused, grid_of(R2), dim3(kFT), 0, s, d, R2, split, imin, imax, jmin, jmax, d.p.tides);
+    return;
+  }
+  // two-kernel form (default; k_prsgrd_fused with ROMS_GPU_PRSGRD_FUSED=1)
+  Range R1{0, b.Lm, 0, b.Mm};
+  hipLaunchKernelGGL(k_prsgrd_P, grid_of(R1), dim3(kBX, kBY), 0, s, d, R1, split, d.p.tides);
   hipLaunchKernelGGL(k_prsgrd_uv, grid3_of(R2, b.N), dim3(kBX, kBY), 0, s, d, R2, split, imin, imax, jmin, jmax);
 }
 

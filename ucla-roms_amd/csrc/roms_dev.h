@@ -33,6 +33,8 @@ struct Params {
   int nonlin_eos, salinity, lmd, uv_vis2, ts_dif2;
   int lmd_rimix, lmd_convec, lmd_nonlocal;  // LMD_RIMIX, LMD_CONVEC, LMD_NONLOCAL (lmd != 0: MIXING+KPP+BKPP)
   int uv_adv, uv_cor;                       // UV_ADV, UV_COR
+  int tides;                                // TIDES pot_tides: ptide in prsgrd
+  int prs_split;                            // 1: two-kernel prsgrd (default), 0: k_prsgrd_fused (ROMS_GPU_PRSGRD_FUSED=1)
   int s2d_split;  // 1: step2d as separate zeta / momentum kernels (ROMS_GPU_S2D_SPLIT=1)
   int colseg;     // 1: segment-partitioned column solvers (k_colseg.h; N > 63, ROMS_GPU_COLSEG=0/1)
   int colreg;     // 1: register-resident column solvers where compiled for N (ROMS_GPU_COLREG=0 disables)
@@ -51,6 +53,7 @@ struct Fields {
   double *h, *hinv, *f, *fomn, *pm, *pn, *dm_r, *dn_r, *dm_u, *dn_u, *dm_v, *dn_v, *dm_p, *dn_p,
       *pmon_u, *pnom_v, *rmask, *pmask, *umask, *vmask;
   double *dndx, *dmde;  // CURVGRID metric derivatives
+  double* ptide;        // tides.F surface tidal potential (TIDES)
   double *Cs_w, *Cs_r;  // scoord.F (N+1)
   // ocean vars
   double *zeta, *ubar, *vbar, *u, *v, *t;

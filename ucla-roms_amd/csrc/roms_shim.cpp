@@ -194,7 +194,7 @@ double** field_slot(Fields& F, int id) {
     case ROMS_swr_frac: return &F.swr_frac; case ROMS_sustr: return &F.sustr; case ROMS_svstr: return &F.svstr;
     case ROMS_stflx: return &F.stflx; case ROMS_srflx: return &F.srflx; case ROMS_swflx: return &F.swflx;
     case ROMS_ru: return &F.ru; case ROMS_rv: return &F.rv;
-    case ROMS_dndx: return &F.dndx; case ROMS_dmde: return &F.dmde;
+    case ROMS_dndx: return &F.dndx; case ROMS_dmde: return &F.dmde; case ROMS_ptide: return &F.ptide;
     default: break;
   }
   if (id >= ROMS_zeta_west && id <= ROMS_t_north) {
@@ -331,6 +331,15 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
   P.lmd_convec = (cfg->lmd_mixing & ROMS_LMD_CONVEC) != 0;
   P.lmd_nonlocal = (cfg->lmd_mixing & ROMS_LMD_NONLOCAL) != 0;
   P.uv_adv = cfg->uv_adv != 0; P.uv_cor = cfg->uv_cor != 0;
+  P.tides = cfg->pot_tides != 0;
+  {
+    // fused one-kernel prsgrd (k_prsgrd_fused): bit-identical, fewer bytes,
+    // but measured slower at C2 (0.50 vs 0.38 ms per call: a per-level walk
+    // of 2 blocks per CU hides less latency than the level-parallel grid)
+    // and only 4% faster at C3 -- opt-in, ROMS_GPU_PRSGRD_FUSED=1
+    const char* e = getenv("ROMS_GPU_PRSGRD_FUSED");
+    P.prs_split = !(e && e[0] == '1');
+  }
   P.uv_vis2 = cfg->uv_vis2; P.ts_dif2 = cfg->ts_dif2;
   {
     const char* e = getenv("ROMS_GPU_S2D_SPLIT");

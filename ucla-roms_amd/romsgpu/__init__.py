@@ -25,7 +25,7 @@ FIELDS = ["h", "hinv", "f", "fomn", "pm", "pn", "dm_r", "dn_r", "dm_u", "dn_u", 
           "DU_avg_bak", "DV_avg_bak", "rho", "rho1", "qp1", "bvf", "Akv", "Akt", "visc2_r", "visc2_p", "diff2",
           "hbls", "hbbl", "ghat", "swr_frac", "sustr", "svstr", "stflx", "srflx", "swflx", "ru", "rv"] + \
          ["%s_%s" % (v, e) for v in ("zeta", "ubar", "vbar", "u", "v", "t") for e in ("west", "east", "south", "north")] + \
-         ["dndx", "dmde"]
+         ["dndx", "dmde", "ptide"]
 FIELD_ID = {n: i for i, n in enumerate(FIELDS)}
 CASE_FILAMENT, CASE_BASIN, CASE_PIPES = 0, 1, 2
 # LMD switch bits (ROMS_LMD_* of include/roms_gpu.h)
@@ -57,7 +57,7 @@ class Cfg(ctypes.Structure):
                 ("T0", ctypes.c_double), ("Scoef", ctypes.c_double), ("S0", ctypes.c_double),
                 ("theta_s", ctypes.c_double), ("theta_b", ctypes.c_double), ("hc", ctypes.c_double),
                 ("obc", ctypes.c_int), ("ubind", ctypes.c_double), ("curvgrid", ctypes.c_int),
-                ("uv_adv", ctypes.c_int), ("uv_cor", ctypes.c_int)]
+                ("uv_adv", ctypes.c_int), ("uv_cor", ctypes.c_int), ("pot_tides", ctypes.c_int)]
 
 
 class Tlev(ctypes.Structure):
@@ -99,6 +99,8 @@ def load_library(path=LIB_PATH):
     L.roms_gpu_field_size.restype = ctypes.c_long
     for fn in ("roms_gpu_copy_in", "roms_gpu_copy_out", "roms_gpu_register"):
         getattr(L, fn).argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_long]
+    L.roms_gpu_upload.argtypes = [ctypes.c_int]
+    L.roms_gpu_download.argtypes = [ctypes.c_int]
     for fn in ROUTINES_T:
         getattr(L, "roms_gpu_" + fn).argtypes = [P(Tlev)]
     L.roms_gpu_rho_eos.argtypes = [ctypes.c_int, P(Tlev)]
@@ -253,6 +255,26 @@ class Model:
 
     def close(self):
         self.L.roms_gpu_finalize()
+        self._host = {}
+
+    # ---- host mirrors (roms_gpu_register / upload / download): the way a
+    # Fortran host hands its module arrays to the library ----
+    def register(self, name, arr):
+        """Borrow the host array `arr` (float64, C-contiguous, the field's
+        Fortran layout) as the mirror of field `name` until close()."""
+        fid = FIELD_ID[name]
+        if arr.dtype != np.float64 or not arr.flags["C_CONTIGUOUS"]:
+            raise ValueError("register: %s must be a contiguous float64 array" % name)
+        self._chk(self.L.roms_gpu_register(fid, arr.ctypes.data, arr.size), "register " + name)
+        if not hasattr(self, "_host"):
+            self._host = {}
+        self._host[name] = arr   # keep the borrowed buffer alive
+
+    def upload(self, name=None):
+        self._chk(self.L.roms_gpu_upload(-1 if name is None else FIELD_ID[name]), "upload")
+
+    def download(self, name=None):
+        self._chk(self.L.roms_gpu_download(-1 if name is None else FIELD_ID[name]), "download")
 
     # ---- state access (Fortran layout, returned as (levels, j, i) C arrays) ----
     def get(self, name):
