@@ -57,8 +57,9 @@ module roms_gpu_mod
   integer(c_int), parameter :: ROMS_GPU_ABI = 5   ! ROMS_GPU_ABI_VERSION, include/roms_gpu.h
 
   ! field ids (enum roms_field) used by the drivers below
+  integer(c_int), parameter :: ROMS_ALL = -1
   integer(c_int), parameter :: ROMS_zeta = 22, ROMS_ubar = 23, ROMS_vbar = 24, ROMS_u = 25, ROMS_v = 26, &
-                               ROMS_t = 27
+                               ROMS_t = 27, ROMS_Hz = 32, ROMS_z_r = 35, ROMS_NFIELDS = 96
 
   interface
     integer(c_int) function roms_gpu_abi_version() bind(c)
@@ -195,6 +196,11 @@ module roms_gpu_mod
       integer(c_int), value :: np_xi, np_eta, device
       type(c_ptr), value :: comm
       type(roms_tlev), intent(out) :: t
+    end function
+    integer(c_int) function roms_gpu_set_weights(ndtfast, weight) bind(c)
+      import :: c_int, c_double, ROMS_MAX_FAST
+      integer(c_int), value :: ndtfast
+      real(c_double), intent(out) :: weight(ROMS_MAX_FAST, 2)
     end function
     integer(c_int) function roms_gpu_diag(t, norms) bind(c)
       import :: c_int, c_double, roms_tlev

@@ -225,8 +225,16 @@ int roms_gpu_halo_plan(int Lm, int Mm, int np_xi, int np_eta, int inode, int jno
 long roms_gpu_halo_map(int Lm, int Mm, int np_xi, int np_eta, int inode, int jnode, int ew_periodic,
                        int ns_periodic, int dir, int unpack, int *i, int *j, long cap);
 
-/* ---- diagnostics (diag.F code_check norms, device reduction) ---- */
+/* ---- diagnostics (diag.F code_check norms, device reduction) ----
+ * KE, KE2b (barotropic), max advective Courant and the vertical Courant at
+ * that point, in the reference's reduction order.  The grid area/volume of
+ * setup_grid2.F are formed on first use from the device's h, pm, pn, rmask
+ * (per-rank pairwise sums, tree over ranks), so a host that registered its
+ * own arrays gets the same norms as roms_gpu_init_case.  Collective.        */
 int roms_gpu_diag(const roms_tlev *t, double norms[4]);
+/* Host-only: set_weights.F restatement -- the fast-time averaging weights of
+ * ndtfast (written into weight, C order [2][288]); returns nfast, or -1.    */
+int roms_gpu_set_weights(int ndtfast, double weight[2][ROMS_MAX_FAST]);
 /* event-timed replay of n steps on the library stream: total milliseconds  */
 int roms_gpu_time_steps(roms_tlev *t, int n, double *ms);
 /* Runs nsteps steps eagerly with HIP events on the library stream around

@@ -209,3 +209,18 @@ def test_graph_replay_bitwise_equals_eager():
         m2.close()
     finally:
         os.environ.pop("ROMS_GPU_NO_GRAPH", None)
+
+
+def test_diag_blowup_flag_is_fatal():
+    """A non-finite norm is diag.F's 'Abnormal termination: BLOWUP'
+    (diag.F:621-633): roms_gpu_diag fails instead of printing NaN."""
+    cfg = oracle.filament_cfg(LLm=32, MMm=24, N=16, np_xi=1, np_eta=1)
+    m = romsgpu.Model.from_case(0, 32, 24, 16, sizex=cfg.sizex, sizey=cfg.sizey)
+    m.step(2)
+    assert all(np.isfinite(m.diag()))
+    u = m.get("u")
+    u[:, 10, 10] = np.nan
+    m.put("u", u)
+    with pytest.raises(romsgpu.RomsGpuError, match="BLOWUP"):
+        m.diag()
+    m.close()

@@ -1,7 +1,11 @@
-// k_diag.hip -- per-column terms of diag_tile (diag.F:58-405): barotropic
-// velocities ub,vb, kinetic energy, barotropic KE, free-surface volume and the
-// advective/vertical Courant numbers.  The reduction-by-pairs and the
-// first-maximum scan (diag.F loop order j, k=N..1, i) finish on the host.
+// k_diag.hip -- diag_tile (diag.F:58-535) on the device: per-column terms
+// (barotropic velocities ub,vb, kinetic energy, barotropic KE, free-surface
+// volume, advective/vertical Courant numbers), the reduction by pairs of
+// each sum and the first-maximum Courant scan (diag.F loop order j, k=N..1,
+// i) in the reference's order, and a blow-up flag.  Five numbers and the
+// flag come back to the host, which combines ranks in the reference's tree.
+#include <utility>
+
 #include "roms_dev.h"
 
 namespace roms {
@@ -62,14 +66,150 @@ __global__ void __launch_bounds__(256) k_diag(Dev d, Range R, int nstp) {
   F.s5[ij] = km;
 }
 
-void launch_diag(const Dev& d, hipStream_t s, const Tlev& t, double* partials) {
-  (void)partials;
+// ---- reduction by pairs on the device (diag.F:409-470 "reduction by
+// pairs" of each rank's tile, restated as host pair_reduce in host_init.cpp):
+// alternating j- and i-halving passes, each one launch that reads one buffer
+// set and writes the other, so every partial sum is formed from the same two
+// operands in the same order as the sequential in-place loops. ----
+struct Trio {
+  double* a[3];
+};
+__global__ void __launch_bounds__(256) k_pairs_j(const Bounds b, Trio src, Trio dst, int istr, int isize, int jstr,
+                                                 int js, int extra) {
+  const int i = istr + (int)(blockIdx.x * blockDim.x + threadIdx.x), j = (int)blockIdx.y;   // j = 0..js(+1)
+  if (i > istr + isize) return;
+  const long t = IJ(b, i, jstr + j);
+  if (j <= js) {
+    const long s0 = IJ(b, i, jstr + 2 * j), s1 = IJ(b, i, jstr + 2 * j + 1);
+#pragma unroll
+    for (int q = 0; q < 3; q++) dst.a[q][t] = src.a[q][s0] + src.a[q][s1];
+  } else if (extra) {   // odd row count: the last row moves down unchanged
+    const long s0 = IJ(b, i, jstr + 2 * j);
+#pragma unroll
+    for (int q = 0; q < 3; q++) dst.a[q][t] = src.a[q][s0];
+  }
+}
+__global__ void __launch_bounds__(256) k_pairs_i(const Bounds b, Trio src, Trio dst, int istr, int is, int extra,
+                                                 int jstr, int jsize) {
+  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x), j = jstr + (int)blockIdx.y;   // i = 0..is(+1)
+  if (j > jstr + jsize) return;
+  const long t = IJ(b, istr + i, j);
+  if (i <= is) {
+    const long s0 = IJ(b, istr + 2 * i, j), s1 = IJ(b, istr + 2 * i + 1, j);
+#pragma unroll
+    for (int q = 0; q < 3; q++) dst.a[q][t] = src.a[q][s0] + src.a[q][s1];
+  } else if (i == is + 1 && extra) {
+    const long s0 = IJ(b, istr + 2 * i, j);
+#pragma unroll
+    for (int q = 0; q < 3; q++) dst.a[q][t] = src.a[q][s0];
+  }
+}
+// MAX_ADV_CFL first maximum in the reference's scan order (j, then k = N..1,
+// then i; strict '>'): per row, the largest Cu; among equal values the
+// larger k, then the smaller i.  One block per row, then one block over rows
+// (first j on ties).  out[0..4] = Cu_adv, Cu_w, ... and a blow-up flag.
+struct CflBest {
+  double cx, cw, k;
+  int i;
+};
+__device__ __forceinline__ bool cfl_better(const CflBest& a, const CflBest& b) {   // a precedes b in the scan
+  if (a.cx != b.cx) return a.cx > b.cx;
+  if (a.k != b.k) return a.k > b.k;
+  return a.i < b.i;
+}
+__global__ void __launch_bounds__(256) k_cfl_rows(const Bounds b, const double* cx, const double* cw, const double* kx,
+                                                  double* rcx, double* rcw) {
+  __shared__ CflBest sh[256];
+  const int j = 1 + (int)blockIdx.x;
+  CflBest best{0.0, 0.0, -1.0, 1 << 30};
+  for (int i = 1 + (int)threadIdx.x; i <= b.Lm; i += blockDim.x) {
+    const long o = IJ(b, i, j);
+    const CflBest c{cx[o], cw[o], kx[o], i};
+    if (c.cx > 0.0 && (best.k < 0.0 || cfl_better(c, best))) best = c;
+  }
+  sh[threadIdx.x] = best;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      const CflBest o = sh[threadIdx.x + w];
+      if (o.k >= 0.0 && (sh[threadIdx.x].k < 0.0 || cfl_better(o, sh[threadIdx.x]))) sh[threadIdx.x] = o;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    rcx[j] = sh[0].k >= 0.0 ? sh[0].cx : 0.0;
+    rcw[j] = sh[0].k >= 0.0 ? sh[0].cw : 0.0;
+  }
+}
+__global__ void __launch_bounds__(256) k_diag_final(const Bounds b, const double* rcx, const double* rcw, Trio sums,
+                                                    double* out) {
+  __shared__ double scx[256], scw[256];
+  __shared__ int sj[256];
+  double bc = 0.0, bw = 0.0;
+  int bj = 1 << 30;
+  for (int j = 1 + (int)threadIdx.x; j <= b.Mm; j += blockDim.x)
+    if (rcx[j] > bc || (rcx[j] == bc && rcx[j] > 0.0 && j < bj)) { bc = rcx[j]; bw = rcw[j]; bj = j; }
+  scx[threadIdx.x] = bc; scw[threadIdx.x] = bw; sj[threadIdx.x] = bj;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      const double c = scx[threadIdx.x + w];
+      const int jj = sj[threadIdx.x + w];
+      if (c > scx[threadIdx.x] || (c == scx[threadIdx.x] && c > 0.0 && jj < sj[threadIdx.x])) {
+        scx[threadIdx.x] = c; scw[threadIdx.x] = scw[threadIdx.x + w]; sj[threadIdx.x] = jj;
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const long o = IJ(b, 1, 1);
+    out[0] = sums.a[0][o];   // avzeta (sum of dA*zeta)
+    out[1] = sums.a[1][o];   // ke
+    out[2] = sums.a[2][o];   // ke2b
+    out[3] = scx[0];
+    out[4] = scw[0];
+    // blow-up: a non-finite norm is what diag.F's check_line scan catches
+    // as "Abnormal termination: BLOWUP" (diag.F:621-633)
+    bool bad = false;
+    for (int q = 0; q < 5; q++) bad = bad || !(out[q] == out[q]) || fabs(out[q]) > 1.0e300;
+    out[5] = bad ? 1.0 : 0.0;
+  }
+}
+
+void launch_diag(const Dev& d, hipStream_t s, const Tlev& t, double* out) {
   const Bounds& b = d.b;
-  (void)hipMemsetAsync(d.f.s0, 0, (size_t)b.n2 * sizeof(double), s);
-  (void)hipMemsetAsync(d.f.s1, 0, (size_t)b.n2 * sizeof(double), s);
-  (void)hipMemsetAsync(d.f.s2, 0, (size_t)b.n2 * sizeof(double), s);
+  const Fields& F = d.f;
+  (void)hipMemsetAsync(F.s0, 0, (size_t)b.n2 * sizeof(double), s);
+  (void)hipMemsetAsync(F.s1, 0, (size_t)b.n2 * sizeof(double), s);
+  (void)hipMemsetAsync(F.s2, 0, (size_t)b.n2 * sizeof(double), s);
   Range R{1, b.Lm, 1, b.Mm};
   hipLaunchKernelGGL(k_diag, grid_of(R), dim3(kBX, kBY), 0, s, d, R, t.nstp);
+  if (!out) return;
+  // per-row CFL maxima into s6 / s7 (index j), then the pair sums of s0..s2
+  hipLaunchKernelGGL(k_cfl_rows, dim3(b.Mm), dim3(256), 0, s, b, F.s3, F.s4, F.s5, F.s6, F.s7);
+  Trio A{{F.s0, F.s1, F.s2}}, B{{F.s8, F.s9, F.s3}};
+  int istr = 1, jstr = 1, isize = b.Lm - 1, jsize = b.Mm - 1;
+  Trio* cur = &A;
+  Trio* nxt = &B;
+  while (isize > 0 || jsize > 0) {
+    if (jsize > 0) {
+      int js = (jsize + 1) / 2 - 1;
+      const int extra = 2 * js + 1 < jsize;
+      hipLaunchKernelGGL(k_pairs_j, dim3((isize + 1 + 255) / 256, js + 1 + extra), dim3(256), 0, s, b, *cur, *nxt,
+                         istr, isize, jstr, js, extra);
+      std::swap(cur, nxt);
+      jsize = js + extra;
+    }
+    if (isize > 0) {
+      int is = (isize + 1) / 2 - 1;
+      const int extra = 2 * is + 1 < isize;
+      hipLaunchKernelGGL(k_pairs_i, dim3((is + 1 + extra + 255) / 256, jsize + 1), dim3(256), 0, s, b, *cur, *nxt,
+                         istr, is, extra, jstr, jsize);
+      std::swap(cur, nxt);
+      isize = is + extra;
+    }
+  }
+  hipLaunchKernelGGL(k_diag_final, dim3(1), dim3(256), 0, s, b, F.s6, F.s7, *cur, out);
 }
 
 }  // namespace roms

@@ -240,7 +240,8 @@ void launch_t3dmix(const Dev& d, hipStream_t s, const Tlev& t);
 void launch_u3dbc(const Dev& d, hipStream_t s, const Tlev& t);
 void launch_v3dbc(const Dev& d, hipStream_t s, const Tlev& t);
 void launch_t3dbc(const Dev& d, hipStream_t s, const Tlev& t, int itrc);
-void launch_diag(const Dev& d, hipStream_t s, const Tlev& t, double* partials);
+// out (device, 6 doubles): avzeta, KE, KE2b sums, Cu_adv, Cu_w, blow-up flag
+void launch_diag(const Dev& d, hipStream_t s, const Tlev& t, double* out);
 void launch_swr_frac(const Dev& d, hipStream_t s);
 void launch_lmd_vmix(const Dev& d, hipStream_t s, const Tlev& t, int tind);
 

@@ -37,11 +37,13 @@ struct Ctx {
   roms_cfg cfg{};
   double w1[kMaxFast], w2[kMaxFast];
   double area = 0.0, volume = 0.0;
+  bool have_volume = false;   // area/volume formed (init_case, or on first diag)
   std::string err;
   // graph cache: key = (nstp, knew at step start)
   std::map<long, hipGraphExec_t> graphs;
   bool use_graphs = true;
-  double* h_diag = nullptr;
+  double* h_diag = nullptr;   // pinned: the diag numbers
+  double* d_diag = nullptr;   // device: the diag numbers (launch_diag)
   Halo halo;               // multi-rank exchange (halo.comm == nullptr: single rank)
   // per-routine timing (roms_gpu_time_routine): events around every launch
   int timed = -1;
@@ -219,6 +221,7 @@ void free_all() {
   g.scratch.clear();
   if (g.d.f.pipe_idx) { (void)hipFree(g.d.f.pipe_idx); g.d.f.pipe_idx = nullptr; }
   if (g.h_diag) { (void)hipHostFree(g.h_diag); g.h_diag = nullptr; }
+  if (g.d_diag) { (void)hipFree(g.d_diag); g.d_diag = nullptr; }
   if (g.s) { (void)hipStreamDestroy(g.s); g.s = nullptr; }
   g.inited = false;
 }
@@ -315,6 +318,8 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
   CHECK_HIP(hipSetDevice(device));
   g.dims = *dims;
   g.cfg = *cfg;
+  g.have_volume = false;
+  g.area = g.volume = 0.0;
   g.d = Dev{};
   g.d.b = make_bounds(*dims);
   g.d.b.nTS = cfg->salinity ? 2 : 1;
@@ -419,7 +424,8 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     for (double** q : l2)
       if (scratch(*q, b.n2)) return -2;
   }
-  CHECK_HIP(hipHostMalloc(&g.h_diag, (size_t)8 * b.n2 * sizeof(double), hipHostMallocDefault));
+  CHECK_HIP(hipHostMalloc(&g.h_diag, 8 * sizeof(double), hipHostMallocDefault));
+  CHECK_HIP(hipMalloc(&g.d_diag, 8 * sizeof(double)));
   if (comm != nullptr) {
     const HaloPlan plan = halo_plan(dims->Lm, dims->Mm, dims->np_xi, dims->np_eta, dims->inode, dims->jnode,
                                     dims->ew_periodic, dims->ns_periodic);
@@ -703,6 +709,7 @@ static int init_case_impl(const roms_case* c, int np_xi, int np_eta, void* comm,
     for (int q = 0; q < np_xi * np_eta; q++) { va.push_back(all[2 * q]); vv.push_back(all[2 * q + 1]); }
     g.area = tree_sum(va);
     g.volume = tree_sum(vv);
+    g.have_volume = true;
   }
   for (int id = 0; id < ROMS_NFIELDS; id++) {
     if (H.arr[id].empty()) continue;
@@ -840,44 +847,67 @@ int roms_gpu_time_steps(roms_tlev* t, int n, double* ms) {
   return 0;
 }
 
-// diag.F code_check norms: per-column terms on the device (launch_diag),
-// reduction-by-pairs and the (j, k desc, i) first-maximum scan on the host.
-int roms_gpu_diag(const roms_tlev* t, double norms[4]) {
-  REQUIRE_INIT();
+// setup_grid2.F area/volume from the device grid (a host that registered its
+// own arrays): per-rank pairwise sums, then the tree over ranks
+static int grid_integrals() {
   const Bounds& b = g.d.b;
-  launch_diag(g.d, g.s, to_tlev(t), nullptr);
-  const long n2 = b.n2;
-  CHECK_HIP(hipMemcpyAsync(g.h_diag, g.d.f.s0, (size_t)n2 * sizeof(double), hipMemcpyDeviceToHost, g.s));
-  CHECK_HIP(hipMemcpyAsync(g.h_diag + n2, g.d.f.s1, (size_t)n2 * sizeof(double), hipMemcpyDeviceToHost, g.s));
-  CHECK_HIP(hipMemcpyAsync(g.h_diag + 2 * n2, g.d.f.s2, (size_t)n2 * sizeof(double), hipMemcpyDeviceToHost, g.s));
-  CHECK_HIP(hipMemcpyAsync(g.h_diag + 3 * n2, g.d.f.s3, (size_t)n2 * sizeof(double), hipMemcpyDeviceToHost, g.s));
-  CHECK_HIP(hipMemcpyAsync(g.h_diag + 4 * n2, g.d.f.s4, (size_t)n2 * sizeof(double), hipMemcpyDeviceToHost, g.s));
-  CHECK_HIP(hipMemcpyAsync(g.h_diag + 5 * n2, g.d.f.s5, (size_t)n2 * sizeof(double), hipMemcpyDeviceToHost, g.s));
-  CHECK_HIP(hipStreamSynchronize(g.s));
   HostState H(b.Lm, b.Mm, b.N, b.NT, b.nTS);
-  std::vector<double> dVol(g.h_diag, g.h_diag + n2), ke(g.h_diag + n2, g.h_diag + 2 * n2),
-      ke2b(g.h_diag + 2 * n2, g.h_diag + 3 * n2);
-  const double* cx = g.h_diag + 3 * n2;
-  const double* cw = g.h_diag + 4 * n2;
-  const double* kx = g.h_diag + 5 * n2;
-  const double avzeta = pair_sum(H, dVol), kes = pair_sum(H, ke), ke2 = pair_sum(H, ke2b);
-  double Cu = 0.0, Cw = 0.0;
-  for (int j = 1; j <= b.Mm; j++) {
-    double best = 0.0, bw = 0.0, bk = -1.0;
+  std::vector<double> h(b.n2), pm(b.n2), pn(b.n2), rm(b.n2);
+  CHECK_HIP(hipMemcpy(h.data(), g.d.f.h, b.n2 * sizeof(double), hipMemcpyDeviceToHost));
+  CHECK_HIP(hipMemcpy(pm.data(), g.d.f.pm, b.n2 * sizeof(double), hipMemcpyDeviceToHost));
+  CHECK_HIP(hipMemcpy(pn.data(), g.d.f.pn, b.n2 * sizeof(double), hipMemcpyDeviceToHost));
+  CHECK_HIP(hipMemcpy(rm.data(), g.d.f.rmask, b.n2 * sizeof(double), hipMemcpyDeviceToHost));
+  std::vector<double> dA(b.n2, 0.0), dV(b.n2, 0.0);
+  for (int j = 1; j <= b.Mm; j++)
     for (int i = 1; i <= b.Lm; i++) {
       const long o = IJ(b, i, j);
-      if (cx[o] > best || (cx[o] == best && best > 0.0 && kx[o] > bk)) { best = cx[o]; bw = cw[o]; bk = kx[o]; }
+      dA[o] = rm[o] / (pm[o] * pn[o]);
+      dV[o] = dA[o] * h[o];
     }
-    if (best > Cu) { Cu = best; Cw = bw; }
+  const double loc[2] = {pair_sum(H, dA), pair_sum(H, dV)};
+  const int nr = g.halo.comm ? comm_size(g.halo.comm) : 1;
+  std::vector<double> all(2 * (size_t)nr);
+  if (halo_allgather(g.halo, g.s, loc, 2, all.data())) { g.err = "roms_gpu_diag: area/volume gather failed"; return -2; }
+  std::vector<double> va, vv;
+  for (int q = 0; q < nr; q++) { va.push_back(all[2 * q]); vv.push_back(all[2 * q + 1]); }
+  g.area = tree_sum(va);
+  g.volume = tree_sum(vv);
+  g.have_volume = true;
+  return 0;
+}
+
+int roms_gpu_set_weights(int ndtfast, double weight[2][ROMS_MAX_FAST]) {
+  if (ndtfast < 1 || !weight) return -1;
+  return set_weights(ndtfast, weight);
+}
+
+// diag.F code_check norms, all on the device (k_diag.hip: per-column terms,
+// reduction by pairs, first-maximum Courant scan, blow-up flag); six numbers
+// come back, ranks combine in the reference's tree order (diag.F:488-535).
+int roms_gpu_diag(const roms_tlev* t, double norms[4]) {
+  REQUIRE_INIT();
+  if (!g.have_volume) {
+    CHECK_HIP(hipStreamSynchronize(g.s));
+    const int r = grid_integrals();
+    if (r) return r;
   }
+  launch_diag(g.d, g.s, to_tlev(t), g.d_diag);
+  CHECK_HIP(hipMemcpyAsync(g.h_diag, g.d_diag, 6 * sizeof(double), hipMemcpyDeviceToHost, g.s));
+  CHECK_HIP(hipStreamSynchronize(g.s));
+  const double avzeta = g.h_diag[0], kes = g.h_diag[1], ke2 = g.h_diag[2], Cu = g.h_diag[3], Cw = g.h_diag[4];
+  const bool blowup = g.h_diag[5] != 0.0;
   if (g.halo.comm) {
     // per-rank partial sums / maxima combined in the reference's tree order (diag.F:488-535)
-    const double loc[5] = {avzeta, kes, ke2, Cu, Cw};
+    const double loc[6] = {avzeta, kes, ke2, Cu, Cw, blowup ? 1.0 : 0.0};
     const int nr = comm_size(g.halo.comm);
-    std::vector<double> all(5 * (size_t)nr);
-    if (halo_allgather(g.halo, g.s, loc, 5, all.data())) { g.err = "roms_gpu_diag: gather failed"; return -2; }
+    std::vector<double> all(6 * (size_t)nr);
+    if (halo_allgather(g.halo, g.s, loc, 6, all.data())) { g.err = "roms_gpu_diag: gather failed"; return -2; }
     std::vector<double> a(nr), k1(nr), k2(nr), cu(nr), cw(nr);
-    for (int q = 0; q < nr; q++) { a[q] = all[5 * q]; k1[q] = all[5 * q + 1]; k2[q] = all[5 * q + 2]; cu[q] = all[5 * q + 3]; cw[q] = all[5 * q + 4]; }
+    bool any = false;
+    for (int q = 0; q < nr; q++) {
+      a[q] = all[6 * q]; k1[q] = all[6 * q + 1]; k2[q] = all[6 * q + 2]; cu[q] = all[6 * q + 3]; cw[q] = all[6 * q + 4];
+      any = any || all[6 * q + 5] != 0.0;
+    }
     int size = nr;
     while (size > 1) {
       const int step = (size + 1) / 2;
@@ -889,12 +919,14 @@ int roms_gpu_diag(const roms_tlev* t, double norms[4]) {
     norms[1] = tree_sum(k2) / (g.volume + tree_sum(a));
     norms[2] = cu[0];
     norms[3] = cw[0];
+    if (any) { g.err = "roms_gpu_diag: Abnormal termination: BLOWUP (non-finite norms, diag.F:621-633)"; return -7; }
     return post_launch();
   }
   norms[0] = kes / (g.volume + avzeta);
   norms[1] = ke2 / (g.volume + avzeta);
   norms[2] = Cu;
   norms[3] = Cw;
+  if (blowup) { g.err = "roms_gpu_diag: Abnormal termination: BLOWUP (non-finite norms, diag.F:621-633)"; return -7; }
   return post_launch();
 }
 
