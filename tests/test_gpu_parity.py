@@ -224,3 +224,39 @@ def test_diag_blowup_flag_is_fatal():
     with pytest.raises(romsgpu.RomsGpuError, match="BLOWUP"):
         m.diag()
     m.close()
+
+
+def _routine_fields(cfg, routine, outs, env, monkeypatch):
+    """One routine from the oracle's state after 3 steps (corrector indices),
+    with the library initialised under `env`; returns the GPU outputs."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    o, m = make_pair(cfg)
+    o.step(3)
+    iic, kstp, knew, nstp, nrhs, nnew = o.tindex()
+    copy_state(o, m)
+    m.set_tindex(iic, kstp, knew, nstp, 3, 3 - nstp, nfast=o.nfast())
+    getattr(m, routine)()
+    m.sync()
+    res = {n: m.get(n).copy() for n in outs}
+    m.close()
+    return res
+
+
+@pytest.mark.parametrize("case", ["filament", "basin", "basin_n100"])
+def test_uv2_fused_bitwise_equals_two_kernels(case, monkeypatch):
+    """k_uv2_fused (one pass, segment-chained sums in the reference's k order)
+    gives exactly the bits of k_uv2_couple + u3dbc/v3dbc + k_uv2_flux, on a
+    periodic domain, a closed basin (edge columns through the split path)
+    and a 100-level basin (25 levels per lane)."""
+    if case == "filament":
+        cfg = oracle.filament_cfg(LLm=32, MMm=24, N=16, np_xi=1, np_eta=1)
+    elif case == "basin":
+        cfg = basin_cfg(nonlin=True)
+    else:
+        cfg = basin_cfg(LLm=40, MMm=36, N=100, nonlin=True)
+    outs = ["u", "v", "ubar", "vbar", "FlxU", "FlxV"]
+    a = _routine_fields(cfg, "step3d_uv2", outs, {"ROMS_GPU_UV2_FUSED": "1"}, monkeypatch)
+    b = _routine_fields(cfg, "step3d_uv2", outs, {"ROMS_GPU_UV2_FUSED": "0"}, monkeypatch)
+    for n in outs:
+        assert np.array_equal(a[n], b[n]), n

@@ -56,6 +56,21 @@ inline int seg_waves(int N) {
   return (S + per - 1) / per;
 }
 
+// Logical block of a segment-solver launch.  ord 0: xcd_tile() order (x
+// fastest); ord 1: z (direction / tracer) fastest, then y (j), then x, so the
+// blocks that share a column's arrays (both directions, all tracers) and the
+// j-neighbour rows run back to back on one XCD; ord 2: z, then x, then y.
+__device__ __forceinline__ uint3 seg_tile(int ord) {
+  uint3 t = xcd_tile();
+  if (ord == 0) return t;
+  const unsigned gx = gridDim.x, gy = gridDim.y, gz = gridDim.z;
+  const unsigned L = t.x + gx * (t.y + gy * t.z);
+  t.z = L % gz;
+  if (ord == 1) { t.y = (L / gz) % gy; t.x = L / (gz * gy); }
+  else { t.x = (L / gz) % gx; t.y = L / (gz * gx); }
+  return t;
+}
+
 // LDS exchange area of one block: 6 end-relation values per (segment, column)
 struct SegXchg {
   double v[6][kSegMaxS][kSegCW];

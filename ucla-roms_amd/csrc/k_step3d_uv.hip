@@ -214,7 +214,7 @@ struct SegRu {
   double r[kSegRows * kSegMaxS][kSegCW];
 };
 __global__ void __launch_bounds__(kSegBlock) k_uv1_seg(Dev d, Range R, int nnew, int nrhs) {
-  const uint3 bI = xcd_tile();
+  const uint3 bI = seg_tile(d.p.seg_order);
   __shared__ SegXchg X;
   __shared__ SegRu Sr;
   constexpr int KR = kSegRows + 1;
@@ -476,9 +476,18 @@ void launch_visc3d(const Dev& d, hipStream_t s, const Tlev& t) {
   hipLaunchKernelGGL(k_visc3d, grid_of(R), dim3(kBX, kBY), 0, s, d, R, t.nstp);
 }
 
+// Columns that k_uv2_fused owns: the coupling range without the rows (u) /
+// columns (v) next to a closed edge, whose coupled values u3dbc/v3dbc copy
+// into the ghost rows before the flux correction.
+__device__ __forceinline__ bool uv2_fused_in(const Bounds& b, int dir, int i, int j) {
+  if (dir == 0)
+    return i >= b.istrU && i <= b.iend && j >= b.jstr + (b.south_edge ? 1 : 0) && j <= b.jend - (b.north_edge ? 1 : 0);
+  return i >= b.istr + (b.west_edge ? 1 : 0) && i <= b.iend - (b.east_edge ? 1 : 0) && j >= b.jstrV && j <= b.jend;
+}
+
 // ---- step3d_uv2 part 1: convert Hz*u to u and remove the mismatch against
 // the fast-time-averaged barotropic flux DU_avg1 (at n+1 depths) ----
-__global__ void __launch_bounds__(256) k_uv2_couple(Dev d, Range R, int nnew) {
+__global__ void __launch_bounds__(256) k_uv2_couple(Dev d, Range R, int nnew, int edges) {
   ROMS_IJ_OR_RETURN(R)
   const Bounds& b = d.b;
   const Fields& F = d.f;
@@ -487,6 +496,7 @@ __global__ void __launch_bounds__(256) k_uv2_couple(Dev d, Range R, int nnew) {
   for (int dir = 0; dir < 2; dir++) {
     if (dir == 0 && !(i >= b.istrU)) continue;
     if (dir == 1 && !(j >= b.jstrV)) continue;
+    if (edges && uv2_fused_in(b, dir, i, j)) continue;   // edge mode: what k_uv2_fused leaves out
     const long s = dir == 0 ? 1 : b.nx2;
     double* __restrict__ Un = (dir == 0 ? F.u : F.v) + (long)(nnew - 1) * b.n3 + ij;
     const double* __restrict__ Hz = F.Hz + ij;
@@ -517,7 +527,8 @@ __global__ void __launch_bounds__(256) k_uv2_couple(Dev d, Range R, int nnew) {
 
 // ---- step3d_uv2 part 2: ubar,vbar(knew) from DU_avg1; corrected fluxes
 // FlxU = DELTA*FlxU + EPSIL*Hz_u*dn_u*(u(nstp)+u(nnew)), mismatch vs DU_avg2 ----
-__global__ void __launch_bounds__(256) k_uv2_flux(Dev d, Range R, int nnew, int nstp, int knew, int iu0, int iu1, int iv0, int iv1) {
+__global__ void __launch_bounds__(256) k_uv2_flux(Dev d, Range R, int nnew, int nstp, int knew, int iu0, int iu1, int iv0,
+                                                  int iv1, int edges) {
   ROMS_IJ_OR_RETURN(R)
   const Bounds& b = d.b;
   const Fields& F = d.f;
@@ -527,6 +538,8 @@ __global__ void __launch_bounds__(256) k_uv2_flux(Dev d, Range R, int nnew, int 
   for (int dir = 0; dir < 2; dir++) {
     if (dir == 0 && !(i >= iu0 && i <= iu1)) continue;
     if (dir == 1 && !(i >= iv0 && i <= iv1 && j >= b.jstr)) continue;
+    // edge mode: only the columns k_uv2_fused leaves out (outside the coupling range)
+    if (edges && uv2_fused_in(b, dir, i, j)) continue;
     const long s = dir == 0 ? 1 : b.nx2;
     double* __restrict__ Un = (dir == 0 ? F.u : F.v) + (long)(nnew - 1) * b.n3 + ij;
     const double* __restrict__ Us = (dir == 0 ? F.u : F.v) + (long)(nstp - 1) * b.n3 + ij;
@@ -571,17 +584,146 @@ __global__ void __launch_bounds__(256) k_uv2_flux(Dev d, Range R, int nnew, int 
   }
 }
 
+// ---- step3d_uv2, fused form: k_uv2_couple and k_uv2_flux for every column
+// of the coupling range in one pass, for both directions.  A wavefront holds
+// 16 columns x 4 vertical segments (lane = 16*g + column, g = 0 the bottom
+// segment of KL levels), so every load covers four 128-B rows; a block is a
+// 16 x 4 patch of columns.  The column's values stay in the lane's registers
+// between the reference's three vertical passes, and the four vertical sums
+// (sum of Hz_u, of Hz_u*u, of Hz_u*dn_u, of the corrected fluxes) run as a
+// chain down the segments, top lane first, handing the running sum to the
+// lane below with a shuffle, so every sum keeps the reference's k = N..1
+// order and the results are bit-identical to the two kernels
+// (step3d_uv2.F:18-786).  The open-edge columns outside the coupling range
+// (walls, ghost rows) follow u3dbc/v3dbc through k_uv2_flux (edge mode). ----
+template <int KL>
+__global__ void __launch_bounds__(256, KL > 13 ? 3 : 4) k_uv2_fused(Dev d, Range R, int nnew, int nstp, int knew) {
+  const uint3 bI = xcd_tile();
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const int N = b.N;
+  const double DELTA = 0.28, EPSIL = 0.36;
+  const int l = (int)(threadIdx.x & 63u), w = (int)(threadIdx.x >> 6);
+  const int col = l & 15, g = l >> 4;
+  const int i = R.i0 + (int)bI.x * 16 + col, j = R.j0 + (int)bI.y * 4 + w;
+  const int lo = 1 + g * KL;
+  const int nk = max(0, min(N, lo + KL - 1) - lo + 1);
+  const long n2 = b.n2;
+  // the sum of the segments above, handed down the chain (lane l+16 -> l)
+  auto chain2 = [&](double& s1, double& s2, auto&& body) {
+    s1 = 0.0; s2 = 0.0;
+#pragma unroll
+    for (int st = 3; st >= 0; st--) {
+      const double in1 = __shfl_down(s1, 16), in2 = __shfl_down(s2, 16);
+      if (g == st) {
+        if (st < 3) { s1 = in1; s2 = in2; }
+        body(s1, s2);
+      }
+    }
+    s1 = __shfl(s1, col);   // totals from the bottom segment
+    s2 = __shfl(s2, col);
+  };
+  for (int dir = 0; dir < 2; dir++) {
+    // the lane's column, clamped into the coupling range (lanes outside
+    // k_uv2_fused's columns compute on a valid column so the shuffles see
+    // defined values, and store nothing)
+    const int ilo = dir == 0 ? b.istrU : b.istr, jlo = dir == 0 ? b.jstr : b.jstrV;
+    const int ic = min(max(i, ilo), b.iend), jc = min(max(j, jlo), b.jend);
+    const bool act = ic == i && jc == j && uv2_fused_in(b, dir, i, j);
+    const long ij = IJ(b, ic, jc), s = dir == 0 ? 1 : b.nx2;
+    double* __restrict__ Un = (dir == 0 ? F.u : F.v) + (long)(nnew - 1) * b.n3 + ij;
+    const double* __restrict__ Us = (dir == 0 ? F.u : F.v) + (long)(nstp - 1) * b.n3 + ij;
+    double* __restrict__ Flx = (dir == 0 ? F.FlxU : F.FlxV) + ij;
+    const double* __restrict__ Hz = F.Hz + ij;
+    const double dn = dir == 0 ? F.dn_u[ij] : F.dm_v[ij];
+    const double avg1 = dir == 0 ? F.DU_avg1[ij] : F.DV_avg1[ij];
+    const double avg2 = dir == 0 ? F.DU_avg2[ij] : F.DV_avg2[ij];
+    const double msk = dir == 0 ? F.umask[ij] : F.vmask[ij];
+    double un[KL], hc[KL];
+#pragma unroll
+    for (int q = 0; q < KL; q++) {
+      if (q < nk) {
+        const long o = (long)(lo + q - 1) * n2;
+        un[q] = Un[o];
+        hc[q] = 0.5 * (Hz[o] + Hz[o - s]);
+      }
+    }
+    // k_uv2_couple: CF0 = sum Hz_u, DC0 = sum Hz*u (k = N..1); u = Hz*u/Hz_u
+    double CF0, DC0;
+    chain2(CF0, DC0, [&](double& a, double& c) {
+#pragma unroll
+      for (int q = KL - 1; q >= 0; q--)
+        if (q < nk) { a = a + hc[q]; c = c + un[q]; }
+    });
+    DC0 = (DC0 * dn - avg1) / (CF0 * dn);
+#pragma unroll
+    for (int q = 0; q < KL; q++)
+      if (q < nk) un[q] = (un[q] / hc[q] - DC0) * msk;
+    // k_uv2_flux: D = sum Hz_u*dn, FC = sum Hz_u*dn*u (k = N..1)
+    double DS, FC0;
+    chain2(DS, FC0, [&](double& a, double& c) {
+#pragma unroll
+      for (int q = KL - 1; q >= 0; q--)
+        if (q < nk) { const double dck = hc[q] * dn; a = a + dck; c = c + dck * un[q]; }
+    });
+    const double DCi = 1.0 / DS;
+    if (act && g == 0) {
+      if (dir == 0) F.ubar[IJL(b, i, j, knew)] = DCi * avg1;
+      else F.vbar[IJL(b, i, j, knew)] = DCi * avg1;
+    }
+    FC0 = DCi * (FC0 - avg1);
+    // corrected u and the fluxes; un[] becomes the flux cfk
+#pragma unroll
+    for (int q = 0; q < KL; q++) {
+      if (q < nk) {
+        const long o = (long)(lo + q - 1) * n2;
+        const double u1 = (un[q] - FC0) * msk;
+        if (act) Un[o] = u1;
+        un[q] = DELTA * Flx[o] + EPSIL * (hc[q] * dn) * (Us[o] + u1);
+      }
+    }
+    double CS, unused;
+    chain2(CS, unused, [&](double& a, double& c) {
+#pragma unroll
+      for (int q = KL - 1; q >= 0; q--)
+        if (q < nk) a = a + un[q];
+    });
+    const double CF1 = DCi * (CS - avg2);
+    if (act) {
+#pragma unroll
+      for (int q = 0; q < KL; q++)
+        if (q < nk) Flx[(long)(lo + q - 1) * n2] = un[q] - (hc[q] * dn) * CF1;
+    }
+  }
+}
+
 void launch_step3d_uv2(const Dev& d, hipStream_t s, const Tlev& t) {
   const Bounds& b = d.b;
   Range R1{b.istr, b.iend, b.jstr, b.jend};
-  hipLaunchKernelGGL(k_uv2_couple, grid_of(R1), dim3(kBX, kBY), 0, s, d, R1, t.nnew);
-  launch_u3dbc(d, s, t);
-  launch_v3dbc(d, s, t);
   const int iu0 = b.istr, iu1 = b.ew_periodic ? b.iend : b.iendR;
   const int iv0 = b.ew_periodic ? b.istr : b.istrR, iv1 = b.ew_periodic ? b.iend : b.iendR;
   const int j0 = b.ns_periodic ? b.jstr : b.jstrR, j1 = b.ns_periodic ? b.jend : b.jendR;
   Range R2{iv0 < iu0 ? iv0 : iu0, iu1 > iv1 ? iu1 : iv1, j0, j1};
-  hipLaunchKernelGGL(k_uv2_flux, grid_of(R2), dim3(kBX, kBY), 0, s, d, R2, t.nnew, t.nstp, t.knew, iu0, iu1, iv0, iv1);
+  const int kl = (b.N + 3) / 4;
+  if (!d.p.obc && d.p.uv2_fused && kl <= 25) {
+    const dim3 gf((R1.i1 - R1.i0 + 16) / 16, (R1.j1 - R1.j0 + 4) / 4);
+    if (kl <= 5) hipLaunchKernelGGL(k_uv2_fused<5>, gf, dim3(256), 0, s, d, R1, t.nnew, t.nstp, t.knew);
+    else if (kl <= 13) hipLaunchKernelGGL(k_uv2_fused<13>, gf, dim3(256), 0, s, d, R1, t.nnew, t.nstp, t.knew);
+    else hipLaunchKernelGGL(k_uv2_fused<25>, gf, dim3(256), 0, s, d, R1, t.nnew, t.nstp, t.knew);
+    if (b.west_edge || b.east_edge || b.south_edge || b.north_edge) {   // columns next to closed edges: couple, u3dbc/v3dbc, flux
+      hipLaunchKernelGGL(k_uv2_couple, grid_of(R1), dim3(kBX, kBY), 0, s, d, R1, t.nnew, 1);
+      launch_u3dbc(d, s, t);
+      launch_v3dbc(d, s, t);
+      hipLaunchKernelGGL(k_uv2_flux, grid_of(R2), dim3(kBX, kBY), 0, s, d, R2, t.nnew, t.nstp, t.knew, iu0, iu1, iv0,
+                         iv1, 1);
+    }
+  } else {
+    hipLaunchKernelGGL(k_uv2_couple, grid_of(R1), dim3(kBX, kBY), 0, s, d, R1, t.nnew, 0);
+    launch_u3dbc(d, s, t);
+    launch_v3dbc(d, s, t);
+    hipLaunchKernelGGL(k_uv2_flux, grid_of(R2), dim3(kBX, kBY), 0, s, d, R2, t.nnew, t.nstp, t.knew, iu0, iu1, iv0, iv1,
+                       0);
+  }
   launch_exchange_list(d, s, ExchList{{d.f.FlxU, d.f.u + (long)(t.nnew - 1) * b.n3, d.f.ubar + (long)(t.knew - 1) * b.n2,
                                         d.f.FlxV, d.f.v + (long)(t.nnew - 1) * b.n3, d.f.vbar + (long)(t.knew - 1) * b.n2},
                                        {b.N, b.N, 1, b.N, b.N, 1}, 6});

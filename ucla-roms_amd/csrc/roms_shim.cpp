@@ -380,6 +380,16 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     const char* e = getenv("ROMS_GPU_COLREG");
     if (e && e[0] == '0') P.colreg = 0;
   }
+  P.uv2_fused = 1;
+  {
+    const char* e = getenv("ROMS_GPU_UV2_FUSED");
+    if (e && e[0] == '0') P.uv2_fused = 0;
+  }
+  P.seg_order = 0;
+  {
+    const char* e = getenv("ROMS_GPU_SEG_ORDER");
+    if (e && e[0] >= '0' && e[0] <= '2') P.seg_order = e[0] - '0';
+  }
   // column-solver scratch: LDS while two (N+1)-level slots per wave fit the
   // default 64 KB (N < 63), global memory for deeper grids;
   // ROMS_GPU_COL_GLOBAL=1/0 forces either (A/B runs)
