@@ -2,6 +2,7 @@
 // visc3d (visc3d_S.F:18-131) and the 2-D/3-D coupling step3d_uv2
 // (step3d_uv2.F:18-786, IMPLICIT_BOTTOM_DRAG branch).
 #include "k_colseg.h"
+#include "k_chain.h"
 
 namespace roms {
 
@@ -603,26 +604,10 @@ __global__ void __launch_bounds__(256, KL > 13 ? 3 : 4) k_uv2_fused(Dev d, Range
   const Fields& F = d.f;
   const int N = b.N;
   const double DELTA = 0.28, EPSIL = 0.36;
-  const int l = (int)(threadIdx.x & 63u), w = (int)(threadIdx.x >> 6);
-  const int col = l & 15, g = l >> 4;
-  const int i = R.i0 + (int)bI.x * 16 + col, j = R.j0 + (int)bI.y * 4 + w;
-  const int lo = 1 + g * KL;
-  const int nk = max(0, min(N, lo + KL - 1) - lo + 1);
+  const ChainLane cl = chain_lane<KL>(R, bI, N);
+  const int i = cl.i, j = cl.j, g = cl.g, lo = cl.lo, nk = cl.nk;
   const long n2 = b.n2;
-  // the sum of the segments above, handed down the chain (lane l+16 -> l)
-  auto chain2 = [&](double& s1, double& s2, auto&& body) {
-    s1 = 0.0; s2 = 0.0;
-#pragma unroll
-    for (int st = 3; st >= 0; st--) {
-      const double in1 = __shfl_down(s1, 16), in2 = __shfl_down(s2, 16);
-      if (g == st) {
-        if (st < 3) { s1 = in1; s2 = in2; }
-        body(s1, s2);
-      }
-    }
-    s1 = __shfl(s1, col);   // totals from the bottom segment
-    s2 = __shfl(s2, col);
-  };
+  auto chain2 = [&](double& s1, double& s2, auto&& body) { chain_down(cl, s1, s2, body); };
   for (int dir = 0; dir < 2; dir++) {
     // the lane's column, clamped into the coupling range (lanes outside
     // k_uv2_fused's columns compute on a valid column so the shuffles see
@@ -706,7 +691,7 @@ void launch_step3d_uv2(const Dev& d, hipStream_t s, const Tlev& t) {
   Range R2{iv0 < iu0 ? iv0 : iu0, iu1 > iv1 ? iu1 : iv1, j0, j1};
   const int kl = (b.N + 3) / 4;
   if (!d.p.obc && d.p.uv2_fused && kl <= 25) {
-    const dim3 gf((R1.i1 - R1.i0 + 16) / 16, (R1.j1 - R1.j0 + 4) / 4);
+    const dim3 gf = chain_grid_of(R1);
     if (kl <= 5) hipLaunchKernelGGL(k_uv2_fused<5>, gf, dim3(256), 0, s, d, R1, t.nnew, t.nstp, t.knew);
     else if (kl <= 13) hipLaunchKernelGGL(k_uv2_fused<13>, gf, dim3(256), 0, s, d, R1, t.nnew, t.nstp, t.knew);
     else hipLaunchKernelGGL(k_uv2_fused<25>, gf, dim3(256), 0, s, d, R1, t.nnew, t.nstp, t.knew);

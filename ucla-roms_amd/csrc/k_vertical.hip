@@ -5,6 +5,7 @@
 // 512-byte row.  Arithmetic order follows the reference statements so FP64
 // results match the CPU reference bit for bit (built with -ffp-contract=off).
 #include "roms_dev.h"
+#include "k_chain.h"
 
 namespace roms {
 
@@ -144,10 +145,73 @@ __global__ void __launch_bounds__(256) k_set_huv1(Dev d, Range R, int nnew, int 
   }
 }
 
+// Chained form (k_chain.h): the column's u and Hz_u*dn stay in the lane's
+// registers between the sum and the correction pass; the two sums run down
+// the segments in the reference's k = N..1 order (bit-identical).
+template <int KL>
+__global__ void __launch_bounds__(256) k_set_huv1_chain(Dev d, Range R, int nnew, int first) {
+  const uint3 bI = xcd_tile();
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const double NOW = 3.63, MID = 4.47, BAK = 2.05;
+  const int N = b.N;
+  const ChainLane cl = chain_lane<KL>(R, bI, N);
+  const long n2 = b.n2;
+#pragma unroll 1
+  for (int dir = 0; dir < 2; dir++) {
+    const int ilo = dir == 0 ? b.istr : b.istrR, jlo = dir == 0 ? b.jstrR : b.jstr;
+    const int ic = min(max(cl.i, ilo), b.iendR), jc = min(max(cl.j, jlo), b.jendR);
+    const bool act = ic == cl.i && jc == cl.j;
+    const long ij = IJ(b, ic, jc), s = dir == 0 ? 1 : b.nx2;
+    const double dn = dir == 0 ? F.dn_u[ij] : F.dm_v[ij];
+    double* __restrict__ u = (dir == 0 ? F.u : F.v) + (long)(nnew - 1) * b.n3 + ij;
+    double* __restrict__ Flx = (dir == 0 ? F.FlxU : F.FlxV) + ij;
+    const double* __restrict__ Hz = F.Hz + ij;
+    double uu[KL], dc[KL];
+#pragma unroll
+    for (int q = 0; q < KL; q++) {
+      if (q < cl.nk) {
+        const long o = (long)(cl.lo + q - 1) * n2;
+        uu[q] = u[o];
+        dc[q] = 0.5 * (Hz[o] + Hz[o - s]) * dn;
+      }
+    }
+    double DC0, FC0;
+    chain_down(cl, DC0, FC0, [&](double& a, double& c) {
+#pragma unroll
+      for (int q = KL - 1; q >= 0; q--)
+        if (q < cl.nk) { a = a + dc[q]; c = c + dc[q] * uu[q]; }
+    });
+    const double a1 = dir == 0 ? F.DU_avg1[ij] : F.DV_avg1[ij];
+    if (first) FC0 = (FC0 - a1) / DC0;
+    else {
+      const double a2 = dir == 0 ? F.DU_avg2[ij] : F.DV_avg2[ij];
+      const double ab = dir == 0 ? F.DU_avg_bak[ij] : F.DV_avg_bak[ij];
+      FC0 = (FC0 - NOW * a1 + MID * a2 - BAK * ab) / DC0;
+    }
+    const double um = dir == 0 ? F.umask[ij] : F.vmask[ij];
+    if (act) {
+#pragma unroll
+      for (int q = 0; q < KL; q++) {
+        if (q < cl.nk) {
+          const long o = (long)(cl.lo + q - 1) * n2;
+          const double un = (uu[q] - FC0) * um;
+          u[o] = un;
+          Flx[o] = dc[q] * (un);
+        }
+      }
+    }
+  }
+}
+
 void launch_set_huv1(const Dev& d, hipStream_t s, const Tlev& t) {
   const Bounds& b = d.b;
   Range R{b.istrR < b.istr ? b.istrR : b.istr, b.iendR, b.jstrR < b.jstr ? b.jstrR : b.jstr, b.jendR};
-  hipLaunchKernelGGL(k_set_huv1, grid_of(R), dim3(kBX, kBY), 0, s, d, R, t.nnew, (int)(t.iic == t.forw_start));
+  const int kl = chain_kl(b.N), first = (int)(t.iic == t.forw_start);
+  if (d.p.chain && kl == 5) hipLaunchKernelGGL(k_set_huv1_chain<5>, chain_grid_of(R), dim3(256), 0, s, d, R, t.nnew, first);
+  else if (d.p.chain && kl == 13) hipLaunchKernelGGL(k_set_huv1_chain<13>, chain_grid_of(R), dim3(256), 0, s, d, R, t.nnew, first);
+  else if (d.p.chain && kl == 25) hipLaunchKernelGGL(k_set_huv1_chain<25>, chain_grid_of(R), dim3(256), 0, s, d, R, t.nnew, first);
+  else hipLaunchKernelGGL(k_set_huv1, grid_of(R), dim3(kBX, kBY), 0, s, d, R, t.nnew, first);
   launch_exchange_list(d, s, ExchList{{d.f.FlxU, d.f.FlxV, d.f.u + (long)(t.nnew - 1) * b.n3,
                                         d.f.v + (long)(t.nnew - 1) * b.n3}, {b.N, b.N, b.N, b.N}, 4});
 }

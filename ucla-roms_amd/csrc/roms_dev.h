@@ -39,6 +39,7 @@ struct Params {
   int colseg;     // 1: segment-partitioned column solvers (k_colseg.h; N > 63, ROMS_GPU_COLSEG=0/1)
   int colreg;     // 1: register-resident column solvers where compiled for N (ROMS_GPU_COLREG=0 disables)
   int uv2_fused;  // 1: one-pass step3d_uv2 (k_uv2_fused; ROMS_GPU_UV2_FUSED=0 disables)
+  int chain;      // 1: chained 4-lane set_HUV1 (k_chain.h; ROMS_GPU_CHAIN=0 disables)
   int seg_order;  // block order of the segment solvers (seg_tile; ROMS_GPU_SEG_ORDER)
   int npip;       // pipe_frc.F: number of pipes (0: pipe_source off)
   int curvgrid;   // CURVGRID && UV_ADV: curvature terms (compute_horiz_rhs_uv_terms.h:8-11)

@@ -385,6 +385,11 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     const char* e = getenv("ROMS_GPU_UV2_FUSED");
     if (e && e[0] == '0') P.uv2_fused = 0;
   }
+  P.chain = 1;
+  {
+    const char* e = getenv("ROMS_GPU_CHAIN");
+    if (e && e[0] == '0') P.chain = 0;
+  }
   P.seg_order = 0;
   {
     const char* e = getenv("ROMS_GPU_SEG_ORDER");
