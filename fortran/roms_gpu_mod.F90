@@ -54,7 +54,7 @@ module roms_gpu_mod
   ! LMD switch bits of lmd_mixing (ROMS_LMD_*)
   integer(c_int), parameter :: ROMS_LMD_MIXING = 1, ROMS_LMD_KPP = 2, ROMS_LMD_BKPP = 4, ROMS_LMD_RIMIX = 8, &
                                ROMS_LMD_CONVEC = 16, ROMS_LMD_NONLOCAL = 32
-  integer(c_int), parameter :: ROMS_GPU_ABI = 5   ! ROMS_GPU_ABI_VERSION, include/roms_gpu.h
+  integer(c_int), parameter :: ROMS_GPU_ABI = 6   ! ROMS_GPU_ABI_VERSION, include/roms_gpu.h
 
   ! field ids (enum roms_field) used by the drivers below
   integer(c_int), parameter :: ROMS_ALL = -1
@@ -175,6 +175,13 @@ module roms_gpu_mod
       integer(c_int), value :: npip
       integer(c_int), intent(in) :: pipe_idx(*)
       real(c_double), intent(in) :: pipe_flx(*), pipe_prf(*), pipe_trc(*)
+    end function
+    ! set_river_frc (river_frc.F:57-282): riv_uflx/riv_vflx as calc_river_flux
+    ! leaves them, riv_vol(nriv), riv_trc(nriv,nt)
+    integer(c_int) function roms_gpu_set_river_frc(nriv, riv_uflx, riv_vflx, riv_vol, riv_trc) bind(c)
+      import :: c_int, c_double
+      integer(c_int), value :: nriv
+      real(c_double), intent(in) :: riv_uflx(*), riv_vflx(*), riv_vol(*), riv_trc(*)
     end function
     integer(c_int) function roms_gpu_step(t) bind(c)
       import :: c_int, roms_tlev

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define ROMS_GPU_ABI_VERSION 5
+#define ROMS_GPU_ABI_VERSION 6
 #define ROMS_MAX_FAST 288
 
 /* Subdomain geometry of this rank: param.F / dimensions.F / mpi_setup.F:39-210 */
@@ -170,6 +170,16 @@ int roms_gpu_swr_frac(const roms_tlev *t);            /* swr_frac(tile)   lmd_sw
  * Call again whenever set_forces updates them; the next step uses them.      */
 int roms_gpu_set_pipe_frc(int npip, const int *pipe_idx, const double *pipe_flx, const double *pipe_prf,
                           const double *pipe_trc);
+/* set_river_frc (river_frc.F:57-96, init_river_frc :98-222, calc_river_flux
+ * :224-282): riv_uflx and riv_vflx as calc_river_flux leaves them on the
+ * (-1:Lm+2,-1:Mm+2) grid (10*iriver + the signed flux fraction on every face
+ * between a river-mouth cell and a wet neighbour, 0 elsewhere), riv_vol(nriv)
+ * [m3/s] and riv_trc(nriv,NT) column-major for the current time.  Passing
+ * riv_uflx = riv_vflx = NULL keeps the face arrays of an earlier call and
+ * updates only the time-dependent riv_vol/riv_trc.  nriv = 0 switches river
+ * sources off.  Returns 0, or -1 on a bad argument. */
+int roms_gpu_set_river_frc(int nriv, const double *riv_uflx, const double *riv_vflx, const double *riv_vol,
+                           const double *riv_trc);
 int roms_gpu_set_depth(const roms_tlev *t);           /* set_depth(tile)  set_depth.F:4    */
 
 /* One whole roms_step (main.F:333-520, forcing held fixed): advances t->iic
@@ -181,7 +191,7 @@ int roms_gpu_step(roms_tlev *t);
 int roms_gpu_init_sequence(roms_tlev *t);
 
 /* ---- analytic cases (host-side ana_grid/ana_init restatements) ---- */
-enum roms_case_id { ROMS_CASE_FILAMENT = 0, ROMS_CASE_BASIN = 1, ROMS_CASE_PIPES = 2 };
+enum roms_case_id { ROMS_CASE_FILAMENT = 0, ROMS_CASE_BASIN = 1, ROMS_CASE_PIPES = 2, ROMS_CASE_RIVERS = 3 };
 typedef struct roms_case {
   int case_id, LLm, MMm, N, NT;
   int salinity, nonlin_eos, lmd_mixing;  /* lmd_mixing: 0 or ROMS_LMD_* bits */

@@ -13,7 +13,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB = os.path.join(_HERE, "liboracle.so")
-CASE_FILAMENT, CASE_BASIN, CASE_PIPES = 0, 1, 2
+CASE_FILAMENT, CASE_BASIN, CASE_PIPES, CASE_RIVERS = 0, 1, 2, 3
 LMD_RIMIX, LMD_CONVEC, LMD_NONLOCAL = 8, 16, 32
 LMD_ALL = 63       # LMD_MIXING+KPP+BKPP+RIMIX+CONVEC+NONLOCAL (tests/Pipes_ana/cppdefs.opt)
 LMD_ICELAND = 47   # all but LMD_CONVEC (Examples/Iceland/Iceland_parent/cppdefs.opt:41-46)
@@ -81,6 +81,8 @@ def lib():
         L.or_rho_eos.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.or_lmd_vmix.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.or_set_iif.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.or_set_river.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                   ctypes.POINTER(ctypes.c_double)]
         _lib = L
     return _lib
 
@@ -118,6 +120,19 @@ def pipes_cfg(LLm=100, MMm=100, N=10, np_xi=3, np_eta=2):
     c.Akt_bak[0] = c.Akt_bak[1] = 0.0
     c.sizex, c.sizey = 30.0e3, 30.0e3
     c.diag_np_xi, c.diag_np_eta = np_xi, np_eta
+    return c
+
+
+def rivers_cfg(LLm=100, MMm=100, N=10, np_xi=3, np_eta=2):
+    """tests/Rivers_ana/{param.opt,benchmark.in,cppdefs.opt,ana_grid.h,ana_init.h,
+    ana_frc_river.h,river_frc.opt}: the Pipes_ana physics (KPP/BKPP/RIMIX/CONVEC/
+    NONLOCAL, NONLIN+SPLIT EOS, T+S, land mask) on a 10 km shelf (depth 5..100 m,
+    f = 0) with one analytic river (river_frc.F: riv_vol = 500 m3/s, T = 24,
+    S = 1) entering through the 20 cells of the channel mouth; dt = 20 s."""
+    c = pipes_cfg(LLm, MMm, N, np_xi, np_eta)
+    c.case_id = CASE_RIVERS
+    c.dt, c.ndtfast = 20.0, 30
+    c.sizex, c.sizey = 10.0e3, 10.0e3
     return c
 
 
@@ -166,6 +181,13 @@ class Oracle:
         p = self.L.or_weights(self.h)
         w = np.ctypeslib.as_array(p, shape=(2 * 288,)).reshape(2, 288)
         return w.copy()
+
+    def set_river(self, vol, trc):
+        """river_frc.F set_river_frc for one river: riv_vol, riv_trc(1:NT)."""
+        v = np.ascontiguousarray([vol], dtype=np.float64)
+        t = np.ascontiguousarray(trc, dtype=np.float64)
+        P = ctypes.POINTER(ctypes.c_double)
+        self.L.or_set_river(self.h, 1, v.ctypes.data_as(P), t.ctypes.data_as(P))
 
     def call(self, routine, *args):
         getattr(self.L, "or_" + routine)(self.h, *args)

@@ -46,6 +46,11 @@ struct or_state {
   /* pipe_frc.F (npip = 1, analytic): pipe_idx>0 cells carry pipe_flx */
   int pipe_source;
   double *pipe_flx, *pipe_idx, pipe_prf[1024], pipe_trc[2];
+  /* river_frc.F: riv_uflx/riv_vflx = 10*iriver + signed fraction on the
+     faces between a river-mouth land cell and its wet neighbours;
+     riv_vol(nriv), riv_trc(nriv,NT) column-major */
+  int river_source, nriv;
+  double *riv_uflx, *riv_vflx, riv_vol[16], riv_trc[16 * 16];
   /* open-boundary data (boundary.F:21-39): [0] west, [1] east (index j, 0:Mm+1),
      [2] south, [3] north (index i, 0:Lm+1); u,v (.,N), t (.,N,NT) */
   int nbry[4];
@@ -104,6 +109,7 @@ void or_v2dbc(or_state *S);
 void or_u3dbc(or_state *S);
 void or_v3dbc(or_state *S);
 void or_t3dbc(or_state *S, int itrc);
+void or_river_uv(or_state *S, int nnew);   /* river velocities in u,v(nnew) */
 /* open boundaries: sponge (set_nudgcof.F) and analytic boundary data */
 void or_set_nudgcof(or_state *S);
 void or_ana_bry(or_state *S);

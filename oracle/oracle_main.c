@@ -62,6 +62,7 @@ or_state *or_create(const or_cfg *cfg) {
   for (int q = 0; q < 6; q++) S->c1[q] = zalloc((size_t)S->nx2 * (S->N + 1));
   if (cfg->lmd) or_lmd_alloc(S);
   S->pipe_flx = zalloc(n2); S->pipe_idx = zalloc(n2);
+  S->riv_uflx = zalloc(n2); S->riv_vflx = zalloc(n2);
   S->dndx = zalloc(n2); S->dmde = zalloc(n2); S->ptide = zalloc(n2);
   /* boundary.F:111-129: zeta_west(0:Mm+1), u_west(0:Mm+1,N), t_west(0:Mm+1,N,NT), ... */
   S->nbry[0] = S->nbry[1] = S->Mm + 2;
@@ -452,6 +453,58 @@ void or_ana_grid(or_state *S) {
         A2(S->pipe_idx, i, j) = idx;
         A2(S->pipe_flx, i, j) = frac * 5e2;
       }
+  } else if (S->c.case_id == OR_CASE_RIVERS) {
+    /* tests/Rivers_ana/ana_grid.h:1-101 (single rank: iSW_corn = jSW_corn = 0),
+       loops over 0..ny+1, 0..nx+1 as written */
+    const double Size_XI = 1.0e4, Size_ETA = 1.0e4, depth = 5., max_depth = 100.0, f0 = 0.0e-4, beta = 0.;
+    const double xl = Size_XI, el = Size_ETA;
+    const double dx = Size_XI / (double)S->c.LLm, dy = Size_ETA / (double)S->c.MMm;
+    double x0 = 0., y0 = 0.;
+    for (int j = 0; j <= ny + 1; j++)
+      for (int i = 0; i <= nx + 1; i++) {
+        A2(S->xr, i, j) = x0 + dx * ((double)i - 0.5);
+        A2(S->yr, i, j) = y0 + dy * ((double)j - 0.5);
+        A2(S->pm, i, j) = 1. / dx;
+        A2(S->pn, i, j) = 1. / dy;
+      }
+    x0 = Size_XI / 2.; y0 = Size_ETA / 2.;
+    for (int j = 0; j <= ny + 1; j++)
+      for (int i = 0; i <= nx + 1; i++) A2(S->f, i, j) = f0 + beta * (A2(S->yr, i, j) - y0);
+    const double shelf = Size_ETA / 5, slope = (max_depth - depth) / (Size_ETA * 4 / 5);
+    for (int j = 0; j <= ny + 1; j++)
+      for (int i = 0; i <= nx + 1; i++) {
+        if (A2(S->yr, i, j) < shelf) A2(S->h, i, j) = depth;
+        else A2(S->h, i, j) = depth + (A2(S->yr, i, j) - shelf) * slope;
+      }
+    const double land = el * 0.1, coast = el * 0.02, riv_west = xl * 0.4, riv_east = xl * 0.6;
+    for (int j = 0; j <= ny + 1; j++)
+      for (int i = 0; i <= nx + 1; i++) {
+        A2(S->rmask, i, j) = 1;
+        if (A2(S->yr, i, j) < land)
+          if (A2(S->xr, i, j) < riv_west || A2(S->xr, i, j) > riv_east) A2(S->rmask, i, j) = 0.0;
+        if (A2(S->yr, i, j) < coast) A2(S->rmask, i, j) = 0.0;
+      }
+    /* river_frc.F init_river_frc (analytical, :118-135) + calc_river_flux
+       (:228-282); one river, ana_frc_river.h: riv_vol = 5e2, riv_trc = (24, 1) */
+    S->river_source = 1;
+    S->nriv = 1;
+    S->riv_vol[0] = 5e2;
+    S->riv_trc[0] = 24.0;
+    if (S->NT > 1) S->riv_trc[1] = 1.0;
+    const double riv_cells = (double)lround((riv_east - riv_west) * A2(S->pm, 1, 1));
+    for (int j = 0; j <= ny + 1; j++)
+      for (int i = 0; i <= nx + 1; i++) {
+        if (!(A2(S->xr, i, j) > riv_west && A2(S->xr, i, j) < riv_east)) continue;
+        if (!(A2(S->rmask, i, j) == 0 && A2(S->rmask, i, j + 1) == 1)) continue;
+        const double rfrc = 1 / riv_cells;
+        const int ridx = 1;
+        /* faces is an integer in calc_river_flux (river_frc.F:233) */
+        const int faces = (int)(A2(S->rmask, i - 1, j) + A2(S->rmask, i + 1, j) + A2(S->rmask, i, j - 1) + A2(S->rmask, i, j + 1));
+        if (A2(S->rmask, i - 1, j) > 0) A2(S->riv_uflx, i, j) = -(rfrc) / faces + 10 * ridx;
+        if (A2(S->rmask, i + 1, j) > 0) A2(S->riv_uflx, i + 1, j) = (rfrc) / faces + 10 * ridx;
+        if (A2(S->rmask, i, j - 1) > 0) A2(S->riv_vflx, i, j) = -(rfrc) / faces + 10 * ridx;
+        if (A2(S->rmask, i, j + 1) > 0) A2(S->riv_vflx, i, j + 1) = (rfrc) / faces + 10 * ridx;
+      }
   } else {
     /* synthetic closed basin (C3 stand-in) */
     const double dx = S->c.sizex / S->c.LLm, dy = S->c.sizey / S->c.MMm;
@@ -542,8 +595,9 @@ void or_ana_init(or_state *S) {
         ZETA(i, j, 2) = ZETA(i, j, 1);
         for (int k = 1; k <= nz; k++) { U(i, j, k, 1) = 0.; U(i, j, k, 2) = U(i, j, k, 1); V(i, j, k, 2) = V(i, j, k, 1); }
       }
-  } else if (S->c.case_id == OR_CASE_PIPES) {
-    /* tests/Pipes_ana/ana_init.h:14-52: rest state, T = 4 + 10 e^{z/50}, S = 36 */
+  } else if (S->c.case_id == OR_CASE_PIPES || S->c.case_id == OR_CASE_RIVERS) {
+    /* tests/Pipes_ana/ana_init.h:14-52, tests/Rivers_ana/ana_init.h:10-40:
+       rest state, T = 4 + 10 e^{z/50}, S = 36 */
     for (int k = 1; k <= nz; k++)
       for (int j = 0; j <= ny + 1; j++)
         for (int i = 0; i <= nx + 1; i++) {
@@ -744,6 +798,7 @@ void or_set_iif(or_state *S, int iif) { S->iif = iif; }
 
 double *or_field(or_state *S, const char *name, size_t *count) {
   struct { const char *n; double *p; size_t c; } tab[] = {
+      {"riv_uflx", S->riv_uflx, S->n2}, {"riv_vflx", S->riv_vflx, S->n2},
       {"zeta", S->zeta, 4 * S->n2}, {"ubar", S->ubar, 4 * S->n2}, {"vbar", S->vbar, 4 * S->n2},
       {"u", S->u, 3 * S->n3}, {"v", S->v, 3 * S->n3}, {"t", S->t, 3 * S->n3 * S->NT},
       {"FlxU", S->FlxU, S->n3}, {"FlxV", S->FlxV, S->n3}, {"We", S->We, S->n3w}, {"Wi", S->Wi, S->n3w},
@@ -782,4 +837,11 @@ double *or_field(or_state *S, const char *name, size_t *count) {
   }
   if (count) *count = 0;
   return NULL;
+}
+
+void or_set_river(or_state *S, int nriv, const double *vol, const double *trc) {
+  if (nriv < 1 || nriv > 16 || nriv * S->NT > 256) return;
+  S->nriv = nriv;
+  for (int r = 0; r < nriv; r++) S->riv_vol[r] = vol[r];
+  for (int q = 0; q < nriv * S->NT; q++) S->riv_trc[q] = trc[q];
 }

@@ -579,7 +579,25 @@ static void horiz_tracer_fluxes(or_state *S, int k, int itrc, int tl, int upstre
         A2(FE, i, j) = 0.5 * (t0 + tm) * F - 0.1666666666666666 * (A2(wrk, i, j - 1) * fmax0(F) + A2(wrk, i, j) * fmin0(F));
       else
         A2(FE, i, j) = 0.5 * (t0 + tm - 0.3333333333333333 * (A2(wrk, i, j) - A2(wrk, i, j - 1))) * F;
-    }
+    }  if (S->river_source) {  /* compute_horiz_tracer_fluxes.h:217-246: river tracer inflow */
+    const int N = S->N;
+    for (int j = jstr; j <= jend; j++)
+      for (int i = istr; i <= iend + 1; i++)
+        if (fabs(A2(S->riv_uflx, i, j)) > 1e-3) {
+          const double riv_depth = 0.5 * (ZW(i - 1, j, N) - ZW(i - 1, j, 0) + ZW(i, j, N) - ZW(i, j, 0));
+          const int iriver = (int)lround(A2(S->riv_uflx, i, j) / 10);
+          const double riv_uvel = S->riv_vol[iriver - 1] * (A2(S->riv_uflx, i, j) - 10 * iriver) / riv_depth;
+          A2(FX, i, j) = S->riv_trc[(iriver - 1) + (itrc - 1) * S->nriv] * 0.5 * (HZ(i - 1, j, k) + HZ(i, j, k)) * riv_uvel;
+        }
+    for (int j = jstr; j <= jend + 1; j++)
+      for (int i = istr; i <= iend; i++)
+        if (fabs(A2(S->riv_vflx, i, j)) > 1e-3) {
+          const double riv_depth = 0.5 * (ZW(i, j - 1, N) - ZW(i, j - 1, 0) + ZW(i, j, N) - ZW(i, j, 0));
+          const int iriver = (int)lround(A2(S->riv_vflx, i, j) / 10);
+          const double riv_vvel = S->riv_vol[iriver - 1] * (A2(S->riv_vflx, i, j) - 10 * iriver) / riv_depth;
+          A2(FE, i, j) = S->riv_trc[(iriver - 1) + (itrc - 1) * S->nriv] * 0.5 * (HZ(i, j - 1, k) + HZ(i, j, k)) * riv_vvel;
+        }
+  }
 }
 
 /* compute_vert_tracer_fluxes.h, SPLINE_TS with natural b.c. */
@@ -819,6 +837,29 @@ static void vert_rhs_uv(or_state *S, int j, double *ru, double *rv) {
 /* ---------------------------------------------------------------------- */
 /* pre_step3d_tile (pre_step3d4S.F:23-742), includes compute_rd_bott_drag.h */
 /* ---------------------------------------------------------------------- */
+/* river velocities in u,v(nnew) over the whole column (pre_step3d4S.F:493-522,
+ * step3d_uv2.F:689-717; the u range is istrU..iend in the predictor and
+ * istr..iend in the corrector, which differ only at a western wall face) */
+static void river_uv(or_state *S, int nnew, int iu0) {
+  const int N = S->N;
+  for (int j = S->jstr; j <= S->jend; j++)
+    for (int i = iu0; i <= S->iend; i++)
+      if (fabs(A2(S->riv_uflx, i, j)) > 1e-3) {
+        const double riv_depth = 0.5 * (ZW(i - 1, j, N) - ZW(i - 1, j, 0) + ZW(i, j, N) - ZW(i, j, 0));
+        const int iriver = (int)lround(A2(S->riv_uflx, i, j) / 10);
+        const double riv_uvel = S->riv_vol[iriver - 1] * (A2(S->riv_uflx, i, j) - 10 * iriver) / (A2(S->dn_u, i, j) * riv_depth);
+        for (int k = 1; k <= N; k++) U(i, j, k, nnew) = riv_uvel;
+      }
+  for (int j = (iu0 == S->istrU ? S->jstrV : S->jstr); j <= S->jend; j++)
+    for (int i = S->istr; i <= S->iend; i++)
+      if (fabs(A2(S->riv_vflx, i, j)) > 1e-3) {
+        const double riv_depth = 0.5 * (ZW(i, j - 1, N) - ZW(i, j - 1, 0) + ZW(i, j, N) - ZW(i, j, 0));
+        const int iriver = (int)lround(A2(S->riv_vflx, i, j) / 10);
+        const double riv_vvel = S->riv_vol[iriver - 1] * (A2(S->riv_vflx, i, j) - 10 * iriver) / (A2(S->dm_v, i, j) * riv_depth);
+        for (int k = 1; k <= N; k++) V(i, j, k, nnew) = riv_vvel;
+      }
+}
+
 void or_pre_step3d(or_state *S) {
   const int N = S->N, NT = S->NT, nstp = S->nstp, nnew = S->nnew, indx = 3 - nstp;
   const double AM3_crv = 1.0 / 6.0;
@@ -979,6 +1020,7 @@ void or_pre_step3d(or_state *S) {
         for (int i = S->istr; i <= S->iend; i++) V(i, j, k, nnew) = C1(DC, i, k) + C1(CF, i, k - 1) * V(i, j, k - 1, nnew);
     }
   }
+  if (S->river_source) river_uv(S, nnew, S->istrU);
   or_u3dbc(S);
   or_v3dbc(S);
   for (int itrc = 1; itrc <= NT; itrc++) {
@@ -1318,6 +1360,24 @@ void or_step2d(or_state *S) {
                                                                      (VBAR(i, jend + 1, knew)) * A2(S->dm_v, i, jend + 1);
     }
   }
+  if (S->river_source) {  /* step2d_FB.F:531-554: river inflow sets ubar, vbar(knew) and the fast-time flux */
+    for (int j = jstr; j <= jend; j++)
+      for (int i = istrU; i <= iend; i++)
+        if (fabs(A2(S->riv_uflx, i, j)) > 1e-3) {
+          const int iriver = (int)lround(A2(S->riv_uflx, i, j) / 10);
+          const double river_flux = S->riv_vol[iriver - 1] * (A2(S->riv_uflx, i, j) - 10 * iriver);
+          UBAR(i, j, knew) = river_flux * 2 / (A2(S->dn_u, i, j) * (A2(Dnew, i - 1, j) + A2(Dnew, i, j)));
+          A2(S->DU_avg1, i, j) = river_flux;
+        }
+    for (int j = jstrV; j <= jend; j++)
+      for (int i = istr; i <= iend; i++)
+        if (fabs(A2(S->riv_vflx, i, j)) > 1e-3) {
+          const int iriver = (int)lround(A2(S->riv_vflx, i, j) / 10);
+          const double river_flux = S->riv_vol[iriver - 1] * (A2(S->riv_vflx, i, j) - 10 * iriver);
+          VBAR(i, j, knew) = river_flux * 2 / (A2(S->dm_v, i, j) * (A2(Dnew, i, j - 1) + A2(Dnew, i, j)));
+          A2(S->DV_avg1, i, j) = river_flux;
+        }
+  }
   if (iif == S->nfast) {
     for (int j = S->jstrR; j <= S->jendR; j++)
       for (int i = S->istrR; i <= S->iendR; i++) ZETA(i, j, knew) = A2(S->Zt_avg1, i, j);
@@ -1432,6 +1492,7 @@ void or_step3d_uv2(or_state *S) {
         for (int i = iv0; i <= iv1; i++) FLXV(i, j, k) = C1(CF, i, k) - C1(DC, i, k) * C1(CF, i, 0);
     }
   }
+  if (S->river_source) river_uv(S, nnew, S->istr);
   or_exch3(S, S->FlxU, N);
   or_exch3(S, S->u + (size_t)(nnew - 1) * S->n3, N);
   or_exch2(S, S->ubar + (size_t)(knew - 1) * S->n2);

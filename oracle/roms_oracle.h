@@ -24,7 +24,7 @@ extern "C" {
 #endif
 
 /* analytic case selector */
-enum { OR_CASE_FILAMENT = 0, OR_CASE_BASIN = 1, OR_CASE_PIPES = 2 };
+enum { OR_CASE_FILAMENT = 0, OR_CASE_BASIN = 1, OR_CASE_PIPES = 2, OR_CASE_RIVERS = 3 };
 enum { OR_LMD_RIMIX = 8, OR_LMD_CONVEC = 16, OR_LMD_NONLOCAL = 32 };
 
 typedef struct or_cfg {
@@ -93,6 +93,8 @@ void or_swr_frac(or_state *S);
 void or_diag(or_state *S);
 void or_set_tindex(or_state *S, const int in[6]);
 void or_set_iif(or_state *S, int iif);
+/* set_river_frc: new riv_vol(nriv), riv_trc(nriv,NT) (faces kept) */
+void or_set_river(or_state *S, int nriv, const double *vol, const double *trc);
 
 #ifdef __cplusplus
 }

@@ -176,6 +176,29 @@ def test_pipes_ana_3x2_within_compiler_spread():
     assert worst <= spread, (worst, spread)
 
 
+def test_rivers_ana_3x2_within_compiler_spread():
+    """Rivers_ana (river_frc.F analytic river, KPP, land mask) on the
+    reference's 3x2 grid.  Its ana_grid.h fills 0..nx+1, 0..ny+1 of each rank
+    and ANA_GRID exchanges nothing (grid.F:444-446), so the outer halo ring
+    keeps its allocation values at the ranks' shared edges and the reference's
+    result depends on its decomposition: the single-domain oracle drifts from
+    the golden log after a few steps (tests/test_oracle_golden.py), while this
+    run, decomposed like the reference, stays within the gnu/ifx spread."""
+    keys = ("ke", "ke2b", "cu_adv", "cu_w")
+    gnu = json.load(open(os.path.join(ROOT, "tests", "golden", "rivers_ana_github_gnu.json")))["rows"]
+    ifx = json.load(open(os.path.join(ROOT, "tests", "golden", "rivers_ana_github_ifx.json")))["rows"]
+    spread = max(abs(float(x[k]) - float(g[k])) / abs(float(g[k])) for g, x in zip(gnu, ifx) for k in keys
+                 if float(g[k]) != 0.0)
+    case = dict(case_id=3, LLm=100, MMm=100, N=10, NT=2, salinity=True, nonlin_eos=True, dt=20.0, ndtfast=30,
+                sizex=10e3, sizey=10e3, lmd=True)
+    _, norms = run_decomposed(case, 3, 2, 20, fields=("zeta",), diag=True)
+    assert len(norms) == 21
+    worst = max(abs(v - float(g[k])) / abs(float(g[k])) for g, n in zip(gnu, norms) for k, v in zip(keys, n)
+                if float(g[k]) != 0.0)
+    # measured: 4.3e-13 (step 1 MAX_VERT_CFL, equal to the ifx value) against a spread of 4.3e-13
+    assert worst <= spread, (worst, spread)
+
+
 RCCL_SCRIPT = r"""
 import os, sys
 sys.path.insert(0, os.path.join(sys.argv[1], "ucla-roms_amd"))

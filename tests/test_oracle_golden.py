@@ -84,3 +84,28 @@ def test_pipes_ana_golden_within_compiler_spread():
     assert worst <= spread, (worst, spread)
     # step 0 (init: omega with the pipe inflow) is bit-exact
     assert [gnu[0][k] for k in _KEYS] == [_fmt(v).strip() for v in got[0]]
+
+
+def test_rivers_ana_golden_single_domain_drift():
+    """tests/Rivers_ana (river_frc.F analytic river, KPP, land mask).  The
+    reference's golden log comes from a 3x2 MPI run whose ana_grid.h fills
+    only 0..nx+1, 0..ny+1 of each rank, and ANA_GRID exchanges nothing
+    (grid.F:444-446): the outer halo ring keeps h = pm = pn = 0 at the ranks'
+    shared edges, so the reference's result depends on its decomposition.
+    The single-domain oracle therefore matches the log within the gnu/ifx
+    spread for the first step and drifts slowly after (measured: 2.4e-11 at
+    step 2, 2e-9 at step 9, then 1e-3 by step 20 once KPP thresholds flip);
+    the GPU run decomposed like the reference reproduces the log within the
+    spread (tests/test_gpu_multirank.py::test_rivers_ana_3x2_within_compiler_spread)."""
+    gnu, ifx = _rows("rivers_ana_github_gnu"), _rows("rivers_ana_github_ifx")
+    o = oracle.Oracle(oracle.rivers_cfg())
+    o.init()
+    assert o.nfast() == 41          # benchmark.result_github_gnu: "nfast =  41"
+    got = [o.norms()]
+    for _ in range(9):
+        o.step()
+        got.append(o.norms())
+    spread = max(_rel(float(x[k]), float(g[k])) for g, x in zip(gnu, ifx) for k in _KEYS)
+    for s, (g, v) in enumerate(zip(gnu, got)):
+        worst = max(_rel(val, float(g[k])) for k, val in zip(_KEYS, v))
+        assert worst <= (spread if s <= 1 else 5e-9), (s, worst, spread)

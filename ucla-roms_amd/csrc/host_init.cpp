@@ -225,6 +225,54 @@ void build_case(const CaseSpec& cs, HostState& H, double& area, double& volume) 
           H.pipe_flx[o] = 1.0 / pipe_cells * 5e2;  // pipe_fraction * pipe_vol(1)
         }
       }
+  } else if (cs.case_id == ROMS_CASE_RIVERS) {
+    // tests/Rivers_ana/ana_grid.h:1-101: 10 km shelf (5..100 m), f = 0, land
+    // strip with the river channel; the reference fills 0..nx+1, 0..ny+1 of
+    // each rank (the outer halo ring keeps the allocation values: 0, rmask 1)
+    const double Size_XI = 1.0e4, Size_ETA = 1.0e4, depth = 5., max_depth = 100.0, f0 = 0.0e-4, beta = 0.;
+    const double xl = Size_XI, el = Size_ETA;
+    const double dx = Size_XI / (double)cs.LLm, dy = Size_ETA / (double)cs.MMm;
+    const double x0 = dx * (double)cs.iSW_corn, y0 = dy * (double)cs.jSW_corn;
+    const double shelf = Size_ETA / 5, slope = (max_depth - depth) / (Size_ETA * 4 / 5);
+    const double land = el * 0.1, coast = el * 0.02, riv_west = xl * 0.4, riv_east = xl * 0.6;
+    for (int j = -1; j <= Mm + 2; j++)
+      for (int i = -1; i <= Lm + 2; i++) A(krmask, i, j) = 1;
+    for (int j = 0; j <= Mm + 1; j++)
+      for (int i = 0; i <= Lm + 1; i++) {
+        const double x = x0 + dx * ((double)i - 0.5), y = y0 + dy * ((double)j - 0.5);
+        A(kxr, i, j) = x; A(kyr, i, j) = y;
+        A(kpm, i, j) = 1. / dx; A(kpn, i, j) = 1. / dy;
+        A(kf, i, j) = f0 + beta * (y - Size_ETA / 2.);
+        A(kh, i, j) = y < shelf ? depth : depth + (y - shelf) * slope;
+        double rm = 1;
+        if (y < land && (x < riv_west || x > riv_east)) rm = 0.0;
+        if (y < coast) rm = 0.0;
+        A(krmask, i, j) = rm;
+      }
+    // river_frc.F init_river_frc (analytical, :118-135) and calc_river_flux
+    // (:228-282) over this rank's 0..nx+1, 0..ny+1; ana_frc_river.h:
+    // riv_vol(1) = 5e2 m3/s, riv_trc(1,1:2) = (24, 1)
+    H.nriv = 1;
+    H.riv_uflx.assign(n2, 0.0);
+    H.riv_vflx.assign(n2, 0.0);
+    H.riv_vol.assign(1, 5e2);
+    H.riv_trc.assign((size_t)NT, 0.0);
+    H.riv_trc[0] = 24.0; if (NT > 1) H.riv_trc[1] = 1.0;
+    const double riv_cells = (double)std::lround((riv_east - riv_west) * A(kpm, 1, 1));
+    auto RU = [&](int i, int j) -> double& { return H.riv_uflx[(i + 1) + (long)(j + 1) * H.nx2]; };
+    auto RV = [&](int i, int j) -> double& { return H.riv_vflx[(i + 1) + (long)(j + 1) * H.nx2]; };
+    for (int j = 0; j <= Mm + 1; j++)
+      for (int i = 0; i <= Lm + 1; i++) {
+        if (!(A(kxr, i, j) > riv_west && A(kxr, i, j) < riv_east)) continue;
+        if (!(A(krmask, i, j) == 0 && A(krmask, i, j + 1) == 1)) continue;
+        const double rfrc = 1 / riv_cells;
+        const int ridx = 1;
+        const int faces = (int)(A(krmask, i - 1, j) + A(krmask, i + 1, j) + A(krmask, i, j - 1) + A(krmask, i, j + 1));
+        if (A(krmask, i - 1, j) > 0) RU(i, j) = -(rfrc) / faces + 10 * ridx;
+        if (A(krmask, i + 1, j) > 0) RU(i + 1, j) = (rfrc) / faces + 10 * ridx;
+        if (A(krmask, i, j - 1) > 0) RV(i, j) = -(rfrc) / faces + 10 * ridx;
+        if (A(krmask, i, j + 1) > 0) RV(i, j + 1) = (rfrc) / faces + 10 * ridx;
+      }
   } else {
     const double dx = cs.sizex / cs.LLm, dy = cs.sizey / cs.MMm;
     const double R = 0.5 * (cs.sizex < cs.sizey ? cs.sizex : cs.sizey);
@@ -421,8 +469,9 @@ void build_case(const CaseSpec& cs, HostState& H, double& area, double& volume) 
         Z(i, j, 2) = Z(i, j, 1);
         for (int k = 1; k <= N; k++) V(i, j, k, 2) = V(i, j, k, 1);
       }
-  } else if (cs.case_id == ROMS_CASE_PIPES) {
-    // tests/Pipes_ana/ana_init.h:14-52: at rest, T = 4 + 10 e^{z/50}, S = 36 (LMD: Akv = Akt = 0)
+  } else if (cs.case_id == ROMS_CASE_PIPES || cs.case_id == ROMS_CASE_RIVERS) {
+    // tests/Pipes_ana/ana_init.h:14-52, tests/Rivers_ana/ana_init.h:10-40:
+    // at rest, T = 4 + 10 e^{z/50}, S = 36 (LMD: Akv = Akt = 0)
     for (int k = 1; k <= N; k++)
       for (int j = 0; j <= Mm + 1; j++)
         for (int i = 0; i <= Lm + 1; i++) {

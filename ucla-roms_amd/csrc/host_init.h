@@ -28,6 +28,9 @@ struct HostState {
   int npip = 0;
   std::vector<int> pipe_idx;
   std::vector<double> pipe_flx, pipe_prf, pipe_trc;
+  // river_frc.F (analytic river): nriv = 0 when river_source is off
+  int nriv = 0;
+  std::vector<double> riv_uflx, riv_vflx, riv_vol, riv_trc;
   HostState(int Lm_, int Mm_, int N_, int NT_, int nTS_);
   std::vector<double>& a(int id);
 };

@@ -135,6 +135,36 @@ __device__ __forceinline__ void tracer_spline_lds(int N, long n2, const double* 
   A[0] = 0.0;
 }
 
+// ---- river_frc.F: velocity through a river face (dir 0: the u face
+// between i-1 and i; dir 1: the v face between j-1 and j) of column ij:
+// riv_vol(iriver)*(riv_flx - 10*iriver) / (dn * riv_depth), dn = dn_u / dm_v
+// for the momentum (pre_step3d4S.F:497-501) or 1 for the tracer flux
+// (compute_horiz_tracer_fluxes.h:223-226); riv_depth is the mean water depth
+// of the two cells. ----
+__device__ __forceinline__ double river_velocity(const Dev& d, int dir, long ij, bool with_dn) {
+  const Fields& F = d.f;
+  const Bounds& b = d.b;
+  const long s = dir == 0 ? 1 : b.nx2, wN = (long)b.N * b.n2;
+  const double flx = dir == 0 ? F.riv_uflx[ij] : F.riv_vflx[ij];
+  const int iriver = (int)lround(flx / 10);
+  const double riv_depth = 0.5 * (F.z_w[ij - s + wN] - F.z_w[ij - s] + F.z_w[ij + wN] - F.z_w[ij]);
+  const double q = F.riv_vol[iriver - 1] * (flx - 10 * iriver);
+  return with_dn ? q / ((dir == 0 ? F.dn_u[ij] : F.dm_v[ij]) * riv_depth) : q / riv_depth;
+}
+// compute_horiz_tracer_fluxes.h:217-246: the tracer flux through a river
+// face at level k carries the river's concentration riv_trc(iriver, itrc)
+__device__ __forceinline__ void river_tracer_flux(const Dev& d, int dir, int i, int j, int k, int itrc, double& Fl) {
+  const Fields& F = d.f;
+  const Bounds& b = d.b;
+  const long ij = IJ(b, i, j);
+  const double flx = dir == 0 ? F.riv_uflx[ij] : F.riv_vflx[ij];
+  if (!(fabs(flx) > 1e-3)) return;
+  const long s = dir == 0 ? 1 : b.nx2, o = ij + (long)(k - 1) * b.n2;
+  const int iriver = (int)lround(flx / 10);
+  const double vel = river_velocity(d, dir, ij, false);
+  Fl = F.riv_trc[(iriver - 1) + (long)(itrc - 1) * d.p.nriv] * 0.5 * (F.Hz[o - s] + F.Hz[o]) * vel;
+}
+
 // ---- horizontal tracer fluxes at one face ----
 // Written over an accessor (t, umask, vmask, FlxU, FlxV at one level); the
 // kernels stage the block's window in LDS (AccTL).  FX at u-point m (row j):

@@ -46,8 +46,12 @@ __global__ void __launch_bounds__(256) k_pre_tracer_h(Dev d, Range R, PreCoef c,
     double* Tn = F.t + (long)(nnew - 1) * b.n3 + tb;
     double* Ti = F.t + (long)(indx - 1) * b.n3 + tb;
     const double* Ts = F.t + (long)(nstp - 1) * b.n3 + tb;
-    const double FX0 = tracer_fx(b, a, i, j, false), FX1 = tracer_fx(b, a, i + 1, j, false);
-    const double FE0 = tracer_fe(b, a, i, j, false), FE1 = tracer_fe(b, a, i, j + 1, false);
+    double FX0 = tracer_fx(b, a, i, j, false), FX1 = tracer_fx(b, a, i + 1, j, false);
+    double FE0 = tracer_fe(b, a, i, j, false), FE1 = tracer_fe(b, a, i, j + 1, false);
+    if (d.p.nriv > 0) {   // river inflow faces (compute_horiz_tracer_fluxes.h:217-246)
+      river_tracer_flux(d, 0, i, j, k, itrc, FX0); river_tracer_flux(d, 0, i + 1, j, k, itrc, FX1);
+      river_tracer_flux(d, 1, i, j, k, itrc, FE0); river_tracer_flux(d, 1, i, j + 1, k, itrc, FE1);
+    }
     const double tsk = Ts[o];
     Tn[o] = hb * (c.cf_stp * tsk + c.cf_bak * Ti[o]) - c.dtau * F.pm[ij] * F.pn[ij] * (FX1 - FX0 + FE1 - FE0);
     Ti[o] = hz * tsk;
@@ -468,6 +472,7 @@ void launch_pre_step3d(const Dev& d, hipStream_t s, const Tlev& t) {
     hipLaunchKernelGGL(k_pre_uv<ColGlb>, gu, dim3(kCX), 0, s, d, RI, c, t.nstp, t.nnew, t.nrhs);
   else
     hipLaunchKernelGGL(k_pre_uv<ColLds>, gu, dim3(kCX), col_lds_bytes(2, b.N), s, d, RI, c, t.nstp, t.nnew, t.nrhs);
+  launch_river_uv(d, s, t.nnew, 1);   // pre_step3d4S.F:493-522
   launch_u3dbc(d, s, t);
   launch_v3dbc(d, s, t);
   for (int itrc = 1; itrc <= b.NT; itrc++) launch_t3dbc(d, s, t, itrc);

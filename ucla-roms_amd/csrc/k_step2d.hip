@@ -823,6 +823,7 @@ void launch_step2d(const Dev& d, hipStream_t s, const Tlev& t, const double* w1,
       hipLaunchKernelGGL(k_s2d_edges, dim3(ph == 2 ? 1 : (4 * L + 255) / 256), dim3(ph == 2 ? 64 : 256), 0, s, d, c, ph);
     }
   }
+  launch_river_s2d(d, s, t.knew);   // step2d_FB.F:531-554
   if (t.iif == t.nfast) {
     hipLaunchKernelGGL(k_s2d_last, grid_of(RB), dim3(kBX, kBY), 0, s, d, RB, t.knew);
     launch_set_depth(d, s, t);

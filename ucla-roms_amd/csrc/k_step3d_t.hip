@@ -29,8 +29,12 @@ __global__ void __launch_bounds__(256) k_step3d_t_h(Dev d, Range R, int nnew, in
     __syncthreads();
     if (!act) continue;
     double* Tn = F.t + (long)(nnew - 1) * b.n3 + tb;
-    const double FX0 = tracer_fx(b, a, i, j, true), FX1 = tracer_fx(b, a, i + 1, j, true);
-    const double FE0 = tracer_fe(b, a, i, j, true), FE1 = tracer_fe(b, a, i, j + 1, true);
+    double FX0 = tracer_fx(b, a, i, j, true), FX1 = tracer_fx(b, a, i + 1, j, true);
+    double FE0 = tracer_fe(b, a, i, j, true), FE1 = tracer_fe(b, a, i, j + 1, true);
+    if (d.p.nriv > 0) {   // river inflow faces (compute_horiz_tracer_fluxes.h:217-246)
+      river_tracer_flux(d, 0, i, j, k, itrc, FX0); river_tracer_flux(d, 0, i + 1, j, k, itrc, FX1);
+      river_tracer_flux(d, 1, i, j, k, itrc, FE0); river_tracer_flux(d, 1, i, j + 1, k, itrc, FE1);
+    }
     Tn[o] = Tn[o] - d.p.dt * F.pm[ij] * F.pn[ij] * (FX1 - FX0 + FE1 - FE0);
   }
 }

@@ -42,6 +42,7 @@ struct Params {
   int chain;      // 1: chained 4-lane set_HUV1 (k_chain.h; ROMS_GPU_CHAIN=0 disables)
   int seg_order;  // block order of the segment solvers (seg_tile; ROMS_GPU_SEG_ORDER)
   int npip;       // pipe_frc.F: number of pipes (0: pipe_source off)
+  int nriv, nrivf;  // river_frc.F: number of rivers (0: river_source off), river faces
   int curvgrid;   // CURVGRID && UV_ADV: curvature terms (compute_horiz_rhs_uv_terms.h:8-11)
   int obc;        // open edges: 1 W, 2 E, 4 S, 8 N (Flather / Orlanski + *_FRC_BRY)
   double ubind;   // OBC binding velocity
@@ -79,6 +80,11 @@ struct Fields {
   // pipe_frc.F: pipe_idx (0: none), pipe_flx, pipe_prf(npip,N), pipe_trc(npip,NT)
   int* pipe_idx;
   double *pipe_flx, *pipe_prf, *pipe_trc;
+  // river_frc.F: riv_uflx/riv_vflx (10*iriver + signed fraction on river
+  // faces), riv_vol(nriv), riv_trc(nriv,NT); riv_face: (dir, i, j) of every
+  // face with |riv_flx| > 1e-3, three ints per face (Params::nrivf of them)
+  double *riv_uflx, *riv_vflx, *riv_vol, *riv_trc;
+  int* riv_face;
   // boundary.F open-boundary data, [0] west, [1] east (index j, 0:Mm+1),
   // [2] south, [3] north (index i, 0:Lm+1); u, v (.,N); t (.,N,NT)
   double *bzeta[4], *bubar[4], *bvbar[4], *bu[4], *bv[4], *bt[4];
@@ -241,6 +247,10 @@ void launch_step3d_uv2(const Dev& d, hipStream_t s, const Tlev& t);
 void launch_step3d_t(const Dev& d, hipStream_t s, const Tlev& t);
 void launch_t3dmix(const Dev& d, hipStream_t s, const Tlev& t);
 void launch_u3dbc(const Dev& d, hipStream_t s, const Tlev& t);
+// river_frc.F hooks (k_river.hip): ubar/vbar(knew) and DU/DV_avg1 at river
+// faces after each fast step; u,v(nnew) at river faces (pred: predictor ranges)
+void launch_river_s2d(const Dev& d, hipStream_t s, int knew);
+void launch_river_uv(const Dev& d, hipStream_t s, int nnew, int pred);
 void launch_v3dbc(const Dev& d, hipStream_t s, const Tlev& t);
 void launch_t3dbc(const Dev& d, hipStream_t s, const Tlev& t, int itrc);
 // out (device, 6 doubles): avzeta, KE, KE2b sums, Cu_adv, Cu_w, blow-up flag

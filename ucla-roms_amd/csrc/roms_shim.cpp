@@ -220,6 +220,7 @@ void free_all() {
   for (double* p : g.scratch) (void)hipFree(p);
   g.scratch.clear();
   if (g.d.f.pipe_idx) { (void)hipFree(g.d.f.pipe_idx); g.d.f.pipe_idx = nullptr; }
+  if (g.d.f.riv_face) { (void)hipFree(g.d.f.riv_face); g.d.f.riv_face = nullptr; }
   if (g.h_diag) { (void)hipHostFree(g.h_diag); g.h_diag = nullptr; }
   if (g.d_diag) { (void)hipFree(g.d_diag); g.d_diag = nullptr; }
   if (g.s) { (void)hipStreamDestroy(g.s); g.s = nullptr; }
@@ -614,6 +615,75 @@ int roms_gpu_set_pipe_frc(int npip, const int* pipe_idx, const double* pipe_flx,
   return 0;
 }
 
+int roms_gpu_set_river_frc(int nriv, const double* riv_uflx, const double* riv_vflx, const double* riv_vol,
+                           const double* riv_trc) {
+  REQUIRE_INIT();
+  const Bounds& b = g.d.b;
+  Fields& F = g.d.f;
+  if (nriv < 0 || nriv > 4096 || (nriv > 0 && (!riv_vol || !riv_trc)) || (!riv_uflx) != (!riv_vflx)) {
+    g.err = "roms_gpu_set_river_frc: bad argument";
+    return -1;
+  }
+  CHECK_HIP(hipStreamSynchronize(g.s));
+  auto drop_graphs = [&]() {   // captured graphs hold the old Params / pointers
+    for (auto& kv : g.graphs) (void)hipGraphExecDestroy(kv.second);
+    g.graphs.clear();
+  };
+  if (nriv == 0) {
+    if (g.d.p.nriv) drop_graphs();
+    g.d.p.nriv = 0;
+    return 0;
+  }
+  if (!riv_uflx && !F.riv_uflx) { g.err = "roms_gpu_set_river_frc: river faces never set"; return -1; }
+  // faces of calc_river_flux: |riv_flx| > 1e-3 (step2d_FB.F:534), river index nint(riv_flx/10)
+  std::vector<int> faces;
+  if (riv_uflx) {
+    for (int dir = 0; dir < 2; dir++) {
+      const double* a = dir == 0 ? riv_uflx : riv_vflx;
+      for (int j = -1; j <= b.Mm + 2; j++)
+        for (int i = -1; i <= b.Lm + 2; i++) {
+          const double v = a[(i + 1) + (long)(j + 1) * b.nx2];
+          if (!(std::fabs(v) > 1e-3)) continue;
+          const long ir = std::lround(v / 10);
+          if (ir < 1 || ir > nriv) { g.err = "roms_gpu_set_river_frc: river index nint(riv_flx/10) out of 1..nriv"; return -1; }
+          faces.push_back(dir); faces.push_back(i); faces.push_back(j);
+        }
+    }
+  }
+  auto release = [&](double*& p) {
+    if (!p) return;
+    for (size_t k = 0; k < g.scratch.size(); k++)
+      if (g.scratch[k] == p) { g.scratch.erase(g.scratch.begin() + (long)k); break; }
+    (void)hipFree(p);
+    p = nullptr;
+  };
+  auto scratch = [&](double*& p, long n) -> int {
+    CHECK_HIP(hipMalloc(&p, (size_t)n * sizeof(double)));
+    g.scratch.push_back(p);
+    return 0;
+  };
+  if (nriv != g.d.p.nriv || !F.riv_vol) {
+    drop_graphs();
+    release(F.riv_vol);
+    release(F.riv_trc);
+    if (scratch(F.riv_vol, nriv) || scratch(F.riv_trc, (long)nriv * b.NT)) return -2;
+  }
+  if (riv_uflx) {
+    drop_graphs();
+    if (!F.riv_uflx && (scratch(F.riv_uflx, b.n2) || scratch(F.riv_vflx, b.n2))) return -2;
+    if (F.riv_face) { (void)hipFree(F.riv_face); F.riv_face = nullptr; }
+    CHECK_HIP(hipMalloc(&F.riv_face, (faces.size() ? faces.size() : 1) * sizeof(int)));
+    if (!faces.empty()) CHECK_HIP(hipMemcpy(F.riv_face, faces.data(), faces.size() * sizeof(int), hipMemcpyHostToDevice));
+    CHECK_HIP(hipMemcpy(F.riv_uflx, riv_uflx, (size_t)b.n2 * sizeof(double), hipMemcpyHostToDevice));
+    CHECK_HIP(hipMemcpy(F.riv_vflx, riv_vflx, (size_t)b.n2 * sizeof(double), hipMemcpyHostToDevice));
+    g.d.p.nrivf = (int)(faces.size() / 3);
+  }
+  CHECK_HIP(hipMemcpy(F.riv_vol, riv_vol, (size_t)nriv * sizeof(double), hipMemcpyHostToDevice));
+  CHECK_HIP(hipMemcpy(F.riv_trc, riv_trc, (size_t)nriv * b.NT * sizeof(double), hipMemcpyHostToDevice));
+  g.d.p.nriv = nriv;
+  return 0;
+}
+
 int roms_gpu_step(roms_tlev* t) {
   REQUIRE_INIT();
   t->iic = t->iic + 1;
@@ -676,8 +746,10 @@ static int init_case_impl(const roms_case* c, int np_xi, int np_eta, void* comm,
   D.inode = rank - D.jnode * np_xi;
   rank_extent(c->LLm, np_xi, D.inode, D.Lm, D.iSW_corn);
   rank_extent(c->MMm, np_eta, D.jnode, D.Mm, D.jSW_corn);
-  if (c->case_id < ROMS_CASE_FILAMENT || c->case_id > ROMS_CASE_PIPES) { g.err = "roms_gpu_init_case: unknown case"; return -1; }
-  const bool fil = c->case_id == ROMS_CASE_FILAMENT, pipes = c->case_id == ROMS_CASE_PIPES;
+  if (c->case_id < ROMS_CASE_FILAMENT || c->case_id > ROMS_CASE_RIVERS) { g.err = "roms_gpu_init_case: unknown case"; return -1; }
+  const bool fil = c->case_id == ROMS_CASE_FILAMENT;
+  // Rivers_ana shares Pipes_ana's physics and benchmark.in coefficients
+  const bool pipes = c->case_id == ROMS_CASE_PIPES || c->case_id == ROMS_CASE_RIVERS;
   D.ew_periodic = D.ns_periodic = fil ? 1 : 0;
   if (!D.ew_periodic) { D.west_exchng = D.inode > 0; D.east_exchng = D.inode < np_xi - 1; }
   if (!D.ns_periodic) { D.south_exchng = D.jnode > 0; D.north_exchng = D.jnode < np_eta - 1; }
@@ -733,6 +805,10 @@ static int init_case_impl(const roms_case* c, int np_xi, int np_eta, void* comm,
   }
   if (H.npip > 0) {
     r = roms_gpu_set_pipe_frc(H.npip, H.pipe_idx.data(), H.pipe_flx.data(), H.pipe_prf.data(), H.pipe_trc.data());
+    if (r) return r;
+  }
+  if (H.nriv > 0) {
+    r = roms_gpu_set_river_frc(H.nriv, H.riv_uflx.data(), H.riv_vflx.data(), H.riv_vol.data(), H.riv_trc.data());
     if (r) return r;
   }
   if (comm != nullptr) {

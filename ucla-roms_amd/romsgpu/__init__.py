@@ -27,7 +27,7 @@ FIELDS = ["h", "hinv", "f", "fomn", "pm", "pn", "dm_r", "dn_r", "dm_u", "dn_u", 
          ["%s_%s" % (v, e) for v in ("zeta", "ubar", "vbar", "u", "v", "t") for e in ("west", "east", "south", "north")] + \
          ["dndx", "dmde", "ptide"]
 FIELD_ID = {n: i for i, n in enumerate(FIELDS)}
-CASE_FILAMENT, CASE_BASIN, CASE_PIPES = 0, 1, 2
+CASE_FILAMENT, CASE_BASIN, CASE_PIPES, CASE_RIVERS = 0, 1, 2, 3
 # LMD switch bits (ROMS_LMD_* of include/roms_gpu.h)
 LMD_MIXING, LMD_KPP, LMD_BKPP, LMD_RIMIX, LMD_CONVEC, LMD_NONLOCAL = 1, 2, 4, 8, 16, 32
 LMD_ALL = 63       # tests/Pipes_ana/cppdefs.opt
@@ -107,6 +107,8 @@ def load_library(path=LIB_PATH):
     L.roms_gpu_lmd_vmix.argtypes = [ctypes.c_int, P(Tlev)]
     L.roms_gpu_set_pipe_frc.argtypes = [ctypes.c_int, P(ctypes.c_int), P(ctypes.c_double), P(ctypes.c_double),
                                         P(ctypes.c_double)]
+    L.roms_gpu_set_river_frc.argtypes = [ctypes.c_int, P(ctypes.c_double), P(ctypes.c_double), P(ctypes.c_double),
+                                         P(ctypes.c_double)]
     L.roms_gpu_diag.argtypes = [P(Tlev), P(ctypes.c_double)]
     L.roms_gpu_time_steps.argtypes = [P(Tlev), ctypes.c_int, P(ctypes.c_double)]
     L.roms_gpu_stream.restype = ctypes.c_void_p
@@ -322,6 +324,24 @@ class Model:
         self._chk(self.L.roms_gpu_set_pipe_frc(npip, idx.ctypes.data_as(P(ctypes.c_int)), flx.ctypes.data_as(P(ctypes.c_double)),
                                                prf.ctypes.data_as(P(ctypes.c_double)), trc.ctypes.data_as(P(ctypes.c_double))),
                   "set_pipe_frc")
+
+    def set_river_frc(self, riv_vol, riv_trc, riv_uflx=None, riv_vflx=None):
+        """river_frc.F:set_river_frc: riv_vol (nriv,), riv_trc (nriv, NT) for the
+        current time; riv_uflx/riv_vflx on the (Mm+4, Lm+4) grid as
+        calc_river_flux leaves them (None: keep the faces already set)."""
+        vol = np.ascontiguousarray(riv_vol, dtype=np.float64).ravel()
+        nriv = vol.shape[0]
+        trc = np.asfortranarray(np.asarray(riv_trc, dtype=np.float64).reshape(nriv, -1)).ravel(order="F")
+        P = ctypes.POINTER
+        D = P(ctypes.c_double)
+        if riv_uflx is None:
+            uf = vf = None
+        else:
+            uf = np.ascontiguousarray(riv_uflx, dtype=np.float64).ravel()
+            vf = np.ascontiguousarray(riv_vflx, dtype=np.float64).ravel()
+        self._chk(self.L.roms_gpu_set_river_frc(nriv, uf.ctypes.data_as(D) if uf is not None else None,
+                                                vf.ctypes.data_as(D) if vf is not None else None,
+                                                vol.ctypes.data_as(D), trc.ctypes.data_as(D)), "set_river_frc")
 
     def _r(self, fn):
         self._chk(getattr(self.L, "roms_gpu_" + fn)(ctypes.byref(self.t)), fn)
