@@ -74,6 +74,7 @@ __device__ __forceinline__ uint3 seg_tile(int ord) {
 // LDS exchange area of one block: 6 end-relation values per (segment, column)
 struct SegXchg {
   double v[6][kSegMaxS][kSegCW];
+  double uv[kSegMaxS > 8 ? 2 : 1][kSegMaxS][kSegCW];   // U_t, V_t of the reduced system (kSegMaxS > 8)
 };
 
 template <int KR>
@@ -110,8 +111,13 @@ struct SegTri {
     X.v[0][s][l] = y; X.v[1][s][l] = al; X.v[2][s][l] = be;
     X.v[3][s][l] = yl; X.v[4][s][l] = all; X.v[5][s][l] = bel;
     __syncthreads();
-    // F_t = U_t + V_t F_{t+1} (first values), L_t = P_t + Q_t F_{t+1} (last values)
-    double U[kSegMaxS], V[kSegMaxS];
+    // F_t = U_t + V_t F_{t+1} (first values), L_t = P_t + Q_t F_{t+1} (last
+    // values).  Every lane of a column runs the same forward recurrence.  Up
+    // to 8 segments U_t, V_t stay in registers; with more, the lane of
+    // segment t leaves them in LDS (S-long register arrays in every lane
+    // would cost 4 S VGPRs) and the backward recurrence reads them back.
+    constexpr bool kUVLds = kSegMaxS > 8;
+    double U[kUVLds ? 1 : kSegMaxS], V[kUVLds ? 1 : kSegMaxS];
     double Pp = 0.0, Qp = 0.0, Ps = 0.0, Qs = 0.0;
 #pragma unroll
     for (int t = 0; t < kSegMaxS; t++) {
@@ -119,22 +125,29 @@ struct SegTri {
         const double yf = X.v[0][t][l], af = X.v[1][t][l], bf = X.v[2][t][l];
         const double yL = X.v[3][t][l], aL = X.v[4][t][l], bL = X.v[5][t][l];
         const double rden = 1.0 / (1.0 - af * Qp);
-        U[t] = (yf + af * Pp) * rden;
-        V[t] = bf * rden;
-        const double Pn = yL + aL * Pp + aL * Qp * U[t];
-        Qp = aL * Qp * V[t] + bL;
+        const double Ut = (yf + af * Pp) * rden;
+        const double Vt = bf * rden;
+        if constexpr (kUVLds) {
+          if (t == s) { X.uv[0][t][l] = Ut; X.uv[1][t][l] = Vt; }
+        } else {
+          U[t] = Ut; V[t] = Vt;
+        }
+        const double Pn = yL + aL * Pp + aL * Qp * Ut;
+        Qp = aL * Qp * Vt + bL;
         Pp = Pn;
         if (t == s - 1) { Ps = Pp; Qs = Qp; }
       }
     }
+    if constexpr (kUVLds) __syncthreads();
     double Fn = 0.0;  // F_{t+1}
     xL = 0.0; xR = 0.0;
 #pragma unroll
     for (int t = kSegMaxS - 1; t >= 0; t--) {
-      if (t < S) {
+      if (t < S && (!kUVLds || t >= s - 1)) {
         if (t == s) xR = Fn;
         if (t == s - 1) xL = Ps + Qs * Fn;
-        Fn = U[t] + V[t] * Fn;
+        if constexpr (kUVLds) Fn = X.uv[0][t][l] + X.uv[1][t][l] * Fn;
+        else Fn = U[t] + V[t] * Fn;
       }
     }
   }

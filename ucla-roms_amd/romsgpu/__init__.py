@@ -15,7 +15,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _PKG = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(_PKG, "libromsgpu.so")
+LIB_PATH = os.environ.get("ROMS_GPU_LIB") or os.path.join(_PKG, "libromsgpu.so")   # ROMS_GPU_LIB: A/B builds only
 MAX_FAST = 288
 
 FIELDS = ["h", "hinv", "f", "fomn", "pm", "pn", "dm_r", "dn_r", "dm_u", "dn_u", "dm_v", "dn_v", "dm_p", "dn_p",
