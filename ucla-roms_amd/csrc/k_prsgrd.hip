@@ -102,8 +102,19 @@ __global__ void __launch_bounds__(256) k_prsgrd_P(Dev d, Range R, int split, int
 // dZ, dR (with the SPLIT_EOS compressibility term), once each, in LDS. ----
 constexpr int kPXW = kBX + 2, kPXN = kPXW * kBY;          // u-points m = i0-1 .. i0+64, tile rows
 constexpr int kPYH = kBY + 2, kPYN = kBX * kPYH;          // v-points m = j0-1 .. j0+4, tile columns
+// Raw window of the level: z_r, rho1 (rho) and qp1 over (i0-2..i0+64) x
+// (j0-2..j0+4), each value loaded from HBM once per block and coalesced; the
+// elementary differences, the harmonic means' split terms and the cell's own
+// z_r and in-situ density are then formed from LDS, so a block issues about
+// a third of the vector-memory instructions of forming every difference
+// from two global loads (measured: the per-cell kernel was bound by the
+// vector-memory instruction rate, not by HBM bytes).
+constexpr int kPWW = kBX + 3, kPWH = kBY + 3, kPWN = kPWW * kPWH;   // raw window (i0-2.., j0-2..)
+constexpr int kPWQ = (kPWN + kBX * kBY - 1) / (kBX * kBY);
+constexpr int kPQ = (kPXN + kPYN + kBX * kBY - 1) / (kBX * kBY);
 __global__ void __launch_bounds__(256) k_prsgrd_uv(Dev d, Range R, int split, int imin, int imax, int jmin, int jmax) {
   const uint3 bI = xcd_tile();
+  __shared__ double sZ[kPWN], sR[kPWN], sQ[kPWN];
   __shared__ double sFCx[kPXN], sRx[kPXN], sFCy[kPYN], sRy[kPYN];
   __shared__ double sdZx[kPXN], sdRx[kPXN], sdZy[kPYN], sdRy[kPYN];
   const Bounds& b = d.b;
@@ -111,55 +122,102 @@ __global__ void __launch_bounds__(256) k_prsgrd_uv(Dev d, Range R, int split, in
   const double g = d.p.g, rho0 = d.p.rho0, qp2 = d.p.qp2;
   const double OneFifth = 0.2, OneTwelfth = 1.0 / 12.0;
   const double HalfGRho = 0.5 * (g / rho0);
-  const double* rho = split ? F.rhos : F.rho;
+  const double* R1 = split ? F.rho1 : F.rho;
   const int k = 1 + (int)bI.z;
   const long kk = (long)(k - 1) * b.n2, sj = b.nx2;
   const int i0 = R.i0 + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * kBY;
   const int tid = threadIdx.x + kBX * threadIdx.y;
-  // elementary differences at clamped u-points (xi) and v-points (eta)
-  for (int q = tid; q < kPXN + kPYN; q += kBX * kBY) {
-    if (q < kPXN) {
-      const int j = j0 + q / kPXW;
-      int m = i0 - 1 + q % kPXW;
-      if (j > b.Mm + 1 || m > b.Lm + 2) { sFCx[q] = sRx[q] = 0.0; continue; }
-      m = iclamp(m, imin, imax);
-      const long om = IJ(b, m, j) + kk;
-      const double um = F.umask[IJ(b, m, j)];
-      sFCx[q] = (F.z_r[om] - F.z_r[om - 1]) * um;
-      if (split) {
-        const double dpth = -0.5 * (F.z_r[om] + F.z_r[om - 1]);
-        sRx[q] = (F.rho1[om] - F.rho1[om - 1] + (F.qp1[om] - F.qp1[om - 1]) * dpth * (1.0 - qp2 * dpth)) * um;
-      } else {
-        sRx[q] = (F.rho[om] - F.rho[om - 1]) * um;
-      }
-    } else {
-      const int qq = q - kPXN;
-      const int i = i0 + qq % kBX;
-      int m = j0 - 1 + qq / kBX;
-      if (i > b.Lm + 1 || m > b.Mm + 2) { sFCy[qq] = sRy[qq] = 0.0; continue; }
-      m = iclamp(m, jmin, jmax);
-      const long om = IJ(b, i, m) + kk;
-      const double vm = F.vmask[IJ(b, i, m)];
-      sFCy[qq] = (F.z_r[om] - F.z_r[om - sj]) * vm;
-      if (split) {
-        const double dpth = -0.5 * (F.z_r[om] + F.z_r[om - sj]);
-        sRy[qq] = (F.rho1[om] - F.rho1[om - sj] + (F.qp1[om] - F.qp1[om - sj]) * dpth * (1.0 - qp2 * dpth)) * vm;
-      } else {
-        sRy[qq] = (F.rho[om] - F.rho[om - sj]) * vm;
+  auto W = [&](int i, int j) { return (i - (i0 - 2)) + (j - (j0 - 2)) * kPWW; };
+  // ---- loads, all issued before the first barrier ----
+  double wz[kPWQ], wr[kPWQ], wq[kPWQ];
+#pragma unroll
+  for (int m = 0; m < kPWQ; m++) {
+    const int q = tid + m * kBX * kBY;
+    wz[m] = wr[m] = wq[m] = 0.0;
+    if (q < kPWN) {
+      const int i = i0 - 2 + q % kPWW, j = j0 - 2 + q / kPWW;
+      if (i <= b.Lm + 2 && j <= b.Mm + 2) {
+        const long o = IJ(b, i, j) + kk;
+        wz[m] = F.z_r[o];
+        wr[m] = R1[o];
+        if (split) wq[m] = F.qp1[o];
       }
     }
   }
+  double mk[kPQ];   // u-/v-mask of the entry's clamped point
+  int e1[kPQ], e0[kPQ];
+  bool eon[kPQ];
+#pragma unroll
+  for (int m = 0; m < kPQ; m++) {
+    const int q = tid + m * kBX * kBY;
+    mk[m] = 0.0; e1[m] = e0[m] = 0; eon[m] = false;
+    if (q < kPXN) {
+      const int j = j0 + q / kPXW;
+      int mm = i0 - 1 + q % kPXW;
+      if (!(j > b.Mm + 1 || mm > b.Lm + 2)) {
+        mm = iclamp(mm, imin, imax);
+        eon[m] = true; e1[m] = W(mm, j); e0[m] = W(mm - 1, j);
+        mk[m] = F.umask[IJ(b, mm, j)];
+      }
+    } else if (q < kPXN + kPYN) {
+      const int qq = q - kPXN;
+      const int i = i0 + qq % kBX;
+      int mm = j0 - 1 + qq / kBX;
+      if (!(i > b.Lm + 1 || mm > b.Mm + 2)) {
+        mm = iclamp(mm, jmin, jmax);
+        eon[m] = true; e1[m] = W(i, mm); e0[m] = W(i, mm - 1);
+        mk[m] = F.vmask[IJ(b, i, mm)];
+      }
+    }
+  }
+  const int i = i0 + (int)threadIdx.x, j = j0 + (int)threadIdx.y;
+  const bool inr = i <= R.i1 && j <= R.j1;
+  const long ij = IJ(b, inr ? i : R.i0, inr ? j : R.j0), o = ij + kk;
+  const bool du = inr && i >= b.istrU && i <= b.iend && j >= b.jstr && j <= b.jend;
+  const bool dv = inr && i >= b.istr && i <= b.iend && j >= b.jstrV && j <= b.jend;
+  double hz0 = 0, hzu = 0, hzv = 0, P0 = 0, Pu = 0, Pv = 0, dnu = 0, dmv = 0;
+  if (du || dv) { hz0 = F.Hz[o]; P0 = F.P[o]; }
+  if (du) { hzu = F.Hz[o - 1]; Pu = F.P[o - 1]; dnu = F.dn_u[ij]; }
+  if (dv) { hzv = F.Hz[o - sj]; Pv = F.P[o - sj]; dmv = F.dm_v[ij]; }
+#pragma unroll
+  for (int m = 0; m < kPWQ; m++) {
+    const int q = tid + m * kBX * kBY;
+    if (q < kPWN) { sZ[q] = wz[m]; sR[q] = wr[m]; sQ[q] = wq[m]; }
+  }
   __syncthreads();
-  // harmonic averages at rho points p = i-1, i (xi) and j-1, j (eta)
-  for (int q = tid; q < kPXN + kPYN; q += kBX * kBY) {
+  // ---- elementary differences at clamped u-points (xi) and v-points (eta) ----
+#pragma unroll
+  for (int m = 0; m < kPQ; m++) {
+    const int q = tid + m * kBX * kBY;
+    if (q >= kPXN + kPYN) continue;
+    double fc = 0.0, rx = 0.0;
+    if (eon[m]) {
+      const double z1 = sZ[e1[m]], z0 = sZ[e0[m]];
+      fc = (z1 - z0) * mk[m];
+      if (split) {
+        const double dpth = -0.5 * (z1 + z0);
+        rx = (sR[e1[m]] - sR[e0[m]] + (sQ[e1[m]] - sQ[e0[m]]) * dpth * (1.0 - qp2 * dpth)) * mk[m];
+      } else {
+        rx = (sR[e1[m]] - sR[e0[m]]) * mk[m];
+      }
+    }
+    if (q < kPXN) { sFCx[q] = fc; sRx[q] = rx; }
+    else { sFCy[q - kPXN] = fc; sRy[q - kPXN] = rx; }
+  }
+  __syncthreads();
+  // ---- harmonic averages at rho points p = i-1, i (xi) and j-1, j (eta) ----
+#pragma unroll
+  for (int m = 0; m < kPQ; m++) {
+    const int q = tid + m * kBX * kBY;
+    if (q >= kPXN + kPYN) continue;
     if (q < kPXN) {
       const int li = q % kPXW;
       if (li == kPXW - 1) continue;
-      const int j = j0 + q / kPXW, p = i0 - 1 + li;
+      const int jj = j0 + q / kPXW, p = i0 - 1 + li;
       double dz = harm(sFCx[q], sFCx[q + 1]), dr = harm(sRx[q], sRx[q + 1]);
-      if (split && j <= b.Mm + 1 && p <= b.Lm + 1) {
-        const long om = IJ(b, p, j) + kk;
-        dr = dr - F.qp1[om] * dz * (1.0 + 2.0 * qp2 * F.z_r[om]);
+      if (split && jj <= b.Mm + 1 && p <= b.Lm + 1) {
+        const int w = W(p, jj);
+        dr = dr - sQ[w] * dz * (1.0 + 2.0 * qp2 * sZ[w]);
       }
       sdZx[q] = dz;
       sdRx[q] = dr;
@@ -167,37 +225,45 @@ __global__ void __launch_bounds__(256) k_prsgrd_uv(Dev d, Range R, int split, in
       const int qq = q - kPXN;
       const int lj = qq / kBX;
       if (lj == kPYH - 1) continue;
-      const int i = i0 + qq % kBX, p = j0 - 1 + lj;
+      const int ii = i0 + qq % kBX, p = j0 - 1 + lj;
       double dz = harm(sFCy[qq], sFCy[qq + kBX]), dr = harm(sRy[qq], sRy[qq + kBX]);
-      if (split && i <= b.Lm + 1 && p <= b.Mm + 1) {
-        const long om = IJ(b, i, p) + kk;
-        dr = dr - F.qp1[om] * dz * (1.0 + 2.0 * qp2 * F.z_r[om]);
+      if (split && ii <= b.Lm + 1 && p <= b.Mm + 1) {
+        const int w = W(ii, p);
+        dr = dr - sQ[w] * dz * (1.0 + 2.0 * qp2 * sZ[w]);
       }
       sdZy[qq] = dz;
       sdRy[qq] = dr;
     }
   }
   __syncthreads();
-  const int i = i0 + (int)threadIdx.x, j = j0 + (int)threadIdx.y;
-  if (i > R.i1 || j > R.j1) return;
-  const long ij = IJ(b, i, j), o = ij + kk;
-  if (i >= b.istrU && i <= b.iend && j >= b.jstr && j <= b.jend) {
+  // in-situ density (k_prsgrd_P's rhos: rho1 + qp1*dpth*(1 - qp2*dpth), dpth = -z_r)
+  auto rhov = [&](int w) {
+    if (split) {
+      const double dpth = -sZ[w];
+      return sR[w] + sQ[w] * dpth * (1.0 - qp2 * dpth);
+    }
+    return sR[w];
+  };
+  const int wc = W(inr ? i : i0, inr ? j : j0);
+  if (du) {
     const int q = threadIdx.x + threadIdx.y * kPXW;   // p = i-1 ; q+1: p = i
     const double dZ0 = sdZx[q], dZ1 = sdZx[q + 1], dR0 = sdRx[q], dR1 = sdRx[q + 1];
-    F.ru[o] = 0.5 * (F.Hz[o] + F.Hz[o - 1]) * F.dn_u[ij] *
-              (F.P[o - 1] - F.P[o] -
-               HalfGRho * ((rho[o] + rho[o - 1]) * (F.z_r[o] - F.z_r[o - 1]) -
-                           OneFifth * ((dR1 - dR0) * (F.z_r[o] - F.z_r[o - 1] - OneTwelfth * (dZ1 + dZ0)) -
-                                       (dZ1 - dZ0) * (rho[o] - rho[o - 1] - OneTwelfth * (dR1 + dR0)))));
+    const double z0 = sZ[wc], zu = sZ[wc - 1], r0 = rhov(wc), ru_ = rhov(wc - 1);
+    F.ru[o] = 0.5 * (hz0 + hzu) * dnu *
+              (Pu - P0 -
+               HalfGRho * ((r0 + ru_) * (z0 - zu) -
+                           OneFifth * ((dR1 - dR0) * (z0 - zu - OneTwelfth * (dZ1 + dZ0)) -
+                                       (dZ1 - dZ0) * (r0 - ru_ - OneTwelfth * (dR1 + dR0)))));
   }
-  if (i >= b.istr && i <= b.iend && j >= b.jstrV && j <= b.jend) {
+  if (dv) {
     const int q = threadIdx.x + threadIdx.y * kBX;    // p = j-1 ; q+kBX: p = j
     const double dZ0 = sdZy[q], dZ1 = sdZy[q + kBX], dR0 = sdRy[q], dR1 = sdRy[q + kBX];
-    F.rv[o] = 0.5 * (F.Hz[o] + F.Hz[o - sj]) * F.dm_v[ij] *
-              (F.P[o - sj] - F.P[o] -
-               HalfGRho * ((rho[o] + rho[o - sj]) * (F.z_r[o] - F.z_r[o - sj]) -
-                           OneFifth * ((dR1 - dR0) * (F.z_r[o] - F.z_r[o - sj] - OneTwelfth * (dZ1 + dZ0)) -
-                                       (dZ1 - dZ0) * (rho[o] - rho[o - sj] - OneTwelfth * (dR1 + dR0)))));
+    const double z0 = sZ[wc], zv = sZ[wc - kPWW], r0 = rhov(wc), rv_ = rhov(wc - kPWW);
+    F.rv[o] = 0.5 * (hz0 + hzv) * dmv *
+              (Pv - P0 -
+               HalfGRho * ((r0 + rv_) * (z0 - zv) -
+                           OneFifth * ((dR1 - dR0) * (z0 - zv - OneTwelfth * (dZ1 + dZ0)) -
+                                       (dZ1 - dZ0) * (r0 - rv_ - OneTwelfth * (dR1 + dR0)))));
   }
 }
 
