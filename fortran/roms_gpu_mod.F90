@@ -32,6 +32,7 @@ module roms_gpu_mod
     integer(c_int) :: curvgrid                   ! CURVGRID
     integer(c_int) :: uv_adv, uv_cor             ! UV_ADV, UV_COR
     integer(c_int) :: pot_tides                  ! TIDES pot_tides
+    integer(c_int) :: bulk_frc                   ! BULK_FRC
   end type
 
   type, bind(c) :: roms_tlev
@@ -49,17 +50,18 @@ module roms_gpu_mod
     integer(c_int) :: island
     integer(c_int) :: curvgrid
     integer(c_int) :: uv_adv, uv_cor
+    integer(c_int) :: bulk_frc
   end type
 
   ! LMD switch bits of lmd_mixing (ROMS_LMD_*)
   integer(c_int), parameter :: ROMS_LMD_MIXING = 1, ROMS_LMD_KPP = 2, ROMS_LMD_BKPP = 4, ROMS_LMD_RIMIX = 8, &
                                ROMS_LMD_CONVEC = 16, ROMS_LMD_NONLOCAL = 32
-  integer(c_int), parameter :: ROMS_GPU_ABI = 6   ! ROMS_GPU_ABI_VERSION, include/roms_gpu.h
+  integer(c_int), parameter :: ROMS_GPU_ABI = 7   ! ROMS_GPU_ABI_VERSION, include/roms_gpu.h
 
   ! field ids (enum roms_field) used by the drivers below
   integer(c_int), parameter :: ROMS_ALL = -1
   integer(c_int), parameter :: ROMS_zeta = 22, ROMS_ubar = 23, ROMS_vbar = 24, ROMS_u = 25, ROMS_v = 26, &
-                               ROMS_t = 27, ROMS_Hz = 32, ROMS_z_r = 35, ROMS_NFIELDS = 96
+                               ROMS_t = 27, ROMS_Hz = 32, ROMS_z_r = 35, ROMS_NFIELDS = 105
 
   interface
     integer(c_int) function roms_gpu_abi_version() bind(c)

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define ROMS_GPU_ABI_VERSION 6
+#define ROMS_GPU_ABI_VERSION 7
 #define ROMS_MAX_FAST 288
 
 /* Subdomain geometry of this rank: param.F / dimensions.F / mpi_setup.F:39-210 */
@@ -83,6 +83,9 @@ typedef struct roms_cfg {
                                     UV_COR (Coriolis, compute_horiz_rhs_uv_terms.h:1-38)              */
   int pot_tides;                 /* TIDES with pot_tides (tides.opt): the surface tidal potential
                                     ptide enters the pressure gradient (prsgrd.F:209-211)             */
+  int bulk_frc;                  /* BULK_FRC: the surface fluxes come from roms_gpu_bulk_flux (COARE,
+                                    bulk_frc.F:143-913) at both set_forces points of the step, and
+                                    lmd_kpp's u* from the rho-point stresses (lmd_kpp.F:173-174)     */
 } roms_cfg;
 
 /* Time-step indices (scalars.F:32-36).  The step entry updates them. */
@@ -124,6 +127,10 @@ enum roms_field {
   ROMS_dndx, ROMS_dmde,
   /* tides.F:26 surface tidal potential [m] (TIDES, pot_tides) */
   ROMS_ptide,
+  /* BULK_FRC inputs at rho points (bulk_frc.F:95-111, surf_flux.F): winds [m/s], air temperature
+     [degC], specific humidity Q [kg/kg], precipitation [cm/day], short-wave (the data read into
+     srflx) and downward long-wave radiation [W/m2]; and the rho-point stresses sustr_r, svstr_r */
+  ROMS_uwnd, ROMS_vwnd, ROMS_tair, ROMS_qair, ROMS_prate, ROMS_swrad, ROMS_lwrad, ROMS_sustr_r, ROMS_svstr_r,
   ROMS_NFIELDS
 };
 
@@ -180,6 +187,14 @@ int roms_gpu_set_pipe_frc(int npip, const int *pipe_idx, const double *pipe_flx,
  * sources off.  Returns 0, or -1 on a bad argument. */
 int roms_gpu_set_river_frc(int nriv, const double *riv_uflx, const double *riv_vflx, const double *riv_vol,
                            const double *riv_trc);
+/* set_bulk_frc -> calc_all_bulk_forces (bulk_frc.F:85-913) on the device:
+ * from the uploaded ROMS_uwnd .. ROMS_lwrad fields and the surface t, u, v at
+ * t->nrhs, sets srflx, stflx(itemp), swflx, sustr_r, svstr_r, sustr and
+ * svstr.  roms_gpu_step calls it itself at both set_forces points when the
+ * library was initialised with bulk_frc; the host only uploads the
+ * time-interpolated atmospheric fields (set_frc_data) before each step.
+ * Returns -4 when the library was initialised without bulk_frc. */
+int roms_gpu_bulk_flux(const roms_tlev *t);
 int roms_gpu_set_depth(const roms_tlev *t);           /* set_depth(tile)  set_depth.F:4    */
 
 /* One whole roms_step (main.F:333-520, forcing held fixed): advances t->iic
@@ -203,6 +218,8 @@ typedef struct roms_case {
   int island;     /* basin only: circular land mask (MASKING)                                   */
   int curvgrid;   /* basin only: non-uniform metrics pm(j), pn(i) and CURVGRID                  */
   int uv_adv, uv_cor;  /* UV_ADV, UV_COR (every reference case defines both: set 1, 1)          */
+  int bulk_frc;   /* basin only: BULK_FRC with an analytic atmosphere (westerly jet, cool humid air)
+                     uploaded as ROMS_uwnd .. ROMS_lwrad; roms_cfg.bulk_frc                         */
 } roms_case;
 /* Builds the analytic grid/ICs on the host (setup_grid1/2, set_scoord,
  * set_weights, ana_init), initialises the device and runs roms_init.        */

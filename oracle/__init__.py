@@ -34,7 +34,8 @@ class OrCfg(ctypes.Structure):
                 ("diag_np_xi", ctypes.c_int), ("diag_np_eta", ctypes.c_int), ("surf_flux", ctypes.c_int),
                 ("obc", ctypes.c_int), ("ubind", ctypes.c_double), ("v_sponge", ctypes.c_double),
                 ("island", ctypes.c_int), ("curvgrid", ctypes.c_int), ("uv_adv", ctypes.c_int),
-                ("uv_cor", ctypes.c_int), ("pot_tides", ctypes.c_int)]
+                ("uv_cor", ctypes.c_int), ("pot_tides", ctypes.c_int),
+                ("bulk_frc", ctypes.c_int)]
 
     def __init__(self, *a, **k):
         super().__init__(*a, **k)
@@ -76,7 +77,7 @@ def lib():
         L.or_destroy.argtypes = [ctypes.c_void_p]
         for fn in ("or_set_HUV", "or_omega", "or_prsgrd", "or_pre_step3d", "or_set_HUV1", "or_step3d_uv1",
                    "or_visc3d", "or_step2d", "or_step3d_uv2", "or_step3d_t", "or_t3dmix", "or_set_depth",
-                   "or_diag", "or_swr_frac"):
+                   "or_diag", "or_swr_frac", "or_bulk_flux"):
             getattr(L, fn).argtypes = [ctypes.c_void_p]
         L.or_rho_eos.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.or_lmd_vmix.argtypes = [ctypes.c_void_p, ctypes.c_int]

@@ -57,6 +57,8 @@ struct or_state {
   double *bry_zeta[4], *bry_ubar[4], *bry_vbar[4], *bry_u[4], *bry_v[4], *bry_t[4];
   /* forcing */
   double *sustr, *svstr, *stflx, *srflx, *swflx;
+  /* BULK_FRC inputs and rho-point stresses (bulk_frc.F, surf_flux.F) */
+  double *uwnd, *vwnd, *tair, *qair, *prate, *swrad, *lwrad, *sustr_r, *svstr_r;
   /* private scratch (A3d(:,1..4), A2d(:,1..)) */
   double *ru, *rv, *P, *rhos3;         /* 3-D scratch */
   double *s2[14];                      /* 2-D scratch */

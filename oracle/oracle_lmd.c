@@ -272,7 +272,10 @@ static void lmd_kpp_tile(or_state *S, int tind) {
       A2(Bosol, i, j) = g * alpha * A2(S->srflx, i, j);
       const double su0 = A2(S->sustr, i, j), su1 = A2(S->sustr, i + 1, j), sv0 = A2(S->svstr, i, j),
                    sv1 = A2(S->svstr, i, j + 1);
-      A2(ustar, i, j) = sqrt(sqrt(0.333333333333 * (su0 * su0 + su1 * su1 + su0 * su1 + sv0 * sv0 + sv1 * sv1 + sv0 * sv1)));
+      if (S->c.bulk_frc)   /* BULK_FRC: rho-point stresses (lmd_kpp.F:173-174) */
+        A2(ustar, i, j) = sqrt(sqrt(A2(S->sustr_r, i, j) * A2(S->sustr_r, i, j) + A2(S->svstr_r, i, j) * A2(S->svstr_r, i, j)));
+      else
+        A2(ustar, i, j) = sqrt(sqrt(0.333333333333 * (su0 * su0 + su1 * su1 + su0 * su1 + sv0 * sv0 + sv1 * sv1 + sv0 * sv1)));
       A2(hbl, i, j) = A2(S->hbls, i, j);
       A2(bbl, i, j) = A2(S->hbbl, i, j);
       kbls[KI(i)] = 0;

@@ -63,6 +63,8 @@ or_state *or_create(const or_cfg *cfg) {
   if (cfg->lmd) or_lmd_alloc(S);
   S->pipe_flx = zalloc(n2); S->pipe_idx = zalloc(n2);
   S->riv_uflx = zalloc(n2); S->riv_vflx = zalloc(n2);
+  S->uwnd = zalloc(n2); S->vwnd = zalloc(n2); S->tair = zalloc(n2); S->qair = zalloc(n2); S->prate = zalloc(n2);
+  S->swrad = zalloc(n2); S->lwrad = zalloc(n2); S->sustr_r = zalloc(n2); S->svstr_r = zalloc(n2);
   S->dndx = zalloc(n2); S->dmde = zalloc(n2); S->ptide = zalloc(n2);
   /* boundary.F:111-129: zeta_west(0:Mm+1), u_west(0:Mm+1,N), t_west(0:Mm+1,N,NT), ... */
   S->nbry[0] = S->nbry[1] = S->Mm + 2;
@@ -634,6 +636,24 @@ void or_ana_init(or_state *S) {
 
 /* set_forces: analytic surface fluxes (analytical.F ana_smflux/srflux/stflux) */
 void or_ana_forces(or_state *S) {
+  if (S->c.case_id == OR_CASE_BASIN && S->c.bulk_frc) {
+    /* BULK_FRC with a synthetic analytic atmosphere (C4 stand-in):
+       westerly jet, air 2-3 degC below the sea surface, humid, light rain */
+    const double pi = 3.14159265358979323;
+    for (int j = -1; j <= S->Mm + 2; j++)
+      for (int i = -1; i <= S->Lm + 2; i++) {
+        const double x = A2(S->xr, i, j), y = A2(S->yr, i, j);
+        A2(S->uwnd, i, j) = 8.0 * sin(pi * y / S->c.sizey);
+        A2(S->vwnd, i, j) = 2.0 * cos(pi * x / S->c.sizex);
+        A2(S->tair, i, j) = 10.0 + 3.0 * cos(2.0 * pi * x / S->c.sizex);
+        A2(S->qair, i, j) = 0.007 + 0.001 * sin(2.0 * pi * y / S->c.sizey);
+        A2(S->prate, i, j) = 0.3;
+        A2(S->swrad, i, j) = 150.0 + 50.0 * sin(pi * y / S->c.sizey);
+        A2(S->lwrad, i, j) = 320.0;
+      }
+    or_bulk_flux(S);
+    return;
+  }
   if (S->c.case_id == OR_CASE_BASIN) {
     const double pi = 3.14159265358979323;
     for (int j = -1; j <= S->Mm + 2; j++)
@@ -762,6 +782,7 @@ int or_step(or_state *S) {
   S->nnew = 3 - S->nstp;
   or_omega(S);
   or_rho_eos(S, S->nrhs);
+  if (S->c.bulk_frc) or_bulk_flux(S);   /* set_forces (main.F:433) */
   if (S->c.lmd) or_lmd_vmix(S, S->nrhs);
   or_prsgrd(S);
   or_step3d_uv1(S);
@@ -799,6 +820,9 @@ void or_set_iif(or_state *S, int iif) { S->iif = iif; }
 double *or_field(or_state *S, const char *name, size_t *count) {
   struct { const char *n; double *p; size_t c; } tab[] = {
       {"riv_uflx", S->riv_uflx, S->n2}, {"riv_vflx", S->riv_vflx, S->n2},
+      {"uwnd", S->uwnd, S->n2}, {"vwnd", S->vwnd, S->n2}, {"tair", S->tair, S->n2}, {"qair", S->qair, S->n2},
+      {"prate", S->prate, S->n2}, {"swrad", S->swrad, S->n2}, {"lwrad", S->lwrad, S->n2},
+      {"sustr_r", S->sustr_r, S->n2}, {"svstr_r", S->svstr_r, S->n2},
       {"zeta", S->zeta, 4 * S->n2}, {"ubar", S->ubar, 4 * S->n2}, {"vbar", S->vbar, 4 * S->n2},
       {"u", S->u, 3 * S->n3}, {"v", S->v, 3 * S->n3}, {"t", S->t, 3 * S->n3 * S->NT},
       {"FlxU", S->FlxU, S->n3}, {"FlxV", S->FlxV, S->n3}, {"We", S->We, S->n3w}, {"Wi", S->Wi, S->n3w},

@@ -52,6 +52,7 @@ typedef struct or_cfg {
   int curvgrid;                  /* CURVGRID (+UV_ADV) curvature terms; basin: non-uniform metrics */
   int uv_adv, uv_cor;            /* UV_ADV, UV_COR */
   int pot_tides;                 /* TIDES pot_tides: ptide in prsgrd (prsgrd.F:209-211) */
+  int bulk_frc;                  /* BULK_FRC (bulk_frc.F); basin: analytic atmosphere (oracle_main.c) */
 } or_cfg;
 
 typedef struct or_state or_state;
@@ -90,6 +91,7 @@ void or_t3dmix(or_state *S);
 void or_set_depth(or_state *S);
 void or_lmd_vmix(or_state *S, int tind);
 void or_swr_frac(or_state *S);
+void or_bulk_flux(or_state *S);   /* calc_all_bulk_forces at nrhs (oracle_bulk.c) */
 void or_diag(or_state *S);
 void or_set_tindex(or_state *S, const int in[6]);
 void or_set_iif(or_state *S, int iif);

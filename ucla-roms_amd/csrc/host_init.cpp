@@ -503,8 +503,24 @@ void build_case(const CaseSpec& cs, HostState& H, double& area, double& volume) 
         for (long q = 0; q < n3w; q++) H.arr[kAkt][q + (long)(it - 1) * n3w] = cs.Akt_bak[it - 1];
     }
     const double piy = 3.14159265358979323;
+    if (cs.bulk_frc) {  // analytic atmosphere for BULK_FRC (oracle_main.c or_ana_forces); the
+                        // device computes the fluxes (k_bulk.hip) at init and in every step
+      for (int id : {kuwnd, kvwnd, ktair, kqair, kprate, kswrad, klwrad}) alloc(id, n2);
+      for (int j = -1; j <= Mm + 2; j++)
+        for (int i = -1; i <= Lm + 2; i++) {
+          const double x = A(kxr, i, j), y = A(kyr, i, j);
+          A(kuwnd, i, j) = 8.0 * std::sin(piy * y / cs.sizey);
+          A(kvwnd, i, j) = 2.0 * std::cos(piy * x / cs.sizex);
+          A(ktair, i, j) = 10.0 + 3.0 * std::cos(2.0 * piy * x / cs.sizex);
+          A(kqair, i, j) = 0.007 + 0.001 * std::sin(2.0 * piy * y / cs.sizey);
+          A(kprate, i, j) = 0.3;
+          A(kswrad, i, j) = 150.0 + 50.0 * std::sin(piy * y / cs.sizey);
+          A(klwrad, i, j) = 320.0;
+        }
+    }
     for (int j = -1; j <= Mm + 2; j++)
       for (int i = -1; i <= Lm + 2; i++) {
+        if (cs.bulk_frc) continue;
         A(ksustr, i, j) = 1.0e-4 * std::sin(piy * A(kyr, i, j) / cs.sizey);
         if (cs.surf_flux) {  // synthetic ana_stflux/ana_srflux (oracle_main.c or_ana_forces)
           const double x = A(kxr, i, j), y = A(kyr, i, j);

@@ -16,6 +16,8 @@ enum HostId : int {
   kz_w = ROMS_z_w, kAkv = ROMS_Akv, kAkt = ROMS_Akt, kvisc2_r = ROMS_visc2_r, kvisc2_p = ROMS_visc2_p,
   kdiff2 = ROMS_diff2, ksustr = ROMS_sustr, ksvstr = ROMS_svstr, kstflx = ROMS_stflx, ksrflx = ROMS_srflx,
   kswflx = ROMS_swflx, kdndx = ROMS_dndx, kdmde = ROMS_dmde,
+  kuwnd = ROMS_uwnd, kvwnd = ROMS_vwnd, ktair = ROMS_tair, kqair = ROMS_qair, kprate = ROMS_prate,
+  kswrad = ROMS_swrad, klwrad = ROMS_lwrad,
   kxr = ROMS_NFIELDS, kyr, kNHost
 };
 
@@ -42,6 +44,7 @@ struct CaseSpec {
   int salinity, lmd, surf_flux;
   int obc, island;   // open edges (bitmask), circular land mask
   int curvgrid;      // non-uniform metrics + dndx/dmde
+  int bulk_frc;      // BULK_FRC analytic atmosphere (basin)
   double v_sponge;   // set_nudgcof.F sponge
   int host_wrap;  // apply periodic halo wraps on the host (single rank)
   double theta_s, theta_b, hc, rho0, Tcoef, visc2, tnu2, Akv_bak, Akt_bak[2];

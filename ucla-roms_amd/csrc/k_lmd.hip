@@ -203,8 +203,14 @@ __global__ void __launch_bounds__(64, 4) k_kpp_ext(Dev d, Range E, int tind, int
   const double sr = F.srflx[ij];
   const double Bo = P.salinity ? g * (alpha * (F.stflx[ij] - sr) - beta * F.stflx[ij + n2]) : g * (alpha * (F.stflx[ij] - sr));
   const double Bosol = g * alpha * sr;
-  const double su0 = F.sustr[ij], su1 = F.sustr[ij + 1], sv0 = F.svstr[ij], sv1 = F.svstr[ij + sj];
-  const double ustar = sqrt(sqrt(0.333333333333 * (su0 * su0 + su1 * su1 + su0 * su1 + sv0 * sv0 + sv1 * sv1 + sv0 * sv1)));
+  double ustar;
+  if (P.bulk_frc) {   // BULK_FRC: rho-point stresses (lmd_kpp.F:173-174)
+    const double sr_ = F.sustr_r[ij], sv_ = F.svstr_r[ij];
+    ustar = sqrt(sqrt(sr_ * sr_ + sv_ * sv_));
+  } else {
+    const double su0 = F.sustr[ij], su1 = F.sustr[ij + 1], sv0 = F.svstr[ij], sv1 = F.svstr[ij + sj];
+    ustar = sqrt(sqrt(0.333333333333 * (su0 * su0 + su1 * su1 + su0 * su1 + sv0 * sv0 + sv1 * sv1 + sv0 * sv1)));
+  }
   const double hbl0 = F.hbls[ij], bbl0 = F.hbbl[ij];
   const double rm = F.rmask[ij], ff = F.f[ij];
   F.lmd_Bo[ij] = Bo;

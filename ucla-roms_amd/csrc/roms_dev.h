@@ -34,6 +34,7 @@ struct Params {
   int lmd_rimix, lmd_convec, lmd_nonlocal;  // LMD_RIMIX, LMD_CONVEC, LMD_NONLOCAL (lmd != 0: MIXING+KPP+BKPP)
   int uv_adv, uv_cor;                       // UV_ADV, UV_COR
   int tides;                                // TIDES pot_tides: ptide in prsgrd
+  int bulk_frc;                             // BULK_FRC (k_bulk.hip; u* from sustr_r/svstr_r in lmd_kpp)
   int prs_split;                            // 1: two-kernel prsgrd (default), 0: k_prsgrd_fused (ROMS_GPU_PRSGRD_FUSED=1)
   int s2d_split;  // 1: step2d as separate zeta / momentum kernels (ROMS_GPU_S2D_SPLIT=1)
   int colseg;     // 1: segment-partitioned column solvers (k_colseg.h; N > 63, ROMS_GPU_COLSEG=0/1)
@@ -58,6 +59,8 @@ struct Fields {
       *pmon_u, *pnom_v, *rmask, *pmask, *umask, *vmask;
   double *dndx, *dmde;  // CURVGRID metric derivatives
   double* ptide;        // tides.F surface tidal potential (TIDES)
+  // BULK_FRC inputs (rho points) and rho-point stresses (bulk_frc.F, surf_flux.F)
+  double *uwnd, *vwnd, *tair, *qair, *prate, *swrad, *lwrad, *sustr_r, *svstr_r;
   double *Cs_w, *Cs_r;  // scoord.F (N+1)
   // ocean vars
   double *zeta, *ubar, *vbar, *u, *v, *t;
@@ -250,6 +253,8 @@ void launch_u3dbc(const Dev& d, hipStream_t s, const Tlev& t);
 // river_frc.F hooks (k_river.hip): ubar/vbar(knew) and DU/DV_avg1 at river
 // faces after each fast step; u,v(nnew) at river faces (pred: predictor ranges)
 void launch_river_s2d(const Dev& d, hipStream_t s, int knew);
+// BULK_FRC: calc_all_bulk_forces (k_bulk.hip)
+void launch_bulk_flux(const Dev& d, hipStream_t s, int nrhs);
 void launch_river_uv(const Dev& d, hipStream_t s, int nnew, int pred);
 void launch_v3dbc(const Dev& d, hipStream_t s, const Tlev& t);
 void launch_t3dbc(const Dev& d, hipStream_t s, const Tlev& t, int itrc);

@@ -197,6 +197,9 @@ double** field_slot(Fields& F, int id) {
     case ROMS_stflx: return &F.stflx; case ROMS_srflx: return &F.srflx; case ROMS_swflx: return &F.swflx;
     case ROMS_ru: return &F.ru; case ROMS_rv: return &F.rv;
     case ROMS_dndx: return &F.dndx; case ROMS_dmde: return &F.dmde; case ROMS_ptide: return &F.ptide;
+    case ROMS_uwnd: return &F.uwnd; case ROMS_vwnd: return &F.vwnd; case ROMS_tair: return &F.tair;
+    case ROMS_qair: return &F.qair; case ROMS_prate: return &F.prate; case ROMS_swrad: return &F.swrad;
+    case ROMS_lwrad: return &F.lwrad; case ROMS_sustr_r: return &F.sustr_r; case ROMS_svstr_r: return &F.svstr_r;
     default: break;
   }
   if (id >= ROMS_zeta_west && id <= ROMS_t_north) {
@@ -262,6 +265,7 @@ void enqueue_step(roms_tlev* t) {
   const Dev& d = g.d;
   hipStream_t s = g.s;
   Tlev T = to_tlev(t);
+  launch_bulk_flux(d, s, T.nrhs);   // set_forces (main.F:386): BULK_FRC only
   TIMED(ROMS_R_RHO_EOS, launch_rho_eos(d, s, T, T.nrhs));
   TIMED(ROMS_R_SET_HUV, launch_set_huv(d, s, T));
   TIMED(ROMS_R_OMEGA, launch_omega(d, s, T));
@@ -274,6 +278,7 @@ void enqueue_step(roms_tlev* t) {
   T = to_tlev(t);
   TIMED(ROMS_R_OMEGA, launch_omega(d, s, T));
   TIMED(ROMS_R_RHO_EOS, launch_rho_eos(d, s, T, T.nrhs));
+  launch_bulk_flux(d, s, T.nrhs);   // set_forces (main.F:433): BULK_FRC only
   if (g.cfg.lmd_mixing) TIMED(ROMS_R_LMD_VMIX, launch_lmd_vmix(d, s, T, T.nrhs));
   TIMED(ROMS_R_PRSGRD, launch_prsgrd(d, s, T));
   TIMED(ROMS_R_STEP3D_UV1, launch_step3d_uv1(d, s, T));
@@ -338,6 +343,7 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
   P.lmd_nonlocal = (cfg->lmd_mixing & ROMS_LMD_NONLOCAL) != 0;
   P.uv_adv = cfg->uv_adv != 0; P.uv_cor = cfg->uv_cor != 0;
   P.tides = cfg->pot_tides != 0;
+  P.bulk_frc = cfg->bulk_frc != 0;
   {
     // fused one-kernel prsgrd (k_prsgrd_fused): bit-identical, fewer bytes,
     // but measured slower at C2 (0.50 vs 0.38 ms per call: a per-level walk
@@ -684,6 +690,14 @@ int roms_gpu_set_river_frc(int nriv, const double* riv_uflx, const double* riv_v
   return 0;
 }
 
+int roms_gpu_bulk_flux(const roms_tlev* t) {
+  REQUIRE_INIT();
+  if (!g.d.p.bulk_frc) { g.err = "roms_gpu_bulk_flux: library initialised without bulk_frc"; return -4; }
+  if (t->nrhs < 1 || t->nrhs > 3) { g.err = "roms_gpu_bulk_flux: bad time index"; return -1; }
+  launch_bulk_flux(g.d, g.s, t->nrhs);
+  return post_launch();
+}
+
 int roms_gpu_step(roms_tlev* t) {
   REQUIRE_INIT();
   t->iic = t->iic + 1;
@@ -767,6 +781,7 @@ static int init_case_impl(const roms_case* c, int np_xi, int np_eta, void* comm,
   C.ubind = 0.1;  // Examples/Iceland/Iceland_parent/roms.in: ubind
   C.curvgrid = c->case_id == ROMS_CASE_BASIN ? c->curvgrid : 0;
   C.uv_adv = c->uv_adv; C.uv_cor = c->uv_cor;
+  C.bulk_frc = c->case_id == ROMS_CASE_BASIN ? c->bulk_frc : 0;
   C.Akv_bak = (fil || pipes) ? 0.0 : 1.0e-4; C.Akt_bak[0] = (fil || pipes) ? 0.0 : 1.0e-5; C.Akt_bak[1] = C.Akt_bak[0];
   int r = roms_gpu_init(&D, &C, device, comm);
   if (r) return r;
@@ -784,6 +799,7 @@ static int init_case_impl(const roms_case* c, int np_xi, int np_eta, void* comm,
   cs.obc = C.obc; cs.island = c->case_id == ROMS_CASE_BASIN ? c->island : 0;
   cs.v_sponge = C.obc ? c->v_sponge : 0.0;
   cs.curvgrid = C.curvgrid;
+  cs.bulk_frc = C.bulk_frc;
   HostState H(D.Lm, D.Mm, D.N, D.NT, C.salinity ? 2 : 1);
   double area = 0.0, volume = 0.0;
   build_case(cs, H, area, volume);
@@ -827,6 +843,7 @@ static int init_case_impl(const roms_case* c, int np_xi, int np_eta, void* comm,
   *t = roms_tlev{};
   t->iic = 0; t->ntstart = 1; t->forw_start = 1; t->iif = 1; t->nfast = C.nfast;
   t->kstp = 1; t->knew = 1; t->nstp = 1; t->nrhs = 1; t->nnew = 1;
+  if (C.bulk_frc) launch_bulk_flux(g.d, g.s, 1);   // set_forces after ana_init (main.F:266)
   return roms_gpu_init_sequence(t);
 }
 

@@ -25,7 +25,7 @@ FIELDS = ["h", "hinv", "f", "fomn", "pm", "pn", "dm_r", "dn_r", "dm_u", "dn_u", 
           "DU_avg_bak", "DV_avg_bak", "rho", "rho1", "qp1", "bvf", "Akv", "Akt", "visc2_r", "visc2_p", "diff2",
           "hbls", "hbbl", "ghat", "swr_frac", "sustr", "svstr", "stflx", "srflx", "swflx", "ru", "rv"] + \
          ["%s_%s" % (v, e) for v in ("zeta", "ubar", "vbar", "u", "v", "t") for e in ("west", "east", "south", "north")] + \
-         ["dndx", "dmde", "ptide"]
+         ["dndx", "dmde", "ptide", "uwnd", "vwnd", "tair", "qair", "prate", "swrad", "lwrad", "sustr_r", "svstr_r"]
 FIELD_ID = {n: i for i, n in enumerate(FIELDS)}
 CASE_FILAMENT, CASE_BASIN, CASE_PIPES, CASE_RIVERS = 0, 1, 2, 3
 # LMD switch bits (ROMS_LMD_* of include/roms_gpu.h)
@@ -57,7 +57,8 @@ class Cfg(ctypes.Structure):
                 ("T0", ctypes.c_double), ("Scoef", ctypes.c_double), ("S0", ctypes.c_double),
                 ("theta_s", ctypes.c_double), ("theta_b", ctypes.c_double), ("hc", ctypes.c_double),
                 ("obc", ctypes.c_int), ("ubind", ctypes.c_double), ("curvgrid", ctypes.c_int),
-                ("uv_adv", ctypes.c_int), ("uv_cor", ctypes.c_int), ("pot_tides", ctypes.c_int)]
+                ("uv_adv", ctypes.c_int), ("uv_cor", ctypes.c_int), ("pot_tides", ctypes.c_int),
+                ("bulk_frc", ctypes.c_int)]
 
 
 class Tlev(ctypes.Structure):
@@ -74,7 +75,8 @@ class Case(ctypes.Structure):
                 ("lmd_mixing", ctypes.c_int), ("dt", ctypes.c_double), ("ndtfast", ctypes.c_int),
                 ("sizex", ctypes.c_double), ("sizey", ctypes.c_double), ("surf_flux", ctypes.c_int),
                 ("obc", ctypes.c_int), ("v_sponge", ctypes.c_double), ("island", ctypes.c_int),
-                ("curvgrid", ctypes.c_int), ("uv_adv", ctypes.c_int), ("uv_cor", ctypes.c_int)]
+                ("curvgrid", ctypes.c_int), ("uv_adv", ctypes.c_int), ("uv_cor", ctypes.c_int),
+                ("bulk_frc", ctypes.c_int)]
 
 
 ROUTINES_T = ["set_huv", "omega", "prsgrd", "pre_step3d", "set_huv1", "step3d_uv1", "visc3d", "step2d",
@@ -109,6 +111,7 @@ def load_library(path=LIB_PATH):
                                         P(ctypes.c_double)]
     L.roms_gpu_set_river_frc.argtypes = [ctypes.c_int, P(ctypes.c_double), P(ctypes.c_double), P(ctypes.c_double),
                                          P(ctypes.c_double)]
+    L.roms_gpu_bulk_flux.argtypes = [P(Tlev)]
     L.roms_gpu_diag.argtypes = [P(Tlev), P(ctypes.c_double)]
     L.roms_gpu_time_steps.argtypes = [P(Tlev), ctypes.c_int, P(ctypes.c_double)]
     L.roms_gpu_stream.restype = ctypes.c_void_p
@@ -228,13 +231,15 @@ class Model:
     @classmethod
     def from_case(cls, case_id, LLm, MMm, N, NT=1, salinity=False, nonlin_eos=False, dt=5.0, ndtfast=60,
                   sizex=12.8e3, sizey=3.2e3, device=0, np_xi=1, np_eta=1, comm=None, rank=0, lmd=False,
-                  surf_flux=False, obc=0, v_sponge=0.0, island=False, curvgrid=False, uv_adv=True, uv_cor=True):
+                  surf_flux=False, obc=0, v_sponge=0.0, island=False, curvgrid=False, uv_adv=True, uv_cor=True,
+                  bulk_frc=False):
         """Analytic case on the whole grid, or on subdomain `rank` of an
         np_xi x np_eta processor grid when a communicator is given.
         lmd: False, True (all LMD switches) or ROMS_LMD_* bits."""
         m = cls()
         c = Case(case_id, LLm, MMm, N, NT, int(salinity), int(nonlin_eos), lmd_bits(lmd), dt, ndtfast, sizex, sizey,
-                 int(surf_flux), int(obc), float(v_sponge), int(island), int(curvgrid), int(uv_adv), int(uv_cor))
+                 int(surf_flux), int(obc), float(v_sponge), int(island), int(curvgrid), int(uv_adv), int(uv_cor),
+                 int(bulk_frc))
         if comm is None and np_xi * np_eta == 1:
             m._chk(m.L.roms_gpu_init_case(ctypes.byref(c), device, ctypes.byref(m.t)), "roms_gpu_init_case")
         else:
@@ -342,6 +347,10 @@ class Model:
         self._chk(self.L.roms_gpu_set_river_frc(nriv, uf.ctypes.data_as(D) if uf is not None else None,
                                                 vf.ctypes.data_as(D) if vf is not None else None,
                                                 vol.ctypes.data_as(D), trc.ctypes.data_as(D)), "set_river_frc")
+
+    def bulk_flux(self):
+        """set_bulk_frc -> calc_all_bulk_forces on the device at the current nrhs."""
+        self._chk(self.L.roms_gpu_bulk_flux(ctypes.byref(self.t)), "bulk_flux")
 
     def _r(self, fn):
         self._chk(getattr(self.L, "roms_gpu_" + fn)(ctypes.byref(self.t)), fn)
