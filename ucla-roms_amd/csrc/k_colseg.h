@@ -33,7 +33,6 @@ namespace roms {
 // blockDim.y wavefronts holds S = blockDim.y*64/kSegCW segments of kSegCW
 // columns.  Small blocks (1-2 wavefronts for N = 50..100) keep several
 // independent blocks per CU whose load and solve phases overlap.
-constexpr int kSegCW = 16;
 struct SegSpan {
   int s, S, c0, n;  // segment index, count, first cell (1-based), cells in segment
   int col;          // column of the lane within the block (0..kSegCW-1)
@@ -59,15 +58,31 @@ inline int seg_waves(int N) {
 // Logical block of a segment-solver launch.  ord 0: xcd_tile() order (x
 // fastest); ord 1: z (direction / tracer) fastest, then y (j), then x, so the
 // blocks that share a column's arrays (both directions, all tracers) and the
-// j-neighbour rows run back to back on one XCD; ord 2: z, then x, then y.
-__device__ __forceinline__ uint3 seg_tile(int ord) {
+// j-neighbour rows run back to back on one XCD; ord 2: z, then x, then y;
+// ord 3: z, then x within a group of xg blocks, then y, then the group, so the
+// blocks resident on an XCD at one time cover xg x (resident/xg/gz) columns
+// blocks of both directions and share their i- and j-neighbour lines in L2.
+__device__ __forceinline__ uint3 seg_tile(int ord, int xg = 4) {
   uint3 t = xcd_tile();
   if (ord == 0) return t;
   const unsigned gx = gridDim.x, gy = gridDim.y, gz = gridDim.z;
   const unsigned L = t.x + gx * (t.y + gy * t.z);
   t.z = L % gz;
   if (ord == 1) { t.y = (L / gz) % gy; t.x = L / (gz * gy); }
-  else { t.x = (L / gz) % gx; t.y = L / (gz * gx); }
+  else if (ord == 2) { t.x = (L / gz) % gx; t.y = L / (gz * gx); }
+  else {
+    const unsigned G = (unsigned)xg < gx ? (unsigned)xg : gx;
+    const unsigned Lp = L / gz, nfull = gx / G, inf = nfull * G * gy;
+    if (Lp < inf) {
+      const unsigned rem = Lp % (G * gy);
+      t.x = (Lp / (G * gy)) * G + rem % G;
+      t.y = rem / G;
+    } else {
+      const unsigned Gl = gx - nfull * G, rem = Lp - inf;
+      t.x = nfull * G + rem % Gl;
+      t.y = rem / Gl;
+    }
+  }
   return t;
 }
 

@@ -282,7 +282,7 @@ __global__ void __launch_bounds__(64) k_pre_uv(Dev d, Range R, PreCoef c, int ns
 // diffusion / viscosity are each one partitioned tridiagonal system whose
 // rows are those of k_pre_tracer_v / pre_uv_col (pre_step3d4S.F:198-489). ----
 __global__ void __launch_bounds__(kSegBlock) k_pre_tracer_seg(Dev d, Range R, PreCoef c, int nnew, int nrhs) {
-  const uint3 bI = seg_tile(d.p.seg_order);
+  const uint3 bI = seg_tile(d.p.seg_order, d.p.seg_xg);
   __shared__ SegXchg X;
   constexpr int KR = kSegRows + 1;
   const Bounds& b = d.b;
@@ -347,7 +347,7 @@ __global__ void __launch_bounds__(kSegBlock) k_pre_tracer_seg(Dev d, Range R, Pr
 }
 
 __global__ void __launch_bounds__(kSegBlock) k_pre_uv_seg(Dev d, Range R, PreCoef c, int nstp, int nnew, int nrhs) {
-  const uint3 bI = seg_tile(d.p.seg_order);
+  const uint3 bI = seg_tile(d.p.seg_order, d.p.seg_xg);
   __shared__ SegXchg X;
   constexpr int KR = kSegRows + 1;
   const Bounds& b = d.b;

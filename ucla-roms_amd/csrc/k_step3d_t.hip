@@ -153,7 +153,7 @@ __global__ void __launch_bounds__(64) k_step3d_t_v(Dev d, Range R, int nnew, int
 // partitioned tridiagonal system; the surface, KPP and pipe terms of the
 // diffusion r.h.s. are those of k_step3d_t_v (step3d_t_ISO.F:913-1100). ----
 __global__ void __launch_bounds__(kSegBlock) k_step3d_t_seg(Dev d, Range R, int nnew, int nrhs) {
-  const uint3 bI = seg_tile(d.p.seg_order);
+  const uint3 bI = seg_tile(d.p.seg_order, d.p.seg_xg);
   __shared__ SegXchg X;
   constexpr int KR = kSegRows + 1;
   const Bounds& b = d.b;

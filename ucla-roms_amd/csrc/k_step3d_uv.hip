@@ -215,7 +215,7 @@ struct SegRu {
   double r[kSegRows * kSegMaxS][kSegCW];
 };
 __global__ void __launch_bounds__(kSegBlock) k_uv1_seg(Dev d, Range R, int nnew, int nrhs) {
-  const uint3 bI = seg_tile(d.p.seg_order);
+  const uint3 bI = seg_tile(d.p.seg_order, d.p.seg_xg);
   __shared__ SegXchg X;
   __shared__ SegRu Sr;
   constexpr int KR = kSegRows + 1;

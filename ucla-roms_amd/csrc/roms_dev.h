@@ -42,6 +42,7 @@ struct Params {
   int uv2_fused;  // 1: one-pass step3d_uv2 (k_uv2_fused; ROMS_GPU_UV2_FUSED=0 disables)
   int chain;      // 1: chained 4-lane set_HUV1 (k_chain.h; ROMS_GPU_CHAIN=0 disables)
   int seg_order;  // block order of the segment solvers (seg_tile; ROMS_GPU_SEG_ORDER)
+  int seg_xg;     // x-blocks per group of seg_order 3 (ROMS_GPU_SEG_XG)
   int npip;       // pipe_frc.F: number of pipes (0: pipe_source off)
   int nriv, nrivf;  // river_frc.F: number of rivers (0: river_source off), river faces
   int curvgrid;   // CURVGRID && UV_ADV: curvature terms (compute_horiz_rhs_uv_terms.h:8-11)
@@ -189,8 +190,12 @@ constexpr int kCX = 64;
 #define ROMS_SEG_MAXS 8
 #endif
 constexpr int kSegRows = ROMS_SEG_ROWS;   // cells per segment (register arrays of kSegRows + 2)
-constexpr int kSegMaxS = ROMS_SEG_MAXS;   // segments per block (16 columns each): N <= kSegRows * kSegMaxS
-constexpr int kSegBlock = ((kSegMaxS * 16 + 63) / 64) * 64;   // threads of a segment-solver block (max)
+constexpr int kSegMaxS = ROMS_SEG_MAXS;   // segments per block (kSegCW columns each): N <= kSegRows * kSegMaxS
+#ifndef ROMS_SEG_CW
+#define ROMS_SEG_CW 16
+#endif
+constexpr int kSegCW = ROMS_SEG_CW;       // columns per segment-solver block (lanes of one segment)
+constexpr int kSegBlock = ((kSegMaxS * kSegCW + 63) / 64) * 64;   // threads of a segment-solver block (max)
 inline dim3 gridc_of(const Range& r) {
   int ni = r.i1 - r.i0 + 1, nj = r.j1 - r.j0 + 1;
   if (ni < 1) ni = 1;

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -400,7 +401,12 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
   P.seg_order = 0;
   {
     const char* e = getenv("ROMS_GPU_SEG_ORDER");
-    if (e && e[0] >= '0' && e[0] <= '2') P.seg_order = e[0] - '0';
+    if (e && e[0] >= '0' && e[0] <= '3') P.seg_order = e[0] - '0';
+  }
+  P.seg_xg = 4;
+  {
+    const char* e = getenv("ROMS_GPU_SEG_XG");
+    if (e && atoi(e) > 0) P.seg_xg = atoi(e);
   }
   // column-solver scratch: LDS while two (N+1)-level slots per wave fit the
   // default 64 KB (N < 63), global memory for deeper grids;
