@@ -216,6 +216,32 @@ module roms_gpu_mod
       type(roms_tlev), intent(in) :: t
       real(c_double), intent(out) :: norms(4)
     end function
+    ! partitioned netCDF restart/history files (basic_output.F, get_init.F);
+    ! path: a NUL-terminated character(kind=c_char) array
+    integer(c_int) function roms_gpu_wrt_rst(path, rec, total_rec, time, t) bind(c)
+      import :: c_int, c_double, c_char, roms_tlev
+      character(kind=c_char), intent(in) :: path(*)
+      integer(c_int), value :: rec, total_rec
+      real(c_double), value :: time
+      type(roms_tlev), intent(in) :: t
+    end function
+    integer(c_int) function roms_gpu_wrt_his(path, rec, total_rec, time, t, wrt_mask) bind(c)
+      import :: c_int, c_double, c_char, roms_tlev
+      character(kind=c_char), intent(in) :: path(*)
+      integer(c_int), value :: rec, total_rec, wrt_mask
+      real(c_double), value :: time
+      type(roms_tlev), intent(in) :: t
+    end function
+    integer(c_int) function roms_gpu_io_wait() bind(c)
+      import :: c_int
+    end function
+    integer(c_int) function roms_gpu_get_init(path, req_rec, tindx, t, start_time) bind(c)
+      import :: c_int, c_double, c_char, roms_tlev
+      character(kind=c_char), intent(in) :: path(*)
+      integer(c_int), value :: req_rec, tindx
+      type(roms_tlev), intent(inout) :: t
+      real(c_double), intent(out) :: start_time
+    end function
     integer(c_int) function roms_gpu_comm_unique_id(id128) bind(c)
       import :: c_int, c_char
       character(kind=c_char), intent(out) :: id128(128)

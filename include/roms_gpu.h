@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define ROMS_GPU_ABI_VERSION 7
+#define ROMS_GPU_ABI_VERSION 8
 #define ROMS_MAX_FAST 288
 
 /* Subdomain geometry of this rank: param.F / dimensions.F / mpi_setup.F:39-210 */
@@ -251,6 +251,48 @@ int roms_gpu_halo_plan(int Lm, int Mm, int np_xi, int np_eta, int inode, int jno
  * Returns the per-level count (<= cap) or -1.                               */
 long roms_gpu_halo_map(int Lm, int Mm, int np_xi, int np_eta, int inode, int jnode, int ew_periodic,
                        int ns_periodic, int dir, int unpack, int *i, int *j, long cap);
+
+/* ---- on-disk formats: partitioned netCDF restart and history files ----
+ * One file per rank, as the reference's PARALLEL_FILES build writes them
+ * (file name chosen by the host: roms_read_write.F:1389-1447 appends the date
+ * and the rank), in the netCDF classic 64-bit-offset format (nf90_open reads
+ * it like the reference's own netCDF-4 files), with the reference's
+ * dimensions (xi_rho, xi_u, eta_rho, eta_v, s_rho, s_w, time, auxil),
+ * variables, attributes and 'partition' global attribute.
+ * roms_gpu_wrt_rst replaces wrt_restart_file (basic_output.F:568-682): it
+ * writes record rec (1-based; rec 1 creates the file, def_vars_rst_ocean_vars
+ * :873-1034) with ocean_time = time, time_step = (t->iic, rec, total_rec, 0,
+ * 0, 0), zeta/ubar/vbar(knew), u/v/tracers(nnew), the EXACT_RESTART
+ * DU/DV_avg1/avg2/avg_bak, hbls/hbbl (LMD) and riv_umask/riv_vmask.
+ * roms_gpu_wrt_his replaces wrt_his_ocean_vars (:273-419) for the fields in
+ * wrt_mask (ocean_vars.opt wrt_* switches).  Both snapshot the record on the
+ * device, in stream order, and return; the PCIe copy and the file write run
+ * behind the next steps.  roms_gpu_io_wait joins the pending write and
+ * returns its status.  roms_gpu_get_init replaces get_init (get_init.F): see
+ * rst_io.hip for the EXACT_RESTART protocol (call it with tindx 2 on record
+ * rec-1, then tindx 1 on rec, then roms_gpu_init_sequence).                 */
+#define ROMS_WRT_Z    1
+#define ROMS_WRT_UB   2
+#define ROMS_WRT_VB   4
+#define ROMS_WRT_U    8
+#define ROMS_WRT_V    16
+#define ROMS_WRT_T    32     /* all tracers (tracers.opt wrt_t)              */
+#define ROMS_WRT_R    64     /* rho1 (SPLIT_EOS) or rho                      */
+#define ROMS_WRT_O    128    /* omega (We)                                   */
+#define ROMS_WRT_AKV  256
+#define ROMS_WRT_AKT  512
+#define ROMS_WRT_AKS  1024
+#define ROMS_WRT_HBLS 2048
+#define ROMS_WRT_HBBL 4096
+#define ROMS_WRT_DEFAULT 63  /* ocean_vars.opt defaults: Z, Ub, Vb, U, V + tracers */
+int roms_gpu_wrt_rst(const char *path, int rec, int total_rec, double time, const roms_tlev *t);
+int roms_gpu_wrt_his(const char *path, int rec, int total_rec, double time, const roms_tlev *t, int wrt_mask);
+int roms_gpu_io_wait(void);
+/* t_vname/t_units/t_lname of tracer itrc (tracers.opt); default temp, salt, trcNN */
+int roms_gpu_io_tracer_name(int itrc, const char *name, const char *units, const char *long_name);
+/* Returns 0 (read), 1 (tindx 2: records not consecutive steps, nothing read),
+ * or a negative error.                                                       */
+int roms_gpu_get_init(const char *path, int req_rec, int tindx, roms_tlev *t, double *start_time);
 
 /* ---- diagnostics (diag.F code_check norms, device reduction) ----
  * KE, KE2b (barotropic), max advective Courant and the vertical Courant at

@@ -16,6 +16,7 @@
 #include "halo.h"
 #include "host_init.h"
 #include "roms_dev.h"
+#include "shim_state.h"
 
 using namespace roms;
 
@@ -212,6 +213,7 @@ double** field_slot(Fields& F, int id) {
 }
 
 void free_all() {
+  io_free();
   for (hipEvent_t e : g.ev) (void)hipEventDestroy(e);
   g.ev.clear();
   halo_free(g.halo);
@@ -248,6 +250,12 @@ Tlev to_tlev(const roms_tlev* t) {
   } while (0)
 
 }  // namespace
+int roms::shim_enter(ShimState& S) {
+  REQUIRE_INIT();
+  S.d = &g.d; S.s = g.s; S.dims = &g.dims; S.cfg = &g.cfg; S.err = &g.err;
+  return 0;
+}
+void roms::shim_set_error(const std::string& e) { g.err = e; }
 void roms::ktimer_mark(hipStream_t s, int id, int end, int count) {
   if (g.timed != id) return;
   if (!end) {
@@ -748,7 +756,9 @@ int roms_gpu_init_sequence(roms_tlev* t) {
   REQUIRE_INIT();
   const Tlev T = to_tlev(t);
   launch_set_depth(g.d, g.s, T);
-  if (g.cfg.lmd_mixing) launch_swr_frac(g.d, g.s);  // main.F:217-220 (zeta at rest)
+  // main.F:217-220 (zeta at rest): at initialisation only, not after a
+  // restart read (get_init leaves iic = ntstart - 1 > 0)
+  if (g.cfg.lmd_mixing && t->iic == 0) launch_swr_frac(g.d, g.s);
   launch_set_huv(g.d, g.s, T);
   launch_omega(g.d, g.s, T);
   launch_rho_eos(g.d, g.s, T, T.nrhs);

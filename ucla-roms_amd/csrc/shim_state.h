@@ -1,0 +1,24 @@
+// shim_state.h -- what the C-ABI modules outside roms_shim.cpp (rst_io.hip)
+// see of the calling thread's library state.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "../../include/roms_gpu.h"
+#include "roms_dev.h"
+
+namespace roms {
+struct ShimState {
+  Dev* d = nullptr;
+  hipStream_t s = nullptr;
+  const roms_dims* dims = nullptr;
+  const roms_cfg* cfg = nullptr;
+  std::string* err = nullptr;
+};
+// The entry checks of every routine (initialised, no failed halo wait, fast-
+// loop exchange joined); fills S.  Returns 0 or the negative error code.
+int shim_enter(ShimState& S);
+void shim_set_error(const std::string& e);
+void io_free();   // rst_io.hip: joins the writer, frees staging (roms_gpu_finalize)
+}  // namespace roms

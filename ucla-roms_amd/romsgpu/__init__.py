@@ -125,6 +125,10 @@ def load_library(path=LIB_PATH):
     L.roms_gpu_halo_plan.argtypes = [ctypes.c_int] * 8 + [P(ctypes.c_int), P(ctypes.c_long), P(ctypes.c_int)]
     L.roms_gpu_halo_map.argtypes = [ctypes.c_int] * 10 + [P(ctypes.c_int), P(ctypes.c_int), ctypes.c_long]
     L.roms_gpu_halo_map.restype = ctypes.c_long
+    L.roms_gpu_wrt_rst.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_double, P(Tlev)]
+    L.roms_gpu_wrt_his.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_double, P(Tlev), ctypes.c_int]
+    L.roms_gpu_get_init.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, P(Tlev), P(ctypes.c_double)]
+    L.roms_gpu_io_tracer_name.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]
     _lib = L
     return L
 
@@ -179,6 +183,9 @@ def halo_map(Lm, Mm, np_xi, np_eta, inode, jnode, ew_periodic, ns_periodic, dire
 
 
 HALO_DIRS = ("W", "E", "S", "N", "SW", "SE", "NW", "NE")
+# ROMS_WRT_* of include/roms_gpu.h (ocean_vars.opt wrt_* switches)
+WRT = dict(Z=1, Ub=2, Vb=4, U=8, V=16, T=32, R=64, O=128, Akv=256, Akt=512, Aks=1024, Hbls=2048, Hbbl=4096)
+WRT_DEFAULT = 63
 # enum roms_routine of include/roms_gpu.h
 ROUTINES = ("rho_eos", "set_HUV", "omega", "prsgrd", "pre_step3d", "set_HUV1", "step3d_uv1", "visc3d", "step2d",
             "step3d_uv2", "step3d_t", "t3dmix", "lmd_vmix",
@@ -394,6 +401,51 @@ class Model:
         out = (ctypes.c_double * 4)()
         self._chk(self.L.roms_gpu_diag(ctypes.byref(self.t), out), "diag")
         return list(out)
+
+    # ---- on-disk formats (basic_output.F, get_init.F) ----
+    def time(self, dt):
+        """Model time at the end of the last step (main.F:487, start_time 0)."""
+        return dt * (self.t.iic - self.t.ntstart + 1) + getattr(self, "start_time", 0.0)
+
+    def wrt_rst(self, path, rec, total_rec, time):
+        """wrt_restart_file: record rec (1-based) of this rank's restart file."""
+        self._chk(self.L.roms_gpu_wrt_rst(path.encode(), rec, total_rec, time, ctypes.byref(self.t)), "wrt_rst")
+
+    def wrt_his(self, path, rec, total_rec, time, mask=WRT_DEFAULT):
+        """wrt_his_ocean_vars: record rec of this rank's history file."""
+        self._chk(self.L.roms_gpu_wrt_his(path.encode(), rec, total_rec, time, ctypes.byref(self.t), mask), "wrt_his")
+
+    def io_wait(self):
+        self._chk(self.L.roms_gpu_io_wait(), "io_wait")
+
+    def get_init(self, path, req_rec, tindx):
+        """get_init(req_rec, tindx); returns 0 (read) or 1 (exact restart not possible)."""
+        st = ctypes.c_double()
+        rc = self.L.roms_gpu_get_init(path.encode(), req_rec, tindx, ctypes.byref(self.t), ctypes.byref(st))
+        if rc < 0:
+            self._chk(rc, "get_init")
+        if tindx == 1:
+            self.start_time = st.value
+        return rc
+
+    def restart(self, path, rec=0, exact=True):
+        """main.F:244-288: get_init(rec-1, 2) [EXACT_RESTART], get_init(rec, 1),
+        then set_depth, set_HUV, omega, rho_eos(nrhs) (roms_gpu_init_sequence).
+        rec 0 = the last record."""
+        self.t.forw_start = 0
+        if exact:
+            nrec = rec if rec > 0 else self._nrecs(path)
+            if nrec >= 2:
+                self.get_init(path, nrec - 1, 2)
+            rec = nrec
+        self.get_init(path, rec, 1)
+        self.init_sequence()
+
+    @staticmethod
+    def _nrecs(path):
+        with open(path, "rb") as f:
+            h = f.read(8)
+        return int.from_bytes(h[4:8], "big")
 
     def time_steps(self, n):
         ms = ctypes.c_double()
