@@ -195,6 +195,14 @@ int roms_gpu_set_river_frc(int nriv, const double *riv_uflx, const double *riv_v
  * time-interpolated atmospheric fields (set_frc_data) before each step.
  * Returns -4 when the library was initialised without bulk_frc. */
 int roms_gpu_bulk_flux(const roms_tlev *t);
+/* SPONGE_TUNE with ub_tune (sponge_tune.F, t3dbc_im.F:73-74): the per-edge
+ * binding coefficients ub_west(j), ub_east(j) (j = 0..Mm+1) and ub_south(i),
+ * ub_north(i) (i = 0..Lm+1) that the host's adjust_orlanski maintains from
+ * the parent/child baroclinic pressure fluxes; t3dbc's Orlanski blend then
+ * uses cext = max(cext, min(ub(j), 1)).  NULL switches an edge off (the
+ * reference default ub_tune = .false., sponge_tune.opt).  Call again after
+ * every adjust_orlanski; the next step uses the new values.                 */
+int roms_gpu_set_ub_tune(const double *ub_west, const double *ub_east, const double *ub_south, const double *ub_north);
 int roms_gpu_set_depth(const roms_tlev *t);           /* set_depth(tile)  set_depth.F:4    */
 
 /* One whole roms_step (main.F:333-520, forcing held fixed): advances t->iic

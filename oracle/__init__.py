@@ -84,6 +84,7 @@ def lib():
         L.or_set_iif.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.or_set_river.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                    ctypes.POINTER(ctypes.c_double)]
+        L.or_set_ub.argtypes = [ctypes.c_void_p] + [ctypes.POINTER(ctypes.c_double)] * 4
         _lib = L
     return _lib
 
@@ -189,6 +190,13 @@ class Oracle:
         t = np.ascontiguousarray(trc, dtype=np.float64)
         P = ctypes.POINTER(ctypes.c_double)
         self.L.or_set_river(self.h, 1, v.ctypes.data_as(P), t.ctypes.data_as(P))
+
+    def set_ub(self, ub):
+        """SPONGE_TUNE ub_west/east/south/north (sequence of 4 arrays or None)."""
+        P = ctypes.POINTER(ctypes.c_double)
+        keep = [None if a is None else np.ascontiguousarray(a, dtype=np.float64) for a in ub]
+        args = [None if a is None else a.ctypes.data_as(P) for a in keep]
+        self.L.or_set_ub(self.h, *args)
 
     def call(self, routine, *args):
         getattr(self.L, "or_" + routine)(self.h, *args)

@@ -55,6 +55,7 @@ struct or_state {
      [2] south, [3] north (index i, 0:Lm+1); u,v (.,N), t (.,N,NT) */
   int nbry[4];
   double *bry_zeta[4], *bry_ubar[4], *bry_vbar[4], *bry_u[4], *bry_v[4], *bry_t[4];
+  double *ub[4];   /* SPONGE_TUNE ub_west/east/south/north (NULL: ub_tune off), indexed like bry_* */
   /* forcing */
   double *sustr, *svstr, *stflx, *srflx, *swflx;
   /* BULK_FRC inputs and rho-point stresses (bulk_frc.F, surf_flux.F) */

@@ -863,6 +863,20 @@ double *or_field(or_state *S, const char *name, size_t *count) {
   return NULL;
 }
 
+/* SPONGE_TUNE (sponge_tune.F, t3dbc_im.F:73-74): the per-edge binding
+ * coefficients ub_west(j), ub_east(j), ub_south(i), ub_north(i) that
+ * adjust_orlanski maintains; NULL switches an edge's floor off. */
+void or_set_ub(or_state *S, const double *w, const double *e, const double *s, const double *n) {
+  const double *src[4] = {w, e, s, n};
+  for (int q = 0; q < 4; q++) {
+    free(S->ub[q]);
+    S->ub[q] = NULL;
+    if (!src[q]) continue;
+    S->ub[q] = zalloc(S->nbry[q]);
+    for (int m = 0; m < S->nbry[q]; m++) S->ub[q][m] = src[q][m];
+  }
+}
+
 void or_set_river(or_state *S, int nriv, const double *vol, const double *trc) {
   if (nriv < 1 || nriv > 16 || nriv * S->NT > 256) return;
   S->nriv = nriv;

@@ -544,6 +544,8 @@ void or_t3dbc(or_state *S, int it) {
           else { cext = -cx; cx = 0.; }
           TT(istr - 1, j, k, nn, it) = (1. - cx) * (TT(istr - 1, j, k, ns, it) - fmax0(cy) * G(0, j) - fmin0(cy) * G(0, j + 1)) +
                                        cx * (TT(istr, j, k, ns, it) - fmax0(cy) * G(1, j) - fmin0(cy) * G(1, j + 1));
+          /* SPONGE_TUNE with ub_tune (t3dbc_im.F:73-74): floor of the binding rate */
+          if (S->ub[SW]) cext = dmax(cext, dmin(S->ub[SW][j], 1.0));
           TT(istr - 1, j, k, nn, it) = (1. - cext) * TT(istr - 1, j, k, nn, it) + cext * BT(SW, j, k, it);
           TT(istr - 1, j, k, nn, it) = TT(istr - 1, j, k, nn, it) * A2(rm, istr - 1, j);
         }
@@ -567,6 +569,8 @@ void or_t3dbc(or_state *S, int it) {
           else { cext = -cx; cx = 0.; }
           TT(iend + 1, j, k, nn, it) = (1. - cx) * (TT(iend + 1, j, k, ns, it) - fmax0(cy) * G(1, j) - fmin0(cy) * G(1, j + 1)) +
                                        cx * (TT(iend, j, k, nn, it) - fmax0(cy) * G(0, j) - fmin0(cy) * G(0, j + 1));
+          /* SPONGE_TUNE with ub_tune (t3dbc_im.F:73-74): floor of the binding rate */
+          if (S->ub[SE]) cext = dmax(cext, dmin(S->ub[SE][j], 1.0));
           TT(iend + 1, j, k, nn, it) = (1. - cext) * TT(iend + 1, j, k, nn, it) + cext * BT(SE, j, k, it);
           TT(iend + 1, j, k, nn, it) = TT(iend + 1, j, k, nn, it) * A2(rm, iend + 1, j);
         }
@@ -590,6 +594,8 @@ void or_t3dbc(or_state *S, int it) {
           else { cext = -cx; cx = 0.; }
           TT(i, jstr - 1, k, nn, it) = (1. - cx) * (TT(i, jstr - 1, k, ns, it) - fmax0(cy) * G(0, i) - fmin0(cy) * G(0, i + 1)) +
                                        cx * (TT(i, jstr, k, ns, it) - fmax0(cy) * G(1, i) - fmin0(cy) * G(1, i + 1));
+          /* SPONGE_TUNE with ub_tune (t3dbc_im.F:73-74): floor of the binding rate */
+          if (S->ub[SS]) cext = dmax(cext, dmin(S->ub[SS][i], 1.0));
           TT(i, jstr - 1, k, nn, it) = (1. - cext) * TT(i, jstr - 1, k, nn, it) + cext * BT(SS, i, k, it);
           TT(i, jstr - 1, k, nn, it) = TT(i, jstr - 1, k, nn, it) * A2(rm, i, jstr - 1);
         }
@@ -613,6 +619,8 @@ void or_t3dbc(or_state *S, int it) {
           else { cext = -cx; cx = 0.; }
           TT(i, jend + 1, k, nn, it) = (1. - cx) * (TT(i, jend + 1, k, ns, it) - fmax0(cy) * G(1, i) - fmin0(cy) * G(1, i + 1)) +
                                        cx * (TT(i, jend, k, nn, it) - fmax0(cy) * G(0, i) - fmin0(cy) * G(0, i + 1));
+          /* SPONGE_TUNE with ub_tune (t3dbc_im.F:73-74): floor of the binding rate */
+          if (S->ub[SN]) cext = dmax(cext, dmin(S->ub[SN][i], 1.0));
           TT(i, jend + 1, k, nn, it) = (1. - cext) * TT(i, jend + 1, k, nn, it) + cext * BT(SN, i, k, it);
           TT(i, jend + 1, k, nn, it) = TT(i, jend + 1, k, nn, it) * A2(rm, i, jend + 1);
         }

@@ -97,6 +97,7 @@ void or_set_tindex(or_state *S, const int in[6]);
 void or_set_iif(or_state *S, int iif);
 /* set_river_frc: new riv_vol(nriv), riv_trc(nriv,NT) (faces kept) */
 void or_set_river(or_state *S, int nriv, const double *vol, const double *trc);
+void or_set_ub(or_state *S, const double *w, const double *e, const double *s, const double *n);
 
 #ifdef __cplusplus
 }

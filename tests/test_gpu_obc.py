@@ -146,3 +146,66 @@ def test_open_basin_decomposition_bitwise(npx, npe):
     (no sponge: the reference sets its bands on each rank's own points only)."""
     from test_gpu_multirank import test_decomposition_bitwise_equals_single_domain as run
     run("basin_obc", npx, npe)
+
+
+def _ub_arrays(cfg, scale):
+    """Per-edge binding coefficients spanning below 0, (0,1) and above the cap 1."""
+    nj, ni = cfg.MMm + 2, cfg.LLm + 2
+    x = lambda n, ph: scale * (0.5 + 1.5 * np.sin(np.arange(n) * 0.37 + ph))
+    return [x(nj, 0.0), x(nj, 1.0), x(ni, 2.0), x(ni, 3.0)]
+
+
+@pytest.mark.parametrize("obc", [15, 5])
+def test_sponge_tune_t3dbc_parity(obc):
+    """SPONGE_TUNE with ub_tune (t3dbc_im.F:73-74): the radiation blend's rate
+    is floored by min(ub(j), 1); step3d_t on identical states, then 20 steps."""
+    cfg = obc_cfg(obc=obc, lmd=oracle.LMD_ICELAND)
+    o, m = make_pair(cfg)
+    ub = _ub_arrays(cfg, 1.0)
+    o.set_ub(ub)
+    m.set_ub_tune(ub)
+    o.step(3)
+    iic, kstp, knew, nstp, nrhs, nnew = o.tindex()
+    nrhs, nnew = 3, 3 - nstp
+    o.set_tindex([iic, kstp, knew, nstp, nrhs, nnew])
+    copy_state(o, m)
+    m.set_tindex(iic, kstp, knew, nstp, nrhs, nnew, iif=2, nfast=o.nfast())
+    o.call("step3d_t")
+    m.step3d_t()
+    m.sync()
+    assert full(m.get("t"), o.field("t")) <= RTOL_ROUTINE
+    m.close()
+    o2, m2 = make_pair(cfg)
+    o2.set_ub(ub)
+    m2.set_ub_tune(ub)
+    o2.step(20)
+    m2.step(20)
+    a, b = m2.get("t"), o2.field("t")
+    assert float(np.sqrt(np.mean((a - b) ** 2))) / max(1.0, float(np.sqrt(np.mean(b ** 2)))) < RMS_RUN
+    m2.close()
+
+
+def test_sponge_tune_limits():
+    """ub <= 0 leaves the Orlanski rate unchanged (bitwise equal to ub_tune
+    off); ub >= 1 pins the boundary tracers to the boundary data."""
+    cfg = obc_cfg(obc=15)
+    m = romsgpu.Model.from_case(cfg.case_id, cfg.LLm, cfg.MMm, cfg.N, cfg.NT, salinity=True, nonlin_eos=True,
+                                dt=cfg.dt, ndtfast=cfg.ndtfast, sizex=cfg.sizex, sizey=cfg.sizey, obc=15,
+                                v_sponge=cfg.v_sponge, island=True)
+    m.step(8)
+    off = m.get("t")
+    m.close()
+    m = romsgpu.Model.from_case(cfg.case_id, cfg.LLm, cfg.MMm, cfg.N, cfg.NT, salinity=True, nonlin_eos=True,
+                                dt=cfg.dt, ndtfast=cfg.ndtfast, sizex=cfg.sizex, sizey=cfg.sizey, obc=15,
+                                v_sponge=cfg.v_sponge, island=True)
+    m.set_ub_tune([-np.ones(cfg.MMm + 2), np.zeros(cfg.MMm + 2), -np.ones(cfg.LLm + 2), np.zeros(cfg.LLm + 2)])
+    m.step(8)
+    assert np.array_equal(m.get("t"), off)
+    m.set_ub_tune([5 * np.ones(cfg.MMm + 2)] * 2 + [5 * np.ones(cfg.LLm + 2)] * 2)
+    m.step(1)
+    t = m.get("t").reshape(cfg.NT, 3, cfg.N, cfg.MMm + 4, cfg.LLm + 4)[:, m.t.nnew - 1]
+    tw = m.get("t_west").reshape(cfg.NT, cfg.N, cfg.MMm + 2)
+    rm = m.get("rmask")[0]
+    j = np.arange(1, cfg.MMm + 1)
+    assert np.array_equal(t[:, :, j + 1, 1], tw[:, :, j] * rm[j + 1, 1])   # western ghost column i = 0
+    m.close()

@@ -259,6 +259,7 @@ __global__ void __launch_bounds__(256) k_t3dbc_obc(Dev d, int nnew, int nstp, in
         double cext;
         val = orl_tangential(cx, cy, T(is - 1, j, nstp), T(is, j, nstp), gr(is - 1, j), gr(is - 1, j + 1), gr(is, j),
                              gr(is, j + 1), cext);
+        if (F.ub[0]) cext = fmax(cext, fmin(F.ub[0][j], 1.0));   // SPONGE_TUNE ub_west (t3dbc_im.F:73-74)
         val = (1. - cext) * val + cext * F.bt[0][j + (long)nbry(b, 0) * nbk];
         val = val * rm(is - 1, j);
       } else {
@@ -275,6 +276,7 @@ __global__ void __launch_bounds__(256) k_t3dbc_obc(Dev d, int nnew, int nstp, in
         // the interior term reads t(iend,nnew) (t3dbc_im.F:133)
         val = orl_tangential(cx, cy, T(ie + 1, j, nstp), T(ie, j, nnew), gr(ie + 1, j), gr(ie + 1, j + 1), gr(ie, j),
                              gr(ie, j + 1), cext);
+        if (F.ub[1]) cext = fmax(cext, fmin(F.ub[1][j], 1.0));   // SPONGE_TUNE ub_east (t3dbc_im.F:73-74)
         val = (1. - cext) * val + cext * F.bt[1][j + (long)nbry(b, 1) * nbk];
         val = val * rm(ie + 1, j);
       } else {
@@ -293,6 +295,7 @@ __global__ void __launch_bounds__(256) k_t3dbc_obc(Dev d, int nnew, int nstp, in
         double cext;
         val = orl_tangential(cx, cy, T(i, js - 1, nstp), T(i, js, nstp), gr(i, js - 1), gr(i + 1, js - 1), gr(i, js),
                              gr(i + 1, js), cext);
+        if (F.ub[2]) cext = fmax(cext, fmin(F.ub[2][i], 1.0));   // SPONGE_TUNE ub_south (t3dbc_im.F:73-74)
         val = (1. - cext) * val + cext * F.bt[2][i + (long)nbry(b, 2) * nbk];
         val = val * rm(i, js - 1);
       } else {
@@ -309,6 +312,7 @@ __global__ void __launch_bounds__(256) k_t3dbc_obc(Dev d, int nnew, int nstp, in
         // the interior term reads t(jend,nnew) (t3dbc_im.F:276)
         val = orl_tangential(cx, cy, T(i, je + 1, nstp), T(i, je, nnew), gr(i, je + 1), gr(i + 1, je + 1), gr(i, je),
                              gr(i + 1, je), cext);
+        if (F.ub[3]) cext = fmax(cext, fmin(F.ub[3][i], 1.0));   // SPONGE_TUNE ub_north (t3dbc_im.F:73-74)
         val = (1. - cext) * val + cext * F.bt[3][i + (long)nbry(b, 3) * nbk];
         val = val * rm(i, je + 1);
       } else {

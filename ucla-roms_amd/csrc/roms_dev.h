@@ -92,6 +92,7 @@ struct Fields {
   // boundary.F open-boundary data, [0] west, [1] east (index j, 0:Mm+1),
   // [2] south, [3] north (index i, 0:Lm+1); u, v (.,N); t (.,N,NT)
   double *bzeta[4], *bubar[4], *bvbar[4], *bu[4], *bv[4], *bt[4];
+  double* ub[4];   // SPONGE_TUNE ub_west/east/south/north (sponge_tune.F; nullptr: ub_tune off)
   // column-solver scratch in global memory, 2*max(NT,2) slots of (0:N) levels
   // (nullptr: the solvers keep their columns in LDS; see ColGlb in k_common.h)
   double* colscr;

@@ -227,6 +227,8 @@ void free_all() {
   g.scratch.clear();
   if (g.d.f.pipe_idx) { (void)hipFree(g.d.f.pipe_idx); g.d.f.pipe_idx = nullptr; }
   if (g.d.f.riv_face) { (void)hipFree(g.d.f.riv_face); g.d.f.riv_face = nullptr; }
+  for (double*& p : g.d.f.ub)
+    if (p) { (void)hipFree(p); p = nullptr; }
   if (g.h_diag) { (void)hipHostFree(g.h_diag); g.h_diag = nullptr; }
   if (g.d_diag) { (void)hipFree(g.d_diag); g.d_diag = nullptr; }
   if (g.s) { (void)hipStreamDestroy(g.s); g.s = nullptr; }
@@ -701,6 +703,27 @@ int roms_gpu_set_river_frc(int nriv, const double* riv_uflx, const double* riv_v
   CHECK_HIP(hipMemcpy(F.riv_vol, riv_vol, (size_t)nriv * sizeof(double), hipMemcpyHostToDevice));
   CHECK_HIP(hipMemcpy(F.riv_trc, riv_trc, (size_t)nriv * b.NT * sizeof(double), hipMemcpyHostToDevice));
   g.d.p.nriv = nriv;
+  return 0;
+}
+
+int roms_gpu_set_ub_tune(const double* ub_west, const double* ub_east, const double* ub_south, const double* ub_north) {
+  REQUIRE_INIT();
+  const double* src[4] = {ub_west, ub_east, ub_south, ub_north};
+  const Bounds& b = g.d.b;
+  // graphs captured with other ub pointers would keep using them
+  for (auto& kv : g.graphs) (void)hipGraphExecDestroy(kv.second);
+  g.graphs.clear();
+  for (int q = 0; q < 4; q++) {
+    double*& p = g.d.f.ub[q];
+    if (!src[q]) {
+      if (p) { CHECK_HIP(hipStreamSynchronize(g.s)); (void)hipFree(p); p = nullptr; }
+      continue;
+    }
+    const long n = q < 2 ? b.Mm + 2 : b.Lm + 2;
+    if (!p) CHECK_HIP(hipMalloc(&p, (size_t)n * sizeof(double)));
+    CHECK_HIP(hipMemcpyAsync(p, src[q], (size_t)n * sizeof(double), hipMemcpyHostToDevice, g.s));
+  }
+  CHECK_HIP(hipStreamSynchronize(g.s));
   return 0;
 }
 

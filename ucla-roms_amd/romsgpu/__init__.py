@@ -112,6 +112,7 @@ def load_library(path=LIB_PATH):
     L.roms_gpu_set_river_frc.argtypes = [ctypes.c_int, P(ctypes.c_double), P(ctypes.c_double), P(ctypes.c_double),
                                          P(ctypes.c_double)]
     L.roms_gpu_bulk_flux.argtypes = [P(Tlev)]
+    L.roms_gpu_set_ub_tune.argtypes = [P(ctypes.c_double)] * 4
     L.roms_gpu_diag.argtypes = [P(Tlev), P(ctypes.c_double)]
     L.roms_gpu_time_steps.argtypes = [P(Tlev), ctypes.c_int, P(ctypes.c_double)]
     L.roms_gpu_stream.restype = ctypes.c_void_p
@@ -354,6 +355,13 @@ class Model:
         self._chk(self.L.roms_gpu_set_river_frc(nriv, uf.ctypes.data_as(D) if uf is not None else None,
                                                 vf.ctypes.data_as(D) if vf is not None else None,
                                                 vol.ctypes.data_as(D), trc.ctypes.data_as(D)), "set_river_frc")
+
+    def set_ub_tune(self, ub):
+        """SPONGE_TUNE: ub_west, ub_east (Mm+2), ub_south, ub_north (Lm+2); None = edge off."""
+        D = ctypes.POINTER(ctypes.c_double)
+        keep = [None if a is None else np.ascontiguousarray(a, dtype=np.float64) for a in ub]
+        self._chk(self.L.roms_gpu_set_ub_tune(*[None if a is None else a.ctypes.data_as(D) for a in keep]),
+                  "set_ub_tune")
 
     def bulk_flux(self):
         """set_bulk_frc -> calc_all_bulk_forces on the device at the current nrhs."""
