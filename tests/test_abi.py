@@ -78,3 +78,14 @@ def test_uninitialised_calls_fail_loudly():
     m = romsgpu.Model()
     with pytest.raises(romsgpu.RomsGpuError):
         m.omega()
+
+
+def test_fortran_module_abi_version_matches_header():
+    """fortran/roms_gpu_mod.F90's ROMS_GPU_ABI must follow ROMS_GPU_ABI_VERSION."""
+    import re
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    h = open(os.path.join(root, "include", "roms_gpu.h")).read()
+    f = open(os.path.join(root, "fortran", "roms_gpu_mod.F90")).read()
+    vh = int(re.search(r"#define ROMS_GPU_ABI_VERSION (\d+)", h).group(1))
+    vf = int(re.search(r"ROMS_GPU_ABI = (\d+)", f).group(1))
+    assert vh == vf

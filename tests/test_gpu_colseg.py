@@ -92,3 +92,32 @@ def test_seg_run_rms(case):
     m.step(30)
     check_fields(o, m, PROGNOSTIC, cfg.LLm, cfg.MMm, RMS_RUN, kind="rms")
     m.close()
+
+
+def _run_colreg(cfg, mask, nsteps):
+    old = os.environ.get("ROMS_GPU_COLREG")
+    os.environ["ROMS_GPU_COLREG"] = str(mask)
+    try:
+        m = make_model(cfg, 0)
+    finally:
+        if old is None:
+            del os.environ["ROMS_GPU_COLREG"]
+        else:
+            os.environ["ROMS_GPU_COLREG"] = old
+    m.step(nsteps)
+    out = {n: m.get(n) for n in ("zeta", "ubar", "vbar", "u", "v", "t", "ru", "rv", "rufrc", "rvfrc", "FlxU", "We")}
+    m.close()
+    return out
+
+
+@pytest.mark.parametrize("lmd", [0, oracle.LMD_ALL])
+def test_register_column_kernels_bitwise(lmd):
+    """N = 50 register-resident column solvers (k_uv1_reg, k_pre_tracer_v_reg:
+    ROMS_GPU_COLREG bits 1, 2) keep the sequential LDS solvers' expressions
+    and order: 12 steps equal the LDS forms bitwise."""
+    cfg = seg_cfg("n50")
+    cfg.lmd, cfg.surf_flux = lmd, int(lmd != 0)
+    a = _run_colreg(cfg, 0, 12)
+    b = _run_colreg(cfg, 3, 12)
+    for n in a:
+        assert np.array_equal(a[n], b[n]), n

@@ -26,6 +26,8 @@ The OBC/SPONGE/CURVGRID branches of the oracle have no runnable golden log
 offline (test_gpu_obc.py): "parity unpinned" there; everything else is
 pinned through the Filament / Pipes_ana goldens (test_oracle_golden.py).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -60,6 +62,10 @@ def test_c2_filament_salinity_100_steps():
     o.step(100)
     m.step(100)
     m.sync()
+    dump = os.environ.get("ROMS_TEST_DUMP")
+    if dump:   # debugging aid: both sides' fields of this run
+        np.savez(dump, **{"gpu_" + n: m.get(n) for n in ("zeta", "u", "v", "t")},
+                 **{"orc_" + n: o.field(n) for n in ("zeta", "u", "v", "t")})
     assert o.tindex() == m.t.as_list()
     check_fields(o, m, PROGNOSTIC, 64, 64, RMS_RUN, kind="rms")
     # both tracers moved and stayed distinct (S is really advected)

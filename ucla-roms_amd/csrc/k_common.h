@@ -10,6 +10,7 @@
 // index clamps at closed (non-periodic) physical edges.
 #pragma once
 #include "roms_dev.h"
+#include <type_traits>
 
 namespace roms {
 
@@ -30,6 +31,16 @@ __device__ __forceinline__ ColLds col_lds(int slot, int N) {
   return ColLds{roms_smem + (long)slot * (N + 1) * kCX + threadIdx.x};
 }
 inline size_t col_lds_bytes(int nslots, int N) { return (size_t)nslots * (N + 1) * kCX * sizeof(double); }
+// Debug builds (-DROMS_LDS_POISON): every lane fills its column slots with NaN
+// at kernel entry, so a read of a slot the kernel never wrote shows up as NaN
+// instead of whatever an earlier dispatch left in LDS.
+template <class C>
+__device__ __forceinline__ void col_lds_poison(int nslots, int N) {
+#ifdef ROMS_LDS_POISON
+  if constexpr (std::is_same<C, ColLds>::value)
+    for (int q = 0; q < nslots * (N + 1); q++) roms_smem[q * kCX + threadIdx.x] = __builtin_nan("");
+#endif
+}
 
 // The same column scratch in global memory (w-point layout, level k of column
 // ij at p[k*n2]: a wavefront still touches 64 consecutive doubles per level).
@@ -131,6 +142,40 @@ __device__ __forceinline__ void tracer_spline_lds(int N, long n2, const double* 
       }
       for (int k = k1; k >= 0; k--) spl_bwd(k, We[(long)(k + 1) * n2]);
     }
+  A[N] = 0.0;
+  A[0] = 0.0;
+}
+
+// ---- register-resident form of tracer_spline_lds for a compile-time depth
+// NN (the k_uv1_reg pattern): FC lives in A[0..NN] (VGPRs), CF in one LDS
+// slot B, and every level loop is fully unrolled so each A[k] is a fixed
+// register and the compiler schedules the (alias-free) global loads ahead.
+// Same expressions and order as tracer_spline_lds: bit-identical results. ----
+template <int NN, class CB>
+__device__ __forceinline__ void tracer_spline_reg(long n2, const double* __restrict__ Hz,
+                                                  const double* __restrict__ Tr, const double* __restrict__ We,
+                                                  double (&A)[NN + 1], const CB& B) {
+  constexpr int N = NN;
+  double cfk = 1.0, fcm = 2.0 * Tr[0], hk = Hz[0], tk = Tr[0];
+  A[0] = fcm;
+#pragma unroll
+  for (int k = 1; k <= N - 1; k++) {
+    const double hk1 = Hz[(long)k * n2], tk1 = Tr[(long)k * n2];
+    const double cff = 1.0 / (2.0 * hk + hk1 * (2.0 - cfk));
+    const double cf1 = cff * hk;
+    const double fck = cff * (3.0 * (hk * tk1 + hk1 * tk) - hk1 * fcm);
+    B[k + 1] = cf1;
+    A[k] = fck;
+    cfk = cf1; fcm = fck; hk = hk1; tk = tk1;
+  }
+  double fc1 = (2.0 * tk - fcm) / (1.0 - cfk);
+#pragma unroll
+  for (int k = N - 1; k >= 0; k--) {
+    const double fck = A[k] - B[k + 1] * fc1;
+    A[k + 1] = fc1 * We[(long)(k + 1) * n2];
+    A[k] = fck;
+    fc1 = fck;
+  }
   A[N] = 0.0;
   A[0] = 0.0;
 }
@@ -504,6 +549,58 @@ __device__ __forceinline__ void uv_vert_flux_lds(const Dev& d, long ij, int nrhs
   A[0] = 0.0;
   A[N] = 0.0;
 }
+// ---- SPLINE_UV flux of a u (dir 0) / v (dir 1) column for a compile-time
+// depth NN: FC in registers A[0..NN], CF in one LDS slot B; on exit A[k] is
+// the vertical advective flux at w-level k (A[0] = A[N] = 0), exactly as
+// uv_vert_flux_lds leaves it.  Used by k_uv1_reg and k_pre_uv_reg. ----
+template <int NN>
+__device__ __forceinline__ void uv_spline_reg(const Dev& d, long ij, int nrhs, int dir, double (&A)[NN + 1],
+                                              const ColLds& B) {
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  constexpr int N = NN;
+  const long n2 = b.n2;
+  const long s = dir == 0 ? 1 : b.nx2;
+  if (!d.p.uv_adv) {
+#pragma unroll
+    for (int k = 0; k <= N; k++) A[k] = 0.0;
+  } else {
+    const double* __restrict__ Uv = (dir == 0 ? F.u : F.v) + (long)(nrhs - 1) * b.n3 + ij;
+    const double* __restrict__ Hz = F.Hz + ij;
+    const double* __restrict__ We = F.We + ij;
+    const double* mask = dir == 0 ? F.umask : F.vmask;
+    auto DCk = [&](int k) {
+      const long o = (long)(k - 1) * n2;
+      return 0.5625 * (Hz[o] + Hz[o - s]) - 0.0625 * (Hz[o + s] + Hz[o - 2 * s]);
+    };
+    double dck = DCk(1), cfk = 1.0, fcm = 2.0 * Uv[0], uk = Uv[0];
+#pragma unroll
+    for (int k = 1; k <= N - 1; k++) {
+      const double dc1 = DCk(k + 1), uk1 = Uv[(long)k * n2];
+      const double cff = 1.0 / (2.0 * dck + dc1 * (2.0 - cfk));
+      const double cf1 = cff * dck;
+      const double fck = cff * (3.0 * (dck * uk1 + dc1 * uk) - dc1 * fcm);
+      B[k + 1] = cf1;
+      A[k] = fck;
+      dck = dc1; cfk = cf1; fcm = fck; uk = uk1;
+      ROMS_LEVEL_FENCE_AT(k);
+    }
+    double fc1 = (2.0 * Uv[(long)(N - 1) * n2] - fcm) / (1.0 - cfk);  // FC(N)
+    const double m1 = mask[ij + s], m0 = mask[ij - s];
+#pragma unroll
+    for (int k = N - 1; k >= 1; k--) {
+      const long w = (long)k * n2;
+      const double wf = We[w] + We[w - s] - 0.125 * ((We[w + s] - We[w]) * m1 - (We[w - s] - We[w - 2 * s]) * m0);
+      const double fck = A[k] - B[k + 1] * fc1;
+      A[k] = fck * 0.5 * wf;
+      fc1 = fck;
+      ROMS_LEVEL_FENCE_AT(k);
+    }
+    A[0] = 0.0;
+    A[N] = 0.0;
+  }
+}
+
 template <class C>
 __device__ __forceinline__ double uv_rr_update(double r, const C& A, int k) {
   return k == 1 ? r - A[1] : r - A[k] + A[k - 1];

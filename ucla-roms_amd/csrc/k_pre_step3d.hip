@@ -63,6 +63,7 @@ __global__ void __launch_bounds__(256) k_pre_tracer_h(Dev d, Range R, PreCoef c,
 template <class C>
 __global__ void __launch_bounds__(64) k_pre_tracer_v(Dev d, Range R, PreCoef c, int nnew, int nrhs) {
   ROMS_IJC_OR_RETURN(R)
+  col_lds_poison<C>(2, d.b.N);
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const int N = b.N;
@@ -134,6 +135,65 @@ __global__ void __launch_bounds__(64) k_pre_tracer_v(Dev d, Range R, PreCoef c, 
       tt = A[k - 1] + B[k] * tt;
       Tn[(long)(k - 1) * n2] = tt;
     }
+  }
+}
+
+// ---- register-resident k_pre_tracer_v for a compile-time depth NN: the
+// FC/DC column in VGPRs, CF in one LDS slot (26 KB per wave at N = 50, six
+// waves per CU instead of three); fully unrolled, same expressions and order,
+// bit-identical. ----
+template <int NN>
+__global__ void __launch_bounds__(64, 2) k_pre_tracer_v_reg(Dev d, Range R, PreCoef c, int nnew, int nrhs) {
+  ROMS_IJC_OR_RETURN(R)
+  col_lds_poison<ColLds>(1, NN);
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  constexpr int N = NN;
+  const long n2 = b.n2, ij = IJ(b, i, j);
+  const double* __restrict__ Hz = F.Hz + ij;
+  const double* __restrict__ We = F.We + ij;
+  const double* __restrict__ Wi = F.Wi + ij;
+  const double* __restrict__ Hf = F.c2 + ij;
+  const ColLds B = col_lds(0, N);
+  double A[N + 1];
+  const int itrc = 1 + (int)bI.z;
+  const long tb = (long)(itrc - 1) * 3 * b.n3;
+  const double* __restrict__ Tr = F.t + (long)(nrhs - 1) * b.n3 + tb + ij;
+  double* __restrict__ Tn = F.t + (long)(nnew - 1) * b.n3 + tb + ij;
+  tracer_spline_reg<N>(n2, Hz, Tr, We, A, B);
+  const double pm = F.pm[ij], pn = F.pn[ij];
+  auto tval = [&](int k) { return Tn[(long)(k - 1) * n2] - c.dtau * pm * pn * (A[k] - A[k - 1]); };
+  const int iAkt = itrc < b.nTS ? itrc : b.nTS;
+  const double* __restrict__ Akt = F.Akt + (long)(iAkt - 1) * b.n3w + ij;
+  const double DC0 = c.dtau * pm * pn;
+  const double hf1 = Hf[0];
+  double hfk = Hf[n2];
+  double FCk = 2.0 * c.dtau * Akt[n2] / (hfk + hf1);
+  double WCk = DC0 * Wi[n2];
+  double cff = 1.0 / (hf1 + FCk + fmax0(WCk));
+  double CFk = cff * (FCk - fmin0(WCk));
+  double DCk = cff * tval(1);
+  B[1] = CFk;
+  A[0] = DCk;
+#pragma unroll
+  for (int k = 2; k <= N - 1; k++) {
+    const double hfk1 = Hf[(long)k * n2];
+    const double FCn = 2.0 * c.dtau * Akt[(long)k * n2] / (hfk1 + hfk);
+    const double WCn = DC0 * Wi[(long)k * n2];
+    cff = 1.0 / (hfk + FCn + fmax0(WCn) + FCk - fmin0(WCk) - CFk * (FCk + fmax0(WCk)));
+    const double CFn = cff * (FCn - fmin0(WCn));
+    const double DCn = cff * (tval(k) + DCk * (FCk + fmax0(WCk)));
+    B[k] = CFn;
+    A[k - 1] = DCn;
+    FCk = FCn; WCk = WCn; CFk = CFn; DCk = DCn; hfk = hfk1;
+  }
+  const long oN = (long)(N - 1) * n2;
+  double tt = (tval(N) + DCk * (FCk + fmax0(WCk))) / (hfk + FCk - fmin0(WCk) - CFk * (FCk + fmax0(WCk)));
+  Tn[oN] = tt;
+#pragma unroll
+  for (int k = N - 1; k >= 1; k--) {
+    tt = A[k - 1] + B[k] * tt;
+    Tn[(long)(k - 1) * n2] = tt;
   }
 }
 
@@ -267,6 +327,7 @@ __device__ __forceinline__ void pre_uv_col(const Dev& d, int i, int j, int dir, 
 template <class C>
 __global__ void __launch_bounds__(64) k_pre_uv(Dev d, Range R, PreCoef c, int nstp, int nnew, int nrhs) {
   ROMS_IJC_OR_RETURN(R)
+  col_lds_poison<C>(2, d.b.N);
   const Bounds& b = d.b;
   const long ij = IJ(b, i, j);
   const C A = ColMake<C>::at(d, 0, (int)bI.z, ij), B = ColMake<C>::at(d, 1, (int)bI.z, ij);
@@ -456,6 +517,8 @@ void launch_pre_step3d(const Dev& d, hipStream_t s, const Tlev& t) {
   if (d.p.colseg)
     hipLaunchKernelGGL(k_pre_tracer_seg, seg_grid_of(RI, b.NT), dim3(kCX, seg_waves(b.N)), 0, s, d, RI, c, t.nnew,
                        t.nrhs);
+  else if ((d.p.colreg & 2) && b.N == 50 && !d.f.colscr)
+    hipLaunchKernelGGL(k_pre_tracer_v_reg<50>, gt, dim3(kCX), col_lds_bytes(1, 50), s, d, RI, c, t.nnew, t.nrhs);
   else if (d.f.colscr)
     hipLaunchKernelGGL(k_pre_tracer_v<ColGlb>, gt, dim3(kCX), 0, s, d, RI, c, t.nnew, t.nrhs);
   else

@@ -45,6 +45,7 @@ __global__ void __launch_bounds__(256) k_step3d_t_h(Dev d, Range R, int nnew, in
 template <class C>
 __global__ void __launch_bounds__(64) k_step3d_t_v(Dev d, Range R, int nnew, int nrhs) {
   ROMS_IJC_OR_RETURN(R)
+  col_lds_poison<C>(2, d.b.N);
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const Params& P = d.p;
@@ -147,6 +148,9 @@ __global__ void __launch_bounds__(64) k_step3d_t_v(Dev d, Range R, int nnew, int
   }
 }
 
+// ---- register-resident k_step3d_t_v for a compile-time depth NN (FC/DC
+// column in VGPRs, CF in one LDS slot: six waves per CU at N = 50 instead of
+// three); fully unrolled, same expressions and order, bit-identical. ----
 // ---- segment-partitioned variant of k_step3d_t_v (k_colseg.h): block =
 // 64 columns x S segment wavefronts, one tracer per grid z.  The spline
 // interface values FC(0:N) and the implicit diffusion are each solved as one

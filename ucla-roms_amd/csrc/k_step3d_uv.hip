@@ -75,6 +75,7 @@ __device__ __forceinline__ void uv1_col(const Dev& d, int i, int j, int dir, int
 template <class C>
 __global__ void __launch_bounds__(64) k_uv1(Dev d, Range R, int nnew, int nrhs) {
   ROMS_IJC_OR_RETURN(R)
+  col_lds_poison<C>(2, d.b.N);
   const Bounds& b = d.b;
   const long ij = IJ(b, i, j);
   const C A = ColMake<C>::at(d, 0, (int)bI.z, ij), B = ColMake<C>::at(d, 1, (int)bI.z, ij);
@@ -92,9 +93,11 @@ __global__ void __launch_bounds__(64) k_uv1(Dev d, Range R, int nnew, int nrhs) 
 // wave doubles the resident waves (6 per CU against 3 for the two-slot LDS
 // form at N = 50; both columns in VGPRs would spill).  Same expressions and
 // order as uv_vert_flux_lds<false> + uv1_col, so results are bit-identical. ----
+constexpr int kUv1Chunk = 5;
 template <int NN>
 __global__ void __launch_bounds__(64, 2) k_uv1_reg(Dev d, Range R, int nnew, int nrhs) {
   ROMS_IJC_OR_RETURN(R)
+  col_lds_poison<ColLds>(1, NN);
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const int dir = (int)bI.z;
@@ -105,45 +108,7 @@ __global__ void __launch_bounds__(64, 2) k_uv1_reg(Dev d, Range R, int nnew, int
   const long s = dir == 0 ? 1 : b.nx2;
   double A[N + 1];               // registers
   const ColLds B = col_lds(0, N);  // LDS: 26 KB per wave at N = 50
-  // SPLINE_UV vertical flux (compute_vert_rhs_uv_terms.h), as uv_vert_flux_lds
-  if (!d.p.uv_adv) {
-#pragma unroll
-    for (int k = 0; k <= N; k++) A[k] = 0.0;
-  } else {
-    const double* __restrict__ Uv = (dir == 0 ? F.u : F.v) + (long)(nrhs - 1) * b.n3 + ij;
-    const double* __restrict__ Hz = F.Hz + ij;
-    const double* __restrict__ We = F.We + ij;
-    const double* mask = dir == 0 ? F.umask : F.vmask;
-    auto DCk = [&](int k) {
-      const long o = (long)(k - 1) * n2;
-      return 0.5625 * (Hz[o] + Hz[o - s]) - 0.0625 * (Hz[o + s] + Hz[o - 2 * s]);
-    };
-    double dck = DCk(1), cfk = 1.0, fcm = 2.0 * Uv[0], uk = Uv[0];
-#pragma unroll
-    for (int k = 1; k <= N - 1; k++) {
-      const double dc1 = DCk(k + 1), uk1 = Uv[(long)k * n2];
-      const double cff = 1.0 / (2.0 * dck + dc1 * (2.0 - cfk));
-      const double cf1 = cff * dck;
-      const double fck = cff * (3.0 * (dck * uk1 + dc1 * uk) - dc1 * fcm);
-      B[k + 1] = cf1;
-      A[k] = fck;
-      dck = dc1; cfk = cf1; fcm = fck; uk = uk1;
-      ROMS_LEVEL_FENCE_AT(k);
-    }
-    double fc1 = (2.0 * Uv[(long)(N - 1) * n2] - fcm) / (1.0 - cfk);  // FC(N)
-    const double m1 = mask[ij + s], m0 = mask[ij - s];
-#pragma unroll
-    for (int k = N - 1; k >= 1; k--) {
-      const long w = (long)k * n2;
-      const double wf = We[w] + We[w - s] - 0.125 * ((We[w + s] - We[w]) * m1 - (We[w - s] - We[w - 2 * s]) * m0);
-      const double fck = A[k] - B[k + 1] * fc1;
-      A[k] = fck * 0.5 * wf;
-      fc1 = fck;
-      ROMS_LEVEL_FENCE_AT(k);
-    }
-    A[0] = 0.0;
-    A[N] = 0.0;
-  }
+  uv_spline_reg<N>(d, ij, nrhs, dir, A, B);
   double* __restrict__ Un = (dir == 0 ? F.u : F.v) + (long)(nnew - 1) * b.n3 + ij;
   double* __restrict__ rr = (dir == 0 ? F.ru : F.rv) + ij;
   const double* Hz = F.Hz + ij;
@@ -154,18 +119,35 @@ __global__ void __launch_bounds__(64, 2) k_uv1_reg(Dev d, Range R, int nnew, int
   const double DC0 = dt * 0.25 * (F.pm[ij] + F.pm[ij - s]) * (F.pn[ij] + F.pn[ij - s]);
   auto hz = [&](int k) { return Hz[(long)(k - 1) * n2]; };
   auto hzm = [&](int k) { return Hz[(long)(k - 1) * n2 - s]; };
-  auto rk = [&](int k) {  // final ru(k): vertical advection added, stored back
-    const long o = (long)(k - 1) * n2;
-    const double r = k == 1 ? rr[o] - A[1] : rr[o] - A[k] + A[k - 1];
-    rr[o] = r;
-    return r;
-  };
+  // pre-pass, k ascending, in chunks whose loads all precede their ru stores
+  // (inside the elimination every later ru load had to wait behind the
+  // previous level's store, may-alias): final ru(k) stored back, the Thomas
+  // right-hand side v(k) = u(nnew) + DC0*ru(k) kept in A[k-1] (A[k-1] is last
+  // read by ru(k)); ru(1) kept for rufrc.
+  double r1 = 0.0;
+#pragma unroll
+  for (int k0 = 1; k0 <= N; k0 += kUv1Chunk) {
+    double r_[kUv1Chunk], un_[kUv1Chunk];
+#pragma unroll
+    for (int q = 0; q < kUv1Chunk; q++) {
+      const long o = (long)(k0 + q - 1) * n2;
+      r_[q] = rr[o]; un_[q] = Un[o];
+    }
+#pragma unroll
+    for (int q = 0; q < kUv1Chunk; q++) {
+      const int k = k0 + q;
+      const double r = k == 1 ? r_[q] - A[1] : r_[q] - A[k] + A[k - 1];
+      rr[(long)(k - 1) * n2] = r;
+      if (k == 1) r1 = r;
+      A[k - 1] = un_[q] + DC0 * r;
+    }
+  }
   double FCk = 2.0 * dt * (Akv[(long)(N - 1) * n2] + Akv[(long)(N - 1) * n2 - s]) /
                (hz(N) + hzm(N) + hz(N - 1) + hzm(N - 1));
   double WCk = DC0 * 0.5 * (Wi[(long)(N - 1) * n2] + Wi[(long)(N - 1) * n2 - s]);
   double cff = 1.0 / (0.5 * (hz(N) + hzm(N)) + FCk - fmin0(WCk));
   double CFk = cff * (FCk + fmax0(WCk));
-  double DCk1 = cff * (Un[(long)(N - 1) * n2] + DC0 * rk(N) + dt * sstr);
+  double DCk1 = cff * (A[N - 1] + dt * sstr);
   A[N] = DCk1;
   B[N - 1] = CFk;
 #pragma unroll
@@ -175,15 +157,14 @@ __global__ void __launch_bounds__(64, 2) k_uv1_reg(Dev d, Range R, int nnew, int
     const double WCl = DC0 * 0.5 * (Wi[(long)(k - 1) * n2] + Wi[(long)(k - 1) * n2 - s]);
     cff = 1.0 / (0.5 * (hz(k) + hzm(k)) + FCl - fmin0(WCl) + FCk + fmax0(WCk) - CFk * (FCk - fmin0(WCk)));
     const double CFl = cff * (FCl + fmax0(WCl));
-    const double DCk = cff * (Un[(long)(k - 1) * n2] + DC0 * rk(k) + DCk1 * (FCk - fmin0(WCk)));
+    const double DCk = cff * (A[k - 1] + DCk1 * (FCk - fmin0(WCk)));
     B[k - 1] = CFl;
     A[k] = DCk;
     DCk1 = DCk; FCk = FCl; WCk = WCl; CFk = CFl;
     ROMS_LEVEL_FENCE_AT(k);
   }
   const double rD = F.r_D[ij], rDm = F.r_D[ij - s];
-  const double r1 = rk(1);
-  double dc = (Un[0] + DC0 * r1 + DCk1 * (FCk - fmin0(WCk))) /
+  double dc = (A[0] + DCk1 * (FCk - fmin0(WCk))) /
               (0.5 * (hz(1) + hzm(1)) + 0.5 * dt * (rD + rDm) + FCk + fmax0(WCk) - CFk * (FCk - fmin0(WCk)));
   Un[0] = dc * 0.5 * (hz(1) + hzm(1));
   const double dmdn = dir == 0 ? F.dm_u[ij] * F.dn_u[ij] : F.dm_v[ij] * F.dn_v[ij];
@@ -303,7 +284,7 @@ void launch_step3d_uv1(const Dev& d, hipStream_t s, const Tlev& t) {
   Range R{b.istr, b.iend, b.jstr, b.jend};
   dim3 g = gridc_of(R);
   g.z = 2;
-  if (d.p.colreg && b.N == 50)
+  if ((d.p.colreg & 1) && b.N == 50)
     hipLaunchKernelGGL(k_uv1_reg<50>, g, dim3(kCX), col_lds_bytes(1, 50), s, d, R, t.nnew, t.nrhs);
   else if (d.p.colseg)
     hipLaunchKernelGGL(k_uv1_seg, seg_grid_of(R, 2), dim3(kCX, seg_waves(b.N)), 0, s, d, R, t.nnew, t.nrhs);

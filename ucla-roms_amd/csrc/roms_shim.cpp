@@ -52,6 +52,11 @@ struct Ctx {
   std::vector<hipEvent_t> ev;
   size_t nev = 0;
   long kcount = 0;   // kernel-level timing: launches covered by the intervals
+  // ROMS_GPU_GUARD=1 (debug): every field and init-time scratch array gets
+  // NaN-filled guard bands before and after it, so an out-of-bounds read
+  // turns into NaN instead of a value of whatever array lies next to it
+  bool guard = false;
+  std::map<double*, double*> guard_base;
 };
 // One context per host thread: a process normally drives one GPU/subdomain
 // from one thread; tests drive several subdomains from threads of one process.
@@ -212,6 +217,25 @@ double** field_slot(Fields& F, int id) {
   return nullptr;
 }
 
+double* dev_base(double* p) {
+  auto it = g.guard_base.find(p);
+  return it == g.guard_base.end() ? p : it->second;
+}
+// zero-initialised device array of n doubles (guard bands when g.guard)
+hipError_t dev_alloc(double*& p, long n) {
+  const long G = g.guard ? 4096 : 0;
+  double* base = nullptr;
+  hipError_t e = hipMalloc(&base, (size_t)(n + 2 * G) * sizeof(double));
+  if (e != hipSuccess) return e;
+  if (G) {
+    e = hipMemsetD32((hipDeviceptr_t)base, 0x7FF87FF8, (size_t)(n + 2 * G) * 2);   // NaN bit pattern
+    if (e != hipSuccess) return e;
+  }
+  p = base + G;
+  if (G) g.guard_base[p] = base;
+  return hipMemset(p, 0, (size_t)n * sizeof(double));
+}
+
 void free_all() {
   io_free();
   for (hipEvent_t e : g.ev) (void)hipEventDestroy(e);
@@ -222,8 +246,9 @@ void free_all() {
   for (auto& kv : g.graphs) (void)hipGraphExecDestroy(kv.second);
   g.graphs.clear();
   for (int id = 0; id < ROMS_NFIELDS; id++)
-    if (g.f[id].d) { (void)hipFree(g.f[id].d); g.f[id] = FieldDesc{}; }
-  for (double* p : g.scratch) (void)hipFree(p);
+    if (g.f[id].d) { (void)hipFree(dev_base(g.f[id].d)); g.f[id] = FieldDesc{}; }
+  for (double* p : g.scratch) (void)hipFree(dev_base(p));
+  g.guard_base.clear();
   g.scratch.clear();
   if (g.d.f.pipe_idx) { (void)hipFree(g.d.f.pipe_idx); g.d.f.pipe_idx = nullptr; }
   if (g.d.f.riv_face) { (void)hipFree(g.d.f.riv_face); g.d.f.riv_face = nullptr; }
@@ -393,10 +418,19 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
   }
   // register-resident sequential solvers (bit-exact) for the depths they are
   // compiled for; ROMS_GPU_COLREG=0 falls back to the LDS form (A/B runs)
-  P.colreg = 1;
+  // bits: 1 step3d_uv1 (k_uv1_reg), 2 pre_step3d tracers (k_pre_tracer_v_reg);
+  // ROMS_GPU_COLREG=<mask> (0: the LDS forms).  Measured at C2 (round 2):
+  // bit 2 pre_step3d 2.06 -> 1.96 ms; bit 1 step3d_uv1 1.24 ms against 1.16
+  // for the LDS form, but the configuration with the LDS form failed the C2
+  // 100-step parity test twice, identically, in one particular test-process
+  // history and is not the default until that is understood;
+  // register forms of pre_uv_col (2.06 -> 2.20 ms) and k_step3d_t_v (its
+  // extra per-level KPP inputs spill at 2 waves/SIMD; 0.84 vs 0.81 ms at 1
+  // wave/SIMD) were slower and are not kept.
+  P.colreg = 1 | 2;
   {
     const char* e = getenv("ROMS_GPU_COLREG");
-    if (e && e[0] == '0') P.colreg = 0;
+    if (e && e[0] >= '0' && e[0] <= '9') P.colreg = atoi(e);
   }
   P.uv2_fused = 1;
   {
@@ -432,19 +466,21 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     return -2;
   }
   CHECK_HIP(hipStreamCreateWithFlags(&g.s, hipStreamNonBlocking));
+  {
+    const char* e = getenv("ROMS_GPU_GUARD");
+    g.guard = e && e[0] == '1';
+  }
   const Bounds& b = g.d.b;
   for (int id = 0; id < ROMS_NFIELDS; id++) {
     const long n = field_count(id, b);
     double* p = nullptr;
-    CHECK_HIP(hipMalloc(&p, (size_t)n * sizeof(double)));
-    CHECK_HIP(hipMemset(p, 0, (size_t)n * sizeof(double)));
+    CHECK_HIP(dev_alloc(p, n));
     g.f[id].d = p;
     g.f[id].count = n;
     *field_slot(g.d.f, id) = p;
   }
   auto scratch = [&](double*& p, long n) -> int {
-    CHECK_HIP(hipMalloc(&p, (size_t)n * sizeof(double)));
-    CHECK_HIP(hipMemset(p, 0, (size_t)n * sizeof(double)));
+    CHECK_HIP(dev_alloc(p, n));
     g.scratch.push_back(p);
     return 0;
   };
@@ -616,7 +652,7 @@ int roms_gpu_set_pipe_frc(int npip, const int* pipe_idx, const double* pipe_flx,
       if (!*q) continue;
       for (size_t k = 0; k < g.scratch.size(); k++)
         if (g.scratch[k] == *q) { g.scratch.erase(g.scratch.begin() + (long)k); break; }
-      (void)hipFree(*q);
+      (void)hipFree(dev_base(*q));
       *q = nullptr;
     }
     g.d.p.npip = 0;
@@ -676,7 +712,7 @@ int roms_gpu_set_river_frc(int nriv, const double* riv_uflx, const double* riv_v
     if (!p) return;
     for (size_t k = 0; k < g.scratch.size(); k++)
       if (g.scratch[k] == p) { g.scratch.erase(g.scratch.begin() + (long)k); break; }
-    (void)hipFree(p);
+    (void)hipFree(dev_base(p));
     p = nullptr;
   };
   auto scratch = [&](double*& p, long n) -> int {
