@@ -23,9 +23,16 @@ ROUTINE_OF = {
     "k_s2d_zetabc": "step2d", "k_s2d_fb": "step2d", "k_visc3d_frc": "visc3d", "k_s2d_edges": "step2d", "k_s2d_last": "step2d", "k_set_depth": "step2d",
     "k_uv2_couple": "step3d_uv2", "k_uv2_flux": "step3d_uv2", "k_step3d_t_h": "step3d_t", "k_step3d_t_v": "step3d_t",
     "k_t3dmix": "t3dmix", "k_step3d_t_seg": "step3d_t", "k_periodic_wrap": "halo", "k_halo_pack": "halo", "k_halo_unpack": "halo",
+    # round-2 kernels: register / segment / chained forms
+    "k_uv1_reg": "step3d_uv1", "k_uv1_seg": "step3d_uv1", "k_pre_tracer_v_reg": "pre_step3d",
+    "k_pre_tracer_seg": "pre_step3d", "k_pre_uv_seg": "pre_step3d", "k_uv2_fused": "step3d_uv2",
+    "k_set_huv1_chain": "set_HUV1", "k_kpp_ext": "lmd_vmix", "k_kpp_int": "lmd_vmix", "k_prsgrd_fused": "prsgrd",
+    "k_bulk_flux": "bulk_flux", "k_t3dbc_edges": "step3d_t", "k_t3dbc_corners": "step3d_t", "k_u3dbc": "step3d_uv2",
+    "k_v3dbc": "step3d_uv2",
 }
 CALLS_PER_STEP = {"rho_eos": 3, "set_HUV": 1, "omega": 3, "prsgrd": 2, "pre_step3d": 1, "set_HUV1": 1,
-                  "step3d_uv1": 1, "visc3d": 1, "step2d": None, "step3d_uv2": 1, "step3d_t": 1, "t3dmix": 1}
+                  "step3d_uv1": 1, "visc3d": 1, "step2d": None, "step3d_uv2": 1, "step3d_t": 1, "t3dmix": 1,
+                  "lmd_vmix": 2, "bulk_flux": 2}
 
 
 def short(name):
