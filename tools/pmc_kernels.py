@@ -9,7 +9,7 @@ import csv
 
 
 def short(n):
-    n = n.split("(")[0]
+    n = n.replace("(anonymous namespace)::", "").split("(")[0]
     return n.replace("void ", "").replace("roms::", "")
 
 

@@ -36,7 +36,7 @@ CALLS_PER_STEP = {"rho_eos": 3, "set_HUV": 1, "omega": 3, "prsgrd": 2, "pre_step
 
 
 def short(name):
-    n = name.split("(")[0].replace("void ", "")
+    n = name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
     return n.split("<")[0].split("::")[-1]
 
 

@@ -31,7 +31,7 @@ def main():
     tot = collections.defaultdict(float)
     cnt = collections.Counter()
     for r in win:
-        name = r["Kernel_Name"].split("(")[0]
+        name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
         tot[name] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
         cnt[name] += 1
     span = (int(win[-1]["End_Timestamp"]) - int(win[0]["Start_Timestamp"])) / 1e3
