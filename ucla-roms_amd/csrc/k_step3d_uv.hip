@@ -238,6 +238,28 @@ __global__ void __launch_bounds__(kSegBlock) k_uv1_seg(Dev d, Range R, int nnew,
     wc = DC0 * 0.5 * (Wi[w] + Wi[w - s]);
   };
   const double rD = F.r_D[ij], rDm = F.r_D[ij - s];
+  // right-hand sides first (all loads of the segment before its ru stores,
+  // which inside the elimination stalled every row: may-alias); ru(k) with
+  // the vertical advection (uv_rr_update) to HBM and LDS, dd = u(nnew) + DC0*ru
+  double rhs[KR];
+  {
+    double r_[KR], un_[KR];
+#pragma unroll
+    for (int p = 0; p < KR; p++)
+      if (p < n) { const long o = cell(c0 + p); r_[p] = rr[o]; un_[p] = Un[o]; }
+#pragma unroll
+    for (int p = 0; p < KR; p++) {
+      if (p < n) {
+        const int k = c0 + p;
+        const double r = k == 1 ? r_[p] - fl[1] : r_[p] - fl[p + 1] + fl[p];
+        if (act) rr[cell(k)] = r;
+        Sr.r[k - 1][sg.col] = r;
+        double v = un_[p] + DC0 * r;
+        if (k == N) v = v + dt * sstr;
+        rhs[p] = v;
+      }
+    }
+  }
   double fcl, wcl;
   fcw(0, fcl, wcl);
   __syncthreads();  // X reused by the second coupling
@@ -246,16 +268,11 @@ __global__ void __launch_bounds__(kSegBlock) k_uv1_seg(Dev d, Range R, int nnew,
     double fcu, wcu;
     fcw(p + 1, fcu, wcu);
     const int k = c0 + p;
-    const long o = cell(k);
     a = -(fcl + fmax0(wcl));
     cc = -(fcu - fmin0(wcu));
     if (k == 1) bb = 0.5 * (hz[p + 1] + hzm[p + 1]) + 0.5 * dt * (rD + rDm) + fcu + fmax0(wcu);
     else bb = 0.5 * (hz[p + 1] + hzm[p + 1]) + fcl - fmin0(wcl) + fcu + fmax0(wcu);
-    const double r = k == 1 ? rr[o] - fl[1] : rr[o] - fl[p + 1] + fl[p];   // uv_rr_update
-    if (act) rr[o] = r;
-    Sr.r[k - 1][sg.col] = r;
-    dd = Un[o] + DC0 * r;
-    if (k == N) dd = dd + dt * sstr;
+    dd = rhs[p];
     fcl = fcu; wcl = wcu;
   });
   double xL, xR;
