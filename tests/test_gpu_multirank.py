@@ -237,3 +237,19 @@ def test_rccl_transport_self_routed_equals_wrap(overlap, transport):
     r = subprocess.run([sys.executable, "-c", RCCL_SCRIPT, ROOT], env=env, capture_output=True, text=True,
                        timeout=300)
     assert r.returncode == 0 and "RCCL_OK" in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
+
+
+def test_rim_first_overlap_bitwise_equals_serial_exchanges():
+    """launch_rim_first (rim strips, exchange forked on the halo stream, interior
+    concurrently; omega, set_HUV, step3d_t, t3dmix) gives the same fields as
+    the serial exchange order (ROMS_GPU_OVERLAP3D=0) on a 2x2 grid."""
+    case = _case("basin_lmd")
+    os.environ["ROMS_GPU_OVERLAP3D"] = "0"
+    try:
+        serial, _ = run_decomposed(case, 2, 2, 6)
+    finally:
+        del os.environ["ROMS_GPU_OVERLAP3D"]
+    over, _ = run_decomposed(case, 2, 2, 6)
+    for r in range(4):
+        for f in FIELDS:
+            assert np.array_equal(serial[r][4][f], over[r][4][f]), (r, f)

@@ -424,6 +424,8 @@ int halo_setup(Halo& H, RomsComm* comm, const HaloPlan& plan, int maxlev, std::s
     // becomes two launches), so it is opt-in: ROMS_GPU_S2D_OVERLAP=1
     const char* e = getenv("ROMS_GPU_S2D_OVERLAP");
     H.overlap = e && e[0] == '1';
+    const char* e3 = getenv("ROMS_GPU_OVERLAP3D");
+    H.overlap3d = !(e3 && e3[0] == '0');
   }
   if (comm && comm->kind == 2) {
     std::lock_guard<std::mutex> lk(comm->grp->m);

@@ -68,6 +68,21 @@ void launch_exchange_list(const Dev& d, hipStream_t s, const ExchList& L) {
   if (nl == 0) return;
   hipLaunchKernelGGL(k_periodic_wrap, dim3((n + 255) / 256, nl), dim3(256), 0, s, b, L);
 }
+bool rim_overlap_on(const Dev& d, const Range& R) {
+  return d.halo && d.halo->comm && d.halo->overlap3d && R.i1 - R.i0 >= 7 && R.j1 - R.j0 >= 7;
+}
+void rim_fork(const Dev& d, hipStream_t s, const ExchList& L) { halo_fork_exchange(*const_cast<Halo*>(d.halo), s, L); }
+void rim_join(const Dev& d, hipStream_t s) { halo_join(*const_cast<Halo*>(d.halo), s); }
+bool tracer_exch_list(const Dev& d, int tlev, ExchList& L) {
+  const Bounds& b = d.b;
+  if (b.NT > 8) return false;
+  L = ExchList{};
+  for (int itrc = 1; itrc <= b.NT; itrc++) {
+    L.p[L.n] = d.f.t + (long)(tlev - 1) * b.n3 + (long)(itrc - 1) * 3 * b.n3;
+    L.nlev[L.n++] = b.N;
+  }
+  return true;
+}
 void launch_exchange_tracers(const Dev& d, hipStream_t s, int tlev) {
   const Bounds& b = d.b;
   ExchList L{};

@@ -148,9 +148,6 @@ __global__ void __launch_bounds__(64) k_step3d_t_v(Dev d, Range R, int nnew, int
   }
 }
 
-// ---- register-resident k_step3d_t_v for a compile-time depth NN (FC/DC
-// column in VGPRs, CF in one LDS slot: six waves per CU at N = 50 instead of
-// three); fully unrolled, same expressions and order, bit-identical. ----
 // ---- segment-partitioned variant of k_step3d_t_v (k_colseg.h): block =
 // 64 columns x S segment wavefronts, one tracer per grid z.  The spline
 // interface values FC(0:N) and the implicit diffusion are each solved as one
@@ -276,19 +273,29 @@ void setup_column_kernels_t(size_t bytes) {
 void launch_step3d_t(const Dev& d, hipStream_t s, const Tlev& t) {
   const Bounds& b = d.b;
   Range R{b.istr, b.iend, b.jstr, b.jend};
-  hipLaunchKernelGGL(k_step3d_t_h, grid3_of(R, b.N), dim3(kBX, kBY), 0, s, d, R, t.nnew, t.nrhs);
-  dim3 gt = gridc_of(R);
-  gt.z = b.NT;
-  if (d.p.colseg) {
-    dim3 gs((R.i1 - R.i0 + kSegCW) / kSegCW, R.j1 - R.j0 + 1, b.NT);
-    hipLaunchKernelGGL(k_step3d_t_seg, gs, dim3(kCX, seg_waves(b.N)), 0, s, d, R, t.nnew, t.nrhs);
+  // horizontal fluxes, then the column solves, on a sub-range of the interior
+  auto run = [&](const Range& r) {
+    hipLaunchKernelGGL(k_step3d_t_h, grid3_of(r, b.N), dim3(kBX, kBY), 0, s, d, r, t.nnew, t.nrhs);
+    dim3 gt = gridc_of(r);
+    gt.z = b.NT;
+    if (d.p.colseg)
+      hipLaunchKernelGGL(k_step3d_t_seg, seg_grid_of(r, b.NT), dim3(kCX, seg_waves(b.N)), 0, s, d, r, t.nnew, t.nrhs);
+    else if (d.f.colscr)
+      hipLaunchKernelGGL(k_step3d_t_v<ColGlb>, gt, dim3(kCX), 0, s, d, r, t.nnew, t.nrhs);
+    else
+      hipLaunchKernelGGL(k_step3d_t_v<ColLds>, gt, dim3(kCX), col_lds_bytes(2, b.N), s, d, r, t.nnew, t.nrhs);
+  };
+  auto edges = [&] {
+    for (int itrc = 1; itrc <= b.NT; itrc++) launch_t3dbc(d, s, t, itrc);
+  };
+  ExchList L;
+  if (tracer_exch_list(d, t.nnew, L)) {
+    launch_rim_first(d, s, R, L, run, edges);
+  } else {
+    run(R);
+    edges();
+    launch_exchange_tracers(d, s, t.nnew);
   }
-  else if (d.f.colscr)
-    hipLaunchKernelGGL(k_step3d_t_v<ColGlb>, gt, dim3(kCX), 0, s, d, R, t.nnew, t.nrhs);
-  else
-    hipLaunchKernelGGL(k_step3d_t_v<ColLds>, gt, dim3(kCX), col_lds_bytes(2, b.N), s, d, R, t.nnew, t.nrhs);
-  for (int itrc = 1; itrc <= b.NT; itrc++) launch_t3dbc(d, s, t, itrc);
-  launch_exchange_tracers(d, s, t.nnew);
 }
 
 // ---- t3dmix: Laplacian diffusion along S, t(nnew) += dt*pm*pn*div(F)/Hz.
@@ -324,8 +331,14 @@ __global__ void __launch_bounds__(256) k_t3dmix(Dev d, Range R, int nnew, int nr
 void launch_t3dmix(const Dev& d, hipStream_t s, const Tlev& t) {
   const Bounds& b = d.b;
   Range R{b.istr, b.iend, b.jstr, b.jend};
-  hipLaunchKernelGGL(k_t3dmix, grid_of(R), dim3(kBX, kBY), 0, s, d, R, t.nnew, t.nrhs);
-  launch_exchange_tracers(d, s, t.nnew);
+  auto run = [&](const Range& r) { hipLaunchKernelGGL(k_t3dmix, grid_of(r), dim3(kBX, kBY), 0, s, d, r, t.nnew, t.nrhs); };
+  ExchList L;
+  if (tracer_exch_list(d, t.nnew, L)) {
+    launch_rim_first(d, s, R, L, run, [] {});
+  } else {
+    run(R);
+    launch_exchange_tracers(d, s, t.nnew);
+  }
 }
 
 }  // namespace roms

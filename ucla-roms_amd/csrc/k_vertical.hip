@@ -93,8 +93,9 @@ __global__ void __launch_bounds__(256) k_set_huv(Dev d, Range R, int nrhs) {
 void launch_set_huv(const Dev& d, hipStream_t s, const Tlev& t) {
   const Bounds& b = d.b;
   Range R{b.istrR < b.istr ? b.istrR : b.istr, b.iendR, b.jstrR < b.jstr ? b.jstrR : b.jstr, b.jendR};
-  hipLaunchKernelGGL(k_set_huv, grid_of(R), dim3(kBX, kBY), 0, s, d, R, t.nrhs);
-  launch_exchange_list(d, s, ExchList{{d.f.FlxU, d.f.FlxV}, {b.N, b.N}, 2});
+  launch_rim_first(
+      d, s, R, ExchList{{d.f.FlxU, d.f.FlxV}, {b.N, b.N}, 2},
+      [&](const Range& r) { hipLaunchKernelGGL(k_set_huv, grid_of(r), dim3(kBX, kBY), 0, s, d, r, t.nrhs); }, [] {});
 }
 
 // ---------------------------------------------------------------------------
@@ -333,12 +334,15 @@ void launch_omega(const Dev& d, hipStream_t s, const Tlev& t) {
   else if (t.iic == t.forw_start) dtau = 0.5 * d.p.dt;
   else dtau = 0.6 * d.p.dt;
   Range R{b.istr, b.iend, b.jstr, b.jend};
-  hipLaunchKernelGGL(k_omega, grid_of(R), dim3(kBX, kBY), 0, s, d, R, dtau);
-  if (b.west_edge || b.east_edge || b.south_edge || b.north_edge) {
-    const int n = 2 * (b.jend - b.jstr + 1) + 2 * (b.iend - b.istr + 1) + 4;
-    hipLaunchKernelGGL(k_omega_edges, dim3((n + 255) / 256, b.N + 1), dim3(256), 0, s, d);
-  }
-  launch_exchange_list(d, s, ExchList{{d.f.We, d.f.Wi}, {b.N + 1, b.N + 1}, 2});
+  launch_rim_first(
+      d, s, R, ExchList{{d.f.We, d.f.Wi}, {b.N + 1, b.N + 1}, 2},
+      [&](const Range& r) { hipLaunchKernelGGL(k_omega, grid_of(r), dim3(kBX, kBY), 0, s, d, r, dtau); },
+      [&] {
+        if (b.west_edge || b.east_edge || b.south_edge || b.north_edge) {
+          const int n = 2 * (b.jend - b.jstr + 1) + 2 * (b.iend - b.istr + 1) + 4;
+          hipLaunchKernelGGL(k_omega_edges, dim3((n + 255) / 256, b.N + 1), dim3(256), 0, s, d);
+        }
+      });
 }
 
 // ---------------------------------------------------------------------------

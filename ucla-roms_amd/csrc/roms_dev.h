@@ -234,6 +234,37 @@ struct ExchList {
   int n;
 };
 void launch_exchange_list(const Dev& d, hipStream_t s, const ExchList& L);
+// ---- rim-first overlap of a producer's trailing exchange (SURVEY.md 8(e);
+// mpi_exchanges.F's swaps overlapped with interior compute).  `run(R')`
+// launches the producer's kernels on a sub-range.  On a multi-rank run the
+// four rim strips (the two rows / columns next to each edge: every cell the
+// exchange packs) go first, then `edges()` (kernels that fill ghost cells
+// from the rim; they travel with the strips), then the exchange of L is
+// forked onto the halo stream while the interior runs on s, and s joins it
+// before the next routine.  Single rank / overlap off: run(R), edges(),
+// exchange.  ROMS_GPU_OVERLAP3D=0 disables it. ----
+bool rim_overlap_on(const Dev& d, const Range& R);
+void rim_fork(const Dev& d, hipStream_t s, const ExchList& L);
+void rim_join(const Dev& d, hipStream_t s);
+template <class Run, class Edges>
+void launch_rim_first(const Dev& d, hipStream_t s, const Range& R, const ExchList& L, Run&& run, Edges&& edges) {
+  if (!rim_overlap_on(d, R)) {
+    run(R);
+    edges();
+    launch_exchange_list(d, s, L);
+    return;
+  }
+  run(Range{R.i0, R.i0 + 1, R.j0, R.j1});
+  run(Range{R.i1 - 1, R.i1, R.j0, R.j1});
+  run(Range{R.i0 + 2, R.i1 - 2, R.j0, R.j0 + 1});
+  run(Range{R.i0 + 2, R.i1 - 2, R.j1 - 1, R.j1});
+  edges();
+  rim_fork(d, s, L);
+  run(Range{R.i0 + 2, R.i1 - 2, R.j0 + 2, R.j1 - 2});
+  rim_join(d, s);
+}
+// the tracer list t(:,:,:,tlev,1:NT) as one exchange list (false if NT > 8)
+bool tracer_exch_list(const Dev& d, int tlev, ExchList& L);
 void launch_exchange_tracers(const Dev& d, hipStream_t s, int tlev);  // t(:,:,:,tlev,1:NT)
 // Column kernels keep 2 (N+1)-level scratch columns per lane in LDS; opt in to
 // the full 160 KB when N needs more than the default 64 KB.  Returns false if
