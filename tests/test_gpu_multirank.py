@@ -242,14 +242,15 @@ def test_rccl_transport_self_routed_equals_wrap(overlap, transport):
 def test_rim_first_overlap_bitwise_equals_serial_exchanges():
     """launch_rim_first (rim strips, exchange forked on the halo stream, interior
     concurrently; omega, set_HUV, step3d_t, t3dmix) gives the same fields as
-    the serial exchange order (ROMS_GPU_OVERLAP3D=0) on a 2x2 grid."""
+    the serial exchange order (the default; ROMS_GPU_OVERLAP3D=1 turns the
+    overlap on) on a 2x2 grid."""
     case = _case("basin_lmd")
-    os.environ["ROMS_GPU_OVERLAP3D"] = "0"
+    serial, _ = run_decomposed(case, 2, 2, 6)
+    os.environ["ROMS_GPU_OVERLAP3D"] = "1"
     try:
-        serial, _ = run_decomposed(case, 2, 2, 6)
+        over, _ = run_decomposed(case, 2, 2, 6)
     finally:
         del os.environ["ROMS_GPU_OVERLAP3D"]
-    over, _ = run_decomposed(case, 2, 2, 6)
     for r in range(4):
         for f in FIELDS:
             assert np.array_equal(serial[r][4][f], over[r][4][f]), (r, f)

@@ -65,7 +65,7 @@ struct Halo {
   int pending = 0;
   HaloIpc ipc;
   int overlap = 0;  // 1: enabled (ROMS_GPU_S2D_OVERLAP=1; off by default, see halo_setup)
-  int overlap3d = 1;  // rim-first overlap of the 3-D exchanges (launch_rim_first; ROMS_GPU_OVERLAP3D=0: off)
+  int overlap3d = 0;  // rim-first overlap of the 3-D exchanges (launch_rim_first; ROMS_GPU_OVERLAP3D=1: on)
 };
 
 int comm_unique_id(void* out128);

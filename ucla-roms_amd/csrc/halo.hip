@@ -424,8 +424,13 @@ int halo_setup(Halo& H, RomsComm* comm, const HaloPlan& plan, int maxlev, std::s
     // becomes two launches), so it is opt-in: ROMS_GPU_S2D_OVERLAP=1
     const char* e = getenv("ROMS_GPU_S2D_OVERLAP");
     H.overlap = e && e[0] == '1';
+    // rim-first 3-D overlap (launch_rim_first): measured with the exchanges
+    // routed through the IPC transport on one MI355X it costs more than it
+    // hides (C2 9.04 -> 11.10 ms/step: the four rim launches of a column
+    // kernel each take a whole column walk's latency, ~40 us, against ~20 us
+    // per exchange), so it is opt-in: ROMS_GPU_OVERLAP3D=1
     const char* e3 = getenv("ROMS_GPU_OVERLAP3D");
-    H.overlap3d = !(e3 && e3[0] == '0');
+    H.overlap3d = e3 && e3[0] == '1';
   }
   if (comm && comm->kind == 2) {
     std::lock_guard<std::mutex> lk(comm->grp->m);

@@ -242,7 +242,7 @@ void launch_exchange_list(const Dev& d, hipStream_t s, const ExchList& L);
 // from the rim; they travel with the strips), then the exchange of L is
 // forked onto the halo stream while the interior runs on s, and s joins it
 // before the next routine.  Single rank / overlap off: run(R), edges(),
-// exchange.  ROMS_GPU_OVERLAP3D=0 disables it. ----
+// exchange.  Opt-in (ROMS_GPU_OVERLAP3D=1), see halo_setup. ----
 bool rim_overlap_on(const Dev& d, const Range& R);
 void rim_fork(const Dev& d, hipStream_t s, const ExchList& L);
 void rim_join(const Dev& d, hipStream_t s);
