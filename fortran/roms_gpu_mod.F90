@@ -56,7 +56,8 @@ module roms_gpu_mod
   ! LMD switch bits of lmd_mixing (ROMS_LMD_*)
   integer(c_int), parameter :: ROMS_LMD_MIXING = 1, ROMS_LMD_KPP = 2, ROMS_LMD_BKPP = 4, ROMS_LMD_RIMIX = 8, &
                                ROMS_LMD_CONVEC = 16, ROMS_LMD_NONLOCAL = 32
-  integer(c_int), parameter :: ROMS_GPU_ABI = 8   ! ROMS_GPU_ABI_VERSION, include/roms_gpu.h
+  integer(c_int), parameter :: ROMS_GPU_ABI = 9   ! ROMS_GPU_ABI_VERSION, include/roms_gpu.h
+  integer(c_int), parameter :: ROMS_FRC_SURFACE = 1, ROMS_FRC_BRY = 2
 
   ! field ids (enum roms_field) used by the drivers below
   integer(c_int), parameter :: ROMS_ALL = -1
@@ -241,6 +242,30 @@ module roms_gpu_mod
       integer(c_int), value :: req_rec, tindx
       type(roms_tlev), intent(inout) :: t
       real(c_double), intent(out) :: start_time
+    end function
+    ! set_frc_data / set_tides on the device (k_forcing.hip)
+    integer(c_int) function roms_gpu_frc_record(field_id, slot, rec_time, data) bind(c)
+      import :: c_int, c_double
+      integer(c_int), value :: field_id, slot
+      real(c_double), value :: rec_time
+      real(c_double), intent(in) :: data(*)
+    end function
+    integer(c_int) function roms_gpu_frc_interp(modtime, kinds) bind(c)
+      import :: c_int, c_double
+      real(c_double), value :: modtime
+      integer(c_int), value :: kinds
+    end function
+    ! the tidal arrays are c_loc(...) of (GLOBAL_2D_ARRAY, ntides) arrays, or c_null_ptr
+    integer(c_int) function roms_gpu_set_tide_data(ntides, ftide, pot_re, pot_im, ztide_re, ztide_im, &
+                                                   utide_re, utide_im, vtide_re, vtide_im) bind(c)
+      import :: c_int, c_double, c_ptr
+      integer(c_int), value :: ntides
+      real(c_double), intent(in) :: ftide(*)
+      type(c_ptr), value :: pot_re, pot_im, ztide_re, ztide_im, utide_re, utide_im, vtide_re, vtide_im
+    end function
+    integer(c_int) function roms_gpu_set_tides(time) bind(c)
+      import :: c_int, c_double
+      real(c_double), value :: time
     end function
     integer(c_int) function roms_gpu_comm_unique_id(id128) bind(c)
       import :: c_int, c_char

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define ROMS_GPU_ABI_VERSION 8
+#define ROMS_GPU_ABI_VERSION 9
 #define ROMS_MAX_FAST 288
 
 /* Subdomain geometry of this rank: param.F / dimensions.F / mpi_setup.F:39-210 */
@@ -259,6 +259,32 @@ int roms_gpu_halo_plan(int Lm, int Mm, int np_xi, int np_eta, int inode, int jno
  * Returns the per-level count (<= cap) or -1.                               */
 long roms_gpu_halo_map(int Lm, int Mm, int np_xi, int np_eta, int inode, int jnode, int ew_periodic,
                        int ns_periodic, int dir, int unpack, int *i, int *j, long cap);
+
+/* ---- forcing and boundary producers on the device (set_forces.F,
+ * set_frc_data roms_read_write.F:303-392, set_bry_all boundary.F:227,
+ * set_tides tides.F:86-254) ----
+ * roms_gpu_frc_record uploads one record (time rec_time in days, like the
+ * reference's forcing times) of a field into record slot 0 or 1; the host
+ * uploads a record only when the model time leaves the window of the two it
+ * holds (as fill_frc_slice does).  roms_gpu_frc_interp forms every field
+ * whose two slots are loaded, of the kinds in `kinds` (ROMS_FRC_SURFACE:
+ * 2-D surface/atmospheric fields, ROMS_FRC_BRY: the *_west.._north boundary
+ * arrays), as cff1*rec(it1) + cff2*rec(it2) at modtime [days], with
+ * set_frc_data's out-of-window error.  roms_gpu_set_tide_data hands over
+ * the tidal constituents (frequencies ftide [1/s]; potential and boundary
+ * elevation/velocity real/imaginary parts, ntides x the field layout,
+ * column-major like the reference's (GLOBAL_2D_ARRAY, ntides) arrays; NULL
+ * pairs switch that part off); roms_gpu_set_tides(time) then sets ptide
+ * (pot_tides) and adds the tides to the open-boundary zeta/ubar/vbar data
+ * (bry_tides) at omT = ftide*(time + dt/2), as set_tides_tile does.       */
+#define ROMS_FRC_SURFACE 1
+#define ROMS_FRC_BRY     2
+int roms_gpu_frc_record(int field_id, int slot, double rec_time, const double *data);
+int roms_gpu_frc_interp(double modtime, int kinds);
+int roms_gpu_set_tide_data(int ntides, const double *ftide, const double *pot_re, const double *pot_im,
+                           const double *ztide_re, const double *ztide_im, const double *utide_re,
+                           const double *utide_im, const double *vtide_re, const double *vtide_im);
+int roms_gpu_set_tides(double time);
 
 /* ---- on-disk formats: partitioned netCDF restart and history files ----
  * One file per rank, as the reference's PARALLEL_FILES build writes them

@@ -1,0 +1,104 @@
+"""Forcing and boundary producers on the device.
+
+* set_frc_data (roms_read_write.F:303-392): two records per field in HBM,
+  interpolated to the model time on the device -- equal bitwise to the
+  reference's cff1*rec(it1) + cff2*rec(it2) restated in numpy, for a 2-D
+  surface field and an open-boundary array, with the kinds filter and the
+  out-of-window error (roms_read_write.F:381).
+* set_tides (tides.F:86-254): pot_tides' ptide and bry_tides' boundary
+  zeta/ubar/vbar sums over the constituents at omT = ftide*(time + dt/2),
+  bitwise against the same sums in numpy (the cos/sin are formed once per
+  constituent on the host in both).  Parity unpinned against the reference
+  itself: its tidal tests need netCDF inputs that are not available offline.
+"""
+import math
+
+import numpy as np
+import pytest
+
+import oracle
+import romsgpu
+from test_gpu_parity import basin_cfg
+from test_gpu_register import host_model
+
+pytestmark = pytest.mark.gpu
+
+
+def open_basin(pot=1):
+    c = basin_cfg(LLm=40, MMm=32, N=12, nonlin=True)
+    c.obc, c.ubind, c.pot_tides = 15, 0.1, pot
+    o = oracle.Oracle(c)
+    o.init()
+    m, _ = host_model(o, c)
+    return c, m
+
+
+def test_frc_interp_bitwise():
+    c, m = open_basin()
+    rng = np.random.default_rng(3)
+    shp = m.get("sustr").shape
+    a, b = rng.standard_normal(shp), rng.standard_normal(shp)
+    nb = m.get("zeta_west").size
+    za, zb = rng.standard_normal(nb), rng.standard_normal(nb)
+    m.frc_record("sustr", 1, 10.5, b)     # slots in either order: it1 is the earlier record
+    m.frc_record("sustr", 0, 10.0, a)
+    m.frc_record("zeta_west", 0, 10.0, za)
+    m.frc_record("zeta_west", 1, 10.5, zb)
+    before = m.get("zeta_west").copy()
+    t = 10.2
+    m.frc_interp(t, m.FRC_SURFACE)
+    cff1, cff2 = (10.5 - t) / (10.5 - 10.0), (t - 10.0) / (10.5 - 10.0)
+    assert np.array_equal(m.get("sustr"), cff1 * a + cff2 * b)
+    assert np.array_equal(m.get("zeta_west"), before)          # not of the requested kind
+    m.frc_interp(t, m.FRC_BRY)
+    assert np.array_equal(m.get("zeta_west").ravel(), cff1 * za + cff2 * zb)
+    with pytest.raises(romsgpu.RomsGpuError, match="outside the records"):
+        m.frc_interp(10.5 + 2 * c.dt + 1.0)   # set_frc_data's window check uses dt as is (roms_read_write.F:381)
+    m.close()
+
+
+def test_set_tides_bitwise():
+    c, m = open_basin()
+    rng = np.random.default_rng(5)
+    nt = 3
+    shp = (nt,) + m.get("zeta").shape[1:]
+    ftide = np.array([1.405e-4, 1.454e-4, 7.29e-5])
+    pr, pi = 0.1 * rng.standard_normal(shp), 0.1 * rng.standard_normal(shp)
+    bry = [(rng.standard_normal(shp), rng.standard_normal(shp)) for _ in range(3)]
+    m.set_tide_data(ftide, pot=(pr, pi), bry=bry)
+    base = {n: m.get(n).copy() for n in ("zeta_west", "ubar_east", "vbar_south", "zeta_north")}
+    time = 3600.0 * 7
+    m.set_tides(time)
+    cs = [math.cos(f * (time + 0.5 * c.dt)) for f in ftide]
+    sn = [math.sin(f * (time + 0.5 * c.dt)) for f in ftide]
+    # pot_tides over (istrR-1..iendR, jstrR-1..jendR) = (-1..L+1, -1..M+1) on a closed-or-open single domain
+    L, M = c.LLm, c.MMm
+    want = pr[0] * cs[0] - pi[0] * sn[0]
+    for t in range(1, nt):
+        want = want + pr[t] * cs[t] - pi[t] * sn[t]
+    got = m.get("ptide")[0]
+    assert np.array_equal(got[0:M + 3, 0:L + 3], want[0:M + 3, 0:L + 3])
+    # bry_tides: western zeta at i = istr-1 = 0, j = jstrR..jendR = 0..M+1
+    z = base["zeta_west"].copy()
+    for t in range(nt):
+        z[0:M + 2] = z[0:M + 2] + bry[0][0][t][1:M + 3, 1] * cs[t] - bry[0][1][t][1:M + 3, 1] * sn[t]
+    assert np.array_equal(m.get("zeta_west"), z)
+    # eastern ubar at i = iend+1 = L+1, j = 0..M+1
+    u = base["ubar_east"].copy()
+    for t in range(nt):
+        u[0:M + 2] = u[0:M + 2] + bry[1][0][t][1:M + 3, L + 2] * cs[t] - bry[1][1][t][1:M + 3, L + 2] * sn[t]
+    assert np.array_equal(m.get("ubar_east"), u)
+    # southern vbar at j = jstrV-1 = 1, i = istrR..iendR = 0..L+1
+    v = base["vbar_south"].copy()
+    for t in range(nt):
+        v[0:L + 2] = v[0:L + 2] + bry[2][0][t][2, 1:L + 3] * cs[t] - bry[2][1][t][2, 1:L + 3] * sn[t]
+    assert np.array_equal(m.get("vbar_south"), v)
+    m.close()
+
+
+def test_tide_data_needs_pairs():
+    c, m = open_basin()
+    shp = (1,) + m.get("zeta").shape[1:]
+    with pytest.raises(romsgpu.RomsGpuError, match="come together"):
+        m.set_tide_data([1e-4], pot=(np.zeros(shp), None))
+    m.close()

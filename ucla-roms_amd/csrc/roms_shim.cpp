@@ -57,6 +57,8 @@ struct Ctx {
   // turns into NaN instead of a value of whatever array lies next to it
   bool guard = false;
   std::map<double*, double*> guard_base;
+  double* small = nullptr;   // shim_scratch_small
+  long small_n = 0;
 };
 // One context per host thread: a process normally drives one GPU/subdomain
 // from one thread; tests drive several subdomains from threads of one process.
@@ -238,6 +240,8 @@ hipError_t dev_alloc(double*& p, long n) {
 
 void free_all() {
   io_free();
+  frc_free();
+  if (g.small) { (void)hipFree(g.small); g.small = nullptr; g.small_n = 0; }
   for (hipEvent_t e : g.ev) (void)hipEventDestroy(e);
   g.ev.clear();
   halo_free(g.halo);
@@ -283,6 +287,15 @@ int roms::shim_enter(ShimState& S) {
   return 0;
 }
 void roms::shim_set_error(const std::string& e) { g.err = e; }
+double* roms::shim_field(int id) { return (id >= 0 && id < ROMS_NFIELDS) ? g.f[id].d : nullptr; }
+double* roms::shim_scratch_small(long n) {
+  if (g.small_n < n) {
+    if (g.small) { (void)hipStreamSynchronize(g.s); (void)hipFree(g.small); g.small = nullptr; }
+    if (hipMalloc(&g.small, (size_t)n * sizeof(double)) != hipSuccess) { g.small_n = 0; return nullptr; }
+    g.small_n = n;
+  }
+  return g.small;
+}
 void roms::ktimer_mark(hipStream_t s, int id, int end, int count) {
   if (g.timed != id) return;
   if (!end) {

@@ -21,4 +21,7 @@ struct ShimState {
 int shim_enter(ShimState& S);
 void shim_set_error(const std::string& e);
 void io_free();   // rst_io.hip: joins the writer, frees staging (roms_gpu_finalize)
+void frc_free();  // k_forcing.hip: forcing records and tide data (roms_gpu_finalize)
+double* shim_field(int field_id);          // device array of a field (nullptr if absent)
+double* shim_scratch_small(long n);        // small device scratch owned by the context (>= n doubles)
 }  // namespace roms

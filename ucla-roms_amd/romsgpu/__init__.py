@@ -113,6 +113,10 @@ def load_library(path=LIB_PATH):
                                          P(ctypes.c_double)]
     L.roms_gpu_bulk_flux.argtypes = [P(Tlev)]
     L.roms_gpu_set_ub_tune.argtypes = [P(ctypes.c_double)] * 4
+    L.roms_gpu_frc_record.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, P(ctypes.c_double)]
+    L.roms_gpu_frc_interp.argtypes = [ctypes.c_double, ctypes.c_int]
+    L.roms_gpu_set_tide_data.argtypes = [ctypes.c_int] + [P(ctypes.c_double)] * 9
+    L.roms_gpu_set_tides.argtypes = [ctypes.c_double]
     L.roms_gpu_diag.argtypes = [P(Tlev), P(ctypes.c_double)]
     L.roms_gpu_time_steps.argtypes = [P(Tlev), ctypes.c_int, P(ctypes.c_double)]
     L.roms_gpu_stream.restype = ctypes.c_void_p
@@ -362,6 +366,38 @@ class Model:
         keep = [None if a is None else np.ascontiguousarray(a, dtype=np.float64) for a in ub]
         self._chk(self.L.roms_gpu_set_ub_tune(*[None if a is None else a.ctypes.data_as(D) for a in keep]),
                   "set_ub_tune")
+
+    # ---- forcing / boundary producers on the device (set_frc_data, set_tides) ----
+    FRC_SURFACE, FRC_BRY = 1, 2
+
+    def frc_record(self, name, slot, rec_time, arr):
+        """One forcing record (time in days) of field `name` into slot 0/1."""
+        a = np.ascontiguousarray(arr, dtype=np.float64).ravel()
+        if a.size != self.L.roms_gpu_field_size(FIELD_ID[name]):
+            raise ValueError("frc_record: %s has %d elements" % (name, a.size))
+        self._chk(self.L.roms_gpu_frc_record(FIELD_ID[name], slot, rec_time,
+                                             a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))), "frc_record")
+
+    def frc_interp(self, modtime, kinds=3):
+        self._chk(self.L.roms_gpu_frc_interp(modtime, kinds), "frc_interp")
+
+    def set_tide_data(self, ftide, pot=None, bry=None):
+        """ftide (ntides,) [1/s]; pot = (re, im), bry = ((zre, zim), (ure, uim), (vre, vim)),
+        each (ntides, Mm+4, Lm+4) or None."""
+        D = ctypes.POINTER(ctypes.c_double)
+        keep = [np.ascontiguousarray(ftide, dtype=np.float64)]
+        def ptr(a):
+            if a is None:
+                return None
+            keep.append(np.ascontiguousarray(a, dtype=np.float64))
+            return keep[-1].ctypes.data_as(D)
+        pr, pi = pot if pot is not None else (None, None)
+        (zr, zi), (ur, ui), (vr, vi) = bry if bry is not None else ((None, None),) * 3
+        self._chk(self.L.roms_gpu_set_tide_data(len(keep[0]), keep[0].ctypes.data_as(D), ptr(pr), ptr(pi), ptr(zr),
+                                                ptr(zi), ptr(ur), ptr(ui), ptr(vr), ptr(vi)), "set_tide_data")
+
+    def set_tides(self, time):
+        self._chk(self.L.roms_gpu_set_tides(time), "set_tides")
 
     def bulk_flux(self):
         """set_bulk_frc -> calc_all_bulk_forces on the device at the current nrhs."""
