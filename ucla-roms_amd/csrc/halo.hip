@@ -30,6 +30,7 @@
 #include <vector>
 
 #include "halo.h"
+#include "shim_state.h"
 
 namespace roms {
 
@@ -296,7 +297,9 @@ static void ipc_setup(Halo& H) {
   if (ok != 0.0 && (hipMemset(I.rbuf2, 0, rbytes) != hipSuccess ||
                     hipMemset(I.flags, 0, 8 * sizeof(unsigned long long)) != hipSuccess ||
                     hipMemset(I.seq, 0, sizeof(unsigned long long)) != hipSuccess ||
-                    hipMemset(I.err_dev, 0, sizeof(int)) != hipSuccess || hipIpcGetMemHandle(&hr, I.rbuf2) != hipSuccess ||
+                    hipMemset(I.err_dev, 0, sizeof(int)) != hipSuccess ||
+                    hipStreamSynchronize(nullptr) != hipSuccess ||   // null-stream fills land first
+                    hipIpcGetMemHandle(&hr, I.rbuf2) != hipSuccess ||
                     hipIpcGetMemHandle(&hf, I.flags) != hipSuccess))
     ok = 0.0;
   if (I.err_host) *I.err_host = 0;
@@ -352,8 +355,8 @@ static void ipc_setup(Halo& H) {
         ok = 0.0;
     for (int r = 0; r < kSelfTestRounds && ok != 0.0; r++) {
       for (long q = 0; q < n; q++) h[q] = 1.0e7 * (me + 1) + 1.0e3 * r + (double)q + 0.25;
-      if (hipMemcpy(A[r], h.data(), n * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
-          hipMemcpy(B[r], h.data(), n * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) ok = 0.0;
+      if (copy_on(A[r], h.data(), n * sizeof(double), hipMemcpyHostToDevice, s) != hipSuccess ||
+          copy_on(B[r], h.data(), n * sizeof(double), hipMemcpyHostToDevice, s) != hipSuccess) ok = 0.0;
     }
     if (ok != 0.0) {
       // the reference result: RCCL; then the IPC exchanges queued back to
@@ -365,8 +368,8 @@ static void ipc_setup(Halo& H) {
       I.ok = 0;
       if (hipStreamSynchronize(s) != hipSuccess || *I.err_host != 0) ok = 0.0;
       for (int r = 0; r < kSelfTestRounds && ok != 0.0; r++) {
-        if (hipMemcpy(ha.data(), A[r], n * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess ||
-            hipMemcpy(hb.data(), B[r], n * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess ||
+        if (copy_on(ha.data(), A[r], n * sizeof(double), hipMemcpyDeviceToHost, s) != hipSuccess ||
+            copy_on(hb.data(), B[r], n * sizeof(double), hipMemcpyDeviceToHost, s) != hipSuccess ||
             std::memcmp(ha.data(), hb.data(), n * sizeof(double)) != 0)
           ok = 0.0;
       }

@@ -210,7 +210,7 @@ int roms_gpu_set_tide_data(int ntides, const double* ftide, const double* pot_re
   const size_t nb = (size_t)ntides * S.d->b.n2 * sizeof(double);
   auto up = [&](double*& d, const double* h) -> bool {
     if (!h || ntides == 0) return true;
-    return hipMalloc(&d, nb) == hipSuccess && hipMemcpy(d, h, nb, hipMemcpyHostToDevice) == hipSuccess;
+    return hipMalloc(&d, nb) == hipSuccess && copy_on(d, h, nb, hipMemcpyHostToDevice, S.s) == hipSuccess;
   };
   if (!up(T.pr, pot_re) || !up(T.pi, pot_im) || !up(T.zr, ztide_re) || !up(T.zi, ztide_im) || !up(T.ur, utide_re) ||
       !up(T.ui, utide_im) || !up(T.vr, vtide_re) || !up(T.vi, vtide_im)) {

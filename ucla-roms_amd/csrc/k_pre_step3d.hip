@@ -299,20 +299,52 @@ __device__ __forceinline__ void pre_uv_col(const Dev& d, int i, int j, int dir, 
   double DCk1 = cff * (DCinit(N, hbN, hbNm) + c.dtau * sstr);  // DC(N)
   A[N] = DCk1;
   B[N - 1] = CFk;
-#pragma unroll 8
-  for (int k = N - 1; k >= 2; k--) {
-    const double hbL = Hb[lev(k - 1)], hfL = Hf[lev(k - 1)], hbLm = Hb[lev(k - 1) + ms], hfLm = Hf[lev(k - 1) + ms];
-    const double FCl =
-        2.0 * c.dtau * (Akv[(long)(k - 1) * n2] + Akv[(long)(k - 1) * n2 - s]) / (hfK + hfKm + hfL + hfLm);
-    const double WCl = DC0 * 0.5 * (Wi[(long)(k - 1) * n2] + Wi[(long)(k - 1) * n2 - s]);
+  // Forward elimination, levels N-1..2.  Iteration k reads level k-1 of
+  // Hb/Hf/Akv/Wi and level k of ru/u/Hz, and stores ru(k) and u(indx)(k).
+  // The compiler cannot prove the ru/u stores of level k miss the loads of
+  // the levels below (same arrays, offsets n2 apart), so it issues no load
+  // ahead of a store; a ring of kPF iterations' raw loads, refilled before
+  // each iteration's stores, keeps kPF levels of loads in flight.  At
+  // <= 1 wave per SIMD (two LDS column slots per wave) the ring's VGPRs cost
+  // no occupancy.  Same arithmetic in the same order as the reference loop.
+  struct Lv { double hb, hf, hbm, hfm, ak, aks, wi, wis, r, us, ui, hz, hzs; };
+  auto load = [&](int k) {   // the raw loads of iteration k (clamped to a valid level)
+    k = k < 2 ? 2 : k;
+    const long o = lev(k), l = lev(k - 1);
+    return Lv{Hb[l], Hf[l], Hb[l + ms], Hf[l + ms], Akv[o], Akv[o - s], Wi[o], Wi[o - s],   // w-level k-1
+              rr[o], Ustp[o], Uidx[o], Hz[o], Hz[o - s]};
+  };
+  auto iter = [&](int k, const Lv& v) {
+    const double FCl = 2.0 * c.dtau * (v.ak + v.aks) / (hfK + hfKm + v.hf + v.hfm);
+    const double WCl = DC0 * 0.5 * (v.wi + v.wis);
     cff = 1.0 / (0.5 * (hfK + hfKm) + FCl - fmin0(WCl) + FCk + fmax0(WCk) - CFk * (FCk - fmin0(WCk)));
     const double CFl = cff * (FCl + fmax0(WCl));
-    const double DCk = cff * (DCinit(k, hbK, hbKm) + DCk1 * (FCk - fmin0(WCk)));
+    const long o = lev(k);
+    const double r = uv_rr_update(v.r, A, k);
+    rr[o] = r;
+    const double dci = 0.5 * (hbK + hbKm) * (c.cf_stp * v.us + c.cf_bak * v.ui) + DC0 * r;
+    Uidx[o] = 0.5 * (v.hz + v.hzs) * v.us;
+    const double DCk = cff * (dci + DCk1 * (FCk - fmin0(WCk)));
     B[k - 1] = CFl;
     A[k] = DCk;
     DCk1 = DCk; FCk = FCl; WCk = WCl; CFk = CFl;
-    hbK = hbL; hfK = hfL; hbKm = hbLm; hfKm = hfLm;
+    hbK = v.hb; hfK = v.hf; hbKm = v.hbm; hfKm = v.hfm;
+  };
+  Lv ring[kPF];
+#pragma unroll
+  for (int q = 0; q < kPF; q++) ring[q] = load(N - 1 - q);
+  int k1 = N - 1;
+  for (; k1 - kPF + 1 >= 2; k1 -= kPF) {
+#pragma unroll
+    for (int q = 0; q < kPF; q++) {
+      const Lv v = ring[q];
+      ring[q] = load(k1 - q - kPF);
+      iter(k1 - q, v);
+    }
   }
+#pragma unroll
+  for (int q = 0; q < kPF; q++)
+    if (k1 - q >= 2) iter(k1 - q, ring[q]);
   const double rd = F.r_D[ij], rdm = F.r_D[ij - s];
   double un = (DCinit(1, hbK, hbKm) + DCk1 * (FCk - fmin0(WCk))) /
               (0.5 * (hfK + hfKm) + 0.5 * c.dtau * (rd + rdm) + FCk + fmax0(WCk) - CFk * (FCk - fmin0(WCk)));

@@ -235,7 +235,12 @@ hipError_t dev_alloc(double*& p, long n) {
   }
   p = base + G;
   if (G) g.guard_base[p] = base;
-  return hipMemset(p, 0, (size_t)n * sizeof(double));
+  // The library's kernels run on a non-blocking stream, which does not wait
+  // for work on the null stream: the zero fill must have landed before the
+  // first kernel reads the array, or it may see what a previous model left in
+  // the same memory (or be zeroed after the kernel wrote it).
+  e = hipMemset(p, 0, (size_t)n * sizeof(double));
+  return e != hipSuccess ? e : hipStreamSynchronize(nullptr);
 }
 
 void free_all() {
@@ -433,14 +438,15 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
   // compiled for; ROMS_GPU_COLREG=0 falls back to the LDS form (A/B runs)
   // bits: 1 step3d_uv1 (k_uv1_reg), 2 pre_step3d tracers (k_pre_tracer_v_reg);
   // ROMS_GPU_COLREG=<mask> (0: the LDS forms).  Measured at C2 (round 2):
-  // bit 2 pre_step3d 2.06 -> 1.96 ms; bit 1 step3d_uv1 1.24 ms against 1.16
-  // for the LDS form, but the configuration with the LDS form failed the C2
-  // 100-step parity test twice, identically, in one particular test-process
-  // history and is not the default until that is understood;
-  // register forms of pre_uv_col (2.06 -> 2.20 ms) and k_step3d_t_v (its
-  // extra per-level KPP inputs spill at 2 waves/SIMD; 0.84 vs 0.81 ms at 1
+  // bit 2 pre_step3d 2.06 -> 1.96 ms; bit 1 step3d_uv1 1.23 ms against 1.16
+  // for the LDS form, so bit 1 is off by default.  (The LDS form once failed
+  // the C2 100-step parity test in some test-process histories: that was the
+  // zero fill of a new model's arrays racing with its first kernels, see
+  // dev_alloc, not the solver; both forms are equal bitwise.)  Register
+  // forms of pre_uv_col (2.06 -> 2.20 ms) and k_step3d_t_v (its extra
+  // per-level KPP inputs spill at 2 waves/SIMD; 0.84 vs 0.81 ms at 1
   // wave/SIMD) were slower and are not kept.
-  P.colreg = 1 | 2;
+  P.colreg = 2;
   {
     const char* e = getenv("ROMS_GPU_COLREG");
     if (e && e[0] >= '0' && e[0] <= '9') P.colreg = atoi(e);
@@ -679,10 +685,10 @@ int roms_gpu_set_pipe_frc(int npip, const int* pipe_idx, const double* pipe_flx,
       return -2;
     g.d.p.npip = npip;
   }
-  CHECK_HIP(hipMemcpy(F.pipe_idx, pipe_idx, (size_t)b.n2 * sizeof(int), hipMemcpyHostToDevice));
-  CHECK_HIP(hipMemcpy(F.pipe_flx, pipe_flx, (size_t)b.n2 * sizeof(double), hipMemcpyHostToDevice));
-  CHECK_HIP(hipMemcpy(F.pipe_prf, pipe_prf, (size_t)npip * b.N * sizeof(double), hipMemcpyHostToDevice));
-  CHECK_HIP(hipMemcpy(F.pipe_trc, pipe_trc, (size_t)npip * b.NT * sizeof(double), hipMemcpyHostToDevice));
+  CHECK_HIP(copy_on(F.pipe_idx, pipe_idx, (size_t)b.n2 * sizeof(int), hipMemcpyHostToDevice, g.s));
+  CHECK_HIP(copy_on(F.pipe_flx, pipe_flx, (size_t)b.n2 * sizeof(double), hipMemcpyHostToDevice, g.s));
+  CHECK_HIP(copy_on(F.pipe_prf, pipe_prf, (size_t)npip * b.N * sizeof(double), hipMemcpyHostToDevice, g.s));
+  CHECK_HIP(copy_on(F.pipe_trc, pipe_trc, (size_t)npip * b.NT * sizeof(double), hipMemcpyHostToDevice, g.s));
   return 0;
 }
 
@@ -744,13 +750,13 @@ int roms_gpu_set_river_frc(int nriv, const double* riv_uflx, const double* riv_v
     if (!F.riv_uflx && (scratch(F.riv_uflx, b.n2) || scratch(F.riv_vflx, b.n2))) return -2;
     if (F.riv_face) { (void)hipFree(F.riv_face); F.riv_face = nullptr; }
     CHECK_HIP(hipMalloc(&F.riv_face, (faces.size() ? faces.size() : 1) * sizeof(int)));
-    if (!faces.empty()) CHECK_HIP(hipMemcpy(F.riv_face, faces.data(), faces.size() * sizeof(int), hipMemcpyHostToDevice));
-    CHECK_HIP(hipMemcpy(F.riv_uflx, riv_uflx, (size_t)b.n2 * sizeof(double), hipMemcpyHostToDevice));
-    CHECK_HIP(hipMemcpy(F.riv_vflx, riv_vflx, (size_t)b.n2 * sizeof(double), hipMemcpyHostToDevice));
+    if (!faces.empty()) CHECK_HIP(copy_on(F.riv_face, faces.data(), faces.size() * sizeof(int), hipMemcpyHostToDevice, g.s));
+    CHECK_HIP(copy_on(F.riv_uflx, riv_uflx, (size_t)b.n2 * sizeof(double), hipMemcpyHostToDevice, g.s));
+    CHECK_HIP(copy_on(F.riv_vflx, riv_vflx, (size_t)b.n2 * sizeof(double), hipMemcpyHostToDevice, g.s));
     g.d.p.nrivf = (int)(faces.size() / 3);
   }
-  CHECK_HIP(hipMemcpy(F.riv_vol, riv_vol, (size_t)nriv * sizeof(double), hipMemcpyHostToDevice));
-  CHECK_HIP(hipMemcpy(F.riv_trc, riv_trc, (size_t)nriv * b.NT * sizeof(double), hipMemcpyHostToDevice));
+  CHECK_HIP(copy_on(F.riv_vol, riv_vol, (size_t)nriv * sizeof(double), hipMemcpyHostToDevice, g.s));
+  CHECK_HIP(copy_on(F.riv_trc, riv_trc, (size_t)nriv * b.NT * sizeof(double), hipMemcpyHostToDevice, g.s));
   g.d.p.nriv = nriv;
   return 0;
 }
@@ -1049,10 +1055,10 @@ static int grid_integrals() {
   const Bounds& b = g.d.b;
   HostState H(b.Lm, b.Mm, b.N, b.NT, b.nTS);
   std::vector<double> h(b.n2), pm(b.n2), pn(b.n2), rm(b.n2);
-  CHECK_HIP(hipMemcpy(h.data(), g.d.f.h, b.n2 * sizeof(double), hipMemcpyDeviceToHost));
-  CHECK_HIP(hipMemcpy(pm.data(), g.d.f.pm, b.n2 * sizeof(double), hipMemcpyDeviceToHost));
-  CHECK_HIP(hipMemcpy(pn.data(), g.d.f.pn, b.n2 * sizeof(double), hipMemcpyDeviceToHost));
-  CHECK_HIP(hipMemcpy(rm.data(), g.d.f.rmask, b.n2 * sizeof(double), hipMemcpyDeviceToHost));
+  CHECK_HIP(copy_on(h.data(), g.d.f.h, b.n2 * sizeof(double), hipMemcpyDeviceToHost, g.s));
+  CHECK_HIP(copy_on(pm.data(), g.d.f.pm, b.n2 * sizeof(double), hipMemcpyDeviceToHost, g.s));
+  CHECK_HIP(copy_on(pn.data(), g.d.f.pn, b.n2 * sizeof(double), hipMemcpyDeviceToHost, g.s));
+  CHECK_HIP(copy_on(rm.data(), g.d.f.rmask, b.n2 * sizeof(double), hipMemcpyDeviceToHost, g.s));
   std::vector<double> dA(b.n2, 0.0), dV(b.n2, 0.0);
   for (int j = 1; j <= b.Mm; j++)
     for (int i = 1; i <= b.Lm; i++) {

@@ -449,9 +449,9 @@ int roms_gpu_get_init(const char* path, int req_rec, int tindx, roms_tlev* t, do
     // host copies of the masks for the partition's slabs
     const long n2 = b.n2;
     std::vector<double> rmask(n2), umask(n2), vmask(n2);
-    if (hipMemcpy(rmask.data(), F.rmask, n2 * 8, hipMemcpyDeviceToHost) != hipSuccess ||
-        hipMemcpy(umask.data(), F.umask, n2 * 8, hipMemcpyDeviceToHost) != hipSuccess ||
-        hipMemcpy(vmask.data(), F.vmask, n2 * 8, hipMemcpyDeviceToHost) != hipSuccess)
+    if (copy_on(rmask.data(), F.rmask, n2 * 8, hipMemcpyDeviceToHost, S.s) != hipSuccess ||
+        copy_on(umask.data(), F.umask, n2 * 8, hipMemcpyDeviceToHost, S.s) != hipSuccess ||
+        copy_on(vmask.data(), F.vmask, n2 * 8, hipMemcpyDeviceToHost, S.s) != hipSuccess)
       throw std::runtime_error("mask download failed");
     auto read_slab = [&](const std::string& name, char g, int nk, std::vector<double>& buf) -> bool {
       const int id = f.find_var(name);
@@ -481,7 +481,7 @@ int roms_gpu_get_init(const char* path, int req_rec, int tindx, roms_tlev* t, do
       Slab s = slab_of(b, p, base, g, nk, sk);
       if (dbuf) { (void)hipFree(dbuf); dbuf = nullptr; }
       if (hipMalloc(&dbuf, buf.size() * 8) != hipSuccess ||
-          hipMemcpy(dbuf, buf.data(), buf.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
+          copy_on(dbuf, buf.data(), buf.size() * 8, hipMemcpyHostToDevice, S.s) != hipSuccess)
         throw std::runtime_error("upload failed");
       hipLaunchKernelGGL(k_io_unpack, dim3(blocks_for((long)buf.size())), dim3(256), 0, S.s, s, (double*)s.src, dbuf);
       if (hipStreamSynchronize(S.s) != hipSuccess) throw std::runtime_error("unpack failed");

@@ -20,7 +20,15 @@ struct ShimState {
 // loop exchange joined); fills S.  Returns 0 or the negative error code.
 int shim_enter(ShimState& S);
 void shim_set_error(const std::string& e);
-void io_free();   // rst_io.hip: joins the writer, frees staging (roms_gpu_finalize)
+void io_free();
+// A blocking copy ordered on the library's stream.  The kernels run on
+// non-blocking streams, which do not wait for null-stream work, so plain
+// hipMemcpy/hipMemset can race with them (a pageable hipMemcpy may return
+// before its DMA has landed).
+inline hipError_t copy_on(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t s) {
+  const hipError_t e = hipMemcpyAsync(dst, src, bytes, kind, s);
+  return e != hipSuccess ? e : hipStreamSynchronize(s);
+}   // rst_io.hip: joins the writer, frees staging (roms_gpu_finalize)
 void frc_free();  // k_forcing.hip: forcing records and tide data (roms_gpu_finalize)
 double* shim_field(int field_id);          // device array of a field (nullptr if absent)
 double* shim_scratch_small(long n);        // small device scratch owned by the context (>= n doubles)
