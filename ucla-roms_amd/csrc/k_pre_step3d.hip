@@ -257,6 +257,10 @@ __global__ void __launch_bounds__(256) k_rd(Dev d, Range R, int nstp) {
 // ---- momentum, per column: vertical spline advection into ru/rv, then
 // implicit viscosity with implicit no-slip bottom (IMPLCT_NO_SLIP_BTTM_BC).
 // LDS: A = spline FC -> flux -> DC(k); B = spline CF -> CF(k-1). ----
+#ifndef ROMS_PREUV_PF
+#define ROMS_PREUV_PF 8
+#endif
+constexpr int kPreUvPF = ROMS_PREUV_PF;   // levels of loads in flight in pre_uv_col's forward sweep
 template <class C>
 __device__ __forceinline__ void pre_uv_col(const Dev& d, int i, int j, int dir, const PreCoef& c, int nstp, int nnew,
                                            int nrhs, const C& A, const C& B) {
@@ -265,7 +269,11 @@ __device__ __forceinline__ void pre_uv_col(const Dev& d, int i, int j, int dir, 
   const int N = b.N, indx = 3 - nstp;
   const long n2 = b.n2, ij = IJ(b, i, j);
   const long s = dir == 0 ? 1 : b.nx2;
+#ifdef ROMS_PREUV_SPLINE_PLAIN
+  uv_vert_flux_lds<false>(d, ij, nrhs, dir, A, B);
+#else
   uv_vert_flux_lds<true>(d, ij, nrhs, dir, A, B);
+#endif
   double* Uall = dir == 0 ? F.u : F.v;
   double* __restrict__ rr = (dir == 0 ? F.ru : F.rv) + ij;
   const double* __restrict__ Ustp = Uall + (long)(nstp - 1) * b.n3 + ij;
@@ -330,20 +338,21 @@ __device__ __forceinline__ void pre_uv_col(const Dev& d, int i, int j, int dir, 
     DCk1 = DCk; FCk = FCl; WCk = WCl; CFk = CFl;
     hbK = v.hb; hfK = v.hf; hbKm = v.hbm; hfKm = v.hfm;
   };
-  Lv ring[kPF];
+  constexpr int PF = kPreUvPF;
+  Lv ring[PF];
 #pragma unroll
-  for (int q = 0; q < kPF; q++) ring[q] = load(N - 1 - q);
+  for (int q = 0; q < PF; q++) ring[q] = load(N - 1 - q);
   int k1 = N - 1;
-  for (; k1 - kPF + 1 >= 2; k1 -= kPF) {
+  for (; k1 - PF + 1 >= 2; k1 -= PF) {
 #pragma unroll
-    for (int q = 0; q < kPF; q++) {
+    for (int q = 0; q < PF; q++) {
       const Lv v = ring[q];
-      ring[q] = load(k1 - q - kPF);
+      ring[q] = load(k1 - q - PF);
       iter(k1 - q, v);
     }
   }
 #pragma unroll
-  for (int q = 0; q < kPF; q++)
+  for (int q = 0; q < PF; q++)
     if (k1 - q >= 2) iter(k1 - q, ring[q]);
   const double rd = F.r_D[ij], rdm = F.r_D[ij - s];
   double un = (DCinit(1, hbK, hbKm) + DCk1 * (FCk - fmin0(WCk))) /
