@@ -8,6 +8,10 @@ namespace roms {
 
 void launch_uv_horiz(const Dev& d, hipStream_t s, int nrhs, int up);
 
+#ifndef ROMS_UV1_PF
+#define ROMS_UV1_PF 8
+#endif
+constexpr int kUv1PF = ROMS_UV1_PF;
 // ---- step3d_uv1: implicit viscosity with implicit bottom drag r_D, result
 // stored as Hz*u in u(nnew); rufrc = vertical integral of ru + stresses ----
 template <class C>
@@ -19,7 +23,11 @@ __device__ __forceinline__ void uv1_col(const Dev& d, int i, int j, int dir, int
   const double dt = d.p.dt;
   const long n2 = b.n2, ij = IJ(b, i, j);
   const long s = dir == 0 ? 1 : b.nx2;
-  uv_vert_flux_lds<false>(d, ij, nrhs, dir, A, B);  // plain sweeps measure faster here
+  // spline sweeps with their prefetch rings, and a ring in the Thomas sweep
+  // below: 1.16 -> 0.90 ms at C2 (profiles/r2_m_uv1_ring_ab.txt; the spline
+  // rings alone 1.61 ms, the Thomas ring alone 0.96 at depth 4 and 1.39 at
+  // depth 8).  ROMS_UV1_PF=0 builds the plain form.
+  uv_vert_flux_lds<(kUv1PF > 0)>(d, ij, nrhs, dir, A, B);
   double* __restrict__ Un = (dir == 0 ? F.u : F.v) + (long)(nnew - 1) * b.n3 + ij;
   double* __restrict__ rr = (dir == 0 ? F.ru : F.rv) + ij;
   const double* __restrict__ Hz = F.Hz + ij;
@@ -43,6 +51,48 @@ __device__ __forceinline__ void uv1_col(const Dev& d, int i, int j, int dir, int
   double DCk1 = cff * (Un[(long)(N - 1) * n2] + DC0 * rk(N) + dt * sstr);
   A[N] = DCk1;
   B[N - 1] = CFk;
+#if ROMS_UV1_PF > 0
+  // Forward elimination through a ring of kUv1PF iterations' raw loads,
+  // refilled ahead of each iteration's ru store (the store of level k would
+  // otherwise hold back the ru load of level k-1: same array, offsets the
+  // compiler cannot separate); same expressions and order as the plain loop.
+  struct Lv { double ak, aks, wi, wis, hl, hlm, un, r; };
+  auto load = [&](int k) {   // iteration k: w-level k-1, rho levels k-1 (Hz) and k (u, ru)
+    k = k < 2 ? 2 : k;
+    const long o = (long)(k - 1) * n2, l = o - n2;
+    return Lv{Akv[o], Akv[o - s], Wi[o], Wi[o - s], Hz[l], Hz[l - s], Un[o], rr[o]};
+  };
+  double hK = hz(N - 1), hKm = hzm(N - 1);
+  auto iter = [&](int k, const Lv& v) {
+    const double FCl = 2.0 * dt * (v.ak + v.aks) / (hK + hKm + v.hl + v.hlm);
+    const double WCl = DC0 * 0.5 * (v.wi + v.wis);
+    cff = 1.0 / (0.5 * (hK + hKm) + FCl - fmin0(WCl) + FCk + fmax0(WCk) - CFk * (FCk - fmin0(WCk)));
+    const double CFl = cff * (FCl + fmax0(WCl));
+    const double r = uv_rr_update(v.r, A, k);
+    rr[(long)(k - 1) * n2] = r;
+    const double DCk = cff * (v.un + DC0 * r + DCk1 * (FCk - fmin0(WCk)));
+    B[k - 1] = CFl;
+    A[k] = DCk;
+    DCk1 = DCk; FCk = FCl; WCk = WCl; CFk = CFl;
+    hK = v.hl; hKm = v.hlm;
+  };
+  constexpr int PF = kUv1PF;
+  Lv ring[PF];
+#pragma unroll
+  for (int q = 0; q < PF; q++) ring[q] = load(N - 1 - q);
+  int k1 = N - 1;
+  for (; k1 - PF + 1 >= 2; k1 -= PF) {
+#pragma unroll
+    for (int q = 0; q < PF; q++) {
+      const Lv v = ring[q];
+      ring[q] = load(k1 - q - PF);
+      iter(k1 - q, v);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < PF; q++)
+    if (k1 - q >= 2) iter(k1 - q, ring[q]);
+#else
 #pragma unroll 8
   for (int k = N - 1; k >= 2; k--) {
     const double FCl = 2.0 * dt * (Akv[(long)(k - 1) * n2] + Akv[(long)(k - 1) * n2 - s]) /
@@ -55,6 +105,7 @@ __device__ __forceinline__ void uv1_col(const Dev& d, int i, int j, int dir, int
     A[k] = DCk;
     DCk1 = DCk; FCk = FCl; WCk = WCl; CFk = CFl;
   }
+#endif
   const double rD = F.r_D[ij], rDm = F.r_D[ij - s];
   const double r1 = rk(1);
   double dc = (Un[0] + DC0 * r1 + DCk1 * (FCk - fmin0(WCk))) /
