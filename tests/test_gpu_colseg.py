@@ -64,6 +64,15 @@ def test_seg_routine_parity(case, routine, mode, outs):
     else:
         nrhs, nnew = nstp, 3
     o.set_tindex([iic, kstp, knew, nstp, nrhs, nnew])
+    # level-varying mixing and implicit vertical fluxes, so every per-level
+    # input of the column solves is distinct (without LMD, Akv/Akt are the
+    # constant background and Wi stays zero in these cases)
+    rng = np.random.default_rng(11)
+    for name in ("Akv", "Akt"):
+        a = o.field(name)
+        a[...] = a * (1.0 + 0.5 * rng.random(a.shape))
+    we, wi = o.field("We"), o.field("Wi")
+    wi[...] = wi + 0.01 * float(np.abs(we).max()) * rng.standard_normal(wi.shape)
     res = {}
     for colseg in (1, 0):
         m = make_model(cfg, colseg)
