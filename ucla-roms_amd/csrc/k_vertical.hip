@@ -221,6 +221,9 @@ void launch_set_huv1(const Dev& d, hipStream_t s, const Tlev& t) {
 // omega_tile (omega.F:17-236): bottom-up continuity, grid-motion removal,
 // Courant-limited explicit/implicit split of the vertical flux (We/Wi).
 // ---------------------------------------------------------------------------
+#ifndef ROMS_OMEGA_PF
+#define ROMS_OMEGA_PF 4
+#endif
 __global__ void __launch_bounds__(256) k_omega(Dev d, Range R, double dtau) {
   ROMS_IJ_OR_RETURN(R)
   const Bounds& b = d.b;
@@ -262,6 +265,69 @@ __global__ void __launch_bounds__(256) k_omega(Dev d, Range R, double dtau) {
   Wi[(long)N * n2] = 0.0;
   We[(long)N * n2] = 0.0;
   const double CX0 = dtau * F.pm[ij] * F.pn[ij];
+#if ROMS_OMEGA_PF > 0
+  // Pass 2 through a ring of ROMS_OMEGA_PF levels' raw loads, refilled
+  // ahead of each level's We/Wi stores (which would otherwise hold back every
+  // later load: the compiler cannot prove the arrays apart); the flux values
+  // of level k serve both its divergence and its Courant number, as in the
+  // reference, so each is loaded once.  Same expressions and order.
+  struct Lv { double fu1, fu0, fv1, fv0, hz, zw; };   // rho level m; zw: w-level m-1
+  auto ld = [&](int m) {
+    m = m > N ? N : m;
+    const long o = (long)(m - 1) * n2;
+    return Lv{FU[o + 1], FU[o], FV[o + sj], FV[o], Hz[o], zw[o]};
+  };
+  Lv cur = ld(1);
+  double cx_k = fmax0(cur.fu1) - fmin0(cur.fu0) + fmax0(cur.fv1) - fmin0(cur.fv0), hz_k = cur.hz;
+  wi = 0.0;
+  auto lev = [&](int k, const Lv& up) {
+    const long o1 = (long)k * n2;  // level k+1 (rho layout) == w-level k
+    wi = wi - cur.fu1 + cur.fu0 - cur.fv1 + cur.fv0;
+    if (pidx > 0) wi = wi + pflx * prf[(long)(k - 1) * d.p.npip];
+    double w = wi - wrk * (up.zw - zw0);
+    const double cx_up = fmax0(up.fu1) - fmin0(up.fu0) + fmax0(up.fv1) - fmin0(up.fv0);
+    const double hz_up = up.hz;
+    const double c2d = dmax(cx_k, cx_up);
+    const double dh = dmin(hz_k, hz_up);
+    const double cw_max = cu_max * dh - c2d * CX0;
+    double we;
+    if (cw_max > 0.0) {
+      const double cw_max2 = cw_max * cw_max;
+      const double cw_min = cw_max * cmnx_ratio;
+      const double cw = fabs(w) * CX0;
+      double cff;
+      if (cw < cw_min) cff = cw_max2;
+      else if (cw < cutoff * cw_max) cff = cw_max2 + r4cmx * ((cw - cw_min) * (cw - cw_min));
+      else cff = cw_max * cw;
+      we = cw_max2 * w / cff;
+      w = w - we;
+    } else {
+      we = 0.0;
+    }
+    We[o1] = we;
+    Wi[o1] = w;
+    cx_k = cx_up;
+    hz_k = hz_up;
+    cur = up;
+  };
+  constexpr int PF = ROMS_OMEGA_PF;
+  Lv ring[PF];
+#pragma unroll
+  for (int q = 0; q < PF; q++) ring[q] = ld(2 + q);
+  int k0 = 1;
+  for (; k0 + PF - 1 <= N - 1; k0 += PF) {
+#pragma unroll
+    for (int q = 0; q < PF; q++) {
+      const Lv up = ring[q];
+      ring[q] = ld(k0 + q + 1 + PF);
+      lev(k0 + q, up);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < PF; q++)
+    if (k0 + q <= N - 1) lev(k0 + q, ring[q]);
+}
+#else
   double cx_k = cx(0), hz_k = Hz[0];
   wi = 0.0;
 #pragma unroll 8
@@ -294,6 +360,7 @@ __global__ void __launch_bounds__(256) k_omega(Dev d, Range R, double dtau) {
     hz_k = hz_up;
   }
 }
+#endif
 
 // Closed-edge copies of We/Wi into the boundary ghost row (omega.F:171-232).
 __global__ void k_omega_edges(Dev d) {
