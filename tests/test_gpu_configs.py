@@ -74,6 +74,32 @@ def test_c2_filament_salinity_100_steps():
     m.close()
 
 
+def test_models_in_sequence_are_independent():
+    """A new model's first kernels see its zero-filled arrays, not what an
+    earlier model of the same process left in recycled device memory: the
+    fill is a null-stream hipMemset, which the library's non-blocking stream
+    does not wait for, so dev_alloc waits for it (before that fix the C2
+    100-step test failed in some test-process histories).  A regression
+    guard: the race itself is timing dependent (tools/memset_race.hip shows
+    it directly), and this sequence passed with the unfixed library too."""
+    def run(cfg, n):
+        m = romsgpu.Model.from_case(cfg.case_id, cfg.LLm, cfg.MMm, cfg.N, cfg.NT, salinity=bool(cfg.salinity),
+                                    nonlin_eos=bool(cfg.nonlin_eos), dt=cfg.dt, ndtfast=cfg.ndtfast,
+                                    sizex=cfg.sizex, sizey=cfg.sizey, lmd=cfg.lmd, surf_flux=bool(cfg.surf_flux))
+        m.step(n)
+        out = {k: m.get(k) for k in ("zeta", "ubar", "u", "v", "t", "We")}
+        m.close()
+        return out
+    c2 = c2_cfg(64, 64)
+    a = run(c2, 20)
+    other = basin_cfg(LLm=40, MMm=24, N=50, nonlin=True)   # leaves nonzero data in freed memory
+    other.lmd, other.surf_flux = oracle.LMD_ALL, 1
+    run(other, 5)
+    b = run(c2, 20)
+    for k in a:
+        assert np.array_equal(a[k], b[k]), k
+
+
 def test_c2_full_grid_2_steps():
     """The bench workload itself (512x512x50, NT = 2) for 2 steps."""
     cfg = c2_cfg(512, 512)
