@@ -367,11 +367,17 @@ __global__ void __launch_bounds__(64) k_kpp_int(Dev d, Range R, EdgeClamp ec, in
   // raw interior Kv, Kt (= Ks) at level k from the smoothed Rig (lmd_vmix.F:249-272, 338-353)
   const double* __restrict__ rig = F.lmd_rig;
   const bool rimix = P.lmd_rimix, convec = P.lmd_convec, nonlocal = P.lmd_nonlocal;
-  auto raw_k = [&](int k, double& kv, double& kt) {
+  // raw_k split into its loads (rload) and its arithmetic (rcomp), so the
+  // loads of level k+2 can be issued ahead of level k's stores (which would
+  // otherwise hold them back: the compiler cannot prove the arrays apart)
+  struct RL { double r[3][3]; double zw; };
+  auto rload = [&](int k, RL& L) {
+    if (rimix) load3x3(b, ec, rig + (long)k * n2, i, j, L.r);
+    L.zw = zw[(long)k * n2];
+  };
+  auto rcomp = [&](const RL& L, double& kv, double& kt) {
     if (rimix) {
-      double r[3][3];
-      load3x3(b, ec, rig + (long)k * n2, i, j, r);
-      const double Rig = smooth_point(r, m);
+      const double Rig = smooth_point(L.r, m);
       const double cff = dmin(1., dmax(0., Rig));
       double nu_sx = 1. - cff * cff;
       nu_sx = nu_sx * nu_sx * nu_sx;
@@ -385,7 +391,7 @@ __global__ void __launch_bounds__(64) k_kpp_int(Dev d, Range R, EdgeClamp ec, in
       kv = kNuwm;
       kt = kNuws;
     }
-    const double zwk = zw[(long)k * n2];
+    const double zwk = L.zw;
     const double dist = zwk - zw0;
     if (dist < kLturb) {
       const double mult = sin(0.5 * kPi * (zwk - zw0) / kLturb);
@@ -399,8 +405,7 @@ __global__ void __launch_bounds__(64) k_kpp_int(Dev d, Range R, EdgeClamp ec, in
   double* __restrict__ ghat = F.ghat + ij;
   const bool wet = rm > 0.5;
   // KPP shape functions (lmd_kpp.F:374-446), BKPP (:447-495), masked copy (:496-528)
-  auto finish = [&](int k, double Kv, double Kt, double Ks) {
-    const double zwk = zw[(long)k * n2];
+  auto finish = [&](int k, double Kv, double Kt, double Ks, double zwk) {
     double wm, ws;
     wscale_wm_ws(zwN - zwk, Bfsfc, hbl, ustar, rm, vonKar, wm, ws);
     const double ssgm = (zwN - zwk) / dmax(hbl, kEPS);
@@ -437,15 +442,22 @@ __global__ void __launch_bounds__(64) k_kpp_int(Dev d, Range R, EdgeClamp ec, in
   // bottom-up stream: padding (lmd_vmix.F:359-370) and the in-place ascending
   // 1-2-1 filter Kv(k) = 0.5 Kv(k) + 0.25 Kv(k-1)[filtered] + 0.25 Kv(k+1)[raw] + bak
   double rv, rt;      // raw level k
-  raw_k(1, rv, rt);
+  RL La, Ln;
+  rload(1, La);
+  if (N - 1 >= 2) rload(2, Ln);
+  rcomp(La, rv, rt);
+  double zk = La.zw;  // z_w of level k
   double rvN = rv, rtN = rt;  // raw level N-1 (known once reached)
   double sv = rv + akv, st = rt + akt, ss = rt + aks;  // level 0 (padded)
-  finish(0, sv, st, ss);
+  finish(0, sv, st, ss, zw0);
   for (int k = 1; k <= N - 1; k++) {
     double nv, nt, ns;  // level k+1 before filtering
-    double rvn = 0., rtn = 0.;
+    double rvn = 0., rtn = 0., zk1 = 0.;
     if (k + 1 <= N - 1) {
-      raw_k(k + 1, rvn, rtn);
+      const RL cur = Ln;
+      if (k + 2 <= N - 1) rload(k + 2, Ln);
+      rcomp(cur, rvn, rtn);
+      zk1 = cur.zw;
       nv = rvn; nt = rtn; ns = rtn;
     } else {
       rvN = rv; rtN = rt;
@@ -454,10 +466,10 @@ __global__ void __launch_bounds__(64) k_kpp_int(Dev d, Range R, EdgeClamp ec, in
     sv = 0.5 * rv + 0.25 * sv + 0.25 * nv + akv;
     st = 0.5 * rt + 0.25 * st + 0.25 * nt + akt;
     ss = 0.5 * rt + 0.25 * ss + 0.25 * ns + aks;
-    finish(k, sv, st, ss);
-    rv = rvn; rt = rtn;
+    finish(k, sv, st, ss, zk);
+    rv = rvn; rt = rtn; zk = zk1;
   }
-  finish(N, rvN + akv, rtN + akt, rtN + aks);
+  finish(N, rvN + akv, rtN + akt, rtN + aks, zwN);
   // hbls/hbbl and their closed-wall ghost copies (lmd_kpp.F:530-620)
   F.hbls[ij] = hbl;
   F.hbbl[ij] = bbl;
