@@ -56,7 +56,7 @@ module roms_gpu_mod
   ! LMD switch bits of lmd_mixing (ROMS_LMD_*)
   integer(c_int), parameter :: ROMS_LMD_MIXING = 1, ROMS_LMD_KPP = 2, ROMS_LMD_BKPP = 4, ROMS_LMD_RIMIX = 8, &
                                ROMS_LMD_CONVEC = 16, ROMS_LMD_NONLOCAL = 32
-  integer(c_int), parameter :: ROMS_GPU_ABI = 9   ! ROMS_GPU_ABI_VERSION, include/roms_gpu.h
+  integer(c_int), parameter :: ROMS_GPU_ABI = 10   ! ROMS_GPU_ABI_VERSION, include/roms_gpu.h
   integer(c_int), parameter :: ROMS_FRC_SURFACE = 1, ROMS_FRC_BRY = 2
 
   ! field ids (enum roms_field) used by the drivers below
@@ -275,6 +275,16 @@ module roms_gpu_mod
       import :: c_int, c_char, c_ptr
       character(kind=c_char), intent(in) :: id128(128)
       integer(c_int), value :: nranks, rank, device
+      type(c_ptr), intent(out) :: comm
+    end function
+    ! host channel: allgather is c_funloc of a bind(c) function
+    ! integer(c_int) function f(ctx, send, nbytes, recv) (MPI_Allgather of
+    ! MPI_BYTE over the model's communicator; INTEGRATION.md)
+    integer(c_int) function roms_gpu_comm_create_host(nranks, rank, device, allgather, ctx, comm) bind(c)
+      import :: c_int, c_ptr, c_funptr
+      integer(c_int), value :: nranks, rank, device
+      type(c_funptr), value :: allgather
+      type(c_ptr), value :: ctx
       type(c_ptr), intent(out) :: comm
     end function
   end interface

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define ROMS_GPU_ABI_VERSION 9
+#define ROMS_GPU_ABI_VERSION 10
 #define ROMS_MAX_FAST 288
 
 /* Subdomain geometry of this rank: param.F / dimensions.F / mpi_setup.F:39-210 */
@@ -244,11 +244,24 @@ int roms_gpu_init_case_comm(const roms_case *c, int np_xi, int np_eta, void *com
 int roms_gpu_comm_unique_id(void *id128);
 int roms_gpu_comm_create(const void *id128, int nranks, int rank, int device, void **comm);
 int roms_gpu_comm_create_local(int group, int nranks, int rank, void **comm);
+/* Host channel: the host supplies its own allgather (every rank calls it
+ * with the same nbytes; recv holds nranks * nbytes, rank r's bytes at
+ * r * nbytes; returns 0 on success) -- MPI_Allgather(MPI_BYTE) over the
+ * reference's communicator (mpi_exchanges.F, mpi_setup.F), a file or socket
+ * channel in a test.  It carries only the IPC handles at init and the small
+ * diag / area-volume gathers; every halo exchange moves GPU to GPU by IPC
+ * peer writes, with RCCL out of the loop.  roms_gpu_init fails if the IPC
+ * transport cannot be set up (its self-test reference is a host-staged
+ * exchange over the same channel).                                          */
+typedef int (*roms_host_allgather_fn)(void *ctx, const void *send, long nbytes, void *recv);
+int roms_gpu_comm_create_host(int nranks, int rank, int device, roms_host_allgather_fn allgather, void *ctx,
+                              void **comm);
 int roms_gpu_comm_destroy(void *comm);
 /* Halo transport of this rank after roms_gpu_init: 0 = RCCL send/recv (or
- * single rank / in-process), 1 = IPC peer writes (enabled after a start-up
- * self-test against RCCL; ROMS_GPU_HALO_IPC=0 disables), -1 = IPC with a
- * timed-out arrival wait since init.                                        */
+ * single rank / in-process), 1 = IPC peer writes (RCCL communicator: enabled
+ * after a start-up self-test against RCCL, ROMS_GPU_HALO_IPC=0 disables;
+ * host-channel communicator: always), -1 = IPC with a timed-out arrival wait
+ * since init.                                                               */
 int roms_gpu_halo_transport(void);
 /* Host-only: neighbour ranks (-1 none), per-level message sizes for the 8
  * directions W,E,S,N,SW,SE,NW,NE, and the strip extents {i0,i1,j0,j1}.      */

@@ -309,6 +309,7 @@ void or_u3dbc(or_state *S) {
             cext = cext * dtw * 0.5 * (A2(S->pm, istr - 1, j) + A2(S->pm, istr, j));
           }
           U(istr, j, k, nn) = ub;
+          if (S->ub[SW]) cext = dmax(cext, dmin(S->ub[SW][j], 1.0));   /* SPONGE_TUNE (u3dbc_im.F:101-103) */
           U(istr, j, k, nn) = (1. - cext) * U(istr, j, k, nn) + cext * B2(bry_u, SW, j, k);
           U(istr, j, k, nn) = U(istr, j, k, nn) * A2(S->umask, istr, j);
         }
@@ -334,6 +335,7 @@ void or_u3dbc(or_state *S) {
             cext = cext * dtw * 0.5 * (A2(S->pm, iend, j) + A2(S->pm, iend + 1, j));
           }
           U(iend + 1, j, k, nn) = ub;
+          if (S->ub[SE]) cext = dmax(cext, dmin(S->ub[SE][j], 1.0));   /* SPONGE_TUNE (u3dbc_im.F:190-192) */
           U(iend + 1, j, k, nn) = (1. - cext) * U(iend + 1, j, k, nn) + cext * B2(bry_u, SE, j, k);
           U(iend + 1, j, k, nn) = U(iend + 1, j, k, nn) * A2(S->umask, iend + 1, j);
         }
@@ -359,6 +361,7 @@ void or_u3dbc(or_state *S) {
           else { cext = -cx; cx = 0.; }
           U(i, jstr - 1, k, nn) = (1. - cx) * (U(i, jstr - 1, k, ns) - fmax0(cy) * G(0, i - 1) - fmin0(cy) * G(0, i)) +
                                   cx * (U(i, jstr, k, ns) - fmax0(cy) * G(1, i - 1) - fmin0(cy) * G(1, i));
+          if (S->ub[SS]) cext = dmax(cext, dmin(S->ub[SS][i], 1.0));   /* SPONGE_TUNE (u3dbc_im.F:262-264) */
           U(i, jstr - 1, k, nn) = (1. - cext) * U(i, jstr - 1, k, nn) + cext * B2(bry_u, SS, i, k);
           U(i, jstr - 1, k, nn) = U(i, jstr - 1, k, nn) * A2(S->umask, i, jstr - 1);
         }
@@ -386,6 +389,7 @@ void or_u3dbc(or_state *S) {
           else { cext = -cx; cx = 0.; }
           U(i, jend + 1, k, nn) = (1. - cx) * (U(i, jend + 1, k, ns) - fmax0(cy) * G(1, i - 1) - fmin0(cy) * G(1, i)) +
                                   cx * (U(i, jend, k, ns) - fmax0(cy) * G(0, i - 1) - fmin0(cy) * G(0, i));
+          if (S->ub[SN]) cext = dmax(cext, dmin(S->ub[SN][i], 1.0));   /* SPONGE_TUNE (u3dbc_im.F:341-343) */
           U(i, jend + 1, k, nn) = (1. - cext) * U(i, jend + 1, k, nn) + cext * B2(bry_u, SN, i, k);
           U(i, jend + 1, k, nn) = U(i, jend + 1, k, nn) * A2(S->umask, i, jend + 1);
         }
@@ -427,6 +431,7 @@ void or_v3dbc(or_state *S) {
             cext = cext * dtw * 0.5 * (A2(S->pn, i, jstr - 1) + A2(S->pn, i, jstr));
           }
           V(i, jstr, k, nn) = vb;
+          if (S->ub[SS]) cext = dmax(cext, dmin(S->ub[SS][i], 1.0));   /* SPONGE_TUNE (v3dbc_im.F:97-99) */
           V(i, jstr, k, nn) = (1. - cext) * V(i, jstr, k, nn) + cext * B2(bry_v, SS, i, k);
           V(i, jstr, k, nn) = V(i, jstr, k, nn) * A2(S->vmask, i, jstr);
         }
@@ -452,6 +457,7 @@ void or_v3dbc(or_state *S) {
             cext = cext * dtw * 0.5 * (A2(S->pn, i, jend) + A2(S->pn, i, jend + 1));
           }
           V(i, jend + 1, k, nn) = vb;
+          if (S->ub[SN]) cext = dmax(cext, dmin(S->ub[SN][i], 1.0));   /* SPONGE_TUNE (v3dbc_im.F:189-191) */
           V(i, jend + 1, k, nn) = (1. - cext) * V(i, jend + 1, k, nn) + cext * B2(bry_v, SN, i, k);
           V(i, jend + 1, k, nn) = V(i, jend + 1, k, nn) * A2(S->vmask, i, jend + 1);
         }
@@ -477,6 +483,7 @@ void or_v3dbc(or_state *S) {
           else { cext = -cx; cx = 0.; }
           V(istr - 1, j, k, nn) = (1. - cx) * (V(istr - 1, j, k, ns) - fmax0(cy) * G(0, j - 1) - fmin0(cy) * G(0, j)) +
                                   cx * (V(istr, j, k, ns) - fmax0(cy) * G(1, j - 1) - fmin0(cy) * G(1, j));
+          if (S->ub[SW]) cext = dmax(cext, dmin(S->ub[SW][j], 1.0));   /* SPONGE_TUNE (v3dbc_im.F:264-266) */
           V(istr - 1, j, k, nn) = (1. - cext) * V(istr - 1, j, k, nn) + cext * B2(bry_v, SW, j, k);
           V(istr - 1, j, k, nn) = V(istr - 1, j, k, nn) * A2(S->vmask, istr - 1, j);
         }
@@ -504,6 +511,7 @@ void or_v3dbc(or_state *S) {
           else { cext = -cx; cx = 0.; }
           V(iend + 1, j, k, nn) = (1. - cx) * (V(iend + 1, j, k, ns) - fmax0(cy) * G(1, j - 1) - fmin0(cy) * G(1, j)) +
                                   cx * (V(iend, j, k, ns) - fmax0(cy) * G(0, j - 1) - fmin0(cy) * G(0, j));
+          if (S->ub[SE]) cext = dmax(cext, dmin(S->ub[SE][j], 1.0));   /* SPONGE_TUNE (v3dbc_im.F:344-346) */
           V(iend + 1, j, k, nn) = (1. - cext) * V(iend + 1, j, k, nn) + cext * B2(bry_v, SE, j, k);
           V(iend + 1, j, k, nn) = V(iend + 1, j, k, nn) * A2(S->vmask, iend + 1, j);
         }

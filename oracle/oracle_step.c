@@ -1528,9 +1528,13 @@ void or_step3d_t(or_state *S) {
                                                                     A2(S->pipe_flx, i, j) * S->pipe_prf[k - 1] *
                                                                     S->pipe_trc[itrc - 1];
         }
+      /* heat of rain (step3d_t_ISO.F:939-951): BULK_FRC uses the 2 m air
+       * temperature tair, otherwise the water's own t(N)/Hz(N) */
       if (itrc == 1)
         for (int i = S->istr; i <= S->iend; i++)
-          TT(i, j, N, nnew, itrc) = TT(i, j, N, nnew, itrc) + dt * A2(S->swflx, i, j) * TT(i, j, N, nnew, itrc) / HZ(i, j, N);
+          TT(i, j, N, nnew, itrc) = TT(i, j, N, nnew, itrc) +
+                                    dt * A2(S->swflx, i, j) *
+                                        (S->c.bulk_frc ? A2(S->tair, i, j) : TT(i, j, N, nnew, itrc) / HZ(i, j, N));
       for (int i = S->istr; i <= S->iend; i++)
         TT(i, j, N, nnew, itrc) = TT(i, j, N, nnew, itrc) + dt * S->stflx[O2(i, j) + (size_t)(itrc - 1) * S->n2];
       if (S->c.lmd) {

@@ -104,3 +104,37 @@ def test_bulk_requires_bulk_case():
     with pytest.raises(romsgpu.RomsGpuError):
         m.bulk_flux()
     m.close()
+
+
+def test_bulk_rain_heat_uses_air_temperature():
+    """step3d_t_ISO.F:939-951: under BULK_FRC the heat of rain is
+    dt*swflx*tair (2 m air temperature), not dt*swflx*t(N)/Hz(N).  step3d_t
+    on identical corrector states with tair as set and shifted by +5 degC:
+    each matches the oracle, and the shift moves T in every wet column with
+    fresh-water flux while S stays put (this failed before the restatement
+    was fixed: tair did not enter step3d_t at all)."""
+    cfg = bulk_cfg(LLm=40, MMm=32, N=16)
+    res = {}
+    for shift in (0.0, 5.0):
+        o, m = make_pair(cfg)
+        o.step(4)
+        iic, kstp, knew, nstp, nrhs, nnew = o.tindex()
+        nrhs, nnew = 3, 3 - nstp
+        o.set_tindex([iic, kstp, knew, nstp, nrhs, nnew])
+        o.field("tair")[...] += shift
+        copy_state(o, m)
+        m.set_tindex(iic, kstp, knew, nstp, nrhs, nnew, iif=1, nfast=o.nfast())
+        o.call("step3d_t")
+        m.step3d_t()
+        m.sync()
+        check_fields(o, m, ["t"], cfg.LLm, cfg.MMm, RTOL_ROUTINE)
+        t = m.get("t").reshape(cfg.NT, 3, cfg.N, cfg.MMm + 4, cfg.LLm + 4)[:, nnew - 1]
+        res[shift] = (t.copy(), o.field("swflx").reshape(cfg.MMm + 4, cfg.LLm + 4).copy())
+        m.close()
+    t0, sw = res[0.0]
+    t1 = res[5.0][0]
+    wet = (np.abs(sw) > 0)[2:-2, 2:-2]
+    assert wet.sum() > 0
+    dT = (t1[0, -1] - t0[0, -1])[2:-2, 2:-2]
+    assert np.all(dT[wet] != 0.0)
+    assert np.array_equal(t1[1], t0[1])   # salinity does not see tair

@@ -46,7 +46,7 @@ def pair(cfg):
                                 nonlin_eos=bool(cfg.nonlin_eos), dt=cfg.dt, ndtfast=cfg.ndtfast, sizex=cfg.sizex,
                                 sizey=cfg.sizey, lmd=cfg.lmd, surf_flux=bool(cfg.surf_flux), obc=cfg.obc,
                                 v_sponge=cfg.v_sponge, island=bool(cfg.island), curvgrid=bool(cfg.curvgrid),
-                                uv_adv=bool(cfg.uv_adv), uv_cor=bool(cfg.uv_cor))
+                                uv_adv=bool(cfg.uv_adv), uv_cor=bool(cfg.uv_cor), bulk_frc=bool(cfg.bulk_frc))
     return o, m
 
 
@@ -116,7 +116,9 @@ def c4_cfg(NT=2, L=192, sponge=1.0e3, island=1):
     c = basin_cfg(LLm=L, MMm=L, N=20, NT=NT, nonlin=True, dt=900.0, ndtfast=30, sizex=15.0e3 * L,
                   sizey=15.0e3 * L)
     c.obc, c.ubind, c.v_sponge, c.island, c.curvgrid = 15, 0.1, sponge, island, 1
-    c.lmd, c.surf_flux = oracle.LMD_ICELAND, 1
+    # BULK_FRC (cppdefs.opt:15) over the synthetic analytic atmosphere: the
+    # surface fluxes, u* under KPP and the rain heat of step3d_t come from it
+    c.lmd, c.surf_flux, c.bulk_frc = oracle.LMD_ICELAND, 0, 1
     return c
 
 
@@ -124,7 +126,7 @@ def _case(cfg):
     return dict(case_id=cfg.case_id, LLm=cfg.LLm, MMm=cfg.MMm, N=cfg.N, NT=cfg.NT, salinity=bool(cfg.salinity),
                 nonlin_eos=bool(cfg.nonlin_eos), dt=cfg.dt, ndtfast=cfg.ndtfast, sizex=cfg.sizex, sizey=cfg.sizey,
                 lmd=cfg.lmd, surf_flux=bool(cfg.surf_flux), obc=cfg.obc, v_sponge=cfg.v_sponge,
-                island=bool(cfg.island), curvgrid=bool(cfg.curvgrid))
+                island=bool(cfg.island), curvgrid=bool(cfg.curvgrid), bulk_frc=bool(cfg.bulk_frc))
 
 
 @pytest.mark.parametrize("NT", [2, 10], ids=["C4", "C5"])
@@ -135,7 +137,9 @@ def test_c4_c5_single_domain_vs_oracle(NT):
     o.step(40)
     m.step(40)
     m.sync()
-    check_fields(o, m, PROGNOSTIC + ["Akv", "Akt", "hbls", "hbbl"], cfg.LLm, cfg.MMm, RMS_RUN, kind="rms")
+    check_fields(o, m, PROGNOSTIC + ["Akv", "Akt", "hbls", "hbbl", "stflx", "swflx", "sustr"], cfg.LLm, cfg.MMm,
+                 RMS_RUN, kind="rms")
+    assert float(np.max(np.abs(o.field("swflx")))) > 0.0   # rain: the BULK_FRC heat-of-rain term is live
     if NT == 10:   # every passive tracer separately (each carries its own blob)
         a, b = m.get("t"), o.field("t")
         n3 = cfg.N
@@ -185,3 +189,31 @@ def test_invalid_lmd_sets_are_rejected():
         with pytest.raises(romsgpu.RomsGpuError):
             romsgpu.Model.from_case(1, 16, 16, 8, 2, salinity=True, nonlin_eos=True, lmd=bad, dt=60.0, ndtfast=30,
                                     sizex=32e3, sizey=32e3)
+
+
+def c3_cfg(L=64, M=48, N=100):
+    """C3's switch set and time step exactly as bench.py --workload c3 runs
+    it: the closed synthetic basin, NONLIN+SPLIT EOS, T+S,
+    LMD_MIXING+KPP+BKPP+RIMIX+NONLOCAL without LMD_CONVEC, wind stress,
+    dt = 300 s, ndtfast = 60 (nfast 82), N = 100 (the segment solvers), on
+    a smaller horizontal grid with the bench's 2 km spacing."""
+    c = basin_cfg(LLm=L, MMm=M, N=N, nonlin=True, dt=300.0, ndtfast=60, sizex=2.0e3 * L, sizey=2.0e3 * M)
+    c.lmd = oracle.LMD_ICELAND
+    return c
+
+
+def test_c3_exact_switches_20_steps_vs_oracle():
+    cfg = c3_cfg()
+    o, m = pair(cfg)
+    assert m.t.nfast == 82
+    o.step(20)
+    m.step(20)
+    m.sync()
+    check_fields(o, m, PROGNOSTIC + ["Akv", "Akt", "hbls", "hbbl", "ghat"], cfg.LLm, cfg.MMm, RMS_RUN, kind="rms")
+    m.close()
+
+
+def test_c3_2x2_n100_bitwise_equals_single_domain():
+    """C3's 2x2 split at N = 100: 101-level halo messages and the segment
+    solvers next to the rank edges, bitwise equal to the single domain."""
+    check_decomposition(_case(c3_cfg(L=72, M=56)), 2, 2, nsteps=3)

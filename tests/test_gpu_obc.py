@@ -209,3 +209,59 @@ def test_sponge_tune_limits():
     j = np.arange(1, cfg.MMm + 1)
     assert np.array_equal(t[:, :, j + 1, 1], tw[:, :, j] * rm[j + 1, 1])   # western ghost column i = 0
     m.close()
+
+
+@pytest.mark.parametrize("routine", ["pre_step3d", "step3d_uv2"])
+def test_sponge_tune_uv3dbc_parity_and_sensitivity(routine):
+    """SPONGE_TUNE on the 3-D momentum edges (u3dbc_im.F:101-103,190-192,
+    262-264,341-343; v3dbc_im.F:97-99,189-191,264-266,344-346): the Orlanski
+    blend's rate is floored by min(ub, 1) on all four sides, normal and
+    tangential.  Both routines that call u3dbc/v3dbc on identical states,
+    ghost rows included, against the oracle; and the edge values move when
+    ub is switched on (this failed before the floor was restated)."""
+    cfg = obc_cfg(obc=15, lmd=oracle.LMD_ICELAND)
+    ub = _ub_arrays(cfg, 1.0)
+    res = {}
+    for tuned in (False, True):
+        o, m = make_pair(cfg)
+        if tuned:
+            o.set_ub(ub)
+            m.set_ub_tune(ub)
+        o.step(3)
+        iic, kstp, knew, nstp, nrhs, nnew = o.tindex()
+        nrhs, nnew = (nstp, 3) if routine == "pre_step3d" else (3, 3 - nstp)
+        o.set_tindex([iic, kstp, knew, nstp, nrhs, nnew])
+        copy_state(o, m)
+        m.set_tindex(iic, kstp, knew, nstp, nrhs, nnew, iif=2, nfast=o.nfast())
+        o.call(routine)
+        getattr(m, routine)()
+        m.sync()
+        bad = [(n, full(m.get(n), o.field(n))) for n in ("u", "v")]
+        bad = [x for x in bad if not x[1] <= RTOL_ROUTINE]
+        assert not bad, (routine, tuned, bad)
+        res[tuned] = (m.get("u").copy(), m.get("v").copy())
+        m.close()
+    L, M = cfg.LLm, cfg.MMm
+    u0, u1 = res[False][0], res[True][0]
+    v0, v1 = res[False][1], res[True][1]
+    # western u column (i = 1 -> index 2) and southern v row (j = 1 -> index 2)
+    assert not np.array_equal(u0[..., 3:M + 1, 2], u1[..., 3:M + 1, 2])
+    assert not np.array_equal(v0[..., 2, 3:L + 1], v1[..., 2, 3:L + 1])
+    # tangential: southern u ghost row (j = 0) and western v ghost column (i = 0)
+    assert not np.array_equal(u0[..., 1, 3:L + 1], u1[..., 1, 3:L + 1])
+    assert not np.array_equal(v0[..., 3:M + 1, 1], v1[..., 3:M + 1, 1])
+
+
+def test_sponge_tune_uv_20_steps_rms():
+    """ub_tune on, 20 steps of the Iceland switch set: u, v, t against the oracle."""
+    cfg = obc_cfg(obc=15, lmd=oracle.LMD_ICELAND)
+    ub = _ub_arrays(cfg, 1.0)
+    o, m = make_pair(cfg)
+    o.set_ub(ub)
+    m.set_ub_tune(ub)
+    o.step(20)
+    m.step(20)
+    for n in ("zeta", "ubar", "vbar", "u", "v", "t"):
+        a, b = m.get(n), o.field(n)
+        assert float(np.sqrt(np.mean((a - b) ** 2))) / max(1.0, float(np.sqrt(np.mean(b ** 2)))) < RMS_RUN, n
+    m.close()

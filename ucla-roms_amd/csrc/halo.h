@@ -3,6 +3,7 @@
 #include <string>
 #include <vector>
 
+#include "../../include/roms_gpu.h"
 #include "roms_dev.h"
 
 namespace roms {
@@ -57,6 +58,7 @@ struct Halo {
   double* rbuf = nullptr;  // 8 x cap receive messages
   double* dred = nullptr;  // gather staging
   long cap = 0;
+  long gcnt = 0;           // host channel: largest per-level message over all ranks
   // fast-loop overlap (launch_step2d): exchange on a second stream while the
   // next fast step's interior tiles run; `pending` = an exchange not yet
   // joined back into the library stream
@@ -71,6 +73,7 @@ struct Halo {
 int comm_unique_id(void* out128);
 RomsComm* comm_create_rccl(const void* id128, int nranks, int rank, std::string& err);
 RomsComm* comm_create_local(int group, int nranks, int rank);
+RomsComm* comm_create_host(int nranks, int rank, roms_host_allgather_fn fn, void* ctx);
 void comm_destroy(RomsComm* c);
 int comm_rank(const RomsComm* c);
 int comm_size(const RomsComm* c);

@@ -202,11 +202,16 @@ std::map<int, LocalGroup*> g_groups;
 }  // namespace
 
 struct RomsComm {
-  int kind;  // 1 = RCCL, 2 = threads of one process
+  int kind;  // 1 = RCCL, 2 = threads of one process, 3 = host channel (IPC halos)
   int rank, nranks;
   ncclComm_t nccl;
   LocalGroup* grp;
   int route_self;  // test hook: send self-messages through RCCL as well
+  // kind 3: the host's own allgather (MPI_Allgather of bytes in a Fortran
+  // host, mpi_exchanges.F's communicator); carries the IPC handles at setup
+  // and the diag / area-volume gathers, never halo payloads
+  roms_host_allgather_fn hfn;
+  void* hctx;
 };
 
 int comm_unique_id(void* out) {
@@ -229,6 +234,9 @@ RomsComm* comm_create_rccl(const void* id, int nranks, int rank, std::string& er
   rc->route_self = env && env[0] == '1';
   return rc;
 }
+RomsComm* comm_create_host(int nranks, int rank, roms_host_allgather_fn fn, void* ctx) {
+  return new RomsComm{3, rank, nranks, nullptr, nullptr, 0, fn, ctx};
+}
 RomsComm* comm_create_local(int group, int nranks, int rank) {
   std::lock_guard<std::mutex> lk(g_groups_m);
   LocalGroup*& gp = g_groups[group];
@@ -238,7 +246,7 @@ RomsComm* comm_create_local(int group, int nranks, int rank) {
     gp->sbuf.assign(nranks, nullptr);
     gp->red.assign(nranks, {});
   }
-  return new RomsComm{2, rank, nranks, nullptr, gp, 0};
+  return new RomsComm{2, rank, nranks, nullptr, gp, 0, nullptr, nullptr};
 }
 void comm_destroy(RomsComm* c) {
   if (!c) return;
@@ -273,9 +281,40 @@ HaloPlan halo_plan(int Lm, int Mm, int npx, int npe, int inode, int jnode, int e
 
 static void ipc_release(Halo& H);
 
+// Host-staged exchange over a host-channel communicator (kind 3): the packed
+// messages travel through the host's allgather (every rank's 8 messages in
+// one fixed-size block of 8 x gcnt x nl doubles) and are scattered from the
+// neighbours' blocks.  Only the IPC self-test uses it: it is the reference
+// the peer-write transport must reproduce bitwise before it is enabled.
+static int exchange_host(const Halo& H, hipStream_t s, const ExchList& L) {
+  const HaloGeom& g = H.plan.g;
+  RomsComm* c = H.comm;
+  int nl = 0;
+  for (int q = 0; q < L.n; q++) nl += L.nlev[q];
+  long mx = 0;
+  for (int d = 0; d < 8; d++) mx = g.cnt[d] > mx ? g.cnt[d] : mx;
+  const dim3 grid((unsigned)((mx + 255) / 256), (unsigned)nl, 8);
+  hipLaunchKernelGGL(k_halo_pack, grid, dim3(256), 0, s, g, L, H.sbuf, H.cap);
+  const long m = H.gcnt * nl;
+  std::vector<double> mine((size_t)8 * m, 0.0), all((size_t)8 * m * c->nranks);
+  for (int d = 0; d < 8; d++)
+    if (g.active[d] &&
+        copy_on(mine.data() + d * m, H.sbuf + d * H.cap, (size_t)(nl * g.cnt[d]) * sizeof(double),
+                hipMemcpyDeviceToHost, s) != hipSuccess)
+      return -2;
+  if (c->hfn(c->hctx, mine.data(), (long)((size_t)8 * m * sizeof(double)), all.data()) != 0) return -3;
+  for (int h = 0; h < 8; h++)
+    if (g.active[h] &&
+        copy_on(H.rbuf + h * H.cap, all.data() + ((size_t)H.plan.peer[h] * 8 + kOpp[h]) * m,
+                (size_t)(nl * g.cnt[h]) * sizeof(double), hipMemcpyHostToDevice, s) != hipSuccess)
+      return -2;
+  hipLaunchKernelGGL(k_halo_unpack, grid, dim3(256), 0, s, g, L, H.rbuf, H.cap);
+  return hipStreamSynchronize(s) == hipSuccess ? 0 : -2;
+}
+
 // IPC transport setup: buffers, handle exchange (allgather over the RCCL
-// communicator), mapping of the neighbours' buffers, then a self-test that
-// must reproduce the RCCL exchange bitwise on every rank (kSelfTestRounds
+// communicator or the host channel), mapping of the neighbours' buffers, then a self-test that
+// must reproduce the RCCL (host channel: host-staged) exchange bitwise on every rank (kSelfTestRounds
 // exchanges of a two-level test field, alternating buffer parities, several
 // exchanges queued back to back) before the transport is used.  Any failure
 // anywhere leaves every rank on RCCL; every rank takes part in every
@@ -362,7 +401,14 @@ static void ipc_setup(Halo& H) {
       // the reference result: RCCL; then the IPC exchanges queued back to
       // back on the stream (both parities, no host sync in between)
       I.ok = 0;
-      for (int r = 0; r < kSelfTestRounds; r++) halo_exchange(H, s, ExchList{{A[r]}, {2}, 1});
+      for (int r = 0; r < kSelfTestRounds; r++) {
+        const ExchList LA{{A[r]}, {2}, 1};
+        if (c->kind == 3) {
+          if (exchange_host(H, s, LA) != 0) ok = 0.0;
+        } else {
+          halo_exchange(H, s, LA);
+        }
+      }
       I.ok = 1;
       for (int r = 0; r < kSelfTestRounds; r++) halo_exchange(H, s, ExchList{{B[r]}, {2}, 1});
       I.ok = 0;
@@ -444,6 +490,22 @@ int halo_setup(Halo& H, RomsComm* comm, const HaloPlan& plan, int maxlev, std::s
     const char* e = getenv("ROMS_GPU_HALO_IPC");
     if (!(e && e[0] == '0')) ipc_setup(H);
   }
+  if (comm && comm->kind == 3) {
+    // the host-staged self-test blocks: every rank uses the largest message of any rank
+    double mine = (double)mx;
+    std::vector<double> all((size_t)comm->nranks);
+    if (halo_allgather(H, H.cs, &mine, 1, all.data()) != 0) {
+      err = "halo_setup: host-channel allgather failed";
+      return -5;
+    }
+    for (double v : all) H.gcnt = (long)v > H.gcnt ? (long)v : H.gcnt;
+    ipc_setup(H);
+    if (!H.ipc.ok) {
+      err = "halo_setup: the IPC halo transport of the host-channel communicator failed its setup or self-test "
+            "(use roms_gpu_comm_create for RCCL)";
+      return -5;
+    }
+  }
   return 0;
 }
 static void ipc_release(Halo& H) {
@@ -481,7 +543,7 @@ long halo_map(const HaloPlan& P, int dir, int unpack, int* iv, int* jv) {
   return n;
 }
 
-bool halo_graph_safe(const Halo* H) { return !H || !H->comm || H->comm->kind == 1; }
+bool halo_graph_safe(const Halo* H) { return !H || !H->comm || H->comm->kind == 1 || H->comm->kind == 3; }
 
 namespace {
 IpcPtrs ipc_ptrs(const Halo& H) {
@@ -533,6 +595,9 @@ void halo_exchange(const Halo& H, hipStream_t s, const ExchList& L) {
       if (g.active[h] && H.plan.peer[h] == me && !c->route_self)
         (void)hipMemcpyAsync(H.rbuf + h * H.cap, H.sbuf + kOpp[h] * H.cap, (size_t)(nl * g.cnt[h]) * sizeof(double),
                              hipMemcpyDeviceToDevice, s);
+  } else if (c->kind == 3) {
+    (void)exchange_host(H, s, L);   // setup failed; roms_gpu_init has already returned the error
+    return;
   } else {
     LocalGroup* G = c->grp;
     (void)hipStreamSynchronize(s);
@@ -569,6 +634,10 @@ int halo_allgather(const Halo& H, hipStream_t s, const double* in, int n, double
     return 0;
   }
   if (n > 64) return -1;
+  if (c->kind == 3) {
+    if (hipStreamSynchronize(s) != hipSuccess) return -2;
+    return c->hfn(c->hctx, in, (long)((size_t)n * sizeof(double)), out) == 0 ? 0 : -3;
+  }
   if (c->kind == 1) {
     double* dsend = H.dred;        // 64 doubles
     double* dall = H.dred + 64;    // 64 * nranks doubles

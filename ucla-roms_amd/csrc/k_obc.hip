@@ -78,6 +78,7 @@ __global__ void __launch_bounds__(256) k_u3dbc_obc(Dev d, int nnew, int nstp, in
           cext = bry > 0. ? bry : d.p.ubind;
           cext = cext * dtfwd * 0.5 * (pm(is - 1, j) + pm(is, j));
         }
+        if (F.ub[0]) cext = fmax(cext, fmin(F.ub[0][j], 1.0));   // SPONGE_TUNE ub_west (u3dbc_im.F:101-103)
         val = (1. - cext) * ub + cext * bry;
         val = val * F.umask[IJ(b, is, j)];
       }
@@ -96,6 +97,7 @@ __global__ void __launch_bounds__(256) k_u3dbc_obc(Dev d, int nnew, int nstp, in
           cext = bry < 0. ? -bry : d.p.ubind;
           cext = cext * dtfwd * 0.5 * (pm(ie, j) + pm(ie + 1, j));
         }
+        if (F.ub[1]) cext = fmax(cext, fmin(F.ub[1][j], 1.0));   // SPONGE_TUNE ub_east (u3dbc_im.F:190-192)
         val = (1. - cext) * ub + cext * bry;
         val = val * F.umask[IJ(b, ie + 1, j)];
       }
@@ -121,6 +123,7 @@ __global__ void __launch_bounds__(256) k_u3dbc_obc(Dev d, int nnew, int nstp, in
         double cext;
         double val = orl_tangential(cx, cy, U(i, jb, nstp), U(i, ji, nstp), gr(i - 1, jb), gr(i, jb), gr(i - 1, ji),
                                     gr(i, ji), cext);
+        if (F.ub[side]) cext = fmax(cext, fmin(F.ub[side][i], 1.0));   // ub_south/north (u3dbc_im.F:262-264,341-343)
         val = (1. - cext) * val + cext * F.bu[side][i + (long)nbry(b, side) * (k - 1)];
         un[IJKL(b, i, jb, k, nnew)] = val * F.umask[IJ(b, i, jb)];
       } else {
@@ -171,6 +174,7 @@ __global__ void __launch_bounds__(256) k_v3dbc_obc(Dev d, int nnew, int nstp, in
           cext = bry > 0. ? bry : d.p.ubind;
           cext = cext * dtfwd * 0.5 * (pn(i, js - 1) + pn(i, js));
         }
+        if (F.ub[2]) cext = fmax(cext, fmin(F.ub[2][i], 1.0));   // SPONGE_TUNE ub_south (v3dbc_im.F:97-99)
         val = (1. - cext) * vb + cext * bry;
         val = val * F.vmask[IJ(b, i, js)];
       }
@@ -189,6 +193,7 @@ __global__ void __launch_bounds__(256) k_v3dbc_obc(Dev d, int nnew, int nstp, in
           cext = bry < 0. ? -bry : d.p.ubind;
           cext = cext * dtfwd * 0.5 * (pn(i, je) + pn(i, je + 1));
         }
+        if (F.ub[3]) cext = fmax(cext, fmin(F.ub[3][i], 1.0));   // SPONGE_TUNE ub_north (v3dbc_im.F:189-191)
         val = (1. - cext) * vb + cext * bry;
         val = val * F.vmask[IJ(b, i, je + 1)];
       }
@@ -214,6 +219,7 @@ __global__ void __launch_bounds__(256) k_v3dbc_obc(Dev d, int nnew, int nstp, in
         double cext;
         double val = orl_tangential(cx, cy, V(ib, j, nstp), V(ii, j, nstp), gr(ib, j - 1), gr(ib, j), gr(ii, j - 1),
                                     gr(ii, j), cext);
+        if (F.ub[side]) cext = fmax(cext, fmin(F.ub[side][j], 1.0));   // ub_west/east (v3dbc_im.F:264-266,344-346)
         val = (1. - cext) * val + cext * F.bv[side][j + (long)nbry(b, side) * (k - 1)];
         vn[IJKL(b, ib, j, k, nnew)] = val * F.vmask[IJ(b, ib, j)];
       } else {

@@ -81,7 +81,8 @@ __global__ void __launch_bounds__(64) k_step3d_t_v(Dev d, Range R, int nnew, int
       double t = tnk - dt * F.pm[ij] * F.pn[ij] * (A[k] - A[k - 1]);
       if (pidx > 0) t = t + dt * F.pm[ij] * F.pn[ij] * pflx * F.pipe_prf[(pidx - 1) + (k - 1) * P.npip] * ptrc;
       if (k == N) {
-        if (itrc == 1) t = t + dt * F.swflx[ij] * t / Hz[o];
+        // heat of rain: 2 m air temperature under BULK_FRC, else the water's (step3d_t_ISO.F:939-951)
+        if (itrc == 1) t = t + dt * F.swflx[ij] * (P.bulk_frc ? F.tair[ij] : t / Hz[o]);
         t = t + dt * stf;
       }
       if (kppT) {
@@ -223,7 +224,7 @@ __global__ void __launch_bounds__(kSegBlock) k_step3d_t_seg(Dev d, Range R, int 
     t = t - dt * F.pm[ij] * F.pn[ij] * dfl;
     if (pidx > 0) t = t + dt * F.pm[ij] * F.pn[ij] * pflx * F.pipe_prf[(pidx - 1) + (k - 1) * P.npip] * ptrc;
     if (k == N) {
-      if (itrc == 1) t = t + dt * F.swflx[ij] * t / Hz[o];
+      if (itrc == 1) t = t + dt * F.swflx[ij] * (P.bulk_frc ? F.tair[ij] : t / Hz[o]);
       t = t + dt * stf;
     }
     if (kppT) {

@@ -961,6 +961,16 @@ int roms_gpu_comm_create(const void* id128, int nranks, int rank, int device, vo
   *comm = c;
   return 0;
 }
+int roms_gpu_comm_create_host(int nranks, int rank, int device, roms_host_allgather_fn allgather, void* ctx,
+                              void** comm) {
+  if (!allgather || !comm || nranks < 1 || rank < 0 || rank >= nranks) {
+    g.err = "roms_gpu_comm_create_host: bad argument";
+    return -1;
+  }
+  CHECK_HIP(hipSetDevice(device));
+  *comm = comm_create_host(nranks, rank, allgather, ctx);
+  return 0;
+}
 int roms_gpu_comm_create_local(int group, int nranks, int rank, void** comm) {
   if (!comm || nranks < 1 || rank < 0 || rank >= nranks) { g.err = "roms_gpu_comm_create_local: bad argument"; return -1; }
   *comm = comm_create_local(group, nranks, rank);

@@ -126,6 +126,8 @@ def load_library(path=LIB_PATH):
     L.roms_gpu_comm_create.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        P(ctypes.c_void_p)]
     L.roms_gpu_comm_create_local.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, P(ctypes.c_void_p)]
+    L.roms_gpu_comm_create_host.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, HOST_ALLGATHER_FN,
+                                            ctypes.c_void_p, P(ctypes.c_void_p)]
     L.roms_gpu_comm_destroy.argtypes = [ctypes.c_void_p]
     L.roms_gpu_halo_plan.argtypes = [ctypes.c_int] * 8 + [P(ctypes.c_int), P(ctypes.c_long), P(ctypes.c_int)]
     L.roms_gpu_halo_map.argtypes = [ctypes.c_int] * 10 + [P(ctypes.c_int), P(ctypes.c_int), ctypes.c_long]
@@ -223,8 +225,74 @@ def comm_create_local(group, nranks, rank):
     return h
 
 
+# roms_host_allgather_fn of include/roms_gpu.h
+HOST_ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p)
+_host_channels = {}   # comm handle value -> the ctypes callback (kept alive while the handle is)
+
+
+def comm_create_host(nranks, rank, allgather, device=0):
+    """Host-channel communicator: `allgather(data: bytes) -> list of nranks
+    bytes objects` is the host's own collective (the MPI_Allgather a Fortran
+    host passes); halos then move by IPC peer writes with RCCL out of the loop."""
+    L = load_library()
+
+    def fn(_ctx, send, nbytes, recv):
+        try:
+            parts = allgather(ctypes.string_at(send, nbytes))
+            if len(parts) != nranks or any(len(x) != nbytes for x in parts):
+                return -1
+            ctypes.memmove(recv, b"".join(parts), nbytes * nranks)
+            return 0
+        except Exception:   # a failed collective is reported as a status, never raised through C
+            return -1
+
+    cb = HOST_ALLGATHER_FN(fn)
+    h = ctypes.c_void_p()
+    _check(L, L.roms_gpu_comm_create_host(nranks, rank, device, cb, None, ctypes.byref(h)), "roms_gpu_comm_create_host")
+    _host_channels[h.value] = cb
+    return h
+
+
+class FileAllgather:
+    """A host allgather through files in a shared directory (tests and
+    single-node runs without MPI): call k of every rank writes its bytes to
+    ag<k>.<rank> and reads everyone's.  A rank's file of call k-2 is removed at
+    call k: by then every rank has finished reading it."""
+
+    def __init__(self, path, nranks, rank, timeout=120.0):
+        self.path, self.n, self.r, self.timeout, self.k = path, nranks, rank, timeout, 0
+
+    def _f(self, k, r):
+        return os.path.join(self.path, "ag%d.%d" % (k, r))
+
+    def __call__(self, data):
+        import time
+        k = self.k
+        self.k += 1
+        tmp = self._f(k, self.r) + ".tmp"
+        with open(tmp, "wb") as fh:
+            fh.write(data)
+        os.rename(tmp, self._f(k, self.r))
+        if k >= 2:
+            try:
+                os.remove(self._f(k - 2, self.r))
+            except OSError:
+                pass
+        out, t0 = [], time.time()
+        for r in range(self.n):
+            f = self._f(k, r)
+            while not os.path.exists(f):
+                if time.time() - t0 > self.timeout:
+                    raise TimeoutError("allgather %d: rank %d missing" % (k, r))
+                time.sleep(0.001)
+            with open(f, "rb") as fh:
+                out.append(fh.read())
+        return out
+
+
 def comm_destroy(h):
     load_library().roms_gpu_comm_destroy(h)
+    _host_channels.pop(getattr(h, "value", h), None)
 
 
 class Model:
