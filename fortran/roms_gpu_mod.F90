@@ -256,6 +256,11 @@ module roms_gpu_mod
       integer(c_int), value :: kinds
     end function
     ! the tidal arrays are c_loc(...) of (GLOBAL_2D_ARRAY, ntides) arrays, or c_null_ptr
+    integer(c_int) function roms_gpu_frc_clock(start_time, on) bind(c)
+      import :: c_int, c_double
+      real(c_double), value :: start_time
+      integer(c_int), value :: on
+    end function
     integer(c_int) function roms_gpu_set_tide_data(ntides, ftide, pot_re, pot_im, ztide_re, ztide_im, &
                                                    utide_re, utide_im, vtide_re, vtide_im) bind(c)
       import :: c_int, c_double, c_ptr

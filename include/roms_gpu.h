@@ -294,6 +294,18 @@ long roms_gpu_halo_map(int Lm, int Mm, int np_xi, int np_eta, int inode, int jno
 #define ROMS_FRC_BRY     2
 int roms_gpu_frc_record(int field_id, int slot, double rec_time, const double *data);
 int roms_gpu_frc_interp(double modtime, int kinds);
+/* In-step forcing: with on = 1, every roms_gpu_step interpolates each field
+ * that holds two records at the reference's own points of roms_step, with
+ * time = start_time + dt*(iic - ntstart) [s] (main.F:373): surface fields at
+ * frc_time 'current' before the first set_forces work (BULK_FRC flux), the
+ * open-boundary data at '1/2 fwd' followed by set_tides, surface fields at
+ * '1/2 fwd' before the second set_forces, boundary data at 'forward' (from
+ * tdays = time + dt/2) followed by set_tides (main.F:384-441,
+ * roms_read_write.F:330-336).  The weights are formed on the host per step
+ * and read by the step graph from device memory.  A step whose time falls
+ * outside a field's records fails (roms_read_write.F:381-388) before
+ * anything is queued.  on = 0: the host interpolates (roms_gpu_frc_interp).  */
+int roms_gpu_frc_clock(double start_time, int on);
 int roms_gpu_set_tide_data(int ntides, const double *ftide, const double *pot_re, const double *pot_im,
                            const double *ztide_re, const double *ztide_im, const double *utide_re,
                            const double *utide_im, const double *vtide_re, const double *vtide_im);
@@ -317,7 +329,11 @@ int roms_gpu_set_tides(double time);
  * behind the next steps.  roms_gpu_io_wait joins the pending write and
  * returns its status.  roms_gpu_get_init replaces get_init (get_init.F): see
  * rst_io.hip for the EXACT_RESTART protocol (call it with tindx 2 on record
- * rec-1, then tindx 1 on rec, then roms_gpu_init_sequence).                 */
+ * rec-1, then tindx 1 on rec, then roms_gpu_init_sequence).  With LMD,
+ * roms_gpu_swr_frac must have run once at rest (after roms_gpu_set_depth
+ * on zeta = 0, main.F:216-220) before get_init; init_sequence fails
+ * otherwise.  After a negative return of get_init the fields it had read
+ * are already replaced: the model state is invalid until re-initialised.    */
 #define ROMS_WRT_Z    1
 #define ROMS_WRT_UB   2
 #define ROMS_WRT_VB   4
@@ -325,7 +341,7 @@ int roms_gpu_set_tides(double time);
 #define ROMS_WRT_V    16
 #define ROMS_WRT_T    32     /* all tracers (tracers.opt wrt_t)              */
 #define ROMS_WRT_R    64     /* rho1 (SPLIT_EOS) or rho                      */
-#define ROMS_WRT_O    128    /* omega (We)                                   */
+#define ROMS_WRT_O    128    /* omega = pm*pn*(We+Wi), m/s (basic_output.F:374-384) */
 #define ROMS_WRT_AKV  256
 #define ROMS_WRT_AKT  512
 #define ROMS_WRT_AKS  1024

@@ -85,6 +85,9 @@ def lib():
         L.or_set_river.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                    ctypes.POINTER(ctypes.c_double)]
         L.or_set_ub.argtypes = [ctypes.c_void_p] + [ctypes.POINTER(ctypes.c_double)] * 4
+        L.or_frc_record.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_double,
+                                    ctypes.POINTER(ctypes.c_double)]
+        L.or_frc_clock.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.c_int]
         _lib = L
     return _lib
 
@@ -197,6 +200,18 @@ class Oracle:
         keep = [None if a is None else np.ascontiguousarray(a, dtype=np.float64) for a in ub]
         args = [None if a is None else a.ctypes.data_as(P) for a in keep]
         self.L.or_set_ub(self.h, *args)
+
+    def frc_record(self, name, slot, rec_time, arr):
+        """set_frc_data record `slot` (0/1) of field `name` at rec_time [days]."""
+        a = np.ascontiguousarray(arr, dtype=np.float64).ravel()
+        if self.L.or_frc_record(self.h, name.encode(), slot, rec_time,
+                                a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))) != 0:
+            raise KeyError(name)
+
+    def frc_clock(self, start_time, on=True):
+        """Interpolate the recorded fields at roms_step's set_forces /
+        set_bry_all points (main.F:373-441), time = start + dt*(iic-ntstart)."""
+        self.L.or_frc_clock(self.h, start_time, int(on))
 
     def call(self, routine, *args):
         getattr(self.L, "or_" + routine)(self.h, *args)

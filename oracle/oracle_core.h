@@ -60,6 +60,11 @@ struct or_state {
   double *sustr, *svstr, *stflx, *srflx, *swflx;
   /* BULK_FRC inputs and rho-point stresses (bulk_frc.F, surf_flux.F) */
   double *uwnd, *vwnd, *tair, *qair, *prate, *swrad, *lwrad, *sustr_r, *svstr_r;
+  /* set_frc_data's two records per field (roms_read_write.F:303-392) and the
+     in-step interpolation points of roms_step (main.F:373-441) */
+  struct { double *dst; size_t n; int bry; double t[2]; double *rec[2]; } frc[64];
+  int nfrc, frc_clock;
+  double frc_start;
   /* private scratch (A3d(:,1..4), A2d(:,1..)) */
   double *ru, *rv, *P, *rhos3;         /* 3-D scratch */
   double *s2[14];                      /* 2-D scratch */

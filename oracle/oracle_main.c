@@ -82,6 +82,7 @@ void or_destroy(or_state *S) {
   if (!S) return;
   /* process exit reclaims memory in tests; free the big ones */
   free(S->u); free(S->v); free(S->t); free(S->zeta); free(S->ubar); free(S->vbar);
+  for (int q = 0; q < S->nfrc; q++) { free(S->frc[q].rec[0]); free(S->frc[q].rec[1]); }
   free(S);
 }
 
@@ -638,9 +639,10 @@ void or_ana_init(or_state *S) {
 void or_ana_forces(or_state *S) {
   if (S->c.case_id == OR_CASE_BASIN && S->c.bulk_frc) {
     /* BULK_FRC with a synthetic analytic atmosphere (C4 stand-in):
-       westerly jet, air 2-3 degC below the sea surface, humid, light rain */
+       westerly jet, air 2-3 degC below the sea surface, humid, light rain;
+       with the in-step clock on, the atmosphere comes from the records */
     const double pi = 3.14159265358979323;
-    for (int j = -1; j <= S->Mm + 2; j++)
+    for (int j = -1; j <= S->Mm + 2 && !S->frc_clock; j++)
       for (int i = -1; i <= S->Lm + 2; i++) {
         const double x = A2(S->xr, i, j), y = A2(S->yr, i, j);
         A2(S->uwnd, i, j) = 8.0 * sin(pi * y / S->c.sizey);
@@ -762,6 +764,42 @@ int or_init(or_state *S) {
   return 0;
 }
 
+/* set_frc_data (roms_read_write.F:303-392): records of one field, it1 the
+ * earlier, cff1*rec(it1) + cff2*rec(it2) at modtime [days] */
+int or_frc_record(or_state *S, const char *name, int slot, double time, const double *data) {
+  size_t n = 0;
+  double *dst = or_field(S, name, &n);
+  if (!dst || slot < 0 || slot > 1) return -1;
+  int q = 0;
+  while (q < S->nfrc && S->frc[q].dst != dst) q++;
+  if (q == S->nfrc) {
+    if (S->nfrc == 64) return -1;
+    S->nfrc++;
+    S->frc[q].dst = dst;
+    S->frc[q].n = n;
+    S->frc[q].bry = strstr(name, "_west") || strstr(name, "_east") || strstr(name, "_south") || strstr(name, "_north");
+    S->frc[q].rec[0] = S->frc[q].rec[1] = NULL;
+  }
+  if (!S->frc[q].rec[slot]) S->frc[q].rec[slot] = zalloc(n);
+  memcpy(S->frc[q].rec[slot], data, n * sizeof(double));
+  S->frc[q].t[slot] = time;
+  return 0;
+}
+void or_frc_clock(or_state *S, double start_time, int on) {
+  S->frc_clock = on;
+  S->frc_start = start_time;
+}
+static void frc_interp(or_state *S, int bry, double modtime) {
+  for (int q = 0; q < S->nfrc; q++) {
+    if (S->frc[q].bry != bry || !S->frc[q].rec[0] || !S->frc[q].rec[1]) continue;
+    const int it1 = S->frc[q].t[0] <= S->frc[q].t[1] ? 0 : 1, it2 = 1 - it1;
+    const double t1 = S->frc[q].t[it1], t2 = S->frc[q].t[it2];
+    const double cff1 = (t2 - modtime) / (t2 - t1), cff2 = (modtime - t1) / (t2 - t1);
+    for (size_t m = 0; m < S->frc[q].n; m++)
+      S->frc[q].dst[m] = cff1 * S->frc[q].rec[it1][m] + cff2 * S->frc[q].rec[it2][m];
+  }
+}
+
 /* ---------------------------------------------------------------------- */
 /* roms_step (main.F:333-520)                                              */
 /* ---------------------------------------------------------------------- */
@@ -770,7 +808,13 @@ int or_step(or_state *S) {
   S->nstp = 1 + (S->iic - S->ntstart) % 2;
   S->nrhs = S->nstp;
   S->nnew = 3;
+  /* model clock and the set_frc_data times of main.F:373-441 */
+  const double sec2day = 1. / 86400., dt = S->dt;
+  const double time = S->frc_start + dt * (double)(S->iic - S->ntstart);
+  const double tdays = time * sec2day;
+  if (S->frc_clock) frc_interp(S, 0, tdays);                        /* set_forces, 'current' */
   or_ana_forces(S);
+  if (S->frc_clock) frc_interp(S, 1, tdays + 0.5 * dt * sec2day);   /* set_bry_all, '1/2 fwd' */
   or_rho_eos(S, S->nrhs);
   or_set_HUV(S);
   or_omega(S);
@@ -782,8 +826,10 @@ int or_step(or_state *S) {
   S->nnew = 3 - S->nstp;
   or_omega(S);
   or_rho_eos(S, S->nrhs);
+  if (S->frc_clock) frc_interp(S, 0, tdays + 0.5 * dt * sec2day);   /* set_forces, '1/2 fwd' */
   if (S->c.bulk_frc) or_bulk_flux(S);   /* set_forces (main.F:433) */
   if (S->c.lmd) or_lmd_vmix(S, S->nrhs);
+  if (S->frc_clock) frc_interp(S, 1, (time + 0.5 * dt) * sec2day + dt * sec2day);   /* 'forward' */
   or_prsgrd(S);
   or_step3d_uv1(S);
   or_visc3d(S);

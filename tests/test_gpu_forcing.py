@@ -102,3 +102,68 @@ def test_tide_data_needs_pairs():
     with pytest.raises(romsgpu.RomsGpuError, match="come together"):
         m.set_tide_data([1e-4], pot=(np.zeros(shp), None))
     m.close()
+
+
+ATMOS = ("uwnd", "vwnd", "tair", "qair", "prate", "swrad", "lwrad")
+BRY = tuple("%s_%s" % (v, e) for v in ("zeta", "ubar", "vbar", "u", "v", "t") for e in ("west", "east", "south", "north"))
+PERTURB = dict(uwnd=lambda a: 1.3 * a, vwnd=lambda a: a + 1.0, tair=lambda a: a + 2.0, qair=lambda a: 0.9 * a,
+               prate=lambda a: 2.0 * a, swrad=lambda a: 1.2 * a, lwrad=lambda a: a + 10.0,
+               zeta=lambda a: a + 0.02, ubar=lambda a: 0.5 * a, vbar=lambda a: 0.5 * a, u=lambda a: 0.5 * a,
+               v=lambda a: 0.5 * a, t=lambda a: a + 0.3)
+
+
+def _clocked_pair(clock):
+    from test_gpu_parity import PROGNOSTIC  # noqa: F401
+    c = basin_cfg(LLm=40, MMm=32, N=12, nonlin=True)
+    c.obc, c.ubind, c.lmd, c.bulk_frc = 15, 0.1, oracle.LMD_ICELAND, 1
+    o = oracle.Oracle(c)
+    o.init()
+    m = romsgpu.Model.from_case(c.case_id, c.LLm, c.MMm, c.N, c.NT, salinity=True, nonlin_eos=True, dt=c.dt,
+                                ndtfast=c.ndtfast, sizex=c.sizex, sizey=c.sizey, lmd=c.lmd, obc=15, bulk_frc=True)
+    t0, t1 = 0.0, 10 * c.dt / 86400.0   # records [days] around the first 12 steps
+    for name in ATMOS + BRY:
+        a = o.field(name).copy()
+        b = PERTURB[name.split("_")[0]](a)
+        for side in ((o,), (m,)):
+            side[0].frc_record(name, 0, t0, a)
+            side[0].frc_record(name, 1, t1, b)
+    if clock:
+        o.frc_clock(0.0)
+        m.frc_clock(0.0)
+    return c, o, m
+
+
+def test_in_step_forcing_two_records_vs_oracle():
+    """Time-varying forcing inside roms_gpu_step: two different
+    records of every BULK_FRC atmospheric field and of every open-boundary
+    array; each step interpolates them at the reference's four points
+    (main.F:384-441: surface at 'current' and '1/2 fwd', boundary data at
+    '1/2 fwd' and 'forward'), on the device and in the oracle, which does the
+    same in plain C.  12 steps (graph replay from step 2) against the oracle,
+    RMS < 1e-10; and the result is not that of one interpolation per step."""
+    from test_gpu_parity import PROGNOSTIC, RMS_RUN, check_fields
+    c, o, m = _clocked_pair(True)
+    o.step(12)
+    m.step(12)
+    m.sync()
+    check_fields(o, m, PROGNOSTIC + ["stflx", "swflx", "sustr", "uwnd", "tair", "hbls"], c.LLm, c.MMm, RMS_RUN,
+                 kind="rms")
+    for n in ("u_west", "t_north", "zeta_south"):   # boundary data at 'forward' of step 12
+        assert np.array_equal(m.get(n).ravel(), o.field(n).ravel()), n
+    got = m.get("t").copy()
+    m.close()
+    # interpolating once per step at 'current' (the host-driven path) gives another state
+    c2, o2, m2 = _clocked_pair(False)
+    for k in range(12):
+        m2.frc_interp(c2.dt * k / 86400.0)
+        m2.step()
+    assert not np.array_equal(m2.get("t"), got)
+    m2.close()
+
+
+def test_in_step_forcing_out_of_window_fails_before_queueing():
+    c, o, m = _clocked_pair(True)
+    m.frc_clock(100 * 86400.0)   # far past the records
+    with pytest.raises(romsgpu.RomsGpuError, match="outside the forcing records"):
+        m.step()
+    m.close()

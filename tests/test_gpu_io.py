@@ -66,7 +66,9 @@ def test_history_records_equal_device_state(tmp_path):
     for rec in (1, 2):
         m.step(3)
         m.wrt_his(p, rec, rec, m.time(FIL["dt"]), mask=romsgpu.WRT_DEFAULT | romsgpu.WRT["O"])
-        snaps.append((state(m), m.get("We"), m.t.iic))
+        # history omega is pm*pn*(We+Wi) in m/s (basic_output.F:374-384)
+        om = m.get("pm")[0] * m.get("pn")[0] * (m.get("We") + m.get("Wi"))
+        snaps.append((state(m), om, m.t.iic))
         m.step(1)   # keeps stepping while the writer drains the snapshot
     m.io_wait()
     L, M = m.Lm, m.Mm

@@ -103,3 +103,23 @@ def test_river_update_riv_vol_trc():
     m.step(3)
     check_fields(o, m, PROGNOSTIC, cfg.LLm, cfg.MMm, RMS_RUN, kind="rms")
     m.close()
+
+
+def test_river_count_below_face_indices_is_rejected():
+    """Faces kept from an earlier call index riv_vol up to their largest river
+    number: a smaller nriv without new faces fails loudly instead of reading
+    past the new arrays on the device; with the faces passed
+    again it is accepted."""
+    m = romsgpu.Model.from_case(3, 40, 40, 10, 2, salinity=True, nonlin_eos=True, dt=20.0, ndtfast=30,
+                                sizex=10e3, sizey=10e3, lmd=True)
+    uf = np.zeros((42 + 2, 42 + 2))
+    vf = np.zeros_like(uf)
+    uf[10, 5] = 10 * 1 + 0.5   # river 1 through one u face ...
+    uf[11, 5] = 10 * 2 + 0.5   # ... river 2 through the next
+    m.set_river_frc([500.0, 300.0], [[24.0, 1.0], [20.0, 2.0]], uf, vf)
+    with pytest.raises(romsgpu.RomsGpuError, match="largest river index"):
+        m.set_river_frc([500.0], [[24.0, 1.0]])
+    uf[11, 5] = 0.0
+    m.set_river_frc([500.0], [[24.0, 1.0]], uf, vf)   # new faces: accepted
+    m.step(1)
+    m.close()

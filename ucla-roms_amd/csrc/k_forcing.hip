@@ -37,15 +37,38 @@ struct TideData {
   double *pr = nullptr, *pi = nullptr;                       // pot_Re/pot_Im (ntides x n2)
   double *zr = nullptr, *zi = nullptr, *ur = nullptr, *ui = nullptr, *vr = nullptr, *vi = nullptr;
 };
+// the in-step schedule (roms_gpu_frc_clock)
+struct FrcStep {
+  bool on = false;
+  double start = 0.0;        // start_time [s] (time = start + dt*(iic-ntstart), main.F:373)
+  long gen = 1;              // bumped when captured graphs would go stale
+  std::vector<int> ids;      // fields with both records: interpolated inside the step
+  double* dev = nullptr;     // [4 points][ids][2 slots] weights, then cos/sin of the tides
+  size_t dev_n = 0;
+  double* pin[4] = {};       // pinned staging ring, one event each
+  hipEvent_t ev[4] = {};
+  size_t pin_n = 0;
+  int ring = 0;
+};
 struct FrcCtx {
   std::vector<FrcField> f;
   TideData tide;
+  FrcStep st;
 };
 thread_local FrcCtx fc;
 
 __global__ void __launch_bounds__(256) k_frc_interp(double* __restrict__ out, const double* __restrict__ a,
                                                     const double* __restrict__ b, double cff1, double cff2, long n) {
   for (long q = blockIdx.x * 256L + threadIdx.x; q < n; q += (long)gridDim.x * 256L) out[q] = cff1 * a[q] + cff2 * b[q];
+}
+
+// weights from device memory (the in-step schedule): out = c[0]*slot0 + c[1]*slot1,
+// which is cff1*rec(it1) + cff2*rec(it2) to the bit in either slot order
+__global__ void __launch_bounds__(256) k_frc_interp_dev(double* __restrict__ out, const double* __restrict__ a,
+                                                        const double* __restrict__ b, const double* __restrict__ c,
+                                                        long n) {
+  const double c0 = c[0], c1 = c[1];
+  for (long q = blockIdx.x * 256L + threadIdx.x; q < n; q += (long)gridDim.x * 256L) out[q] = c0 * a[q] + c1 * b[q];
 }
 
 // set_tides_tile, pot_tides part: ptide over (istrR-1..iendR, jstrR-1..jendR)
@@ -111,13 +134,148 @@ int field_kind(int id) {
   return ROMS_FRC_SURFACE;
 }
 
+// set_tides_tile on the device (tides.F:106-254) with cos/sin of omT in dcs
+// (ntides each); bry: also the open-boundary sums
+void launch_tides(const Dev& d, hipStream_t s, const double* dcs, bool pot, bool bry) {
+  const TideData& T = fc.tide;
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  if (T.pr && pot) {
+    const long n = (long)(b.iendR - b.istrR + 2) * (b.jendR - b.jstrR + 2);
+    hipLaunchKernelGGL(k_tide_pot, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, b, F.ptide, T.pr, T.pi, dcs,
+                       dcs + T.ntides, T.ntides);
+  }
+  if (T.zr && d.p.obc && bry) {
+    TideBry B{};
+    for (int q = 0; q < 4; q++) { B.z[q] = F.bzeta[q]; B.u[q] = F.bubar[q]; B.v[q] = F.bvbar[q]; }
+    B.zr = T.zr; B.zi = T.zi; B.ur = T.ur; B.ui = T.ui; B.vr = T.vr; B.vi = T.vi;
+    B.obc = d.p.obc;
+    const int n = (b.Lm > b.Mm ? b.Lm : b.Mm) + 4;
+    hipLaunchKernelGGL(k_tide_bry, dim3((unsigned)((n + 255) / 256), 4), dim3(256), 0, s, b, B, dcs, dcs + T.ntides,
+                       T.ntides);
+  }
+}
+
+// (it1, it2) and the weights of set_frc_data (roms_read_write.F:330-388) at
+// modtime [days]; false when modtime is outside the records' window
+bool frc_weights(const FrcField& F, double modtime, double dt, double& c0, double& c1) {
+  const int it1 = F.time[0] <= F.time[1] ? 0 : 1, it2 = 1 - it1;
+  const double t1 = F.time[it1], t2 = F.time[it2];
+  if (!(t2 > t1) || t1 > modtime + dt || t2 < modtime - dt) return false;
+  const double cff1 = (t2 - modtime) / (t2 - t1), cff2 = (modtime - t1) / (t2 - t1);
+  c0 = it1 == 0 ? cff1 : cff2;
+  c1 = it1 == 0 ? cff2 : cff1;
+  return true;
+}
+
 }  // namespace
+
+long frc_step_gen() { return fc.st.on ? fc.st.gen : 0; }
+
+int frc_step_prepare(hipStream_t s, const Dev& d, double dt, const roms_tlev& t, std::string& err) {
+  FrcStep& st = fc.st;
+  if (!st.on) return 0;
+  (void)d;
+  std::vector<int> ids;
+  for (int id = 0; id < (int)fc.f.size(); id++)
+    if (fc.f[id].have[0] && fc.f[id].have[1]) ids.push_back(id);
+  if (ids != st.ids) { st.ids = ids; st.gen++; }
+  const int nid = (int)ids.size(), nt = fc.tide.ntides;
+  const size_t n = (size_t)8 * nid + 2 * nt + 1;
+  if (st.dev_n < n) {
+    if (st.dev) { (void)hipStreamSynchronize(s); (void)hipFree(st.dev); st.dev = nullptr; }
+    if (hipMalloc(&st.dev, n * sizeof(double)) != hipSuccess) { err = "frc_step: allocation failed"; st.dev_n = 0; return -2; }
+    st.dev_n = n;
+    st.gen++;
+  }
+  if (st.pin_n < n) {
+    for (int r = 0; r < 4; r++) {
+      if (st.ev[r]) (void)hipEventSynchronize(st.ev[r]);
+      if (st.pin[r]) (void)hipHostFree(st.pin[r]);
+      st.pin[r] = nullptr;
+      if (hipHostMalloc((void**)&st.pin[r], n * sizeof(double), hipHostMallocDefault) != hipSuccess) {
+        err = "frc_step: pinned allocation failed";
+        st.pin_n = 0;
+        return -2;
+      }
+      if (!st.ev[r] && hipEventCreateWithFlags(&st.ev[r], hipEventDisableTiming) != hipSuccess) {
+        err = "frc_step: event creation failed";
+        return -2;
+      }
+    }
+    st.pin_n = n;
+  }
+  // main.F:373-441: time of step n, and the four set_frc_data model times
+  const double sec2day = 1. / 86400.;
+  const double time = st.start + dt * (double)(t.iic - t.ntstart);
+  const double tdays = time * sec2day;
+  const double mod[4] = {tdays,                                      // set_forces, frc_time 'current'
+                         tdays + 0.5 * dt * sec2day,                 // set_bry_all, '1/2 fwd'
+                         tdays + 0.5 * dt * sec2day,                 // set_forces, '1/2 fwd'
+                         (time + 0.5 * dt) * sec2day + dt * sec2day};  // set_bry_all, 'forward'
+  const int r = st.ring;
+  (void)hipEventSynchronize(st.ev[r]);   // its previous copy has landed
+  double* h = st.pin[r];
+  for (int p = 0; p < 4; p++)
+    for (int q = 0; q < nid; q++) {
+      const FrcField& F = fc.f[ids[q]];
+      double* c = h + ((size_t)p * nid + q) * 2;
+      c[0] = c[1] = 0.0;
+      if ((p % 2 == 0) != (F.kind == ROMS_FRC_SURFACE)) continue;
+      if (!frc_weights(F, mod[p], dt, c[0], c[1])) {
+        err = "roms_gpu_step: model time outside the forcing records of field " + std::to_string(ids[q]) +
+              " (set_frc_data, roms_read_write.F:381-388)";
+        return -1;
+      }
+    }
+  for (int q = 0; q < nt; q++) {   // omT = ftide*(time + 0.5*dt) (tides.F:129), both set_tides calls
+    const double omT = fc.tide.ftide[q] * (time + 0.5 * dt);
+    h[(size_t)8 * nid + q] = std::cos(omT);
+    h[(size_t)8 * nid + nt + q] = std::sin(omT);
+  }
+  if (hipMemcpyAsync(st.dev, h, n * sizeof(double), hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipEventRecord(st.ev[r], s) != hipSuccess) {
+    err = "frc_step: weight upload failed";
+    return -2;
+  }
+  st.ring = (r + 1) % 4;
+  return 0;
+}
+
+void frc_step_phase(const Dev& d, hipStream_t s, int phase, bool pot_tides) {
+  const FrcStep& st = fc.st;
+  if (!st.on || !st.dev) return;
+  const int nid = (int)st.ids.size();
+  const int kind = phase % 2 == 0 ? ROMS_FRC_SURFACE : ROMS_FRC_BRY;
+  bool bry = false;
+  for (int q = 0; q < nid; q++) {
+    const int id = st.ids[q];
+    const FrcField& F = fc.f[id];
+    if (F.kind != kind) continue;
+    if (id >= ROMS_zeta_west && id <= ROMS_vbar_north) bry = true;
+    const long nb = (F.n + 255) / 256;
+    hipLaunchKernelGGL(k_frc_interp_dev, dim3((unsigned)(nb < 8192 ? nb : 8192)), dim3(256), 0, s, shim_field(id),
+                       F.slot[0], F.slot[1], st.dev + ((size_t)phase * nid + q) * 2, F.n);
+  }
+  // set_tides after each set_bry_all (main.F:394,441): the boundary sums go
+  // onto freshly interpolated zeta/ubar/vbar data only
+  if (kind == ROMS_FRC_BRY && fc.tide.ntides > 0) launch_tides(d, s, st.dev + (size_t)8 * nid, pot_tides, bry);
+}
 
 void frc_free() {
   for (FrcField& f : fc.f)
     for (double*& p : f.slot)
       if (p) { (void)hipFree(p); p = nullptr; }
   fc.f.clear();
+  FrcStep& st = fc.st;
+  if (st.dev) { (void)hipFree(st.dev); st.dev = nullptr; }
+  for (int r = 0; r < 4; r++) {
+    if (st.ev[r]) { (void)hipEventSynchronize(st.ev[r]); (void)hipEventDestroy(st.ev[r]); st.ev[r] = nullptr; }
+    if (st.pin[r]) { (void)hipHostFree(st.pin[r]); st.pin[r] = nullptr; }
+  }
+  const long gen = st.gen + 1;
+  st = FrcStep{};
+  st.gen = gen;
   TideData& T = fc.tide;
   for (double** p : {&T.pr, &T.pi, &T.zr, &T.zi, &T.ur, &T.ui, &T.vr, &T.vi})
     if (*p) { (void)hipFree(*p); *p = nullptr; }
@@ -146,6 +304,7 @@ int roms_gpu_frc_record(int field_id, int slot, double rec_time, const double* d
       *S.err = "roms_gpu_frc_record: allocation failed";
       return -2;
     }
+    fc.st.gen++;   // a captured step graph does not know this buffer
   }
   F.n = n;
   F.kind = field_kind(field_id);
@@ -189,6 +348,16 @@ int roms_gpu_frc_interp(double modtime, int kinds) {
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
+int roms_gpu_frc_clock(double start_time, int on) {
+  ShimState S;
+  int r = shim_enter(S);
+  if (r) return r;
+  fc.st.on = on != 0;
+  fc.st.start = start_time;
+  fc.st.gen++;
+  return 0;
+}
+
 int roms_gpu_set_tide_data(int ntides, const double* ftide, const double* pot_re, const double* pot_im,
                            const double* ztide_re, const double* ztide_im, const double* utide_re,
                            const double* utide_im, const double* vtide_re, const double* vtide_im) {
@@ -203,8 +372,10 @@ int roms_gpu_set_tide_data(int ntides, const double* ftide, const double* pot_re
     return -1;
   }
   TideData& T = fc.tide;
+  (void)hipStreamSynchronize(S.s);   // a queued step may still read the old constituents
   for (double** p : {&T.pr, &T.pi, &T.zr, &T.zi, &T.ur, &T.ui, &T.vr, &T.vi})
     if (*p) { (void)hipFree(*p); *p = nullptr; }
+  fc.st.gen++;
   T.ntides = ntides;
   T.ftide.assign(ftide, ftide + ntides);
   const size_t nb = (size_t)ntides * S.d->b.n2 * sizeof(double);
@@ -226,7 +397,6 @@ int roms_gpu_set_tides(double time) {
   if (r) return r;
   TideData& T = fc.tide;
   if (T.ntides == 0) return 0;
-  const Bounds& b = S.d->b;
   // omT = ftide*(time + 0.5*dt) (tides.F:129); cos/sin once per constituent, on the host
   std::vector<double> cs(T.ntides), sn(T.ntides);
   for (int t = 0; t < T.ntides; t++) {
@@ -242,21 +412,7 @@ int roms_gpu_set_tides(double time) {
     *S.err = "roms_gpu_set_tides: upload failed";
     return -2;
   }
-  const Fields& F = S.d->f;
-  if (T.pr && S.cfg->pot_tides) {
-    const long n = (long)(b.iendR - b.istrR + 2) * (b.jendR - b.jstrR + 2);
-    hipLaunchKernelGGL(k_tide_pot, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, S.s, b, F.ptide, T.pr, T.pi, dcs,
-                       dcs + T.ntides, T.ntides);
-  }
-  if (T.zr && S.d->p.obc) {
-    TideBry B{};
-    for (int q = 0; q < 4; q++) { B.z[q] = F.bzeta[q]; B.u[q] = F.bubar[q]; B.v[q] = F.bvbar[q]; }
-    B.zr = T.zr; B.zi = T.zi; B.ur = T.ur; B.ui = T.ui; B.vr = T.vr; B.vi = T.vi;
-    B.obc = S.d->p.obc;
-    const int n = (b.Lm > b.Mm ? b.Lm : b.Mm) + 4;
-    hipLaunchKernelGGL(k_tide_bry, dim3((unsigned)((n + 255) / 256), 4), dim3(256), 0, S.s, b, B, dcs,
-                       dcs + T.ntides, T.ntides);
-  }
+  launch_tides(*S.d, S.s, dcs, S.cfg->pot_tides != 0, true);
   // the cos/sin buffer is reused by the next call: keep the host in step
   if (hipStreamSynchronize(S.s) != hipSuccess) { *S.err = "roms_gpu_set_tides: kernel failed"; return -3; }
   return 0;

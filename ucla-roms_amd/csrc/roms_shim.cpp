@@ -40,6 +40,9 @@ struct Ctx {
   double w1[kMaxFast], w2[kMaxFast];
   double area = 0.0, volume = 0.0;
   bool have_volume = false;   // area/volume formed (init_case, or on first diag)
+  long riv_maxidx = 0;        // largest river index nint(riv_flx/10) of the faces on the device
+  bool have_swr = false;      // swr_frac formed (at rest, main.F:216-220)
+  long graph_frc_gen = 0;     // frc_step_gen() the step graphs were captured with
   std::string err;
   // graph cache: key = (nstp, knew at step start)
   std::map<long, hipGraphExec_t> graphs;
@@ -261,6 +264,8 @@ void free_all() {
   g.scratch.clear();
   if (g.d.f.pipe_idx) { (void)hipFree(g.d.f.pipe_idx); g.d.f.pipe_idx = nullptr; }
   if (g.d.f.riv_face) { (void)hipFree(g.d.f.riv_face); g.d.f.riv_face = nullptr; }
+  g.riv_maxidx = 0;
+  g.have_swr = false;
   for (double*& p : g.d.f.ub)
     if (p) { (void)hipFree(p); p = nullptr; }
   if (g.h_diag) { (void)hipHostFree(g.h_diag); g.h_diag = nullptr; }
@@ -319,7 +324,10 @@ void enqueue_step(roms_tlev* t) {
   const Dev& d = g.d;
   hipStream_t s = g.s;
   Tlev T = to_tlev(t);
+  const bool pot = g.cfg.pot_tides != 0;
+  frc_step_phase(d, s, 0, pot);     // set_forces, frc_time 'current' (main.F:384-385)
   launch_bulk_flux(d, s, T.nrhs);   // set_forces (main.F:386): BULK_FRC only
+  frc_step_phase(d, s, 1, pot);     // set_bry_all '1/2 fwd' + set_tides (main.F:389-394)
   TIMED(ROMS_R_RHO_EOS, launch_rho_eos(d, s, T, T.nrhs));
   TIMED(ROMS_R_SET_HUV, launch_set_huv(d, s, T));
   TIMED(ROMS_R_OMEGA, launch_omega(d, s, T));
@@ -332,8 +340,10 @@ void enqueue_step(roms_tlev* t) {
   T = to_tlev(t);
   TIMED(ROMS_R_OMEGA, launch_omega(d, s, T));
   TIMED(ROMS_R_RHO_EOS, launch_rho_eos(d, s, T, T.nrhs));
+  frc_step_phase(d, s, 2, pot);     // set_forces, '1/2 fwd' (main.F:433)
   launch_bulk_flux(d, s, T.nrhs);   // set_forces (main.F:433): BULK_FRC only
   if (g.cfg.lmd_mixing) TIMED(ROMS_R_LMD_VMIX, launch_lmd_vmix(d, s, T, T.nrhs));
+  frc_step_phase(d, s, 3, pot);     // set_bry_all 'forward' + set_tides (main.F:438-441)
   TIMED(ROMS_R_PRSGRD, launch_prsgrd(d, s, T));
   TIMED(ROMS_R_STEP3D_UV1, launch_step3d_uv1(d, s, T));
   if (g.cfg.uv_vis2) TIMED(ROMS_R_VISC3D, launch_visc3d(d, s, T));
@@ -645,6 +655,7 @@ int roms_gpu_swr_frac(const roms_tlev* t) {
   (void)t;
   REQUIRE_INIT();
   launch_swr_frac(g.d, g.s);
+  g.have_swr = true;
   return post_launch();
 }
 int roms_gpu_set_pipe_frc(int npip, const int* pipe_idx, const double* pipe_flx, const double* pipe_prf,
@@ -712,8 +723,16 @@ int roms_gpu_set_river_frc(int nriv, const double* riv_uflx, const double* riv_v
     return 0;
   }
   if (!riv_uflx && !F.riv_uflx) { g.err = "roms_gpu_set_river_frc: river faces never set"; return -1; }
+  // faces kept from an earlier call index riv_vol/riv_trc up to riv_maxidx:
+  // a smaller nriv without new faces would read past the new arrays
+  if (!riv_uflx && nriv < g.riv_maxidx) {
+    g.err = "roms_gpu_set_river_frc: nriv smaller than the largest river index of the faces on the device "
+            "(pass riv_uflx/riv_vflx again)";
+    return -1;
+  }
   // faces of calc_river_flux: |riv_flx| > 1e-3 (step2d_FB.F:534), river index nint(riv_flx/10)
   std::vector<int> faces;
+  long maxidx = 0;
   if (riv_uflx) {
     for (int dir = 0; dir < 2; dir++) {
       const double* a = dir == 0 ? riv_uflx : riv_vflx;
@@ -724,6 +743,7 @@ int roms_gpu_set_river_frc(int nriv, const double* riv_uflx, const double* riv_v
           const long ir = std::lround(v / 10);
           if (ir < 1 || ir > nriv) { g.err = "roms_gpu_set_river_frc: river index nint(riv_flx/10) out of 1..nriv"; return -1; }
           faces.push_back(dir); faces.push_back(i); faces.push_back(j);
+          if (ir > maxidx) maxidx = ir;
         }
     }
   }
@@ -754,6 +774,7 @@ int roms_gpu_set_river_frc(int nriv, const double* riv_uflx, const double* riv_v
     CHECK_HIP(copy_on(F.riv_uflx, riv_uflx, (size_t)b.n2 * sizeof(double), hipMemcpyHostToDevice, g.s));
     CHECK_HIP(copy_on(F.riv_vflx, riv_vflx, (size_t)b.n2 * sizeof(double), hipMemcpyHostToDevice, g.s));
     g.d.p.nrivf = (int)(faces.size() / 3);
+    g.riv_maxidx = maxidx;
   }
   CHECK_HIP(copy_on(F.riv_vol, riv_vol, (size_t)nriv * sizeof(double), hipMemcpyHostToDevice, g.s));
   CHECK_HIP(copy_on(F.riv_trc, riv_trc, (size_t)nriv * b.NT * sizeof(double), hipMemcpyHostToDevice, g.s));
@@ -797,6 +818,18 @@ int roms_gpu_step(roms_tlev* t) {
   t->nrhs = t->nstp;
   t->nnew = 3;
   t->nfast = g.cfg.nfast;
+  {
+    // in-step forcing weights of this step (roms_gpu_frc_clock), queued ahead of its kernels
+    const int r = frc_step_prepare(g.s, g.d, g.cfg.dt, *t, g.err);
+    if (r) return r;
+    const long gen = frc_step_gen();
+    if (gen != g.graph_frc_gen) {   // graphs captured with other forcing buffers / field lists
+      CHECK_HIP(hipStreamSynchronize(g.s));
+      for (auto& kv : g.graphs) (void)hipGraphExecDestroy(kv.second);
+      g.graphs.clear();
+      g.graph_frc_gen = gen;
+    }
+  }
   const bool first = (t->iic == t->forw_start);
   if (!g.use_graphs || first) {
     enqueue_step(t);
@@ -836,7 +869,16 @@ int roms_gpu_init_sequence(roms_tlev* t) {
   launch_set_depth(g.d, g.s, T);
   // main.F:217-220 (zeta at rest): at initialisation only, not after a
   // restart read (get_init leaves iic = ntstart - 1 > 0)
-  if (g.cfg.lmd_mixing && t->iic == 0) launch_swr_frac(g.d, g.s);
+  if (g.cfg.lmd_mixing && t->iic == 0) {
+    launch_swr_frac(g.d, g.s);
+    g.have_swr = true;
+  }
+  if (g.cfg.lmd_mixing && !g.have_swr) {
+    // after get_init the depths are no longer the rest state swr_frac is formed on
+    g.err = "roms_gpu_init_sequence: swr_frac was never formed; call roms_gpu_swr_frac after set_depth at rest "
+            "and before roms_gpu_get_init (main.F:216-220)";
+    return -4;
+  }
   launch_set_huv(g.d, g.s, T);
   launch_omega(g.d, g.s, T);
   launch_rho_eos(g.d, g.s, T, T.nrhs);

@@ -39,6 +39,10 @@ struct Slab {
   int ni, nj, nk;
   long sj, sk;         // row and level strides
   int as_mask;         // riv_umask/riv_vmask: 1 where the river face array is non-zero
+  // history omega (basic_output.F:374-384): pm*pn*(We+Wi) in m/s when src2
+  // (Wi) is set; pm/pn are 2-D, element (i0, j0)
+  const double* src2;
+  const double *pm, *pn;
 };
 
 __global__ void __launch_bounds__(256) k_io_pack(Slab s, double* __restrict__ dst) {
@@ -47,7 +51,9 @@ __global__ void __launch_bounds__(256) k_io_pack(Slab s, double* __restrict__ ds
     const int i = (int)(q % s.ni);
     const long r = q / s.ni;
     const int j = (int)(r % s.nj), k = (int)(r / s.nj);
-    const double v = s.src ? s.src[i + j * s.sj + k * s.sk] : 0.0;
+    const long o = i + j * s.sj;
+    double v = s.src ? s.src[o + k * s.sk] : 0.0;
+    if (s.src2) v = s.pm[o] * s.pn[o] * (v + s.src2[o + k * s.sk]);
     dst[q] = s.as_mask ? (v != 0.0 ? 1.0 : 0.0) : v;
   }
 }
@@ -230,7 +236,14 @@ std::vector<OutVar> record_vars(const ShimState& S, const roms_tlev& t, bool rst
   if (!rst && (mask & ROMS_WRT_R)) {   // rho1 (SPLIT_EOS) or rho
     add("rho", "density anomaly", "kilogram meter-3", 'r', N, S.cfg->nonlin_eos ? F.rho1 : F.rho, n2);
   }
-  if (!rst && (mask & ROMS_WRT_O)) add("omega", "S-coordinate vertical momentum component", "meter second-1", 'r', N + 1, F.We, n2);
+  if (!rst && (mask & ROMS_WRT_O)) {   // pm*pn*(We+Wi), m/s (basic_output.F:374-384)
+    add("omega", "S-coordinate vertical momentum component", "meter second-1", 'r', N + 1, F.We, n2);
+    Slab& o = v.back().slab;
+    const long off = o.src - F.We;   // element (i0, j0)
+    o.src2 = F.Wi + off;
+    o.pm = F.pm + off;
+    o.pn = F.pn + off;
+  }
   if (!rst && (mask & ROMS_WRT_AKV)) add("AKv", "vertical viscosity coefficient", "meter2 second-1", 'r', N + 1, F.Akv, n2);
   if (!rst && (mask & ROMS_WRT_AKT))
     add("AKt", "temperature vertical diffusion coefficient", "meter2 second-1", 'r', N + 1, F.Akt, n2);
@@ -476,7 +489,12 @@ int roms_gpu_get_init(const char* path, int req_rec, int tindx, roms_tlev* t, do
             buf[q] = buf[q] * (m[ij] + rm);
           }
     };
-    double* dbuf = nullptr;
+    // upload staging, released on every exit (an error return included)
+    struct DevBuf {
+      double* p = nullptr;
+      ~DevBuf() { if (p) (void)hipFree(p); }
+    } stage;
+    double*& dbuf = stage.p;
     auto upload = [&](const std::vector<double>& buf, double* base, char g, int nk, long sk) {
       Slab s = slab_of(b, p, base, g, nk, sk);
       if (dbuf) { (void)hipFree(dbuf); dbuf = nullptr; }
@@ -556,7 +574,6 @@ int roms_gpu_get_init(const char* path, int req_rec, int tindx, roms_tlev* t, do
           exch(hd[q], 1);
         }
     }
-    if (dbuf) (void)hipFree(dbuf);
   } catch (const std::exception& e) {
     *S.err = std::string("roms_gpu_get_init: ") + path + ": " + e.what();
     return -7;

@@ -30,6 +30,18 @@ inline hipError_t copy_on(void* dst, const void* src, size_t bytes, hipMemcpyKin
   return e != hipSuccess ? e : hipStreamSynchronize(s);
 }   // rst_io.hip: joins the writer, frees staging (roms_gpu_finalize)
 void frc_free();  // k_forcing.hip: forcing records and tide data (roms_gpu_finalize)
+// In-step forcing (roms_gpu_frc_clock, k_forcing.hip): the set_forces /
+// set_bry_all / set_tides points of roms_step run inside roms_gpu_step.
+// frc_step_prepare forms the step's interpolation weights on the host and
+// queues them to the device before the step's kernels (0 or negative error);
+// frc_step_phase enqueues the interpolations of one point (0: surface at
+// 'current', 1: boundary at '1/2 fwd' + set_tides, 2: surface at '1/2 fwd',
+// 3: boundary at 'forward' + set_tides), reading the weights from device
+// memory so a captured step graph replays them; frc_step_gen changes
+// whenever a captured graph would hold stale buffers or field lists.
+int frc_step_prepare(hipStream_t s, const Dev& d, double dt, const roms_tlev& t, std::string& err);
+void frc_step_phase(const Dev& d, hipStream_t s, int phase, bool pot_tides);
+long frc_step_gen();
 double* shim_field(int field_id);          // device array of a field (nullptr if absent)
 double* shim_scratch_small(long n);        // small device scratch owned by the context (>= n doubles)
 }  // namespace roms

@@ -115,6 +115,7 @@ def load_library(path=LIB_PATH):
     L.roms_gpu_set_ub_tune.argtypes = [P(ctypes.c_double)] * 4
     L.roms_gpu_frc_record.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, P(ctypes.c_double)]
     L.roms_gpu_frc_interp.argtypes = [ctypes.c_double, ctypes.c_int]
+    L.roms_gpu_frc_clock.argtypes = [ctypes.c_double, ctypes.c_int]
     L.roms_gpu_set_tide_data.argtypes = [ctypes.c_int] + [P(ctypes.c_double)] * 9
     L.roms_gpu_set_tides.argtypes = [ctypes.c_double]
     L.roms_gpu_diag.argtypes = [P(Tlev), P(ctypes.c_double)]
@@ -448,6 +449,11 @@ class Model:
 
     def frc_interp(self, modtime, kinds=3):
         self._chk(self.L.roms_gpu_frc_interp(modtime, kinds), "frc_interp")
+
+    def frc_clock(self, start_time, on=True):
+        """In-step forcing: every step interpolates the recorded fields at
+        roms_step's set_forces / set_bry_all points (and runs set_tides)."""
+        self._chk(self.L.roms_gpu_frc_clock(start_time, int(on)), "frc_clock")
 
     def set_tide_data(self, ftide, pot=None, bry=None):
         """ftide (ntides,) [1/s]; pot = (re, im), bry = ((zre, zim), (ure, uim), (vre, vim)),
