@@ -46,8 +46,11 @@ def make_model(cfg, colseg):
             os.environ["ROMS_GPU_COLSEG"] = old
 
 
-ROUTINES = [("pre_step3d", "pred", ["t", "u", "v", "ru", "rv"]),
-            ("step3d_uv1", "corr", ["u", "v", "ru", "rv", "rufrc", "rvfrc"]),
+# ru/rv after pre_step3d and step3d_uv1 are dead in the reference (the next
+# read is preceded by prsgrd's assignment, prsgrd.F:293), so the segment
+# solvers do not store them; their effect is checked through u, v, rufrc, rvfrc
+ROUTINES = [("pre_step3d", "pred", ["t", "u", "v"]),
+            ("step3d_uv1", "corr", ["u", "v", "rufrc", "rvfrc"]),
             ("step3d_t", "corr", ["t"])]
 
 

@@ -92,24 +92,39 @@ struct SegXchg {
   double uv[kSegMaxS > 8 ? 2 : 1][kSegMaxS][kSegCW];   // U_t, V_t of the reduced system (kSegMaxS > 8)
 };
 
+// Every per-row loop below is straight-line code over all KR rows: rows
+// q >= n (the segment is shorter than KR) are computed on clamped inputs and
+// discarded by selects, never skipped by a lane-dependent branch.  Branches
+// split the unrolled loops into basic blocks, and the compiler then waited
+// for every row's loads before the next row's (one s_waitcnt vmcnt(0) per
+// load); straight-line rows let it issue the loads of many rows back to back.
+// The live rows keep their expressions and order: results are unchanged.
+#ifndef ROMS_SEG_LOAD_GROUP
+#define ROMS_SEG_LOAD_GROUP 5
+#endif
+constexpr int kSegLoadGroup = ROMS_SEG_LOAD_GROUP;
+
 template <int KR>
 struct SegTri {
   double C[KR], D[KR], E[KR];
   // forward elimination of rows q = 0..n-1; row(q, a, b, c, d): a x_{q-1} + b x_q + c x_{q+1} = d
+  // (row() is called for every q < KR and must be free of side effects)
   template <class RowF>
   __device__ __forceinline__ void eliminate(int n, RowF row) {
     double Cp = 0.0, Dp = 0.0, Ep = 1.0;  // x_{-1} = x_L
 #pragma unroll
     for (int q = 0; q < KR; q++) {
-      if (q < n) {
-        double a, b, c, d;
-        row(q, a, b, c, d);
-        const double rm = 1.0 / (b - a * Cp);
-        C[q] = c * rm;
-        D[q] = (d - a * Dp) * rm;
-        E[q] = -a * Ep * rm;
-        Cp = C[q]; Dp = D[q]; Ep = E[q];
-      }
+      double a, b, c, d;
+      row(q, a, b, c, d);
+      const double rm = 1.0 / (b - a * Cp);
+      const double Cq = c * rm, Dq = (d - a * Dp) * rm, Eq = -a * Ep * rm;
+      const bool live = q < n;
+      C[q] = live ? Cq : 0.0;
+      D[q] = live ? Dq : 0.0;
+      E[q] = live ? Eq : 0.0;
+      Cp = C[q]; Dp = D[q]; Ep = E[q];
+      // rows' loads run at most a group ahead of the elimination (register pressure)
+      if (q % kSegLoadGroup == kSegLoadGroup - 1) __builtin_amdgcn_sched_barrier(0);
     }
   }
   // publish the first/last-row relations, barrier, reduced solve -> x_L, x_R
@@ -118,10 +133,14 @@ struct SegTri {
     double y = 0.0, al = 0.0, be = 0.0, yl = 0.0, all = 0.0, bel = 0.0;
 #pragma unroll
     for (int q = KR - 1; q >= 0; q--) {
-      if (q < n) {
-        if (q == n - 1) { y = D[q]; al = E[q]; be = -C[q]; yl = y; all = al; bel = be; }
-        else { y = D[q] - C[q] * y; al = E[q] - C[q] * al; be = -C[q] * be; }
-      }
+      const bool last = q == n - 1, live = q < n;
+      const double yn = D[q] - C[q] * y, aln = E[q] - C[q] * al, ben = -C[q] * be;
+      y = last ? D[q] : (live ? yn : y);
+      al = last ? E[q] : (live ? aln : al);
+      be = last ? -C[q] : (live ? ben : be);
+      yl = last ? D[q] : yl;
+      all = last ? E[q] : all;
+      bel = last ? -C[q] : bel;
     }
     X.v[0][s][l] = y; X.v[1][s][l] = al; X.v[2][s][l] = be;
     X.v[3][s][l] = yl; X.v[4][s][l] = all; X.v[5][s][l] = bel;
@@ -150,7 +169,8 @@ struct SegTri {
         const double Pn = yL + aL * Pp + aL * Qp * Ut;
         Qp = aL * Qp * Vt + bL;
         Pp = Pn;
-        if (t == s - 1) { Ps = Pp; Qs = Qp; }
+        Ps = t == s - 1 ? Pp : Ps;
+        Qs = t == s - 1 ? Qp : Qs;
       }
     }
     if constexpr (kUVLds) __syncthreads();
@@ -159,8 +179,8 @@ struct SegTri {
 #pragma unroll
     for (int t = kSegMaxS - 1; t >= 0; t--) {
       if (t < S && (!kUVLds || t >= s - 1)) {
-        if (t == s) xR = Fn;
-        if (t == s - 1) xL = Ps + Qs * Fn;
+        xR = t == s ? Fn : xR;
+        xL = t == s - 1 ? Ps + Qs * Fn : xL;
         if constexpr (kUVLds) Fn = X.uv[0][t][l] + X.uv[1][t][l] * Fn;
         else Fn = U[t] + V[t] * Fn;
       }
@@ -171,10 +191,10 @@ struct SegTri {
     double xn = xR;
 #pragma unroll
     for (int q = KR - 1; q >= 0; q--) {
-      if (q < n) {
-        xn = D[q] + E[q] * xL - C[q] * xn;
-        D[q] = xn;
-      }
+      const double v = D[q] + E[q] * xL - C[q] * xn;
+      const bool live = q < n;
+      xn = live ? v : xn;
+      D[q] = live ? v : D[q];
     }
   }
 };
@@ -194,19 +214,19 @@ __device__ __forceinline__ void spline_fc_seg(const SegSpan& sg, int N, SegXchg&
   SegTri<KR> T;
   T.eliminate(ns, [&](int q, double& a, double& bb, double& c, double& dd) {
     const int r = c0 - 1 + q;
-    if (r == 0) { a = 0.0; bb = 1.0; c = 1.0; dd = 2.0 * f[1]; }
-    else if (r == N) { a = 1.0; bb = 1.0; c = 0.0; dd = 2.0 * f[q]; }
-    else {
-      a = w[q + 1]; bb = 2.0 * (w[q] + w[q + 1]); c = w[q];
-      dd = 3.0 * (w[q] * f[q + 1] + w[q + 1] * f[q]);
-    }
+    const int q1 = q + 1 < KR ? q + 1 : KR - 1;   // f[q+1] of a row that can be live
+    const double ai = w[q + 1], bi = 2.0 * (w[q] + w[q + 1]), ci = w[q];
+    const double di = 3.0 * (w[q] * f[q1] + w[q + 1] * f[q]);
+    a = r == 0 ? 0.0 : (r == N ? 1.0 : ai);
+    bb = (r == 0 || r == N) ? 1.0 : bi;
+    c = r == 0 ? 1.0 : (r == N ? 0.0 : ci);
+    dd = r == 0 ? 2.0 * f[1] : (r == N ? 2.0 * f[q] : di);
   });
   double xL, xR;
   T.couple(sg, ns, X, xL, xR);
   T.solve(ns, xL, xR);
 #pragma unroll
-  for (int q = 0; q < KR; q++)
-    if (q <= n) fc[q] = q < ns ? T.D[q] : xR;
+  for (int q = 0; q < KR; q++) fc[q] = q < ns ? T.D[q] : xR;
 }
 
 // SPLINE_UV advective flux of a u (dir 0) / v (dir 1) column at interfaces
@@ -230,22 +250,22 @@ __device__ __forceinline__ void uv_spline_seg(const Dev& d, const SegSpan& sg, S
   const double* mask = dir == 0 ? F.umask : F.vmask;
   double dc[KR + 1], uu[KR];
 #pragma unroll
-  for (int q = 0; q < KR + 1; q++) {
+  for (int q = 0; q < KR + 1; q++) {   // all rows (clamped levels): straight-line loads
     const long L = (long)(min(max(c0 - 1 + q, 1), N) - 1) * n2;
-    if (q <= n + 1) dc[q] = 0.5625 * (Hz[L] + Hz[L - s]) - 0.0625 * (Hz[L + s] + Hz[L - 2 * s]);
-    if (q <= n && q < KR) uu[q] = Uv[L];
+    dc[q] = 0.5625 * (Hz[L] + Hz[L - s]) - 0.0625 * (Hz[L + s] + Hz[L - 2 * s]);
+    if (q < KR) uu[q] = Uv[L];
+    // groups of kSegLoadGroup rows: their loads issue together, the next
+    // group's wait (without the barrier all 5 (KR+1) loads were hoisted and spilled)
+    if (q % kSegLoadGroup == kSegLoadGroup - 1) __builtin_amdgcn_sched_barrier(0);
   }
   spline_fc_seg<KR>(sg, N, X, dc, uu, fl);
   const double m1 = mask[ij + s], m0 = mask[ij - s];
 #pragma unroll
   for (int q = 0; q < KR; q++) {
-    if (q <= n) {
-      const int r = c0 - 1 + q;
-      if (r == 0 || r == N) { fl[q] = 0.0; continue; }
-      const long w = (long)r * n2;
-      const double wf = We[w] + We[w - s] - 0.125 * ((We[w + s] - We[w]) * m1 - (We[w - s] - We[w - 2 * s]) * m0);
-      fl[q] = fl[q] * 0.5 * wf;
-    }
+    const int r = c0 - 1 + q;
+    const long w = (long)min(max(r, 1), N - 1) * n2;
+    const double wf = We[w] + We[w - s] - 0.125 * ((We[w + s] - We[w]) * m1 - (We[w - s] - We[w - 2 * s]) * m0);
+    fl[q] = (r == 0 || r == N) ? 0.0 : fl[q] * 0.5 * wf;
   }
 }
 
@@ -259,10 +279,9 @@ __device__ __forceinline__ void tracer_spline_seg(const SegSpan& sg, int N, long
   spline_fc_seg<KR>(sg, N, X, hz, tt, fl);
 #pragma unroll
   for (int q = 0; q < KR; q++) {
-    if (q <= sg.n) {
-      const int r = sg.c0 - 1 + q;
-      fl[q] = (r == 0 || r == N) ? 0.0 : fl[q] * We[(long)r * n2];
-    }
+    const int r = sg.c0 - 1 + q;
+    const double we = We[(long)min(max(r, 1), N - 1) * n2];
+    fl[q] = (r == 0 || r == N) ? 0.0 : fl[q] * we;
   }
 }
 

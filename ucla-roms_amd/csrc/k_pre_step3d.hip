@@ -383,7 +383,7 @@ __global__ void __launch_bounds__(64) k_pre_uv(Dev d, Range R, PreCoef c, int ns
 // 16 columns x S segments.  The spline reconstruction and the implicit
 // diffusion / viscosity are each one partitioned tridiagonal system whose
 // rows are those of k_pre_tracer_v / pre_uv_col (pre_step3d4S.F:198-489). ----
-__global__ void __launch_bounds__(kSegBlock) k_pre_tracer_seg(Dev d, Range R, PreCoef c, int nnew, int nrhs) {
+__global__ void __launch_bounds__(kSegBlock, 2) k_pre_tracer_seg(Dev d, Range R, PreCoef c, int nnew, int nrhs) {
   const uint3 bI = seg_tile(d.p.seg_order, d.p.seg_xg);
   __shared__ SegXchg X;
   constexpr int KR = kSegRows + 1;
@@ -397,7 +397,7 @@ __global__ void __launch_bounds__(kSegBlock) k_pre_tracer_seg(Dev d, Range R, Pr
   const int itrc = 1 + (int)bI.z;
   const long n2 = b.n2, ij = IJ(b, i, j);
   const int c0 = sg.c0, n = sg.n;
-  auto cell = [&](int k) { return (long)(k - 1) * n2; };
+  auto cell = [&](int k) { return (long)(min(max(k, 1), N) - 1) * n2; };   // rho level k (clamped)
   const double* __restrict__ Hz = F.Hz + ij;
   const double* __restrict__ Hf = F.c2 + ij;   // Hz_fwd (k_pre_tracer_h)
   const long tb = (long)(itrc - 1) * 3 * b.n3;
@@ -405,25 +405,28 @@ __global__ void __launch_bounds__(kSegBlock) k_pre_tracer_seg(Dev d, Range R, Pr
   double* __restrict__ Tn = F.t + (long)(nnew - 1) * b.n3 + tb + ij;
   double hz[KR + 1], tt[KR], fl[KR];
 #pragma unroll
-  for (int q = 0; q < KR + 1; q++) {
-    const long L = cell(min(max(c0 - 1 + q, 1), N));
-    if (q <= n + 1) hz[q] = Hz[L];
-    if (q <= n && q < KR) tt[q] = Tr[L];
+  for (int q = 0; q < KR + 1; q++) {   // all rows, clamped levels: straight-line loads
+    hz[q] = Hz[cell(c0 - 1 + q)];
+    if (q < KR) tt[q] = Tr[cell(c0 - 1 + q)];
   }
   tracer_spline_seg<KR>(sg, N, n2, X, hz, tt, F.We + ij, fl);
-  // implicit diffusion on Hz_fwd, cells k = c0+p
+  // implicit diffusion on Hz_fwd, cells k = c0+p (its loads kept out of the spline phase)
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-  for (int q = 0; q < KR + 1; q++)
-    if (q <= n + 1) hz[q] = Hf[cell(min(max(c0 - 1 + q, 1), N))];
+  for (int q = 0; q < KR + 1; q++) hz[q] = Hf[cell(c0 - 1 + q)];
   const int iAkt = itrc < b.nTS ? itrc : b.nTS;
   const double* __restrict__ Akt = F.Akt + (long)(iAkt - 1) * b.n3w + ij;
   const double* __restrict__ Wi = F.Wi + ij;
   const double DC0 = c.dtau * F.pm[ij] * F.pn[ij];
-  auto fcw = [&](int q, double& fc, double& wc) {   // interface c0-1+q
+  auto fcw = [&](int q, double& fc, double& wc) {   // interface c0-1+q (0 at the bottom and the surface)
     const int r = c0 - 1 + q;
-    if (r <= 0 || r >= N) { fc = 0.0; wc = 0.0; return; }
-    fc = 2.0 * c.dtau * Akt[(long)r * n2] / (hz[q + 1] + hz[q]);
-    wc = DC0 * Wi[(long)r * n2];
+    const long w = (long)min(max(r, 1), N - 1) * n2;
+    const bool in = r > 0 && r < N;
+    const int qa = q + 1 < KR + 1 ? q + 1 : KR;
+    const double f = 2.0 * c.dtau * Akt[w] / (hz[qa] + hz[q]);
+    const double wv = DC0 * Wi[w];
+    fc = in ? f : 0.0;
+    wc = in ? wv : 0.0;
   };
   double fcl, wcl;
   fcw(0, fcl, wcl);
@@ -435,7 +438,7 @@ __global__ void __launch_bounds__(kSegBlock) k_pre_tracer_seg(Dev d, Range R, Pr
     a = -(fcl + fmax0(wcl));
     bb = hz[p + 1] + fcu + fmax0(wcu) + fcl - fmin0(wcl);
     cc = -(fcu - fmin0(wcu));
-    dd = Tn[cell(c0 + p)] - c.dtau * F.pm[ij] * F.pn[ij] * (fl[p + 1] - fl[p]);
+    dd = Tn[cell(c0 + p)] - c.dtau * F.pm[ij] * F.pn[ij] * (fl[p + 1 < KR ? p + 1 : KR - 1] - fl[p]);
     fcl = fcu; wcl = wcu;
   });
   double xL, xR;
@@ -448,7 +451,7 @@ __global__ void __launch_bounds__(kSegBlock) k_pre_tracer_seg(Dev d, Range R, Pr
   }
 }
 
-__global__ void __launch_bounds__(kSegBlock) k_pre_uv_seg(Dev d, Range R, PreCoef c, int nstp, int nnew, int nrhs) {
+__global__ void __launch_bounds__(kSegBlock, 2) k_pre_uv_seg(Dev d, Range R, PreCoef c, int nstp, int nnew, int nrhs) {
   const uint3 bI = seg_tile(d.p.seg_order, d.p.seg_xg);
   __shared__ SegXchg X;
   constexpr int KR = kSegRows + 1;
@@ -462,11 +465,12 @@ __global__ void __launch_bounds__(kSegBlock) k_pre_uv_seg(Dev d, Range R, PreCoe
   const bool act = col.act;
   const long n2 = b.n2, ij = IJ(b, col.i, col.j), s = dir == 0 ? 1 : b.nx2;
   const int c0 = sg.c0, n = sg.n;
-  auto cell = [&](int k) { return (long)(k - 1) * n2; };
+  auto cell = [&](int k) { return (long)(min(max(k, 1), N) - 1) * n2; };   // rho level k (clamped)
   double fl[KR];
   uv_spline_seg<KR>(d, sg, X, ij, nrhs, dir, fl);
+  __builtin_amdgcn_sched_barrier(0);   // the viscosity phase's loads stay out of the spline phase
   double* Uall = dir == 0 ? F.u : F.v;
-  double* __restrict__ rr = (dir == 0 ? F.ru : F.rv) + ij;
+  const double* __restrict__ rr = (dir == 0 ? F.ru : F.rv) + ij;
   const double* __restrict__ Ustp = Uall + (long)(nstp - 1) * b.n3 + ij;
   double* __restrict__ Uidx = Uall + (long)(indx - 1) * b.n3 + ij;
   double* __restrict__ Unew = Uall + (long)(nnew - 1) * b.n3 + ij;
@@ -477,21 +481,34 @@ __global__ void __launch_bounds__(kSegBlock) k_pre_uv_seg(Dev d, Range R, PreCoe
   const double* __restrict__ Hb = F.c3 + ij;
   const double sstr = dir == 0 ? F.sustr[ij] : F.svstr[ij];
   const double DC0 = c.dtau * 0.25 * (F.pm[ij] + F.pm[ij - s]) * (F.pn[ij] + F.pn[ij - s]);
+  // row p's right-hand side: ru(k) with the vertical advection (uv_rr_update;
+  // the updated ru itself is dead -- the corrector's prsgrd overwrites it,
+  // prsgrd.F:293 -- so it is not stored); u(indx) = Hz*u(nstp) is stored
+  // after the solve, so the rows carry no stores (no may-alias ordering)
+  auto rhs = [&](int p) {
+    const int k = c0 + p;
+    const long o = cell(k);
+    const double r = k == 1 ? rr[o] - fl[1] : rr[o] - fl[p + 1 < KR ? p + 1 : KR - 1] + fl[p];
+    const double us = Ustp[o];
+    const double v = 0.5 * (Hb[o] + Hb[o - s]) * (c.cf_stp * us + c.cf_bak * Uidx[o]) + DC0 * r;
+    return k == N ? v + c.dtau * sstr : v;
+  };
   double hf[KR + 1], hfm[KR + 1];   // Hz_fwd(c0-1+q) of the column and of its (i-1) / (j-1) neighbour
 #pragma unroll
   for (int q = 0; q < KR + 1; q++) {
-    if (q <= n + 1) {
-      const long L = cell(min(max(c0 - 1 + q, 1), N));
-      hf[q] = Hf[L];
-      hfm[q] = Hf[L - s];
-    }
+    const long L = cell(c0 - 1 + q);
+    hf[q] = Hf[L];
+    hfm[q] = Hf[L - s];
   }
-  auto fcw = [&](int q, double& fc, double& wc) {   // interface c0-1+q
+  auto fcw = [&](int q, double& fc, double& wc) {   // interface c0-1+q (0 at the bottom and the surface)
     const int r = c0 - 1 + q;
-    if (r <= 0 || r >= N) { fc = 0.0; wc = 0.0; return; }
-    const long w = (long)r * n2;
-    fc = 2.0 * c.dtau * (Akv[w] + Akv[w - s]) / (hf[q + 1] + hfm[q + 1] + hf[q] + hfm[q]);
-    wc = DC0 * 0.5 * (Wi[w] + Wi[w - s]);
+    const long w = (long)min(max(r, 1), N - 1) * n2;
+    const bool in = r > 0 && r < N;
+    const int qa = q + 1 < KR + 1 ? q + 1 : KR;
+    const double f = 2.0 * c.dtau * (Akv[w] + Akv[w - s]) / (hf[qa] + hfm[qa] + hf[q] + hfm[q]);
+    const double wv = DC0 * 0.5 * (Wi[w] + Wi[w - s]);
+    fc = in ? f : 0.0;
+    wc = in ? wv : 0.0;
   };
   const double rd = F.r_D[ij], rdm = F.r_D[ij - s];
   double fcl, wcl;
@@ -502,30 +519,32 @@ __global__ void __launch_bounds__(kSegBlock) k_pre_uv_seg(Dev d, Range R, PreCoe
     double fcu, wcu;
     fcw(p + 1, fcu, wcu);
     const int k = c0 + p;
-    const long o = cell(k);
     a = -(fcl + fmax0(wcl));
     cc = -(fcu - fmin0(wcu));
-    if (k == 1) bb = 0.5 * (hf[p + 1] + hfm[p + 1]) + 0.5 * c.dtau * (rd + rdm) + fcu + fmax0(wcu);
-    else bb = 0.5 * (hf[p + 1] + hfm[p + 1]) + fcl - fmin0(wcl) + fcu + fmax0(wcu);
-    // ru(k) with the vertical advection (uv_rr_update), u(indx) = Hz*u(nstp)
-    const double r = k == 1 ? rr[o] - fl[1] : rr[o] - fl[p + 1] + fl[p];
-    const double us = Ustp[o];
-    double v = 0.5 * (Hb[o] + Hb[o - s]) * (c.cf_stp * us + c.cf_bak * Uidx[o]) + DC0 * r;
-    if (act) {
-      rr[o] = r;
-      Uidx[o] = 0.5 * (Hz[o] + Hz[o - s]) * us;
-    }
-    if (k == N) v = v + c.dtau * sstr;
-    dd = v;
+    const double b1 = 0.5 * (hf[p + 1] + hfm[p + 1]) + 0.5 * c.dtau * (rd + rdm) + fcu + fmax0(wcu);
+    const double bk = 0.5 * (hf[p + 1] + hfm[p + 1]) + fcl - fmin0(wcl) + fcu + fmax0(wcu);
+    bb = k == 1 ? b1 : bk;
+    dd = rhs(p);
     fcl = fcu; wcl = wcu;
   });
   double xL, xR;
   T.couple(sg, n, X, xL, xR);
   T.solve(n, xL, xR);
   if (act) {
+    // u(indx) = Hz*u(nstp), formed here from reloads (L2-warm) rather than
+    // kept in registers across the solve
+    double uix[KR];
+#pragma unroll
+    for (int p = 0; p < KR; p++) {
+      const long o = cell(c0 + p);
+      uix[p] = 0.5 * (Hz[o] + Hz[o - s]) * Ustp[o];
+    }
 #pragma unroll
     for (int p = 0; p < KR; p++)
-      if (p < n) Unew[cell(c0 + p)] = T.D[p];
+      if (p < n) {
+        Unew[cell(c0 + p)] = T.D[p];
+        Uidx[cell(c0 + p)] = uix[p];
+      }
   }
 }
 

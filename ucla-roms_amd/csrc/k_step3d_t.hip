@@ -154,7 +154,7 @@ __global__ void __launch_bounds__(64) k_step3d_t_v(Dev d, Range R, int nnew, int
 // interface values FC(0:N) and the implicit diffusion are each solved as one
 // partitioned tridiagonal system; the surface, KPP and pipe terms of the
 // diffusion r.h.s. are those of k_step3d_t_v (step3d_t_ISO.F:913-1100). ----
-__global__ void __launch_bounds__(kSegBlock) k_step3d_t_seg(Dev d, Range R, int nnew, int nrhs) {
+__global__ void __launch_bounds__(kSegBlock, 2) k_step3d_t_seg(Dev d, Range R, int nnew, int nrhs) {
   const uint3 bI = seg_tile(d.p.seg_order, d.p.seg_xg);
   __shared__ SegXchg X;
   constexpr int KR = kSegRows + 1;
@@ -175,87 +175,111 @@ __global__ void __launch_bounds__(kSegBlock) k_step3d_t_seg(Dev d, Range R, int 
   const double* __restrict__ Tr = F.t + (long)(nrhs - 1) * b.n3 + (long)(itrc - 1) * 3 * b.n3 + ij;
   double* __restrict__ Tn = F.t + (long)(nnew - 1) * b.n3 + (long)(itrc - 1) * 3 * b.n3 + ij;
   const double* __restrict__ We = F.We + ij;
-  auto cell = [&](int k) { return (long)(k - 1) * n2; };   // rho level k
-  // hz[q] = Hz(c0-1+q), q = 0..n+1 (clamped to 1..N); tt[q] = t(nrhs)(c0-1+q), q = 0..n
+  auto cell = [&](int k) { return (long)(min(max(k, 1), N) - 1) * n2; };   // rho level k (clamped)
+  // hz[q] = Hz(c0-1+q), q = 0..KR; tt[q] = t(nrhs)(c0-1+q), q = 0..KR-1 (clamped to 1..N)
   double hz[KR + 1], tt[KR];
 #pragma unroll
   for (int q = 0; q < KR + 1; q++) {
-    if (q <= n + 1) hz[q] = Hz[cell(min(max(c0 - 1 + q, 1), N))];
-    if (q <= n && q < KR) tt[q] = Tr[cell(min(max(c0 - 1 + q, 1), N))];
+    hz[q] = Hz[cell(c0 - 1 + q)];
+    if (q < KR) tt[q] = Tr[cell(c0 - 1 + q)];
   }
-  // spline rows: interfaces r = c0-1+q, q = 0..n-1 (+ r = N in the last segment)
-  SegTri<KR> T;
-  const int ns = n + (last ? 1 : 0);
-  T.eliminate(ns, [&](int q, double& a, double& bb, double& c, double& dd) {
-    const int r = c0 - 1 + q;
-    if (r == 0) { a = 0.0; bb = 1.0; c = 1.0; dd = 2.0 * tt[1]; }
-    else if (r == N) { a = 1.0; bb = 1.0; c = 0.0; dd = 2.0 * tt[q]; }
-    else {
-      a = hz[q + 1]; bb = 2.0 * (hz[q] + hz[q + 1]); c = hz[q];
-      dd = 3.0 * (hz[q] * tt[q + 1] + hz[q + 1] * tt[q]);
-    }
-  });
-  double xL, xR;
-  T.couple(sg, ns, X, xL, xR);
-  T.solve(ns, xL, xR);
-  // vertical advective fluxes FC(r)*We(r) at interfaces r = c0-1+q, q = 0..n (into tt)
+  // spline interface values FC(c0-1+q) and the advective fluxes FC*We (into tt)
+  {
+    double fc[KR];
+    spline_fc_seg<KR>(sg, N, X, hz, tt, fc);
 #pragma unroll
-  for (int q = 0; q < KR; q++) {
-    if (q <= n) {
+    for (int q = 0; q < KR; q++) {
       const int r = c0 - 1 + q;
-      const double fc = q < ns ? T.D[q] : xR;
-      tt[q] = (r == 0 || r == N) ? 0.0 : fc * We[(long)r * n2];
+      const double we = We[(long)min(max(r, 1), N - 1) * n2];
+      tt[q] = (r == 0 || r == N) ? 0.0 : fc[q] * we;
     }
   }
-  // implicit diffusion rows, cells k = c0+p, p = 0..n-1
+  // implicit diffusion rows, cells k = c0+p, p = 0..n-1.  The scheduling
+  // barrier keeps this phase's loads out of the spline phase (hoisted there
+  // they pushed the kernel to 281 VGPRs, one wave per SIMD)
+  __builtin_amdgcn_sched_barrier(0);
   const int iAkt = itrc < b.nTS ? itrc : b.nTS;
   const double* __restrict__ Akt = F.Akt + (long)(iAkt - 1) * b.n3w + ij;
   const double* __restrict__ Wi = F.Wi + ij;
   const double DC0 = dt * F.pm[ij] * F.pn[ij];
   const bool kppT = P.lmd && itrc == 1, kppS = P.lmd_nonlocal && itrc == 2 && P.salinity;
-  auto gh = [&](long o) { return P.lmd_nonlocal ? F.ghat[ij + o] : 0.0; };
   const double sr = F.srflx[ij];
   const double stf = F.stflx[ij + (long)(itrc - 1) * n2];
-  const int pidx = P.npip > 0 ? F.pipe_idx[ij] : 0;
-  const double pflx = pidx > 0 ? F.pipe_flx[ij] : 0.0;
-  const double ptrc = pidx > 0 ? F.pipe_trc[(pidx - 1) + (itrc - 1) * P.npip] : 0.0;
-  auto tval = [&](int k, double t, double dfl) {
-    const long o = cell(k);
-    t = t - dt * F.pm[ij] * F.pn[ij] * dfl;
-    if (pidx > 0) t = t + dt * F.pm[ij] * F.pn[ij] * pflx * F.pipe_prf[(pidx - 1) + (k - 1) * P.npip] * ptrc;
-    if (k == N) {
-      if (itrc == 1) t = t + dt * F.swflx[ij] * (P.bulk_frc ? F.tair[ij] : t / Hz[o]);
-      t = t + dt * stf;
+  // right-hand sides (step3d_t_ISO.F:922-1040): flux divergence, pipes, rain
+  // heat, surface flux, KPP solar / non-local terms, in the reference's order
+  double rhs[KR];
+#pragma unroll
+  for (int p = 0; p < KR; p++) rhs[p] = Tn[cell(c0 + p)] - dt * F.pm[ij] * F.pn[ij] * (tt[p + 1 < KR ? p + 1 : KR - 1] - tt[p]);
+  if (P.npip > 0) {   // pipe_frc.F sources (step3d_t_ISO.F:927-934)
+    const int pidx = F.pipe_idx[ij];
+    if (pidx > 0) {
+      const double pflx = F.pipe_flx[ij], ptrc = F.pipe_trc[(pidx - 1) + (itrc - 1) * P.npip];
+#pragma unroll
+      for (int p = 0; p < KR; p++) {
+        const int k = min(c0 + p, N);
+        rhs[p] = rhs[p] + dt * F.pm[ij] * F.pn[ij] * pflx * F.pipe_prf[(pidx - 1) + (k - 1) * P.npip] * ptrc;
+      }
     }
-    if (kppT) {
-      if (k <= N - 1) t = t + dt * (sr * F.swr_frac[ij + (long)k * n2] - gh((long)k * n2) * (stf - sr));
-      if (k >= 2) t = t - dt * (sr * F.swr_frac[ij + o] - gh(o) * (stf - sr));
-    } else if (kppS) {
-      if (k <= N - 1) t = t + (-dt * F.ghat[ij + (long)k * n2] * stf);
-      if (k >= 2) t = t - (-dt * F.ghat[ij + o] * stf);
+  }
+  {
+    // the surface cell k = N (row n-1 of the last segment): heat of rain --
+    // the 2 m air temperature under BULK_FRC, else the water's own -- and the
+    // surface flux (step3d_t_ISO.F:939-959); picked out and put back by selects
+    const bool top = last;
+    double t = 0.0;
+#pragma unroll
+    for (int p = 0; p < KR; p++) t = p == n - 1 ? rhs[p] : t;
+    const double swf = F.swflx[ij], hzN = Hz[cell(N)];
+    if (itrc == 1) t = t + dt * swf * (P.bulk_frc ? F.tair[ij] : t / hzN);
+    t = t + dt * stf;
+#pragma unroll
+    for (int p = 0; p < KR; p++) rhs[p] = (top && p == n - 1) ? t : rhs[p];
+  }
+  if (kppT || kppS) {
+    auto gh = [&](long o) { return P.lmd_nonlocal ? F.ghat[ij + o] : 0.0; };
+#pragma unroll
+    for (int p = 0; p < KR; p++) {
+      const int k = min(c0 + p, N);
+      const long ou = (long)min(k, N - 1) * n2, ol = (long)max(k - 1, 1) * n2;   // w-levels k and k-1
+      double t = rhs[p];
+      if (kppT) {
+        const double up = dt * (sr * F.swr_frac[ij + ou] - gh(ou) * (stf - sr));
+        const double lo = dt * (sr * F.swr_frac[ij + ol] - gh(ol) * (stf - sr));
+        t = k <= N - 1 ? t + up : t;
+        t = k >= 2 ? t - lo : t;
+      } else {
+        const double up = -dt * F.ghat[ij + ou] * stf, lo = -dt * F.ghat[ij + ol] * stf;
+        t = k <= N - 1 ? t + up : t;
+        t = k >= 2 ? t - lo : t;
+      }
+      rhs[p] = t;
     }
-    return t;
-  };
+  }
   // FC, WC at interface r (0 at the bottom and the surface)
   auto fcw = [&](int q, double& fc, double& wc) {   // interface c0-1+q
     const int r = c0 - 1 + q;
-    if (r <= 0 || r >= N) { fc = 0.0; wc = 0.0; return; }
-    fc = 2.0 * dt * Akt[(long)r * n2] / (hz[q] + hz[q + 1]);
-    wc = DC0 * Wi[(long)r * n2];
+    const long w = (long)min(max(r, 1), N - 1) * n2;
+    const bool in = r > 0 && r < N;
+    const int qa = q + 1 < KR + 1 ? q + 1 : KR;
+    const double f = 2.0 * dt * Akt[w] / (hz[q] + hz[qa]);
+    const double c = DC0 * Wi[w];
+    fc = in ? f : 0.0;
+    wc = in ? c : 0.0;
   };
   double fcl, wcl;
   fcw(0, fcl, wcl);
   __syncthreads();  // X reused by the second coupling
+  SegTri<KR> T;
   T.eliminate(n, [&](int p, double& a, double& bb, double& c, double& dd) {
     double fcu, wcu;
     fcw(p + 1, fcu, wcu);
-    const int k = c0 + p;
     a = -(fcl + fmax0(wcl));
     bb = hz[p + 1] + fcu + fmax0(wcu) + fcl - fmin0(wcl);
     c = -(fcu - fmin0(wcu));
-    dd = tval(k, Tn[cell(k)], tt[p + 1] - tt[p]);
+    dd = rhs[p];
     fcl = fcu; wcl = wcu;
   });
+  double xL, xR;
   T.couple(sg, n, X, xL, xR);
   T.solve(n, xL, xR);
   if (act) {

@@ -246,7 +246,7 @@ __global__ void __launch_bounds__(64, 2) k_uv1_reg(Dev d, Range R, int nnew, int
 struct SegRu {
   double r[kSegRows * kSegMaxS][kSegCW];
 };
-__global__ void __launch_bounds__(kSegBlock) k_uv1_seg(Dev d, Range R, int nnew, int nrhs) {
+__global__ void __launch_bounds__(kSegBlock, 2) k_uv1_seg(Dev d, Range R, int nnew, int nrhs) {
   const uint3 bI = seg_tile(d.p.seg_order, d.p.seg_xg);
   __shared__ SegXchg X;
   __shared__ SegRu Sr;
@@ -262,55 +262,49 @@ __global__ void __launch_bounds__(kSegBlock) k_uv1_seg(Dev d, Range R, int nnew,
   const bool act = col.act;
   const long n2 = b.n2, ij = IJ(b, col.i, col.j), s = dir == 0 ? 1 : b.nx2;
   const int c0 = sg.c0, n = sg.n;
-  auto cell = [&](int k) { return (long)(k - 1) * n2; };
+  auto cell = [&](int k) { return (long)(min(max(k, 1), N) - 1) * n2; };   // rho level k (clamped)
   double fl[KR];
   uv_spline_seg<KR>(d, sg, X, ij, nrhs, dir, fl);
+  __builtin_amdgcn_sched_barrier(0);   // the viscosity phase's loads stay out of the spline phase
   double* __restrict__ Un = (dir == 0 ? F.u : F.v) + (long)(nnew - 1) * b.n3 + ij;
-  double* __restrict__ rr = (dir == 0 ? F.ru : F.rv) + ij;
+  const double* __restrict__ rr = (dir == 0 ? F.ru : F.rv) + ij;
   const double* __restrict__ Hz = F.Hz + ij;
   const double* __restrict__ Akv = F.Akv + ij;
   const double* __restrict__ Wi = F.Wi + ij;
   const double sstr = dir == 0 ? F.sustr[ij] : F.svstr[ij];
   const double DC0 = dt * 0.25 * (F.pm[ij] + F.pm[ij - s]) * (F.pn[ij] + F.pn[ij - s]);
+  // right-hand sides first: ru(k) with the vertical advection (uv_rr_update)
+  // to LDS for rufrc -- the updated ru itself is dead after this routine (the
+  // next step's prsgrd overwrites it, prsgrd.F:293), so it is not stored --
+  // and dd = u(nnew) + DC0*ru
+  double rhs[KR];
+#pragma unroll
+  for (int p = 0; p < KR; p++) {
+    const int k = c0 + p;
+    const long o = cell(k);
+    const double r = k == 1 ? rr[o] - fl[1] : rr[o] - fl[p + 1 < KR ? p + 1 : KR - 1] + fl[p];
+    if (p < n) Sr.r[k - 1][sg.col] = r;
+    const double v = Un[o] + DC0 * r;
+    rhs[p] = k == N ? v + dt * sstr : v;
+  }
   double hz[KR + 1], hzm[KR + 1];   // Hz(c0-1+q) of the column and of its (i-1) / (j-1) neighbour
 #pragma unroll
   for (int q = 0; q < KR + 1; q++) {
-    if (q <= n + 1) {
-      const long L = cell(min(max(c0 - 1 + q, 1), N));
-      hz[q] = Hz[L];
-      hzm[q] = Hz[L - s];
-    }
+    const long L = cell(c0 - 1 + q);
+    hz[q] = Hz[L];
+    hzm[q] = Hz[L - s];
   }
-  auto fcw = [&](int q, double& fc, double& wc) {   // interface c0-1+q
+  auto fcw = [&](int q, double& fc, double& wc) {   // interface c0-1+q (0 at the bottom and the surface)
     const int r = c0 - 1 + q;
-    if (r <= 0 || r >= N) { fc = 0.0; wc = 0.0; return; }
-    const long w = (long)r * n2;
-    fc = 2.0 * dt * (Akv[w] + Akv[w - s]) / (hz[q + 1] + hzm[q + 1] + hz[q] + hzm[q]);
-    wc = DC0 * 0.5 * (Wi[w] + Wi[w - s]);
+    const long w = (long)min(max(r, 1), N - 1) * n2;
+    const bool in = r > 0 && r < N;
+    const int qa = q + 1 < KR + 1 ? q + 1 : KR;
+    const double f = 2.0 * dt * (Akv[w] + Akv[w - s]) / (hz[qa] + hzm[qa] + hz[q] + hzm[q]);
+    const double wv = DC0 * 0.5 * (Wi[w] + Wi[w - s]);
+    fc = in ? f : 0.0;
+    wc = in ? wv : 0.0;
   };
   const double rD = F.r_D[ij], rDm = F.r_D[ij - s];
-  // right-hand sides first (all loads of the segment before its ru stores,
-  // which inside the elimination stalled every row: may-alias); ru(k) with
-  // the vertical advection (uv_rr_update) to HBM and LDS, dd = u(nnew) + DC0*ru
-  double rhs[KR];
-  {
-    double r_[KR], un_[KR];
-#pragma unroll
-    for (int p = 0; p < KR; p++)
-      if (p < n) { const long o = cell(c0 + p); r_[p] = rr[o]; un_[p] = Un[o]; }
-#pragma unroll
-    for (int p = 0; p < KR; p++) {
-      if (p < n) {
-        const int k = c0 + p;
-        const double r = k == 1 ? r_[p] - fl[1] : r_[p] - fl[p + 1] + fl[p];
-        if (act) rr[cell(k)] = r;
-        Sr.r[k - 1][sg.col] = r;
-        double v = un_[p] + DC0 * r;
-        if (k == N) v = v + dt * sstr;
-        rhs[p] = v;
-      }
-    }
-  }
   double fcl, wcl;
   fcw(0, fcl, wcl);
   __syncthreads();  // X reused by the second coupling
@@ -321,8 +315,9 @@ __global__ void __launch_bounds__(kSegBlock) k_uv1_seg(Dev d, Range R, int nnew,
     const int k = c0 + p;
     a = -(fcl + fmax0(wcl));
     cc = -(fcu - fmin0(wcu));
-    if (k == 1) bb = 0.5 * (hz[p + 1] + hzm[p + 1]) + 0.5 * dt * (rD + rDm) + fcu + fmax0(wcu);
-    else bb = 0.5 * (hz[p + 1] + hzm[p + 1]) + fcl - fmin0(wcl) + fcu + fmax0(wcu);
+    const double b1 = 0.5 * (hz[p + 1] + hzm[p + 1]) + 0.5 * dt * (rD + rDm) + fcu + fmax0(wcu);
+    const double bk = 0.5 * (hz[p + 1] + hzm[p + 1]) + fcl - fmin0(wcl) + fcu + fmax0(wcu);
+    bb = k == 1 ? b1 : bk;
     dd = rhs[p];
     fcl = fcu; wcl = wcu;
   });
