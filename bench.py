@@ -55,6 +55,12 @@ NT_TS = 2
 C3_L, C3_N, C3_DT, C3_DX = 1024, 100, 300.0, 2.0e3
 
 
+# k_pre_uv_seg's share of pre_step3d's passes: u, v(nstp);
+# u, v(indx) read and written; u, v(nnew) written; ru, rv; Hz, We, Wi, Akv.
+# (The Hz_fwd / Hz_bak scratch it also reads is not a reference array: not counted.)
+PRE_UV_SEG_PASSES = 14
+
+
 def routine_passes(NT_, NT_TS_, lmd=False):
     """unique 3-D array passes per call; step2d counts 35 2-D
     passes per fast step (flagged with None).  lmd: the C3 switch set
@@ -126,7 +132,7 @@ def host_cores():
     cap = os.environ.get("OMP_NUM_THREADS")   # the GPU box exports its CPU share (16) here
     if cap and cap.isdigit() and int(cap) > 0:
         n = min(n, int(cap))
-    return max(1, min(n, 16))
+    return max(1, n)
 
 
 def cpu_baseline(kind):
@@ -238,6 +244,11 @@ def run_workload(kind, romsgpu, comm, rank, world, local_rank, steps, warmup, ti
     D = routines[dom]
     # the fused barotropic kernel alone: 35 2-D passes per fast step over its
     # launch time (one event interval per fast loop on a single rank)
+    # C3: the dominant kernel, pre_step3d's momentum segment solver, alone
+    if c3:
+        pk_ms, pk_n = m.time_routine("k_pre_uv_seg", timing_steps)
+        pk_bytes = 8.0 * PRE_UV_SEG_PASSES * cells3
+        pk_gbs = pk_bytes / (pk_ms * 1e-3) / 1e9 if pk_ms > 0 else 0.0
     fb_ms, fb_n = m.time_routine("k_s2d_fb", timing_steps)
     fb_bytes = 35.0 * 8 * Lr * Mr
     fb_gbs = fb_bytes / (fb_ms * 1e-3) / 1e9 if fb_ms > 0 else 0.0
@@ -259,9 +270,12 @@ def run_workload(kind, romsgpu, comm, rank, world, local_rank, steps, warmup, ti
                     "frac": fb_gbs / HBM_PEAK_GBS, "traffic": pmc_kernel_traffic("k_s2d_fb"),
                     "kernel": "k_s2d_fb", "bytes_per_launch": fb_bytes, "ms_per_launch": fb_ms}
     else:
-        roofline = {"bound": "hbm", "achieved": D["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": D["frac"], "traffic": None, "kernel": dom + " (routine)",
-                    "bytes_per_launch": D["bytes_per_call"], "ms_per_launch": D["ms_per_call"]}
+        # dominant kernel by time per step in the C3 kernel trace
+        # (profiles/r3_*_c3_per_step.txt): k_pre_uv_seg
+        roofline = {"bound": "hbm", "achieved": pk_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": pk_gbs / HBM_PEAK_GBS, "traffic": pmc_kernel_traffic("k_pre_uv_seg", c3=True),
+                    "kernel": "k_pre_uv_seg", "bytes_per_launch": pk_bytes, "ms_per_launch": pk_ms,
+                    "passes": PRE_UV_SEG_PASSES}
     return {
         "value": total_cells * steps / elapsed,
         "ms_per_step": ms_step,
@@ -275,7 +289,7 @@ def run_workload(kind, romsgpu, comm, rank, world, local_rank, steps, warmup, ti
         "steps": steps, "warmup": warmup,
         "roofline": roofline,
         "roofline_routine": {"bound": "hbm", "achieved": D["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                             "frac": D["frac"], "traffic": None if c3 else pmc_traffic(dom),
+                             "frac": D["frac"], "traffic": pmc_traffic(dom, c3),
                              "routine": dom + (" (one fast step: k_s2d_fb + edges + halo)" if dom == "step2d" else ""),
                              "bytes_per_launch": D["bytes_per_call"], "ms_per_launch": D["ms_per_call"]},
         "roofline_step": {"bound": "hbm", "achieved": step_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -285,8 +299,8 @@ def run_workload(kind, romsgpu, comm, rank, world, local_rank, steps, warmup, ti
     }
 
 
-def _pmc():
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def _pmc(c3=False):
+    p = os.path.join(ROOT, "profiles", "pmc_traffic_c3.json" if c3 else "pmc_traffic.json")
     if not os.path.exists(p):
         return {}
     try:
@@ -295,19 +309,20 @@ def _pmc():
         return {}
 
 
-def pmc_kernel_traffic(kernel):
-    """HBM bytes per dispatch of one kernel (C2) from profiles/pmc_traffic.json
-    (2*FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md), or None when absent."""
+def pmc_kernel_traffic(kernel, c3=False):
+    """HBM bytes per dispatch of one kernel from profiles/pmc_traffic.json
+    (C2) or pmc_traffic_c3.json (2*FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md),
+    or None when absent."""
     try:
-        k = _pmc().get("kernels", {}).get(kernel)
+        k = _pmc(c3).get("kernels", {}).get(kernel)
         return None if k is None else float(k["traffic_bytes"]) / float(k["dispatches"])
     except (KeyError, TypeError, ZeroDivisionError, ValueError):
         return None
 
 
-def pmc_traffic(routine):
+def pmc_traffic(routine, c3=False):
     try:
-        r = _pmc().get("routines", {}).get(routine)
+        r = _pmc(c3).get("routines", {}).get(routine)
         return None if r is None else float(r["bytes_per_launch"])
     except (KeyError, TypeError, ValueError):
         return None

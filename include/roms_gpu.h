@@ -377,6 +377,9 @@ enum roms_routine {
   ROMS_R_STEP3D_UV1, ROMS_R_VISC3D, ROMS_R_STEP2D, ROMS_R_STEP3D_UV2, ROMS_R_STEP3D_T, ROMS_R_T3DMIX,
   ROMS_R_LMD_VMIX,
   ROMS_R_K_S2D_FB,  /* kernel level: the fused barotropic kernel k_s2d_fb alone (one fast step) */
+  ROMS_R_K_PRE_UV_SEG,     /* kernel level: pre_step3d's momentum segment solver (N > 63) */
+  ROMS_R_K_UV1_SEG,        /* kernel level: step3d_uv1's momentum segment solver (N > 63) */
+  ROMS_R_K_STEP3D_T_SEG,   /* kernel level: step3d_t's tracer segment solver (N > 63) */
   ROMS_R_COUNT
 };
 int roms_gpu_time_routine(int routine, int nsteps, roms_tlev *t, double *avg_ms, long *launches);

@@ -88,6 +88,7 @@ def lib():
         L.or_frc_record.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_double,
                                     ctypes.POINTER(ctypes.c_double)]
         L.or_frc_clock.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.c_int]
+        L.or_set_pipes.argtypes = [ctypes.c_void_p, ctypes.c_int] + [ctypes.POINTER(ctypes.c_double)] * 4
         _lib = L
     return _lib
 
@@ -200,6 +201,19 @@ class Oracle:
         keep = [None if a is None else np.ascontiguousarray(a, dtype=np.float64) for a in ub]
         args = [None if a is None else a.ctypes.data_as(P) for a in keep]
         self.L.or_set_ub(self.h, *args)
+
+    def set_pipes(self, idx, flx, prf, trc):
+        """set_pipe_frc (pipe_frc.F:33-80): idx/flx on the (-1:Lm+2,-1:Mm+2) grid
+        (pipe number, 0 = none), prf (npip, N), trc (npip, NT)."""
+        P = ctypes.POINTER(ctypes.c_double)
+        prf = np.asfortranarray(prf, dtype=np.float64)
+        trc = np.asfortranarray(trc, dtype=np.float64)
+        keep = [np.ascontiguousarray(idx, dtype=np.float64).ravel(), np.ascontiguousarray(flx, dtype=np.float64).ravel(),
+                prf.ravel(order="F"), trc.ravel(order="F")]
+        assert keep[0].size == self.nx2 * self.ny2 and keep[1].size == self.nx2 * self.ny2
+        assert prf.shape[1] == self.cfg.N and trc.shape == (prf.shape[0], self.cfg.NT)
+        if self.L.or_set_pipes(self.h, prf.shape[0], *[a.ctypes.data_as(P) for a in keep]) != 0:
+            raise ValueError("or_set_pipes")
 
     def frc_record(self, name, slot, rec_time, arr):
         """set_frc_data record `slot` (0/1) of field `name` at rec_time [days]."""

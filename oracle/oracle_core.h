@@ -43,9 +43,11 @@ struct or_state {
   double *hbls, *hbbl, *ghat, *swr_frac;
   double *lmdKv, *lmdKt, *lmdKs, *lmdRig;  /* lmd_vmix A3d scratch (0:N) */
   double *lmd2[9];                         /* lmd_kpp A2d scratch */
-  /* pipe_frc.F (npip = 1, analytic): pipe_idx>0 cells carry pipe_flx */
-  int pipe_source;
-  double *pipe_flx, *pipe_idx, pipe_prf[1024], pipe_trc[2];
+  /* pipe_frc.F: pipe_idx>0 cells carry pipe_flx of pipe pidx = pipe_idx;
+     pipe_prf(npip,N) and pipe_trc(npip,NT) column-major (pipe_frc.F:34-35,198),
+     indexed by pidx as omega.F:102-108 and step3d_t_ISO.F:927-934 do */
+  int pipe_source, npip;
+  double *pipe_flx, *pipe_idx, *pipe_prf, *pipe_trc;
   /* river_frc.F: riv_uflx/riv_vflx = 10*iriver + signed fraction on the
      faces between a river-mouth land cell and its wet neighbours;
      riv_vol(nriv), riv_trc(nriv,NT) column-major */

@@ -62,6 +62,8 @@ or_state *or_create(const or_cfg *cfg) {
   for (int q = 0; q < 6; q++) S->c1[q] = zalloc((size_t)S->nx2 * (S->N + 1));
   if (cfg->lmd) or_lmd_alloc(S);
   S->pipe_flx = zalloc(n2); S->pipe_idx = zalloc(n2);
+  S->npip = 1;
+  S->pipe_prf = zalloc((size_t)S->N); S->pipe_trc = zalloc((size_t)S->NT);
   S->riv_uflx = zalloc(n2); S->riv_vflx = zalloc(n2);
   S->uwnd = zalloc(n2); S->vwnd = zalloc(n2); S->tair = zalloc(n2); S->qair = zalloc(n2); S->prate = zalloc(n2);
   S->swrad = zalloc(n2); S->lwrad = zalloc(n2); S->sustr_r = zalloc(n2); S->svstr_r = zalloc(n2);
@@ -445,6 +447,7 @@ void or_ana_grid(or_state *S) {
     const double psz = SizeX * 0.02, px = SizeX * .5, py = SizeY * .5;
     const double pipe_cells = (double)(lround(psz / dx) * lround(psz / dx));
     S->pipe_source = 1;
+    S->npip = 1;
     for (int k = 0; k < S->N; k++) S->pipe_prf[k] = 0.0;
     S->pipe_prf[0] = 0.5; S->pipe_prf[1] = 0.5;
     S->pipe_trc[0] = 24.0; S->pipe_trc[1] = 1.0;
@@ -785,6 +788,22 @@ int or_frc_record(or_state *S, const char *name, int slot, double time, const do
   S->frc[q].t[slot] = time;
   return 0;
 }
+/* set_pipe_frc (pipe_frc.F:33-80): npip pipes; pipe_idx/pipe_flx on the grid,
+ * pipe_prf(npip,N), pipe_trc(npip,NT) column-major; npip = 0 switches off */
+int or_set_pipes(or_state *S, int npip, const double *idx, const double *flx, const double *prf, const double *trc) {
+  if (npip < 0) return -1;
+  S->pipe_source = npip > 0;
+  if (npip == 0) return 0;
+  free(S->pipe_prf); free(S->pipe_trc);
+  S->npip = npip;
+  S->pipe_prf = zalloc((size_t)npip * S->N);
+  S->pipe_trc = zalloc((size_t)npip * S->NT);
+  memcpy(S->pipe_prf, prf, (size_t)npip * S->N * sizeof(double));
+  memcpy(S->pipe_trc, trc, (size_t)npip * S->NT * sizeof(double));
+  memcpy(S->pipe_idx, idx, S->n2 * sizeof(double));
+  memcpy(S->pipe_flx, flx, S->n2 * sizeof(double));
+  return 0;
+}
 void or_frc_clock(or_state *S, double start_time, int on) {
   S->frc_clock = on;
   S->frc_start = start_time;
@@ -866,6 +885,7 @@ void or_set_iif(or_state *S, int iif) { S->iif = iif; }
 double *or_field(or_state *S, const char *name, size_t *count) {
   struct { const char *n; double *p; size_t c; } tab[] = {
       {"riv_uflx", S->riv_uflx, S->n2}, {"riv_vflx", S->riv_vflx, S->n2},
+      {"pipe_idx", S->pipe_idx, S->n2}, {"pipe_flx", S->pipe_flx, S->n2},
       {"uwnd", S->uwnd, S->n2}, {"vwnd", S->vwnd, S->n2}, {"tair", S->tair, S->n2}, {"qair", S->qair, S->n2},
       {"prate", S->prate, S->n2}, {"swrad", S->swrad, S->n2}, {"lwrad", S->lwrad, S->n2},
       {"sustr_r", S->sustr_r, S->n2}, {"svstr_r", S->svstr_r, S->n2},

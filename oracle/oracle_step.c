@@ -193,8 +193,10 @@ void or_omega(or_state *S) {
     for (int k = 1; k <= N; k++)
       for (int i = S->istr; i <= S->iend; i++) {
         WI(i, j, k) = WI(i, j, k - 1) - FLXU(i + 1, j, k) + FLXU(i, j, k) - FLXV(i, j + 1, k) + FLXV(i, j, k);
-        if (S->pipe_source && A2(S->pipe_idx, i, j) > 0)  /* omega.F:102-108 */
-          WI(i, j, k) = WI(i, j, k) + A2(S->pipe_flx, i, j) * S->pipe_prf[k - 1];
+        if (S->pipe_source && A2(S->pipe_idx, i, j) > 0) {  /* omega.F:102-108: pipe_prf(pidx,k) */
+          const int pidx = (int)A2(S->pipe_idx, i, j);
+          WI(i, j, k) = WI(i, j, k) + A2(S->pipe_flx, i, j) * S->pipe_prf[(pidx - 1) + (size_t)S->npip * (k - 1)];
+        }
         C1(CX, i, k) = fmax0(FLXU(i + 1, j, k)) - fmin0(FLXU(i, j, k)) + fmax0(FLXV(i, j + 1, k)) -
                        fmin0(FLXV(i, j, k));
       }
@@ -1523,10 +1525,13 @@ void or_step3d_t(or_state *S) {
         for (int i = S->istr; i <= S->iend; i++) {
           TT(i, j, k, nnew, itrc) =
               TT(i, j, k, nnew, itrc) - dt * A2(S->pm, i, j) * A2(S->pn, i, j) * (C1(FC, i, k) - C1(FC, i, k - 1));
-          if (S->pipe_source && A2(S->pipe_idx, i, j) > 0.)  /* step3d_t_ISO.F:927-934 */
+          if (S->pipe_source && A2(S->pipe_idx, i, j) > 0.) {  /* step3d_t_ISO.F:927-934 */
+            const int pidx = (int)A2(S->pipe_idx, i, j);
             TT(i, j, k, nnew, itrc) = TT(i, j, k, nnew, itrc) + dt * A2(S->pm, i, j) * A2(S->pn, i, j) *
-                                                                    A2(S->pipe_flx, i, j) * S->pipe_prf[k - 1] *
-                                                                    S->pipe_trc[itrc - 1];
+                                                                    A2(S->pipe_flx, i, j) *
+                                                                    S->pipe_prf[(pidx - 1) + (size_t)S->npip * (k - 1)] *
+                                                                    S->pipe_trc[(pidx - 1) + (size_t)S->npip * (itrc - 1)];
+          }
         }
       /* heat of rain (step3d_t_ISO.F:939-951): BULK_FRC uses the 2 m air
        * temperature tair, otherwise the water's own t(N)/Hz(N) */

@@ -75,6 +75,8 @@ double   *or_field(or_state *S, const char *name, size_t *count);
 /* set_frc_data records (time in days) and the in-step clock (start_time [s]) */
 int       or_frc_record(or_state *S, const char *name, int slot, double time, const double *data);
 void      or_frc_clock(or_state *S, double start_time, int on);
+int       or_set_pipes(or_state *S, int npip, const double *idx, const double *flx, const double *prf,
+                       const double *trc);
 /* scalar time indices: iic kstp knew nstp nrhs nnew */
 void      or_tindex(const or_state *S, int out[6]);
 

@@ -35,12 +35,16 @@ namespace roms {
 // independent blocks per CU whose load and solve phases overlap.
 struct SegSpan {
   int s, S, c0, n;  // segment index, count, first cell (1-based), cells in segment
-  int col;          // column of the lane within the block (0..kSegCW-1)
+  int col;          // column of the lane within the block row (0..kSegCW-1)
+  int row;          // row j of the lane within the block (threadIdx.z)
+  int l;            // the lane's column slot in the block's LDS exchange (col + kSegCW*row)
 };
 __device__ __forceinline__ SegSpan seg_span(int N) {
   SegSpan r;
   const int t = (int)(threadIdx.x + blockDim.x * threadIdx.y);
   r.col = t % kSegCW;
+  r.row = (int)threadIdx.z;
+  r.l = r.col + kSegCW * r.row;
   r.s = t / kSegCW;
   r.S = (int)(blockDim.x * blockDim.y) / kSegCW;
   const int base = N / r.S, rem = N % r.S;
@@ -88,8 +92,8 @@ __device__ __forceinline__ uint3 seg_tile(int ord, int xg = 4) {
 
 // LDS exchange area of one block: 6 end-relation values per (segment, column)
 struct SegXchg {
-  double v[6][kSegMaxS][kSegCW];
-  double uv[kSegMaxS > 8 ? 2 : 1][kSegMaxS][kSegCW];   // U_t, V_t of the reduced system (kSegMaxS > 8)
+  double v[6][kSegMaxS][kSegCW * kSegJMax];
+  double uv[kSegMaxS > 8 ? 2 : 1][kSegMaxS][kSegCW * kSegJMax];   // U_t, V_t of the reduced system (kSegMaxS > 8)
 };
 
 // Every per-row loop below is straight-line code over all KR rows: rows
@@ -129,7 +133,7 @@ struct SegTri {
   }
   // publish the first/last-row relations, barrier, reduced solve -> x_L, x_R
   __device__ __forceinline__ void couple(const SegSpan& sp, int n, SegXchg& X, double& xL, double& xR) {
-    const int s = sp.s, S = sp.S, l = sp.col;
+    const int s = sp.s, S = sp.S, l = sp.l;
     double y = 0.0, al = 0.0, be = 0.0, yl = 0.0, all = 0.0, bel = 0.0;
 #pragma unroll
     for (int q = KR - 1; q >= 0; q--) {
@@ -286,27 +290,27 @@ __device__ __forceinline__ void tracer_spline_seg(const SegSpan& sg, int N, long
 }
 
 // Block prologue of the momentum column kernels: grid z = direction (0: u at
-// i >= istrU, 1: v at j >= jstrV), 16 columns per block row.  Lanes past the
-// column range solve a clamped duplicate column (they take part in the
-// barriers) and store nothing.  Returns false for a block with no v column.
+// i >= istrU, 1: v at j >= jstrV), 16 columns x blockDim.z rows j per block.
+// Lanes outside the column range (i or j) solve a clamped duplicate column
+// (they take part in the barriers) and store nothing.
 struct SegCol {
   int i, j, dir;
   bool act;
 };
-__device__ __forceinline__ bool seg_uv_col(const Dev& d, const Range& R, const uint3& bI, const SegSpan& sg,
+__device__ __forceinline__ void seg_uv_col(const Dev& d, const Range& R, const uint3& bI, const SegSpan& sg,
                                            SegCol& c) {
   const Bounds& b = d.b;
   c.dir = (int)bI.z;
-  c.j = R.j0 + (int)bI.y;
-  if (c.dir == 1 && c.j < b.jstrV) return false;   // uniform over the block
   const int ilo = c.dir == 0 ? b.istrU : b.istr;
+  const int jlo = c.dir == 1 ? (b.jstrV > R.j0 ? b.jstrV : R.j0) : R.j0;
   const int iu = R.i0 + (int)bI.x * kSegCW + sg.col;
-  c.act = iu >= ilo && iu <= R.i1;
+  const int ju = R.j0 + (int)bI.y * (int)blockDim.z + sg.row;
+  c.act = iu >= ilo && iu <= R.i1 && ju >= jlo && ju <= R.j1;
   c.i = iu < ilo ? ilo : (iu > R.i1 ? R.i1 : iu);
-  return true;
+  c.j = ju < jlo ? jlo : (ju > R.j1 ? R.j1 : ju);
 }
-inline dim3 seg_grid_of(const Range& R, int nz) {
-  return dim3((R.i1 - R.i0 + kSegCW) / kSegCW, R.j1 - R.j0 + 1, nz);
+inline dim3 seg_grid_of(const Range& R, int nz, int jrows = 1) {
+  return dim3((R.i1 - R.i0 + kSegCW) / kSegCW, (R.j1 - R.j0 + jrows) / jrows, nz);
 }
 
 }  // namespace roms

@@ -451,7 +451,7 @@ __global__ void __launch_bounds__(kSegBlock, 2) k_pre_tracer_seg(Dev d, Range R,
   }
 }
 
-__global__ void __launch_bounds__(kSegBlock, 2) k_pre_uv_seg(Dev d, Range R, PreCoef c, int nstp, int nnew, int nrhs) {
+__global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_pre_uv_seg(Dev d, Range R, PreCoef c, int nstp, int nnew, int nrhs) {
   const uint3 bI = seg_tile(d.p.seg_order, d.p.seg_xg);
   __shared__ SegXchg X;
   constexpr int KR = kSegRows + 1;
@@ -460,7 +460,7 @@ __global__ void __launch_bounds__(kSegBlock, 2) k_pre_uv_seg(Dev d, Range R, Pre
   const int N = b.N, indx = 3 - nstp;
   const SegSpan sg = seg_span(N);
   SegCol col;
-  if (!seg_uv_col(d, R, bI, sg, col)) return;
+  seg_uv_col(d, R, bI, sg, col);
   const int dir = col.dir;
   const bool act = col.act;
   const long n2 = b.n2, ij = IJ(b, col.i, col.j), s = dir == 0 ? 1 : b.nx2;
@@ -588,9 +588,12 @@ void launch_pre_step3d(const Dev& d, hipStream_t s, const Tlev& t) {
   hipLaunchKernelGGL(k_rd, grid_of(Rd), dim3(kBX, kBY), 0, s, d, Rd, t.nstp);
   dim3 gu = gridc_of(RI);
   gu.z = 2;
-  if (d.p.colseg)
-    hipLaunchKernelGGL(k_pre_uv_seg, seg_grid_of(RI, 2), dim3(kCX, seg_waves(b.N)), 0, s, d, RI, c, t.nstp, t.nnew,
-                       t.nrhs);
+  if (d.p.colseg) {
+    ktimer_mark(s, kTimedPreUvSeg, 0);
+    hipLaunchKernelGGL(k_pre_uv_seg, seg_grid_of(RI, 2, d.p.seg_jrows), dim3(kCX, seg_waves(b.N), d.p.seg_jrows), 0, s,
+                       d, RI, c, t.nstp, t.nnew, t.nrhs);
+    ktimer_mark(s, kTimedPreUvSeg, 1, 1);
+  }
   else if (d.f.colscr)
     hipLaunchKernelGGL(k_pre_uv<ColGlb>, gu, dim3(kCX), 0, s, d, RI, c, t.nstp, t.nnew, t.nrhs);
   else

@@ -303,8 +303,11 @@ void launch_step3d_t(const Dev& d, hipStream_t s, const Tlev& t) {
     hipLaunchKernelGGL(k_step3d_t_h, grid3_of(r, b.N), dim3(kBX, kBY), 0, s, d, r, t.nnew, t.nrhs);
     dim3 gt = gridc_of(r);
     gt.z = b.NT;
-    if (d.p.colseg)
+    if (d.p.colseg) {
+      ktimer_mark(s, kTimedStep3dTSeg, 0);
       hipLaunchKernelGGL(k_step3d_t_seg, seg_grid_of(r, b.NT), dim3(kCX, seg_waves(b.N)), 0, s, d, r, t.nnew, t.nrhs);
+      ktimer_mark(s, kTimedStep3dTSeg, 1, 1);
+    }
     else if (d.f.colscr)
       hipLaunchKernelGGL(k_step3d_t_v<ColGlb>, gt, dim3(kCX), 0, s, d, r, t.nnew, t.nrhs);
     else

@@ -243,13 +243,12 @@ __global__ void __launch_bounds__(64, 2) k_uv1_reg(Dev d, Range R, int nnew, int
 // the implicit viscosity are each one partitioned tridiagonal system with the
 // rows of uv1_col; the final ru(k) of every level go to LDS, from where the
 // first segment forms rufrc/rvfrc in the reference's k = 1..N order. ----
-struct SegRu {
-  double r[kSegRows * kSegMaxS][kSegCW];
-};
-__global__ void __launch_bounds__(kSegBlock, 2) k_uv1_seg(Dev d, Range R, int nnew, int nrhs) {
+// ru(k) of the block's columns for rufrc: dynamic LDS, level k-1 of lane
+// slot l at roms_smem[(k-1)*ncol + l], ncol = kSegCW*blockDim.z
+__global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_uv1_seg(Dev d, Range R, int nnew, int nrhs) {
   const uint3 bI = seg_tile(d.p.seg_order, d.p.seg_xg);
   __shared__ SegXchg X;
-  __shared__ SegRu Sr;
+  double* const Sr = roms_smem;   // (see above)
   constexpr int KR = kSegRows + 1;
   const Bounds& b = d.b;
   const Fields& F = d.f;
@@ -257,7 +256,8 @@ __global__ void __launch_bounds__(kSegBlock, 2) k_uv1_seg(Dev d, Range R, int nn
   const double dt = d.p.dt;
   const SegSpan sg = seg_span(N);
   SegCol col;
-  if (!seg_uv_col(d, R, bI, sg, col)) return;
+  seg_uv_col(d, R, bI, sg, col);
+  const int ncol = kSegCW * (int)blockDim.z;
   const int dir = col.dir;
   const bool act = col.act;
   const long n2 = b.n2, ij = IJ(b, col.i, col.j), s = dir == 0 ? 1 : b.nx2;
@@ -283,7 +283,7 @@ __global__ void __launch_bounds__(kSegBlock, 2) k_uv1_seg(Dev d, Range R, int nn
     const int k = c0 + p;
     const long o = cell(k);
     const double r = k == 1 ? rr[o] - fl[1] : rr[o] - fl[p + 1 < KR ? p + 1 : KR - 1] + fl[p];
-    if (p < n) Sr.r[k - 1][sg.col] = r;
+    if (p < n) Sr[(k - 1) * ncol + sg.l] = r;
     const double v = Un[o] + DC0 * r;
     rhs[p] = k == N ? v + dt * sstr : v;
   }
@@ -330,8 +330,8 @@ __global__ void __launch_bounds__(kSegBlock, 2) k_uv1_seg(Dev d, Range R, int nn
     if (p < n) Un[cell(c0 + p)] = T.D[p] * 0.5 * (hz[p + 1] + hzm[p + 1]);
   if (sg.s == 0) {
     const double dmdn = dir == 0 ? F.dm_u[ij] * F.dn_u[ij] : F.dm_v[ij] * F.dn_v[ij];
-    double frc = Sr.r[0][sg.col] + dmdn * (sstr - 0.5 * (rDm + rD) * T.D[0]);
-    for (int k = 2; k <= N; k++) frc = frc + Sr.r[k - 1][sg.col];
+    double frc = Sr[sg.l] + dmdn * (sstr - 0.5 * (rDm + rD) * T.D[0]);
+    for (int k = 2; k <= N; k++) frc = frc + Sr[(k - 1) * ncol + sg.l];
     if (dir == 0) F.rufrc[ij] = frc;
     else F.rvfrc[ij] = frc;
   }
@@ -339,6 +339,11 @@ __global__ void __launch_bounds__(kSegBlock, 2) k_uv1_seg(Dev d, Range R, int nn
 
 void setup_column_kernels_uv1(size_t bytes) {
   (void)hipFuncSetAttribute((const void*)k_uv1<ColLds>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+// the ru levels of k_uv1_seg's rows-j blocks (up to kSegJMax rows, N <= kSegRows*kSegMaxS)
+void setup_uv1_seg() {
+  (void)hipFuncSetAttribute((const void*)k_uv1_seg, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)((size_t)kSegRows * kSegMaxS * kSegCW * kSegJMax * sizeof(double)));
 }
 
 void launch_step3d_uv1(const Dev& d, hipStream_t s, const Tlev& t) {
@@ -349,8 +354,12 @@ void launch_step3d_uv1(const Dev& d, hipStream_t s, const Tlev& t) {
   g.z = 2;
   if ((d.p.colreg & 1) && b.N == 50)
     hipLaunchKernelGGL(k_uv1_reg<50>, g, dim3(kCX), col_lds_bytes(1, 50), s, d, R, t.nnew, t.nrhs);
-  else if (d.p.colseg)
-    hipLaunchKernelGGL(k_uv1_seg, seg_grid_of(R, 2), dim3(kCX, seg_waves(b.N)), 0, s, d, R, t.nnew, t.nrhs);
+  else if (d.p.colseg) {
+    ktimer_mark(s, kTimedUv1Seg, 0);
+    hipLaunchKernelGGL(k_uv1_seg, seg_grid_of(R, 2, d.p.seg_jrows), dim3(kCX, seg_waves(b.N), d.p.seg_jrows),
+                       (size_t)b.N * kSegCW * d.p.seg_jrows * sizeof(double), s, d, R, t.nnew, t.nrhs);
+    ktimer_mark(s, kTimedUv1Seg, 1, 1);
+  }
   else if (d.f.colscr)
     hipLaunchKernelGGL(k_uv1<ColGlb>, g, dim3(kCX), 0, s, d, R, t.nnew, t.nrhs);
   else

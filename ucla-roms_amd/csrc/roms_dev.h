@@ -43,6 +43,7 @@ struct Params {
   int chain;      // 1: chained 4-lane set_HUV1 (k_chain.h; ROMS_GPU_CHAIN=0 disables)
   int seg_order;  // block order of the segment solvers (seg_tile; ROMS_GPU_SEG_ORDER)
   int seg_xg;     // x-blocks per group of seg_order 3 (ROMS_GPU_SEG_XG)
+  int seg_jrows;  // rows j per block of the momentum segment solvers (1..kSegJMax; ROMS_GPU_SEG_JROWS)
   int npip;       // pipe_frc.F: number of pipes (0: pipe_source off)
   int nriv, nrivf;  // river_frc.F: number of rivers (0: river_source off), river faces
   int curvgrid;   // CURVGRID && UV_ADV: curvature terms (compute_horiz_rhs_uv_terms.h:8-11)
@@ -197,6 +198,10 @@ constexpr int kSegMaxS = ROMS_SEG_MAXS;   // segments per block (kSegCW columns 
 #endif
 constexpr int kSegCW = ROMS_SEG_CW;       // columns per segment-solver block (lanes of one segment)
 constexpr int kSegBlock = ((kSegMaxS * kSegCW + 63) / 64) * 64;   // threads of a segment-solver block (max)
+// The momentum solvers' blocks may hold several rows j (blockDim.z) of the
+// same 16 columns, so the v columns' j-1, j-2, j+1 stencil rows are loaded
+// by the neighbouring rows' waves of the same block, close together in time.
+constexpr int kSegJMax = 4;
 inline dim3 gridc_of(const Range& r) {
   int ni = r.i1 - r.i0 + 1, nj = r.j1 - r.j0 + 1;
   if (ni < 1) ni = 1;
@@ -224,6 +229,7 @@ struct Tlev {
 // events on the launch stream opening (end = 0) and closing (end = 1) an
 // interval that covers `count` launches of one kernel
 constexpr int kTimedS2dFb = 13;   // ROMS_R_K_S2D_FB
+constexpr int kTimedPreUvSeg = 14, kTimedUv1Seg = 15, kTimedStep3dTSeg = 16;   // ROMS_R_K_*_SEG
 void ktimer_mark(hipStream_t s, int kernel_id, int end, int count = 0);
 
 void launch_exchange(const Dev& d, hipStream_t s, double* a, int nlev);
@@ -270,6 +276,7 @@ void launch_exchange_tracers(const Dev& d, hipStream_t s, int tlev);  // t(:,:,:
 // the full 160 KB when N needs more than the default 64 KB.  Returns false if
 // N is too deep for one wavefront's columns to fit.
 bool setup_column_kernels(int N);
+void setup_uv1_seg();   // k_uv1_seg's dynamic LDS limit (k_step3d_uv.hip)
 inline size_t col_smem_bytes(const Dev& d, int nslots) {
   return d.f.colscr ? 0 : (size_t)nslots * (d.b.N + 1) * 64 * sizeof(double);
 }

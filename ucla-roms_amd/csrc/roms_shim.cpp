@@ -481,6 +481,11 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     const char* e = getenv("ROMS_GPU_SEG_XG");
     if (e && atoi(e) > 0) P.seg_xg = atoi(e);
   }
+  P.seg_jrows = 2;
+  {
+    const char* e = getenv("ROMS_GPU_SEG_JROWS");
+    if (e && atoi(e) >= 1 && atoi(e) <= kSegJMax) P.seg_jrows = atoi(e);
+  }
   // column-solver scratch: LDS while two (N+1)-level slots per wave fit the
   // default 64 KB (N < 63), global memory for deeper grids;
   // ROMS_GPU_COL_GLOBAL=1/0 forces either (A/B runs)
@@ -490,6 +495,7 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     if (e && e[0] == '1') col_global = true;
     if (e && e[0] == '0') col_global = false;
   }
+  setup_uv1_seg();
   if (!col_global && !setup_column_kernels(dims->N)) {
     g.err = "roms_gpu_init: N too large for the LDS column kernels (2*(N+1)*512 B > 160 KB)";
     return -2;
@@ -1062,6 +1068,8 @@ int roms_gpu_time_routine(int routine, int nsteps, roms_tlev* t, double* avg_ms,
     t->nrhs = t->nstp;
     t->nnew = 3;
     t->nfast = g.cfg.nfast;
+    const int r = frc_step_prepare(g.s, g.d, g.cfg.dt, *t, g.err);   // in-step forcing, as roms_gpu_step
+    if (r) { g.timed = -1; return r; }
     enqueue_step(t);
   }
   g.timed = -1;
