@@ -211,6 +211,36 @@ def test_graph_replay_bitwise_equals_eager():
         os.environ.pop("ROMS_GPU_NO_GRAPH", None)
 
 
+@pytest.mark.parametrize("graphs", [True, False])
+def test_rho_eos_reuse_bitwise_and_invalidated(graphs, monkeypatch):
+    """A step opens with rho_eos(nrhs) (main.F:397) on the t, z_r, Hz the
+    previous step's closing rho_eos(nnew) (main.F:479) already used; the
+    library skips the repeat (roms_shim.cpp g.rho_slot).  With the skip on
+    and off the runs are bitwise equal, including after the host rewrites t
+    between steps (copy_in must invalidate the reuse)."""
+    if not graphs:
+        monkeypatch.setenv("ROMS_GPU_NO_GRAPH", "1")
+    cfg = oracle.pipes_cfg(LLm=40, MMm=40, np_xi=1, np_eta=1)
+
+    def run(reuse):
+        monkeypatch.setenv("ROMS_GPU_RHO_REUSE", "1" if reuse else "0")
+        m = romsgpu.Model.from_case(cfg.case_id, cfg.LLm, cfg.MMm, cfg.N, cfg.NT, salinity=True, nonlin_eos=True,
+                                    dt=cfg.dt, ndtfast=cfg.ndtfast, sizex=cfg.sizex, sizey=cfg.sizey, lmd=cfg.lmd)
+        m.step(3)
+        m.diag()
+        t = m.get("t")
+        t[:, 15:25, 15:25] += 0.75     # every level and slot of T (and S) in a patch
+        m.put("t", t)
+        m.step(3)
+        out = {n: m.get(n) for n in ("rho1", "qp1", "bvf", "t", "u", "v", "zeta", "Akv", "Akt")}
+        m.close()
+        return out
+
+    a, b = run(True), run(False)
+    for n in a:
+        assert np.array_equal(a[n], b[n]), n
+
+
 def test_diag_blowup_flag_is_fatal():
     """A non-finite norm is diag.F's 'Abnormal termination: BLOWUP'
     (diag.F:621-633): roms_gpu_diag fails instead of printing NaN."""

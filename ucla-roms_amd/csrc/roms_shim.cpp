@@ -43,6 +43,15 @@ struct Ctx {
   long riv_maxidx = 0;        // largest river index nint(riv_flx/10) of the faces on the device
   bool have_swr = false;      // swr_frac formed (at rest, main.F:216-220)
   long graph_frc_gen = 0;     // frc_step_gen() the step graphs were captured with
+  // rho_eos reuse: the T slot whose rho1/qp1/bvf/rhoA/rhoS are current because
+  // the last thing done to the model was a step, which ended with
+  // rho_eos(nnew) (main.F:479).  The next step's opening rho_eos(nrhs)
+  // (main.F:397) reads the same t(nstp), z_r, Hz, z_w (set_depth ran in the
+  // last fast step, step2d_FB.F:569) and would rewrite the same values, so it
+  // is skipped.  Every entry that may change the state clears it
+  // (REQUIRE_INIT); the read-only ones keep it (REQUIRE_INIT_RO).
+  int rho_slot = 0;
+  bool rho_reuse = true;      // ROMS_GPU_RHO_REUSE=0 turns the skip off
   std::string err;
   // graph cache: key = (nstp, knew at step start)
   std::map<long, hipGraphExec_t> graphs;
@@ -120,7 +129,13 @@ void rank_extent(int LL, int np, int node, int& len, int& sw) {
     REQUIRE_INIT_NOJOIN();                              \
     REQUIRE_HALO_OK();                                  \
     if (g.d.halo) halo_join(g.halo, g.s);               \
+    g.rho_slot = 0;                                     \
   } while (0)
+// entries that leave every model field as it was keep g.rho_slot
+#define REQUIRE_INIT_RO()                               \
+  const int rho_keep_ = g.rho_slot;                     \
+  REQUIRE_INIT();                                       \
+  g.rho_slot = rho_keep_
 
 int post_launch() {
   hipError_t e = hipGetLastError();
@@ -291,8 +306,10 @@ Tlev to_tlev(const roms_tlev* t) {
   } while (0)
 
 }  // namespace
-int roms::shim_enter(ShimState& S) {
+int roms::shim_enter(ShimState& S, bool read_only) {
+  const int rho_keep = g.rho_slot;
   REQUIRE_INIT();
+  if (read_only) g.rho_slot = rho_keep;
   S.d = &g.d; S.s = g.s; S.dims = &g.dims; S.cfg = &g.cfg; S.err = &g.err;
   return 0;
 }
@@ -320,15 +337,17 @@ namespace {
 
 // the roms_step sequence for one step whose indices are already set in *t
 // (nstp,nrhs=nstp,nnew=3 on entry); enqueues everything on g.s
-void enqueue_step(roms_tlev* t) {
+// rho_current: rho_eos(nrhs) is already current (g.rho_slot, see there)
+void enqueue_step(roms_tlev* t, bool rho_current) {
   const Dev& d = g.d;
   hipStream_t s = g.s;
   Tlev T = to_tlev(t);
   const bool pot = g.cfg.pot_tides != 0;
+  g.rho_slot = 0;
   frc_step_phase(d, s, 0, pot);     // set_forces, frc_time 'current' (main.F:384-385)
   launch_bulk_flux(d, s, T.nrhs);   // set_forces (main.F:386): BULK_FRC only
   frc_step_phase(d, s, 1, pot);     // set_bry_all '1/2 fwd' + set_tides (main.F:389-394)
-  TIMED(ROMS_R_RHO_EOS, launch_rho_eos(d, s, T, T.nrhs));
+  if (!rho_current) TIMED(ROMS_R_RHO_EOS, launch_rho_eos(d, s, T, T.nrhs));
   TIMED(ROMS_R_SET_HUV, launch_set_huv(d, s, T));
   TIMED(ROMS_R_OMEGA, launch_omega(d, s, T));
   if (g.cfg.lmd_mixing) TIMED(ROMS_R_LMD_VMIX, launch_lmd_vmix(d, s, T, T.nstp));
@@ -360,6 +379,7 @@ void enqueue_step(roms_tlev* t) {
   TIMED(ROMS_R_STEP3D_T, launch_step3d_t(d, s, T));
   if (g.cfg.ts_dif2) TIMED(ROMS_R_T3DMIX, launch_t3dmix(d, s, T));
   TIMED(ROMS_R_RHO_EOS, launch_rho_eos(d, s, T, T.nnew));
+  g.rho_slot = T.nnew;
 }
 
 }  // namespace
@@ -544,6 +564,9 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
   }
   const char* env = getenv("ROMS_GPU_NO_GRAPH");
   g.use_graphs = !(env && env[0] == '1') && halo_graph_safe(g.d.halo);
+  env = getenv("ROMS_GPU_RHO_REUSE");
+  g.rho_reuse = !(env && env[0] == '0');
+  g.rho_slot = 0;
   g.inited = true;
   return 0;
 }
@@ -588,7 +611,7 @@ static int xfer(int id, bool up) {
   return 0;
 }
 int roms_gpu_upload(int id) { REQUIRE_INIT(); return xfer(id, true); }
-int roms_gpu_download(int id) { REQUIRE_INIT(); return xfer(id, false); }
+int roms_gpu_download(int id) { REQUIRE_INIT_RO(); return xfer(id, false); }
 
 int roms_gpu_copy_in(int id, const double* src, long count) {
   REQUIRE_INIT();
@@ -598,7 +621,7 @@ int roms_gpu_copy_in(int id, const double* src, long count) {
   return 0;
 }
 int roms_gpu_copy_out(int id, double* dst, long count) {
-  REQUIRE_INIT();
+  REQUIRE_INIT_RO();
   if (id < 0 || id >= ROMS_NFIELDS || count != g.f[id].count) { g.err = "roms_gpu_copy_out: bad field/size"; return -1; }
   CHECK_HIP(hipMemcpyAsync(dst, g.f[id].d, (size_t)count * sizeof(double), hipMemcpyDeviceToHost, g.s));
   CHECK_HIP(hipStreamSynchronize(g.s));
@@ -606,7 +629,7 @@ int roms_gpu_copy_out(int id, double* dst, long count) {
   return 0;
 }
 int roms_gpu_sync(void) {
-  REQUIRE_INIT();
+  REQUIRE_INIT_RO();
   CHECK_HIP(hipStreamSynchronize(g.s));
   REQUIRE_HALO_OK();
   return post_launch();
@@ -818,12 +841,14 @@ int roms_gpu_bulk_flux(const roms_tlev* t) {
 }
 
 int roms_gpu_step(roms_tlev* t) {
-  REQUIRE_INIT();
+  REQUIRE_INIT_RO();
+  g.rho_slot = 0;
   t->iic = t->iic + 1;
   t->nstp = 1 + (t->iic - t->ntstart) % 2;
   t->nrhs = t->nstp;
   t->nnew = 3;
   t->nfast = g.cfg.nfast;
+  const bool rho_current = g.rho_reuse && rho_keep_ == t->nrhs;
   {
     // in-step forcing weights of this step (roms_gpu_frc_clock), queued ahead of its kernels
     const int r = frc_step_prepare(g.s, g.d, g.cfg.dt, *t, g.err);
@@ -838,16 +863,16 @@ int roms_gpu_step(roms_tlev* t) {
   }
   const bool first = (t->iic == t->forw_start);
   if (!g.use_graphs || first) {
-    enqueue_step(t);
+    enqueue_step(t, rho_current);
     return post_launch();
   }
-  const long key = (long)t->nstp * 16 + t->knew;
+  const long key = (long)t->nstp * 16 + t->knew + (rho_current ? 256 : 0);
   auto it = g.graphs.find(key);
   roms_tlev t0 = *t;
   if (it == g.graphs.end()) {
     hipGraph_t graph;
     CHECK_HIP(hipStreamBeginCapture(g.s, hipStreamCaptureModeThreadLocal));
-    enqueue_step(t);
+    enqueue_step(t, rho_current);
     CHECK_HIP(hipStreamEndCapture(g.s, &graph));
     hipGraphExec_t exec;
     CHECK_HIP(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
@@ -860,6 +885,7 @@ int roms_gpu_step(roms_tlev* t) {
   CHECK_HIP(hipGraphLaunch(it->second, g.s));
   t->nrhs = 3;
   t->nnew = 3 - t->nstp;
+  g.rho_slot = t->nnew;   // the replayed step ended with rho_eos(nnew)
   for (int iif = 1; iif <= t->nfast; iif++) {
     t->iif = iif;
     t->kstp = t->knew;
@@ -1047,7 +1073,7 @@ int roms_gpu_halo_plan(int Lm, int Mm, int np_xi, int np_eta, int inode, int jno
 }
 
 int roms_gpu_time_routine(int routine, int nsteps, roms_tlev* t, double* avg_ms, long* launches) {
-  REQUIRE_INIT();
+  REQUIRE_INIT_RO();   // runs whole steps, as roms_gpu_step
   if (routine < 0 || routine >= ROMS_R_COUNT || nsteps < 1 || !avg_ms || !launches) {
     g.err = "roms_gpu_time_routine: bad argument";
     return -1;
@@ -1070,7 +1096,7 @@ int roms_gpu_time_routine(int routine, int nsteps, roms_tlev* t, double* avg_ms,
     t->nfast = g.cfg.nfast;
     const int r = frc_step_prepare(g.s, g.d, g.cfg.dt, *t, g.err);   // in-step forcing, as roms_gpu_step
     if (r) { g.timed = -1; return r; }
-    enqueue_step(t);
+    enqueue_step(t, g.rho_reuse && g.rho_slot == t->nrhs);
   }
   g.timed = -1;
   CHECK_HIP(hipStreamSynchronize(g.s));
@@ -1090,7 +1116,7 @@ int roms_gpu_time_routine(int routine, int nsteps, roms_tlev* t, double* avg_ms,
 }
 
 int roms_gpu_time_steps(roms_tlev* t, int n, double* ms) {
-  REQUIRE_INIT();
+  REQUIRE_INIT_RO();
   hipEvent_t a, b;
   CHECK_HIP(hipEventCreate(&a));
   CHECK_HIP(hipEventCreate(&b));
@@ -1147,7 +1173,7 @@ int roms_gpu_set_weights(int ndtfast, double weight[2][ROMS_MAX_FAST]) {
 // reduction by pairs, first-maximum Courant scan, blow-up flag); six numbers
 // come back, ranks combine in the reference's tree order (diag.F:488-535).
 int roms_gpu_diag(const roms_tlev* t, double norms[4]) {
-  REQUIRE_INIT();
+  REQUIRE_INIT_RO();
   if (!g.have_volume) {
     CHECK_HIP(hipStreamSynchronize(g.s));
     const int r = grid_integrals();

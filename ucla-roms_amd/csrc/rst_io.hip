@@ -290,7 +290,7 @@ void define_file(nc::File& f, const ShimState& S, const std::vector<OutVar>& var
 
 int write_record(const char* path, int rec, int total_rec, double time, const roms_tlev* t, bool rst, int mask) {
   ShimState S;
-  int r = shim_enter(S);
+  int r = shim_enter(S, true);
   if (r) return r;
   if (!path || rec < 1 || !t) { *S.err = "roms_gpu_wrt: bad path/record/time levels"; return -1; }
   if ((r = io_join(*S.err))) return r;

@@ -18,7 +18,7 @@ struct ShimState {
 };
 // The entry checks of every routine (initialised, no failed halo wait, fast-
 // loop exchange joined); fills S.  Returns 0 or the negative error code.
-int shim_enter(ShimState& S);
+int shim_enter(ShimState& S, bool read_only = false);   // read_only: the call changes no model field
 void shim_set_error(const std::string& e);
 void io_free();
 // A blocking copy ordered on the library's stream.  The kernels run on
