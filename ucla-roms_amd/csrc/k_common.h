@@ -456,6 +456,47 @@ __device__ __forceinline__ void uv_horiz_rhs(const Dev& d, const A& a, int i, in
   }
 }
 
+// uv_horiz_rhs without CURVGRID on values the caller loaded ahead (ru, rv,
+// Hz at (i,j), (i-1,j), (i,j-1) and fomn at the same points): the kernel
+// issues these loads together with its window loads (one memory wait per
+// block).  Same arithmetic as uv_horiz_rhs.
+struct UVPre {
+  double ru, rv, hz0, hzx, hzy, f0, fx, fy;
+};
+template <class A>
+__device__ __forceinline__ void uv_horiz_rhs_pre(const Dev& d, const A& a, int i, int j, long o, const UVPre& p,
+                                                 const UVBounds& r, bool up) {
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const bool ucor = d.p.uv_cor, adv = d.p.uv_adv;
+  if (i >= b.istrU && i <= b.iend && j >= b.jstr && j <= b.jend) {
+    double ru = p.ru;
+    if (ucor) {
+      const double c0 = 0.5 * p.hz0 * (p.f0);
+      const double c1 = 0.5 * p.hzx * (p.fx);
+      const double U0 = c0 * (a.v(i, j) + a.v(i, j + 1)), U1 = c1 * (a.v(i - 1, j) + a.v(i - 1, j + 1));
+      ru = ru + 0.5 * (U0 + U1);
+    }
+    if (adv)
+      ru = ru - adv_UFx(a, i, j, r, up) + adv_UFx(a, i - 1, j, r, up) - adv_UFe(a, i, j + 1, r, up) +
+           adv_UFe(a, i, j, r, up);
+    F.ru[o] = ru;
+  }
+  if (i >= b.istr && i <= b.iend && j >= b.jstrV && j <= b.jend) {
+    double rv = p.rv;
+    if (ucor) {
+      const double c0 = 0.5 * p.hz0 * (p.f0);
+      const double c1 = 0.5 * p.hzy * (p.fy);
+      const double V0 = c0 * (a.u(i, j) + a.u(i + 1, j)), V1 = c1 * (a.u(i, j - 1) + a.u(i + 1, j - 1));
+      rv = rv - 0.5 * (V0 + V1);
+    }
+    if (adv)
+      rv = rv - adv_VFx(a, i + 1, j, r, up) + adv_VFx(a, i, j, r, up) - adv_VFe(a, i, j, r, up) +
+           adv_VFe(a, i, j - 1, r, up);
+    F.rv[o] = rv;
+  }
+}
+
 // ---- SPLINE_UV with LDS column scratch: leaves the vertical advective flux
 // of u (dir 0) / v (dir 1) at w-levels in A[k], k=0..N, A[0]=A[N]=0
 // (compute_vert_rhs_uv_terms.h); the r.h.s. update is rr(k) = rr(k) - A[k] +

@@ -58,6 +58,94 @@ __global__ void __launch_bounds__(256) k_pre_tracer_h(Dev d, Range R, PreCoef c,
   }
 }
 
+// ---- the same for NTT <= 2 tracers with every global load issued at entry:
+// the windows (masks, FlxU/FlxV, each tracer) and the lane's own inputs
+// (pseudo-continuity terms, t(nstp), t(indx)) land together, so a block waits
+// for memory once instead of once per phase.  The per-phase form above waits
+// 2 + 2 NT times and, with ~7 blocks per CU, was bound by those round trips,
+// not by bandwidth.  Same expressions in the same order: bit-identical. ----
+template <int NTT>
+struct TracerWinN {
+  double UM[kUVN], VM[kUVN], FU[kUVN], FV[kUVN], T[NTT][kUVN];
+};
+template <int NTT>
+__global__ void __launch_bounds__(256) k_pre_tracer_h1(Dev d, Range R, PreCoef c, int nstp, int nnew, int nrhs) {
+  const uint3 bI = xcd_tile();
+  __shared__ TracerWinN<NTT> W;
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const int k = 1 + (int)bI.z, indx = 3 - nstp;
+  const int i0 = R.i0 + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * kBY;
+  const int ib = i0 - 2, jb = j0 - 2;
+  const long kk = (long)(k - 1) * b.n2, n2 = b.n2;
+  const int tid = threadIdx.x + kBX * threadIdx.y;
+  constexpr int NR = (kUVN + kBX * kBY - 1) / (kBX * kBY);
+  double wUM[NR], wVM[NR], wFU[NR], wFV[NR], wT[NTT][NR];
+#pragma unroll
+  for (int r = 0; r < NR; r++) {
+    const int q = tid + r * kBX * kBY;
+    const int i = ib + q % kUVW, j = jb + q / kUVW;
+    const bool ok = q < kUVN && i >= -1 && i <= b.Lm + 2 && j >= -1 && j <= b.Mm + 2;
+    const long o = ok ? IJ(b, i, j) : 0;
+    wUM[r] = ok ? F.umask[o] : 0.0;
+    wVM[r] = ok ? F.vmask[o] : 0.0;
+    wFU[r] = ok ? F.FlxU[o + kk] : 0.0;
+    wFV[r] = ok ? F.FlxV[o + kk] : 0.0;
+#pragma unroll
+    for (int t = 0; t < NTT; t++)
+      wT[t][r] = ok ? F.t[(long)(nrhs - 1) * b.n3 + (long)t * 3 * b.n3 + o + kk] : 0.0;
+  }
+  const int i = i0 + (int)threadIdx.x, j = j0 + (int)threadIdx.y;
+  const bool act = i <= R.i1 && j <= R.j1;
+  const bool in = act && i >= b.istr && j >= b.jstr;
+  const long ij = act ? IJ(b, i, j) : IJ(b, R.i0, R.j0), o = ij + kk, w = ij + (long)k * n2;
+  // hz_bak_fwd's inputs (pre_step3d4S.F:136-148) and the tracer time levels
+  const double fu0 = F.FlxU[o], fu1 = F.FlxU[o + 1], fv0 = F.FlxV[o], fv1 = F.FlxV[o + b.nx2];
+  const double we1 = F.We[w], wi1 = F.Wi[w], we0 = F.We[w - n2], wi0 = F.Wi[w - n2];
+  const double pm = F.pm[ij], pn = F.pn[ij], hzo = F.Hz[o];
+  double ts[NTT], ti[NTT];
+#pragma unroll
+  for (int t = 0; t < NTT; t++) {
+    const long tb = (long)t * 3 * b.n3;
+    ts[t] = F.t[(long)(nstp - 1) * b.n3 + tb + o];
+    ti[t] = F.t[(long)(indx - 1) * b.n3 + tb + o];
+  }
+#pragma unroll
+  for (int r = 0; r < NR; r++) {
+    const int q = tid + r * kBX * kBY;
+    if (q < kUVN) {
+      W.UM[q] = wUM[r]; W.VM[q] = wVM[r]; W.FU[q] = wFU[r]; W.FV[q] = wFV[r];
+#pragma unroll
+      for (int t = 0; t < NTT; t++) W.T[t][q] = wT[t][r];
+    }
+  }
+  __syncthreads();
+  if (!act) return;
+  const double cff = 0.5 * c.dtau;
+  const double FlxDiv = cff * pm * pn * (fu1 - fu0 + fv1 - fv0 + we1 + wi1 - we0 - wi0);
+  const double hb = hzo + FlxDiv, hf = hzo - FlxDiv;
+  F.c2[o] = hf;  // Hz_fwd, Hz_bak kept for the column solves (range istr-1.., jstr-1..)
+  F.c3[o] = hb;
+  if (!in) return;
+  const double hz = hzo;
+#pragma unroll
+  for (int t = 0; t < NTT; t++) {
+    const int itrc = t + 1;
+    const AccTL a{W.T[t], W.UM, W.VM, W.FU, W.FV, ib, jb};
+    double FX0 = tracer_fx(b, a, i, j, false), FX1 = tracer_fx(b, a, i + 1, j, false);
+    double FE0 = tracer_fe(b, a, i, j, false), FE1 = tracer_fe(b, a, i, j + 1, false);
+    if (d.p.nriv > 0) {   // river inflow faces (compute_horiz_tracer_fluxes.h:217-246)
+      river_tracer_flux(d, 0, i, j, k, itrc, FX0); river_tracer_flux(d, 0, i + 1, j, k, itrc, FX1);
+      river_tracer_flux(d, 1, i, j, k, itrc, FE0); river_tracer_flux(d, 1, i, j + 1, k, itrc, FE1);
+    }
+    const long tb = (long)t * 3 * b.n3;
+    const double tsk = ts[t];
+    F.t[(long)(nnew - 1) * b.n3 + tb + o] =
+        hb * (c.cf_stp * tsk + c.cf_bak * ti[t]) - c.dtau * pm * pn * (FX1 - FX0 + FE1 - FE0);
+    F.t[(long)(indx - 1) * b.n3 + tb + o] = hz * tsk;
+  }
+}
+
 // ---- tracers, vertical part per column: spline advection on t(nrhs), then
 // implicit diffusion with Wi up-winding on Hz_fwd (LDS slots A, B). ----
 template <class C>
@@ -212,20 +300,56 @@ __global__ void __launch_bounds__(256) k_uv_horiz(Dev d, Range R, int nrhs, UVBo
   const double* V = F.v + (long)(nrhs - 1) * b.n3 + kk;
   const double* FU = F.FlxU + kk;
   const double* FV = F.FlxV + kk;
-  for (int q = threadIdx.x + kBX * threadIdx.y; q < kUVN; q += kBX * kBY) {
-    const int i = ib + q % kUVW, j = jb + q / kUVW;
-    if (i < -1 || i > b.Lm + 2 || j < -1 || j > b.Mm + 2) continue;  // never read
-    const long o = IJ(b, i, j);
-    sU[q] = U[o];
-    sV[q] = V[o];
-    sFU[q] = FU[o];
-    sFV[q] = FV[o];
+  const int i = i0 + (int)threadIdx.x, j = j0 + (int)threadIdx.y;
+  const bool act = i <= R.i1 && j <= R.j1;
+  if (!d.p.hoist || d.p.curvgrid) {
+    for (int q = threadIdx.x + kBX * threadIdx.y; q < kUVN; q += kBX * kBY) {
+      const int ii = ib + q % kUVW, jj = jb + q / kUVW;
+      if (ii < -1 || ii > b.Lm + 2 || jj < -1 || jj > b.Mm + 2) continue;  // never read
+      const long o = IJ(b, ii, jj);
+      sU[q] = U[o];
+      sV[q] = V[o];
+      sFU[q] = FU[o];
+      sFV[q] = FV[o];
+    }
+    __syncthreads();
+    if (!act) return;
+    const AccL a{sU, sV, sFU, sFV, ib, jb};
+    uv_horiz_rhs(d, a, i, j, k, ub, up != 0);
+    return;
+  }
+  // window and the lane's own inputs loaded together (one memory wait)
+  const int tid = threadIdx.x + kBX * threadIdx.y;
+  constexpr int NR = (kUVN + kBX * kBY - 1) / (kBX * kBY);
+  double wU[NR], wV[NR], wFU[NR], wFV[NR];
+#pragma unroll
+  for (int r = 0; r < NR; r++) {
+    const int q = tid + r * kBX * kBY;
+    const int ii = ib + q % kUVW, jj = jb + q / kUVW;
+    const bool ok = q < kUVN && ii >= -1 && ii <= b.Lm + 2 && jj >= -1 && jj <= b.Mm + 2;
+    const long o = ok ? IJ(b, ii, jj) : 0;
+    wU[r] = ok ? U[o] : 0.0;
+    wV[r] = ok ? V[o] : 0.0;
+    wFU[r] = ok ? FU[o] : 0.0;
+    wFV[r] = ok ? FV[o] : 0.0;
+  }
+  const long ij = act ? IJ(b, i, j) : IJ(b, R.i0, R.j0), o = ij + kk;
+  UVPre p;
+  p.ru = F.ru[o]; p.rv = F.rv[o];
+  p.hz0 = p.hzx = p.hzy = p.f0 = p.fx = p.fy = 0.0;
+  if (d.p.uv_cor) {
+    p.hz0 = F.Hz[o]; p.hzx = F.Hz[o - 1]; p.hzy = F.Hz[o - b.nx2];
+    p.f0 = F.fomn[ij]; p.fx = F.fomn[ij - 1]; p.fy = F.fomn[ij - b.nx2];
+  }
+#pragma unroll
+  for (int r = 0; r < NR; r++) {
+    const int q = tid + r * kBX * kBY;
+    if (q < kUVN) { sU[q] = wU[r]; sV[q] = wV[r]; sFU[q] = wFU[r]; sFV[q] = wFV[r]; }
   }
   __syncthreads();
-  const int i = i0 + (int)threadIdx.x, j = j0 + (int)threadIdx.y;
-  if (i > R.i1 || j > R.j1) return;
+  if (!act) return;
   const AccL a{sU, sV, sFU, sFV, ib, jb};
-  uv_horiz_rhs(d, a, i, j, k, ub, up != 0);
+  uv_horiz_rhs_pre(d, a, i, j, o, p, ub, up != 0);
 }
 
 void launch_uv_horiz(const Dev& d, hipStream_t s, int nrhs, int up) {
@@ -571,7 +695,12 @@ void launch_pre_step3d(const Dev& d, hipStream_t s, const Tlev& t) {
   else { c.dtau = d.p.dt * (1.0 - AM3_crv); c.cf_stp = 0.5 + AM3_crv; c.cf_bak = 0.5 - AM3_crv; }
   Range RI{b.istr, b.iend, b.jstr, b.jend};
   Range RH{b.istr - 1, b.iend, b.jstr - 1, b.jend};
-  hipLaunchKernelGGL(k_pre_tracer_h, grid3_of(RH, b.N), dim3(kBX, kBY), 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs);
+  if (d.p.hoist && b.NT == 2)
+    hipLaunchKernelGGL(k_pre_tracer_h1<2>, grid3_of(RH, b.N), dim3(kBX, kBY), 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs);
+  else if (d.p.hoist && b.NT == 1)
+    hipLaunchKernelGGL(k_pre_tracer_h1<1>, grid3_of(RH, b.N), dim3(kBX, kBY), 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs);
+  else
+    hipLaunchKernelGGL(k_pre_tracer_h, grid3_of(RH, b.N), dim3(kBX, kBY), 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs);
   dim3 gt = gridc_of(RI);
   gt.z = b.NT;
   if (d.p.colseg)

@@ -39,6 +39,71 @@ __global__ void __launch_bounds__(256) k_step3d_t_h(Dev d, Range R, int nnew, in
   }
 }
 
+// The same for NTT <= 2 tracers with every global load issued at entry (see
+// k_pre_tracer_h1): one memory wait per block.  Bit-identical.
+template <int NTT>
+struct TracerWinS {
+  double UM[kUVN], VM[kUVN], FU[kUVN], FV[kUVN], T[NTT][kUVN];
+};
+template <int NTT>
+__global__ void __launch_bounds__(256) k_step3d_t_h1(Dev d, Range R, int nnew, int nrhs) {
+  const uint3 bI = xcd_tile();
+  __shared__ TracerWinS<NTT> W;
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const int k = 1 + (int)bI.z;
+  const int i0 = R.i0 + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * kBY;
+  const int ib = i0 - 2, jb = j0 - 2;
+  const long kk = (long)(k - 1) * b.n2;
+  const int tid = threadIdx.x + kBX * threadIdx.y;
+  constexpr int NR = (kUVN + kBX * kBY - 1) / (kBX * kBY);
+  double wUM[NR], wVM[NR], wFU[NR], wFV[NR], wT[NTT][NR];
+#pragma unroll
+  for (int r = 0; r < NR; r++) {
+    const int q = tid + r * kBX * kBY;
+    const int i = ib + q % kUVW, j = jb + q / kUVW;
+    const bool ok = q < kUVN && i >= -1 && i <= b.Lm + 2 && j >= -1 && j <= b.Mm + 2;
+    const long o = ok ? IJ(b, i, j) : 0;
+    wUM[r] = ok ? F.umask[o] : 0.0;
+    wVM[r] = ok ? F.vmask[o] : 0.0;
+    wFU[r] = ok ? F.FlxU[o + kk] : 0.0;
+    wFV[r] = ok ? F.FlxV[o + kk] : 0.0;
+#pragma unroll
+    for (int t = 0; t < NTT; t++)
+      wT[t][r] = ok ? F.t[(long)(nrhs - 1) * b.n3 + (long)t * 3 * b.n3 + o + kk] : 0.0;
+  }
+  const int i = i0 + (int)threadIdx.x, j = j0 + (int)threadIdx.y;
+  const bool act = i <= R.i1 && j <= R.j1;
+  const long ij = act ? IJ(b, i, j) : IJ(b, R.i0, R.j0), o = ij + kk;
+  const double pm = F.pm[ij], pn = F.pn[ij];
+  double tn[NTT];
+#pragma unroll
+  for (int t = 0; t < NTT; t++) tn[t] = F.t[(long)(nnew - 1) * b.n3 + (long)t * 3 * b.n3 + o];
+#pragma unroll
+  for (int r = 0; r < NR; r++) {
+    const int q = tid + r * kBX * kBY;
+    if (q < kUVN) {
+      W.UM[q] = wUM[r]; W.VM[q] = wVM[r]; W.FU[q] = wFU[r]; W.FV[q] = wFV[r];
+#pragma unroll
+      for (int t = 0; t < NTT; t++) W.T[t][q] = wT[t][r];
+    }
+  }
+  __syncthreads();
+  if (!act) return;
+#pragma unroll
+  for (int t = 0; t < NTT; t++) {
+    const int itrc = t + 1;
+    const AccTL a{W.T[t], W.UM, W.VM, W.FU, W.FV, ib, jb};
+    double FX0 = tracer_fx(b, a, i, j, true), FX1 = tracer_fx(b, a, i + 1, j, true);
+    double FE0 = tracer_fe(b, a, i, j, true), FE1 = tracer_fe(b, a, i, j + 1, true);
+    if (d.p.nriv > 0) {   // river inflow faces (compute_horiz_tracer_fluxes.h:217-246)
+      river_tracer_flux(d, 0, i, j, k, itrc, FX0); river_tracer_flux(d, 0, i + 1, j, k, itrc, FX1);
+      river_tracer_flux(d, 1, i, j, k, itrc, FE0); river_tracer_flux(d, 1, i, j + 1, k, itrc, FE1);
+    }
+    F.t[(long)(nnew - 1) * b.n3 + (long)t * 3 * b.n3 + o] = tn[t] - d.p.dt * pm * pn * (FX1 - FX0 + FE1 - FE0);
+  }
+}
+
 // Vertical part per column: spline advection on t(nrhs), surface fluxes
 // (+ KPP non-local and solar terms), implicit diffusion.  LDS slots: A holds
 // FC (spline) then DC(k) at A[k-1]; B holds the spline CF then Thomas CF.
@@ -300,7 +365,12 @@ void launch_step3d_t(const Dev& d, hipStream_t s, const Tlev& t) {
   Range R{b.istr, b.iend, b.jstr, b.jend};
   // horizontal fluxes, then the column solves, on a sub-range of the interior
   auto run = [&](const Range& r) {
-    hipLaunchKernelGGL(k_step3d_t_h, grid3_of(r, b.N), dim3(kBX, kBY), 0, s, d, r, t.nnew, t.nrhs);
+    if (d.p.hoist && b.NT == 2)
+      hipLaunchKernelGGL(k_step3d_t_h1<2>, grid3_of(r, b.N), dim3(kBX, kBY), 0, s, d, r, t.nnew, t.nrhs);
+    else if (d.p.hoist && b.NT == 1)
+      hipLaunchKernelGGL(k_step3d_t_h1<1>, grid3_of(r, b.N), dim3(kBX, kBY), 0, s, d, r, t.nnew, t.nrhs);
+    else
+      hipLaunchKernelGGL(k_step3d_t_h, grid3_of(r, b.N), dim3(kBX, kBY), 0, s, d, r, t.nnew, t.nrhs);
     dim3 gt = gridc_of(r);
     gt.z = b.NT;
     if (d.p.colseg) {

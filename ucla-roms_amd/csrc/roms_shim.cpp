@@ -501,6 +501,10 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     const char* e = getenv("ROMS_GPU_SEG_XG");
     if (e && atoi(e) > 0) P.seg_xg = atoi(e);
   }
+  {
+    const char* e = getenv("ROMS_GPU_HOIST");
+    P.hoist = !(e && e[0] == '0');
+  }
   P.seg_jrows = 2;
   {
     const char* e = getenv("ROMS_GPU_SEG_JROWS");
