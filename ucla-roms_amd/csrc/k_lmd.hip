@@ -406,11 +406,13 @@ __global__ void __launch_bounds__(64) k_kpp_int(Dev d, Range R, EdgeClamp ec, in
   const bool wet = rm > 0.5;
   // KPP shape functions (lmd_kpp.F:374-446), BKPP (:447-495), masked copy (:496-528)
   auto finish = [&](int k, double Kv, double Kt, double Ks, double zwk) {
-    double wm, ws;
-    wscale_wm_ws(zwN - zwk, Bfsfc, hbl, ustar, rm, vonKar, wm, ws);
     const double ssgm = (zwN - zwk) / dmax(hbl, kEPS);
     double gh = 0.;
     if (ssgm < 1.) {
+      // the turbulent velocity scales are only used inside the boundary layer
+      // (lmd_kpp.F:407-441 forms them at every level and discards them below)
+      double wm, ws;
+      wscale_wm_ws(zwN - zwk, Bfsfc, hbl, ustar, rm, vonKar, wm, ws);
       double cff;
       if (ssgm < 0.07) cff = 0.5 * ((ssgm - 0.07) * (ssgm - 0.07)) / 0.07;
       else cff = 0.;

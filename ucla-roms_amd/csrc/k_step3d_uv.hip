@@ -482,6 +482,9 @@ __global__ void __launch_bounds__(256) k_visc3d(Dev d, Range R, int nstp) {
     const double* Hk = F.Hz + kk;
     const double* Uk = U + kk;
     const double* Vk = V + kk;
+    // the lane's u/v(indx) of this level, loaded with the stress inputs (one
+    // memory wait per level instead of a second one after the barriers)
+    const double ui = du ? Ui[ij + kk] : 0.0, vi = dv ? Vi[ij + kk] : 0.0;
     if (k > 1) __syncthreads();  // previous level's stresses consumed
 #pragma unroll
     for (int m = 0; m < kVQ; m++) {
@@ -511,12 +514,12 @@ __global__ void __launch_bounds__(256) k_visc3d(Dev d, Range R, int nstp) {
     const long o = ij + kk;
     if (du) {
       const double cff = cu0 * (cun * (sUFx[qr] - sUFx[qr - 1]) + cum * (sUFe[qp + kVW] - sUFe[qp]));
-      Ui[o] = Ui[o] + d.p.dt * cff;
+      Ui[o] = ui + d.p.dt * cff;
       fu = fu + cff;
     }
     if (dv) {
       const double cff = cv0 * (cvn * (sVFx[qp + 1] - sVFx[qp]) + cvm * (sVFe[qr] - sVFe[qr - kVW]));
-      Vi[o] = Vi[o] + d.p.dt * cff;
+      Vi[o] = vi + d.p.dt * cff;
       fv = fv + cff;
     }
   }
