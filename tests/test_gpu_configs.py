@@ -79,9 +79,9 @@ def test_models_in_sequence_are_independent():
     earlier model of the same process left in recycled device memory: the
     fill is a null-stream hipMemset, which the library's non-blocking stream
     does not wait for, so dev_alloc waits for it (before that fix the C2
-    100-step test failed in some test-process histories).  A regression
-    guard: the race itself is timing dependent (tools/memset_race.hip shows
-    it directly), and this sequence passed with the unfixed library too."""
+    100-step test failed in some test-process histories).  This sequence is
+    the end-to-end symptom; test_zero_fill_lands_before_the_stream below
+    drives the allocation path itself."""
     def run(cfg, n):
         m = romsgpu.Model.from_case(cfg.case_id, cfg.LLm, cfg.MMm, cfg.N, cfg.NT, salinity=bool(cfg.salinity),
                                     nonlin_eos=bool(cfg.nonlin_eos), dt=cfg.dt, ndtfast=cfg.ndtfast,
@@ -98,6 +98,19 @@ def test_models_in_sequence_are_independent():
     b = run(c2, 20)
     for k in a:
         assert np.array_equal(a[k], b[k]), k
+
+
+def test_zero_fill_lands_before_the_stream():
+    """Regression test of the round-2 race, through the library's own
+    allocator: 1 GiB filled with ones and freed, allocated again (same
+    memory) with the zero fill, and counted on the library stream at once.
+    With the null-stream fill not joined (the unfixed dev_alloc) the count
+    is nonzero -- tools/memset_race.hip's probe of the same sequence read
+    stale data in 20 of 20 tries."""
+    m = romsgpu.Model.from_case(0, 32, 24, 16, sizex=12.8e3, sizey=3.2e3)
+    for n, chunks in ((1 << 27, 1), (1 << 22, 32), (1 << 18, 256)):
+        assert m.selftest_zero_fill(n, chunks) == 0, (n, chunks)
+    m.close()
 
 
 def test_c2_full_grid_2_steps():

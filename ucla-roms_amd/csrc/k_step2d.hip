@@ -425,8 +425,9 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int cl
     __syncthreads();
     // the edge kernels read zeta_new / Dnew from global scratch: every block
     // stores the window cells it computed or set (identical values where
-    // windows overlap)
-    for (int q = tid; q < kFN; q += NT) {
+    // windows overlap); with the edges folded in (closed == 2) the block
+    // reads them from its window instead
+    for (int q = tid; q < kFN && closed == 1; q += NT) {
       if (!T.st[q]) continue;
       const long o = IJ(b, i0 - 1 + q % kFX, j0 - 1 + q / kFX);
       F.s0[o] = T.zn[q];
@@ -435,11 +436,13 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int cl
   }
   // P3: zeta(knew), fast averages, pressure gradient, momentum
   const int i = i0 + (int)threadIdx.x, j = j0 + (int)threadIdx.y;
-  if (i > R.i1 || j > R.j1) return;
+  const bool pin = i <= R.i1 && j <= R.j1;
+  if (closed != 2 && !pin) return;
   const int q = (threadIdx.x + 1) + (threadIdx.y + 1) * kFX;  // (i,j); q-1 = (i-1,j); q-kFX = (i,j-1)
   const int g = G(i, j);                                        // g-1: (i-1,j); g-kGX: (i,j-1)
   const long ij = IJ(b, i, j);
-  {
+  double ubn = 0.0, vbn = 0.0;   // ubar/vbar(knew) this lane formed (closed == 2)
+  if (pin) {
     const double z = T.zn[q];
     F.zeta[ij + (long)(c.knew - 1) * n2] = z;
     const double du = DU(i, j), dv = DV(i, j);
@@ -457,57 +460,123 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int cl
       F.DV_avg2[ij] = (pint ? x_DV2 : F.DV_avg2[ij]) + c.w2 * dv;
     }
   }
-  if (!pint) return;
-  const double gh = 0.5 * d.p.g;
-  const double h0 = T.h[g], hxm = T.h[g - 1], hym = T.h[g - kGX];
-  const double rA0 = x_rA0, rAx = x_rAx, rAy = x_rAy;
-  // pressure gradient at u (neighbour q-1) and v (neighbour q-kFX) points
-  auto pgf = [&](int qm, double hm, double rAm, double dn) {
-    return gh * dn *
-           ((hm + h0) * (T.rz[qm] - T.rz[q]) + T.rz2[qm] - T.rz2[q] +
-            (hm - h0) * (T.rzSA[qm] + T.rzSA[q] + 0.333333333333 * (rAm - rA0) * (T.zw[qm] - T.zw[q])));
-  };
-  const double dn_u = x_dnu, dm_v = x_dmv;
-  double rubar = pgf(q - 1, hxm, rAx, dn_u);
-  double rvbar = pgf(q - kFX, hym, rAy, dm_v);
-  double rufrc = x_rufrc, rvfrc = x_rvfrc;
-  if (c.iif == 1) {
-    rufrc = rufrc - rubar;
-    rvfrc = rvfrc - rvbar;
-    F.rufrc[ij] = rufrc;
-    F.rvfrc[ij] = rvfrc;
-    auto corr = [&](int qq, int gg, double rS, double rA, double& zwrk, double& rzeta, double& rzeta2,
-                    double& rzetaSA) {
-      const double zn = T.zn[qq], zk = T.z0[gg];
-      zwrk = zn - zk;
-      rzeta = (1.0 + rS) * zwrk;
-      rzeta2 = rzeta * (zn + zk);
-      rzetaSA = zwrk * (rS - rA);
+  if (pint) {
+    const double gh = 0.5 * d.p.g;
+    const double h0 = T.h[g], hxm = T.h[g - 1], hym = T.h[g - kGX];
+    const double rA0 = x_rA0, rAx = x_rAx, rAy = x_rAy;
+    // pressure gradient at u (neighbour q-1) and v (neighbour q-kFX) points
+    auto pgf = [&](int qm, double hm, double rAm, double dn) {
+      return gh * dn *
+             ((hm + h0) * (T.rz[qm] - T.rz[q]) + T.rz2[qm] - T.rz2[q] +
+              (hm - h0) * (T.rzSA[qm] + T.rzSA[q] + 0.333333333333 * (rAm - rA0) * (T.zw[qm] - T.zw[q])));
     };
-    double zw0, rz0, rz20, sa0, zw1, rz1, rz21, sa1, zw2, rz2_, rz22, sa2;
-    corr(q, g, x_rS0, rA0, zw0, rz0, rz20, sa0);
-    corr(q - 1, g - 1, x_rSx, rAx, zw1, rz1, rz21, sa1);
-    corr(q - kFX, g - kGX, x_rSy, rAy, zw2, rz2_, rz22, sa2);
-    rubar = rubar + gh * dn_u *
-                        ((hxm + h0) * (rz1 - rz0) + rz21 - rz20 +
-                         (hxm - h0) * (sa1 + sa0 + 0.333333333333 * (rAx - rA0) * (zw1 - zw0)));
-    rvbar = rvbar + gh * dm_v *
-                        ((hym + h0) * (rz2_ - rz0) + rz22 - rz20 +
-                         (hym - h0) * (sa2 + sa0 + 0.333333333333 * (rAy - rA0) * (zw2 - zw0)));
+    const double dn_u = x_dnu, dm_v = x_dmv;
+    double rubar = pgf(q - 1, hxm, rAx, dn_u);
+    double rvbar = pgf(q - kFX, hym, rAy, dm_v);
+    double rufrc = x_rufrc, rvfrc = x_rvfrc;
+    if (c.iif == 1) {
+      rufrc = rufrc - rubar;
+      rvfrc = rvfrc - rvbar;
+      F.rufrc[ij] = rufrc;
+      F.rvfrc[ij] = rvfrc;
+      auto corr = [&](int qq, int gg, double rS, double rA, double& zwrk, double& rzeta, double& rzeta2,
+                      double& rzetaSA) {
+        const double zn = T.zn[qq], zk = T.z0[gg];
+        zwrk = zn - zk;
+        rzeta = (1.0 + rS) * zwrk;
+        rzeta2 = rzeta * (zn + zk);
+        rzetaSA = zwrk * (rS - rA);
+      };
+      double zw0, rz0, rz20, sa0, zw1, rz1, rz21, sa1, zw2, rz2_, rz22, sa2;
+      corr(q, g, x_rS0, rA0, zw0, rz0, rz20, sa0);
+      corr(q - 1, g - 1, x_rSx, rAx, zw1, rz1, rz21, sa1);
+      corr(q - kFX, g - kGX, x_rSy, rAy, zw2, rz2_, rz22, sa2);
+      rubar = rubar + gh * dn_u *
+                          ((hxm + h0) * (rz1 - rz0) + rz21 - rz20 +
+                           (hxm - h0) * (sa1 + sa0 + 0.333333333333 * (rAx - rA0) * (zw1 - zw0)));
+      rvbar = rvbar + gh * dm_v *
+                          ((hym + h0) * (rz2_ - rz0) + rz22 - rz20 +
+                           (hym - h0) * (sa2 + sa0 + 0.333333333333 * (rAy - rA0) * (zw2 - zw0)));
+    }
+    const double cff = 0.5 * d.p.dtfast, cff1 = 0.5 * c.w1;
+    const double Dstp0 = T.z0[g] + h0;
+    if (i >= b.istrU) {
+      const double Dstpm = T.z0[g - 1] + hxm;
+      const double DUnew = ((Dstp0 + Dstpm) * x_ub + cff * (x_pm0 + x_pmx) * (x_pn0 + x_pnx) * (rubar + rufrc)) * x_um;
+      ubn = DUnew / (T.Dn[q] + T.Dn[q - 1]);
+      F.ubar[ij + (long)(c.knew - 1) * n2] = ubn;
+      F.DU_avg1[ij] = (c.iif == 1 ? 0.0 : x_DU1) + cff1 * dn_u * (DUnew);
+    }
+    if (j >= b.jstrV) {
+      const double Dstpm = T.z0[g - kGX] + hym;
+      const double DVnew = ((Dstp0 + Dstpm) * x_vb + cff * (x_pm0 + x_pmy) * (x_pn0 + x_pny) * (rvbar + rvfrc)) * x_vm;
+      vbn = DVnew / (T.Dn[q] + T.Dn[q - kFX]);
+      F.vbar[ij + (long)(c.knew - 1) * n2] = vbn;
+      F.DV_avg1[ij] = (c.iif == 1 ? 0.0 : x_DV1) + cff1 * dm_v * (DVnew);
+    }
   }
-  const double cff = 0.5 * d.p.dtfast, cff1 = 0.5 * c.w1;
-  const double Dstp0 = T.z0[g] + h0;
-  if (i >= b.istrU) {
-    const double Dstpm = T.z0[g - 1] + hxm;
-    const double DUnew = ((Dstp0 + Dstpm) * x_ub + cff * (x_pm0 + x_pmx) * (x_pn0 + x_pnx) * (rubar + rufrc)) * x_um;
-    F.ubar[ij + (long)(c.knew - 1) * n2] = DUnew / (T.Dn[q] + T.Dn[q - 1]);
-    F.DU_avg1[ij] = (c.iif == 1 ? 0.0 : x_DU1) + cff1 * dn_u * (DUnew);
-  }
-  if (j >= b.jstrV) {
-    const double Dstpm = T.z0[g - kGX] + hym;
-    const double DVnew = ((Dstp0 + Dstpm) * x_vb + cff * (x_pm0 + x_pmy) * (x_pn0 + x_pny) * (rvbar + rvfrc)) * x_vm;
-    F.vbar[ij + (long)(c.knew - 1) * n2] = DVnew / (T.Dn[q] + T.Dn[q - kFX]);
-    F.DV_avg1[ij] = (c.iif == 1 ? 0.0 : x_DV1) + cff1 * dm_v * (DVnew);
+  if (closed != 2) return;
+  // ---- closed walls folded in (k_s2d_edges phases 0, 1, 3 with no open
+  // edge; the host folds only when every edge cell and its interior
+  // neighbour fall in one tile).  Same expressions as k_s2d_edges. ----
+  {
+    const int is = b.istr, ie = b.iend, js = b.jstr, je = b.jend;
+    const long kn = (long)(c.knew - 1) * n2;
+    double* sU = T.z1;   // ubar / vbar(knew) of the tile cells (z1, z2: last read in P2)
+    double* sV = T.z2;
+    const int t = threadIdx.x + kBX * threadIdx.y;
+    // phase 0: wall-normal components (u2dbc_im.F / v2dbc_im.F closed walls)
+    if (pin && j >= js && j <= je && ((b.west_edge && i == is) || (b.east_edge && i == ie + 1))) {
+      ubn = 0.0;
+      F.ubar[ij + kn] = ubn;
+    }
+    if (pin && i >= is && i <= ie && ((b.south_edge && j == js) || (b.north_edge && j == je + 1))) {
+      vbn = 0.0;
+      F.vbar[ij + kn] = vbn;
+    }
+    sU[t] = ubn;
+    sV[t] = vbn;
+    __syncthreads();
+    if (!pin) return;
+    const double g2 = d.p.gamma2;
+    // phase 1: tangential components from the first interior row / column
+    {
+      const int i0t = b.ew_periodic ? b.istrU : is, i1t = b.ew_periodic ? ie : b.iendR;
+      if (b.south_edge && j == js - 1 && i >= i0t && i <= i1t) {
+        ubn = g2 * sU[t + kBX] * F.umask[ij];
+        F.ubar[ij + kn] = ubn;
+      }
+      if (b.north_edge && j == je + 1 && i >= i0t && i <= i1t) {
+        ubn = g2 * sU[t - kBX] * F.umask[ij];
+        F.ubar[ij + kn] = ubn;
+      }
+      const int j0t = b.ns_periodic ? b.jstrV : js, j1t = b.ns_periodic ? je : b.jendR;
+      if (b.west_edge && i == is - 1 && j >= j0t && j <= j1t) {
+        vbn = g2 * sV[t + 1] * F.vmask[ij];
+        F.vbar[ij + kn] = vbn;
+      }
+      if (b.east_edge && i == ie + 1 && j >= j0t && j <= j1t) {
+        vbn = g2 * sV[t - 1] * F.vmask[ij];
+        F.vbar[ij + kn] = vbn;
+      }
+    }
+    // phase 3: fast-time-averaged fluxes through the boundary faces; Dnew of
+    // a window cell is Dn (computed) or h + zeta_new (set by zetabc)
+    auto Dn = [&](int qq, int gg) { return T.st[qq] == 1 ? T.Dn[qq] : T.h[gg] + T.zn[qq]; };
+    const double cff1 = 0.5 * c.w1;
+    const long sj = b.nx2;
+    bool du = false, dv = false;
+    if (b.west_edge && i == b.istrU - 1 && j >= b.jstrR && j <= b.jendR) du = true;
+    if (b.east_edge && i == ie + 1 && j >= b.jstrR && j <= b.jendR) du = true;
+    if (b.south_edge && j == js - 1 && i >= b.istrU && i <= ie) du = true;
+    if (b.north_edge && j == je + 1 && i >= b.istrU && i <= ie) du = true;
+    if (b.west_edge && i == is - 1 && j >= b.jstrV && j <= je) dv = true;
+    if (b.east_edge && i == ie + 1 && j >= b.jstrV && j <= je) dv = true;
+    if (b.south_edge && j == b.jstrV - 1 && i >= b.istrR && i <= b.iendR) dv = true;
+    if (b.north_edge && j == je + 1 && i >= b.istrR && i <= b.iendR) dv = true;
+    if (du) F.DU_avg1[ij] = F.DU_avg1[ij] + cff1 * (Dn(q, g) + Dn(q - 1, g - 1)) * (ubn) * F.dn_u[ij];
+    if (dv) F.DV_avg1[ij] = F.DV_avg1[ij] + cff1 * (Dn(q, g) + Dn(q - kFX, g - kGX)) * (vbn) * F.dm_v[ij];
+    (void)sj;
   }
 }
 
@@ -780,6 +849,13 @@ void launch_step2d(const Dev& d, hipStream_t s, const Tlev& t, const double* w1,
   c.w2 = w2[t.iif - 1];
   const bool closed = b.west_edge || b.east_edge || b.south_edge || b.north_edge;
   Range RB{b.istrR, b.iendR, b.jstrR, b.jendR};
+  // closed walls folded into k_s2d_fb when no edge is open and every edge
+  // row / column shares its tile with the interior row / column beside it
+  // (tiles start at istrR / jstrR; ROMS_GPU_S2D_EDGES=1 keeps k_s2d_edges)
+  const bool fold = closed && !d.p.obc && !d.p.s2d_split && d.p.s2d_fold &&
+                    (!b.east_edge || (b.iendR - b.istrR) % kBX != 0) &&
+                    (!b.north_edge || (b.jendR - b.jstrR) % kBY != 0);
+  const int cmode = !closed ? 0 : (fold ? 2 : 1);
   Halo* H = const_cast<Halo*>(d.halo);   // multi-rank exchange state (host bookkeeping)
   // single rank (no halo exchange object) with the fused kernel: periodic
   // halos of the fast-time fields are read through their images
@@ -796,9 +872,9 @@ void launch_step2d(const Dev& d, hipStream_t s, const Tlev& t, const double* w1,
   } else {
     auto fb = [&](int part) {
       if (d.p.npip > 0)
-        hipLaunchKernelGGL(k_s2d_fb<true>, grid_of(RB), dim3(kBX, kBY), 0, s, d, RB, c, (int)closed, vwrap, part);
+        hipLaunchKernelGGL(k_s2d_fb<true>, grid_of(RB), dim3(kBX, kBY), 0, s, d, RB, c, cmode, vwrap, part);
       else
-        hipLaunchKernelGGL(k_s2d_fb<false>, grid_of(RB), dim3(kBX, kBY), 0, s, d, RB, c, (int)closed, vwrap, part);
+        hipLaunchKernelGGL(k_s2d_fb<false>, grid_of(RB), dim3(kBX, kBY), 0, s, d, RB, c, cmode, vwrap, part);
     };
     // kernel-level timing: one interval per fast loop when nothing else runs
     // between the fused kernels (single rank, no closed edges), else one per launch
@@ -816,7 +892,7 @@ void launch_step2d(const Dev& d, hipStream_t s, const Tlev& t, const double* w1,
     if (!span) ktimer_mark(s, kTimedS2dFb, 1, 1);
     else if (t.iif == t.nfast) ktimer_mark(s, kTimedS2dFb, 1, t.nfast);
   }
-  if (closed) {
+  if (closed && !fold) {
     const int L = b.nx2 > b.Mm + 4 ? b.nx2 : b.Mm + 4;
     for (int ph = 0; ph < 4; ph++) {
       if (ph == 2 && !d.p.obc) continue;

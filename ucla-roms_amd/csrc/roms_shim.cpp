@@ -387,6 +387,42 @@ void enqueue_step(roms_tlev* t, bool rho_current) {
 extern "C" {
 
 int roms_gpu_abi_version(void) { return ROMS_GPU_ABI_VERSION; }
+
+// The zero fill of a new array must land before the library's stream reads
+// it (dev_alloc): `chunks` arrays of n doubles are filled with ones on the
+// library stream and freed, then allocated again one by one through
+// dev_alloc (the runtime recycles the memory, as it does between models of
+// one process) and each counted on the library stream at once for elements
+// that are not zero.  0 unless the fill and the stream race.
+int roms_gpu_selftest_zero_fill(long n, int chunks, long* nonzero) {
+  REQUIRE_INIT();
+  if (n < 1 || chunks < 1 || chunks > 1024 || !nonzero) { g.err = "roms_gpu_selftest_zero_fill: bad argument"; return -1; }
+  std::vector<double*> a((size_t)chunks, nullptr);
+  for (double*& p : a) {
+    CHECK_HIP(hipMalloc(&p, (size_t)n * sizeof(double)));
+    launch_fill_ones(p, n, g.s);
+  }
+  CHECK_HIP(hipStreamSynchronize(g.s));
+  for (double* p : a) CHECK_HIP(hipFree(p));
+  unsigned long long* cnt = nullptr;
+  CHECK_HIP(hipMalloc(&cnt, sizeof(unsigned long long)));
+  CHECK_HIP(hipMemsetAsync(cnt, 0, sizeof(unsigned long long), g.s));
+  for (double*& p : a) {
+    CHECK_HIP(dev_alloc(p, n));
+    launch_count_nonzero(p, n, cnt, g.s);
+  }
+  unsigned long long h = 0;
+  CHECK_HIP(hipMemcpyAsync(&h, cnt, sizeof(h), hipMemcpyDeviceToHost, g.s));
+  CHECK_HIP(hipStreamSynchronize(g.s));
+  const long G = g.guard ? 4096 : 0;
+  for (double* p : a) {
+    CHECK_HIP(hipFree(G ? g.guard_base[p] : p));
+    if (G) g.guard_base.erase(p);
+  }
+  (void)hipFree(cnt);
+  *nonzero = (long)h;
+  return 0;
+}
 const char* roms_gpu_last_error(void) { return g.err.c_str(); }
 void* roms_gpu_stream(void) { return (void*)g.s; }
 
@@ -500,6 +536,10 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
   {
     const char* e = getenv("ROMS_GPU_SEG_XG");
     if (e && atoi(e) > 0) P.seg_xg = atoi(e);
+  }
+  {
+    const char* e = getenv("ROMS_GPU_S2D_EDGES");
+    P.s2d_fold = !(e && e[0] == '1');
   }
   {
     const char* e = getenv("ROMS_GPU_HOIST");

@@ -511,6 +511,15 @@ class Model:
                                                ctypes.byref(n)), "time_routine")
         return ms.value, n.value
 
+    def selftest_zero_fill(self, n, chunks=1):
+        """roms_gpu_selftest_zero_fill: nonzero elements that fresh zero-filled
+        allocations (chunks x n doubles, recycled memory) show to the
+        library's stream (0 expected)."""
+        nz = ctypes.c_long()
+        self._chk(self.L.roms_gpu_selftest_zero_fill(ctypes.c_long(n), ctypes.c_int(chunks), ctypes.byref(nz)),
+                  "selftest_zero_fill")
+        return nz.value
+
     def halo_transport(self):
         """'ipc', 'rccl' (or single rank / in-process), or 'ipc-timeout'."""
         r = self.L.roms_gpu_halo_transport()
