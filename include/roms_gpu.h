@@ -265,10 +265,12 @@ int roms_gpu_comm_destroy(void *comm);
 int roms_gpu_halo_transport(void);
 /* Self-test of the allocation path: `chunks` arrays of n doubles filled
  * with ones and freed, then allocated again through the library's
- * zero-filling allocator and each counted on the library's stream at once;
- * *nonzero = elements that are not zero (0 unless the null-stream fill races
- * the library's non-blocking stream, the round-2 failure mode).             */
-int roms_gpu_selftest_zero_fill(long n, int chunks, long *nonzero);
+ * zero-filling allocator; on the library's stream each is read at once
+ * (elements not zero: stale data) and overwritten with ones, and after the
+ * device drains the elements not one are counted (writes undone by a late
+ * fill).  *bad = both counts (0 unless the null-stream fill races the
+ * library's non-blocking stream, the round-2 failure mode).                 */
+int roms_gpu_selftest_zero_fill(long n, int chunks, long *bad);
 /* Host-only: neighbour ranks (-1 none), per-level message sizes for the 8
  * directions W,E,S,N,SW,SE,NW,NE, and the strip extents {i0,i1,j0,j1}.      */
 int roms_gpu_halo_plan(int Lm, int Mm, int np_xi, int np_eta, int inode, int jnode, int ew_periodic,

@@ -241,6 +241,27 @@ def test_rho_eos_reuse_bitwise_and_invalidated(graphs, monkeypatch):
         assert np.array_equal(a[n], b[n]), n
 
 
+def test_s2d_edges_folded_bitwise(monkeypatch):
+    """The closed-wall edge phases of the fast step run inside k_s2d_fb
+    (default) or as the separate k_s2d_edges launches (ROMS_GPU_S2D_EDGES=1,
+    u2dbc/v2dbc and the boundary flux averages of step2d_FB.F:444-529): the
+    runs are bitwise equal, on a grid whose last tile row / column holds more
+    than the edge cell (folded) and on one where the host must fall back."""
+    for LLm, MMm in ((40, 26), (63, 27)):
+        cfg = basin_cfg(LLm=LLm, MMm=MMm, N=12, nonlin=True)
+        out = []
+        for env in ("1", "0"):
+            monkeypatch.setenv("ROMS_GPU_S2D_EDGES", env)
+            m = romsgpu.Model.from_case(cfg.case_id, cfg.LLm, cfg.MMm, cfg.N, cfg.NT, salinity=bool(cfg.salinity),
+                                        nonlin_eos=True, dt=cfg.dt, ndtfast=cfg.ndtfast, sizex=cfg.sizex,
+                                        sizey=cfg.sizey)
+            m.step(4)
+            out.append({n: m.get(n) for n in ("zeta", "ubar", "vbar", "u", "v", "t", "DU_avg1", "DV_avg1")})
+            m.close()
+        for n in out[0]:
+            assert np.array_equal(out[0][n], out[1][n]), (LLm, MMm, n)
+
+
 def test_diag_blowup_flag_is_fatal():
     """A non-finite norm is diag.F's 'Abnormal termination: BLOWUP'
     (diag.F:621-633): roms_gpu_diag fails instead of printing NaN."""

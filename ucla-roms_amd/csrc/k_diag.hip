@@ -216,9 +216,9 @@ void launch_diag(const Dev& d, hipStream_t s, const Tlev& t, double* out) {
 // ---- library self-test (roms_gpu_selftest_zero_fill): how many of n doubles
 // are not +0.0, counted on stream s (vector atomics) ----
 __global__ void __launch_bounds__(256) k_count_nonzero(const double* __restrict__ p, long n,
-                                                       unsigned long long* __restrict__ cnt) {
+                                                       unsigned long long* __restrict__ cnt, double v) {
   unsigned long long c = 0;
-  for (long q = blockIdx.x * 256L + threadIdx.x; q < n; q += (long)gridDim.x * 256L) c += p[q] != 0.0;
+  for (long q = blockIdx.x * 256L + threadIdx.x; q < n; q += (long)gridDim.x * 256L) c += p[q] != v;
   if (c) atomicAdd(cnt, c);
 }
 __global__ void __launch_bounds__(256) k_fill_ones(double* __restrict__ p, long n) {
@@ -227,7 +227,7 @@ __global__ void __launch_bounds__(256) k_fill_ones(double* __restrict__ p, long 
 void launch_fill_ones(double* p, long n, hipStream_t s) {
   hipLaunchKernelGGL(k_fill_ones, dim3(2048), dim3(256), 0, s, p, n);
 }
-void launch_count_nonzero(const double* p, long n, unsigned long long* cnt, hipStream_t s) {
-  hipLaunchKernelGGL(k_count_nonzero, dim3(2048), dim3(256), 0, s, p, n, cnt);
+void launch_count_nonzero(const double* p, long n, unsigned long long* cnt, hipStream_t s, double v) {
+  hipLaunchKernelGGL(k_count_nonzero, dim3(2048), dim3(256), 0, s, p, n, cnt, v);
 }
 }  // namespace roms

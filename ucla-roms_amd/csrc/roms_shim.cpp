@@ -388,15 +388,18 @@ extern "C" {
 
 int roms_gpu_abi_version(void) { return ROMS_GPU_ABI_VERSION; }
 
-// The zero fill of a new array must land before the library's stream reads
+// The zero fill of a new array must land before the library's stream uses
 // it (dev_alloc): `chunks` arrays of n doubles are filled with ones on the
 // library stream and freed, then allocated again one by one through
-// dev_alloc (the runtime recycles the memory, as it does between models of
-// one process) and each counted on the library stream at once for elements
-// that are not zero.  0 unless the fill and the stream race.
-int roms_gpu_selftest_zero_fill(long n, int chunks, long* nonzero) {
+// dev_alloc (recycled memory, as between models of one process); on the
+// library stream at once each is counted for elements that are not zero
+// (a fill that lands late: stale data read) and then overwritten with ones;
+// after the whole device has drained, the elements that are not one are
+// counted (a fill that lands late: the stream's writes zeroed).  The sum of
+// both counts is 0 unless the fill and the stream race.
+int roms_gpu_selftest_zero_fill(long n, int chunks, long* bad) {
   REQUIRE_INIT();
-  if (n < 1 || chunks < 1 || chunks > 1024 || !nonzero) { g.err = "roms_gpu_selftest_zero_fill: bad argument"; return -1; }
+  if (n < 1 || chunks < 1 || chunks > 1024 || !bad) { g.err = "roms_gpu_selftest_zero_fill: bad argument"; return -1; }
   std::vector<double*> a((size_t)chunks, nullptr);
   for (double*& p : a) {
     CHECK_HIP(hipMalloc(&p, (size_t)n * sizeof(double)));
@@ -405,14 +408,18 @@ int roms_gpu_selftest_zero_fill(long n, int chunks, long* nonzero) {
   CHECK_HIP(hipStreamSynchronize(g.s));
   for (double* p : a) CHECK_HIP(hipFree(p));
   unsigned long long* cnt = nullptr;
-  CHECK_HIP(hipMalloc(&cnt, sizeof(unsigned long long)));
-  CHECK_HIP(hipMemsetAsync(cnt, 0, sizeof(unsigned long long), g.s));
+  CHECK_HIP(hipMalloc(&cnt, 2 * sizeof(unsigned long long)));
+  CHECK_HIP(hipMemsetAsync(cnt, 0, 2 * sizeof(unsigned long long), g.s));
+  CHECK_HIP(hipStreamSynchronize(g.s));
   for (double*& p : a) {
     CHECK_HIP(dev_alloc(p, n));
-    launch_count_nonzero(p, n, cnt, g.s);
+    launch_count_nonzero(p, n, cnt, g.s, 0.0);
+    launch_fill_ones(p, n, g.s);
   }
-  unsigned long long h = 0;
-  CHECK_HIP(hipMemcpyAsync(&h, cnt, sizeof(h), hipMemcpyDeviceToHost, g.s));
+  CHECK_HIP(hipDeviceSynchronize());
+  for (double* p : a) launch_count_nonzero(p, n, cnt + 1, g.s, 1.0);
+  unsigned long long h[2] = {0, 0};
+  CHECK_HIP(hipMemcpyAsync(h, cnt, sizeof(h), hipMemcpyDeviceToHost, g.s));
   CHECK_HIP(hipStreamSynchronize(g.s));
   const long G = g.guard ? 4096 : 0;
   for (double* p : a) {
@@ -420,7 +427,7 @@ int roms_gpu_selftest_zero_fill(long n, int chunks, long* nonzero) {
     if (G) g.guard_base.erase(p);
   }
   (void)hipFree(cnt);
-  *nonzero = (long)h;
+  *bad = (long)(h[0] + h[1]);
   return 0;
 }
 const char* roms_gpu_last_error(void) { return g.err.c_str(); }

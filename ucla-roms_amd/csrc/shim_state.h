@@ -30,7 +30,7 @@ inline hipError_t copy_on(void* dst, const void* src, size_t bytes, hipMemcpyKin
   return e != hipSuccess ? e : hipStreamSynchronize(s);
 }   // rst_io.hip: joins the writer, frees staging (roms_gpu_finalize)
 void launch_fill_ones(double* p, long n, hipStream_t s);                               // k_diag.hip (self-test)
-void launch_count_nonzero(const double* p, long n, unsigned long long* cnt, hipStream_t s);
+void launch_count_nonzero(const double* p, long n, unsigned long long* cnt, hipStream_t s, double v = 0.0);   // elements != v
 void frc_free();  // k_forcing.hip: forcing records and tide data (roms_gpu_finalize)
 // In-step forcing (roms_gpu_frc_clock, k_forcing.hip): the set_forces /
 // set_bry_all / set_tides points of roms_step run inside roms_gpu_step.
