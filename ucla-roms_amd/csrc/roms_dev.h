@@ -203,7 +203,10 @@ constexpr int kSegBlock = ((kSegMaxS * kSegCW + 63) / 64) * 64;   // threads of 
 // The momentum solvers' blocks may hold several rows j (blockDim.z) of the
 // same 16 columns, so the v columns' j-1, j-2, j+1 stencil rows are loaded
 // by the neighbouring rows' waves of the same block, close together in time.
-constexpr int kSegJMax = 4;
+#ifndef ROMS_SEG_JMAX
+#define ROMS_SEG_JMAX 4
+#endif
+constexpr int kSegJMax = ROMS_SEG_JMAX;
 inline dim3 gridc_of(const Range& r) {
   int ni = r.i1 - r.i0 + 1, nj = r.j1 - r.j0 + 1;
   if (ni < 1) ni = 1;

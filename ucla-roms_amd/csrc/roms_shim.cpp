@@ -552,7 +552,7 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     const char* e = getenv("ROMS_GPU_HOIST");
     P.hoist = !(e && e[0] == '0');
   }
-  P.seg_jrows = 2;
+  P.seg_jrows = kSegJMax < 2 ? kSegJMax : 2;
   {
     const char* e = getenv("ROMS_GPU_SEG_JROWS");
     if (e && atoi(e) >= 1 && atoi(e) <= kSegJMax) P.seg_jrows = atoi(e);
