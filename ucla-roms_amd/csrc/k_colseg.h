@@ -290,7 +290,7 @@ __device__ __forceinline__ void tracer_spline_seg(const SegSpan& sg, int N, long
 }
 
 // Block prologue of the momentum column kernels: grid z = direction (0: u at
-// i >= istrU, 1: v at j >= jstrV), 16 columns x blockDim.z rows j per block.
+// i >= istrU, 1: v at j >= jstrV), kSegCW columns x blockDim.z rows j per block.
 // Lanes outside the column range (i or j) solve a clamped duplicate column
 // (they take part in the barriers) and store nothing.
 struct SegCol {

@@ -504,7 +504,7 @@ __global__ void __launch_bounds__(64) k_pre_uv(Dev d, Range R, PreCoef c, int ns
 }
 
 // ---- segment-partitioned variants (k_colseg.h) for deep grids: block =
-// 16 columns x S segments.  The spline reconstruction and the implicit
+// kSegCW columns x S segments.  The spline reconstruction and the implicit
 // diffusion / viscosity are each one partitioned tridiagonal system whose
 // rows are those of k_pre_tracer_v / pre_uv_col (pre_step3d4S.F:198-489). ----
 __global__ void __launch_bounds__(kSegBlock, 2) k_pre_tracer_seg(Dev d, Range R, PreCoef c, int nnew, int nrhs) {

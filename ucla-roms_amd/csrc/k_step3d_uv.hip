@@ -239,7 +239,7 @@ __global__ void __launch_bounds__(64, 2) k_uv1_reg(Dev d, Range R, int nnew, int
 }
 
 // ---- segment-partitioned variant of k_uv1 (k_colseg.h) for deep grids:
-// block = 16 columns x S segments, grid z = direction.  Spline advection and
+// block = kSegCW columns x S segments, grid z = direction.  Spline advection and
 // the implicit viscosity are each one partitioned tridiagonal system with the
 // rows of uv1_col; the final ru(k) of every level go to LDS, from where the
 // first segment forms rufrc/rvfrc in the reference's k = 1..N order. ----

@@ -196,15 +196,15 @@ constexpr int kCX = 64;
 constexpr int kSegRows = ROMS_SEG_ROWS;   // cells per segment (register arrays of kSegRows + 2)
 constexpr int kSegMaxS = ROMS_SEG_MAXS;   // segments per block (kSegCW columns each): N <= kSegRows * kSegMaxS
 #ifndef ROMS_SEG_CW
-#define ROMS_SEG_CW 16
+#define ROMS_SEG_CW 64   // round 3: 64-wide blocks (one segment per wavefront) 1-2% faster at C3 than 16 (r3_l_seg_shape_ab.txt)
 #endif
 constexpr int kSegCW = ROMS_SEG_CW;       // columns per segment-solver block (lanes of one segment)
 constexpr int kSegBlock = ((kSegMaxS * kSegCW + 63) / 64) * 64;   // threads of a segment-solver block (max)
 // The momentum solvers' blocks may hold several rows j (blockDim.z) of the
-// same 16 columns, so the v columns' j-1, j-2, j+1 stencil rows are loaded
+// same kSegCW columns, so the v columns' j-1, j-2, j+1 stencil rows are loaded
 // by the neighbouring rows' waves of the same block, close together in time.
 #ifndef ROMS_SEG_JMAX
-#define ROMS_SEG_JMAX 4
+#define ROMS_SEG_JMAX (ROMS_SEG_CW >= 64 ? 1 : 4)
 #endif
 constexpr int kSegJMax = ROMS_SEG_JMAX;
 inline dim3 gridc_of(const Range& r) {
