@@ -64,28 +64,29 @@ __global__ void __launch_bounds__(256) k_pre_tracer_h(Dev d, Range R, PreCoef c,
 // for memory once instead of once per phase.  The per-phase form above waits
 // 2 + 2 NT times and, with ~7 blocks per CU, was bound by those round trips,
 // not by bandwidth.  Same expressions in the same order: bit-identical. ----
-template <int NTT>
+template <int NTT, int TY>
 struct TracerWinN {
-  double UM[kUVN], VM[kUVN], FU[kUVN], FV[kUVN], T[NTT][kUVN];
+  static constexpr int kN = kUVW * (TY + 4);
+  double UM[kN], VM[kN], FU[kN], FV[kN], T[NTT][kN];
 };
-template <int NTT>
-__global__ void __launch_bounds__(256) k_pre_tracer_h1(Dev d, Range R, PreCoef c, int nstp, int nnew, int nrhs) {
+template <int NTT, int TY>
+__global__ void __launch_bounds__(kBX * TY) k_pre_tracer_h1(Dev d, Range R, PreCoef c, int nstp, int nnew, int nrhs) {
   const uint3 bI = xcd_tile();
-  __shared__ TracerWinN<NTT> W;
+  __shared__ TracerWinN<NTT, TY> W;
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const int k = 1 + (int)bI.z, indx = 3 - nstp;
-  const int i0 = R.i0 + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * kBY;
+  const int i0 = R.i0 + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * TY;
   const int ib = i0 - 2, jb = j0 - 2;
   const long kk = (long)(k - 1) * b.n2, n2 = b.n2;
   const int tid = threadIdx.x + kBX * threadIdx.y;
-  constexpr int NR = (kUVN + kBX * kBY - 1) / (kBX * kBY);
+  constexpr int NW = kUVW * (TY + 4), NR = (NW + kBX * TY - 1) / (kBX * TY);
   double wUM[NR], wVM[NR], wFU[NR], wFV[NR], wT[NTT][NR];
 #pragma unroll
   for (int r = 0; r < NR; r++) {
-    const int q = tid + r * kBX * kBY;
+    const int q = tid + r * kBX * TY;
     const int i = ib + q % kUVW, j = jb + q / kUVW;
-    const bool ok = q < kUVN && i >= -1 && i <= b.Lm + 2 && j >= -1 && j <= b.Mm + 2;
+    const bool ok = q < NW && i >= -1 && i <= b.Lm + 2 && j >= -1 && j <= b.Mm + 2;
     const long o = ok ? IJ(b, i, j) : 0;
     wUM[r] = ok ? F.umask[o] : 0.0;
     wVM[r] = ok ? F.vmask[o] : 0.0;
@@ -112,8 +113,8 @@ __global__ void __launch_bounds__(256) k_pre_tracer_h1(Dev d, Range R, PreCoef c
   }
 #pragma unroll
   for (int r = 0; r < NR; r++) {
-    const int q = tid + r * kBX * kBY;
-    if (q < kUVN) {
+    const int q = tid + r * kBX * TY;
+    if (q < NW) {
       W.UM[q] = wUM[r]; W.VM[q] = wVM[r]; W.FU[q] = wFU[r]; W.FV[q] = wFV[r];
 #pragma unroll
       for (int t = 0; t < NTT; t++) W.T[t][q] = wT[t][r];
@@ -302,31 +303,49 @@ __global__ void __launch_bounds__(256) k_uv_horiz(Dev d, Range R, int nrhs, UVBo
   const double* FV = F.FlxV + kk;
   const int i = i0 + (int)threadIdx.x, j = j0 + (int)threadIdx.y;
   const bool act = i <= R.i1 && j <= R.j1;
-  if (!d.p.hoist || d.p.curvgrid) {
-    for (int q = threadIdx.x + kBX * threadIdx.y; q < kUVN; q += kBX * kBY) {
-      const int ii = ib + q % kUVW, jj = jb + q / kUVW;
-      if (ii < -1 || ii > b.Lm + 2 || jj < -1 || jj > b.Mm + 2) continue;  // never read
-      const long o = IJ(b, ii, jj);
-      sU[q] = U[o];
-      sV[q] = V[o];
-      sFU[q] = FU[o];
-      sFV[q] = FV[o];
-    }
-    __syncthreads();
-    if (!act) return;
-    const AccL a{sU, sV, sFU, sFV, ib, jb};
-    uv_horiz_rhs(d, a, i, j, k, ub, up != 0);
-    return;
+  for (int q = threadIdx.x + kBX * threadIdx.y; q < kUVN; q += kBX * kBY) {
+    const int ii = ib + q % kUVW, jj = jb + q / kUVW;
+    if (ii < -1 || ii > b.Lm + 2 || jj < -1 || jj > b.Mm + 2) continue;  // never read
+    const long o = IJ(b, ii, jj);
+    sU[q] = U[o];
+    sV[q] = V[o];
+    sFU[q] = FU[o];
+    sFV[q] = FV[o];
   }
-  // window and the lane's own inputs loaded together (one memory wait)
+  __syncthreads();
+  if (!act) return;
+  const AccL a{sU, sV, sFU, sFV, ib, jb};
+  uv_horiz_rhs(d, a, i, j, k, ub, up != 0);
+}
+
+// The same without CURVGRID with every global load issued at block entry
+// (the window and the lane's own ru, rv, Hz, fomn): one memory wait per
+// block.  Bit-identical.
+template <int TY>
+__global__ void __launch_bounds__(kBX * TY) k_uv_horiz1(Dev d, Range R, int nrhs, UVBounds ub, int up) {
+  const uint3 bI = xcd_tile();
+  constexpr int NW = kUVW * (TY + 4);
+  __shared__ double sU[NW], sV[NW], sFU[NW], sFV[NW];
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const int k = 1 + (int)bI.z;
+  const int i0 = R.i0 + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * TY;
+  const int ib = i0 - 2, jb = j0 - 2;
+  const long kk = (long)(k - 1) * b.n2;
+  const double* U = F.u + (long)(nrhs - 1) * b.n3 + kk;
+  const double* V = F.v + (long)(nrhs - 1) * b.n3 + kk;
+  const double* FU = F.FlxU + kk;
+  const double* FV = F.FlxV + kk;
+  const int i = i0 + (int)threadIdx.x, j = j0 + (int)threadIdx.y;
+  const bool act = i <= R.i1 && j <= R.j1;
   const int tid = threadIdx.x + kBX * threadIdx.y;
-  constexpr int NR = (kUVN + kBX * kBY - 1) / (kBX * kBY);
+  constexpr int NR = (NW + kBX * TY - 1) / (kBX * TY);
   double wU[NR], wV[NR], wFU[NR], wFV[NR];
 #pragma unroll
   for (int r = 0; r < NR; r++) {
-    const int q = tid + r * kBX * kBY;
+    const int q = tid + r * kBX * TY;
     const int ii = ib + q % kUVW, jj = jb + q / kUVW;
-    const bool ok = q < kUVN && ii >= -1 && ii <= b.Lm + 2 && jj >= -1 && jj <= b.Mm + 2;
+    const bool ok = q < NW && ii >= -1 && ii <= b.Lm + 2 && jj >= -1 && jj <= b.Mm + 2;
     const long o = ok ? IJ(b, ii, jj) : 0;
     wU[r] = ok ? U[o] : 0.0;
     wV[r] = ok ? V[o] : 0.0;
@@ -343,8 +362,8 @@ __global__ void __launch_bounds__(256) k_uv_horiz(Dev d, Range R, int nrhs, UVBo
   }
 #pragma unroll
   for (int r = 0; r < NR; r++) {
-    const int q = tid + r * kBX * kBY;
-    if (q < kUVN) { sU[q] = wU[r]; sV[q] = wV[r]; sFU[q] = wFU[r]; sFV[q] = wFV[r]; }
+    const int q = tid + r * kBX * TY;
+    if (q < NW) { sU[q] = wU[r]; sV[q] = wV[r]; sFU[q] = wFU[r]; sFV[q] = wFV[r]; }
   }
   __syncthreads();
   if (!act) return;
@@ -352,11 +371,18 @@ __global__ void __launch_bounds__(256) k_uv_horiz(Dev d, Range R, int nrhs, UVBo
   uv_horiz_rhs_pre(d, a, i, j, o, p, ub, up != 0);
 }
 
+
 void launch_uv_horiz(const Dev& d, hipStream_t s, int nrhs, int up) {
   const Bounds& b = d.b;
   if (!d.p.uv_cor && !d.p.uv_adv) return;   // compute_horiz_rhs_uv_terms.h adds nothing
   Range R{b.istr, b.iend, b.jstr, b.jend};
-  hipLaunchKernelGGL(k_uv_horiz, grid3_of(R, b.N), dim3(kBX, kBY), 0, s, d, R, nrhs, uv_bounds(b), up);
+  const UVBounds ub = uv_bounds(b);
+  if (!d.p.hoist || d.p.curvgrid)
+    hipLaunchKernelGGL(k_uv_horiz, grid3_of(R, b.N), dim3(kBX, kBY), 0, s, d, R, nrhs, ub, up);
+  else if (d.p.h_ty == 8)
+    hipLaunchKernelGGL(k_uv_horiz1<8>, grid3_ty(R, b.N, 8), dim3(kBX, 8), 0, s, d, R, nrhs, ub, up);
+  else
+    hipLaunchKernelGGL(k_uv_horiz1<4>, grid3_ty(R, b.N, 4), dim3(kBX, 4), 0, s, d, R, nrhs, ub, up);
 }
 
 // ---- bottom drag r_D (compute_rd_bott_drag.h), log-layer with Zob ----
@@ -695,10 +721,12 @@ void launch_pre_step3d(const Dev& d, hipStream_t s, const Tlev& t) {
   else { c.dtau = d.p.dt * (1.0 - AM3_crv); c.cf_stp = 0.5 + AM3_crv; c.cf_bak = 0.5 - AM3_crv; }
   Range RI{b.istr, b.iend, b.jstr, b.jend};
   Range RH{b.istr - 1, b.iend, b.jstr - 1, b.jend};
-  if (d.p.hoist && b.NT == 2)
-    hipLaunchKernelGGL(k_pre_tracer_h1<2>, grid3_of(RH, b.N), dim3(kBX, kBY), 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs);
+  if (d.p.hoist && b.NT == 2 && d.p.h_ty == 8)
+    hipLaunchKernelGGL((k_pre_tracer_h1<2, 8>), grid3_ty(RH, b.N, 8), dim3(kBX, 8), 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs);
+  else if (d.p.hoist && b.NT == 2)
+    hipLaunchKernelGGL((k_pre_tracer_h1<2, 4>), grid3_ty(RH, b.N, 4), dim3(kBX, 4), 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs);
   else if (d.p.hoist && b.NT == 1)
-    hipLaunchKernelGGL(k_pre_tracer_h1<1>, grid3_of(RH, b.N), dim3(kBX, kBY), 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs);
+    hipLaunchKernelGGL((k_pre_tracer_h1<1, 4>), grid3_ty(RH, b.N, 4), dim3(kBX, 4), 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs);
   else
     hipLaunchKernelGGL(k_pre_tracer_h, grid3_of(RH, b.N), dim3(kBX, kBY), 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs);
   dim3 gt = gridc_of(RI);

@@ -41,28 +41,29 @@ __global__ void __launch_bounds__(256) k_step3d_t_h(Dev d, Range R, int nnew, in
 
 // The same for NTT <= 2 tracers with every global load issued at entry (see
 // k_pre_tracer_h1): one memory wait per block.  Bit-identical.
-template <int NTT>
+template <int NTT, int TY>
 struct TracerWinS {
-  double UM[kUVN], VM[kUVN], FU[kUVN], FV[kUVN], T[NTT][kUVN];
+  static constexpr int kN = kUVW * (TY + 4);
+  double UM[kN], VM[kN], FU[kN], FV[kN], T[NTT][kN];
 };
-template <int NTT>
-__global__ void __launch_bounds__(256) k_step3d_t_h1(Dev d, Range R, int nnew, int nrhs) {
+template <int NTT, int TY>
+__global__ void __launch_bounds__(kBX * TY) k_step3d_t_h1(Dev d, Range R, int nnew, int nrhs) {
   const uint3 bI = xcd_tile();
-  __shared__ TracerWinS<NTT> W;
+  __shared__ TracerWinS<NTT, TY> W;
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const int k = 1 + (int)bI.z;
-  const int i0 = R.i0 + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * kBY;
+  const int i0 = R.i0 + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * TY;
   const int ib = i0 - 2, jb = j0 - 2;
   const long kk = (long)(k - 1) * b.n2;
   const int tid = threadIdx.x + kBX * threadIdx.y;
-  constexpr int NR = (kUVN + kBX * kBY - 1) / (kBX * kBY);
+  constexpr int NW = kUVW * (TY + 4), NR = (NW + kBX * TY - 1) / (kBX * TY);
   double wUM[NR], wVM[NR], wFU[NR], wFV[NR], wT[NTT][NR];
 #pragma unroll
   for (int r = 0; r < NR; r++) {
-    const int q = tid + r * kBX * kBY;
+    const int q = tid + r * kBX * TY;
     const int i = ib + q % kUVW, j = jb + q / kUVW;
-    const bool ok = q < kUVN && i >= -1 && i <= b.Lm + 2 && j >= -1 && j <= b.Mm + 2;
+    const bool ok = q < NW && i >= -1 && i <= b.Lm + 2 && j >= -1 && j <= b.Mm + 2;
     const long o = ok ? IJ(b, i, j) : 0;
     wUM[r] = ok ? F.umask[o] : 0.0;
     wVM[r] = ok ? F.vmask[o] : 0.0;
@@ -81,8 +82,8 @@ __global__ void __launch_bounds__(256) k_step3d_t_h1(Dev d, Range R, int nnew, i
   for (int t = 0; t < NTT; t++) tn[t] = F.t[(long)(nnew - 1) * b.n3 + (long)t * 3 * b.n3 + o];
 #pragma unroll
   for (int r = 0; r < NR; r++) {
-    const int q = tid + r * kBX * kBY;
-    if (q < kUVN) {
+    const int q = tid + r * kBX * TY;
+    if (q < NW) {
       W.UM[q] = wUM[r]; W.VM[q] = wVM[r]; W.FU[q] = wFU[r]; W.FV[q] = wFV[r];
 #pragma unroll
       for (int t = 0; t < NTT; t++) W.T[t][q] = wT[t][r];
@@ -365,10 +366,12 @@ void launch_step3d_t(const Dev& d, hipStream_t s, const Tlev& t) {
   Range R{b.istr, b.iend, b.jstr, b.jend};
   // horizontal fluxes, then the column solves, on a sub-range of the interior
   auto run = [&](const Range& r) {
-    if (d.p.hoist && b.NT == 2)
-      hipLaunchKernelGGL(k_step3d_t_h1<2>, grid3_of(r, b.N), dim3(kBX, kBY), 0, s, d, r, t.nnew, t.nrhs);
+    if (d.p.hoist && b.NT == 2 && d.p.h_ty == 8)
+      hipLaunchKernelGGL((k_step3d_t_h1<2, 8>), grid3_ty(r, b.N, 8), dim3(kBX, 8), 0, s, d, r, t.nnew, t.nrhs);
+    else if (d.p.hoist && b.NT == 2)
+      hipLaunchKernelGGL((k_step3d_t_h1<2, 4>), grid3_ty(r, b.N, 4), dim3(kBX, 4), 0, s, d, r, t.nnew, t.nrhs);
     else if (d.p.hoist && b.NT == 1)
-      hipLaunchKernelGGL(k_step3d_t_h1<1>, grid3_of(r, b.N), dim3(kBX, kBY), 0, s, d, r, t.nnew, t.nrhs);
+      hipLaunchKernelGGL((k_step3d_t_h1<1, 4>), grid3_ty(r, b.N, 4), dim3(kBX, 4), 0, s, d, r, t.nnew, t.nrhs);
     else
       hipLaunchKernelGGL(k_step3d_t_h, grid3_of(r, b.N), dim3(kBX, kBY), 0, s, d, r, t.nnew, t.nrhs);
     dim3 gt = gridc_of(r);

@@ -44,7 +44,8 @@ struct Params {
   int seg_order;  // block order of the segment solvers (seg_tile; ROMS_GPU_SEG_ORDER)
   int seg_xg;     // x-blocks per group of seg_order 3 (ROMS_GPU_SEG_XG)
   int s2d_fold;   // closed-wall edges of the fast step inside k_s2d_fb (ROMS_GPU_S2D_EDGES=1: separate kernels)
-  int hoist;      // per-level horizontal kernels with every global load at entry (ROMS_GPU_HOIST=0: per-phase forms)
+  int hoist;
+  int h_ty;       // tile rows of the hoisted horizontal kernels: 4 or 8 (ROMS_GPU_HTY)      // per-level horizontal kernels with every global load at entry (ROMS_GPU_HOIST=0: per-phase forms)
   int seg_jrows;  // rows j per block of the momentum segment solvers (1..kSegJMax; ROMS_GPU_SEG_JROWS)
   int npip;       // pipe_frc.F: number of pipes (0: pipe_source off)
   int nriv, nrivf;  // river_frc.F: number of rivers (0: river_source off), river faces

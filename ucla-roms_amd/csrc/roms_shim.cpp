@@ -549,6 +549,10 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     P.s2d_fold = !(e && e[0] == '1');
   }
   {
+    const char* e = getenv("ROMS_GPU_HTY");
+    P.h_ty = (e && atoi(e) == 8) ? 8 : 4;
+  }
+  {
     const char* e = getenv("ROMS_GPU_HOIST");
     P.hoist = !(e && e[0] == '0');
   }
