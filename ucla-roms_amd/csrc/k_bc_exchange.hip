@@ -24,9 +24,11 @@ __global__ void __launch_bounds__(256) k_periodic_wrap(Bounds b, ExchList L) {
     i = p - r * b.nx2 - 1;
     j = r < 2 ? r - 1 : Mm - 1 + r;
   } else {
+    // the four halo columns of one row j are neighbouring threads, so each
+    // pair (-1,0) / (Lm+1,Lm+2) shares one line per access
     const int q = p - nrow;
-    const int c = q / Mm;
-    j = q - c * Mm + 1;
+    const int c = q & 3;
+    j = (q >> 2) + 1;
     i = c < 2 ? c - 1 : Lm - 1 + c;
   }
   const bool xh = i < 1 || i > Lm, yh = j < 1 || j > Mm;
