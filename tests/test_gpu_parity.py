@@ -262,6 +262,29 @@ def test_s2d_edges_folded_bitwise(monkeypatch):
             assert np.array_equal(out[0][n], out[1][n]), (LLm, MMm, n)
 
 
+@pytest.mark.parametrize("case", ["basin", "filament"])
+def test_prsgrd_uv_fused_bitwise(case, monkeypatch):
+    """Whole steps run the horizontal momentum r.h.s. of pre_step3d /
+    step3d_uv1 inside the prsgrd kernel before them (compute_horiz_rhs_uv_terms.h
+    on the same u, v, FlxU, FlxV, Hz; ru/rv stored once); ROMS_GPU_PRS_UV=0
+    keeps the two kernels.  Bitwise equal."""
+    if case == "basin":
+        cfg = basin_cfg(LLm=40, MMm=26, N=12, nonlin=True)
+    else:
+        cfg = oracle.filament_cfg(LLm=48, MMm=32, N=16, np_xi=1, np_eta=1)
+    out = []
+    for env in ("0", "1"):
+        monkeypatch.setenv("ROMS_GPU_PRS_UV", env)
+        m = romsgpu.Model.from_case(cfg.case_id, cfg.LLm, cfg.MMm, cfg.N, cfg.NT, salinity=bool(cfg.salinity),
+                                    nonlin_eos=bool(cfg.nonlin_eos), dt=cfg.dt, ndtfast=cfg.ndtfast,
+                                    sizex=cfg.sizex, sizey=cfg.sizey)
+        m.step(4)
+        out.append({n: m.get(n) for n in ("zeta", "ubar", "vbar", "u", "v", "t", "ru", "rv", "rufrc", "rvfrc")})
+        m.close()
+    for n in out[0]:
+        assert np.array_equal(out[0][n], out[1][n]), n
+
+
 def test_diag_blowup_flag_is_fatal():
     """A non-finite norm is diag.F's 'Abnormal termination: BLOWUP'
     (diag.F:621-633): roms_gpu_diag fails instead of printing NaN."""

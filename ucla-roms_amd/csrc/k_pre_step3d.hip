@@ -713,7 +713,7 @@ bool setup_column_kernels(int N) {
   return true;
 }
 
-void launch_pre_step3d(const Dev& d, hipStream_t s, const Tlev& t) {
+void launch_pre_step3d(const Dev& d, hipStream_t s, const Tlev& t, bool uv_done) {
   const Bounds& b = d.b;
   PreCoef c;
   const double AM3_crv = 1.0 / 6.0;
@@ -740,7 +740,7 @@ void launch_pre_step3d(const Dev& d, hipStream_t s, const Tlev& t) {
     hipLaunchKernelGGL(k_pre_tracer_v<ColGlb>, gt, dim3(kCX), 0, s, d, RI, c, t.nnew, t.nrhs);
   else
     hipLaunchKernelGGL(k_pre_tracer_v<ColLds>, gt, dim3(kCX), col_lds_bytes(2, b.N), s, d, RI, c, t.nnew, t.nrhs);
-  launch_uv_horiz(d, s, t.nrhs, 0);
+  if (!uv_done) launch_uv_horiz(d, s, t.nrhs, 0);
   Range Rd{b.istrU - 1, b.iend, b.jstrV - 1, b.jend};
   hipLaunchKernelGGL(k_rd, grid_of(Rd), dim3(kBX, kBY), 0, s, d, Rd, t.nstp);
   dim3 gu = gridc_of(RI);

@@ -8,7 +8,7 @@
 // Kernel 2 (per column): XI and ETA components ru, rv; each lane rebuilds the
 // three u-point (v-point) elementary differences it needs, with the
 // reference's one-sided extrapolation at closed edges expressed as a clamp.
-#include "roms_dev.h"
+#include "k_common.h"
 
 namespace roms {
 
@@ -112,11 +112,25 @@ constexpr int kPYH = kBY + 2, kPYN = kBX * kPYH;          // v-points m = j0-1 .
 constexpr int kPWW = kBX + 3, kPWH = kBY + 3, kPWN = kPWW * kPWH;   // raw window (i0-2.., j0-2..)
 constexpr int kPWQ = (kPWN + kBX * kBY - 1) / (kBX * kBY);
 constexpr int kPQ = (kPXN + kPYN + kBX * kBY - 1) / (kBX * kBY);
-__global__ void __launch_bounds__(256) k_prsgrd_uv(Dev d, Range R, int split, int imin, int imax, int jmin, int jmax) {
+template <bool FUSE>
+__global__ void __launch_bounds__(256) k_prsgrd_uv(Dev d, Range R, int split, int imin, int imax, int jmin, int jmax,
+                                                   UVBounds ub, int up, int nrhs) {
   const uint3 bI = xcd_tile();
-  __shared__ double sZ[kPWN], sR[kPWN], sQ[kPWN];
-  __shared__ double sFCx[kPXN], sRx[kPXN], sFCy[kPYN], sRy[kPYN];
-  __shared__ double sdZx[kPXN], sdRx[kPXN], sdZy[kPYN], sdRy[kPYN];
+  // one LDS block: the raw window, the elementary differences and the
+  // harmonic means (and, FUSE, the u/v window after them)
+  constexpr int kPL = 3 * kPWN + 4 * kPXN + 4 * kPYN;
+  __shared__ double sL[kPL];
+  double* const sZ = sL;
+  double* const sR = sZ + kPWN;
+  double* const sQ = sR + kPWN;
+  double* const sFCx = sQ + kPWN;
+  double* const sRx = sFCx + kPXN;
+  double* const sFCy = sRx + kPXN;
+  double* const sRy = sFCy + kPYN;
+  double* const sdZx = sRy + kPYN;
+  double* const sdRx = sdZx + kPXN;
+  double* const sdZy = sdRx + kPXN;
+  double* const sdRy = sdZy + kPYN;
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const double g = d.p.g, rho0 = d.p.rho0, qp2 = d.p.qp2;
@@ -179,6 +193,31 @@ __global__ void __launch_bounds__(256) k_prsgrd_uv(Dev d, Range R, int split, in
   if (du || dv) { hz0 = F.Hz[o]; P0 = F.P[o]; }
   if (du) { hzu = F.Hz[o - 1]; Pu = F.P[o - 1]; dnu = F.dn_u[ij]; }
   if (dv) { hzv = F.Hz[o - sj]; Pv = F.P[o - sj]; dmv = F.dm_v[ij]; }
+  // FUSE: the horizontal momentum r.h.s. of the same cell (k_uv_horiz1's
+  // window of u, v, FlxU, FlxV at nrhs and its lane inputs), loaded here
+  // with everything else; ru/rv then go to HBM once, after both terms
+  constexpr int UW = kUVN, UR = (UW + kBX * kBY - 1) / (kBX * kBY);
+  double wU[FUSE ? UR : 1], wV[FUSE ? UR : 1], wFU[FUSE ? UR : 1], wFV[FUSE ? UR : 1];
+  double fo0 = 0.0, fox = 0.0, foy = 0.0;
+  if constexpr (FUSE) {
+    const long kn = kk + (long)(nrhs - 1) * b.n3;
+#pragma unroll
+    for (int r = 0; r < UR; r++) {
+      const int q = tid + r * kBX * kBY;
+      const int ii = i0 - 2 + q % kUVW, jj = j0 - 2 + q / kUVW;
+      const bool ok = q < UW && ii >= -1 && ii <= b.Lm + 2 && jj >= -1 && jj <= b.Mm + 2;
+      const long oo = ok ? IJ(b, ii, jj) : 0;
+      wU[r] = ok ? F.u[oo + kn] : 0.0;
+      wV[r] = ok ? F.v[oo + kn] : 0.0;
+      wFU[r] = ok ? F.FlxU[oo + kk] : 0.0;
+      wFV[r] = ok ? F.FlxV[oo + kk] : 0.0;
+    }
+    if (d.p.uv_cor && (du || dv)) {
+      fo0 = F.fomn[ij]; fox = F.fomn[ij - 1]; foy = F.fomn[ij - sj];
+      if (!du) hzu = F.Hz[o - 1];
+      if (!dv) hzv = F.Hz[o - sj];
+    }
+  }
 #pragma unroll
   for (int m = 0; m < kPWQ; m++) {
     const int q = tid + m * kBX * kBY;
@@ -245,11 +284,12 @@ __global__ void __launch_bounds__(256) k_prsgrd_uv(Dev d, Range R, int split, in
     return sR[w];
   };
   const int wc = W(inr ? i : i0, inr ? j : j0);
+  double pru = 0.0, prv = 0.0;   // the pressure-gradient terms
   if (du) {
     const int q = threadIdx.x + threadIdx.y * kPXW;   // p = i-1 ; q+1: p = i
     const double dZ0 = sdZx[q], dZ1 = sdZx[q + 1], dR0 = sdRx[q], dR1 = sdRx[q + 1];
     const double z0 = sZ[wc], zu = sZ[wc - 1], r0 = rhov(wc), ru_ = rhov(wc - 1);
-    F.ru[o] = 0.5 * (hz0 + hzu) * dnu *
+    pru = 0.5 * (hz0 + hzu) * dnu *
               (Pu - P0 -
                HalfGRho * ((r0 + ru_) * (z0 - zu) -
                            OneFifth * ((dR1 - dR0) * (z0 - zu - OneTwelfth * (dZ1 + dZ0)) -
@@ -259,13 +299,39 @@ __global__ void __launch_bounds__(256) k_prsgrd_uv(Dev d, Range R, int split, in
     const int q = threadIdx.x + threadIdx.y * kBX;    // p = j-1 ; q+kBX: p = j
     const double dZ0 = sdZy[q], dZ1 = sdZy[q + kBX], dR0 = sdRy[q], dR1 = sdRy[q + kBX];
     const double z0 = sZ[wc], zv = sZ[wc - kPWW], r0 = rhov(wc), rv_ = rhov(wc - kPWW);
-    F.rv[o] = 0.5 * (hz0 + hzv) * dmv *
+    prv = 0.5 * (hz0 + hzv) * dmv *
               (Pv - P0 -
                HalfGRho * ((r0 + rv_) * (z0 - zv) -
                            OneFifth * ((dR1 - dR0) * (z0 - zv - OneTwelfth * (dZ1 + dZ0)) -
                                        (dZ1 - dZ0) * (r0 - rv_ - OneTwelfth * (dR1 + dR0)))));
   }
+  if constexpr (!FUSE) {
+    if (du) F.ru[o] = pru;
+    if (dv) F.rv[o] = prv;
+  } else {
+    // the window of u, v, FlxU, FlxV into the LDS of the finished stages
+    __syncthreads();
+    double* sU = sL;            // the finished stages' LDS, reused
+    double* sV = sU + kUVN;
+    double* sFU = sV + kUVN;
+    double* sFV = sFU + kUVN;
+    static_assert(4 * kUVN <= kPL, "uv window fits");
+#pragma unroll
+    for (int r = 0; r < UR; r++) {
+      const int q = tid + r * kBX * kBY;
+      if (q < UW) { sU[q] = wU[r]; sV[q] = wV[r]; sFU[q] = wFU[r]; sFV[q] = wFV[r]; }
+    }
+    __syncthreads();
+    if (!(du || dv)) return;
+    UVPre pp;
+    pp.ru = pru; pp.rv = prv;
+    pp.hz0 = hz0; pp.hzx = hzu; pp.hzy = hzv;
+    pp.f0 = fo0; pp.fx = fox; pp.fy = foy;
+    const AccL a{sU, sV, sFU, sFV, i0 - 2, j0 - 2};
+    uv_horiz_rhs_pre(d, a, i, j, o, pp, ub, up != 0);
+  }
 }
+
 
 // ---- fused form: one block per 64x4 tile walks the levels top-down.  Its
 // 325 "P columns" (the tile plus one column to the west and one row to the
@@ -506,7 +572,7 @@ __global__ void __launch_bounds__(kFT) k_prsgrd_fused(Dev d, Range R, int split,
   }
 }
 
-void launch_prsgrd(const Dev& d, hipStream_t s, const Tlev& t) {
+void launch_prsgrd(const Dev& d, hipStream_t s, const Tlev& t, int uv_up) {
   const Bounds& b = d.b;
   const int split = d.p.nonlin_eos;
   int imin, imax, jmin, jmax;
@@ -526,7 +592,18 @@ void launch_prsgrd(const Dev& d, hipStream_t s, const Tlev& t) {
   // two-kernel form (default; k_prsgrd_fused with ROMS_GPU_PRSGRD_FUSED=1)
   Range R1{0, b.Lm, 0, b.Mm};
   hipLaunchKernelGGL(k_prsgrd_P, grid_of(R1), dim3(kBX, kBY), 0, s, d, R1, split, d.p.tides);
-  hipLaunchKernelGGL(k_prsgrd_uv, grid3_of(R2, b.N), dim3(kBX, kBY), 0, s, d, R2, split, imin, imax, jmin, jmax);
+  if (uv_up >= 0)
+    hipLaunchKernelGGL(k_prsgrd_uv<true>, grid3_of(R2, b.N), dim3(kBX, kBY), 0, s, d, R2, split, imin, imax, jmin, jmax,
+                       uv_bounds(b), uv_up, t.nrhs);
+  else
+    hipLaunchKernelGGL(k_prsgrd_uv<false>, grid3_of(R2, b.N), dim3(kBX, kBY), 0, s, d, R2, split, imin, imax, jmin, jmax,
+                       uv_bounds(b), 0, t.nrhs);
+}
+// k_prsgrd_uv<true> adds the horizontal momentum r.h.s. of k_uv_horiz1 on
+// the same inputs: usable when the caller runs uv_horiz next with nothing
+// between them that changes u, v(nrhs), FlxU, FlxV, Hz or ru, rv
+bool prsgrd_can_fuse_uv(const Dev& d) {
+  return d.p.prs_split && d.p.hoist && d.p.prs_fuse_uv && !d.p.curvgrid && (d.p.uv_cor || d.p.uv_adv);
 }
 
 }  // namespace roms

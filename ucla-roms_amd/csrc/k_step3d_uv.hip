@@ -346,9 +346,9 @@ void setup_uv1_seg() {
                             (int)((size_t)kSegRows * kSegMaxS * kSegCW * kSegJMax * sizeof(double)));
 }
 
-void launch_step3d_uv1(const Dev& d, hipStream_t s, const Tlev& t) {
+void launch_step3d_uv1(const Dev& d, hipStream_t s, const Tlev& t, bool uv_done) {
   const Bounds& b = d.b;
-  launch_uv_horiz(d, s, t.nrhs, 1);
+  if (!uv_done) launch_uv_horiz(d, s, t.nrhs, 1);
   Range R{b.istr, b.iend, b.jstr, b.jend};
   dim3 g = gridc_of(R);
   g.z = 2;

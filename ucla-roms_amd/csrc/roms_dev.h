@@ -45,6 +45,7 @@ struct Params {
   int seg_xg;     // x-blocks per group of seg_order 3 (ROMS_GPU_SEG_XG)
   int s2d_fold;   // closed-wall edges of the fast step inside k_s2d_fb (ROMS_GPU_S2D_EDGES=1: separate kernels)
   int hoist;
+  int prs_fuse_uv;  // whole steps: horizontal momentum r.h.s. inside prsgrd (ROMS_GPU_PRS_UV=0: separate)
   int h_ty;       // tile rows of the hoisted horizontal kernels: 4 or 8 (ROMS_GPU_HTY)      // per-level horizontal kernels with every global load at entry (ROMS_GPU_HOIST=0: per-phase forms)
   int seg_jrows;  // rows j per block of the momentum segment solvers (1..kSegJMax; ROMS_GPU_SEG_JROWS)
   int npip;       // pipe_frc.F: number of pipes (0: pipe_source off)
@@ -291,9 +292,13 @@ void launch_set_huv(const Dev& d, hipStream_t s, const Tlev& t);
 void launch_set_huv1(const Dev& d, hipStream_t s, const Tlev& t);
 void launch_omega(const Dev& d, hipStream_t s, const Tlev& t);
 void launch_rho_eos(const Dev& d, hipStream_t s, const Tlev& t, int tidx);
-void launch_prsgrd(const Dev& d, hipStream_t s, const Tlev& t);
-void launch_pre_step3d(const Dev& d, hipStream_t s, const Tlev& t);
-void launch_step3d_uv1(const Dev& d, hipStream_t s, const Tlev& t);
+// uv_up >= 0: also add the horizontal momentum r.h.s. (UPSTREAM_UV if 1) of
+// the following pre_step3d / step3d_uv1 (prsgrd_can_fuse_uv; the caller then
+// passes uv_done to it)
+void launch_prsgrd(const Dev& d, hipStream_t s, const Tlev& t, int uv_up = -1);
+bool prsgrd_can_fuse_uv(const Dev& d);
+void launch_pre_step3d(const Dev& d, hipStream_t s, const Tlev& t, bool uv_done = false);
+void launch_step3d_uv1(const Dev& d, hipStream_t s, const Tlev& t, bool uv_done = false);
 void launch_visc3d(const Dev& d, hipStream_t s, const Tlev& t);
 void launch_step2d(const Dev& d, hipStream_t s, const Tlev& t, const double* w1, const double* w2);
 void launch_step3d_uv2(const Dev& d, hipStream_t s, const Tlev& t);

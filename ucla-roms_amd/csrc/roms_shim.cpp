@@ -351,8 +351,12 @@ void enqueue_step(roms_tlev* t, bool rho_current) {
   TIMED(ROMS_R_SET_HUV, launch_set_huv(d, s, T));
   TIMED(ROMS_R_OMEGA, launch_omega(d, s, T));
   if (g.cfg.lmd_mixing) TIMED(ROMS_R_LMD_VMIX, launch_lmd_vmix(d, s, T, T.nstp));
-  TIMED(ROMS_R_PRSGRD, launch_prsgrd(d, s, T));
-  TIMED(ROMS_R_PRE_STEP3D, launch_pre_step3d(d, s, T));
+  // the horizontal momentum r.h.s. of pre_step3d / step3d_uv1 rides in the
+  // prsgrd kernel just before them (prsgrd_can_fuse_uv; nothing between the
+  // two touches u, v(nrhs), FlxU, FlxV, Hz or ru, rv)
+  const bool fuse_uv = prsgrd_can_fuse_uv(d);
+  TIMED(ROMS_R_PRSGRD, launch_prsgrd(d, s, T, fuse_uv ? 0 : -1));
+  TIMED(ROMS_R_PRE_STEP3D, launch_pre_step3d(d, s, T, fuse_uv));
   TIMED(ROMS_R_SET_HUV1, launch_set_huv1(d, s, T));
   t->nrhs = 3;
   t->nnew = 3 - t->nstp;
@@ -363,8 +367,8 @@ void enqueue_step(roms_tlev* t, bool rho_current) {
   launch_bulk_flux(d, s, T.nrhs);   // set_forces (main.F:433): BULK_FRC only
   if (g.cfg.lmd_mixing) TIMED(ROMS_R_LMD_VMIX, launch_lmd_vmix(d, s, T, T.nrhs));
   frc_step_phase(d, s, 3, pot);     // set_bry_all 'forward' + set_tides (main.F:438-441)
-  TIMED(ROMS_R_PRSGRD, launch_prsgrd(d, s, T));
-  TIMED(ROMS_R_STEP3D_UV1, launch_step3d_uv1(d, s, T));
+  TIMED(ROMS_R_PRSGRD, launch_prsgrd(d, s, T, fuse_uv ? 1 : -1));
+  TIMED(ROMS_R_STEP3D_UV1, launch_step3d_uv1(d, s, T, fuse_uv));
   if (g.cfg.uv_vis2) TIMED(ROMS_R_VISC3D, launch_visc3d(d, s, T));
   for (int iif = 1; iif <= t->nfast; iif++) {
     t->iif = iif;
@@ -547,6 +551,10 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
   {
     const char* e = getenv("ROMS_GPU_S2D_EDGES");
     P.s2d_fold = !(e && e[0] == '1');
+  }
+  {
+    const char* e = getenv("ROMS_GPU_PRS_UV");
+    P.prs_fuse_uv = !(e && e[0] == '0');
   }
   {
     const char* e = getenv("ROMS_GPU_HTY");
