@@ -5,7 +5,9 @@ in separate passes (FETCH_SIZE costs 3 TCC counters, WRITE_SIZE 2); on gfx950
 FETCH_SIZE reports half the bytes of a wide coalesced read, so
 traffic = 2*FETCH_SIZE + WRITE_SIZE (KB units -> bytes).  Kernels map to the
 reference routine that launches them; k_uv_horiz runs once in pre_step3d and
-once in step3d_uv1 and is split evenly; halo wraps are reported separately.
+once in step3d_uv1 and is split evenly (in whole steps it rides inside
+k_prsgrd_uv, whose bytes then count as prsgrd); halo wraps are reported
+separately.  rho_eos runs twice per step (the step-opening one is reused).
 
 usage: python tools/pmc_traffic.py FETCH_counter_collection.csv WRITE_counter_collection.csv
           --steps-marker k_step3d_t_v --out profiles/pmc_traffic.json
@@ -28,9 +30,9 @@ ROUTINE_OF = {
     "k_pre_tracer_seg": "pre_step3d", "k_pre_uv_seg": "pre_step3d", "k_uv2_fused": "step3d_uv2",
     "k_set_huv1_chain": "set_HUV1", "k_kpp_ext": "lmd_vmix", "k_kpp_int": "lmd_vmix", "k_prsgrd_fused": "prsgrd",
     "k_bulk_flux": "bulk_flux", "k_t3dbc_edges": "step3d_t", "k_t3dbc_corners": "step3d_t", "k_u3dbc": "step3d_uv2",
-    "k_v3dbc": "step3d_uv2",
+    "k_v3dbc": "step3d_uv2", "k_pre_tracer_h1": "pre_step3d", "k_step3d_t_h1": "step3d_t",
 }
-CALLS_PER_STEP = {"rho_eos": 3, "set_HUV": 1, "omega": 3, "prsgrd": 2, "pre_step3d": 1, "set_HUV1": 1,
+CALLS_PER_STEP = {"rho_eos": 2, "set_HUV": 1, "omega": 3, "prsgrd": 2, "pre_step3d": 1, "set_HUV1": 1,
                   "step3d_uv1": 1, "visc3d": 1, "step2d": None, "step3d_uv2": 1, "step3d_t": 1, "t3dmix": 1,
                   "lmd_vmix": 2, "bulk_flux": 2}
 
@@ -72,7 +74,7 @@ def main():
         kern[k] = {"dispatches": fc.get(k, 0), "fetch_size_bytes": f.get(k, 0.0), "write_size_bytes": w.get(k, 0.0),
                    "traffic_bytes": b}
         r = ROUTINE_OF.get(k)
-        if k == "k_uv_horiz":
+        if k in ("k_uv_horiz", "k_uv_horiz1"):
             per_routine["pre_step3d"] += 0.5 * b
             per_routine["step3d_uv1"] += 0.5 * b
         elif r:
