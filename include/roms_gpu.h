@@ -388,6 +388,7 @@ enum roms_routine {
   ROMS_R_K_PRE_UV_SEG,     /* kernel level: pre_step3d's momentum segment solver (N > 63) */
   ROMS_R_K_UV1_SEG,        /* kernel level: step3d_uv1's momentum segment solver (N > 63) */
   ROMS_R_K_STEP3D_T_SEG,   /* kernel level: step3d_t's tracer segment solver (N > 63) */
+  ROMS_R_K_PRSGRD_UV,      /* kernel level: prsgrd's ru/rv kernel (with the horizontal momentum r.h.s. in whole steps) */
   ROMS_R_COUNT
 };
 int roms_gpu_time_routine(int routine, int nsteps, roms_tlev *t, double *avg_ms, long *launches);

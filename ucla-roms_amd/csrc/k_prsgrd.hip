@@ -592,12 +592,14 @@ void launch_prsgrd(const Dev& d, hipStream_t s, const Tlev& t, int uv_up) {
   // two-kernel form (default; k_prsgrd_fused with ROMS_GPU_PRSGRD_FUSED=1)
   Range R1{0, b.Lm, 0, b.Mm};
   hipLaunchKernelGGL(k_prsgrd_P, grid_of(R1), dim3(kBX, kBY), 0, s, d, R1, split, d.p.tides);
+  ktimer_mark(s, kTimedPrsgrdUv, 0);
   if (uv_up >= 0)
     hipLaunchKernelGGL(k_prsgrd_uv<true>, grid3_of(R2, b.N), dim3(kBX, kBY), 0, s, d, R2, split, imin, imax, jmin, jmax,
                        uv_bounds(b), uv_up, t.nrhs);
   else
     hipLaunchKernelGGL(k_prsgrd_uv<false>, grid3_of(R2, b.N), dim3(kBX, kBY), 0, s, d, R2, split, imin, imax, jmin, jmax,
                        uv_bounds(b), 0, t.nrhs);
+  ktimer_mark(s, kTimedPrsgrdUv, 1, 1);
 }
 // k_prsgrd_uv<true> adds the horizontal momentum r.h.s. of k_uv_horiz1 on
 // the same inputs: usable when the caller runs uv_horiz next with nothing

@@ -237,6 +237,7 @@ struct Tlev {
 // interval that covers `count` launches of one kernel
 constexpr int kTimedS2dFb = 13;   // ROMS_R_K_S2D_FB
 constexpr int kTimedPreUvSeg = 14, kTimedUv1Seg = 15, kTimedStep3dTSeg = 16;   // ROMS_R_K_*_SEG
+constexpr int kTimedPrsgrdUv = 17;   // ROMS_R_K_PRSGRD_UV
 void ktimer_mark(hipStream_t s, int kernel_id, int end, int count = 0);
 
 void launch_exchange(const Dev& d, hipStream_t s, double* a, int nlev);

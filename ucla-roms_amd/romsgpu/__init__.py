@@ -198,7 +198,7 @@ WRT_DEFAULT = 63
 ROUTINES = ("rho_eos", "set_HUV", "omega", "prsgrd", "pre_step3d", "set_HUV1", "step3d_uv1", "visc3d", "step2d",
             "step3d_uv2", "step3d_t", "t3dmix", "lmd_vmix",
             "k_s2d_fb",  # kernel level: the fused barotropic kernel alone
-            "k_pre_uv_seg", "k_uv1_seg", "k_step3d_t_seg")  # kernel level: the N > 63 column solvers
+            "k_pre_uv_seg", "k_uv1_seg", "k_step3d_t_seg", "k_prsgrd_uv")  # kernel level: the N > 63 column solvers
 HALO_OPP = (1, 0, 3, 2, 7, 6, 5, 4)
 
 
