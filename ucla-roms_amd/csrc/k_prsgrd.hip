@@ -3,8 +3,9 @@
 //
 // Kernel 1 (per column over 0..nx x 0..ny): elementary vertical differences,
 // harmonic averages dR,dZ and the top-down hydrostatic pressure P, all in
-// registers (rolling window over k) -- no (N+1)-deep scratch.  For SPLIT_EOS it
-// also materialises the in-situ density rho = rho1 + qp1*dpth*(1-qp2*dpth).
+// registers (rolling window over k) -- no (N+1)-deep scratch.  (The in-situ
+// density rho1 + qp1*dpth*(1-qp2*dpth) of SPLIT_EOS is re-formed from the
+// raw window wherever kernel 2 needs it; it is not stored.)
 // Kernel 2 (per column): XI and ETA components ru, rv; each lane rebuilds the
 // three u-point (v-point) elementary differences it needs, with the
 // reference's one-sided extrapolation at closed edges expressed as a clamp.
@@ -30,7 +31,6 @@ __global__ void __launch_bounds__(256) k_prsgrd_P(Dev d, Range R, int split, int
   const double* __restrict__ rho = F.rho + ij;
   const double* __restrict__ rho1 = F.rho1 + ij;
   const double* __restrict__ qp1 = F.qp1 + ij;
-  double* __restrict__ rhos = F.rhos + ij;
   double* __restrict__ Pp = F.P + ij;
   // Top-down walk with a rolling register window: z_r, rho1, qp1 (or rho) of
   // each level are loaded once; the elementary differences, harmonic
@@ -71,7 +71,6 @@ __global__ void __launch_bounds__(256) k_prsgrd_P(Dev d, Range R, int split, int
     if (split) {
       const double dpth = -zC;
       dRk = dRk - qC * dZk * (1.0 - 2.0 * qp2 * dpth);
-      rhos[o] = v0;
     }
     if (doP) {
       double Pk;

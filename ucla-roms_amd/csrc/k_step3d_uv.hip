@@ -664,7 +664,8 @@ __global__ void __launch_bounds__(256, KL > 13 ? 3 : 4) k_uv2_fused(Dev d, Range
   const int i = cl.i, j = cl.j, g = cl.g, lo = cl.lo, nk = cl.nk;
   const long n2 = b.n2;
   auto chain2 = [&](double& s1, double& s2, auto&& body) { chain_down(cl, s1, s2, body); };
-  for (int dir = 0; dir < 2; dir++) {
+  const int d0 = gridDim.z == 2 ? (int)bI.z : 0, d1 = gridDim.z == 2 ? d0 + 1 : 2;   // grid z = 2: a direction per block
+  for (int dir = d0; dir < d1; dir++) {
     // the lane's column, clamped into the coupling range (lanes outside
     // k_uv2_fused's columns compute on a valid column so the shuffles see
     // defined values, and store nothing)
@@ -747,7 +748,8 @@ void launch_step3d_uv2(const Dev& d, hipStream_t s, const Tlev& t) {
   Range R2{iv0 < iu0 ? iv0 : iu0, iu1 > iv1 ? iu1 : iv1, j0, j1};
   const int kl = (b.N + 3) / 4;
   if (!d.p.obc && d.p.uv2_fused && kl <= 25) {
-    const dim3 gf = chain_grid_of(R1);
+    dim3 gf = chain_grid_of(R1);
+    gf.z = d.p.chain_dirz ? 2 : 1;
     if (kl <= 5) hipLaunchKernelGGL(k_uv2_fused<5>, gf, dim3(256), 0, s, d, R1, t.nnew, t.nstp, t.knew);
     else if (kl <= 13) hipLaunchKernelGGL(k_uv2_fused<13>, gf, dim3(256), 0, s, d, R1, t.nnew, t.nstp, t.knew);
     else hipLaunchKernelGGL(k_uv2_fused<25>, gf, dim3(256), 0, s, d, R1, t.nnew, t.nstp, t.knew);

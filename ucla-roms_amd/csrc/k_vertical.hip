@@ -158,8 +158,11 @@ __global__ void __launch_bounds__(256) k_set_huv1_chain(Dev d, Range R, int nnew
   const int N = b.N;
   const ChainLane cl = chain_lane<KL>(R, bI, N);
   const long n2 = b.n2;
+  // grid z = 2: one direction per block (both directions' loads in flight
+  // at once across blocks); grid z = 1: both, one after the other
+  const int d0 = gridDim.z == 2 ? (int)bI.z : 0, d1 = gridDim.z == 2 ? d0 + 1 : 2;
 #pragma unroll 1
-  for (int dir = 0; dir < 2; dir++) {
+  for (int dir = d0; dir < d1; dir++) {
     const int ilo = dir == 0 ? b.istr : b.istrR, jlo = dir == 0 ? b.jstrR : b.jstr;
     const int ic = min(max(cl.i, ilo), b.iendR), jc = min(max(cl.j, jlo), b.jendR);
     const bool act = ic == cl.i && jc == cl.j;
@@ -209,9 +212,11 @@ void launch_set_huv1(const Dev& d, hipStream_t s, const Tlev& t) {
   const Bounds& b = d.b;
   Range R{b.istrR < b.istr ? b.istrR : b.istr, b.iendR, b.jstrR < b.jstr ? b.jstrR : b.jstr, b.jendR};
   const int kl = chain_kl(b.N), first = (int)(t.iic == t.forw_start);
-  if (d.p.chain && kl == 5) hipLaunchKernelGGL(k_set_huv1_chain<5>, chain_grid_of(R), dim3(256), 0, s, d, R, t.nnew, first);
-  else if (d.p.chain && kl == 13) hipLaunchKernelGGL(k_set_huv1_chain<13>, chain_grid_of(R), dim3(256), 0, s, d, R, t.nnew, first);
-  else if (d.p.chain && kl == 25) hipLaunchKernelGGL(k_set_huv1_chain<25>, chain_grid_of(R), dim3(256), 0, s, d, R, t.nnew, first);
+  dim3 gc = chain_grid_of(R);
+  gc.z = d.p.chain_dirz ? 2 : 1;
+  if (d.p.chain && kl == 5) hipLaunchKernelGGL(k_set_huv1_chain<5>, gc, dim3(256), 0, s, d, R, t.nnew, first);
+  else if (d.p.chain && kl == 13) hipLaunchKernelGGL(k_set_huv1_chain<13>, gc, dim3(256), 0, s, d, R, t.nnew, first);
+  else if (d.p.chain && kl == 25) hipLaunchKernelGGL(k_set_huv1_chain<25>, gc, dim3(256), 0, s, d, R, t.nnew, first);
   else hipLaunchKernelGGL(k_set_huv1, grid_of(R), dim3(kBX, kBY), 0, s, d, R, t.nnew, first);
   launch_exchange_list(d, s, ExchList{{d.f.FlxU, d.f.FlxV, d.f.u + (long)(t.nnew - 1) * b.n3,
                                         d.f.v + (long)(t.nnew - 1) * b.n3}, {b.N, b.N, b.N, b.N}, 4});

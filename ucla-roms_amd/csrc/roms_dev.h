@@ -45,6 +45,7 @@ struct Params {
   int seg_xg;     // x-blocks per group of seg_order 3 (ROMS_GPU_SEG_XG)
   int s2d_fold;   // closed-wall edges of the fast step inside k_s2d_fb (ROMS_GPU_S2D_EDGES=1: separate kernels)
   int hoist;
+  int chain_dirz;   // chain kernels (set_HUV1, uv2): one direction per block (ROMS_GPU_CHAIN_DIRZ=0: both in turn)
   int prs_fuse_uv;  // whole steps: horizontal momentum r.h.s. inside prsgrd (ROMS_GPU_PRS_UV=0: separate)
   int h_ty;       // tile rows of the hoisted horizontal kernels: 4 or 8 (ROMS_GPU_HTY)      // per-level horizontal kernels with every global load at entry (ROMS_GPU_HOIST=0: per-phase forms)
   int seg_jrows;  // rows j per block of the momentum segment solvers (1..kSegJMax; ROMS_GPU_SEG_JROWS)

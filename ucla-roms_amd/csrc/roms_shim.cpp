@@ -553,6 +553,10 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     P.s2d_fold = !(e && e[0] == '1');
   }
   {
+    const char* e = getenv("ROMS_GPU_CHAIN_DIRZ");
+    P.chain_dirz = !(e && e[0] == '0');   // set_HUV1 2.55 -> 2.03 ms at C3 (r3_s_chain_dirz_ab.txt)
+  }
+  {
     const char* e = getenv("ROMS_GPU_PRS_UV");
     P.prs_fuse_uv = !(e && e[0] == '0');
   }
