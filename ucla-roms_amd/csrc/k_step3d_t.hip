@@ -409,6 +409,37 @@ __global__ void __launch_bounds__(256) k_t3dmix(Dev d, Range R, int nnew, int nr
   const long ij = IJ(b, i, j), sj = b.nx2, n2 = b.n2;
   const double* __restrict__ Hz = F.Hz;
   const double pmn = d.p.dt * F.pm[ij] * F.pn[ij];
+  if (b.NT == 2) {
+    // both tracers in one walk over k (each level's loads of T and S in
+    // flight together); per tracer the same expressions as below
+    double ax0[2], ax1[2], ay0[2], ay1[2];
+    const double* __restrict__ Tr[2];
+    double* __restrict__ Tn[2];
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+      const double* d2 = F.diff2 + (long)q * n2;
+      Tr[q] = F.t + (long)(nrhs - 1) * b.n3 + (long)q * 3 * b.n3;
+      Tn[q] = F.t + (long)(nnew - 1) * b.n3 + (long)q * 3 * b.n3;
+      ax0[q] = 0.25 * (d2[ij] + d2[ij - 1]) * F.pmon_u[ij];
+      ax1[q] = 0.25 * (d2[ij + 1] + d2[ij]) * F.pmon_u[ij + 1];
+      ay0[q] = 0.25 * (d2[ij] + d2[ij - sj]) * F.pnom_v[ij];
+      ay1[q] = 0.25 * (d2[ij + sj] + d2[ij]) * F.pnom_v[ij + sj];
+    }
+    const double um0 = F.umask[ij], um1 = F.umask[ij + 1], vm0 = F.vmask[ij], vm1 = F.vmask[ij + sj];
+#pragma unroll 2
+    for (int k = 1; k <= b.N; k++) {
+      const long o = ij + (long)(k - 1) * n2;
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
+        const double FX1 = ax1[q] * (Hz[o + 1] + Hz[o]) * (Tr[q][o + 1] - Tr[q][o]) * um1;
+        const double FX0 = ax0[q] * (Hz[o] + Hz[o - 1]) * (Tr[q][o] - Tr[q][o - 1]) * um0;
+        const double FE1 = ay1[q] * (Hz[o + sj] + Hz[o]) * (Tr[q][o + sj] - Tr[q][o]) * vm1;
+        const double FE0 = ay0[q] * (Hz[o] + Hz[o - sj]) * (Tr[q][o] - Tr[q][o - sj]) * vm0;
+        Tn[q][o] = Tn[q][o] + pmn * (FX1 - FX0 + FE1 - FE0) / Hz[o];
+      }
+    }
+    return;
+  }
   for (int itrc = 1; itrc <= b.NT; itrc++) {
     const double* d2 = F.diff2 + (long)(itrc - 1) * n2;
     const double* __restrict__ Tr = F.t + (long)(nrhs - 1) * b.n3 + (long)(itrc - 1) * 3 * b.n3;
