@@ -133,3 +133,21 @@ def test_register_column_kernels_bitwise(lmd):
     b = _run_colreg(cfg, 3, 12)
     for n in a:
         assert np.array_equal(a[n], b[n]), n
+
+
+@pytest.mark.parametrize("case", ["n50", "n100"])
+def test_pre_uv_seg_lds_bitwise(case, monkeypatch):
+    """k_pre_uv_seg<true> (ROMS_GPU_PREUV_LDS, default) forms the predictor's
+    cf_stp*u(nstp) + cf_bak*u(indx) and u(indx) = Hz*u(nstp) in its spline
+    phase and keeps them in LDS instead of reloading u and Hz later; the same
+    expressions on the same values: 6 steps equal the reload form bitwise."""
+    cfg = seg_cfg(case)
+    out = []
+    for env in ("0", "1"):
+        monkeypatch.setenv("ROMS_GPU_PREUV_LDS", env)
+        m = make_model(cfg, 1)
+        m.step(6)
+        out.append({n: m.get(n) for n in ("zeta", "ubar", "vbar", "u", "v", "t", "rufrc", "rvfrc")})
+        m.close()
+    for n in out[0]:
+        assert np.array_equal(out[0][n], out[1][n]), n

@@ -236,9 +236,17 @@ __device__ __forceinline__ void spline_fc_seg(const SegSpan& sg, int N, SegXchg&
 // SPLINE_UV advective flux of a u (dir 0) / v (dir 1) column at interfaces
 // r = c0-1+q, q = 0..n (0 at the bottom and the surface): FC(r) * 0.5 * the
 // 4-point We average with the reference's masked curvature correction.
-template <int KR>
+// row(q, L, hz, hzm, u) is called in the load phase for q = 1..KR-1 (cells
+// c0..c0+KR-2, clamped; the rows q > n are dead) with the column's Hz, its
+// (i-1)/(j-1) neighbour's Hz and u(nrhs) there, unconditionally (a branch on
+// n would split the straight-line loads).  k_pre_uv_seg forms its u(indx)
+// terms from them.  Without UV_ADV the hook is not called.
+struct NoSplineRow {
+  __device__ __forceinline__ void operator()(int, long, double, double, double) const {}
+};
+template <int KR, class RowF = NoSplineRow>
 __device__ __forceinline__ void uv_spline_seg(const Dev& d, const SegSpan& sg, SegXchg& X, long ij, int nrhs, int dir,
-                                              double (&fl)[KR]) {
+                                              double (&fl)[KR], RowF row = RowF()) {
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const int N = b.N, c0 = sg.c0, n = sg.n;
@@ -256,8 +264,10 @@ __device__ __forceinline__ void uv_spline_seg(const Dev& d, const SegSpan& sg, S
 #pragma unroll
   for (int q = 0; q < KR + 1; q++) {   // all rows (clamped levels): straight-line loads
     const long L = (long)(min(max(c0 - 1 + q, 1), N) - 1) * n2;
-    dc[q] = 0.5625 * (Hz[L] + Hz[L - s]) - 0.0625 * (Hz[L + s] + Hz[L - 2 * s]);
+    const double h0 = Hz[L], h1 = Hz[L - s];
+    dc[q] = 0.5625 * (h0 + h1) - 0.0625 * (Hz[L + s] + Hz[L - 2 * s]);
     if (q < KR) uu[q] = Uv[L];
+    if (q >= 1 && q < KR) row(q, L, h0, h1, uu[q]);
     // groups of kSegLoadGroup rows: their loads issue together, the next
     // group's wait (without the barrier all 5 (KR+1) loads were hoisted and spilled)
     if (q % kSegLoadGroup == kSegLoadGroup - 1) __builtin_amdgcn_sched_barrier(0);

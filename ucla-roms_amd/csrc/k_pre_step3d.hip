@@ -601,6 +601,14 @@ __global__ void __launch_bounds__(kSegBlock, 2) k_pre_tracer_seg(Dev d, Range R,
   }
 }
 
+// kLds (UV_ADV, nrhs == nstp -- always so in the predictor): the spline
+// phase, which loads Hz, Hz of the (i-1)/(j-1) neighbour and u(nrhs) = u(nstp)
+// of every row anyway, also loads u(indx) and leaves in dynamic LDS the row's
+// cf_stp*u(nstp) + cf_bak*u(indx) and the new u(indx) = Hz*u(nstp); the
+// viscosity phase and the store phase then read no u(nstp), u(indx) or Hz
+// (at C3 these reloads missed L2: 4 of the v column's 18 array passes).
+// Dynamic LDS: 2 x (KR-1) doubles per thread, [row][thread].
+template <bool kLds>
 __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_pre_uv_seg(Dev d, Range R, PreCoef c, int nstp, int nnew, int nrhs) {
   const uint3 bI = seg_tile(d.p.seg_order, d.p.seg_xg);
   __shared__ SegXchg X;
@@ -616,10 +624,22 @@ __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_pre_uv_seg(Dev d, R
   const long n2 = b.n2, ij = IJ(b, col.i, col.j), s = dir == 0 ? 1 : b.nx2;
   const int c0 = sg.c0, n = sg.n;
   auto cell = [&](int k) { return (long)(min(max(k, 1), N) - 1) * n2; };   // rho level k (clamped)
-  double fl[KR];
-  uv_spline_seg<KR>(d, sg, X, ij, nrhs, dir, fl);
-  __builtin_amdgcn_sched_barrier(0);   // the viscosity phase's loads stay out of the spline phase
   double* Uall = dir == 0 ? F.u : F.v;
+  const int nthr = (int)(blockDim.x * blockDim.y * blockDim.z);
+  const int tid = (int)(threadIdx.x + blockDim.x * (threadIdx.y + blockDim.y * threadIdx.z));
+  double* const Sb = roms_smem + tid;                        // row q-1: cf_stp*u(nstp) + cf_bak*u(indx)
+  double* const Su = roms_smem + (long)(KR - 1) * nthr + tid;  // row q-1: Hz*u(nstp), the new u(indx)
+  double fl[KR];
+  if constexpr (kLds) {
+    const double* __restrict__ Uix = Uall + (long)(indx - 1) * b.n3 + ij;
+    uv_spline_seg<KR>(d, sg, X, ij, nrhs, dir, fl, [&](int q, long L, double h0, double h1, double u) {
+      Sb[(q - 1) * nthr] = c.cf_stp * u + c.cf_bak * Uix[L];
+      Su[(q - 1) * nthr] = 0.5 * (h0 + h1) * u;
+    });
+  } else {
+    uv_spline_seg<KR>(d, sg, X, ij, nrhs, dir, fl);
+  }
+  __builtin_amdgcn_sched_barrier(0);   // the viscosity phase's loads stay out of the spline phase
   const double* __restrict__ rr = (dir == 0 ? F.ru : F.rv) + ij;
   const double* __restrict__ Ustp = Uall + (long)(nstp - 1) * b.n3 + ij;
   double* __restrict__ Uidx = Uall + (long)(indx - 1) * b.n3 + ij;
@@ -639,8 +659,10 @@ __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_pre_uv_seg(Dev d, R
     const int k = c0 + p;
     const long o = cell(k);
     const double r = k == 1 ? rr[o] - fl[1] : rr[o] - fl[p + 1 < KR ? p + 1 : KR - 1] + fl[p];
-    const double us = Ustp[o];
-    const double v = 0.5 * (Hb[o] + Hb[o - s]) * (c.cf_stp * us + c.cf_bak * Uidx[o]) + DC0 * r;
+    double ub;
+    if constexpr (kLds) ub = Sb[(p < KR - 1 ? p : KR - 2) * nthr];
+    else ub = c.cf_stp * Ustp[o] + c.cf_bak * Uidx[o];
+    const double v = 0.5 * (Hb[o] + Hb[o - s]) * ub + DC0 * r;
     return k == N ? v + c.dtau * sstr : v;
   };
   double hf[KR + 1], hfm[KR + 1];   // Hz_fwd(c0-1+q) of the column and of its (i-1) / (j-1) neighbour
@@ -681,13 +703,14 @@ __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_pre_uv_seg(Dev d, R
   T.couple(sg, n, X, xL, xR);
   T.solve(n, xL, xR);
   if (act) {
-    // u(indx) = Hz*u(nstp), formed here from reloads (L2-warm) rather than
-    // kept in registers across the solve
+    // u(indx) = Hz*u(nstp): from LDS (kLds), else formed here from reloads
+    // rather than kept in registers across the solve
     double uix[KR];
 #pragma unroll
     for (int p = 0; p < KR; p++) {
       const long o = cell(c0 + p);
-      uix[p] = 0.5 * (Hz[o] + Hz[o - s]) * Ustp[o];
+      if constexpr (kLds) uix[p] = Su[(p < KR - 1 ? p : KR - 2) * nthr];
+      else uix[p] = 0.5 * (Hz[o] + Hz[o - s]) * Ustp[o];
     }
 #pragma unroll
     for (int p = 0; p < KR; p++)
@@ -696,6 +719,14 @@ __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_pre_uv_seg(Dev d, R
         Uidx[cell(c0 + p)] = uix[p];
       }
   }
+}
+
+static size_t pre_uv_seg_lds_bytes(unsigned nthr) {
+  return (size_t)2 * kSegRows * nthr * sizeof(double);
+}
+void setup_pre_uv_seg() {
+  (void)hipFuncSetAttribute((const void*)k_pre_uv_seg<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)pre_uv_seg_lds_bytes(kSegBlock * kSegJMax));
 }
 
 void setup_column_kernels_t(size_t bytes);
@@ -746,9 +777,13 @@ void launch_pre_step3d(const Dev& d, hipStream_t s, const Tlev& t, bool uv_done)
   dim3 gu = gridc_of(RI);
   gu.z = 2;
   if (d.p.colseg) {
+    const dim3 gs = seg_grid_of(RI, 2, d.p.seg_jrows), bs(kCX, seg_waves(b.N), d.p.seg_jrows);
     ktimer_mark(s, kTimedPreUvSeg, 0);
-    hipLaunchKernelGGL(k_pre_uv_seg, seg_grid_of(RI, 2, d.p.seg_jrows), dim3(kCX, seg_waves(b.N), d.p.seg_jrows), 0, s,
-                       d, RI, c, t.nstp, t.nnew, t.nrhs);
+    if (d.p.preuv_lds && d.p.uv_adv && t.nrhs == t.nstp)
+      hipLaunchKernelGGL(k_pre_uv_seg<true>, gs, bs, pre_uv_seg_lds_bytes(bs.x * bs.y * bs.z), s, d, RI, c, t.nstp,
+                         t.nnew, t.nrhs);
+    else
+      hipLaunchKernelGGL(k_pre_uv_seg<false>, gs, bs, 0, s, d, RI, c, t.nstp, t.nnew, t.nrhs);
     ktimer_mark(s, kTimedPreUvSeg, 1, 1);
   }
   else if (d.f.colscr)

@@ -44,10 +44,11 @@ struct Params {
   int seg_order;  // block order of the segment solvers (seg_tile; ROMS_GPU_SEG_ORDER)
   int seg_xg;     // x-blocks per group of seg_order 3 (ROMS_GPU_SEG_XG)
   int s2d_fold;   // closed-wall edges of the fast step inside k_s2d_fb (ROMS_GPU_S2D_EDGES=1: separate kernels)
-  int hoist;
+  int hoist;        // per-level horizontal kernels with every global load at entry (ROMS_GPU_HOIST=0: per-phase forms)
   int chain_dirz;   // chain kernels (set_HUV1, uv2): one direction per block (ROMS_GPU_CHAIN_DIRZ=0: both in turn)
   int prs_fuse_uv;  // whole steps: horizontal momentum r.h.s. inside prsgrd (ROMS_GPU_PRS_UV=0: separate)
-  int h_ty;       // tile rows of the hoisted horizontal kernels: 4 or 8 (ROMS_GPU_HTY)      // per-level horizontal kernels with every global load at entry (ROMS_GPU_HOIST=0: per-phase forms)
+  int h_ty;       // tile rows of the hoisted horizontal kernels: 4 or 8 (ROMS_GPU_HTY)
+  int preuv_lds;  // k_pre_uv_seg: u(indx) stored and u(nstp)/u(indx) combined in the spline phase (ROMS_GPU_PREUV_LDS=0: reloads)
   int seg_jrows;  // rows j per block of the momentum segment solvers (1..kSegJMax; ROMS_GPU_SEG_JROWS)
   int npip;       // pipe_frc.F: number of pipes (0: pipe_source off)
   int nriv, nrivf;  // river_frc.F: number of rivers (0: river_source off), river faces
@@ -285,7 +286,8 @@ void launch_exchange_tracers(const Dev& d, hipStream_t s, int tlev);  // t(:,:,:
 // the full 160 KB when N needs more than the default 64 KB.  Returns false if
 // N is too deep for one wavefront's columns to fit.
 bool setup_column_kernels(int N);
-void setup_uv1_seg();   // k_uv1_seg's dynamic LDS limit (k_step3d_uv.hip)
+void setup_uv1_seg();      // k_uv1_seg's dynamic LDS limit (k_step3d_uv.hip)
+void setup_pre_uv_seg();   // k_pre_uv_seg<true>'s dynamic LDS limit (k_pre_step3d.hip)
 inline size_t col_smem_bytes(const Dev& d, int nslots) {
   return d.f.colscr ? 0 : (size_t)nslots * (d.b.N + 1) * 64 * sizeof(double);
 }

@@ -561,6 +561,10 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     P.prs_fuse_uv = !(e && e[0] == '0');
   }
   {
+    const char* e = getenv("ROMS_GPU_PREUV_LDS");
+    P.preuv_lds = !(e && e[0] == '0');
+  }
+  {
     const char* e = getenv("ROMS_GPU_HTY");
     P.h_ty = (e && atoi(e) == 8) ? 8 : 4;
   }
@@ -583,6 +587,7 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     if (e && e[0] == '0') col_global = false;
   }
   setup_uv1_seg();
+  setup_pre_uv_seg();
   if (!col_global && !setup_column_kernels(dims->N)) {
     g.err = "roms_gpu_init: N too large for the LDS column kernels (2*(N+1)*512 B > 160 KB)";
     return -2;
