@@ -136,15 +136,19 @@ def test_register_column_kernels_bitwise(lmd):
 
 
 @pytest.mark.parametrize("case", ["n50", "n100"])
-def test_pre_uv_seg_lds_bitwise(case, monkeypatch):
-    """k_pre_uv_seg<true> (ROMS_GPU_PREUV_LDS, default) forms the predictor's
-    cf_stp*u(nstp) + cf_bak*u(indx) and u(indx) = Hz*u(nstp) in its spline
-    phase and keeps them in LDS instead of reloading u and Hz later; the same
-    expressions on the same values: 6 steps equal the reload form bitwise."""
+@pytest.mark.parametrize("switch", ["ROMS_GPU_PREUV_LDS", "ROMS_GPU_OMEGA_SEG"])
+def test_seg_variants_bitwise(case, switch, monkeypatch):
+    """Variants that keep the reference's operations and order, so 6 steps
+    equal the plain forms bitwise:
+    - k_pre_uv_seg<true> (ROMS_GPU_PREUV_LDS, default) forms the predictor's
+      cf_stp*u(nstp) + cf_bak*u(indx) and u(indx) = Hz*u(nstp) in its spline
+      phase and keeps them in LDS instead of reloading u and Hz later;
+    - k_omega_seg (ROMS_GPU_OMEGA_SEG, default) reads each input once and runs
+      the partial sums of the divergence as one chain through the waves."""
     cfg = seg_cfg(case)
     out = []
     for env in ("0", "1"):
-        monkeypatch.setenv("ROMS_GPU_PREUV_LDS", env)
+        monkeypatch.setenv(switch, env)
         m = make_model(cfg, 1)
         m.step(6)
         out.append({n: m.get(n) for n in ("zeta", "ubar", "vbar", "u", "v", "t", "rufrc", "rvfrc")})

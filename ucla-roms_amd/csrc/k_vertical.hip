@@ -6,6 +6,7 @@
 // results match the CPU reference bit for bit (built with -ffp-contract=off).
 #include "roms_dev.h"
 #include "k_chain.h"
+#include "k_colseg.h"
 
 namespace roms {
 
@@ -367,6 +368,118 @@ __global__ void __launch_bounds__(256) k_omega(Dev d, Range R, double dtau) {
 }
 #endif
 
+// Segment form of k_omega for deep grids (one read of every input).  k_omega's
+// lane walks its column twice -- pass 1 for the column total of the
+// divergence, pass 2 to re-form the same partial sums for the Courant split --
+// and so reads FlxU/FlxV twice (at C3 the second read misses L2: 9.3 array
+// passes of traffic for 6 of data).  Here a block of S wavefronts covers 64
+// columns of one row j and wave s holds the raw inputs of its segment of
+// levels (k_colseg.h seg_span) in registers, loaded once:
+//   1. the partial sums wi(k) run up the column as one chain through the
+//      waves in k order (wave s starts from wave s-1's last sum, handed over
+//      in LDS between barriers): the same operations in the same order as
+//      omega.F:102-108, so every wi(k) and the total are bit-identical;
+//   2. with the total's wrk every level's Courant split (omega.F:120-165) is
+//      independent: Courant number and Hz of the level above come from the
+//      wave above through LDS at the segment top.
+// Lanes outside the range solve a clamped duplicate column and store nothing.
+constexpr int kOmR = kSegRows;   // levels per wave (N <= kSegRows * kSegMaxS)
+__global__ void __launch_bounds__(kSegBlock, 2) k_omega_seg(Dev d, Range R, double dtau) {
+  const uint3 bI = xcd_tile();
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const int N = b.N;
+  const double cu_min = 0.6, cu_max = 1.0, cmnx_ratio = cu_min / cu_max, cutoff = 2.0 - cmnx_ratio,
+               r4cmx = 0.25 / (1.0 - cmnx_ratio);
+  const SegSpan sg = seg_span(N);
+  const int s = sg.s, S = sg.S, c0 = sg.c0, n = sg.n, l = sg.col;
+  const int iu = R.i0 + (int)bI.x * kSegCW + l, ju = R.j0 + (int)bI.y;
+  const bool act = iu <= R.i1 && ju <= R.j1;
+  const int i = iu < R.i1 ? iu : R.i1, j = ju < R.j1 ? ju : R.j1;
+  const long ij = IJ(b, i, j), n2 = b.n2, sj = b.nx2;
+  const double* __restrict__ FU = F.FlxU + ij;
+  const double* __restrict__ FV = F.FlxV + ij;
+  const double* __restrict__ Hz = F.Hz + ij;
+  const double* __restrict__ zw = F.z_w + ij;
+  __shared__ double Lw[kSegMaxS][kSegCW], Lcx[kSegMaxS][kSegCW], Lhz[kSegMaxS][kSegCW];
+  double fu1[kOmR], fu0[kOmR], fv1[kOmR], fv0[kOmR], cx[kOmR], hz[kOmR], zk[kOmR];
+#pragma unroll
+  for (int q = 0; q < kOmR; q++) {   // rho level k = c0+q (clamped), w-level k
+    const int k = min(c0 + q, N);
+    const long o = (long)(k - 1) * n2;
+    fu1[q] = FU[o + 1]; fu0[q] = FU[o]; fv1[q] = FV[o + sj]; fv0[q] = FV[o];
+    hz[q] = Hz[o];
+    zk[q] = zw[(long)k * n2];
+  }
+  const double zw0 = zw[0], zwN = zw[(long)N * n2];
+  const double wsrf = F.swflx[ij] * F.dm_r[ij] * F.dn_r[ij];
+  const double CX0 = dtau * F.pm[ij] * F.pn[ij];
+  const int pidx = d.p.npip > 0 ? F.pipe_idx[ij] : 0;
+  const double pflx = pidx > 0 ? F.pipe_flx[ij] : 0.0;
+  const double* __restrict__ prf = pidx > 0 ? F.pipe_prf + (pidx - 1) : nullptr;
+#pragma unroll
+  for (int q = 0; q < kOmR; q++) cx[q] = fmax0(fu1[q]) - fmin0(fu0[q]) + fmax0(fv1[q]) - fmin0(fv0[q]);
+  Lcx[s][l] = cx[0];
+  Lhz[s][l] = hz[0];
+  // 1. the partial sums, wave by wave in k order
+  double wk[kOmR];
+  for (int t = 0; t < S; t++) {
+    if (s == t) {
+      double wi = t == 0 ? 0.0 : Lw[t - 1][l];
+#pragma unroll
+      for (int q = 0; q < kOmR; q++) {
+        double v = wi - fu1[q] + fu0[q] - fv1[q] + fv0[q];
+        if (pidx > 0) v = v + pflx * prf[(long)(min(c0 + q, N) - 1) * d.p.npip];
+        wi = q < n ? v : wi;
+        wk[q] = wi;
+      }
+      Lw[t][l] = wi;
+    }
+    __syncthreads();
+  }
+  // 2. the Courant split of w-levels k = c0..c0+n-1 (k <= N-1)
+  const double wrk = (Lw[S - 1][l] + wsrf) / (zwN - zw0);
+  const double cx_top = s + 1 < S ? Lcx[s + 1][l] : 0.0, hz_top = s + 1 < S ? Lhz[s + 1][l] : 0.0;
+  if (!act) return;
+  double* __restrict__ Wi = F.Wi + ij;
+  double* __restrict__ We = F.We + ij;
+  if (s == 0) {
+    Wi[0] = 0.0;
+    We[0] = 0.0;
+    Wi[(long)N * n2] = 0.0;
+    We[(long)N * n2] = 0.0;
+  }
+#pragma unroll
+  for (int q = 0; q < kOmR; q++) {
+    const int k = c0 + q;
+    double w = wk[q] - wrk * (zk[q] - zw0);
+    const double cx_up = q + 1 < n ? cx[q + 1 < kOmR ? q + 1 : kOmR - 1] : cx_top;
+    const double hz_up = q + 1 < n ? hz[q + 1 < kOmR ? q + 1 : kOmR - 1] : hz_top;
+    const double c2d = dmax(cx[q], cx_up);
+    const double dh = dmin(hz[q], hz_up);
+    const double cw_max = cu_max * dh - c2d * CX0;
+    double we;
+    if (cw_max > 0.0) {
+      const double cw_max2 = cw_max * cw_max;
+      const double cw_min = cw_max * cmnx_ratio;
+      const double cw = fabs(w) * CX0;
+      double cff;
+      if (cw < cw_min) cff = cw_max2;
+      else if (cw < cutoff * cw_max) cff = cw_max2 + r4cmx * ((cw - cw_min) * (cw - cw_min));
+      else cff = cw_max * cw;
+      we = cw_max2 * w / cff;
+      w = w - we;
+    } else {
+      we = 0.0;
+    }
+    if (q < n && k <= N - 1) {
+      const long o1 = (long)k * n2;
+      We[o1] = we;
+      Wi[o1] = w;
+    }
+  }
+}
+
 // Closed-edge copies of We/Wi into the boundary ghost row (omega.F:171-232).
 __global__ void k_omega_edges(Dev d) {
   const Bounds& b = d.b;
@@ -408,7 +521,14 @@ void launch_omega(const Dev& d, hipStream_t s, const Tlev& t) {
   Range R{b.istr, b.iend, b.jstr, b.jend};
   launch_rim_first(
       d, s, R, ExchList{{d.f.We, d.f.Wi}, {b.N + 1, b.N + 1}, 2},
-      [&](const Range& r) { hipLaunchKernelGGL(k_omega, grid_of(r), dim3(kBX, kBY), 0, s, d, r, dtau); },
+      [&](const Range& r) {
+        // the segment form for full-width ranges (rim strips keep k_omega)
+        if (d.p.omega_seg && b.N <= kSegRows * kSegMaxS && r.i1 - r.i0 + 1 >= 32)
+          hipLaunchKernelGGL(k_omega_seg, dim3((r.i1 - r.i0 + kSegCW) / kSegCW, r.j1 - r.j0 + 1), dim3(kCX, seg_waves(b.N)),
+                             0, s, d, r, dtau);
+        else
+          hipLaunchKernelGGL(k_omega, grid_of(r), dim3(kBX, kBY), 0, s, d, r, dtau);
+      },
       [&] {
         if (b.west_edge || b.east_edge || b.south_edge || b.north_edge) {
           const int n = 2 * (b.jend - b.jstr + 1) + 2 * (b.iend - b.istr + 1) + 4;
