@@ -351,3 +351,23 @@ def test_chain_kernels_bitwise_equal_column_sweeps(case, routine, outs, monkeypa
     b = _routine_fields(cfg, routine, outs, {"ROMS_GPU_CHAIN": "0"}, monkeypatch)
     for n in outs:
         assert np.array_equal(a[n], b[n]), n
+
+
+@pytest.mark.parametrize("grp", ["1", "2"])
+def test_tile_group_order_bitwise(grp, monkeypatch):
+    """ROMS_GPU_TILE_GRP re-orders the tiles of the hoisted per-level kernels
+    (h_tile: y fastest inside groups of grp x-tiles, a narrower last group);
+    every tile is still computed once: 4 steps equal the plain order bitwise.
+    152 x 40 columns give 3 x-tiles (one full group of 2 and a remainder)."""
+    cfg = basin_cfg(LLm=150, MMm=40, N=8, nonlin=True, sizex=300e3)
+    out = []
+    for env in ("0", grp):
+        monkeypatch.setenv("ROMS_GPU_TILE_GRP", env)
+        m = romsgpu.Model.from_case(cfg.case_id, cfg.LLm, cfg.MMm, cfg.N, cfg.NT, salinity=bool(cfg.salinity),
+                                    nonlin_eos=bool(cfg.nonlin_eos), dt=cfg.dt, ndtfast=cfg.ndtfast,
+                                    sizex=cfg.sizex, sizey=cfg.sizey)
+        m.step(4)
+        out.append({n: m.get(n) for n in ("zeta", "ubar", "vbar", "u", "v", "t", "rufrc", "rvfrc")})
+        m.close()
+    for n in out[0]:
+        assert np.array_equal(out[0][n], out[1][n]), n

@@ -71,7 +71,7 @@ struct TracerWinN {
 };
 template <int NTT, int TY>
 __global__ void __launch_bounds__(kBX * TY) k_pre_tracer_h1(Dev d, Range R, PreCoef c, int nstp, int nnew, int nrhs) {
-  const uint3 bI = xcd_tile();
+  const uint3 bI = h_tile(d.p.tile_grp);
   __shared__ TracerWinN<NTT, TY> W;
   const Bounds& b = d.b;
   const Fields& F = d.f;
@@ -323,7 +323,7 @@ __global__ void __launch_bounds__(256) k_uv_horiz(Dev d, Range R, int nrhs, UVBo
 // block.  Bit-identical.
 template <int TY>
 __global__ void __launch_bounds__(kBX * TY) k_uv_horiz1(Dev d, Range R, int nrhs, UVBounds ub, int up) {
-  const uint3 bI = xcd_tile();
+  const uint3 bI = h_tile(d.p.tile_grp);
   constexpr int NW = kUVW * (TY + 4);
   __shared__ double sU[NW], sV[NW], sFU[NW], sFV[NW];
   const Bounds& b = d.b;

@@ -114,7 +114,7 @@ constexpr int kPQ = (kPXN + kPYN + kBX * kBY - 1) / (kBX * kBY);
 template <bool FUSE>
 __global__ void __launch_bounds__(256) k_prsgrd_uv(Dev d, Range R, int split, int imin, int imax, int jmin, int jmax,
                                                    UVBounds ub, int up, int nrhs) {
-  const uint3 bI = xcd_tile();
+  const uint3 bI = h_tile(d.p.tile_grp);
   // one LDS block: the raw window, the elementary differences and the
   // harmonic means (and, FUSE, the u/v window after them)
   constexpr int kPL = 3 * kPWN + 4 * kPXN + 4 * kPYN;

@@ -48,7 +48,7 @@ struct TracerWinS {
 };
 template <int NTT, int TY>
 __global__ void __launch_bounds__(kBX * TY) k_step3d_t_h1(Dev d, Range R, int nnew, int nrhs) {
-  const uint3 bI = xcd_tile();
+  const uint3 bI = h_tile(d.p.tile_grp);
   __shared__ TracerWinS<NTT, TY> W;
   const Bounds& b = d.b;
   const Fields& F = d.f;

@@ -48,6 +48,7 @@ struct Params {
   int chain_dirz;   // chain kernels (set_HUV1, uv2): one direction per block (ROMS_GPU_CHAIN_DIRZ=0: both in turn)
   int prs_fuse_uv;  // whole steps: horizontal momentum r.h.s. inside prsgrd (ROMS_GPU_PRS_UV=0: separate)
   int h_ty;       // tile rows of the hoisted horizontal kernels: 4 or 8 (ROMS_GPU_HTY)
+  int tile_grp;   // h_tile group width of the hoisted per-level kernels (ROMS_GPU_TILE_GRP; 0: xcd_tile order)
   int omega_seg;  // omega: segment form k_omega_seg, one read of each input (ROMS_GPU_OMEGA_SEG=0: two-pass k_omega)
   int preuv_lds;  // k_pre_uv_seg: u(indx) stored and u(nstp)/u(indx) combined in the spline phase (ROMS_GPU_PREUV_LDS=0: reloads)
   int seg_jrows;  // rows j per block of the momentum segment solvers (1..kSegJMax; ROMS_GPU_SEG_JROWS)
@@ -157,6 +158,31 @@ __device__ __forceinline__ uint3 xcd_tile() {
   t.x = logical % gx;
   t.y = (logical / gx) % gy;
   t.z = logical / (gx * gy);
+  return t;
+}
+
+// Per-level horizontal kernels with halo windows: xcd_tile()'s sequence
+// re-ordered within each level (z) so that y runs fastest inside groups of
+// grp x-tiles (grp <= 0: plain xcd_tile order).  The tiles resident on one
+// XCD then cover a grp-wide strip of consecutive rows, whose shared halo
+// rows (j-neighbours) and halo lines (i-neighbours inside the group) are
+// fetched by neighbours close together in time.
+__device__ __forceinline__ uint3 h_tile(int grp) {
+  uint3 t = xcd_tile();
+  if (grp <= 0) return t;
+  const unsigned gx = gridDim.x, gy = gridDim.y;
+  const unsigned L = t.x + gx * t.y;
+  const unsigned G = (unsigned)grp < gx ? (unsigned)grp : gx;
+  const unsigned nfull = gx / G, inf = nfull * G * gy;
+  if (L < inf) {
+    const unsigned rem = L % (G * gy);
+    t.x = (L / (G * gy)) * G + rem % G;
+    t.y = rem / G;
+  } else {
+    const unsigned Gl = gx - nfull * G, rem = L - inf;
+    t.x = nfull * G + rem % Gl;
+    t.y = rem / Gl;
+  }
   return t;
 }
 
