@@ -425,7 +425,7 @@ __device__ __forceinline__ void pre_uv_col(const Dev& d, int i, int j, int dir, 
   uv_vert_flux_lds<true>(d, ij, nrhs, dir, A, B);
 #endif
   double* Uall = dir == 0 ? F.u : F.v;
-  double* __restrict__ rr = (dir == 0 ? F.ru : F.rv) + ij;
+  const double* __restrict__ rr = (dir == 0 ? F.ru : F.rv) + ij;
   const double* __restrict__ Ustp = Uall + (long)(nstp - 1) * b.n3 + ij;
   double* __restrict__ Uidx = Uall + (long)(indx - 1) * b.n3 + ij;
   double* __restrict__ Unew = Uall + (long)(nnew - 1) * b.n3 + ij;
@@ -434,11 +434,12 @@ __device__ __forceinline__ void pre_uv_col(const Dev& d, int i, int j, int dir, 
   const double* __restrict__ Wi = F.Wi + ij;
   const double sstr = dir == 0 ? F.sustr[ij] : F.svstr[ij];
   const double DC0 = c.dtau * 0.25 * (F.pm[ij] + F.pm[ij - s]) * (F.pn[ij] + F.pn[ij - s]);
-  // DC(k) before elimination; also stores u(indx) = Hz*u(nstp) and the final ru
+  // DC(k) before elimination; also stores u(indx) = Hz*u(nstp).  The updated
+  // ru(k) is dead after pre_step3d -- the corrector's prsgrd assigns ru before
+  // any read (prsgrd.F:293) -- so it is not stored (as in k_pre_uv_seg)
   auto DCinit = [&](int k, double hbk, double hbkm) {
     const long o = (long)(k - 1) * n2;
     const double r = uv_rr_update(rr[o], A, k);
-    rr[o] = r;
     const double us = Ustp[o];
     const double v = 0.5 * (hbk + hbkm) * (c.cf_stp * us + c.cf_bak * Uidx[o]) + DC0 * r;
     Uidx[o] = 0.5 * (Hz[o] + Hz[o - s]) * us;
@@ -458,8 +459,8 @@ __device__ __forceinline__ void pre_uv_col(const Dev& d, int i, int j, int dir, 
   A[N] = DCk1;
   B[N - 1] = CFk;
   // Forward elimination, levels N-1..2.  Iteration k reads level k-1 of
-  // Hb/Hf/Akv/Wi and level k of ru/u/Hz, and stores ru(k) and u(indx)(k).
-  // The compiler cannot prove the ru/u stores of level k miss the loads of
+  // Hb/Hf/Akv/Wi and level k of ru/u/Hz, and stores u(indx)(k).
+  // The compiler cannot prove the u stores of level k miss the loads of
   // the levels below (same arrays, offsets n2 apart), so it issues no load
   // ahead of a store; a ring of kPF iterations' raw loads, refilled before
   // each iteration's stores, keeps kPF levels of loads in flight.  At
@@ -479,7 +480,6 @@ __device__ __forceinline__ void pre_uv_col(const Dev& d, int i, int j, int dir, 
     const double CFl = cff * (FCl + fmax0(WCl));
     const long o = lev(k);
     const double r = uv_rr_update(v.r, A, k);
-    rr[o] = r;
     const double dci = 0.5 * (hbK + hbKm) * (c.cf_stp * v.us + c.cf_bak * v.ui) + DC0 * r;
     Uidx[o] = 0.5 * (v.hz + v.hzs) * v.us;
     const double DCk = cff * (dci + DCk1 * (FCk - fmin0(WCk)));
