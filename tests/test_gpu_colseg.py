@@ -136,7 +136,7 @@ def test_register_column_kernels_bitwise(lmd):
 
 
 @pytest.mark.parametrize("case", ["n50", "n100"])
-@pytest.mark.parametrize("switch", ["ROMS_GPU_PREUV_LDS", "ROMS_GPU_OMEGA_SEG"])
+@pytest.mark.parametrize("switch", ["ROMS_GPU_PREUV_LDS", "ROMS_GPU_OMEGA_SEG", "ROMS_GPU_UV1_LDS"])
 def test_seg_variants_bitwise(case, switch, monkeypatch):
     """Variants that keep the reference's operations and order, so 6 steps
     equal the plain forms bitwise:
@@ -144,7 +144,10 @@ def test_seg_variants_bitwise(case, switch, monkeypatch):
       cf_stp*u(nstp) + cf_bak*u(indx) and u(indx) = Hz*u(nstp) in its spline
       phase and keeps them in LDS instead of reloading u and Hz later;
     - k_omega_seg (ROMS_GPU_OMEGA_SEG, default) reads each input once and runs
-      the partial sums of the divergence as one chain through the waves."""
+      the partial sums of the divergence as one chain through the waves;
+    - k_uv1_seg<true> (ROMS_GPU_UV1_LDS, default) keeps the spline phase's Hz
+      pairs in LDS for the viscosity rows and chains the rufrc sum through
+      the waves in k order."""
     cfg = seg_cfg(case)
     out = []
     for env in ("0", "1"):

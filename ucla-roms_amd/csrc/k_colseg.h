@@ -236,11 +236,12 @@ __device__ __forceinline__ void spline_fc_seg(const SegSpan& sg, int N, SegXchg&
 // SPLINE_UV advective flux of a u (dir 0) / v (dir 1) column at interfaces
 // r = c0-1+q, q = 0..n (0 at the bottom and the surface): FC(r) * 0.5 * the
 // 4-point We average with the reference's masked curvature correction.
-// row(q, L, hz, hzm, u) is called in the load phase for q = 1..KR-1 (cells
-// c0..c0+KR-2, clamped; the rows q > n are dead) with the column's Hz, its
-// (i-1)/(j-1) neighbour's Hz and u(nrhs) there, unconditionally (a branch on
-// n would split the straight-line loads).  k_pre_uv_seg forms its u(indx)
-// terms from them.  Without UV_ADV the hook is not called.
+// row(q, L, hz, hzm, u) is called in the load phase for q = 0..KR (cells
+// c0-1+q clamped to 1..N; rows outside the segment are dead) with the
+// column's Hz, its (i-1)/(j-1) neighbour's Hz and u(nrhs) there (0 at
+// q = KR), unconditionally (a branch on n would split the straight-line
+// loads).  k_pre_uv_seg forms its u(indx) terms from them, k_uv1_seg keeps
+// the Hz pairs for its viscosity rows.  Without UV_ADV the hook is not called.
 struct NoSplineRow {
   __device__ __forceinline__ void operator()(int, long, double, double, double) const {}
 };
@@ -267,7 +268,7 @@ __device__ __forceinline__ void uv_spline_seg(const Dev& d, const SegSpan& sg, S
     const double h0 = Hz[L], h1 = Hz[L - s];
     dc[q] = 0.5625 * (h0 + h1) - 0.0625 * (Hz[L + s] + Hz[L - 2 * s]);
     if (q < KR) uu[q] = Uv[L];
-    if (q >= 1 && q < KR) row(q, L, h0, h1, uu[q]);
+    row(q, L, h0, h1, q < KR ? uu[q] : 0.0);
     // groups of kSegLoadGroup rows: their loads issue together, the next
     // group's wait (without the barrier all 5 (KR+1) loads were hoisted and spilled)
     if (q % kSegLoadGroup == kSegLoadGroup - 1) __builtin_amdgcn_sched_barrier(0);

@@ -633,8 +633,10 @@ __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_pre_uv_seg(Dev d, R
   if constexpr (kLds) {
     const double* __restrict__ Uix = Uall + (long)(indx - 1) * b.n3 + ij;
     uv_spline_seg<KR>(d, sg, X, ij, nrhs, dir, fl, [&](int q, long L, double h0, double h1, double u) {
-      Sb[(q - 1) * nthr] = c.cf_stp * u + c.cf_bak * Uix[L];
-      Su[(q - 1) * nthr] = 0.5 * (h0 + h1) * u;
+      if (q >= 1 && q < KR) {   // cells c0..c0+KR-2 (q is a constant of the unrolled load loop)
+        Sb[(q - 1) * nthr] = c.cf_stp * u + c.cf_bak * Uix[L];
+        Su[(q - 1) * nthr] = 0.5 * (h0 + h1) * u;
+      }
     });
   } else {
     uv_spline_seg<KR>(d, sg, X, ij, nrhs, dir, fl);

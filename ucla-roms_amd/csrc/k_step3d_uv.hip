@@ -244,11 +244,23 @@ __global__ void __launch_bounds__(64, 2) k_uv1_reg(Dev d, Range R, int nnew, int
 // rows of uv1_col; the final ru(k) of every level go to LDS, from where the
 // first segment forms rufrc/rvfrc in the reference's k = 1..N order. ----
 // ru(k) of the block's columns for rufrc: dynamic LDS, level k-1 of lane
-// slot l at roms_smem[(k-1)*ncol + l], ncol = kSegCW*blockDim.z
+// slot l at roms_smem[(k-1)*ncol + l], ncol = kSegCW*blockDim.z.
+//
+// kLds (UV_ADV): the spline phase's Hz loads serve the viscosity rows too --
+// the Hz of the column and of its (i-1)/(j-1) neighbour at the segment's
+// cells c0-1..c0+KR-1, exactly the levels the viscosity rows read -- kept in
+// dynamic LDS ([2][KR+1][threads], 123 KB at N = 100) instead of reloaded
+// (at C3 these reloads missed L2: 2 of the v column's 17 array passes).  The
+// ru(k) for rufrc then stay in the lane's registers and the sum runs as a
+// chain through the waves in k order (wave s adds its levels to wave s-1's
+// running sum, handed over in LDS between barriers): the reference's
+// operations in its order, bit-identical.
+template <bool kLds>
 __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_uv1_seg(Dev d, Range R, int nnew, int nrhs) {
   const uint3 bI = seg_tile(d.p.seg_order, d.p.seg_xg);
   __shared__ SegXchg X;
-  double* const Sr = roms_smem;   // (see above)
+  __shared__ double Lf[kLds ? kSegMaxS : 1][kSegCW * kSegJMax];   // kLds: rufrc running sums
+  double* const Sr = roms_smem;   // !kLds (see above)
   constexpr int KR = kSegRows + 1;
   const Bounds& b = d.b;
   const Fields& F = d.f;
@@ -263,8 +275,19 @@ __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_uv1_seg(Dev d, Rang
   const long n2 = b.n2, ij = IJ(b, col.i, col.j), s = dir == 0 ? 1 : b.nx2;
   const int c0 = sg.c0, n = sg.n;
   auto cell = [&](int k) { return (long)(min(max(k, 1), N) - 1) * n2; };   // rho level k (clamped)
+  const int nthr = (int)(blockDim.x * blockDim.y * blockDim.z);
+  const int tid = (int)(threadIdx.x + blockDim.x * (threadIdx.y + blockDim.y * threadIdx.z));
+  double* const Sh = roms_smem + tid;                             // kLds: Hz(c0-1+q) at Sh[q*nthr]
+  double* const Shm = roms_smem + (long)(KR + 1) * nthr + tid;    //       its neighbour's at Shm[q*nthr]
   double fl[KR];
-  uv_spline_seg<KR>(d, sg, X, ij, nrhs, dir, fl);
+  if constexpr (kLds) {
+    uv_spline_seg<KR>(d, sg, X, ij, nrhs, dir, fl, [&](int q, long, double h0, double h1, double) {
+      Sh[q * nthr] = h0;
+      Shm[q * nthr] = h1;
+    });
+  } else {
+    uv_spline_seg<KR>(d, sg, X, ij, nrhs, dir, fl);
+  }
   __builtin_amdgcn_sched_barrier(0);   // the viscosity phase's loads stay out of the spline phase
   double* __restrict__ Un = (dir == 0 ? F.u : F.v) + (long)(nnew - 1) * b.n3 + ij;
   const double* __restrict__ rr = (dir == 0 ? F.ru : F.rv) + ij;
@@ -274,32 +297,47 @@ __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_uv1_seg(Dev d, Rang
   const double sstr = dir == 0 ? F.sustr[ij] : F.svstr[ij];
   const double DC0 = dt * 0.25 * (F.pm[ij] + F.pm[ij - s]) * (F.pn[ij] + F.pn[ij - s]);
   // right-hand sides first: ru(k) with the vertical advection (uv_rr_update)
-  // to LDS for rufrc -- the updated ru itself is dead after this routine (the
-  // next step's prsgrd overwrites it, prsgrd.F:293), so it is not stored --
-  // and dd = u(nnew) + DC0*ru
-  double rhs[KR];
+  // for rufrc (LDS, or kLds: registers) -- the updated ru itself is dead
+  // after this routine (the next step's prsgrd overwrites it, prsgrd.F:293),
+  // so it is not stored -- and dd = u(nnew) + DC0*ru
+  // (kLds: only ru(k) here; dd is formed in the elimination rows, u(nnew)
+  // loaded there -- one register array less)
+  double rhs[kLds ? 1 : KR], rk[kLds ? KR : 1];
 #pragma unroll
   for (int p = 0; p < KR; p++) {
     const int k = c0 + p;
     const long o = cell(k);
     const double r = k == 1 ? rr[o] - fl[1] : rr[o] - fl[p + 1 < KR ? p + 1 : KR - 1] + fl[p];
-    if (p < n) Sr[(k - 1) * ncol + sg.l] = r;
-    const double v = Un[o] + DC0 * r;
-    rhs[p] = k == N ? v + dt * sstr : v;
+    if constexpr (kLds) {
+      rk[p] = r;
+    } else {
+      if (p < n) Sr[(k - 1) * ncol + sg.l] = r;
+      const double v = Un[o] + DC0 * r;
+      rhs[p] = k == N ? v + dt * sstr : v;
+    }
   }
-  double hz[KR + 1], hzm[KR + 1];   // Hz(c0-1+q) of the column and of its (i-1) / (j-1) neighbour
+  double hz[kLds ? 1 : KR + 1], hzm[kLds ? 1 : KR + 1];   // !kLds: Hz(c0-1+q) of the column and of its (i-1) / (j-1) neighbour
+  if constexpr (!kLds) {
 #pragma unroll
-  for (int q = 0; q < KR + 1; q++) {
-    const long L = cell(c0 - 1 + q);
-    hz[q] = Hz[L];
-    hzm[q] = Hz[L - s];
+    for (int q = 0; q < KR + 1; q++) {
+      const long L = cell(c0 - 1 + q);
+      hz[q] = Hz[L];
+      hzm[q] = Hz[L - s];
+    }
   }
+  // kLds: the LDS reads go through an opaque offset, so the compiler cannot
+  // forward the spline phase's stored values and keep them in registers
+  // across the spline solve instead (it did: 256 VGPRs and spills)
+  int tl = tid;
+  __asm__ volatile("" : "+v"(tl));
+  auto HZ = [&](int q) { if constexpr (kLds) return roms_smem[tl + q * nthr]; else return hz[q]; };
+  auto HZM = [&](int q) { if constexpr (kLds) return roms_smem[(KR + 1 + q) * nthr + tl]; else return hzm[q]; };
   auto fcw = [&](int q, double& fc, double& wc) {   // interface c0-1+q (0 at the bottom and the surface)
     const int r = c0 - 1 + q;
     const long w = (long)min(max(r, 1), N - 1) * n2;
     const bool in = r > 0 && r < N;
     const int qa = q + 1 < KR + 1 ? q + 1 : KR;
-    const double f = 2.0 * dt * (Akv[w] + Akv[w - s]) / (hz[qa] + hzm[qa] + hz[q] + hzm[q]);
+    const double f = 2.0 * dt * (Akv[w] + Akv[w - s]) / (HZ(qa) + HZM(qa) + HZ(q) + HZM(q));
     const double wv = DC0 * 0.5 * (Wi[w] + Wi[w - s]);
     fc = in ? f : 0.0;
     wc = in ? wv : 0.0;
@@ -315,35 +353,68 @@ __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_uv1_seg(Dev d, Rang
     const int k = c0 + p;
     a = -(fcl + fmax0(wcl));
     cc = -(fcu - fmin0(wcu));
-    const double b1 = 0.5 * (hz[p + 1] + hzm[p + 1]) + 0.5 * dt * (rD + rDm) + fcu + fmax0(wcu);
-    const double bk = 0.5 * (hz[p + 1] + hzm[p + 1]) + fcl - fmin0(wcl) + fcu + fmax0(wcu);
+    const double b1 = 0.5 * (HZ(p + 1) + HZM(p + 1)) + 0.5 * dt * (rD + rDm) + fcu + fmax0(wcu);
+    const double bk = 0.5 * (HZ(p + 1) + HZM(p + 1)) + fcl - fmin0(wcl) + fcu + fmax0(wcu);
     bb = k == 1 ? b1 : bk;
-    dd = rhs[p];
+    if constexpr (kLds) {
+      const double v = Un[cell(k)] + DC0 * rk[p];
+      dd = k == N ? v + dt * sstr : v;
+    } else {
+      dd = rhs[p];
+    }
     fcl = fcu; wcl = wcu;
   });
   double xL, xR;
   T.couple(sg, n, X, xL, xR);   // its barrier also publishes Sr
   T.solve(n, xL, xR);
-  if (!act) return;
+  const double dmdn = dir == 0 ? F.dm_u[ij] * F.dn_u[ij] : F.dm_v[ij] * F.dn_v[ij];
+  if constexpr (kLds) {
+    // rufrc = ru(1) + dmdn*(sstr - r_D*u(1)) + ru(2) + ... + ru(N), wave by wave
+    const int S = sg.S, sl = sg.l;
+    for (int t = 0; t < S; t++) {
+      if (sg.s == t) {
+        double frc;
+        if (t == 0) frc = rk[0] + dmdn * (sstr - 0.5 * (rDm + rD) * T.D[0]);
+        else frc = Lf[t - 1][sl] + rk[0];
 #pragma unroll
-  for (int p = 0; p < KR; p++)
-    if (p < n) Un[cell(c0 + p)] = T.D[p] * 0.5 * (hz[p + 1] + hzm[p + 1]);
-  if (sg.s == 0) {
-    const double dmdn = dir == 0 ? F.dm_u[ij] * F.dn_u[ij] : F.dm_v[ij] * F.dn_v[ij];
-    double frc = Sr[sg.l] + dmdn * (sstr - 0.5 * (rDm + rD) * T.D[0]);
-    for (int k = 2; k <= N; k++) frc = frc + Sr[(k - 1) * ncol + sg.l];
-    if (dir == 0) F.rufrc[ij] = frc;
-    else F.rvfrc[ij] = frc;
+        for (int p = 1; p < KR; p++) frc = p < n ? frc + rk[p] : frc;
+        Lf[t][sl] = frc;
+      }
+      __syncthreads();
+    }
+    if (!act) return;
+#pragma unroll
+    for (int p = 0; p < KR; p++)
+      if (p < n) Un[cell(c0 + p)] = T.D[p] * 0.5 * (HZ(p + 1) + HZM(p + 1));
+    if (sg.s == 0) {
+      if (dir == 0) F.rufrc[ij] = Lf[S - 1][sl];
+      else F.rvfrc[ij] = Lf[S - 1][sl];
+    }
+  } else {
+    if (!act) return;
+#pragma unroll
+    for (int p = 0; p < KR; p++)
+      if (p < n) Un[cell(c0 + p)] = T.D[p] * 0.5 * (hz[p + 1] + hzm[p + 1]);
+    if (sg.s == 0) {
+      double frc = Sr[sg.l] + dmdn * (sstr - 0.5 * (rDm + rD) * T.D[0]);
+      for (int k = 2; k <= N; k++) frc = frc + Sr[(k - 1) * ncol + sg.l];
+      if (dir == 0) F.rufrc[ij] = frc;
+      else F.rvfrc[ij] = frc;
+    }
   }
 }
 
 void setup_column_kernels_uv1(size_t bytes) {
   (void)hipFuncSetAttribute((const void*)k_uv1<ColLds>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
-// the ru levels of k_uv1_seg's rows-j blocks (up to kSegJMax rows, N <= kSegRows*kSegMaxS)
+// the ru levels of k_uv1_seg's rows-j blocks (up to kSegJMax rows, N <= kSegRows*kSegMaxS);
+// kLds: the Hz pairs of every thread's KR+1 rows
+static size_t uv1_seg_lds_bytes(unsigned nthr) { return (size_t)2 * (kSegRows + 2) * nthr * sizeof(double); }
 void setup_uv1_seg() {
-  (void)hipFuncSetAttribute((const void*)k_uv1_seg, hipFuncAttributeMaxDynamicSharedMemorySize,
+  (void)hipFuncSetAttribute((const void*)k_uv1_seg<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)((size_t)kSegRows * kSegMaxS * kSegCW * kSegJMax * sizeof(double)));
+  (void)hipFuncSetAttribute((const void*)k_uv1_seg<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)uv1_seg_lds_bytes(kSegBlock * kSegJMax));
 }
 
 void launch_step3d_uv1(const Dev& d, hipStream_t s, const Tlev& t, bool uv_done) {
@@ -355,9 +426,13 @@ void launch_step3d_uv1(const Dev& d, hipStream_t s, const Tlev& t, bool uv_done)
   if ((d.p.colreg & 1) && b.N == 50)
     hipLaunchKernelGGL(k_uv1_reg<50>, g, dim3(kCX), col_lds_bytes(1, 50), s, d, R, t.nnew, t.nrhs);
   else if (d.p.colseg) {
+    const dim3 gs = seg_grid_of(R, 2, d.p.seg_jrows), bs(kCX, seg_waves(b.N), d.p.seg_jrows);
     ktimer_mark(s, kTimedUv1Seg, 0);
-    hipLaunchKernelGGL(k_uv1_seg, seg_grid_of(R, 2, d.p.seg_jrows), dim3(kCX, seg_waves(b.N), d.p.seg_jrows),
-                       (size_t)b.N * kSegCW * d.p.seg_jrows * sizeof(double), s, d, R, t.nnew, t.nrhs);
+    if (d.p.uv1_lds && d.p.uv_adv)
+      hipLaunchKernelGGL(k_uv1_seg<true>, gs, bs, uv1_seg_lds_bytes(bs.x * bs.y * bs.z), s, d, R, t.nnew, t.nrhs);
+    else
+      hipLaunchKernelGGL(k_uv1_seg<false>, gs, bs, (size_t)b.N * kSegCW * d.p.seg_jrows * sizeof(double), s, d, R,
+                         t.nnew, t.nrhs);
     ktimer_mark(s, kTimedUv1Seg, 1, 1);
   }
   else if (d.f.colscr)

@@ -49,6 +49,7 @@ struct Params {
   int prs_fuse_uv;  // whole steps: horizontal momentum r.h.s. inside prsgrd (ROMS_GPU_PRS_UV=0: separate)
   int h_ty;       // tile rows of the hoisted horizontal kernels: 4 or 8 (ROMS_GPU_HTY)
   int tile_grp;   // h_tile group width of the hoisted per-level kernels (ROMS_GPU_TILE_GRP; 0: xcd_tile order)
+  int uv1_lds;    // k_uv1_seg: Hz pairs kept in LDS from the spline phase, rufrc chained (ROMS_GPU_UV1_LDS=0: reloads)
   int omega_seg;  // omega: segment form k_omega_seg, one read of each input (ROMS_GPU_OMEGA_SEG=0: two-pass k_omega)
   int preuv_lds;  // k_pre_uv_seg: u(indx) stored and u(nstp)/u(indx) combined in the spline phase (ROMS_GPU_PREUV_LDS=0: reloads)
   int seg_jrows;  // rows j per block of the momentum segment solvers (1..kSegJMax; ROMS_GPU_SEG_JROWS)

@@ -565,6 +565,10 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     P.tile_grp = e ? atoi(e) : 0;
   }
   {
+    const char* e = getenv("ROMS_GPU_UV1_LDS");
+    P.uv1_lds = !(e && e[0] == '0');
+  }
+  {
     const char* e = getenv("ROMS_GPU_OMEGA_SEG");
     P.omega_seg = !(e && e[0] == '0');
   }
