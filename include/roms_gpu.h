@@ -153,6 +153,12 @@ int  roms_gpu_download(int field_id);    /* device -> host, ROMS_ALL allowed */
 /* direct synchronous copies without registration                            */
 int  roms_gpu_copy_in(int field_id, const double *src, long count);
 int  roms_gpu_copy_out(int field_id, double *dst, long count);
+/* ROMS_Hz_u / ROMS_Hz_v (set_HUV's cell heights, set_depth.F:220,227) are
+ * read by no routine of the step, only by extract_data.F:726.  roms_gpu_step
+ * stores them only while either is registered for transfer or the
+ * environment sets ROMS_GPU_HZ_UV=1 (2 array passes per step saved); after a
+ * step that did not, downloading or copying them out returns -5.  The
+ * routine roms_gpu_set_huv always stores them. */
 int  roms_gpu_sync(void);
 void *roms_gpu_stream(void);             /* hipStream_t the routines run on  */
 

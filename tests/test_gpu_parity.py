@@ -371,3 +371,30 @@ def test_tile_group_order_bitwise(grp, monkeypatch):
         m.close()
     for n in out[0]:
         assert np.array_equal(out[0][n], out[1][n]), n
+
+
+def test_hz_uv_stored_on_request(monkeypatch):
+    """Hz_u/Hz_v (set_depth.F:220,227) feed only extract_data.F; whole steps
+    skip their stores unless asked (ROMS_GPU_HZ_UV=1 or a registered host
+    mirror).  Asked: after 3 steps they equal the oracle's set_HUV values.
+    Not asked: reading them fails loudly instead of returning stale data, and
+    the prognostic state is bitwise the same either way."""
+    cfg = basin_cfg(LLm=40, MMm=32, N=10, nonlin=True)
+    out = {}
+    for env in ("1", "0"):
+        monkeypatch.setenv("ROMS_GPU_HZ_UV", env)
+        o, m = make_pair(cfg)
+        o.step(3)
+        m.step(3)
+        out[env] = {n: m.get(n) for n in ("zeta", "u", "v", "t", "FlxU", "FlxV")}
+        if env == "1":
+            check_fields(o, m, ["Hz_u", "Hz_v"], cfg.LLm, cfg.MMm, RTOL_ROUTINE)
+        else:
+            with pytest.raises(romsgpu.RomsGpuError, match="Hz_u/Hz_v"):
+                m.get("Hz_u")
+            m.set_HUV()   # the routine itself always stores them
+            m.sync()
+            assert np.isfinite(m.get("Hz_v")).all()
+        m.close()
+    for n in out["0"]:
+        assert np.array_equal(out["0"][n], out["1"][n]), n

@@ -58,7 +58,7 @@ void launch_set_depth(const Dev& d, hipStream_t s, const Tlev& t) {
 // ---------------------------------------------------------------------------
 // set_HUV_tile (set_depth.F:190-234)
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_set_huv(Dev d, Range R, int nrhs) {
+__global__ void __launch_bounds__(256) k_set_huv(Dev d, Range R, int nrhs, int huv) {
   ROMS_IJ_OR_RETURN(R)
   const Bounds& b = d.b;
   const Fields& F = d.f;
@@ -81,22 +81,25 @@ __global__ void __launch_bounds__(256) k_set_huv(Dev d, Range R, int nrhs) {
     if (du) {
       const double hzm = Hz[o - 1];
       FU[o] = 0.5 * (hz + hzm) * dnu * (U[o]);
-      HU[o] = 0.5 * (hz + hzm);
+      if (huv) HU[o] = 0.5 * (hz + hzm);
     }
     if (dv) {
       const double hzm = Hz[o - b.nx2];
       FV[o] = 0.5 * (hz + hzm) * dmv * (V[o]);
-      HV[o] = 0.5 * (hz + hzm);
+      if (huv) HV[o] = 0.5 * (hz + hzm);
     }
   }
 }
 
-void launch_set_huv(const Dev& d, hipStream_t s, const Tlev& t) {
+void launch_set_huv(const Dev& d, hipStream_t s, const Tlev& t, bool store_huv) {
   const Bounds& b = d.b;
   Range R{b.istrR < b.istr ? b.istrR : b.istr, b.iendR, b.jstrR < b.jstr ? b.jstrR : b.jstr, b.jendR};
   launch_rim_first(
       d, s, R, ExchList{{d.f.FlxU, d.f.FlxV}, {b.N, b.N}, 2},
-      [&](const Range& r) { hipLaunchKernelGGL(k_set_huv, grid_of(r), dim3(kBX, kBY), 0, s, d, r, t.nrhs); }, [] {});
+      [&](const Range& r) {
+        hipLaunchKernelGGL(k_set_huv, grid_of(r), dim3(kBX, kBY), 0, s, d, r, t.nrhs, (int)store_huv);
+      },
+      [] {});
 }
 
 // ---------------------------------------------------------------------------

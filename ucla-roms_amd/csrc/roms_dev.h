@@ -320,7 +320,8 @@ inline size_t col_smem_bytes(const Dev& d, int nslots) {
   return d.f.colscr ? 0 : (size_t)nslots * (d.b.N + 1) * 64 * sizeof(double);
 }
 void launch_set_depth(const Dev& d, hipStream_t s, const Tlev& t);
-void launch_set_huv(const Dev& d, hipStream_t s, const Tlev& t);
+// store_huv: also Hz_u/Hz_v (set_depth.F:220,227), read only by extract_data.F
+void launch_set_huv(const Dev& d, hipStream_t s, const Tlev& t, bool store_huv = true);
 void launch_set_huv1(const Dev& d, hipStream_t s, const Tlev& t);
 void launch_omega(const Dev& d, hipStream_t s, const Tlev& t);
 void launch_rho_eos(const Dev& d, hipStream_t s, const Tlev& t, int tidx);

@@ -51,6 +51,12 @@ struct Ctx {
   // is skipped.  Every entry that may change the state clears it
   // (REQUIRE_INIT); the read-only ones keep it (REQUIRE_INIT_RO).
   int rho_slot = 0;
+  // Hz_u/Hz_v (set_HUV's cell heights at u/v points) are read by no kernel of
+  // the step, only by the reference's extract_data.F:726: whole steps store
+  // them when the host registered either for transfer or set
+  // ROMS_GPU_HZ_UV=1; otherwise they go stale and reading them fails
+  bool hzuv_env = false;
+  bool hzuv_valid = true;
   bool rho_reuse = true;      // ROMS_GPU_RHO_REUSE=0 turns the skip off
   std::string err;
   // graph cache: key = (nstp, knew at step start)
@@ -338,7 +344,7 @@ namespace {
 // the roms_step sequence for one step whose indices are already set in *t
 // (nstp,nrhs=nstp,nnew=3 on entry); enqueues everything on g.s
 // rho_current: rho_eos(nrhs) is already current (g.rho_slot, see there)
-void enqueue_step(roms_tlev* t, bool rho_current) {
+void enqueue_step(roms_tlev* t, bool rho_current, bool store_huv) {
   const Dev& d = g.d;
   hipStream_t s = g.s;
   Tlev T = to_tlev(t);
@@ -348,7 +354,7 @@ void enqueue_step(roms_tlev* t, bool rho_current) {
   launch_bulk_flux(d, s, T.nrhs);   // set_forces (main.F:386): BULK_FRC only
   frc_step_phase(d, s, 1, pot);     // set_bry_all '1/2 fwd' + set_tides (main.F:389-394)
   if (!rho_current) TIMED(ROMS_R_RHO_EOS, launch_rho_eos(d, s, T, T.nrhs));
-  TIMED(ROMS_R_SET_HUV, launch_set_huv(d, s, T));
+  TIMED(ROMS_R_SET_HUV, launch_set_huv(d, s, T, store_huv));
   TIMED(ROMS_R_OMEGA, launch_omega(d, s, T));
   if (g.cfg.lmd_mixing) TIMED(ROMS_R_LMD_VMIX, launch_lmd_vmix(d, s, T, T.nstp));
   // the horizontal momentum r.h.s. of pre_step3d / step3d_uv1 rides in the
@@ -646,6 +652,11 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     if (r) return r;
     g.d.halo = &g.halo;
   }
+  {
+    const char* e = getenv("ROMS_GPU_HZ_UV");
+    g.hzuv_env = e && e[0] == '1';
+    g.hzuv_valid = true;
+  }
   const char* env = getenv("ROMS_GPU_NO_GRAPH");
   g.use_graphs = !(env && env[0] == '1') && halo_graph_safe(g.d.halo);
   env = getenv("ROMS_GPU_RHO_REUSE");
@@ -677,6 +688,13 @@ int roms_gpu_register(int id, double* host, long count) {
   return 0;
 }
 
+// Hz_u/Hz_v after whole steps that did not store them (see Global::hzuv_valid)
+static bool hzuv_readable(int id) {
+  if ((id != ROMS_Hz_u && id != ROMS_Hz_v) || g.hzuv_valid) return true;
+  g.err = "Hz_u/Hz_v are not maintained by whole steps unless registered for transfer or ROMS_GPU_HZ_UV=1 "
+          "(extract_data inputs, set_depth.F:220,227)";
+  return false;
+}
 static int xfer(int id, bool up) {
   if (id == ROMS_ALL) {
     for (int q = 0; q < ROMS_NFIELDS; q++)
@@ -688,6 +706,8 @@ static int xfer(int id, bool up) {
   }
   if (id < 0 || id >= ROMS_NFIELDS) { g.err = "bad field id"; return -1; }
   if (!g.f[id].host) { g.err = "field not registered"; return -1; }
+  if (!up && !hzuv_readable(id)) return -5;
+  if (up && (id == ROMS_Hz_u || id == ROMS_Hz_v)) g.hzuv_valid = true;
   const size_t nb = (size_t)g.f[id].count * sizeof(double);
   if (up) CHECK_HIP(hipMemcpyAsync(g.f[id].d, g.f[id].host, nb, hipMemcpyHostToDevice, g.s));
   else CHECK_HIP(hipMemcpyAsync(g.f[id].host, g.f[id].d, nb, hipMemcpyDeviceToHost, g.s));
@@ -700,6 +720,7 @@ int roms_gpu_download(int id) { REQUIRE_INIT_RO(); return xfer(id, false); }
 int roms_gpu_copy_in(int id, const double* src, long count) {
   REQUIRE_INIT();
   if (id < 0 || id >= ROMS_NFIELDS || count != g.f[id].count) { g.err = "roms_gpu_copy_in: bad field/size"; return -1; }
+  if (id == ROMS_Hz_u || id == ROMS_Hz_v) g.hzuv_valid = true;
   CHECK_HIP(hipMemcpyAsync(g.f[id].d, src, (size_t)count * sizeof(double), hipMemcpyHostToDevice, g.s));
   CHECK_HIP(hipStreamSynchronize(g.s));
   return 0;
@@ -707,6 +728,7 @@ int roms_gpu_copy_in(int id, const double* src, long count) {
 int roms_gpu_copy_out(int id, double* dst, long count) {
   REQUIRE_INIT_RO();
   if (id < 0 || id >= ROMS_NFIELDS || count != g.f[id].count) { g.err = "roms_gpu_copy_out: bad field/size"; return -1; }
+  if (!hzuv_readable(id)) return -5;
   CHECK_HIP(hipMemcpyAsync(dst, g.f[id].d, (size_t)count * sizeof(double), hipMemcpyDeviceToHost, g.s));
   CHECK_HIP(hipStreamSynchronize(g.s));
   REQUIRE_HALO_OK();
@@ -726,7 +748,7 @@ int roms_gpu_sync(void) {
     call;                             \
     return post_launch();             \
   }
-ROUTINE(roms_gpu_set_huv, launch_set_huv(g.d, g.s, T))
+ROUTINE(roms_gpu_set_huv, (launch_set_huv(g.d, g.s, T), g.hzuv_valid = true))
 ROUTINE(roms_gpu_omega, launch_omega(g.d, g.s, T))
 ROUTINE(roms_gpu_prsgrd, launch_prsgrd(g.d, g.s, T))
 ROUTINE(roms_gpu_pre_step3d, launch_pre_step3d(g.d, g.s, T))
@@ -946,17 +968,19 @@ int roms_gpu_step(roms_tlev* t) {
     }
   }
   const bool first = (t->iic == t->forw_start);
+  const bool store_huv = g.hzuv_env || g.f[ROMS_Hz_u].host != nullptr || g.f[ROMS_Hz_v].host != nullptr;
+  g.hzuv_valid = store_huv;
   if (!g.use_graphs || first) {
-    enqueue_step(t, rho_current);
+    enqueue_step(t, rho_current, store_huv);
     return post_launch();
   }
-  const long key = (long)t->nstp * 16 + t->knew + (rho_current ? 256 : 0);
+  const long key = (long)t->nstp * 16 + t->knew + (rho_current ? 256 : 0) + (store_huv ? 512 : 0);
   auto it = g.graphs.find(key);
   roms_tlev t0 = *t;
   if (it == g.graphs.end()) {
     hipGraph_t graph;
     CHECK_HIP(hipStreamBeginCapture(g.s, hipStreamCaptureModeThreadLocal));
-    enqueue_step(t, rho_current);
+    enqueue_step(t, rho_current, store_huv);
     CHECK_HIP(hipStreamEndCapture(g.s, &graph));
     hipGraphExec_t exec;
     CHECK_HIP(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
@@ -996,6 +1020,7 @@ int roms_gpu_init_sequence(roms_tlev* t) {
     return -4;
   }
   launch_set_huv(g.d, g.s, T);
+  g.hzuv_valid = true;
   launch_omega(g.d, g.s, T);
   launch_rho_eos(g.d, g.s, T, T.nrhs);
   return post_launch();
@@ -1180,7 +1205,9 @@ int roms_gpu_time_routine(int routine, int nsteps, roms_tlev* t, double* avg_ms,
     t->nfast = g.cfg.nfast;
     const int r = frc_step_prepare(g.s, g.d, g.cfg.dt, *t, g.err);   // in-step forcing, as roms_gpu_step
     if (r) { g.timed = -1; return r; }
-    enqueue_step(t, g.rho_reuse && g.rho_slot == t->nrhs);
+    const bool store_huv = g.hzuv_env || g.f[ROMS_Hz_u].host != nullptr || g.f[ROMS_Hz_v].host != nullptr;
+    g.hzuv_valid = store_huv;
+    enqueue_step(t, g.rho_reuse && g.rho_slot == t->nrhs, store_huv);
   }
   g.timed = -1;
   CHECK_HIP(hipStreamSynchronize(g.s));
