@@ -19,7 +19,7 @@ import json
 
 ROUTINE_OF = {
     "k_rho_eos_linear": "rho_eos", "k_rho_eos_split": "rho_eos", "k_set_huv": "set_HUV", "k_omega": "omega",
-    "k_omega_edges": "omega", "k_prsgrd_P": "prsgrd", "k_prsgrd_uv": "prsgrd", "k_pre_tracer_h": "pre_step3d",
+    "k_omega_edges": "omega", "k_omega_seg": "omega", "k_prsgrd_P": "prsgrd", "k_prsgrd_uv": "prsgrd", "k_pre_tracer_h": "pre_step3d",
     "k_pre_tracer_v": "pre_step3d", "k_rd": "pre_step3d", "k_pre_uv": "pre_step3d", "k_set_huv1": "set_HUV1",
     "k_uv1": "step3d_uv1", "k_visc3d": "visc3d", "k_s2d_zeta": "step2d", "k_s2d_mom": "step2d",
     "k_s2d_zetabc": "step2d", "k_s2d_fb": "step2d", "k_visc3d_frc": "visc3d", "k_s2d_edges": "step2d", "k_s2d_last": "step2d", "k_set_depth": "step2d",
