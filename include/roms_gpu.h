@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define ROMS_GPU_ABI_VERSION 10
+#define ROMS_GPU_ABI_VERSION 11
 #define ROMS_MAX_FAST 288
 
 /* Subdomain geometry of this rank: param.F / dimensions.F / mpi_setup.F:39-210 */
@@ -39,8 +39,9 @@ typedef struct roms_dims {
 
 /* LMD switch bits of roms_cfg.lmd_mixing / roms_case.lmd_mixing (cppdefs.opt).
  * Accepted sets are the ones the reference builds and runs correctly:
- *   0 (no LMD_MIXING), or MIXING|KPP|BKPP plus any of RIMIX, NONLOCAL and
- *   CONVEC (CONVEC needs RIMIX).  KPP without BKPP does not compile in the
+ *   0 (no LMD_MIXING), or MIXING|KPP|BKPP plus any of RIMIX, NONLOCAL,
+ *   CONVEC (CONVEC needs RIMIX) and DDMIX (double diffusion, lmd_vmix.F:279-
+ *   360; needs SALINITY for t(..,isalt)).  KPP without BKPP does not compile in the
  *   reference (lmd_kpp.F:178 reads hbbl, imported only under LMD_BKPP,
  *   lmd_kpp.F:37-39); MIXING without KPP/BKPP filters Kv(0), Kv(N) that are
  *   never set (lmd_vmix.F:405-420); CONVEC without RIMIX tests an unset Rig
@@ -52,8 +53,9 @@ typedef struct roms_dims {
 #define ROMS_LMD_RIMIX    8
 #define ROMS_LMD_CONVEC   16
 #define ROMS_LMD_NONLOCAL 32
-#define ROMS_LMD_ALL      63
+#define ROMS_LMD_ALL      63   /* MIXING..NONLOCAL: the Pipes_ana set (no DDMIX) */
 #define ROMS_LMD_ICELAND  47   /* all but LMD_CONVEC */
+#define ROMS_LMD_DDMIX    64
 
 /* cppdefs.opt switches and run scalars (scalars.F, read_inp_mod.F, set_weights.F).
  * Switches that need no flag here: MASKING is carried by the mask arrays

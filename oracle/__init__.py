@@ -14,7 +14,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB = os.path.join(_HERE, "liboracle.so")
 CASE_FILAMENT, CASE_BASIN, CASE_PIPES, CASE_RIVERS = 0, 1, 2, 3
-LMD_RIMIX, LMD_CONVEC, LMD_NONLOCAL = 8, 16, 32
+LMD_RIMIX, LMD_CONVEC, LMD_NONLOCAL, LMD_DDMIX = 8, 16, 32, 64
 LMD_ALL = 63       # LMD_MIXING+KPP+BKPP+RIMIX+CONVEC+NONLOCAL (tests/Pipes_ana/cppdefs.opt)
 LMD_ICELAND = 47   # all but LMD_CONVEC (Examples/Iceland/Iceland_parent/cppdefs.opt:41-46)
 

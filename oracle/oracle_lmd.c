@@ -3,8 +3,8 @@
  *
  * Plain-C restatement of the LMD/KPP vertical mixing of the reference for
  * the switch set of tests/Pipes_ana and the C3 basin (LMD_MIXING, LMD_KPP,
- * LMD_BKPP, LMD_RIMIX, LMD_CONVEC, LMD_NONLOCAL, SALINITY, MASKING; no
- * LMD_DDMIX, no BULK_FRC, no MERGE_OVERLAP, no LIMIT_UNSTABLE_ONLY):
+ * LMD_BKPP, LMD_RIMIX, LMD_CONVEC, LMD_NONLOCAL, LMD_DDMIX, SALINITY,
+ * MASKING; no MERGE_OVERLAP, no LIMIT_UNSTABLE_ONLY):
  *   or_swr_frac       lmd_swr_frac.F:13-88   (Jerlov type 1, at init)
  *   lmd_vmix_tile     lmd_vmix.F:31-433      (SMOOTH_RIG)
  *   lmd_kpp_tile      lmd_kpp.F:7-651        (INT_AT_RHO_POINTS, SMOOTH_HBL)
@@ -106,6 +106,45 @@ static void smooth2(or_state *S, double *w, int rmask_after) {
   }
 }
 
+/* LMD_DDMIX (lmd_vmix.F:95-101, 279-360): double-diffusive mixing added to
+ * Kt and Ks at w-level k from t(k), t(k+1) at tind and z_w(k) */
+static void ddmix(or_state *S, int i, int j, int k, int tind, double *kt, double *ks) {
+  const double A0 = +0.665157E-01, A1 = +0.170907E-01, A2 = -0.203814E-03, A3 = +0.298357E-05,
+               A4 = -0.255019E-07, B0 = +0.378110E-02, B1 = -0.846960E-04, C0 = -0.678662E-05,
+               D0 = +0.380374E-04, D1 = -0.933746E-06, D2 = +0.791325E-08, E0 = -0.164759E-06,
+               F0 = -0.251520E-11, G0 = +0.512857E-12, H0 = -0.302285E-13, Smean = 35.0;
+  const double lmd_nu = 1.5e-6, lmd_Rrho0 = 1.9, lmd_nuf = 10.0e-4, lmd_fdd = 0.7, lmd_tdd1 = 0.909,
+               lmd_tdd2 = 4.6, lmd_tdd3 = 0.54, lmd_sdd1 = 0.15, lmd_sdd2 = 1.85, lmd_sdd3 = 0.85, eps = 1.E-14;
+  const double t0 = TT(i, j, k, tind, 1), t1 = TT(i, j, k + 1, tind, 1);
+  const double s0 = TT(i, j, k, tind, 2), s1 = TT(i, j, k + 1, tind, 2);
+  const double Tt = 0.5 * (t0 + t1);
+  const double Ts = 0.5 * (s0 + s1) - Smean;
+  const double Tp = -ZW(i, j, k);
+  const double alfaobeta = A0 + Tt * (A1 + Tt * (A2 + Tt * (A3 + Tt * A4))) + Ts * (B0 + Tt * B1 + Ts * C0) +
+                           Tp * (D0 + Tt * (D1 + Tt * D2) + Ts * E0 + Tp * (Ts * F0 + Tt * Tt * G0 + Tp * H0));
+  const double ddDT = t1 - t0;
+  double ddDS = s1 - s0;
+  ddDS = copysign(1., ddDS) * dmax(fabs(ddDS), eps);
+  double Rrho = alfaobeta * ddDT / ddDS;
+  double nu_dds, nu_ddt;
+  if (Rrho > 1. && ddDS > 0.) {  /* salt fingering */
+    Rrho = dmin(Rrho, lmd_Rrho0);
+    const double x = (Rrho - 1.) / (lmd_Rrho0 - 1.);
+    nu_dds = 1. - x * x;
+    nu_dds = lmd_nuf * nu_dds * nu_dds * nu_dds;
+    nu_ddt = lmd_fdd * nu_dds;
+  } else if (Rrho < 1. && Rrho > 0. && ddDS < 0.) {  /* diffusive convection */
+    nu_ddt = lmd_nu * lmd_tdd1 * exp(lmd_tdd2 * exp(-lmd_tdd3 * ((1. / Rrho) - 1.)));
+    if (Rrho < 0.5) nu_dds = nu_ddt * lmd_sdd1 * Rrho;
+    else nu_dds = nu_ddt * (lmd_sdd2 * Rrho - lmd_sdd3);
+  } else {
+    nu_ddt = 0.;
+    nu_dds = 0.;
+  }
+  *kt = *kt + nu_ddt;
+  *ks = *ks + nu_dds;
+}
+
 /* lmd_vmix_tile (lmd_vmix.F:31-433): interior Kv, Kt, Ks at w-levels 0..N */
 static void lmd_vmix_tile(or_state *S, int tind) {
   const int N = S->N;
@@ -115,13 +154,16 @@ static void lmd_vmix_tile(or_state *S, int tind) {
   ext_range(S, &imin, &imax, &jmin, &jmax);
   double *Rk = S->lmd2[3];
   const int rimix = (S->c.lmd & OR_LMD_RIMIX) != 0, convec = (S->c.lmd & OR_LMD_CONVEC) != 0;
+  const int dd = (S->c.lmd & OR_LMD_DDMIX) != 0 && S->c.salinity;
   for (int k = 1; k <= N - 1; k++) {
     if (!rimix) {  /* internal waves only (lmd_vmix.F:262-264) */
       for (int j = S->jstr; j <= S->jend; j++)
         for (int i = S->istr; i <= S->iend; i++) {
+          double kt = nuws, ks = nuws;
+          if (dd) ddmix(S, i, j, k, tind, &kt, &ks);
           KV(i, j, k) = nuwm;
-          KT(i, j, k) = nuws;
-          KS(i, j, k) = nuws;
+          KT(i, j, k) = kt;
+          KS(i, j, k) = ks;
         }
       continue;
     }
@@ -143,9 +185,11 @@ static void lmd_vmix_tile(or_state *S, int tind) {
         nu_sx = nu_sx * nu_sx * nu_sx;
         double kv = nuwm + nu0m * nu_sx, kt = nuws + nu0s * nu_sx;
         if (convec && rig < 0.) { kv = kv + nu0c; kt = kt + nu0c; }  /* LMD_CONVEC (lmd_vmix.F:269-274) */
+        double ks = kt;
+        if (dd) ddmix(S, i, j, k, tind, &kt, &ks);
         KV(i, j, k) = kv;
         KT(i, j, k) = kt;
-        KS(i, j, k) = kt;
+        KS(i, j, k) = ks;
       }
   }
   for (int k = 1; k <= N - 1; k++)

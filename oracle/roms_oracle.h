@@ -25,7 +25,7 @@ extern "C" {
 
 /* analytic case selector */
 enum { OR_CASE_FILAMENT = 0, OR_CASE_BASIN = 1, OR_CASE_PIPES = 2, OR_CASE_RIVERS = 3 };
-enum { OR_LMD_RIMIX = 8, OR_LMD_CONVEC = 16, OR_LMD_NONLOCAL = 32 };
+enum { OR_LMD_RIMIX = 8, OR_LMD_CONVEC = 16, OR_LMD_NONLOCAL = 32, OR_LMD_DDMIX = 64 };
 
 typedef struct or_cfg {
   int LLm, MMm, N, NT;           /* interior dims, tracers (T[,S,passive]) */
@@ -33,7 +33,7 @@ typedef struct or_cfg {
   int salinity, nonlin_eos;      /* nonlin_eos implies SPLIT_EOS */
   int lmd;                       /* 0 or LMD switch bits (as ROMS_LMD_* of include/roms_gpu.h):
                                     1 MIXING, 2 KPP, 4 BKPP (MIXING|KPP|BKPP always together),
-                                    8 RIMIX, 16 CONVEC, 32 NONLOCAL */
+                                    8 RIMIX, 16 CONVEC, 32 NONLOCAL, 64 DDMIX */
   int case_id;
   int ntimes;
   double dt; int ndtfast;

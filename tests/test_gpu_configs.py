@@ -204,6 +204,11 @@ def test_invalid_lmd_sets_are_rejected():
         with pytest.raises(romsgpu.RomsGpuError):
             romsgpu.Model.from_case(1, 16, 16, 8, 2, salinity=True, nonlin_eos=True, lmd=bad, dt=60.0, ndtfast=30,
                                     sizex=32e3, sizey=32e3)
+    # LMD_DDMIX reads t(..,isalt) (lmd_vmix.F:289-296): not without SALINITY
+    with pytest.raises(romsgpu.RomsGpuError):
+        romsgpu.Model.from_case(1, 16, 16, 8, 1, salinity=False, nonlin_eos=True,
+                                lmd=romsgpu.LMD_ICELAND | romsgpu.LMD_DDMIX, dt=60.0, ndtfast=30, sizex=32e3,
+                                sizey=32e3)
 
 
 def c3_cfg(L=64, M=48, N=100):

@@ -40,6 +40,44 @@ constexpr double kEPS = 1.E-20;
 constexpr double kRi0 = 0.7, kNu0m = 1.e-2, kNu0s = 1.e-2, kNuwm = 1.0e-4, kNuws = 0.1e-4, kNu0c = 0.1, kLturb = 10.;
 constexpr double kPi = 3.14159265358979323;  // scalars.F:126
 
+// LMD_DDMIX (lmd_vmix.F:95-101, 279-360): double-diffusive additions to Kt
+// and Ks at a w-level from t(k), t(k+1) (T and S at tind) and z_w(k)
+__device__ __forceinline__ void ddmix(double t0, double t1, double s0, double s1, double zwk, double& kt,
+                                      double& ks) {
+  const double A0 = +0.665157E-01, A1 = +0.170907E-01, A2 = -0.203814E-03, A3 = +0.298357E-05,
+               A4 = -0.255019E-07, B0 = +0.378110E-02, B1 = -0.846960E-04, C0 = -0.678662E-05,
+               D0 = +0.380374E-04, D1 = -0.933746E-06, D2 = +0.791325E-08, E0 = -0.164759E-06,
+               F0 = -0.251520E-11, G0 = +0.512857E-12, H0 = -0.302285E-13, Smean = 35.0;
+  const double lmd_nu = 1.5e-6, lmd_Rrho0 = 1.9, lmd_nuf = 10.0e-4, lmd_fdd = 0.7, lmd_tdd1 = 0.909,
+               lmd_tdd2 = 4.6, lmd_tdd3 = 0.54, lmd_sdd1 = 0.15, lmd_sdd2 = 1.85, lmd_sdd3 = 0.85, eps = 1.E-14;
+  const double Tt = 0.5 * (t0 + t1);
+  const double Ts = 0.5 * (s0 + s1) - Smean;
+  const double Tp = -zwk;
+  const double alfaobeta = A0 + Tt * (A1 + Tt * (A2 + Tt * (A3 + Tt * A4))) + Ts * (B0 + Tt * B1 + Ts * C0) +
+                           Tp * (D0 + Tt * (D1 + Tt * D2) + Ts * E0 + Tp * (Ts * F0 + Tt * Tt * G0 + Tp * H0));
+  const double ddDT = t1 - t0;
+  double ddDS = s1 - s0;
+  ddDS = copysign(1., ddDS) * dmax(fabs(ddDS), eps);   // sign(1.,ddDS)*max(abs(ddDS),eps)
+  double Rrho = alfaobeta * ddDT / ddDS;
+  double nu_dds, nu_ddt;
+  if (Rrho > 1. && ddDS > 0.) {   // salt fingering
+    Rrho = dmin(Rrho, lmd_Rrho0);
+    const double x = (Rrho - 1.) / (lmd_Rrho0 - 1.);
+    nu_dds = 1. - x * x;
+    nu_dds = lmd_nuf * nu_dds * nu_dds * nu_dds;
+    nu_ddt = lmd_fdd * nu_dds;
+  } else if (Rrho < 1. && Rrho > 0. && ddDS < 0.) {   // diffusive convection
+    nu_ddt = lmd_nu * lmd_tdd1 * exp(lmd_tdd2 * exp(-lmd_tdd3 * ((1. / Rrho) - 1.)));
+    if (Rrho < 0.5) nu_dds = nu_ddt * lmd_sdd1 * Rrho;
+    else nu_dds = nu_ddt * (lmd_sdd2 * Rrho - lmd_sdd3);
+  } else {
+    nu_ddt = 0.;
+    nu_dds = 0.;
+  }
+  kt = kt + nu_ddt;
+  ks = ks + nu_dds;
+}
+
 struct KppConst {
   double Cg, Vtc;  // lmd_kpp.F:137-138 (power functions: evaluated on the host)
 };
@@ -314,6 +352,7 @@ __global__ void __launch_bounds__(64, 4) k_kpp_ext(Dev d, Range E, int tind, int
 }
 
 // ---- pass 2: interior ----
+template <bool kDD>   // LMD_DDMIX (its T/S loads and registers only where it is on)
 __global__ void __launch_bounds__(64) k_kpp_int(Dev d, Range R, EdgeClamp ec, int tind, int nstp, int first,
                                                 KppConst kc) {
   ROMS_IJC_OR_RETURN(R)
@@ -370,12 +409,20 @@ __global__ void __launch_bounds__(64) k_kpp_int(Dev d, Range R, EdgeClamp ec, in
   // raw_k split into its loads (rload) and its arithmetic (rcomp), so the
   // loads of level k+2 can be issued ahead of level k's stores (which would
   // otherwise hold them back: the compiler cannot prove the arrays apart)
-  struct RL { double r[3][3]; double zw; };
+  // LMD_DDMIX: T and S at levels k, k+1 (tind)
+  constexpr bool dd = kDD;
+  const double* __restrict__ Tt = F.t + (long)(tind - 1) * b.n3 + ij;
+  const double* __restrict__ St = Tt + 3 * b.n3;
+  struct RL { double r[3][3]; double zw, t0, t1, s0, s1; };
   auto rload = [&](int k, RL& L) {
     if (rimix) load3x3(b, ec, rig + (long)k * n2, i, j, L.r);
     L.zw = zw[(long)k * n2];
+    if (dd) {
+      const long o = (long)(k - 1) * n2;
+      L.t0 = Tt[o]; L.t1 = Tt[o + n2]; L.s0 = St[o]; L.s1 = St[o + n2];
+    }
   };
-  auto rcomp = [&](const RL& L, double& kv, double& kt) {
+  auto rcomp = [&](const RL& L, double& kv, double& kt, double& ks) {
     if (rimix) {
       const double Rig = smooth_point(L.r, m);
       const double cff = dmin(1., dmax(0., Rig));
@@ -391,12 +438,15 @@ __global__ void __launch_bounds__(64) k_kpp_int(Dev d, Range R, EdgeClamp ec, in
       kv = kNuwm;
       kt = kNuws;
     }
+    ks = kt;
+    if (dd) ddmix(L.t0, L.t1, L.s0, L.s1, L.zw, kt, ks);
     const double zwk = L.zw;
     const double dist = zwk - zw0;
     if (dist < kLturb) {
       const double mult = sin(0.5 * kPi * (zwk - zw0) / kLturb);
       kv = kv * mult;
       kt = kt * mult;
+      ks = ks * mult;
     }
   };
   double* __restrict__ Akv = F.Akv + ij;
@@ -443,35 +493,35 @@ __global__ void __launch_bounds__(64) k_kpp_int(Dev d, Range R, EdgeClamp ec, in
   };
   // bottom-up stream: padding (lmd_vmix.F:359-370) and the in-place ascending
   // 1-2-1 filter Kv(k) = 0.5 Kv(k) + 0.25 Kv(k-1)[filtered] + 0.25 Kv(k+1)[raw] + bak
-  double rv, rt;      // raw level k
+  double rv, rt, rs;  // raw level k (rs = rt unless LMD_DDMIX)
   RL La, Ln;
   rload(1, La);
   if (N - 1 >= 2) rload(2, Ln);
-  rcomp(La, rv, rt);
+  rcomp(La, rv, rt, rs);
   double zk = La.zw;  // z_w of level k
-  double rvN = rv, rtN = rt;  // raw level N-1 (known once reached)
-  double sv = rv + akv, st = rt + akt, ss = rt + aks;  // level 0 (padded)
+  double rvN = rv, rtN = rt, rsN = rs;  // raw level N-1 (known once reached)
+  double sv = rv + akv, st = rt + akt, ss = rs + aks;  // level 0 (padded)
   finish(0, sv, st, ss, zw0);
   for (int k = 1; k <= N - 1; k++) {
     double nv, nt, ns;  // level k+1 before filtering
-    double rvn = 0., rtn = 0., zk1 = 0.;
+    double rvn = 0., rtn = 0., rsn = 0., zk1 = 0.;
     if (k + 1 <= N - 1) {
       const RL cur = Ln;
       if (k + 2 <= N - 1) rload(k + 2, Ln);
-      rcomp(cur, rvn, rtn);
+      rcomp(cur, rvn, rtn, rsn);
       zk1 = cur.zw;
-      nv = rvn; nt = rtn; ns = rtn;
+      nv = rvn; nt = rtn; ns = rsn;
     } else {
-      rvN = rv; rtN = rt;
-      nv = rv + akv; nt = rt + akt; ns = rt + aks;
+      rvN = rv; rtN = rt; rsN = rs;
+      nv = rv + akv; nt = rt + akt; ns = rs + aks;
     }
     sv = 0.5 * rv + 0.25 * sv + 0.25 * nv + akv;
     st = 0.5 * rt + 0.25 * st + 0.25 * nt + akt;
-    ss = 0.5 * rt + 0.25 * ss + 0.25 * ns + aks;
+    ss = 0.5 * rs + 0.25 * ss + 0.25 * ns + aks;
     finish(k, sv, st, ss, zk);
-    rv = rvn; rt = rtn; zk = zk1;
+    rv = rvn; rt = rtn; rs = rsn; zk = zk1;
   }
-  finish(N, rvN + akv, rtN + akt, rtN + aks, zwN);
+  finish(N, rvN + akv, rtN + akt, rsN + aks, zwN);
   // hbls/hbbl and their closed-wall ghost copies (lmd_kpp.F:530-620)
   F.hbls[ij] = hbl;
   F.hbbl[ij] = bbl;
@@ -517,7 +567,10 @@ void launch_lmd_vmix(const Dev& d, hipStream_t s, const Tlev& t, int tind) {
     hipLaunchKernelGGL(k_kpp_ext<ColGlb>, gridc_of(E), dim3(kCX), 0, s, d, E, tind, t.nstp, kc);
   else
     hipLaunchKernelGGL(k_kpp_ext<ColLds>, gridc_of(E), dim3(kCX), col_lds_bytes(1, b.N), s, d, E, tind, t.nstp, kc);
-  hipLaunchKernelGGL(k_kpp_int, gridc_of(R), dim3(kCX), 0, s, d, R, edge_clamp(b), tind, t.nstp, first, kc);
+  if (d.p.lmd_ddmix)
+    hipLaunchKernelGGL(k_kpp_int<true>, gridc_of(R), dim3(kCX), 0, s, d, R, edge_clamp(b), tind, t.nstp, first, kc);
+  else
+    hipLaunchKernelGGL(k_kpp_int<false>, gridc_of(R), dim3(kCX), 0, s, d, R, edge_clamp(b), tind, t.nstp, first, kc);
   // lmd_kpp.F:631-649: Akv, hbls, hbbl, Akt(itemp), Akt(isalt)
   ExchList L{};
   L.p[0] = d.f.Akv; L.nlev[0] = b.N + 1;

@@ -32,6 +32,7 @@ struct Bounds {
 struct Params {
   int nonlin_eos, salinity, lmd, uv_vis2, ts_dif2;
   int lmd_rimix, lmd_convec, lmd_nonlocal;  // LMD_RIMIX, LMD_CONVEC, LMD_NONLOCAL (lmd != 0: MIXING+KPP+BKPP)
+  int lmd_ddmix;                            // LMD_DDMIX (needs SALINITY)
   int uv_adv, uv_cor;                       // UV_ADV, UV_COR
   int tides;                                // TIDES pot_tides: ptide in prsgrd
   int bulk_frc;                             // BULK_FRC (k_bulk.hip; u* from sustr_r/svstr_r in lmd_kpp)

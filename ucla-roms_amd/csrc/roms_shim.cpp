@@ -469,8 +469,10 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
   Params& P = g.d.p;
   {
     const int m = cfg->lmd_mixing, base = ROMS_LMD_MIXING | ROMS_LMD_KPP | ROMS_LMD_BKPP;
-    if (m != 0 && ((m & ~ROMS_LMD_ALL) || (m & base) != base || ((m & ROMS_LMD_CONVEC) && !(m & ROMS_LMD_RIMIX)))) {
-      g.err = "roms_gpu_init: lmd_mixing must be 0 or LMD_MIXING|LMD_KPP|LMD_BKPP [|RIMIX|NONLOCAL|CONVEC(needs RIMIX)]";
+    if (m != 0 && ((m & ~(ROMS_LMD_ALL | ROMS_LMD_DDMIX)) || (m & base) != base ||
+                   ((m & ROMS_LMD_CONVEC) && !(m & ROMS_LMD_RIMIX)) || ((m & ROMS_LMD_DDMIX) && !cfg->salinity))) {
+      g.err = "roms_gpu_init: lmd_mixing must be 0 or LMD_MIXING|LMD_KPP|LMD_BKPP [|RIMIX|NONLOCAL|CONVEC(needs RIMIX)"
+              "|DDMIX(needs SALINITY)]";
       return -1;
     }
   }
@@ -478,6 +480,7 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
   P.lmd_rimix = (cfg->lmd_mixing & ROMS_LMD_RIMIX) != 0;
   P.lmd_convec = (cfg->lmd_mixing & ROMS_LMD_CONVEC) != 0;
   P.lmd_nonlocal = (cfg->lmd_mixing & ROMS_LMD_NONLOCAL) != 0;
+  P.lmd_ddmix = (cfg->lmd_mixing & ROMS_LMD_DDMIX) != 0;
   P.uv_adv = cfg->uv_adv != 0; P.uv_cor = cfg->uv_cor != 0;
   P.tides = cfg->pot_tides != 0;
   P.bulk_frc = cfg->bulk_frc != 0;

@@ -30,6 +30,7 @@ FIELD_ID = {n: i for i, n in enumerate(FIELDS)}
 CASE_FILAMENT, CASE_BASIN, CASE_PIPES, CASE_RIVERS = 0, 1, 2, 3
 # LMD switch bits (ROMS_LMD_* of include/roms_gpu.h)
 LMD_MIXING, LMD_KPP, LMD_BKPP, LMD_RIMIX, LMD_CONVEC, LMD_NONLOCAL = 1, 2, 4, 8, 16, 32
+LMD_DDMIX = 64    # double diffusion (lmd_vmix.F:279-360), needs salinity
 LMD_ALL = 63       # tests/Pipes_ana/cppdefs.opt
 LMD_ICELAND = 47   # Examples/Iceland/Iceland_parent/cppdefs.opt: no LMD_CONVEC
 
