@@ -11,7 +11,9 @@ analytic initial state.  One "step" = one full roms_step (main.F:333-520):
 rho_eos(nrhs) (main.F:397) reads exactly the t, z_r, Hz the previous step's
 closing rho_eos(nnew) (main.F:479) read, so the library keeps those outputs
 instead of recomputing them (bitwise-equal runs, ROMS_GPU_RHO_REUSE=0 turns it
-off); roofline_step's byte count leaves that pass out.  State is resident in
+off); roofline_step's byte count leaves that pass out, and the two Hz_u/Hz_v
+stores of set_HUV that whole steps skip (extract_data inputs only,
+ROMS_GPU_HZ_UV=1 keeps them).  State is resident in
 HBM before the timed region; steady steps replay captured HIP graphs.  N GPUs:
 weak scaling on an npx x npe processor grid (1x1, 2x1, 2x2, 4x2) of 512x512
 subdomains of one periodic domain, halo exchanges inside the step graphs.
@@ -69,15 +71,22 @@ PRE_UV_SEG_PASSES = 14
 PRSGRD_UV_PASSES = 11
 
 
+# set_HUV's Hz_u/Hz_v (set_depth.F:220,227) feed only extract_data.F; whole
+# steps store them only on request (ROMS_GPU_HZ_UV=1, include/roms_gpu.h), so
+# set_HUV's pass count is 5 (Hz, u, v read; FlxU, FlxV written), else 7
+HZ_UV_PASSES = 2 if os.environ.get("ROMS_GPU_HZ_UV") == "1" else 0
+
+
 def routine_passes(NT_, NT_TS_, lmd=False):
     """unique 3-D array passes per call; step2d counts 35 2-D
     passes per fast step (flagged with None).  lmd: the C3 switch set
     (NONLIN+SPLIT EOS, SALINITY, LMD/KPP), P3D = 150 + 10*NT."""
+    huv = 5 + HZ_UV_PASSES
     if lmd:
-        return {"rho_eos": 7, "set_HUV": 7, "omega": 6, "prsgrd": 6, "pre_step3d": 18 + 4 * NT_, "set_HUV1": 7,
+        return {"rho_eos": 7, "set_HUV": huv, "omega": 6, "prsgrd": 6, "pre_step3d": 18 + 4 * NT_, "set_HUV1": 7,
                 "step3d_uv1": 14, "visc3d": 7, "step2d": None, "step3d_uv2": 11, "step3d_t": 9 + 3 * NT_,
                 "t3dmix": 1 + 3 * NT_, "lmd_vmix": 11}
-    return {"rho_eos": 2 + NT_TS_, "set_HUV": 7, "omega": 6, "prsgrd": 5, "pre_step3d": 16 + NT_TS_ + 4 * NT_,
+    return {"rho_eos": 2 + NT_TS_, "set_HUV": huv, "omega": 6, "prsgrd": 5, "pre_step3d": 16 + NT_TS_ + 4 * NT_,
             "set_HUV1": 7, "step3d_uv1": 14, "visc3d": 7, "step2d": None, "step3d_uv2": 11,
             "step3d_t": 5 + NT_TS_ + 3 * NT_, "t3dmix": 1 + 3 * NT_, "lmd_vmix": 0}
 
@@ -85,9 +94,11 @@ def routine_passes(NT_, NT_TS_, lmd=False):
 def step_bytes(I, J, N, NT_, NT_TS_, nfast, lmd=False):
     """B_step = 8*(P3D*I*J*N + 35*nfast*I*J),
     P3D = 105+5*NT_TS+10*NT (Filament) or 150+10*NT (C3 switches), less the
-    one rho_eos call per step the library does not repeat (see above)."""
+    one rho_eos call per step the library does not repeat and the Hz_u/Hz_v
+    stores whole steps skip (see above)."""
     P3D = (150 + 10 * NT_) if lmd else (105 + 5 * NT_TS_ + 10 * NT_)
     P3D -= routine_passes(NT_, NT_TS_, lmd)["rho_eos"]
+    P3D -= 2 - HZ_UV_PASSES
     return 8.0 * (P3D * I * J * N + 35.0 * nfast * I * J)
 
 
