@@ -136,7 +136,7 @@ def test_register_column_kernels_bitwise(lmd):
 
 
 @pytest.mark.parametrize("case", ["n50", "n100"])
-@pytest.mark.parametrize("switch", ["ROMS_GPU_PREUV_LDS", "ROMS_GPU_OMEGA_SEG", "ROMS_GPU_UV1_LDS"])
+@pytest.mark.parametrize("switch", ["ROMS_GPU_PREUV_LDS", "ROMS_GPU_OMEGA_SEG", "ROMS_GPU_UV1_LDS", "ROMS_GPU_OMEGA_HB"])
 def test_seg_variants_bitwise(case, switch, monkeypatch):
     """Variants that keep the reference's operations and order, so 6 steps
     equal the plain forms bitwise:
@@ -147,7 +147,10 @@ def test_seg_variants_bitwise(case, switch, monkeypatch):
       the partial sums of the divergence as one chain through the waves;
     - k_uv1_seg<true> (ROMS_GPU_UV1_LDS, default) keeps the spline phase's Hz
       pairs in LDS for the viscosity rows and chains the rufrc sum through
-      the waves in k order."""
+      the waves in k order;
+    - k_omega_seg<true> (ROMS_GPU_OMEGA_HB, default) forms pre_step3d's
+      Hz_bak/Hz_fwd in the predictor's omega with k_pre_tracer_h1's
+      expression, the tracer kernel loading them instead."""
     cfg = seg_cfg(case)
     out = []
     for env in ("0", "1"):

@@ -398,3 +398,25 @@ def test_hz_uv_stored_on_request(monkeypatch):
         m.close()
     for n in out["0"]:
         assert np.array_equal(out["0"][n], out["1"][n]), n
+
+
+@pytest.mark.parametrize("case", ["filament", "basin"])
+def test_omega_forms_hz_bak_fwd_bitwise(case, monkeypatch):
+    """The predictor's omega forms pre_step3d's Hz_bak/Hz_fwd of the interior
+    cells (ROMS_GPU_OMEGA_HB, default): 4 whole steps bitwise equal to
+    pre_step3d forming them (=0), periodic (Filament) and closed (basin)."""
+    if case == "basin":
+        cfg = basin_cfg(LLm=70, MMm=40, N=12, nonlin=True)
+    else:
+        cfg = oracle.filament_cfg(LLm=64, MMm=40, N=16, np_xi=1, np_eta=1)
+    out = []
+    for env in ("0", "1"):
+        monkeypatch.setenv("ROMS_GPU_OMEGA_HB", env)
+        m = romsgpu.Model.from_case(cfg.case_id, cfg.LLm, cfg.MMm, cfg.N, cfg.NT, salinity=bool(cfg.salinity),
+                                    nonlin_eos=bool(cfg.nonlin_eos), dt=cfg.dt, ndtfast=cfg.ndtfast,
+                                    sizex=cfg.sizex, sizey=cfg.sizey)
+        m.step(4)
+        out.append({n: m.get(n) for n in ("zeta", "ubar", "vbar", "u", "v", "t", "We", "Wi", "rufrc", "rvfrc")})
+        m.close()
+    for n in out[0]:
+        assert np.array_equal(out[0][n], out[1][n]), n

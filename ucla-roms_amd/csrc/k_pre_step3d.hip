@@ -69,7 +69,11 @@ struct TracerWinN {
   static constexpr int kN = kUVW * (TY + 4);
   double UM[kN], VM[kN], FU[kN], FV[kN], T[NTT][kN];
 };
-template <int NTT, int TY>
+// kHB: the interior cells' Hz_bak / Hz_fwd are already in c3 / c2 (the
+// predictor's k_omega_seg<true> formed them with this expression); those
+// cells load Hz_bak instead of the fluxes and We/Wi, the ring i = istr-1 /
+// j = jstr-1 still forms both.
+template <int NTT, int TY, bool kHB>
 __global__ void __launch_bounds__(kBX * TY) k_pre_tracer_h1(Dev d, Range R, PreCoef c, int nstp, int nnew, int nrhs) {
   const uint3 bI = h_tile(d.p.tile_grp);
   __shared__ TracerWinN<NTT, TY> W;
@@ -101,8 +105,14 @@ __global__ void __launch_bounds__(kBX * TY) k_pre_tracer_h1(Dev d, Range R, PreC
   const bool in = act && i >= b.istr && j >= b.jstr;
   const long ij = act ? IJ(b, i, j) : IJ(b, R.i0, R.j0), o = ij + kk, w = ij + (long)k * n2;
   // hz_bak_fwd's inputs (pre_step3d4S.F:136-148) and the tracer time levels
-  const double fu0 = F.FlxU[o], fu1 = F.FlxU[o + 1], fv0 = F.FlxV[o], fv1 = F.FlxV[o + b.nx2];
-  const double we1 = F.We[w], wi1 = F.Wi[w], we0 = F.We[w - n2], wi0 = F.Wi[w - n2];
+  const bool formed = kHB && in;   // Hz_bak/fwd from omega
+  double fu0 = 0.0, fu1 = 0.0, fv0 = 0.0, fv1 = 0.0, we1 = 0.0, wi1 = 0.0, we0 = 0.0, wi0 = 0.0, hbo = 0.0;
+  if (formed) {
+    hbo = F.c3[o];
+  } else {
+    fu0 = F.FlxU[o]; fu1 = F.FlxU[o + 1]; fv0 = F.FlxV[o]; fv1 = F.FlxV[o + b.nx2];
+    we1 = F.We[w]; wi1 = F.Wi[w]; we0 = F.We[w - n2]; wi0 = F.Wi[w - n2];
+  }
   const double pm = F.pm[ij], pn = F.pn[ij], hzo = F.Hz[o];
   double ts[NTT], ti[NTT];
 #pragma unroll
@@ -122,11 +132,17 @@ __global__ void __launch_bounds__(kBX * TY) k_pre_tracer_h1(Dev d, Range R, PreC
   }
   __syncthreads();
   if (!act) return;
-  const double cff = 0.5 * c.dtau;
-  const double FlxDiv = cff * pm * pn * (fu1 - fu0 + fv1 - fv0 + we1 + wi1 - we0 - wi0);
-  const double hb = hzo + FlxDiv, hf = hzo - FlxDiv;
-  F.c2[o] = hf;  // Hz_fwd, Hz_bak kept for the column solves (range istr-1.., jstr-1..)
-  F.c3[o] = hb;
+  double hb;
+  if (formed) {
+    hb = hbo;
+  } else {
+    const double cff = 0.5 * c.dtau;
+    const double FlxDiv = cff * pm * pn * (fu1 - fu0 + fv1 - fv0 + we1 + wi1 - we0 - wi0);
+    hb = hzo + FlxDiv;
+    const double hf = hzo - FlxDiv;
+    F.c2[o] = hf;  // Hz_fwd, Hz_bak kept for the column solves (range istr-1.., jstr-1..)
+    F.c3[o] = hb;
+  }
   if (!in) return;
   const double hz = hzo;
 #pragma unroll
@@ -746,22 +762,40 @@ bool setup_column_kernels(int N) {
   return true;
 }
 
-void launch_pre_step3d(const Dev& d, hipStream_t s, const Tlev& t, bool uv_done) {
+double pre_step3d_dtau(const Dev& d, const Tlev& t) {
+  const double AM3_crv = 1.0 / 6.0;
+  return t.iic == t.forw_start ? 0.5 * d.p.dt : d.p.dt * (1.0 - AM3_crv);
+}
+
+void launch_pre_step3d(const Dev& d, hipStream_t s, const Tlev& t, bool uv_done, bool hb_done) {
   const Bounds& b = d.b;
   PreCoef c;
   const double AM3_crv = 1.0 / 6.0;
   if (t.iic == t.forw_start) { c.dtau = 0.5 * d.p.dt; c.cf_stp = 1.0; c.cf_bak = 0.0; }
   else { c.dtau = d.p.dt * (1.0 - AM3_crv); c.cf_stp = 0.5 + AM3_crv; c.cf_bak = 0.5 - AM3_crv; }
+  c.dtau = pre_step3d_dtau(d, t);   // (the same value; omega's Hz_bak/fwd use it too)
+  // hb_done only with the hoisted tracer kernel (k_pre_tracer_h forms everything)
+  hb_done = hb_done && d.p.hoist && b.NT <= 2;
   Range RI{b.istr, b.iend, b.jstr, b.jend};
   Range RH{b.istr - 1, b.iend, b.jstr - 1, b.jend};
-  if (d.p.hoist && b.NT == 2 && d.p.h_ty == 8)
-    hipLaunchKernelGGL((k_pre_tracer_h1<2, 8>), grid3_ty(RH, b.N, 8), dim3(kBX, 8), 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs);
-  else if (d.p.hoist && b.NT == 2)
-    hipLaunchKernelGGL((k_pre_tracer_h1<2, 4>), grid3_ty(RH, b.N, 4), dim3(kBX, 4), 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs);
-  else if (d.p.hoist && b.NT == 1)
-    hipLaunchKernelGGL((k_pre_tracer_h1<1, 4>), grid3_ty(RH, b.N, 4), dim3(kBX, 4), 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs);
-  else
+  if (d.p.hoist && b.NT == 2 && d.p.h_ty == 8) {
+    if (hb_done)
+      hipLaunchKernelGGL((k_pre_tracer_h1<2, 8, true>), grid3_ty(RH, b.N, 8), dim3(kBX, 8), 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs);
+    else
+      hipLaunchKernelGGL((k_pre_tracer_h1<2, 8, false>), grid3_ty(RH, b.N, 8), dim3(kBX, 8), 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs);
+  } else if (d.p.hoist && b.NT == 2) {
+    if (hb_done)
+      hipLaunchKernelGGL((k_pre_tracer_h1<2, 4, true>), grid3_ty(RH, b.N, 4), dim3(kBX, 4), 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs);
+    else
+      hipLaunchKernelGGL((k_pre_tracer_h1<2, 4, false>), grid3_ty(RH, b.N, 4), dim3(kBX, 4), 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs);
+  } else if (d.p.hoist && b.NT == 1) {
+    if (hb_done)
+      hipLaunchKernelGGL((k_pre_tracer_h1<1, 4, true>), grid3_ty(RH, b.N, 4), dim3(kBX, 4), 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs);
+    else
+      hipLaunchKernelGGL((k_pre_tracer_h1<1, 4, false>), grid3_ty(RH, b.N, 4), dim3(kBX, 4), 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs);
+  } else {
     hipLaunchKernelGGL(k_pre_tracer_h, grid3_of(RH, b.N), dim3(kBX, kBY), 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs);
+  }
   dim3 gt = gridc_of(RI);
   gt.z = b.NT;
   if (d.p.colseg)

@@ -386,8 +386,17 @@ __global__ void __launch_bounds__(256) k_omega(Dev d, Range R, double dtau) {
 //      independent: Courant number and Hz of the level above come from the
 //      wave above through LDS at the segment top.
 // Lanes outside the range solve a clamped duplicate column and store nothing.
+//
+// kHB (the predictor's omega, ROMS_GPU_OMEGA_HB): the same block also forms
+// pre_step3d's Hz_bak / Hz_fwd = Hz +- 0.5 dtau pm pn (div(FlxU, FlxV) +
+// We + Wi at the top - at the bottom) of its cells (pre_step3d4S.F:136-148,
+// k_pre_tracer_h1's expression and order) into c3 / c2: the fluxes, Hz and
+// the new We/Wi are all in its registers, and nothing between omega and
+// pre_step3d writes them.  The flux differences of the level are kept in
+// dynamic LDS across the chain ([kOmR][threads], through an opaque offset).
 constexpr int kOmR = kSegRows;   // levels per wave (N <= kSegRows * kSegMaxS)
-__global__ void __launch_bounds__(kSegBlock, 2) k_omega_seg(Dev d, Range R, double dtau) {
+template <bool kHB>
+__global__ void __launch_bounds__(kSegBlock, 2) k_omega_seg(Dev d, Range R, double dtau, double hcff) {
   const uint3 bI = xcd_tile();
   const Bounds& b = d.b;
   const Fields& F = d.f;
@@ -405,6 +414,7 @@ __global__ void __launch_bounds__(kSegBlock, 2) k_omega_seg(Dev d, Range R, doub
   const double* __restrict__ Hz = F.Hz + ij;
   const double* __restrict__ zw = F.z_w + ij;
   __shared__ double Lw[kSegMaxS][kSegCW], Lcx[kSegMaxS][kSegCW], Lhz[kSegMaxS][kSegCW];
+  __shared__ double Lte[kHB ? kSegMaxS : 1][kSegCW], Lti[kHB ? kSegMaxS : 1][kSegCW];   // kHB: segment tops' We, Wi
   double fu1[kOmR], fu0[kOmR], fv1[kOmR], fv0[kOmR], cx[kOmR], hz[kOmR], zk[kOmR];
 #pragma unroll
   for (int q = 0; q < kOmR; q++) {   // rho level k = c0+q (clamped), w-level k
@@ -422,6 +432,13 @@ __global__ void __launch_bounds__(kSegBlock, 2) k_omega_seg(Dev d, Range R, doub
   const double* __restrict__ prf = pidx > 0 ? F.pipe_prf + (pidx - 1) : nullptr;
 #pragma unroll
   for (int q = 0; q < kOmR; q++) cx[q] = fmax0(fu1[q]) - fmin0(fu0[q]) + fmax0(fv1[q]) - fmin0(fv0[q]);
+  const int nthr = (int)(blockDim.x * blockDim.y);
+  int tl = (int)(threadIdx.x + blockDim.x * threadIdx.y);
+  __asm__ volatile("" : "+v"(tl));
+  if constexpr (kHB) {
+#pragma unroll
+    for (int q = 0; q < kOmR; q++) roms_smem[q * nthr + tl] = fu1[q] - fu0[q] + fv1[q] - fv0[q];
+  }
   Lcx[s][l] = cx[0];
   Lhz[s][l] = hz[0];
   // 1. the partial sums, wave by wave in k order
@@ -443,10 +460,24 @@ __global__ void __launch_bounds__(kSegBlock, 2) k_omega_seg(Dev d, Range R, doub
   // 2. the Courant split of w-levels k = c0..c0+n-1 (k <= N-1)
   const double wrk = (Lw[S - 1][l] + wsrf) / (zwN - zw0);
   const double cx_top = s + 1 < S ? Lcx[s + 1][l] : 0.0, hz_top = s + 1 < S ? Lhz[s + 1][l] : 0.0;
-  if (!act) return;
+  if (!kHB && !act) return;
   double* __restrict__ Wi = F.Wi + ij;
   double* __restrict__ We = F.We + ij;
-  if (s == 0) {
+  // kHB: Hz_bak/fwd of cell k needs We, Wi at w-levels k and k-1
+  const double hbf = kHB ? hcff * F.pm[ij] * F.pn[ij] : 0.0;
+  double* __restrict__ Hf = F.c2 + ij;
+  double* __restrict__ Hb = F.c3 + ij;
+  double we_p = 0.0, wi_p = 0.0, we_f = 0.0, wi_f = 0.0;   // previous level's, the segment's first level's
+  int tr = tl;
+  __asm__ volatile("" : "+v"(tr));   // a second opaque offset: the stored differences are not forwarded
+  auto hb_store = [&](int q, double we1, double wi1, double we0, double wi0) {
+    const double div = roms_smem[q * nthr + tr];
+    const double FlxDiv = hbf * (div + we1 + wi1 - we0 - wi0);
+    const long o = (long)(c0 + q - 1) * n2;
+    Hf[o] = hz[q] - FlxDiv;
+    Hb[o] = hz[q] + FlxDiv;
+  };
+  if (act && s == 0) {
     Wi[0] = 0.0;
     We[0] = 0.0;
     Wi[(long)N * n2] = 0.0;
@@ -475,11 +506,23 @@ __global__ void __launch_bounds__(kSegBlock, 2) k_omega_seg(Dev d, Range R, doub
     } else {
       we = 0.0;
     }
-    if (q < n && k <= N - 1) {
+    if (act && q < n && k <= N - 1) {
       const long o1 = (long)k * n2;
       We[o1] = we;
       Wi[o1] = w;
     }
+    if constexpr (kHB) {
+      const double we1 = k <= N - 1 ? we : 0.0, wi1 = k <= N - 1 ? w : 0.0;   // We(N) = Wi(N) = 0
+      if (q == 0) { we_f = we1; wi_f = wi1; }
+      if (act && q >= 1 && q < n) hb_store(q, we1, wi1, we_p, wi_p);
+      if (q == n - 1) { Lte[s][l] = we1; Lti[s][l] = wi1; }   // this segment's top w-level, for the wave above
+      we_p = we1; wi_p = wi1;
+    }
+  }
+  if constexpr (kHB) {
+    __syncthreads();
+    const double we0 = s > 0 ? Lte[s - 1][l] : 0.0, wi0 = s > 0 ? Lti[s - 1][l] : 0.0;   // We(0) = Wi(0) = 0
+    if (act) hb_store(0, we_f, wi_f, we0, wi0);
   }
 }
 
@@ -515,20 +558,33 @@ __global__ void k_omega_edges(Dev d) {
   F.Wi[dst] = F.Wi[src];
 }
 
-void launch_omega(const Dev& d, hipStream_t s, const Tlev& t) {
+static size_t omega_hb_lds_bytes(unsigned nthr) { return (size_t)kOmR * nthr * sizeof(double); }
+void setup_omega_seg() {
+  (void)hipFuncSetAttribute((const void*)k_omega_seg<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)omega_hb_lds_bytes(kSegBlock));
+}
+
+// hcff > 0 (the predictor's call): also form pre_step3d's Hz_bak / Hz_fwd of
+// the interior cells into c3 / c2 with 0.5*dtau = hcff (k_omega_seg<true>);
+// returns whether it did (one segment launch over the whole interior)
+bool launch_omega(const Dev& d, hipStream_t s, const Tlev& t, double hcff) {
   const Bounds& b = d.b;
   double dtau;
   if (t.nrhs == 3) dtau = d.p.dt;
   else if (t.iic == t.forw_start) dtau = 0.5 * d.p.dt;
   else dtau = 0.6 * d.p.dt;
   Range R{b.istr, b.iend, b.jstr, b.jend};
+  const bool seg_ok = d.p.omega_seg && b.N <= kSegRows * kSegMaxS;
+  const bool hb = hcff > 0.0 && seg_ok && R.i1 - R.i0 + 1 >= 32 && !rim_overlap_on(d, R);
   launch_rim_first(
       d, s, R, ExchList{{d.f.We, d.f.Wi}, {b.N + 1, b.N + 1}, 2},
       [&](const Range& r) {
         // the segment form for full-width ranges (rim strips keep k_omega)
-        if (d.p.omega_seg && b.N <= kSegRows * kSegMaxS && r.i1 - r.i0 + 1 >= 32)
-          hipLaunchKernelGGL(k_omega_seg, dim3((r.i1 - r.i0 + kSegCW) / kSegCW, r.j1 - r.j0 + 1), dim3(kCX, seg_waves(b.N)),
-                             0, s, d, r, dtau);
+        const dim3 gs((r.i1 - r.i0 + kSegCW) / kSegCW, r.j1 - r.j0 + 1), bs(kCX, seg_waves(b.N));
+        if (hb)
+          hipLaunchKernelGGL(k_omega_seg<true>, gs, bs, omega_hb_lds_bytes(bs.x * bs.y), s, d, r, dtau, hcff);
+        else if (seg_ok && r.i1 - r.i0 + 1 >= 32)
+          hipLaunchKernelGGL(k_omega_seg<false>, gs, bs, 0, s, d, r, dtau, 0.0);
         else
           hipLaunchKernelGGL(k_omega, grid_of(r), dim3(kBX, kBY), 0, s, d, r, dtau);
       },
@@ -538,6 +594,7 @@ void launch_omega(const Dev& d, hipStream_t s, const Tlev& t) {
           hipLaunchKernelGGL(k_omega_edges, dim3((n + 255) / 256, b.N + 1), dim3(256), 0, s, d);
         }
       });
+  return hb;
 }
 
 // ---------------------------------------------------------------------------

@@ -52,6 +52,7 @@ struct Params {
   int tile_grp;   // h_tile group width of the hoisted per-level kernels (ROMS_GPU_TILE_GRP; 0: xcd_tile order)
   int uv1_lds;    // k_uv1_seg: Hz pairs kept in LDS from the spline phase, rufrc chained (ROMS_GPU_UV1_LDS=0: reloads)
   int omega_seg;  // omega: segment form k_omega_seg, one read of each input (ROMS_GPU_OMEGA_SEG=0: two-pass k_omega)
+  int omega_hb;   // the predictor's omega forms pre_step3d's Hz_bak/Hz_fwd (ROMS_GPU_OMEGA_HB=0: pre_step3d does)
   int preuv_lds;  // k_pre_uv_seg: u(indx) stored and u(nstp)/u(indx) combined in the spline phase (ROMS_GPU_PREUV_LDS=0: reloads)
   int seg_jrows;  // rows j per block of the momentum segment solvers (1..kSegJMax; ROMS_GPU_SEG_JROWS)
   int npip;       // pipe_frc.F: number of pipes (0: pipe_source off)
@@ -324,14 +325,19 @@ void launch_set_depth(const Dev& d, hipStream_t s, const Tlev& t);
 // store_huv: also Hz_u/Hz_v (set_depth.F:220,227), read only by extract_data.F
 void launch_set_huv(const Dev& d, hipStream_t s, const Tlev& t, bool store_huv = true);
 void launch_set_huv1(const Dev& d, hipStream_t s, const Tlev& t);
-void launch_omega(const Dev& d, hipStream_t s, const Tlev& t);
+// hcff > 0: the predictor's call also forms pre_step3d's Hz_bak/Hz_fwd (c3/c2) of the
+// interior cells with 0.5*dtau = hcff; returns whether it did (k_vertical.hip)
+bool launch_omega(const Dev& d, hipStream_t s, const Tlev& t, double hcff = 0.0);
+void setup_omega_seg();   // k_omega_seg<true>'s dynamic LDS limit
+double pre_step3d_dtau(const Dev& d, const Tlev& t);   // pre_step3d's dtau (k_pre_step3d.hip)
 void launch_rho_eos(const Dev& d, hipStream_t s, const Tlev& t, int tidx);
 // uv_up >= 0: also add the horizontal momentum r.h.s. (UPSTREAM_UV if 1) of
 // the following pre_step3d / step3d_uv1 (prsgrd_can_fuse_uv; the caller then
 // passes uv_done to it)
 void launch_prsgrd(const Dev& d, hipStream_t s, const Tlev& t, int uv_up = -1);
 bool prsgrd_can_fuse_uv(const Dev& d);
-void launch_pre_step3d(const Dev& d, hipStream_t s, const Tlev& t, bool uv_done = false);
+// hb_done: the interior cells' Hz_bak/Hz_fwd are in c3/c2 already (launch_omega)
+void launch_pre_step3d(const Dev& d, hipStream_t s, const Tlev& t, bool uv_done = false, bool hb_done = false);
 void launch_step3d_uv1(const Dev& d, hipStream_t s, const Tlev& t, bool uv_done = false);
 void launch_visc3d(const Dev& d, hipStream_t s, const Tlev& t);
 void launch_step2d(const Dev& d, hipStream_t s, const Tlev& t, const double* w1, const double* w2);

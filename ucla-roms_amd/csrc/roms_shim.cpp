@@ -355,14 +355,18 @@ void enqueue_step(roms_tlev* t, bool rho_current, bool store_huv) {
   frc_step_phase(d, s, 1, pot);     // set_bry_all '1/2 fwd' + set_tides (main.F:389-394)
   if (!rho_current) TIMED(ROMS_R_RHO_EOS, launch_rho_eos(d, s, T, T.nrhs));
   TIMED(ROMS_R_SET_HUV, launch_set_huv(d, s, T, store_huv));
-  TIMED(ROMS_R_OMEGA, launch_omega(d, s, T));
+  // the predictor's omega also forms pre_step3d's Hz_bak/Hz_fwd (nothing in
+  // between -- lmd_vmix, prsgrd -- writes FlxU, FlxV, Hz, We or Wi)
+  bool hb_done = false;
+  TIMED(ROMS_R_OMEGA, hb_done = launch_omega(d, s, T, d.p.omega_hb && d.p.hoist && T.nrhs != 3 ?
+                                                          0.5 * pre_step3d_dtau(d, T) : 0.0));
   if (g.cfg.lmd_mixing) TIMED(ROMS_R_LMD_VMIX, launch_lmd_vmix(d, s, T, T.nstp));
   // the horizontal momentum r.h.s. of pre_step3d / step3d_uv1 rides in the
   // prsgrd kernel just before them (prsgrd_can_fuse_uv; nothing between the
   // two touches u, v(nrhs), FlxU, FlxV, Hz or ru, rv)
   const bool fuse_uv = prsgrd_can_fuse_uv(d);
   TIMED(ROMS_R_PRSGRD, launch_prsgrd(d, s, T, fuse_uv ? 0 : -1));
-  TIMED(ROMS_R_PRE_STEP3D, launch_pre_step3d(d, s, T, fuse_uv));
+  TIMED(ROMS_R_PRE_STEP3D, launch_pre_step3d(d, s, T, fuse_uv, hb_done));
   TIMED(ROMS_R_SET_HUV1, launch_set_huv1(d, s, T));
   t->nrhs = 3;
   t->nnew = 3 - t->nstp;
@@ -578,6 +582,10 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     P.uv1_lds = !(e && e[0] == '0');
   }
   {
+    const char* e = getenv("ROMS_GPU_OMEGA_HB");
+    P.omega_hb = !(e && e[0] == '0');
+  }
+  {
     const char* e = getenv("ROMS_GPU_OMEGA_SEG");
     P.omega_seg = !(e && e[0] == '0');
   }
@@ -609,6 +617,7 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
   }
   setup_uv1_seg();
   setup_pre_uv_seg();
+  setup_omega_seg();
   if (!col_global && !setup_column_kernels(dims->N)) {
     g.err = "roms_gpu_init: N too large for the LDS column kernels (2*(N+1)*512 B > 160 KB)";
     return -2;
