@@ -401,17 +401,22 @@ def test_hz_uv_stored_on_request(monkeypatch):
 
 
 @pytest.mark.parametrize("case", ["filament", "basin"])
-def test_omega_forms_hz_bak_fwd_bitwise(case, monkeypatch):
-    """The predictor's omega forms pre_step3d's Hz_bak/Hz_fwd of the interior
-    cells (ROMS_GPU_OMEGA_HB, default): 4 whole steps bitwise equal to
-    pre_step3d forming them (=0), periodic (Filament) and closed (basin)."""
+@pytest.mark.parametrize("switch", ["ROMS_GPU_OMEGA_HB", "ROMS_GPU_P_IN_RHO"])
+def test_step_producer_variants_bitwise(case, switch, monkeypatch):
+    """Producers that form a later routine's inputs with its expressions: 4
+    whole steps bitwise equal to the consumer forming them (=0), periodic
+    (Filament, linear EOS) and closed (basin, split EOS):
+    - ROMS_GPU_OMEGA_HB: the predictor's omega forms pre_step3d's
+      Hz_bak/Hz_fwd of the interior cells;
+    - ROMS_GPU_P_IN_RHO: every rho_eos also forms prsgrd's P in its sweep,
+      so whole steps skip k_prsgrd_P."""
     if case == "basin":
         cfg = basin_cfg(LLm=70, MMm=40, N=12, nonlin=True)
     else:
         cfg = oracle.filament_cfg(LLm=64, MMm=40, N=16, np_xi=1, np_eta=1)
     out = []
     for env in ("0", "1"):
-        monkeypatch.setenv("ROMS_GPU_OMEGA_HB", env)
+        monkeypatch.setenv(switch, env)
         m = romsgpu.Model.from_case(cfg.case_id, cfg.LLm, cfg.MMm, cfg.N, cfg.NT, salinity=bool(cfg.salinity),
                                     nonlin_eos=bool(cfg.nonlin_eos), dt=cfg.dt, ndtfast=cfg.ndtfast,
                                     sizex=cfg.sizex, sizey=cfg.sizey)

@@ -571,7 +571,7 @@ __global__ void __launch_bounds__(kFT) k_prsgrd_fused(Dev d, Range R, int split,
   }
 }
 
-void launch_prsgrd(const Dev& d, hipStream_t s, const Tlev& t, int uv_up) {
+void launch_prsgrd(const Dev& d, hipStream_t s, const Tlev& t, int uv_up, bool p_ready) {
   const Bounds& b = d.b;
   const int split = d.p.nonlin_eos;
   int imin, imax, jmin, jmax;
@@ -590,7 +590,7 @@ void launch_prsgrd(const Dev& d, hipStream_t s, const Tlev& t, int uv_up) {
   }
   // two-kernel form (default; k_prsgrd_fused with ROMS_GPU_PRSGRD_FUSED=1)
   Range R1{0, b.Lm, 0, b.Mm};
-  hipLaunchKernelGGL(k_prsgrd_P, grid_of(R1), dim3(kBX, kBY), 0, s, d, R1, split, d.p.tides);
+  if (!p_ready) hipLaunchKernelGGL(k_prsgrd_P, grid_of(R1), dim3(kBX, kBY), 0, s, d, R1, split, d.p.tides);
   ktimer_mark(s, kTimedPrsgrdUv, 0);
   if (uv_up >= 0)
     hipLaunchKernelGGL(k_prsgrd_uv<true>, grid3_of(R2, b.N), dim3(kBX, kBY), 0, s, d, R2, split, imin, imax, jmin, jmax,

@@ -602,6 +602,93 @@ bool launch_omega(const Dev& d, hipStream_t s, const Tlev& t, double hcff) {
 // Linear EOS -> rho; NONLIN_EOS -> JM95 split form rho1,qp1 (DUKO_2001).
 // bvf for LMD; VAR_RHO_2D column integrals rhoA, rhoS.
 // ---------------------------------------------------------------------------
+// prsgrd's hydrostatic pressure P (k_prsgrd_P, prsgrd.F:200-330) carried
+// along rho_eos's own top-down sweep (kP, ROMS_GPU_P_IN_RHO): the sweep has
+// z_r and the fresh rho1/qp1 (rho) of every level in registers, so P costs no
+// reads of its own.  P of level m needs level m-1, so it runs one level
+// behind: level(k) feeds the values of level k and completes P(k+1); last()
+// completes P(1).  Expressions and order of k_prsgrd_P (bit-identical).
+struct PColumn {
+  double g, grho, HalfGRho, qp2, zwN, ptide;
+  bool split, tides, doP;
+  double* Pp;
+  long n2;
+  int N;
+  double zC, rC, qC;                     // level m (pending)
+  double eZk, eRk, dZ1, dR1, P1, z1, v1;
+  __device__ __forceinline__ double rhov(double r1, double q1, double z) const {
+    if (split) {
+      const double dpth = -z;
+      return r1 + q1 * dpth * (1.0 - qp2 * dpth);
+    }
+    return r1;
+  }
+  __device__ __forceinline__ double eRof(double ru, double rl, double qu, double ql, double zu, double zl) const {
+    if (split) {
+      const double dpth = -0.5 * (zu + zl);
+      return ru - rl + (qu - ql) * dpth * (1.0 - qp2 * dpth);
+    }
+    return ru - rl;
+  }
+  // P-iteration of level m with level m-1 = (zM, rM, qM) (m >= 2) or none (m = 1)
+  __device__ __forceinline__ void iter(int m, double zM, double rM, double qM) {
+    const double OneFifth = 0.2, OneTwelfth = 1.0 / 12.0;
+    if (m == N) {
+      eZk = zC - zM;
+      eRk = eRof(rC, rM, qC, qM, zC, zM);   // e(N) = e(N-1)
+      dZ1 = 0.0; dR1 = 0.0; P1 = 0.0; z1 = 0.0; v1 = 0.0;
+    }
+    double eZm, eRm;
+    if (m >= 2) { eZm = zC - zM; eRm = eRof(rC, rM, qC, qM, zC, zM); }
+    else { eZm = eZk; eRm = eRk; }     // e(0) = e(1)
+    const double dZk = [&] { const double c = 2.0 * eZk * eZm; return c / (eZk + eZm); }();
+    double dRk;
+    {
+      const double c = 2.0 * eRk * eRm;
+      dRk = c > 0.0 ? c / (eRk + eRm) : 0.0;
+    }
+    const double v0 = rhov(rC, qC, zC);
+    if (split) {
+      const double dpth = -zC;
+      dRk = dRk - qC * dZk * (1.0 - 2.0 * qp2 * dpth);
+    }
+    double Pk;
+    if (m == N) {
+      const double rNm = rhov(rM, qM, zM);
+      Pk = g * zwN + grho * (v0 + 0.5 * (v0 - rNm) * (zwN - zC) / (zC - zM)) * (zwN - zC);
+      if (tides) Pk = Pk - g * ptide;
+    } else {
+      Pk = P1 + HalfGRho * ((v1 + v0) * (z1 - zC) -
+                            OneFifth * ((dR1 - dRk) * (z1 - zC - OneTwelfth * (dZ1 + dZk)) -
+                                        (dZ1 - dZk) * (v1 - v0 - OneTwelfth * (dR1 + dRk))));
+    }
+    if (doP) Pp[(long)(m - 1) * n2] = Pk;
+    P1 = Pk;
+    dZ1 = dZk; dR1 = dRk;
+    eZk = eZm; eRk = eRm;
+    z1 = zC; v1 = v0;
+  }
+  // rho_eos produced level k (k = N..1)
+  __device__ __forceinline__ void level(int k, double z, double r, double q) {
+    if (k < N) iter(k + 1, z, r, q);
+    zC = z; rC = r; qC = q;
+  }
+  __device__ __forceinline__ void last() { iter(1, 0.0, 0.0, 0.0); }
+};
+__device__ __forceinline__ PColumn p_column(const Dev& d, int i, int j, long ij, bool split) {
+  const Bounds& b = d.b;
+  PColumn c;
+  c.g = d.p.g; c.grho = d.p.g / d.p.rho0; c.HalfGRho = 0.5 * c.grho; c.qp2 = d.p.qp2;
+  c.split = split; c.tides = d.p.tides != 0; c.N = b.N; c.n2 = b.n2;
+  // k_prsgrd_P's range (0..Lm x 0..Mm) and its doP columns
+  c.doP = i >= 0 && i <= b.Lm && j >= 0 && j <= b.Mm && i >= b.istrU - 1 && i <= b.iend;
+  c.Pp = d.f.P + ij;
+  c.zwN = d.f.z_w[ij + (long)b.N * b.n2];
+  c.ptide = c.tides ? d.f.ptide[ij] : 0.0;
+  return c;
+}
+
+template <bool kP>
 __global__ void __launch_bounds__(256) k_rho_eos_linear(Dev d, Range R, int tidx) {
   ROMS_IJ_OR_RETURN(R)
   const Bounds& b = d.b;
@@ -622,9 +709,13 @@ __global__ void __launch_bounds__(256) k_rho_eos_linear(Dev d, Range R, int tidx
     return r * rm;
   };
   // rho(k) and the VAR_RHO_2D integrals from the top down in one pass
+  PColumn pc;
+  if constexpr (kP) pc = p_column(d, i, j, ij, false);
+  const double* __restrict__ zrp = F.z_r + ij;
   long o = (long)(N - 1) * n2;
   double rk = rhok(o);
   rho[o] = rk;
+  if constexpr (kP) pc.level(N, zrp[o], rk, 0.0);
   double cff = Hz[o] * rk;
   double rhoS = 0.5 * cff * Hz[o];
   double rhoA = cff;
@@ -633,11 +724,13 @@ __global__ void __launch_bounds__(256) k_rho_eos_linear(Dev d, Range R, int tidx
     o = (long)(k - 1) * n2;
     rk = rhok(o);
     rho[o] = rk;
+    if constexpr (kP) pc.level(k, zrp[o], rk, 0.0);
     const double hz = Hz[o];
     cff = hz * rk;
     rhoS = rhoS + hz * (rhoA + 0.5 * cff);
     rhoA = rhoA + cff;
   }
+  if constexpr (kP) pc.last();
   if (P.lmd) {
     const double c = P.g / P.rho0;
     const double* __restrict__ zr = F.z_r + ij;
@@ -655,6 +748,7 @@ __global__ void __launch_bounds__(256) k_rho_eos_linear(Dev d, Range R, int tidx
   F.rhoS[ij] = 2.0 * cff * cff * cff1 * rhoS;
 }
 
+template <bool kP>
 __global__ void __launch_bounds__(256) k_rho_eos_split(Dev d, Range R, int tidx) {
   ROMS_IJ_OR_RETURN(R)
   const Bounds& b = d.b;
@@ -689,6 +783,8 @@ __global__ void __launch_bounds__(256) k_rho_eos_split(Dev d, Range R, int tidx)
   const double gr = P.g / rho0;
   double r1p = 0.0, q1p = 0.0, zrp = 0.0;  // level k+1
   double rhoA = 0.0, rhoS = 0.0;
+  PColumn pc;
+  if constexpr (kP) pc = p_column(d, i, j, ij, true);
 #pragma unroll 4
   for (int k = N; k >= 1; k--) {
     const long o = (long)(k - 1) * n2;
@@ -705,6 +801,7 @@ __global__ void __launch_bounds__(256) k_rho_eos_split(Dev d, Range R, int tidx)
     const double q1 = 0.1 * (rho0 + r1) * (K0_Duk - K0) / ((K00 + K0) * (K00 + K0_Duk)) * rm;
     qp1[o] = q1;
     const double zrk = zr[o], hz = Hz[o];
+    if constexpr (kP) pc.level(k, zrk, r1, q1);
     if (lmd && k < N) {
       const double dpth = -0.5 * (zrp + zrk);
       bvf[(long)k * n2] = -gr * (r1p - r1 + (q1p - q1) * dpth * (1.0 - qp2 * dpth)) / (zrp - zrk) * rm;
@@ -720,6 +817,7 @@ __global__ void __launch_bounds__(256) k_rho_eos_split(Dev d, Range R, int tidx)
     }
     r1p = r1; q1p = q1; zrp = zrk;
   }
+  if constexpr (kP) pc.last();
   if (lmd) {
     bvf[(long)N * n2] = bvf[(long)(N - 1) * n2];
     bvf[0] = bvf[n2];
@@ -730,13 +828,27 @@ __global__ void __launch_bounds__(256) k_rho_eos_split(Dev d, Range R, int tidx)
   F.rhoS[ij] = 2.0 * cff * cff * cff1 * rhoS;
 }
 
+// P in rho_eos (PColumn): every rho_eos of the library then leaves P
+// current for its rho1/qp1, so whole steps skip k_prsgrd_P.  Split EOS only:
+// the linear EOS sweep is short and memory-bound, and P's per-level division
+// chain at its lower occupancy made it slower than k_prsgrd_P
+// (r3_zl_p_in_rho_ab.txt: C2 +0.08 ms/step, C3 -2.2 ms/step)
+bool p_in_rho(const Dev& d) {
+  const Bounds& b = d.b;
+  return d.p.p_in_rho && d.p.nonlin_eos && d.p.prs_split && !d.p.tides && b.N >= 2 && b.istrE <= 0 &&
+         b.iendE >= b.Lm && b.jstrE <= 0 && b.jendE >= b.Mm;
+}
 void launch_rho_eos(const Dev& d, hipStream_t s, const Tlev& t, int tidx) {
   const Bounds& b = d.b;
   Range R{b.istrE, b.iendE, b.jstrE, b.jendE};
-  if (d.p.nonlin_eos)
-    hipLaunchKernelGGL(k_rho_eos_split, grid_of(R), dim3(kBX, kBY), 0, s, d, R, tidx);
-  else
-    hipLaunchKernelGGL(k_rho_eos_linear, grid_of(R), dim3(kBX, kBY), 0, s, d, R, tidx);
+  const bool kp = p_in_rho(d);
+  if (d.p.nonlin_eos) {
+    if (kp) hipLaunchKernelGGL(k_rho_eos_split<true>, grid_of(R), dim3(kBX, kBY), 0, s, d, R, tidx);
+    else hipLaunchKernelGGL(k_rho_eos_split<false>, grid_of(R), dim3(kBX, kBY), 0, s, d, R, tidx);
+  } else {
+    if (kp) hipLaunchKernelGGL(k_rho_eos_linear<true>, grid_of(R), dim3(kBX, kBY), 0, s, d, R, tidx);
+    else hipLaunchKernelGGL(k_rho_eos_linear<false>, grid_of(R), dim3(kBX, kBY), 0, s, d, R, tidx);
+  }
 }
 
 }  // namespace roms

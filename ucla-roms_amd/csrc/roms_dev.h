@@ -52,6 +52,7 @@ struct Params {
   int tile_grp;   // h_tile group width of the hoisted per-level kernels (ROMS_GPU_TILE_GRP; 0: xcd_tile order)
   int uv1_lds;    // k_uv1_seg: Hz pairs kept in LDS from the spline phase, rufrc chained (ROMS_GPU_UV1_LDS=0: reloads)
   int omega_seg;  // omega: segment form k_omega_seg, one read of each input (ROMS_GPU_OMEGA_SEG=0: two-pass k_omega)
+  int p_in_rho;   // rho_eos's sweep also forms prsgrd's P (ROMS_GPU_P_IN_RHO=0: k_prsgrd_P)
   int omega_hb;   // the predictor's omega forms pre_step3d's Hz_bak/Hz_fwd (ROMS_GPU_OMEGA_HB=0: pre_step3d does)
   int preuv_lds;  // k_pre_uv_seg: u(indx) stored and u(nstp)/u(indx) combined in the spline phase (ROMS_GPU_PREUV_LDS=0: reloads)
   int seg_jrows;  // rows j per block of the momentum segment solvers (1..kSegJMax; ROMS_GPU_SEG_JROWS)
@@ -334,7 +335,9 @@ void launch_rho_eos(const Dev& d, hipStream_t s, const Tlev& t, int tidx);
 // uv_up >= 0: also add the horizontal momentum r.h.s. (UPSTREAM_UV if 1) of
 // the following pre_step3d / step3d_uv1 (prsgrd_can_fuse_uv; the caller then
 // passes uv_done to it)
-void launch_prsgrd(const Dev& d, hipStream_t s, const Tlev& t, int uv_up = -1);
+// p_ready: P is current from the last rho_eos (p_in_rho), k_prsgrd_P is skipped
+void launch_prsgrd(const Dev& d, hipStream_t s, const Tlev& t, int uv_up = -1, bool p_ready = false);
+bool p_in_rho(const Dev& d);   // every rho_eos also forms prsgrd's P (k_vertical.hip)
 bool prsgrd_can_fuse_uv(const Dev& d);
 // hb_done: the interior cells' Hz_bak/Hz_fwd are in c3/c2 already (launch_omega)
 void launch_pre_step3d(const Dev& d, hipStream_t s, const Tlev& t, bool uv_done = false, bool hb_done = false);

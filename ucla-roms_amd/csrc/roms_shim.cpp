@@ -365,7 +365,10 @@ void enqueue_step(roms_tlev* t, bool rho_current, bool store_huv) {
   // prsgrd kernel just before them (prsgrd_can_fuse_uv; nothing between the
   // two touches u, v(nrhs), FlxU, FlxV, Hz or ru, rv)
   const bool fuse_uv = prsgrd_can_fuse_uv(d);
-  TIMED(ROMS_R_PRSGRD, launch_prsgrd(d, s, T, fuse_uv ? 0 : -1));
+  // every rho_eos of the library leaves P current (p_in_rho): the
+  // step-opening one, or the previous step's closing one it reuses
+  const bool p_ready = p_in_rho(d);
+  TIMED(ROMS_R_PRSGRD, launch_prsgrd(d, s, T, fuse_uv ? 0 : -1, p_ready));
   TIMED(ROMS_R_PRE_STEP3D, launch_pre_step3d(d, s, T, fuse_uv, hb_done));
   TIMED(ROMS_R_SET_HUV1, launch_set_huv1(d, s, T));
   t->nrhs = 3;
@@ -377,7 +380,7 @@ void enqueue_step(roms_tlev* t, bool rho_current, bool store_huv) {
   launch_bulk_flux(d, s, T.nrhs);   // set_forces (main.F:433): BULK_FRC only
   if (g.cfg.lmd_mixing) TIMED(ROMS_R_LMD_VMIX, launch_lmd_vmix(d, s, T, T.nrhs));
   frc_step_phase(d, s, 3, pot);     // set_bry_all 'forward' + set_tides (main.F:438-441)
-  TIMED(ROMS_R_PRSGRD, launch_prsgrd(d, s, T, fuse_uv ? 1 : -1));
+  TIMED(ROMS_R_PRSGRD, launch_prsgrd(d, s, T, fuse_uv ? 1 : -1, p_ready));
   TIMED(ROMS_R_STEP3D_UV1, launch_step3d_uv1(d, s, T, fuse_uv));
   if (g.cfg.uv_vis2) TIMED(ROMS_R_VISC3D, launch_visc3d(d, s, T));
   for (int iif = 1; iif <= t->nfast; iif++) {
@@ -580,6 +583,10 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
   {
     const char* e = getenv("ROMS_GPU_UV1_LDS");
     P.uv1_lds = !(e && e[0] == '0');
+  }
+  {
+    const char* e = getenv("ROMS_GPU_P_IN_RHO");
+    P.p_in_rho = !(e && e[0] == '0');
   }
   {
     const char* e = getenv("ROMS_GPU_OMEGA_HB");
