@@ -33,6 +33,7 @@ module roms_gpu_mod
     integer(c_int) :: uv_adv, uv_cor             ! UV_ADV, UV_COR
     integer(c_int) :: pot_tides                  ! TIDES pot_tides
     integer(c_int) :: bulk_frc                   ! BULK_FRC
+    integer(c_int) :: adv_isoneutral             ! ADV_ISONEUTRAL (+SW_TRIADS, STABILIZE)
   end type
 
   type, bind(c) :: roms_tlev
@@ -51,12 +52,13 @@ module roms_gpu_mod
     integer(c_int) :: curvgrid
     integer(c_int) :: uv_adv, uv_cor
     integer(c_int) :: bulk_frc
+    integer(c_int) :: adv_isoneutral
   end type
 
   ! LMD switch bits of lmd_mixing (ROMS_LMD_*)
   integer(c_int), parameter :: ROMS_LMD_MIXING = 1, ROMS_LMD_KPP = 2, ROMS_LMD_BKPP = 4, ROMS_LMD_RIMIX = 8, &
                                ROMS_LMD_CONVEC = 16, ROMS_LMD_NONLOCAL = 32, ROMS_LMD_DDMIX = 64
-  integer(c_int), parameter :: ROMS_GPU_ABI = 11   ! ROMS_GPU_ABI_VERSION, include/roms_gpu.h
+  integer(c_int), parameter :: ROMS_GPU_ABI = 12   ! ROMS_GPU_ABI_VERSION, include/roms_gpu.h
   integer(c_int), parameter :: ROMS_FRC_SURFACE = 1, ROMS_FRC_BRY = 2
 
   ! field ids (enum roms_field) used by the drivers below

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define ROMS_GPU_ABI_VERSION 11
+#define ROMS_GPU_ABI_VERSION 12
 #define ROMS_MAX_FAST 288
 
 /* Subdomain geometry of this rank: param.F / dimensions.F / mpi_setup.F:39-210 */
@@ -88,6 +88,11 @@ typedef struct roms_cfg {
   int bulk_frc;                  /* BULK_FRC: the surface fluxes come from roms_gpu_bulk_flux (COARE,
                                     bulk_frc.F:143-913) at both set_forces points of the step, and
                                     lmd_kpp's u* from the rho-point stresses (lmd_kpp.F:173-174)     */
+  int adv_isoneutral;            /* ADV_ISONEUTRAL (with SW_TRIADS and STABILIZE, step3d_t_ISO.F:15-18):
+                                    corrector prsgrd forms the slopes dRdx/dRde (prsgrd.F:307-338),
+                                    step3d_uv2 diff3u/diff3v/idRz (step3d_uv2.F:572-697), step3d_t
+                                    centred (not UPSTREAM_TS) fluxes, the rotated biharmonic operator
+                                    and Akt+Akz in the implicit diffusion (step3d_t_ISO.F:253-1065)  */
 } roms_cfg;
 
 /* Time-step indices (scalars.F:32-36).  The step entry updates them. */
@@ -236,6 +241,7 @@ typedef struct roms_case {
   int uv_adv, uv_cor;  /* UV_ADV, UV_COR (every reference case defines both: set 1, 1)          */
   int bulk_frc;   /* basin only: BULK_FRC with an analytic atmosphere (westerly jet, cool humid air)
                      uploaded as ROMS_uwnd .. ROMS_lwrad; roms_cfg.bulk_frc                         */
+  int adv_isoneutral;  /* ADV_ISONEUTRAL (roms_cfg.adv_isoneutral), any case                            */
 } roms_case;
 /* Builds the analytic grid/ICs on the host (setup_grid1/2, set_scoord,
  * set_weights, ana_init), initialises the device and runs roms_init.        */

@@ -35,7 +35,7 @@ class OrCfg(ctypes.Structure):
                 ("obc", ctypes.c_int), ("ubind", ctypes.c_double), ("v_sponge", ctypes.c_double),
                 ("island", ctypes.c_int), ("curvgrid", ctypes.c_int), ("uv_adv", ctypes.c_int),
                 ("uv_cor", ctypes.c_int), ("pot_tides", ctypes.c_int),
-                ("bulk_frc", ctypes.c_int)]
+                ("bulk_frc", ctypes.c_int), ("adv_isoneutral", ctypes.c_int)]
 
     def __init__(self, *a, **k):
         super().__init__(*a, **k)

@@ -67,6 +67,11 @@ struct or_state {
   struct { double *dst; size_t n; int bry; double t[2]; double *rec[2]; } frc[64];
   int nfrc, frc_clock;
   double frc_start;
+  /* ADV_ISONEUTRAL (oracle_iso.c): eos_vars.F:28-31 slopes and inverse
+     vertical gradient, mixing.F:24-27 diff3u/v, step3d_t's Akz (0:N), and
+     the operator's two-slice scratch FSC, dTdz, dTdx, dTde (2 x n2) + LapT */
+  double *dRdx, *dRde, *idRz, *diff3u, *diff3v, *Akz;
+  double *iso_FSC, *iso_dTdz, *iso_dTdx, *iso_dTde, *iso_LapT;
   /* private scratch (A3d(:,1..4), A2d(:,1..)) */
   double *ru, *rv, *P, *rhos3;         /* 3-D scratch */
   double *s2[14];                      /* 2-D scratch */
@@ -130,4 +135,11 @@ void or_ana_forces(or_state *S);
 /* LMD/KPP (oracle_lmd.c) */
 void or_lmd_vmix_impl(or_state *S, int tind);
 void or_lmd_alloc(or_state *S);
+/* ADV_ISONEUTRAL (oracle_iso.c) */
+void or_iso_dRdx(or_state *S, int k, double *rx, int imin, int imax);
+void or_iso_dRde(or_state *S, int k, double *rx, int jmin, int jmax);
+void or_iso_exch_slopes(or_state *S);
+void or_iso_diff3(or_state *S, int iu0, int iu1, int iv0, int iv1, int j0, int j1);
+void or_iso_exch_diff3(or_state *S);
+void or_iso_tracer(or_state *S, int itrc);
 #endif

@@ -61,6 +61,12 @@ or_state *or_create(const or_cfg *cfg) {
   for (int q = 0; q < 14; q++) S->s2[q] = zalloc(n2);
   for (int q = 0; q < 6; q++) S->c1[q] = zalloc((size_t)S->nx2 * (S->N + 1));
   if (cfg->lmd) or_lmd_alloc(S);
+  if (cfg->adv_isoneutral) {
+    S->dRdx = zalloc(n3); S->dRde = zalloc(n3); S->idRz = zalloc(n3w);
+    S->diff3u = zalloc(n3); S->diff3v = zalloc(n3); S->Akz = zalloc(n3w);
+    S->iso_FSC = zalloc(2 * n2); S->iso_dTdz = zalloc(2 * n2); S->iso_dTdx = zalloc(2 * n2);
+    S->iso_dTde = zalloc(2 * n2); S->iso_LapT = zalloc(n3);
+  }
   S->pipe_flx = zalloc(n2); S->pipe_idx = zalloc(n2);
   S->npip = 1;
   S->pipe_prf = zalloc((size_t)S->N); S->pipe_trc = zalloc((size_t)S->NT);
@@ -910,6 +916,9 @@ double *or_field(or_state *S, const char *name, size_t *count) {
       {"srflx", S->srflx, S->n2}, {"swflx", S->swflx, S->n2}, {"hbls", S->hbls, S->n2}, {"hbbl", S->hbbl, S->n2},
       {"ghat", S->ghat, S->n3w}, {"swr_frac", S->swr_frac, S->n3w}, {"Cs_w", S->Cs_w, (size_t)S->N + 1},
       {"Cs_r", S->Cs_r, (size_t)S->N + 1},
+      {"dRdx", S->dRdx, S->dRdx ? S->n3 : 0}, {"dRde", S->dRde, S->dRde ? S->n3 : 0},
+      {"idRz", S->idRz, S->idRz ? S->n3w : 0}, {"diff3u", S->diff3u, S->diff3u ? S->n3 : 0},
+      {"diff3v", S->diff3v, S->diff3v ? S->n3 : 0}, {"Akz", S->Akz, S->Akz ? S->n3w : 0},
   };
   for (size_t q = 0; q < sizeof(tab) / sizeof(tab[0]); q++)
     if (strcmp(tab[q].n, name) == 0) { if (count) *count = tab[q].c; return tab[q].p; }

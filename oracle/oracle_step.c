@@ -482,6 +482,9 @@ void or_prsgrd(or_state *S) {
                                           OneTwelfth * (A2(dRx, i, j) + A2(dRx, i - 1, j))))));
       }
     }
+    /* ADV_ISONEUTRAL, corrector stage: slopes dRdx from this k's rx (prsgrd.F:307-338) */
+    const int iso = S->c.adv_isoneutral && S->nrhs == 3;
+    if (iso) or_iso_dRdx(S, k, rx, imin, imax);
     /* ETA component */
     for (int j = jmin; j <= jmax; j++)
       for (int i = S->istr; i <= S->iend; i++) {
@@ -524,7 +527,9 @@ void or_prsgrd(or_state *S) {
                                             OneTwelfth * (A2(dRx, i, j) + A2(dRx, i, j - 1))))));
         }
     }
+    if (iso) or_iso_dRde(S, k, rx, jmin, jmax);   /* prsgrd.F:423-453 */
   }
+  if (S->c.adv_isoneutral && S->nrhs == 3) or_iso_exch_slopes(S);   /* step3d_uv1.F:529-532 */
 }
 
 /* ---------------------------------------------------------------------- */
@@ -1494,7 +1499,9 @@ void or_step3d_uv2(or_state *S) {
         for (int i = iv0; i <= iv1; i++) FLXV(i, j, k) = C1(CF, i, k) - C1(DC, i, k) * C1(CF, i, 0);
     }
   }
+  if (S->c.adv_isoneutral) or_iso_diff3(S, iu0, iu1, iv0, iv1, j0, j1);   /* before the river faces */
   if (S->river_source) river_uv(S, nnew, S->istr);
+  if (S->c.adv_isoneutral) or_iso_exch_diff3(S);   /* step3d_uv2.F:730-732 */
   or_exch3(S, S->FlxU, N);
   or_exch3(S, S->u + (size_t)(nnew - 1) * S->n3, N);
   or_exch2(S, S->ubar + (size_t)(knew - 1) * S->n2);
@@ -1511,14 +1518,16 @@ void or_step3d_t(or_state *S) {
   const double dt = S->dt;
   double *FX = S->s2[4], *FE = S->s2[5], *wrk1 = S->s2[6];
   double *WC = S->c1[0], *FC = S->c1[1], *CF = S->c1[2], *DC = S->c1[3];
+  const int iso = S->c.adv_isoneutral;   /* ADV_ISONEUTRAL: centred fluxes (no UPSTREAM_TS, step3d_t_ISO.F:4-6) */
   for (int itrc = 1; itrc <= NT; itrc++) {
     for (int k = 1; k <= N; k++) {
-      horiz_tracer_fluxes(S, k, itrc, nrhs, 1, FX, FE, wrk1);
+      horiz_tracer_fluxes(S, k, itrc, nrhs, !iso, FX, FE, wrk1);
       for (int j = S->jstr; j <= S->jend; j++)
         for (int i = S->istr; i <= S->iend; i++)
           TT(i, j, k, nnew, itrc) = TT(i, j, k, nnew, itrc) - dt * A2(S->pm, i, j) * A2(S->pn, i, j) *
                                                                   (A2(FX, i + 1, j) - A2(FX, i, j) + A2(FE, i, j + 1) - A2(FE, i, j));
     }
+    if (iso) or_iso_tracer(S, itrc);   /* step3d_t_ISO.F:253-846 */
     for (int j = S->jstr; j <= S->jend; j++) {
       vert_tracer_fluxes(S, j, itrc, nrhs, FC, CF, S->Hz);
       for (int k = 1; k <= N; k++)
@@ -1565,7 +1574,9 @@ void or_step3d_t(or_state *S) {
       const int iAkt = itrc < S->nTS ? itrc : S->nTS;
       for (int i = S->istr; i <= S->iend; i++) {
         C1(DC, i, 0) = dt * A2(S->pm, i, j) * A2(S->pn, i, j);
-        C1(FC, i, 1) = 2.0 * dt * AKT(i, j, 1, iAkt) / (HZ(i, j, 1) + HZ(i, j, 2));
+        /* ADV_ISONEUTRAL && STABILIZE: Akt + Akz (step3d_t_ISO.F:1049-1053) */
+        C1(FC, i, 1) = 2.0 * dt * (iso ? AKT(i, j, 1, iAkt) + W3(S->Akz, i, j, 1) : AKT(i, j, 1, iAkt)) /
+                       (HZ(i, j, 1) + HZ(i, j, 2));
         C1(WC, i, 1) = C1(DC, i, 0) * WI(i, j, 1);
         const double cff = 1.0 / (HZ(i, j, 1) + C1(FC, i, 1) + fmax0(C1(WC, i, 1)));
         C1(CF, i, 1) = cff * (C1(FC, i, 1) - fmin0(C1(WC, i, 1)));
@@ -1573,7 +1584,8 @@ void or_step3d_t(or_state *S) {
       }
       for (int k = 2; k <= N - 1; k++)
         for (int i = S->istr; i <= S->iend; i++) {
-          C1(FC, i, k) = 2.0 * dt * AKT(i, j, k, iAkt) / (HZ(i, j, k) + HZ(i, j, k + 1));
+          C1(FC, i, k) = 2.0 * dt * (iso ? AKT(i, j, k, iAkt) + W3(S->Akz, i, j, k) : AKT(i, j, k, iAkt)) /
+                         (HZ(i, j, k) + HZ(i, j, k + 1));
           C1(WC, i, k) = WI(i, j, k) * C1(DC, i, 0);
           const double cff = 1.0 / (HZ(i, j, k) + C1(FC, i, k) + fmax0(C1(WC, i, k)) + C1(FC, i, k - 1) - fmin0(C1(WC, i, k - 1)) -
                                     C1(CF, i, k - 1) * (C1(FC, i, k - 1) + fmax0(C1(WC, i, k - 1))));

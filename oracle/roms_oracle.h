@@ -53,6 +53,7 @@ typedef struct or_cfg {
   int uv_adv, uv_cor;            /* UV_ADV, UV_COR */
   int pot_tides;                 /* TIDES pot_tides: ptide in prsgrd (prsgrd.F:209-211) */
   int bulk_frc;                  /* BULK_FRC (bulk_frc.F); basin: analytic atmosphere (oracle_main.c) */
+  int adv_isoneutral;            /* ADV_ISONEUTRAL (+SW_TRIADS, STABILIZE): oracle_iso.c */
 } or_cfg;
 
 typedef struct or_state or_state;

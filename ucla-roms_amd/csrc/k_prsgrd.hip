@@ -573,6 +573,7 @@ __global__ void __launch_bounds__(kFT) k_prsgrd_fused(Dev d, Range R, int split,
 
 void launch_prsgrd(const Dev& d, hipStream_t s, const Tlev& t, int uv_up, bool p_ready) {
   const Bounds& b = d.b;
+  if (d.p.iso && t.nrhs == 3) launch_iso_slopes(d, s);   // ADV_ISONEUTRAL, CORR_STAGE (prsgrd.F:307-338)
   const int split = d.p.nonlin_eos;
   int imin, imax, jmin, jmax;
   if (!b.ew_periodic) {

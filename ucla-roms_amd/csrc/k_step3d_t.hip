@@ -7,7 +7,8 @@
 namespace roms {
 
 // Horizontal advection, one thread per (i,j,k) cell, all tracers.
-__global__ void __launch_bounds__(256) k_step3d_t_h(Dev d, Range R, int nnew, int nrhs) {
+// up: UPSTREAM_TS; ADV_ISONEUTRAL builds without it (step3d_t_ISO.F:4-6)
+__global__ void __launch_bounds__(256) k_step3d_t_h(Dev d, Range R, int nnew, int nrhs, int up) {
   const uint3 bI = xcd_tile();
   __shared__ TracerWin W;
   const Bounds& b = d.b;
@@ -29,8 +30,8 @@ __global__ void __launch_bounds__(256) k_step3d_t_h(Dev d, Range R, int nnew, in
     __syncthreads();
     if (!act) continue;
     double* Tn = F.t + (long)(nnew - 1) * b.n3 + tb;
-    double FX0 = tracer_fx(b, a, i, j, true), FX1 = tracer_fx(b, a, i + 1, j, true);
-    double FE0 = tracer_fe(b, a, i, j, true), FE1 = tracer_fe(b, a, i, j + 1, true);
+    double FX0 = tracer_fx(b, a, i, j, up), FX1 = tracer_fx(b, a, i + 1, j, up);
+    double FE0 = tracer_fe(b, a, i, j, up), FE1 = tracer_fe(b, a, i, j + 1, up);
     if (d.p.nriv > 0) {   // river inflow faces (compute_horiz_tracer_fluxes.h:217-246)
       river_tracer_flux(d, 0, i, j, k, itrc, FX0); river_tracer_flux(d, 0, i + 1, j, k, itrc, FX1);
       river_tracer_flux(d, 1, i, j, k, itrc, FE0); river_tracer_flux(d, 1, i, j + 1, k, itrc, FE1);
@@ -108,7 +109,8 @@ __global__ void __launch_bounds__(kBX * TY) k_step3d_t_h1(Dev d, Range R, int nn
 // Vertical part per column: spline advection on t(nrhs), surface fluxes
 // (+ KPP non-local and solar terms), implicit diffusion.  LDS slots: A holds
 // FC (spline) then DC(k) at A[k-1]; B holds the spline CF then Thomas CF.
-template <class C>
+// ISO: ADV_ISONEUTRAL's STABILIZE diffusivity Akz joins Akt (step3d_t_ISO.F:1049-1065)
+template <class C, bool ISO = false>
 __global__ void __launch_bounds__(64) k_step3d_t_v(Dev d, Range R, int nnew, int nrhs) {
   ROMS_IJC_OR_RETURN(R)
   col_lds_poison<C>(2, d.b.N);
@@ -132,7 +134,12 @@ __global__ void __launch_bounds__(64) k_step3d_t_v(Dev d, Range R, int nnew, int
     A[0] = 0.0;
     // advective update + surface/KPP terms fused into the Thomas elimination
     const int iAkt = itrc < b.nTS ? itrc : b.nTS;
-    const double* __restrict__ Akt = F.Akt + (long)(iAkt - 1) * b.n3w + ij;
+    const double* __restrict__ Akt0 = F.Akt + (long)(iAkt - 1) * b.n3w + ij;
+    const double* __restrict__ Akz = ISO ? F.Akz + ij : nullptr;
+    struct AktAkz {   // Akt(k) [+ Akz(k)]
+      const double *a, *z;
+      __device__ double operator[](long w) const { return ISO ? a[w] + z[w] : a[w]; }
+    } const Akt{Akt0, Akz};
     const double* __restrict__ Wi = F.Wi + ij;
     const double DC0 = dt * F.pm[ij] * F.pn[ij];
     const bool kppT = P.lmd && itrc == 1, kppS = P.lmd_nonlocal && itrc == 2 && P.salinity;
@@ -359,11 +366,29 @@ __global__ void __launch_bounds__(kSegBlock, 2) k_step3d_t_seg(Dev d, Range R, i
 void setup_column_kernels_t(size_t bytes) {
   (void)hipFuncSetAttribute((const void*)k_step3d_t_v<ColLds>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)bytes);
+  (void)hipFuncSetAttribute((const void*)k_step3d_t_v<ColLds, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)bytes);
 }
 
 void launch_step3d_t(const Dev& d, hipStream_t s, const Tlev& t) {
   const Bounds& b = d.b;
   Range R{b.istr, b.iend, b.jstr, b.jend};
+  if (d.p.iso) {
+    // ADV_ISONEUTRAL: centred horizontal fluxes, the rotated biharmonic
+    // operator per tracer, then the column part with Akt + Akz; in order,
+    // no rim-first overlap
+    hipLaunchKernelGGL(k_step3d_t_h, grid3_of(R, b.N), dim3(kBX, kBY), 0, s, d, R, t.nnew, t.nrhs, 0);
+    for (int itrc = 1; itrc <= b.NT; itrc++) launch_iso_tracer(d, s, t, itrc);
+    dim3 gt = gridc_of(R);
+    gt.z = b.NT;
+    if (d.f.colscr)
+      hipLaunchKernelGGL((k_step3d_t_v<ColGlb, true>), gt, dim3(kCX), 0, s, d, R, t.nnew, t.nrhs);
+    else
+      hipLaunchKernelGGL((k_step3d_t_v<ColLds, true>), gt, dim3(kCX), col_lds_bytes(2, b.N), s, d, R, t.nnew, t.nrhs);
+    for (int itrc = 1; itrc <= b.NT; itrc++) launch_t3dbc(d, s, t, itrc);
+    launch_exchange_tracers(d, s, t.nnew);
+    return;
+  }
   // horizontal fluxes, then the column solves, on a sub-range of the interior
   auto run = [&](const Range& r) {
     if (d.p.hoist && b.NT == 2 && d.p.h_ty == 8)
@@ -373,7 +398,7 @@ void launch_step3d_t(const Dev& d, hipStream_t s, const Tlev& t) {
     else if (d.p.hoist && b.NT == 1)
       hipLaunchKernelGGL((k_step3d_t_h1<1, 4>), grid3_ty(r, b.N, 4), dim3(kBX, 4), 0, s, d, r, t.nnew, t.nrhs);
     else
-      hipLaunchKernelGGL(k_step3d_t_h, grid3_of(r, b.N), dim3(kBX, kBY), 0, s, d, r, t.nnew, t.nrhs);
+      hipLaunchKernelGGL(k_step3d_t_h, grid3_of(r, b.N), dim3(kBX, kBY), 0, s, d, r, t.nnew, t.nrhs, 1);
     dim3 gt = gridc_of(r);
     gt.z = b.NT;
     if (d.p.colseg) {

@@ -842,7 +842,10 @@ void launch_step3d_uv2(const Dev& d, hipStream_t s, const Tlev& t) {
     hipLaunchKernelGGL(k_uv2_flux, grid_of(R2), dim3(kBX, kBY), 0, s, d, R2, t.nnew, t.nstp, t.knew, iu0, iu1, iv0, iv1,
                        0);
   }
+  // ADV_ISONEUTRAL: diff3u/v and idRz from the corrected u,v(nnew), before the river faces
+  if (d.p.iso) launch_iso_diff3(d, s, t, iu0, iu1, iv0, iv1, j0, j1);
   launch_river_uv(d, s, t.nnew, 0);   // step3d_uv2.F:689-717
+  if (d.p.iso) launch_iso_exch_diff3(d, s);
   launch_exchange_list(d, s, ExchList{{d.f.FlxU, d.f.u + (long)(t.nnew - 1) * b.n3, d.f.ubar + (long)(t.knew - 1) * b.n2,
                                         d.f.FlxV, d.f.v + (long)(t.nnew - 1) * b.n3, d.f.vbar + (long)(t.knew - 1) * b.n2},
                                        {b.N, b.N, 1, b.N, b.N, 1}, 6});

@@ -33,6 +33,7 @@ struct Params {
   int nonlin_eos, salinity, lmd, uv_vis2, ts_dif2;
   int lmd_rimix, lmd_convec, lmd_nonlocal;  // LMD_RIMIX, LMD_CONVEC, LMD_NONLOCAL (lmd != 0: MIXING+KPP+BKPP)
   int lmd_ddmix;                            // LMD_DDMIX (needs SALINITY)
+  int iso;                                  // ADV_ISONEUTRAL (+SW_TRIADS, STABILIZE): k_iso.hip
   int uv_adv, uv_cor;                       // UV_ADV, UV_COR
   int tides;                                // TIDES pot_tides: ptide in prsgrd
   int bulk_frc;                             // BULK_FRC (k_bulk.hip; u* from sustr_r/svstr_r in lmd_kpp)
@@ -109,6 +110,11 @@ struct Fields {
   // column-solver scratch in global memory, 2*max(NT,2) slots of (0:N) levels
   // (nullptr: the solvers keep their columns in LDS; see ColGlb in k_common.h)
   double* colscr;
+  // ADV_ISONEUTRAL (k_iso.hip; nullptr when off): eos_vars.F:28-31 dRdx, dRde
+  // (N) and idRz (0:N), mixing.F:24-27 diff3u, diff3v (N), step3d_t's Akz
+  // (0:N), and the operator's 3-D work fields dTdz, FSC (0:N), dTdx, dTde, LapT (N)
+  double *dRdx, *dRde, *idRz, *diff3u, *diff3v, *Akz;
+  double *iso_dTdz, *iso_FSC, *iso_dTdx, *iso_dTde, *iso_LapT;
 };
 
 struct Halo;  // halo.h: multi-rank exchange state (host object; nullptr = single rank)
@@ -360,5 +366,12 @@ void launch_t3dbc(const Dev& d, hipStream_t s, const Tlev& t, int itrc);
 void launch_diag(const Dev& d, hipStream_t s, const Tlev& t, double* out);
 void launch_swr_frac(const Dev& d, hipStream_t s);
 void launch_lmd_vmix(const Dev& d, hipStream_t s, const Tlev& t, int tind);
+// ADV_ISONEUTRAL (k_iso.hip): prsgrd's corrector slopes (+ their exchange),
+// step3d_uv2's diff3u/diff3v/idRz over its flux-correction ranges and their
+// exchange, and step3d_t's rotated biharmonic operator for one tracer
+void launch_iso_slopes(const Dev& d, hipStream_t s);
+void launch_iso_diff3(const Dev& d, hipStream_t s, const Tlev& t, int iu0, int iu1, int iv0, int iv1, int j0, int j1);
+void launch_iso_exch_diff3(const Dev& d, hipStream_t s);
+void launch_iso_tracer(const Dev& d, hipStream_t s, const Tlev& t, int itrc);
 
 }  // namespace roms

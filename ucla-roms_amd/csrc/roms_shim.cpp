@@ -491,6 +491,7 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
   P.uv_adv = cfg->uv_adv != 0; P.uv_cor = cfg->uv_cor != 0;
   P.tides = cfg->pot_tides != 0;
   P.bulk_frc = cfg->bulk_frc != 0;
+  P.iso = cfg->adv_isoneutral != 0;
   {
     // fused one-kernel prsgrd (k_prsgrd_fused): bit-identical, fewer bytes,
     // but measured slower at C2 (0.50 vs 0.38 ms per call: a per-level walk
@@ -656,6 +657,14 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
   for (double** q : s2)
     if (scratch(*q, b.n2)) return -2;
   if (col_global && scratch(F.colscr, 2L * (b.NT > 2 ? b.NT : 2) * b.n3w)) return -2;
+  if (P.iso) {   // ADV_ISONEUTRAL fields (k_iso.hip), zero like the reference's allocations (eos_vars.F:50-52)
+    double** r3[] = {&F.dRdx, &F.dRde, &F.diff3u, &F.diff3v, &F.iso_dTdx, &F.iso_dTde, &F.iso_LapT};
+    for (double** q : r3)
+      if (scratch(*q, b.n3)) return -2;
+    double** w3[] = {&F.idRz, &F.Akz, &F.iso_dTdz, &F.iso_FSC};
+    for (double** q : w3)
+      if (scratch(*q, b.n3w)) return -2;
+  }
   if (P.lmd) {
     if (scratch(F.lmd_rig, b.n3w)) return -2;
     double** l2[] = {&F.lmd_hbl, &F.lmd_bbl, &F.lmd_Bo, &F.lmd_Bosol, &F.lmd_ustar};
@@ -1078,6 +1087,7 @@ static int init_case_impl(const roms_case* c, int np_xi, int np_eta, void* comm,
   C.curvgrid = c->case_id == ROMS_CASE_BASIN ? c->curvgrid : 0;
   C.uv_adv = c->uv_adv; C.uv_cor = c->uv_cor;
   C.bulk_frc = c->case_id == ROMS_CASE_BASIN ? c->bulk_frc : 0;
+  C.adv_isoneutral = c->adv_isoneutral;
   C.Akv_bak = (fil || pipes) ? 0.0 : 1.0e-4; C.Akt_bak[0] = (fil || pipes) ? 0.0 : 1.0e-5; C.Akt_bak[1] = C.Akt_bak[0];
   int r = roms_gpu_init(&D, &C, device, comm);
   if (r) return r;

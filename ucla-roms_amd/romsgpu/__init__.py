@@ -59,7 +59,7 @@ class Cfg(ctypes.Structure):
                 ("theta_s", ctypes.c_double), ("theta_b", ctypes.c_double), ("hc", ctypes.c_double),
                 ("obc", ctypes.c_int), ("ubind", ctypes.c_double), ("curvgrid", ctypes.c_int),
                 ("uv_adv", ctypes.c_int), ("uv_cor", ctypes.c_int), ("pot_tides", ctypes.c_int),
-                ("bulk_frc", ctypes.c_int)]
+                ("bulk_frc", ctypes.c_int), ("adv_isoneutral", ctypes.c_int)]
 
 
 class Tlev(ctypes.Structure):
@@ -77,7 +77,7 @@ class Case(ctypes.Structure):
                 ("sizex", ctypes.c_double), ("sizey", ctypes.c_double), ("surf_flux", ctypes.c_int),
                 ("obc", ctypes.c_int), ("v_sponge", ctypes.c_double), ("island", ctypes.c_int),
                 ("curvgrid", ctypes.c_int), ("uv_adv", ctypes.c_int), ("uv_cor", ctypes.c_int),
-                ("bulk_frc", ctypes.c_int)]
+                ("bulk_frc", ctypes.c_int), ("adv_isoneutral", ctypes.c_int)]
 
 
 ROUTINES_T = ["set_huv", "omega", "prsgrd", "pre_step3d", "set_huv1", "step3d_uv1", "visc3d", "step2d",
@@ -315,14 +315,14 @@ class Model:
     def from_case(cls, case_id, LLm, MMm, N, NT=1, salinity=False, nonlin_eos=False, dt=5.0, ndtfast=60,
                   sizex=12.8e3, sizey=3.2e3, device=0, np_xi=1, np_eta=1, comm=None, rank=0, lmd=False,
                   surf_flux=False, obc=0, v_sponge=0.0, island=False, curvgrid=False, uv_adv=True, uv_cor=True,
-                  bulk_frc=False):
+                  bulk_frc=False, adv_isoneutral=False):
         """Analytic case on the whole grid, or on subdomain `rank` of an
         np_xi x np_eta processor grid when a communicator is given.
         lmd: False, True (all LMD switches) or ROMS_LMD_* bits."""
         m = cls()
         c = Case(case_id, LLm, MMm, N, NT, int(salinity), int(nonlin_eos), lmd_bits(lmd), dt, ndtfast, sizex, sizey,
                  int(surf_flux), int(obc), float(v_sponge), int(island), int(curvgrid), int(uv_adv), int(uv_cor),
-                 int(bulk_frc))
+                 int(bulk_frc), int(adv_isoneutral))
         if comm is None and np_xi * np_eta == 1:
             m._chk(m.L.roms_gpu_init_case(ctypes.byref(c), device, ctypes.byref(m.t)), "roms_gpu_init_case")
         else:
