@@ -425,3 +425,45 @@ def test_step_producer_variants_bitwise(case, switch, monkeypatch):
         m.close()
     for n in out[0]:
         assert np.array_equal(out[0][n], out[1][n]), n
+
+
+@pytest.mark.parametrize("case", ["filament", "basin"])
+def test_prsgrd_uv_tile_rows_bitwise(case, monkeypatch):
+    """k_prsgrd_uv on 64x8 tiles (ROMS_GPU_PRS_TY=8) equals the 64x4 form
+    bitwise over 4 whole steps (periodic Filament, closed split-EOS basin)."""
+    if case == "basin":
+        cfg = basin_cfg(LLm=70, MMm=42, N=12, nonlin=True)
+    else:
+        cfg = oracle.filament_cfg(LLm=64, MMm=40, N=16, np_xi=1, np_eta=1)
+    out = []
+    for env in ("4", "8"):
+        monkeypatch.setenv("ROMS_GPU_PRS_TY", env)
+        m = romsgpu.Model.from_case(cfg.case_id, cfg.LLm, cfg.MMm, cfg.N, cfg.NT, salinity=bool(cfg.salinity),
+                                    nonlin_eos=bool(cfg.nonlin_eos), dt=cfg.dt, ndtfast=cfg.ndtfast,
+                                    sizex=cfg.sizex, sizey=cfg.sizey)
+        m.step(4)
+        out.append({n: m.get(n) for n in ("zeta", "ubar", "vbar", "u", "v", "t", "rufrc", "rvfrc")})
+        m.close()
+    for n in out[0]:
+        assert np.array_equal(out[0][n], out[1][n]), n
+
+
+@pytest.mark.parametrize("lmd", [oracle.LMD_ICELAND, oracle.LMD_ALL | oracle.LMD_DDMIX])
+def test_kpp_int_staged_rig_bitwise(lmd, monkeypatch):
+    """k_kpp_int with the Rig stencil windows staged in LDS (ROMS_GPU_KPP_TY
+    4 = the default, 8, 43) equals the one-row form (=0) bitwise over 4 whole steps of
+    the split-EOS basin with KPP (edge clamps at all four closed walls, a
+    partial last block row: MMm = 42)."""
+    cfg = basin_cfg(LLm=70, MMm=42, N=12, nonlin=True)
+    out = []
+    for env in ("0", "4", "8", "43"):   # one row; 64x4; 64x8; 64x4 at 3 waves/SIMD
+        monkeypatch.setenv("ROMS_GPU_KPP_TY", env)
+        m = romsgpu.Model.from_case(cfg.case_id, cfg.LLm, cfg.MMm, cfg.N, cfg.NT, salinity=True, nonlin_eos=True,
+                                    dt=cfg.dt, ndtfast=cfg.ndtfast, sizex=cfg.sizex, sizey=cfg.sizey, lmd=lmd,
+                                    surf_flux=True)
+        m.step(4)
+        out.append({n: m.get(n) for n in ("u", "v", "t", "Akv", "Akt", "hbls", "hbbl", "ghat")})
+        m.close()
+    for o in out[1:]:
+        for n in out[0]:
+            assert np.array_equal(out[0][n], o[n]), n

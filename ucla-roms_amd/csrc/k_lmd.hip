@@ -352,10 +352,26 @@ __global__ void __launch_bounds__(64, 4) k_kpp_ext(Dev d, Range E, int tind, int
 }
 
 // ---- pass 2: interior ----
-template <bool kDD>   // LMD_DDMIX (its T/S loads and registers only where it is on)
-__global__ void __launch_bounds__(64) k_kpp_int(Dev d, Range R, EdgeClamp ec, int tind, int nstp, int first,
-                                                KppConst kc) {
-  ROMS_IJC_OR_RETURN(R)
+// kDD: LMD_DDMIX (its T/S loads and registers only where it is on).
+// TY > 0 (LMD_RIMIX only): blocks of 64 x TY columns stage each level's
+// smoothed-Rig stencil window ((64+2) x (TY+2) raw Rig values, clamped at
+// the edges like load3x3) in LDS once, double-buffered with one barrier per
+// level, instead of nine global loads per lane; lanes past the range walk
+// the levels too (barriers) and store nothing.  Same values bitwise.
+template <bool kDD, int TY = 0, int MW = 1>   // MW: minimum waves per SIMD (VGPR cap)
+__global__ void __launch_bounds__(TY > 0 ? kCX * TY : 64, MW) k_kpp_int(Dev d, Range R, EdgeClamp ec, int tind, int nstp,
+                                                                   int first, KppConst kc) {
+  constexpr bool STG = TY > 0;
+  constexpr int TYB = STG ? TY : 1, WW = kCX + 2, WN = WW * (TYB + 2), NTH = kCX * TYB, WQ = (WN + NTH - 1) / NTH;
+  const uint3 bI = xcd_tile();
+  int i = R.i0 + (int)(bI.x * kCX + threadIdx.x);
+  int j = R.j0 + (int)(bI.y * TYB + threadIdx.y);
+  const bool act = i <= R.i1 && j <= R.j1;
+  if (!STG && !act) return;
+  if (!act) { i = i < R.i1 ? i : R.i1; j = j < R.j1 ? j : R.j1; }
+  __shared__ double sW[STG ? 2 : 1][STG ? WN : 1];
+  const int tid = threadIdx.x + kCX * threadIdx.y;
+  const int wi0 = R.i0 + (int)bI.x * kCX - 1, wj0 = R.j0 + (int)bI.y * TYB - 1;
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const Params& P = d.p;
@@ -413,9 +429,18 @@ __global__ void __launch_bounds__(64) k_kpp_int(Dev d, Range R, EdgeClamp ec, in
   constexpr bool dd = kDD;
   const double* __restrict__ Tt = F.t + (long)(tind - 1) * b.n3 + ij;
   const double* __restrict__ St = Tt + 3 * b.n3;
-  struct RL { double r[3][3]; double zw, t0, t1, s0, s1; };
+  struct RL { double r[3][3]; double zw, t0, t1, s0, s1; double win[STG ? WQ : 1]; int k; };
   auto rload = [&](int k, RL& L) {
-    if (rimix) load3x3(b, ec, rig + (long)k * n2, i, j, L.r);
+    L.k = k;
+    if (STG) {   // this thread's entries of the level's window (rimix is on)
+#pragma unroll
+      for (int m = 0; m < WQ; m++) {
+        const int q = tid + m * NTH;
+        L.win[m] = q < WN ? rig[(long)k * n2 + ec.at(b, wi0 + q % WW, wj0 + q / WW)] : 0.0;
+      }
+    } else if (rimix) {
+      load3x3(b, ec, rig + (long)k * n2, i, j, L.r);
+    }
     L.zw = zw[(long)k * n2];
     if (dd) {
       const long o = (long)(k - 1) * n2;
@@ -424,7 +449,24 @@ __global__ void __launch_bounds__(64) k_kpp_int(Dev d, Range R, EdgeClamp ec, in
   };
   auto rcomp = [&](const RL& L, double& kv, double& kt, double& ks) {
     if (rimix) {
-      const double Rig = smooth_point(L.r, m);
+      double Rig;
+      if (STG) {
+        double* buf = sW[STG ? (L.k & 1) : 0];
+#pragma unroll
+        for (int mq = 0; mq < WQ; mq++) {
+          const int q = tid + mq * NTH;
+          if (q < WN) buf[q] = L.win[mq];
+        }
+        __syncthreads();
+        double w[3][3];
+#pragma unroll
+        for (int dj = 0; dj < 3; dj++)
+#pragma unroll
+          for (int di = 0; di < 3; di++) w[dj][di] = buf[(threadIdx.y + dj) * WW + threadIdx.x + di];
+        Rig = smooth_point(w, m);
+      } else {
+        Rig = smooth_point(L.r, m);
+      }
       const double cff = dmin(1., dmax(0., Rig));
       double nu_sx = 1. - cff * cff;
       nu_sx = nu_sx * nu_sx * nu_sx;
@@ -477,6 +519,7 @@ __global__ void __launch_bounds__(64) k_kpp_int(Dev d, Range R, EdgeClamp ec, in
       Ks = sqrt(a * a + q * q);
       if (Bfsfc < 0.) gh = -(kc.Cg * ssgm * ((1. - ssgm) * (1. - ssgm)));
     }
+    if (!act) return;
     if (nonlocal) ghat[(long)k * n2] = gh;   // LMD_NONLOCAL (lmd_kpp.F:436-446)
     const double sgmb = (zwk - zw0 + Zob) / (bbl + Zob);
     if (sgmb < 1.) {
@@ -523,6 +566,7 @@ __global__ void __launch_bounds__(64) k_kpp_int(Dev d, Range R, EdgeClamp ec, in
   }
   finish(N, rvN + akv, rtN + akt, rsN + aks, zwN);
   // hbls/hbbl and their closed-wall ghost copies (lmd_kpp.F:530-620)
+  if (!act) return;
   F.hbls[ij] = hbl;
   F.hbbl[ij] = bbl;
   const bool W = !b.ew_periodic && b.west_edge && i == b.istr, E = !b.ew_periodic && b.east_edge && i == b.iend;
@@ -567,10 +611,24 @@ void launch_lmd_vmix(const Dev& d, hipStream_t s, const Tlev& t, int tind) {
     hipLaunchKernelGGL(k_kpp_ext<ColGlb>, gridc_of(E), dim3(kCX), 0, s, d, E, tind, t.nstp, kc);
   else
     hipLaunchKernelGGL(k_kpp_ext<ColLds>, gridc_of(E), dim3(kCX), col_lds_bytes(1, b.N), s, d, E, tind, t.nstp, kc);
-  if (d.p.lmd_ddmix)
+  if (d.p.kpp_ty && d.p.lmd_rimix) {   // staged Rig windows on 64 x TY column blocks
+    const int ty = (d.p.kpp_ty == 8 && !d.p.lmd_ddmix) ? 8 : 4;   // the DDMIX form is instantiated on 64x4 only
+    dim3 g = gridc_of(R);
+    g.y = (g.y + ty - 1) / ty;
+    const EdgeClamp ec = edge_clamp(b);
+    if (d.p.lmd_ddmix)
+      hipLaunchKernelGGL((k_kpp_int<true, 4>), g, dim3(kCX, 4), 0, s, d, R, ec, tind, t.nstp, first, kc);
+    else if (d.p.kpp_ty == 8)
+      hipLaunchKernelGGL((k_kpp_int<false, 8>), g, dim3(kCX, 8), 0, s, d, R, ec, tind, t.nstp, first, kc);
+    else if (d.p.kpp_ty == 43)
+      hipLaunchKernelGGL((k_kpp_int<false, 4, 3>), g, dim3(kCX, 4), 0, s, d, R, ec, tind, t.nstp, first, kc);
+    else
+      hipLaunchKernelGGL((k_kpp_int<false, 4>), g, dim3(kCX, 4), 0, s, d, R, ec, tind, t.nstp, first, kc);
+  } else if (d.p.lmd_ddmix) {
     hipLaunchKernelGGL(k_kpp_int<true>, gridc_of(R), dim3(kCX), 0, s, d, R, edge_clamp(b), tind, t.nstp, first, kc);
-  else
+  } else {
     hipLaunchKernelGGL(k_kpp_int<false>, gridc_of(R), dim3(kCX), 0, s, d, R, edge_clamp(b), tind, t.nstp, first, kc);
+  }
   // lmd_kpp.F:631-649: Akv, hbls, hbbl, Akt(itemp), Akt(isalt)
   ExchList L{};
   L.p[0] = d.f.Akv; L.nlev[0] = b.N + 1;

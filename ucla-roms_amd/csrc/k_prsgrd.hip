@@ -111,25 +111,29 @@ constexpr int kPYH = kBY + 2, kPYN = kBX * kPYH;          // v-points m = j0-1 .
 constexpr int kPWW = kBX + 3, kPWH = kBY + 3, kPWN = kPWW * kPWH;   // raw window (i0-2.., j0-2..)
 constexpr int kPWQ = (kPWN + kBX * kBY - 1) / (kBX * kBY);
 constexpr int kPQ = (kPXN + kPYN + kBX * kBY - 1) / (kBX * kBY);
-template <bool FUSE>
-__global__ void __launch_bounds__(256) k_prsgrd_uv(Dev d, Range R, int split, int imin, int imax, int jmin, int jmax,
+template <bool FUSE, int TY = kBY>
+__global__ void __launch_bounds__(kBX * TY) k_prsgrd_uv(Dev d, Range R, int split, int imin, int imax, int jmin, int jmax,
                                                    UVBounds ub, int up, int nrhs) {
   const uint3 bI = h_tile(d.p.tile_grp);
+  // the file-scope window sizes for a 64 x TY tile (TY = kBY: the constants above)
+  constexpr int NT = kBX * TY, XN = kPXW * TY, YH = TY + 2, YN = kBX * YH;
+  constexpr int WN = kPWW * (TY + 3), WQ = (WN + NT - 1) / NT, PQ = (XN + YN + NT - 1) / NT;
+  constexpr int UWN = kUVW * (TY + 4);
   // one LDS block: the raw window, the elementary differences and the
   // harmonic means (and, FUSE, the u/v window after them)
-  constexpr int kPL = 3 * kPWN + 4 * kPXN + 4 * kPYN;
+  constexpr int kPL = 3 * WN + 4 * XN + 4 * YN;
   __shared__ double sL[kPL];
   double* const sZ = sL;
-  double* const sR = sZ + kPWN;
-  double* const sQ = sR + kPWN;
-  double* const sFCx = sQ + kPWN;
-  double* const sRx = sFCx + kPXN;
-  double* const sFCy = sRx + kPXN;
-  double* const sRy = sFCy + kPYN;
-  double* const sdZx = sRy + kPYN;
-  double* const sdRx = sdZx + kPXN;
-  double* const sdZy = sdRx + kPXN;
-  double* const sdRy = sdZy + kPYN;
+  double* const sR = sZ + WN;
+  double* const sQ = sR + WN;
+  double* const sFCx = sQ + WN;
+  double* const sRx = sFCx + XN;
+  double* const sFCy = sRx + XN;
+  double* const sRy = sFCy + YN;
+  double* const sdZx = sRy + YN;
+  double* const sdRx = sdZx + XN;
+  double* const sdZy = sdRx + XN;
+  double* const sdRy = sdZy + YN;
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const double g = d.p.g, rho0 = d.p.rho0, qp2 = d.p.qp2;
@@ -138,16 +142,16 @@ __global__ void __launch_bounds__(256) k_prsgrd_uv(Dev d, Range R, int split, in
   const double* R1 = split ? F.rho1 : F.rho;
   const int k = 1 + (int)bI.z;
   const long kk = (long)(k - 1) * b.n2, sj = b.nx2;
-  const int i0 = R.i0 + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * kBY;
+  const int i0 = R.i0 + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * TY;
   const int tid = threadIdx.x + kBX * threadIdx.y;
   auto W = [&](int i, int j) { return (i - (i0 - 2)) + (j - (j0 - 2)) * kPWW; };
   // ---- loads, all issued before the first barrier ----
-  double wz[kPWQ], wr[kPWQ], wq[kPWQ];
+  double wz[WQ], wr[WQ], wq[WQ];
 #pragma unroll
-  for (int m = 0; m < kPWQ; m++) {
-    const int q = tid + m * kBX * kBY;
+  for (int m = 0; m < WQ; m++) {
+    const int q = tid + m * NT;
     wz[m] = wr[m] = wq[m] = 0.0;
-    if (q < kPWN) {
+    if (q < WN) {
       const int i = i0 - 2 + q % kPWW, j = j0 - 2 + q / kPWW;
       if (i <= b.Lm + 2 && j <= b.Mm + 2) {
         const long o = IJ(b, i, j) + kk;
@@ -157,14 +161,14 @@ __global__ void __launch_bounds__(256) k_prsgrd_uv(Dev d, Range R, int split, in
       }
     }
   }
-  double mk[kPQ];   // u-/v-mask of the entry's clamped point
-  int e1[kPQ], e0[kPQ];
-  bool eon[kPQ];
+  double mk[PQ];   // u-/v-mask of the entry's clamped point
+  int e1[PQ], e0[PQ];
+  bool eon[PQ];
 #pragma unroll
-  for (int m = 0; m < kPQ; m++) {
-    const int q = tid + m * kBX * kBY;
+  for (int m = 0; m < PQ; m++) {
+    const int q = tid + m * NT;
     mk[m] = 0.0; e1[m] = e0[m] = 0; eon[m] = false;
-    if (q < kPXN) {
+    if (q < XN) {
       const int j = j0 + q / kPXW;
       int mm = i0 - 1 + q % kPXW;
       if (!(j > b.Mm + 1 || mm > b.Lm + 2)) {
@@ -172,8 +176,8 @@ __global__ void __launch_bounds__(256) k_prsgrd_uv(Dev d, Range R, int split, in
         eon[m] = true; e1[m] = W(mm, j); e0[m] = W(mm - 1, j);
         mk[m] = F.umask[IJ(b, mm, j)];
       }
-    } else if (q < kPXN + kPYN) {
-      const int qq = q - kPXN;
+    } else if (q < XN + YN) {
+      const int qq = q - XN;
       const int i = i0 + qq % kBX;
       int mm = j0 - 1 + qq / kBX;
       if (!(i > b.Lm + 1 || mm > b.Mm + 2)) {
@@ -195,14 +199,14 @@ __global__ void __launch_bounds__(256) k_prsgrd_uv(Dev d, Range R, int split, in
   // FUSE: the horizontal momentum r.h.s. of the same cell (k_uv_horiz1's
   // window of u, v, FlxU, FlxV at nrhs and its lane inputs), loaded here
   // with everything else; ru/rv then go to HBM once, after both terms
-  constexpr int UW = kUVN, UR = (UW + kBX * kBY - 1) / (kBX * kBY);
+  constexpr int UW = UWN, UR = (UW + NT - 1) / (NT);
   double wU[FUSE ? UR : 1], wV[FUSE ? UR : 1], wFU[FUSE ? UR : 1], wFV[FUSE ? UR : 1];
   double fo0 = 0.0, fox = 0.0, foy = 0.0;
   if constexpr (FUSE) {
     const long kn = kk + (long)(nrhs - 1) * b.n3;
 #pragma unroll
     for (int r = 0; r < UR; r++) {
-      const int q = tid + r * kBX * kBY;
+      const int q = tid + r * NT;
       const int ii = i0 - 2 + q % kUVW, jj = j0 - 2 + q / kUVW;
       const bool ok = q < UW && ii >= -1 && ii <= b.Lm + 2 && jj >= -1 && jj <= b.Mm + 2;
       const long oo = ok ? IJ(b, ii, jj) : 0;
@@ -218,16 +222,16 @@ __global__ void __launch_bounds__(256) k_prsgrd_uv(Dev d, Range R, int split, in
     }
   }
 #pragma unroll
-  for (int m = 0; m < kPWQ; m++) {
-    const int q = tid + m * kBX * kBY;
-    if (q < kPWN) { sZ[q] = wz[m]; sR[q] = wr[m]; sQ[q] = wq[m]; }
+  for (int m = 0; m < WQ; m++) {
+    const int q = tid + m * NT;
+    if (q < WN) { sZ[q] = wz[m]; sR[q] = wr[m]; sQ[q] = wq[m]; }
   }
   __syncthreads();
   // ---- elementary differences at clamped u-points (xi) and v-points (eta) ----
 #pragma unroll
-  for (int m = 0; m < kPQ; m++) {
-    const int q = tid + m * kBX * kBY;
-    if (q >= kPXN + kPYN) continue;
+  for (int m = 0; m < PQ; m++) {
+    const int q = tid + m * NT;
+    if (q >= XN + YN) continue;
     double fc = 0.0, rx = 0.0;
     if (eon[m]) {
       const double z1 = sZ[e1[m]], z0 = sZ[e0[m]];
@@ -239,16 +243,16 @@ __global__ void __launch_bounds__(256) k_prsgrd_uv(Dev d, Range R, int split, in
         rx = (sR[e1[m]] - sR[e0[m]]) * mk[m];
       }
     }
-    if (q < kPXN) { sFCx[q] = fc; sRx[q] = rx; }
-    else { sFCy[q - kPXN] = fc; sRy[q - kPXN] = rx; }
+    if (q < XN) { sFCx[q] = fc; sRx[q] = rx; }
+    else { sFCy[q - XN] = fc; sRy[q - XN] = rx; }
   }
   __syncthreads();
   // ---- harmonic averages at rho points p = i-1, i (xi) and j-1, j (eta) ----
 #pragma unroll
-  for (int m = 0; m < kPQ; m++) {
-    const int q = tid + m * kBX * kBY;
-    if (q >= kPXN + kPYN) continue;
-    if (q < kPXN) {
+  for (int m = 0; m < PQ; m++) {
+    const int q = tid + m * NT;
+    if (q >= XN + YN) continue;
+    if (q < XN) {
       const int li = q % kPXW;
       if (li == kPXW - 1) continue;
       const int jj = j0 + q / kPXW, p = i0 - 1 + li;
@@ -260,9 +264,9 @@ __global__ void __launch_bounds__(256) k_prsgrd_uv(Dev d, Range R, int split, in
       sdZx[q] = dz;
       sdRx[q] = dr;
     } else {
-      const int qq = q - kPXN;
+      const int qq = q - XN;
       const int lj = qq / kBX;
-      if (lj == kPYH - 1) continue;
+      if (lj == YH - 1) continue;
       const int ii = i0 + qq % kBX, p = j0 - 1 + lj;
       double dz = harm(sFCy[qq], sFCy[qq + kBX]), dr = harm(sRy[qq], sRy[qq + kBX]);
       if (split && ii <= b.Lm + 1 && p <= b.Mm + 1) {
@@ -311,13 +315,13 @@ __global__ void __launch_bounds__(256) k_prsgrd_uv(Dev d, Range R, int split, in
     // the window of u, v, FlxU, FlxV into the LDS of the finished stages
     __syncthreads();
     double* sU = sL;            // the finished stages' LDS, reused
-    double* sV = sU + kUVN;
-    double* sFU = sV + kUVN;
-    double* sFV = sFU + kUVN;
-    static_assert(4 * kUVN <= kPL, "uv window fits");
+    double* sV = sU + UWN;
+    double* sFU = sV + UWN;
+    double* sFV = sFU + UWN;
+    static_assert(4 * UWN <= kPL, "uv window fits");
 #pragma unroll
     for (int r = 0; r < UR; r++) {
-      const int q = tid + r * kBX * kBY;
+      const int q = tid + r * NT;
       if (q < UW) { sU[q] = wU[r]; sV[q] = wV[r]; sFU[q] = wFU[r]; sFV[q] = wFV[r]; }
     }
     __syncthreads();
@@ -593,9 +597,15 @@ void launch_prsgrd(const Dev& d, hipStream_t s, const Tlev& t, int uv_up, bool p
   Range R1{0, b.Lm, 0, b.Mm};
   if (!p_ready) hipLaunchKernelGGL(k_prsgrd_P, grid_of(R1), dim3(kBX, kBY), 0, s, d, R1, split, d.p.tides);
   ktimer_mark(s, kTimedPrsgrdUv, 0);
-  if (uv_up >= 0)
+  if (uv_up >= 0 && d.p.prs_ty == 8)
+    hipLaunchKernelGGL((k_prsgrd_uv<true, 8>), grid3_ty(R2, b.N, 8), dim3(kBX, 8), 0, s, d, R2, split, imin, imax, jmin,
+                       jmax, uv_bounds(b), uv_up, t.nrhs);
+  else if (uv_up >= 0)
     hipLaunchKernelGGL(k_prsgrd_uv<true>, grid3_of(R2, b.N), dim3(kBX, kBY), 0, s, d, R2, split, imin, imax, jmin, jmax,
                        uv_bounds(b), uv_up, t.nrhs);
+  else if (d.p.prs_ty == 8)
+    hipLaunchKernelGGL((k_prsgrd_uv<false, 8>), grid3_ty(R2, b.N, 8), dim3(kBX, 8), 0, s, d, R2, split, imin, imax, jmin,
+                       jmax, uv_bounds(b), 0, t.nrhs);
   else
     hipLaunchKernelGGL(k_prsgrd_uv<false>, grid3_of(R2, b.N), dim3(kBX, kBY), 0, s, d, R2, split, imin, imax, jmin, jmax,
                        uv_bounds(b), 0, t.nrhs);

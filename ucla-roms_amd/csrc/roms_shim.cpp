@@ -606,6 +606,17 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     P.h_ty = (e && atoi(e) == 8) ? 8 : 4;
   }
   {
+    const char* e = getenv("ROMS_GPU_PRS_TY");
+    P.prs_ty = (e && atoi(e) == 8) ? 8 : 4;
+  }
+  {
+    // staged Rig windows in k_kpp_int (bitwise): measured 3.49-3.68 -> 3.32-3.38 ms
+    // per lmd_vmix at C3 (r3_zo_prsty_kppty_ab.txt); ROMS_GPU_KPP_TY=0 for one row per block
+    const char* e = getenv("ROMS_GPU_KPP_TY");
+    P.kpp_ty = 4;
+    if (e && (atoi(e) == 0 || atoi(e) == 8 || atoi(e) == 43)) P.kpp_ty = atoi(e);
+  }
+  {
     const char* e = getenv("ROMS_GPU_HOIST");
     P.hoist = !(e && e[0] == '0');
   }
