@@ -467,3 +467,25 @@ def test_kpp_int_staged_rig_bitwise(lmd, monkeypatch):
     for o in out[1:]:
         for n in out[0]:
             assert np.array_equal(out[0][n], o[n]), n
+
+
+@pytest.mark.parametrize("obc", [15, 0])
+def test_visc3d_staged_windows_bitwise(obc, monkeypatch):
+    """visc3d with the level's raw u, v, Hz windows staged in LDS
+    (ROMS_GPU_VISC_STG=1) equals the per-point-load form bitwise over 4 whole
+    steps: the open basin with an island and sponge bands (nonzero visc2_r /
+    visc2_p there), and the closed basin."""
+    cfg = basin_cfg(LLm=70, MMm=42, N=12, nonlin=True)
+    out = []
+    for env in ("0", "1"):
+        monkeypatch.setenv("ROMS_GPU_VISC_STG", env)
+        m = romsgpu.Model.from_case(cfg.case_id, cfg.LLm, cfg.MMm, cfg.N, cfg.NT, salinity=True, nonlin_eos=True,
+                                    dt=cfg.dt, ndtfast=cfg.ndtfast, sizex=cfg.sizex, sizey=cfg.sizey, obc=obc,
+                                    v_sponge=1.0 if obc else 0.0, island=bool(obc))
+        if obc:
+            assert float(np.abs(m.get("visc2_r")).max()) > 0
+        m.step(4)
+        out.append({n: m.get(n) for n in ("u", "v", "t", "rufrc", "rvfrc", "ubar", "vbar")})
+        m.close()
+    for n in out[0]:
+        assert np.array_equal(out[0][n], out[1][n]), n

@@ -602,10 +602,159 @@ __global__ void __launch_bounds__(256) k_visc3d(Dev d, Range R, int nstp) {
   if (dv) F.rvfrc[ij] = fv;
 }
 
+// The same with each level's raw u, v(nstp) and Hz windows staged in LDS
+// once per block (u over i0-1..i0+65 x j0-1..j0+4, v over i0-1..i0+64 x
+// j0-1..j0+5, Hz over i0-1..i0+64 x j0-1..j0+4: about 5 loads per lane per
+// level instead of about 22), the next level's window in registers while
+// this one is consumed.  Two barriers per level, as above.  Bit-identical.
+constexpr int kVUW = kBX + 3, kVUN = kVUW * (kBY + 2);   // u window
+constexpr int kVVW = kBX + 2, kVVN = kVVW * (kBY + 3);   // v window
+constexpr int kVHW = kBX + 2, kVHN = kVHW * (kBY + 2);   // Hz window
+constexpr int kVSN = kVUN + kVVN + kVHN, kVSQ = (kVSN + kBX * kBY - 1) / (kBX * kBY);
+__global__ void __launch_bounds__(256, 3) k_visc3d_stg(Dev d, Range R, int nstp) {
+  const uint3 bI = xcd_tile();
+  __shared__ double sUFx[kVN], sVFe[kVN], sUFe[kVN], sVFx[kVN];
+  __shared__ double sRaw[kVSN];
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const int indx = 3 - nstp;
+  const int i0 = R.i0 + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * kBY;
+  const long sj = b.nx2;
+  const double* pm = F.pm;
+  const double* pn = F.pn;
+  const int tid = threadIdx.x + kBX * threadIdx.y;
+  ViscRho gr[kVQ];
+  ViscPsi gp[kVQ];
+#pragma unroll
+  for (int m = 0; m < kVQ; m++) {
+    const int q = tid + m * kBX * kBY;
+    const int li = q % kVW, lj = q / kVW;
+    const int ir = i0 - 1 + li, jr = j0 - 1 + lj;  // rho point
+    ViscRho& r = gr[m];
+    r.on = q < kVN && ir >= 0 && ir <= b.Lm + 1 && jr >= 0 && jr <= b.Mm + 1;
+    r.ij = IJ(b, ir, jr);
+    if (r.on) {
+      const long ij = r.ij;
+      r.v2 = F.visc2_r[ij];
+      r.X = F.dn_r[ij] * pm[ij]; r.sx1 = pn[ij] + pn[ij + 1]; r.sx0 = pn[ij - 1] + pn[ij];
+      r.Y = F.dm_r[ij] * pn[ij]; r.sy1 = pm[ij] + pm[ij + sj]; r.sy0 = pm[ij - sj] + pm[ij];
+      r.dn = F.dn_r[ij]; r.dm = F.dm_r[ij];
+    }
+    const int ip = i0 + li, jp = j0 + lj;  // psi point
+    ViscPsi& p = gp[m];
+    p.on = q < kVN && ip >= 0 && ip <= b.Lm + 2 && jp >= 0 && jp <= b.Mm + 2;
+    p.ij = IJ(b, ip, jp);
+    if (p.on) {
+      const long ij = p.ij;
+      p.v2 = F.visc2_p[ij];
+      p.P1 = 0.25 * (pm[ij - 1] + pm[ij] + pm[ij - 1 - sj] + pm[ij - sj]) * F.dn_p[ij];
+      p.a1 = pn[ij - sj] + pn[ij]; p.a0 = pn[ij - 1 - sj] + pn[ij - 1];
+      p.P2 = 0.25 * (pn[ij - 1] + pn[ij] + pn[ij - 1 - sj] + pn[ij - sj]) * F.dm_p[ij];
+      p.b1 = pm[ij - 1] + pm[ij]; p.b0 = pm[ij - 1 - sj] + pm[ij - sj];
+      p.msk = F.pmask[ij]; p.dm = F.dm_p[ij]; p.dn = F.dn_p[ij];
+    }
+  }
+  const double* U = F.u + (long)(nstp - 1) * b.n3;
+  const double* V = F.v + (long)(nstp - 1) * b.n3;
+  // this thread's raw window entries: field (0 u, 1 v, 2 Hz, -1 none) and 2-D offset
+  long wo[kVSQ];
+  int wf[kVSQ];
+#pragma unroll
+  for (int m = 0; m < kVSQ; m++) {
+    const int q = tid + m * kBX * kBY;
+    int ii = 0, jj = 0, f = -1;
+    if (q < kVUN) { f = 0; ii = i0 - 1 + q % kVUW; jj = j0 - 1 + q / kVUW; }
+    else if (q < kVUN + kVVN) { const int qq = q - kVUN; f = 1; ii = i0 - 1 + qq % kVVW; jj = j0 - 1 + qq / kVVW; }
+    else if (q < kVSN) { const int qq = q - kVUN - kVVN; f = 2; ii = i0 - 1 + qq % kVHW; jj = j0 - 1 + qq / kVHW; }
+    if (f >= 0 && !(ii >= -1 && ii <= b.Lm + 2 && jj >= -1 && jj <= b.Mm + 2)) f = -1;
+    wf[m] = f;
+    wo[m] = f >= 0 ? IJ(b, ii, jj) : 0;
+  }
+  auto ldraw = [&](int k, double (&x)[kVSQ]) {
+    const long kk = (long)(k - 1) * b.n2;
+#pragma unroll
+    for (int m = 0; m < kVSQ; m++)
+      x[m] = wf[m] == 0 ? U[wo[m] + kk] : wf[m] == 1 ? V[wo[m] + kk] : wf[m] == 2 ? F.Hz[wo[m] + kk] : 0.0;
+  };
+  auto Uw = [&](int ii, int jj) { return sRaw[(ii - (i0 - 1)) + (jj - (j0 - 1)) * kVUW]; };
+  auto Vw = [&](int ii, int jj) { return sRaw[kVUN + (ii - (i0 - 1)) + (jj - (j0 - 1)) * kVVW]; };
+  auto Hw = [&](int ii, int jj) { return sRaw[kVUN + kVVN + (ii - (i0 - 1)) + (jj - (j0 - 1)) * kVHW]; };
+  const int i = i0 + (int)threadIdx.x, j = j0 + (int)threadIdx.y;
+  const bool act = i <= R.i1 && j <= R.j1;
+  const long ij = IJ(b, i, j);
+  const bool du = act && i >= b.istrU && i <= b.iend, dv = act && j >= b.jstrV && j <= b.jend;
+  double cum = 0.0, cun = 0.0, cvm = 0.0, cvn = 0.0, fu = 0.0, fv = 0.0;
+  if (du) { cum = pm[ij - 1] + pm[ij]; cun = pn[ij - 1] + pn[ij]; fu = F.rufrc[ij]; }
+  if (dv) { cvm = pm[ij] + pm[ij - sj]; cvn = pn[ij] + pn[ij - sj]; fv = F.rvfrc[ij]; }
+  const double cu0 = 0.125 * cum * cun, cv0 = 0.125 * cvm * cvn;
+  double* Ui = F.u + (long)(indx - 1) * b.n3;
+  double* Vi = F.v + (long)(indx - 1) * b.n3;
+  const int qr = (threadIdx.x + 1) + (threadIdx.y + 1) * kVW;  // rho (i,j); -1: (i-1,j); -kVW: (i,j-1)
+  const int qp = threadIdx.x + threadIdx.y * kVW;              // psi (i,j); +1: (i+1,j); +kVW: (i,j+1)
+  double raw[kVSQ];
+  ldraw(1, raw);
+  for (int k = 1; k <= b.N; k++) {
+    const long kk = (long)(k - 1) * b.n2;
+    const double ui = du ? Ui[ij + kk] : 0.0, vi = dv ? Vi[ij + kk] : 0.0;
+    // every lane finished the previous level's stress reads of sRaw before
+    // its second barrier, so the raw window can be overwritten here
+#pragma unroll
+    for (int m = 0; m < kVSQ; m++) {
+      const int q = tid + m * kBX * kBY;
+      if (q < kVSN) sRaw[q] = raw[m];
+    }
+    if (k < b.N) ldraw(k + 1, raw);
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < kVQ; m++) {
+      const int q = tid + m * kBX * kBY;
+      if (q >= kVN) break;
+      const int li = q % kVW, lj = q / kVW;
+      double ufx = 0.0, vfe = 0.0, ufe = 0.0, vfx = 0.0;
+      const ViscRho& r = gr[m];
+      if (r.on) {
+        const int ir = i0 - 1 + li, jr = j0 - 1 + lj;
+        const double cff = 0.5 * Hw(ir, jr) * r.v2 * (r.X * (r.sx1 * Uw(ir + 1, jr) - r.sx0 * Uw(ir, jr)) -
+                                                      r.Y * (r.sy1 * Vw(ir, jr + 1) - r.sy0 * Vw(ir, jr)));
+        ufx = cff * r.dn * r.dn;
+        vfe = -cff * r.dm * r.dm;
+      }
+      const ViscPsi& p = gp[m];
+      if (p.on) {
+        const int ip = i0 + li, jp = j0 + lj;
+        const double cff = 0.125 * (Hw(ip - 1, jp) + Hw(ip, jp) + Hw(ip - 1, jp - 1) + Hw(ip, jp - 1)) * p.v2 *
+                           (p.P1 * (p.a1 * Vw(ip, jp) - p.a0 * Vw(ip - 1, jp)) +
+                            p.P2 * (p.b1 * Uw(ip, jp) - p.b0 * Uw(ip, jp - 1))) *
+                           p.msk;
+        ufe = cff * p.dm * p.dm;
+        vfx = cff * p.dn * p.dn;
+      }
+      sUFx[q] = ufx; sVFe[q] = vfe; sUFe[q] = ufe; sVFx[q] = vfx;
+    }
+    __syncthreads();
+    const long o = ij + kk;
+    if (du) {
+      const double cff = cu0 * (cun * (sUFx[qr] - sUFx[qr - 1]) + cum * (sUFe[qp + kVW] - sUFe[qp]));
+      Ui[o] = ui + d.p.dt * cff;
+      fu = fu + cff;
+    }
+    if (dv) {
+      const double cff = cv0 * (cvn * (sVFx[qp + 1] - sVFx[qp]) + cvm * (sVFe[qr] - sVFe[qr - kVW]));
+      Vi[o] = vi + d.p.dt * cff;
+      fv = fv + cff;
+    }
+  }
+  if (du) F.rufrc[ij] = fu;
+  if (dv) F.rvfrc[ij] = fv;
+}
+
 void launch_visc3d(const Dev& d, hipStream_t s, const Tlev& t) {
   const Bounds& b = d.b;
   Range R{b.istr, b.iend, b.jstr, b.jend};
-  hipLaunchKernelGGL(k_visc3d, grid_of(R), dim3(kBX, kBY), 0, s, d, R, t.nstp);
+  if (d.p.visc_stg)
+    hipLaunchKernelGGL(k_visc3d_stg, grid_of(R), dim3(kBX, kBY), 0, s, d, R, t.nstp);
+  else
+    hipLaunchKernelGGL(k_visc3d, grid_of(R), dim3(kBX, kBY), 0, s, d, R, t.nstp);
 }
 
 // Columns that k_uv2_fused owns: the coupling range without the rows (u) /

@@ -610,8 +610,14 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     P.prs_ty = (e && atoi(e) == 8) ? 8 : 4;
   }
   {
-    // staged Rig windows in k_kpp_int (bitwise): measured 3.49-3.68 -> 3.32-3.38 ms
-    // per lmd_vmix at C3 (r3_zo_prsty_kppty_ab.txt); ROMS_GPU_KPP_TY=0 for one row per block
+    // visc3d with staged raw windows (bitwise): C3 2.34 -> 1.94 ms, C2 0.35 -> 0.30 ms
+    // (r3_zq_visc_stg_ab.txt); ROMS_GPU_VISC_STG=0 for per-point loads
+    const char* e = getenv("ROMS_GPU_VISC_STG");
+    P.visc_stg = !(e && e[0] == '0');
+  }
+  {
+    // staged Rig windows in k_kpp_int (bitwise): lmd_vmix 3.49 -> 3.22 ms per
+    // call at C3 (r3_zp_kpp_ty_ab.txt); ROMS_GPU_KPP_TY=0 for one row per block
     const char* e = getenv("ROMS_GPU_KPP_TY");
     P.kpp_ty = 4;
     if (e && (atoi(e) == 0 || atoi(e) == 8 || atoi(e) == 43)) P.kpp_ty = atoi(e);
