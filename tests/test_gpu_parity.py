@@ -489,3 +489,24 @@ def test_visc3d_staged_windows_bitwise(obc, monkeypatch):
         m.close()
     for n in out[0]:
         assert np.array_equal(out[0][n], out[1][n]), n
+
+
+@pytest.mark.parametrize("obc", [15, 0])
+def test_t3dmix_staged_windows_bitwise(obc, monkeypatch):
+    """t3dmix with the level's Hz, T, S windows staged in LDS
+    (ROMS_GPU_T3DMIX_STG=1) equals the per-point-load form bitwise over 4
+    whole steps (sponge bands give nonzero diff2 in the open basin)."""
+    cfg = basin_cfg(LLm=70, MMm=42, N=12, nonlin=True)
+    out = []
+    for env in ("0", "1"):
+        monkeypatch.setenv("ROMS_GPU_T3DMIX_STG", env)
+        m = romsgpu.Model.from_case(cfg.case_id, cfg.LLm, cfg.MMm, cfg.N, cfg.NT, salinity=True, nonlin_eos=True,
+                                    dt=cfg.dt, ndtfast=cfg.ndtfast, sizex=cfg.sizex, sizey=cfg.sizey, obc=obc,
+                                    v_sponge=1.0 if obc else 0.0, island=bool(obc))
+        if obc:
+            assert float(np.abs(m.get("diff2")).max()) > 0
+        m.step(4)
+        out.append({n: m.get(n) for n in ("u", "v", "t", "zeta")})
+        m.close()
+    for n in out[0]:
+        assert np.array_equal(out[0][n], out[1][n]), n

@@ -485,10 +485,92 @@ __global__ void __launch_bounds__(256) k_t3dmix(Dev d, Range R, int nnew, int nr
   }
 }
 
+// Two tracers with each level's Hz, T(nrhs), S(nrhs) windows (i0-1..i0+64 x
+// j0-1..j0+4) staged in LDS once per block and the next level's in flight in
+// registers (about 5 loads per lane per level for the stencils instead of
+// 15); the per-tracer expressions of k_t3dmix, bit-identical.  Lanes past
+// the range walk the levels too (barriers) and store nothing.
+constexpr int kTMW = kBX + 2, kTMN = kTMW * (kBY + 2), kTMQ = (3 * kTMN + kBX * kBY - 1) / (kBX * kBY);
+__global__ void __launch_bounds__(256) k_t3dmix_stg(Dev d, Range R, int nnew, int nrhs) {
+  const uint3 bI = xcd_tile();
+  __shared__ double sW[3 * kTMN];   // Hz, T, S
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const int i0 = R.i0 + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * kBY;
+  int i = i0 + (int)threadIdx.x, j = j0 + (int)threadIdx.y;
+  const bool act = i <= R.i1 && j <= R.j1;
+  if (!act) { i = i < R.i1 ? i : R.i1; j = j < R.j1 ? j : R.j1; }
+  const long ij = IJ(b, i, j), sj = b.nx2, n2 = b.n2;
+  const int tid = threadIdx.x + kBX * threadIdx.y;
+  const double pmn = d.p.dt * F.pm[ij] * F.pn[ij];
+  double ax0[2], ax1[2], ay0[2], ay1[2];
+  double* __restrict__ Tn[2];
+  const double* Tr[2];
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    const double* d2 = F.diff2 + (long)q * n2;
+    Tr[q] = F.t + (long)(nrhs - 1) * b.n3 + (long)q * 3 * b.n3;
+    Tn[q] = F.t + (long)(nnew - 1) * b.n3 + (long)q * 3 * b.n3;
+    ax0[q] = 0.25 * (d2[ij] + d2[ij - 1]) * F.pmon_u[ij];
+    ax1[q] = 0.25 * (d2[ij + 1] + d2[ij]) * F.pmon_u[ij + 1];
+    ay0[q] = 0.25 * (d2[ij] + d2[ij - sj]) * F.pnom_v[ij];
+    ay1[q] = 0.25 * (d2[ij + sj] + d2[ij]) * F.pnom_v[ij + sj];
+  }
+  const double um0 = F.umask[ij], um1 = F.umask[ij + 1], vm0 = F.vmask[ij], vm1 = F.vmask[ij + sj];
+  // window entries of this thread: field (0 Hz, 1 T, 2 S, -1 none) and 2-D offset
+  long wo[kTMQ];
+  int wf[kTMQ];
+#pragma unroll
+  for (int m = 0; m < kTMQ; m++) {
+    const int q = tid + m * kBX * kBY;
+    const int f = q < 3 * kTMN ? q / kTMN : -1, qq = q - (f < 0 ? 0 : f) * kTMN;
+    const int ii = i0 - 1 + qq % kTMW, jj = j0 - 1 + qq / kTMW;
+    const bool ok = f >= 0 && ii >= -1 && ii <= b.Lm + 2 && jj >= -1 && jj <= b.Mm + 2;
+    wf[m] = ok ? f : -1;
+    wo[m] = ok ? IJ(b, ii, jj) : 0;
+  }
+  auto ldw = [&](int k, double (&x)[kTMQ]) {
+    const long kk = (long)(k - 1) * n2;
+#pragma unroll
+    for (int m = 0; m < kTMQ; m++)
+      x[m] = wf[m] == 0 ? F.Hz[wo[m] + kk] : wf[m] == 1 ? Tr[0][wo[m] + kk] : wf[m] == 2 ? Tr[1][wo[m] + kk] : 0.0;
+  };
+  const int c = (threadIdx.x + 1) + (threadIdx.y + 1) * kTMW;   // the lane's cell in the window
+  double w[kTMQ];
+  ldw(1, w);
+  for (int k = 1; k <= b.N; k++) {
+    const long o = ij + (long)(k - 1) * n2;
+    const double tn0 = Tn[0][o], tn1 = Tn[1][o];
+    if (k > 1) __syncthreads();   // the previous level's window consumed
+#pragma unroll
+    for (int m = 0; m < kTMQ; m++) {
+      const int q = tid + m * kBX * kBY;
+      if (q < 3 * kTMN) sW[q] = w[m];
+    }
+    if (k < b.N) ldw(k + 1, w);
+    __syncthreads();
+    const double* H = sW;
+    const double hz = H[c];
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+      const double* T = sW + (1 + q) * kTMN;
+      const double FX1 = ax1[q] * (H[c + 1] + hz) * (T[c + 1] - T[c]) * um1;
+      const double FX0 = ax0[q] * (hz + H[c - 1]) * (T[c] - T[c - 1]) * um0;
+      const double FE1 = ay1[q] * (H[c + kTMW] + hz) * (T[c + kTMW] - T[c]) * vm1;
+      const double FE0 = ay0[q] * (hz + H[c - kTMW]) * (T[c] - T[c - kTMW]) * vm0;
+      if (act) Tn[q][o] = (q == 0 ? tn0 : tn1) + pmn * (FX1 - FX0 + FE1 - FE0) / hz;
+    }
+  }
+}
+
 void launch_t3dmix(const Dev& d, hipStream_t s, const Tlev& t) {
   const Bounds& b = d.b;
   Range R{b.istr, b.iend, b.jstr, b.jend};
-  auto run = [&](const Range& r) { hipLaunchKernelGGL(k_t3dmix, grid_of(r), dim3(kBX, kBY), 0, s, d, r, t.nnew, t.nrhs); };
+  const bool stg = d.p.t3dmix_stg && b.NT == 2;
+  auto run = [&](const Range& r) {
+    if (stg) hipLaunchKernelGGL(k_t3dmix_stg, grid_of(r), dim3(kBX, kBY), 0, s, d, r, t.nnew, t.nrhs);
+    else hipLaunchKernelGGL(k_t3dmix, grid_of(r), dim3(kBX, kBY), 0, s, d, r, t.nnew, t.nrhs);
+  };
   ExchList L;
   if (tracer_exch_list(d, t.nnew, L)) {
     launch_rim_first(d, s, R, L, run, [] {});

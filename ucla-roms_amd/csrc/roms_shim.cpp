@@ -616,6 +616,10 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     P.visc_stg = !(e && e[0] == '0');
   }
   {
+    const char* e = getenv("ROMS_GPU_T3DMIX_STG");
+    P.t3dmix_stg = e && e[0] == '1';
+  }
+  {
     // staged Rig windows in k_kpp_int (bitwise): lmd_vmix 3.49 -> 3.22 ms per
     // call at C3 (r3_zp_kpp_ty_ab.txt); ROMS_GPU_KPP_TY=0 for one row per block
     const char* e = getenv("ROMS_GPU_KPP_TY");
