@@ -31,6 +31,8 @@ ROUTINE_OF = {
     "k_set_huv1_chain": "set_HUV1", "k_kpp_ext": "lmd_vmix", "k_kpp_int": "lmd_vmix", "k_prsgrd_fused": "prsgrd",
     "k_bulk_flux": "bulk_flux", "k_t3dbc_edges": "step3d_t", "k_t3dbc_corners": "step3d_t", "k_u3dbc": "step3d_uv2",
     "k_v3dbc": "step3d_uv2", "k_pre_tracer_h1": "pre_step3d", "k_step3d_t_h1": "step3d_t",
+    # round-3 late: staged-window forms
+    "k_visc3d_stg": "visc3d", "k_t3dmix_stg": "t3dmix",
 }
 CALLS_PER_STEP = {"rho_eos": 2, "set_HUV": 1, "omega": 3, "prsgrd": 2, "pre_step3d": 1, "set_HUV1": 1,
                   "step3d_uv1": 1, "visc3d": 1, "step2d": None, "step3d_uv2": 1, "step3d_t": 1, "t3dmix": 1,

@@ -616,8 +616,10 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     P.visc_stg = !(e && e[0] == '0');
   }
   {
+    // t3dmix with staged windows (bitwise): C3 1.65 -> 1.31 ms, C2 0.218 -> 0.145 ms
+    // (r3_zs_t3dmix_stg_ab.txt); ROMS_GPU_T3DMIX_STG=0 for per-point loads
     const char* e = getenv("ROMS_GPU_T3DMIX_STG");
-    P.t3dmix_stg = e && e[0] == '1';
+    P.t3dmix_stg = !(e && e[0] == '0');
   }
   {
     // staged Rig windows in k_kpp_int (bitwise): lmd_vmix 3.49 -> 3.22 ms per
