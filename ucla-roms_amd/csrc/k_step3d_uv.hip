@@ -784,24 +784,33 @@ __global__ void __launch_bounds__(256) k_uv2_couple(Dev d, Range R, int nnew, in
     const double dn = dir == 0 ? F.dn_u[ij] : F.dm_v[ij];
     const double avg1 = dir == 0 ? F.DU_avg1[ij] : F.DV_avg1[ij];
     const double msk = dir == 0 ? F.umask[ij] : F.vmask[ij];
+    // sums first (read-only, so the loads of all levels pipeline), then the
+    // per-level quotient and correction in chunks whose loads precede their
+    // stores: the reference's values (step3d_uv2.F:103-133) without a
+    // may-alias wait per level (edge columns walk alone: their latency is the
+    // kernel's)
     long o = (long)(N - 1) * n2;
     double CF0 = 0.5 * (Hz[o] + Hz[o - s]);
     double DC0 = Un[o];
-    Un[o] = Un[o] / CF0;
 #pragma unroll 8
     for (int k = N - 1; k >= 1; k--) {
       o = (long)(k - 1) * n2;
-      const double cff = 0.5 * (Hz[o] + Hz[o - s]);
-      const double un = Un[o];
-      CF0 = CF0 + cff;
-      DC0 = DC0 + un;
-      Un[o] = un / cff;
+      CF0 = CF0 + 0.5 * (Hz[o] + Hz[o - s]);
+      DC0 = DC0 + Un[o];
     }
     DC0 = (DC0 * dn - avg1) / (CF0 * dn);
-#pragma unroll 8
-    for (int k = 1; k <= N; k++) {
-      o = (long)(k - 1) * n2;
-      Un[o] = (Un[o] - DC0) * msk;
+    constexpr int CH = 8;
+    for (int k0 = 1; k0 <= N; k0 += CH) {
+      double uc[CH], cc[CH];
+#pragma unroll
+      for (int q = 0; q < CH; q++) {
+        const long oq = (long)(min(k0 + q, N) - 1) * n2;
+        uc[q] = Un[oq];
+        cc[q] = 0.5 * (Hz[oq] + Hz[oq - s]);
+      }
+#pragma unroll
+      for (int q = 0; q < CH; q++)
+        if (k0 + q <= N) Un[(long)(k0 + q - 1) * n2] = (uc[q] / cc[q] - DC0) * msk;
     }
   }
 }
@@ -847,14 +856,28 @@ __global__ void __launch_bounds__(256) k_uv2_flux(Dev d, Range R, int nnew, int 
     else F.vbar[IJL(b, i, j, knew)] = DC0 * avg1;
     FC0 = DC0 * (FC0 - avg1);
     double CF0 = 0.0;
-#pragma unroll 8
-    for (int k = N; k >= 1; k--) {
-      o = (long)(k - 1) * n2;
-      const double un = (Un[o] - FC0) * msk;
-      Un[o] = un;
-      const double cfk = DELTA * Flx[o] + EPSIL * DCk(k) * (Us[o] + un);
-      CFs[(long)k * n2] = cfk;
-      CF0 = CF0 + cfk;
+    // chunks of levels whose loads precede their stores (see k_uv2_couple)
+    constexpr int CH = 8;
+    for (int k0 = N; k0 >= 1; k0 -= CH) {
+      double uc[CH], fc[CH], sc[CH], dc[CH];
+#pragma unroll
+      for (int q = 0; q < CH; q++) {
+        const int k = max(k0 - q, 1);
+        const long oq = (long)(k - 1) * n2;
+        uc[q] = Un[oq]; fc[q] = Flx[oq]; sc[q] = Us[oq]; dc[q] = DCk(k);
+      }
+#pragma unroll
+      for (int q = 0; q < CH; q++) {
+        const int k = k0 - q;
+        if (k >= 1) {
+          const long oq = (long)(k - 1) * n2;
+          const double un = (uc[q] - FC0) * msk;
+          Un[oq] = un;
+          const double cfk = DELTA * fc[q] + EPSIL * dc[q] * (sc[q] + un);
+          CFs[(long)k * n2] = cfk;
+          CF0 = CF0 + cfk;
+        }
+      }
     }
     CF0 = DC0 * (CF0 - avg2);
 #pragma unroll 8
