@@ -401,39 +401,75 @@ def main():
 
     dist = None
     comm = None
+    bootstrap = "none (single rank)"
     # ROMS_BENCH_FORCE_COMM=1: take the multi-rank path even at world size 1
     # (RCCL comm + self-addressed exchanges; rehearses the N>1 plumbing)
     force = os.environ.get("ROMS_BENCH_FORCE_COMM") == "1"
+
+    def rccl_comm():
+        # the library's own RCCL communicator, its id broadcast through
+        # torch.distributed; halos then move by IPC peer writes when the
+        # library's init self-test passes, else by RCCL send/recv
+        import torch
+        uid = torch.zeros(128, dtype=torch.uint8)
+        if rank == 0:
+            uid.copy_(torch.frombuffer(bytearray(romsgpu.comm_unique_id()), dtype=torch.uint8))
+        dist.broadcast(uid, src=0)
+        return romsgpu.comm_create(bytes(uid.numpy().tobytes()), world, rank, local_rank)
+
     if world > 1 or force:
         if force:
             os.environ.setdefault("ROMS_GPU_RCCL_SELF", "1")
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", init_method="env://")
-        # bootstrap the library's own RCCL communicator through torch.distributed
-        uid = torch.zeros(128, dtype=torch.uint8, device="cuda")
-        if rank == 0:
-            uid.copy_(torch.frombuffer(bytearray(romsgpu.comm_unique_id()), dtype=torch.uint8))
-        dist.broadcast(uid, src=0)
-        comm = romsgpu.comm_create(bytes(uid.cpu().numpy().tobytes()), world, rank, local_rank)
+        # torch.distributed is host plumbing only here (barrier, max over
+        # ranks, the communicators' bootstrap): gloo on the CPU; the halo
+        # traffic is the library's own (IPC peer writes or RCCL)
+        dist.init_process_group("gloo", init_method="env://")
+        if force or os.environ.get("ROMS_BENCH_COMM") == "rccl":
+            comm, bootstrap = rccl_comm(), "rccl"
+        else:
+            # default: the host-channel communicator (roms_gpu_comm_create_host),
+            # the deployment a Fortran host uses with its MPI_Allgather and the
+            # transport the multi-process tests exercise: every halo exchange is
+            # an IPC peer write, RCCL is not in the library at all
+            def allgather(data):
+                t = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+                parts = [torch.empty_like(t) for _ in range(world)]
+                dist.all_gather(parts, t)
+                return [bytes(p.numpy().tobytes()) for p in parts]
+
+            comm, bootstrap = romsgpu.comm_create_host(world, rank, allgather, local_rank), "host allgather (gloo)"
 
     def barrier():
         if dist is not None:
             import torch
-            torch.cuda.synchronize()
+            torch.cuda.synchronize(local_rank)
             dist.barrier()
 
     def allmax(x):
         if dist is None:
             return x
         import torch
-        tt = torch.tensor([x], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([x], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         return float(tt.item())
 
-    prim = run_workload(args.workload, romsgpu, comm, rank, world, local_rank, args.steps, args.warmup,
-                        args.timing_steps, barrier, allmax)
+    try:
+        prim = run_workload(args.workload, romsgpu, comm, rank, world, local_rank, args.steps, args.warmup,
+                            args.timing_steps, barrier, allmax)
+    except romsgpu.RomsGpuError as e:
+        # the host channel carries no RCCL fallback: when the IPC transport
+        # fails its set-up or self-test (a collective verdict, so every rank
+        # lands here) the ranks re-bootstrap over RCCL, which falls back to
+        # RCCL send/recv by itself
+        if not bootstrap.startswith("host") or "IPC" not in str(e):
+            raise
+        romsgpu.comm_destroy(comm)
+        comm, bootstrap = rccl_comm(), "rccl (host-channel IPC self-test failed: %s)" % str(e)[:120]
+        prim = run_workload(args.workload, romsgpu, comm, rank, world, local_rank, args.steps, args.warmup,
+                            args.timing_steps, barrier, allmax)
+    prim["config"]["comm_bootstrap"] = bootstrap
     out = {
         "metric": "grid-cell-updates/sec",
         "value": prim["value"],

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define ROMS_GPU_ABI_VERSION 12
+#define ROMS_GPU_ABI_VERSION 13
 #define ROMS_MAX_FAST 288
 
 /* Subdomain geometry of this rank: param.F / dimensions.F / mpi_setup.F:39-210 */
@@ -299,13 +299,19 @@ long roms_gpu_halo_map(int Lm, int Mm, int np_xi, int np_eta, int inode, int jno
  * set_frc_data roms_read_write.F:303-392, set_bry_all boundary.F:227,
  * set_tides tides.F:86-254) ----
  * roms_gpu_frc_record uploads one record (time rec_time in days, like the
- * reference's forcing times) of a field into record slot 0 or 1; the host
- * uploads a record only when the model time leaves the window of the two it
- * holds (as fill_frc_slice does).  roms_gpu_frc_interp forms every field
- * whose two slots are loaded, of the kinds in `kinds` (ROMS_FRC_SURFACE:
- * 2-D surface/atmospheric fields, ROMS_FRC_BRY: the *_west.._north boundary
+ * reference's forcing times) of a field into record slot 0, 1 or 2 (ABI 13:
+ * a third slot); the host uploads a record only when the model time leaves
+ * the window of those it holds (as fill_frc_slice does).  At a model time
+ * modtime the pair (it1, it2) is the one set_frc_data would hold: the
+ * earliest consecutive pair of the loaded records, in time order, whose
+ * later time is >= modtime (the reference refreshes to (it2, next record)
+ * once times(it2) < modtime, roms_read_write.F:341-350).  A modtime past
+ * every loaded record fails with -8 before anything is queued (load the
+ * next record first).  roms_gpu_frc_interp forms every field holding two or
+ * more records, of the kinds in `kinds` (ROMS_FRC_SURFACE: 2-D
+ * surface/atmospheric fields, ROMS_FRC_BRY: the *_west.._north boundary
  * arrays), as cff1*rec(it1) + cff2*rec(it2) at modtime [days], with
- * set_frc_data's out-of-window error.  roms_gpu_set_tide_data hands over
+ * set_frc_data's out-of-window error (-1).  roms_gpu_set_tide_data hands over
  * the tidal constituents (frequencies ftide [1/s]; potential and boundary
  * elevation/velocity real/imaginary parts, ntides x the field layout,
  * column-major like the reference's (GLOBAL_2D_ARRAY, ntides) arrays; NULL
@@ -324,9 +330,14 @@ int roms_gpu_frc_interp(double modtime, int kinds);
  * '1/2 fwd' before the second set_forces, boundary data at 'forward' (from
  * tdays = time + dt/2) followed by set_tides (main.F:384-441,
  * roms_read_write.F:330-336).  The weights are formed on the host per step
- * and read by the step graph from device memory.  A step whose time falls
- * outside a field's records fails (roms_read_write.F:381-388) before
- * anything is queued.  on = 0: the host interpolates (roms_gpu_frc_interp).  */
+ * and read by the step graph from device memory; each of the four points
+ * picks its own record pair, so with three records loaded a refresh that
+ * falls inside a step (t2 between the '1/2 fwd' and 'forward' points) is
+ * reproduced.  A step with any point past a field's last record fails with
+ * -8, one outside the window (roms_read_write.F:381-388) with -1, both
+ * before anything is queued; with boundary tides on, every open side's
+ * zeta/ubar/vbar data must hold two records (set_bry_all re-sets them before
+ * each set_tides).  on = 0: the host interpolates (roms_gpu_frc_interp).  */
 int roms_gpu_frc_clock(double start_time, int on);
 int roms_gpu_set_tide_data(int ntides, const double *ftide, const double *pot_re, const double *pot_im,
                            const double *ztide_re, const double *ztide_im, const double *utide_re,

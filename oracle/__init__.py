@@ -216,7 +216,7 @@ class Oracle:
             raise ValueError("or_set_pipes")
 
     def frc_record(self, name, slot, rec_time, arr):
-        """set_frc_data record `slot` (0/1) of field `name` at rec_time [days]."""
+        """set_frc_data record `slot` (0/1/2) of field `name` at rec_time [days]."""
         a = np.ascontiguousarray(arr, dtype=np.float64).ravel()
         if self.L.or_frc_record(self.h, name.encode(), slot, rec_time,
                                 a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))) != 0:

@@ -64,7 +64,7 @@ struct or_state {
   double *uwnd, *vwnd, *tair, *qair, *prate, *swrad, *lwrad, *sustr_r, *svstr_r;
   /* set_frc_data's two records per field (roms_read_write.F:303-392) and the
      in-step interpolation points of roms_step (main.F:373-441) */
-  struct { double *dst; size_t n; int bry; double t[2]; double *rec[2]; } frc[64];
+  struct { double *dst; size_t n; int bry; double t[3]; double *rec[3]; int k; } frc[64];   /* k: it1's place in time order */
   int nfrc, frc_clock;
   double frc_start;
   /* ADV_ISONEUTRAL (oracle_iso.c): eos_vars.F:28-31 slopes and inverse

@@ -90,7 +90,7 @@ void or_destroy(or_state *S) {
   if (!S) return;
   /* process exit reclaims memory in tests; free the big ones */
   free(S->u); free(S->v); free(S->t); free(S->zeta); free(S->ubar); free(S->vbar);
-  for (int q = 0; q < S->nfrc; q++) { free(S->frc[q].rec[0]); free(S->frc[q].rec[1]); }
+  for (int q = 0; q < S->nfrc; q++) { free(S->frc[q].rec[0]); free(S->frc[q].rec[1]); free(S->frc[q].rec[2]); }
   free(S);
 }
 
@@ -773,12 +773,14 @@ int or_init(or_state *S) {
   return 0;
 }
 
-/* set_frc_data (roms_read_write.F:303-392): records of one field, it1 the
- * earlier, cff1*rec(it1) + cff2*rec(it2) at modtime [days] */
+/* set_frc_data (roms_read_write.F:303-392): up to three records of one
+ * field stand for the forcing file; the pair (it1, it2) starts at the two
+ * earliest and moves to (it2, next) whenever times(it2) < modtime (:341-350),
+ * then cff1*rec(it1) + cff2*rec(it2) at modtime [days] (:376-379) */
 int or_frc_record(or_state *S, const char *name, int slot, double time, const double *data) {
   size_t n = 0;
   double *dst = or_field(S, name, &n);
-  if (!dst || slot < 0 || slot > 1) return -1;
+  if (!dst || slot < 0 || slot > 2) return -1;
   int q = 0;
   while (q < S->nfrc && S->frc[q].dst != dst) q++;
   if (q == S->nfrc) {
@@ -787,8 +789,9 @@ int or_frc_record(or_state *S, const char *name, int slot, double time, const do
     S->frc[q].dst = dst;
     S->frc[q].n = n;
     S->frc[q].bry = strstr(name, "_west") || strstr(name, "_east") || strstr(name, "_south") || strstr(name, "_north");
-    S->frc[q].rec[0] = S->frc[q].rec[1] = NULL;
+    S->frc[q].rec[0] = S->frc[q].rec[1] = S->frc[q].rec[2] = NULL;
   }
+  S->frc[q].k = 0;
   if (!S->frc[q].rec[slot]) S->frc[q].rec[slot] = zalloc(n);
   memcpy(S->frc[q].rec[slot], data, n * sizeof(double));
   S->frc[q].t[slot] = time;
@@ -816,8 +819,18 @@ void or_frc_clock(or_state *S, double start_time, int on) {
 }
 static void frc_interp(or_state *S, int bry, double modtime) {
   for (int q = 0; q < S->nfrc; q++) {
-    if (S->frc[q].bry != bry || !S->frc[q].rec[0] || !S->frc[q].rec[1]) continue;
-    const int it1 = S->frc[q].t[0] <= S->frc[q].t[1] ? 0 : 1, it2 = 1 - it1;
+    if (S->frc[q].bry != bry) continue;
+    int ord[3], n = 0;   /* the loaded records in time order: the "file" */
+    for (int s = 0; s < 3; s++)
+      if (S->frc[q].rec[s]) {
+        int k = n++;
+        while (k > 0 && S->frc[q].t[ord[k - 1]] > S->frc[q].t[s]) { ord[k] = ord[k - 1]; k--; }
+        ord[k] = s;
+      }
+    if (n < 2) continue;
+    /* refresh: it1 <- it2, it2 <- the next record, while times(it2) < modtime */
+    while (S->frc[q].k + 2 < n && S->frc[q].t[ord[S->frc[q].k + 1]] < modtime) S->frc[q].k++;
+    const int it1 = ord[S->frc[q].k], it2 = ord[S->frc[q].k + 1];
     const double t1 = S->frc[q].t[it1], t2 = S->frc[q].t[it2];
     const double cff1 = (t2 - modtime) / (t2 - t1), cff2 = (modtime - t1) / (t2 - t1);
     for (size_t m = 0; m < S->frc[q].n; m++)

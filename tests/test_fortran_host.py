@@ -20,7 +20,8 @@ FDIR = os.path.join(ROOT, "fortran")
 def test_fortran_module_and_driver_build():
     r = subprocess.run(["make", "-C", FDIR], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert os.path.exists(os.path.join(FDIR, "filament_driver"))
+    for exe in ("filament_driver", "register_driver", "dropin_driver"):
+        assert os.path.exists(os.path.join(FDIR, exe)), exe
 
 
 def test_dropins_keep_reference_signatures():
@@ -94,6 +95,21 @@ def test_fortran_register_driver_matches_golden():
             ref = float(g[key])
             assert abs(val - ref) <= 1e-11 * abs(ref), (s, key, val, ref)
     assert "checksum" in out
+
+
+@pytest.mark.gpu
+def test_fortran_dropin_sequence_matches_golden():
+    """The reference's roms_step kept in Fortran (fortran/seq/dropin_driver.F90,
+    main.F:374-479) calling rho_eos, set_HUV, omega, prsgrd, pre_step3d,
+    set_HUV1, step3d_uv1, visc3d, step2d x nfast, step3d_uv2, step3d_t, t3dmix
+    by name; the linked subroutines are the drop-ins themselves
+    (fortran/dropin/*.F).  20 steps, diag norms vs the golden log."""
+    gold, rows, _ = _golden_rows(os.path.join(FDIR, "dropin_driver"))
+    assert len(rows) == 21
+    for s, (g, row) in enumerate(zip(gold, rows)):
+        for key, val in zip(("ke", "ke2b", "cu_adv"), row[:3]):
+            ref = float(g[key])
+            assert abs(val - ref) <= 1e-11 * abs(ref), (s, key, val, ref)
 
 
 @pytest.mark.gpu

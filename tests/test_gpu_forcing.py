@@ -52,8 +52,17 @@ def test_frc_interp_bitwise():
     assert np.array_equal(m.get("zeta_west"), before)          # not of the requested kind
     m.frc_interp(t, m.FRC_BRY)
     assert np.array_equal(m.get("zeta_west").ravel(), cff1 * za + cff2 * zb)
-    with pytest.raises(romsgpu.RomsGpuError, match="outside the records"):
-        m.frc_interp(10.5 + 2 * c.dt + 1.0)   # set_frc_data's window check uses dt as is (roms_read_write.F:381)
+    with pytest.raises(romsgpu.RomsGpuError, match="outside the forcing records"):
+        m.frc_interp(10.0 - 2 * c.dt - 1.0)   # set_frc_data's window check uses dt as is (roms_read_write.F:381)
+    with pytest.raises(romsgpu.RomsGpuError, match="past the last forcing record"):
+        m.frc_interp(10.6)                    # set_frc_data would read the next record here
+    # a third record: past 10.5 the pair is (10.5, 11.0), as after the reference's refresh
+    cz = rng.standard_normal(shp)
+    m.frc_record("sustr", 2, 11.0, cz)
+    t = 10.7
+    m.frc_interp(t, m.FRC_SURFACE)
+    cff1, cff2 = (11.0 - t) / (11.0 - 10.5), (t - 10.5) / (11.0 - 10.5)
+    assert np.array_equal(m.get("sustr"), cff1 * b + cff2 * cz)
     m.close()
 
 
@@ -112,35 +121,43 @@ PERTURB = dict(uwnd=lambda a: 1.3 * a, vwnd=lambda a: a + 1.0, tair=lambda a: a 
                v=lambda a: 0.5 * a, t=lambda a: a + 0.3)
 
 
-def _clocked_pair(clock):
-    from test_gpu_parity import PROGNOSTIC  # noqa: F401
+def _clocked_pair(clock, nrec=3):
+    """Records [days] at 0, 6 dt and 14 dt.  Step iic's set_frc_data points
+    are (iic-1) dt ('current'), (iic-1/2) dt ('1/2 fwd') and (iic+1/2) dt
+    ('forward'), so the boundary data move to the second pair at 'forward' of
+    step 6 -- between that step's two set_bry_all calls -- and the surface
+    fields at '1/2 fwd' of step 7 (a refresh inside a step).  The
+    third record is not on the line through the first two."""
     c = basin_cfg(LLm=40, MMm=32, N=12, nonlin=True)
     c.obc, c.ubind, c.lmd, c.bulk_frc = 15, 0.1, oracle.LMD_ICELAND, 1
     o = oracle.Oracle(c)
     o.init()
     m = romsgpu.Model.from_case(c.case_id, c.LLm, c.MMm, c.N, c.NT, salinity=True, nonlin_eos=True, dt=c.dt,
                                 ndtfast=c.ndtfast, sizex=c.sizex, sizey=c.sizey, lmd=c.lmd, obc=15, bulk_frc=True)
-    t0, t1 = 0.0, 10 * c.dt / 86400.0   # records [days] around the first 12 steps
+    day = c.dt / 86400.0
     for name in ATMOS + BRY:
         a = o.field(name).copy()
         b = PERTURB[name.split("_")[0]](a)
-        for side in ((o,), (m,)):
-            side[0].frc_record(name, 0, t0, a)
-            side[0].frc_record(name, 1, t1, b)
+        recs = [(0.0, a), (6 * day, b), (14 * day, 0.5 * (a + b))][:nrec]
+        for side in (o, m):
+            for slot, (tr, r) in ((2, recs[2]), (0, recs[0]), (1, recs[1]))[3 - nrec:]:
+                side.frc_record(name, slot, tr, r)
     if clock:
         o.frc_clock(0.0)
         m.frc_clock(0.0)
     return c, o, m
 
 
-def test_in_step_forcing_two_records_vs_oracle():
-    """Time-varying forcing inside roms_gpu_step: two different
+def test_in_step_forcing_records_vs_oracle():
+    """Time-varying forcing inside roms_gpu_step: three
     records of every BULK_FRC atmospheric field and of every open-boundary
     array; each step interpolates them at the reference's four points
     (main.F:384-441: surface at 'current' and '1/2 fwd', boundary data at
-    '1/2 fwd' and 'forward'), on the device and in the oracle, which does the
-    same in plain C.  12 steps (graph replay from step 2) against the oracle,
-    RMS < 1e-10; and the result is not that of one interpolation per step."""
+    '1/2 fwd' and 'forward'), each point on its own record pair, on the device
+    (a stateless pair choice per point) and in the oracle (set_frc_data's
+    stateful refresh restated in plain C).  12 steps (graph replay from step
+    2) against the oracle, RMS < 1e-10; and the result is not that of one
+    interpolation per step."""
     from test_gpu_parity import PROGNOSTIC, RMS_RUN, check_fields
     c, o, m = _clocked_pair(True)
     o.step(12)
@@ -161,9 +178,60 @@ def test_in_step_forcing_two_records_vs_oracle():
     m2.close()
 
 
+def test_in_step_forcing_refresh_inside_a_step_bitwise():
+    """Step 6's 'forward' boundary point is past the second record: with the
+    third record loaded the boundary arrays after step 6 equal
+    cff1*rec(2) + cff2*rec(3) at (6 + 1/2) dt exactly (the pair set_frc_data
+    holds after its refresh), while '1/2 fwd' of the same step used the first
+    pair."""
+    c, o, m = _clocked_pair(True)
+    m.step(6)
+    m.sync()
+    day = c.dt / 86400.0
+    t1, t2, mt = 6 * day, 14 * day, 6.5 * day
+    cff1, cff2 = (t2 - mt) / (t2 - t1), (mt - t1) / (t2 - t1)
+    for n in ("zeta_west", "u_east", "t_north"):
+        a = o.field(n).copy()    # the oracle has not stepped: its arrays are record 1
+        b = PERTURB[n.split("_")[0]](a)
+        want = cff1 * b + cff2 * (0.5 * (a + b))
+        assert np.array_equal(m.get(n).ravel(), want.ravel()), n
+    m.close()
+
+
+def test_in_step_forcing_past_last_record_fails_before_queueing():
+    """With only two records, step 6's 'forward' point needs the next record
+    (the reference refreshes there, roms_read_write.F:341): the step fails
+    with -8 before anything is queued, and the state is that of step 5."""
+    c, o, m = _clocked_pair(True, nrec=2)
+    m.step(5)
+    m.sync()
+    before = m.get("t").copy()
+    with pytest.raises(romsgpu.RomsGpuError, match="past the last forcing record"):
+        m.step()
+    assert np.array_equal(m.get("t"), before)
+    m.close()
+
+
 def test_in_step_forcing_out_of_window_fails_before_queueing():
     c, o, m = _clocked_pair(True)
-    m.frc_clock(100 * 86400.0)   # far past the records
+    m.frc_clock(-100 * 86400.0)   # far before the records (set_frc_data's window check, :381)
     with pytest.raises(romsgpu.RomsGpuError, match="outside the forcing records"):
+        m.step()
+    m.close()
+
+
+def test_boundary_tides_need_interpolated_boundary_data():
+    """bry_tides adds onto boundary arrays that set_bry_all has
+    just re-set; an open side's zeta/ubar/vbar array that is never
+    interpolated in-step would accumulate the sums, so the step refuses."""
+    c, m = open_basin(pot=0)
+    shp = (1,) + m.get("zeta").shape[1:]
+    z = np.zeros(shp)
+    m.set_tide_data([1.4e-4], bry=((z, z), (z, z), (z, z)))
+    nb = m.get("zeta_west").size
+    m.frc_record("zeta_west", 0, 0.0, np.zeros(nb))
+    m.frc_record("zeta_west", 1, 1.0, np.zeros(nb))
+    m.frc_clock(0.0)
+    with pytest.raises(romsgpu.RomsGpuError, match="boundary tides need two records"):
         m.step()
     m.close()

@@ -65,6 +65,17 @@ def rms(a, b):
     return float(np.sqrt(np.mean((a - b) ** 2))) / scale
 
 
+def rms_abs(a, b):
+    """Field RMS error in the field's own units (north_star: u, v, w, T, S, zeta)."""
+    return float(np.sqrt(np.mean((a - b) ** 2)))
+
+
+# north_star's prognostic fields: their whole-run bound is absolute (T in
+# deg C and S in PSU are O(10), so a bound relative to their RMS would be
+# ~35x looser); w = pm*pn*(We + Wi) in m/s is formed from the fluxes
+ABSOLUTE = ("zeta", "ubar", "vbar", "u", "v", "t", "w")
+
+
 def copy_state(o, m):
     for name in romsgpu.FIELDS:
         m.put(name, o.field(name))
@@ -73,14 +84,35 @@ def copy_state(o, m):
 PROGNOSTIC = ["zeta", "ubar", "vbar", "u", "v", "t", "Hz", "z_r", "z_w", "FlxU", "FlxV", "We", "Wi"]
 
 
+def _w(src, get):
+    """pm*pn*(We+Wi) at w points (basic_output.F's history omega)."""
+    pmpn = get("pm") * get("pn")
+    return (get("We") + get("Wi")) * pmpn
+
+
 def check_fields(o, m, names, Lm, Mm, tol, kind="rel"):
-    bad = []
+    """Interior (1..Lm, 1..Mm) error of every named field, relative to the
+    field's max for kind 'rel' (per-routine checks), RMS for kind 'rms' (whole
+    runs: absolute for ABSOLUTE, scaled for the rest; a run that checks We
+    and Wi also checks w absolutely).  Returns {name: error}."""
+    names = list(names)
+    if kind == "rms" and "We" in names and "Wi" in names and "w" not in names:
+        names.append("w")
+    bad, errs = [], {}
     for n in names:
-        a, b = interior(m.get(n), Lm, Mm), interior(o.field(n), Lm, Mm)
-        e = relerr(a, b) if kind == "rel" else rms(a, b)
+        if n == "w":
+            a, b = interior(_w(m, m.get), Lm, Mm), interior(_w(o, o.field), Lm, Mm)
+        else:
+            a, b = interior(m.get(n), Lm, Mm), interior(o.field(n), Lm, Mm)
+        if kind == "rel":
+            e = relerr(a, b)
+        else:
+            e = rms_abs(a, b) if n in ABSOLUTE else rms(a, b)
+        errs[n] = e
         if not (e <= tol):
             bad.append((n, e))
     assert not bad, bad
+    return errs
 
 
 def test_filament_init_matches_oracle():
@@ -216,29 +248,57 @@ def test_rho_eos_reuse_bitwise_and_invalidated(graphs, monkeypatch):
     """A step opens with rho_eos(nrhs) (main.F:397) on the t, z_r, Hz the
     previous step's closing rho_eos(nnew) (main.F:479) already used; the
     library skips the repeat (roms_shim.cpp g.rho_slot).  With the skip on
-    and off the runs are bitwise equal, including after the host rewrites t
-    between steps (copy_in must invalidate the reuse)."""
+    and off the runs are bitwise equal, including after the host changes the
+    state between steps through each entry that can: copy_in of
+    t, a registered mirror's upload of t, copy_in of z_r, new pipe sources
+    (set_pipe_frc) and a host-side forcing interpolation (frc_record +
+    frc_interp of stflx) -- each must invalidate the reuse."""
     if not graphs:
         monkeypatch.setenv("ROMS_GPU_NO_GRAPH", "1")
     cfg = oracle.pipes_cfg(LLm=40, MMm=40, np_xi=1, np_eta=1)
 
-    def run(reuse):
+    def edit(m, how):
+        if how == "copy_in_t":
+            t = m.get("t")
+            t[:, 15:25, 15:25] += 0.75     # every level and slot of T (and S) in a patch
+            m.put("t", t)
+        elif how == "upload_t":
+            t = np.ascontiguousarray(m.get("t")).ravel().copy()
+            m.register("t", t)
+            t.reshape(m.get("t").shape)[:, 10:20, 20:30] -= 0.5
+            m.upload("t")
+        elif how == "copy_in_zr":
+            z = m.get("z_r")
+            z[:, 12:18, 12:18] *= 1.001
+            m.put("z_r", z)
+        elif how == "pipe":
+            idx = np.zeros(m.shape2, dtype=np.int32)
+            flx = np.zeros(m.shape2)
+            idx[20, 20] = 1
+            flx[20, 20] = 1.0
+            m.set_pipe_frc(idx, flx, np.full((1, cfg.N), 1.0 / cfg.N), np.array([[5.0, 1.0]]))
+        elif how == "frc_interp":
+            st = m.get("stflx")
+            m.frc_record("stflx", 0, 0.0, st)
+            m.frc_record("stflx", 1, 1.0, st + 1e-5)
+            m.frc_interp(0.5, m.FRC_SURFACE)
+
+    def run(reuse, how):
         monkeypatch.setenv("ROMS_GPU_RHO_REUSE", "1" if reuse else "0")
         m = romsgpu.Model.from_case(cfg.case_id, cfg.LLm, cfg.MMm, cfg.N, cfg.NT, salinity=True, nonlin_eos=True,
                                     dt=cfg.dt, ndtfast=cfg.ndtfast, sizex=cfg.sizex, sizey=cfg.sizey, lmd=cfg.lmd)
         m.step(3)
         m.diag()
-        t = m.get("t")
-        t[:, 15:25, 15:25] += 0.75     # every level and slot of T (and S) in a patch
-        m.put("t", t)
+        edit(m, how)
         m.step(3)
         out = {n: m.get(n) for n in ("rho1", "qp1", "bvf", "t", "u", "v", "zeta", "Akv", "Akt")}
         m.close()
         return out
 
-    a, b = run(True), run(False)
-    for n in a:
-        assert np.array_equal(a[n], b[n]), n
+    for how in ("copy_in_t", "upload_t", "copy_in_zr", "pipe", "frc_interp"):
+        a, b = run(True, how), run(False, how)
+        for n in a:
+            assert np.array_equal(a[n], b[n]), (how, n)
 
 
 def test_s2d_edges_folded_bitwise(monkeypatch):

@@ -24,10 +24,15 @@
 namespace roms {
 namespace {
 
+// up to three records of one field: the reference's pair (it1, it2) plus the
+// next record, so that a refresh falling inside a step (set_frc_data moves
+// to (it2, next) once times(it2) < modtime, roms_read_write.F:341-350) is
+// reproduced at the phase where it happens
+constexpr int kFrcSlots = 3;
 struct FrcField {
-  double* slot[2] = {nullptr, nullptr};
-  double time[2] = {0.0, 0.0};
-  bool have[2] = {false, false};
+  double* slot[kFrcSlots] = {nullptr, nullptr, nullptr};
+  double time[kFrcSlots] = {0.0, 0.0, 0.0};
+  bool have[kFrcSlots] = {false, false, false};
   long n = 0;
   int kind = 0;   // ROMS_FRC_SURFACE / ROMS_FRC_BRY
 };
@@ -42,8 +47,8 @@ struct FrcStep {
   bool on = false;
   double start = 0.0;        // start_time [s] (time = start + dt*(iic-ntstart), main.F:373)
   long gen = 1;              // bumped when captured graphs would go stale
-  std::vector<int> ids;      // fields with both records: interpolated inside the step
-  double* dev = nullptr;     // [4 points][ids][2 slots] weights, then cos/sin of the tides
+  std::vector<int> ids;      // fields with two or more records: interpolated inside the step
+  double* dev = nullptr;     // [4 points][ids][slot a, slot b, cff1, cff2], then cos/sin of the tides
   size_t dev_n = 0;
   double* pin[4] = {};       // pinned staging ring, one event each
   hipEvent_t ev[4] = {};
@@ -62,12 +67,17 @@ __global__ void __launch_bounds__(256) k_frc_interp(double* __restrict__ out, co
   for (long q = blockIdx.x * 256L + threadIdx.x; q < n; q += (long)gridDim.x * 256L) out[q] = cff1 * a[q] + cff2 * b[q];
 }
 
-// weights from device memory (the in-step schedule): out = c[0]*slot0 + c[1]*slot1,
-// which is cff1*rec(it1) + cff2*rec(it2) to the bit in either slot order
-__global__ void __launch_bounds__(256) k_frc_interp_dev(double* __restrict__ out, const double* __restrict__ a,
-                                                        const double* __restrict__ b, const double* __restrict__ c,
-                                                        long n) {
-  const double c0 = c[0], c1 = c[1];
+// pair and weights from device memory (the in-step schedule, formed per step
+// on the host): out = cff1*rec(it1) + cff2*rec(it2) with it1 = slot c[0],
+// it2 = slot c[1] -- the graph keeps the slot pointers, the step picks the pair
+struct FrcSlots {
+  const double* s[kFrcSlots];
+};
+__global__ void __launch_bounds__(256) k_frc_interp_dev(double* __restrict__ out, FrcSlots r,
+                                                        const double* __restrict__ c, long n) {
+  const double* __restrict__ a = r.s[(int)c[0]];
+  const double* __restrict__ b = r.s[(int)c[1]];
+  const double c0 = c[2], c1 = c[3];
   for (long q = blockIdx.x * 256L + threadIdx.x; q < n; q += (long)gridDim.x * 256L) out[q] = c0 * a[q] + c1 * b[q];
 }
 
@@ -156,16 +166,52 @@ void launch_tides(const Dev& d, hipStream_t s, const double* dcs, bool pot, bool
   }
 }
 
-// (it1, it2) and the weights of set_frc_data (roms_read_write.F:330-388) at
-// modtime [days]; false when modtime is outside the records' window
-bool frc_weights(const FrcField& F, double modtime, double dt, double& c0, double& c1) {
-  const int it1 = F.time[0] <= F.time[1] ? 0 : 1, it2 = 1 - it1;
-  const double t1 = F.time[it1], t2 = F.time[it2];
-  if (!(t2 > t1) || t1 > modtime + dt || t2 < modtime - dt) return false;
-  const double cff1 = (t2 - modtime) / (t2 - t1), cff2 = (modtime - t1) / (t2 - t1);
-  c0 = it1 == 0 ? cff1 : cff2;
-  c1 = it1 == 0 ? cff2 : cff1;
-  return true;
+// The record pair and weights set_frc_data uses at modtime [days]
+// (roms_read_write.F:338-381).  The reference keeps (it1, it2) and, whenever
+// times(it2) < modtime, refreshes to (it2, next record) (:341-350); for model
+// times that only grow this is the earliest consecutive pair of the loaded
+// records (in time order) whose later time is >= modtime.  Returns 0 with
+// slot ia = it1, ib = it2 and cff1/cff2 (:376-377); 1 when modtime is past
+// every loaded record (the reference would read the next record here: the
+// host must load it first); -1 for the out-of-window check (:381, dt as the
+// reference has it); -2 for records with equal times.
+int frc_pair(const FrcField& F, double modtime, double dt, int& ia, int& ib, double& cff1, double& cff2) {
+  int ord[kFrcSlots], n = 0;
+  for (int s = 0; s < kFrcSlots; s++)
+    if (F.have[s]) {
+      int k = n++;
+      while (k > 0 && F.time[ord[k - 1]] > F.time[s]) { ord[k] = ord[k - 1]; k--; }
+      ord[k] = s;
+    }
+  if (n < 2) return -1;
+  for (int k = 0; k + 1 < n; k++)
+    if (!(F.time[ord[k + 1]] > F.time[ord[k]])) return -2;
+  int k = 0;
+  while (k + 2 < n && F.time[ord[k + 1]] < modtime) k++;
+  ia = ord[k];
+  ib = ord[k + 1];
+  const double t1 = F.time[ia], t2 = F.time[ib];
+  if (t2 < modtime) return 1;
+  if (t1 > modtime + dt || t2 < modtime - dt) return -1;
+  cff1 = (t2 - modtime) / (t2 - t1);
+  cff2 = (modtime - t1) / (t2 - t1);
+  return 0;
+}
+
+int nrec(const FrcField& F) {
+  int n = 0;
+  for (int s = 0; s < kFrcSlots; s++) n += F.have[s] ? 1 : 0;
+  return n;
+}
+
+std::string frc_pair_error(int rc, int id, double modtime, const char* where, const char* entry) {
+  const std::string f = " of field " + std::to_string(id) + " at model time " + std::to_string(modtime) + " days (" +
+                        where + ")";
+  if (rc == 1)
+    return std::string(entry) + ": model time past the last forcing record" + f +
+           ": load the next record first (set_frc_data refresh, roms_read_write.F:341-350)";
+  if (rc == -2) return std::string(entry) + ": two records have the same time" + f;
+  return std::string(entry) + ": model time outside the forcing records" + f + " (set_frc_data, roms_read_write.F:381-388)";
 }
 
 }  // namespace
@@ -175,13 +221,31 @@ long frc_step_gen() { return fc.st.on ? fc.st.gen : 0; }
 int frc_step_prepare(hipStream_t s, const Dev& d, double dt, const roms_tlev& t, std::string& err) {
   FrcStep& st = fc.st;
   if (!st.on) return 0;
-  (void)d;
   std::vector<int> ids;
   for (int id = 0; id < (int)fc.f.size(); id++)
-    if (fc.f[id].have[0] && fc.f[id].have[1]) ids.push_back(id);
+    if (nrec(fc.f[id]) >= 2) ids.push_back(id);
   if (ids != st.ids) { st.ids = ids; st.gen++; }
   const int nid = (int)ids.size(), nt = fc.tide.ntides;
-  const size_t n = (size_t)8 * nid + 2 * nt + 1;
+  // bry_tides adds the constituents onto every open side's zeta/ubar/vbar
+  // data after each set_bry_all (main.F:389-394, 438-441), which re-sets
+  // those arrays first: each of them must be interpolated in-step, or the
+  // sums would pile up from step to step
+  if (nt > 0 && fc.tide.zr && d.p.obc) {
+    const int edge[4] = {d.b.west_edge, d.b.east_edge, d.b.south_edge, d.b.north_edge};
+    for (int side = 0; side < 4; side++) {
+      if (!(d.p.obc & (1 << side)) || !edge[side]) continue;
+      for (int var = 0; var < 3; var++) {
+        const int id = ROMS_zeta_west + 4 * var + side;
+        if (id >= (int)fc.f.size() || nrec(fc.f[id]) < 2) {
+          err = "roms_gpu_step: boundary tides need two records of every open side's zeta/ubar/vbar data "
+                "(set_bry_all re-sets them before set_tides, main.F:389-394); field " + std::to_string(id) +
+                " has fewer";
+          return -1;
+        }
+      }
+    }
+  }
+  const size_t n = (size_t)16 * nid + 2 * nt + 1;
   if (st.dev_n < n) {
     if (st.dev) { (void)hipStreamSynchronize(s); (void)hipFree(st.dev); st.dev = nullptr; }
     if (hipMalloc(&st.dev, n * sizeof(double)) != hipSuccess) { err = "frc_step: allocation failed"; st.dev_n = 0; return -2; }
@@ -213,25 +277,30 @@ int frc_step_prepare(hipStream_t s, const Dev& d, double dt, const roms_tlev& t,
                          tdays + 0.5 * dt * sec2day,                 // set_bry_all, '1/2 fwd'
                          tdays + 0.5 * dt * sec2day,                 // set_forces, '1/2 fwd'
                          (time + 0.5 * dt) * sec2day + dt * sec2day};  // set_bry_all, 'forward'
+  static const char* const where[4] = {"set_forces 'current'", "set_bry_all '1/2 fwd'", "set_forces '1/2 fwd'",
+                                        "set_bry_all 'forward'"};
   const int r = st.ring;
   (void)hipEventSynchronize(st.ev[r]);   // its previous copy has landed
   double* h = st.pin[r];
   for (int p = 0; p < 4; p++)
     for (int q = 0; q < nid; q++) {
       const FrcField& F = fc.f[ids[q]];
-      double* c = h + ((size_t)p * nid + q) * 2;
-      c[0] = c[1] = 0.0;
+      double* c = h + ((size_t)p * nid + q) * 4;
+      c[0] = c[1] = c[2] = c[3] = 0.0;
       if ((p % 2 == 0) != (F.kind == ROMS_FRC_SURFACE)) continue;
-      if (!frc_weights(F, mod[p], dt, c[0], c[1])) {
-        err = "roms_gpu_step: model time outside the forcing records of field " + std::to_string(ids[q]) +
-              " (set_frc_data, roms_read_write.F:381-388)";
-        return -1;
+      int ia = 0, ib = 0;
+      const int rc = frc_pair(F, mod[p], dt, ia, ib, c[2], c[3]);
+      if (rc) {
+        err = frc_pair_error(rc, ids[q], mod[p], where[p], "roms_gpu_step");
+        return rc == 1 ? -8 : -1;
       }
+      c[0] = ia;
+      c[1] = ib;
     }
   for (int q = 0; q < nt; q++) {   // omT = ftide*(time + 0.5*dt) (tides.F:129), both set_tides calls
     const double omT = fc.tide.ftide[q] * (time + 0.5 * dt);
-    h[(size_t)8 * nid + q] = std::cos(omT);
-    h[(size_t)8 * nid + nt + q] = std::sin(omT);
+    h[(size_t)16 * nid + q] = std::cos(omT);
+    h[(size_t)16 * nid + nt + q] = std::sin(omT);
   }
   if (hipMemcpyAsync(st.dev, h, n * sizeof(double), hipMemcpyHostToDevice, s) != hipSuccess ||
       hipEventRecord(st.ev[r], s) != hipSuccess) {
@@ -254,12 +323,15 @@ void frc_step_phase(const Dev& d, hipStream_t s, int phase, bool pot_tides) {
     if (F.kind != kind) continue;
     if (id >= ROMS_zeta_west && id <= ROMS_vbar_north) bry = true;
     const long nb = (F.n + 255) / 256;
-    hipLaunchKernelGGL(k_frc_interp_dev, dim3((unsigned)(nb < 8192 ? nb : 8192)), dim3(256), 0, s, shim_field(id),
-                       F.slot[0], F.slot[1], st.dev + ((size_t)phase * nid + q) * 2, F.n);
+    FrcSlots r{};
+    for (int k = 0; k < kFrcSlots; k++) r.s[k] = F.slot[k] ? F.slot[k] : F.slot[0];
+    hipLaunchKernelGGL(k_frc_interp_dev, dim3((unsigned)(nb < 8192 ? nb : 8192)), dim3(256), 0, s, shim_field(id), r,
+                       st.dev + ((size_t)phase * nid + q) * 4, F.n);
   }
   // set_tides after each set_bry_all (main.F:394,441): the boundary sums go
-  // onto freshly interpolated zeta/ubar/vbar data only
-  if (kind == ROMS_FRC_BRY && fc.tide.ntides > 0) launch_tides(d, s, st.dev + (size_t)8 * nid, pot_tides, bry);
+  // onto freshly interpolated zeta/ubar/vbar data only (frc_step_prepare
+  // requires two records of every open side's arrays when tides are on)
+  if (kind == ROMS_FRC_BRY && fc.tide.ntides > 0) launch_tides(d, s, st.dev + (size_t)16 * nid, pot_tides, bry);
 }
 
 void frc_free() {
@@ -292,7 +364,7 @@ int roms_gpu_frc_record(int field_id, int slot, double rec_time, const double* d
   ShimState S;
   int r = shim_enter(S);
   if (r) return r;
-  if (field_id < 0 || field_id >= ROMS_NFIELDS || slot < 0 || slot > 1 || !data) {
+  if (field_id < 0 || field_id >= ROMS_NFIELDS || slot < 0 || slot >= kFrcSlots || !data) {
     *S.err = "roms_gpu_frc_record: bad field/slot/data";
     return -1;
   }
@@ -327,23 +399,26 @@ int roms_gpu_frc_interp(double modtime, int kinds) {
   // set_frc_data compares times in days with modtime +- dt, dt in seconds
   // (roms_read_write.F:381): kept as the reference has it
   const double dtw = S.cfg->dt;
-  for (int id = 0; id < (int)fc.f.size(); id++) {
-    FrcField& F = fc.f[id];
-    if (!(F.have[0] && F.have[1]) || !(kinds & F.kind)) continue;
-    const int it1 = F.time[0] <= F.time[1] ? 0 : 1, it2 = 1 - it1;
-    const double t1 = F.time[it1], t2 = F.time[it2];
-    if (!(t2 > t1)) { *S.err = "roms_gpu_frc_interp: the two records of a field have the same time"; return -1; }
-    // set_frc_data's out-of-window check (roms_read_write.F:381-388)
-    if (t1 > modtime + dtw || t2 < modtime - dtw) {
-      *S.err = "roms_gpu_frc_interp: model time outside the records of field " + std::to_string(id);
-      return -1;
+  struct Job { int id, ia, ib; double c1, c2; };
+  std::vector<Job> jobs;
+  for (int id = 0; id < (int)fc.f.size(); id++) {   // every check before anything is queued
+    const FrcField& F = fc.f[id];
+    if (nrec(F) < 2 || !(kinds & F.kind)) continue;
+    Job j{id, 0, 0, 0.0, 0.0};
+    const int rc = frc_pair(F, modtime, dtw, j.ia, j.ib, j.c1, j.c2);
+    if (rc) {
+      *S.err = frc_pair_error(rc, id, modtime, "frc_interp", "roms_gpu_frc_interp");
+      return rc == 1 ? -8 : -1;
     }
-    const double cff1 = (t2 - modtime) / (t2 - t1), cff2 = (modtime - t1) / (t2 - t1);
-    double* out = shim_field(id);   // the field's device array
+    jobs.push_back(j);
+  }
+  for (const Job& j : jobs) {
+    const FrcField& F = fc.f[j.id];
+    double* out = shim_field(j.id);   // the field's device array
     const long n = F.n;
     const long nb = (n + 255) / 256;
-    hipLaunchKernelGGL(k_frc_interp, dim3((unsigned)(nb < 8192 ? nb : 8192)), dim3(256), 0, S.s, out, F.slot[it1],
-                       F.slot[it2], cff1, cff2, n);
+    hipLaunchKernelGGL(k_frc_interp, dim3((unsigned)(nb < 8192 ? nb : 8192)), dim3(256), 0, S.s, out, F.slot[j.ia],
+                       F.slot[j.ib], j.c1, j.c2, n);
   }
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }

@@ -418,32 +418,53 @@ int roms_gpu_selftest_zero_fill(long n, int chunks, long* bad) {
   REQUIRE_INIT();
   if (n < 1 || chunks < 1 || chunks > 1024 || !bad) { g.err = "roms_gpu_selftest_zero_fill: bad argument"; return -1; }
   std::vector<double*> a((size_t)chunks, nullptr);
+  unsigned long long* cnt = nullptr;
+  bool guarded = false;   // a[] came from dev_alloc (guard_base entries when g.guard)
+  // every exit frees what was taken, on error paths too
+  auto release = [&]() {
+    (void)hipStreamSynchronize(g.s);
+    for (double*& p : a) {
+      if (!p) continue;
+      if (guarded && g.guard) {
+        (void)hipFree(dev_base(p));
+        g.guard_base.erase(p);
+      } else {
+        (void)hipFree(p);
+      }
+      p = nullptr;
+    }
+    if (cnt) { (void)hipFree(cnt); cnt = nullptr; }
+  };
+  auto fail = [&](hipError_t e, const char* what) -> int {
+    g.err = std::string("roms_gpu_selftest_zero_fill: ") + what + ": " + hipGetErrorString(e);
+    release();
+    return -2;
+  };
+  hipError_t e;
   for (double*& p : a) {
-    CHECK_HIP(hipMalloc(&p, (size_t)n * sizeof(double)));
+    if ((e = hipMalloc(&p, (size_t)n * sizeof(double))) != hipSuccess) { p = nullptr; return fail(e, "hipMalloc"); }
     launch_fill_ones(p, n, g.s);
   }
-  CHECK_HIP(hipStreamSynchronize(g.s));
-  for (double* p : a) CHECK_HIP(hipFree(p));
-  unsigned long long* cnt = nullptr;
-  CHECK_HIP(hipMalloc(&cnt, 2 * sizeof(unsigned long long)));
-  CHECK_HIP(hipMemsetAsync(cnt, 0, 2 * sizeof(unsigned long long), g.s));
-  CHECK_HIP(hipStreamSynchronize(g.s));
+  if ((e = hipStreamSynchronize(g.s)) != hipSuccess) return fail(e, "fill");
   for (double*& p : a) {
-    CHECK_HIP(dev_alloc(p, n));
+    (void)hipFree(p);
+    p = nullptr;
+  }
+  if ((e = hipMalloc(&cnt, 2 * sizeof(unsigned long long))) != hipSuccess) { cnt = nullptr; return fail(e, "hipMalloc"); }
+  if ((e = hipMemsetAsync(cnt, 0, 2 * sizeof(unsigned long long), g.s)) != hipSuccess) return fail(e, "memset");
+  if ((e = hipStreamSynchronize(g.s)) != hipSuccess) return fail(e, "memset");
+  guarded = true;
+  for (double*& p : a) {
+    if ((e = dev_alloc(p, n)) != hipSuccess) { p = nullptr; return fail(e, "dev_alloc"); }
     launch_count_nonzero(p, n, cnt, g.s, 0.0);
     launch_fill_ones(p, n, g.s);
   }
-  CHECK_HIP(hipDeviceSynchronize());
+  if ((e = hipDeviceSynchronize()) != hipSuccess) return fail(e, "drain");
   for (double* p : a) launch_count_nonzero(p, n, cnt + 1, g.s, 1.0);
   unsigned long long h[2] = {0, 0};
-  CHECK_HIP(hipMemcpyAsync(h, cnt, sizeof(h), hipMemcpyDeviceToHost, g.s));
-  CHECK_HIP(hipStreamSynchronize(g.s));
-  const long G = g.guard ? 4096 : 0;
-  for (double* p : a) {
-    CHECK_HIP(hipFree(G ? g.guard_base[p] : p));
-    if (G) g.guard_base.erase(p);
-  }
-  (void)hipFree(cnt);
+  if ((e = hipMemcpyAsync(h, cnt, sizeof(h), hipMemcpyDeviceToHost, g.s)) != hipSuccess) return fail(e, "copy");
+  if ((e = hipStreamSynchronize(g.s)) != hipSuccess) return fail(e, "copy");
+  release();
   *bad = (long)(h[0] + h[1]);
   return 0;
 }
