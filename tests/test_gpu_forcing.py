@@ -138,10 +138,11 @@ def _clocked_pair(clock, nrec=3):
     for name in ATMOS + BRY:
         a = o.field(name).copy()
         b = PERTURB[name.split("_")[0]](a)
-        recs = [(0.0, a), (6 * day, b), (14 * day, 0.5 * (a + b))][:nrec]
+        recs = [(0.0, a), (6 * day, b), (14 * day, 0.5 * (a + b))]
+        order = (2, 0, 1) if nrec == 3 else (0, 1)   # slots in any order: the pair follows the times
         for side in (o, m):
-            for slot, (tr, r) in ((2, recs[2]), (0, recs[0]), (1, recs[1]))[3 - nrec:]:
-                side.frc_record(name, slot, tr, r)
+            for slot in order:
+                side.frc_record(name, slot, recs[slot][0], recs[slot][1])
     if clock:
         o.frc_clock(0.0)
         m.frc_clock(0.0)
@@ -187,8 +188,10 @@ def test_in_step_forcing_refresh_inside_a_step_bitwise():
     c, o, m = _clocked_pair(True)
     m.step(6)
     m.sync()
-    day = c.dt / 86400.0
-    t1, t2, mt = 6 * day, 14 * day, 6.5 * day
+    day, sec2day = c.dt / 86400.0, 1.0 / 86400.0
+    time = 5 * c.dt    # step 6: time = start_time + dt*(iic - ntstart) (main.F:374)
+    t1, t2 = 6 * day, 14 * day
+    mt = (time + 0.5 * c.dt) * sec2day + c.dt * sec2day   # 'forward' (main.F:438, roms_read_write.F:335)
     cff1, cff2 = (t2 - mt) / (t2 - t1), (mt - t1) / (t2 - t1)
     for n in ("zeta_west", "u_east", "t_north"):
         a = o.field(n).copy()    # the oracle has not stepped: its arrays are record 1

@@ -14,14 +14,15 @@ namespace roms {
 
 __global__ void __launch_bounds__(256) k_periodic_wrap(Bounds b, ExchList L) {
   const int Lm = b.Lm, Mm = b.Mm;
-  const int nrow = 4 * b.nx2;           // rows j=-1,0,Mm+1,Mm+2, all i
+  const int W = Lm + 4;                 // i = -1..Lm+2 (not the row padding)
+  const int nrow = 4 * W;               // rows j=-1,0,Mm+1,Mm+2, all i
   const int ncol = 4 * Mm;              // columns i=-1,0,Lm+1,Lm+2, j=1..Mm
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= nrow + ncol) return;
   int i, j;
   if (p < nrow) {
-    const int r = p / b.nx2;
-    i = p - r * b.nx2 - 1;
+    const int r = p / W;
+    i = p - r * W - 1;
     j = r < 2 ? r - 1 : Mm - 1 + r;
   } else {
     // the four halo columns of one row j are neighbouring threads, so each
@@ -64,7 +65,7 @@ void launch_exchange_list(const Dev& d, hipStream_t s, const ExchList& L) {
     return;
   }
   if (!b.ew_periodic && !b.ns_periodic) return;
-  const int n = 4 * b.nx2 + 4 * b.Mm;
+  const int n = 4 * (b.Lm + 4) + 4 * b.Mm;
   int nl = 0;
   for (int q = 0; q < L.n; q++) nl += L.nlev[q];
   if (nl == 0) return;

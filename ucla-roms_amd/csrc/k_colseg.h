@@ -304,24 +304,56 @@ __device__ __forceinline__ void tracer_spline_seg(const SegSpan& sg, int N, long
 // i >= istrU, 1: v at j >= jstrV), kSegCW columns x blockDim.z rows j per block.
 // Lanes outside the column range (i or j) solve a clamped duplicate column
 // (they take part in the barriers) and store nothing.
+// v columns (Params::seg_vtile, kSegCW = 64): a wavefront's 64 lanes hold a
+// 16 x 4 tile of columns instead of one row of 64.  The v stencils read the
+// rows j-2..j+1 of Hz and We and j-1 of Hz_fwd/bak, Akv, Wi; with one row per
+// wavefront every one of those rows is another block's row and comes from
+// HBM again (no L2 reuse at ~1 MB of columns per block), with four rows per
+// wavefront the tile's 7 (4) distinct rows serve its 16 (8) row reads.  A
+// 16-wide row is one 128-B line at the device row pitch (roms_dev.h).  The
+// blocks of the two directions enumerate their own tiles; a block whose
+// tile lies outside the range is idle (returns before any barrier).
+constexpr int kVTX = 16, kVTY = 4;
 struct SegCol {
   int i, j, dir;
-  bool act;
+  bool act, idle;
 };
+__device__ __forceinline__ bool seg_vtile_on(const Dev& d) { return d.p.seg_vtile && kSegCW == kVTX * kVTY; }
 __device__ __forceinline__ void seg_uv_col(const Dev& d, const Range& R, const uint3& bI, const SegSpan& sg,
                                            SegCol& c) {
   const Bounds& b = d.b;
   c.dir = (int)bI.z;
   const int ilo = c.dir == 0 ? b.istrU : b.istr;
   const int jlo = c.dir == 1 ? (b.jstrV > R.j0 ? b.jstrV : R.j0) : R.j0;
-  const int iu = R.i0 + (int)bI.x * kSegCW + sg.col;
-  const int ju = R.j0 + (int)bI.y * (int)blockDim.z + sg.row;
+  int iu, ju;
+  if (c.dir == 1 && seg_vtile_on(d)) {
+    const int ntx = (R.i1 - R.i0 + kVTX) / kVTX, nty = (R.j1 - R.j0 + kVTY) / kVTY;
+    const int t = (int)bI.x + (int)gridDim.x * (int)bI.y;
+    c.idle = t >= ntx * nty;
+    iu = R.i0 + (t % ntx) * kVTX + sg.col % kVTX;
+    ju = R.j0 + (t / ntx) * kVTY + sg.col / kVTX;
+  } else {
+    iu = R.i0 + (int)bI.x * kSegCW + sg.col;
+    ju = R.j0 + (int)bI.y * (int)blockDim.z + sg.row;
+    c.idle = R.j0 + (int)bI.y * (int)blockDim.z > R.j1;
+  }
   c.act = iu >= ilo && iu <= R.i1 && ju >= jlo && ju <= R.j1;
   c.i = iu < ilo ? ilo : (iu > R.i1 ? R.i1 : iu);
   c.j = ju < jlo ? jlo : (ju > R.j1 ? R.j1 : ju);
 }
 inline dim3 seg_grid_of(const Range& R, int nz, int jrows = 1) {
   return dim3((R.i1 - R.i0 + kSegCW) / kSegCW, (R.j1 - R.j0 + jrows) / jrows, nz);
+}
+// the momentum kernels' grid: enough blocks in (x, y) for the u rows and for
+// the v tiles (seg_uv_col)
+inline dim3 seg_uv_grid(const Dev& d, const Range& R, int jrows) {
+  dim3 g = seg_grid_of(R, 2, jrows);
+  if (d.p.seg_vtile && kSegCW == kVTX * kVTY && jrows == 1) {
+    const long nvt = (long)((R.i1 - R.i0 + kVTX) / kVTX) * ((R.j1 - R.j0 + kVTY) / kVTY);
+    const long gy = (nvt + g.x - 1) / g.x;
+    if (gy > (long)g.y) g.y = (unsigned)gy;
+  }
+  return g;
 }
 
 }  // namespace roms

@@ -225,6 +225,19 @@ struct AccTL {
   __device__ __forceinline__ double fu(int i, int j) const { return FU[at(i, j)]; }
   __device__ __forceinline__ double fv(int i, int j) const { return FV[at(i, j)]; }
 };
+// The same windows as a ring of kRingH rows (j-marching kernels): row j sits
+// in slot (j - jb) mod kRingH, jb the first window row of the block's chunk.
+constexpr int kRingH = 8;
+struct AccTR {
+  const double *T, *UM, *VM, *FU, *FV;
+  int ib, jb;
+  __device__ __forceinline__ int at(int i, int j) const { return (i - ib) + ((j - jb) & (kRingH - 1)) * kUVW; }
+  __device__ __forceinline__ double t(int i, int j) const { return T[at(i, j)]; }
+  __device__ __forceinline__ double um(int i, int j) const { return UM[at(i, j)]; }
+  __device__ __forceinline__ double vm(int i, int j) const { return VM[at(i, j)]; }
+  __device__ __forceinline__ double fu(int i, int j) const { return FU[at(i, j)]; }
+  __device__ __forceinline__ double fv(int i, int j) const { return FV[at(i, j)]; }
+};
 template <class A>
 __device__ __forceinline__ double tracer_fx(const Bounds& b, const A& a, int m, int j, bool upstream) {
   const int lo = b.west_edge ? b.istr : -1000000, hi = b.east_edge ? b.iend + 1 : 1000000;
@@ -280,6 +293,14 @@ __device__ __forceinline__ void tracer_win_fill(const Bounds& b, const Fields& F
   }
 }
 
+// grid of the j-marching per-level kernels: 64-wide strips x chunks of jc
+// rows (marched 4 rows at a time) x levels
+inline dim3 grid3_jc(const Range& r, int nk, int jc) {
+  int ni = r.i1 - r.i0 + 1, nj = r.j1 - r.j0 + 1;
+  if (ni < 1) ni = 1;
+  if (nj < 1) nj = 1;
+  return dim3((ni + kBX - 1) / kBX, (nj + jc - 1) / jc, nk);
+}
 // grid of the per-level horizontal kernels with 64 x ty tiles (Params::h_ty)
 inline dim3 grid3_ty(const Range& r, int nk, int ty) {
   int ni = r.i1 - r.i0 + 1, nj = r.j1 - r.j0 + 1;

@@ -224,6 +224,18 @@ __global__ void __launch_bounds__(256) k_count_nonzero(const double* __restrict_
 __global__ void __launch_bounds__(256) k_fill_ones(double* __restrict__ p, long n) {
   for (long q = blockIdx.x * 256L + threadIdx.x; q < n; q += (long)gridDim.x * 256L) p[q] = 1.0;
 }
+__global__ void __launch_bounds__(256) k_rows_copy(double* __restrict__ dst, long dpitch, const double* __restrict__ src,
+                                                   long spitch, long width, long rows) {
+  const long n = width * rows;
+  for (long q = blockIdx.x * 256L + threadIdx.x; q < n; q += (long)gridDim.x * 256L) {
+    const long r = q / width, c = q - r * width;
+    dst[r * dpitch + c] = src[r * spitch + c];
+  }
+}
+void launch_rows_copy(double* dst, long dpitch, const double* src, long spitch, long width, long rows, hipStream_t s) {
+  const long n = width * rows, nb = (n + 255) / 256;
+  if (n > 0) hipLaunchKernelGGL(k_rows_copy, dim3((unsigned)(nb < 65536 ? nb : 65536)), dim3(256), 0, s, dst, dpitch, src, spitch, width, rows);
+}
 void launch_fill_ones(double* p, long n, hipStream_t s) {
   hipLaunchKernelGGL(k_fill_ones, dim3(2048), dim3(256), 0, s, p, n);
 }

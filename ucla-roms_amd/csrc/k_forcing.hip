@@ -368,7 +368,7 @@ int roms_gpu_frc_record(int field_id, int slot, double rec_time, const double* d
     *S.err = "roms_gpu_frc_record: bad field/slot/data";
     return -1;
   }
-  const long n = roms_gpu_field_size(field_id);
+  const long n = shim_field_dev_count(field_id);   // the record lives in the device layout, like the field
   if ((long)fc.f.size() < ROMS_NFIELDS) fc.f.resize(ROMS_NFIELDS);
   FrcField& F = fc.f[field_id];
   if (!F.slot[slot]) {
@@ -382,8 +382,7 @@ int roms_gpu_frc_record(int field_id, int slot, double rec_time, const double* d
   F.kind = field_kind(field_id);
   // ordered after the kernels already queued (a slot may still be read by an
   // interpolation of the current step)
-  if (hipMemcpyAsync(F.slot[slot], data, (size_t)n * sizeof(double), hipMemcpyHostToDevice, S.s) != hipSuccess ||
-      hipStreamSynchronize(S.s) != hipSuccess) {
+  if (shim_field_h2d(field_id, F.slot[slot], data) != hipSuccess) {
     *S.err = "roms_gpu_frc_record: upload failed";
     return -2;
   }
@@ -453,10 +452,12 @@ int roms_gpu_set_tide_data(int ntides, const double* ftide, const double* pot_re
   fc.st.gen++;
   T.ntides = ntides;
   T.ftide.assign(ftide, ftide + ntides);
+  // ntides planes of the host layout into the device layout (rows of nx2)
   const size_t nb = (size_t)ntides * S.d->b.n2 * sizeof(double);
+  const long rows = (long)ntides * (S.d->b.Mm + 4);
   auto up = [&](double*& d, const double* h) -> bool {
     if (!h || ntides == 0) return true;
-    return hipMalloc(&d, nb) == hipSuccess && copy_on(d, h, nb, hipMemcpyHostToDevice, S.s) == hipSuccess;
+    return hipMalloc(&d, nb) == hipSuccess && shim_rows_h2d(d, h, rows) == hipSuccess;
   };
   if (!up(T.pr, pot_re) || !up(T.pi, pot_im) || !up(T.zr, ztide_re) || !up(T.zi, ztide_im) || !up(T.ur, utide_re) ||
       !up(T.ui, utide_im) || !up(T.vr, vtide_re) || !up(T.vi, vtide_im)) {

@@ -163,6 +163,154 @@ __global__ void __launch_bounds__(kBX * TY) k_pre_tracer_h1(Dev d, Range R, PreC
   }
 }
 
+// ---- j-marching form of k_pre_tracer_h1 (Params::h_jc): a block of 64 x 4
+// threads walks a 64-wide strip through jc rows of one level, 4 rows per
+// step.  The windows (masks, FlxU/FlxV, each tracer) live in an 8-row LDS ring
+// (AccTR): each step brings in only the 4 rows the next tile needs beyond the
+// ones already there, loaded into registers while the current tile computes
+// (with the next tile's lane inputs), so every window row is read from HBM
+// once per strip instead of twice (the 64 x 4 tiles' 4-row j-halo: 8 window
+// rows per 4 tile rows).  Same expressions, same order: bit-identical. ----
+template <int NTT>
+struct TracerRing {
+  double UM[kRingH * kUVW], VM[kRingH * kUVW], FU[kRingH * kUVW], FV[kRingH * kUVW], T[NTT][kRingH * kUVW];
+};
+// window rows [r0, r0 + nr) of the ring fields: entry q of the row block is
+// register m of thread tid (q = tid + m*256)
+template <int NTT, int NR>
+struct TracerRows {
+  double um[NR], vm[NR], fu[NR], fv[NR], t[NTT][NR];
+  __device__ __forceinline__ void load(const Bounds& b, const Fields& F, int tid, int ib, int r0, int nr, long kk,
+                                       long tlev) {
+#pragma unroll
+    for (int m = 0; m < NR; m++) {
+      const int q = tid + m * kBX * kBY;
+      const int i = ib + q % kUVW, j = r0 + q / kUVW;
+      const bool ok = q < nr * kUVW && i >= -1 && i <= b.Lm + 2 && j >= -1 && j <= b.Mm + 2;
+      const long o = ok ? IJ(b, i, j) : 0;
+      um[m] = ok ? F.umask[o] : 0.0;
+      vm[m] = ok ? F.vmask[o] : 0.0;
+      fu[m] = ok ? F.FlxU[o + kk] : 0.0;
+      fv[m] = ok ? F.FlxV[o + kk] : 0.0;
+#pragma unroll
+      for (int t = 0; t < NTT; t++) this->t[t][m] = ok ? F.t[tlev + (long)t * 3 * b.n3 + o + kk] : 0.0;
+    }
+  }
+  __device__ __forceinline__ void store(TracerRing<NTT>& W, int tid, int r0, int nr, int jb) const {
+#pragma unroll
+    for (int m = 0; m < NR; m++) {
+      const int q = tid + m * kBX * kBY;
+      if (q < nr * kUVW) {
+        const int s = (q % kUVW) + ((r0 + q / kUVW - jb) & (kRingH - 1)) * kUVW;
+        W.UM[s] = um[m]; W.VM[s] = vm[m]; W.FU[s] = fu[m]; W.FV[s] = fv[m];
+#pragma unroll
+        for (int t = 0; t < NTT; t++) W.T[t][s] = this->t[t][m];
+      }
+    }
+  }
+};
+template <int NTT, bool kHB>
+__global__ void __launch_bounds__(kBX * kBY) k_pre_tracer_hj(Dev d, Range R, PreCoef c, int nstp, int nnew, int nrhs,
+                                                           int jc) {
+  const uint3 bI = xcd_tile();
+  __shared__ TracerRing<NTT> W;
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const int k = 1 + (int)bI.z, indx = 3 - nstp;
+  const int i0 = R.i0 + (int)bI.x * kBX, jc0 = R.j0 + (int)bI.y * jc;
+  const int jend = min(jc0 + jc - 1, R.j1);
+  const int ib = i0 - 2, jb = jc0 - 2;
+  const long kk = (long)(k - 1) * b.n2, n2 = b.n2, tlev = (long)(nrhs - 1) * b.n3;
+  const int tid = threadIdx.x + kBX * threadIdx.y;
+  constexpr int NT = kBX * kBY;
+  constexpr int NR0 = (kRingH * kUVW + NT - 1) / NT, NR4 = (kBY * kUVW + NT - 1) / NT;
+  // the lane's own inputs of tile row j (hz_bak_fwd's, pre_step3d4S.F:136-148, and the time levels)
+  struct Lane {
+    double fu0, fu1, fv0, fv1, we1, wi1, we0, wi0, hbo, pm, pn, hzo, ts[NTT], ti[NTT];
+  };
+  const int i = i0 + (int)threadIdx.x;
+  auto load_lane = [&](Lane& L, int j) {
+    const bool act = i <= R.i1 && j <= jend;
+    const bool formed = kHB && act && i >= b.istr && j >= b.jstr;
+    const long ij = act ? IJ(b, i, j) : IJ(b, R.i0, R.j0), o = ij + kk, w = ij + (long)k * n2;
+    L.fu0 = L.fu1 = L.fv0 = L.fv1 = L.we1 = L.wi1 = L.we0 = L.wi0 = L.hbo = 0.0;
+    if (formed) {
+      L.hbo = F.c3[o];
+    } else {
+      L.fu0 = F.FlxU[o]; L.fu1 = F.FlxU[o + 1]; L.fv0 = F.FlxV[o]; L.fv1 = F.FlxV[o + b.nx2];
+      L.we1 = F.We[w]; L.wi1 = F.Wi[w]; L.we0 = F.We[w - n2]; L.wi0 = F.Wi[w - n2];
+    }
+    L.pm = F.pm[ij]; L.pn = F.pn[ij]; L.hzo = F.Hz[o];
+#pragma unroll
+    for (int t = 0; t < NTT; t++) {
+      const long tb = (long)t * 3 * b.n3;
+      L.ts[t] = F.t[(long)(nstp - 1) * b.n3 + tb + o];
+      L.ti[t] = F.t[(long)(indx - 1) * b.n3 + tb + o];
+    }
+  };
+  // prologue: the first tile's window (8 rows) and lane inputs
+  Lane L;
+  {
+    TracerRows<NTT, NR0> X;
+    X.load(b, F, tid, ib, jb, kRingH, kk, tlev);
+    load_lane(L, jc0 + (int)threadIdx.y);
+    X.store(W, tid, jb, kRingH, jb);
+  }
+  __syncthreads();
+  const AccTR a0{nullptr, W.UM, W.VM, W.FU, W.FV, ib, jb};
+  for (int j0 = jc0; j0 <= jend; j0 += kBY) {
+    const bool more = j0 + kBY <= jend;
+    TracerRows<NTT, NR4> X;
+    Lane Ln;
+    if (more) {   // the next tile's 4 new window rows and lane inputs, in flight during this tile
+      X.load(b, F, tid, ib, j0 + kBY + 2, kBY, kk, tlev);
+      load_lane(Ln, j0 + kBY + (int)threadIdx.y);
+    }
+    const int j = j0 + (int)threadIdx.y;
+    const bool act = i <= R.i1 && j <= jend;
+    const bool in = act && i >= b.istr && j >= b.jstr;
+    if (act) {
+      const long ij = IJ(b, i, j), o = ij + kk;
+      double hb;
+      if (kHB && in) {
+        hb = L.hbo;
+      } else {
+        const double cff = 0.5 * c.dtau;
+        const double FlxDiv = cff * L.pm * L.pn * (L.fu1 - L.fu0 + L.fv1 - L.fv0 + L.we1 + L.wi1 - L.we0 - L.wi0);
+        hb = L.hzo + FlxDiv;
+        const double hf = L.hzo - FlxDiv;
+        F.c2[o] = hf;  // Hz_fwd, Hz_bak kept for the column solves (range istr-1.., jstr-1..)
+        F.c3[o] = hb;
+      }
+      if (in) {
+        const double hz = L.hzo;
+#pragma unroll
+        for (int t = 0; t < NTT; t++) {
+          const int itrc = t + 1;
+          AccTR a = a0;
+          a.T = W.T[t];
+          double FX0 = tracer_fx(b, a, i, j, false), FX1 = tracer_fx(b, a, i + 1, j, false);
+          double FE0 = tracer_fe(b, a, i, j, false), FE1 = tracer_fe(b, a, i, j + 1, false);
+          if (d.p.nriv > 0) {   // river inflow faces (compute_horiz_tracer_fluxes.h:217-246)
+            river_tracer_flux(d, 0, i, j, k, itrc, FX0); river_tracer_flux(d, 0, i + 1, j, k, itrc, FX1);
+            river_tracer_flux(d, 1, i, j, k, itrc, FE0); river_tracer_flux(d, 1, i, j + 1, k, itrc, FE1);
+          }
+          const long tb = (long)t * 3 * b.n3;
+          const double tsk = L.ts[t];
+          F.t[(long)(nnew - 1) * b.n3 + tb + o] =
+              hb * (c.cf_stp * tsk + c.cf_bak * L.ti[t]) - c.dtau * L.pm * L.pn * (FX1 - FX0 + FE1 - FE0);
+          F.t[(long)(indx - 1) * b.n3 + tb + o] = hz * tsk;
+        }
+      }
+    }
+    if (!more) break;
+    __syncthreads();   // this tile's reads of the 4 oldest rows are done
+    X.store(W, tid, j0 + kBY + 2, kBY, jb);
+    L = Ln;
+    __syncthreads();
+  }
+}
+
 // ---- tracers, vertical part per column: spline advection on t(nrhs), then
 // implicit diffusion with Wi up-winding on Hz_fwd (LDS slots A, B). ----
 template <class C>
@@ -635,6 +783,7 @@ __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_pre_uv_seg(Dev d, R
   const SegSpan sg = seg_span(N);
   SegCol col;
   seg_uv_col(d, R, bI, sg, col);
+  if (col.idle) return;   // uniform over the block
   const int dir = col.dir;
   const bool act = col.act;
   const long n2 = b.n2, ij = IJ(b, col.i, col.j), s = dir == 0 ? 1 : b.nx2;
@@ -778,7 +927,18 @@ void launch_pre_step3d(const Dev& d, hipStream_t s, const Tlev& t, bool uv_done,
   hb_done = hb_done && d.p.hoist && b.NT <= 2;
   Range RI{b.istr, b.iend, b.jstr, b.jend};
   Range RH{b.istr - 1, b.iend, b.jstr - 1, b.jend};
-  if (d.p.hoist && b.NT == 2 && d.p.h_ty == 8) {
+  if (d.p.hoist && d.p.h_jc > 0 && (b.NT == 1 || b.NT == 2)) {
+    const dim3 g = grid3_jc(RH, b.N, d.p.h_jc), bs(kBX, kBY);
+    const int jc = d.p.h_jc;
+    if (b.NT == 2 && hb_done)
+      hipLaunchKernelGGL((k_pre_tracer_hj<2, true>), g, bs, 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs, jc);
+    else if (b.NT == 2)
+      hipLaunchKernelGGL((k_pre_tracer_hj<2, false>), g, bs, 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs, jc);
+    else if (hb_done)
+      hipLaunchKernelGGL((k_pre_tracer_hj<1, true>), g, bs, 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs, jc);
+    else
+      hipLaunchKernelGGL((k_pre_tracer_hj<1, false>), g, bs, 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs, jc);
+  } else if (d.p.hoist && b.NT == 2 && d.p.h_ty == 8) {
     if (hb_done)
       hipLaunchKernelGGL((k_pre_tracer_h1<2, 8, true>), grid3_ty(RH, b.N, 8), dim3(kBX, 8), 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs);
     else
@@ -813,7 +973,7 @@ void launch_pre_step3d(const Dev& d, hipStream_t s, const Tlev& t, bool uv_done,
   dim3 gu = gridc_of(RI);
   gu.z = 2;
   if (d.p.colseg) {
-    const dim3 gs = seg_grid_of(RI, 2, d.p.seg_jrows), bs(kCX, seg_waves(b.N), d.p.seg_jrows);
+    const dim3 gs = seg_uv_grid(d, RI, d.p.seg_jrows), bs(kCX, seg_waves(b.N), d.p.seg_jrows);
     ktimer_mark(s, kTimedPreUvSeg, 0);
     if (d.p.preuv_lds && d.p.uv_adv && t.nrhs == t.nstp)
       hipLaunchKernelGGL(k_pre_uv_seg<true>, gs, bs, pre_uv_seg_lds_bytes(bs.x * bs.y * bs.z), s, d, RI, c, t.nstp,

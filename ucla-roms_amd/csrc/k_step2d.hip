@@ -607,7 +607,7 @@ __global__ void k_s2d_edges(Dev d, FBCoef c, int phase) {
   const Fields& F = d.f;
   const long n2 = b.n2, kn = (long)(c.knew - 1) * n2, ksl = (long)(c.kstp - 1) * n2;
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  const int L = b.nx2 > b.Mm + 4 ? b.nx2 : b.Mm + 4;  // edge lanes per side
+  const int L = b.Lm + 4 > b.Mm + 4 ? b.Lm + 4 : b.Mm + 4;  // edge lanes per side
   const int side = p / L, q = p - side * L;
   if (side > 3) return;
   double* ub = F.ubar + kn;
@@ -893,7 +893,7 @@ void launch_step2d(const Dev& d, hipStream_t s, const Tlev& t, const double* w1,
     else if (t.iif == t.nfast) ktimer_mark(s, kTimedS2dFb, 1, t.nfast);
   }
   if (closed && !fold) {
-    const int L = b.nx2 > b.Mm + 4 ? b.nx2 : b.Mm + 4;
+    const int L = b.Lm + 4 > b.Mm + 4 ? b.Lm + 4 : b.Mm + 4;
     for (int ph = 0; ph < 4; ph++) {
       if (ph == 2 && !d.p.obc) continue;
       hipLaunchKernelGGL(k_s2d_edges, dim3(ph == 2 ? 1 : (4 * L + 255) / 256), dim3(ph == 2 ? 64 : 256), 0, s, d, c, ph);

@@ -269,6 +269,7 @@ __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_uv1_seg(Dev d, Rang
   const SegSpan sg = seg_span(N);
   SegCol col;
   seg_uv_col(d, R, bI, sg, col);
+  if (col.idle) return;   // uniform over the block
   const int ncol = kSegCW * (int)blockDim.z;
   const int dir = col.dir;
   const bool act = col.act;
@@ -426,7 +427,7 @@ void launch_step3d_uv1(const Dev& d, hipStream_t s, const Tlev& t, bool uv_done)
   if ((d.p.colreg & 1) && b.N == 50)
     hipLaunchKernelGGL(k_uv1_reg<50>, g, dim3(kCX), col_lds_bytes(1, 50), s, d, R, t.nnew, t.nrhs);
   else if (d.p.colseg) {
-    const dim3 gs = seg_grid_of(R, 2, d.p.seg_jrows), bs(kCX, seg_waves(b.N), d.p.seg_jrows);
+    const dim3 gs = seg_uv_grid(d, R, d.p.seg_jrows), bs(kCX, seg_waves(b.N), d.p.seg_jrows);
     ktimer_mark(s, kTimedUv1Seg, 0);
     if (d.p.uv1_lds && d.p.uv_adv)
       hipLaunchKernelGGL(k_uv1_seg<true>, gs, bs, uv1_seg_lds_bytes(bs.x * bs.y * bs.z), s, d, R, t.nnew, t.nrhs);

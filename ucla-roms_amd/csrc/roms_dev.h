@@ -1,11 +1,15 @@
 // roms_dev.h -- device-side state and index helpers of the MI355X ROMS hot path.
 //
 // Every array keeps the reference's Fortran layout (ocean_vars.F:68-116):
-// horizontal extent (-1:Lm+2, -1:Mm+2), i fastest, so element (i,j) sits at
-// (i+1) + (j+1)*(Lm+4); rho-point 3-D arrays stack N levels (1:N), w-point
-// arrays N+1 levels (0:N); u,v add 3 time levels, zeta/ubar/vbar 4, t(...,3,NT).
-// Bulk host<->device copies therefore need no transpose, and a wavefront of 64
-// consecutive i at fixed (j,k) reads one contiguous 512-byte run.
+// horizontal extent (-1:Lm+2, -1:Mm+2), i fastest; rho-point 3-D arrays stack
+// N levels (1:N), w-point arrays N+1 levels (0:N); u,v add 3 time levels,
+// zeta/ubar/vbar 4, t(...,3,NT).  On the device a row j holds nx2 doubles:
+// Lm+4 rounded up to kRowAlign (128 B), and every array's base is shifted by
+// kAlignOff doubles, so element (i,j) sits at (i+1) + (j+1)*nx2 and i = 1 of
+// every row and level starts a 128-B line: a wavefront of 64 consecutive i
+// from i = 1 reads exactly four lines (at nx2 = Lm+4 the rows drift 32 B per
+// row against the lines and most such runs touch five).  Host copies re-pitch
+// the rows (roms_shim.cpp); no transpose anywhere.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstddef>
@@ -14,11 +18,13 @@
 namespace roms {
 
 constexpr int kMaxFast = 288;  // coupling.F:19, weight(2,288)
+constexpr int kRowAlign = 16;  // device row pitch granule: 16 doubles = one 128-B line
+constexpr int kAlignOff = 14;  // base shift: element i = 1 (index 2 of a row) on a line start
 
 // Loop bounds of the single tile that covers one rank's subdomain
 // (compute_tile_bounds.h, compute_auxiliary_bounds.h, compute_extended_bounds.h).
 struct Bounds {
-  int Lm, Mm, N, NT, nTS, nx2;
+  int Lm, Mm, N, NT, nTS, nx2;   // nx2: device row pitch (>= Lm+4)
   long n2, n3, n3w;
   int istr, iend, jstr, jend;
   int istrU, istrR, iendR, jstrV, jstrR, jendR;   // auxiliary
@@ -50,6 +56,7 @@ struct Params {
   int chain_dirz;   // chain kernels (set_HUV1, uv2): one direction per block (ROMS_GPU_CHAIN_DIRZ=0: both in turn)
   int prs_fuse_uv;  // whole steps: horizontal momentum r.h.s. inside prsgrd (ROMS_GPU_PRS_UV=0: separate)
   int h_ty;       // tile rows of the hoisted horizontal kernels: 4 or 8 (ROMS_GPU_HTY)
+  int h_jc;       // rows per block of the j-marching horizontal kernels (multiple of 4; ROMS_GPU_HJC, 0: 64 x h_ty tiles)
   int prs_ty;     // tile rows of k_prsgrd_uv: 4 or 8 (ROMS_GPU_PRS_TY)
   int visc_stg;   // visc3d: raw u/v/Hz windows staged in LDS per level (default; ROMS_GPU_VISC_STG=0: per-point loads)
   int t3dmix_stg; // t3dmix (two tracers): Hz/T/S windows staged in LDS per level (default; ROMS_GPU_T3DMIX_STG=0: per-point loads)
@@ -61,6 +68,7 @@ struct Params {
   int omega_hb;   // the predictor's omega forms pre_step3d's Hz_bak/Hz_fwd (ROMS_GPU_OMEGA_HB=0: pre_step3d does)
   int preuv_lds;  // k_pre_uv_seg: u(indx) stored and u(nstp)/u(indx) combined in the spline phase (ROMS_GPU_PREUV_LDS=0: reloads)
   int seg_jrows;  // rows j per block of the momentum segment solvers (1..kSegJMax; ROMS_GPU_SEG_JROWS)
+  int seg_vtile;  // v columns of the momentum segment solvers on 16 x 4 tiles per wavefront (ROMS_GPU_SEG_VTILE=0: rows of 64)
   int npip;       // pipe_frc.F: number of pipes (0: pipe_source off)
   int nriv, nrivf;  // river_frc.F: number of rivers (0: river_source off), river faces
   int curvgrid;   // CURVGRID && UV_ADV: curvature terms (compute_horiz_rhs_uv_terms.h:8-11)

@@ -24,7 +24,9 @@ namespace {
 
 struct FieldDesc {
   double* d = nullptr;
-  long count = 0;
+  long count = 0;        // elements in the device layout (rows nx2 apart)
+  long hcount = 0;       // elements in the host (reference) layout: what the ABI exchanges
+  bool planar = false;   // (i,j)-planes of the horizontal grid (rows to re-pitch); Cs_*/boundary arrays not
   double* host = nullptr;
   long host_count = 0;
 };
@@ -77,6 +79,14 @@ struct Ctx {
   std::map<double*, double*> guard_base;
   double* small = nullptr;   // shim_scratch_small
   long small_n = 0;
+  // Device row pitch (roms_dev.h): rows of nx2 = Lm+4 rounded up to 16
+  // doubles (128 B), every array's base shifted by kAlignOff so that i = 1 of
+  // every row starts a 128-B line.  Host copies re-pitch rows through a
+  // device staging buffer (ROMS_GPU_PITCH=0: the host layout on the device).
+  long off = 0;
+  Bounds hb{};               // the host layout's Bounds (nx2 = Lm+4)
+  double* stage = nullptr;
+  long stage_n = 0;
 };
 // One context per host thread: a process normally drives one GPU/subdomain
 // from one thread; tests drive several subdomains from threads of one process.
@@ -152,12 +162,12 @@ int post_launch() {
   return 0;
 }
 
-Bounds make_bounds(const roms_dims& D) {
+Bounds make_bounds(const roms_dims& D, int pitch) {
   Bounds b{};
   b.Lm = D.Lm; b.Mm = D.Mm; b.N = D.N; b.NT = D.NT;
   b.nTS = 1;
-  b.nx2 = D.Lm + 4;
-  b.n2 = (long)(D.Lm + 4) * (D.Mm + 4);
+  b.nx2 = pitch;
+  b.n2 = (long)pitch * (D.Mm + 4);
   b.n3 = b.n2 * D.N;
   b.n3w = b.n2 * (D.N + 1);
   b.istr = 1; b.iend = D.Lm; b.jstr = 1; b.jend = D.Mm;
@@ -181,6 +191,9 @@ Bounds make_bounds(const roms_dims& D) {
   b.jendE = (D.ns_periodic || D.north_exchng) ? b.jend + 2 : b.jend + 1;
   return b;
 }
+
+// boundary arrays and the vertical stretching curves are not (i,j) planes
+bool planar_field(int id) { return !(id == ROMS_Cs_w || id == ROMS_Cs_r || (id >= ROMS_zeta_west && id <= ROMS_t_north)); }
 
 long field_count(int id, const Bounds& b) {
   const long n2 = b.n2, n3 = b.n3, n3w = b.n3w;
@@ -250,15 +263,16 @@ double* dev_base(double* p) {
 // zero-initialised device array of n doubles (guard bands when g.guard)
 hipError_t dev_alloc(double*& p, long n) {
   const long G = g.guard ? 4096 : 0;
+  const long pad = g.off ? kRowAlign : 0;   // room for the alignment shift (hipMalloc is 256-B aligned)
   double* base = nullptr;
-  hipError_t e = hipMalloc(&base, (size_t)(n + 2 * G) * sizeof(double));
+  hipError_t e = hipMalloc(&base, (size_t)(n + 2 * G + pad) * sizeof(double));
   if (e != hipSuccess) return e;
   if (G) {
-    e = hipMemsetD32((hipDeviceptr_t)base, 0x7FF87FF8, (size_t)(n + 2 * G) * 2);   // NaN bit pattern
+    e = hipMemsetD32((hipDeviceptr_t)base, 0x7FF87FF8, (size_t)(n + 2 * G + pad) * 2);   // NaN bit pattern
     if (e != hipSuccess) return e;
   }
-  p = base + G;
-  if (G) g.guard_base[p] = base;
+  p = base + G + g.off;
+  if (G || g.off) g.guard_base[p] = base;
   // The library's kernels run on a non-blocking stream, which does not wait
   // for work on the null stream: the zero fill must have landed before the
   // first kernel reads the array, or it may see what a previous model left in
@@ -271,6 +285,7 @@ void free_all() {
   io_free();
   frc_free();
   if (g.small) { (void)hipFree(g.small); g.small = nullptr; g.small_n = 0; }
+  if (g.stage) { (void)hipFree(g.stage); g.stage = nullptr; g.stage_n = 0; }
   for (hipEvent_t e : g.ev) (void)hipEventDestroy(e);
   g.ev.clear();
   halo_free(g.halo);
@@ -311,6 +326,9 @@ Tlev to_tlev(const roms_tlev* t) {
     if (on_) { (void)hipEventRecord(g.ev[g.nev + 1], s); g.nev += 2; }      \
   } while (0)
 
+// host <-> device layout copies (defined below)
+hipError_t field_h2d(int id, double* dev, const double* host);
+hipError_t rows_h2d(double* dev, const double* host, long rows);
 }  // namespace
 int roms::shim_enter(ShimState& S, bool read_only) {
   const int rho_keep = g.rho_slot;
@@ -321,6 +339,9 @@ int roms::shim_enter(ShimState& S, bool read_only) {
 }
 void roms::shim_set_error(const std::string& e) { g.err = e; }
 double* roms::shim_field(int id) { return (id >= 0 && id < ROMS_NFIELDS) ? g.f[id].d : nullptr; }
+long roms::shim_field_dev_count(int id) { return (id >= 0 && id < ROMS_NFIELDS) ? g.f[id].count : -1; }
+hipError_t roms::shim_field_h2d(int id, double* dev, const double* host) { return field_h2d(id, dev, host); }
+hipError_t roms::shim_rows_h2d(double* dev, const double* host, long rows) { return rows_h2d(dev, host, rows); }
 double* roms::shim_scratch_small(long n) {
   if (g.small_n < n) {
     if (g.small) { (void)hipStreamSynchronize(g.s); (void)hipFree(g.small); g.small = nullptr; }
@@ -401,6 +422,62 @@ void enqueue_step(roms_tlev* t, bool rho_current, bool store_huv) {
 
 }  // namespace
 
+namespace {
+// ---- host (rows of Lm+4) <-> device (rows of nx2) copies, blocking on the
+// library stream.  Equal pitches: one DMA.  Otherwise the compact rows go
+// through the device staging buffer and one row-copy kernel re-pitches them
+// (a strided hipMemcpy2D from pageable memory would move row by row). ----
+double* stage_get(long n) {
+  if (g.stage_n < n) {
+    if (g.stage) { (void)hipStreamSynchronize(g.s); (void)hipFree(g.stage); g.stage = nullptr; g.stage_n = 0; }
+    if (hipMalloc(&g.stage, (size_t)n * sizeof(double)) != hipSuccess) return nullptr;
+    g.stage_n = n;
+  }
+  return g.stage;
+}
+hipError_t rows_h2d(double* dev, const double* host, long rows) {
+  const Bounds& b = g.d.b;
+  const long hx = g.hb.nx2, n = rows * hx;
+  if (b.nx2 == hx) return copy_on(dev, host, (size_t)n * sizeof(double), hipMemcpyHostToDevice, g.s);
+  double* st = stage_get(n);
+  if (!st) return hipErrorOutOfMemory;
+  hipError_t e = hipMemcpyAsync(st, host, (size_t)n * sizeof(double), hipMemcpyHostToDevice, g.s);
+  if (e != hipSuccess) return e;
+  launch_rows_copy(dev, b.nx2, st, hx, hx, rows, g.s);
+  return hipStreamSynchronize(g.s);
+}
+hipError_t rows_d2h(double* host, const double* dev, long rows) {
+  const Bounds& b = g.d.b;
+  const long hx = g.hb.nx2, n = rows * hx;
+  if (b.nx2 == hx) return copy_on(host, dev, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, g.s);
+  double* st = stage_get(n);
+  if (!st) return hipErrorOutOfMemory;
+  launch_rows_copy(st, hx, dev, b.nx2, hx, rows, g.s);
+  hipError_t e = hipMemcpyAsync(host, st, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, g.s);
+  return e != hipSuccess ? e : hipStreamSynchronize(g.s);
+}
+hipError_t field_h2d(int id, double* dev, const double* host) {
+  const FieldDesc& f = g.f[id];
+  if (!f.planar) return copy_on(dev, host, (size_t)f.hcount * sizeof(double), hipMemcpyHostToDevice, g.s);
+  return rows_h2d(dev, host, f.hcount / g.hb.nx2);
+}
+hipError_t field_d2h(int id, double* host, const double* dev) {
+  const FieldDesc& f = g.f[id];
+  if (!f.planar) return copy_on(host, dev, (size_t)f.hcount * sizeof(double), hipMemcpyDeviceToHost, g.s);
+  return rows_d2h(host, dev, f.hcount / g.hb.nx2);
+}
+// a host-layout int / double plane array as a device-layout host vector
+template <class T>
+std::vector<T> to_dev_layout(const T* h, long planes) {
+  const Bounds& b = g.d.b;
+  const long hx = g.hb.nx2, rows = (long)(b.Mm + 4) * planes;
+  std::vector<T> v((size_t)(b.n2 * planes), T(0));
+  for (long r = 0; r < rows; r++) std::memcpy(v.data() + r * b.nx2, h + r * hx, (size_t)hx * sizeof(T));
+  return v;
+}
+
+}  // namespace
+
 extern "C" {
 
 int roms_gpu_abi_version(void) { return ROMS_GPU_ABI_VERSION; }
@@ -425,7 +502,7 @@ int roms_gpu_selftest_zero_fill(long n, int chunks, long* bad) {
     (void)hipStreamSynchronize(g.s);
     for (double*& p : a) {
       if (!p) continue;
-      if (guarded && g.guard) {
+      if (guarded && (g.guard || g.off)) {
         (void)hipFree(dev_base(p));
         g.guard_base.erase(p);
       } else {
@@ -492,8 +569,17 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
   g.have_volume = false;
   g.area = g.volume = 0.0;
   g.d = Dev{};
-  g.d.b = make_bounds(*dims);
-  g.d.b.nTS = cfg->salinity ? 2 : 1;
+  {
+    // device row pitch: Lm+4 rounded up to 128 B, base shifted so that i = 1
+    // starts a line (roms_dev.h); ROMS_GPU_PITCH=0 keeps the host layout
+    const char* e = getenv("ROMS_GPU_PITCH");
+    const bool pad = !(e && e[0] == '0');
+    const int hx = dims->Lm + 4;
+    g.off = pad ? kAlignOff : 0;
+    g.d.b = make_bounds(*dims, pad ? (hx + kRowAlign - 1) / kRowAlign * kRowAlign : hx);
+    g.hb = make_bounds(*dims, hx);
+  }
+  g.d.b.nTS = g.hb.nTS = cfg->salinity ? 2 : 1;
   Params& P = g.d.p;
   {
     const int m = cfg->lmd_mixing, base = ROMS_LMD_MIXING | ROMS_LMD_KPP | ROMS_LMD_BKPP;
@@ -627,6 +713,16 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     P.h_ty = (e && atoi(e) == 8) ? 8 : 4;
   }
   {
+    // j-marching per-level horizontal kernels: rows per block (ROMS_GPU_HJC;
+    // 0 = off, the default: k_pre_tracer_hj measured slower at C3, 12.15 ->
+    // 12.65 ms per pre_step3d, r4c: the 64 x 4 tiles' j-halo rows are mostly
+    // L2 hits already (PMC 16.2 passes against 14), and the ring's in-flight
+    // rows and lanes halve the waves per SIMD)
+    const char* e = getenv("ROMS_GPU_HJC");
+    P.h_jc = 0;
+    if (e && atoi(e) >= 0) P.h_jc = atoi(e) / 4 * 4;
+  }
+  {
     const char* e = getenv("ROMS_GPU_PRS_TY");
     P.prs_ty = (e && atoi(e) == 8) ? 8 : 4;
   }
@@ -652,6 +748,10 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
   {
     const char* e = getenv("ROMS_GPU_HOIST");
     P.hoist = !(e && e[0] == '0');
+  }
+  {
+    const char* e = getenv("ROMS_GPU_SEG_VTILE");
+    P.seg_vtile = !(e && e[0] == '0');
   }
   P.seg_jrows = kSegJMax < 2 ? kSegJMax : 2;
   {
@@ -686,6 +786,8 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     CHECK_HIP(dev_alloc(p, n));
     g.f[id].d = p;
     g.f[id].count = n;
+    g.f[id].hcount = field_count(id, g.hb);
+    g.f[id].planar = planar_field(id);
     *field_slot(g.d.f, id) = p;
   }
   auto scratch = [&](double*& p, long n) -> int {
@@ -718,8 +820,10 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
   CHECK_HIP(hipHostMalloc(&g.h_diag, 8 * sizeof(double), hipHostMallocDefault));
   CHECK_HIP(hipMalloc(&g.d_diag, 8 * sizeof(double)));
   if (comm != nullptr) {
-    const HaloPlan plan = halo_plan(dims->Lm, dims->Mm, dims->np_xi, dims->np_eta, dims->inode, dims->jnode,
-                                    dims->ew_periodic, dims->ns_periodic);
+    HaloPlan plan = halo_plan(dims->Lm, dims->Mm, dims->np_xi, dims->np_eta, dims->inode, dims->jnode,
+                              dims->ew_periodic, dims->ns_periodic);
+    plan.g.nx2 = b.nx2;   // the device row pitch: pack/unpack index the device arrays
+    plan.g.n2 = b.n2;
     const int r = halo_setup(g.halo, (RomsComm*)comm, plan, 8 * (dims->N + 1), g.err);
     if (r) return r;
     g.d.halo = &g.halo;
@@ -748,13 +852,13 @@ int roms_gpu_finalize(void) {
 
 long roms_gpu_field_size(int id) {
   if (!g.inited || id < 0 || id >= ROMS_NFIELDS) return -1;
-  return g.f[id].count;
+  return g.f[id].hcount;
 }
 
 int roms_gpu_register(int id, double* host, long count) {
   REQUIRE_INIT();
   if (id < 0 || id >= ROMS_NFIELDS) { g.err = "roms_gpu_register: bad field id"; return -1; }
-  if (count != g.f[id].count) { g.err = "roms_gpu_register: size mismatch for field"; return -1; }
+  if (count != g.f[id].hcount) { g.err = "roms_gpu_register: size mismatch for field"; return -1; }
   g.f[id].host = host;
   g.f[id].host_count = count;
   return 0;
@@ -780,10 +884,7 @@ static int xfer(int id, bool up) {
   if (!g.f[id].host) { g.err = "field not registered"; return -1; }
   if (!up && !hzuv_readable(id)) return -5;
   if (up && (id == ROMS_Hz_u || id == ROMS_Hz_v)) g.hzuv_valid = true;
-  const size_t nb = (size_t)g.f[id].count * sizeof(double);
-  if (up) CHECK_HIP(hipMemcpyAsync(g.f[id].d, g.f[id].host, nb, hipMemcpyHostToDevice, g.s));
-  else CHECK_HIP(hipMemcpyAsync(g.f[id].host, g.f[id].d, nb, hipMemcpyDeviceToHost, g.s));
-  CHECK_HIP(hipStreamSynchronize(g.s));
+  CHECK_HIP(up ? field_h2d(id, g.f[id].d, g.f[id].host) : field_d2h(id, g.f[id].host, g.f[id].d));
   return 0;
 }
 int roms_gpu_upload(int id) { REQUIRE_INIT(); return xfer(id, true); }
@@ -791,18 +892,16 @@ int roms_gpu_download(int id) { REQUIRE_INIT_RO(); return xfer(id, false); }
 
 int roms_gpu_copy_in(int id, const double* src, long count) {
   REQUIRE_INIT();
-  if (id < 0 || id >= ROMS_NFIELDS || count != g.f[id].count) { g.err = "roms_gpu_copy_in: bad field/size"; return -1; }
+  if (id < 0 || id >= ROMS_NFIELDS || count != g.f[id].hcount) { g.err = "roms_gpu_copy_in: bad field/size"; return -1; }
   if (id == ROMS_Hz_u || id == ROMS_Hz_v) g.hzuv_valid = true;
-  CHECK_HIP(hipMemcpyAsync(g.f[id].d, src, (size_t)count * sizeof(double), hipMemcpyHostToDevice, g.s));
-  CHECK_HIP(hipStreamSynchronize(g.s));
+  CHECK_HIP(field_h2d(id, g.f[id].d, src));
   return 0;
 }
 int roms_gpu_copy_out(int id, double* dst, long count) {
   REQUIRE_INIT_RO();
-  if (id < 0 || id >= ROMS_NFIELDS || count != g.f[id].count) { g.err = "roms_gpu_copy_out: bad field/size"; return -1; }
+  if (id < 0 || id >= ROMS_NFIELDS || count != g.f[id].hcount) { g.err = "roms_gpu_copy_out: bad field/size"; return -1; }
   if (!hzuv_readable(id)) return -5;
-  CHECK_HIP(hipMemcpyAsync(dst, g.f[id].d, (size_t)count * sizeof(double), hipMemcpyDeviceToHost, g.s));
-  CHECK_HIP(hipStreamSynchronize(g.s));
+  CHECK_HIP(field_d2h(id, dst, g.f[id].d));
   REQUIRE_HALO_OK();
   return 0;
 }
@@ -875,7 +974,7 @@ int roms_gpu_set_pipe_frc(int npip, const int* pipe_idx, const double* pipe_flx,
     return -1;
   }
   if (npip == 0) { g.d.p.npip = 0; return 0; }
-  for (long q = 0; q < b.n2; q++)
+  for (long q = 0; q < g.hb.n2; q++)
     if (pipe_idx[q] < 0 || pipe_idx[q] > npip) { g.err = "roms_gpu_set_pipe_frc: pipe_idx out of 0..npip"; return -1; }
   CHECK_HIP(hipStreamSynchronize(g.s));
   if (npip != g.d.p.npip || !F.pipe_idx) {
@@ -903,8 +1002,12 @@ int roms_gpu_set_pipe_frc(int npip, const int* pipe_idx, const double* pipe_flx,
       return -2;
     g.d.p.npip = npip;
   }
-  CHECK_HIP(copy_on(F.pipe_idx, pipe_idx, (size_t)b.n2 * sizeof(int), hipMemcpyHostToDevice, g.s));
-  CHECK_HIP(copy_on(F.pipe_flx, pipe_flx, (size_t)b.n2 * sizeof(double), hipMemcpyHostToDevice, g.s));
+  {
+    const std::vector<int> di = to_dev_layout(pipe_idx, 1);
+    const std::vector<double> df = to_dev_layout(pipe_flx, 1);
+    CHECK_HIP(copy_on(F.pipe_idx, di.data(), (size_t)b.n2 * sizeof(int), hipMemcpyHostToDevice, g.s));
+    CHECK_HIP(copy_on(F.pipe_flx, df.data(), (size_t)b.n2 * sizeof(double), hipMemcpyHostToDevice, g.s));
+  }
   CHECK_HIP(copy_on(F.pipe_prf, pipe_prf, (size_t)npip * b.N * sizeof(double), hipMemcpyHostToDevice, g.s));
   CHECK_HIP(copy_on(F.pipe_trc, pipe_trc, (size_t)npip * b.NT * sizeof(double), hipMemcpyHostToDevice, g.s));
   return 0;
@@ -945,7 +1048,7 @@ int roms_gpu_set_river_frc(int nriv, const double* riv_uflx, const double* riv_v
       const double* a = dir == 0 ? riv_uflx : riv_vflx;
       for (int j = -1; j <= b.Mm + 2; j++)
         for (int i = -1; i <= b.Lm + 2; i++) {
-          const double v = a[(i + 1) + (long)(j + 1) * b.nx2];
+          const double v = a[IJ(g.hb, i, j)];   // the host's layout
           if (!(std::fabs(v) > 1e-3)) continue;
           const long ir = std::lround(v / 10);
           if (ir < 1 || ir > nriv) { g.err = "roms_gpu_set_river_frc: river index nint(riv_flx/10) out of 1..nriv"; return -1; }
@@ -978,8 +1081,8 @@ int roms_gpu_set_river_frc(int nriv, const double* riv_uflx, const double* riv_v
     if (F.riv_face) { (void)hipFree(F.riv_face); F.riv_face = nullptr; }
     CHECK_HIP(hipMalloc(&F.riv_face, (faces.size() ? faces.size() : 1) * sizeof(int)));
     if (!faces.empty()) CHECK_HIP(copy_on(F.riv_face, faces.data(), faces.size() * sizeof(int), hipMemcpyHostToDevice, g.s));
-    CHECK_HIP(copy_on(F.riv_uflx, riv_uflx, (size_t)b.n2 * sizeof(double), hipMemcpyHostToDevice, g.s));
-    CHECK_HIP(copy_on(F.riv_vflx, riv_vflx, (size_t)b.n2 * sizeof(double), hipMemcpyHostToDevice, g.s));
+    CHECK_HIP(rows_h2d(F.riv_uflx, riv_uflx, b.Mm + 4));
+    CHECK_HIP(rows_h2d(F.riv_vflx, riv_vflx, b.Mm + 4));
     g.d.p.nrivf = (int)(faces.size() / 3);
     g.riv_maxidx = maxidx;
   }
@@ -1329,12 +1432,12 @@ static int grid_integrals() {
   CHECK_HIP(copy_on(pm.data(), g.d.f.pm, b.n2 * sizeof(double), hipMemcpyDeviceToHost, g.s));
   CHECK_HIP(copy_on(pn.data(), g.d.f.pn, b.n2 * sizeof(double), hipMemcpyDeviceToHost, g.s));
   CHECK_HIP(copy_on(rm.data(), g.d.f.rmask, b.n2 * sizeof(double), hipMemcpyDeviceToHost, g.s));
-  std::vector<double> dA(b.n2, 0.0), dV(b.n2, 0.0);
+  std::vector<double> dA(g.hb.n2, 0.0), dV(g.hb.n2, 0.0);   // the host layout pair_sum walks
   for (int j = 1; j <= b.Mm; j++)
     for (int i = 1; i <= b.Lm; i++) {
-      const long o = IJ(b, i, j);
-      dA[o] = rm[o] / (pm[o] * pn[o]);
-      dV[o] = dA[o] * h[o];
+      const long o = IJ(b, i, j), q = IJ(g.hb, i, j);
+      dA[q] = rm[o] / (pm[o] * pn[o]);
+      dV[q] = dA[q] * h[o];
     }
   const double loc[2] = {pair_sum(H, dA), pair_sum(H, dV)};
   const int nr = g.halo.comm ? comm_size(g.halo.comm) : 1;

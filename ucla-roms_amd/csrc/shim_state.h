@@ -45,5 +45,12 @@ int frc_step_prepare(hipStream_t s, const Dev& d, double dt, const roms_tlev& t,
 void frc_step_phase(const Dev& d, hipStream_t s, int phase, bool pot_tides);
 long frc_step_gen();
 double* shim_field(int field_id);          // device array of a field (nullptr if absent)
+long shim_field_dev_count(int field_id);   // elements of a field in the device layout (row pitch nx2)
+// host-layout field data (the ABI's, rows of Lm+4) into a device-layout
+// array of the field's shape, blocking on the library stream
+hipError_t shim_field_h2d(int field_id, double* dev, const double* host);
+hipError_t shim_rows_h2d(double* dev, const double* host, long rows);   // `rows` rows of Lm+4 -> nx2
+// dst[r*dpitch + c] = src[r*spitch + c], c < width, r < rows (device arrays; k_diag.hip)
+void launch_rows_copy(double* dst, long dpitch, const double* src, long spitch, long width, long rows, hipStream_t s);
 double* shim_scratch_small(long n);        // small device scratch owned by the context (>= n doubles)
 }  // namespace roms
