@@ -67,8 +67,11 @@ C3_L, C3_N, C3_DT, C3_DX = 1024, 100, 300.0, 2.0e3
 PRE_UV_SEG_PASSES = 14
 # k_prsgrd_uv in whole steps (the prsgrd ru/rv kernel with the horizontal
 # momentum r.h.s. of the following pre_step3d / step3d_uv1): z_r, rho1, qp1,
-# Hz, P; u, v(nrhs), FlxU, FlxV read; ru, rv written.
-PRSGRD_UV_PASSES = 11
+# Hz; u, v(nrhs), FlxU, FlxV read; ru, rv written.  The hydrostatic pressure
+# P it also reads is prsgrd's own work array (prsgrd.F:200-330 forms it in
+# the routine; here rho_eos's sweep stores it): not a model array, so it is
+# not counted -- the bytes it costs lower the fraction.
+PRSGRD_UV_PASSES = 10
 
 
 # set_HUV's Hz_u/Hz_v (set_depth.F:220,227) feed only extract_data.F; whole

@@ -26,6 +26,7 @@ struct ChainLane {
   int col, g;    // column in the wavefront's row, segment (0 = bottom)
   int i, j;      // the lane's column (unclamped)
   int lo, nk;    // first level of the segment and its number of levels
+  bool in;       // i >= R.i0: the aligned first tile's lanes left of the range store nothing
 };
 template <int KL>
 __device__ __forceinline__ ChainLane chain_lane(const Range& R, const uint3& bI, int N) {
@@ -33,14 +34,15 @@ __device__ __forceinline__ ChainLane chain_lane(const Range& R, const uint3& bI,
   const int l = (int)(threadIdx.x & 63u), w = (int)(threadIdx.x >> 6);
   c.col = l & (kChainCW - 1);
   c.g = l / kChainCW;
-  c.i = R.i0 + (int)bI.x * kChainCW + c.col;
+  c.i = tile_i0(R.i0) + (int)bI.x * kChainCW + c.col;
+  c.in = c.i >= R.i0;
   c.j = R.j0 + (int)bI.y * 4 + w;
   c.lo = 1 + c.g * KL;
   c.nk = max(0, min(N, c.lo + KL - 1) - c.lo + 1);
   return c;
 }
 inline dim3 chain_grid_of(const Range& R) {
-  return dim3((R.i1 - R.i0 + kChainCW) / kChainCW, (R.j1 - R.j0 + 4) / 4);
+  return dim3((R.i1 - tile_i0(R.i0) + kChainCW) / kChainCW, (R.j1 - R.j0 + 4) / 4);
 }
 // segment length for N levels: ceil(N / 4) rounded up to a compiled size
 inline int chain_kl(int N) {

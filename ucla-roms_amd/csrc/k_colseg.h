@@ -327,13 +327,14 @@ __device__ __forceinline__ void seg_uv_col(const Dev& d, const Range& R, const u
   const int jlo = c.dir == 1 ? (b.jstrV > R.j0 ? b.jstrV : R.j0) : R.j0;
   int iu, ju;
   if (c.dir == 1 && seg_vtile_on(d)) {
-    const int ntx = (R.i1 - R.i0 + kVTX) / kVTX, nty = (R.j1 - R.j0 + kVTY) / kVTY;
+    const int ti0 = tile_i0(R.i0);
+    const int ntx = (R.i1 - ti0 + kVTX) / kVTX, nty = (R.j1 - R.j0 + kVTY) / kVTY;
     const int t = (int)bI.x + (int)gridDim.x * (int)bI.y;
     c.idle = t >= ntx * nty;
-    iu = R.i0 + (t % ntx) * kVTX + sg.col % kVTX;
+    iu = ti0 + (t % ntx) * kVTX + sg.col % kVTX;
     ju = R.j0 + (t / ntx) * kVTY + sg.col / kVTX;
   } else {
-    iu = R.i0 + (int)bI.x * kSegCW + sg.col;
+    iu = tile_i0(R.i0) + (int)bI.x * kSegCW + sg.col;
     ju = R.j0 + (int)bI.y * (int)blockDim.z + sg.row;
     c.idle = R.j0 + (int)bI.y * (int)blockDim.z > R.j1;
   }
@@ -342,14 +343,14 @@ __device__ __forceinline__ void seg_uv_col(const Dev& d, const Range& R, const u
   c.j = ju < jlo ? jlo : (ju > R.j1 ? R.j1 : ju);
 }
 inline dim3 seg_grid_of(const Range& R, int nz, int jrows = 1) {
-  return dim3((R.i1 - R.i0 + kSegCW) / kSegCW, (R.j1 - R.j0 + jrows) / jrows, nz);
+  return dim3((R.i1 - tile_i0(R.i0) + kSegCW) / kSegCW, (R.j1 - R.j0 + jrows) / jrows, nz);
 }
 // the momentum kernels' grid: enough blocks in (x, y) for the u rows and for
 // the v tiles (seg_uv_col)
 inline dim3 seg_uv_grid(const Dev& d, const Range& R, int jrows) {
   dim3 g = seg_grid_of(R, 2, jrows);
   if (d.p.seg_vtile && kSegCW == kVTX * kVTY && jrows == 1) {
-    const long nvt = (long)((R.i1 - R.i0 + kVTX) / kVTX) * ((R.j1 - R.j0 + kVTY) / kVTY);
+    const long nvt = (long)((R.i1 - tile_i0(R.i0) + kVTX) / kVTX) * ((R.j1 - R.j0 + kVTY) / kVTY);
     const long gy = (nvt + g.x - 1) / g.x;
     if (gy > (long)g.y) g.y = (unsigned)gy;
   }

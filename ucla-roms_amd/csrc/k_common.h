@@ -296,14 +296,14 @@ __device__ __forceinline__ void tracer_win_fill(const Bounds& b, const Fields& F
 // grid of the j-marching per-level kernels: 64-wide strips x chunks of jc
 // rows (marched 4 rows at a time) x levels
 inline dim3 grid3_jc(const Range& r, int nk, int jc) {
-  int ni = r.i1 - r.i0 + 1, nj = r.j1 - r.j0 + 1;
+  int ni = r.i1 - tile_i0(r.i0) + 1, nj = r.j1 - r.j0 + 1;
   if (ni < 1) ni = 1;
   if (nj < 1) nj = 1;
   return dim3((ni + kBX - 1) / kBX, (nj + jc - 1) / jc, nk);
 }
 // grid of the per-level horizontal kernels with 64 x ty tiles (Params::h_ty)
 inline dim3 grid3_ty(const Range& r, int nk, int ty) {
-  int ni = r.i1 - r.i0 + 1, nj = r.j1 - r.j0 + 1;
+  int ni = r.i1 - tile_i0(r.i0) + 1, nj = r.j1 - r.j0 + 1;
   if (ni < 1) ni = 1;
   if (nj < 1) nj = 1;
   return dim3((ni + kBX - 1) / kBX, (nj + ty - 1) / ty, nk);

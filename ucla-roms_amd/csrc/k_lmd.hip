@@ -364,14 +364,15 @@ __global__ void __launch_bounds__(TY > 0 ? kCX * TY : 64, MW) k_kpp_int(Dev d, R
   constexpr bool STG = TY > 0;
   constexpr int TYB = STG ? TY : 1, WW = kCX + 2, WN = WW * (TYB + 2), NTH = kCX * TYB, WQ = (WN + NTH - 1) / NTH;
   const uint3 bI = xcd_tile();
-  int i = R.i0 + (int)(bI.x * kCX + threadIdx.x);
+  const int ti0 = tile_i0(R.i0);
+  int i = ti0 + (int)(bI.x * kCX + threadIdx.x);
   int j = R.j0 + (int)(bI.y * TYB + threadIdx.y);
-  const bool act = i <= R.i1 && j <= R.j1;
+  const bool act = i >= R.i0 && i <= R.i1 && j <= R.j1;
   if (!STG && !act) return;
-  if (!act) { i = i < R.i1 ? i : R.i1; j = j < R.j1 ? j : R.j1; }
+  if (!act) { i = i < R.i0 ? R.i0 : (i < R.i1 ? i : R.i1); j = j < R.j1 ? j : R.j1; }
   __shared__ double sW[STG ? 2 : 1][STG ? WN : 1];
   const int tid = threadIdx.x + kCX * threadIdx.y;
-  const int wi0 = R.i0 + (int)bI.x * kCX - 1, wj0 = R.j0 + (int)bI.y * TYB - 1;
+  const int wi0 = ti0 + (int)bI.x * kCX - 1, wj0 = R.j0 + (int)bI.y * TYB - 1;   // (EdgeClamp keeps i >= -1)
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const Params& P = d.p;

@@ -19,12 +19,12 @@ __global__ void __launch_bounds__(256) k_pre_tracer_h(Dev d, Range R, PreCoef c,
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const int k = 1 + (int)bI.z, indx = 3 - nstp;
-  const int i0 = R.i0 + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * kBY;
+  const int i0 = tile_i0(R.i0) + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * kBY;
   const int ib = i0 - 2, jb = j0 - 2;
   const long kk = (long)(k - 1) * b.n2;
   tracer_win_fill(b, F, W, ib, jb, kk, nullptr);
   const int i = i0 + (int)threadIdx.x, j = j0 + (int)threadIdx.y;
-  const bool act = i <= R.i1 && j <= R.j1;
+  const bool act = i >= R.i0 && i <= R.i1 && j <= R.j1;
   const long ij = IJ(b, i, j), o = ij + kk;
   double hb = 0.0;
   if (act) {
@@ -80,7 +80,7 @@ __global__ void __launch_bounds__(kBX * TY) k_pre_tracer_h1(Dev d, Range R, PreC
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const int k = 1 + (int)bI.z, indx = 3 - nstp;
-  const int i0 = R.i0 + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * TY;
+  const int i0 = tile_i0(R.i0) + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * TY;
   const int ib = i0 - 2, jb = j0 - 2;
   const long kk = (long)(k - 1) * b.n2, n2 = b.n2;
   const int tid = threadIdx.x + kBX * threadIdx.y;
@@ -101,7 +101,7 @@ __global__ void __launch_bounds__(kBX * TY) k_pre_tracer_h1(Dev d, Range R, PreC
       wT[t][r] = ok ? F.t[(long)(nrhs - 1) * b.n3 + (long)t * 3 * b.n3 + o + kk] : 0.0;
   }
   const int i = i0 + (int)threadIdx.x, j = j0 + (int)threadIdx.y;
-  const bool act = i <= R.i1 && j <= R.j1;
+  const bool act = i >= R.i0 && i <= R.i1 && j <= R.j1;
   const bool in = act && i >= b.istr && j >= b.jstr;
   const long ij = act ? IJ(b, i, j) : IJ(b, R.i0, R.j0), o = ij + kk, w = ij + (long)k * n2;
   // hz_bak_fwd's inputs (pre_step3d4S.F:136-148) and the tracer time levels
@@ -217,7 +217,7 @@ __global__ void __launch_bounds__(kBX * kBY) k_pre_tracer_hj(Dev d, Range R, Pre
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const int k = 1 + (int)bI.z, indx = 3 - nstp;
-  const int i0 = R.i0 + (int)bI.x * kBX, jc0 = R.j0 + (int)bI.y * jc;
+  const int i0 = tile_i0(R.i0) + (int)bI.x * kBX, jc0 = R.j0 + (int)bI.y * jc;
   const int jend = min(jc0 + jc - 1, R.j1);
   const int ib = i0 - 2, jb = jc0 - 2;
   const long kk = (long)(k - 1) * b.n2, n2 = b.n2, tlev = (long)(nrhs - 1) * b.n3;
@@ -230,7 +230,7 @@ __global__ void __launch_bounds__(kBX * kBY) k_pre_tracer_hj(Dev d, Range R, Pre
   };
   const int i = i0 + (int)threadIdx.x;
   auto load_lane = [&](Lane& L, int j) {
-    const bool act = i <= R.i1 && j <= jend;
+    const bool act = i >= R.i0 && i <= R.i1 && j <= jend;
     const bool formed = kHB && act && i >= b.istr && j >= b.jstr;
     const long ij = act ? IJ(b, i, j) : IJ(b, R.i0, R.j0), o = ij + kk, w = ij + (long)k * n2;
     L.fu0 = L.fu1 = L.fv0 = L.fv1 = L.we1 = L.wi1 = L.we0 = L.wi0 = L.hbo = 0.0;
@@ -267,7 +267,7 @@ __global__ void __launch_bounds__(kBX * kBY) k_pre_tracer_hj(Dev d, Range R, Pre
       load_lane(Ln, j0 + kBY + (int)threadIdx.y);
     }
     const int j = j0 + (int)threadIdx.y;
-    const bool act = i <= R.i1 && j <= jend;
+    const bool act = i >= R.i0 && i <= R.i1 && j <= jend;
     const bool in = act && i >= b.istr && j >= b.jstr;
     if (act) {
       const long ij = IJ(b, i, j), o = ij + kk;
@@ -458,7 +458,7 @@ __global__ void __launch_bounds__(256) k_uv_horiz(Dev d, Range R, int nrhs, UVBo
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const int k = 1 + (int)bI.z;
-  const int i0 = R.i0 + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * kBY;
+  const int i0 = tile_i0(R.i0) + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * kBY;
   const int ib = i0 - 2, jb = j0 - 2;
   const long kk = (long)(k - 1) * b.n2;
   const double* U = F.u + (long)(nrhs - 1) * b.n3 + kk;
@@ -466,7 +466,7 @@ __global__ void __launch_bounds__(256) k_uv_horiz(Dev d, Range R, int nrhs, UVBo
   const double* FU = F.FlxU + kk;
   const double* FV = F.FlxV + kk;
   const int i = i0 + (int)threadIdx.x, j = j0 + (int)threadIdx.y;
-  const bool act = i <= R.i1 && j <= R.j1;
+  const bool act = i >= R.i0 && i <= R.i1 && j <= R.j1;
   for (int q = threadIdx.x + kBX * threadIdx.y; q < kUVN; q += kBX * kBY) {
     const int ii = ib + q % kUVW, jj = jb + q / kUVW;
     if (ii < -1 || ii > b.Lm + 2 || jj < -1 || jj > b.Mm + 2) continue;  // never read
@@ -493,7 +493,7 @@ __global__ void __launch_bounds__(kBX * TY) k_uv_horiz1(Dev d, Range R, int nrhs
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const int k = 1 + (int)bI.z;
-  const int i0 = R.i0 + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * TY;
+  const int i0 = tile_i0(R.i0) + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * TY;
   const int ib = i0 - 2, jb = j0 - 2;
   const long kk = (long)(k - 1) * b.n2;
   const double* U = F.u + (long)(nrhs - 1) * b.n3 + kk;
@@ -501,7 +501,7 @@ __global__ void __launch_bounds__(kBX * TY) k_uv_horiz1(Dev d, Range R, int nrhs
   const double* FU = F.FlxU + kk;
   const double* FV = F.FlxV + kk;
   const int i = i0 + (int)threadIdx.x, j = j0 + (int)threadIdx.y;
-  const bool act = i <= R.i1 && j <= R.j1;
+  const bool act = i >= R.i0 && i <= R.i1 && j <= R.j1;
   const int tid = threadIdx.x + kBX * threadIdx.y;
   constexpr int NR = (NW + kBX * TY - 1) / (kBX * TY);
   double wU[NR], wV[NR], wFU[NR], wFV[NR];
@@ -705,9 +705,9 @@ __global__ void __launch_bounds__(kSegBlock, 2) k_pre_tracer_seg(Dev d, Range R,
   const Fields& F = d.f;
   const int N = b.N;
   const SegSpan sg = seg_span(N);
-  const int iu = R.i0 + (int)bI.x * kSegCW + sg.col;
-  const bool act = iu <= R.i1;
-  const int i = act ? iu : R.i1, j = R.j0 + (int)bI.y;
+  const int iu = tile_i0(R.i0) + (int)bI.x * kSegCW + sg.col;
+  const bool act = iu >= R.i0 && iu <= R.i1;
+  const int i = act ? iu : (iu < R.i0 ? R.i0 : R.i1), j = R.j0 + (int)bI.y;
   const int itrc = 1 + (int)bI.z;
   const long n2 = b.n2, ij = IJ(b, i, j);
   const int c0 = sg.c0, n = sg.n;

@@ -142,7 +142,7 @@ __global__ void __launch_bounds__(kBX * TY) k_prsgrd_uv(Dev d, Range R, int spli
   const double* R1 = split ? F.rho1 : F.rho;
   const int k = 1 + (int)bI.z;
   const long kk = (long)(k - 1) * b.n2, sj = b.nx2;
-  const int i0 = R.i0 + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * TY;
+  const int i0 = tile_i0(R.i0) + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * TY;
   const int tid = threadIdx.x + kBX * threadIdx.y;
   auto W = [&](int i, int j) { return (i - (i0 - 2)) + (j - (j0 - 2)) * kPWW; };
   // ---- loads, all issued before the first barrier ----
@@ -153,7 +153,7 @@ __global__ void __launch_bounds__(kBX * TY) k_prsgrd_uv(Dev d, Range R, int spli
     wz[m] = wr[m] = wq[m] = 0.0;
     if (q < WN) {
       const int i = i0 - 2 + q % kPWW, j = j0 - 2 + q / kPWW;
-      if (i <= b.Lm + 2 && j <= b.Mm + 2) {
+      if (i >= -1 && i <= b.Lm + 2 && j <= b.Mm + 2) {
         const long o = IJ(b, i, j) + kk;
         wz[m] = F.z_r[o];
         wr[m] = R1[o];
@@ -171,7 +171,7 @@ __global__ void __launch_bounds__(kBX * TY) k_prsgrd_uv(Dev d, Range R, int spli
     if (q < XN) {
       const int j = j0 + q / kPXW;
       int mm = i0 - 1 + q % kPXW;
-      if (!(j > b.Mm + 1 || mm > b.Lm + 2)) {
+      if (!(j > b.Mm + 1 || mm > b.Lm + 2 || mm < -1)) {
         mm = iclamp(mm, imin, imax);
         eon[m] = true; e1[m] = W(mm, j); e0[m] = W(mm - 1, j);
         mk[m] = F.umask[IJ(b, mm, j)];
@@ -180,7 +180,7 @@ __global__ void __launch_bounds__(kBX * TY) k_prsgrd_uv(Dev d, Range R, int spli
       const int qq = q - XN;
       const int i = i0 + qq % kBX;
       int mm = j0 - 1 + qq / kBX;
-      if (!(i > b.Lm + 1 || mm > b.Mm + 2)) {
+      if (!(i > b.Lm + 1 || i < -1 || mm > b.Mm + 2)) {
         mm = iclamp(mm, jmin, jmax);
         eon[m] = true; e1[m] = W(i, mm); e0[m] = W(i, mm - 1);
         mk[m] = F.vmask[IJ(b, i, mm)];
@@ -188,7 +188,7 @@ __global__ void __launch_bounds__(kBX * TY) k_prsgrd_uv(Dev d, Range R, int spli
     }
   }
   const int i = i0 + (int)threadIdx.x, j = j0 + (int)threadIdx.y;
-  const bool inr = i <= R.i1 && j <= R.j1;
+  const bool inr = i >= R.i0 && i <= R.i1 && j <= R.j1;
   const long ij = IJ(b, inr ? i : R.i0, inr ? j : R.j0), o = ij + kk;
   const bool du = inr && i >= b.istrU && i <= b.iend && j >= b.jstr && j <= b.jend;
   const bool dv = inr && i >= b.istr && i <= b.iend && j >= b.jstrV && j <= b.jend;
@@ -370,7 +370,7 @@ __global__ void __launch_bounds__(kFT) k_prsgrd_fused(Dev d, Range R, int split,
   const double OneFifth = 0.2, OneTwelfth = 1.0 / 12.0;
   const double grho = g / rho0, HalfGRho = 0.5 * grho;
   const long n2 = b.n2, sj = b.nx2;
-  const int i0 = R.i0 + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * kBY;
+  const int i0 = tile_i0(R.i0) + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * kBY;
   const int tid = threadIdx.x;
   const double* R1 = split ? F.rho1 : F.rho;
   // window entries owned by this thread
@@ -380,7 +380,7 @@ __global__ void __launch_bounds__(kFT) k_prsgrd_fused(Dev d, Range R, int split,
   for (int m = 0; m < kFQ; m++) {
     const int e = tid + m * kFT;
     const int i = i0 - 2 + e % kFW, j = j0 - 2 + e / kFW;
-    won[m] = e < kFN && i <= b.Lm + 2 && j <= b.Mm + 2;
+    won[m] = e < kFN && i >= -1 && i <= b.Lm + 2 && j <= b.Mm + 2;
     wo[m] = IJ(b, i, j);
   }
   auto load = [&](int k, PrsPre& X) {
@@ -409,7 +409,7 @@ __global__ void __launch_bounds__(kFT) k_prsgrd_fused(Dev d, Range R, int split,
   const bool pcol = tid < kFPN;
   const int pci = tid % kFPW, pcj = tid / kFPW;
   const int pi = i0 - 1 + pci, pj = j0 - 1 + pcj;
-  const bool pon = pcol && pi <= b.Lm + 1 && pj <= b.Mm + 1;
+  const bool pon = pcol && pi >= -1 && pi <= b.Lm + 1 && pj <= b.Mm + 1;
   const int pw = (pci + 1) + (pcj + 1) * kFW;   // its window position
   const long pij = IJ(b, pi, pj);
   auto rhov = [&](double r1, double q1, double z) {
@@ -429,7 +429,7 @@ __global__ void __launch_bounds__(kFT) k_prsgrd_fused(Dev d, Range R, int split,
   // tile lane: clamped u-/v-point window offsets and masks (level independent)
   const int ti = tid % kBX, tj = tid / kBX;
   const int i = i0 + ti, j = j0 + tj;
-  const bool tile = tid < kBX * kBY && i <= R.i1 && j <= R.j1;
+  const bool tile = tid < kBX * kBY && i >= R.i0 && i <= R.i1 && j <= R.j1;
   const long ij = IJ(b, i, j);
   const bool du = tile && i >= b.istrU && i <= b.iend && j >= b.jstr && j <= b.jend;
   const bool dv = tile && i >= b.istr && i <= b.iend && j >= b.jstrV && j <= b.jend;

@@ -243,7 +243,7 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int cl
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const long sj = b.nx2, n2 = b.n2;
-  const int i0 = R.i0 + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * kBY;
+  const int i0 = tile_i0(R.i0) + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * kBY;
   const int tid = threadIdx.x + kBX * threadIdx.y;
   constexpr int NT = kBX * kBY;
   auto G = [&](int i, int j) { return (i - (i0 - 2)) + (j - (j0 - 2)) * kGX; };
@@ -314,7 +314,7 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int cl
     }
   }
   const int pi = i0 + (int)threadIdx.x, pj = j0 + (int)threadIdx.y;
-  const bool pact = pi <= R.i1 && pj <= R.j1;
+  const bool pact = pi >= R.i0 && pi <= R.i1 && pj <= R.j1;
   const bool pint = pact && pi >= b.istr && pi <= b.iend && pj >= b.jstr && pj <= b.jend;
   const long pij = pact ? IJ(b, pi, pj) : 0;
   double x_rA0 = 0, x_rAx = 0, x_rAy = 0, x_dnu = 0, x_dmv = 0, x_rufrc = 0, x_rvfrc = 0, x_ub = 0, x_vb = 0;
@@ -436,7 +436,7 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int cl
   }
   // P3: zeta(knew), fast averages, pressure gradient, momentum
   const int i = i0 + (int)threadIdx.x, j = j0 + (int)threadIdx.y;
-  const bool pin = i <= R.i1 && j <= R.j1;
+  const bool pin = i >= R.i0 && i <= R.i1 && j <= R.j1;
   if (closed != 2 && !pin) return;
   const int q = (threadIdx.x + 1) + (threadIdx.y + 1) * kFX;  // (i,j); q-1 = (i-1,j); q-kFX = (i,j-1)
   const int g = G(i, j);                                        // g-1: (i-1,j); g-kGX: (i,j-1)
@@ -851,9 +851,10 @@ void launch_step2d(const Dev& d, hipStream_t s, const Tlev& t, const double* w1,
   Range RB{b.istrR, b.iendR, b.jstrR, b.jendR};
   // closed walls folded into k_s2d_fb when no edge is open and every edge
   // row / column shares its tile with the interior row / column beside it
-  // (tiles start at istrR / jstrR; ROMS_GPU_S2D_EDGES=1 keeps k_s2d_edges)
+  // (tiles start at tile_i0(istrR) / jstrR; ROMS_GPU_S2D_EDGES=1 keeps k_s2d_edges)
   const bool fold = closed && !d.p.obc && !d.p.s2d_split && d.p.s2d_fold &&
-                    (!b.east_edge || (b.iendR - b.istrR) % kBX != 0) &&
+                    (!b.east_edge || (b.iendR - tile_i0(b.istrR)) % kBX != 0) &&
+                    (!b.west_edge || (b.istrR - tile_i0(b.istrR)) % kBX != kBX - 1) &&
                     (!b.north_edge || (b.jendR - b.jstrR) % kBY != 0);
   const int cmode = !closed ? 0 : (fold ? 2 : 1);
   Halo* H = const_cast<Halo*>(d.halo);   // multi-rank exchange state (host bookkeeping)

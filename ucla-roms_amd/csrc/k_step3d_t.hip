@@ -14,12 +14,12 @@ __global__ void __launch_bounds__(256) k_step3d_t_h(Dev d, Range R, int nnew, in
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const int k = 1 + (int)bI.z;
-  const int i0 = R.i0 + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * kBY;
+  const int i0 = tile_i0(R.i0) + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * kBY;
   const int ib = i0 - 2, jb = j0 - 2;
   const long kk = (long)(k - 1) * b.n2;
   tracer_win_fill(b, F, W, ib, jb, kk, nullptr);
   const int i = i0 + (int)threadIdx.x, j = j0 + (int)threadIdx.y;
-  const bool act = i <= R.i1 && j <= R.j1;
+  const bool act = i >= R.i0 && i <= R.i1 && j <= R.j1;
   const long ij = IJ(b, i, j), o = ij + kk;
   const AccTL a{W.T, W.UM, W.VM, W.FU, W.FV, ib, jb};
   for (int itrc = 1; itrc <= b.NT; itrc++) {
@@ -54,7 +54,7 @@ __global__ void __launch_bounds__(kBX * TY) k_step3d_t_h1(Dev d, Range R, int nn
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const int k = 1 + (int)bI.z;
-  const int i0 = R.i0 + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * TY;
+  const int i0 = tile_i0(R.i0) + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * TY;
   const int ib = i0 - 2, jb = j0 - 2;
   const long kk = (long)(k - 1) * b.n2;
   const int tid = threadIdx.x + kBX * threadIdx.y;
@@ -75,7 +75,7 @@ __global__ void __launch_bounds__(kBX * TY) k_step3d_t_h1(Dev d, Range R, int nn
       wT[t][r] = ok ? F.t[(long)(nrhs - 1) * b.n3 + (long)t * 3 * b.n3 + o + kk] : 0.0;
   }
   const int i = i0 + (int)threadIdx.x, j = j0 + (int)threadIdx.y;
-  const bool act = i <= R.i1 && j <= R.j1;
+  const bool act = i >= R.i0 && i <= R.i1 && j <= R.j1;
   const long ij = act ? IJ(b, i, j) : IJ(b, R.i0, R.j0), o = ij + kk;
   const double pm = F.pm[ij], pn = F.pn[ij];
   double tn[NTT];
@@ -237,9 +237,9 @@ __global__ void __launch_bounds__(kSegBlock, 2) k_step3d_t_seg(Dev d, Range R, i
   const int N = b.N;
   const double dt = P.dt;
   const SegSpan sg = seg_span(N);
-  const int iu = R.i0 + (int)bI.x * kSegCW + sg.col;
-  const bool act = iu <= R.i1;
-  const int i = act ? iu : R.i1, j = R.j0 + (int)bI.y;
+  const int iu = tile_i0(R.i0) + (int)bI.x * kSegCW + sg.col;
+  const bool act = iu >= R.i0 && iu <= R.i1;
+  const int i = act ? iu : (iu < R.i0 ? R.i0 : R.i1), j = R.j0 + (int)bI.y;
   const int itrc = 1 + (int)bI.z;
   const long n2 = b.n2, ij = IJ(b, i, j);
   const int c0 = sg.c0, n = sg.n;
@@ -496,10 +496,10 @@ __global__ void __launch_bounds__(256) k_t3dmix_stg(Dev d, Range R, int nnew, in
   __shared__ double sW[3 * kTMN];   // Hz, T, S
   const Bounds& b = d.b;
   const Fields& F = d.f;
-  const int i0 = R.i0 + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * kBY;
+  const int i0 = tile_i0(R.i0) + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * kBY;
   int i = i0 + (int)threadIdx.x, j = j0 + (int)threadIdx.y;
-  const bool act = i <= R.i1 && j <= R.j1;
-  if (!act) { i = i < R.i1 ? i : R.i1; j = j < R.j1 ? j : R.j1; }
+  const bool act = i >= R.i0 && i <= R.i1 && j <= R.j1;
+  if (!act) { i = i < R.i0 ? R.i0 : (i < R.i1 ? i : R.i1); j = j < R.j1 ? j : R.j1; }
   const long ij = IJ(b, i, j), sj = b.nx2, n2 = b.n2;
   const int tid = threadIdx.x + kBX * threadIdx.y;
   const double pmn = d.p.dt * F.pm[ij] * F.pn[ij];

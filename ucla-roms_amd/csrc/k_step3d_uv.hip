@@ -503,7 +503,7 @@ __global__ void __launch_bounds__(256) k_visc3d(Dev d, Range R, int nstp) {
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const int indx = 3 - nstp;
-  const int i0 = R.i0 + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * kBY;
+  const int i0 = tile_i0(R.i0) + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * kBY;
   const long sj = b.nx2;
   const double* pm = F.pm;
   const double* pn = F.pn;
@@ -540,7 +540,7 @@ __global__ void __launch_bounds__(256) k_visc3d(Dev d, Range R, int nstp) {
     }
   }
   const int i = i0 + (int)threadIdx.x, j = j0 + (int)threadIdx.y;
-  const bool act = i <= R.i1 && j <= R.j1;
+  const bool act = i >= R.i0 && i <= R.i1 && j <= R.j1;
   const long ij = IJ(b, i, j);
   const bool du = act && i >= b.istrU && i <= b.iend, dv = act && j >= b.jstrV && j <= b.jend;
   double cum = 0.0, cun = 0.0, cvm = 0.0, cvn = 0.0, fu = 0.0, fv = 0.0;
@@ -619,7 +619,7 @@ __global__ void __launch_bounds__(256, 3) k_visc3d_stg(Dev d, Range R, int nstp)
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const int indx = 3 - nstp;
-  const int i0 = R.i0 + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * kBY;
+  const int i0 = tile_i0(R.i0) + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * kBY;
   const long sj = b.nx2;
   const double* pm = F.pm;
   const double* pn = F.pn;
@@ -681,7 +681,7 @@ __global__ void __launch_bounds__(256, 3) k_visc3d_stg(Dev d, Range R, int nstp)
   auto Vw = [&](int ii, int jj) { return sRaw[kVUN + (ii - (i0 - 1)) + (jj - (j0 - 1)) * kVVW]; };
   auto Hw = [&](int ii, int jj) { return sRaw[kVUN + kVVN + (ii - (i0 - 1)) + (jj - (j0 - 1)) * kVHW]; };
   const int i = i0 + (int)threadIdx.x, j = j0 + (int)threadIdx.y;
-  const bool act = i <= R.i1 && j <= R.j1;
+  const bool act = i >= R.i0 && i <= R.i1 && j <= R.j1;
   const long ij = IJ(b, i, j);
   const bool du = act && i >= b.istrU && i <= b.iend, dv = act && j >= b.jstrV && j <= b.jend;
   double cum = 0.0, cun = 0.0, cvm = 0.0, cvn = 0.0, fu = 0.0, fv = 0.0;
@@ -919,7 +919,7 @@ __global__ void __launch_bounds__(256, KL > 13 ? 3 : 4) k_uv2_fused(Dev d, Range
     // defined values, and store nothing)
     const int ilo = dir == 0 ? b.istrU : b.istr, jlo = dir == 0 ? b.jstr : b.jstrV;
     const int ic = min(max(i, ilo), b.iend), jc = min(max(j, jlo), b.jend);
-    const bool act = ic == i && jc == j && uv2_fused_in(b, dir, i, j);
+    const bool act = ic == i && jc == j && cl.in && uv2_fused_in(b, dir, i, j);
     const long ij = IJ(b, ic, jc), s = dir == 0 ? 1 : b.nx2;
     double* __restrict__ Un = (dir == 0 ? F.u : F.v) + (long)(nnew - 1) * b.n3 + ij;
     const double* __restrict__ Us = (dir == 0 ? F.u : F.v) + (long)(nstp - 1) * b.n3 + ij;

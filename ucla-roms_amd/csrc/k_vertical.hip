@@ -169,7 +169,7 @@ __global__ void __launch_bounds__(256) k_set_huv1_chain(Dev d, Range R, int nnew
   for (int dir = d0; dir < d1; dir++) {
     const int ilo = dir == 0 ? b.istr : b.istrR, jlo = dir == 0 ? b.jstrR : b.jstr;
     const int ic = min(max(cl.i, ilo), b.iendR), jc = min(max(cl.j, jlo), b.jendR);
-    const bool act = ic == cl.i && jc == cl.j;
+    const bool act = ic == cl.i && jc == cl.j && cl.in;
     const long ij = IJ(b, ic, jc), s = dir == 0 ? 1 : b.nx2;
     const double dn = dir == 0 ? F.dn_u[ij] : F.dm_v[ij];
     double* __restrict__ u = (dir == 0 ? F.u : F.v) + (long)(nnew - 1) * b.n3 + ij;
@@ -405,9 +405,9 @@ __global__ void __launch_bounds__(kSegBlock, 2) k_omega_seg(Dev d, Range R, doub
                r4cmx = 0.25 / (1.0 - cmnx_ratio);
   const SegSpan sg = seg_span(N);
   const int s = sg.s, S = sg.S, c0 = sg.c0, n = sg.n, l = sg.col;
-  const int iu = R.i0 + (int)bI.x * kSegCW + l, ju = R.j0 + (int)bI.y;
-  const bool act = iu <= R.i1 && ju <= R.j1;
-  const int i = iu < R.i1 ? iu : R.i1, j = ju < R.j1 ? ju : R.j1;
+  const int iu = tile_i0(R.i0) + (int)bI.x * kSegCW + l, ju = R.j0 + (int)bI.y;
+  const bool act = iu >= R.i0 && iu <= R.i1 && ju <= R.j1;
+  const int i = iu < R.i0 ? R.i0 : (iu < R.i1 ? iu : R.i1), j = ju < R.j1 ? ju : R.j1;
   const long ij = IJ(b, i, j), n2 = b.n2, sj = b.nx2;
   const double* __restrict__ FU = F.FlxU + ij;
   const double* __restrict__ FV = F.FlxV + ij;
@@ -580,7 +580,7 @@ bool launch_omega(const Dev& d, hipStream_t s, const Tlev& t, double hcff) {
       d, s, R, ExchList{{d.f.We, d.f.Wi}, {b.N + 1, b.N + 1}, 2},
       [&](const Range& r) {
         // the segment form for full-width ranges (rim strips keep k_omega)
-        const dim3 gs((r.i1 - r.i0 + kSegCW) / kSegCW, r.j1 - r.j0 + 1), bs(kCX, seg_waves(b.N));
+        const dim3 gs((r.i1 - tile_i0(r.i0) + kSegCW) / kSegCW, r.j1 - r.j0 + 1), bs(kCX, seg_waves(b.N));
         if (hb)
           hipLaunchKernelGGL(k_omega_seg<true>, gs, bs, omega_hb_lds_bytes(bs.x * bs.y), s, d, r, dtau, hcff);
         else if (seg_ok && r.i1 - r.i0 + 1 >= 32)

@@ -224,8 +224,17 @@ struct Range {
   int i0, i1, j0, j1;
 };
 constexpr int kBX = 64, kBY = 4;
+// First tile column of a launch over [i0, i1]: i0 rounded down to a line
+// start of the device rows (i = 1 mod kRowAlign, roms_dev.h layout), so the
+// wavefront rows of every tile read whole 128-B lines; the lanes left of i0
+// in the first tile idle.  (Ranges from istrR/istrE = 0 or -1, istrU = 2 and
+// the multi-rank rim strips all start off a line.)
+#ifndef ROMS_TILE_ALIGN
+#define ROMS_TILE_ALIGN 1   // 0: tiles start at the range's first column (A/B builds, tools/build_variant.sh)
+#endif
+__host__ __device__ __forceinline__ int tile_i0(int i0) { return ROMS_TILE_ALIGN ? i0 - ((i0 - 1) & (kRowAlign - 1)) : i0; }
 inline dim3 grid_of(const Range& r) {
-  int ni = r.i1 - r.i0 + 1, nj = r.j1 - r.j0 + 1;
+  int ni = r.i1 - tile_i0(r.i0) + 1, nj = r.j1 - r.j0 + 1;
   if (ni < 1) ni = 1;
   if (nj < 1) nj = 1;
   return dim3((ni + kBX - 1) / kBX, (nj + kBY - 1) / kBY, 1);
@@ -261,21 +270,21 @@ constexpr int kSegBlock = ((kSegMaxS * kSegCW + 63) / 64) * 64;   // threads of 
 #endif
 constexpr int kSegJMax = ROMS_SEG_JMAX;
 inline dim3 gridc_of(const Range& r) {
-  int ni = r.i1 - r.i0 + 1, nj = r.j1 - r.j0 + 1;
+  int ni = r.i1 - tile_i0(r.i0) + 1, nj = r.j1 - r.j0 + 1;
   if (ni < 1) ni = 1;
   if (nj < 1) nj = 1;
   return dim3((ni + kCX - 1) / kCX, nj, 1);
 }
-#define ROMS_IJC_OR_RETURN(R)                                   \
-  const uint3 bI = xcd_tile();                                  \
-  const int i = (R).i0 + (int)(bI.x * kCX + threadIdx.x);       \
-  const int j = (R).j0 + (int)bI.y;                             \
-  if (i > (R).i1 || j > (R).j1) return;
-#define ROMS_IJ_OR_RETURN(R)                                   \
-  const uint3 bI = xcd_tile();                                 \
-  const int i = (R).i0 + (int)(bI.x * kBX + threadIdx.x);      \
-  const int j = (R).j0 + (int)(bI.y * kBY + threadIdx.y);      \
-  if (i > (R).i1 || j > (R).j1) return;
+#define ROMS_IJC_OR_RETURN(R)                                       \
+  const uint3 bI = xcd_tile();                                      \
+  const int i = tile_i0((R).i0) + (int)(bI.x * kCX + threadIdx.x);  \
+  const int j = (R).j0 + (int)bI.y;                                 \
+  if (i < (R).i0 || i > (R).i1 || j > (R).j1) return;
+#define ROMS_IJ_OR_RETURN(R)                                        \
+  const uint3 bI = xcd_tile();                                      \
+  const int i = tile_i0((R).i0) + (int)(bI.x * kBX + threadIdx.x); \
+  const int j = (R).j0 + (int)(bI.y * kBY + threadIdx.y);           \
+  if (i < (R).i0 || i > (R).i1 || j > (R).j1) return;
 
 // ---- launcher declarations (one translation unit per routine family) ----
 // Each takes the rank's device state and a stream; all enqueue asynchronously.
