@@ -916,7 +916,7 @@ double pre_step3d_dtau(const Dev& d, const Tlev& t) {
   return t.iic == t.forw_start ? 0.5 * d.p.dt : d.p.dt * (1.0 - AM3_crv);
 }
 
-void launch_pre_step3d(const Dev& d, hipStream_t s, const Tlev& t, bool uv_done, bool hb_done) {
+void launch_pre_step3d(const Dev& d, hipStream_t s, const Tlev& t, bool uv_done, bool hb_done, const Side* side) {
   const Bounds& b = d.b;
   PreCoef c;
   const double AM3_crv = 1.0 / 6.0;
@@ -956,17 +956,29 @@ void launch_pre_step3d(const Dev& d, hipStream_t s, const Tlev& t, bool uv_done,
   } else {
     hipLaunchKernelGGL(k_pre_tracer_h, grid3_of(RH, b.N), dim3(kBX, kBY), 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs);
   }
+  // The tracer column solves (t(nnew), reading Hz_fwd) and the momentum ones
+  // (u, v(nnew), u, v(indx), reading Hz_fwd/bak, ru, rv) share no output:
+  // with a side stream they run side by side once the horizontal tracer
+  // kernel has formed the ring of Hz_fwd/bak both read
+  hipStream_t st = s;
+  if (side) {
+    (void)hipEventRecord(side->efork, s);
+    (void)hipStreamWaitEvent(side->s2, side->efork, 0);
+    st = side->s2;
+  }
   dim3 gt = gridc_of(RI);
   gt.z = b.NT;
   if (d.p.colseg)
-    hipLaunchKernelGGL(k_pre_tracer_seg, seg_grid_of(RI, b.NT), dim3(kCX, seg_waves(b.N)), 0, s, d, RI, c, t.nnew,
+    hipLaunchKernelGGL(k_pre_tracer_seg, seg_grid_of(RI, b.NT), dim3(kCX, seg_waves(b.N)), 0, st, d, RI, c, t.nnew,
                        t.nrhs);
   else if ((d.p.colreg & 2) && b.N == 50 && !d.f.colscr)
-    hipLaunchKernelGGL(k_pre_tracer_v_reg<50>, gt, dim3(kCX), col_lds_bytes(1, 50), s, d, RI, c, t.nnew, t.nrhs);
+    hipLaunchKernelGGL(k_pre_tracer_v_reg<50>, gt, dim3(kCX), col_lds_bytes(1, 50), st, d, RI, c, t.nnew, t.nrhs);
   else if (d.f.colscr)
-    hipLaunchKernelGGL(k_pre_tracer_v<ColGlb>, gt, dim3(kCX), 0, s, d, RI, c, t.nnew, t.nrhs);
+    hipLaunchKernelGGL(k_pre_tracer_v<ColGlb>, gt, dim3(kCX), 0, st, d, RI, c, t.nnew, t.nrhs);
   else
-    hipLaunchKernelGGL(k_pre_tracer_v<ColLds>, gt, dim3(kCX), col_lds_bytes(2, b.N), s, d, RI, c, t.nnew, t.nrhs);
+    hipLaunchKernelGGL(k_pre_tracer_v<ColLds>, gt, dim3(kCX), col_lds_bytes(2, b.N), st, d, RI, c, t.nnew, t.nrhs);
+  for (int itrc = 1; itrc <= b.NT && side; itrc++) launch_t3dbc(d, st, t, itrc);
+  if (side) launch_exchange_tracers(d, st, t.nnew);
   if (!uv_done) launch_uv_horiz(d, s, t.nrhs, 0);
   Range Rd{b.istrU - 1, b.iend, b.jstrV - 1, b.jend};
   hipLaunchKernelGGL(k_rd, grid_of(Rd), dim3(kBX, kBY), 0, s, d, Rd, t.nstp);
@@ -989,6 +1001,11 @@ void launch_pre_step3d(const Dev& d, hipStream_t s, const Tlev& t, bool uv_done,
   launch_river_uv(d, s, t.nnew, 1);   // pre_step3d4S.F:493-522
   launch_u3dbc(d, s, t);
   launch_v3dbc(d, s, t);
+  if (side) {
+    (void)hipEventRecord(side->ejoin, st);
+    (void)hipStreamWaitEvent(s, side->ejoin, 0);
+    return;
+  }
   for (int itrc = 1; itrc <= b.NT; itrc++) launch_t3dbc(d, s, t, itrc);
   launch_exchange_tracers(d, s, t.nnew);
 }

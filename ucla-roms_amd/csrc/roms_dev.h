@@ -366,8 +366,18 @@ void launch_rho_eos(const Dev& d, hipStream_t s, const Tlev& t, int tidx);
 void launch_prsgrd(const Dev& d, hipStream_t s, const Tlev& t, int uv_up = -1, bool p_ready = false);
 bool p_in_rho(const Dev& d);   // every rho_eos also forms prsgrd's P (k_vertical.hip)
 bool prsgrd_can_fuse_uv(const Dev& d);
+// A second stream for work with no data dependence on the main stream's
+// (enqueue_step, single rank): the callee forks `s2` off `s` with `efork`
+// and joins it back with `ejoin` before returning.
+struct Side {
+  hipStream_t s2;
+  hipEvent_t efork, ejoin;
+};
 // hb_done: the interior cells' Hz_bak/Hz_fwd are in c3/c2 already (launch_omega)
-void launch_pre_step3d(const Dev& d, hipStream_t s, const Tlev& t, bool uv_done = false, bool hb_done = false);
+// side: the tracer solves (and their boundary conditions and exchange) run on
+// side->s2 beside the momentum ones
+void launch_pre_step3d(const Dev& d, hipStream_t s, const Tlev& t, bool uv_done = false, bool hb_done = false,
+                       const Side* side = nullptr);
 void launch_step3d_uv1(const Dev& d, hipStream_t s, const Tlev& t, bool uv_done = false);
 void launch_visc3d(const Dev& d, hipStream_t s, const Tlev& t);
 void launch_step2d(const Dev& d, hipStream_t s, const Tlev& t, const double* w1, const double* w2);

@@ -87,6 +87,11 @@ struct Ctx {
   Bounds hb{};               // the host layout's Bounds (nx2 = Lm+4)
   double* stage = nullptr;
   long stage_n = 0;
+  // Routines with no data dependence between them run on two streams inside
+  // the step (single rank; ROMS_GPU_PAR=0 serialises): see enqueue_step
+  bool par = true;
+  hipStream_t s2 = nullptr;
+  hipEvent_t pev[8] = {};
 };
 // One context per host thread: a process normally drives one GPU/subdomain
 // from one thread; tests drive several subdomains from threads of one process.
@@ -307,6 +312,9 @@ void free_all() {
   if (g.h_diag) { (void)hipHostFree(g.h_diag); g.h_diag = nullptr; }
   if (g.d_diag) { (void)hipFree(g.d_diag); g.d_diag = nullptr; }
   if (g.s) { (void)hipStreamDestroy(g.s); g.s = nullptr; }
+  if (g.s2) { (void)hipStreamDestroy(g.s2); g.s2 = nullptr; }
+  for (hipEvent_t& e : g.pev)
+    if (e) { (void)hipEventDestroy(e); e = nullptr; }
   g.inited = false;
 }
 
@@ -371,6 +379,26 @@ void enqueue_step(roms_tlev* t, bool rho_current, bool store_huv) {
   Tlev T = to_tlev(t);
   const bool pot = g.cfg.pot_tides != 0;
   g.rho_slot = 0;
+  // Two streams where the reference's order has no data dependence (single
+  // rank -- a multi-rank halo exchange keeps one order on its transport --
+  // and not while one routine is being timed):
+  //   predictor: lmd_vmix(nstp) (writes Akv, Akt, hbls, hbbl, ghat and its
+  //     own work arrays) beside prsgrd (writes ru, rv); pre_step3d reads both
+  //   corrector: omega (We, Wi) beside rho_eos (rho1, qp1, P, bvf, rhoA,
+  //     rhoS), then lmd_vmix(nrhs) beside prsgrd; step3d_uv1 reads all
+  // Same kernels, same inputs: the results are bitwise those of one stream.
+  // The low-occupancy column kernels (KPP, omega) fill CUs the other
+  // routine leaves idle.
+  const bool par = g.par && d.halo == nullptr && g.timed < 0;
+  hipStream_t s2 = g.s2;
+  auto fork = [&](int k) {   // s2 continues after everything queued on s so far
+    (void)hipEventRecord(g.pev[k], s);
+    (void)hipStreamWaitEvent(s2, g.pev[k], 0);
+  };
+  auto join = [&](int k) {   // s continues after everything queued on s2 so far
+    (void)hipEventRecord(g.pev[k], s2);
+    (void)hipStreamWaitEvent(s, g.pev[k], 0);
+  };
   frc_step_phase(d, s, 0, pot);     // set_forces, frc_time 'current' (main.F:384-385)
   launch_bulk_flux(d, s, T.nrhs);   // set_forces (main.F:386): BULK_FRC only
   frc_step_phase(d, s, 1, pot);     // set_bry_all '1/2 fwd' + set_tides (main.F:389-394)
@@ -381,7 +409,13 @@ void enqueue_step(roms_tlev* t, bool rho_current, bool store_huv) {
   bool hb_done = false;
   TIMED(ROMS_R_OMEGA, hb_done = launch_omega(d, s, T, d.p.omega_hb && d.p.hoist && T.nrhs != 3 ?
                                                           0.5 * pre_step3d_dtau(d, T) : 0.0));
-  if (g.cfg.lmd_mixing) TIMED(ROMS_R_LMD_VMIX, launch_lmd_vmix(d, s, T, T.nstp));
+  const bool lmd2 = g.cfg.lmd_mixing && par;
+  if (lmd2) {
+    fork(0);
+    launch_lmd_vmix(d, s2, T, T.nstp);
+  } else if (g.cfg.lmd_mixing) {
+    TIMED(ROMS_R_LMD_VMIX, launch_lmd_vmix(d, s, T, T.nstp));
+  }
   // the horizontal momentum r.h.s. of pre_step3d / step3d_uv1 rides in the
   // prsgrd kernel just before them (prsgrd_can_fuse_uv; nothing between the
   // two touches u, v(nrhs), FlxU, FlxV, Hz or ru, rv)
@@ -390,18 +424,31 @@ void enqueue_step(roms_tlev* t, bool rho_current, bool store_huv) {
   // step-opening one, or the previous step's closing one it reuses
   const bool p_ready = p_in_rho(d);
   TIMED(ROMS_R_PRSGRD, launch_prsgrd(d, s, T, fuse_uv ? 0 : -1, p_ready));
-  TIMED(ROMS_R_PRE_STEP3D, launch_pre_step3d(d, s, T, fuse_uv, hb_done));
+  if (lmd2) join(1);
+  const Side side{s2, g.pev[5], g.pev[6]};
+  TIMED(ROMS_R_PRE_STEP3D, launch_pre_step3d(d, s, T, fuse_uv, hb_done, par ? &side : nullptr));
   TIMED(ROMS_R_SET_HUV1, launch_set_huv1(d, s, T));
   t->nrhs = 3;
   t->nnew = 3 - t->nstp;
   T = to_tlev(t);
-  TIMED(ROMS_R_OMEGA, launch_omega(d, s, T));
+  if (par) {
+    fork(2);
+    launch_omega(d, s2, T);
+  } else {
+    TIMED(ROMS_R_OMEGA, launch_omega(d, s, T));
+  }
   TIMED(ROMS_R_RHO_EOS, launch_rho_eos(d, s, T, T.nrhs));
   frc_step_phase(d, s, 2, pot);     // set_forces, '1/2 fwd' (main.F:433)
   launch_bulk_flux(d, s, T.nrhs);   // set_forces (main.F:433): BULK_FRC only
-  if (g.cfg.lmd_mixing) TIMED(ROMS_R_LMD_VMIX, launch_lmd_vmix(d, s, T, T.nrhs));
+  if (lmd2) {
+    fork(3);   // after rho_eos (bvf) and the bulk fluxes (stflx, srflx, sustr_r)
+    launch_lmd_vmix(d, s2, T, T.nrhs);
+  } else if (g.cfg.lmd_mixing) {
+    TIMED(ROMS_R_LMD_VMIX, launch_lmd_vmix(d, s, T, T.nrhs));
+  }
   frc_step_phase(d, s, 3, pot);     // set_bry_all 'forward' + set_tides (main.F:438-441)
   TIMED(ROMS_R_PRSGRD, launch_prsgrd(d, s, T, fuse_uv ? 1 : -1, p_ready));
+  if (par) join(4);
   TIMED(ROMS_R_STEP3D_UV1, launch_step3d_uv1(d, s, T, fuse_uv));
   if (g.cfg.uv_vis2) TIMED(ROMS_R_VISC3D, launch_visc3d(d, s, T));
   for (int iif = 1; iif <= t->nfast; iif++) {
@@ -775,6 +822,12 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     return -2;
   }
   CHECK_HIP(hipStreamCreateWithFlags(&g.s, hipStreamNonBlocking));
+  CHECK_HIP(hipStreamCreateWithFlags(&g.s2, hipStreamNonBlocking));
+  for (hipEvent_t& e : g.pev) CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  {
+    const char* e = getenv("ROMS_GPU_PAR");
+    g.par = !(e && e[0] == '0');
+  }
   {
     const char* e = getenv("ROMS_GPU_GUARD");
     g.guard = e && e[0] == '1';
