@@ -288,6 +288,8 @@ def run_workload(kind, romsgpu, comm, rank, world, local_rank, steps, warmup, ti
                  "ms_per_step": fb_ms * fb_n / timing_steps, "bytes_per_launch": fb_bytes,
                  "achieved_GBs": fb_gbs, "frac": fb_gbs / HBM_PEAK_GBS}
     transport = m.halo_transport() if comm is not None else "none (single rank)"
+    # exchanges per step (the fast loop's zeta/ubar/vbar swap every K fast steps)
+    exch, fast_k = m.halo_exchanges() if comm is not None else (0, 1)
     norms = m.diag()   # blow-up check as diag.F does (collective)
     if not all(x == x and abs(x) < 1e30 for x in norms):
         raise SystemExit("bench: non-finite diag norms %r" % norms)
@@ -316,7 +318,8 @@ def run_workload(kind, romsgpu, comm, rank, world, local_rank, steps, warmup, ti
                                 "dt=300s, ndtfast=60 (nfast=%d)" % nfast) if c3 else
                                "C2: Filament+S 512x512x50 per GPU, NT=2, dt=5s, ndtfast=60 (nfast=%d)" % nfast,
                    "grid_per_gpu": [Lr, Mr, Nz], "proc_grid": [npx, npe], "NT": NT, "dt": dt_step, "nfast": nfast,
-                   "parallelism": "domain decomposition %dx%d" % (npx, npe), "halo_transport": transport},
+                   "parallelism": "domain decomposition %dx%d" % (npx, npe), "halo_transport": transport,
+                   "halo_exchanges_per_step": exch, "fast_exchange_interval": fast_k},
         "scaling": "strong" if c3 else "weak",
         "steps": steps, "warmup": warmup,
         "roofline": roofline,
@@ -423,6 +426,14 @@ def main():
     if world > 1 or force:
         if force:
             os.environ.setdefault("ROMS_GPU_RCCL_SELF", "1")
+            if world_env is None:   # a plain single-process run: a world of one over loopback
+                import socket
+                with socket.socket() as so:
+                    so.bind(("127.0.0.1", 0))
+                    port = so.getsockname()[1]
+                for k, v in (("RANK", "0"), ("WORLD_SIZE", "1"), ("MASTER_ADDR", "127.0.0.1"),
+                             ("MASTER_PORT", str(port))):
+                    os.environ.setdefault(k, v)
         import torch
         import torch.distributed as dist
         # torch.distributed is host plumbing only here (barrier, max over

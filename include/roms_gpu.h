@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define ROMS_GPU_ABI_VERSION 13
+#define ROMS_GPU_ABI_VERSION 14
 #define ROMS_MAX_FAST 288
 
 /* Subdomain geometry of this rank: param.F / dimensions.F / mpi_setup.F:39-210 */
@@ -277,6 +277,14 @@ int roms_gpu_comm_destroy(void *comm);
  * host-channel communicator: always), -1 = IPC with a timed-out arrival wait
  * since init.                                                               */
 int roms_gpu_halo_transport(void);
+/* Halo exchanges (one reference exchange_xxx call each) in the last whole
+ * step this rank enqueued (eager or graph capture; 0 on one rank without a
+ * communicator), and the fast-loop exchange interval: the barotropic loop
+ * exchanges zeta/ubar/vbar after every *fast_interval-th fast step over
+ * 2*fast_interval-deep halos and recomputes the overlap in between (1: every
+ * fast step, as step2d_FB.F:572-574; multi-rank runs without open edges
+ * default to 2, ROMS_GPU_S2D_K=1..4; rivers and pipes take every step).     */
+int roms_gpu_halo_exchanges(long *per_step, int *fast_interval);
 /* Self-test of the allocation path: `chunks` arrays of n doubles filled
  * with ones and freed, then allocated again through the library's
  * zero-filling allocator; on the library's stream each is read at once

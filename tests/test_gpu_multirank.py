@@ -48,9 +48,10 @@ def _case(kind):
                 sizex=72e3, sizey=56e3, lmd=(kind == "basin_lmd"))
 
 
-def run_decomposed(case, npx, npe, nsteps, fields=FIELDS, diag=False):
+def run_decomposed(case, npx, npe, nsteps, fields=FIELDS, diag=False, probe=None):
     """Run every subdomain in its own thread; returns per-rank field dicts
-    (and per-step diag norms of rank 0 when diag=True)."""
+    (and per-step diag norms of rank 0 when diag=True); probe(model) after
+    the steps lands as the 6th item of each rank's tuple."""
     n = npx * npe
     _group[0] += 1
     grp = _group[0]
@@ -70,7 +71,7 @@ def run_decomposed(case, npx, npe, nsteps, fields=FIELDS, diag=False):
                 if diag and rank == 0:
                     norms.append(d)
             m.sync()
-            out[rank] = (m.iSW, m.jSW, m.Lm, m.Mm, {f: m.get(f) for f in fields})
+            out[rank] = (m.iSW, m.jSW, m.Lm, m.Mm, {f: m.get(f) for f in fields}, probe(m) if probe else None)
             m.close()
             romsgpu.comm_destroy(h)
         except Exception as e:  # surfaced in the main thread
@@ -106,7 +107,7 @@ def check_decomposition(case, npx, npe, nsteps=5, fields=None):
     m.close()
     parts, _ = run_decomposed(case, npx, npe, nsteps, fields=fields)
     bad = []
-    for rank, (iSW, jSW, Lm, Mm, got) in enumerate(parts):
+    for rank, (iSW, jSW, Lm, Mm, got, _) in enumerate(parts):
         jn, inn = divmod(rank, npx)
         # owned cells: interior + the closed-edge ghost row/column the BC code sets
         i_lo = 0 if (not per and inn == 0) else 1
@@ -138,6 +139,41 @@ def test_fast_loop_overlap_bitwise(kind, monkeypatch):
     equal the single-domain run bitwise."""
     monkeypatch.setenv("ROMS_GPU_S2D_OVERLAP", "1")
     test_decomposition_bitwise_equals_single_domain(kind, 2, 2)
+
+
+@pytest.mark.parametrize("k", ["1", "3", "4"])
+@pytest.mark.parametrize("kind,npx,npe", [("filament", 2, 2), ("basin", 3, 2), ("basin_lmd", 2, 2),
+                                          ("basin_flux", 1, 2), ("filament", 3, 2)])
+def test_fast_loop_exchange_interval_bitwise(kind, npx, npe, k, monkeypatch):
+    """Barotropic exchange reduction (launch_step2d): the fast loop swaps
+    zeta/ubar/vbar 2K deep after every K-th fast step and recomputes the
+    overlap in between, instead of the reference's 2-deep swap after every
+    fast step (step2d_FB.F:572-574).  K = 1 (every step), 3 and 4 give
+    subdomains bitwise equal to the single-domain run, as the default K = 2
+    does in test_decomposition_bitwise_equals_single_domain."""
+    monkeypatch.setenv("ROMS_GPU_S2D_K", k)
+    check_decomposition(_case(kind), npx, npe)
+
+
+def test_fast_loop_exchange_count(monkeypatch):
+    """Exchanges per whole step on a 2x2 grid: one per fast step at K = 1;
+    with K > 1 one per K fast steps plus the start-of-loop swap of the fast
+    step's other inputs, and nothing else changes."""
+    case = _case("basin")
+    got = {}
+    for k in ("1", "2", "3", "4"):
+        monkeypatch.setenv("ROMS_GPU_S2D_K", k)
+        parts, _ = run_decomposed(case, 2, 2, 2, fields=("zeta",), probe=lambda m: m.halo_exchanges() + (m.t.nfast,))
+        counts = {p[5] for p in parts}
+        assert len(counts) == 1, counts   # every rank enqueues the same exchanges
+        got[int(k)] = counts.pop()
+    n1, k1, nfast = got[1]
+    assert k1 == 1 and nfast > 8
+    for k in (2, 3, 4):
+        nk, kk, _ = got[k]
+        assert kk == k
+        assert nk == n1 - nfast + (nfast + k - 1) // k + 1, (k, nk, n1, nfast)
+    print("exchanges per step (K: count):", {k: v[0] for k, v in got.items()}, "nfast", nfast)
 
 
 def test_filament_3x2_matches_golden_digits():

@@ -14,6 +14,7 @@ enum HaloDir : int { kW = 0, kE, kS, kN, kSW, kSE, kNW, kNE };
 struct HaloGeom {
   int Lm, Mm, nx2;
   long n2;
+  int w;           // strip width: 2 (the reference's halo), 2*s2d_k for the fast loop's wide exchanges
   int j0, j1;      // rows of the W/E strips
   int i0, i1;      // columns of the S/N strips
   int active[8];   // neighbour present in direction d
@@ -54,6 +55,8 @@ struct HaloIpc {
 struct Halo {
   RomsComm* comm = nullptr;
   HaloPlan plan{};
+  HaloPlan wide{};         // same neighbours, w-wide strips (ExchList::w > 2; wide.g.w == 0: none)
+  long nexch = 0;          // exchanges enqueued since setup (host count; roms_gpu_exchange_count)
   double* sbuf = nullptr;  // 8 x cap send messages
   double* rbuf = nullptr;  // 8 x cap receive messages
   double* dred = nullptr;  // gather staging
@@ -78,8 +81,10 @@ void comm_destroy(RomsComm* c);
 int comm_rank(const RomsComm* c);
 int comm_size(const RomsComm* c);
 
-HaloPlan halo_plan(int Lm, int Mm, int npx, int npe, int inode, int jnode, int ewp, int nsp);
-int halo_setup(Halo& H, RomsComm* comm, const HaloPlan& plan, int maxlev, std::string& err);
+HaloPlan halo_plan(int Lm, int Mm, int npx, int npe, int inode, int jnode, int ewp, int nsp, int w = 2);
+// wide: the w-wide plan of the fast loop (w == 0: none), wide_maxlev its largest list
+int halo_setup(Halo& H, RomsComm* comm, const HaloPlan& plan, int maxlev, const HaloPlan& wide, int wide_maxlev,
+               std::string& err);
 void halo_free(Halo& H);
 bool halo_graph_safe(const Halo* H);
 long halo_map(const HaloPlan& P, int dir, int unpack, int* iv, int* jv);

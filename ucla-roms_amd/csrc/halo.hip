@@ -37,30 +37,32 @@ namespace roms {
 namespace {
 constexpr int kOpp[8] = {kE, kW, kN, kS, kNE, kNW, kSE, kSW};
 
+// strips are g.w wide (2: the reference's halo; wider for the fast loop's
+// exchanges); corners g.w x g.w
 __host__ __device__ __forceinline__ void halo_src(const HaloGeom& g, int dir, long e, int& i, int& j) {
-  const int nxs = g.i1 - g.i0 + 1;
+  const int nxs = g.i1 - g.i0 + 1, w = g.w;
   switch (dir) {
-    case kW: i = 1 + (int)(e % 2); j = g.j0 + (int)(e / 2); break;
-    case kE: i = g.Lm - 1 + (int)(e % 2); j = g.j0 + (int)(e / 2); break;
+    case kW: i = 1 + (int)(e % w); j = g.j0 + (int)(e / w); break;
+    case kE: i = g.Lm - w + 1 + (int)(e % w); j = g.j0 + (int)(e / w); break;
     case kS: i = g.i0 + (int)(e % nxs); j = 1 + (int)(e / nxs); break;
-    case kN: i = g.i0 + (int)(e % nxs); j = g.Mm - 1 + (int)(e / nxs); break;
-    case kSW: i = 1 + (int)(e % 2); j = 1 + (int)(e / 2); break;
-    case kSE: i = g.Lm - 1 + (int)(e % 2); j = 1 + (int)(e / 2); break;
-    case kNW: i = 1 + (int)(e % 2); j = g.Mm - 1 + (int)(e / 2); break;
-    default: i = g.Lm - 1 + (int)(e % 2); j = g.Mm - 1 + (int)(e / 2); break;
+    case kN: i = g.i0 + (int)(e % nxs); j = g.Mm - w + 1 + (int)(e / nxs); break;
+    case kSW: i = 1 + (int)(e % w); j = 1 + (int)(e / w); break;
+    case kSE: i = g.Lm - w + 1 + (int)(e % w); j = 1 + (int)(e / w); break;
+    case kNW: i = 1 + (int)(e % w); j = g.Mm - w + 1 + (int)(e / w); break;
+    default: i = g.Lm - w + 1 + (int)(e % w); j = g.Mm - w + 1 + (int)(e / w); break;
   }
 }
 __host__ __device__ __forceinline__ void halo_dst(const HaloGeom& g, int h, long e, int& i, int& j) {
-  const int nxs = g.i1 - g.i0 + 1;
+  const int nxs = g.i1 - g.i0 + 1, w = g.w;
   switch (h) {
-    case kW: i = -1 + (int)(e % 2); j = g.j0 + (int)(e / 2); break;
-    case kE: i = g.Lm + 1 + (int)(e % 2); j = g.j0 + (int)(e / 2); break;
-    case kS: i = g.i0 + (int)(e % nxs); j = -1 + (int)(e / nxs); break;
+    case kW: i = 1 - w + (int)(e % w); j = g.j0 + (int)(e / w); break;
+    case kE: i = g.Lm + 1 + (int)(e % w); j = g.j0 + (int)(e / w); break;
+    case kS: i = g.i0 + (int)(e % nxs); j = 1 - w + (int)(e / nxs); break;
     case kN: i = g.i0 + (int)(e % nxs); j = g.Mm + 1 + (int)(e / nxs); break;
-    case kSW: i = -1 + (int)(e % 2); j = -1 + (int)(e / 2); break;
-    case kSE: i = g.Lm + 1 + (int)(e % 2); j = -1 + (int)(e / 2); break;
-    case kNW: i = -1 + (int)(e % 2); j = g.Mm + 1 + (int)(e / 2); break;
-    default: i = g.Lm + 1 + (int)(e % 2); j = g.Mm + 1 + (int)(e / 2); break;
+    case kSW: i = 1 - w + (int)(e % w); j = 1 - w + (int)(e / w); break;
+    case kSE: i = g.Lm + 1 + (int)(e % w); j = 1 - w + (int)(e / w); break;
+    case kNW: i = 1 - w + (int)(e % w); j = g.Mm + 1 + (int)(e / w); break;
+    default: i = g.Lm + 1 + (int)(e % w); j = g.Mm + 1 + (int)(e / w); break;
   }
 }
 // (array, level) of list-level index lev
@@ -257,23 +259,25 @@ int comm_rank(const RomsComm* c) { return c ? c->rank : 0; }
 int comm_size(const RomsComm* c) { return c ? c->nranks : 1; }
 
 // neighbour table and message geometry from the processor grid (mpi_setup.F:59-139)
-HaloPlan halo_plan(int Lm, int Mm, int npx, int npe, int inode, int jnode, int ewp, int nsp) {
+HaloPlan halo_plan(int Lm, int Mm, int npx, int npe, int inode, int jnode, int ewp, int nsp, int width) {
   HaloPlan P{};
   HaloGeom& g = P.g;
   g.Lm = Lm; g.Mm = Mm; g.nx2 = Lm + 4; g.n2 = (long)(Lm + 4) * (Mm + 4);
-  const bool w = ewp || inode > 0, e = ewp || inode < npx - 1;
+  g.w = width;
+  const int w = width;
+  const bool wn = ewp || inode > 0, e = ewp || inode < npx - 1;
   const bool s = nsp || jnode > 0, n = nsp || jnode < npe - 1;
   g.j0 = s ? 1 : 0; g.j1 = n ? Mm : Mm + 1;
-  g.i0 = w ? 1 : 0; g.i1 = e ? Lm : Lm + 1;
-  const bool act[8] = {w, e, s, n, s && w, s && e, n && w, n && e};
+  g.i0 = wn ? 1 : 0; g.i1 = e ? Lm : Lm + 1;
+  const bool act[8] = {wn, e, s, n, s && wn, s && e, n && wn, n && e};
   const int di[8] = {-1, 1, 0, 0, -1, 1, -1, 1}, dj[8] = {0, 0, -1, 1, -1, -1, 1, 1};
   for (int d = 0; d < 8; d++) {
     g.active[d] = act[d];
     const int in = (inode + di[d] + npx) % npx, jn = (jnode + dj[d] + npe) % npe;
     P.peer[d] = act[d] ? in + jn * npx : -1;
-    if (d < 2) g.cnt[d] = 2L * (g.j1 - g.j0 + 1);
-    else if (d < 4) g.cnt[d] = 2L * (g.i1 - g.i0 + 1);
-    else g.cnt[d] = 4;
+    if (d < 2) g.cnt[d] = (long)w * (g.j1 - g.j0 + 1);
+    else if (d < 4) g.cnt[d] = (long)w * (g.i1 - g.i0 + 1);
+    else g.cnt[d] = (long)w * w;
     if (!act[d]) g.cnt[d] = 0;
   }
   return P;
@@ -287,7 +291,7 @@ static void ipc_release(Halo& H);
 // neighbours' blocks.  Only the IPC self-test uses it: it is the reference
 // the peer-write transport must reproduce bitwise before it is enabled.
 static int exchange_host(const Halo& H, hipStream_t s, const ExchList& L) {
-  const HaloGeom& g = H.plan.g;
+  const HaloGeom& g = L.w > 2 ? H.wide.g : H.plan.g;
   RomsComm* c = H.comm;
   int nl = 0;
   for (int q = 0; q < L.n; q++) nl += L.nlev[q];
@@ -447,12 +451,18 @@ bool halo_failed(const Halo& H) {
   return H.ipc.ok && H.ipc.err_host && __atomic_load_n(H.ipc.err_host, __ATOMIC_ACQUIRE) != 0;
 }
 
-int halo_setup(Halo& H, RomsComm* comm, const HaloPlan& plan, int maxlev, std::string& err) {
+int halo_setup(Halo& H, RomsComm* comm, const HaloPlan& plan, int maxlev, const HaloPlan& wide, int wide_maxlev,
+               std::string& err) {
   H.comm = comm;
   H.plan = plan;
-  long mx = 0;
+  H.wide = wide;
+  H.nexch = 0;
+  long mx = 0, mxw = 0;
   for (int d = 0; d < 8; d++) mx = plan.g.cnt[d] > mx ? plan.g.cnt[d] : mx;
-  H.cap = mx * (long)maxlev;
+  if (wide.g.w > 0)
+    for (int d = 0; d < 8; d++) mxw = wide.g.cnt[d] > mxw ? wide.g.cnt[d] : mxw;
+  // one slot of a message buffer holds the largest message of either plan
+  H.cap = mx * (long)maxlev > mxw * (long)wide_maxlev ? mx * (long)maxlev : mxw * (long)wide_maxlev;
   if (hipMalloc(&H.sbuf, (size_t)8 * H.cap * sizeof(double)) != hipSuccess ||
       hipMalloc(&H.rbuf, (size_t)8 * H.cap * sizeof(double)) != hipSuccess ||
       hipMalloc(&H.dred, (size_t)64 * (1 + (comm ? comm->nranks : 1)) * sizeof(double)) != hipSuccess) {
@@ -492,7 +502,7 @@ int halo_setup(Halo& H, RomsComm* comm, const HaloPlan& plan, int maxlev, std::s
   }
   if (comm && comm->kind == 3) {
     // the host-staged self-test blocks: every rank uses the largest message of any rank
-    double mine = (double)mx;
+    double mine = (double)(mx > mxw ? mx : mxw);
     std::vector<double> all((size_t)comm->nranks);
     if (halo_allgather(H, H.cs, &mine, 1, all.data()) != 0) {
       err = "halo_setup: host-channel allgather failed";
@@ -506,6 +516,7 @@ int halo_setup(Halo& H, RomsComm* comm, const HaloPlan& plan, int maxlev, std::s
       return -5;
     }
   }
+  H.nexch = 0;   // the self-test's exchanges do not count
   return 0;
 }
 static void ipc_release(Halo& H) {
@@ -554,25 +565,30 @@ IpcPtrs ipc_ptrs(const Halo& H) {
   P.timeout = H.ipc.timeout_ticks;
   return P;
 }
-void exchange_ipc(const Halo& H, hipStream_t s, const ExchList& L, const dim3& grid) {
+void exchange_ipc(const Halo& H, hipStream_t s, const HaloGeom& g, const ExchList& L, const dim3& grid) {
   const IpcPtrs P = ipc_ptrs(H);
-  hipLaunchKernelGGL(k_halo_pack_ipc, grid, dim3(256), 0, s, H.plan.g, L, P, H.cap);
+  hipLaunchKernelGGL(k_halo_pack_ipc, grid, dim3(256), 0, s, g, L, P, H.cap);
   const int drop = H.ipc.drop_at >= 0 && H.ipc.nexch++ == H.ipc.drop_at;
-  hipLaunchKernelGGL(k_halo_wait_ipc, dim3(1), dim3(64), 0, s, H.plan.g, P, drop);
-  hipLaunchKernelGGL(k_halo_unpack_ipc, grid, dim3(256), 0, s, H.plan.g, L, P, H.cap);
+  hipLaunchKernelGGL(k_halo_wait_ipc, dim3(1), dim3(64), 0, s, g, P, drop);
+  hipLaunchKernelGGL(k_halo_unpack_ipc, grid, dim3(256), 0, s, g, L, P, H.cap);
 }
 }  // namespace
 
 void halo_exchange(const Halo& H, hipStream_t s, const ExchList& L) {
-  const HaloGeom& g = H.plan.g;
+  const HaloGeom& g = L.w > 2 ? H.wide.g : H.plan.g;
+  if (L.w > 2 && g.w != L.w) {
+    fprintf(stderr, "roms_gpu: %d-wide exchange without a matching halo plan (wide plan %d)\n", L.w, g.w);
+    std::abort();
+  }
   int nl = 0;
   for (int q = 0; q < L.n; q++) nl += L.nlev[q];
   if (nl == 0) return;
+  const_cast<Halo&>(H).nexch++;
   long mx = 0;
   for (int d = 0; d < 8; d++) mx = g.cnt[d] > mx ? g.cnt[d] : mx;
   const dim3 grid((unsigned)((mx + 255) / 256), (unsigned)nl, 8);
   if (H.ipc.ok) {
-    exchange_ipc(H, s, L, grid);
+    exchange_ipc(H, s, g, L, grid);
     return;
   }
   hipLaunchKernelGGL(k_halo_pack, grid, dim3(256), 0, s, g, L, H.sbuf, H.cap);

@@ -224,17 +224,25 @@ __global__ void __launch_bounds__(256) k_count_nonzero(const double* __restrict_
 __global__ void __launch_bounds__(256) k_fill_ones(double* __restrict__ p, long n) {
   for (long q = blockIdx.x * 256L + threadIdx.x; q < n; q += (long)gridDim.x * 256L) p[q] = 1.0;
 }
-__global__ void __launch_bounds__(256) k_rows_copy(double* __restrict__ dst, long dpitch, const double* __restrict__ src,
-                                                   long spitch, long width, long rows) {
+// rows of `width` doubles, `prow` rows per plane: row r of plane p sits at
+// p*plane + r*pitch on either side (host planes: compact rows; device planes:
+// nx2-pitched rows, plane stride n2 with the wide-halo rows, roms_dev.h)
+__global__ void __launch_bounds__(256) k_rows_copy(double* __restrict__ dst, long dpitch, long dplane,
+                                                   const double* __restrict__ src, long spitch, long splane,
+                                                   long width, long rows, long prow) {
   const long n = width * rows;
   for (long q = blockIdx.x * 256L + threadIdx.x; q < n; q += (long)gridDim.x * 256L) {
     const long r = q / width, c = q - r * width;
-    dst[r * dpitch + c] = src[r * spitch + c];
+    const long pl = r / prow, rr = r - pl * prow;
+    dst[pl * dplane + rr * dpitch + c] = src[pl * splane + rr * spitch + c];
   }
 }
-void launch_rows_copy(double* dst, long dpitch, const double* src, long spitch, long width, long rows, hipStream_t s) {
+void launch_rows_copy(double* dst, long dpitch, long dplane, const double* src, long spitch, long splane, long width,
+                      long rows, long prow, hipStream_t s) {
   const long n = width * rows, nb = (n + 255) / 256;
-  if (n > 0) hipLaunchKernelGGL(k_rows_copy, dim3((unsigned)(nb < 65536 ? nb : 65536)), dim3(256), 0, s, dst, dpitch, src, spitch, width, rows);
+  if (n > 0)
+    hipLaunchKernelGGL(k_rows_copy, dim3((unsigned)(nb < 65536 ? nb : 65536)), dim3(256), 0, s, dst, dpitch, dplane, src,
+                       spitch, splane, width, rows, prow);
 }
 void launch_fill_ones(double* p, long n, hipStream_t s) {
   hipLaunchKernelGGL(k_fill_ones, dim3(2048), dim3(256), 0, s, p, n);

@@ -575,6 +575,12 @@ __global__ void __launch_bounds__(kFT) k_prsgrd_fused(Dev d, Range R, int split,
   }
 }
 
+// prsgrd's hydrostatic pressure P alone (the two-kernel form's first kernel)
+void launch_prsgrd_P(const Dev& d, hipStream_t s) {
+  const Bounds& b = d.b;
+  Range R1{0, b.Lm, 0, b.Mm};
+  hipLaunchKernelGGL(k_prsgrd_P, grid_of(R1), dim3(kBX, kBY), 0, s, d, R1, d.p.nonlin_eos, d.p.tides);
+}
 void launch_prsgrd(const Dev& d, hipStream_t s, const Tlev& t, int uv_up, bool p_ready) {
   const Bounds& b = d.b;
   if (d.p.iso && t.nrhs == 3) launch_iso_slopes(d, s);   // ADV_ISONEUTRAL, CORR_STAGE (prsgrd.F:307-338)

@@ -247,7 +247,10 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int cl
   const int tid = threadIdx.x + kBX * threadIdx.y;
   constexpr int NT = kBX * kBY;
   auto G = [&](int i, int j) { return (i - (i0 - 2)) + (j - (j0 - 2)) * kGX; };
-  auto inarr = [&](int i, int j) { return i >= -1 && i <= b.Lm + 2 && j >= -1 && j <= b.Mm + 2; };
+  // inside the allocated planes (wide fast halos: gx more ghost cells, roms_dev.h)
+  auto inarr = [&](int i, int j) {
+    return i >= -1 - b.gx && i <= b.Lm + 2 + b.gx && j >= -1 - b.gx && j <= b.Mm + 2 + b.gx;
+  };
   // vwrap: single-rank periodic directions read the fast-time fields' halo
   // cells from their periodic images (the per-step wrap is deferred to the
   // end of the fast loop, see launch_step2d)
@@ -281,7 +284,7 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int cl
     f_a[r] = f_b[r] = f_c[r] = f_d[r] = 0.0;
     if (q < kUN) {
       const int i = i0 - 1 + q % kUX, j = j0 - 1 + q / kUX;
-      if (i >= 0 && inarr(i, j)) {
+      if (i >= -b.gx && inarr(i, j)) {   // DUon needs Drhs(i-1)
         const long ij = IJ(b, i, j), ft = FT(i, j);
         f_a[r] = F.ubar[ft + (long)(c.kstp - 1) * n2]; f_b[r] = F.ubar[ft + (long)(c.kbak - 1) * n2];
         f_c[r] = F.ubar[ft + (long)(c.kold - 1) * n2]; f_d[r] = F.dn_u[ij];
@@ -289,7 +292,7 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int cl
     } else if (q < kUN + kVN) {
       const int qq = q - kUN;
       const int i = i0 - 1 + qq % kFX, j = j0 - 1 + qq / kFX;
-      if (j >= 0 && inarr(i, j)) {
+      if (j >= -b.gx && inarr(i, j)) {   // DVom needs Drhs(j-1)
         const long ij = IJ(b, i, j), ft = FT(i, j);
         f_a[r] = F.vbar[ft + (long)(c.kstp - 1) * n2]; f_b[r] = F.vbar[ft + (long)(c.kbak - 1) * n2];
         f_c[r] = F.vbar[ft + (long)(c.kold - 1) * n2]; f_d[r] = F.dm_v[ij];
@@ -349,7 +352,7 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int cl
     if (q < kUN) {
       const int i = i0 - 1 + q % kUX, j = j0 - 1 + q / kUX;
       double v = 0.0;
-      if (i >= 0 && inarr(i, j)) {
+      if (i >= -b.gx && inarr(i, j)) {   // DUon needs Drhs(i-1)
         const double urhs = c.fwd * f_a[r] + c.fwd1 * f_b[r] + c.fwd2 * f_c[r];
         v = 0.5 * (T.Dr[G(i, j)] + T.Dr[G(i - 1, j)]) * f_d[r] * (urhs);
       }
@@ -358,7 +361,7 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int cl
       const int qq = q - kUN;
       const int i = i0 - 1 + qq % kFX, j = j0 - 1 + qq / kFX;
       double v = 0.0;
-      if (j >= 0 && inarr(i, j)) {
+      if (j >= -b.gx && inarr(i, j)) {   // DVom needs Drhs(j-1)
         const double vrhs = c.fwd * f_a[r] + c.fwd1 * f_b[r] + c.fwd2 * f_c[r];
         v = 0.5 * (T.Dr[G(i, j)] + T.Dr[G(i, j - 1)]) * f_d[r] * (vrhs);
       }
@@ -607,7 +610,7 @@ __global__ void k_s2d_edges(Dev d, FBCoef c, int phase) {
   const Fields& F = d.f;
   const long n2 = b.n2, kn = (long)(c.knew - 1) * n2, ksl = (long)(c.kstp - 1) * n2;
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  const int L = b.Lm + 4 > b.Mm + 4 ? b.Lm + 4 : b.Mm + 4;  // edge lanes per side
+  const int L = (b.Lm > b.Mm ? b.Lm : b.Mm) + 4 + 2 * b.gx;  // edge lanes per side
   const int side = p / L, q = p - side * L;
   if (side > 3) return;
   double* ub = F.ubar + kn;
@@ -826,6 +829,8 @@ __global__ void __launch_bounds__(256) k_s2d_last(Dev d, Range R, int knew) {
   d.f.zeta[ij + (long)(knew - 1) * d.b.n2] = d.f.Zt_avg1[ij];
 }
 
+void launch_fast_step(const Dev& d, hipStream_t s, const FBCoef& c, const Tlev& t);
+
 void launch_step2d(const Dev& d, hipStream_t s, const Tlev& t, const double* w1, const double* w2) {
   const Bounds& b = d.b;
   FBCoef c;
@@ -847,6 +852,89 @@ void launch_step2d(const Dev& d, hipStream_t s, const Tlev& t, const double* w1,
   }
   c.w1 = w1[t.iif - 1];
   c.w2 = w2[t.iif - 1];
+  // Multi-rank fast loop with wide halos (Params::s2d_k = K > 1): the
+  // zeta/ubar/vbar levels are exchanged 2K deep after every K-th fast step
+  // only.  One fast step reads its inputs up to 2 cells beyond the cells it
+  // updates, so the m-th step of a group updates the subdomain widened by
+  // 2(K-m) cells on every exchange side -- the same cells, with the same
+  // inputs and operations, as the neighbour owning them -- and the group's
+  // last step updates the subdomain alone.  The exchange after it carries the
+  // group's last min(K,3) levels (the AB3 steps read three).  The fields the
+  // fast step reads besides those levels are exchanged 2K deep before the
+  // first fast step.  Rivers and pipes (their face lists are the owner's)
+  // take every step.
+  const Halo* Hk = d.halo;
+  const int K = (d.p.s2d_k > 1 && Hk && Hk->comm && Hk->wide.g.w == 2 * d.p.s2d_k && d.p.npip == 0 &&
+                 d.p.nriv == 0 && !d.p.s2d_split) ? d.p.s2d_k : 1;
+  const int gend = K > 1 ? ((t.iif - 1) / K + 1) * K < t.nfast ? ((t.iif - 1) / K + 1) * K : t.nfast : t.iif;
+  Dev de = d;   // the bounds this fast step updates
+  if (K > 1) {
+    const long n2 = b.n2, ks = (long)(t.kstp - 1) * n2;
+    const int w = 2 * K;
+    if (t.iif == 1) {
+      const Fields& F = d.f;
+      launch_exchange_list(d, s, ExchList{{F.zeta + ks, F.ubar + ks, F.vbar + ks, F.rufrc, F.rvfrc, F.rhoS, F.rhoA, F.swflx,
+                                           F.h, F.pm, F.pn, F.dn_u, F.dm_v, F.rmask, F.umask, F.vmask},
+                                          {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1}, 16, w});
+    }
+    const int ext = 2 * (gend - t.iif);
+    Bounds& e = de.b;
+    if (!e.west_edge) e.istr -= ext;
+    if (!e.east_edge) e.iend += ext;
+    if (!e.south_edge) e.jstr -= ext;
+    if (!e.north_edge) e.jend += ext;
+    e.istrR = e.west_edge ? e.istr - 1 : e.istr;
+    e.istrU = e.west_edge ? e.istr + 1 : e.istr;
+    e.iendR = e.east_edge ? e.iend + 1 : e.iend;
+    e.jstrR = e.south_edge ? e.jstr - 1 : e.jstr;
+    e.jstrV = e.south_edge ? e.jstr + 1 : e.jstr;
+    e.jendR = e.north_edge ? e.jend + 1 : e.jend;
+  }
+  launch_fast_step(de, s, c, t);
+  launch_river_s2d(d, s, t.knew);   // step2d_FB.F:531-554
+  if (t.iif == t.nfast) {
+    const Range RB{b.istrR, b.iendR, b.jstrR, b.jendR};
+    hipLaunchKernelGGL(k_s2d_last, grid_of(RB), dim3(kBX, kBY), 0, s, d, RB, t.knew);
+    launch_set_depth(d, s, t);
+  }
+  const int vwrap = (d.halo == nullptr && !d.p.s2d_split) ? (b.ew_periodic ? 1 : 0) | (b.ns_periodic ? 2 : 0) : 0;
+  if (vwrap) {
+    // halos were read from periodic images during the loop; refresh all four
+    // time slots once at its end (the same values the per-step wraps give)
+    if (t.iif == t.nfast) launch_exchange_list(d, s, ExchList{{d.f.zeta, d.f.ubar, d.f.vbar}, {4, 4, 4}, 3});
+    return;
+  }
+  if (K > 1) {
+    if (t.iif != gend) return;
+    const int gstart = ((t.iif - 1) / K) * K + 1;
+    const int nl = t.iif - gstart + 1 < 3 ? t.iif - gstart + 1 : 3;
+    ExchList L{};
+    for (int m = 0; m < nl; m++) {
+      const long kl = (long)((((t.knew - 1 - m) % 4) + 4) % 4) * b.n2;   // knew of fast step iif-m
+      L.p[L.n] = d.f.zeta + kl; L.nlev[L.n++] = 1;
+      L.p[L.n] = d.f.ubar + kl; L.nlev[L.n++] = 1;
+      L.p[L.n] = d.f.vbar + kl; L.nlev[L.n++] = 1;
+    }
+    L.w = 2 * K;
+    launch_exchange_list(d, s, L);
+    return;
+  }
+  const long kn = (long)(t.knew - 1) * b.n2;
+  const ExchList L{{d.f.zeta + kn, d.f.ubar + kn, d.f.vbar + kn}, {1, 1, 1}, 3};
+  Halo* H = const_cast<Halo*>(d.halo);
+  if (H && H->overlap && t.iif < t.nfast && !d.p.s2d_split) {
+    // overlap the exchange with the next fast step's interior tiles; that
+    // step joins it before its rim tiles (the last fast step never forks)
+    halo_fork_exchange(*H, s, L);
+    return;
+  }
+  launch_exchange_list(d, s, L);
+}
+
+// one fast step's kernels over the bounds of d (launch_step2d): the fused
+// step (or the split form), then the open / closed edges
+void launch_fast_step(const Dev& d, hipStream_t s, const FBCoef& c, const Tlev& t) {
+  const Bounds& b = d.b;
   const bool closed = b.west_edge || b.east_edge || b.south_edge || b.north_edge;
   Range RB{b.istrR, b.iendR, b.jstrR, b.jendR};
   // closed walls folded into k_s2d_fb when no edge is open and every edge
@@ -894,32 +982,12 @@ void launch_step2d(const Dev& d, hipStream_t s, const Tlev& t, const double* w1,
     else if (t.iif == t.nfast) ktimer_mark(s, kTimedS2dFb, 1, t.nfast);
   }
   if (closed && !fold) {
-    const int L = b.Lm + 4 > b.Mm + 4 ? b.Lm + 4 : b.Mm + 4;
+    const int L = (b.Lm > b.Mm ? b.Lm : b.Mm) + 4 + 2 * b.gx;
     for (int ph = 0; ph < 4; ph++) {
       if (ph == 2 && !d.p.obc) continue;
       hipLaunchKernelGGL(k_s2d_edges, dim3(ph == 2 ? 1 : (4 * L + 255) / 256), dim3(ph == 2 ? 64 : 256), 0, s, d, c, ph);
     }
   }
-  launch_river_s2d(d, s, t.knew);   // step2d_FB.F:531-554
-  if (t.iif == t.nfast) {
-    hipLaunchKernelGGL(k_s2d_last, grid_of(RB), dim3(kBX, kBY), 0, s, d, RB, t.knew);
-    launch_set_depth(d, s, t);
-  }
-  if (vwrap) {
-    // halos were read from periodic images during the loop; refresh all four
-    // time slots once at its end (the same values the per-step wraps give)
-    if (t.iif == t.nfast) launch_exchange_list(d, s, ExchList{{d.f.zeta, d.f.ubar, d.f.vbar}, {4, 4, 4}, 3});
-    return;
-  }
-  const long kn = (long)(t.knew - 1) * b.n2;
-  const ExchList L{{d.f.zeta + kn, d.f.ubar + kn, d.f.vbar + kn}, {1, 1, 1}, 3};
-  if (H && H->overlap && t.iif < t.nfast && !d.p.s2d_split) {
-    // overlap the exchange with the next fast step's interior tiles; that
-    // step joins it before its rim tiles (the last fast step never forks)
-    halo_fork_exchange(*H, s, L);
-    return;
-  }
-  launch_exchange_list(d, s, L);
 }
 
 }  // namespace roms

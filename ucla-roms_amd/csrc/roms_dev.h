@@ -10,6 +10,15 @@
 // from i = 1 reads exactly four lines (at nx2 = Lm+4 the rows drift 32 B per
 // row against the lines and most such runs touch five).  Host copies re-pitch
 // the rows (roms_shim.cpp); no transpose anywhere.
+//
+// Wide fast-time halos (multi-rank, Bounds::gx > 0): every plane also holds
+// gx extra ghost rows below j = -1 and above j = Mm+2, and every row gx extra
+// ghost columns left of i = -1 and right of i = Lm+2.  The indexing above is
+// unchanged: the plane stride n2 covers Mm+4+2gx rows, the base of every
+// array sits gx rows into its allocation, and the columns i < -1 of row j are
+// the last gx doubles of row j-1's pitch (nx2 >= Lm+4+2gx keeps them apart
+// from that row's own columns).  Only the barotropic fast loop reads them
+// (launch_step2d: 2+gx-wide exchanges every 1+gx/2 fast steps).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstddef>
@@ -24,8 +33,9 @@ constexpr int kAlignOff = 14;  // base shift: element i = 1 (index 2 of a row) o
 // Loop bounds of the single tile that covers one rank's subdomain
 // (compute_tile_bounds.h, compute_auxiliary_bounds.h, compute_extended_bounds.h).
 struct Bounds {
-  int Lm, Mm, N, NT, nTS, nx2;   // nx2: device row pitch (>= Lm+4)
-  long n2, n3, n3w;
+  int Lm, Mm, N, NT, nTS, nx2;   // nx2: device row pitch (>= Lm+4+2gx)
+  long n2, n3, n3w;              // n2 = nx2 * (Mm+4+2gx): plane stride
+  int gx;                        // extra ghost rows/columns beyond the reference's 2 (wide fast halos)
   int istr, iend, jstr, jend;
   int istrU, istrR, iendR, jstrV, jstrR, jendR;   // auxiliary
   int istrE, iendE, jstrE, jendE;                  // extended
@@ -69,6 +79,7 @@ struct Params {
   int preuv_lds;  // k_pre_uv_seg: u(indx) stored and u(nstp)/u(indx) combined in the spline phase (ROMS_GPU_PREUV_LDS=0: reloads)
   int seg_jrows;  // rows j per block of the momentum segment solvers (1..kSegJMax; ROMS_GPU_SEG_JROWS)
   int seg_vtile;  // v columns of the momentum segment solvers on 16 x 4 tiles per wavefront (ROMS_GPU_SEG_VTILE=0: rows of 64)
+  int s2d_k;      // fast steps per zeta/ubar/vbar exchange (multi-rank, wide halos of 2*s2d_k; 1: every step)
   int npip;       // pipe_frc.F: number of pipes (0: pipe_source off)
   int nriv, nrivf;  // river_frc.F: number of rivers (0: river_source off), river faces
   int curvgrid;   // CURVGRID && UV_ADV: curvature terms (compute_horiz_rhs_uv_terms.h:8-11)
@@ -301,11 +312,14 @@ constexpr int kTimedPrsgrdUv = 17;   // ROMS_R_K_PRSGRD_UV
 void ktimer_mark(hipStream_t s, int kernel_id, int end, int count = 0);
 
 void launch_exchange(const Dev& d, hipStream_t s, double* a, int nlev);
-// several arrays in one launch (one reference exchange_xxx(A,B,C,D) call)
+// several arrays in one launch (one reference exchange_xxx(A,B,C,D) call);
+// w > 2: a wide exchange (halo w deep, Bounds::gx >= w-2; the fast loop's)
+constexpr int kExchMax = 16;
 struct ExchList {
-  double* p[8];
-  int nlev[8];
+  double* p[kExchMax];
+  int nlev[kExchMax];
   int n;
+  int w = 2;
 };
 void launch_exchange_list(const Dev& d, hipStream_t s, const ExchList& L);
 // ---- rim-first overlap of a producer's trailing exchange (SURVEY.md 8(e);
@@ -365,6 +379,7 @@ void launch_rho_eos(const Dev& d, hipStream_t s, const Tlev& t, int tidx);
 // p_ready: P is current from the last rho_eos (p_in_rho), k_prsgrd_P is skipped
 void launch_prsgrd(const Dev& d, hipStream_t s, const Tlev& t, int uv_up = -1, bool p_ready = false);
 bool p_in_rho(const Dev& d);   // every rho_eos also forms prsgrd's P (k_vertical.hip)
+void launch_prsgrd_P(const Dev& d, hipStream_t s);   // prsgrd's P alone (k_prsgrd_P)
 bool prsgrd_can_fuse_uv(const Dev& d);
 // A second stream for work with no data dependence on the main stream's
 // (enqueue_step, single rank): the callee forks `s2` off `s` with `efork`

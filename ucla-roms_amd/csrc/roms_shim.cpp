@@ -90,6 +90,7 @@ struct Ctx {
   // Routines with no data dependence between them run on two streams inside
   // the step (single rank; ROMS_GPU_PAR=0 serialises): see enqueue_step
   bool par = true;
+  long step_exch = 0;        // halo exchanges in the last enqueued step (roms_gpu_halo_exchanges)
   hipStream_t s2 = nullptr;
   hipEvent_t pev[8] = {};
 };
@@ -167,12 +168,13 @@ int post_launch() {
   return 0;
 }
 
-Bounds make_bounds(const roms_dims& D, int pitch) {
+Bounds make_bounds(const roms_dims& D, int pitch, int gx = 0) {
   Bounds b{};
   b.Lm = D.Lm; b.Mm = D.Mm; b.N = D.N; b.NT = D.NT;
   b.nTS = 1;
   b.nx2 = pitch;
-  b.n2 = (long)pitch * (D.Mm + 4);
+  b.gx = gx;
+  b.n2 = (long)pitch * (D.Mm + 4 + 2 * gx);
   b.n3 = b.n2 * D.N;
   b.n3w = b.n2 * (D.N + 1);
   b.istr = 1; b.iend = D.Lm; b.jstr = 1; b.jend = D.Mm;
@@ -268,21 +270,28 @@ double* dev_base(double* p) {
 // zero-initialised device array of n doubles (guard bands when g.guard)
 hipError_t dev_alloc(double*& p, long n) {
   const long G = g.guard ? 4096 : 0;
-  const long pad = g.off ? kRowAlign : 0;   // room for the alignment shift (hipMalloc is 256-B aligned)
+  const Bounds& b = g.d.b;
+  // alignment shift (hipMalloc is 256-B aligned) and, with wide fast halos,
+  // the gx ghost rows below the first plane's j = -1 plus the gx columns left
+  // of its i = -1 (roms_dev.h); the last plane's extra rows are inside n
+  const long lead = g.off ? g.off : b.gx;   // g.off = kAlignOff >= gx (checked at init)
+  const long pre = (long)b.gx * b.nx2 + lead;
+  const long pad = (g.off || b.gx) ? kRowAlign : 0;
   double* base = nullptr;
-  hipError_t e = hipMalloc(&base, (size_t)(n + 2 * G + pad) * sizeof(double));
+  hipError_t e = hipMalloc(&base, (size_t)(n + 2 * G + pad + (long)b.gx * b.nx2) * sizeof(double));
   if (e != hipSuccess) return e;
   if (G) {
-    e = hipMemsetD32((hipDeviceptr_t)base, 0x7FF87FF8, (size_t)(n + 2 * G + pad) * 2);   // NaN bit pattern
+    e = hipMemsetD32((hipDeviceptr_t)base, 0x7FF87FF8, (size_t)(n + 2 * G + pad + (long)b.gx * b.nx2) * 2);   // NaN bit pattern
     if (e != hipSuccess) return e;
   }
-  p = base + G + g.off;
-  if (G || g.off) g.guard_base[p] = base;
+  p = base + G + pre;
+  if (G || pre) g.guard_base[p] = base;
   // The library's kernels run on a non-blocking stream, which does not wait
   // for work on the null stream: the zero fill must have landed before the
   // first kernel reads the array, or it may see what a previous model left in
-  // the same memory (or be zeroed after the kernel wrote it).
-  e = hipMemset(p, 0, (size_t)n * sizeof(double));
+  // the same memory (or be zeroed after the kernel wrote it).  The fill covers
+  // the leading ghost rows too.
+  e = hipMemset(p - pre + lead - b.gx, 0, (size_t)(n + pre - lead + b.gx) * sizeof(double));
   return e != hipSuccess ? e : hipStreamSynchronize(nullptr);
 }
 
@@ -377,6 +386,7 @@ void enqueue_step(roms_tlev* t, bool rho_current, bool store_huv) {
   const Dev& d = g.d;
   hipStream_t s = g.s;
   Tlev T = to_tlev(t);
+  const long exch0 = g.halo.nexch;
   const bool pot = g.cfg.pot_tides != 0;
   g.rho_slot = 0;
   // Two streams where the reference's order has no data dependence (single
@@ -403,12 +413,23 @@ void enqueue_step(roms_tlev* t, bool rho_current, bool store_huv) {
   launch_bulk_flux(d, s, T.nrhs);   // set_forces (main.F:386): BULK_FRC only
   frc_step_phase(d, s, 1, pot);     // set_bry_all '1/2 fwd' + set_tides (main.F:389-394)
   if (!rho_current) TIMED(ROMS_R_RHO_EOS, launch_rho_eos(d, s, T, T.nrhs));
+  // every rho_eos of the library leaves P current (p_in_rho): the
+  // step-opening one, or the previous step's closing one it reuses; else
+  // (linear EOS) prsgrd's P integral (rho, z_r, z_w: nothing set_HUV or
+  // omega writes) runs on the side stream beside them
+  const bool p_ready = p_in_rho(d);
+  const bool p_side = par && !p_ready && d.p.prs_split;
+  if (p_side) {
+    fork(7);
+    launch_prsgrd_P(d, s2);
+  }
   TIMED(ROMS_R_SET_HUV, launch_set_huv(d, s, T, store_huv));
   // the predictor's omega also forms pre_step3d's Hz_bak/Hz_fwd (nothing in
   // between -- lmd_vmix, prsgrd -- writes FlxU, FlxV, Hz, We or Wi)
   bool hb_done = false;
   TIMED(ROMS_R_OMEGA, hb_done = launch_omega(d, s, T, d.p.omega_hb && d.p.hoist && T.nrhs != 3 ?
                                                           0.5 * pre_step3d_dtau(d, T) : 0.0));
+  if (p_side) join(7);
   const bool lmd2 = g.cfg.lmd_mixing && par;
   if (lmd2) {
     fork(0);
@@ -420,10 +441,7 @@ void enqueue_step(roms_tlev* t, bool rho_current, bool store_huv) {
   // prsgrd kernel just before them (prsgrd_can_fuse_uv; nothing between the
   // two touches u, v(nrhs), FlxU, FlxV, Hz or ru, rv)
   const bool fuse_uv = prsgrd_can_fuse_uv(d);
-  // every rho_eos of the library leaves P current (p_in_rho): the
-  // step-opening one, or the previous step's closing one it reuses
-  const bool p_ready = p_in_rho(d);
-  TIMED(ROMS_R_PRSGRD, launch_prsgrd(d, s, T, fuse_uv ? 0 : -1, p_ready));
+  TIMED(ROMS_R_PRSGRD, launch_prsgrd(d, s, T, fuse_uv ? 0 : -1, p_ready || p_side));
   if (lmd2) join(1);
   const Side side{s2, g.pev[5], g.pev[6]};
   TIMED(ROMS_R_PRE_STEP3D, launch_pre_step3d(d, s, T, fuse_uv, hb_done, par ? &side : nullptr));
@@ -465,6 +483,7 @@ void enqueue_step(roms_tlev* t, bool rho_current, bool store_huv) {
   if (g.cfg.ts_dif2) TIMED(ROMS_R_T3DMIX, launch_t3dmix(d, s, T));
   TIMED(ROMS_R_RHO_EOS, launch_rho_eos(d, s, T, T.nnew));
   g.rho_slot = T.nnew;
+  g.step_exch = g.halo.nexch - exch0;
 }
 
 }  // namespace
@@ -482,24 +501,27 @@ double* stage_get(long n) {
   }
   return g.stage;
 }
+// `rows` host rows: whole planes of Mm+4 rows (plane stride hb.n2 on the
+// host, b.n2 on the device)
+bool same_layout() { return g.d.b.nx2 == g.hb.nx2 && g.d.b.n2 == g.hb.n2; }
 hipError_t rows_h2d(double* dev, const double* host, long rows) {
   const Bounds& b = g.d.b;
   const long hx = g.hb.nx2, n = rows * hx;
-  if (b.nx2 == hx) return copy_on(dev, host, (size_t)n * sizeof(double), hipMemcpyHostToDevice, g.s);
+  if (same_layout()) return copy_on(dev, host, (size_t)n * sizeof(double), hipMemcpyHostToDevice, g.s);
   double* st = stage_get(n);
   if (!st) return hipErrorOutOfMemory;
   hipError_t e = hipMemcpyAsync(st, host, (size_t)n * sizeof(double), hipMemcpyHostToDevice, g.s);
   if (e != hipSuccess) return e;
-  launch_rows_copy(dev, b.nx2, st, hx, hx, rows, g.s);
+  launch_rows_copy(dev, b.nx2, b.n2, st, hx, g.hb.n2, hx, rows, b.Mm + 4, g.s);
   return hipStreamSynchronize(g.s);
 }
 hipError_t rows_d2h(double* host, const double* dev, long rows) {
   const Bounds& b = g.d.b;
   const long hx = g.hb.nx2, n = rows * hx;
-  if (b.nx2 == hx) return copy_on(host, dev, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, g.s);
+  if (same_layout()) return copy_on(host, dev, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, g.s);
   double* st = stage_get(n);
   if (!st) return hipErrorOutOfMemory;
-  launch_rows_copy(st, hx, dev, b.nx2, hx, rows, g.s);
+  launch_rows_copy(st, hx, g.hb.n2, dev, b.nx2, b.n2, hx, rows, b.Mm + 4, g.s);
   hipError_t e = hipMemcpyAsync(host, st, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, g.s);
   return e != hipSuccess ? e : hipStreamSynchronize(g.s);
 }
@@ -517,9 +539,11 @@ hipError_t field_d2h(int id, double* host, const double* dev) {
 template <class T>
 std::vector<T> to_dev_layout(const T* h, long planes) {
   const Bounds& b = g.d.b;
-  const long hx = g.hb.nx2, rows = (long)(b.Mm + 4) * planes;
+  const long hx = g.hb.nx2, prow = b.Mm + 4;
   std::vector<T> v((size_t)(b.n2 * planes), T(0));
-  for (long r = 0; r < rows; r++) std::memcpy(v.data() + r * b.nx2, h + r * hx, (size_t)hx * sizeof(T));
+  for (long p = 0; p < planes; p++)
+    for (long r = 0; r < prow; r++)
+      std::memcpy(v.data() + p * b.n2 + r * b.nx2, h + (p * prow + r) * hx, (size_t)hx * sizeof(T));
   return v;
 }
 
@@ -622,9 +646,28 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     const char* e = getenv("ROMS_GPU_PITCH");
     const bool pad = !(e && e[0] == '0');
     const int hx = dims->Lm + 4;
+    // Multi-rank runs: the barotropic fast loop exchanges zeta/ubar/vbar
+    // every s2d_k fast steps over 2*s2d_k-wide halos and recomputes the
+    // steps between on the overlap (launch_step2d), so the device planes
+    // carry gx = 2*(s2d_k-1) extra ghost rows/columns (roms_dev.h).  Not with
+    // open boundaries (their 1-D boundary arrays end at the reference's halo)
+    // or the split fast-step kernels; rivers and pipes fall back to every step
+    // at run time.  ROMS_GPU_S2D_K=1..4 (default 2; 1: every step).
+    int k = 2;
+    const char* ek = getenv("ROMS_GPU_S2D_K");
+    if (ek && ek[0] >= '1' && ek[0] <= '4') k = ek[0] - '0';
+    const char* es = getenv("ROMS_GPU_S2D_SPLIT");
+    const bool split = es && es[0] == '1';
+    const int obc = cfg->obc & ((dims->ew_periodic ? 0 : 3) | (dims->ns_periodic ? 0 : 12));
+    // every rank decides alike (global sizes; rank_extent's subdomains are
+    // at least LLm/np_xi - 2 wide, the 2k-wide strips must fit in all of them)
+    if (comm == nullptr || split || obc || dims->LLm / dims->np_xi < 2 * k + 2 || dims->MMm / dims->np_eta < 2 * k + 2) k = 1;
+    const int gx = 2 * (k - 1);
     g.off = pad ? kAlignOff : 0;
-    g.d.b = make_bounds(*dims, pad ? (hx + kRowAlign - 1) / kRowAlign * kRowAlign : hx);
+    const int w = hx + 2 * gx;
+    g.d.b = make_bounds(*dims, pad ? (w + kRowAlign - 1) / kRowAlign * kRowAlign : w, gx);
     g.hb = make_bounds(*dims, hx);
+    g.d.p.s2d_k = k;
   }
   g.d.b.nTS = g.hb.nTS = cfg->salinity ? 2 : 1;
   Params& P = g.d.p;
@@ -877,7 +920,14 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
                               dims->ew_periodic, dims->ns_periodic);
     plan.g.nx2 = b.nx2;   // the device row pitch: pack/unpack index the device arrays
     plan.g.n2 = b.n2;
-    const int r = halo_setup(g.halo, (RomsComm*)comm, plan, 8 * (dims->N + 1), g.err);
+    HaloPlan wide{};
+    if (P.s2d_k > 1) {
+      wide = halo_plan(dims->Lm, dims->Mm, dims->np_xi, dims->np_eta, dims->inode, dims->jnode, dims->ew_periodic,
+                       dims->ns_periodic, 2 * P.s2d_k);
+      wide.g.nx2 = b.nx2;
+      wide.g.n2 = b.n2;
+    }
+    const int r = halo_setup(g.halo, (RomsComm*)comm, plan, 8 * (dims->N + 1), wide, kExchMax, g.err);
     if (r) return r;
     g.d.halo = &g.halo;
   }
@@ -988,6 +1038,13 @@ ROUTINE(roms_gpu_set_depth, launch_set_depth(g.d, g.s, T))
 int roms_gpu_halo_transport(void) {
   REQUIRE_INIT_NOJOIN();
   return g.d.halo ? halo_transport(g.halo) : 0;
+}
+
+int roms_gpu_halo_exchanges(long* per_step, int* fast_interval) {
+  REQUIRE_INIT_NOJOIN();
+  if (per_step) *per_step = g.step_exch;
+  if (fast_interval) *fast_interval = g.d.p.s2d_k;
+  return 0;
 }
 
 int roms_gpu_step2d(const roms_tlev* t) {

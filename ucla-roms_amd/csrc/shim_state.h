@@ -49,8 +49,9 @@ long shim_field_dev_count(int field_id);   // elements of a field in the device 
 // host-layout field data (the ABI's, rows of Lm+4) into a device-layout
 // array of the field's shape, blocking on the library stream
 hipError_t shim_field_h2d(int field_id, double* dev, const double* host);
-hipError_t shim_rows_h2d(double* dev, const double* host, long rows);   // `rows` rows of Lm+4 -> nx2
-// dst[r*dpitch + c] = src[r*spitch + c], c < width, r < rows (device arrays; k_diag.hip)
-void launch_rows_copy(double* dst, long dpitch, const double* src, long spitch, long width, long rows, hipStream_t s);
+hipError_t shim_rows_h2d(double* dev, const double* host, long rows);   // `rows` rows of Lm+4 (whole planes of Mm+4) -> device planes
+// row r = p*prow + q: dst[p*dplane + q*dpitch + c] = src[p*splane + q*spitch + c], c < width (device arrays; k_diag.hip)
+void launch_rows_copy(double* dst, long dpitch, long dplane, const double* src, long spitch, long splane, long width,
+                      long rows, long prow, hipStream_t s);
 double* shim_scratch_small(long n);        // small device scratch owned by the context (>= n doubles)
 }  // namespace roms

@@ -526,6 +526,13 @@ class Model:
         r = self.L.roms_gpu_halo_transport()
         return {1: "ipc", 0: "rccl", -1: "ipc-timeout"}.get(r, "error")
 
+    def halo_exchanges(self):
+        """(exchanges in the last enqueued step, fast-loop exchange interval)
+        -- roms_gpu_halo_exchanges."""
+        n, k = ctypes.c_long(), ctypes.c_int()
+        self._chk(self.L.roms_gpu_halo_exchanges(ctypes.byref(n), ctypes.byref(k)), "halo_exchanges")
+        return n.value, k.value
+
     def diag(self):
         out = (ctypes.c_double * 4)()
         self._chk(self.L.roms_gpu_diag(ctypes.byref(self.t), out), "diag")
