@@ -141,15 +141,15 @@ def test_fast_loop_overlap_bitwise(kind, monkeypatch):
     test_decomposition_bitwise_equals_single_domain(kind, 2, 2)
 
 
-@pytest.mark.parametrize("k", ["1", "3", "4"])
+@pytest.mark.parametrize("k", ["1", "2", "3"])
 @pytest.mark.parametrize("kind,npx,npe", [("filament", 2, 2), ("basin", 3, 2), ("basin_lmd", 2, 2),
                                           ("basin_flux", 1, 2), ("filament", 3, 2)])
 def test_fast_loop_exchange_interval_bitwise(kind, npx, npe, k, monkeypatch):
     """Barotropic exchange reduction (launch_step2d): the fast loop swaps
     zeta/ubar/vbar 2K deep after every K-th fast step and recomputes the
     overlap in between, instead of the reference's 2-deep swap after every
-    fast step (step2d_FB.F:572-574).  K = 1 (every step), 3 and 4 give
-    subdomains bitwise equal to the single-domain run, as the default K = 2
+    fast step (step2d_FB.F:572-574).  K = 1 (every step), 2 and 3 give
+    subdomains bitwise equal to the single-domain run, as the default K = 4
     does in test_decomposition_bitwise_equals_single_domain."""
     monkeypatch.setenv("ROMS_GPU_S2D_K", k)
     check_decomposition(_case(kind), npx, npe)

@@ -230,8 +230,12 @@ struct FBTile {
   unsigned char st[kFN];  // 0: outside, 1: computed, 2: set by zetabc
 };
 
-template <bool kPipe>
-__global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int closed, int vwrap, int part) {
+// kClosed: 0 no closed edge, 1 closed edges finished by k_s2d_edges, 2 closed
+// walls folded in; kWrap: single-rank periodic images (vwrap bits).  Compile-
+// time switches, so each instance carries only its own branches.
+template <bool kPipe, int kClosed, bool kWrap>
+__global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int vwrap, int part) {
+  constexpr int closed = kClosed;
   const uint3 bI = xcd_tile();
   // part 1: interior tiles only (their windows hold no halo cell), 2: the rim
   // tiles, 0: all (see the fast-loop overlap in launch_step2d)
@@ -255,8 +259,8 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int cl
   // cells from their periodic images (the per-step wrap is deferred to the
   // end of the fast loop, see launch_step2d)
   auto FT = [&](int i, int j) -> long {
-    if (vwrap & 1) i = i < 1 ? i + b.Lm : (i > b.Lm ? i - b.Lm : i);
-    if (vwrap & 2) j = j < 1 ? j + b.Mm : (j > b.Mm ? j - b.Mm : j);
+    if (kWrap && (vwrap & 1)) i = i < 1 ? i + b.Lm : (i > b.Lm ? i - b.Lm : i);
+    if (kWrap && (vwrap & 2)) j = j < 1 ? j + b.Mm : (j > b.Mm ? j - b.Mm : j);
     return IJ(b, i, j);
   };
   // All global loads are issued at entry -- the staging window first, then
@@ -401,7 +405,7 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int cl
     T.rz2[q] = rzeta * zwrk;
   }
   __syncthreads();
-  if (closed) {
+  if (closed != 0) {
     // zetabc_tile (zetabc.F), closed walls: edges, then corners
     auto L = [&](int i, int j) { return (i - (i0 - 1)) + (j - (j0 - 1)) * kFX; };
     auto in = [&](int i, int j) { return i >= i0 - 1 && i <= i0 + kBX - 1 && j >= j0 - 1 && j <= j0 + kBY - 1; };
@@ -960,10 +964,19 @@ void launch_fast_step(const Dev& d, hipStream_t s, const FBCoef& c, const Tlev& 
     hipLaunchKernelGGL(k_s2d_mom, grid_of(RB), dim3(kBX, kBY), 0, s, d, RB, c);
   } else {
     auto fb = [&](int part) {
-      if (d.p.npip > 0)
-        hipLaunchKernelGGL(k_s2d_fb<true>, grid_of(RB), dim3(kBX, kBY), 0, s, d, RB, c, cmode, vwrap, part);
-      else
-        hipLaunchKernelGGL(k_s2d_fb<false>, grid_of(RB), dim3(kBX, kBY), 0, s, d, RB, c, cmode, vwrap, part);
+      const dim3 gr = grid_of(RB), bl(kBX, kBY);
+#define S2D_FB(P, C, W) hipLaunchKernelGGL((k_s2d_fb<P, C, W>), gr, bl, 0, s, d, RB, c, vwrap, part)
+      const bool wr = vwrap != 0;
+      if (d.p.npip > 0) {
+        if (cmode == 0) { if (wr) S2D_FB(true, 0, true); else S2D_FB(true, 0, false); }
+        else if (cmode == 1) { if (wr) S2D_FB(true, 1, true); else S2D_FB(true, 1, false); }
+        else { if (wr) S2D_FB(true, 2, true); else S2D_FB(true, 2, false); }
+      } else {
+        if (cmode == 0) { if (wr) S2D_FB(false, 0, true); else S2D_FB(false, 0, false); }
+        else if (cmode == 1) { if (wr) S2D_FB(false, 1, true); else S2D_FB(false, 1, false); }
+        else { if (wr) S2D_FB(false, 2, true); else S2D_FB(false, 2, false); }
+      }
+#undef S2D_FB
     };
     // kernel-level timing: one interval per fast loop when nothing else runs
     // between the fused kernels (single rank, no closed edges), else one per launch

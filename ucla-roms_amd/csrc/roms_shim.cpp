@@ -88,7 +88,7 @@ struct Ctx {
   double* stage = nullptr;
   long stage_n = 0;
   // Routines with no data dependence between them run on two streams inside
-  // the step (single rank; ROMS_GPU_PAR=0 serialises): see enqueue_step
+  // the step (single rank; opt-in, ROMS_GPU_PAR=1): see enqueue_step
   bool par = true;
   long step_exch = 0;        // halo exchanges in the last enqueued step (roms_gpu_halo_exchanges)
   hipStream_t s2 = nullptr;
@@ -652,8 +652,11 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     // carry gx = 2*(s2d_k-1) extra ghost rows/columns (roms_dev.h).  Not with
     // open boundaries (their 1-D boundary arrays end at the reference's halo)
     // or the split fast-step kernels; rivers and pipes fall back to every step
-    // at run time.  ROMS_GPU_S2D_K=1..4 (default 2; 1: every step).
-    int k = 2;
+    // at run time.  ROMS_GPU_S2D_K=1..4 (default 4; 1: every step).  One
+    // GPU with every exchange self-addressed through IPC (C2, 92 exchanges
+    // per step at K = 1): 7.48 / 7.11 / 7.01 / 6.98 ms per step at K = 1..4
+    // against 6.49 without a communicator (profiles/r4_j_fast_exchange_interval_ab.txt).
+    int k = 4;
     const char* ek = getenv("ROMS_GPU_S2D_K");
     if (ek && ek[0] >= '1' && ek[0] <= '4') k = ek[0] - '0';
     const char* es = getenv("ROMS_GPU_S2D_SPLIT");
@@ -868,8 +871,12 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
   CHECK_HIP(hipStreamCreateWithFlags(&g.s2, hipStreamNonBlocking));
   for (hipEvent_t& e : g.pev) CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   {
+    // measured slower than one stream (C3 60.5 -> 62.5, C2 6.40 -> 6.46 ms per
+    // step, profiles/r4_j_two_stream_ab.txt): the concurrent kernels compete
+    // for CUs and LDS (the segment solvers hold one block per CU), so the
+    // second stream is opt-in, ROMS_GPU_PAR=1
     const char* e = getenv("ROMS_GPU_PAR");
-    g.par = !(e && e[0] == '0');
+    g.par = e && e[0] == '1';
   }
   {
     const char* e = getenv("ROMS_GPU_GUARD");
