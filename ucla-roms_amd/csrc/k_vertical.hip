@@ -395,16 +395,8 @@ __global__ void __launch_bounds__(256) k_omega(Dev d, Range R, double dtau) {
 // pre_step3d writes them.  The flux differences of the level are kept in
 // dynamic LDS across the chain ([kOmR][threads], through an opaque offset).
 constexpr int kOmR = kSegRows;   // levels per wave (N <= kSegRows * kSegMaxS)
-// kFlx (the predictor's whole steps): set_HUV folded in.  The grid covers
-// set_HUV's range R (set_depth.F:190-234); every lane forms the fluxes of its
-// own faces and those of its i+1 / j+1 neighbours from u, v(nrhs) and Hz with
-// set_HUV's expression, stores its own FlxU / FlxV where set_HUV would, and
-// the lanes inside omega's range Ro carry on with omega on those fluxes: the
-// same values as set_HUV's stores (and, on the halo faces, as its exchange),
-// without the second pass over FlxU / FlxV.
-template <bool kHB, bool kFlx>
-__global__ void __launch_bounds__(kSegBlock, 2) k_omega_seg(Dev d, Range R, Range Ro, double dtau, double hcff,
-                                                           int nrhs) {
+template <bool kHB>
+__global__ void __launch_bounds__(kSegBlock, 2) k_omega_seg(Dev d, Range R, double dtau, double hcff) {
   const uint3 bI = xcd_tile();
   const Bounds& b = d.b;
   const Fields& F = d.f;
@@ -414,42 +406,15 @@ __global__ void __launch_bounds__(kSegBlock, 2) k_omega_seg(Dev d, Range R, Rang
   const SegSpan sg = seg_span(N);
   const int s = sg.s, S = sg.S, c0 = sg.c0, n = sg.n, l = sg.col;
   const int iu = tile_i0(R.i0) + (int)bI.x * kSegCW + l, ju = R.j0 + (int)bI.y;
-  const bool inR = iu >= R.i0 && iu <= R.i1 && ju <= R.j1;
+  const bool act = iu >= R.i0 && iu <= R.i1 && ju <= R.j1;
   const int i = iu < R.i0 ? R.i0 : (iu < R.i1 ? iu : R.i1), j = ju < R.j1 ? ju : R.j1;
-  const bool act = kFlx ? inR && i >= Ro.i0 && i <= Ro.i1 && j >= Ro.j0 && j <= Ro.j1 : inR;
   const long ij = IJ(b, i, j), n2 = b.n2, sj = b.nx2;
-  // kFlx: the fluxes are stored and read back by the same lane (no restrict)
-  const double* FU = F.FlxU + ij;
-  const double* FV = F.FlxV + ij;
+  const double* __restrict__ FU = F.FlxU + ij;
+  const double* __restrict__ FV = F.FlxV + ij;
   const double* __restrict__ Hz = F.Hz + ij;
   const double* __restrict__ zw = F.z_w + ij;
   __shared__ double Lw[kSegMaxS][kSegCW], Lcx[kSegMaxS][kSegCW], Lhz[kSegMaxS][kSegCW];
   __shared__ double Lte[kHB ? kSegMaxS : 1][kSegCW], Lti[kHB ? kSegMaxS : 1][kSegCW];   // kHB: segment tops' We, Wi
-  if constexpr (kFlx) {
-    // set_HUV of the wave's levels: every lane stores its own faces where
-    // set_HUV would (du / dv), and omega's lanes also the i+1 / j+1 faces
-    // they read (the same values as the owners store; on halo faces the
-    // exchange after the kernel writes them again, bitwise alike), so each
-    // lane below reads back only what it stored itself
-    const double* __restrict__ U = F.u + (long)(nrhs - 1) * b.n3 + ij;
-    const double* __restrict__ V = F.v + (long)(nrhs - 1) * b.n3 + ij;
-    double* Fu = F.FlxU + ij;
-    double* Fv = F.FlxV + ij;
-    const bool du = inR && i >= b.istr && i <= b.iendR && j >= b.jstrR && j <= b.jendR;
-    const bool dv = inR && i >= b.istrR && i <= b.iendR && j >= b.jstr && j <= b.jendR;
-    const double dnu0 = F.dn_u[ij], dnu1 = F.dn_u[ij + 1], dmv0 = F.dm_v[ij], dmv1 = F.dm_v[ij + sj];
-    for (int q = 0; q < n; q++) {
-      const long o = (long)(c0 + q - 1) * n2;
-      const double h0 = Hz[o];
-      if (du) Fu[o] = 0.5 * (h0 + Hz[o - 1]) * dnu0 * (U[o]);
-      if (dv) Fv[o] = 0.5 * (h0 + Hz[o - sj]) * dmv0 * (V[o]);
-      if (act) {
-        Fu[o + 1] = 0.5 * (Hz[o + 1] + h0) * dnu1 * (U[o + 1]);
-        Fv[o + sj] = 0.5 * (Hz[o + sj] + h0) * dmv1 * (V[o + sj]);
-      }
-    }
-    __threadfence_block();   // the stores complete before the loads below
-  }
   double fu1[kOmR], fu0[kOmR], fv1[kOmR], fv0[kOmR], cx[kOmR], hz[kOmR], zk[kOmR];
 #pragma unroll
   for (int q = 0; q < kOmR; q++) {   // rho level k = c0+q (clamped), w-level k
@@ -595,9 +560,7 @@ __global__ void k_omega_edges(Dev d) {
 
 static size_t omega_hb_lds_bytes(unsigned nthr) { return (size_t)kOmR * nthr * sizeof(double); }
 void setup_omega_seg() {
-  (void)hipFuncSetAttribute((const void*)k_omega_seg<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)omega_hb_lds_bytes(kSegBlock));
-  (void)hipFuncSetAttribute((const void*)k_omega_seg<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  (void)hipFuncSetAttribute((const void*)k_omega_seg<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)omega_hb_lds_bytes(kSegBlock));
 }
 
@@ -619,10 +582,9 @@ bool launch_omega(const Dev& d, hipStream_t s, const Tlev& t, double hcff) {
         // the segment form for full-width ranges (rim strips keep k_omega)
         const dim3 gs((r.i1 - tile_i0(r.i0) + kSegCW) / kSegCW, r.j1 - r.j0 + 1), bs(kCX, seg_waves(b.N));
         if (hb)
-          hipLaunchKernelGGL((k_omega_seg<true, false>), gs, bs, omega_hb_lds_bytes(bs.x * bs.y), s, d, r, r, dtau,
-                             hcff, 0);
+          hipLaunchKernelGGL(k_omega_seg<true>, gs, bs, omega_hb_lds_bytes(bs.x * bs.y), s, d, r, dtau, hcff);
         else if (seg_ok && r.i1 - r.i0 + 1 >= 32)
-          hipLaunchKernelGGL((k_omega_seg<false, false>), gs, bs, 0, s, d, r, r, dtau, 0.0, 0);
+          hipLaunchKernelGGL(k_omega_seg<false>, gs, bs, 0, s, d, r, dtau, 0.0);
         else
           hipLaunchKernelGGL(k_omega, grid_of(r), dim3(kBX, kBY), 0, s, d, r, dtau);
       },
@@ -632,38 +594,6 @@ bool launch_omega(const Dev& d, hipStream_t s, const Tlev& t, double hcff) {
           hipLaunchKernelGGL(k_omega_edges, dim3((n + 255) / 256, b.N + 1), dim3(256), 0, s, d);
         }
       });
-  return hb;
-}
-
-double omega_dtau(const Dev& d, const Tlev& t) {
-  if (t.nrhs == 3) return d.p.dt;
-  return t.iic == t.forw_start ? 0.5 * d.p.dt : 0.6 * d.p.dt;
-}
-bool set_huv_omega_fusable(const Dev& d) {
-  const Bounds& b = d.b;
-  const Range Ro{b.istr, b.iend, b.jstr, b.jend};
-  return d.p.omega_seg && b.N <= kSegRows * kSegMaxS && Ro.i1 - Ro.i0 + 1 >= 32 && !rim_overlap_on(d, Ro);
-}
-// set_HUV (without Hz_u/Hz_v) and omega in one segment launch over set_HUV's
-// range (k_omega_seg<., true>); hcff as launch_omega.  The two exchanges
-// (FlxU, FlxV; We, Wi) become one, after omega's closed-edge copies.
-bool launch_set_huv_omega(const Dev& d, hipStream_t s, const Tlev& t, double hcff) {
-  const Bounds& b = d.b;
-  const double dtau = omega_dtau(d, t);
-  const Range Rh{b.istrR < b.istr ? b.istrR : b.istr, b.iendR, b.jstrR < b.jstr ? b.jstrR : b.jstr, b.jendR};
-  const Range Ro{b.istr, b.iend, b.jstr, b.jend};
-  const bool hb = hcff > 0.0;
-  const dim3 gs((Rh.i1 - tile_i0(Rh.i0) + kSegCW) / kSegCW, Rh.j1 - Rh.j0 + 1), bs(kCX, seg_waves(b.N));
-  if (hb)
-    hipLaunchKernelGGL((k_omega_seg<true, true>), gs, bs, omega_hb_lds_bytes(bs.x * bs.y), s, d, Rh, Ro, dtau, hcff,
-                       t.nrhs);
-  else
-    hipLaunchKernelGGL((k_omega_seg<false, true>), gs, bs, 0, s, d, Rh, Ro, dtau, 0.0, t.nrhs);
-  if (b.west_edge || b.east_edge || b.south_edge || b.north_edge) {
-    const int n = 2 * (b.jend - b.jstr + 1) + 2 * (b.iend - b.istr + 1) + 4;
-    hipLaunchKernelGGL(k_omega_edges, dim3((n + 255) / 256, b.N + 1), dim3(256), 0, s, d);
-  }
-  launch_exchange_list(d, s, ExchList{{d.f.FlxU, d.f.FlxV, d.f.We, d.f.Wi}, {b.N, b.N, b.N + 1, b.N + 1}, 4});
   return hb;
 }
 

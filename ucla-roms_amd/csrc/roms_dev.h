@@ -76,7 +76,6 @@ struct Params {
   int omega_seg;  // omega: segment form k_omega_seg, one read of each input (ROMS_GPU_OMEGA_SEG=0: two-pass k_omega)
   int p_in_rho;   // rho_eos's sweep also forms prsgrd's P (ROMS_GPU_P_IN_RHO=0: k_prsgrd_P)
   int omega_hb;   // the predictor's omega forms pre_step3d's Hz_bak/Hz_fwd (ROMS_GPU_OMEGA_HB=0: pre_step3d does)
-  int huv_omega;  // whole steps: the predictor's set_HUV folded into omega's segment kernel (ROMS_GPU_HUV_OMEGA=0: separate)
   int preuv_lds;  // k_pre_uv_seg: u(indx) stored and u(nstp)/u(indx) combined in the spline phase (ROMS_GPU_PREUV_LDS=0: reloads)
   int seg_jrows;  // rows j per block of the momentum segment solvers (1..kSegJMax; ROMS_GPU_SEG_JROWS)
   int seg_vtile;  // v columns of the momentum segment solvers on 16 x 4 tiles per wavefront (ROMS_GPU_SEG_VTILE=0: rows of 64)
@@ -371,10 +370,6 @@ void launch_set_huv1(const Dev& d, hipStream_t s, const Tlev& t);
 // hcff > 0: the predictor's call also forms pre_step3d's Hz_bak/Hz_fwd (c3/c2) of the
 // interior cells with 0.5*dtau = hcff; returns whether it did (k_vertical.hip)
 bool launch_omega(const Dev& d, hipStream_t s, const Tlev& t, double hcff = 0.0);
-// set_HUV (FlxU, FlxV; no Hz_u/Hz_v) and omega in one segment launch when
-// set_huv_omega_fusable; returns as launch_omega (k_vertical.hip)
-bool set_huv_omega_fusable(const Dev& d);
-bool launch_set_huv_omega(const Dev& d, hipStream_t s, const Tlev& t, double hcff);
 void setup_omega_seg();   // k_omega_seg<true>'s dynamic LDS limit
 double pre_step3d_dtau(const Dev& d, const Tlev& t);   // pre_step3d's dtau (k_pre_step3d.hip)
 void launch_rho_eos(const Dev& d, hipStream_t s, const Tlev& t, int tidx);

@@ -423,18 +423,12 @@ void enqueue_step(roms_tlev* t, bool rho_current, bool store_huv) {
     fork(7);
     launch_prsgrd_P(d, s2);
   }
+  TIMED(ROMS_R_SET_HUV, launch_set_huv(d, s, T, store_huv));
   // the predictor's omega also forms pre_step3d's Hz_bak/Hz_fwd (nothing in
   // between -- lmd_vmix, prsgrd -- writes FlxU, FlxV, Hz, We or Wi)
   bool hb_done = false;
-  const double hcff = d.p.omega_hb && d.p.hoist && T.nrhs != 3 ? 0.5 * pre_step3d_dtau(d, T) : 0.0;
-  // set_HUV folded into the predictor's omega (launch_set_huv_omega; not
-  // while either is timed alone, nor when Hz_u/Hz_v are wanted)
-  if (d.p.huv_omega && !store_huv && g.timed != ROMS_R_SET_HUV && g.timed != ROMS_R_OMEGA && set_huv_omega_fusable(d)) {
-    hb_done = launch_set_huv_omega(d, s, T, hcff);
-  } else {
-    TIMED(ROMS_R_SET_HUV, launch_set_huv(d, s, T, store_huv));
-    TIMED(ROMS_R_OMEGA, hb_done = launch_omega(d, s, T, hcff));
-  }
+  TIMED(ROMS_R_OMEGA, hb_done = launch_omega(d, s, T, d.p.omega_hb && d.p.hoist && T.nrhs != 3 ?
+                                                          0.5 * pre_step3d_dtau(d, T) : 0.0));
   if (p_side) join(7);
   const bool lmd2 = g.cfg.lmd_mixing && par;
   if (lmd2) {
@@ -798,12 +792,6 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
   {
     const char* e = getenv("ROMS_GPU_OMEGA_HB");
     P.omega_hb = !(e && e[0] == '0');
-  }
-  {
-    // whole steps: the predictor's set_HUV inside omega's segment kernel
-    // (launch_set_huv_omega); opt-in until measured, ROMS_GPU_HUV_OMEGA=1
-    const char* e = getenv("ROMS_GPU_HUV_OMEGA");
-    P.huv_omega = e && e[0] == '1';
   }
   {
     const char* e = getenv("ROMS_GPU_OMEGA_SEG");
