@@ -370,7 +370,7 @@ void setup_column_kernels_t(size_t bytes) {
                             (int)bytes);
 }
 
-void launch_step3d_t(const Dev& d, hipStream_t s, const Tlev& t) {
+void launch_step3d_t(const Dev& d, hipStream_t s, const Tlev& t, bool exchange) {
   const Bounds& b = d.b;
   Range R{b.istr, b.iend, b.jstr, b.jend};
   if (d.p.iso) {
@@ -415,7 +415,10 @@ void launch_step3d_t(const Dev& d, hipStream_t s, const Tlev& t) {
     for (int itrc = 1; itrc <= b.NT; itrc++) launch_t3dbc(d, s, t, itrc);
   };
   ExchList L;
-  if (tracer_exch_list(d, t.nnew, L)) {
+  if (!exchange) {   // t3dmix follows and exchanges t(nnew) itself
+    run(R);
+    edges();
+  } else if (tracer_exch_list(d, t.nnew, L)) {
     launch_rim_first(d, s, R, L, run, edges);
   } else {
     run(R);

@@ -397,7 +397,10 @@ void launch_step3d_uv1(const Dev& d, hipStream_t s, const Tlev& t, bool uv_done 
 void launch_visc3d(const Dev& d, hipStream_t s, const Tlev& t);
 void launch_step2d(const Dev& d, hipStream_t s, const Tlev& t, const double* w1, const double* w2);
 void launch_step3d_uv2(const Dev& d, hipStream_t s, const Tlev& t);
-void launch_step3d_t(const Dev& d, hipStream_t s, const Tlev& t);
+// exchange = false: skip the closing t(nnew) exchange (whole steps with
+// TS_DIF2: t3dmix reads only t(nrhs) and its own cells of t(nnew), and its
+// own exchange of t(nnew) follows; the closed-wall ghosts are still set here)
+void launch_step3d_t(const Dev& d, hipStream_t s, const Tlev& t, bool exchange = true);
 void launch_t3dmix(const Dev& d, hipStream_t s, const Tlev& t);
 void launch_u3dbc(const Dev& d, hipStream_t s, const Tlev& t);
 // river_frc.F hooks (k_river.hip): ubar/vbar(knew) and DU/DV_avg1 at river

@@ -479,7 +479,9 @@ void enqueue_step(roms_tlev* t, bool rho_current, bool store_huv) {
   }
   TIMED(ROMS_R_STEP3D_UV2, launch_step3d_uv2(d, s, T));
   TIMED(ROMS_R_OMEGA, launch_omega(d, s, T));
-  TIMED(ROMS_R_STEP3D_T, launch_step3d_t(d, s, T));
+  // with TS_DIF2 the tracer exchange after step3d_t is overwritten by
+  // t3dmix's before anything reads the halo (t3dmix_S.F reads t(nrhs)): one
+  TIMED(ROMS_R_STEP3D_T, launch_step3d_t(d, s, T, !g.cfg.ts_dif2 || d.p.iso));
   if (g.cfg.ts_dif2) TIMED(ROMS_R_T3DMIX, launch_t3dmix(d, s, T));
   TIMED(ROMS_R_RHO_EOS, launch_rho_eos(d, s, T, T.nnew));
   g.rho_slot = T.nnew;
