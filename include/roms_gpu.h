@@ -302,6 +302,11 @@ int roms_gpu_halo_plan(int Lm, int Mm, int np_xi, int np_eta, int inode, int jno
  * Returns the per-level count (<= cap) or -1.                               */
 long roms_gpu_halo_map(int Lm, int Mm, int np_xi, int np_eta, int inode, int jnode, int ew_periodic,
                        int ns_periodic, int dir, int unpack, int *i, int *j, long cap);
+/* Host-only: roms_gpu_halo_map for a `width`-deep exchange (2: the
+ * reference's halo, as roms_gpu_halo_map; 2K: the fast loop's swap every K
+ * fast steps, roms_gpu_halo_exchanges).  width <= Lm, Mm.                   */
+long roms_gpu_halo_map_wide(int Lm, int Mm, int np_xi, int np_eta, int inode, int jnode, int ew_periodic,
+                            int ns_periodic, int width, int dir, int unpack, int *i, int *j, long cap);
 
 /* ---- forcing and boundary producers on the device (set_forces.F,
  * set_frc_data roms_read_write.F:303-392, set_bry_all boundary.F:227,

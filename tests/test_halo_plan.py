@@ -52,28 +52,29 @@ def test_plan_is_symmetric(npx, npe, ewp, nsp):
         assert (peer[3] >= 0) == bool(nsp or jn < npe - 1)
 
 
-def _global_field(LLm, MMm, ewp, nsp, seed):
-    """Global (MMm+4, LLm+4) field with halos: periodic wrap, or random
-    physical ghost rows at closed edges (the second ghost row stays NaN)."""
+def _global_field(LLm, MMm, ewp, nsp, seed, H=2):
+    """Global (MMm+2H, LLm+2H) field with H-deep halos (global cell (i, j) at
+    [j+H-1, i+H-1]): periodic wrap, or random physical ghost rows at closed
+    edges (the rows beyond stay NaN)."""
     rng = np.random.default_rng(seed)
-    G = np.full((MMm + 4, LLm + 4), np.nan)
-    G[2:MMm + 2, 2:LLm + 2] = rng.standard_normal((MMm, LLm))
+    G = np.full((MMm + 2 * H, LLm + 2 * H), np.nan)
+    G[H:MMm + H, H:LLm + H] = rng.standard_normal((MMm, LLm))
     if not ewp:
-        G[1:MMm + 3, 1] = rng.standard_normal(MMm + 2)
-        G[1:MMm + 3, LLm + 2] = rng.standard_normal(MMm + 2)
+        G[H - 1:MMm + H + 1, H - 1] = rng.standard_normal(MMm + 2)
+        G[H - 1:MMm + H + 1, LLm + H] = rng.standard_normal(MMm + 2)
     if not nsp:
-        G[1, 1:LLm + 3] = rng.standard_normal(LLm + 2)
-        G[MMm + 2, 1:LLm + 3] = rng.standard_normal(LLm + 2)
+        G[H - 1, H - 1:LLm + H + 1] = rng.standard_normal(LLm + 2)
+        G[MMm + H, H - 1:LLm + H + 1] = rng.standard_normal(LLm + 2)
     if ewp:
-        G[:, 0:2] = G[:, LLm:LLm + 2]
-        G[:, LLm + 2:LLm + 4] = G[:, 2:4]
+        G[:, 0:H] = G[:, LLm:LLm + H]
+        G[:, LLm + H:LLm + 2 * H] = G[:, H:2 * H]
     if nsp:
-        G[0:2, :] = G[MMm:MMm + 2, :]
-        G[MMm + 2:MMm + 4, :] = G[2:4, :]
+        G[0:H, :] = G[MMm:MMm + H, :]
+        G[MMm + H:MMm + 2 * H, :] = G[H:2 * H, :]
     return G
 
 
-def _exchange_worker(rank, world, port, LLm, MMm, npx, npe, ewp, nsp, nlev, q):
+def _exchange_worker(rank, world, port, LLm, MMm, npx, npe, ewp, nsp, nlev, q, H=2):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -82,9 +83,12 @@ def _exchange_worker(rank, world, port, LLm, MMm, npx, npe, ewp, nsp, nlev, q):
         Lm, iSW = R.rank_extent(LLm, npx, inn)
         Mm, jSW = R.rank_extent(MMm, npe, jn)
         peer, cnt, _ = R.halo_plan(Lm, Mm, npx, npe, inn, jn, ewp, nsp)
-        Gs = [_global_field(LLm, MMm, ewp, nsp, 100 + k) for k in range(nlev)]
-        # local windows: local (i,j) <-> global (iSW+i, jSW+j); array index +1
-        win = [G[jSW:jSW + Mm + 4, iSW:iSW + Lm + 4] for G in Gs]
+        if H != 2:
+            cnt = [len(R.halo_map(Lm, Mm, npx, npe, inn, jn, ewp, nsp, d, False, width=H)[0]) for d in range(8)]
+        Gs = [_global_field(LLm, MMm, ewp, nsp, 100 + k, H) for k in range(nlev)]
+        # local windows: local (i,j) <-> global (iSW+i, jSW+j); array index +H-1
+        o = H - 1
+        win = [G[jSW:jSW + Mm + 2 * H, iSW:iSW + Lm + 2 * H] for G in Gs]
         A = [np.full_like(w, np.nan) for w in win]
         # cells this rank owns: interior plus its physical (closed-edge) ghost
         # row/column, which the BC code -- not the exchange -- sets
@@ -93,15 +97,15 @@ def _exchange_worker(rank, world, port, LLm, MMm, npx, npe, ewp, nsp, nlev, q):
         j_lo = 0 if (not nsp and jn == 0) else 1
         j_hi = Mm + 1 if (not nsp and jn == npe - 1) else Mm
         for a, w in zip(A, win):
-            a[j_lo + 1:j_hi + 2, i_lo + 1:i_hi + 2] = w[j_lo + 1:j_hi + 2, i_lo + 1:i_hi + 2]
-        maps = [R.halo_map(Lm, Mm, npx, npe, inn, jn, ewp, nsp, d, False) for d in range(8)]
-        umaps = [R.halo_map(Lm, Mm, npx, npe, inn, jn, ewp, nsp, d, True) for d in range(8)]
+            a[j_lo + o:j_hi + o + 1, i_lo + o:i_hi + o + 1] = w[j_lo + o:j_hi + o + 1, i_lo + o:i_hi + o + 1]
+        maps = [R.halo_map(Lm, Mm, npx, npe, inn, jn, ewp, nsp, d, False, width=H) for d in range(8)]
+        umaps = [R.halo_map(Lm, Mm, npx, npe, inn, jn, ewp, nsp, d, True, width=H) for d in range(8)]
         send = {}
         for d in range(8):
             if peer[d] < 0:
                 continue
             iv, jv = maps[d]
-            send[d] = torch.from_numpy(np.concatenate([a[jv + 1, iv + 1] for a in A]))
+            send[d] = torch.from_numpy(np.concatenate([a[jv + o, iv + o] for a in A]))
         reqs, recv = [], {}
         # the transport's ordering: messages to a peer in direction order,
         # receives for halo opp(d) in the same order (tag = sender's direction)
@@ -122,7 +126,7 @@ def _exchange_worker(rank, world, port, LLm, MMm, npx, npe, ewp, nsp, nlev, q):
             iv, jv = umaps[h]
             parts = buf.numpy().reshape(nlev, cnt[h])
             for a, part in zip(A, parts):
-                a[jv + 1, iv + 1] = part
+                a[jv + o, iv + o] = part
         bad = 0
         for a, w in zip(A, win):
             defined = ~np.isnan(w)
@@ -148,6 +152,26 @@ def test_gloo_exchange_fills_every_halo(npx, npe, ewp, nsp):
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_exchange_worker, args=(r, world, port, 13, 11, npx, npe, ewp, nsp, 3, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert all(v == 0 for v in res.values()), res
+
+
+@pytest.mark.parametrize("H", [4, 8])
+@pytest.mark.parametrize("npx,npe,ewp,nsp", [(2, 1, 1, 1), (2, 2, 1, 1), (2, 2, 0, 0), (2, 2, 1, 0), (1, 2, 1, 0)])
+def test_gloo_wide_exchange_fills_every_halo(npx, npe, ewp, nsp, H):
+    """The fast loop's H-deep exchange (H = 2K, roms_gpu_halo_map_wide): every
+    cell of the H-deep frame that has a neighbour, a periodic image or a
+    closed-edge ghost row holds the global field's value after the swap."""
+    world = npx * npe
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_exchange_worker, args=(r, world, port, 23, 19, npx, npe, ewp, nsp, 2, q, H))
              for r in range(world)]
     for p in procs:
         p.start()

@@ -1,6 +1,8 @@
 // k_step3d_uv.hip -- corrector momentum: step3d_uv1 (step3d_uv1.F:23-534),
 // visc3d (visc3d_S.F:18-131) and the 2-D/3-D coupling step3d_uv2
 // (step3d_uv2.F:18-786, IMPLICIT_BOTTOM_DRAG branch).
+#include <vector>
+
 #include "k_colseg.h"
 #include "k_chain.h"
 
@@ -761,7 +763,7 @@ void launch_visc3d(const Dev& d, hipStream_t s, const Tlev& t) {
 // Columns that k_uv2_fused owns: the coupling range without the rows (u) /
 // columns (v) next to a closed edge, whose coupled values u3dbc/v3dbc copy
 // into the ghost rows before the flux correction.
-__device__ __forceinline__ bool uv2_fused_in(const Bounds& b, int dir, int i, int j) {
+__host__ __device__ __forceinline__ bool uv2_fused_in(const Bounds& b, int dir, int i, int j) {
   if (dir == 0)
     return i >= b.istrU && i <= b.iend && j >= b.jstr + (b.south_edge ? 1 : 0) && j <= b.jend - (b.north_edge ? 1 : 0);
   return i >= b.istr + (b.west_edge ? 1 : 0) && i <= b.iend - (b.east_edge ? 1 : 0) && j >= b.jstrV && j <= b.jend;
@@ -987,6 +989,129 @@ __global__ void __launch_bounds__(256, KL > 13 ? 3 : 4) k_uv2_fused(Dev d, Range
   }
 }
 
+// ---- step3d_uv2 on the closed-edge columns that k_uv2_fused leaves out,
+// in k_uv2_fused's chain layout (16 columns x 4 vertical segments per
+// wavefront) over a list of (dir, i, j) columns: kCouple = k_uv2_couple's
+// pass (the coupling range's edge rows / columns), else k_uv2_flux's (those
+// plus the wall faces and ghost rows u3dbc/v3dbc set in between).  The same
+// operations in the same order as k_uv2_couple / k_uv2_flux (and as the
+// fused kernel's two halves), bit-identical; a column's dependent level walk
+// is a quarter of theirs, which is what the one-lane-per-column edge mode's
+// time was (each level a page away: a TLB miss per load). ----
+template <int KL, bool kCouple>
+__global__ void __launch_bounds__(256) k_uv2_edge(Dev d, const int* __restrict__ cols, int ncol, int nnew, int nstp,
+                                                  int knew) {
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const int N = b.N;
+  const double DELTA = 0.28, EPSIL = 0.36;
+  const int l = (int)(threadIdx.x & 63u), w = (int)(threadIdx.x >> 6);
+  ChainLane cl;
+  cl.col = l & (kChainCW - 1);
+  cl.g = l / kChainCW;
+  cl.lo = 1 + cl.g * KL;
+  cl.nk = max(0, min(N, cl.lo + KL - 1) - cl.lo + 1);
+  const int c = ((int)blockIdx.x * 4 + w) * kChainCW + cl.col;
+  const bool act = c < ncol;
+  const int cc = act ? c : ncol - 1;   // idle lanes repeat the last column (shuffles see defined values)
+  const int dir = cols[3 * cc], i = cols[3 * cc + 1], j = cols[3 * cc + 2];
+  cl.i = i; cl.j = j; cl.in = true;
+  const long n2 = b.n2, ij = IJ(b, i, j), s = dir == 0 ? 1 : b.nx2;
+  auto chain2 = [&](double& s1, double& s2, auto&& body) { chain_down(cl, s1, s2, body); };
+  double* __restrict__ Un = (dir == 0 ? F.u : F.v) + (long)(nnew - 1) * b.n3 + ij;
+  const double* __restrict__ Hz = F.Hz + ij;
+  const double dn = dir == 0 ? F.dn_u[ij] : F.dm_v[ij];
+  const double avg1 = dir == 0 ? F.DU_avg1[ij] : F.DV_avg1[ij];
+  const double msk = dir == 0 ? F.umask[ij] : F.vmask[ij];
+  double un[KL], hc[KL];
+#pragma unroll
+  for (int q = 0; q < KL; q++) {
+    if (q < cl.nk) {
+      const long o = (long)(cl.lo + q - 1) * n2;
+      un[q] = Un[o];
+      hc[q] = 0.5 * (Hz[o] + Hz[o - s]);
+    }
+  }
+  if constexpr (kCouple) {
+    double CF0, DC0;
+    chain2(CF0, DC0, [&](double& a, double& c2) {
+#pragma unroll
+      for (int q = KL - 1; q >= 0; q--)
+        if (q < cl.nk) { a = a + hc[q]; c2 = c2 + un[q]; }
+    });
+    DC0 = (DC0 * dn - avg1) / (CF0 * dn);
+    if (act) {
+#pragma unroll
+      for (int q = 0; q < KL; q++)
+        if (q < cl.nk) Un[(long)(cl.lo + q - 1) * n2] = (un[q] / hc[q] - DC0) * msk;
+    }
+  } else {
+    const double* __restrict__ Us = (dir == 0 ? F.u : F.v) + (long)(nstp - 1) * b.n3 + ij;
+    double* __restrict__ Flx = (dir == 0 ? F.FlxU : F.FlxV) + ij;
+    const double avg2 = dir == 0 ? F.DU_avg2[ij] : F.DV_avg2[ij];
+    double DS, FC0;
+    chain2(DS, FC0, [&](double& a, double& c2) {
+#pragma unroll
+      for (int q = KL - 1; q >= 0; q--)
+        if (q < cl.nk) { const double dck = hc[q] * dn; a = a + dck; c2 = c2 + dck * un[q]; }
+    });
+    const double DCi = 1.0 / DS;
+    if (act && cl.g == 0) {
+      if (dir == 0) F.ubar[IJL(b, i, j, knew)] = DCi * avg1;
+      else F.vbar[IJL(b, i, j, knew)] = DCi * avg1;
+    }
+    FC0 = DCi * (FC0 - avg1);
+#pragma unroll
+    for (int q = 0; q < KL; q++) {
+      if (q < cl.nk) {
+        const long o = (long)(cl.lo + q - 1) * n2;
+        const double u1 = (un[q] - FC0) * msk;
+        if (act) Un[o] = u1;
+        un[q] = DELTA * Flx[o] + EPSIL * (hc[q] * dn) * (Us[o] + u1);
+      }
+    }
+    double CS, unused;
+    chain2(CS, unused, [&](double& a, double& c2) {
+#pragma unroll
+      for (int q = KL - 1; q >= 0; q--)
+        if (q < cl.nk) a = a + un[q];
+    });
+    const double CF1 = DCi * (CS - avg2);
+    if (act) {
+#pragma unroll
+      for (int q = 0; q < KL; q++)
+        if (q < cl.nk) Flx[(long)(cl.lo + q - 1) * n2] = un[q] - (hc[q] * dn) * CF1;
+    }
+  }
+}
+
+// The (dir, i, j) lists of k_uv2_edge: the columns k_uv2_couple (couple) and
+// k_uv2_flux (flux) visit in edge mode, in their ranges and order.
+void uv2_edge_lists(const Bounds& b, std::vector<int>& couple, std::vector<int>& flux) {
+  couple.clear();
+  flux.clear();
+  if (!(b.west_edge || b.east_edge || b.south_edge || b.north_edge)) return;
+  const int iu0 = b.istr, iu1 = b.ew_periodic ? b.iend : b.iendR;
+  const int iv0 = b.ew_periodic ? b.istr : b.istrR, iv1 = b.ew_periodic ? b.iend : b.iendR;
+  const int j0 = b.ns_periodic ? b.jstr : b.jstrR, j1 = b.ns_periodic ? b.jend : b.jendR;
+  for (int dir = 0; dir < 2; dir++)
+    for (int j = b.jstr; j <= b.jend; j++)
+      for (int i = b.istr; i <= b.iend; i++) {
+        if (dir == 0 && !(i >= b.istrU)) continue;
+        if (dir == 1 && !(j >= b.jstrV)) continue;
+        if (uv2_fused_in(b, dir, i, j)) continue;
+        couple.insert(couple.end(), {dir, i, j});
+      }
+  for (int dir = 0; dir < 2; dir++)
+    for (int j = j0; j <= j1; j++)
+      for (int i = (iv0 < iu0 ? iv0 : iu0); i <= (iu1 > iv1 ? iu1 : iv1); i++) {
+        if (dir == 0 && !(i >= iu0 && i <= iu1)) continue;
+        if (dir == 1 && !(i >= iv0 && i <= iv1 && j >= b.jstr)) continue;
+        if (uv2_fused_in(b, dir, i, j)) continue;
+        flux.insert(flux.end(), {dir, i, j});
+      }
+}
+
 void launch_step3d_uv2(const Dev& d, hipStream_t s, const Tlev& t) {
   const Bounds& b = d.b;
   Range R1{b.istr, b.iend, b.jstr, b.jend};
@@ -1001,7 +1126,18 @@ void launch_step3d_uv2(const Dev& d, hipStream_t s, const Tlev& t) {
     if (kl <= 5) hipLaunchKernelGGL(k_uv2_fused<5>, gf, dim3(256), 0, s, d, R1, t.nnew, t.nstp, t.knew);
     else if (kl <= 13) hipLaunchKernelGGL(k_uv2_fused<13>, gf, dim3(256), 0, s, d, R1, t.nnew, t.nstp, t.knew);
     else hipLaunchKernelGGL(k_uv2_fused<25>, gf, dim3(256), 0, s, d, R1, t.nnew, t.nstp, t.knew);
-    if (b.west_edge || b.east_edge || b.south_edge || b.north_edge) {   // columns next to closed edges: couple, u3dbc/v3dbc, flux
+    if (d.f.uv2e_couple && d.p.uv2e_nc > 0 && d.p.uv2e_nf > 0) {   // closed edges: chain form over the column lists
+      const int nc = d.p.uv2e_nc, nf = d.p.uv2e_nf;
+      const dim3 gc((nc + 63) / 64), gf2((nf + 63) / 64);
+      if (kl <= 5) hipLaunchKernelGGL((k_uv2_edge<5, true>), gc, dim3(256), 0, s, d, d.f.uv2e_couple, nc, t.nnew, t.nstp, t.knew);
+      else if (kl <= 13) hipLaunchKernelGGL((k_uv2_edge<13, true>), gc, dim3(256), 0, s, d, d.f.uv2e_couple, nc, t.nnew, t.nstp, t.knew);
+      else hipLaunchKernelGGL((k_uv2_edge<25, true>), gc, dim3(256), 0, s, d, d.f.uv2e_couple, nc, t.nnew, t.nstp, t.knew);
+      launch_u3dbc(d, s, t);
+      launch_v3dbc(d, s, t);
+      if (kl <= 5) hipLaunchKernelGGL((k_uv2_edge<5, false>), gf2, dim3(256), 0, s, d, d.f.uv2e_flux, nf, t.nnew, t.nstp, t.knew);
+      else if (kl <= 13) hipLaunchKernelGGL((k_uv2_edge<13, false>), gf2, dim3(256), 0, s, d, d.f.uv2e_flux, nf, t.nnew, t.nstp, t.knew);
+      else hipLaunchKernelGGL((k_uv2_edge<25, false>), gf2, dim3(256), 0, s, d, d.f.uv2e_flux, nf, t.nnew, t.nstp, t.knew);
+    } else if (b.west_edge || b.east_edge || b.south_edge || b.north_edge) {   // columns next to closed edges: couple, u3dbc/v3dbc, flux
       hipLaunchKernelGGL(k_uv2_couple, grid_of(R1), dim3(kBX, kBY), 0, s, d, R1, t.nnew, 1);
       launch_u3dbc(d, s, t);
       launch_v3dbc(d, s, t);

@@ -80,6 +80,7 @@ struct Params {
   int seg_jrows;  // rows j per block of the momentum segment solvers (1..kSegJMax; ROMS_GPU_SEG_JROWS)
   int seg_vtile;  // v columns of the momentum segment solvers on 16 x 4 tiles per wavefront (ROMS_GPU_SEG_VTILE=0: rows of 64)
   int s2d_k;      // fast steps per zeta/ubar/vbar exchange (multi-rank, wide halos of 2*s2d_k; 1: every step)
+  int uv2e_nc, uv2e_nf;   // lengths of Fields::uv2e_couple / uv2e_flux
   int npip;       // pipe_frc.F: number of pipes (0: pipe_source off)
   int nriv, nrivf;  // river_frc.F: number of rivers (0: river_source off), river faces
   int curvgrid;   // CURVGRID && UV_ADV: curvature terms (compute_horiz_rhs_uv_terms.h:8-11)
@@ -126,6 +127,9 @@ struct Fields {
   // face with |riv_flx| > 1e-3, three ints per face (Params::nrivf of them)
   double *riv_uflx, *riv_vflx, *riv_vol, *riv_trc;
   int* riv_face;
+  // step3d_uv2's closed-edge columns (uv2_edge_lists): (dir, i, j) triples of
+  // the couple and the flux pass (Params::uv2e_nc / uv2e_nf of them; nullptr: the one-lane edge mode)
+  int *uv2e_couple, *uv2e_flux;
   // boundary.F open-boundary data, [0] west, [1] east (index j, 0:Mm+1),
   // [2] south, [3] north (index i, 0:Lm+1); u, v (.,N); t (.,N,NT)
   double *bzeta[4], *bubar[4], *bvbar[4], *bu[4], *bv[4], *bt[4];

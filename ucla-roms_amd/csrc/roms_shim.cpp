@@ -314,6 +314,8 @@ void free_all() {
   g.scratch.clear();
   if (g.d.f.pipe_idx) { (void)hipFree(g.d.f.pipe_idx); g.d.f.pipe_idx = nullptr; }
   if (g.d.f.riv_face) { (void)hipFree(g.d.f.riv_face); g.d.f.riv_face = nullptr; }
+  if (g.d.f.uv2e_couple) { (void)hipFree(g.d.f.uv2e_couple); g.d.f.uv2e_couple = nullptr; }
+  if (g.d.f.uv2e_flux) { (void)hipFree(g.d.f.uv2e_flux); g.d.f.uv2e_flux = nullptr; }
   g.riv_maxidx = 0;
   g.have_swr = false;
   for (double*& p : g.d.f.ub)
@@ -922,6 +924,21 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     for (double** q : l2)
       if (scratch(*q, b.n2)) return -2;
   }
+  {
+    // step3d_uv2's closed-edge columns in the chain form (k_uv2_edge; opt-in
+    // until measured, ROMS_GPU_UV2_EDGE=1), else the one-lane edge mode
+    const char* e = getenv("ROMS_GPU_UV2_EDGE");
+    std::vector<int> lc, lf;
+    if (e && e[0] == '1') uv2_edge_lists(b, lc, lf);
+    if (!lc.empty() && !lf.empty()) {
+      CHECK_HIP(hipMalloc(&F.uv2e_couple, lc.size() * sizeof(int)));
+      CHECK_HIP(hipMalloc(&F.uv2e_flux, lf.size() * sizeof(int)));
+      CHECK_HIP(copy_on(F.uv2e_couple, lc.data(), lc.size() * sizeof(int), hipMemcpyHostToDevice, g.s));
+      CHECK_HIP(copy_on(F.uv2e_flux, lf.data(), lf.size() * sizeof(int), hipMemcpyHostToDevice, g.s));
+      P.uv2e_nc = (int)(lc.size() / 3);
+      P.uv2e_nf = (int)(lf.size() / 3);
+    }
+  }
   CHECK_HIP(hipHostMalloc(&g.h_diag, 8 * sizeof(double), hipHostMallocDefault));
   CHECK_HIP(hipMalloc(&g.d_diag, 8 * sizeof(double)));
   if (comm != nullptr) {
@@ -1464,6 +1481,15 @@ long roms_gpu_halo_map(int Lm, int Mm, int np_xi, int np_eta, int inode, int jno
       dir < 0 || dir > 7)
     return -1;
   const HaloPlan P = halo_plan(Lm, Mm, np_xi, np_eta, inode, jnode, ew_periodic, ns_periodic);
+  if (P.g.cnt[dir] > cap) return -1;
+  return halo_map(P, dir, unpack, iv, jv);
+}
+long roms_gpu_halo_map_wide(int Lm, int Mm, int np_xi, int np_eta, int inode, int jnode, int ew_periodic,
+                            int ns_periodic, int width, int dir, int unpack, int* iv, int* jv, long cap) {
+  if (Lm < 2 || Mm < 2 || np_xi < 1 || np_eta < 1 || inode < 0 || inode >= np_xi || jnode < 0 || jnode >= np_eta ||
+      dir < 0 || dir > 7 || width < 1 || width > Lm || width > Mm)
+    return -1;
+  const HaloPlan P = halo_plan(Lm, Mm, np_xi, np_eta, inode, jnode, ew_periodic, ns_periodic, width);
   if (P.g.cnt[dir] > cap) return -1;
   return halo_map(P, dir, unpack, iv, jv);
 }

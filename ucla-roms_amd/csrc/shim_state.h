@@ -1,6 +1,7 @@
 // shim_state.h -- what the C-ABI modules outside roms_shim.cpp (rst_io.hip)
 // see of the calling thread's library state.
 #pragma once
+#include <vector>
 #include <hip/hip_runtime.h>
 
 #include <string>
@@ -54,4 +55,6 @@ hipError_t shim_rows_h2d(double* dev, const double* host, long rows);   // `rows
 void launch_rows_copy(double* dst, long dpitch, long dplane, const double* src, long spitch, long splane, long width,
                       long rows, long prow, hipStream_t s);
 double* shim_scratch_small(long n);        // small device scratch owned by the context (>= n doubles)
+// step3d_uv2's closed-edge column lists (k_step3d_uv.hip): (dir, i, j) triples
+void uv2_edge_lists(const Bounds& b, std::vector<int>& couple, std::vector<int>& flux);
 }  // namespace roms

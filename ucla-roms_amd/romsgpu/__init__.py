@@ -134,6 +134,7 @@ def load_library(path=LIB_PATH):
     L.roms_gpu_halo_plan.argtypes = [ctypes.c_int] * 8 + [P(ctypes.c_int), P(ctypes.c_long), P(ctypes.c_int)]
     L.roms_gpu_halo_map.argtypes = [ctypes.c_int] * 10 + [P(ctypes.c_int), P(ctypes.c_int), ctypes.c_long]
     L.roms_gpu_halo_map.restype = ctypes.c_long
+    L.roms_gpu_halo_map_wide.restype = ctypes.c_long
     L.roms_gpu_wrt_rst.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_double, P(Tlev)]
     L.roms_gpu_wrt_his.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_double, P(Tlev), ctypes.c_int]
     L.roms_gpu_get_init.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, P(Tlev), P(ctypes.c_double)]
@@ -177,15 +178,20 @@ def halo_plan(Lm, Mm, np_xi, np_eta, inode, jnode, ew_periodic, ns_periodic):
     return list(peer), list(cnt), tuple(strip)
 
 
-def halo_map(Lm, Mm, np_xi, np_eta, inode, jnode, ew_periodic, ns_periodic, direction, unpack):
+def halo_map(Lm, Mm, np_xi, np_eta, inode, jnode, ew_periodic, ns_periodic, direction, unpack, width=2):
     """(i, j) arrays of the cells direction `direction` packs (unpack=False) or
-    fills (unpack=True), in message order (host-only call)."""
+    fills (unpack=True), in message order (host-only call); width > 2: the
+    fast loop's width-deep exchange (roms_gpu_halo_map_wide)."""
     L = load_library()
-    cap = 4 * (max(Lm, Mm) + 4)
+    cap = max(width, 2) * (max(Lm, Mm) + 4)
     iv = (ctypes.c_int * cap)()
     jv = (ctypes.c_int * cap)()
-    n = L.roms_gpu_halo_map(Lm, Mm, np_xi, np_eta, inode, jnode, int(ew_periodic), int(ns_periodic), direction,
-                            int(unpack), iv, jv, cap)
+    if width == 2:
+        n = L.roms_gpu_halo_map(Lm, Mm, np_xi, np_eta, inode, jnode, int(ew_periodic), int(ns_periodic), direction,
+                                int(unpack), iv, jv, cap)
+    else:
+        n = L.roms_gpu_halo_map_wide(Lm, Mm, np_xi, np_eta, inode, jnode, int(ew_periodic), int(ns_periodic), width,
+                                     direction, int(unpack), iv, jv, cap)
     if n < 0:
         raise ValueError("bad halo map arguments")
     return np.array(iv[:n]), np.array(jv[:n])
