@@ -925,11 +925,13 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
       if (scratch(*q, b.n2)) return -2;
   }
   {
-    // step3d_uv2's closed-edge columns in the chain form (k_uv2_edge; opt-in
-    // until measured, ROMS_GPU_UV2_EDGE=1), else the one-lane edge mode
+    // step3d_uv2's closed-edge columns in the chain form (k_uv2_edge): C3
+    // uv2 3.93 -> 3.39 ms, step 60.8 -> 59.7 ms same box
+    // (profiles/r4_p_uv2_edge_colreg_ab.txt); ROMS_GPU_UV2_EDGE=0: the
+    // one-lane edge mode
     const char* e = getenv("ROMS_GPU_UV2_EDGE");
     std::vector<int> lc, lf;
-    if (e && e[0] == '1') uv2_edge_lists(b, lc, lf);
+    if (!(e && e[0] == '0')) uv2_edge_lists(b, lc, lf);
     if (!lc.empty() && !lf.empty()) {
       CHECK_HIP(hipMalloc(&F.uv2e_couple, lc.size() * sizeof(int)));
       CHECK_HIP(hipMalloc(&F.uv2e_flux, lf.size() * sizeof(int)));
