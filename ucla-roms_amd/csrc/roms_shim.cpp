@@ -89,7 +89,7 @@ struct Ctx {
   long stage_n = 0;
   // Routines with no data dependence between them run on two streams inside
   // the step (single rank; opt-in, ROMS_GPU_PAR=1): see enqueue_step
-  bool par = true;
+  int par = 0;               // two-stream pair mask (enqueue_step)
   long step_exch = 0;        // halo exchanges in the last enqueued step (roms_gpu_halo_exchanges)
   hipStream_t s2 = nullptr;
   hipEvent_t pev[8] = {};
@@ -401,7 +401,11 @@ void enqueue_step(roms_tlev* t, bool rho_current, bool store_huv) {
   // Same kernels, same inputs: the results are bitwise those of one stream.
   // The low-occupancy column kernels (KPP, omega) fill CUs the other
   // routine leaves idle.
-  const bool par = g.par && d.halo == nullptr && g.timed < 0;
+  // g.par: a mask of the pairs (ROMS_GPU_PAR=1: all; ROMS_GPU_PAR_MASK=bits):
+  // 1 predictor lmd_vmix | prsgrd, 2 corrector omega | rho_eos, 4 corrector
+  // lmd_vmix | prsgrd, 8 pre_step3d tracer | momentum solves, 16 predictor P
+  // (linear EOS) | set_HUV, omega
+  const int pm = d.halo == nullptr && g.timed < 0 ? g.par : 0;
   hipStream_t s2 = g.s2;
   auto fork = [&](int k) {   // s2 continues after everything queued on s so far
     (void)hipEventRecord(g.pev[k], s);
@@ -420,7 +424,7 @@ void enqueue_step(roms_tlev* t, bool rho_current, bool store_huv) {
   // (linear EOS) prsgrd's P integral (rho, z_r, z_w: nothing set_HUV or
   // omega writes) runs on the side stream beside them
   const bool p_ready = p_in_rho(d);
-  const bool p_side = par && !p_ready && d.p.prs_split;
+  const bool p_side = (pm & 16) && !p_ready && d.p.prs_split;
   if (p_side) {
     fork(7);
     launch_prsgrd_P(d, s2);
@@ -432,7 +436,7 @@ void enqueue_step(roms_tlev* t, bool rho_current, bool store_huv) {
   TIMED(ROMS_R_OMEGA, hb_done = launch_omega(d, s, T, d.p.omega_hb && d.p.hoist && T.nrhs != 3 ?
                                                           0.5 * pre_step3d_dtau(d, T) : 0.0));
   if (p_side) join(7);
-  const bool lmd2 = g.cfg.lmd_mixing && par;
+  const bool lmd2 = g.cfg.lmd_mixing && (pm & 1);
   if (lmd2) {
     fork(0);
     launch_lmd_vmix(d, s2, T, T.nstp);
@@ -446,12 +450,12 @@ void enqueue_step(roms_tlev* t, bool rho_current, bool store_huv) {
   TIMED(ROMS_R_PRSGRD, launch_prsgrd(d, s, T, fuse_uv ? 0 : -1, p_ready || p_side));
   if (lmd2) join(1);
   const Side side{s2, g.pev[5], g.pev[6]};
-  TIMED(ROMS_R_PRE_STEP3D, launch_pre_step3d(d, s, T, fuse_uv, hb_done, par ? &side : nullptr));
+  TIMED(ROMS_R_PRE_STEP3D, launch_pre_step3d(d, s, T, fuse_uv, hb_done, (pm & 8) ? &side : nullptr));
   TIMED(ROMS_R_SET_HUV1, launch_set_huv1(d, s, T));
   t->nrhs = 3;
   t->nnew = 3 - t->nstp;
   T = to_tlev(t);
-  if (par) {
+  if (pm & 2) {
     fork(2);
     launch_omega(d, s2, T);
   } else {
@@ -460,7 +464,8 @@ void enqueue_step(roms_tlev* t, bool rho_current, bool store_huv) {
   TIMED(ROMS_R_RHO_EOS, launch_rho_eos(d, s, T, T.nrhs));
   frc_step_phase(d, s, 2, pot);     // set_forces, '1/2 fwd' (main.F:433)
   launch_bulk_flux(d, s, T.nrhs);   // set_forces (main.F:433): BULK_FRC only
-  if (lmd2) {
+  const bool lmd2c = g.cfg.lmd_mixing && (pm & 4);
+  if (lmd2c) {
     fork(3);   // after rho_eos (bvf) and the bulk fluxes (stflx, srflx, sustr_r)
     launch_lmd_vmix(d, s2, T, T.nrhs);
   } else if (g.cfg.lmd_mixing) {
@@ -468,7 +473,7 @@ void enqueue_step(roms_tlev* t, bool rho_current, bool store_huv) {
   }
   frc_step_phase(d, s, 3, pot);     // set_bry_all 'forward' + set_tides (main.F:438-441)
   TIMED(ROMS_R_PRSGRD, launch_prsgrd(d, s, T, fuse_uv ? 1 : -1, p_ready));
-  if (par) join(4);
+  if ((pm & 2) || lmd2c) join(4);
   TIMED(ROMS_R_STEP3D_UV1, launch_step3d_uv1(d, s, T, fuse_uv));
   if (g.cfg.uv_vis2) TIMED(ROMS_R_VISC3D, launch_visc3d(d, s, T));
   for (int iif = 1; iif <= t->nfast; iif++) {
@@ -880,7 +885,9 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     // for CUs and LDS (the segment solvers hold one block per CU), so the
     // second stream is opt-in, ROMS_GPU_PAR=1
     const char* e = getenv("ROMS_GPU_PAR");
-    g.par = e && e[0] == '1';
+    const char* em = getenv("ROMS_GPU_PAR_MASK");
+    g.par = e && e[0] == '1' ? 31 : 0;
+    if (em) g.par = atoi(em) & 31;
   }
   {
     const char* e = getenv("ROMS_GPU_GUARD");
