@@ -233,7 +233,25 @@ struct FBTile {
 // kClosed: 0 no closed edge, 1 closed edges finished by k_s2d_edges, 2 closed
 // walls folded in; kWrap: single-rank periodic images (vwrap bits).  Compile-
 // time switches, so each instance carries only its own branches.
-template <bool kPipe, int kClosed, bool kWrap>
+// How the fast step's results are stored.  1 (default): write-through
+// (sc1, an agent-scope relaxed atomic store): the lines go on to memory while
+// the kernel runs instead of sitting dirty in the XCDs' L2s until the end of
+// the dispatch, whose write-back the next fast step would wait for -- 16.8 MB
+// per C2 launch; -10% per fast step at C2 and C3 (profiles/r4_y_s2d_store_ab.txt).
+// 0 plain stores, 2 nontemporal (no gain); ROMS_GPU_S2D_WT selects for A/B.
+// (Write-through in the long 3-D kernels measured neutral at C2 and 1 ms/step
+// slower at C3, so they keep plain stores.)
+template <int WT>
+__device__ __forceinline__ void gst(double* p, double v) {
+  if constexpr (WT == 1)
+    __hip_atomic_store((unsigned long long*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  else if constexpr (WT == 2)
+    __builtin_nontemporal_store(v, p);
+  else
+    *p = v;
+}
+template <bool kPipe, int kClosed, bool kWrap, int kWT = 1>
 __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int vwrap, int part) {
   constexpr int closed = kClosed;
   const uint3 bI = xcd_tile();
@@ -437,8 +455,8 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int vw
     for (int q = tid; q < kFN && closed == 1; q += NT) {
       if (!T.st[q]) continue;
       const long o = IJ(b, i0 - 1 + q % kFX, j0 - 1 + q / kFX);
-      F.s0[o] = T.zn[q];
-      if (T.st[q] == 1) F.s1[o] = T.Dn[q];
+      gst<kWT>(&F.s0[o], T.zn[q]);
+      if (T.st[q] == 1) gst<kWT>(&F.s1[o], T.Dn[q]);
     }
   }
   // P3: zeta(knew), fast averages, pressure gradient, momentum
@@ -451,20 +469,20 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int vw
   double ubn = 0.0, vbn = 0.0;   // ubar/vbar(knew) this lane formed (closed == 2)
   if (pin) {
     const double z = T.zn[q];
-    F.zeta[ij + (long)(c.knew - 1) * n2] = z;
+    gst<kWT>(&F.zeta[ij + (long)(c.knew - 1) * n2], z);
     const double du = DU(i, j), dv = DV(i, j);
     if (c.iif == 1) {
-      F.DU_avg_bak[ij] = (pint ? x_DU1 : F.DU_avg1[ij]) - 0.1024390243902439 * (pint ? x_DU2 : F.DU_avg2[ij]);
-      F.DV_avg_bak[ij] = (pint ? x_DV1 : F.DV_avg1[ij]) - 0.1024390243902439 * (pint ? x_DV2 : F.DV_avg2[ij]);
-      F.Zt_avg1[ij] = c.w1 * z;
-      F.DU_avg1[ij] = 0.0;
-      F.DV_avg1[ij] = 0.0;
-      F.DU_avg2[ij] = c.w2 * du;
-      F.DV_avg2[ij] = c.w2 * dv;
+      gst<kWT>(&F.DU_avg_bak[ij], (pint ? x_DU1 : F.DU_avg1[ij]) - 0.1024390243902439 * (pint ? x_DU2 : F.DU_avg2[ij]));
+      gst<kWT>(&F.DV_avg_bak[ij], (pint ? x_DV1 : F.DV_avg1[ij]) - 0.1024390243902439 * (pint ? x_DV2 : F.DV_avg2[ij]));
+      gst<kWT>(&F.Zt_avg1[ij], c.w1 * z);
+      gst<kWT>(&F.DU_avg1[ij], 0.0);
+      gst<kWT>(&F.DV_avg1[ij], 0.0);
+      gst<kWT>(&F.DU_avg2[ij], c.w2 * du);
+      gst<kWT>(&F.DV_avg2[ij], c.w2 * dv);
     } else {
-      F.Zt_avg1[ij] = (pint ? x_Zt : F.Zt_avg1[ij]) + c.w1 * z;
-      F.DU_avg2[ij] = (pint ? x_DU2 : F.DU_avg2[ij]) + c.w2 * du;
-      F.DV_avg2[ij] = (pint ? x_DV2 : F.DV_avg2[ij]) + c.w2 * dv;
+      gst<kWT>(&F.Zt_avg1[ij], (pint ? x_Zt : F.Zt_avg1[ij]) + c.w1 * z);
+      gst<kWT>(&F.DU_avg2[ij], (pint ? x_DU2 : F.DU_avg2[ij]) + c.w2 * du);
+      gst<kWT>(&F.DV_avg2[ij], (pint ? x_DV2 : F.DV_avg2[ij]) + c.w2 * dv);
     }
   }
   if (pint) {
@@ -484,8 +502,8 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int vw
     if (c.iif == 1) {
       rufrc = rufrc - rubar;
       rvfrc = rvfrc - rvbar;
-      F.rufrc[ij] = rufrc;
-      F.rvfrc[ij] = rvfrc;
+      gst<kWT>(&F.rufrc[ij], rufrc);
+      gst<kWT>(&F.rvfrc[ij], rvfrc);
       auto corr = [&](int qq, int gg, double rS, double rA, double& zwrk, double& rzeta, double& rzeta2,
                       double& rzetaSA) {
         const double zn = T.zn[qq], zk = T.z0[gg];
@@ -511,15 +529,15 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int vw
       const double Dstpm = T.z0[g - 1] + hxm;
       const double DUnew = ((Dstp0 + Dstpm) * x_ub + cff * (x_pm0 + x_pmx) * (x_pn0 + x_pnx) * (rubar + rufrc)) * x_um;
       ubn = DUnew / (T.Dn[q] + T.Dn[q - 1]);
-      F.ubar[ij + (long)(c.knew - 1) * n2] = ubn;
-      F.DU_avg1[ij] = (c.iif == 1 ? 0.0 : x_DU1) + cff1 * dn_u * (DUnew);
+      gst<kWT>(&F.ubar[ij + (long)(c.knew - 1) * n2], ubn);
+      gst<kWT>(&F.DU_avg1[ij], (c.iif == 1 ? 0.0 : x_DU1) + cff1 * dn_u * (DUnew));
     }
     if (j >= b.jstrV) {
       const double Dstpm = T.z0[g - kGX] + hym;
       const double DVnew = ((Dstp0 + Dstpm) * x_vb + cff * (x_pm0 + x_pmy) * (x_pn0 + x_pny) * (rvbar + rvfrc)) * x_vm;
       vbn = DVnew / (T.Dn[q] + T.Dn[q - kFX]);
-      F.vbar[ij + (long)(c.knew - 1) * n2] = vbn;
-      F.DV_avg1[ij] = (c.iif == 1 ? 0.0 : x_DV1) + cff1 * dm_v * (DVnew);
+      gst<kWT>(&F.vbar[ij + (long)(c.knew - 1) * n2], vbn);
+      gst<kWT>(&F.DV_avg1[ij], (c.iif == 1 ? 0.0 : x_DV1) + cff1 * dm_v * (DVnew));
     }
   }
   if (closed != 2) return;
@@ -535,11 +553,11 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int vw
     // phase 0: wall-normal components (u2dbc_im.F / v2dbc_im.F closed walls)
     if (pin && j >= js && j <= je && ((b.west_edge && i == is) || (b.east_edge && i == ie + 1))) {
       ubn = 0.0;
-      F.ubar[ij + kn] = ubn;
+      gst<kWT>(&F.ubar[ij + kn], ubn);
     }
     if (pin && i >= is && i <= ie && ((b.south_edge && j == js) || (b.north_edge && j == je + 1))) {
       vbn = 0.0;
-      F.vbar[ij + kn] = vbn;
+      gst<kWT>(&F.vbar[ij + kn], vbn);
     }
     sU[t] = ubn;
     sV[t] = vbn;
@@ -551,20 +569,20 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int vw
       const int i0t = b.ew_periodic ? b.istrU : is, i1t = b.ew_periodic ? ie : b.iendR;
       if (b.south_edge && j == js - 1 && i >= i0t && i <= i1t) {
         ubn = g2 * sU[t + kBX] * F.umask[ij];
-        F.ubar[ij + kn] = ubn;
+        gst<kWT>(&F.ubar[ij + kn], ubn);
       }
       if (b.north_edge && j == je + 1 && i >= i0t && i <= i1t) {
         ubn = g2 * sU[t - kBX] * F.umask[ij];
-        F.ubar[ij + kn] = ubn;
+        gst<kWT>(&F.ubar[ij + kn], ubn);
       }
       const int j0t = b.ns_periodic ? b.jstrV : js, j1t = b.ns_periodic ? je : b.jendR;
       if (b.west_edge && i == is - 1 && j >= j0t && j <= j1t) {
         vbn = g2 * sV[t + 1] * F.vmask[ij];
-        F.vbar[ij + kn] = vbn;
+        gst<kWT>(&F.vbar[ij + kn], vbn);
       }
       if (b.east_edge && i == ie + 1 && j >= j0t && j <= j1t) {
         vbn = g2 * sV[t - 1] * F.vmask[ij];
-        F.vbar[ij + kn] = vbn;
+        gst<kWT>(&F.vbar[ij + kn], vbn);
       }
     }
     // phase 3: fast-time-averaged fluxes through the boundary faces; Dnew of
@@ -581,8 +599,8 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int vw
     if (b.east_edge && i == ie + 1 && j >= b.jstrV && j <= je) dv = true;
     if (b.south_edge && j == b.jstrV - 1 && i >= b.istrR && i <= b.iendR) dv = true;
     if (b.north_edge && j == je + 1 && i >= b.istrR && i <= b.iendR) dv = true;
-    if (du) F.DU_avg1[ij] = F.DU_avg1[ij] + cff1 * (Dn(q, g) + Dn(q - 1, g - 1)) * (ubn) * F.dn_u[ij];
-    if (dv) F.DV_avg1[ij] = F.DV_avg1[ij] + cff1 * (Dn(q, g) + Dn(q - kFX, g - kGX)) * (vbn) * F.dm_v[ij];
+    if (du) gst<kWT>(&F.DU_avg1[ij], F.DU_avg1[ij] + cff1 * (Dn(q, g) + Dn(q - 1, g - 1)) * (ubn) * F.dn_u[ij]);
+    if (dv) gst<kWT>(&F.DV_avg1[ij], F.DV_avg1[ij] + cff1 * (Dn(q, g) + Dn(q - kFX, g - kGX)) * (vbn) * F.dm_v[ij]);
     (void)sj;
   }
 }
@@ -972,7 +990,13 @@ void launch_fast_step(const Dev& d, hipStream_t s, const FBCoef& c, const Tlev& 
         else if (cmode == 1) { if (wr) S2D_FB(true, 1, true); else S2D_FB(true, 1, false); }
         else { if (wr) S2D_FB(true, 2, true); else S2D_FB(true, 2, false); }
       } else {
-        if (cmode == 0) { if (wr) S2D_FB(false, 0, true); else S2D_FB(false, 0, false); }
+        // store-flavour A/B on the two bench instances (C2: periodic, C3: closed walls folded in)
+        static const int wt = [] { const char* e = getenv("ROMS_GPU_S2D_WT"); return e ? atoi(e) : 1; }();
+        if (cmode == 0 && wr && wt == 0) hipLaunchKernelGGL((k_s2d_fb<false, 0, true, 0>), gr, bl, 0, s, d, RB, c, vwrap, part);
+        else if (cmode == 0 && wr && wt == 2) hipLaunchKernelGGL((k_s2d_fb<false, 0, true, 2>), gr, bl, 0, s, d, RB, c, vwrap, part);
+        else if (cmode == 2 && !wr && wt == 0) hipLaunchKernelGGL((k_s2d_fb<false, 2, false, 0>), gr, bl, 0, s, d, RB, c, vwrap, part);
+        else if (cmode == 2 && !wr && wt == 2) hipLaunchKernelGGL((k_s2d_fb<false, 2, false, 2>), gr, bl, 0, s, d, RB, c, vwrap, part);
+        else if (cmode == 0) { if (wr) S2D_FB(false, 0, true); else S2D_FB(false, 0, false); }
         else if (cmode == 1) { if (wr) S2D_FB(false, 1, true); else S2D_FB(false, 1, false); }
         else { if (wr) S2D_FB(false, 2, true); else S2D_FB(false, 2, false); }
       }
