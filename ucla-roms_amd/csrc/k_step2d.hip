@@ -914,16 +914,19 @@ void launch_step2d(const Dev& d, hipStream_t s, const Tlev& t, const double* w1,
   }
   launch_fast_step(de, s, c, t);
   launch_river_s2d(d, s, t.knew);   // step2d_FB.F:531-554
+  const int vwrap = (d.halo == nullptr && !d.p.s2d_split) ? (b.ew_periodic ? 1 : 0) | (b.ns_periodic ? 2 : 0) : 0;
   if (t.iif == t.nfast) {
     const Range RB{b.istrR, b.iendR, b.jstrR, b.jendR};
     hipLaunchKernelGGL(k_s2d_last, grid_of(RB), dim3(kBX, kBY), 0, s, d, RB, t.knew);
-    launch_set_depth(d, s, t);
+    launch_set_depth(d, s, t, !vwrap);   // vwrap: its z_w, z_r, Hz wrap joins the list below
   }
-  const int vwrap = (d.halo == nullptr && !d.p.s2d_split) ? (b.ew_periodic ? 1 : 0) | (b.ns_periodic ? 2 : 0) : 0;
   if (vwrap) {
     // halos were read from periodic images during the loop; refresh all four
-    // time slots once at its end (the same values the per-step wraps give)
-    if (t.iif == t.nfast) launch_exchange_list(d, s, ExchList{{d.f.zeta, d.f.ubar, d.f.vbar}, {4, 4, 4}, 3});
+    // time slots once at its end (the same values the per-step wraps give),
+    // in one launch with set_depth's z_w, z_r, Hz (set_depth reads no zeta halo)
+    if (t.iif == t.nfast)
+      launch_exchange_list(d, s, ExchList{{d.f.zeta, d.f.ubar, d.f.vbar, d.f.z_w, d.f.z_r, d.f.Hz},
+                                          {4, 4, 4, b.N + 1, b.N, b.N}, 6});
     return;
   }
   if (K > 1) {

@@ -47,12 +47,12 @@ __global__ void __launch_bounds__(256) k_set_depth(Dev d, Range R, int iic, int 
   }
 }
 
-void launch_set_depth(const Dev& d, hipStream_t s, const Tlev& t) {
+void launch_set_depth(const Dev& d, hipStream_t s, const Tlev& t, bool exchange) {
   const Bounds& b = d.b;
   Range R{b.istrR, b.iendR, b.jstrR, b.jendR};
   hipLaunchKernelGGL(k_set_depth, grid_of(R), dim3(kBX, kBY), 0, s, d, R, t.iic, t.knew);
   if (t.iic == 0) launch_exchange(d, s, d.f.hinv, 1);
-  launch_exchange_list(d, s, ExchList{{d.f.z_w, d.f.z_r, d.f.Hz}, {b.N + 1, b.N, b.N}, 3});
+  if (exchange) launch_exchange_list(d, s, ExchList{{d.f.z_w, d.f.z_r, d.f.Hz}, {b.N + 1, b.N, b.N}, 3});
 }
 
 // ---------------------------------------------------------------------------
