@@ -155,6 +155,21 @@ def test_fast_loop_exchange_interval_bitwise(kind, npx, npe, k, monkeypatch):
     check_decomposition(_case(kind), npx, npe)
 
 
+@pytest.mark.parametrize("k", ["6", "8"])
+@pytest.mark.parametrize("kind,npx,npe", [("filament", 2, 1), ("basin", 2, 1)])
+def test_fast_loop_wide_interval_bitwise(kind, npx, npe, k, monkeypatch):
+    """The longest exchange intervals (halos 12 and 16 deep, 10 and 14 extra
+    ghost cells) on subdomains just wide enough (LLm/np >= 2K+2): bitwise
+    equal to the single domain, and the interval actually taken (one
+    zeta/ubar/vbar swap per K fast steps)."""
+    monkeypatch.setenv("ROMS_GPU_S2D_K", k)
+    case = _case(kind)
+    assert case["LLm"] // npx >= 2 * int(k) + 2 and case["MMm"] // npe >= 2 * int(k) + 2
+    check_decomposition(case, npx, npe)
+    parts, _ = run_decomposed(case, npx, npe, 1, fields=("zeta",), probe=lambda m: m.halo_exchanges())
+    assert {p[5][1] for p in parts} == {int(k)}
+
+
 def test_fast_loop_exchange_count(monkeypatch):
     """Exchanges per whole step on a 2x2 grid: one per fast step at K = 1;
     with K > 1 one per K fast steps plus the start-of-loop swap of the fast

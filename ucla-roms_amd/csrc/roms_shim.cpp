@@ -661,13 +661,13 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     // carry gx = 2*(s2d_k-1) extra ghost rows/columns (roms_dev.h).  Not with
     // open boundaries (their 1-D boundary arrays end at the reference's halo)
     // or the split fast-step kernels; rivers and pipes fall back to every step
-    // at run time.  ROMS_GPU_S2D_K=1..4 (default 4; 1: every step).  One
+    // at run time.  ROMS_GPU_S2D_K=1..8 (default 4; 1: every step).  One
     // GPU with every exchange self-addressed through IPC (C2, 92 exchanges
     // per step at K = 1): 7.48 / 7.11 / 7.01 / 6.98 ms per step at K = 1..4
     // against 6.49 without a communicator (profiles/r4_j_fast_exchange_interval_ab.txt).
     int k = 4;
-    const char* ek = getenv("ROMS_GPU_S2D_K");
-    if (ek && ek[0] >= '1' && ek[0] <= '4') k = ek[0] - '0';
+    const char* ek = getenv("ROMS_GPU_S2D_K");   // 1..8 (an interconnect slower than one GPU's may want 6-8)
+    if (ek && atoi(ek) >= 1 && atoi(ek) <= 8) k = atoi(ek);
     const char* es = getenv("ROMS_GPU_S2D_SPLIT");
     const bool split = es && es[0] == '1';
     const int obc = cfg->obc & ((dims->ew_periodic ? 0 : 3) | (dims->ns_periodic ? 0 : 12));
