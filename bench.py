@@ -264,6 +264,16 @@ def run_workload(kind, romsgpu, comm, rank, world, local_rank, steps, warmup, ti
         gbs = nbytes / (avg * 1e-3) / 1e9 if avg > 0 else 0.0
         routines[r] = {"ms_per_call": avg, "calls_per_step": per_step, "ms_per_step": avg * per_step,
                        "bytes_per_call": nbytes, "achieved_GBs": gbs, "frac": gbs / HBM_PEAK_GBS}
+        if r == "prsgrd":
+            # whole steps run the horizontal momentum r.h.s. of the following
+            # pre_step3d / step3d_uv1 inside prsgrd's kernel (k_prsgrd_uv<true>):
+            # its time is in this routine; bytes_per_call stays prsgrd's own
+            # passes, the *_with_rhs figures add the r.h.s. inputs u, v(nrhs),
+            # FlxU, FlxV (4 passes) that the fused kernel reads
+            wb = nbytes + 8.0 * 4 * cells3
+            routines[r].update({"includes": "uv horizontal r.h.s. of pre_step3d and step3d_uv1",
+                                "bytes_per_call_with_rhs": wb,
+                                "frac_with_rhs": (wb / (avg * 1e-3) / 1e9 if avg > 0 else 0.0) / HBM_PEAK_GBS})
     dom = max(routines, key=lambda k: routines[k]["ms_per_step"])
     D = routines[dom]
     # the fused barotropic kernel alone: 35 2-D passes per fast step over its
