@@ -161,17 +161,20 @@ def test_gloo_exchange_fills_every_halo(npx, npe, ewp, nsp):
     assert all(v == 0 for v in res.values()), res
 
 
-@pytest.mark.parametrize("H", [4, 8])
-@pytest.mark.parametrize("npx,npe,ewp,nsp", [(2, 1, 1, 1), (2, 2, 1, 1), (2, 2, 0, 0), (2, 2, 1, 0), (1, 2, 1, 0)])
-def test_gloo_wide_exchange_fills_every_halo(npx, npe, ewp, nsp, H):
-    """The fast loop's H-deep exchange (H = 2K, roms_gpu_halo_map_wide): every
-    cell of the H-deep frame that has a neighbour, a periodic image or a
-    closed-edge ghost row holds the global field's value after the swap."""
+@pytest.mark.parametrize("H,L,M,npx,npe,ewp,nsp",
+                         [(H, 23, 19) + c for H in (4, 8)
+                          for c in ((2, 1, 1, 1), (2, 2, 1, 1), (2, 2, 0, 0), (2, 2, 1, 0), (1, 2, 1, 0))] +
+                         [(H, 40, 36, 2, 2, 1, 1) for H in (12, 16)] + [(16, 40, 36, 2, 2, 1, 0)])
+def test_gloo_wide_exchange_fills_every_halo(H, L, M, npx, npe, ewp, nsp):
+    """The fast loop's H-deep exchange (H = 2K, roms_gpu_halo_map_wide; K up
+    to 8): every cell of the H-deep frame that has a neighbour, a periodic
+    image or a closed-edge ghost row holds the global field's value after
+    the swap."""
     world = npx * npe
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_exchange_worker, args=(r, world, port, 23, 19, npx, npe, ewp, nsp, 2, q, H))
+    procs = [ctx.Process(target=_exchange_worker, args=(r, world, port, L, M, npx, npe, ewp, nsp, 2, q, H))
              for r in range(world)]
     for p in procs:
         p.start()
