@@ -845,12 +845,6 @@ __global__ void k_s2d_edges(Dev d, FBCoef c, int phase) {
   }
 }
 
-__global__ void __launch_bounds__(256) k_s2d_last(Dev d, Range R, int knew) {
-  ROMS_IJ_OR_RETURN(R)
-  const long ij = IJ(d.b, i, j);
-  d.f.zeta[ij + (long)(knew - 1) * d.b.n2] = d.f.Zt_avg1[ij];
-}
-
 void launch_fast_step(const Dev& d, hipStream_t s, const FBCoef& c, const Tlev& t);
 
 void launch_step2d(const Dev& d, hipStream_t s, const Tlev& t, const double* w1, const double* w2) {
@@ -915,11 +909,8 @@ void launch_step2d(const Dev& d, hipStream_t s, const Tlev& t, const double* w1,
   launch_fast_step(de, s, c, t);
   launch_river_s2d(d, s, t.knew);   // step2d_FB.F:531-554
   const int vwrap = (d.halo == nullptr && !d.p.s2d_split) ? (b.ew_periodic ? 1 : 0) | (b.ns_periodic ? 2 : 0) : 0;
-  if (t.iif == t.nfast) {
-    const Range RB{b.istrR, b.iendR, b.jstrR, b.jendR};
-    hipLaunchKernelGGL(k_s2d_last, grid_of(RB), dim3(kBX, kBY), 0, s, d, RB, t.knew);
-    launch_set_depth(d, s, t, !vwrap);   // vwrap: its z_w, z_r, Hz wrap joins the list below
-  }
+  if (t.iif == t.nfast)   // zeta(knew) = Zt_avg1 (step2d_FB.F:566) inside set_depth's kernel, same range
+    launch_set_depth(d, s, t, !vwrap, true);   // vwrap: its z_w, z_r, Hz wrap joins the list below
   if (vwrap) {
     // halos were read from periodic images during the loop; refresh all four
     // time slots once at its end (the same values the per-step wraps give),

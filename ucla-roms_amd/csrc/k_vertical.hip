@@ -14,7 +14,10 @@ namespace roms {
 // set_depth_tile (set_depth.F:16-186): z_w, z_r, Hz from zeta(knew); at iic=0
 // also hinv and the initial fast-time fluxes DU_avg1/DV_avg1.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_set_depth(Dev d, Range R, int iic, int knew) {
+// last: the end of the fast loop -- zeta(knew) = Zt_avg1 first (the fast-time
+// average replaces the last fast step's zeta, step2d_FB.F:566), stored here
+// on the same range instead of by a launch of its own
+__global__ void __launch_bounds__(256) k_set_depth(Dev d, Range R, int iic, int knew, int last) {
   ROMS_IJ_OR_RETURN(R)
   const Bounds& b = d.b;
   const Fields& F = d.f;
@@ -32,7 +35,13 @@ __global__ void __launch_bounds__(256) k_set_depth(Dev d, Range R, int iic, int 
   const double hc = d.p.hc, ds = 1.0 / (double)N;
   const double hh = F.h[ij];
   const double hi = iic == 0 ? 1.0 / (hh + hc) : F.hinv[ij];
-  const double z = F.zeta[IJL(b, i, j, knew)];
+  double z;
+  if (last) {
+    z = F.Zt_avg1[ij];
+    F.zeta[IJL(b, i, j, knew)] = z;
+  } else {
+    z = F.zeta[IJL(b, i, j, knew)];
+  }
   double zw_prev = -hh;
   F.z_w[ij] = zw_prev;
   for (int k = 1; k <= N; k++) {
@@ -47,10 +56,10 @@ __global__ void __launch_bounds__(256) k_set_depth(Dev d, Range R, int iic, int 
   }
 }
 
-void launch_set_depth(const Dev& d, hipStream_t s, const Tlev& t, bool exchange) {
+void launch_set_depth(const Dev& d, hipStream_t s, const Tlev& t, bool exchange, bool last) {
   const Bounds& b = d.b;
   Range R{b.istrR, b.iendR, b.jstrR, b.jendR};
-  hipLaunchKernelGGL(k_set_depth, grid_of(R), dim3(kBX, kBY), 0, s, d, R, t.iic, t.knew);
+  hipLaunchKernelGGL(k_set_depth, grid_of(R), dim3(kBX, kBY), 0, s, d, R, t.iic, t.knew, (int)last);
   if (t.iic == 0) launch_exchange(d, s, d.f.hinv, 1);
   if (exchange) launch_exchange_list(d, s, ExchList{{d.f.z_w, d.f.z_r, d.f.Hz}, {b.N + 1, b.N, b.N}, 3});
 }

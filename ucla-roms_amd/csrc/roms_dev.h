@@ -367,8 +367,9 @@ void setup_pre_uv_seg();   // k_pre_uv_seg<true>'s dynamic LDS limit (k_pre_step
 inline size_t col_smem_bytes(const Dev& d, int nslots) {
   return d.f.colscr ? 0 : (size_t)nslots * (d.b.N + 1) * 64 * sizeof(double);
 }
-// exchange = false: the caller exchanges z_w, z_r, Hz itself (merged with its own list)
-void launch_set_depth(const Dev& d, hipStream_t s, const Tlev& t, bool exchange = true);
+// exchange = false: the caller exchanges z_w, z_r, Hz itself (merged with its own list);
+// last: end of the fast loop, zeta(knew) = Zt_avg1 stored first (step2d_FB.F:566)
+void launch_set_depth(const Dev& d, hipStream_t s, const Tlev& t, bool exchange = true, bool last = false);
 // store_huv: also Hz_u/Hz_v (set_depth.F:220,227), read only by extract_data.F
 void launch_set_huv(const Dev& d, hipStream_t s, const Tlev& t, bool store_huv = true);
 void launch_set_huv1(const Dev& d, hipStream_t s, const Tlev& t);
