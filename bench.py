@@ -2,26 +2,30 @@
 model-seconds/wallclock-sec + grid-cell-updates/sec at 1/2/4/8 GPU; % HBM
 roofline).
 
-Primary workload (BASELINE.json configs[1]): Filament
-physics + salinity (linear EOS, T and S), 512x512x50 per GPU, dt=5 s,
-ndtfast=60 -> nfast=82, dx=100 m, dy=25 m, doubly periodic, synthetic
-analytic initial state.  One "step" = one full roms_step (main.F:333-520):
-3 rho_eos, 3 omega, 2 prsgrd, pre_step3d, set_HUV/HUV1, step3d_uv1, visc3d,
-82 barotropic step2d_FB, step3d_uv2, step3d_t, t3dmix.  The step-opening
-rho_eos(nrhs) (main.F:397) reads exactly the t, z_r, Hz the previous step's
-closing rho_eos(nnew) (main.F:479) read, so the library keeps those outputs
-instead of recomputing them (bitwise-equal runs, ROMS_GPU_RHO_REUSE=0 turns it
-off); roofline_step's byte count leaves that pass out, and the two Hz_u/Hz_v
-stores of set_HUV that whole steps skip (extract_data inputs only,
-ROMS_GPU_HZ_UV=1 keeps them).  State is resident in
-HBM before the timed region; steady steps replay captured HIP graphs.  N GPUs:
-weak scaling on an npx x npe processor grid (1x1, 2x1, 2x2, 4x2) of 512x512
-subdomains of one periodic domain, halo exchanges inside the step graphs.
-
-Secondary workload, reported in the same JSON line as "c3" (SURVEY.md 8(d)
-C3, the north_star's roofline target): the 1024x1024x100 closed basin with
+Primary workload (the north_star's target configuration, SURVEY.md 8(d) C3,
+BASELINE.json configs[2] on one GPU): the 1024x1024x100 closed basin with
 NONLIN+SPLIT EOS, T+S and LMD_MIXING+KPP+BKPP+RIMIX+NONLOCAL (dt=300 s,
-nfast=82), strong-scaled over the same processor grid.
+ndtfast=60 -> nfast=82), synthetic analytic initial state.  One "step" = one
+full roms_step (main.F:333-520): rho_eos, set_HUV, omega, lmd_vmix, prsgrd,
+pre_step3d, set_HUV1, omega, rho_eos, lmd_vmix, prsgrd, step3d_uv1, visc3d,
+82 barotropic step2d_FB, step3d_uv2, omega, step3d_t, t3dmix, rho_eos.  The
+step-opening rho_eos(nrhs) (main.F:397) reads exactly the t, z_r, Hz the
+previous step's closing rho_eos(nnew) (main.F:479) read, so the library keeps
+those outputs instead of recomputing them (bitwise-equal runs,
+ROMS_GPU_RHO_REUSE=0 turns it off); roofline_step's byte count leaves that pass
+out, and the two Hz_u/Hz_v stores of set_HUV that whole steps skip
+(extract_data inputs only, ROMS_GPU_HZ_UV=1 keeps them).  State is resident in
+HBM before the timed region; steady steps replay captured HIP graphs.  N GPUs:
+strong scaling of the one basin over an npx x npe processor grid (1x1, 2x1,
+2x2, 4x2), halo exchanges inside the step graphs.  "north_star_loop" is the
+north_star's own roofline target: step2d_FB + step3d_uv1 + step3d_uv2 +
+step3d_t algorithmic bytes over their summed routine time.
+
+Secondary workload, reported in the same JSON line as "c2" (BASELINE.json
+configs[1]): Filament physics + salinity (linear EOS, T and
+S), 512x512x50 per GPU, dt=5 s, ndtfast=60 -> nfast=82, dx=100 m, dy=25 m,
+doubly periodic, weak-scaled (512x512 per GPU).  --workload c2 makes it the
+primary line and C3 the secondary ("c3").
 
 value = grid-cell updates per second summed over ranks (interior I*J*N per
 baroclinic step); model seconds per wall second beside it.  roofline: the
@@ -34,7 +38,7 @@ cpu_baseline (rank 0, N=1): the plain-C oracle (oracle/, the CPU restatement,
 host core (P processes x 1 thread, each on its own cut of the grid, started
 together), run before the GPU is touched.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3] [--no-c3]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2] [--no-secondary]
 With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py starts the N
 ranks itself (one process per GPU, RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set
 before any GPU call) and relays rank 0's line; under torchrun it is one rank.
@@ -224,7 +228,8 @@ def launch_ranks(args, argv):
 # ---------------------------------------------------------------------------
 # one workload on this rank
 # ---------------------------------------------------------------------------
-def run_workload(kind, romsgpu, comm, rank, world, local_rank, steps, warmup, timing_steps, barrier, allmax):
+def run_workload(kind, romsgpu, comm, rank, world, local_rank, steps, warmup, timing_steps, barrier, allmax,
+                 step_only=False):
     npx, npe = proc_grid(world)
     c3 = kind == "c3"
     if c3:
@@ -250,6 +255,10 @@ def run_workload(kind, romsgpu, comm, rank, world, local_rank, steps, warmup, ti
     wall = time.perf_counter() - t0
     barrier()
     elapsed = allmax(max(wall, ev_ms / 1e3))
+    if step_only:   # the whole-step time alone (the exchange-overlap A/B of a multi-rank run)
+        m.close()
+        return {"ms_per_step": 1e3 * elapsed / steps, "value": total_cells * steps / elapsed,
+                "steps": steps}
 
     # per-routine rooflines: HIP events around each routine's launches
     cells3 = Lr * Mr * Nz
@@ -276,6 +285,16 @@ def run_workload(kind, romsgpu, comm, rank, world, local_rank, steps, warmup, ti
                                 "frac_with_rhs": (wb / (avg * 1e-3) / 1e9 if avg > 0 else 0.0) / HBM_PEAK_GBS})
     dom = max(routines, key=lambda k: routines[k]["ms_per_step"])
     D = routines[dom]
+    # the north_star's roofline target: "the step2d_FB + step3d_uv/t fused
+    # loop" = the fast loop + step3d_uv1 + step3d_uv2 + step3d_t, their
+    # SURVEY.md 8(d) algorithmic bytes per step over their summed event time
+    loop = ("step2d", "step3d_uv1", "step3d_uv2", "step3d_t")
+    lb = sum(routines[r]["bytes_per_call"] * routines[r]["calls_per_step"] for r in loop)
+    lms = sum(routines[r]["ms_per_step"] for r in loop)
+    lg = lb / (lms * 1e-3) / 1e9 if lms > 0 else 0.0
+    north_star_loop = {"bound": "hbm", "achieved": lg, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": lg / HBM_PEAK_GBS,
+                       "target_frac": 0.40, "bytes_per_step": lb, "ms_per_step": lms, "routines": list(loop),
+                       "per_routine_frac": {r: routines[r]["frac"] for r in loop}}
     # the fused barotropic kernel alone: 35 2-D passes per fast step over its
     # launch time (one event interval per fast loop on a single rank)
     # C3: the dominant kernel, pre_step3d's momentum segment solver, alone
@@ -337,6 +356,7 @@ def run_workload(kind, romsgpu, comm, rank, world, local_rank, steps, warmup, ti
         "scaling": "strong" if c3 else "weak",
         "steps": steps, "warmup": warmup,
         "roofline": roofline,
+        "north_star_loop": north_star_loop,
         "roofline_routine": {"bound": "hbm", "achieved": D["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": D["frac"], "traffic": pmc_traffic(dom, c3),
                              "routine": dom + (" (one fast step: k_s2d_fb + edges + halo)" if dom == "step2d" else ""),
@@ -387,9 +407,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--timing-steps", type=int, default=3, help="eager steps per routine for the event timings")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", choices=("c2", "c3"), default="c2", help="the workload of the primary line")
-    ap.add_argument("--no-c3", action="store_true", help="skip the secondary C3 object")
+    ap.add_argument("--workload", choices=("c2", "c3"), default="c3", help="the workload of the primary line")
+    ap.add_argument("--no-secondary", "--no-c3", dest="no_secondary", action="store_true",
+                    help="skip the secondary workload's object (c2 under the default c3 line)")
     args = ap.parse_args()
+    secondary = "c2" if args.workload == "c3" else "c3"
     world_env = os.environ.get("WORLD_SIZE")
     if args.gpus > 1 and world_env is None:
         return launch_ranks(args, sys.argv[1:])
@@ -409,8 +431,8 @@ def main():
     cpu = {}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu[args.workload] = cpu_baseline(args.workload)
-        if args.workload == "c2" and not args.no_c3:
-            cpu["c3"] = cpu_baseline("c3")
+        if not args.no_secondary:
+            cpu[secondary] = cpu_baseline(secondary)
 
     # the JSON line is the only thing on stdout: libraries (RCCL prints a
     # version banner at init) write to fd 1, so point it at stderr for the run
@@ -498,6 +520,19 @@ def main():
         prim = run_workload(args.workload, romsgpu, comm, rank, world, local_rank, args.steps, args.warmup,
                             args.timing_steps, barrier, allmax)
     prim["config"]["comm_bootstrap"] = bootstrap
+    if comm is not None and world > 1 and os.environ.get("ROMS_GPU_XOVERLAP") is None:
+        # the deferred-exchange overlap (on by default with > 1 rank) A/B'd in
+        # the same job: the same workload with every exchange in place
+        os.environ["ROMS_GPU_XOVERLAP"] = "0"
+        try:
+            off = run_workload(args.workload, romsgpu, comm, rank, world, local_rank, args.steps, args.warmup,
+                               args.timing_steps, barrier, allmax, step_only=True)
+        finally:
+            del os.environ["ROMS_GPU_XOVERLAP"]
+        prim["config"]["exchange_overlap"] = {
+            "default": "on (3-D exchanges deferred beside the next non-reading routine)",
+            "ms_per_step_on": prim["ms_per_step"], "ms_per_step_off": off["ms_per_step"],
+            "value_off": off["value"]}
     out = {
         "metric": "grid-cell-updates/sec",
         "value": prim["value"],
@@ -515,20 +550,23 @@ def main():
         "config": prim["config"],
         "model_seconds_per_wallclock_sec": prim["model_seconds_per_wallclock_sec"],
     }
-    for k in ("roofline", "roofline_routine", "roofline_step", "routines", "kernel_s2d_fb"):
+    for k in ("roofline", "north_star_loop", "roofline_routine", "roofline_step", "routines", "kernel_s2d_fb"):
         out[k] = prim[k]
     if args.workload in cpu:
         out["cpu_baseline"] = cpu[args.workload]
-    if args.workload == "c2" and not args.no_c3:
-        # the north_star's target configuration, fewer steps (84 ms each on one GPU)
-        sec = run_workload("c3", romsgpu, comm, rank, world, local_rank, min(args.steps, 10), min(args.warmup, 2),
-                           min(args.timing_steps, 2), barrier, allmax)
+    if not args.no_secondary:
+        # the other BASELINE configuration, fewer steps when it is C3 (61 ms each on one GPU)
+        c3s = secondary == "c3"
+        sec = run_workload(secondary, romsgpu, comm, rank, world, local_rank, min(args.steps, 10) if c3s else args.steps,
+                           min(args.warmup, 2) if c3s else args.warmup, min(args.timing_steps, 2) if c3s else
+                           args.timing_steps, barrier, allmax)
         sec["metric"] = "grid-cell-updates/sec"
         sec["unit"] = "cell-updates/s"
-        sec["data"] = "synthetic (analytic closed basin, SURVEY.md 8(d) C3)"
-        if "c3" in cpu:
-            sec["cpu_baseline"] = cpu["c3"]
-        out["c3"] = sec
+        sec["data"] = ("synthetic (analytic closed basin, SURVEY.md 8(d) C3)" if c3s else
+                       "synthetic (analytic Filament+S initial state, ana_grid/ana_init of tests/Filament)")
+        if secondary in cpu:
+            sec["cpu_baseline"] = cpu[secondary]
+        out[secondary] = sec
     if comm is not None:
         romsgpu.comm_destroy(comm)
     if rank == 0:

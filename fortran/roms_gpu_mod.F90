@@ -294,6 +294,14 @@ module roms_gpu_mod
       type(c_ptr), value :: ctx
       type(c_ptr), intent(out) :: comm
     end function
+    integer(c_int) function roms_gpu_comm_destroy(comm) bind(c)
+      import :: c_int, c_ptr
+      type(c_ptr), value :: comm
+    end function
+    ! 1: IPC peer writes, 0: RCCL send/recv (or one rank), -1: a wait timed out
+    integer(c_int) function roms_gpu_halo_transport() bind(c)
+      import :: c_int
+    end function
   end interface
 
 contains

@@ -11,6 +11,7 @@ program dropin_driver
   use roms_gpu_mod
   use roms_gpu_glue
   use scalars
+  use roms_step_seq
   implicit none
   type(roms_case) :: c
   type(roms_tlev) :: tl
@@ -44,34 +45,4 @@ program dropin_driver
   end do
   call roms_gpu_check(roms_gpu_finalize(), 'finalize')
 
-contains
-
-  ! main.F:374-479 with the Filament switches (no LMD_MIXING, no forcing)
-  subroutine roms_step
-    nstp = 1 + mod(iic - ntstart, 2)
-    nrhs = nstp; nnew = 3
-    call rho_eos(nrhs)
-    call set_HUV
-    call omega
-    call prsgrd
-    call pre_step3d(0)
-    call set_HUV1(0)
-    nrhs = 3; nnew = 3 - nstp
-    call omega
-    call rho_eos(nrhs)
-    call prsgrd
-    call step3d_uv1(0)
-    call visc3d
-    do iif = 1, nfast
-      kstp = knew
-      knew = kstp + 1
-      if (knew > 4) knew = 1
-      call step2d
-    end do
-    call step3d_uv2(0)
-    call omega
-    call step3d_t(0)
-    call t3dmix
-    call rho_eos(nnew)
-  end subroutine roms_step
 end program dropin_driver

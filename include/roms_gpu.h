@@ -283,7 +283,9 @@ int roms_gpu_halo_transport(void);
  * exchanges zeta/ubar/vbar after every *fast_interval-th fast step over
  * 2*fast_interval-deep halos and recomputes the overlap in between (1: every
  * fast step, as step2d_FB.F:572-574; multi-rank runs without open edges
- * default to 4, ROMS_GPU_S2D_K=1..4; rivers and pipes take every step).     */
+ * default to 4, ROMS_GPU_S2D_K=1..8; K is lowered until 2K+2 fits the
+ * smallest subdomain of the mpi_setup.F split, the same on every rank;
+ * rivers and pipes take every step).                                         */
 int roms_gpu_halo_exchanges(long *per_step, int *fast_interval);
 /* Self-test of the allocation path: `chunks` arrays of n doubles filled
  * with ones and freed, then allocated again through the library's

@@ -30,6 +30,9 @@ the same state bitwise, and the oracle's within the north_star RMS bound:
   * the C4 Iceland stand-in switch set (open edges, sponge, island, CURVGRID,
     BULK_FRC) at a small size, 10 steps.
 """
+import os
+import signal
+import subprocess
 import threading
 
 import numpy as np
@@ -200,3 +203,56 @@ def test_dropin_sequence_c1_filament_128_2x2():
             g = got[f][..., 2:Mm + 2, 2:Lm + 2]
             e = float(np.sqrt(np.mean((g - w) ** 2)))
             assert e < RMS_RUN, (f, iSW, jSW, e)
+
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+MPIEXEC = "/opt/conda/bin/mpiexec"
+MPI_DRIVER = os.path.join(ROOT, "fortran", "dropin_mpi_driver")
+
+
+def _oracle_c1_2x2(nsteps):
+    cfg = oracle.filament_cfg(LLm=128, MMm=128, N=20, np_xi=2, np_eta=2)
+    o = oracle.Oracle(cfg)
+    o.init()
+    want = [o.norms()]
+    for _ in range(nsteps):
+        o.step()
+        want.append(o.norms())
+    return want
+
+
+@pytest.mark.skipif(not os.path.exists(MPIEXEC), reason="MPICH mpiexec not in this image")
+def test_fortran_mpi_dropin_c1_2x2_processes():
+    """The north_star's deployment as it would run: a Fortran + MPI host
+    (fortran/mpi/dropin_mpi_driver.F90) started by mpiexec as 4 processes,
+    bootstrapped like the reference (MPI_Init, mpi_setup's 2x2 grid,
+    main.F:26-28 / mpi_setup.F:14-211), the library's communicator built by
+    roms_gpu_comm_create_host over a Fortran MPI_Allgather callback, and the
+    reference's roms_step calling the drop-ins by name.  The processes share
+    this box's one GPU; halos move by IPC peer writes between them.  Rank 0's
+    per-step diag norms of BASELINE C1 (Filament 128x128x20, 20 steps) equal
+    the oracle's 2x2 per-rank sums in every ES23.16 column."""
+    assert os.path.exists(MPI_DRIVER), "build() makes fortran/dropin_mpi_driver"
+    nsteps = 20
+    p = subprocess.Popen([MPIEXEC, "-n", "4", MPI_DRIVER, str(nsteps), "2", "2"], stdout=subprocess.PIPE,
+                         stderr=subprocess.PIPE, text=True, start_new_session=True)
+    try:
+        out, err = p.communicate(timeout=300)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        raise
+    assert p.returncode == 0, (p.returncode, out[-2000:], err[-3000:])
+    head = [ln for ln in out.splitlines() if ln.startswith("#")]
+    assert head and "halo transport ipc" in head[0], out[-2000:]
+    rows = [ln.split() for ln in out.splitlines() if ln.strip() and not ln.startswith("#")]
+    got = {int(r[0]): [float(x) for x in r[1:5]] for r in rows if len(r) == 5 and r[0].isdigit()}
+    assert sorted(got) == list(range(nsteps + 1)), out[-2000:]
+    want = _oracle_c1_2x2(nsteps)
+    exact = 0
+    for s_, b in enumerate(want):
+        for x, y in zip(got[s_], b):
+            assert abs(x - y) <= 1e-12 * abs(y), (s_, got[s_], b)
+            exact += ("%23.16E" % x) == ("%23.16E" % y)
+    print("Fortran+MPI C1 2x2 (4 processes): diag columns equal to the oracle's digits: %d of %d" %
+          (exact, 4 * (nsteps + 1)))
+    assert exact == 4 * (nsteps + 1)

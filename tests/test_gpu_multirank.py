@@ -170,6 +170,24 @@ def test_fast_loop_wide_interval_bitwise(kind, npx, npe, k, monkeypatch):
     assert {p[5][1] for p in parts} == {int(k)}
 
 
+@pytest.mark.parametrize("kind", ["filament", "basin"])
+@pytest.mark.parametrize("LL,npx,k,k_taken", [(81, 8, "4", 2), (100, 12, "3", 1)])
+def test_fast_loop_interval_fits_uneven_split(kind, LL, npx, k, k_taken, monkeypatch):
+    """Uneven mpi_setup splits (mpi_setup.F:115-125): the edge ranks lose the
+    remainder, so LLm/np is not the smallest subdomain (81 over 8: the east
+    rank is 7 wide; 100 over 12: the edge ranks are 5 wide).  The library
+    lowers K until 2K+2 fits the narrowest rank -- every rank
+    takes the same K -- and the run stays bitwise equal to the single domain."""
+    monkeypatch.setenv("ROMS_GPU_S2D_K", k)
+    base = _case(kind)
+    case = dict(base, LLm=LL, MMm=16, sizex=base["sizex"] * LL / base["LLm"], sizey=base["sizey"] * 16 / base["MMm"])
+    widths = [romsgpu.rank_extent(LL, npx, r)[0] for r in range(npx)]
+    assert min(widths) < LL // npx
+    check_decomposition(case, npx, 1, nsteps=3)
+    parts, _ = run_decomposed(case, npx, 1, 1, fields=("zeta",), probe=lambda m: m.halo_exchanges())
+    assert {p[5][1] for p in parts} == {k_taken}, (widths, [p[5] for p in parts])
+
+
 def test_fast_loop_exchange_count(monkeypatch):
     """Exchanges per whole step on a 2x2 grid: one per fast step at K = 1;
     with K > 1 one per K fast steps plus the start-of-loop swap of the fast
@@ -305,3 +323,48 @@ def test_rim_first_overlap_bitwise_equals_serial_exchanges():
     for r in range(4):
         for f in FIELDS:
             assert np.array_equal(serial[r][4][f], over[r][4][f]), (r, f)
+
+
+@pytest.mark.parametrize("kind", ["basin_lmd", "filament", "basin_flux", "pipes"])
+@pytest.mark.parametrize("npx,npe", [(2, 2), (3, 2)])
+def test_deferred_exchanges_late_unpack_bitwise(kind, npx, npe, monkeypatch):
+    """Deferred 3-D exchanges (on by default with > 1 rank):
+    set_HUV's beside lmd_vmix(nstp), omega's and lmd_vmix's beside prsgrd,
+    pre_step3d's tracer swap beside set_HUV1, set_HUV1's beside rho_eos(nrhs),
+    the corrector's omega and lmd_vmix beside prsgrd, the closing omega's
+    beside step3d_t.  With every forked exchange's unpack held back 300 us
+    (ROMS_GPU_XDELAY_US) a routine that reads a halo before its join would
+    read the previous step's values: the subdomains still equal the single
+    domain bitwise."""
+    monkeypatch.setenv("ROMS_GPU_XDELAY_US", "300")
+    check_decomposition(_case(kind), npx, npe)
+
+
+def test_deferred_exchanges_off_equals_on():
+    """ROMS_GPU_XOVERLAP=0 (every exchange in place, the reference's order)
+    and the default deferred order give the same fields bitwise."""
+    case = _case("basin_lmd")
+    on, _ = run_decomposed(case, 2, 2, 5)
+    os.environ["ROMS_GPU_XOVERLAP"] = "0"
+    try:
+        off, _ = run_decomposed(case, 2, 2, 5)
+    finally:
+        del os.environ["ROMS_GPU_XOVERLAP"]
+    for r in range(4):
+        for f in FIELDS:
+            assert np.array_equal(on[r][4][f], off[r][4][f]), (r, f)
+
+
+@pytest.mark.parametrize("bit,reader", [(2, "pre_step3d"), (4, "rho_eos(nrhs)"), (8, "omega (corrector)"),
+                                        (16, "step3d_uv1")])
+def test_deferred_exchange_missing_join_is_detected(bit, reader, monkeypatch):
+    """The delay hook is a real check: with one join left out (test hook
+    ROMS_GPU_XTEST_SKIPJOIN=bit) the routine after it reads a halo before the
+    late unpack and the decomposition no longer matches.  (The join before
+    the predictor's omega, bit 1, cannot be shown this way: set_HUV
+    recomputes exactly the FlxU that step3d_uv2 left in the halo, so the
+    stale and the fresh halo are equal bitwise.)"""
+    monkeypatch.setenv("ROMS_GPU_XDELAY_US", "2000")
+    monkeypatch.setenv("ROMS_GPU_XTEST_SKIPJOIN", str(bit))
+    with pytest.raises(AssertionError):
+        check_decomposition(_case("basin_flux"), 2, 2)

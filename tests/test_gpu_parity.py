@@ -508,6 +508,36 @@ def test_prsgrd_uv_tile_rows_bitwise(case, monkeypatch):
         assert np.array_equal(out[0][n], out[1][n]), n
 
 
+@pytest.mark.parametrize("case", ["filament", "basin_odd", "basin_obc_odd"])
+def test_ld16_windows_bitwise(case, monkeypatch):
+    """LDS windows read two doubles per lane (ROMS_GPU_LD16, default with the
+    padded pitch: k_prsgrd_uv's raw and u/v windows) equal the 8-B form
+    bitwise over 4 whole steps and one prsgrd routine call; odd Lm puts the
+    last pair of a row half outside -1..Lm+2 (its upper double must read as 0)."""
+    if case == "basin_odd":
+        cfg = basin_cfg(LLm=71, MMm=41, N=12, nonlin=True)
+    elif case == "basin_obc_odd":
+        cfg = basin_cfg(LLm=69, MMm=37, N=10, nonlin=True)
+        cfg.obc, cfg.island, cfg.curvgrid = 15, 1, 0
+    else:
+        cfg = oracle.filament_cfg(LLm=64, MMm=40, N=16, np_xi=1, np_eta=1)
+    out = []
+    for env in ("0", "1"):
+        monkeypatch.setenv("ROMS_GPU_LD16", env)
+        m = romsgpu.Model.from_case(cfg.case_id, cfg.LLm, cfg.MMm, cfg.N, cfg.NT, salinity=bool(cfg.salinity),
+                                    nonlin_eos=bool(cfg.nonlin_eos), dt=cfg.dt, ndtfast=cfg.ndtfast,
+                                    sizex=cfg.sizex, sizey=cfg.sizey, obc=cfg.obc, island=bool(cfg.island))
+        m.step(4)
+        r = {n: m.get(n) for n in ("zeta", "ubar", "vbar", "u", "v", "t", "rufrc", "rvfrc")}
+        m.prsgrd()
+        m.sync()
+        r["ru"], r["rv"] = m.get("ru"), m.get("rv")
+        out.append(r)
+        m.close()
+    for n in out[0]:
+        assert np.array_equal(out[0][n], out[1][n]), n
+
+
 @pytest.mark.parametrize("lmd", [oracle.LMD_ICELAND, oracle.LMD_ALL | oracle.LMD_DDMIX])
 def test_kpp_int_staged_rig_bitwise(lmd, monkeypatch):
     """k_kpp_int with the Rig stencil windows staged in LDS (ROMS_GPU_KPP_TY

@@ -24,7 +24,7 @@ r = d["routines"]
 print("%-28s %7.2f ms/step | " % (sys.argv[2], d["ms_per_step"]) + " ".join("%s=%.3f" % (k, v["ms_per_call"]) for k, v in r.items()))
 PY
 }
-wargs() { if [ "$1" = c3 ]; then echo "--workload c3 --steps 5 --warmup 2 --timing-steps 2"; else echo "--steps 20 --warmup 3 --timing-steps 3 --no-c3"; fi; }
+wargs() { if [ "$1" = c3 ]; then echo "--workload c3 --steps 5 --warmup 2 --timing-steps 2"; else echo "--workload c2 --steps 20 --warmup 3 --timing-steps 3 --no-secondary"; fi; }
 case $CMD in
 suite)
   timeout -k 10 1500 $PYT tests -m gpu -x > $O/tests_$TAG.log 2>&1 || { echo TESTFAIL; tail -30 $O/tests_$TAG.log; exit 1; }
@@ -42,15 +42,15 @@ bench)
 trace)
   W=${1:-c3}; M=k_step3d_t_seg; [ $W = c2 ] && M=k_step3d_t_v
   cd /tmp && export TMPDIR=/tmp
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_$TAG -o run -- python $R/bench.py --workload $W --steps 5 --warmup 1 --timing-steps 1 --no-cpu-baseline --no-c3 > $O/kt_$TAG.json 2> $O/kt_$TAG.err || { tail -5 $O/kt_$TAG.err; exit 1; }
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_$TAG -o run -- python $R/bench.py --workload $W --steps 5 --warmup 1 --timing-steps 1 --no-cpu-baseline --no-secondary > $O/kt_$TAG.json 2> $O/kt_$TAG.err || { tail -5 $O/kt_$TAG.err; exit 1; }
   python3 $R/tools/prof_summary.py $(find $O/kt_$TAG -name "*kernel_trace.csv") --steps 4 --marker $M > $O/kt_$TAG.txt 2>&1
   head -30 $O/kt_$TAG.txt ;;
 pmc)
   cd /tmp && export TMPDIR=/tmp
   export ROMS_GPU_NO_GRAPH=1
   for W in c2 c3; do
-    if [ $W = c2 ]; then B="python $R/bench.py --no-cpu-baseline --no-c3 --timing-steps 1 --steps 4 --warmup 1"; M=k_step3d_t_v
-    else B="python $R/bench.py --no-cpu-baseline --no-c3 --workload c3 --timing-steps 1 --steps 2 --warmup 1"; M=k_step3d_t_seg; fi
+    if [ $W = c2 ]; then B="python $R/bench.py --no-cpu-baseline --no-secondary --workload c2 --timing-steps 1 --steps 4 --warmup 1"; M=k_step3d_t_v
+    else B="python $R/bench.py --no-cpu-baseline --no-secondary --workload c3 --timing-steps 1 --steps 2 --warmup 1"; M=k_step3d_t_seg; fi
     timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pt_f_$W -o run -- $B > $O/pt_f_$W.log 2>&1 || exit 1
     timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pt_w_$W -o run -- $B > $O/pt_w_$W.log 2>&1 || exit 1
     python3 $R/tools/pmc_traffic.py $(find $O/pt_f_$W -name '*counter_collection.csv') $(find $O/pt_w_$W -name '*counter_collection.csv') \

@@ -42,9 +42,11 @@ def main():
         if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
             tr = (2 * m["FETCH_SIZE"] + m["WRITE_SIZE"]) * 1024.0 / 1e6
         rows.append((k, calls, us, tr, m))
-    rows.sort(key=lambda r: -(r[2] * r[1] if r[2] == r[2] else 0))
-    print("%-40s %6s %9s %9s %7s %6s %6s %6s %7s %7s %6s" % ("kernel", "calls", "us/call", "trafMB", "GB/s", "wait%",
-                                                               "stall%", "actv%", "valu/w", "waves", "L2hit"))
+    # by time per step (trace) or, without one, by wave cycles over all dispatches
+    rows.sort(key=lambda r: -(r[2] * r[1] if r[2] == r[2] else r[4].get("SQ_WAVE_CYCLES", 0.0) * r[1]))
+    print("%-40s %6s %9s %9s %7s %6s %6s %6s %7s %7s %7s %6s %7s %6s" % (
+        "kernel", "calls", "us/call", "trafMB", "GB/s", "wait%", "stall%", "actv%", "valu/w", "salu/w", "vmem/w",
+        "lds%", "waves", "L2hit"))
     for k, calls, us, tr, m in rows[:a.top]:
         wc = m.get("SQ_WAVE_CYCLES")
         pct = lambda c: (100.0 * m[c] / wc) if (wc and c in m) else float("nan")
@@ -53,9 +55,11 @@ def main():
         gbs = tr / us * 1e3 if (tr is not None and us == us) else float("nan")
         hit = m.get("TCC_HIT_sum"); miss = m.get("TCC_MISS_sum")
         l2 = 100.0 * hit / (hit + miss) if (hit is not None and miss is not None and hit + miss) else float("nan")
-        print("%-40s %6d %9.1f %9s %7.0f %6.1f %6.1f %6.1f %7.0f %7.0f %6.1f" % (
+        per = lambda c: m[c] / waves if (c in m and waves == waves and waves) else float("nan")
+        vmem = per("SQ_INSTS_VMEM_RD") + (per("SQ_INSTS_VMEM_WR") if "SQ_INSTS_VMEM_WR" in m else 0.0)
+        print("%-40s %6d %9.1f %9s %7.0f %6.1f %6.1f %6.1f %7.0f %7.0f %7.0f %6.1f %7.0f %6.1f" % (
             k, calls, us, "%.1f" % tr if tr is not None else "-", gbs, pct("SQ_WAIT_ANY"), pct("SQ_WAIT_INST_ANY"),
-            pct("SQ_ACTIVE_INST_ANY"), vpw, waves, l2))
+            pct("SQ_ACTIVE_INST_ANY"), vpw, per("SQ_INSTS_SALU"), vmem, pct("SQ_WAIT_INST_LDS"), waves, l2))
 
 
 if __name__ == "__main__":

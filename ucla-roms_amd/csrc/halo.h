@@ -62,15 +62,38 @@ struct Halo {
   double* dred = nullptr;  // gather staging
   long cap = 0;
   long gcnt = 0;           // host channel: largest per-level message over all ranks
-  // fast-loop overlap (launch_step2d): exchange on a second stream while the
-  // next fast step's interior tiles run; `pending` = an exchange not yet
-  // joined back into the library stream
+  // Exchanges forked onto the halo stream `cs` (halo_fork_exchange): each
+  // gets a ticket (its fork count) and an event in a ring; the library stream
+  // joins them back in ticket order (halo_join_to / halo_join).  cs runs them
+  // in fork order, so joining ticket t joins every earlier one too.
+  static constexpr int kRing = 16;
   hipStream_t cs = nullptr;
-  hipEvent_t efork = nullptr, ejoin = nullptr;
-  int pending = 0;
+  hipEvent_t efork = nullptr;
+  hipEvent_t xev[kRing] = {};
+  long nfork = 0;   // exchanges forked onto cs since setup
+  long njoin = 0;   // tickets < njoin are joined into the library stream
   HaloIpc ipc;
   int overlap = 0;  // 1: enabled (ROMS_GPU_S2D_OVERLAP=1; off by default, see halo_setup)
   int overlap3d = 0;  // rim-first overlap of the 3-D exchanges (launch_rim_first; ROMS_GPU_OVERLAP3D=1: on)
+  // Deferred 3-D exchanges (enqueue_step): on multi-rank runs
+  // a producer's trailing exchange runs on cs beside the next routine that
+  // reads none of its halo; the step joins it before the first reader.
+  // xoverlap: enabled (default with a communicator of > 1 rank;
+  // ROMS_GPU_XOVERLAP=0/1 forces it); defer > 0: launch_exchange_list forks
+  // instead of exchanging on the caller's stream (set around one producer).
+  int xoverlap = 0;
+  int defer = 0;
+  // test hook (ROMS_GPU_XDELAY_US): a bounded spin of that many microseconds
+  // on cs before each forked exchange's unpack, so a reader the step forgot to
+  // join reads the stale halo (tests/test_gpu_multirank.py)
+  int xdelay_us = 0;
+  long long xdelay_ticks = 0;
+  // test hook (ROMS_GPU_XTEST_SKIPJOIN=bits): enqueue_step leaves out the
+  // joins whose bit is set (1 before omega, 2 before pre_step3d, 4 before the
+  // corrector's rho_eos, 8 before its omega, 16 before step3d_uv1), so the
+  // tests can show that the delay hook catches each missing join (never set
+  // outside tests/test_gpu_multirank.py)
+  int xskip = 0;
 };
 
 int comm_unique_id(void* out128);
@@ -89,10 +112,13 @@ void halo_free(Halo& H);
 bool halo_graph_safe(const Halo* H);
 long halo_map(const HaloPlan& P, int dir, int unpack, int* iv, int* jv);
 void halo_exchange(const Halo& H, hipStream_t s, const ExchList& L);
-// exchange L on H.cs after the work already queued on s (fork); halo_join
-// makes s wait for it.  Both are no-ops without a pending exchange.
-void halo_fork_exchange(Halo& H, hipStream_t s, const ExchList& L);
+// exchange L on H.cs after the work already queued on s (fork), returns its
+// ticket; halo_join makes s wait for every forked exchange, halo_join_to for
+// ticket t and those before it (no-ops for exchanges already joined)
+long halo_fork_exchange(Halo& H, hipStream_t s, const ExchList& L);
 void halo_join(Halo& H, hipStream_t s);
+void halo_join_to(Halo& H, hipStream_t s, long ticket);
+inline bool halo_pending(const Halo& H) { return H.nfork > H.njoin; }
 int halo_allgather(const Halo& H, hipStream_t s, const double* in, int n, double* out);
 // 1 if the IPC transport is in use, 0 if RCCL; -1 if a wait timed out since setup
 int halo_transport(const Halo& H);

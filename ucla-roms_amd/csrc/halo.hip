@@ -146,9 +146,15 @@ __global__ void __launch_bounds__(64) k_halo_wait_ipc(HaloGeom g, IpcPtrs P, int
   if (h < 8 && g.active[h] && !dead && !nosignal)
     __hip_atomic_fetch_add(P.pflags[h] + kOpp[h], 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   if (h < 8 && g.active[h] && !dead) {
+    // relaxed polls (system scope: uncached, always fresh), then ONE acquire
+    // below: an acquire per poll invalidates this CU's caches every
+    // iteration, and with the exchange running beside compute on the other
+    // stream (deferred exchanges, enqueue_step) those polls cost the chip a
+    // large share of its bandwidth (MI355X_MICROARCH.md: polling with acquire
+    // loads; measured here 66.2 vs 61.4 ms per C3 step, 2 ranks on one GPU)
     const long long t0 = wall_clock64();
-    while (__hip_atomic_load(P.flags + h, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < want) {
-      __builtin_amdgcn_s_sleep(2);
+    while (__hip_atomic_load(P.flags + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < want) {
+      __builtin_amdgcn_s_sleep(8);
       if (wall_clock64() - t0 > P.timeout) {
         atomicExch(P.err_dev, 1);
         __hip_atomic_store(P.err_host, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -156,6 +162,7 @@ __global__ void __launch_bounds__(64) k_halo_wait_ipc(HaloGeom g, IpcPtrs P, int
       }
     }
   }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // system scope: the payload the counters released
   __syncthreads();
   if (h == 0) *P.seq = want;
 }
@@ -470,12 +477,35 @@ int halo_setup(Halo& H, RomsComm* comm, const HaloPlan& plan, int maxlev, const 
     return -2;
   }
   if (hipStreamCreateWithFlags(&H.cs, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&H.efork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&H.ejoin, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&H.efork, hipEventDisableTiming) != hipSuccess) {
     err = "halo_setup: stream/event creation failed";
     return -2;
   }
-  H.pending = 0;
+  for (hipEvent_t& e : H.xev)
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+      err = "halo_setup: event creation failed";
+      return -2;
+    }
+  H.nfork = H.njoin = 0;
+  H.defer = 0;
+  {
+    // deferred 3-D exchanges beside the next routine (enqueue_step): on by
+    // default whenever there is a neighbour to talk to (a single rank has no
+    // exchanges to hide: N = 1 runs are untouched by construction)
+    const char* ex = getenv("ROMS_GPU_XOVERLAP");
+    H.xoverlap = ex ? (ex[0] == '1') : (comm && comm->nranks > 1);
+    const char* es = getenv("ROMS_GPU_XTEST_SKIPJOIN");
+    H.xskip = es ? atoi(es) : 0;
+    const char* ed = getenv("ROMS_GPU_XDELAY_US");
+    H.xdelay_us = ed ? atoi(ed) : 0;
+    if (H.xdelay_us < 0 || H.xdelay_us > 100000) H.xdelay_us = 0;
+    int khz = 0, dev = 0;
+    (void)hipGetDevice(&dev);
+    if (H.xdelay_us && hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) == hipSuccess && khz > 0)
+      H.xdelay_ticks = (long long)khz * H.xdelay_us / 1000;
+    else
+      H.xdelay_us = 0;
+  }
   {
     // measured on one MI355X with every exchange routed through RCCL: the
     // overlap costs more than it hides (13.8 vs 12.9 ms/step at C2: the RCCL
@@ -537,11 +567,15 @@ void halo_free(Halo& H) {
   if (H.dred) (void)hipFree(H.dred);
   H.sbuf = H.rbuf = H.dred = nullptr;
   if (H.efork) (void)hipEventDestroy(H.efork);
-  if (H.ejoin) (void)hipEventDestroy(H.ejoin);
+  for (hipEvent_t& e : H.xev) {
+    if (e) (void)hipEventDestroy(e);
+    e = nullptr;
+  }
   if (H.cs) (void)hipStreamDestroy(H.cs);
-  H.efork = H.ejoin = nullptr;
+  H.efork = nullptr;
   H.cs = nullptr;
-  H.pending = 0;
+  H.nfork = H.njoin = 0;
+  H.defer = 0;
 }
 
 // host copy of the pack (unpack=0) or unpack (unpack=1) index map of one direction
@@ -565,11 +599,21 @@ IpcPtrs ipc_ptrs(const Halo& H) {
   P.timeout = H.ipc.timeout_ticks;
   return P;
 }
+// test hook (Halo::xdelay_us): one lane spins for `ticks` wall-clock ticks
+// (bounded: it ends by itself), so the unpack that follows lands late
+__global__ void k_halo_delay(long long ticks) {
+  const long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+void xdelay(const Halo& H, hipStream_t s) {
+  if (H.xdelay_us > 0 && s == H.cs) hipLaunchKernelGGL(k_halo_delay, dim3(1), dim3(64), 0, s, H.xdelay_ticks);
+}
 void exchange_ipc(const Halo& H, hipStream_t s, const HaloGeom& g, const ExchList& L, const dim3& grid) {
   const IpcPtrs P = ipc_ptrs(H);
   hipLaunchKernelGGL(k_halo_pack_ipc, grid, dim3(256), 0, s, g, L, P, H.cap);
   const int drop = H.ipc.drop_at >= 0 && H.ipc.nexch++ == H.ipc.drop_at;
   hipLaunchKernelGGL(k_halo_wait_ipc, dim3(1), dim3(64), 0, s, g, P, drop);
+  xdelay(H, s);
   hipLaunchKernelGGL(k_halo_unpack_ipc, grid, dim3(256), 0, s, g, L, P, H.cap);
 }
 }  // namespace
@@ -625,22 +669,26 @@ void halo_exchange(const Halo& H, hipStream_t s, const ExchList& L) {
     (void)hipStreamSynchronize(s);
     G->barrier();
   }
+  xdelay(H, s);
   hipLaunchKernelGGL(k_halo_unpack, grid, dim3(256), 0, s, g, L, H.rbuf, H.cap);
 }
 
-void halo_fork_exchange(Halo& H, hipStream_t s, const ExchList& L) {
-  halo_join(H, s);  // at most one exchange in flight
+long halo_fork_exchange(Halo& H, hipStream_t s, const ExchList& L) {
+  // a ring event is recorded again only after the library stream has joined
+  // the exchange it marked
+  if (H.nfork - H.njoin >= Halo::kRing) halo_join_to(H, s, H.nfork - Halo::kRing);
   (void)hipEventRecord(H.efork, s);
   (void)hipStreamWaitEvent(H.cs, H.efork, 0);
   halo_exchange(H, H.cs, L);
-  (void)hipEventRecord(H.ejoin, H.cs);
-  H.pending = 1;
+  (void)hipEventRecord(H.xev[H.nfork % Halo::kRing], H.cs);
+  return H.nfork++;
 }
-void halo_join(Halo& H, hipStream_t s) {
-  if (!H.pending) return;
-  (void)hipStreamWaitEvent(s, H.ejoin, 0);
-  H.pending = 0;
+void halo_join_to(Halo& H, hipStream_t s, long ticket) {
+  if (ticket < H.njoin || ticket >= H.nfork) return;
+  (void)hipStreamWaitEvent(s, H.xev[ticket % Halo::kRing], 0);
+  H.njoin = ticket + 1;
 }
+void halo_join(Halo& H, hipStream_t s) { halo_join_to(H, s, H.nfork - 1); }
 
 // out[r*n + q] = in_r[q] for every rank r (blocking)
 int halo_allgather(const Halo& H, hipStream_t s, const double* in, int n, double* out) {

@@ -61,7 +61,14 @@ __global__ void __launch_bounds__(256) k_periodic_wrap(Bounds b, ExchList L) {
 void launch_exchange_list(const Dev& d, hipStream_t s, const ExchList& L) {
   const Bounds& b = d.b;
   if (d.halo && d.halo->comm) {
-    halo_exchange(*d.halo, s, L);
+    Halo& H = *const_cast<Halo*>(d.halo);
+    if (H.defer > 0) {   // a deferred producer's exchange (enqueue_step): onto the halo stream
+      (void)halo_fork_exchange(H, s, L);
+      return;
+    }
+    // one order on the transport: every exchange follows the forked ones
+    halo_join(H, s);
+    halo_exchange(H, s, L);
     return;
   }
   if (!b.ew_periodic && !b.ns_periodic) return;

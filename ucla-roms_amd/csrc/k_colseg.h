@@ -103,6 +103,13 @@ struct SegXchg {
 // for every row's loads before the next row's (one s_waitcnt vmcnt(0) per
 // load); straight-line rows let it issue the loads of many rows back to back.
 // The live rows keep their expressions and order: results are unchanged.
+// Every segment of a launch has at least kSegNMin rows (seg_rows_ok, checked
+// on the host before a segment solver is chosen: N >= 50 at <= 13 rows per
+// segment gives 11), so rows q < kSegNMin are live in every wave and their
+// selects fold away at compile time; only the last rows pay for them.
+__device__ __forceinline__ bool seg_live(int q, int n) { return q < kSegNMin || q < n; }
+__device__ __forceinline__ bool seg_last(int q, int n) { return q >= kSegNMin - 1 && q == n - 1; }
+
 #ifndef ROMS_SEG_LOAD_GROUP
 #define ROMS_SEG_LOAD_GROUP 5
 #endif
@@ -122,7 +129,7 @@ struct SegTri {
       row(q, a, b, c, d);
       const double rm = 1.0 / (b - a * Cp);
       const double Cq = c * rm, Dq = (d - a * Dp) * rm, Eq = -a * Ep * rm;
-      const bool live = q < n;
+      const bool live = seg_live(q, n);
       C[q] = live ? Cq : 0.0;
       D[q] = live ? Dq : 0.0;
       E[q] = live ? Eq : 0.0;
@@ -137,7 +144,7 @@ struct SegTri {
     double y = 0.0, al = 0.0, be = 0.0, yl = 0.0, all = 0.0, bel = 0.0;
 #pragma unroll
     for (int q = KR - 1; q >= 0; q--) {
-      const bool last = q == n - 1, live = q < n;
+      const bool last = seg_last(q, n), live = seg_live(q, n);
       const double yn = D[q] - C[q] * y, aln = E[q] - C[q] * al, ben = -C[q] * be;
       y = last ? D[q] : (live ? yn : y);
       al = last ? E[q] : (live ? aln : al);
@@ -196,7 +203,7 @@ struct SegTri {
 #pragma unroll
     for (int q = KR - 1; q >= 0; q--) {
       const double v = D[q] + E[q] * xL - C[q] * xn;
-      const bool live = q < n;
+      const bool live = seg_live(q, n);
       xn = live ? v : xn;
       D[q] = live ? v : D[q];
     }
@@ -230,7 +237,7 @@ __device__ __forceinline__ void spline_fc_seg(const SegSpan& sg, int N, SegXchg&
   T.couple(sg, ns, X, xL, xR);
   T.solve(ns, xL, xR);
 #pragma unroll
-  for (int q = 0; q < KR; q++) fc[q] = q < ns ? T.D[q] : xR;
+  for (int q = 0; q < KR; q++) fc[q] = seg_live(q, ns) ? T.D[q] : xR;
 }
 
 // SPLINE_UV advective flux of a u (dir 0) / v (dir 1) column at interfaces

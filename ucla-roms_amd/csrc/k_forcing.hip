@@ -376,6 +376,14 @@ int roms_gpu_frc_record(int field_id, int slot, double rec_time, const double* d
       *S.err = "roms_gpu_frc_record: allocation failed";
       return -2;
     }
+    // the upload fills only the host layout's rows and columns: the row-pitch
+    // padding and the wide-ghost frame, which the interpolation copies into
+    // the field and aligned tiles read, stay zero as dev_alloc leaves them
+    // (ADVICE r4), ordered on the library stream before the upload
+    if (hipMemsetAsync(F.slot[slot], 0, (size_t)n * sizeof(double), S.s) != hipSuccess) {
+      *S.err = "roms_gpu_frc_record: zero fill failed";
+      return -2;
+    }
     fc.st.gen++;   // a captured step graph does not know this buffer
   }
   F.n = n;

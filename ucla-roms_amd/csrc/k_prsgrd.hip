@@ -108,11 +108,21 @@ constexpr int kPYH = kBY + 2, kPYN = kBX * kPYH;          // v-points m = j0-1 .
 // a third of the vector-memory instructions of forming every difference
 // from two global loads (measured: the per-cell kernel was bound by the
 // vector-memory instruction rate, not by HBM bytes).
-constexpr int kPWW = kBX + 3, kPWH = kBY + 3, kPWN = kPWW * kPWH;   // raw window (i0-2.., j0-2..)
+// The row is 68 wide (one unused column at i0+65): an even width keeps every
+// row of the window on a 16-B boundary in LDS, so the L16 form stores two
+// doubles per lane.
+constexpr int kPWW = kBX + 4, kPWH = kBY + 3, kPWN = kPWW * kPWH;   // raw window (i0-2.., j0-2..)
 constexpr int kPWQ = (kPWN + kBX * kBY - 1) / (kBX * kBY);
 constexpr int kPQ = (kPXN + kPYN + kBX * kBY - 1) / (kBX * kBY);
-template <bool FUSE, int TY = kBY>
-__global__ void __launch_bounds__(kBX * TY) k_prsgrd_uv(Dev d, Range R, int split, int imin, int imax, int jmin, int jmax,
+// L16 (Params::ld16, the padded device pitch): the raw window and the u/v
+// window are read two doubles per lane (global_load_dwordx4 / ds_write_b128):
+// a window row starts at i0-2, and i0 = 1 (mod 16) puts i0-2 and every second
+// column after it on a 16-B boundary, so half the vector-memory instructions
+// fetch the same bytes (the per-cell kernel is bound by that instruction rate,
+// DESIGN.md section 4).  Cells outside -1..Lm+2 / -1..Mm+2 read as 0, as in
+// the 8-B form: bit-identical.
+template <bool FUSE, int TY = kBY, bool L16 = false>
+__global__ void __launch_bounds__(kBX * TY, L16 && TY == kBY ? 5 : 1) k_prsgrd_uv(Dev d, Range R, int split, int imin, int imax, int jmin, int jmax,
                                                    UVBounds ub, int up, int nrhs) {
   const uint3 bI = h_tile(d.p.tile_grp);
   // the file-scope window sizes for a 64 x TY tile (TY = kBY: the constants above)
@@ -122,7 +132,7 @@ __global__ void __launch_bounds__(kBX * TY) k_prsgrd_uv(Dev d, Range R, int spli
   // one LDS block: the raw window, the elementary differences and the
   // harmonic means (and, FUSE, the u/v window after them)
   constexpr int kPL = 3 * WN + 4 * XN + 4 * YN;
-  __shared__ double sL[kPL];
+  __shared__ __attribute__((aligned(16))) double sL[kPL];
   double* const sZ = sL;
   double* const sR = sZ + WN;
   double* const sQ = sR + WN;
@@ -146,18 +156,34 @@ __global__ void __launch_bounds__(kBX * TY) k_prsgrd_uv(Dev d, Range R, int spli
   const int tid = threadIdx.x + kBX * threadIdx.y;
   auto W = [&](int i, int j) { return (i - (i0 - 2)) + (j - (j0 - 2)) * kPWW; };
   // ---- loads, all issued before the first barrier ----
-  double wz[WQ], wr[WQ], wq[WQ];
+  // 8-B form: entry q of the window per lane and round; L16: the pair of
+  // entries 2p, 2p+1 (one row holds kPWW / 2 pairs)
+  constexpr int WP = WN / 2, WPQ = (WP + NT - 1) / NT;
+  constexpr int WL = L16 ? WPQ : WQ;
+  double2 wz[WL], wr[WL], wq[WL];
 #pragma unroll
-  for (int m = 0; m < WQ; m++) {
+  for (int m = 0; m < WL; m++) {
     const int q = tid + m * NT;
-    wz[m] = wr[m] = wq[m] = 0.0;
-    if (q < WN) {
+    wz[m] = wr[m] = wq[m] = double2{0.0, 0.0};
+    if (L16) {
+      if (q < WP) {
+        const int i = i0 - 2 + 2 * (q % (kPWW / 2)), j = j0 - 2 + q / (kPWW / 2);
+        if (i >= -1 && i <= b.Lm + 2 && j <= b.Mm + 2) {
+          const long o = IJ(b, i, j) + kk;
+          const bool hi = i + 1 <= b.Lm + 2;
+          wz[m] = *reinterpret_cast<const double2*>(F.z_r + o);
+          wr[m] = *reinterpret_cast<const double2*>(R1 + o);
+          if (split) wq[m] = *reinterpret_cast<const double2*>(F.qp1 + o);
+          if (!hi) { wz[m].y = 0.0; wr[m].y = 0.0; wq[m].y = 0.0; }
+        }
+      }
+    } else if (q < WN) {
       const int i = i0 - 2 + q % kPWW, j = j0 - 2 + q / kPWW;
       if (i >= -1 && i <= b.Lm + 2 && j <= b.Mm + 2) {
         const long o = IJ(b, i, j) + kk;
-        wz[m] = F.z_r[o];
-        wr[m] = R1[o];
-        if (split) wq[m] = F.qp1[o];
+        wz[m].x = F.z_r[o];
+        wr[m].x = R1[o];
+        if (split) wq[m].x = F.qp1[o];
       }
     }
   }
@@ -199,21 +225,35 @@ __global__ void __launch_bounds__(kBX * TY) k_prsgrd_uv(Dev d, Range R, int spli
   // FUSE: the horizontal momentum r.h.s. of the same cell (k_uv_horiz1's
   // window of u, v, FlxU, FlxV at nrhs and its lane inputs), loaded here
   // with everything else; ru/rv then go to HBM once, after both terms
-  constexpr int UW = UWN, UR = (UW + NT - 1) / (NT);
-  double wU[FUSE ? UR : 1], wV[FUSE ? UR : 1], wFU[FUSE ? UR : 1], wFV[FUSE ? UR : 1];
+  constexpr int UW = UWN, UR0 = (UW + NT - 1) / (NT), UP = UW / 2, URP = (UP + NT - 1) / NT;
+  constexpr int UR = L16 ? URP : UR0;
+  double2 wU[FUSE ? UR : 1], wV[FUSE ? UR : 1], wFU[FUSE ? UR : 1], wFV[FUSE ? UR : 1];
   double fo0 = 0.0, fox = 0.0, foy = 0.0;
   if constexpr (FUSE) {
     const long kn = kk + (long)(nrhs - 1) * b.n3;
 #pragma unroll
     for (int r = 0; r < UR; r++) {
       const int q = tid + r * NT;
-      const int ii = i0 - 2 + q % kUVW, jj = j0 - 2 + q / kUVW;
-      const bool ok = q < UW && ii >= -1 && ii <= b.Lm + 2 && jj >= -1 && jj <= b.Mm + 2;
-      const long oo = ok ? IJ(b, ii, jj) : 0;
-      wU[r] = ok ? F.u[oo + kn] : 0.0;
-      wV[r] = ok ? F.v[oo + kn] : 0.0;
-      wFU[r] = ok ? F.FlxU[oo + kk] : 0.0;
-      wFV[r] = ok ? F.FlxV[oo + kk] : 0.0;
+      if (L16) {   // pairs (ii, ii+1), ii = i0-2+2c, of the kUVW-wide rows
+        const int ii = i0 - 2 + 2 * (q % (kUVW / 2)), jj = j0 - 2 + q / (kUVW / 2);
+        const bool ok = q < UP && ii >= -1 && ii <= b.Lm + 2 && jj >= -1 && jj <= b.Mm + 2;
+        const bool hi = ii + 1 <= b.Lm + 2;
+        const long oo = ok ? IJ(b, ii, jj) : 0;
+        const double2 z2{0.0, 0.0};
+        wU[r] = ok ? *reinterpret_cast<const double2*>(F.u + oo + kn) : z2;
+        wV[r] = ok ? *reinterpret_cast<const double2*>(F.v + oo + kn) : z2;
+        wFU[r] = ok ? *reinterpret_cast<const double2*>(F.FlxU + oo + kk) : z2;
+        wFV[r] = ok ? *reinterpret_cast<const double2*>(F.FlxV + oo + kk) : z2;
+        if (!hi) { wU[r].y = 0.0; wV[r].y = 0.0; wFU[r].y = 0.0; wFV[r].y = 0.0; }
+      } else {
+        const int ii = i0 - 2 + q % kUVW, jj = j0 - 2 + q / kUVW;
+        const bool ok = q < UW && ii >= -1 && ii <= b.Lm + 2 && jj >= -1 && jj <= b.Mm + 2;
+        const long oo = ok ? IJ(b, ii, jj) : 0;
+        wU[r].x = ok ? F.u[oo + kn] : 0.0;
+        wV[r].x = ok ? F.v[oo + kn] : 0.0;
+        wFU[r].x = ok ? F.FlxU[oo + kk] : 0.0;
+        wFV[r].x = ok ? F.FlxV[oo + kk] : 0.0;
+      }
     }
     if (d.p.uv_cor && (du || dv)) {
       fo0 = F.fomn[ij]; fox = F.fomn[ij - 1]; foy = F.fomn[ij - sj];
@@ -222,9 +262,17 @@ __global__ void __launch_bounds__(kBX * TY) k_prsgrd_uv(Dev d, Range R, int spli
     }
   }
 #pragma unroll
-  for (int m = 0; m < WQ; m++) {
+  for (int m = 0; m < WL; m++) {
     const int q = tid + m * NT;
-    if (q < WN) { sZ[q] = wz[m]; sR[q] = wr[m]; sQ[q] = wq[m]; }
+    if (L16) {
+      if (q < WP) {
+        *reinterpret_cast<double2*>(sZ + 2 * q) = wz[m];
+        *reinterpret_cast<double2*>(sR + 2 * q) = wr[m];
+        *reinterpret_cast<double2*>(sQ + 2 * q) = wq[m];
+      }
+    } else if (q < WN) {
+      sZ[q] = wz[m].x; sR[q] = wr[m].x; sQ[q] = wq[m].x;
+    }
   }
   __syncthreads();
   // ---- elementary differences at clamped u-points (xi) and v-points (eta) ----
@@ -322,7 +370,16 @@ __global__ void __launch_bounds__(kBX * TY) k_prsgrd_uv(Dev d, Range R, int spli
 #pragma unroll
     for (int r = 0; r < UR; r++) {
       const int q = tid + r * NT;
-      if (q < UW) { sU[q] = wU[r]; sV[q] = wV[r]; sFU[q] = wFU[r]; sFV[q] = wFV[r]; }
+      if (L16) {
+        if (q < UP) {
+          *reinterpret_cast<double2*>(sU + 2 * q) = wU[r];
+          *reinterpret_cast<double2*>(sV + 2 * q) = wV[r];
+          *reinterpret_cast<double2*>(sFU + 2 * q) = wFU[r];
+          *reinterpret_cast<double2*>(sFV + 2 * q) = wFV[r];
+        }
+      } else if (q < UW) {
+        sU[q] = wU[r].x; sV[q] = wV[r].x; sFU[q] = wFU[r].x; sFV[q] = wFV[r].x;
+      }
     }
     __syncthreads();
     if (!(du || dv)) return;
@@ -603,7 +660,13 @@ void launch_prsgrd(const Dev& d, hipStream_t s, const Tlev& t, int uv_up, bool p
   Range R1{0, b.Lm, 0, b.Mm};
   if (!p_ready) hipLaunchKernelGGL(k_prsgrd_P, grid_of(R1), dim3(kBX, kBY), 0, s, d, R1, split, d.p.tides);
   ktimer_mark(s, kTimedPrsgrdUv, 0);
-  if (uv_up >= 0 && d.p.prs_ty == 8)
+  if (uv_up >= 0 && d.p.ld16 && d.p.prs_ty != 8)
+    hipLaunchKernelGGL((k_prsgrd_uv<true, kBY, true>), grid3_of(R2, b.N), dim3(kBX, kBY), 0, s, d, R2, split, imin, imax,
+                       jmin, jmax, uv_bounds(b), uv_up, t.nrhs);
+  else if (!(uv_up >= 0) && d.p.ld16 && d.p.prs_ty != 8)
+    hipLaunchKernelGGL((k_prsgrd_uv<false, kBY, true>), grid3_of(R2, b.N), dim3(kBX, kBY), 0, s, d, R2, split, imin, imax,
+                       jmin, jmax, uv_bounds(b), 0, t.nrhs);
+  else if (uv_up >= 0 && d.p.prs_ty == 8)
     hipLaunchKernelGGL((k_prsgrd_uv<true, 8>), grid3_ty(R2, b.N, 8), dim3(kBX, 8), 0, s, d, R2, split, imin, imax, jmin,
                        jmax, uv_bounds(b), uv_up, t.nrhs);
   else if (uv_up >= 0)

@@ -1000,7 +1000,7 @@ void launch_fast_step(const Dev& d, hipStream_t s, const FBCoef& c, const Tlev& 
     // between the fused kernels (single rank, no closed edges), else one per launch
     const bool span = d.halo == nullptr && !closed;
     if (!span || t.iif == 1) ktimer_mark(s, kTimedS2dFb, 0);
-    if (H && H->pending) {
+    if (H && halo_pending(*H)) {
       // the previous fast step's zeta/ubar/vbar(knew) exchange is still in
       // flight on the halo stream: interior tiles first, the rim after it
       fb(1);

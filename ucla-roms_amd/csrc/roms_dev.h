@@ -68,6 +68,7 @@ struct Params {
   int h_ty;       // tile rows of the hoisted horizontal kernels: 4 or 8 (ROMS_GPU_HTY)
   int h_jc;       // rows per block of the j-marching horizontal kernels (multiple of 4; ROMS_GPU_HJC, 0: 64 x h_ty tiles)
   int prs_ty;     // tile rows of k_prsgrd_uv: 4 or 8 (ROMS_GPU_PRS_TY)
+  int ld16;       // padded pitch: LDS windows read two doubles per lane (16-B loads; ROMS_GPU_LD16=0: 8-B)
   int visc_stg;   // visc3d: raw u/v/Hz windows staged in LDS per level (default; ROMS_GPU_VISC_STG=0: per-point loads)
   int t3dmix_stg; // t3dmix (two tracers): Hz/T/S windows staged in LDS per level (default; ROMS_GPU_T3DMIX_STG=0: per-point loads)
   int kpp_ty;     // k_kpp_int: 4 (default) staged Rig windows on 64x4 blocks, 8 on 64x8, 43 64x4 at 3 waves/SIMD, 0 one row per block (ROMS_GPU_KPP_TY)
@@ -284,6 +285,18 @@ constexpr int kSegBlock = ((kSegMaxS * kSegCW + 63) / 64) * 64;   // threads of 
 #define ROMS_SEG_JMAX (ROMS_SEG_CW >= 64 ? 1 : 4)
 #endif
 constexpr int kSegJMax = ROMS_SEG_JMAX;
+// the fewest rows any segment of a launch may have (k_colseg.h seg_live)
+#ifndef ROMS_SEG_NMIN
+#define ROMS_SEG_NMIN 11   // 0: every row select kept (the round-4 code; A/B builds)
+#endif
+constexpr int kSegNMin = ROMS_SEG_NMIN;
+// segments of an N-level column (one per wavefront at kSegCW = 64, seg_waves)
+// and whether each of them gets at least kSegNMin rows
+inline int seg_count(int N) {
+  const int per = kCX / kSegCW, S = (N + kSegRows - 1) / kSegRows;
+  return (S + per - 1) / per * per;
+}
+inline bool seg_rows_ok(int N) { return N / seg_count(N) >= kSegNMin; }
 inline dim3 gridc_of(const Range& r) {
   int ni = r.i1 - tile_i0(r.i0) + 1, nj = r.j1 - r.j0 + 1;
   if (ni < 1) ni = 1;

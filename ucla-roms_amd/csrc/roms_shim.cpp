@@ -4,6 +4,7 @@
 // with per-phase HIP-graph replay, analytic-case setup and diag norms.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
@@ -115,6 +116,21 @@ void rank_extent(int LL, int np, int node, int& len, int& sw) {
   len = base;
   if (node == 0) len -= off / 2;
   if (node == np - 1) len -= (off + 1) / 2;
+}
+// the smallest subdomain extent of any rank along one direction: the edge
+// ranks lose the uneven-split remainder (mpi_setup.F:115-125), the interior
+// ones keep the base width (LL/np is not a lower bound)
+int min_rank_extent(int LL, int np) {
+  int mn = LL, len, sw;
+  for (int node : {0, np - 1}) {
+    rank_extent(LL, np, node, len, sw);
+    mn = len < mn ? len : mn;
+  }
+  if (np > 2) {
+    rank_extent(LL, np, 1, len, sw);
+    mn = len < mn ? len : mn;
+  }
+  return mn;
 }
 
 #define CHECK_HIP(x)                                                                  \
@@ -415,6 +431,35 @@ void enqueue_step(roms_tlev* t, bool rho_current, bool store_huv) {
     (void)hipEventRecord(g.pev[k], s2);
     (void)hipStreamWaitEvent(s, g.pev[k], 0);
   };
+  // Multi-rank runs (Halo::xoverlap, default with > 1 rank; not while one
+  // routine is timed): the trailing exchange of a producer in DEFER(...) runs
+  // on the halo stream beside the routines that follow it, and XJOIN(t) makes
+  // the library stream wait for it just before the first routine that reads
+  // its halo (mpi_exchanges.F:672-800 posts and waits on every
+  // exchange in place).  Where the reference's order allows (no data
+  // dependence either way) a routine that reads none of the halo moves in
+  // between: lmd_vmix(nstp) ahead of omega, rho_eos(nrhs) ahead of the
+  // corrector's omega.  Same kernels on the same inputs, so the fields are
+  // bitwise those of the serial order (tests/test_gpu_multirank.py, with a
+  // delay hook that makes a missing join read stale halos).
+  const bool xo = d.halo != nullptr && g.halo.xoverlap && g.timed < 0;
+  long xt = -1;   // ticket of the last deferred exchange
+#define DEFER(call)                          \
+  do {                                       \
+    if (xo) g.halo.defer = 1;                \
+    call;                                    \
+    g.halo.defer = 0;                        \
+    if (xo) xt = g.halo.nfork - 1;           \
+  } while (0)
+#define XJOIN(t)                                   \
+  do {                                             \
+    if (xo) halo_join_to(g.halo, s, (t));          \
+  } while (0)
+  // Halo::xskip (test hook): leave out the joins whose bit is set
+#define XJOIN_T(bit, t)                            \
+  do {                                             \
+    if (!(g.halo.xskip & (bit))) XJOIN(t);         \
+  } while (0)
   frc_step_phase(d, s, 0, pot);     // set_forces, frc_time 'current' (main.F:384-385)
   launch_bulk_flux(d, s, T.nrhs);   // set_forces (main.F:386): BULK_FRC only
   frc_step_phase(d, s, 1, pot);     // set_bry_all '1/2 fwd' + set_tides (main.F:389-394)
@@ -429,39 +474,61 @@ void enqueue_step(roms_tlev* t, bool rho_current, bool store_huv) {
     fork(7);
     launch_prsgrd_P(d, s2);
   }
-  TIMED(ROMS_R_SET_HUV, launch_set_huv(d, s, T, store_huv));
+  TIMED(ROMS_R_SET_HUV, DEFER(launch_set_huv(d, s, T, store_huv)));   // FlxU, FlxV
+  const long x_huv = xt;
+  const bool lmd2 = g.cfg.lmd_mixing && (pm & 1);
+  // lmd_vmix(nstp) reads u, v(nstp), bvf, Hz, z_r, z_w and the surface fluxes:
+  // none of set_HUV's or omega's outputs, so on a multi-rank run it goes first
+  // and covers set_HUV's exchange (Akv, Akt, hbls, hbbl follow on the halo stream)
+  const bool lmd_early = xo && g.cfg.lmd_mixing && !lmd2;
+  if (lmd_early) TIMED(ROMS_R_LMD_VMIX, DEFER(launch_lmd_vmix(d, s, T, T.nstp)));
+  XJOIN_T(1, x_huv);   // omega reads FlxU(iend+1), FlxV(jend+1)
   // the predictor's omega also forms pre_step3d's Hz_bak/Hz_fwd (nothing in
   // between -- lmd_vmix, prsgrd -- writes FlxU, FlxV, Hz, We or Wi)
   bool hb_done = false;
-  TIMED(ROMS_R_OMEGA, hb_done = launch_omega(d, s, T, d.p.omega_hb && d.p.hoist && T.nrhs != 3 ?
-                                                          0.5 * pre_step3d_dtau(d, T) : 0.0));
+  TIMED(ROMS_R_OMEGA, DEFER(hb_done = launch_omega(d, s, T, d.p.omega_hb && d.p.hoist && T.nrhs != 3 ?
+                                                                 0.5 * pre_step3d_dtau(d, T) : 0.0)));
   if (p_side) join(7);
-  const bool lmd2 = g.cfg.lmd_mixing && (pm & 1);
   if (lmd2) {
     fork(0);
     launch_lmd_vmix(d, s2, T, T.nstp);
-  } else if (g.cfg.lmd_mixing) {
+  } else if (g.cfg.lmd_mixing && !lmd_early) {
     TIMED(ROMS_R_LMD_VMIX, launch_lmd_vmix(d, s, T, T.nstp));
   }
   // the horizontal momentum r.h.s. of pre_step3d / step3d_uv1 rides in the
   // prsgrd kernel just before them (prsgrd_can_fuse_uv; nothing between the
-  // two touches u, v(nrhs), FlxU, FlxV, Hz or ru, rv)
+  // two touches u, v(nrhs), FlxU, FlxV, Hz or ru, rv); it reads neither We, Wi
+  // nor the mixing coefficients, whose exchanges it covers
   const bool fuse_uv = prsgrd_can_fuse_uv(d);
   TIMED(ROMS_R_PRSGRD, launch_prsgrd(d, s, T, fuse_uv ? 0 : -1, p_ready || p_side));
   if (lmd2) join(1);
+  XJOIN_T(2, xt);   // pre_step3d reads We, Akv, Akt across the halo
   const Side side{s2, g.pev[5], g.pev[6]};
-  TIMED(ROMS_R_PRE_STEP3D, launch_pre_step3d(d, s, T, fuse_uv, hb_done, (pm & 8) ? &side : nullptr));
-  TIMED(ROMS_R_SET_HUV1, launch_set_huv1(d, s, T));
+  TIMED(ROMS_R_PRE_STEP3D,
+        DEFER(launch_pre_step3d(d, s, T, fuse_uv, hb_done, (pm & 8) ? &side : nullptr)));   // t(nnew)
+  const long x_pre = xt;
+  // set_HUV1 reads u, v(nnew), Hz and the barotropic averages, no tracer
+  TIMED(ROMS_R_SET_HUV1, DEFER(launch_set_huv1(d, s, T)));   // FlxU, FlxV, u, v(nnew)
+  const long x_huv1 = xt;
   t->nrhs = 3;
   t->nnew = 3 - t->nstp;
   T = to_tlev(t);
-  if (pm & 2) {
-    fork(2);
-    launch_omega(d, s2, T);
+  if (xo) {
+    // rho_eos(nrhs) reads t(nrhs) across the halo (pre_step3d's exchange) and
+    // none of set_HUV1's outputs: it covers set_HUV1's exchange, then omega
+    XJOIN_T(4, x_pre);
+    TIMED(ROMS_R_RHO_EOS, launch_rho_eos(d, s, T, T.nrhs));
+    XJOIN_T(8, x_huv1);
+    TIMED(ROMS_R_OMEGA, DEFER(launch_omega(d, s, T)));   // We, Wi
   } else {
-    TIMED(ROMS_R_OMEGA, launch_omega(d, s, T));
+    if (pm & 2) {
+      fork(2);
+      launch_omega(d, s2, T);
+    } else {
+      TIMED(ROMS_R_OMEGA, launch_omega(d, s, T));
+    }
+    TIMED(ROMS_R_RHO_EOS, launch_rho_eos(d, s, T, T.nrhs));
   }
-  TIMED(ROMS_R_RHO_EOS, launch_rho_eos(d, s, T, T.nrhs));
   frc_step_phase(d, s, 2, pot);     // set_forces, '1/2 fwd' (main.F:433)
   launch_bulk_flux(d, s, T.nrhs);   // set_forces (main.F:433): BULK_FRC only
   const bool lmd2c = g.cfg.lmd_mixing && (pm & 4);
@@ -469,28 +536,46 @@ void enqueue_step(roms_tlev* t, bool rho_current, bool store_huv) {
     fork(3);   // after rho_eos (bvf) and the bulk fluxes (stflx, srflx, sustr_r)
     launch_lmd_vmix(d, s2, T, T.nrhs);
   } else if (g.cfg.lmd_mixing) {
-    TIMED(ROMS_R_LMD_VMIX, launch_lmd_vmix(d, s, T, T.nrhs));
+    TIMED(ROMS_R_LMD_VMIX, DEFER(launch_lmd_vmix(d, s, T, T.nrhs)));   // Akv, Akt, hbls, hbbl
   }
   frc_step_phase(d, s, 3, pot);     // set_bry_all 'forward' + set_tides (main.F:438-441)
   TIMED(ROMS_R_PRSGRD, launch_prsgrd(d, s, T, fuse_uv ? 1 : -1, p_ready));
   if ((pm & 2) || lmd2c) join(4);
+  XJOIN_T(16, xt);   // step3d_uv1 reads We and Akv across the halo
   TIMED(ROMS_R_STEP3D_UV1, launch_step3d_uv1(d, s, T, fuse_uv));
   if (g.cfg.uv_vis2) TIMED(ROMS_R_VISC3D, launch_visc3d(d, s, T));
+  // the fast loop is timed as one interval over its nfast steps (kernel-level
+  // count, as the graph replays it: no event between two fast steps)
+  const bool t2d = g.timed == ROMS_R_STEP2D && g.nev + 2 <= g.ev.size();
+  if (t2d) (void)hipEventRecord(g.ev[g.nev], s);
   for (int iif = 1; iif <= t->nfast; iif++) {
     t->iif = iif;
     t->kstp = t->knew;
     t->knew = t->kstp + 1;
     if (t->knew > 4) t->knew = 1;
     T = to_tlev(t);
-    TIMED(ROMS_R_STEP2D, launch_step2d(d, s, T, g.w1, g.w2));
+    launch_step2d(d, s, T, g.w1, g.w2);
+  }
+  if (t2d) {
+    (void)hipEventRecord(g.ev[g.nev + 1], s);
+    g.nev += 2;
+    g.kcount += t->nfast;
   }
   TIMED(ROMS_R_STEP3D_UV2, launch_step3d_uv2(d, s, T));
-  TIMED(ROMS_R_OMEGA, launch_omega(d, s, T));
+  // step3d_t reads We, Wi in its own columns only (the vertical fluxes and
+  // the implicit solve): omega's exchange runs beside it, and the tracer
+  // exchange that closes the step (t3dmix's or step3d_t's) joins it
+  TIMED(ROMS_R_OMEGA, DEFER(launch_omega(d, s, T)));
   // with TS_DIF2 the tracer exchange after step3d_t is overwritten by
   // t3dmix's before anything reads the halo (t3dmix_S.F reads t(nrhs)): one
   TIMED(ROMS_R_STEP3D_T, launch_step3d_t(d, s, T, !g.cfg.ts_dif2 || d.p.iso));
   if (g.cfg.ts_dif2) TIMED(ROMS_R_T3DMIX, launch_t3dmix(d, s, T));
+  XJOIN(xt);
   TIMED(ROMS_R_RHO_EOS, launch_rho_eos(d, s, T, T.nnew));
+  if (d.halo) halo_join(g.halo, s);   // nothing forked outlives the step (graph capture)
+#undef DEFER
+#undef XJOIN
+#undef XJOIN_T
   g.rho_slot = T.nnew;
   g.step_exch = g.halo.nexch - exch0;
 }
@@ -582,7 +667,7 @@ int roms_gpu_selftest_zero_fill(long n, int chunks, long* bad) {
     (void)hipStreamSynchronize(g.s);
     for (double*& p : a) {
       if (!p) continue;
-      if (guarded && (g.guard || g.off)) {
+      if (guarded) {   // dev_alloc offsets whenever it records a base (guard, pitch offset or wide ghosts)
         (void)hipFree(dev_base(p));
         g.guard_base.erase(p);
       } else {
@@ -671,9 +756,13 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     const char* es = getenv("ROMS_GPU_S2D_SPLIT");
     const bool split = es && es[0] == '1';
     const int obc = cfg->obc & ((dims->ew_periodic ? 0 : 3) | (dims->ns_periodic ? 0 : 12));
-    // every rank decides alike (global sizes; rank_extent's subdomains are
-    // at least LLm/np_xi - 2 wide, the 2k-wide strips must fit in all of them)
-    if (comm == nullptr || split || obc || dims->LLm / dims->np_xi < 2 * k + 2 || dims->MMm / dims->np_eta < 2 * k + 2) k = 1;
+    // every rank decides alike, from the global sizes: the 2k-wide strips
+    // (and the 2(k-1) cells a widened fast step reaches into its neighbour)
+    // must lie inside the neighbour's own cells on every rank, so k shrinks
+    // until 2k+2 fits the smallest subdomain of the mpi_setup split
+    if (comm == nullptr || split || obc) k = 1;
+    const int mext = std::min(min_rank_extent(dims->LLm, dims->np_xi), min_rank_extent(dims->MMm, dims->np_eta));
+    while (k > 1 && mext < 2 * k + 2) k--;
     const int gx = 2 * (k - 1);
     g.off = pad ? kAlignOff : 0;
     const int w = hx + 2 * gx;
@@ -731,11 +820,13 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
   // (measured: at N = 50 the LDS sweep is faster, the partitioned solve
   // costs ~3x the VALU instructions per level).
   // ROMS_GPU_COLSEG=0/1 forces either (A/B and parity runs).
-  P.colseg = (size_t)2 * (dims->N + 1) * kCX * sizeof(double) > 64 * 1024 && dims->N <= kSegRows * kSegMaxS;
+  // (every segment must hold at least kSegNMin rows: seg_rows_ok, k_colseg.h)
+  const bool seg_fits = dims->N <= kSegRows * kSegMaxS && seg_rows_ok(dims->N);
+  P.colseg = (size_t)2 * (dims->N + 1) * kCX * sizeof(double) > 64 * 1024 && seg_fits;
   {
     const char* e = getenv("ROMS_GPU_COLSEG");
     if (e && e[0] == '0') P.colseg = 0;
-    if (e && e[0] == '1') P.colseg = dims->N <= kSegRows * kSegMaxS;
+    if (e && e[0] == '1') P.colseg = seg_fits;
   }
   // register-resident sequential solvers (bit-exact) for the depths they are
   // compiled for; ROMS_GPU_COLREG=0 falls back to the LDS form (A/B runs)
@@ -827,6 +918,12 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
   {
     const char* e = getenv("ROMS_GPU_PRS_TY");
     P.prs_ty = (e && atoi(e) == 8) ? 8 : 4;
+  }
+  {
+    // 16-B window loads need every row's i0-2 on a 16-B boundary: the padded
+    // device pitch (g.off) gives that (roms_dev.h); ROMS_GPU_LD16=0 keeps the 8-B form
+    const char* e = getenv("ROMS_GPU_LD16");
+    P.ld16 = g.off != 0 && !(e && e[0] == '0');
   }
   {
     // visc3d with staged raw windows (bitwise): C3 2.34 -> 1.94 ms, C2 0.35 -> 0.30 ms

@@ -134,6 +134,7 @@ def load_library(path=LIB_PATH):
     L.roms_gpu_halo_plan.argtypes = [ctypes.c_int] * 8 + [P(ctypes.c_int), P(ctypes.c_long), P(ctypes.c_int)]
     L.roms_gpu_halo_map.argtypes = [ctypes.c_int] * 10 + [P(ctypes.c_int), P(ctypes.c_int), ctypes.c_long]
     L.roms_gpu_halo_map.restype = ctypes.c_long
+    L.roms_gpu_halo_map_wide.argtypes = [ctypes.c_int] * 11 + [P(ctypes.c_int), P(ctypes.c_int), ctypes.c_long]
     L.roms_gpu_halo_map_wide.restype = ctypes.c_long
     L.roms_gpu_wrt_rst.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_double, P(Tlev)]
     L.roms_gpu_wrt_his.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_double, P(Tlev), ctypes.c_int]
