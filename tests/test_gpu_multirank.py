@@ -325,9 +325,35 @@ def test_rim_first_overlap_bitwise_equals_serial_exchanges():
             assert np.array_equal(serial[r][4][f], over[r][4][f]), (r, f)
 
 
+# The deferred-exchange checks run in a child process with 16 hardware
+# queues (GPU_MAX_HW_QUEUES; HIP's default of 4 is shared by every rank's
+# library and halo streams here, and streams that share a hardware queue run
+# in submission order, which would join every exchange by accident).
+DEFER_SCRIPT = r"""
+import os, sys
+sys.path.insert(0, os.path.join(sys.argv[1], "ucla-roms_amd"))
+sys.path.insert(0, os.path.join(sys.argv[1], "tests"))
+import test_gpu_multirank as mr
+try:
+    mr.check_decomposition(mr._case(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]))
+except AssertionError as e:
+    print("MISMATCH", str(e)[:400])
+    raise SystemExit(3)
+print("BITWISE")
+"""
+
+
+def _deferred(kind, npx, npe, env):
+    e = dict(os.environ, GPU_MAX_HW_QUEUES="16", **env)
+    r = subprocess.run([sys.executable, "-c", DEFER_SCRIPT, ROOT, kind, str(npx), str(npe)], env=e,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode in (0, 3), (r.returncode, r.stdout[-1500:], r.stderr[-3000:])
+    return r.returncode == 0, r.stdout
+
+
 @pytest.mark.parametrize("kind", ["basin_lmd", "filament", "basin_flux", "pipes"])
-@pytest.mark.parametrize("npx,npe", [(2, 2), (3, 2)])
-def test_deferred_exchanges_late_unpack_bitwise(kind, npx, npe, monkeypatch):
+@pytest.mark.parametrize("npx,npe", [(2, 1), (2, 2)])
+def test_deferred_exchanges_late_unpack_bitwise(kind, npx, npe):
     """Deferred 3-D exchanges (on by default with > 1 rank):
     set_HUV's beside lmd_vmix(nstp), omega's and lmd_vmix's beside prsgrd,
     pre_step3d's tracer swap beside set_HUV1, set_HUV1's beside rho_eos(nrhs),
@@ -336,8 +362,8 @@ def test_deferred_exchanges_late_unpack_bitwise(kind, npx, npe, monkeypatch):
     (ROMS_GPU_XDELAY_US) a routine that reads a halo before its join would
     read the previous step's values: the subdomains still equal the single
     domain bitwise."""
-    monkeypatch.setenv("ROMS_GPU_XDELAY_US", "300")
-    check_decomposition(_case(kind), npx, npe)
+    ok, out = _deferred(kind, npx, npe, {"ROMS_GPU_XDELAY_US": "300"})
+    assert ok, out[-1500:]
 
 
 def test_deferred_exchanges_off_equals_on():
@@ -355,16 +381,18 @@ def test_deferred_exchanges_off_equals_on():
             assert np.array_equal(on[r][4][f], off[r][4][f]), (r, f)
 
 
-@pytest.mark.parametrize("bit,reader", [(2, "pre_step3d"), (4, "rho_eos(nrhs)"), (8, "omega (corrector)"),
-                                        (16, "step3d_uv1")])
-def test_deferred_exchange_missing_join_is_detected(bit, reader, monkeypatch):
+@pytest.mark.parametrize("bit,reader", [(8, "omega (corrector)"), (16, "step3d_uv1")])
+def test_deferred_exchange_missing_join_is_detected(bit, reader):
     """The delay hook is a real check: with one join left out (test hook
     ROMS_GPU_XTEST_SKIPJOIN=bit) the routine after it reads a halo before the
-    late unpack and the decomposition no longer matches.  (The join before
-    the predictor's omega, bit 1, cannot be shown this way: set_HUV
-    recomputes exactly the FlxU that step3d_uv2 left in the halo, so the
-    stale and the fresh halo are equal bitwise.)"""
-    monkeypatch.setenv("ROMS_GPU_XDELAY_US", "2000")
-    monkeypatch.setenv("ROMS_GPU_XTEST_SKIPJOIN", str(bit))
-    with pytest.raises(AssertionError):
-        check_decomposition(_case("basin_flux"), 2, 2)
+    late unpack and the decomposition no longer matches.  Only the joins of
+    the last exchange forked before their reader can be shown this way: the
+    in-process transport's host waits inside every exchange complete the
+    earlier ones (so bits 2 and 4 are covered by the bitwise runs above, not
+    here), and the join before the predictor's omega (bit 1) guards a halo
+    whose stale and fresh values are equal (set_HUV recomputes the FlxU that
+    step3d_uv2 left there)."""
+    ok, out = _deferred("basin_flux", 2, 1, {"ROMS_GPU_XDELAY_US": "2000", "ROMS_GPU_XTEST_SKIPJOIN": str(bit)})
+    assert not ok, out[-1500:]
+    ok, out = _deferred("basin_flux", 2, 1, {"ROMS_GPU_XDELAY_US": "2000"})
+    assert ok, out[-1500:]

@@ -291,6 +291,13 @@ __device__ __forceinline__ void uv_spline_seg(const Dev& d, const SegSpan& sg, S
   }
 }
 
+// A load whose value feeds only one arm of a select is sunk by the compiler
+// into a branch of its own, and every such branch waits for its load alone:
+// 14 serialized round trips per segment in the tracer flux rows (measured in
+// the disassembly).  Loading every row first and pinning the values after
+// all loads are issued keeps them one batch; the select is unchanged.
+__device__ __forceinline__ void pin(double& x) { __asm__ volatile("" : "+v"(x)); }
+
 // SPLINE_TS advective flux FC(r)*We(r) of a tracer column at interfaces
 // r = c0-1+q, q = 0..n (0 at the bottom and the surface); hz, tt as w, f of
 // spline_fc_seg.
@@ -299,11 +306,15 @@ __device__ __forceinline__ void tracer_spline_seg(const SegSpan& sg, int N, long
                                                   const double (&hz)[KR + 1], const double (&tt)[KR],
                                                   const double* __restrict__ We, double (&fl)[KR]) {
   spline_fc_seg<KR>(sg, N, X, hz, tt, fl);
+  double we[KR];
+#pragma unroll
+  for (int q = 0; q < KR; q++) we[q] = We[(long)min(max(sg.c0 - 1 + q, 1), N - 1) * n2];
+#pragma unroll
+  for (int q = 0; q < KR; q++) pin(we[q]);
 #pragma unroll
   for (int q = 0; q < KR; q++) {
     const int r = sg.c0 - 1 + q;
-    const double we = We[(long)min(max(r, 1), N - 1) * n2];
-    fl[q] = (r == 0 || r == N) ? 0.0 : fl[q] * we;
+    fl[q] = (r == 0 || r == N) ? 0.0 : fl[q] * we[q];
   }
 }
 

@@ -14,6 +14,32 @@
 
 namespace roms {
 
+// Raw-buffer view of one device array (gfx950 buffer_load / buffer_store):
+// the lane's byte offset in a VGPR (32-bit), the level's in an SGPR
+// (soffset), so a column walk keeps no 64-bit address per level in vector
+// registers -- the straight-line level loops of the column kernels otherwise
+// hold one address pair per level live across their passes (k_uv2_fused
+// spilled ~200 VGPRs that way).  Offsets must stay below 4 GiB from the base
+// (one 3-D field or one time slot: 855 MB at 1024^2 x 100).
+// With the array's extent given, an access beyond it is dropped by the
+// hardware (a store does nothing, a load returns 0): lanes that must not store
+// pass kBufOff instead of branching around the store, which keeps a level
+// loop straight-line code.
+constexpr unsigned kBufOff = 0x80000000u;   // + any level offset below 2 GiB: beyond every extent used here
+struct BufF64 {
+  __amdgpu_buffer_rsrc_t r;
+  __device__ __forceinline__ explicit BufF64(const double* p, long n = 0)
+      : r(__builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(p), (short)0,
+                                            n > 0 ? (int)(unsigned)(n * 8) : (int)0x7fffffff, 0x00020000)) {}
+  __device__ __forceinline__ double ld(unsigned vb, unsigned sb) const {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)vb, (int)sb, 0));
+  }
+  __device__ __forceinline__ void st(double v, unsigned vb, unsigned sb) const {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) int, v), r, (int)vb,
+                                          (int)sb, 0);
+  }
+};
+
 // LDS window of a 64x4 tile with a 2-cell halo on every side (i0-2.., j0-2..)
 constexpr int kUVW = kBX + 4, kUVH = kBY + 4, kUVN = kUVW * kUVH;
 

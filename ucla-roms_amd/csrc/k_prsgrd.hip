@@ -108,10 +108,9 @@ constexpr int kPYH = kBY + 2, kPYN = kBX * kPYH;          // v-points m = j0-1 .
 // a third of the vector-memory instructions of forming every difference
 // from two global loads (measured: the per-cell kernel was bound by the
 // vector-memory instruction rate, not by HBM bytes).
-// The row is 68 wide (one unused column at i0+65): an even width keeps every
-// row of the window on a 16-B boundary in LDS, so the L16 form stores two
-// doubles per lane.
-constexpr int kPWW = kBX + 4, kPWH = kBY + 3, kPWN = kPWW * kPWH;   // raw window (i0-2.., j0-2..)
+// (The L16 form's rows are 68 wide -- one unused column at i0+65 -- so that
+// every row of the window starts on a 16-B boundary in LDS.)
+constexpr int kPWW = kBX + 3, kPWH = kBY + 3, kPWN = kPWW * kPWH;   // raw window (i0-2.., j0-2..)
 constexpr int kPWQ = (kPWN + kBX * kBY - 1) / (kBX * kBY);
 constexpr int kPQ = (kPXN + kPYN + kBX * kBY - 1) / (kBX * kBY);
 // L16 (Params::ld16, the padded device pitch): the raw window and the u/v
@@ -127,7 +126,8 @@ __global__ void __launch_bounds__(kBX * TY, L16 && TY == kBY ? 5 : 1) k_prsgrd_u
   const uint3 bI = h_tile(d.p.tile_grp);
   // the file-scope window sizes for a 64 x TY tile (TY = kBY: the constants above)
   constexpr int NT = kBX * TY, XN = kPXW * TY, YH = TY + 2, YN = kBX * YH;
-  constexpr int WN = kPWW * (TY + 3), WQ = (WN + NT - 1) / NT, PQ = (XN + YN + NT - 1) / NT;
+  constexpr int PWW = L16 ? kPWW + 1 : kPWW;   // raw window row (even for L16)
+  constexpr int WN = PWW * (TY + 3), WQ = (WN + NT - 1) / NT, PQ = (XN + YN + NT - 1) / NT;
   constexpr int UWN = kUVW * (TY + 4);
   // one LDS block: the raw window, the elementary differences and the
   // harmonic means (and, FUSE, the u/v window after them)
@@ -154,10 +154,10 @@ __global__ void __launch_bounds__(kBX * TY, L16 && TY == kBY ? 5 : 1) k_prsgrd_u
   const long kk = (long)(k - 1) * b.n2, sj = b.nx2;
   const int i0 = tile_i0(R.i0) + (int)bI.x * kBX, j0 = R.j0 + (int)bI.y * TY;
   const int tid = threadIdx.x + kBX * threadIdx.y;
-  auto W = [&](int i, int j) { return (i - (i0 - 2)) + (j - (j0 - 2)) * kPWW; };
+  auto W = [&](int i, int j) { return (i - (i0 - 2)) + (j - (j0 - 2)) * PWW; };
   // ---- loads, all issued before the first barrier ----
   // 8-B form: entry q of the window per lane and round; L16: the pair of
-  // entries 2p, 2p+1 (one row holds kPWW / 2 pairs)
+  // entries 2p, 2p+1 (one row holds PWW / 2 pairs)
   constexpr int WP = WN / 2, WPQ = (WP + NT - 1) / NT;
   constexpr int WL = L16 ? WPQ : WQ;
   double2 wz[WL], wr[WL], wq[WL];
@@ -167,7 +167,7 @@ __global__ void __launch_bounds__(kBX * TY, L16 && TY == kBY ? 5 : 1) k_prsgrd_u
     wz[m] = wr[m] = wq[m] = double2{0.0, 0.0};
     if (L16) {
       if (q < WP) {
-        const int i = i0 - 2 + 2 * (q % (kPWW / 2)), j = j0 - 2 + q / (kPWW / 2);
+        const int i = i0 - 2 + 2 * (q % (PWW / 2)), j = j0 - 2 + q / (PWW / 2);
         if (i >= -1 && i <= b.Lm + 2 && j <= b.Mm + 2) {
           const long o = IJ(b, i, j) + kk;
           const bool hi = i + 1 <= b.Lm + 2;
@@ -178,7 +178,7 @@ __global__ void __launch_bounds__(kBX * TY, L16 && TY == kBY ? 5 : 1) k_prsgrd_u
         }
       }
     } else if (q < WN) {
-      const int i = i0 - 2 + q % kPWW, j = j0 - 2 + q / kPWW;
+      const int i = i0 - 2 + q % PWW, j = j0 - 2 + q / PWW;
       if (i >= -1 && i <= b.Lm + 2 && j <= b.Mm + 2) {
         const long o = IJ(b, i, j) + kk;
         wz[m].x = F.z_r[o];
@@ -349,7 +349,7 @@ __global__ void __launch_bounds__(kBX * TY, L16 && TY == kBY ? 5 : 1) k_prsgrd_u
   if (dv) {
     const int q = threadIdx.x + threadIdx.y * kBX;    // p = j-1 ; q+kBX: p = j
     const double dZ0 = sdZy[q], dZ1 = sdZy[q + kBX], dR0 = sdRy[q], dR1 = sdRy[q + kBX];
-    const double z0 = sZ[wc], zv = sZ[wc - kPWW], r0 = rhov(wc), rv_ = rhov(wc - kPWW);
+    const double z0 = sZ[wc], zv = sZ[wc - PWW], r0 = rhov(wc), rv_ = rhov(wc - PWW);
     prv = 0.5 * (hz0 + hzv) * dmv *
               (Pv - P0 -
                HalfGRho * ((r0 + rv_) * (z0 - zv) -

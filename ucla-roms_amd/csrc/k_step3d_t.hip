@@ -260,11 +260,15 @@ __global__ void __launch_bounds__(kSegBlock, 2) k_step3d_t_seg(Dev d, Range R, i
   {
     double fc[KR];
     spline_fc_seg<KR>(sg, N, X, hz, tt, fc);
+    double we[KR];   // every row's We issued as one batch (pin, k_colseg.h)
+#pragma unroll
+    for (int q = 0; q < KR; q++) we[q] = We[(long)min(max(c0 - 1 + q, 1), N - 1) * n2];
+#pragma unroll
+    for (int q = 0; q < KR; q++) pin(we[q]);
 #pragma unroll
     for (int q = 0; q < KR; q++) {
       const int r = c0 - 1 + q;
-      const double we = We[(long)min(max(r, 1), N - 1) * n2];
-      tt[q] = (r == 0 || r == N) ? 0.0 : fc[q] * we;
+      tt[q] = (r == 0 || r == N) ? 0.0 : fc[q] * we[q];
     }
   }
   // implicit diffusion rows, cells k = c0+p, p = 0..n-1.  The scheduling

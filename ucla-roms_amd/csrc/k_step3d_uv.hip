@@ -903,15 +903,22 @@ __global__ void __launch_bounds__(256) k_uv2_flux(Dev d, Range R, int nnew, int 
 // order and the results are bit-identical to the two kernels
 // (step3d_uv2.F:18-786).  The open-edge columns outside the coupling range
 // (walls, ghost rows) follow u3dbc/v3dbc through k_uv2_flux (edge mode). ----
-template <int KL>
+// KL > 13 (N > 52): the lane's KL Hz_u levels sit in LDS (hc[] below) -- in
+// registers beside the KL u levels they spilled (29 VGPRs at KL = 25); three
+// 256-thread blocks per CU keep the same occupancy
+// FULL: N == 4*KL, every segment holds KL levels (C3's N = 100), so the
+// per-level guards fold away and the level loops are straight-line code
+template <int KL, bool FULL = false>
 __global__ void __launch_bounds__(256, KL > 13 ? 3 : 4) k_uv2_fused(Dev d, Range R, int nnew, int nstp, int knew) {
+  constexpr bool kHcLds = KL > 13;
+  __shared__ double sHc[kHcLds ? KL * 256 : 1];
   const uint3 bI = xcd_tile();
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const int N = b.N;
   const double DELTA = 0.28, EPSIL = 0.36;
   const ChainLane cl = chain_lane<KL>(R, bI, N);
-  const int i = cl.i, j = cl.j, g = cl.g, lo = cl.lo, nk = cl.nk;
+  const int i = cl.i, j = cl.j, g = cl.g, lo = cl.lo, nk = FULL ? KL : cl.nk;
   const long n2 = b.n2;
   auto chain2 = [&](double& s1, double& s2, auto&& body) { chain_down(cl, s1, s2, body); };
   const int d0 = gridDim.z == 2 ? (int)bI.z : 0, d1 = gridDim.z == 2 ? d0 + 1 : 2;   // grid z = 2: a direction per block
@@ -931,14 +938,35 @@ __global__ void __launch_bounds__(256, KL > 13 ? 3 : 4) k_uv2_fused(Dev d, Range
     const double avg1 = dir == 0 ? F.DU_avg1[ij] : F.DV_avg1[ij];
     const double avg2 = dir == 0 ? F.DU_avg2[ij] : F.DV_avg2[ij];
     const double msk = dir == 0 ? F.umask[ij] : F.vmask[ij];
-    double un[KL], hc[KL];
+    // FULL: the level loops' memory operations as raw-buffer accesses, the
+    // lane's column offset in a VGPR and the level's in an SGPR
+    const double* const Ub = (dir == 0 ? F.u : F.v);
+    const BufF64 bUn(Ub + (long)(nnew - 1) * b.n3, b.n3), bUs(Ub + (long)(nstp - 1) * b.n3, b.n3), bHz(F.Hz, b.n3),
+        bFl(dir == 0 ? F.FlxU : F.FlxV, b.n3);
+    const unsigned vo = (unsigned)((ij + (long)(lo - 1) * n2) * 8), vom = vo - (unsigned)(s * 8);
+    const unsigned vst = act ? vo : kBufOff;   // inactive lanes' stores fall outside the extent (dropped)
+    auto so = [&](int q) { return (unsigned)((long)q * n2 * 8); };
+    double un[KL];
+    double hcr[kHcLds ? 1 : KL];
+    struct HcRef {   // hc[q]: Hz_u of the lane's level lo+q, in LDS (kHcLds) or registers
+      double* l;
+      double* r;
+      __device__ __forceinline__ double& operator[](int q) const { return kHcLds ? l[q * 256] : r[q]; }
+    } const hc{sHc + threadIdx.x, hcr};
 #pragma unroll
     for (int q = 0; q < KL; q++) {
       if (q < nk) {
-        const long o = (long)(lo + q - 1) * n2;
-        un[q] = Un[o];
-        hc[q] = 0.5 * (Hz[o] + Hz[o - s]);
+        if (FULL) {
+          un[q] = bUn.ld(vo, so(q));
+          hc[q] = 0.5 * (bHz.ld(vo, so(q)) + bHz.ld(vom, so(q)));
+        } else {
+          const long o = (long)(lo + q - 1) * n2;
+          un[q] = Un[o];
+          hc[q] = 0.5 * (Hz[o] + Hz[o - s]);
+        }
       }
+      // FULL: the loads of 8 levels in flight at a time (all 25 hoisted spilled)
+      if (FULL && q % 8 == 7) __builtin_amdgcn_sched_barrier(0);
     }
     // k_uv2_couple: CF0 = sum Hz_u, DC0 = sum Hz*u (k = N..1); u = Hz*u/Hz_u
     double CF0, DC0;
@@ -964,15 +992,24 @@ __global__ void __launch_bounds__(256, KL > 13 ? 3 : 4) k_uv2_fused(Dev d, Range
       else F.vbar[IJL(b, i, j, knew)] = DCi * avg1;
     }
     FC0 = DCi * (FC0 - avg1);
-    // corrected u and the fluxes; un[] becomes the flux cfk
+    // corrected u and the fluxes; un[] becomes the flux cfk (FULL: the
+    // straight-line level loop's loads of u(nstp) and Flx stay here, not
+    // hoisted above the chains, where they spilled)
+    if (FULL) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int q = 0; q < KL; q++) {
       if (q < nk) {
-        const long o = (long)(lo + q - 1) * n2;
         const double u1 = (un[q] - FC0) * msk;
-        if (act) Un[o] = u1;
-        un[q] = DELTA * Flx[o] + EPSIL * (hc[q] * dn) * (Us[o] + u1);
+        if (FULL) {
+          bUn.st(u1, vst, so(q));
+          un[q] = DELTA * bFl.ld(vo, so(q)) + EPSIL * (hc[q] * dn) * (bUs.ld(vo, so(q)) + u1);
+        } else {
+          const long o = (long)(lo + q - 1) * n2;
+          if (act) Un[o] = u1;
+          un[q] = DELTA * Flx[o] + EPSIL * (hc[q] * dn) * (Us[o] + u1);
+        }
       }
+      if (FULL && q % 8 == 7) __builtin_amdgcn_sched_barrier(0);
     }
     double CS, unused;
     chain2(CS, unused, [&](double& a, double& c) {
@@ -981,7 +1018,10 @@ __global__ void __launch_bounds__(256, KL > 13 ? 3 : 4) k_uv2_fused(Dev d, Range
         if (q < nk) a = a + un[q];
     });
     const double CF1 = DCi * (CS - avg2);
-    if (act) {
+    if (FULL) {
+#pragma unroll
+      for (int q = 0; q < KL; q++) bFl.st(un[q] - (hc[q] * dn) * CF1, vst, so(q));
+    } else if (act) {
 #pragma unroll
       for (int q = 0; q < KL; q++)
         if (q < nk) Flx[(long)(lo + q - 1) * n2] = un[q] - (hc[q] * dn) * CF1;
@@ -1125,6 +1165,7 @@ void launch_step3d_uv2(const Dev& d, hipStream_t s, const Tlev& t) {
     gf.z = d.p.chain_dirz ? 2 : 1;
     if (kl <= 5) hipLaunchKernelGGL(k_uv2_fused<5>, gf, dim3(256), 0, s, d, R1, t.nnew, t.nstp, t.knew);
     else if (kl <= 13) hipLaunchKernelGGL(k_uv2_fused<13>, gf, dim3(256), 0, s, d, R1, t.nnew, t.nstp, t.knew);
+    else if (b.N == 100) hipLaunchKernelGGL((k_uv2_fused<25, true>), gf, dim3(256), 0, s, d, R1, t.nnew, t.nstp, t.knew);
     else hipLaunchKernelGGL(k_uv2_fused<25>, gf, dim3(256), 0, s, d, R1, t.nnew, t.nstp, t.knew);
     if (d.f.uv2e_couple && d.p.uv2e_nc > 0 && d.p.uv2e_nf > 0) {   // closed edges: chain form over the column lists
       const int nc = d.p.uv2e_nc, nf = d.p.uv2e_nf;

@@ -920,10 +920,12 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     P.prs_ty = (e && atoi(e) == 8) ? 8 : 4;
   }
   {
-    // 16-B window loads need every row's i0-2 on a 16-B boundary: the padded
-    // device pitch (g.off) gives that (roms_dev.h); ROMS_GPU_LD16=0 keeps the 8-B form
+    // 16-B window loads (they need every row's i0-2 on a 16-B boundary: the
+    // padded device pitch, g.off, gives that, roms_dev.h) measured slower at
+    // C3 (k_prsgrd_uv 4.20-4.26 vs 3.96 ms per call, same box, the 8-B form
+    // with a 67-wide window 3.6 ms): opt-in, ROMS_GPU_LD16=1
     const char* e = getenv("ROMS_GPU_LD16");
-    P.ld16 = g.off != 0 && !(e && e[0] == '0');
+    P.ld16 = g.off != 0 && e && e[0] == '1';
   }
   {
     // visc3d with staged raw windows (bitwise): C3 2.34 -> 1.94 ms, C2 0.35 -> 0.30 ms
