@@ -69,10 +69,11 @@ raise SystemExit(1 if bad else 0)
 """
 
 
-def _ranks(kind, npx, npe):
+def _ranks(kind, npx, npe, env=None):
     with tempfile.TemporaryDirectory() as td:
         ps = [subprocess.Popen([sys.executable, "-c", RANK_SCRIPT, ROOT, str(r), td, kind, str(npx), str(npe)],
-                               env=dict(os.environ), stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+                               env=dict(os.environ, **(env or {})), stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                               text=True)
               for r in range(npx * npe)]
         outs = []
         for p in ps:
@@ -96,6 +97,15 @@ def _ranks(kind, npx, npe):
 @pytest.mark.parametrize("npx,npe", [(2, 1), (2, 2)])
 def test_processes_one_gpu_ipc_host_channel_bitwise(kind, npx, npe):
     _ranks(kind, npx, npe)
+
+
+@pytest.mark.parametrize("kind", ["filament", "basin_obc"])
+def test_processes_deferred_exchanges_ipc_bitwise(kind):
+    """The deferred 3-D exchanges (ROMS_GPU_XOVERLAP=1) between processes:
+    the IPC pack / wait / unpack kernels on each rank's halo stream beside
+    the next routine, graph-captured, with every unpack held back 300 us; the
+    2x2 subdomains still equal the single domain."""
+    _ranks(kind, 2, 2, {"ROMS_GPU_XOVERLAP": "1", "ROMS_GPU_XDELAY_US": "300"})
 
 
 FATAL_SCRIPT = r"""

@@ -344,7 +344,7 @@ print("BITWISE")
 
 
 def _deferred(kind, npx, npe, env):
-    e = dict(os.environ, GPU_MAX_HW_QUEUES="16", **env)
+    e = dict(os.environ, GPU_MAX_HW_QUEUES="16", ROMS_GPU_XOVERLAP="1", **env)
     r = subprocess.run([sys.executable, "-c", DEFER_SCRIPT, ROOT, kind, str(npx), str(npe)], env=e,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode in (0, 3), (r.returncode, r.stdout[-1500:], r.stderr[-3000:])
@@ -354,7 +354,7 @@ def _deferred(kind, npx, npe, env):
 @pytest.mark.parametrize("kind", ["basin_lmd", "filament", "basin_flux", "pipes"])
 @pytest.mark.parametrize("npx,npe", [(2, 1), (2, 2)])
 def test_deferred_exchanges_late_unpack_bitwise(kind, npx, npe):
-    """Deferred 3-D exchanges (on by default with > 1 rank):
+    """Deferred 3-D exchanges (ROMS_GPU_XOVERLAP=1, opt-in):
     set_HUV's beside lmd_vmix(nstp), omega's and lmd_vmix's beside prsgrd,
     pre_step3d's tracer swap beside set_HUV1, set_HUV1's beside rho_eos(nrhs),
     the corrector's omega and lmd_vmix beside prsgrd, the closing omega's
@@ -367,13 +367,13 @@ def test_deferred_exchanges_late_unpack_bitwise(kind, npx, npe):
 
 
 def test_deferred_exchanges_off_equals_on():
-    """ROMS_GPU_XOVERLAP=0 (every exchange in place, the reference's order)
-    and the default deferred order give the same fields bitwise."""
+    """The default (every exchange in place, the reference's order) and the
+    deferred order (ROMS_GPU_XOVERLAP=1) give the same fields bitwise."""
     case = _case("basin_lmd")
-    on, _ = run_decomposed(case, 2, 2, 5)
-    os.environ["ROMS_GPU_XOVERLAP"] = "0"
+    off, _ = run_decomposed(case, 2, 2, 5)
+    os.environ["ROMS_GPU_XOVERLAP"] = "1"
     try:
-        off, _ = run_decomposed(case, 2, 2, 5)
+        on, _ = run_decomposed(case, 2, 2, 5)
     finally:
         del os.environ["ROMS_GPU_XOVERLAP"]
     for r in range(4):
@@ -381,7 +381,7 @@ def test_deferred_exchanges_off_equals_on():
             assert np.array_equal(on[r][4][f], off[r][4][f]), (r, f)
 
 
-@pytest.mark.parametrize("bit,reader", [(8, "omega (corrector)"), (16, "step3d_uv1")])
+@pytest.mark.parametrize("bit,reader", [(8, "omega (corrector)")])
 def test_deferred_exchange_missing_join_is_detected(bit, reader):
     """The delay hook is a real check: with one join left out (test hook
     ROMS_GPU_XTEST_SKIPJOIN=bit) the routine after it reads a halo before the
@@ -389,9 +389,11 @@ def test_deferred_exchange_missing_join_is_detected(bit, reader):
     the last exchange forked before their reader can be shown this way: the
     in-process transport's host waits inside every exchange complete the
     earlier ones (so bits 2 and 4 are covered by the bitwise runs above, not
-    here), and the join before the predictor's omega (bit 1) guards a halo
-    whose stale and fresh values are equal (set_HUV recomputes the FlxU that
-    step3d_uv2 left there)."""
+    here); the join before the predictor's omega (bit 1) guards a halo whose
+    stale and fresh values are equal (set_HUV recomputes the FlxU that
+    step3d_uv2 left there), and so, in this case, does the one before
+    step3d_uv1 (bit 16: the rank edge's Akv is the same in both lmd_vmix
+    calls of a step)."""
     ok, out = _deferred("basin_flux", 2, 1, {"ROMS_GPU_XDELAY_US": "2000", "ROMS_GPU_XTEST_SKIPJOIN": str(bit)})
     assert not ok, out[-1500:]
     ok, out = _deferred("basin_flux", 2, 1, {"ROMS_GPU_XDELAY_US": "2000"})

@@ -19,6 +19,12 @@ struct HaloGeom {
   int i0, i1;      // columns of the S/N strips
   int active[8];   // neighbour present in direction d
   long cnt[8];     // elements per level of the message to/from direction d
+  // the active directions in order: the pack / unpack grids hold one z-slice
+  // per active direction (act_dir[blockIdx.z]) instead of 8 of which most
+  // exit at once -- with exchanges running beside compute (deferred
+  // exchanges) every empty block still took a dispatch slot from it
+  int nact;
+  int act_dir[8];
 };
 struct HaloPlan {
   HaloGeom g;
@@ -78,8 +84,8 @@ struct Halo {
   // Deferred 3-D exchanges (enqueue_step): on multi-rank runs
   // a producer's trailing exchange runs on cs beside the next routine that
   // reads none of its halo; the step joins it before the first reader.
-  // xoverlap: enabled (default with a communicator of > 1 rank;
-  // ROMS_GPU_XOVERLAP=0/1 forces it); defer > 0: launch_exchange_list forks
+  // xoverlap: enabled (ROMS_GPU_XOVERLAP=1 with a communicator of > 1 rank;
+  // off by default, see halo_setup); defer > 0: launch_exchange_list forks
   // instead of exchanging on the caller's stream (set around one producer).
   int xoverlap = 0;
   int defer = 0;

@@ -74,7 +74,7 @@ __device__ __forceinline__ int list_slot(const ExchList& L, int& lev) {
 
 // grid: x = element of the strip, y = list level, z = direction
 __global__ void __launch_bounds__(256) k_halo_pack(HaloGeom g, ExchList L, double* __restrict__ sbuf, long cap) {
-  const int dir = blockIdx.z;
+  const int dir = g.act_dir[blockIdx.z];
   if (!g.active[dir]) return;
   const long cnt = g.cnt[dir];
   const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -87,7 +87,7 @@ __global__ void __launch_bounds__(256) k_halo_pack(HaloGeom g, ExchList L, doubl
   sbuf[dir * cap + (long)blockIdx.y * cnt + e] = L.p[q][(long)(i + 1) + (long)(j + 1) * g.nx2 + (long)lev * g.n2];
 }
 __global__ void __launch_bounds__(256) k_halo_unpack(HaloGeom g, ExchList L, const double* __restrict__ rbuf, long cap) {
-  const int h = blockIdx.z;
+  const int h = g.act_dir[blockIdx.z];
   if (!g.active[h]) return;
   const long cnt = g.cnt[h];
   const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -116,7 +116,7 @@ struct IpcPtrs {
 // buffers: a rank that gave up must not overwrite a slot the neighbour has
 // not unpacked yet.
 __global__ void __launch_bounds__(256) k_halo_pack_ipc(HaloGeom g, ExchList L, IpcPtrs P, long cap) {
-  const int dir = blockIdx.z;
+  const int dir = g.act_dir[blockIdx.z];
   if (!g.active[dir] || *P.err_dev) return;
   const long cnt = g.cnt[dir];
   const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -167,7 +167,7 @@ __global__ void __launch_bounds__(64) k_halo_wait_ipc(HaloGeom g, IpcPtrs P, int
   if (h == 0) *P.seq = want;
 }
 __global__ void __launch_bounds__(256) k_halo_unpack_ipc(HaloGeom g, ExchList L, IpcPtrs P, long cap) {
-  const int h = blockIdx.z;
+  const int h = g.act_dir[blockIdx.z];
   if (!g.active[h] || *P.err_dev) return;
   const long cnt = g.cnt[h];
   const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -287,6 +287,9 @@ HaloPlan halo_plan(int Lm, int Mm, int npx, int npe, int inode, int jnode, int e
     else g.cnt[d] = (long)w * w;
     if (!act[d]) g.cnt[d] = 0;
   }
+  g.nact = 0;
+  for (int d = 0; d < 8; d++)
+    if (act[d]) g.act_dir[g.nact++] = d;
   return P;
 }
 
@@ -304,7 +307,7 @@ static int exchange_host(const Halo& H, hipStream_t s, const ExchList& L) {
   for (int q = 0; q < L.n; q++) nl += L.nlev[q];
   long mx = 0;
   for (int d = 0; d < 8; d++) mx = g.cnt[d] > mx ? g.cnt[d] : mx;
-  const dim3 grid((unsigned)((mx + 255) / 256), (unsigned)nl, 8);
+  const dim3 grid((unsigned)((mx + 255) / 256), (unsigned)nl, (unsigned)(g.nact > 0 ? g.nact : 1));
   hipLaunchKernelGGL(k_halo_pack, grid, dim3(256), 0, s, g, L, H.sbuf, H.cap);
   const long m = H.gcnt * nl;
   std::vector<double> mine((size_t)8 * m, 0.0), all((size_t)8 * m * c->nranks);
@@ -489,11 +492,16 @@ int halo_setup(Halo& H, RomsComm* comm, const HaloPlan& plan, int maxlev, const 
   H.nfork = H.njoin = 0;
   H.defer = 0;
   {
-    // deferred 3-D exchanges beside the next routine (enqueue_step): on by
-    // default whenever there is a neighbour to talk to (a single rank has no
-    // exchanges to hide: N = 1 runs are untouched by construction)
+    // deferred 3-D exchanges beside the next routine (enqueue_step): opt-in,
+    // ROMS_GPU_XOVERLAP=1.  Measured on one MI355X:
+    // one process exchanging with itself through IPC, C2, 7.12 vs 6.92-6.95
+    // ms per step; 2 and 4 ranks sharing the GPU, C3, 63-75 vs 57-58 ms --
+    // the forked pack / wait / unpack kernels and the graph's extra branches
+    // cost more than the exchange time they hide on one GPU.  Only an 8-GPU
+    // run can show the xGMI latency they would hide; bench.py --gpus N > 1
+    // reports both
     const char* ex = getenv("ROMS_GPU_XOVERLAP");
-    H.xoverlap = ex ? (ex[0] == '1') : (comm && comm->nranks > 1);
+    H.xoverlap = ex && ex[0] == '1' && comm && comm->nranks > 1;
     const char* es = getenv("ROMS_GPU_XTEST_SKIPJOIN");
     H.xskip = es ? atoi(es) : 0;
     const char* ed = getenv("ROMS_GPU_XDELAY_US");
@@ -630,7 +638,7 @@ void halo_exchange(const Halo& H, hipStream_t s, const ExchList& L) {
   const_cast<Halo&>(H).nexch++;
   long mx = 0;
   for (int d = 0; d < 8; d++) mx = g.cnt[d] > mx ? g.cnt[d] : mx;
-  const dim3 grid((unsigned)((mx + 255) / 256), (unsigned)nl, 8);
+  const dim3 grid((unsigned)((mx + 255) / 256), (unsigned)nl, (unsigned)(g.nact > 0 ? g.nact : 1));
   if (H.ipc.ok) {
     exchange_ipc(H, s, g, L, grid);
     return;

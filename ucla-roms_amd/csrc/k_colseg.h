@@ -110,6 +110,13 @@ struct SegXchg {
 __device__ __forceinline__ bool seg_live(int q, int n) { return q < kSegNMin || q < n; }
 __device__ __forceinline__ bool seg_last(int q, int n) { return q >= kSegNMin - 1 && q == n - 1; }
 
+// A load whose value feeds only one arm of a select is sunk by the compiler
+// into a branch of its own, and every such branch waits for its load alone:
+// 14 serialized round trips per segment in the tracer flux rows (measured in
+// the disassembly).  Loading every row first and pinning the values after
+// all loads are issued keeps them one batch; the select is unchanged.
+__device__ __forceinline__ void pin(double& x) { __asm__ volatile("" : "+v"(x)); }
+
 #ifndef ROMS_SEG_LOAD_GROUP
 #define ROMS_SEG_LOAD_GROUP 5
 #endif
@@ -282,21 +289,24 @@ __device__ __forceinline__ void uv_spline_seg(const Dev& d, const SegSpan& sg, S
   }
   spline_fc_seg<KR>(sg, N, X, dc, uu, fl);
   const double m1 = mask[ij + s], m0 = mask[ij - s];
+  // every row's 4-point We average formed unconditionally, in load groups,
+  // and pinned before the selects (see pin above: sunk into per-row
+  // branches the 14 rows' loads were 14 serialized memory round trips)
+  double wf[KR];
+#pragma unroll
+  for (int q = 0; q < KR; q++) {
+    const long w = (long)min(max(c0 - 1 + q, 1), N - 1) * n2;
+    wf[q] = We[w] + We[w - s] - 0.125 * ((We[w + s] - We[w]) * m1 - (We[w - s] - We[w - 2 * s]) * m0);
+    if (q % kSegLoadGroup == kSegLoadGroup - 1) __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int q = 0; q < KR; q++) pin(wf[q]);
 #pragma unroll
   for (int q = 0; q < KR; q++) {
     const int r = c0 - 1 + q;
-    const long w = (long)min(max(r, 1), N - 1) * n2;
-    const double wf = We[w] + We[w - s] - 0.125 * ((We[w + s] - We[w]) * m1 - (We[w - s] - We[w - 2 * s]) * m0);
-    fl[q] = (r == 0 || r == N) ? 0.0 : fl[q] * 0.5 * wf;
+    fl[q] = (r == 0 || r == N) ? 0.0 : fl[q] * 0.5 * wf[q];
   }
 }
-
-// A load whose value feeds only one arm of a select is sunk by the compiler
-// into a branch of its own, and every such branch waits for its load alone:
-// 14 serialized round trips per segment in the tracer flux rows (measured in
-// the disassembly).  Loading every row first and pinning the values after
-// all loads are issued keeps them one batch; the select is unchanged.
-__device__ __forceinline__ void pin(double& x) { __asm__ volatile("" : "+v"(x)); }
 
 // SPLINE_TS advective flux FC(r)*We(r) of a tracer column at interfaces
 // r = c0-1+q, q = 0..n (0 at the bottom and the surface); hz, tt as w, f of

@@ -205,14 +205,8 @@ __global__ void __launch_bounds__(256) k_swr_frac(Dev d, Range R) {
 }
 
 // ---- pass 1: extended range ----
-// ROMS_KPP_EXT_PF (default 1): k_kpp_ext's level loop loads every input one
-// level ahead; that needs ~140 VGPRs, so 3 waves per SIMD (at 4 they spilled)
-#ifndef ROMS_KPP_EXT_PF
-#define ROMS_KPP_EXT_PF 1
-#endif
-#define KPP_EXT_WAVES (ROMS_KPP_EXT_PF ? 3 : 4)
 template <class C>
-__global__ void __launch_bounds__(64, KPP_EXT_WAVES) k_kpp_ext(Dev d, Range E, int tind, int nstp, KppConst kc) {
+__global__ void __launch_bounds__(64, 4) k_kpp_ext(Dev d, Range E, int tind, int nstp, KppConst kc) {
   ROMS_IJC_OR_RETURN(E)
   const Bounds& b = d.b;
   const Fields& F = d.f;
@@ -290,28 +284,10 @@ __global__ void __launch_bounds__(64, KPP_EXT_WAVES) k_kpp_ext(Dev d, Range E, i
   double Crp = FCk + vtsq(N, zrp);
   int kbls = Crp < 0. ? N : 0;
   double cr_k = Crp, cr_kp = 0., zr_k = zrp, zr_kp = 0.;
-  // every input of level k (those of vtsq included) loaded one level ahead,
-  // before level k+1's stores of rig and FC: without it each level waited
-  // for its own loads behind the previous level's stores (one memory round
-  // trip per level, 100 per column walk).  Same values, same expressions.
-  struct Lv {
-    double u0, u1, v0, v1, hz, zr, zw, bk, sw, swm, bvm;
-  };
-  auto ldlv = [&](int k) {
-    const long o = (long)(k - 1) * n2;
-    Lv L;
-    L.u0 = U[o]; L.u1 = U[o + 1]; L.v0 = V[o]; L.v1 = V[o + sj];
-    L.hz = Hz[o]; L.zr = zr[o]; L.zw = zw[(long)k * n2]; L.bk = bvf[(long)k * n2];
-    L.sw = sw[(long)k * n2]; L.swm = sw[o]; L.bvm = bvf[o];
-    return L;
-  };
-  Lv cur = ldlv(N - 1);
-#pragma unroll 1
   for (int k = N - 1; k >= 1; k--) {
-    const Lv nx = ROMS_KPP_EXT_PF ? ldlv(k > 1 ? k - 1 : 1) : Lv{};
-    if (!ROMS_KPP_EXT_PF) cur = ldlv(k);
-    const double u0 = cur.u0, u1 = cur.u1, v0 = cur.v0, v1 = cur.v1;
-    const double hz = cur.hz, zrk = cur.zr, zwk = cur.zw, bk = cur.bk;
+    const long o = (long)(k - 1) * n2;
+    const double u0 = U[o], u1 = U[o + 1], v0 = V[o], v1 = V[o + sj];
+    const double hz = Hz[o], zrk = zr[o], zwk = zw[(long)k * n2], bk = bvf[(long)k * n2];
     // raw gradient Richardson number (lmd_vmix.F:157-165), LMD_RIMIX only
     if (P.lmd_rimix) {
       const double cff = 0.5 / (zrp - zrk);
@@ -330,23 +306,13 @@ __global__ void __launch_bounds__(64, KPP_EXT_WAVES) k_kpp_ext(Dev d, Range E, i
       FCk = FCk + Kern * (0.5 * (du * du + dv * dv) / hh - 0.5 * hh * (Ri_inv * bk + kC_Ek * ff * ff));
       FC[k] = FCk;
     }
-    // vtsq(k, zrk) on the prefetched sw(k), sw(k-1), bvf(k-1)
-    double vt;
-    {
-      const double swdk_r = sqrt(cur.sw * cur.swm);
-      const double zscale = zwN - zrk;
-      const double Bfsfc = Bo + Bosol * (1. - swdk_r);
-      const double ws = wscale_ws(zscale, Bfsfc, hbl0, ustar, rm, vonKar);
-      vt = 1.8 * kc.Vtc * ws * sqrt(dmax(1.e-5, cur.bvm));
-    }
-    const double Cr = FCk + vt;
+    const double Cr = FCk + vtsq(k, zrk);
     if (kbls == 0 && Cr < 0.) {
       kbls = k;
       cr_k = Cr; cr_kp = Crp; zr_k = zrk; zr_kp = zrp;
     }
     Crp = Cr;
     u0p = u0; u1p = u1; v0p = v0; v1p = v1; hzp = hz; zrp = zrk;
-    if (ROMS_KPP_EXT_PF) cur = nx;
   }
   // FC(0) (lmd_kpp.F:216-229): level-1 values are the carried ones
   {

@@ -930,22 +930,25 @@ __global__ void __launch_bounds__(256, KL > 13 ? 3 : 4) k_uv2_fused(Dev d, Range
     const int ic = min(max(i, ilo), b.iend), jc = min(max(j, jlo), b.jend);
     const bool act = ic == i && jc == j && cl.in && uv2_fused_in(b, dir, i, j);
     const long ij = IJ(b, ic, jc), s = dir == 0 ? 1 : b.nx2;
-    double* __restrict__ Un = (dir == 0 ? F.u : F.v) + (long)(nnew - 1) * b.n3 + ij;
-    const double* __restrict__ Us = (dir == 0 ? F.u : F.v) + (long)(nstp - 1) * b.n3 + ij;
-    double* __restrict__ Flx = (dir == 0 ? F.FlxU : F.FlxV) + ij;
-    const double* __restrict__ Hz = F.Hz + ij;
     const double dn = dir == 0 ? F.dn_u[ij] : F.dm_v[ij];
     const double avg1 = dir == 0 ? F.DU_avg1[ij] : F.DV_avg1[ij];
     const double avg2 = dir == 0 ? F.DU_avg2[ij] : F.DV_avg2[ij];
     const double msk = dir == 0 ? F.umask[ij] : F.vmask[ij];
-    // FULL: the level loops' memory operations as raw-buffer accesses, the
-    // lane's column offset in a VGPR and the level's in an SGPR
+    // The level loops' memory operations are raw-buffer accesses: the lane's
+    // column offset in a VGPR, the level's in an SGPR (no 64-bit address per
+    // level held in registers across the passes; they spilled ~200 VGPRs).
+    // A level the lane does not own (q >= nk: past N in the top segment)
+    // and every store of an inactive lane take the offset kBufOff, outside
+    // the extent: the load returns 0 and the store is dropped -- straight-line
+    // level loops without branches.  The sums skip those levels by selects.
     const double* const Ub = (dir == 0 ? F.u : F.v);
     const BufF64 bUn(Ub + (long)(nnew - 1) * b.n3, b.n3), bUs(Ub + (long)(nstp - 1) * b.n3, b.n3), bHz(F.Hz, b.n3),
         bFl(dir == 0 ? F.FlxU : F.FlxV, b.n3);
     const unsigned vo = (unsigned)((ij + (long)(lo - 1) * n2) * 8), vom = vo - (unsigned)(s * 8);
-    const unsigned vst = act ? vo : kBufOff;   // inactive lanes' stores fall outside the extent (dropped)
     auto so = [&](int q) { return (unsigned)((long)q * n2 * 8); };
+    auto vq = [&](int q) { return q < nk ? vo : kBufOff; };              // loads of level lo+q
+    auto vqm = [&](int q) { return q < nk ? vom : kBufOff; };            // ... of its (i-1) / (j-1) neighbour
+    auto vsq = [&](int q) { return act && q < nk ? vo : kBufOff; };      // stores
     double un[KL];
     double hcr[kHcLds ? 1 : KL];
     struct HcRef {   // hc[q]: Hz_u of the lane's level lo+q, in LDS (kHcLds) or registers
@@ -955,36 +958,32 @@ __global__ void __launch_bounds__(256, KL > 13 ? 3 : 4) k_uv2_fused(Dev d, Range
     } const hc{sHc + threadIdx.x, hcr};
 #pragma unroll
     for (int q = 0; q < KL; q++) {
-      if (q < nk) {
-        if (FULL) {
-          un[q] = bUn.ld(vo, so(q));
-          hc[q] = 0.5 * (bHz.ld(vo, so(q)) + bHz.ld(vom, so(q)));
-        } else {
-          const long o = (long)(lo + q - 1) * n2;
-          un[q] = Un[o];
-          hc[q] = 0.5 * (Hz[o] + Hz[o - s]);
-        }
-      }
-      // FULL: the loads of 8 levels in flight at a time (all 25 hoisted spilled)
-      if (FULL && q % 8 == 7) __builtin_amdgcn_sched_barrier(0);
+      un[q] = bUn.ld(vq(q), so(q));
+      hc[q] = 0.5 * (bHz.ld(vq(q), so(q)) + bHz.ld(vqm(q), so(q)));
+      // the loads of 8 levels in flight at a time (all 25 hoisted spilled)
+      if (q % 8 == 7) __builtin_amdgcn_sched_barrier(0);
     }
     // k_uv2_couple: CF0 = sum Hz_u, DC0 = sum Hz*u (k = N..1); u = Hz*u/Hz_u
     double CF0, DC0;
     chain2(CF0, DC0, [&](double& a, double& c) {
 #pragma unroll
-      for (int q = KL - 1; q >= 0; q--)
-        if (q < nk) { a = a + hc[q]; c = c + un[q]; }
+      for (int q = KL - 1; q >= 0; q--) {
+        a = q < nk ? a + hc[q] : a;
+        c = q < nk ? c + un[q] : c;
+      }
     });
     DC0 = (DC0 * dn - avg1) / (CF0 * dn);
 #pragma unroll
-    for (int q = 0; q < KL; q++)
-      if (q < nk) un[q] = (un[q] / hc[q] - DC0) * msk;
+    for (int q = 0; q < KL; q++) un[q] = (un[q] / hc[q] - DC0) * msk;   // (dead levels: never used)
     // k_uv2_flux: D = sum Hz_u*dn, FC = sum Hz_u*dn*u (k = N..1)
     double DS, FC0;
     chain2(DS, FC0, [&](double& a, double& c) {
 #pragma unroll
-      for (int q = KL - 1; q >= 0; q--)
-        if (q < nk) { const double dck = hc[q] * dn; a = a + dck; c = c + dck * un[q]; }
+      for (int q = KL - 1; q >= 0; q--) {
+        const double dck = hc[q] * dn;
+        a = q < nk ? a + dck : a;
+        c = q < nk ? c + dck * un[q] : c;
+      }
     });
     const double DCi = 1.0 / DS;
     if (act && g == 0) {
@@ -992,40 +991,24 @@ __global__ void __launch_bounds__(256, KL > 13 ? 3 : 4) k_uv2_fused(Dev d, Range
       else F.vbar[IJL(b, i, j, knew)] = DCi * avg1;
     }
     FC0 = DCi * (FC0 - avg1);
-    // corrected u and the fluxes; un[] becomes the flux cfk (FULL: the
-    // straight-line level loop's loads of u(nstp) and Flx stay here, not
-    // hoisted above the chains, where they spilled)
-    if (FULL) __builtin_amdgcn_sched_barrier(0);
+    // corrected u and the fluxes; un[] becomes the flux cfk (the level loop's
+    // loads of u(nstp) and Flx stay here, not hoisted above the chains)
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int q = 0; q < KL; q++) {
-      if (q < nk) {
-        const double u1 = (un[q] - FC0) * msk;
-        if (FULL) {
-          bUn.st(u1, vst, so(q));
-          un[q] = DELTA * bFl.ld(vo, so(q)) + EPSIL * (hc[q] * dn) * (bUs.ld(vo, so(q)) + u1);
-        } else {
-          const long o = (long)(lo + q - 1) * n2;
-          if (act) Un[o] = u1;
-          un[q] = DELTA * Flx[o] + EPSIL * (hc[q] * dn) * (Us[o] + u1);
-        }
-      }
-      if (FULL && q % 8 == 7) __builtin_amdgcn_sched_barrier(0);
+      const double u1 = (un[q] - FC0) * msk;
+      bUn.st(u1, vsq(q), so(q));
+      un[q] = DELTA * bFl.ld(vq(q), so(q)) + EPSIL * (hc[q] * dn) * (bUs.ld(vq(q), so(q)) + u1);
+      if (q % 8 == 7) __builtin_amdgcn_sched_barrier(0);
     }
     double CS, unused;
     chain2(CS, unused, [&](double& a, double& c) {
 #pragma unroll
-      for (int q = KL - 1; q >= 0; q--)
-        if (q < nk) a = a + un[q];
+      for (int q = KL - 1; q >= 0; q--) a = q < nk ? a + un[q] : a;
     });
     const double CF1 = DCi * (CS - avg2);
-    if (FULL) {
 #pragma unroll
-      for (int q = 0; q < KL; q++) bFl.st(un[q] - (hc[q] * dn) * CF1, vst, so(q));
-    } else if (act) {
-#pragma unroll
-      for (int q = 0; q < KL; q++)
-        if (q < nk) Flx[(long)(lo + q - 1) * n2] = un[q] - (hc[q] * dn) * CF1;
-    }
+    for (int q = 0; q < KL; q++) bFl.st(un[q] - (hc[q] * dn) * CF1, vsq(q), so(q));
   }
 }
 
