@@ -27,7 +27,7 @@ PY
 wargs() { if [ "$1" = c3 ]; then echo "--workload c3 --steps 5 --warmup 2 --timing-steps 2"; else echo "--workload c2 --steps 20 --warmup 3 --timing-steps 3 --no-secondary"; fi; }
 case $CMD in
 suite)
-  timeout -k 10 1500 $PYT tests -m gpu -x > $O/tests_$TAG.log 2>&1 || { echo TESTFAIL; tail -30 $O/tests_$TAG.log; exit 1; }
+  timeout -k 10 1500 $PYT -v -rf tests -m gpu -x > $O/tests_$TAG.log 2>&1 || { echo TESTFAIL; tail -30 $O/tests_$TAG.log; exit 1; }
   tail -1 $O/tests_$TAG.log
   timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke_$TAG.log 2>&1 || { echo SMOKEFAIL; tail -20 $O/smoke_$TAG.log; exit 1; }
   tail -1 $O/smoke_$TAG.log
