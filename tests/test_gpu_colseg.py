@@ -161,3 +161,44 @@ def test_seg_variants_bitwise(case, switch, monkeypatch):
         m.close()
     for n in out[0]:
         assert np.array_equal(out[0][n], out[1][n]), n
+
+
+@pytest.mark.parametrize("lmd", [0, oracle.LMD_ALL])
+def test_seg_buffer_forms_bitwise(lmd, monkeypatch):
+    """Segment solvers with buffer loads (ROMS_GPU_SEG_BUF bits: 1
+    k_pre_tracer_segb, 2 k_step3d_t_segb -- wave-uniform level offsets in
+    SGPRs, the lane's column in one VGPR --, 4 / 16 their diffusion r.h.s.
+    prefetched with the spline inputs, 8 step3d_t reloading Hz for its
+    diffusion rows) keep the expressions and their order: 6 steps at
+    N = 100, with and without KPP, equal the pointer forms bitwise."""
+    cfg = seg_cfg("n100")
+    cfg.lmd, cfg.surf_flux = lmd, int(lmd != 0)
+    out = []
+    for env in ("0", "3", "23", "11"):
+        monkeypatch.setenv("ROMS_GPU_SEG_BUF", env)
+        m = make_model(cfg, 1)
+        m.step(6)
+        out.append({n: m.get(n) for n in ("zeta", "ubar", "vbar", "u", "v", "t", "rufrc", "rvfrc")})
+        m.close()
+    for o in out[1:]:
+        for n in out[0]:
+            assert np.array_equal(out[0][n], o[n]), n
+
+
+@pytest.mark.parametrize("chunk", ["5", "16"])
+def test_tracer_strip_chunks_bitwise(chunk, monkeypatch):
+    """ROMS_GPU_TCHUNK: the tracer horizontal kernels and segment solvers of
+    pre_step3d and step3d_t alternate over strips of rows (the first strip
+    of the predictor also forms the ring j = jstr-1); 6 steps at N = 100 with
+    KPP equal the whole-range launches bitwise."""
+    cfg = seg_cfg("n100")
+    cfg.lmd, cfg.surf_flux = oracle.LMD_ALL, 1
+    out = []
+    for env in ("0", chunk):
+        monkeypatch.setenv("ROMS_GPU_TCHUNK", env)
+        m = make_model(cfg, 1)
+        m.step(6)
+        out.append({n: m.get(n) for n in ("zeta", "ubar", "vbar", "u", "v", "t", "rufrc", "rvfrc")})
+        m.close()
+    for n in out[0]:
+        assert np.array_equal(out[0][n], out[1][n]), n

@@ -52,6 +52,16 @@ __device__ __forceinline__ SegSpan seg_span(int N) {
   r.n = base + (r.s < rem ? 1 : 0);
   return r;
 }
+// With one segment per wavefront (kSegCW = 64) the segment index, first cell
+// and row count are wave-uniform: readfirstlane tells the compiler so, and
+// the level offsets derived from them live in SGPRs (buffer-load soffsets).
+__device__ __forceinline__ void seg_uniform(SegSpan& r) {
+  if constexpr (kSegCW == kCX) {
+    r.s = __builtin_amdgcn_readfirstlane(r.s);
+    r.c0 = __builtin_amdgcn_readfirstlane(r.c0);
+    r.n = __builtin_amdgcn_readfirstlane(r.n);
+  }
+}
 // wavefronts per block for N levels: S = ceil(N / kSegRows) rounded up to whole wavefronts
 inline int seg_waves(int N) {
   const int per = kCX / kSegCW;
@@ -93,7 +103,6 @@ __device__ __forceinline__ uint3 seg_tile(int ord, int xg = 4) {
 // LDS exchange area of one block: 6 end-relation values per (segment, column)
 struct SegXchg {
   double v[6][kSegMaxS][kSegCW * kSegJMax];
-  double uv[kSegMaxS > 8 ? 2 : 1][kSegMaxS][kSegCW * kSegJMax];   // U_t, V_t of the reduced system (kSegMaxS > 8)
 };
 
 // Every per-row loop below is straight-line code over all KR rows: rows
@@ -121,13 +130,17 @@ __device__ __forceinline__ void pin(double& x) { __asm__ volatile("" : "+v"(x));
 #define ROMS_SEG_LOAD_GROUP 5
 #endif
 constexpr int kSegLoadGroup = ROMS_SEG_LOAD_GROUP;
+#ifndef ROMS_SEG_COUPLE_GROUP
+#define ROMS_SEG_COUPLE_GROUP 8
+#endif
+constexpr int kSegCoupleGroup = ROMS_SEG_COUPLE_GROUP;
 
 template <int KR>
 struct SegTri {
   double C[KR], D[KR], E[KR];
   // forward elimination of rows q = 0..n-1; row(q, a, b, c, d): a x_{q-1} + b x_q + c x_{q+1} = d
   // (row() is called for every q < KR and must be free of side effects)
-  template <class RowF>
+  template <int G = kSegLoadGroup, class RowF>
   __device__ __forceinline__ void eliminate(int n, RowF row) {
     double Cp = 0.0, Dp = 0.0, Ep = 1.0;  // x_{-1} = x_L
 #pragma unroll
@@ -142,7 +155,7 @@ struct SegTri {
       E[q] = live ? Eq : 0.0;
       Cp = C[q]; Dp = D[q]; Ep = E[q];
       // rows' loads run at most a group ahead of the elimination (register pressure)
-      if (q % kSegLoadGroup == kSegLoadGroup - 1) __builtin_amdgcn_sched_barrier(0);
+      if (q % G == G - 1) __builtin_amdgcn_sched_barrier(0);
     }
   }
   // publish the first/last-row relations, barrier, reduced solve -> x_L, x_R
@@ -164,13 +177,12 @@ struct SegTri {
     X.v[3][s][l] = yl; X.v[4][s][l] = all; X.v[5][s][l] = bel;
     __syncthreads();
     // F_t = U_t + V_t F_{t+1} (first values), L_t = P_t + Q_t F_{t+1} (last
-    // values).  Every lane of a column runs the same forward recurrence.  Up
-    // to 8 segments U_t, V_t stay in registers; with more, the lane of
-    // segment t leaves them in LDS (S-long register arrays in every lane
-    // would cost 4 S VGPRs) and the backward recurrence reads them back.
-    constexpr bool kUVLds = kSegMaxS > 8;
-    double U[kUVLds ? 1 : kSegMaxS], V[kUVLds ? 1 : kSegMaxS];
-    double Pp = 0.0, Qp = 0.0, Ps = 0.0, Qs = 0.0;
+    // values), F_S = 0.  Every lane of a column runs the same forward
+    // recurrence; the segment's own (U_s, V_s) and the composition of the
+    // maps of the segments above it, F_{s+1} = ga + gb F_{t+1}, are carried
+    // as running values, so F_{s+1} = ga at the end and no S-long arrays of
+    // U_t, V_t are live at the register peak (32 VGPRs at S = 8).
+    double Pp = 0.0, Qp = 0.0, Ps = 0.0, Qs = 0.0, Us = 0.0, Vs = 0.0, ga = 0.0, gb = 1.0;
 #pragma unroll
     for (int t = 0; t < kSegMaxS; t++) {
       if (t < S) {
@@ -179,30 +191,22 @@ struct SegTri {
         const double rden = 1.0 / (1.0 - af * Qp);
         const double Ut = (yf + af * Pp) * rden;
         const double Vt = bf * rden;
-        if constexpr (kUVLds) {
-          if (t == s) { X.uv[0][t][l] = Ut; X.uv[1][t][l] = Vt; }
-        } else {
-          U[t] = Ut; V[t] = Vt;
-        }
+        Us = t == s ? Ut : Us;
+        Vs = t == s ? Vt : Vs;
+        const double gan = ga + gb * Ut, gbn = gb * Vt;
+        ga = t > s ? gan : ga;
+        gb = t > s ? gbn : gb;
         const double Pn = yL + aL * Pp + aL * Qp * Ut;
         Qp = aL * Qp * Vt + bL;
         Pp = Pn;
         Ps = t == s - 1 ? Pp : Ps;
         Qs = t == s - 1 ? Qp : Qs;
       }
+      // LDS reads of at most kSegCoupleGroup segments ahead (register peak)
+      if (t % kSegCoupleGroup == kSegCoupleGroup - 1) __builtin_amdgcn_sched_barrier(0);
     }
-    if constexpr (kUVLds) __syncthreads();
-    double Fn = 0.0;  // F_{t+1}
-    xL = 0.0; xR = 0.0;
-#pragma unroll
-    for (int t = kSegMaxS - 1; t >= 0; t--) {
-      if (t < S && (!kUVLds || t >= s - 1)) {
-        xR = t == s ? Fn : xR;
-        xL = t == s - 1 ? Ps + Qs * Fn : xL;
-        if constexpr (kUVLds) Fn = X.uv[0][t][l] + X.uv[1][t][l] * Fn;
-        else Fn = U[t] + V[t] * Fn;
-      }
-    }
+    xR = ga;                        // F_{s+1}
+    xL = Ps + Qs * (Us + Vs * ga);  // L_{s-1} from F_s
   }
   // back-substitution; x_q is left in D[q]
   __device__ __forceinline__ void solve(int n, double xL, double xR) {

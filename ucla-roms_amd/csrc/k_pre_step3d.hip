@@ -765,6 +765,100 @@ __global__ void __launch_bounds__(kSegBlock, 2) k_pre_tracer_seg(Dev d, Range R,
   }
 }
 
+// ---- k_pre_tracer_seg with buffer loads/stores (Params::seg_buf, see
+// k_step3d_t_segb): wave-uniform level offsets in SGPRs, the lane's column in
+// one VGPR.  PF: the diffusion phase's t(nnew) rows and Hz_fwd loaded at
+// entry with the spline inputs.  Same expressions and order: bitwise equal
+// to k_pre_tracer_seg. ----
+template <bool PF>
+__global__ void __launch_bounds__(kSegBlock, ROMS_SEG_BUF_WAVES) k_pre_tracer_segb(Dev d, Range R, PreCoef c, int nnew,
+                                                                                   int nrhs) {
+  const uint3 bI = seg_tile(d.p.seg_order, d.p.seg_xg);
+  __shared__ SegXchg X;
+  constexpr int KR = kSegRows + 1;
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const int N = b.N;
+  SegSpan sg = seg_span(N);
+  seg_uniform(sg);
+  const int iu = tile_i0(R.i0) + (int)bI.x * kSegCW + sg.col;
+  const bool act = iu >= R.i0 && iu <= R.i1;
+  const int i = act ? iu : (iu < R.i0 ? R.i0 : R.i1), j = R.j0 + (int)bI.y;
+  const int itrc = 1 + (int)bI.z;
+  const long n2 = b.n2, ij = IJ(b, i, j);
+  const int c0 = sg.c0, n = sg.n;
+  const unsigned vo = (unsigned)ij * 8u;
+  auto lev = [&](int k) { return (unsigned)(min(max(k, 1), N) - 1) * (unsigned)n2 * 8u; };
+  auto wlev = [&](int r) { return (unsigned)min(max(r, 1), N - 1) * (unsigned)n2 * 8u; };
+  const BufF64 Hz(F.Hz), Hf(F.c2), We(F.We), Wi(F.Wi);
+  const long tb = (long)(itrc - 1) * 3 * b.n3;
+  const BufF64 Tr(F.t + (long)(nrhs - 1) * b.n3 + tb), Tn(F.t + (long)(nnew - 1) * b.n3 + tb);
+  double hz[KR + 1], tt[KR], fl[KR], hf[KR + 1], tn[KR];
+#pragma unroll
+  for (int q = 0; q < KR + 1; q++) {
+    hz[q] = Hz.ld(vo, lev(c0 - 1 + q));
+    if (q < KR) tt[q] = Tr.ld(vo, lev(c0 - 1 + q));
+  }
+  if constexpr (PF) {
+#pragma unroll
+    for (int q = 0; q < KR + 1; q++) {
+      hf[q] = Hf.ld(vo, lev(c0 - 1 + q));
+      if (q < KR) tn[q] = Tn.ld(vo, lev(c0 + q));
+    }
+  }
+  spline_fc_seg<KR>(sg, N, X, hz, tt, fl);
+  {
+    double we[KR];
+#pragma unroll
+    for (int q = 0; q < KR; q++) we[q] = We.ld(vo, wlev(c0 - 1 + q));
+#pragma unroll
+    for (int q = 0; q < KR; q++) pin(we[q]);
+#pragma unroll
+    for (int q = 0; q < KR; q++) {
+      const int r = c0 - 1 + q;
+      fl[q] = (r == 0 || r == N) ? 0.0 : fl[q] * we[q];
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int q = 0; q < KR + 1; q++) hz[q] = PF ? hf[q] : Hf.ld(vo, lev(c0 - 1 + q));
+  const int iAkt = itrc < b.nTS ? itrc : b.nTS;
+  const BufF64 Akt(F.Akt + (long)(iAkt - 1) * b.n3w);
+  const BufF64 Pm(F.pm), Pn(F.pn);   // 2-D metrics through the lane's offset too (no 64-bit ij kept live)
+  const double pm = Pm.ld(vo, 0), pn = Pn.ld(vo, 0);
+  const double DC0 = c.dtau * pm * pn;
+  auto fcw = [&](int q, double& fc, double& wc) {
+    const int r = c0 - 1 + q;
+    const unsigned w = wlev(r);
+    const bool in = r > 0 && r < N;
+    const int qa = q + 1 < KR + 1 ? q + 1 : KR;
+    const double f = 2.0 * c.dtau * Akt.ld(vo, w) / (hz[qa] + hz[q]);
+    const double wv = DC0 * Wi.ld(vo, w);
+    fc = in ? f : 0.0;
+    wc = in ? wv : 0.0;
+  };
+  double fcl, wcl;
+  fcw(0, fcl, wcl);
+  __syncthreads();  // X reused by the second coupling
+  SegTri<KR> T;
+  T.eliminate(n, [&](int p, double& a, double& bb, double& cc, double& dd) {
+    double fcu, wcu;
+    fcw(p + 1, fcu, wcu);
+    a = -(fcl + fmax0(wcl));
+    bb = hz[p + 1] + fcu + fmax0(wcu) + fcl - fmin0(wcl);
+    cc = -(fcu - fmin0(wcu));
+    dd = (PF ? tn[p] : Tn.ld(vo, lev(c0 + p))) - c.dtau * pm * pn * (fl[p + 1 < KR ? p + 1 : KR - 1] - fl[p]);
+    fcl = fcu; wcl = wcu;
+  });
+  double xL, xR;
+  T.couple(sg, n, X, xL, xR);
+  T.solve(n, xL, xR);
+  const unsigned vs = act ? vo : kBufOff;
+#pragma unroll
+  for (int p = 0; p < KR; p++)
+    if (p < n) Tn.st(T.D[p], vs, lev(c0 + p));
+}
+
 // kLds (UV_ADV, nrhs == nstp -- always so in the predictor): the spline
 // phase, which loads Hz, Hz of the (i-1)/(j-1) neighbour and u(nrhs) = u(nstp)
 // of every row anyway, also loads u(indx) and leaves in dynamic LDS the row's
@@ -927,56 +1021,82 @@ void launch_pre_step3d(const Dev& d, hipStream_t s, const Tlev& t, bool uv_done,
   hb_done = hb_done && d.p.hoist && b.NT <= 2;
   Range RI{b.istr, b.iend, b.jstr, b.jend};
   Range RH{b.istr - 1, b.iend, b.jstr - 1, b.jend};
-  if (d.p.hoist && d.p.h_jc > 0 && (b.NT == 1 || b.NT == 2)) {
-    const dim3 g = grid3_jc(RH, b.N, d.p.h_jc), bs(kBX, kBY);
-    const int jc = d.p.h_jc;
-    if (b.NT == 2 && hb_done)
-      hipLaunchKernelGGL((k_pre_tracer_hj<2, true>), g, bs, 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs, jc);
-    else if (b.NT == 2)
-      hipLaunchKernelGGL((k_pre_tracer_hj<2, false>), g, bs, 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs, jc);
-    else if (hb_done)
-      hipLaunchKernelGGL((k_pre_tracer_hj<1, true>), g, bs, 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs, jc);
+  // horizontal part on rows rh (the ring i = istr-1, j = jstr-1 included)
+  auto horiz = [&](const Range& rh) {
+    if (d.p.hoist && d.p.h_jc > 0 && (b.NT == 1 || b.NT == 2)) {
+      const dim3 g = grid3_jc(rh, b.N, d.p.h_jc), bs(kBX, kBY);
+      const int jc = d.p.h_jc;
+      if (b.NT == 2 && hb_done)
+        hipLaunchKernelGGL((k_pre_tracer_hj<2, true>), g, bs, 0, s, d, rh, c, t.nstp, t.nnew, t.nrhs, jc);
+      else if (b.NT == 2)
+        hipLaunchKernelGGL((k_pre_tracer_hj<2, false>), g, bs, 0, s, d, rh, c, t.nstp, t.nnew, t.nrhs, jc);
+      else if (hb_done)
+        hipLaunchKernelGGL((k_pre_tracer_hj<1, true>), g, bs, 0, s, d, rh, c, t.nstp, t.nnew, t.nrhs, jc);
+      else
+        hipLaunchKernelGGL((k_pre_tracer_hj<1, false>), g, bs, 0, s, d, rh, c, t.nstp, t.nnew, t.nrhs, jc);
+    } else if (d.p.hoist && b.NT == 2 && d.p.h_ty == 8) {
+      if (hb_done)
+        hipLaunchKernelGGL((k_pre_tracer_h1<2, 8, true>), grid3_ty(rh, b.N, 8), dim3(kBX, 8), 0, s, d, rh, c, t.nstp, t.nnew, t.nrhs);
+      else
+        hipLaunchKernelGGL((k_pre_tracer_h1<2, 8, false>), grid3_ty(rh, b.N, 8), dim3(kBX, 8), 0, s, d, rh, c, t.nstp, t.nnew, t.nrhs);
+    } else if (d.p.hoist && b.NT == 2) {
+      if (hb_done)
+        hipLaunchKernelGGL((k_pre_tracer_h1<2, 4, true>), grid3_ty(rh, b.N, 4), dim3(kBX, 4), 0, s, d, rh, c, t.nstp, t.nnew, t.nrhs);
+      else
+        hipLaunchKernelGGL((k_pre_tracer_h1<2, 4, false>), grid3_ty(rh, b.N, 4), dim3(kBX, 4), 0, s, d, rh, c, t.nstp, t.nnew, t.nrhs);
+    } else if (d.p.hoist && b.NT == 1) {
+      if (hb_done)
+        hipLaunchKernelGGL((k_pre_tracer_h1<1, 4, true>), grid3_ty(rh, b.N, 4), dim3(kBX, 4), 0, s, d, rh, c, t.nstp, t.nnew, t.nrhs);
+      else
+        hipLaunchKernelGGL((k_pre_tracer_h1<1, 4, false>), grid3_ty(rh, b.N, 4), dim3(kBX, 4), 0, s, d, rh, c, t.nstp, t.nnew, t.nrhs);
+    } else {
+      hipLaunchKernelGGL(k_pre_tracer_h, grid3_of(rh, b.N), dim3(kBX, kBY), 0, s, d, rh, c, t.nstp, t.nnew, t.nrhs);
+    }
+  };
+  // column solves on rows ri
+  auto cols = [&](const Range& ri, hipStream_t st) {
+    dim3 gt = gridc_of(ri);
+    gt.z = b.NT;
+    if (d.p.colseg && (d.p.seg_buf & 1) && (d.p.seg_buf & 16))
+      hipLaunchKernelGGL(k_pre_tracer_segb<true>, seg_grid_of(ri, b.NT), dim3(kCX, seg_waves(b.N)), 0, st, d, ri, c,
+                         t.nnew, t.nrhs);
+    else if (d.p.colseg && (d.p.seg_buf & 1))
+      hipLaunchKernelGGL(k_pre_tracer_segb<false>, seg_grid_of(ri, b.NT), dim3(kCX, seg_waves(b.N)), 0, st, d, ri, c,
+                         t.nnew, t.nrhs);
+    else if (d.p.colseg)
+      hipLaunchKernelGGL(k_pre_tracer_seg, seg_grid_of(ri, b.NT), dim3(kCX, seg_waves(b.N)), 0, st, d, ri, c, t.nnew,
+                         t.nrhs);
+    else if ((d.p.colreg & 2) && b.N == 50 && !d.f.colscr)
+      hipLaunchKernelGGL(k_pre_tracer_v_reg<50>, gt, dim3(kCX), col_lds_bytes(1, 50), st, d, ri, c, t.nnew, t.nrhs);
+    else if (d.f.colscr)
+      hipLaunchKernelGGL(k_pre_tracer_v<ColGlb>, gt, dim3(kCX), 0, st, d, ri, c, t.nnew, t.nrhs);
     else
-      hipLaunchKernelGGL((k_pre_tracer_hj<1, false>), g, bs, 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs, jc);
-  } else if (d.p.hoist && b.NT == 2 && d.p.h_ty == 8) {
-    if (hb_done)
-      hipLaunchKernelGGL((k_pre_tracer_h1<2, 8, true>), grid3_ty(RH, b.N, 8), dim3(kBX, 8), 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs);
-    else
-      hipLaunchKernelGGL((k_pre_tracer_h1<2, 8, false>), grid3_ty(RH, b.N, 8), dim3(kBX, 8), 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs);
-  } else if (d.p.hoist && b.NT == 2) {
-    if (hb_done)
-      hipLaunchKernelGGL((k_pre_tracer_h1<2, 4, true>), grid3_ty(RH, b.N, 4), dim3(kBX, 4), 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs);
-    else
-      hipLaunchKernelGGL((k_pre_tracer_h1<2, 4, false>), grid3_ty(RH, b.N, 4), dim3(kBX, 4), 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs);
-  } else if (d.p.hoist && b.NT == 1) {
-    if (hb_done)
-      hipLaunchKernelGGL((k_pre_tracer_h1<1, 4, true>), grid3_ty(RH, b.N, 4), dim3(kBX, 4), 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs);
-    else
-      hipLaunchKernelGGL((k_pre_tracer_h1<1, 4, false>), grid3_ty(RH, b.N, 4), dim3(kBX, 4), 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs);
+      hipLaunchKernelGGL(k_pre_tracer_v<ColLds>, gt, dim3(kCX), col_lds_bytes(2, b.N), st, d, ri, c, t.nnew, t.nrhs);
+  };
+  // Params::t_chunk: horizontal part and column solves alternate over strips
+  // of t_chunk rows, so each strip's t(nnew) -- the horizontal result the
+  // solver reads back -- is still in the Infinity Cache when it is read
+  if (d.p.t_chunk > 0 && !side && d.p.colseg) {
+    for (int ja = b.jstr; ja <= b.jend; ja += d.p.t_chunk) {
+      const int jb = min(ja + d.p.t_chunk - 1, b.jend);
+      horiz(Range{b.istr - 1, b.iend, ja == b.jstr ? b.jstr - 1 : ja, jb});
+      cols(Range{b.istr, b.iend, ja, jb}, s);
+    }
   } else {
-    hipLaunchKernelGGL(k_pre_tracer_h, grid3_of(RH, b.N), dim3(kBX, kBY), 0, s, d, RH, c, t.nstp, t.nnew, t.nrhs);
+    horiz(RH);
+    // The tracer column solves (t(nnew), reading Hz_fwd) and the momentum ones
+    // (u, v(nnew), u, v(indx), reading Hz_fwd/bak, ru, rv) share no output:
+    // with a side stream they run side by side once the horizontal tracer
+    // kernel has formed the ring of Hz_fwd/bak both read
+    hipStream_t st = s;
+    if (side) {
+      (void)hipEventRecord(side->efork, s);
+      (void)hipStreamWaitEvent(side->s2, side->efork, 0);
+      st = side->s2;
+    }
+    cols(RI, st);
   }
-  // The tracer column solves (t(nnew), reading Hz_fwd) and the momentum ones
-  // (u, v(nnew), u, v(indx), reading Hz_fwd/bak, ru, rv) share no output:
-  // with a side stream they run side by side once the horizontal tracer
-  // kernel has formed the ring of Hz_fwd/bak both read
-  hipStream_t st = s;
-  if (side) {
-    (void)hipEventRecord(side->efork, s);
-    (void)hipStreamWaitEvent(side->s2, side->efork, 0);
-    st = side->s2;
-  }
-  dim3 gt = gridc_of(RI);
-  gt.z = b.NT;
-  if (d.p.colseg)
-    hipLaunchKernelGGL(k_pre_tracer_seg, seg_grid_of(RI, b.NT), dim3(kCX, seg_waves(b.N)), 0, st, d, RI, c, t.nnew,
-                       t.nrhs);
-  else if ((d.p.colreg & 2) && b.N == 50 && !d.f.colscr)
-    hipLaunchKernelGGL(k_pre_tracer_v_reg<50>, gt, dim3(kCX), col_lds_bytes(1, 50), st, d, RI, c, t.nnew, t.nrhs);
-  else if (d.f.colscr)
-    hipLaunchKernelGGL(k_pre_tracer_v<ColGlb>, gt, dim3(kCX), 0, st, d, RI, c, t.nnew, t.nrhs);
-  else
-    hipLaunchKernelGGL(k_pre_tracer_v<ColLds>, gt, dim3(kCX), col_lds_bytes(2, b.N), st, d, RI, c, t.nnew, t.nrhs);
+  hipStream_t st = side ? side->s2 : s;
   for (int itrc = 1; itrc <= b.NT && side; itrc++) launch_t3dbc(d, st, t, itrc);
   if (side) launch_exchange_tracers(d, st, t.nnew);
   if (!uv_done) launch_uv_horiz(d, s, t.nrhs, 0);

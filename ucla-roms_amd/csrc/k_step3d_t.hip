@@ -367,6 +367,167 @@ __global__ void __launch_bounds__(kSegBlock, 2) k_step3d_t_seg(Dev d, Range R, i
   }
 }
 
+// ---- k_step3d_t_seg with buffer loads/stores (Params::seg_buf): a wave is
+// one segment, so its first cell c0 and row count n are wave-uniform
+// (readfirstlane); every level offset is then one SGPR shared by all fields
+// (soffset), the lane's column one VGPR (voffset), and no load carries a
+// 64-bit per-row address.  Same expressions in the same order: bitwise equal
+// to k_step3d_t_seg. ----
+#ifndef ROMS_SEG_T_GROUP
+#define ROMS_SEG_T_GROUP kSegLoadGroup
+#endif
+// PF: t(nnew) of the segment's rows (the diffusion r.h.s.) loaded at entry
+// with the spline phase's inputs, so they land during its solve.  RL: Hz
+// reloaded for the diffusion phase instead of kept live across the spline
+// solve (30 VGPRs at its register peak).
+template <bool PF, bool RL = false>
+__global__ void __launch_bounds__(kSegBlock, ROMS_SEG_BUF_WAVES) k_step3d_t_segb(Dev d, Range R, int nnew, int nrhs) {
+  const uint3 bI = seg_tile(d.p.seg_order, d.p.seg_xg);
+  __shared__ SegXchg X;
+  constexpr int KR = kSegRows + 1;
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const Params& P = d.p;
+  const int N = b.N;
+  const double dt = P.dt;
+  SegSpan sg = seg_span(N);
+  seg_uniform(sg);
+  const int iu = tile_i0(R.i0) + (int)bI.x * kSegCW + sg.col;
+  const bool act = iu >= R.i0 && iu <= R.i1;
+  const int i = act ? iu : (iu < R.i0 ? R.i0 : R.i1), j = R.j0 + (int)bI.y;
+  const int itrc = 1 + (int)bI.z;
+  const long n2 = b.n2, ij = IJ(b, i, j);
+  const int c0 = sg.c0, n = sg.n;
+  const bool last = sg.s == sg.S - 1;
+  const unsigned vo = (unsigned)ij * 8u;
+  // byte offset of rho level k (clamped to 1..N) / w level r (clamped to lo..hi)
+  auto lev = [&](int k) { return (unsigned)(min(max(k, 1), N) - 1) * (unsigned)n2 * 8u; };
+  auto wlev = [&](int r, int lo, int hi) { return (unsigned)min(max(r, lo), hi) * (unsigned)n2 * 8u; };
+  const BufF64 Hz(F.Hz), We(F.We), Wi(F.Wi);
+  const BufF64 Tr(F.t + (long)(nrhs - 1) * b.n3 + (long)(itrc - 1) * 3 * b.n3);
+  const BufF64 Tn(F.t + (long)(nnew - 1) * b.n3 + (long)(itrc - 1) * 3 * b.n3);
+  double hz[KR + 1], tt[KR], tn[KR];
+#pragma unroll
+  for (int q = 0; q < KR + 1; q++) {
+    hz[q] = Hz.ld(vo, lev(c0 - 1 + q));
+    if (q < KR) tt[q] = Tr.ld(vo, lev(c0 - 1 + q));
+  }
+  if constexpr (PF) {
+#pragma unroll
+    for (int p = 0; p < KR; p++) tn[p] = Tn.ld(vo, lev(c0 + p));
+  }
+  {
+    double fc[KR];
+    spline_fc_seg<KR>(sg, N, X, hz, tt, fc);
+    double we[KR];
+#pragma unroll
+    for (int q = 0; q < KR; q++) we[q] = We.ld(vo, wlev(c0 - 1 + q, 1, N - 1));
+#pragma unroll
+    for (int q = 0; q < KR; q++) pin(we[q]);
+#pragma unroll
+    for (int q = 0; q < KR; q++) {
+      const int r = c0 - 1 + q;
+      tt[q] = (r == 0 || r == N) ? 0.0 : fc[q] * we[q];
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  if constexpr (RL) {
+#pragma unroll
+    for (int q = 0; q < KR + 1; q++) hz[q] = Hz.ld(vo, lev(c0 - 1 + q));
+  }
+  const int iAkt = itrc < b.nTS ? itrc : b.nTS;
+  const BufF64 Akt(F.Akt + (long)(iAkt - 1) * b.n3w);
+  const BufF64 Pm(F.pm), Pn(F.pn);
+  const double pm = Pm.ld(vo, 0), pn = Pn.ld(vo, 0);
+  const double DC0 = dt * pm * pn;
+  const bool kppT = P.lmd && itrc == 1, kppS = P.lmd_nonlocal && itrc == 2 && P.salinity;
+  const double sr = BufF64(F.srflx).ld(vo, 0);
+  const double stf = BufF64(F.stflx).ld(vo, (unsigned)(itrc - 1) * (unsigned)n2 * 8u);
+  // right-hand sides (step3d_t_ISO.F:922-1040): flux divergence, pipes, rain
+  // heat, surface flux, KPP solar / non-local terms, in the reference's order;
+  // every row's loads issued before the elimination
+  double rhs[KR];
+#pragma unroll
+  for (int p = 0; p < KR; p++)
+    rhs[p] = (PF ? tn[p] : Tn.ld(vo, lev(c0 + p))) - dt * pm * pn * (tt[p + 1 < KR ? p + 1 : KR - 1] - tt[p]);
+  if (P.npip > 0) {   // pipe_frc.F sources (step3d_t_ISO.F:927-934)
+    const int pidx = F.pipe_idx[ij];
+    if (pidx > 0) {
+      const double pflx = F.pipe_flx[ij], ptrc = F.pipe_trc[(pidx - 1) + (itrc - 1) * P.npip];
+#pragma unroll
+      for (int p = 0; p < KR; p++) {
+        const int k = min(c0 + p, N);
+        rhs[p] = rhs[p] + dt * pm * pn * pflx * F.pipe_prf[(pidx - 1) + (k - 1) * P.npip] * ptrc;
+      }
+    }
+  }
+  if (last) {   // the surface cell k = N, row n-1 of the last segment (wave-uniform)
+    double t = 0.0;
+#pragma unroll
+    for (int p = 0; p < KR; p++) t = p == n - 1 ? rhs[p] : t;
+    if (itrc == 1) {
+      const double swf = BufF64(F.swflx).ld(vo, 0);
+      t = t + dt * swf * (P.bulk_frc ? BufF64(F.tair).ld(vo, 0) : t / Hz.ld(vo, lev(N)));
+    }
+    t = t + dt * stf;
+#pragma unroll
+    for (int p = 0; p < KR; p++) rhs[p] = p == n - 1 ? t : rhs[p];
+  }
+  if (kppT || kppS) {
+    // the KPP term of w level m is added to the cell below it (k = m, m <=
+    // N-1) and subtracted from the cell above (k = m+1, m >= 1): one load
+    // per level, each row's upper term its next row's lower one
+    const BufF64 Sw(F.swr_frac), Gh(F.ghat);
+    const bool nl = P.lmd_nonlocal;
+    auto term = [&](int m) {
+      const unsigned o = wlev(m, 1, N - 1);
+      return kppT ? dt * (sr * Sw.ld(vo, o) - (nl ? Gh.ld(vo, o) : 0.0) * (stf - sr)) : -dt * Gh.ld(vo, o) * stf;
+    };
+    double lo = term(c0 - 1);
+#pragma unroll
+    for (int p = 0; p < KR; p++) {
+      const int k = min(c0 + p, N);
+      const double up = term(c0 + p);
+      double t = rhs[p];
+      t = k <= N - 1 ? t + up : t;
+      t = k >= 2 ? t - lo : t;
+      rhs[p] = t;
+      lo = up;
+    }
+  }
+  auto fcw = [&](int q, double& fc, double& wc) {   // interface c0-1+q
+    const int r = c0 - 1 + q;
+    const unsigned w = wlev(r, 1, N - 1);
+    const bool in = r > 0 && r < N;
+    const int qa = q + 1 < KR + 1 ? q + 1 : KR;
+    const double f = 2.0 * dt * Akt.ld(vo, w) / (hz[q] + hz[qa]);
+    const double c = DC0 * Wi.ld(vo, w);
+    fc = in ? f : 0.0;
+    wc = in ? c : 0.0;
+  };
+  double fcl, wcl;
+  fcw(0, fcl, wcl);
+  __syncthreads();  // X reused by the second coupling
+  SegTri<KR> T;
+  T.template eliminate<ROMS_SEG_T_GROUP>(n, [&](int p, double& a, double& bb, double& c, double& dd) {
+    double fcu, wcu;
+    fcw(p + 1, fcu, wcu);
+    a = -(fcl + fmax0(wcl));
+    bb = hz[p + 1] + fcu + fmax0(wcu) + fcl - fmin0(wcl);
+    c = -(fcu - fmin0(wcu));
+    dd = rhs[p];
+    fcl = fcu; wcl = wcu;
+  });
+  double xL, xR;
+  T.couple(sg, n, X, xL, xR);
+  T.solve(n, xL, xR);
+  const double rm = BufF64(F.rmask).ld(vo, 0);
+  const unsigned vs = act ? vo : kBufOff;
+#pragma unroll
+  for (int p = 0; p < KR; p++)
+    if (p < n) Tn.st(T.D[p] * rm, vs, lev(c0 + p));
+}
+
 void setup_column_kernels_t(size_t bytes) {
   (void)hipFuncSetAttribute((const void*)k_step3d_t_v<ColLds>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)bytes);
@@ -407,7 +568,15 @@ void launch_step3d_t(const Dev& d, hipStream_t s, const Tlev& t, bool exchange) 
     gt.z = b.NT;
     if (d.p.colseg) {
       ktimer_mark(s, kTimedStep3dTSeg, 0);
-      hipLaunchKernelGGL(k_step3d_t_seg, seg_grid_of(r, b.NT), dim3(kCX, seg_waves(b.N)), 0, s, d, r, t.nnew, t.nrhs);
+      if ((d.p.seg_buf & 2) && (d.p.seg_buf & 8))
+        hipLaunchKernelGGL((k_step3d_t_segb<false, true>), seg_grid_of(r, b.NT), dim3(kCX, seg_waves(b.N)), 0, s, d, r,
+                           t.nnew, t.nrhs);
+      else if ((d.p.seg_buf & 2) && (d.p.seg_buf & 4))
+        hipLaunchKernelGGL(k_step3d_t_segb<true>, seg_grid_of(r, b.NT), dim3(kCX, seg_waves(b.N)), 0, s, d, r, t.nnew, t.nrhs);
+      else if (d.p.seg_buf & 2)
+        hipLaunchKernelGGL(k_step3d_t_segb<false>, seg_grid_of(r, b.NT), dim3(kCX, seg_waves(b.N)), 0, s, d, r, t.nnew, t.nrhs);
+      else
+        hipLaunchKernelGGL(k_step3d_t_seg, seg_grid_of(r, b.NT), dim3(kCX, seg_waves(b.N)), 0, s, d, r, t.nnew, t.nrhs);
       ktimer_mark(s, kTimedStep3dTSeg, 1, 1);
     }
     else if (d.f.colscr)
@@ -418,14 +587,23 @@ void launch_step3d_t(const Dev& d, hipStream_t s, const Tlev& t, bool exchange) 
   auto edges = [&] {
     for (int itrc = 1; itrc <= b.NT; itrc++) launch_t3dbc(d, s, t, itrc);
   };
+  // Params::t_chunk: the horizontal part and the column solve alternate over
+  // strips of t_chunk rows (see launch_pre_step3d)
+  auto run_all = [&] {
+    if (d.p.t_chunk > 0 && d.p.colseg) {
+      for (int ja = R.j0; ja <= R.j1; ja += d.p.t_chunk) run(Range{R.i0, R.i1, ja, min(ja + d.p.t_chunk - 1, R.j1)});
+    } else {
+      run(R);
+    }
+  };
   ExchList L;
   if (!exchange) {   // t3dmix follows and exchanges t(nnew) itself
-    run(R);
+    run_all();
     edges();
   } else if (tracer_exch_list(d, t.nnew, L)) {
     launch_rim_first(d, s, R, L, run, edges);
   } else {
-    run(R);
+    run_all();
     edges();
     launch_exchange_tracers(d, s, t.nnew);
   }

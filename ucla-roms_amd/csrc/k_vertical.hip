@@ -412,28 +412,29 @@ __global__ void __launch_bounds__(kSegBlock, 2) k_omega_seg(Dev d, Range R, doub
   const int N = b.N;
   const double cu_min = 0.6, cu_max = 1.0, cmnx_ratio = cu_min / cu_max, cutoff = 2.0 - cmnx_ratio,
                r4cmx = 0.25 / (1.0 - cmnx_ratio);
-  const SegSpan sg = seg_span(N);
+  SegSpan sg = seg_span(N);
+  seg_uniform(sg);   // level offsets in SGPRs
   const int s = sg.s, S = sg.S, c0 = sg.c0, n = sg.n, l = sg.col;
   const int iu = tile_i0(R.i0) + (int)bI.x * kSegCW + l, ju = R.j0 + (int)bI.y;
   const bool act = iu >= R.i0 && iu <= R.i1 && ju <= R.j1;
   const int i = iu < R.i0 ? R.i0 : (iu < R.i1 ? iu : R.i1), j = ju < R.j1 ? ju : R.j1;
   const long ij = IJ(b, i, j), n2 = b.n2, sj = b.nx2;
-  const double* __restrict__ FU = F.FlxU + ij;
-  const double* __restrict__ FV = F.FlxV + ij;
-  const double* __restrict__ Hz = F.Hz + ij;
-  const double* __restrict__ zw = F.z_w + ij;
+  // buffer loads: the lane's column (and its i+1 / j+1 neighbour) in a VGPR,
+  // the level in an SGPR (no 64-bit address per level)
+  const unsigned vo = (unsigned)ij * 8u, lv = (unsigned)n2 * 8u;
+  const BufF64 FU(F.FlxU), FV(F.FlxV), Hz(F.Hz), zw(F.z_w);
   __shared__ double Lw[kSegMaxS][kSegCW], Lcx[kSegMaxS][kSegCW], Lhz[kSegMaxS][kSegCW];
   __shared__ double Lte[kHB ? kSegMaxS : 1][kSegCW], Lti[kHB ? kSegMaxS : 1][kSegCW];   // kHB: segment tops' We, Wi
   double fu1[kOmR], fu0[kOmR], fv1[kOmR], fv0[kOmR], cx[kOmR], hz[kOmR], zk[kOmR];
 #pragma unroll
   for (int q = 0; q < kOmR; q++) {   // rho level k = c0+q (clamped), w-level k
     const int k = min(c0 + q, N);
-    const long o = (long)(k - 1) * n2;
-    fu1[q] = FU[o + 1]; fu0[q] = FU[o]; fv1[q] = FV[o + sj]; fv0[q] = FV[o];
-    hz[q] = Hz[o];
-    zk[q] = zw[(long)k * n2];
+    const unsigned o = (unsigned)(k - 1) * lv;
+    fu1[q] = FU.ld(vo + 8u, o); fu0[q] = FU.ld(vo, o); fv1[q] = FV.ld(vo + (unsigned)sj * 8u, o); fv0[q] = FV.ld(vo, o);
+    hz[q] = Hz.ld(vo, o);
+    zk[q] = zw.ld(vo, (unsigned)k * lv);
   }
-  const double zw0 = zw[0], zwN = zw[(long)N * n2];
+  const double zw0 = zw.ld(vo, 0), zwN = zw.ld(vo, (unsigned)N * lv);
   const double wsrf = F.swflx[ij] * F.dm_r[ij] * F.dn_r[ij];
   const double CX0 = dtau * F.pm[ij] * F.pn[ij];
   const int pidx = d.p.npip > 0 ? F.pipe_idx[ij] : 0;
@@ -470,27 +471,26 @@ __global__ void __launch_bounds__(kSegBlock, 2) k_omega_seg(Dev d, Range R, doub
   const double wrk = (Lw[S - 1][l] + wsrf) / (zwN - zw0);
   const double cx_top = s + 1 < S ? Lcx[s + 1][l] : 0.0, hz_top = s + 1 < S ? Lhz[s + 1][l] : 0.0;
   if (!kHB && !act) return;
-  double* __restrict__ Wi = F.Wi + ij;
-  double* __restrict__ We = F.We + ij;
+  const BufF64 Wi(F.Wi), We(F.We);
+  const unsigned vs = act ? vo : kBufOff;   // lanes outside the range store nothing
   // kHB: Hz_bak/fwd of cell k needs We, Wi at w-levels k and k-1
   const double hbf = kHB ? hcff * F.pm[ij] * F.pn[ij] : 0.0;
-  double* __restrict__ Hf = F.c2 + ij;
-  double* __restrict__ Hb = F.c3 + ij;
+  const BufF64 Hf(F.c2), Hb(F.c3);
   double we_p = 0.0, wi_p = 0.0, we_f = 0.0, wi_f = 0.0;   // previous level's, the segment's first level's
   int tr = tl;
   __asm__ volatile("" : "+v"(tr));   // a second opaque offset: the stored differences are not forwarded
   auto hb_store = [&](int q, double we1, double wi1, double we0, double wi0) {
     const double div = roms_smem[q * nthr + tr];
     const double FlxDiv = hbf * (div + we1 + wi1 - we0 - wi0);
-    const long o = (long)(c0 + q - 1) * n2;
-    Hf[o] = hz[q] - FlxDiv;
-    Hb[o] = hz[q] + FlxDiv;
+    const unsigned o = (unsigned)(c0 + q - 1) * lv;
+    Hf.st(hz[q] - FlxDiv, vs, o);
+    Hb.st(hz[q] + FlxDiv, vs, o);
   };
-  if (act && s == 0) {
-    Wi[0] = 0.0;
-    We[0] = 0.0;
-    Wi[(long)N * n2] = 0.0;
-    We[(long)N * n2] = 0.0;
+  if (s == 0) {
+    Wi.st(0.0, vs, 0);
+    We.st(0.0, vs, 0);
+    Wi.st(0.0, vs, (unsigned)N * lv);
+    We.st(0.0, vs, (unsigned)N * lv);
   }
 #pragma unroll
   for (int q = 0; q < kOmR; q++) {
@@ -515,15 +515,14 @@ __global__ void __launch_bounds__(kSegBlock, 2) k_omega_seg(Dev d, Range R, doub
     } else {
       we = 0.0;
     }
-    if (act && q < n && k <= N - 1) {
-      const long o1 = (long)k * n2;
-      We[o1] = we;
-      Wi[o1] = w;
+    if (q < n && k <= N - 1) {   // wave-uniform
+      We.st(we, vs, (unsigned)k * lv);
+      Wi.st(w, vs, (unsigned)k * lv);
     }
     if constexpr (kHB) {
       const double we1 = k <= N - 1 ? we : 0.0, wi1 = k <= N - 1 ? w : 0.0;   // We(N) = Wi(N) = 0
       if (q == 0) { we_f = we1; wi_f = wi1; }
-      if (act && q >= 1 && q < n) hb_store(q, we1, wi1, we_p, wi_p);
+      if (q >= 1 && q < n) hb_store(q, we1, wi1, we_p, wi_p);
       if (q == n - 1) { Lte[s][l] = we1; Lti[s][l] = wi1; }   // this segment's top w-level, for the wave above
       we_p = we1; wi_p = wi1;
     }
@@ -531,7 +530,7 @@ __global__ void __launch_bounds__(kSegBlock, 2) k_omega_seg(Dev d, Range R, doub
   if constexpr (kHB) {
     __syncthreads();
     const double we0 = s > 0 ? Lte[s - 1][l] : 0.0, wi0 = s > 0 ? Lti[s - 1][l] : 0.0;   // We(0) = Wi(0) = 0
-    if (act) hb_store(0, we_f, wi_f, we0, wi0);
+    hb_store(0, we_f, wi_f, we0, wi0);
   }
 }
 

@@ -79,6 +79,8 @@ struct Params {
   int omega_hb;   // the predictor's omega forms pre_step3d's Hz_bak/Hz_fwd (ROMS_GPU_OMEGA_HB=0: pre_step3d does)
   int preuv_lds;  // k_pre_uv_seg: u(indx) stored and u(nstp)/u(indx) combined in the spline phase (ROMS_GPU_PREUV_LDS=0: reloads)
   int seg_jrows;  // rows j per block of the momentum segment solvers (1..kSegJMax; ROMS_GPU_SEG_JROWS)
+  int t_chunk;    // tracer horizontal part + column solve alternating over strips of t_chunk rows (ROMS_GPU_TCHUNK; 0: off)
+  int seg_buf;    // segment solvers with buffer loads, wave-uniform level offsets (ROMS_GPU_SEG_BUF bits)
   int seg_vtile;  // v columns of the momentum segment solvers on 16 x 4 tiles per wavefront (ROMS_GPU_SEG_VTILE=0: rows of 64)
   int s2d_k;      // fast steps per zeta/ubar/vbar exchange (multi-rank, wide halos of 2*s2d_k; 1: every step)
   int uv2e_nc, uv2e_nf;   // lengths of Fields::uv2e_couple / uv2e_flux
@@ -290,6 +292,11 @@ constexpr int kSegJMax = ROMS_SEG_JMAX;
 #define ROMS_SEG_NMIN 11   // 0: every row select kept (the round-4 code; A/B builds)
 #endif
 constexpr int kSegNMin = ROMS_SEG_NMIN;
+// waves per SIMD the buffer-addressed segment solvers are built for (2: one
+// 512-thread block per CU at <= 256 VGPRs; 4: two blocks at <= 128)
+#ifndef ROMS_SEG_BUF_WAVES
+#define ROMS_SEG_BUF_WAVES 2
+#endif
 // segments of an N-level column (one per wavefront at kSegCW = 64, seg_waves)
 // and whether each of them gets at least kSegNMin rows
 inline int seg_count(int N) {

@@ -951,6 +951,19 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     P.hoist = !(e && e[0] == '0');
   }
   {
+    const char* e = getenv("ROMS_GPU_TCHUNK");
+    P.t_chunk = e ? atoi(e) : 0;
+    if (P.t_chunk < 0) P.t_chunk = 0;
+  }
+  {
+    const char* e = getenv("ROMS_GPU_SEG_BUF");
+    // bits: 1 k_pre_tracer_segb, 2 k_step3d_t_segb, 4 its t(nnew) prefetch,
+    // 8 its Hz reload, 16 k_pre_tracer_segb's prefetch.  Default 7: C3
+    // 57.4-57.7 -> 56.7 ms/step, step3d_t 5.98 -> 5.75 ms, pre_step3d
+    // 11.5 -> 11.3 ms (same box, profiles/r5_c_seg_buf_ab.txt)
+    P.seg_buf = e ? atoi(e) : 7;
+  }
+  {
     const char* e = getenv("ROMS_GPU_SEG_VTILE");
     P.seg_vtile = !(e && e[0] == '0');
   }
