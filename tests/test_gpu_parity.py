@@ -396,17 +396,18 @@ def test_uv2_fused_bitwise_equals_two_kernels(case, monkeypatch):
         assert np.array_equal(a[n], b[n]), n
 
 
-@pytest.mark.parametrize("case", ["filament", "basin", "basin_n100"])
+@pytest.mark.parametrize("case", ["filament", "basin", "basin_n100", "basin_n90"])
 @pytest.mark.parametrize("routine,outs", [("set_HUV1", ["u", "v", "FlxU", "FlxV"])])
 def test_chain_kernels_bitwise_equal_column_sweeps(case, routine, outs, monkeypatch):
-    """The chained 4-lane column kernel (k_chain.h: set_HUV1) gives
-    exactly the bits of the one-lane-per-column sweeps (ROMS_GPU_CHAIN=0)."""
+    """The chained 4-lane column kernel (k_chain.h: set_HUV1; buffer-addressed,
+    with N = 100 the full-segment form and N = 90 the guarded one of KL = 25)
+    gives exactly the bits of the one-lane-per-column sweeps (ROMS_GPU_CHAIN=0)."""
     if case == "filament":
         cfg = oracle.filament_cfg(LLm=32, MMm=24, N=16, np_xi=1, np_eta=1)
     elif case == "basin":
         cfg = basin_cfg(nonlin=True)
     else:
-        cfg = basin_cfg(LLm=40, MMm=36, N=100, nonlin=True)
+        cfg = basin_cfg(LLm=40, MMm=36, N=int(case[7:]), nonlin=True)
     a = _routine_fields(cfg, routine, outs, {"ROMS_GPU_CHAIN": "1"}, monkeypatch)
     b = _routine_fields(cfg, routine, outs, {"ROMS_GPU_CHAIN": "0"}, monkeypatch)
     for n in outs:

@@ -312,6 +312,59 @@ __device__ __forceinline__ void uv_spline_seg(const Dev& d, const SegSpan& sg, S
   }
 }
 
+// uv_spline_seg with buffer loads (the segment solvers' buffer forms): the
+// lane's column and its (i-1)/(j-1), (i+1)/(j+1), (i-2)/(j-2) neighbours in
+// four VGPR offsets, each row's level in an SGPR (seg_uniform).  row(q, so,
+// h0, h1, u) gets the row's level byte offset in place of the element offset.
+// Same expressions and order: bitwise equal to uv_spline_seg.
+struct NoSplineRowB {
+  __device__ __forceinline__ void operator()(int, unsigned, double, double, double) const {}
+};
+template <int KR, class RowF = NoSplineRowB>
+__device__ __forceinline__ void uv_spline_segb(const Dev& d, const SegSpan& sg, SegXchg& X, long ij, int nrhs, int dir,
+                                               double (&fl)[KR], RowF row = RowF()) {
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const int N = b.N, c0 = sg.c0, n = sg.n;
+  if (!d.p.uv_adv) {
+#pragma unroll
+    for (int q = 0; q < KR; q++) fl[q] = 0.0;
+    return;
+  }
+  const long s = dir == 0 ? 1 : b.nx2;
+  const unsigned lv = (unsigned)b.n2 * 8u, vo = (unsigned)ij * 8u, ds = (unsigned)s * 8u;
+  const unsigned vm = vo - ds, vp = vo + ds, vm2 = vo - 2u * ds;
+  const BufF64 Uv((dir == 0 ? F.u : F.v) + (long)(nrhs - 1) * b.n3), Hz(F.Hz), We(F.We);
+  const double* mask = dir == 0 ? F.umask : F.vmask;
+  double dc[KR + 1], uu[KR];
+#pragma unroll
+  for (int q = 0; q < KR + 1; q++) {
+    const unsigned L = (unsigned)(min(max(c0 - 1 + q, 1), N) - 1) * lv;
+    const double h0 = Hz.ld(vo, L), h1 = Hz.ld(vm, L);
+    dc[q] = 0.5625 * (h0 + h1) - 0.0625 * (Hz.ld(vp, L) + Hz.ld(vm2, L));
+    if (q < KR) uu[q] = Uv.ld(vo, L);
+    row(q, L, h0, h1, q < KR ? uu[q] : 0.0);
+    if (q % kSegLoadGroup == kSegLoadGroup - 1) __builtin_amdgcn_sched_barrier(0);
+  }
+  spline_fc_seg<KR>(sg, N, X, dc, uu, fl);
+  const double m1 = mask[ij + s], m0 = mask[ij - s];
+  double wf[KR];
+#pragma unroll
+  for (int q = 0; q < KR; q++) {
+    const unsigned w = (unsigned)min(max(c0 - 1 + q, 1), N - 1) * lv;
+    const double we0 = We.ld(vo, w), wem = We.ld(vm, w);
+    wf[q] = we0 + wem - 0.125 * ((We.ld(vp, w) - we0) * m1 - (wem - We.ld(vm2, w)) * m0);
+    if (q % kSegLoadGroup == kSegLoadGroup - 1) __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int q = 0; q < KR; q++) pin(wf[q]);
+#pragma unroll
+  for (int q = 0; q < KR; q++) {
+    const int r = c0 - 1 + q;
+    fl[q] = (r == 0 || r == N) ? 0.0 : fl[q] * 0.5 * wf[q];
+  }
+}
+
 // SPLINE_TS advective flux FC(r)*We(r) of a tracer column at interfaces
 // r = c0-1+q, q = 0..n (0 at the bottom and the surface); hz, tt as w, f of
 // spline_fc_seg.

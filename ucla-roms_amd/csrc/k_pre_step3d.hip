@@ -982,11 +982,109 @@ __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_pre_uv_seg(Dev d, R
   }
 }
 
+// ---- k_pre_uv_seg<true> with buffer loads/stores (Params::seg_buf bit
+// 128): wave-uniform level offsets in SGPRs (seg_uniform), the lane's column
+// and its neighbour in VGPR offsets.  Same expressions and order: bitwise
+// equal to k_pre_uv_seg<true>. ----
+__global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_pre_uv_segb(Dev d, Range R, PreCoef c, int nstp, int nnew,
+                                                                         int nrhs) {
+  const uint3 bI = seg_tile(d.p.seg_order, d.p.seg_xg);
+  __shared__ SegXchg X;
+  constexpr int KR = kSegRows + 1;
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const int N = b.N, indx = 3 - nstp;
+  SegSpan sg = seg_span(N);
+  seg_uniform(sg);
+  SegCol col;
+  seg_uv_col(d, R, bI, sg, col);
+  if (col.idle) return;   // uniform over the block
+  const int dir = col.dir;
+  const bool act = col.act;
+  const long n2 = b.n2, ij = IJ(b, col.i, col.j), s = dir == 0 ? 1 : b.nx2;
+  const int c0 = sg.c0, n = sg.n;
+  const unsigned lv = (unsigned)n2 * 8u, vo = (unsigned)ij * 8u, vm = vo - (unsigned)s * 8u;
+  auto lev = [&](int k) { return (unsigned)(min(max(k, 1), N) - 1) * lv; };   // rho level k (clamped)
+  double* Uall = dir == 0 ? F.u : F.v;
+  const int nthr = (int)(blockDim.x * blockDim.y * blockDim.z);
+  const int tid = (int)(threadIdx.x + blockDim.x * (threadIdx.y + blockDim.y * threadIdx.z));
+  double* const Sb = roms_smem + tid;                        // row q-1: cf_stp*u(nstp) + cf_bak*u(indx)
+  double* const Su = roms_smem + (long)(KR - 1) * nthr + tid;  // row q-1: Hz*u(nstp), the new u(indx)
+  const BufF64 Uix(Uall + (long)(indx - 1) * b.n3), Unew(Uall + (long)(nnew - 1) * b.n3);
+  double fl[KR];
+  uv_spline_segb<KR>(d, sg, X, ij, nrhs, dir, fl, [&](int q, unsigned L, double h0, double h1, double u) {
+    if (q >= 1 && q < KR) {   // cells c0..c0+KR-2 (q is a constant of the unrolled load loop)
+      Sb[(q - 1) * nthr] = c.cf_stp * u + c.cf_bak * Uix.ld(vo, L);
+      Su[(q - 1) * nthr] = 0.5 * (h0 + h1) * u;
+    }
+  });
+  __builtin_amdgcn_sched_barrier(0);   // the viscosity phase's loads stay out of the spline phase
+  const BufF64 rr(dir == 0 ? F.ru : F.rv), Akv(F.Akv), Wi(F.Wi), Hf(F.c2), Hb(F.c3);
+  const double sstr = dir == 0 ? F.sustr[ij] : F.svstr[ij];
+  const double DC0 = c.dtau * 0.25 * (F.pm[ij] + F.pm[ij - s]) * (F.pn[ij] + F.pn[ij - s]);
+  auto rhs = [&](int p) {
+    const int k = c0 + p;
+    const unsigned o = lev(k);
+    const double rro = rr.ld(vo, o);
+    const double r = k == 1 ? rro - fl[1] : rro - fl[p + 1 < KR ? p + 1 : KR - 1] + fl[p];
+    const double ub = Sb[(p < KR - 1 ? p : KR - 2) * nthr];
+    const double v = 0.5 * (Hb.ld(vo, o) + Hb.ld(vm, o)) * ub + DC0 * r;
+    return k == N ? v + c.dtau * sstr : v;
+  };
+  double hf[KR + 1], hfm[KR + 1];   // Hz_fwd(c0-1+q) of the column and of its (i-1) / (j-1) neighbour
+#pragma unroll
+  for (int q = 0; q < KR + 1; q++) {
+    const unsigned L = lev(c0 - 1 + q);
+    hf[q] = Hf.ld(vo, L);
+    hfm[q] = Hf.ld(vm, L);
+  }
+  auto fcw = [&](int q, double& fc, double& wc) {   // interface c0-1+q (0 at the bottom and the surface)
+    const int r = c0 - 1 + q;
+    const unsigned w = (unsigned)min(max(r, 1), N - 1) * lv;
+    const bool in = r > 0 && r < N;
+    const int qa = q + 1 < KR + 1 ? q + 1 : KR;
+    const double f = 2.0 * c.dtau * (Akv.ld(vo, w) + Akv.ld(vm, w)) / (hf[qa] + hfm[qa] + hf[q] + hfm[q]);
+    const double wv = DC0 * 0.5 * (Wi.ld(vo, w) + Wi.ld(vm, w));
+    fc = in ? f : 0.0;
+    wc = in ? wv : 0.0;
+  };
+  const double rd = F.r_D[ij], rdm = F.r_D[ij - s];
+  double fcl, wcl;
+  fcw(0, fcl, wcl);
+  __syncthreads();  // X reused by the second coupling
+  SegTri<KR> T;
+  T.eliminate(n, [&](int p, double& a, double& bb, double& cc, double& dd) {
+    double fcu, wcu;
+    fcw(p + 1, fcu, wcu);
+    const int k = c0 + p;
+    a = -(fcl + fmax0(wcl));
+    cc = -(fcu - fmin0(wcu));
+    const double b1 = 0.5 * (hf[p + 1] + hfm[p + 1]) + 0.5 * c.dtau * (rd + rdm) + fcu + fmax0(wcu);
+    const double bk = 0.5 * (hf[p + 1] + hfm[p + 1]) + fcl - fmin0(wcl) + fcu + fmax0(wcu);
+    bb = k == 1 ? b1 : bk;
+    dd = rhs(p);
+    fcl = fcu; wcl = wcu;
+  });
+  double xL, xR;
+  T.couple(sg, n, X, xL, xR);
+  T.solve(n, xL, xR);
+  const unsigned vs = act ? vo : kBufOff;
+#pragma unroll
+  for (int p = 0; p < KR; p++)
+    if (p < n) {
+      const unsigned o = lev(c0 + p);
+      Unew.st(T.D[p], vs, o);
+      Uix.st(Su[(p < KR - 1 ? p : KR - 2) * nthr], vs, o);
+    }
+}
+
 static size_t pre_uv_seg_lds_bytes(unsigned nthr) {
   return (size_t)2 * kSegRows * nthr * sizeof(double);
 }
 void setup_pre_uv_seg() {
   (void)hipFuncSetAttribute((const void*)k_pre_uv_seg<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)pre_uv_seg_lds_bytes(kSegBlock * kSegJMax));
+  (void)hipFuncSetAttribute((const void*)k_pre_uv_segb, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)pre_uv_seg_lds_bytes(kSegBlock * kSegJMax));
 }
 
@@ -1107,7 +1205,10 @@ void launch_pre_step3d(const Dev& d, hipStream_t s, const Tlev& t, bool uv_done,
   if (d.p.colseg) {
     const dim3 gs = seg_uv_grid(d, RI, d.p.seg_jrows), bs(kCX, seg_waves(b.N), d.p.seg_jrows);
     ktimer_mark(s, kTimedPreUvSeg, 0);
-    if (d.p.preuv_lds && d.p.uv_adv && t.nrhs == t.nstp)
+    if (d.p.preuv_lds && d.p.uv_adv && t.nrhs == t.nstp && (d.p.seg_buf & 128))
+      hipLaunchKernelGGL(k_pre_uv_segb, gs, bs, pre_uv_seg_lds_bytes(bs.x * bs.y * bs.z), s, d, RI, c, t.nstp, t.nnew,
+                         t.nrhs);
+    else if (d.p.preuv_lds && d.p.uv_adv && t.nrhs == t.nstp)
       hipLaunchKernelGGL(k_pre_uv_seg<true>, gs, bs, pre_uv_seg_lds_bytes(bs.x * bs.y * bs.z), s, d, RI, c, t.nstp,
                          t.nnew, t.nrhs);
     else

@@ -407,6 +407,116 @@ __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_uv1_seg(Dev d, Rang
   }
 }
 
+// ---- k_uv1_seg<true> with buffer loads/stores (Params::seg_buf bit 32):
+// wave-uniform level offsets in SGPRs (seg_uniform), the lane's column and
+// its neighbour in VGPR offsets; PF: u(nnew) of the segment's rows loaded
+// with the spline phase's inputs.  Same expressions and order: bitwise equal
+// to k_uv1_seg<true>. ----
+template <bool PF>
+__global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_uv1_segb(Dev d, Range R, int nnew, int nrhs) {
+  const uint3 bI = seg_tile(d.p.seg_order, d.p.seg_xg);
+  __shared__ SegXchg X;
+  __shared__ double Lf[kSegMaxS][kSegCW * kSegJMax];   // rufrc running sums
+  constexpr int KR = kSegRows + 1;
+  const Bounds& b = d.b;
+  const Fields& F = d.f;
+  const int N = b.N;
+  const double dt = d.p.dt;
+  SegSpan sg = seg_span(N);
+  seg_uniform(sg);
+  SegCol col;
+  seg_uv_col(d, R, bI, sg, col);
+  if (col.idle) return;   // uniform over the block
+  const int dir = col.dir;
+  const bool act = col.act;
+  const long n2 = b.n2, ij = IJ(b, col.i, col.j), s = dir == 0 ? 1 : b.nx2;
+  const int c0 = sg.c0, n = sg.n;
+  const unsigned lv = (unsigned)n2 * 8u, vo = (unsigned)ij * 8u, vm = vo - (unsigned)s * 8u;
+  auto lev = [&](int k) { return (unsigned)(min(max(k, 1), N) - 1) * lv; };   // rho level k (clamped)
+  const int nthr = (int)(blockDim.x * blockDim.y * blockDim.z);
+  const int tid = (int)(threadIdx.x + blockDim.x * (threadIdx.y + blockDim.y * threadIdx.z));
+  double* const Sh = roms_smem + tid;                             // Hz(c0-1+q) at Sh[q*nthr]
+  double* const Shm = roms_smem + (long)(KR + 1) * nthr + tid;    // its neighbour's at Shm[q*nthr]
+  const BufF64 Un((dir == 0 ? F.u : F.v) + (long)(nnew - 1) * b.n3);
+  double fl[KR], un[PF ? KR : 1];
+  if constexpr (PF) {
+#pragma unroll
+    for (int p = 0; p < KR; p++) un[p] = Un.ld(vo, lev(c0 + p));
+  }
+  uv_spline_segb<KR>(d, sg, X, ij, nrhs, dir, fl, [&](int q, unsigned, double h0, double h1, double) {
+    Sh[q * nthr] = h0;
+    Shm[q * nthr] = h1;
+  });
+  __builtin_amdgcn_sched_barrier(0);   // the viscosity phase's loads stay out of the spline phase
+  const BufF64 rr(dir == 0 ? F.ru : F.rv), Akv(F.Akv), Wi(F.Wi);
+  const double sstr = dir == 0 ? F.sustr[ij] : F.svstr[ij];
+  const double DC0 = dt * 0.25 * (F.pm[ij] + F.pm[ij - s]) * (F.pn[ij] + F.pn[ij - s]);
+  double rk[KR];
+#pragma unroll
+  for (int p = 0; p < KR; p++) {
+    const int k = c0 + p;
+    const double rro = rr.ld(vo, lev(k));
+    rk[p] = k == 1 ? rro - fl[1] : rro - fl[p + 1 < KR ? p + 1 : KR - 1] + fl[p];
+  }
+  int tl = tid;
+  __asm__ volatile("" : "+v"(tl));
+  auto HZ = [&](int q) { return roms_smem[tl + q * nthr]; };
+  auto HZM = [&](int q) { return roms_smem[(KR + 1 + q) * nthr + tl]; };
+  auto fcw = [&](int q, double& fc, double& wc) {   // interface c0-1+q (0 at the bottom and the surface)
+    const int r = c0 - 1 + q;
+    const unsigned w = (unsigned)min(max(r, 1), N - 1) * lv;
+    const bool in = r > 0 && r < N;
+    const int qa = q + 1 < KR + 1 ? q + 1 : KR;
+    const double f = 2.0 * dt * (Akv.ld(vo, w) + Akv.ld(vm, w)) / (HZ(qa) + HZM(qa) + HZ(q) + HZM(q));
+    const double wv = DC0 * 0.5 * (Wi.ld(vo, w) + Wi.ld(vm, w));
+    fc = in ? f : 0.0;
+    wc = in ? wv : 0.0;
+  };
+  const double rD = F.r_D[ij], rDm = F.r_D[ij - s];
+  double fcl, wcl;
+  fcw(0, fcl, wcl);
+  __syncthreads();  // X reused by the second coupling
+  SegTri<KR> T;
+  T.eliminate(n, [&](int p, double& a, double& bb, double& cc, double& dd) {
+    double fcu, wcu;
+    fcw(p + 1, fcu, wcu);
+    const int k = c0 + p;
+    a = -(fcl + fmax0(wcl));
+    cc = -(fcu - fmin0(wcu));
+    const double b1 = 0.5 * (HZ(p + 1) + HZM(p + 1)) + 0.5 * dt * (rD + rDm) + fcu + fmax0(wcu);
+    const double bk = 0.5 * (HZ(p + 1) + HZM(p + 1)) + fcl - fmin0(wcl) + fcu + fmax0(wcu);
+    bb = k == 1 ? b1 : bk;
+    const double v = (PF ? un[p] : Un.ld(vo, lev(k))) + DC0 * rk[p];
+    dd = k == N ? v + dt * sstr : v;
+    fcl = fcu; wcl = wcu;
+  });
+  double xL, xR;
+  T.couple(sg, n, X, xL, xR);
+  T.solve(n, xL, xR);
+  const double dmdn = dir == 0 ? F.dm_u[ij] * F.dn_u[ij] : F.dm_v[ij] * F.dn_v[ij];
+  // rufrc = ru(1) + dmdn*(sstr - r_D*u(1)) + ru(2) + ... + ru(N), wave by wave
+  const int S = sg.S, sl = sg.l;
+  for (int t = 0; t < S; t++) {
+    if (sg.s == t) {
+      double frc;
+      if (t == 0) frc = rk[0] + dmdn * (sstr - 0.5 * (rDm + rD) * T.D[0]);
+      else frc = Lf[t - 1][sl] + rk[0];
+#pragma unroll
+      for (int p = 1; p < KR; p++) frc = p < n ? frc + rk[p] : frc;
+      Lf[t][sl] = frc;
+    }
+    __syncthreads();
+  }
+  const unsigned vs = act ? vo : kBufOff;
+#pragma unroll
+  for (int p = 0; p < KR; p++)
+    if (p < n) Un.st(T.D[p] * 0.5 * (HZ(p + 1) + HZM(p + 1)), vs, lev(c0 + p));
+  if (act && sg.s == 0) {
+    if (dir == 0) F.rufrc[ij] = Lf[S - 1][sl];
+    else F.rvfrc[ij] = Lf[S - 1][sl];
+  }
+}
+
 void setup_column_kernels_uv1(size_t bytes) {
   (void)hipFuncSetAttribute((const void*)k_uv1<ColLds>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
@@ -417,6 +527,10 @@ void setup_uv1_seg() {
   (void)hipFuncSetAttribute((const void*)k_uv1_seg<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)((size_t)kSegRows * kSegMaxS * kSegCW * kSegJMax * sizeof(double)));
   (void)hipFuncSetAttribute((const void*)k_uv1_seg<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)uv1_seg_lds_bytes(kSegBlock * kSegJMax));
+  (void)hipFuncSetAttribute((const void*)k_uv1_segb<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)uv1_seg_lds_bytes(kSegBlock * kSegJMax));
+  (void)hipFuncSetAttribute((const void*)k_uv1_segb<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)uv1_seg_lds_bytes(kSegBlock * kSegJMax));
 }
 
@@ -431,7 +545,11 @@ void launch_step3d_uv1(const Dev& d, hipStream_t s, const Tlev& t, bool uv_done)
   else if (d.p.colseg) {
     const dim3 gs = seg_uv_grid(d, R, d.p.seg_jrows), bs(kCX, seg_waves(b.N), d.p.seg_jrows);
     ktimer_mark(s, kTimedUv1Seg, 0);
-    if (d.p.uv1_lds && d.p.uv_adv)
+    if (d.p.uv1_lds && d.p.uv_adv && (d.p.seg_buf & 32) && (d.p.seg_buf & 64))
+      hipLaunchKernelGGL(k_uv1_segb<true>, gs, bs, uv1_seg_lds_bytes(bs.x * bs.y * bs.z), s, d, R, t.nnew, t.nrhs);
+    else if (d.p.uv1_lds && d.p.uv_adv && (d.p.seg_buf & 32))
+      hipLaunchKernelGGL(k_uv1_segb<false>, gs, bs, uv1_seg_lds_bytes(bs.x * bs.y * bs.z), s, d, R, t.nnew, t.nrhs);
+    else if (d.p.uv1_lds && d.p.uv_adv)
       hipLaunchKernelGGL(k_uv1_seg<true>, gs, bs, uv1_seg_lds_bytes(bs.x * bs.y * bs.z), s, d, R, t.nnew, t.nrhs);
     else
       hipLaunchKernelGGL(k_uv1_seg<false>, gs, bs, (size_t)b.N * kSegCW * d.p.seg_jrows * sizeof(double), s, d, R,

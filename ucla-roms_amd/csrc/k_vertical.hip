@@ -161,15 +161,24 @@ __global__ void __launch_bounds__(256) k_set_huv1(Dev d, Range R, int nnew, int 
 
 // Chained form (k_chain.h): the column's u and Hz_u*dn stay in the lane's
 // registers between the sum and the correction pass; the two sums run down
-// the segments in the reference's k = N..1 order (bit-identical).
-template <int KL>
-__global__ void __launch_bounds__(256) k_set_huv1_chain(Dev d, Range R, int nnew, int first) {
+// the segments in the reference's k = N..1 order (bit-identical).  The level
+// loops are raw-buffer accesses as in k_uv2_fused: the lane's column and
+// segment in one VGPR offset, the level in an SGPR; a level the lane does not
+// own and every store of an inactive lane take kBufOff (load 0, store
+// dropped), so the loops are straight-line code.  FULL: N == 4*KL (C3).
+// KL > 13: the lane's Hz_u*dn levels sit in LDS (as k_uv2_fused's Hz_u), so
+// the block fits 4 waves per SIMD in registers
+template <int KL, bool FULL = false>
+__global__ void __launch_bounds__(256, KL > 13 ? 3 : 4) k_set_huv1_chain(Dev d, Range R, int nnew, int first) {
+  constexpr bool kDcLds = KL > 13;
+  __shared__ double sDc[kDcLds ? KL * 256 : 1];
   const uint3 bI = xcd_tile();
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const double NOW = 3.63, MID = 4.47, BAK = 2.05;
   const int N = b.N;
   const ChainLane cl = chain_lane<KL>(R, bI, N);
+  const int nk = FULL ? KL : cl.nk;
   const long n2 = b.n2;
   // grid z = 2: one direction per block (both directions' loads in flight
   // at once across blocks); grid z = 1: both, one after the other
@@ -181,23 +190,32 @@ __global__ void __launch_bounds__(256) k_set_huv1_chain(Dev d, Range R, int nnew
     const bool act = ic == cl.i && jc == cl.j && cl.in;
     const long ij = IJ(b, ic, jc), s = dir == 0 ? 1 : b.nx2;
     const double dn = dir == 0 ? F.dn_u[ij] : F.dm_v[ij];
-    double* __restrict__ u = (dir == 0 ? F.u : F.v) + (long)(nnew - 1) * b.n3 + ij;
-    double* __restrict__ Flx = (dir == 0 ? F.FlxU : F.FlxV) + ij;
-    const double* __restrict__ Hz = F.Hz + ij;
-    double uu[KL], dc[KL];
+    const BufF64 bU((dir == 0 ? F.u : F.v) + (long)(nnew - 1) * b.n3, b.n3), bHz(F.Hz, b.n3),
+        bFl(dir == 0 ? F.FlxU : F.FlxV, b.n3);
+    const unsigned vo = (unsigned)((ij + (long)(cl.lo - 1) * n2) * 8), vom = vo - (unsigned)(s * 8);
+    auto so = [&](int q) { return (unsigned)((long)q * n2 * 8); };
+    auto vq = [&](int q) { return q < nk ? vo : kBufOff; };
+    auto vqm = [&](int q) { return q < nk ? vom : kBufOff; };
+    auto vsq = [&](int q) { return act && q < nk ? vo : kBufOff; };
+    double uu[KL], dcr[kDcLds ? 1 : KL];
+    struct DcRef {   // dc[q]: Hz_u*dn of the lane's level lo+q, in LDS (kDcLds) or registers
+      double* l;
+      double* r;
+      __device__ __forceinline__ double& operator[](int q) const { return kDcLds ? l[q * 256] : r[q]; }
+    } const dc{sDc + threadIdx.x, dcr};
 #pragma unroll
     for (int q = 0; q < KL; q++) {
-      if (q < cl.nk) {
-        const long o = (long)(cl.lo + q - 1) * n2;
-        uu[q] = u[o];
-        dc[q] = 0.5 * (Hz[o] + Hz[o - s]) * dn;
-      }
+      uu[q] = bU.ld(vq(q), so(q));
+      dc[q] = 0.5 * (bHz.ld(vq(q), so(q)) + bHz.ld(vqm(q), so(q))) * dn;
+      if (q % 8 == 7) __builtin_amdgcn_sched_barrier(0);
     }
     double DC0, FC0;
     chain_down(cl, DC0, FC0, [&](double& a, double& c) {
 #pragma unroll
-      for (int q = KL - 1; q >= 0; q--)
-        if (q < cl.nk) { a = a + dc[q]; c = c + dc[q] * uu[q]; }
+      for (int q = KL - 1; q >= 0; q--) {
+        a = q < nk ? a + dc[q] : a;
+        c = q < nk ? c + dc[q] * uu[q] : c;
+      }
     });
     const double a1 = dir == 0 ? F.DU_avg1[ij] : F.DV_avg1[ij];
     if (first) FC0 = (FC0 - a1) / DC0;
@@ -207,16 +225,11 @@ __global__ void __launch_bounds__(256) k_set_huv1_chain(Dev d, Range R, int nnew
       FC0 = (FC0 - NOW * a1 + MID * a2 - BAK * ab) / DC0;
     }
     const double um = dir == 0 ? F.umask[ij] : F.vmask[ij];
-    if (act) {
 #pragma unroll
-      for (int q = 0; q < KL; q++) {
-        if (q < cl.nk) {
-          const long o = (long)(cl.lo + q - 1) * n2;
-          const double un = (uu[q] - FC0) * um;
-          u[o] = un;
-          Flx[o] = dc[q] * (un);
-        }
-      }
+    for (int q = 0; q < KL; q++) {
+      const double un = (uu[q] - FC0) * um;
+      bU.st(un, vsq(q), so(q));
+      bFl.st(dc[q] * (un), vsq(q), so(q));
     }
   }
 }
@@ -229,6 +242,8 @@ void launch_set_huv1(const Dev& d, hipStream_t s, const Tlev& t) {
   gc.z = d.p.chain_dirz ? 2 : 1;
   if (d.p.chain && kl == 5) hipLaunchKernelGGL(k_set_huv1_chain<5>, gc, dim3(256), 0, s, d, R, t.nnew, first);
   else if (d.p.chain && kl == 13) hipLaunchKernelGGL(k_set_huv1_chain<13>, gc, dim3(256), 0, s, d, R, t.nnew, first);
+  else if (d.p.chain && kl == 25 && b.N == 100)
+    hipLaunchKernelGGL((k_set_huv1_chain<25, true>), gc, dim3(256), 0, s, d, R, t.nnew, first);
   else if (d.p.chain && kl == 25) hipLaunchKernelGGL(k_set_huv1_chain<25>, gc, dim3(256), 0, s, d, R, t.nnew, first);
   else hipLaunchKernelGGL(k_set_huv1, grid_of(R), dim3(kBX, kBY), 0, s, d, R, t.nnew, first);
   launch_exchange_list(d, s, ExchList{{d.f.FlxU, d.f.FlxV, d.f.u + (long)(t.nnew - 1) * b.n3,
