@@ -462,7 +462,7 @@ def test_hz_uv_stored_on_request(monkeypatch):
 
 
 @pytest.mark.parametrize("case", ["filament", "basin"])
-@pytest.mark.parametrize("switch", ["ROMS_GPU_OMEGA_HB", "ROMS_GPU_P_IN_RHO"])
+@pytest.mark.parametrize("switch", ["ROMS_GPU_OMEGA_HB", "ROMS_GPU_P_IN_RHO", "ROMS_GPU_PRS_BUF"])
 def test_step_producer_variants_bitwise(case, switch, monkeypatch):
     """Producers that form a later routine's inputs with its expressions: 4
     whole steps bitwise equal to the consumer forming them (=0), periodic
@@ -470,7 +470,8 @@ def test_step_producer_variants_bitwise(case, switch, monkeypatch):
     - ROMS_GPU_OMEGA_HB: the predictor's omega forms pre_step3d's
       Hz_bak/Hz_fwd of the interior cells;
     - ROMS_GPU_P_IN_RHO: every rho_eos also forms prsgrd's P in its sweep,
-      so whole steps skip k_prsgrd_P."""
+      so whole steps skip k_prsgrd_P;
+    - ROMS_GPU_PRS_BUF: k_prsgrd_uv's windows through buffer loads."""
     if case == "basin":
         cfg = basin_cfg(LLm=70, MMm=40, N=12, nonlin=True)
     else:

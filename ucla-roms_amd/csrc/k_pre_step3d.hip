@@ -985,7 +985,9 @@ __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_pre_uv_seg(Dev d, R
 // ---- k_pre_uv_seg<true> with buffer loads/stores (Params::seg_buf bit
 // 128): wave-uniform level offsets in SGPRs (seg_uniform), the lane's column
 // and its neighbour in VGPR offsets.  Same expressions and order: bitwise
-// equal to k_pre_uv_seg<true>. ----
+// equal to k_pre_uv_seg<true>.  PF: the viscosity rows' Hz_fwd pairs
+// loaded at entry with the spline inputs. ----
+template <bool PF>
 __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_pre_uv_segb(Dev d, Range R, PreCoef c, int nstp, int nnew,
                                                                          int nrhs) {
   const uint3 bI = seg_tile(d.p.seg_order, d.p.seg_xg);
@@ -1010,7 +1012,17 @@ __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_pre_uv_segb(Dev d, 
   const int tid = (int)(threadIdx.x + blockDim.x * (threadIdx.y + blockDim.y * threadIdx.z));
   double* const Sb = roms_smem + tid;                        // row q-1: cf_stp*u(nstp) + cf_bak*u(indx)
   double* const Su = roms_smem + (long)(KR - 1) * nthr + tid;  // row q-1: Hz*u(nstp), the new u(indx)
-  const BufF64 Uix(Uall + (long)(indx - 1) * b.n3), Unew(Uall + (long)(nnew - 1) * b.n3);
+  const BufF64 Uix(Uall + (long)(indx - 1) * b.n3), Unew(Uall + (long)(nnew - 1) * b.n3), Hf(F.c2);
+  double hf[KR + 1], hfm[KR + 1];   // Hz_fwd(c0-1+q) of the column and of its (i-1) / (j-1) neighbour
+  auto load_hf = [&] {
+#pragma unroll
+    for (int q = 0; q < KR + 1; q++) {
+      const unsigned L = lev(c0 - 1 + q);
+      hf[q] = Hf.ld(vo, L);
+      hfm[q] = Hf.ld(vm, L);
+    }
+  };
+  if constexpr (PF) load_hf();
   double fl[KR];
   uv_spline_segb<KR>(d, sg, X, ij, nrhs, dir, fl, [&](int q, unsigned L, double h0, double h1, double u) {
     if (q >= 1 && q < KR) {   // cells c0..c0+KR-2 (q is a constant of the unrolled load loop)
@@ -1019,7 +1031,7 @@ __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_pre_uv_segb(Dev d, 
     }
   });
   __builtin_amdgcn_sched_barrier(0);   // the viscosity phase's loads stay out of the spline phase
-  const BufF64 rr(dir == 0 ? F.ru : F.rv), Akv(F.Akv), Wi(F.Wi), Hf(F.c2), Hb(F.c3);
+  const BufF64 rr(dir == 0 ? F.ru : F.rv), Akv(F.Akv), Wi(F.Wi), Hb(F.c3);
   const double sstr = dir == 0 ? F.sustr[ij] : F.svstr[ij];
   const double DC0 = c.dtau * 0.25 * (F.pm[ij] + F.pm[ij - s]) * (F.pn[ij] + F.pn[ij - s]);
   auto rhs = [&](int p) {
@@ -1031,13 +1043,7 @@ __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_pre_uv_segb(Dev d, 
     const double v = 0.5 * (Hb.ld(vo, o) + Hb.ld(vm, o)) * ub + DC0 * r;
     return k == N ? v + c.dtau * sstr : v;
   };
-  double hf[KR + 1], hfm[KR + 1];   // Hz_fwd(c0-1+q) of the column and of its (i-1) / (j-1) neighbour
-#pragma unroll
-  for (int q = 0; q < KR + 1; q++) {
-    const unsigned L = lev(c0 - 1 + q);
-    hf[q] = Hf.ld(vo, L);
-    hfm[q] = Hf.ld(vm, L);
-  }
+  if constexpr (!PF) load_hf();
   auto fcw = [&](int q, double& fc, double& wc) {   // interface c0-1+q (0 at the bottom and the surface)
     const int r = c0 - 1 + q;
     const unsigned w = (unsigned)min(max(r, 1), N - 1) * lv;
@@ -1084,7 +1090,9 @@ static size_t pre_uv_seg_lds_bytes(unsigned nthr) {
 void setup_pre_uv_seg() {
   (void)hipFuncSetAttribute((const void*)k_pre_uv_seg<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)pre_uv_seg_lds_bytes(kSegBlock * kSegJMax));
-  (void)hipFuncSetAttribute((const void*)k_pre_uv_segb, hipFuncAttributeMaxDynamicSharedMemorySize,
+  (void)hipFuncSetAttribute((const void*)k_pre_uv_segb<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)pre_uv_seg_lds_bytes(kSegBlock * kSegJMax));
+  (void)hipFuncSetAttribute((const void*)k_pre_uv_segb<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)pre_uv_seg_lds_bytes(kSegBlock * kSegJMax));
 }
 
@@ -1205,8 +1213,11 @@ void launch_pre_step3d(const Dev& d, hipStream_t s, const Tlev& t, bool uv_done,
   if (d.p.colseg) {
     const dim3 gs = seg_uv_grid(d, RI, d.p.seg_jrows), bs(kCX, seg_waves(b.N), d.p.seg_jrows);
     ktimer_mark(s, kTimedPreUvSeg, 0);
-    if (d.p.preuv_lds && d.p.uv_adv && t.nrhs == t.nstp && (d.p.seg_buf & 128))
-      hipLaunchKernelGGL(k_pre_uv_segb, gs, bs, pre_uv_seg_lds_bytes(bs.x * bs.y * bs.z), s, d, RI, c, t.nstp, t.nnew,
+    if (d.p.preuv_lds && d.p.uv_adv && t.nrhs == t.nstp && (d.p.seg_buf & 128) && (d.p.seg_buf & 256))
+      hipLaunchKernelGGL(k_pre_uv_segb<true>, gs, bs, pre_uv_seg_lds_bytes(bs.x * bs.y * bs.z), s, d, RI, c, t.nstp,
+                         t.nnew, t.nrhs);
+    else if (d.p.preuv_lds && d.p.uv_adv && t.nrhs == t.nstp && (d.p.seg_buf & 128))
+      hipLaunchKernelGGL(k_pre_uv_segb<false>, gs, bs, pre_uv_seg_lds_bytes(bs.x * bs.y * bs.z), s, d, RI, c, t.nstp, t.nnew,
                          t.nrhs);
     else if (d.p.preuv_lds && d.p.uv_adv && t.nrhs == t.nstp)
       hipLaunchKernelGGL(k_pre_uv_seg<true>, gs, bs, pre_uv_seg_lds_bytes(bs.x * bs.y * bs.z), s, d, RI, c, t.nstp,

@@ -120,7 +120,11 @@ constexpr int kPQ = (kPXN + kPYN + kBX * kBY - 1) / (kBX * kBY);
 // fetch the same bytes (the per-cell kernel is bound by that instruction rate,
 // DESIGN.md section 4).  Cells outside -1..Lm+2 / -1..Mm+2 read as 0, as in
 // the 8-B form: bit-identical.
-template <bool FUSE, int TY = kBY, bool L16 = false>
+// BUF (8-B form only, Params::prs_buf): the windows through raw-buffer loads,
+// the entry's column in a 32-bit VGPR offset and the level in an SGPR
+// (a window entry outside the grid takes kBufOff and reads 0): no 64-bit
+// address arithmetic per entry.  Bit-identical.
+template <bool FUSE, int TY = kBY, bool L16 = false, bool BUF = false>
 __global__ void __launch_bounds__(kBX * TY, L16 && TY == kBY ? 5 : 1) k_prsgrd_uv(Dev d, Range R, int split, int imin, int imax, int jmin, int jmax,
                                                    UVBounds ub, int up, int nrhs) {
   const uint3 bI = h_tile(d.p.tile_grp);
@@ -177,6 +181,13 @@ __global__ void __launch_bounds__(kBX * TY, L16 && TY == kBY ? 5 : 1) k_prsgrd_u
           if (!hi) { wz[m].y = 0.0; wr[m].y = 0.0; wq[m].y = 0.0; }
         }
       }
+    } else if (BUF) {
+      const int i = i0 - 2 + q % PWW, j = j0 - 2 + q / PWW;
+      const bool ok = q < WN && i >= -1 && i <= b.Lm + 2 && j <= b.Mm + 2;
+      const unsigned vq = ok ? (unsigned)IJ(b, i, j) * 8u : kBufOff, sk = (unsigned)kk * 8u;
+      wz[m].x = BufF64(F.z_r).ld(vq, sk);
+      wr[m].x = BufF64(R1).ld(vq, sk);
+      if (split) wq[m].x = BufF64(F.qp1).ld(vq, sk);
     } else if (q < WN) {
       const int i = i0 - 2 + q % PWW, j = j0 - 2 + q / PWW;
       if (i >= -1 && i <= b.Lm + 2 && j <= b.Mm + 2) {
@@ -245,6 +256,14 @@ __global__ void __launch_bounds__(kBX * TY, L16 && TY == kBY ? 5 : 1) k_prsgrd_u
         wFU[r] = ok ? *reinterpret_cast<const double2*>(F.FlxU + oo + kk) : z2;
         wFV[r] = ok ? *reinterpret_cast<const double2*>(F.FlxV + oo + kk) : z2;
         if (!hi) { wU[r].y = 0.0; wV[r].y = 0.0; wFU[r].y = 0.0; wFV[r].y = 0.0; }
+      } else if (BUF) {
+        const int ii = i0 - 2 + q % kUVW, jj = j0 - 2 + q / kUVW;
+        const bool ok = q < UW && ii >= -1 && ii <= b.Lm + 2 && jj >= -1 && jj <= b.Mm + 2;
+        const unsigned vq = ok ? (unsigned)IJ(b, ii, jj) * 8u : kBufOff, sk = (unsigned)kk * 8u;
+        wU[r].x = BufF64(F.u + (long)(nrhs - 1) * b.n3).ld(vq, sk);
+        wV[r].x = BufF64(F.v + (long)(nrhs - 1) * b.n3).ld(vq, sk);
+        wFU[r].x = BufF64(F.FlxU).ld(vq, sk);
+        wFV[r].x = BufF64(F.FlxV).ld(vq, sk);
       } else {
         const int ii = i0 - 2 + q % kUVW, jj = j0 - 2 + q / kUVW;
         const bool ok = q < UW && ii >= -1 && ii <= b.Lm + 2 && jj >= -1 && jj <= b.Mm + 2;
@@ -669,6 +688,9 @@ void launch_prsgrd(const Dev& d, hipStream_t s, const Tlev& t, int uv_up, bool p
   else if (uv_up >= 0 && d.p.prs_ty == 8)
     hipLaunchKernelGGL((k_prsgrd_uv<true, 8>), grid3_ty(R2, b.N, 8), dim3(kBX, 8), 0, s, d, R2, split, imin, imax, jmin,
                        jmax, uv_bounds(b), uv_up, t.nrhs);
+  else if (uv_up >= 0 && d.p.prs_buf)
+    hipLaunchKernelGGL((k_prsgrd_uv<true, kBY, false, true>), grid3_of(R2, b.N), dim3(kBX, kBY), 0, s, d, R2, split, imin,
+                       imax, jmin, jmax, uv_bounds(b), uv_up, t.nrhs);
   else if (uv_up >= 0)
     hipLaunchKernelGGL(k_prsgrd_uv<true>, grid3_of(R2, b.N), dim3(kBX, kBY), 0, s, d, R2, split, imin, imax, jmin, jmax,
                        uv_bounds(b), uv_up, t.nrhs);

@@ -68,7 +68,8 @@ struct Params {
   int h_ty;       // tile rows of the hoisted horizontal kernels: 4 or 8 (ROMS_GPU_HTY)
   int h_jc;       // rows per block of the j-marching horizontal kernels (multiple of 4; ROMS_GPU_HJC, 0: 64 x h_ty tiles)
   int prs_ty;     // tile rows of k_prsgrd_uv: 4 or 8 (ROMS_GPU_PRS_TY)
-  int ld16;       // padded pitch: LDS windows read two doubles per lane (16-B loads; ROMS_GPU_LD16=0: 8-B)
+  int ld16;
+  int prs_buf;    // k_prsgrd_uv windows through buffer loads (ROMS_GPU_PRS_BUF)       // padded pitch: LDS windows read two doubles per lane (16-B loads; ROMS_GPU_LD16=0: 8-B)
   int visc_stg;   // visc3d: raw u/v/Hz windows staged in LDS per level (default; ROMS_GPU_VISC_STG=0: per-point loads)
   int t3dmix_stg; // t3dmix (two tracers): Hz/T/S windows staged in LDS per level (default; ROMS_GPU_T3DMIX_STG=0: per-point loads)
   int kpp_ty;     // k_kpp_int: 4 (default) staged Rig windows on 64x4 blocks, 8 on 64x8, 43 64x4 at 3 waves/SIMD, 0 one row per block (ROMS_GPU_KPP_TY)
