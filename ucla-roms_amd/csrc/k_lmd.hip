@@ -26,6 +26,7 @@
 // Every expression keeps the reference's operation order (FP64, no FMA
 // contraction); integer powers are products, real powers pow().
 #include <cmath>
+#include <type_traits>
 
 #include "k_common.h"
 
@@ -214,7 +215,19 @@ __global__ void __launch_bounds__(64, 4) k_kpp_ext(Dev d, Range E, int tind, int
   const int N = b.N;
   const long n2 = b.n2, ij = IJ(b, i, j), sj = b.nx2;
   const double g = P.g, vonKar = P.vonKar, Ri_inv = 1. / kRicr;
-  const C FC = ColMake<C>::at(d, 0, 0, ij);
+  // FC(0:N): the LDS column, or the global scratch column through the
+  // column's buffer offset (ColGlb: no 64-bit address per level)
+  const C FCc = ColMake<C>::at(d, 0, 0, ij);
+  const BufF64 FCg(d.f.colscr);
+  constexpr bool kGlb = std::is_same<C, ColGlb>::value;
+  auto fc_set = [&](int k, double v) {
+    if constexpr (kGlb) FCg.st(v, (unsigned)ij * 8u, (unsigned)k * (unsigned)n2 * 8u);
+    else FCc[k] = v;
+  };
+  auto fc_get = [&](int k) {
+    if constexpr (kGlb) return FCg.ld((unsigned)ij * 8u, (unsigned)k * (unsigned)n2 * 8u);
+    else return FCc[k];
+  };
   // alfabeta.F:46-78 at t(N,nstp); Bo, Bosol, ustar (lmd_kpp.F:154-181)
   double alpha, beta;
   const double Tt = F.t[ij + (long)(N - 1) * n2 + (long)(nstp - 1) * b.n3];
@@ -255,45 +268,43 @@ __global__ void __launch_bounds__(64, 4) k_kpp_ext(Dev d, Range E, int tind, int
   F.lmd_Bosol[ij] = Bosol;
   F.lmd_ustar[ij] = ustar;
 
-  const double* __restrict__ U = F.u + (long)(tind - 1) * b.n3 + ij;
-  const double* __restrict__ V = F.v + (long)(tind - 1) * b.n3 + ij;
-  const double* __restrict__ Hz = F.Hz + ij;
-  const double* __restrict__ zr = F.z_r + ij;
-  const double* __restrict__ zw = F.z_w + ij;
-  const double* __restrict__ bvf = F.bvf + ij;
-  const double* __restrict__ sw = F.swr_frac + ij;
-  double* __restrict__ rig = F.lmd_rig + ij;
-  const double zwN = zw[(long)N * n2], zw0 = zw[0];
+  // buffer accesses: the column (and its i+1 / j+1 neighbour) in VGPR
+  // offsets, the level in an SGPR (no 64-bit address per level)
+  const unsigned vo = (unsigned)ij * 8u, vx = vo + 8u, vy = vo + (unsigned)sj * 8u, lv = (unsigned)n2 * 8u;
+  const BufF64 U(F.u + (long)(tind - 1) * b.n3), V(F.v + (long)(tind - 1) * b.n3), Hz(F.Hz), zr(F.z_r), zw(F.z_w),
+      bvf(F.bvf), sw(F.swr_frac), rig(F.lmd_rig);
+  const double zwN = zw.ld(vo, (unsigned)N * lv), zw0 = zw.ld(vo, 0);
   const double eh = kEpssfc * hbl0, eb = kEpssfc * bbl0;
   const double eh2 = eh * eh, eb2 = eb * eb;
 
   // k = N: FC(N) = 0, Cr(N) = Vtsq(N)
   auto vtsq = [&](int k, double zrk) {
-    const double swk = sw[(long)k * n2], swm = sw[(long)(k - 1) * n2];
+    const double swk = sw.ld(vo, (unsigned)k * lv), swm = sw.ld(vo, (unsigned)(k - 1) * lv);
     const double swdk_r = sqrt(swk * swm);
     const double zscale = zwN - zrk;
     const double Bfsfc = Bo + Bosol * (1. - swdk_r);
     const double ws = wscale_ws(zscale, Bfsfc, hbl0, ustar, rm, vonKar);
-    return 1.8 * kc.Vtc * ws * sqrt(dmax(1.e-5, bvf[(long)(k - 1) * n2]));
+    return 1.8 * kc.Vtc * ws * sqrt(dmax(1.e-5, bvf.ld(vo, (unsigned)(k - 1) * lv)));
   };
-  double u0p = U[(long)(N - 1) * n2], u1p = U[(long)(N - 1) * n2 + 1];  // level k+1
-  double v0p = V[(long)(N - 1) * n2], v1p = V[(long)(N - 1) * n2 + sj];
-  double hzp = Hz[(long)(N - 1) * n2], zrp = zr[(long)(N - 1) * n2];
+  const unsigned oN = (unsigned)(N - 1) * lv;
+  double u0p = U.ld(vo, oN), u1p = U.ld(vx, oN);  // level k+1
+  double v0p = V.ld(vo, oN), v1p = V.ld(vy, oN);
+  double hzp = Hz.ld(vo, oN), zrp = zr.ld(vo, oN);
   double FCk = 0.;
-  FC[N] = 0.;
+  fc_set(N, 0.);
   double Crp = FCk + vtsq(N, zrp);
   int kbls = Crp < 0. ? N : 0;
   double cr_k = Crp, cr_kp = 0., zr_k = zrp, zr_kp = 0.;
   for (int k = N - 1; k >= 1; k--) {
-    const long o = (long)(k - 1) * n2;
-    const double u0 = U[o], u1 = U[o + 1], v0 = V[o], v1 = V[o + sj];
-    const double hz = Hz[o], zrk = zr[o], zwk = zw[(long)k * n2], bk = bvf[(long)k * n2];
+    const unsigned o = (unsigned)(k - 1) * lv, ow = (unsigned)k * lv;
+    const double u0 = U.ld(vo, o), u1 = U.ld(vx, o), v0 = V.ld(vo, o), v1 = V.ld(vy, o);
+    const double hz = Hz.ld(vo, o), zrk = zr.ld(vo, o), zwk = zw.ld(vo, ow), bk = bvf.ld(vo, ow);
     // raw gradient Richardson number (lmd_vmix.F:157-165), LMD_RIMIX only
     if (P.lmd_rimix) {
       const double cff = 0.5 / (zrp - zrk);
       const double dudz = cff * (u0p - u0 + u1p - u1);
       const double dvdz = cff * (v0p - v0 + v1p - v1);
-      rig[(long)k * n2] = bk / (kRi0 * dmax(dudz * dudz + dvdz * dvdz, 1.E-10));
+      rig.st(bk / (kRi0 * dmax(dudz * dudz + dvdz * dvdz, 1.E-10)), vo, ow);
     }
     // bulk Richardson integral (lmd_kpp.F:200-215)
     {
@@ -304,7 +315,7 @@ __global__ void __launch_bounds__(64, 4) k_kpp_ext(Dev d, Range E, int tind, int
       const double dv = v0p + v1p - v0 - v1;
       const double hh = hz + hzp;
       FCk = FCk + Kern * (0.5 * (du * du + dv * dv) / hh - 0.5 * hh * (Ri_inv * bk + kC_Ek * ff * ff));
-      FC[k] = FCk;
+      fc_set(k, FCk);
     }
     const double Cr = FCk + vtsq(k, zrk);
     if (kbls == 0 && Cr < 0.) {
@@ -314,7 +325,8 @@ __global__ void __launch_bounds__(64, 4) k_kpp_ext(Dev d, Range E, int tind, int
     Crp = Cr;
     u0p = u0; u1p = u1; v0p = v0; v1p = v1; hzp = hz; zrp = zrk;
   }
-  // FC(0) (lmd_kpp.F:216-229): level-1 values are the carried ones
+  // FC(0) (lmd_kpp.F:216-229): level-1 values are the carried ones, FCk is FC(1)
+  double fc0;
   {
     const double hz1 = hzp;
     const double z_bl = zw0 + 0.25 * hz1;
@@ -322,26 +334,27 @@ __global__ void __launch_bounds__(64, 4) k_kpp_ext(Dev d, Range E, int tind, int
     const double cff_up = cu * cu, cff_dn = cd * cd;
     const double Kern = cff_up * cff_dn / ((cff_up + eh2) * (cff_dn + eb2));
     const double su = u0p + u1p, sv = v0p + v1p;
-    FC[0] = FC[1] + Kern * (0.5 * (su * su + sv * sv) / hz1 - 0.5 * hz1 * (Ri_inv * bvf[n2] + kC_Ek * ff * ff));
+    fc0 = FCk + Kern * (0.5 * (su * su + sv * sv) / hz1 - 0.5 * hz1 * (Ri_inv * bvf.ld(vo, lv) + kC_Ek * ff * ff));
+    fc_set(0, fc0);
   }
   double hbl;
   if (kbls > 0) {
-    if (kbls == N) hbl = zwN - zr[(long)(N - 1) * n2];
+    if (kbls == N) hbl = zwN - zr.ld(vo, oN);
     else hbl = zwN - (zr_k * cr_kp - zr_kp * cr_k) / (cr_kp - cr_k);
   } else {
     hbl = zwN - zw0;
   }
   F.lmd_hbl[ij] = hbl * rm;
   // bottom layer (lmd_kpp.F:276-305): Cr(k) = FC(k) - FC(0), first k upward with Cr > 0
-  const double FC0 = FC[0];
+  const double FC0 = fc0;
   double bbl = zwN - zw0;
   double crm = 0.;
   for (int k = 1; k <= N; k++) {
-    const double cr = FC[k] - FC0;
+    const double cr = fc_get(k) - FC0;
     if (cr > 0.) {
-      if (k == 1) bbl = zr[0] - zw0;
+      if (k == 1) bbl = zr.ld(vo, 0) - zw0;
       else {
-        const double zrm = zr[(long)(k - 2) * n2], zrk = zr[(long)(k - 1) * n2];
+        const double zrm = zr.ld(vo, (unsigned)(k - 2) * lv), zrk = zr.ld(vo, (unsigned)(k - 1) * lv);
         bbl = (zrm * cr - zrk * crm) / (cr - crm) - zw0;
       }
       break;
@@ -392,19 +405,21 @@ __global__ void __launch_bounds__(TY > 0 ? kCX * TY : 64, MW) k_kpp_int(Dev d, R
     hbl = 0.5 * (hbl + F.hbls[ij]);
     bbl = 0.5 * (bbl + F.hbbl[ij]);
   }
-  const double* __restrict__ zw = F.z_w + ij;
-  const double* __restrict__ sw = F.swr_frac + ij;
-  const double zwN = zw[(long)N * n2], zw0 = zw[0];
+  // buffer accesses: the column in one VGPR offset, the level in an SGPR
+  const unsigned vo = (unsigned)ij * 8u, lv = (unsigned)n2 * 8u;
+  const BufF64 zw(F.z_w), sw(F.swr_frac);
+  const double zwN = zw.ld(vo, (unsigned)N * lv), zw0 = zw.ld(vo, 0);
   // kbls and the buoyancy forcing at the boundary-layer depth (lmd_kpp.F:348-372)
   int kbls = N;
   for (int k = N - 1; k >= 1; k--)
-    if (zw[(long)k * n2] > zwN - hbl) kbls = k;
+    if (zw.ld(vo, (unsigned)k * lv) > zwN - hbl) kbls = k;
   const double Bo = F.lmd_Bo[ij], Bosol = F.lmd_Bosol[ij], ustar = F.lmd_ustar[ij];
   double Bfsfc;
   {
     const double z_bl = zwN - hbl;
-    const double swm = sw[(long)(kbls - 1) * n2], swk = sw[(long)kbls * n2];
-    const double zwk = zw[(long)kbls * n2], zwm = zw[(long)(kbls - 1) * n2];
+    const unsigned ok = (unsigned)kbls * lv, om = (unsigned)(kbls - 1) * lv;
+    const double swm = sw.ld(vo, om), swk = sw.ld(vo, ok);
+    const double zwk = zw.ld(vo, ok), zwm = zw.ld(vo, om);
     if (swm > 0.)
       Bfsfc = Bo + Bosol * (1. - swm * swk * (zwk - zwm) / (swk * (zwk - z_bl) + swm * (z_bl - zwm)));
     else
@@ -422,6 +437,16 @@ __global__ void __launch_bounds__(TY > 0 ? kCX * TY : 64, MW) k_kpp_int(Dev d, R
 
   // raw interior Kv, Kt (= Ks) at level k from the smoothed Rig (lmd_vmix.F:249-272, 338-353)
   const double* __restrict__ rig = F.lmd_rig;
+  const BufF64 Rg(F.lmd_rig);
+  // the staged window's entries of this thread: column offsets (level-independent)
+  unsigned wo[STG ? WQ : 1];
+  if constexpr (STG) {
+#pragma unroll
+    for (int m = 0; m < WQ; m++) {
+      const int q = tid + m * NTH;
+      wo[m] = q < WN ? (unsigned)ec.at(b, wi0 + q % WW, wj0 + q / WW) * 8u : kBufOff;
+    }
+  }
   const bool rimix = P.lmd_rimix, convec = P.lmd_convec, nonlocal = P.lmd_nonlocal;
   // raw_k split into its loads (rload) and its arithmetic (rcomp), so the
   // loads of level k+2 can be issued ahead of level k's stores (which would
@@ -435,14 +460,11 @@ __global__ void __launch_bounds__(TY > 0 ? kCX * TY : 64, MW) k_kpp_int(Dev d, R
     L.k = k;
     if (STG) {   // this thread's entries of the level's window (rimix is on)
 #pragma unroll
-      for (int m = 0; m < WQ; m++) {
-        const int q = tid + m * NTH;
-        L.win[m] = q < WN ? rig[(long)k * n2 + ec.at(b, wi0 + q % WW, wj0 + q / WW)] : 0.0;
-      }
+      for (int m = 0; m < WQ; m++) L.win[m] = Rg.ld(wo[m], (unsigned)k * lv);   // kBufOff entries read 0
     } else if (rimix) {
       load3x3(b, ec, rig + (long)k * n2, i, j, L.r);
     }
-    L.zw = zw[(long)k * n2];
+    L.zw = zw.ld(vo, (unsigned)k * lv);
     if (dd) {
       const long o = (long)(k - 1) * n2;
       L.t0 = Tt[o]; L.t1 = Tt[o + n2]; L.s0 = St[o]; L.s1 = St[o + n2];
@@ -492,10 +514,8 @@ __global__ void __launch_bounds__(TY > 0 ? kCX * TY : 64, MW) k_kpp_int(Dev d, R
       ks = ks * mult;
     }
   };
-  double* __restrict__ Akv = F.Akv + ij;
-  double* __restrict__ AktT = F.Akt + ij;
-  double* __restrict__ AktS = F.Akt + b.n3w + ij;
-  double* __restrict__ ghat = F.ghat + ij;
+  const BufF64 Akv(F.Akv), AktT(F.Akt), AktS(F.Akt + b.n3w), ghat(F.ghat);
+  const unsigned vs = act ? vo : kBufOff;   // lanes past the range store nothing
   const bool wet = rm > 0.5;
   // KPP shape functions (lmd_kpp.F:374-446), BKPP (:447-495), masked copy (:496-528)
   auto finish = [&](int k, double Kv, double Kt, double Ks, double zwk) {
@@ -520,8 +540,8 @@ __global__ void __launch_bounds__(TY > 0 ? kCX * TY : 64, MW) k_kpp_int(Dev d, R
       Ks = sqrt(a * a + q * q);
       if (Bfsfc < 0.) gh = -(kc.Cg * ssgm * ((1. - ssgm) * (1. - ssgm)));
     }
-    if (!act) return;
-    if (nonlocal) ghat[(long)k * n2] = gh;   // LMD_NONLOCAL (lmd_kpp.F:436-446)
+    const unsigned ow = (unsigned)k * lv;
+    if (nonlocal) ghat.st(gh, vs, ow);   // LMD_NONLOCAL (lmd_kpp.F:436-446)
     const double sgmb = (zwk - zw0 + Zob) / (bbl + Zob);
     if (sgmb < 1.) {
       const double cff1 = sgmb * ((1. - sgmb) * (1. - sgmb));
@@ -531,9 +551,9 @@ __global__ void __launch_bounds__(TY > 0 ? kCX * TY : 64, MW) k_kpp_int(Dev d, R
       Kt = sqrt(Kt * Kt + q * q);
       Ks = sqrt(Ks * Ks + q * q);
     }
-    Akv[(long)k * n2] = wet ? Kv : 0.;
-    AktT[(long)k * n2] = wet ? Kt : 0.;
-    if (b.nTS > 1) AktS[(long)k * n2] = wet ? Ks : 0.;
+    Akv.st(wet ? Kv : 0., vs, ow);
+    AktT.st(wet ? Kt : 0., vs, ow);
+    if (b.nTS > 1) AktS.st(wet ? Ks : 0., vs, ow);
   };
   // bottom-up stream: padding (lmd_vmix.F:359-370) and the in-place ascending
   // 1-2-1 filter Kv(k) = 0.5 Kv(k) + 0.25 Kv(k-1)[filtered] + 0.25 Kv(k+1)[raw] + bak

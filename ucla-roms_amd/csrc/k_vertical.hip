@@ -633,9 +633,9 @@ bool launch_omega(const Dev& d, hipStream_t s, const Tlev& t, double hcff) {
 // completes P(1).  Expressions and order of k_prsgrd_P (bit-identical).
 struct PColumn {
   double g, grho, HalfGRho, qp2, zwN, ptide;
-  bool split, tides, doP;
-  double* Pp;
-  long n2;
+  bool split, tides;
+  BufF64 Pb{nullptr};   // P, stored through the column's buffer offset (kBufOff: a column outside doP)
+  unsigned vP, lv;
   int N;
   double zC, rC, qC;                     // level m (pending)
   double eZk, eRk, dZ1, dR1, P1, z1, v1;
@@ -685,7 +685,7 @@ struct PColumn {
                             OneFifth * ((dR1 - dRk) * (z1 - zC - OneTwelfth * (dZ1 + dZk)) -
                                         (dZ1 - dZk) * (v1 - v0 - OneTwelfth * (dR1 + dRk))));
     }
-    if (doP) Pp[(long)(m - 1) * n2] = Pk;
+    Pb.st(Pk, vP, (unsigned)(m - 1) * lv);
     P1 = Pk;
     dZ1 = dZk; dR1 = dRk;
     eZk = eZm; eRk = eRm;
@@ -702,10 +702,11 @@ __device__ __forceinline__ PColumn p_column(const Dev& d, int i, int j, long ij,
   const Bounds& b = d.b;
   PColumn c;
   c.g = d.p.g; c.grho = d.p.g / d.p.rho0; c.HalfGRho = 0.5 * c.grho; c.qp2 = d.p.qp2;
-  c.split = split; c.tides = d.p.tides != 0; c.N = b.N; c.n2 = b.n2;
-  // k_prsgrd_P's range (0..Lm x 0..Mm) and its doP columns
-  c.doP = i >= 0 && i <= b.Lm && j >= 0 && j <= b.Mm && i >= b.istrU - 1 && i <= b.iend;
-  c.Pp = d.f.P + ij;
+  c.split = split; c.tides = d.p.tides != 0; c.N = b.N; c.lv = (unsigned)b.n2 * 8u;
+  // k_prsgrd_P's range (0..Lm x 0..Mm) and its P columns
+  const bool doP = i >= 0 && i <= b.Lm && j >= 0 && j <= b.Mm && i >= b.istrU - 1 && i <= b.iend;
+  c.Pb = BufF64(d.f.P);
+  c.vP = doP ? (unsigned)ij * 8u : kBufOff;
   c.zwN = d.f.z_w[ij + (long)b.N * b.n2];
   c.ptide = c.tides ? d.f.ptide[ij] : 0.0;
   return c;
@@ -771,6 +772,9 @@ __global__ void __launch_bounds__(256) k_rho_eos_linear(Dev d, Range R, int tidx
   F.rhoS[ij] = 2.0 * cff * cff * cff1 * rhoS;
 }
 
+#ifndef ROMS_RHO_UNROLL
+#define ROMS_RHO_UNROLL 4
+#endif
 template <bool kP>
 __global__ void __launch_bounds__(256) k_rho_eos_split(Dev d, Range R, int tidx) {
   ROMS_IJ_OR_RETURN(R)
@@ -795,39 +799,39 @@ __global__ void __launch_bounds__(256) k_rho_eos_split(Dev d, Range R, int tidx)
   // and k+1 (:270-300) and the rhoA/rhoS column integrals (:365-395), each
   // expression in the reference's order; restrict pointers let the loads of
   // the next levels issue ahead of this level's stores
-  const double* __restrict__ T = F.t + (long)(tidx - 1) * b.n3 + ij;
-  const double* __restrict__ Sa = T + 3 * b.n3;
-  const double* __restrict__ zr = F.z_r + ij;
-  const double* __restrict__ Hz = F.Hz + ij;
-  double* __restrict__ rho1 = F.rho1 + ij;
-  double* __restrict__ qp1 = F.qp1 + ij;
-  double* __restrict__ bvf = F.bvf + ij;
+  // buffer accesses: the column in one VGPR offset, the level in an SGPR
+  const unsigned vo = (unsigned)ij * 8u, lv = (unsigned)n2 * 8u;
+  const BufF64 T(F.t + (long)(tidx - 1) * b.n3), Sa(F.t + (long)(tidx - 1) * b.n3 + 3 * b.n3), zr(F.z_r), Hz(F.Hz),
+      rho1(F.rho1), qp1(F.qp1), bvf(F.bvf);
   const bool lmd = P.lmd;
   const double gr = P.g / rho0;
   double r1p = 0.0, q1p = 0.0, zrp = 0.0;  // level k+1
-  double rhoA = 0.0, rhoS = 0.0;
+  double rhoA = 0.0, rhoS = 0.0, bvN1 = 0.0, bv1 = 0.0;
   PColumn pc;
   if constexpr (kP) pc = p_column(d, i, j, ij, true);
-#pragma unroll 4
+#pragma unroll ROMS_RHO_UNROLL
   for (int k = N; k >= 1; k--) {
-    const long o = (long)(k - 1) * n2;
-    Tt = T[o];
-    Ts = Sa[o];
+    const unsigned o = (unsigned)(k - 1) * lv;
+    Tt = T.ld(vo, o);
+    Ts = Sa.ld(vo, o);
     sqrtTs = sqrt(dmax(0.0, Ts));
     const double r1 = (dr00 + Tt * (r01 + Tt * (r02 + Tt * (r03 + Tt * (r04 + Tt * r05)))) +
                        Ts * (r10 + Tt * (r11 + Tt * (r12 + Tt * (r13 + Tt * r14))) + sqrtTs * (rS0 + Tt * (rS1 + Tt * rS2)) +
                              Ts * r20)) *
                       rm;
-    rho1[o] = r1;
+    rho1.st(r1, vo, o);
     const double K0 = Tt * (K01 + Tt * (K02 + Tt * (K03 + Tt * K04))) +
                       Ts * (K10 + Tt * (K11 + Tt * (K12 + Tt * K13)) + sqrtTs * (KS0 + Tt * (KS1 + Tt * KS2)));
     const double q1 = 0.1 * (rho0 + r1) * (K0_Duk - K0) / ((K00 + K0) * (K00 + K0_Duk)) * rm;
-    qp1[o] = q1;
-    const double zrk = zr[o], hz = Hz[o];
+    qp1.st(q1, vo, o);
+    const double zrk = zr.ld(vo, o), hz = Hz.ld(vo, o);
     if constexpr (kP) pc.level(k, zrk, r1, q1);
     if (lmd && k < N) {
       const double dpth = -0.5 * (zrp + zrk);
-      bvf[(long)k * n2] = -gr * (r1p - r1 + (q1p - q1) * dpth * (1.0 - qp2 * dpth)) / (zrp - zrk) * rm;
+      const double bv = -gr * (r1p - r1 + (q1p - q1) * dpth * (1.0 - qp2 * dpth)) / (zrp - zrk) * rm;
+      bvf.st(bv, vo, (unsigned)k * lv);
+      bvN1 = k == N - 1 ? bv : bvN1;   // the boundary copies below
+      bv1 = k == 1 ? bv : bv1;
     }
     const double dpth = -zrk;
     const double cff = hz * (r1 + q1 * dpth * (1.0 - qp2 * dpth));
@@ -841,9 +845,9 @@ __global__ void __launch_bounds__(256) k_rho_eos_split(Dev d, Range R, int tidx)
     r1p = r1; q1p = q1; zrp = zrk;
   }
   if constexpr (kP) pc.last();
-  if (lmd) {
-    bvf[(long)N * n2] = bvf[(long)(N - 1) * n2];
-    bvf[0] = bvf[n2];
+  if (lmd && N >= 2) {   // bvf(N) = bvf(N-1), bvf(0) = bvf(1) (rho_eos.F:300-305)
+    bvf.st(bvN1, vo, (unsigned)N * lv);
+    bvf.st(bv1, vo, 0);
   }
   const double cff1 = 1.0 / rho0;
   const double cff = 1.0 / (F.z_w[ij + (long)N * n2] - F.z_w[ij]);
