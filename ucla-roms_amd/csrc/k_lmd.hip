@@ -206,8 +206,11 @@ __global__ void __launch_bounds__(256) k_swr_frac(Dev d, Range R) {
 }
 
 // ---- pass 1: extended range ----
+#ifndef ROMS_KPP_EXT_WAVES
+#define ROMS_KPP_EXT_WAVES 3   // waves per SIMD the register budget is cut for (the next level in flight: 3)
+#endif
 template <class C>
-__global__ void __launch_bounds__(64, 4) k_kpp_ext(Dev d, Range E, int tind, int nstp, KppConst kc) {
+__global__ void __launch_bounds__(64, ROMS_KPP_EXT_WAVES) k_kpp_ext(Dev d, Range E, int tind, int nstp, KppConst kc) {
   ROMS_IJC_OR_RETURN(E)
   const Bounds& b = d.b;
   const Fields& F = d.f;
@@ -277,28 +280,44 @@ __global__ void __launch_bounds__(64, 4) k_kpp_ext(Dev d, Range E, int tind, int
   const double eh = kEpssfc * hbl0, eb = kEpssfc * bbl0;
   const double eh2 = eh * eh, eb2 = eb * eb;
 
-  // k = N: FC(N) = 0, Cr(N) = Vtsq(N)
-  auto vtsq = [&](int k, double zrk) {
-    const double swk = sw.ld(vo, (unsigned)k * lv), swm = sw.ld(vo, (unsigned)(k - 1) * lv);
+  // Cr(k) = FC(k) + Vtsq(k) with sw(k), sw(k-1), bvf(k-1) at the w levels
+  auto vtsq = [&](double zrk, double swk, double swm, double bm) {
     const double swdk_r = sqrt(swk * swm);
     const double zscale = zwN - zrk;
     const double Bfsfc = Bo + Bosol * (1. - swdk_r);
     const double ws = wscale_ws(zscale, Bfsfc, hbl0, ustar, rm, vonKar);
-    return 1.8 * kc.Vtc * ws * sqrt(dmax(1.e-5, bvf.ld(vo, (unsigned)(k - 1) * lv)));
+    return 1.8 * kc.Vtc * ws * sqrt(dmax(1.e-5, bm));
   };
+  // a level's inputs: u, v (and the i+1 / j+1 neighbours), Hz, z_r at rho
+  // level k, z_w at w level k, sw and bvf at w level k-1 (its w level k
+  // values are the level above's); the next level's are loaded before this
+  // level's stores, so a level costs one memory round trip, not three
+  struct Lv { double u0, u1, v0, v1, hz, zr, zw, swm, bm; };
+  auto ldlev = [&](int k, Lv& L) {
+    const unsigned o = (unsigned)(k - 1) * lv, ow = (unsigned)k * lv;
+    L.u0 = U.ld(vo, o); L.u1 = U.ld(vx, o); L.v0 = V.ld(vo, o); L.v1 = V.ld(vy, o);
+    L.hz = Hz.ld(vo, o); L.zr = zr.ld(vo, o); L.zw = zw.ld(vo, ow);
+    L.swm = sw.ld(vo, o); L.bm = bvf.ld(vo, o);
+  };
+  // k = N: FC(N) = 0, Cr(N) = Vtsq(N)
   const unsigned oN = (unsigned)(N - 1) * lv;
   double u0p = U.ld(vo, oN), u1p = U.ld(vx, oN);  // level k+1
   double v0p = V.ld(vo, oN), v1p = V.ld(vy, oN);
   double hzp = Hz.ld(vo, oN), zrp = zr.ld(vo, oN);
+  double swc = sw.ld(vo, oN), bc = bvf.ld(vo, oN);   // sw, bvf at w level k (carried down)
+  Lv cur{};
+  if (N - 1 >= 1) ldlev(N - 1, cur);
   double FCk = 0.;
   fc_set(N, 0.);
-  double Crp = FCk + vtsq(N, zrp);
+  double Crp = FCk + vtsq(zrp, sw.ld(vo, (unsigned)N * lv), swc, bc);
   int kbls = Crp < 0. ? N : 0;
   double cr_k = Crp, cr_kp = 0., zr_k = zrp, zr_kp = 0.;
   for (int k = N - 1; k >= 1; k--) {
-    const unsigned o = (unsigned)(k - 1) * lv, ow = (unsigned)k * lv;
-    const double u0 = U.ld(vo, o), u1 = U.ld(vx, o), v0 = V.ld(vo, o), v1 = V.ld(vy, o);
-    const double hz = Hz.ld(vo, o), zrk = zr.ld(vo, o), zwk = zw.ld(vo, ow), bk = bvf.ld(vo, ow);
+    Lv nxt = cur;
+    if (k > 1) ldlev(k - 1, nxt);
+    const unsigned ow = (unsigned)k * lv;
+    const double u0 = cur.u0, u1 = cur.u1, v0 = cur.v0, v1 = cur.v1;
+    const double hz = cur.hz, zrk = cur.zr, zwk = cur.zw, bk = bc;
     // raw gradient Richardson number (lmd_vmix.F:157-165), LMD_RIMIX only
     if (P.lmd_rimix) {
       const double cff = 0.5 / (zrp - zrk);
@@ -317,13 +336,15 @@ __global__ void __launch_bounds__(64, 4) k_kpp_ext(Dev d, Range E, int tind, int
       FCk = FCk + Kern * (0.5 * (du * du + dv * dv) / hh - 0.5 * hh * (Ri_inv * bk + kC_Ek * ff * ff));
       fc_set(k, FCk);
     }
-    const double Cr = FCk + vtsq(k, zrk);
+    const double Cr = FCk + vtsq(zrk, swc, cur.swm, cur.bm);
     if (kbls == 0 && Cr < 0.) {
       kbls = k;
       cr_k = Cr; cr_kp = Crp; zr_k = zrk; zr_kp = zrp;
     }
     Crp = Cr;
     u0p = u0; u1p = u1; v0p = v0; v1p = v1; hzp = hz; zrp = zrk;
+    swc = cur.swm; bc = cur.bm;
+    cur = nxt;
   }
   // FC(0) (lmd_kpp.F:216-229): level-1 values are the carried ones, FCk is FC(1)
   double fc0;

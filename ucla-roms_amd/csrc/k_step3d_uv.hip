@@ -814,9 +814,12 @@ __global__ void __launch_bounds__(256, 3) k_visc3d_stg(Dev d, Range R, int nstp)
   const int qp = threadIdx.x + threadIdx.y * kVW;              // psi (i,j); +1: (i+1,j); +kVW: (i,j+1)
   double raw[kVSQ];
   ldraw(1, raw);
+  // u, v(indx) of the lane's cell: level k+1's loaded with level k+1's
+  // window, before level k's stores (which vmcnt counts with the loads)
+  double nui = du ? Ui[ij] : 0.0, nvi = dv ? Vi[ij] : 0.0;
   for (int k = 1; k <= b.N; k++) {
     const long kk = (long)(k - 1) * b.n2;
-    const double ui = du ? Ui[ij + kk] : 0.0, vi = dv ? Vi[ij + kk] : 0.0;
+    const double ui = nui, vi = nvi;
     // every lane finished the previous level's stress reads of sRaw before
     // its second barrier, so the raw window can be overwritten here
 #pragma unroll
@@ -824,7 +827,11 @@ __global__ void __launch_bounds__(256, 3) k_visc3d_stg(Dev d, Range R, int nstp)
       const int q = tid + m * kBX * kBY;
       if (q < kVSN) sRaw[q] = raw[m];
     }
-    if (k < b.N) ldraw(k + 1, raw);
+    if (k < b.N) {
+      ldraw(k + 1, raw);
+      nui = du ? Ui[ij + kk + b.n2] : 0.0;
+      nvi = dv ? Vi[ij + kk + b.n2] : 0.0;
+    }
     __syncthreads();
 #pragma unroll
     for (int m = 0; m < kVQ; m++) {

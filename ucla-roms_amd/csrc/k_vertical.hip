@@ -775,6 +775,9 @@ __global__ void __launch_bounds__(256) k_rho_eos_linear(Dev d, Range R, int tidx
 #ifndef ROMS_RHO_UNROLL
 #define ROMS_RHO_UNROLL 4
 #endif
+#ifndef ROMS_RHO_PF
+#define ROMS_RHO_PF 4
+#endif
 template <bool kP>
 __global__ void __launch_bounds__(256) k_rho_eos_split(Dev d, Range R, int tidx) {
   ROMS_IJ_OR_RETURN(R)
@@ -809,11 +812,28 @@ __global__ void __launch_bounds__(256) k_rho_eos_split(Dev d, Range R, int tidx)
   double rhoA = 0.0, rhoS = 0.0, bvN1 = 0.0, bv1 = 0.0;
   PColumn pc;
   if constexpr (kP) pc = p_column(d, i, j, ij, true);
+  // the next levels' inputs are loaded before this level's stores (a ring
+  // of ROMS_RHO_PF levels), so the stores -- counted with the loads by
+  // vmcnt -- do not hold back the loads below them
+  constexpr int PF = ROMS_RHO_PF;
+  double pT[PF], pS[PF], pZ[PF], pH[PF];
+#pragma unroll
+  for (int q = 0; q < PF; q++) {
+    const unsigned o = (unsigned)max(N - 1 - q, 0) * lv;
+    pT[q] = T.ld(vo, o); pS[q] = Sa.ld(vo, o); pZ[q] = zr.ld(vo, o); pH[q] = Hz.ld(vo, o);
+  }
 #pragma unroll ROMS_RHO_UNROLL
   for (int k = N; k >= 1; k--) {
     const unsigned o = (unsigned)(k - 1) * lv;
-    Tt = T.ld(vo, o);
-    Ts = Sa.ld(vo, o);
+    Tt = pT[0];
+    Ts = pS[0];
+    const double zrk = pZ[0], hz = pH[0];
+#pragma unroll
+    for (int q = 0; q + 1 < PF; q++) { pT[q] = pT[q + 1]; pS[q] = pS[q + 1]; pZ[q] = pZ[q + 1]; pH[q] = pH[q + 1]; }
+    {
+      const unsigned on = (unsigned)max(k - 1 - PF, 0) * lv;   // level k - PF (clamped; unused past the bottom)
+      pT[PF - 1] = T.ld(vo, on); pS[PF - 1] = Sa.ld(vo, on); pZ[PF - 1] = zr.ld(vo, on); pH[PF - 1] = Hz.ld(vo, on);
+    }
     sqrtTs = sqrt(dmax(0.0, Ts));
     const double r1 = (dr00 + Tt * (r01 + Tt * (r02 + Tt * (r03 + Tt * (r04 + Tt * r05)))) +
                        Ts * (r10 + Tt * (r11 + Tt * (r12 + Tt * (r13 + Tt * r14))) + sqrtTs * (rS0 + Tt * (rS1 + Tt * rS2)) +
@@ -824,7 +844,6 @@ __global__ void __launch_bounds__(256) k_rho_eos_split(Dev d, Range R, int tidx)
                       Ts * (K10 + Tt * (K11 + Tt * (K12 + Tt * K13)) + sqrtTs * (KS0 + Tt * (KS1 + Tt * KS2)));
     const double q1 = 0.1 * (rho0 + r1) * (K0_Duk - K0) / ((K00 + K0) * (K00 + K0_Duk)) * rm;
     qp1.st(q1, vo, o);
-    const double zrk = zr.ld(vo, o), hz = Hz.ld(vo, o);
     if constexpr (kP) pc.level(k, zrk, r1, q1);
     if (lmd && k < N) {
       const double dpth = -0.5 * (zrp + zrk);
