@@ -723,23 +723,16 @@ __global__ void __launch_bounds__(256) k_t3dmix_stg(Dev d, Range R, int nnew, in
   const int c = (threadIdx.x + 1) + (threadIdx.y + 1) * kTMW;   // the lane's cell in the window
   double w[kTMQ];
   ldw(1, w);
-  // t(nnew) of the lane's cell: level k+1's loaded with level k+1's window,
-  // before level k's stores (which vmcnt counts with the loads)
-  double ntn0 = Tn[0][ij], ntn1 = Tn[1][ij];
   for (int k = 1; k <= b.N; k++) {
     const long o = ij + (long)(k - 1) * n2;
-    const double tn0 = ntn0, tn1 = ntn1;
+    const double tn0 = Tn[0][o], tn1 = Tn[1][o];
     if (k > 1) __syncthreads();   // the previous level's window consumed
 #pragma unroll
     for (int m = 0; m < kTMQ; m++) {
       const int q = tid + m * kBX * kBY;
       if (q < 3 * kTMN) sW[q] = w[m];
     }
-    if (k < b.N) {
-      ldw(k + 1, w);
-      ntn0 = Tn[0][o + n2];
-      ntn1 = Tn[1][o + n2];
-    }
+    if (k < b.N) ldw(k + 1, w);
     __syncthreads();
     const double* H = sW;
     const double hz = H[c];
