@@ -1119,12 +1119,24 @@ __global__ void __launch_bounds__(256, KL > 13 ? 3 : 4) k_uv2_fused(Dev d, Range
     // corrected u and the fluxes; un[] becomes the flux cfk (the level loop's
     // loads of u(nstp) and Flx stay here, not hoisted above the chains)
     __builtin_amdgcn_sched_barrier(0);
+    // in groups of 8 levels, the group's Flx and u(nstp) loads are issued
+    // before its u stores (vmcnt counts stores: a load issued after a store
+    // waits for it too)
 #pragma unroll
-    for (int q = 0; q < KL; q++) {
-      const double u1 = (un[q] - FC0) * msk;
-      bUn.st(u1, vsq(q), so(q));
-      un[q] = DELTA * bFl.ld(vq(q), so(q)) + EPSIL * (hc[q] * dn) * (bUs.ld(vq(q), so(q)) + u1);
-      if (q % 8 == 7) __builtin_amdgcn_sched_barrier(0);
+    for (int q0 = 0; q0 < KL; q0 += 8) {
+      double fl[8], us[8];
+#pragma unroll
+      for (int q = q0; q < q0 + 8 && q < KL; q++) {
+        fl[q - q0] = bFl.ld(vq(q), so(q));
+        us[q - q0] = bUs.ld(vq(q), so(q));
+      }
+#pragma unroll
+      for (int q = q0; q < q0 + 8 && q < KL; q++) {
+        const double u1 = (un[q] - FC0) * msk;
+        bUn.st(u1, vsq(q), so(q));
+        un[q] = DELTA * fl[q - q0] + EPSIL * (hc[q] * dn) * (us[q - q0] + u1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
     }
     double CS, unused;
     chain2(CS, unused, [&](double& a, double& c) {

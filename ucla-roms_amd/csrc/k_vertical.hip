@@ -83,34 +83,19 @@ __global__ void __launch_bounds__(256) k_set_huv(Dev d, Range R, int nrhs, int h
   double* __restrict__ FV = F.FlxV + ij;
   double* __restrict__ HU = F.Hz_u + ij;
   double* __restrict__ HV = F.Hz_v + ij;
-  // a ring of the next PF levels' inputs, loaded before this level's stores
-  // (vmcnt counts stores with the loads: a load issued after a store waits
-  // for it too)
-  constexpr int PF = 4;
-  const long sj = b.nx2;
-  double rh[PF], rhx[PF], rhy[PF], ru[PF], rv[PF];
-  auto ld = [&](int q, int k) {
-    const long o = (long)(min(k, b.N) - 1) * n2;
-    rh[q] = Hz[o];
-    rhx[q] = du ? Hz[o - 1] : 0.0; ru[q] = du ? U[o] : 0.0;
-    rhy[q] = dv ? Hz[o - sj] : 0.0; rv[q] = dv ? V[o] : 0.0;
-  };
-#pragma unroll
-  for (int q = 0; q < PF; q++) ld(q, 1 + q);
 #pragma unroll 4
   for (int k = 1; k <= b.N; k++) {
     const long o = (long)(k - 1) * n2;
-    const double hz = rh[0], hzx = rhx[0], hzy = rhy[0], uk = ru[0], vk = rv[0];
-#pragma unroll
-    for (int q = 0; q + 1 < PF; q++) { rh[q] = rh[q + 1]; rhx[q] = rhx[q + 1]; rhy[q] = rhy[q + 1]; ru[q] = ru[q + 1]; rv[q] = rv[q + 1]; }
-    ld(PF - 1, k + PF);
+    const double hz = Hz[o];
     if (du) {
-      FU[o] = 0.5 * (hz + hzx) * dnu * (uk);
-      if (huv) HU[o] = 0.5 * (hz + hzx);
+      const double hzm = Hz[o - 1];
+      FU[o] = 0.5 * (hz + hzm) * dnu * (U[o]);
+      if (huv) HU[o] = 0.5 * (hz + hzm);
     }
     if (dv) {
-      FV[o] = 0.5 * (hz + hzy) * dmv * (vk);
-      if (huv) HV[o] = 0.5 * (hz + hzy);
+      const double hzm = Hz[o - b.nx2];
+      FV[o] = 0.5 * (hz + hzm) * dmv * (V[o]);
+      if (huv) HV[o] = 0.5 * (hz + hzm);
     }
   }
 }
