@@ -320,7 +320,9 @@ __device__ __forceinline__ void uv_spline_seg(const Dev& d, const SegSpan& sg, S
 struct NoSplineRowB {
   __device__ __forceinline__ void operator()(int, unsigned, double, double, double) const {}
 };
-template <int KR, class RowF = NoSplineRowB>
+// UNI: the segment is wave-uniform (seg_uniform) and level offsets go in
+// the SGPR soffset; else they are added to the VGPR offset.
+template <int KR, bool UNI = true, class RowF = NoSplineRowB>
 __device__ __forceinline__ void uv_spline_segb(const Dev& d, const SegSpan& sg, SegXchg& X, long ij, int nrhs, int dir,
                                                double (&fl)[KR], RowF row = RowF()) {
   const Bounds& b = d.b;
@@ -336,13 +338,14 @@ __device__ __forceinline__ void uv_spline_segb(const Dev& d, const SegSpan& sg, 
   const unsigned vm = vo - ds, vp = vo + ds, vm2 = vo - 2u * ds;
   const BufF64 Uv((dir == 0 ? F.u : F.v) + (long)(nrhs - 1) * b.n3), Hz(F.Hz), We(F.We);
   const double* mask = dir == 0 ? F.umask : F.vmask;
+  auto LD = [&](const BufF64& B, unsigned v, unsigned l) { return UNI ? B.ld(v, l) : B.ld(v + l, 0u); };
   double dc[KR + 1], uu[KR];
 #pragma unroll
   for (int q = 0; q < KR + 1; q++) {
     const unsigned L = (unsigned)(min(max(c0 - 1 + q, 1), N) - 1) * lv;
-    const double h0 = Hz.ld(vo, L), h1 = Hz.ld(vm, L);
-    dc[q] = 0.5625 * (h0 + h1) - 0.0625 * (Hz.ld(vp, L) + Hz.ld(vm2, L));
-    if (q < KR) uu[q] = Uv.ld(vo, L);
+    const double h0 = LD(Hz, vo, L), h1 = LD(Hz, vm, L);
+    dc[q] = 0.5625 * (h0 + h1) - 0.0625 * (LD(Hz, vp, L) + LD(Hz, vm2, L));
+    if (q < KR) uu[q] = LD(Uv, vo, L);
     row(q, L, h0, h1, q < KR ? uu[q] : 0.0);
     if (q % kSegLoadGroup == kSegLoadGroup - 1) __builtin_amdgcn_sched_barrier(0);
   }
@@ -352,8 +355,8 @@ __device__ __forceinline__ void uv_spline_segb(const Dev& d, const SegSpan& sg, 
 #pragma unroll
   for (int q = 0; q < KR; q++) {
     const unsigned w = (unsigned)min(max(c0 - 1 + q, 1), N - 1) * lv;
-    const double we0 = We.ld(vo, w), wem = We.ld(vm, w);
-    wf[q] = we0 + wem - 0.125 * ((We.ld(vp, w) - we0) * m1 - (wem - We.ld(vm2, w)) * m0);
+    const double we0 = LD(We, vo, w), wem = LD(We, vm, w);
+    wf[q] = we0 + wem - 0.125 * ((LD(We, vp, w) - we0) * m1 - (wem - LD(We, vm2, w)) * m0);
     if (q % kSegLoadGroup == kSegLoadGroup - 1) __builtin_amdgcn_sched_barrier(0);
   }
 #pragma unroll

@@ -412,7 +412,8 @@ __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_uv1_seg(Dev d, Rang
 // its neighbour in VGPR offsets; PF: u(nnew) of the segment's rows loaded
 // with the spline phase's inputs.  Same expressions and order: bitwise equal
 // to k_uv1_seg<true>. ----
-template <bool PF>
+// UNI false: the level offsets in the VGPR offset (no seg_uniform, no SGPR pressure)
+template <bool PF, bool UNI = true>
 __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_uv1_segb(Dev d, Range R, int nnew, int nrhs) {
   const uint3 bI = seg_tile(d.p.seg_order, d.p.seg_xg);
   __shared__ SegXchg X;
@@ -423,7 +424,7 @@ __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_uv1_segb(Dev d, Ran
   const int N = b.N;
   const double dt = d.p.dt;
   SegSpan sg = seg_span(N);
-  seg_uniform(sg);
+  if constexpr (UNI) seg_uniform(sg);
   SegCol col;
   seg_uv_col(d, R, bI, sg, col);
   if (col.idle) return;   // uniform over the block
@@ -438,12 +439,13 @@ __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_uv1_segb(Dev d, Ran
   double* const Sh = roms_smem + tid;                             // Hz(c0-1+q) at Sh[q*nthr]
   double* const Shm = roms_smem + (long)(KR + 1) * nthr + tid;    // its neighbour's at Shm[q*nthr]
   const BufF64 Un((dir == 0 ? F.u : F.v) + (long)(nnew - 1) * b.n3);
+  auto LD = [&](const BufF64& B, unsigned v, unsigned l) { return UNI ? B.ld(v, l) : B.ld(v + l, 0u); };
   double fl[KR], un[PF ? KR : 1];
   if constexpr (PF) {
 #pragma unroll
-    for (int p = 0; p < KR; p++) un[p] = Un.ld(vo, lev(c0 + p));
+    for (int p = 0; p < KR; p++) un[p] = LD(Un, vo, lev(c0 + p));
   }
-  uv_spline_segb<KR>(d, sg, X, ij, nrhs, dir, fl, [&](int q, unsigned, double h0, double h1, double) {
+  uv_spline_segb<KR, UNI>(d, sg, X, ij, nrhs, dir, fl, [&](int q, unsigned, double h0, double h1, double) {
     Sh[q * nthr] = h0;
     Shm[q * nthr] = h1;
   });
@@ -455,7 +457,7 @@ __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_uv1_segb(Dev d, Ran
 #pragma unroll
   for (int p = 0; p < KR; p++) {
     const int k = c0 + p;
-    const double rro = rr.ld(vo, lev(k));
+    const double rro = LD(rr, vo, lev(k));
     rk[p] = k == 1 ? rro - fl[1] : rro - fl[p + 1 < KR ? p + 1 : KR - 1] + fl[p];
   }
   int tl = tid;
@@ -467,8 +469,8 @@ __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_uv1_segb(Dev d, Ran
     const unsigned w = (unsigned)min(max(r, 1), N - 1) * lv;
     const bool in = r > 0 && r < N;
     const int qa = q + 1 < KR + 1 ? q + 1 : KR;
-    const double f = 2.0 * dt * (Akv.ld(vo, w) + Akv.ld(vm, w)) / (HZ(qa) + HZM(qa) + HZ(q) + HZM(q));
-    const double wv = DC0 * 0.5 * (Wi.ld(vo, w) + Wi.ld(vm, w));
+    const double f = 2.0 * dt * (LD(Akv, vo, w) + LD(Akv, vm, w)) / (HZ(qa) + HZM(qa) + HZ(q) + HZM(q));
+    const double wv = DC0 * 0.5 * (LD(Wi, vo, w) + LD(Wi, vm, w));
     fc = in ? f : 0.0;
     wc = in ? wv : 0.0;
   };
@@ -486,7 +488,7 @@ __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_uv1_segb(Dev d, Ran
     const double b1 = 0.5 * (HZ(p + 1) + HZM(p + 1)) + 0.5 * dt * (rD + rDm) + fcu + fmax0(wcu);
     const double bk = 0.5 * (HZ(p + 1) + HZM(p + 1)) + fcl - fmin0(wcl) + fcu + fmax0(wcu);
     bb = k == 1 ? b1 : bk;
-    const double v = (PF ? un[p] : Un.ld(vo, lev(k))) + DC0 * rk[p];
+    const double v = (PF ? un[p] : LD(Un, vo, lev(k))) + DC0 * rk[p];
     dd = k == N ? v + dt * sstr : v;
     fcl = fcu; wcl = wcu;
   });
@@ -510,7 +512,10 @@ __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_uv1_segb(Dev d, Ran
   const unsigned vs = act ? vo : kBufOff;
 #pragma unroll
   for (int p = 0; p < KR; p++)
-    if (p < n) Un.st(T.D[p] * 0.5 * (HZ(p + 1) + HZM(p + 1)), vs, lev(c0 + p));
+    if (p < n) {
+      if constexpr (UNI) Un.st(T.D[p] * 0.5 * (HZ(p + 1) + HZM(p + 1)), vs, lev(c0 + p));
+      else Un.st(T.D[p] * 0.5 * (HZ(p + 1) + HZM(p + 1)), act ? vo + lev(c0 + p) : kBufOff, 0u);
+    }
   if (act && sg.s == 0) {
     if (dir == 0) F.rufrc[ij] = Lf[S - 1][sl];
     else F.rvfrc[ij] = Lf[S - 1][sl];
@@ -532,6 +537,8 @@ void setup_uv1_seg() {
                             (int)uv1_seg_lds_bytes(kSegBlock * kSegJMax));
   (void)hipFuncSetAttribute((const void*)k_uv1_segb<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)uv1_seg_lds_bytes(kSegBlock * kSegJMax));
+  (void)hipFuncSetAttribute((const void*)k_uv1_segb<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)uv1_seg_lds_bytes(kSegBlock * kSegJMax));
 }
 
 void launch_step3d_uv1(const Dev& d, hipStream_t s, const Tlev& t, bool uv_done) {
@@ -545,7 +552,10 @@ void launch_step3d_uv1(const Dev& d, hipStream_t s, const Tlev& t, bool uv_done)
   else if (d.p.colseg) {
     const dim3 gs = seg_uv_grid(d, R, d.p.seg_jrows), bs(kCX, seg_waves(b.N), d.p.seg_jrows);
     ktimer_mark(s, kTimedUv1Seg, 0);
-    if (d.p.uv1_lds && d.p.uv_adv && (d.p.seg_buf & 32) && (d.p.seg_buf & 64))
+    if (d.p.uv1_lds && d.p.uv_adv && (d.p.seg_buf & 32) && (d.p.seg_buf & 512))
+      hipLaunchKernelGGL((k_uv1_segb<false, false>), gs, bs, uv1_seg_lds_bytes(bs.x * bs.y * bs.z), s, d, R, t.nnew,
+                         t.nrhs);
+    else if (d.p.uv1_lds && d.p.uv_adv && (d.p.seg_buf & 32) && (d.p.seg_buf & 64))
       hipLaunchKernelGGL(k_uv1_segb<true>, gs, bs, uv1_seg_lds_bytes(bs.x * bs.y * bs.z), s, d, R, t.nnew, t.nrhs);
     else if (d.p.uv1_lds && d.p.uv_adv && (d.p.seg_buf & 32))
       hipLaunchKernelGGL(k_uv1_segb<false>, gs, bs, uv1_seg_lds_bytes(bs.x * bs.y * bs.z), s, d, R, t.nnew, t.nrhs);
@@ -1119,24 +1129,12 @@ __global__ void __launch_bounds__(256, KL > 13 ? 3 : 4) k_uv2_fused(Dev d, Range
     // corrected u and the fluxes; un[] becomes the flux cfk (the level loop's
     // loads of u(nstp) and Flx stay here, not hoisted above the chains)
     __builtin_amdgcn_sched_barrier(0);
-    // in groups of 8 levels, the group's Flx and u(nstp) loads are issued
-    // before its u stores (vmcnt counts stores: a load issued after a store
-    // waits for it too)
 #pragma unroll
-    for (int q0 = 0; q0 < KL; q0 += 8) {
-      double fl[8], us[8];
-#pragma unroll
-      for (int q = q0; q < q0 + 8 && q < KL; q++) {
-        fl[q - q0] = bFl.ld(vq(q), so(q));
-        us[q - q0] = bUs.ld(vq(q), so(q));
-      }
-#pragma unroll
-      for (int q = q0; q < q0 + 8 && q < KL; q++) {
-        const double u1 = (un[q] - FC0) * msk;
-        bUn.st(u1, vsq(q), so(q));
-        un[q] = DELTA * fl[q - q0] + EPSIL * (hc[q] * dn) * (us[q - q0] + u1);
-      }
-      __builtin_amdgcn_sched_barrier(0);
+    for (int q = 0; q < KL; q++) {
+      const double u1 = (un[q] - FC0) * msk;
+      bUn.st(u1, vsq(q), so(q));
+      un[q] = DELTA * bFl.ld(vq(q), so(q)) + EPSIL * (hc[q] * dn) * (bUs.ld(vq(q), so(q)) + u1);
+      if (q % 8 == 7) __builtin_amdgcn_sched_barrier(0);
     }
     double CS, unused;
     chain2(CS, unused, [&](double& a, double& c) {
