@@ -169,14 +169,15 @@ def test_seg_buffer_forms_bitwise(lmd, monkeypatch):
     k_pre_tracer_segb, 2 k_step3d_t_segb, 32 k_uv1_segb, 128 k_pre_uv_segb
     -- wave-uniform level offsets in SGPRs, the lane's column in one VGPR --,
     4 / 16 / 64 / 256 their diffusion rows' inputs prefetched with the spline inputs, 8
-    step3d_t reloading Hz for its diffusion rows, 512 k_uv1_segb with the
-    level offsets in the VGPR offset) keep the expressions and
+    step3d_t reloading Hz for its diffusion rows, 512 / 1024 the momentum /
+    tracer forms with the level offsets in the VGPR offset) keep the
+    expressions and
     their order: 6 steps at
     N = 100, with and without KPP, equal the pointer forms bitwise."""
     cfg = seg_cfg("n100")
     cfg.lmd, cfg.surf_flux = lmd, int(lmd != 0)
     out = []
-    for env in ("0", "3", "23", "11", "32", "96", "128", "487", "551"):
+    for env in ("0", "3", "23", "11", "32", "96", "128", "487", "551", "679", "1031"):
         monkeypatch.setenv("ROMS_GPU_SEG_BUF", env)
         m = make_model(cfg, 1)
         m.step(6)

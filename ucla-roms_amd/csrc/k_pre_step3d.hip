@@ -770,7 +770,7 @@ __global__ void __launch_bounds__(kSegBlock, 2) k_pre_tracer_seg(Dev d, Range R,
 // one VGPR.  PF: the diffusion phase's t(nnew) rows and Hz_fwd loaded at
 // entry with the spline inputs.  Same expressions and order: bitwise equal
 // to k_pre_tracer_seg. ----
-template <bool PF>
+template <bool PF, bool UNI = true>
 __global__ void __launch_bounds__(kSegBlock, ROMS_SEG_BUF_WAVES) k_pre_tracer_segb(Dev d, Range R, PreCoef c, int nnew,
                                                                                    int nrhs) {
   const uint3 bI = seg_tile(d.p.seg_order, d.p.seg_xg);
@@ -780,7 +780,13 @@ __global__ void __launch_bounds__(kSegBlock, ROMS_SEG_BUF_WAVES) k_pre_tracer_se
   const Fields& F = d.f;
   const int N = b.N;
   SegSpan sg = seg_span(N);
-  seg_uniform(sg);
+  if constexpr (UNI) seg_uniform(sg);
+  // UNI: level offsets in the SGPR soffset; else added to the VGPR offset
+  auto LD = [&](const BufF64& B, unsigned v, unsigned l) { return UNI ? B.ld(v, l) : B.ld(v + l, 0u); };
+  auto ST = [&](const BufF64& B, double x, unsigned v, unsigned l) {
+    if constexpr (UNI) B.st(x, v, l);
+    else B.st(x, v + l, 0u);   // v = kBufOff stays beyond the extent
+  };
   const int iu = tile_i0(R.i0) + (int)bI.x * kSegCW + sg.col;
   const bool act = iu >= R.i0 && iu <= R.i1;
   const int i = act ? iu : (iu < R.i0 ? R.i0 : R.i1), j = R.j0 + (int)bI.y;
@@ -796,21 +802,21 @@ __global__ void __launch_bounds__(kSegBlock, ROMS_SEG_BUF_WAVES) k_pre_tracer_se
   double hz[KR + 1], tt[KR], fl[KR], hf[KR + 1], tn[KR];
 #pragma unroll
   for (int q = 0; q < KR + 1; q++) {
-    hz[q] = Hz.ld(vo, lev(c0 - 1 + q));
-    if (q < KR) tt[q] = Tr.ld(vo, lev(c0 - 1 + q));
+    hz[q] = LD(Hz, vo, lev(c0 - 1 + q));
+    if (q < KR) tt[q] = LD(Tr, vo, lev(c0 - 1 + q));
   }
   if constexpr (PF) {
 #pragma unroll
     for (int q = 0; q < KR + 1; q++) {
-      hf[q] = Hf.ld(vo, lev(c0 - 1 + q));
-      if (q < KR) tn[q] = Tn.ld(vo, lev(c0 + q));
+      hf[q] = LD(Hf, vo, lev(c0 - 1 + q));
+      if (q < KR) tn[q] = LD(Tn, vo, lev(c0 + q));
     }
   }
   spline_fc_seg<KR>(sg, N, X, hz, tt, fl);
   {
     double we[KR];
 #pragma unroll
-    for (int q = 0; q < KR; q++) we[q] = We.ld(vo, wlev(c0 - 1 + q));
+    for (int q = 0; q < KR; q++) we[q] = LD(We, vo, wlev(c0 - 1 + q));
 #pragma unroll
     for (int q = 0; q < KR; q++) pin(we[q]);
 #pragma unroll
@@ -821,19 +827,19 @@ __global__ void __launch_bounds__(kSegBlock, ROMS_SEG_BUF_WAVES) k_pre_tracer_se
   }
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-  for (int q = 0; q < KR + 1; q++) hz[q] = PF ? hf[q] : Hf.ld(vo, lev(c0 - 1 + q));
+  for (int q = 0; q < KR + 1; q++) hz[q] = PF ? hf[q] : LD(Hf, vo, lev(c0 - 1 + q));
   const int iAkt = itrc < b.nTS ? itrc : b.nTS;
   const BufF64 Akt(F.Akt + (long)(iAkt - 1) * b.n3w);
   const BufF64 Pm(F.pm), Pn(F.pn);   // 2-D metrics through the lane's offset too (no 64-bit ij kept live)
-  const double pm = Pm.ld(vo, 0), pn = Pn.ld(vo, 0);
+  const double pm = LD(Pm, vo, 0), pn = LD(Pn, vo, 0);
   const double DC0 = c.dtau * pm * pn;
   auto fcw = [&](int q, double& fc, double& wc) {
     const int r = c0 - 1 + q;
     const unsigned w = wlev(r);
     const bool in = r > 0 && r < N;
     const int qa = q + 1 < KR + 1 ? q + 1 : KR;
-    const double f = 2.0 * c.dtau * Akt.ld(vo, w) / (hz[qa] + hz[q]);
-    const double wv = DC0 * Wi.ld(vo, w);
+    const double f = 2.0 * c.dtau * LD(Akt, vo, w) / (hz[qa] + hz[q]);
+    const double wv = DC0 * LD(Wi, vo, w);
     fc = in ? f : 0.0;
     wc = in ? wv : 0.0;
   };
@@ -847,7 +853,7 @@ __global__ void __launch_bounds__(kSegBlock, ROMS_SEG_BUF_WAVES) k_pre_tracer_se
     a = -(fcl + fmax0(wcl));
     bb = hz[p + 1] + fcu + fmax0(wcu) + fcl - fmin0(wcl);
     cc = -(fcu - fmin0(wcu));
-    dd = (PF ? tn[p] : Tn.ld(vo, lev(c0 + p))) - c.dtau * pm * pn * (fl[p + 1 < KR ? p + 1 : KR - 1] - fl[p]);
+    dd = (PF ? tn[p] : LD(Tn, vo, lev(c0 + p))) - c.dtau * pm * pn * (fl[p + 1 < KR ? p + 1 : KR - 1] - fl[p]);
     fcl = fcu; wcl = wcu;
   });
   double xL, xR;
@@ -856,7 +862,7 @@ __global__ void __launch_bounds__(kSegBlock, ROMS_SEG_BUF_WAVES) k_pre_tracer_se
   const unsigned vs = act ? vo : kBufOff;
 #pragma unroll
   for (int p = 0; p < KR; p++)
-    if (p < n) Tn.st(T.D[p], vs, lev(c0 + p));
+    if (p < n) ST(Tn, T.D[p], vs, lev(c0 + p));
 }
 
 // kLds (UV_ADV, nrhs == nstp -- always so in the predictor): the spline
@@ -987,7 +993,7 @@ __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_pre_uv_seg(Dev d, R
 // and its neighbour in VGPR offsets.  Same expressions and order: bitwise
 // equal to k_pre_uv_seg<true>.  PF: the viscosity rows' Hz_fwd pairs
 // loaded at entry with the spline inputs. ----
-template <bool PF>
+template <bool PF, bool UNI = true>
 __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_pre_uv_segb(Dev d, Range R, PreCoef c, int nstp, int nnew,
                                                                          int nrhs) {
   const uint3 bI = seg_tile(d.p.seg_order, d.p.seg_xg);
@@ -997,7 +1003,13 @@ __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_pre_uv_segb(Dev d, 
   const Fields& F = d.f;
   const int N = b.N, indx = 3 - nstp;
   SegSpan sg = seg_span(N);
-  seg_uniform(sg);
+  if constexpr (UNI) seg_uniform(sg);
+  // UNI: level offsets in the SGPR soffset; else added to the VGPR offset
+  auto LD = [&](const BufF64& B, unsigned v, unsigned l) { return UNI ? B.ld(v, l) : B.ld(v + l, 0u); };
+  auto ST = [&](const BufF64& B, double x, unsigned v, unsigned l) {
+    if constexpr (UNI) B.st(x, v, l);
+    else B.st(x, v + l, 0u);   // v = kBufOff stays beyond the extent
+  };
   SegCol col;
   seg_uv_col(d, R, bI, sg, col);
   if (col.idle) return;   // uniform over the block
@@ -1018,15 +1030,15 @@ __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_pre_uv_segb(Dev d, 
 #pragma unroll
     for (int q = 0; q < KR + 1; q++) {
       const unsigned L = lev(c0 - 1 + q);
-      hf[q] = Hf.ld(vo, L);
-      hfm[q] = Hf.ld(vm, L);
+      hf[q] = LD(Hf, vo, L);
+      hfm[q] = LD(Hf, vm, L);
     }
   };
   if constexpr (PF) load_hf();
   double fl[KR];
-  uv_spline_segb<KR>(d, sg, X, ij, nrhs, dir, fl, [&](int q, unsigned L, double h0, double h1, double u) {
+  uv_spline_segb<KR, UNI>(d, sg, X, ij, nrhs, dir, fl, [&](int q, unsigned L, double h0, double h1, double u) {
     if (q >= 1 && q < KR) {   // cells c0..c0+KR-2 (q is a constant of the unrolled load loop)
-      Sb[(q - 1) * nthr] = c.cf_stp * u + c.cf_bak * Uix.ld(vo, L);
+      Sb[(q - 1) * nthr] = c.cf_stp * u + c.cf_bak * LD(Uix, vo, L);
       Su[(q - 1) * nthr] = 0.5 * (h0 + h1) * u;
     }
   });
@@ -1037,10 +1049,10 @@ __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_pre_uv_segb(Dev d, 
   auto rhs = [&](int p) {
     const int k = c0 + p;
     const unsigned o = lev(k);
-    const double rro = rr.ld(vo, o);
+    const double rro = LD(rr, vo, o);
     const double r = k == 1 ? rro - fl[1] : rro - fl[p + 1 < KR ? p + 1 : KR - 1] + fl[p];
     const double ub = Sb[(p < KR - 1 ? p : KR - 2) * nthr];
-    const double v = 0.5 * (Hb.ld(vo, o) + Hb.ld(vm, o)) * ub + DC0 * r;
+    const double v = 0.5 * (LD(Hb, vo, o) + LD(Hb, vm, o)) * ub + DC0 * r;
     return k == N ? v + c.dtau * sstr : v;
   };
   if constexpr (!PF) load_hf();
@@ -1049,8 +1061,8 @@ __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_pre_uv_segb(Dev d, 
     const unsigned w = (unsigned)min(max(r, 1), N - 1) * lv;
     const bool in = r > 0 && r < N;
     const int qa = q + 1 < KR + 1 ? q + 1 : KR;
-    const double f = 2.0 * c.dtau * (Akv.ld(vo, w) + Akv.ld(vm, w)) / (hf[qa] + hfm[qa] + hf[q] + hfm[q]);
-    const double wv = DC0 * 0.5 * (Wi.ld(vo, w) + Wi.ld(vm, w));
+    const double f = 2.0 * c.dtau * (LD(Akv, vo, w) + LD(Akv, vm, w)) / (hf[qa] + hfm[qa] + hf[q] + hfm[q]);
+    const double wv = DC0 * 0.5 * (LD(Wi, vo, w) + LD(Wi, vm, w));
     fc = in ? f : 0.0;
     wc = in ? wv : 0.0;
   };
@@ -1079,8 +1091,8 @@ __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_pre_uv_segb(Dev d, 
   for (int p = 0; p < KR; p++)
     if (p < n) {
       const unsigned o = lev(c0 + p);
-      Unew.st(T.D[p], vs, o);
-      Uix.st(Su[(p < KR - 1 ? p : KR - 2) * nthr], vs, o);
+      ST(Unew, T.D[p], vs, o);
+      ST(Uix, Su[(p < KR - 1 ? p : KR - 2) * nthr], vs, o);
     }
 }
 
@@ -1093,6 +1105,8 @@ void setup_pre_uv_seg() {
   (void)hipFuncSetAttribute((const void*)k_pre_uv_segb<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)pre_uv_seg_lds_bytes(kSegBlock * kSegJMax));
   (void)hipFuncSetAttribute((const void*)k_pre_uv_segb<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)pre_uv_seg_lds_bytes(kSegBlock * kSegJMax));
+  (void)hipFuncSetAttribute((const void*)k_pre_uv_segb<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)pre_uv_seg_lds_bytes(kSegBlock * kSegJMax));
 }
 
@@ -1166,6 +1180,9 @@ void launch_pre_step3d(const Dev& d, hipStream_t s, const Tlev& t, bool uv_done,
     if (d.p.colseg && (d.p.seg_buf & 1) && (d.p.seg_buf & 16))
       hipLaunchKernelGGL(k_pre_tracer_segb<true>, seg_grid_of(ri, b.NT), dim3(kCX, seg_waves(b.N)), 0, st, d, ri, c,
                          t.nnew, t.nrhs);
+    else if (d.p.colseg && (d.p.seg_buf & 1) && (d.p.seg_buf & 1024))
+      hipLaunchKernelGGL((k_pre_tracer_segb<false, false>), seg_grid_of(ri, b.NT), dim3(kCX, seg_waves(b.N)), 0, st, d, ri,
+                         c, t.nnew, t.nrhs);
     else if (d.p.colseg && (d.p.seg_buf & 1))
       hipLaunchKernelGGL(k_pre_tracer_segb<false>, seg_grid_of(ri, b.NT), dim3(kCX, seg_waves(b.N)), 0, st, d, ri, c,
                          t.nnew, t.nrhs);
@@ -1216,6 +1233,9 @@ void launch_pre_step3d(const Dev& d, hipStream_t s, const Tlev& t, bool uv_done,
     if (d.p.preuv_lds && d.p.uv_adv && t.nrhs == t.nstp && (d.p.seg_buf & 128) && (d.p.seg_buf & 256))
       hipLaunchKernelGGL(k_pre_uv_segb<true>, gs, bs, pre_uv_seg_lds_bytes(bs.x * bs.y * bs.z), s, d, RI, c, t.nstp,
                          t.nnew, t.nrhs);
+    else if (d.p.preuv_lds && d.p.uv_adv && t.nrhs == t.nstp && (d.p.seg_buf & 128) && (d.p.seg_buf & 512))
+      hipLaunchKernelGGL((k_pre_uv_segb<false, false>), gs, bs, pre_uv_seg_lds_bytes(bs.x * bs.y * bs.z), s, d, RI, c,
+                         t.nstp, t.nnew, t.nrhs);
     else if (d.p.preuv_lds && d.p.uv_adv && t.nrhs == t.nstp && (d.p.seg_buf & 128))
       hipLaunchKernelGGL(k_pre_uv_segb<false>, gs, bs, pre_uv_seg_lds_bytes(bs.x * bs.y * bs.z), s, d, RI, c, t.nstp, t.nnew,
                          t.nrhs);

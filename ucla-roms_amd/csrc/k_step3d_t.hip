@@ -380,7 +380,7 @@ __global__ void __launch_bounds__(kSegBlock, 2) k_step3d_t_seg(Dev d, Range R, i
 // with the spline phase's inputs, so they land during its solve.  RL: Hz
 // reloaded for the diffusion phase instead of kept live across the spline
 // solve (30 VGPRs at its register peak).
-template <bool PF, bool RL = false>
+template <bool PF, bool RL = false, bool UNI = true>
 __global__ void __launch_bounds__(kSegBlock, ROMS_SEG_BUF_WAVES) k_step3d_t_segb(Dev d, Range R, int nnew, int nrhs) {
   const uint3 bI = seg_tile(d.p.seg_order, d.p.seg_xg);
   __shared__ SegXchg X;
@@ -391,7 +391,13 @@ __global__ void __launch_bounds__(kSegBlock, ROMS_SEG_BUF_WAVES) k_step3d_t_segb
   const int N = b.N;
   const double dt = P.dt;
   SegSpan sg = seg_span(N);
-  seg_uniform(sg);
+  if constexpr (UNI) seg_uniform(sg);
+  // UNI: level offsets in the SGPR soffset; else added to the VGPR offset
+  auto LD = [&](const BufF64& B, unsigned v, unsigned l) { return UNI ? B.ld(v, l) : B.ld(v + l, 0u); };
+  auto ST = [&](const BufF64& B, double x, unsigned v, unsigned l) {
+    if constexpr (UNI) B.st(x, v, l);
+    else B.st(x, v + l, 0u);   // v = kBufOff stays beyond the extent
+  };
   const int iu = tile_i0(R.i0) + (int)bI.x * kSegCW + sg.col;
   const bool act = iu >= R.i0 && iu <= R.i1;
   const int i = act ? iu : (iu < R.i0 ? R.i0 : R.i1), j = R.j0 + (int)bI.y;
@@ -409,19 +415,19 @@ __global__ void __launch_bounds__(kSegBlock, ROMS_SEG_BUF_WAVES) k_step3d_t_segb
   double hz[KR + 1], tt[KR], tn[KR];
 #pragma unroll
   for (int q = 0; q < KR + 1; q++) {
-    hz[q] = Hz.ld(vo, lev(c0 - 1 + q));
-    if (q < KR) tt[q] = Tr.ld(vo, lev(c0 - 1 + q));
+    hz[q] = LD(Hz, vo, lev(c0 - 1 + q));
+    if (q < KR) tt[q] = LD(Tr, vo, lev(c0 - 1 + q));
   }
   if constexpr (PF) {
 #pragma unroll
-    for (int p = 0; p < KR; p++) tn[p] = Tn.ld(vo, lev(c0 + p));
+    for (int p = 0; p < KR; p++) tn[p] = LD(Tn, vo, lev(c0 + p));
   }
   {
     double fc[KR];
     spline_fc_seg<KR>(sg, N, X, hz, tt, fc);
     double we[KR];
 #pragma unroll
-    for (int q = 0; q < KR; q++) we[q] = We.ld(vo, wlev(c0 - 1 + q, 1, N - 1));
+    for (int q = 0; q < KR; q++) we[q] = LD(We, vo, wlev(c0 - 1 + q, 1, N - 1));
 #pragma unroll
     for (int q = 0; q < KR; q++) pin(we[q]);
 #pragma unroll
@@ -433,7 +439,7 @@ __global__ void __launch_bounds__(kSegBlock, ROMS_SEG_BUF_WAVES) k_step3d_t_segb
   __builtin_amdgcn_sched_barrier(0);
   if constexpr (RL) {
 #pragma unroll
-    for (int q = 0; q < KR + 1; q++) hz[q] = Hz.ld(vo, lev(c0 - 1 + q));
+    for (int q = 0; q < KR + 1; q++) hz[q] = LD(Hz, vo, lev(c0 - 1 + q));
   }
   const int iAkt = itrc < b.nTS ? itrc : b.nTS;
   const BufF64 Akt(F.Akt + (long)(iAkt - 1) * b.n3w);
@@ -449,7 +455,7 @@ __global__ void __launch_bounds__(kSegBlock, ROMS_SEG_BUF_WAVES) k_step3d_t_segb
   double rhs[KR];
 #pragma unroll
   for (int p = 0; p < KR; p++)
-    rhs[p] = (PF ? tn[p] : Tn.ld(vo, lev(c0 + p))) - dt * pm * pn * (tt[p + 1 < KR ? p + 1 : KR - 1] - tt[p]);
+    rhs[p] = (PF ? tn[p] : LD(Tn, vo, lev(c0 + p))) - dt * pm * pn * (tt[p + 1 < KR ? p + 1 : KR - 1] - tt[p]);
   if (P.npip > 0) {   // pipe_frc.F sources (step3d_t_ISO.F:927-934)
     const int pidx = F.pipe_idx[ij];
     if (pidx > 0) {
@@ -467,7 +473,7 @@ __global__ void __launch_bounds__(kSegBlock, ROMS_SEG_BUF_WAVES) k_step3d_t_segb
     for (int p = 0; p < KR; p++) t = p == n - 1 ? rhs[p] : t;
     if (itrc == 1) {
       const double swf = BufF64(F.swflx).ld(vo, 0);
-      t = t + dt * swf * (P.bulk_frc ? BufF64(F.tair).ld(vo, 0) : t / Hz.ld(vo, lev(N)));
+      t = t + dt * swf * (P.bulk_frc ? BufF64(F.tair).ld(vo, 0) : t / LD(Hz, vo, lev(N)));
     }
     t = t + dt * stf;
 #pragma unroll
@@ -481,7 +487,7 @@ __global__ void __launch_bounds__(kSegBlock, ROMS_SEG_BUF_WAVES) k_step3d_t_segb
     const bool nl = P.lmd_nonlocal;
     auto term = [&](int m) {
       const unsigned o = wlev(m, 1, N - 1);
-      return kppT ? dt * (sr * Sw.ld(vo, o) - (nl ? Gh.ld(vo, o) : 0.0) * (stf - sr)) : -dt * Gh.ld(vo, o) * stf;
+      return kppT ? dt * (sr * LD(Sw, vo, o) - (nl ? LD(Gh, vo, o) : 0.0) * (stf - sr)) : -dt * LD(Gh, vo, o) * stf;
     };
     double lo = term(c0 - 1);
 #pragma unroll
@@ -500,8 +506,8 @@ __global__ void __launch_bounds__(kSegBlock, ROMS_SEG_BUF_WAVES) k_step3d_t_segb
     const unsigned w = wlev(r, 1, N - 1);
     const bool in = r > 0 && r < N;
     const int qa = q + 1 < KR + 1 ? q + 1 : KR;
-    const double f = 2.0 * dt * Akt.ld(vo, w) / (hz[q] + hz[qa]);
-    const double c = DC0 * Wi.ld(vo, w);
+    const double f = 2.0 * dt * LD(Akt, vo, w) / (hz[q] + hz[qa]);
+    const double c = DC0 * LD(Wi, vo, w);
     fc = in ? f : 0.0;
     wc = in ? c : 0.0;
   };
@@ -525,7 +531,7 @@ __global__ void __launch_bounds__(kSegBlock, ROMS_SEG_BUF_WAVES) k_step3d_t_segb
   const unsigned vs = act ? vo : kBufOff;
 #pragma unroll
   for (int p = 0; p < KR; p++)
-    if (p < n) Tn.st(T.D[p] * rm, vs, lev(c0 + p));
+    if (p < n) ST(Tn, T.D[p] * rm, vs, lev(c0 + p));
 }
 
 void setup_column_kernels_t(size_t bytes) {
@@ -571,6 +577,9 @@ void launch_step3d_t(const Dev& d, hipStream_t s, const Tlev& t, bool exchange) 
       if ((d.p.seg_buf & 2) && (d.p.seg_buf & 8))
         hipLaunchKernelGGL((k_step3d_t_segb<false, true>), seg_grid_of(r, b.NT), dim3(kCX, seg_waves(b.N)), 0, s, d, r,
                            t.nnew, t.nrhs);
+      else if ((d.p.seg_buf & 2) && (d.p.seg_buf & 4) && (d.p.seg_buf & 1024))
+        hipLaunchKernelGGL((k_step3d_t_segb<true, false, false>), seg_grid_of(r, b.NT), dim3(kCX, seg_waves(b.N)), 0, s, d,
+                           r, t.nnew, t.nrhs);
       else if ((d.p.seg_buf & 2) && (d.p.seg_buf & 4))
         hipLaunchKernelGGL(k_step3d_t_segb<true>, seg_grid_of(r, b.NT), dim3(kCX, seg_waves(b.N)), 0, s, d, r, t.nnew, t.nrhs);
       else if (d.p.seg_buf & 2)

@@ -964,8 +964,9 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     const char* e = getenv("ROMS_GPU_SEG_BUF");
     // bits: 1 k_pre_tracer_segb, 2 k_step3d_t_segb, 4 its t(nnew) prefetch,
     // 8 its Hz reload, 16 k_pre_tracer_segb's prefetch, 32 k_uv1_segb, 64 its
-    // u(nnew) prefetch, 128 k_pre_uv_segb, 256 its Hz_fwd prefetch, 512
-    // k_uv1_segb without seg_uniform (level offsets in the VGPR offset).  Default 7: C3
+    // u(nnew) prefetch, 128 k_pre_uv_segb, 256 its Hz_fwd prefetch, 512 the
+    // momentum solvers' buffer forms without seg_uniform (level offsets in
+    // the VGPR offset), 1024 the same for the tracer solvers.  Default 7: C3
     // 57.4-57.7 -> 56.7 ms/step, step3d_t 5.98 -> 5.75 ms, pre_step3d
     // 11.5 -> 11.3 ms (same box, profiles/r5_c_seg_buf_ab.txt); the momentum
     // solvers' buffer forms (32, 128, + prefetch) measured slower (step3d_uv1
