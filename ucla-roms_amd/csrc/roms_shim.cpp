@@ -966,12 +966,15 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     // 8 its Hz reload, 16 k_pre_tracer_segb's prefetch, 32 k_uv1_segb, 64 its
     // u(nnew) prefetch, 128 k_pre_uv_segb, 256 its Hz_fwd prefetch, 512 the
     // momentum solvers' buffer forms without seg_uniform (level offsets in
-    // the VGPR offset), 1024 the same for the tracer solvers.  Default 7: C3
+    // the VGPR offset), 1024 the same for the tracer solvers.  Default 679
+    // (7 + the momentum solvers' buffer forms with VGPR level offsets):
+    // pre_step3d 11.24-11.31 -> 10.88-11.08 ms, step3d_uv1 4.63 -> 4.50-4.53
+    // (profiles/r5_l_seg_buf_vgpr_ab.txt)  Default 7: C3
     // 57.4-57.7 -> 56.7 ms/step, step3d_t 5.98 -> 5.75 ms, pre_step3d
     // 11.5 -> 11.3 ms (same box, profiles/r5_c_seg_buf_ab.txt); the momentum
     // solvers' buffer forms (32, 128, + prefetch) measured slower (step3d_uv1
     // 4.6 -> 6.0-6.6 ms, pre_step3d +0.3-2.1 ms: r5_d_seg_buf_chunk_prs_ab.txt)
-    P.seg_buf = e ? atoi(e) : 7;
+    P.seg_buf = e ? atoi(e) : 679;
   }
   {
     const char* e = getenv("ROMS_GPU_SEG_VTILE");
