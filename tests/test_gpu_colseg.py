@@ -177,7 +177,7 @@ def test_seg_buffer_forms_bitwise(lmd, monkeypatch):
     cfg = seg_cfg("n100")
     cfg.lmd, cfg.surf_flux = lmd, int(lmd != 0)
     out = []
-    for env in ("0", "3", "23", "11", "32", "96", "128", "487", "551", "679", "1031"):
+    for env in ("0", "3", "23", "11", "32", "96", "128", "487", "551", "679", "743", "1031"):
         monkeypatch.setenv("ROMS_GPU_SEG_BUF", env)
         m = make_model(cfg, 1)
         m.step(6)

@@ -1108,6 +1108,8 @@ void setup_pre_uv_seg() {
                             (int)pre_uv_seg_lds_bytes(kSegBlock * kSegJMax));
   (void)hipFuncSetAttribute((const void*)k_pre_uv_segb<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)pre_uv_seg_lds_bytes(kSegBlock * kSegJMax));
+  (void)hipFuncSetAttribute((const void*)k_pre_uv_segb<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)pre_uv_seg_lds_bytes(kSegBlock * kSegJMax));
 }
 
 void setup_column_kernels_t(size_t bytes);
@@ -1230,9 +1232,14 @@ void launch_pre_step3d(const Dev& d, hipStream_t s, const Tlev& t, bool uv_done,
   if (d.p.colseg) {
     const dim3 gs = seg_uv_grid(d, RI, d.p.seg_jrows), bs(kCX, seg_waves(b.N), d.p.seg_jrows);
     ktimer_mark(s, kTimedPreUvSeg, 0);
-    if (d.p.preuv_lds && d.p.uv_adv && t.nrhs == t.nstp && (d.p.seg_buf & 128) && (d.p.seg_buf & 256))
+    if (d.p.preuv_lds && d.p.uv_adv && t.nrhs == t.nstp && (d.p.seg_buf & 128) && (d.p.seg_buf & 256) &&
+        !(d.p.seg_buf & 512))
       hipLaunchKernelGGL(k_pre_uv_segb<true>, gs, bs, pre_uv_seg_lds_bytes(bs.x * bs.y * bs.z), s, d, RI, c, t.nstp,
                          t.nnew, t.nrhs);
+    else if (d.p.preuv_lds && d.p.uv_adv && t.nrhs == t.nstp && (d.p.seg_buf & 128) && (d.p.seg_buf & 512) &&
+             (d.p.seg_buf & 256))
+      hipLaunchKernelGGL((k_pre_uv_segb<true, false>), gs, bs, pre_uv_seg_lds_bytes(bs.x * bs.y * bs.z), s, d, RI, c,
+                         t.nstp, t.nnew, t.nrhs);
     else if (d.p.preuv_lds && d.p.uv_adv && t.nrhs == t.nstp && (d.p.seg_buf & 128) && (d.p.seg_buf & 512))
       hipLaunchKernelGGL((k_pre_uv_segb<false, false>), gs, bs, pre_uv_seg_lds_bytes(bs.x * bs.y * bs.z), s, d, RI, c,
                          t.nstp, t.nnew, t.nrhs);

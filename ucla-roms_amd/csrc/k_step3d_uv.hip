@@ -539,6 +539,8 @@ void setup_uv1_seg() {
                             (int)uv1_seg_lds_bytes(kSegBlock * kSegJMax));
   (void)hipFuncSetAttribute((const void*)k_uv1_segb<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)uv1_seg_lds_bytes(kSegBlock * kSegJMax));
+  (void)hipFuncSetAttribute((const void*)k_uv1_segb<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)uv1_seg_lds_bytes(kSegBlock * kSegJMax));
 }
 
 void launch_step3d_uv1(const Dev& d, hipStream_t s, const Tlev& t, bool uv_done) {
@@ -552,7 +554,10 @@ void launch_step3d_uv1(const Dev& d, hipStream_t s, const Tlev& t, bool uv_done)
   else if (d.p.colseg) {
     const dim3 gs = seg_uv_grid(d, R, d.p.seg_jrows), bs(kCX, seg_waves(b.N), d.p.seg_jrows);
     ktimer_mark(s, kTimedUv1Seg, 0);
-    if (d.p.uv1_lds && d.p.uv_adv && (d.p.seg_buf & 32) && (d.p.seg_buf & 512))
+    if (d.p.uv1_lds && d.p.uv_adv && (d.p.seg_buf & 32) && (d.p.seg_buf & 512) && (d.p.seg_buf & 64))
+      hipLaunchKernelGGL((k_uv1_segb<true, false>), gs, bs, uv1_seg_lds_bytes(bs.x * bs.y * bs.z), s, d, R, t.nnew,
+                         t.nrhs);
+    else if (d.p.uv1_lds && d.p.uv_adv && (d.p.seg_buf & 32) && (d.p.seg_buf & 512))
       hipLaunchKernelGGL((k_uv1_segb<false, false>), gs, bs, uv1_seg_lds_bytes(bs.x * bs.y * bs.z), s, d, R, t.nnew,
                          t.nrhs);
     else if (d.p.uv1_lds && d.p.uv_adv && (d.p.seg_buf & 32) && (d.p.seg_buf & 64))
