@@ -50,7 +50,7 @@ pmc)
   export ROMS_GPU_NO_GRAPH=1
   for W in c2 c3; do
     if [ $W = c2 ]; then B="python $R/bench.py --no-cpu-baseline --no-secondary --workload c2 --timing-steps 1 --steps 4 --warmup 1"; M=k_step3d_t_v
-    else B="python $R/bench.py --no-cpu-baseline --no-secondary --workload c3 --timing-steps 1 --steps 2 --warmup 1"; M=k_step3d_t_seg; fi
+    else B="python $R/bench.py --no-cpu-baseline --no-secondary --workload c3 --timing-steps 1 --steps 2 --warmup 1"; M=k_step3d_t_segb; fi
     timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pt_f_$W -o run -- $B > $O/pt_f_$W.log 2>&1 || exit 1
     timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pt_w_$W -o run -- $B > $O/pt_w_$W.log 2>&1 || exit 1
     python3 $R/tools/pmc_traffic.py $(find $O/pt_f_$W -name '*counter_collection.csv') $(find $O/pt_w_$W -name '*counter_collection.csv') \

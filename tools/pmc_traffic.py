@@ -33,6 +33,9 @@ ROUTINE_OF = {
     "k_v3dbc": "step3d_uv2", "k_pre_tracer_h1": "pre_step3d", "k_step3d_t_h1": "step3d_t",
     # round-3 late: staged-window forms
     "k_visc3d_stg": "visc3d", "k_t3dmix_stg": "t3dmix",
+    # round 5: buffer-addressed segment solvers
+    "k_pre_tracer_segb": "pre_step3d", "k_pre_uv_segb": "pre_step3d", "k_uv1_segb": "step3d_uv1",
+    "k_step3d_t_segb": "step3d_t",
 }
 CALLS_PER_STEP = {"rho_eos": 2, "set_HUV": 1, "omega": 3, "prsgrd": 2, "pre_step3d": 1, "set_HUV1": 1,
                   "step3d_uv1": 1, "visc3d": 1, "step2d": None, "step3d_uv2": 1, "step3d_t": 1, "t3dmix": 1,
