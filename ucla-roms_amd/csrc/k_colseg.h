@@ -39,32 +39,36 @@ struct SegSpan {
   int row;          // row j of the lane within the block (threadIdx.z)
   int l;            // the lane's column slot in the block's LDS exchange (col + kSegCW*row)
 };
+// CW: columns per segment (kSegCW for the column solvers; k_omega_seg keeps
+// 64, its own kOmCW)
+template <int CW = kSegCW>
 __device__ __forceinline__ SegSpan seg_span(int N) {
   SegSpan r;
   const int t = (int)(threadIdx.x + blockDim.x * threadIdx.y);
-  r.col = t % kSegCW;
+  r.col = t % CW;
   r.row = (int)threadIdx.z;
-  r.l = r.col + kSegCW * r.row;
-  r.s = t / kSegCW;
-  r.S = (int)(blockDim.x * blockDim.y) / kSegCW;
+  r.l = r.col + CW * r.row;
+  r.s = t / CW;
+  r.S = (int)(blockDim.x * blockDim.y) / CW;
   const int base = N / r.S, rem = N % r.S;
   r.c0 = 1 + r.s * base + min(r.s, rem);
   r.n = base + (r.s < rem ? 1 : 0);
   return r;
 }
-// With one segment per wavefront (kSegCW = 64) the segment index, first cell
+// With one segment per wavefront (CW = 64) the segment index, first cell
 // and row count are wave-uniform: readfirstlane tells the compiler so, and
 // the level offsets derived from them live in SGPRs (buffer-load soffsets).
+template <int CW = kSegCW>
 __device__ __forceinline__ void seg_uniform(SegSpan& r) {
-  if constexpr (kSegCW == kCX) {
-    r.s = __builtin_amdgcn_readfirstlane(r.s);
-    r.c0 = __builtin_amdgcn_readfirstlane(r.c0);
-    r.n = __builtin_amdgcn_readfirstlane(r.n);
-  }
+  static_assert(CW == kCX, "seg_uniform needs one segment per wavefront");
+  r.s = __builtin_amdgcn_readfirstlane(r.s);
+  r.c0 = __builtin_amdgcn_readfirstlane(r.c0);
+  r.n = __builtin_amdgcn_readfirstlane(r.n);
 }
 // wavefronts per block for N levels: S = ceil(N / kSegRows) rounded up to whole wavefronts
+template <int CW = kSegCW>
 inline int seg_waves(int N) {
-  const int per = kCX / kSegCW;
+  const int per = kCX / CW;
   const int S = (N + kSegRows - 1) / kSegRows;
   return (S + per - 1) / per;
 }
@@ -392,8 +396,8 @@ __device__ __forceinline__ void tracer_spline_seg(const SegSpan& sg, int N, long
 // i >= istrU, 1: v at j >= jstrV), kSegCW columns x blockDim.z rows j per block.
 // Lanes outside the column range (i or j) solve a clamped duplicate column
 // (they take part in the barriers) and store nothing.
-// v columns (Params::seg_vtile, kSegCW = 64): a wavefront's 64 lanes hold a
-// 16 x 4 tile of columns instead of one row of 64.  The v stencils read the
+// v columns (Params::seg_vtile): a segment's kSegCW lanes hold a
+// (kSegCW/4) x 4 tile of columns instead of one row (16 x 4 at 64 columns).  The v stencils read the
 // rows j-2..j+1 of Hz and We and j-1 of Hz_fwd/bak, Akv, Wi; with one row per
 // wavefront every one of those rows is another block's row and comes from
 // HBM again (no L2 reuse at ~1 MB of columns per block), with four rows per
@@ -401,7 +405,7 @@ __device__ __forceinline__ void tracer_spline_seg(const SegSpan& sg, int N, long
 // 16-wide row is one 128-B line at the device row pitch (roms_dev.h).  The
 // blocks of the two directions enumerate their own tiles; a block whose
 // tile lies outside the range is idle (returns before any barrier).
-constexpr int kVTX = 16, kVTY = 4;
+constexpr int kVTY = 4, kVTX = kSegCW / kVTY;   // 16 x 4 at 64 columns, 8 x 4 at 32
 struct SegCol {
   int i, j, dir;
   bool act, idle;

@@ -780,11 +780,12 @@ __global__ void __launch_bounds__(kSegBlock, ROMS_SEG_BUF_WAVES) k_pre_tracer_se
   const Fields& F = d.f;
   const int N = b.N;
   SegSpan sg = seg_span(N);
-  if constexpr (UNI) seg_uniform(sg);
+  constexpr bool kU = UNI && kSegCW == kCX;   // scalar level offsets need one segment per wavefront
+  if constexpr (kU) seg_uniform(sg);
   // UNI: level offsets in the SGPR soffset; else added to the VGPR offset
-  auto LD = [&](const BufF64& B, unsigned v, unsigned l) { return UNI ? B.ld(v, l) : B.ld(v + l, 0u); };
+  auto LD = [&](const BufF64& B, unsigned v, unsigned l) { return kU ? B.ld(v, l) : B.ld(v + l, 0u); };
   auto ST = [&](const BufF64& B, double x, unsigned v, unsigned l) {
-    if constexpr (UNI) B.st(x, v, l);
+    if constexpr (kU) B.st(x, v, l);
     else B.st(x, v + l, 0u);   // v = kBufOff stays beyond the extent
   };
   const int iu = tile_i0(R.i0) + (int)bI.x * kSegCW + sg.col;
@@ -1003,11 +1004,12 @@ __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_pre_uv_segb(Dev d, 
   const Fields& F = d.f;
   const int N = b.N, indx = 3 - nstp;
   SegSpan sg = seg_span(N);
-  if constexpr (UNI) seg_uniform(sg);
+  constexpr bool kU = UNI && kSegCW == kCX;   // scalar level offsets need one segment per wavefront
+  if constexpr (kU) seg_uniform(sg);
   // UNI: level offsets in the SGPR soffset; else added to the VGPR offset
-  auto LD = [&](const BufF64& B, unsigned v, unsigned l) { return UNI ? B.ld(v, l) : B.ld(v + l, 0u); };
+  auto LD = [&](const BufF64& B, unsigned v, unsigned l) { return kU ? B.ld(v, l) : B.ld(v + l, 0u); };
   auto ST = [&](const BufF64& B, double x, unsigned v, unsigned l) {
-    if constexpr (UNI) B.st(x, v, l);
+    if constexpr (kU) B.st(x, v, l);
     else B.st(x, v + l, 0u);   // v = kBufOff stays beyond the extent
   };
   SegCol col;
@@ -1036,7 +1038,7 @@ __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_pre_uv_segb(Dev d, 
   };
   if constexpr (PF) load_hf();
   double fl[KR];
-  uv_spline_segb<KR, UNI>(d, sg, X, ij, nrhs, dir, fl, [&](int q, unsigned L, double h0, double h1, double u) {
+  uv_spline_segb<KR, kU>(d, sg, X, ij, nrhs, dir, fl, [&](int q, unsigned L, double h0, double h1, double u) {
     if (q >= 1 && q < KR) {   // cells c0..c0+KR-2 (q is a constant of the unrolled load loop)
       Sb[(q - 1) * nthr] = c.cf_stp * u + c.cf_bak * LD(Uix, vo, L);
       Su[(q - 1) * nthr] = 0.5 * (h0 + h1) * u;

@@ -391,11 +391,12 @@ __global__ void __launch_bounds__(kSegBlock, ROMS_SEG_BUF_WAVES) k_step3d_t_segb
   const int N = b.N;
   const double dt = P.dt;
   SegSpan sg = seg_span(N);
-  if constexpr (UNI) seg_uniform(sg);
+  constexpr bool kU = UNI && kSegCW == kCX;   // scalar level offsets need one segment per wavefront
+  if constexpr (kU) seg_uniform(sg);
   // UNI: level offsets in the SGPR soffset; else added to the VGPR offset
-  auto LD = [&](const BufF64& B, unsigned v, unsigned l) { return UNI ? B.ld(v, l) : B.ld(v + l, 0u); };
+  auto LD = [&](const BufF64& B, unsigned v, unsigned l) { return kU ? B.ld(v, l) : B.ld(v + l, 0u); };
   auto ST = [&](const BufF64& B, double x, unsigned v, unsigned l) {
-    if constexpr (UNI) B.st(x, v, l);
+    if constexpr (kU) B.st(x, v, l);
     else B.st(x, v + l, 0u);   // v = kBufOff stays beyond the extent
   };
   const int iu = tile_i0(R.i0) + (int)bI.x * kSegCW + sg.col;

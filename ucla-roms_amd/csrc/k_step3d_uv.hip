@@ -424,7 +424,8 @@ __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_uv1_segb(Dev d, Ran
   const int N = b.N;
   const double dt = d.p.dt;
   SegSpan sg = seg_span(N);
-  if constexpr (UNI) seg_uniform(sg);
+  constexpr bool kU = UNI && kSegCW == kCX;   // scalar level offsets need one segment per wavefront
+  if constexpr (kU) seg_uniform(sg);
   SegCol col;
   seg_uv_col(d, R, bI, sg, col);
   if (col.idle) return;   // uniform over the block
@@ -439,13 +440,13 @@ __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_uv1_segb(Dev d, Ran
   double* const Sh = roms_smem + tid;                             // Hz(c0-1+q) at Sh[q*nthr]
   double* const Shm = roms_smem + (long)(KR + 1) * nthr + tid;    // its neighbour's at Shm[q*nthr]
   const BufF64 Un((dir == 0 ? F.u : F.v) + (long)(nnew - 1) * b.n3);
-  auto LD = [&](const BufF64& B, unsigned v, unsigned l) { return UNI ? B.ld(v, l) : B.ld(v + l, 0u); };
+  auto LD = [&](const BufF64& B, unsigned v, unsigned l) { return kU ? B.ld(v, l) : B.ld(v + l, 0u); };
   double fl[KR], un[PF ? KR : 1];
   if constexpr (PF) {
 #pragma unroll
     for (int p = 0; p < KR; p++) un[p] = LD(Un, vo, lev(c0 + p));
   }
-  uv_spline_segb<KR, UNI>(d, sg, X, ij, nrhs, dir, fl, [&](int q, unsigned, double h0, double h1, double) {
+  uv_spline_segb<KR, kU>(d, sg, X, ij, nrhs, dir, fl, [&](int q, unsigned, double h0, double h1, double) {
     Sh[q * nthr] = h0;
     Shm[q * nthr] = h1;
   });
@@ -513,7 +514,7 @@ __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_uv1_segb(Dev d, Ran
 #pragma unroll
   for (int p = 0; p < KR; p++)
     if (p < n) {
-      if constexpr (UNI) Un.st(T.D[p] * 0.5 * (HZ(p + 1) + HZM(p + 1)), vs, lev(c0 + p));
+      if constexpr (kU) Un.st(T.D[p] * 0.5 * (HZ(p + 1) + HZM(p + 1)), vs, lev(c0 + p));
       else Un.st(T.D[p] * 0.5 * (HZ(p + 1) + HZM(p + 1)), act ? vo + lev(c0 + p) : kBufOff, 0u);
     }
   if (act && sg.s == 0) {

@@ -419,18 +419,21 @@ __global__ void __launch_bounds__(256) k_omega(Dev d, Range R, double dtau) {
 // pre_step3d writes them.  The flux differences of the level are kept in
 // dynamic LDS across the chain ([kOmR][threads], through an opaque offset).
 constexpr int kOmR = kSegRows;   // levels per wave (N <= kSegRows * kSegMaxS)
+// one segment per wavefront whatever the column solvers' kSegCW: 32-column
+// blocks measured slower here (1.27 -> 1.76 ms per C3 call, r5_p_seg_cw32_ab.txt)
+constexpr int kOmCW = kCX, kOmBlock = kSegMaxS * kOmCW;
 template <bool kHB>
-__global__ void __launch_bounds__(kSegBlock, 2) k_omega_seg(Dev d, Range R, double dtau, double hcff) {
+__global__ void __launch_bounds__(kOmBlock, 2) k_omega_seg(Dev d, Range R, double dtau, double hcff) {
   const uint3 bI = xcd_tile();
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const int N = b.N;
   const double cu_min = 0.6, cu_max = 1.0, cmnx_ratio = cu_min / cu_max, cutoff = 2.0 - cmnx_ratio,
                r4cmx = 0.25 / (1.0 - cmnx_ratio);
-  SegSpan sg = seg_span(N);
-  seg_uniform(sg);   // level offsets in SGPRs
+  SegSpan sg = seg_span<kOmCW>(N);
+  seg_uniform<kOmCW>(sg);   // level offsets in SGPRs
   const int s = sg.s, S = sg.S, c0 = sg.c0, n = sg.n, l = sg.col;
-  const int iu = tile_i0(R.i0) + (int)bI.x * kSegCW + l, ju = R.j0 + (int)bI.y;
+  const int iu = tile_i0(R.i0) + (int)bI.x * kOmCW + l, ju = R.j0 + (int)bI.y;
   const bool act = iu >= R.i0 && iu <= R.i1 && ju <= R.j1;
   const int i = iu < R.i0 ? R.i0 : (iu < R.i1 ? iu : R.i1), j = ju < R.j1 ? ju : R.j1;
   const long ij = IJ(b, i, j), n2 = b.n2, sj = b.nx2;
@@ -438,8 +441,8 @@ __global__ void __launch_bounds__(kSegBlock, 2) k_omega_seg(Dev d, Range R, doub
   // the level in an SGPR (no 64-bit address per level)
   const unsigned vo = (unsigned)ij * 8u, lv = (unsigned)n2 * 8u;
   const BufF64 FU(F.FlxU), FV(F.FlxV), Hz(F.Hz), zw(F.z_w);
-  __shared__ double Lw[kSegMaxS][kSegCW], Lcx[kSegMaxS][kSegCW], Lhz[kSegMaxS][kSegCW];
-  __shared__ double Lte[kHB ? kSegMaxS : 1][kSegCW], Lti[kHB ? kSegMaxS : 1][kSegCW];   // kHB: segment tops' We, Wi
+  __shared__ double Lw[kSegMaxS][kOmCW], Lcx[kSegMaxS][kOmCW], Lhz[kSegMaxS][kOmCW];
+  __shared__ double Lte[kHB ? kSegMaxS : 1][kOmCW], Lti[kHB ? kSegMaxS : 1][kOmCW];   // kHB: segment tops' We, Wi
   double fu1[kOmR], fu0[kOmR], fv1[kOmR], fv0[kOmR], cx[kOmR], hz[kOmR], zk[kOmR];
 #pragma unroll
   for (int q = 0; q < kOmR; q++) {   // rho level k = c0+q (clamped), w-level k
@@ -584,7 +587,7 @@ __global__ void k_omega_edges(Dev d) {
 static size_t omega_hb_lds_bytes(unsigned nthr) { return (size_t)kOmR * nthr * sizeof(double); }
 void setup_omega_seg() {
   (void)hipFuncSetAttribute((const void*)k_omega_seg<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)omega_hb_lds_bytes(kSegBlock));
+                            (int)omega_hb_lds_bytes(kOmBlock));
 }
 
 // hcff > 0 (the predictor's call): also form pre_step3d's Hz_bak / Hz_fwd of
@@ -603,7 +606,7 @@ bool launch_omega(const Dev& d, hipStream_t s, const Tlev& t, double hcff) {
       d, s, R, ExchList{{d.f.We, d.f.Wi}, {b.N + 1, b.N + 1}, 2},
       [&](const Range& r) {
         // the segment form for full-width ranges (rim strips keep k_omega)
-        const dim3 gs((r.i1 - tile_i0(r.i0) + kSegCW) / kSegCW, r.j1 - r.j0 + 1), bs(kCX, seg_waves(b.N));
+        const dim3 gs((r.i1 - tile_i0(r.i0) + kOmCW) / kOmCW, r.j1 - r.j0 + 1), bs(kCX, seg_waves<kOmCW>(b.N));
         if (hb)
           hipLaunchKernelGGL(k_omega_seg<true>, gs, bs, omega_hb_lds_bytes(bs.x * bs.y), s, d, r, dtau, hcff);
         else if (seg_ok && r.i1 - r.i0 + 1 >= 32)

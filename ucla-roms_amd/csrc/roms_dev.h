@@ -277,7 +277,11 @@ constexpr int kCX = 64;
 constexpr int kSegRows = ROMS_SEG_ROWS;   // cells per segment (register arrays of kSegRows + 2)
 constexpr int kSegMaxS = ROMS_SEG_MAXS;   // segments per block (kSegCW columns each): N <= kSegRows * kSegMaxS
 #ifndef ROMS_SEG_CW
-#define ROMS_SEG_CW 64   // round 3: 64-wide blocks (one segment per wavefront) 1-2% faster at C3 than 16 (r3_l_seg_shape_ab.txt)
+// round 5: 32-column blocks (two segments per wavefront, 256-thread blocks,
+// two per CU): pre_step3d -0.8 ms, step3d_uv1 -0.3 ms at C3
+// (r5_p_seg_cw32_ab.txt); round 3 had measured 64 ahead of 16
+// (r3_l_seg_shape_ab.txt, before the solvers kept their reloads in LDS)
+#define ROMS_SEG_CW 32
 #endif
 constexpr int kSegCW = ROMS_SEG_CW;       // columns per segment-solver block (lanes of one segment)
 constexpr int kSegBlock = ((kSegMaxS * kSegCW + 63) / 64) * 64;   // threads of a segment-solver block (max)
@@ -285,7 +289,7 @@ constexpr int kSegBlock = ((kSegMaxS * kSegCW + 63) / 64) * 64;   // threads of 
 // same kSegCW columns, so the v columns' j-1, j-2, j+1 stencil rows are loaded
 // by the neighbouring rows' waves of the same block, close together in time.
 #ifndef ROMS_SEG_JMAX
-#define ROMS_SEG_JMAX (ROMS_SEG_CW >= 64 ? 1 : 4)
+#define ROMS_SEG_JMAX 1
 #endif
 constexpr int kSegJMax = ROMS_SEG_JMAX;
 // the fewest rows any segment of a launch may have (k_colseg.h seg_live)
