@@ -396,8 +396,8 @@ __device__ __forceinline__ void tracer_spline_seg(const SegSpan& sg, int N, long
 // i >= istrU, 1: v at j >= jstrV), kSegCW columns x blockDim.z rows j per block.
 // Lanes outside the column range (i or j) solve a clamped duplicate column
 // (they take part in the barriers) and store nothing.
-// v columns (Params::seg_vtile): a segment's kSegCW lanes hold a
-// (kSegCW/4) x 4 tile of columns instead of one row (16 x 4 at 64 columns).  The v stencils read the
+// v columns (Params::seg_vtile, kSegCW = 64): a wavefront's 64 lanes hold a
+// 16 x 4 tile of columns instead of one row of 64.  The v stencils read the
 // rows j-2..j+1 of Hz and We and j-1 of Hz_fwd/bak, Akv, Wi; with one row per
 // wavefront every one of those rows is another block's row and comes from
 // HBM again (no L2 reuse at ~1 MB of columns per block), with four rows per
@@ -405,7 +405,10 @@ __device__ __forceinline__ void tracer_spline_seg(const SegSpan& sg, int N, long
 // 16-wide row is one 128-B line at the device row pitch (roms_dev.h).  The
 // blocks of the two directions enumerate their own tiles; a block whose
 // tile lies outside the range is idle (returns before any barrier).
-constexpr int kVTY = 4, kVTX = kSegCW / kVTY;   // 16 x 4 at 64 columns, 8 x 4 at 32
+// (16 x 4 at 64 columns; the 8 x 4 tiles of 32-column segments measured
+// much slower, C3 58.3 vs 53.9 ms, r5_r_vtile_cw32_ab.txt, so segments of 32
+// columns keep their v columns in rows)
+constexpr int kVTX = 16, kVTY = 4;
 struct SegCol {
   int i, j, dir;
   bool act, idle;
