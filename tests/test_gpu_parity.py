@@ -543,12 +543,12 @@ def test_ld16_windows_bitwise(case, monkeypatch):
 @pytest.mark.parametrize("lmd", [oracle.LMD_ICELAND, oracle.LMD_ALL | oracle.LMD_DDMIX])
 def test_kpp_int_staged_rig_bitwise(lmd, monkeypatch):
     """k_kpp_int with the Rig stencil windows staged in LDS (ROMS_GPU_KPP_TY
-    4 = the default, 8, 43) equals the one-row form (=0) bitwise over 4 whole steps of
+    4 = the default, 2, 8, 43) equals the one-row form (=0) bitwise over 4 whole steps of
     the split-EOS basin with KPP (edge clamps at all four closed walls, a
     partial last block row: MMm = 42)."""
     cfg = basin_cfg(LLm=70, MMm=42, N=12, nonlin=True)
     out = []
-    for env in ("0", "4", "8", "43"):   # one row; 64x4; 64x8; 64x4 at 3 waves/SIMD
+    for env in ("0", "4", "2", "8", "43"):   # one row; 64x4; 64x2; 64x8; 64x4 at 3 waves/SIMD
         monkeypatch.setenv("ROMS_GPU_KPP_TY", env)
         m = romsgpu.Model.from_case(cfg.case_id, cfg.LLm, cfg.MMm, cfg.N, cfg.NT, salinity=True, nonlin_eos=True,
                                     dt=cfg.dt, ndtfast=cfg.ndtfast, sizex=cfg.sizex, sizey=cfg.sizey, lmd=lmd,

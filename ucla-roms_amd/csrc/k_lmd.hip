@@ -654,12 +654,14 @@ void launch_lmd_vmix(const Dev& d, hipStream_t s, const Tlev& t, int tind) {
   else
     hipLaunchKernelGGL(k_kpp_ext<ColLds>, gridc_of(E), dim3(kCX), col_lds_bytes(1, b.N), s, d, E, tind, t.nstp, kc);
   if (d.p.kpp_ty && d.p.lmd_rimix) {   // staged Rig windows on 64 x TY column blocks
-    const int ty = (d.p.kpp_ty == 8 && !d.p.lmd_ddmix) ? 8 : 4;   // the DDMIX form is instantiated on 64x4 only
+    const int ty = d.p.lmd_ddmix ? 4 : (d.p.kpp_ty == 8 || d.p.kpp_ty == 2) ? d.p.kpp_ty : 4;   // the DDMIX form is instantiated on 64x4 only
     dim3 g = gridc_of(R);
     g.y = (g.y + ty - 1) / ty;
     const EdgeClamp ec = edge_clamp(b);
     if (d.p.lmd_ddmix)
       hipLaunchKernelGGL((k_kpp_int<true, 4>), g, dim3(kCX, 4), 0, s, d, R, ec, tind, t.nstp, first, kc);
+    else if (d.p.kpp_ty == 2)
+      hipLaunchKernelGGL((k_kpp_int<false, 2>), g, dim3(kCX, 2), 0, s, d, R, ec, tind, t.nstp, first, kc);
     else if (d.p.kpp_ty == 8)
       hipLaunchKernelGGL((k_kpp_int<false, 8>), g, dim3(kCX, 8), 0, s, d, R, ec, tind, t.nstp, first, kc);
     else if (d.p.kpp_ty == 43)

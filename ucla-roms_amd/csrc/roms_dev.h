@@ -277,11 +277,12 @@ constexpr int kCX = 64;
 constexpr int kSegRows = ROMS_SEG_ROWS;   // cells per segment (register arrays of kSegRows + 2)
 constexpr int kSegMaxS = ROMS_SEG_MAXS;   // segments per block (kSegCW columns each): N <= kSegRows * kSegMaxS
 #ifndef ROMS_SEG_CW
-// round 5: 32-column blocks (two segments per wavefront, 256-thread blocks,
-// two per CU): pre_step3d -0.8 ms, step3d_uv1 -0.3 ms at C3
-// (r5_p_seg_cw32_ab.txt); round 3 had measured 64 ahead of 16
+// round 5: 16-column blocks (four segments per wavefront, 128-thread
+// blocks, four per CU): against 64 columns pre_step3d 11.1 -> 9.9 ms,
+// step3d_uv1 4.55 -> 3.93 ms at C3 (r5_q_seg_cw32_default_ab.txt,
+// r5_s_seg_cw16_ab.txt); round 3 had measured 64 ahead of 16
 // (r3_l_seg_shape_ab.txt, before the solvers kept their reloads in LDS)
-#define ROMS_SEG_CW 32
+#define ROMS_SEG_CW 16
 #endif
 constexpr int kSegCW = ROMS_SEG_CW;       // columns per segment-solver block (lanes of one segment)
 constexpr int kSegBlock = ((kSegMaxS * kSegCW + 63) / 64) * 64;   // threads of a segment-solver block (max)

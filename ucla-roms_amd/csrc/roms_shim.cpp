@@ -944,7 +944,7 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     // call at C3 (r3_zp_kpp_ty_ab.txt); ROMS_GPU_KPP_TY=0 for one row per block
     const char* e = getenv("ROMS_GPU_KPP_TY");
     P.kpp_ty = 4;
-    if (e && (atoi(e) == 0 || atoi(e) == 8 || atoi(e) == 43)) P.kpp_ty = atoi(e);
+    if (e && (atoi(e) == 0 || atoi(e) == 2 || atoi(e) == 8 || atoi(e) == 43)) P.kpp_ty = atoi(e);
   }
   {
     const char* e = getenv("ROMS_GPU_HOIST");
