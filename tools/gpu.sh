@@ -13,6 +13,8 @@
 #                             V = lib:<tag> (ucla-roms_amd/libromsgpu_<tag>.so from tools/build_variant.sh;
 #                             lib:cur the in-tree build) or env:VAR=1,VAR2=0 (environment switches)
 #   stall                     issue/wait PMC of the C2 kernels (tools/pmc_stall.sh)
+#   final TAG                 the default bench line, C3/C2 kernel traces, PMC tables and a 2-rank
+#                             one-GPU rehearsal (both exchange orders): the round's profile set
 CMD=$1; TAG=$2; shift 2
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}; O=$R/gpurun_out; mkdir -p $O; cd $R
 PYT="python -u -m pytest -q --timeout 300 --timeout-method thread"
@@ -84,5 +86,14 @@ ab)
   done ;;
 stall)
   bash $R/tools/pmc_stall.sh ;;
-*) echo "usage: bash tools/gpu.sh suite|tests|bench|trace|pmc|ab|stall TAG ..."; exit 2 ;;
+final)
+  timeout -k 10 500 python bench.py > $O/bench_$TAG.json 2> $O/bench_$TAG.err || { echo BENCHFAIL; tail -20 $O/bench_$TAG.err; exit 1; }
+  row $O/bench_$TAG.json bench
+  bash $R/tools/gpu.sh trace ${TAG}_c3 c3 || exit 1
+  bash $R/tools/gpu.sh trace ${TAG}_c2 c2 || exit 1
+  bash $R/tools/gpu.sh pmc x || exit 1
+  cd $R
+  timeout -k 10 300 python bench.py --gpus 2 --steps 5 --warmup 1 --no-cpu-baseline --no-secondary > $O/bench_${TAG}_n2.json 2> $O/bench_${TAG}_n2.err || { tail -10 $O/bench_${TAG}_n2.err; exit 1; }
+  python3 -c "import json; d=json.load(open('$O/bench_${TAG}_n2.json')); print('n2', d['ms_per_step'], d['config'].get('exchange_overlap'))" ;;
+*) echo "usage: bash tools/gpu.sh suite|tests|bench|trace|pmc|ab|stall|final TAG ..."; exit 2 ;;
 esac
