@@ -205,3 +205,67 @@ def test_tracer_strip_chunks_bitwise(chunk, monkeypatch):
         m.close()
     for n in out[0]:
         assert np.array_equal(out[0][n], out[1][n]), n
+
+
+def _omega_cfg(case):
+    if case == "n50":
+        return seg_cfg("n50")
+    c = basin_cfg(nonlin=True, LLm=40, MMm=16, N=100)   # >= 32 columns wide: the segment form runs
+    c.lmd, c.surf_flux = oracle.LMD_ALL, 1
+    return c
+
+
+@pytest.mark.parametrize("case", ["n50", "n100"])
+def test_omega_blocks(case, monkeypatch):
+    """k_omega_seg on 64-, 32- and 16-column blocks (ROMS_GPU_OMEGA_CW), with
+    the k-order chain of partial sums (ROMS_GPU_OMEGA_PAR=0) and with each
+    segment summing its own levels while the others do (PAR=1):
+    - the chain keeps the reference's order: 6 whole steps (predictor omega
+      with Hz_bak/Hz_fwd, corrector, closing omega) equal across block widths
+      bitwise; so do the PAR forms among themselves (same segment partition);
+    - PAR reassociates the sums: one omega call within RTOL_ROUTINE of the
+      oracle, and 6 whole steps within RMS_RUN of the chain form."""
+    cfg = _omega_cfg(case)
+    names = ("zeta", "ubar", "vbar", "u", "v", "t", "We", "Wi", "rufrc", "rvfrc")
+    runs = {}
+    for par in ("0", "1"):
+        for cw in ("64", "32", "16"):
+            monkeypatch.setenv("ROMS_GPU_OMEGA_PAR", par)
+            monkeypatch.setenv("ROMS_GPU_OMEGA_CW", cw)
+            m = make_model(cfg, 1)
+            m.step(6)
+            runs[par, cw] = {n: m.get(n) for n in names}
+            m.close()
+    for par in ("0", "1"):
+        for cw in ("32", "16"):
+            for n in names:
+                assert np.array_equal(runs[par, "64"][n], runs[par, cw][n]), (par, cw, n)
+    for n in names:
+        a, b = runs["0", "64"][n], runs["1", "64"][n]
+        rms = float(np.sqrt(np.mean((a - b) ** 2)))
+        # Wi is cancellation noise (~1e-13) where the Courant split leaves it
+        # zero: measured against We's scale, as in test_gpu_bulk
+        ref = runs["0", "64"]["We" if n == "Wi" else n]
+        assert rms <= RMS_RUN * max(float(np.sqrt(np.mean(ref ** 2))), 1e-30), (n, rms)
+    o = oracle.Oracle(cfg)
+    o.init()
+    o.step(3)
+    iic, kstp, knew, nstp, nrhs, nnew = o.tindex()
+    o.set_tindex([iic, kstp, knew, nstp, 3, 3 - nstp])
+    for cw in ("64", "16"):
+        monkeypatch.setenv("ROMS_GPU_OMEGA_PAR", "1")
+        monkeypatch.setenv("ROMS_GPU_OMEGA_CW", cw)
+        m = make_model(cfg, 1)
+        copy_state(o, m)
+        m.set_tindex(iic, kstp, knew, nstp, 3, 3 - nstp, nfast=o.nfast())
+        m.omega()
+        m.sync()
+        res = {n: interior(m.get(n), cfg.LLm, cfg.MMm) for n in ("We", "Wi")}
+        m.close()
+        if cw == "64":
+            o.call("omega")
+        for n in ("We", "Wi"):
+            ref = interior(o.field(n), cfg.LLm, cfg.MMm)
+            scale = float(np.abs(interior(o.field("We"), cfg.LLm, cfg.MMm)).max())
+            err = float(np.abs(res[n] - ref).max()) / scale
+            assert err <= RTOL_ROUTINE, (cw, n, err)

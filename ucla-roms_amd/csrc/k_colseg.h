@@ -39,8 +39,8 @@ struct SegSpan {
   int row;          // row j of the lane within the block (threadIdx.z)
   int l;            // the lane's column slot in the block's LDS exchange (col + kSegCW*row)
 };
-// CW: columns per segment (kSegCW for the column solvers; k_omega_seg keeps
-// 64, its own kOmCW)
+// CW: columns per segment (kSegCW for the column solvers; k_omega_seg has
+// its own, ROMS_GPU_OMEGA_CW)
 template <int CW = kSegCW>
 __device__ __forceinline__ SegSpan seg_span(int N) {
   SegSpan r;

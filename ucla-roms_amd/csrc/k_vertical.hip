@@ -419,38 +419,51 @@ __global__ void __launch_bounds__(256) k_omega(Dev d, Range R, double dtau) {
 // pre_step3d writes them.  The flux differences of the level are kept in
 // dynamic LDS across the chain ([kOmR][threads], through an opaque offset).
 constexpr int kOmR = kSegRows;   // levels per wave (N <= kSegRows * kSegMaxS)
-// one segment per wavefront whatever the column solvers' kSegCW: 32-column
-// blocks measured slower here (1.27 -> 1.76 ms per C3 call, r5_p_seg_cw32_ab.txt)
+// CW columns per block (ROMS_GPU_OMEGA_CW, default 16: four segments per
+// wavefront, several blocks per CU whose load and chain phases overlap;
+// 1.41 -> 1.24 ms per C3 call against 64, r5_w_omega_cw_par_ab.txt; level
+// offsets then go in the VGPR offset -- with SGPR offsets 32 columns had
+// measured 1.76 ms, r5_p_seg_cw32_ab.txt).  PAR (ROMS_GPU_OMEGA_PAR, opt-in):
+// each segment sums its own levels from zero while the others do, one
+// barrier, then adds the lower segments' totals in k order -- the chain of S
+// barrier steps becomes one (sums reassociated: not bitwise to PAR false;
+// no faster at 16 columns).
 constexpr int kOmCW = kCX, kOmBlock = kSegMaxS * kOmCW;
-template <bool kHB>
-__global__ void __launch_bounds__(kOmBlock, 2) k_omega_seg(Dev d, Range R, double dtau, double hcff) {
+template <bool kHB, int CW = kOmCW, bool PAR = false>
+__global__ void __launch_bounds__(kSegMaxS * CW, 2) k_omega_seg(Dev d, Range R, double dtau, double hcff) {
   const uint3 bI = xcd_tile();
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const int N = b.N;
   const double cu_min = 0.6, cu_max = 1.0, cmnx_ratio = cu_min / cu_max, cutoff = 2.0 - cmnx_ratio,
                r4cmx = 0.25 / (1.0 - cmnx_ratio);
-  SegSpan sg = seg_span<kOmCW>(N);
-  seg_uniform<kOmCW>(sg);   // level offsets in SGPRs
+  SegSpan sg = seg_span<CW>(N);
+  constexpr bool kU = CW == kCX;   // one segment per wavefront: level offsets in SGPRs
+  if constexpr (kU) seg_uniform<CW>(sg);
   const int s = sg.s, S = sg.S, c0 = sg.c0, n = sg.n, l = sg.col;
-  const int iu = tile_i0(R.i0) + (int)bI.x * kOmCW + l, ju = R.j0 + (int)bI.y;
+  const int iu = tile_i0(R.i0) + (int)bI.x * CW + l, ju = R.j0 + (int)bI.y;
   const bool act = iu >= R.i0 && iu <= R.i1 && ju <= R.j1;
   const int i = iu < R.i0 ? R.i0 : (iu < R.i1 ? iu : R.i1), j = ju < R.j1 ? ju : R.j1;
   const long ij = IJ(b, i, j), n2 = b.n2, sj = b.nx2;
   // buffer loads: the lane's column (and its i+1 / j+1 neighbour) in a VGPR,
-  // the level in an SGPR (no 64-bit address per level)
+  // the level in an SGPR (kU) or added to the VGPR offset
   const unsigned vo = (unsigned)ij * 8u, lv = (unsigned)n2 * 8u;
   const BufF64 FU(F.FlxU), FV(F.FlxV), Hz(F.Hz), zw(F.z_w);
-  __shared__ double Lw[kSegMaxS][kOmCW], Lcx[kSegMaxS][kOmCW], Lhz[kSegMaxS][kOmCW];
-  __shared__ double Lte[kHB ? kSegMaxS : 1][kOmCW], Lti[kHB ? kSegMaxS : 1][kOmCW];   // kHB: segment tops' We, Wi
+  auto LD = [&](const BufF64& B, unsigned v, unsigned o) { return kU ? B.ld(v, o) : B.ld(v + o, 0u); };
+  auto ST = [&](const BufF64& B, double x, unsigned v, unsigned o) {
+    if constexpr (kU) B.st(x, v, o);
+    else B.st(x, v + o, 0u);   // v = kBufOff stays beyond the extent
+  };
+  __shared__ double Lw[kSegMaxS][CW], Lcx[kSegMaxS][CW], Lhz[kSegMaxS][CW];
+  __shared__ double Lte[kHB ? kSegMaxS : 1][CW], Lti[kHB ? kSegMaxS : 1][CW];   // kHB: segment tops' We, Wi
   double fu1[kOmR], fu0[kOmR], fv1[kOmR], fv0[kOmR], cx[kOmR], hz[kOmR], zk[kOmR];
 #pragma unroll
   for (int q = 0; q < kOmR; q++) {   // rho level k = c0+q (clamped), w-level k
     const int k = min(c0 + q, N);
     const unsigned o = (unsigned)(k - 1) * lv;
-    fu1[q] = FU.ld(vo + 8u, o); fu0[q] = FU.ld(vo, o); fv1[q] = FV.ld(vo + (unsigned)sj * 8u, o); fv0[q] = FV.ld(vo, o);
-    hz[q] = Hz.ld(vo, o);
-    zk[q] = zw.ld(vo, (unsigned)k * lv);
+    fu1[q] = LD(FU, vo + 8u, o); fu0[q] = LD(FU, vo, o); fv1[q] = LD(FV, vo + (unsigned)sj * 8u, o); fv0[q] = LD(FV, vo, o);
+    hz[q] = LD(Hz, vo, o);
+    zk[q] = LD(zw, vo, (unsigned)k * lv);
   }
   const double zw0 = zw.ld(vo, 0), zwN = zw.ld(vo, (unsigned)N * lv);
   const double wsrf = F.swflx[ij] * F.dm_r[ij] * F.dn_r[ij];
@@ -471,6 +484,22 @@ __global__ void __launch_bounds__(kOmBlock, 2) k_omega_seg(Dev d, Range R, doubl
   Lhz[s][l] = hz[0];
   // 1. the partial sums, wave by wave in k order
   double wk[kOmR];
+  if constexpr (PAR) {
+    double wi = 0.0;
+#pragma unroll
+    for (int q = 0; q < kOmR; q++) {
+      double v = wi - fu1[q] + fu0[q] - fv1[q] + fv0[q];
+      if (pidx > 0) v = v + pflx * prf[(long)(min(c0 + q, N) - 1) * d.p.npip];
+      wi = q < n ? v : wi;
+      wk[q] = wi;
+    }
+    Lw[s][l] = wi;
+    __syncthreads();
+    double base = 0.0;
+    for (int t = 0; t < s; t++) base = base + Lw[t][l];
+#pragma unroll
+    for (int q = 0; q < kOmR; q++) wk[q] = base + wk[q];
+  } else
   for (int t = 0; t < S; t++) {
     if (s == t) {
       double wi = t == 0 ? 0.0 : Lw[t - 1][l];
@@ -486,7 +515,12 @@ __global__ void __launch_bounds__(kOmBlock, 2) k_omega_seg(Dev d, Range R, doubl
     __syncthreads();
   }
   // 2. the Courant split of w-levels k = c0..c0+n-1 (k <= N-1)
-  const double wrk = (Lw[S - 1][l] + wsrf) / (zwN - zw0);
+  double wtot = Lw[S - 1][l];
+  if constexpr (PAR) {
+    wtot = 0.0;
+    for (int t = 0; t < S; t++) wtot = wtot + Lw[t][l];
+  }
+  const double wrk = (wtot + wsrf) / (zwN - zw0);
   const double cx_top = s + 1 < S ? Lcx[s + 1][l] : 0.0, hz_top = s + 1 < S ? Lhz[s + 1][l] : 0.0;
   if (!kHB && !act) return;
   const BufF64 Wi(F.Wi), We(F.We);
@@ -501,14 +535,14 @@ __global__ void __launch_bounds__(kOmBlock, 2) k_omega_seg(Dev d, Range R, doubl
     const double div = roms_smem[q * nthr + tr];
     const double FlxDiv = hbf * (div + we1 + wi1 - we0 - wi0);
     const unsigned o = (unsigned)(c0 + q - 1) * lv;
-    Hf.st(hz[q] - FlxDiv, vs, o);
-    Hb.st(hz[q] + FlxDiv, vs, o);
+    ST(Hf, hz[q] - FlxDiv, vs, o);
+    ST(Hb, hz[q] + FlxDiv, vs, o);
   };
   if (s == 0) {
-    Wi.st(0.0, vs, 0);
-    We.st(0.0, vs, 0);
-    Wi.st(0.0, vs, (unsigned)N * lv);
-    We.st(0.0, vs, (unsigned)N * lv);
+    ST(Wi, 0.0, vs, 0);
+    ST(We, 0.0, vs, 0);
+    ST(Wi, 0.0, vs, (unsigned)N * lv);
+    ST(We, 0.0, vs, (unsigned)N * lv);
   }
 #pragma unroll
   for (int q = 0; q < kOmR; q++) {
@@ -533,9 +567,9 @@ __global__ void __launch_bounds__(kOmBlock, 2) k_omega_seg(Dev d, Range R, doubl
     } else {
       we = 0.0;
     }
-    if (q < n && k <= N - 1) {   // wave-uniform
-      We.st(we, vs, (unsigned)k * lv);
-      Wi.st(w, vs, (unsigned)k * lv);
+    if (q < n && k <= N - 1) {   // wave-uniform when kU
+      ST(We, we, vs, (unsigned)k * lv);
+      ST(Wi, w, vs, (unsigned)k * lv);
     }
     if constexpr (kHB) {
       const double we1 = k <= N - 1 ? we : 0.0, wi1 = k <= N - 1 ? w : 0.0;   // We(N) = Wi(N) = 0
@@ -588,6 +622,24 @@ static size_t omega_hb_lds_bytes(unsigned nthr) { return (size_t)kOmR * nthr * s
 void setup_omega_seg() {
   (void)hipFuncSetAttribute((const void*)k_omega_seg<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)omega_hb_lds_bytes(kOmBlock));
+  (void)hipFuncSetAttribute((const void*)k_omega_seg<true, kOmCW, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)omega_hb_lds_bytes(kOmBlock));
+}
+
+// k_omega_seg<kHB, CW, PAR> by ROMS_GPU_OMEGA_CW / ROMS_GPU_OMEGA_PAR
+template <bool kHB, int CW>
+static void omega_seg_cw(const Dev& d, hipStream_t s, const Range& r, double dtau, double hcff) {
+  const Bounds& b = d.b;
+  const dim3 gs((r.i1 - tile_i0(r.i0) + CW) / CW, r.j1 - r.j0 + 1), bs(kCX, seg_waves<CW>(b.N));
+  const size_t lds = kHB ? omega_hb_lds_bytes(bs.x * bs.y) : 0;
+  if (d.p.omega_par) hipLaunchKernelGGL((k_omega_seg<kHB, CW, true>), gs, bs, lds, s, d, r, dtau, hcff);
+  else hipLaunchKernelGGL((k_omega_seg<kHB, CW, false>), gs, bs, lds, s, d, r, dtau, hcff);
+}
+template <bool kHB>
+static void omega_seg(const Dev& d, hipStream_t s, const Range& r, double dtau, double hcff) {
+  if (d.p.omega_cw == 16) omega_seg_cw<kHB, 16>(d, s, r, dtau, hcff);
+  else if (d.p.omega_cw == 32) omega_seg_cw<kHB, 32>(d, s, r, dtau, hcff);
+  else omega_seg_cw<kHB, kOmCW>(d, s, r, dtau, hcff);
 }
 
 // hcff > 0 (the predictor's call): also form pre_step3d's Hz_bak / Hz_fwd of
@@ -606,11 +658,10 @@ bool launch_omega(const Dev& d, hipStream_t s, const Tlev& t, double hcff) {
       d, s, R, ExchList{{d.f.We, d.f.Wi}, {b.N + 1, b.N + 1}, 2},
       [&](const Range& r) {
         // the segment form for full-width ranges (rim strips keep k_omega)
-        const dim3 gs((r.i1 - tile_i0(r.i0) + kOmCW) / kOmCW, r.j1 - r.j0 + 1), bs(kCX, seg_waves<kOmCW>(b.N));
         if (hb)
-          hipLaunchKernelGGL(k_omega_seg<true>, gs, bs, omega_hb_lds_bytes(bs.x * bs.y), s, d, r, dtau, hcff);
+          omega_seg<true>(d, s, r, dtau, hcff);
         else if (seg_ok && r.i1 - r.i0 + 1 >= 32)
-          hipLaunchKernelGGL(k_omega_seg<false>, gs, bs, 0, s, d, r, dtau, 0.0);
+          omega_seg<false>(d, s, r, dtau, 0.0);
         else
           hipLaunchKernelGGL(k_omega, grid_of(r), dim3(kBX, kBY), 0, s, d, r, dtau);
       },

@@ -68,14 +68,16 @@ struct Params {
   int h_ty;       // tile rows of the hoisted horizontal kernels: 4 or 8 (ROMS_GPU_HTY)
   int h_jc;       // rows per block of the j-marching horizontal kernels (multiple of 4; ROMS_GPU_HJC, 0: 64 x h_ty tiles)
   int prs_ty;     // tile rows of k_prsgrd_uv: 4 or 8 (ROMS_GPU_PRS_TY)
-  int ld16;
-  int prs_buf;    // k_prsgrd_uv windows through buffer loads (ROMS_GPU_PRS_BUF)       // padded pitch: LDS windows read two doubles per lane (16-B loads; ROMS_GPU_LD16=0: 8-B)
+  int ld16;       // padded pitch: LDS windows read two doubles per lane (16-B loads; ROMS_GPU_LD16=0: 8-B)
+  int prs_buf;    // k_prsgrd_uv windows through buffer loads (ROMS_GPU_PRS_BUF)
   int visc_stg;   // visc3d: raw u/v/Hz windows staged in LDS per level (default; ROMS_GPU_VISC_STG=0: per-point loads)
   int t3dmix_stg; // t3dmix (two tracers): Hz/T/S windows staged in LDS per level (default; ROMS_GPU_T3DMIX_STG=0: per-point loads)
   int kpp_ty;     // k_kpp_int: 4 (default) staged Rig windows on 64x4 blocks, 8 on 64x8, 43 64x4 at 3 waves/SIMD, 0 one row per block (ROMS_GPU_KPP_TY)
   int tile_grp;   // h_tile group width of the hoisted per-level kernels (ROMS_GPU_TILE_GRP; 0: xcd_tile order)
   int uv1_lds;    // k_uv1_seg: Hz pairs kept in LDS from the spline phase, rufrc chained (ROMS_GPU_UV1_LDS=0: reloads)
   int omega_seg;  // omega: segment form k_omega_seg, one read of each input (ROMS_GPU_OMEGA_SEG=0: two-pass k_omega)
+  int omega_cw;   // k_omega_seg columns per block: 64, 32 or 16 (ROMS_GPU_OMEGA_CW)
+  int omega_par;  // k_omega_seg: segment partial sums in parallel, one barrier (ROMS_GPU_OMEGA_PAR; not bitwise to the k-order chain)
   int p_in_rho;   // rho_eos's sweep also forms prsgrd's P (ROMS_GPU_P_IN_RHO=0: k_prsgrd_P)
   int omega_hb;   // the predictor's omega forms pre_step3d's Hz_bak/Hz_fwd (ROMS_GPU_OMEGA_HB=0: pre_step3d does)
   int preuv_lds;  // k_pre_uv_seg: u(indx) stored and u(nstp)/u(indx) combined in the spline phase (ROMS_GPU_PREUV_LDS=0: reloads)

@@ -898,6 +898,17 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     P.omega_seg = !(e && e[0] == '0');
   }
   {
+    // 16-column blocks (four segments per wavefront, 4 blocks per CU) with
+    // the k-order chain: omega 1.41 -> 1.24 ms per C3 call, as fast as the
+    // parallel partial sums and bitwise to the 64-column form
+    // (r5_w_omega_cw_par_ab.txt)
+    const char* e = getenv("ROMS_GPU_OMEGA_CW");
+    const int v = e ? atoi(e) : 16;
+    P.omega_cw = v == 32 || v == 64 ? v : 16;
+    e = getenv("ROMS_GPU_OMEGA_PAR");
+    P.omega_par = e && e[0] == '1';
+  }
+  {
     const char* e = getenv("ROMS_GPU_PREUV_LDS");
     P.preuv_lds = !(e && e[0] == '0');
   }
