@@ -855,12 +855,17 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     const char* e = getenv("ROMS_GPU_CHAIN");
     if (e && e[0] == '0') P.chain = 0;
   }
-  P.seg_order = 0;
+  // order 3 in groups of 8 x-blocks: on 16-column blocks the resident
+  // blocks of an XCD then cover 8 x 16 columns of consecutive rows, sharing
+  // their i- and j-neighbour lines in L2 (pre_step3d 9.81-9.84 -> 9.61-9.65
+  // ms, step3d_uv1 3.92-3.94 -> 3.81-3.83 ms per C3 call against order 0,
+  // r5_x_seg_order_ab.txt)
+  P.seg_order = 3;
   {
     const char* e = getenv("ROMS_GPU_SEG_ORDER");
     if (e && e[0] >= '0' && e[0] <= '3') P.seg_order = e[0] - '0';
   }
-  P.seg_xg = 4;
+  P.seg_xg = 8;
   {
     const char* e = getenv("ROMS_GPU_SEG_XG");
     if (e && atoi(e) > 0) P.seg_xg = atoi(e);
@@ -902,8 +907,9 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     // the k-order chain: omega 1.41 -> 1.24 ms per C3 call, as fast as the
     // parallel partial sums and bitwise to the 64-column form
     // (r5_w_omega_cw_par_ab.txt)
+    // (at N <= 63, C2, 64 columns stay: 0.161 against 0.167 ms per call)
     const char* e = getenv("ROMS_GPU_OMEGA_CW");
-    const int v = e ? atoi(e) : 16;
+    const int v = e ? atoi(e) : (dims->N > 63 ? 16 : 64);
     P.omega_cw = v == 32 || v == 64 ? v : 16;
     e = getenv("ROMS_GPU_OMEGA_PAR");
     P.omega_par = e && e[0] == '1';
