@@ -205,6 +205,12 @@ __global__ void __launch_bounds__(256) k_swr_frac(Dev d, Range R) {
   }
 }
 
+// levels per load batch of the KPP depth scans (kbls, the bottom layer)
+#ifndef ROMS_KBLS_G
+#define ROMS_KBLS_G 16
+#endif
+constexpr int kKblsG = ROMS_KBLS_G;
+
 // ---- pass 1: extended range ----
 #ifndef ROMS_KPP_EXT_WAVES
 #define ROMS_KPP_EXT_WAVES 3   // waves per SIMD the register budget is cut for (the next level in flight: 3)
@@ -369,18 +375,33 @@ __global__ void __launch_bounds__(64, ROMS_KPP_EXT_WAVES) k_kpp_ext(Dev d, Range
   // bottom layer (lmd_kpp.F:276-305): Cr(k) = FC(k) - FC(0), first k upward with Cr > 0
   const double FC0 = fc0;
   double bbl = zwN - zw0;
-  double crm = 0.;
-  for (int k = 1; k <= N; k++) {
-    const double cr = fc_get(k) - FC0;
-    if (cr > 0.) {
-      if (k == 1) bbl = zr.ld(vo, 0) - zw0;
-      else {
-        const double zrm = zr.ld(vo, (unsigned)(k - 2) * lv), zrk = zr.ld(vo, (unsigned)(k - 1) * lv);
-        bbl = (zrm * cr - zrk * crm) / (cr - crm) - zw0;
+  // the first k upward with Cr(k) > 0 and Cr(k-1) (0 below k = 1): FC read
+  // kKblsG levels at a time, the scan ends once every lane of the wave has
+  // its level (one load per iteration waited on a round trip per level)
+  int kb = 0;
+  double crk = 0., crmk = 0.;
+  {
+    constexpr int G = kKblsG;
+    double crm = 0.;
+    for (int k0 = 1; k0 <= N; k0 += G) {   // k0 wave-uniform
+      double c[G];
+#pragma unroll
+      for (int q = 0; q < G; q++) c[q] = fc_get(k0 + q <= N ? k0 + q : N);
+#pragma unroll
+      for (int q = 0; q < G; q++) {
+        if (kb == 0 && k0 + q <= N) {
+          const double cr = c[q] - FC0;
+          if (cr > 0.) { kb = k0 + q; crk = cr; crmk = crm; }
+          crm = cr;
+        }
       }
-      break;
+      if (__all(kb != 0)) break;
     }
-    crm = cr;
+  }
+  if (kb == 1) bbl = zr.ld(vo, 0) - zw0;
+  else if (kb > 1) {   // per-lane level: VGPR offsets
+    const double zrm = zr.ld(vo + (unsigned)(kb - 2) * lv, 0u), zrk = zr.ld(vo + (unsigned)(kb - 1) * lv, 0u);
+    bbl = (zrm * crk - zrk * crmk) / (crk - crmk) - zw0;
   }
   F.lmd_bbl[ij] = bbl * rm;
 }
@@ -431,16 +452,30 @@ __global__ void __launch_bounds__(TY > 0 ? kCX * TY : 64, MW) k_kpp_int(Dev d, R
   const BufF64 zw(F.z_w), sw(F.swr_frac);
   const double zwN = zw.ld(vo, (unsigned)N * lv), zw0 = zw.ld(vo, 0);
   // kbls and the buoyancy forcing at the boundary-layer depth (lmd_kpp.F:348-372)
+  // (the downward scan keeps its last hit: kbls is the smallest k in 1..N-1
+  // with z_w(k) > zwN - hbl, else N).  Levels are loaded kKblsG at a time --
+  // a scan with one load per iteration waited on 99 round trips per column.
   int kbls = N;
-  for (int k = N - 1; k >= 1; k--)
-    if (zw.ld(vo, (unsigned)k * lv) > zwN - hbl) kbls = k;
+  {
+    constexpr int G = kKblsG;
+    for (int k0 = N - 1; k0 >= 1; k0 -= G) {   // k0 wave-uniform: scalar level offsets
+      double z[G];
+#pragma unroll
+      for (int q = 0; q < G; q++) z[q] = zw.ld(vo, (unsigned)(k0 - q >= 1 ? k0 - q : 1) * lv);
+#pragma unroll
+      for (int q = 0; q < G; q++)
+        if (k0 - q >= 1 && z[q] > zwN - hbl) kbls = k0 - q;
+    }
+  }
   const double Bo = F.lmd_Bo[ij], Bosol = F.lmd_Bosol[ij], ustar = F.lmd_ustar[ij];
   double Bfsfc;
   {
     const double z_bl = zwN - hbl;
-    const unsigned ok = (unsigned)kbls * lv, om = (unsigned)(kbls - 1) * lv;
-    const double swm = sw.ld(vo, om), swk = sw.ld(vo, ok);
-    const double zwk = zw.ld(vo, ok), zwm = zw.ld(vo, om);
+    // kbls differs between lanes: its level offsets go in the VGPR offset
+    // (an SGPR offset would be a loop over the wave's distinct values)
+    const unsigned ok = vo + (unsigned)kbls * lv, om = vo + (unsigned)(kbls - 1) * lv;
+    const double swm = sw.ld(om, 0u), swk = sw.ld(ok, 0u);
+    const double zwk = zw.ld(ok, 0u), zwm = zw.ld(om, 0u);
     if (swm > 0.)
       Bfsfc = Bo + Bosol * (1. - swm * swk * (zwk - zwm) / (swk * (zwk - z_bl) + swm * (z_bl - zwm)));
     else
