@@ -483,18 +483,35 @@ __global__ void __launch_bounds__(kSegBlock, ROMS_SEG_BUF_WAVES) k_step3d_t_segb
   if (kppT || kppS) {
     // the KPP term of w level m is added to the cell below it (k = m, m <=
     // N-1) and subtracted from the cell above (k = m+1, m >= 1): one load
-    // per level, each row's upper term its next row's lower one
+    // per level, each row's upper term its next row's lower one.  Every
+    // level's swr_frac / ghat is loaded first, outside any data-dependent
+    // branch, so the loads issue together (a load per term inside the
+    // kppT / nl selects waited on a round trip per row)
     const BufF64 Sw(F.swr_frac), Gh(F.ghat);
     const bool nl = P.lmd_nonlocal;
-    auto term = [&](int m) {
-      const unsigned o = wlev(m, 1, N - 1);
-      return kppT ? dt * (sr * LD(Sw, vo, o) - (nl ? LD(Gh, vo, o) : 0.0) * (stf - sr)) : -dt * LD(Gh, vo, o) * stf;
+    double swv[KR + 1], ghv[KR + 1];
+    if (kppT) {
+#pragma unroll
+      for (int q = 0; q < KR + 1; q++) {
+        const unsigned o = wlev(c0 - 1 + q, 1, N - 1);
+        swv[q] = LD(Sw, vo, o);
+        ghv[q] = LD(Gh, vo, o);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < KR + 1; q++) {
+        swv[q] = 0.0;
+        ghv[q] = LD(Gh, vo, wlev(c0 - 1 + q, 1, N - 1));
+      }
+    }
+    auto term = [&](int q) {   // w level c0-1+q
+      return kppT ? dt * (sr * swv[q] - (nl ? ghv[q] : 0.0) * (stf - sr)) : -dt * ghv[q] * stf;
     };
-    double lo = term(c0 - 1);
+    double lo = term(0);
 #pragma unroll
     for (int p = 0; p < KR; p++) {
       const int k = min(c0 + p, N);
-      const double up = term(c0 + p);
+      const double up = term(p + 1);
       double t = rhs[p];
       t = k <= N - 1 ? t + up : t;
       t = k >= 2 ? t - lo : t;
