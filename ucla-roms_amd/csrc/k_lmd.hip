@@ -210,6 +210,11 @@ __global__ void __launch_bounds__(256) k_swr_frac(Dev d, Range R) {
 #define ROMS_KBLS_G 16
 #endif
 constexpr int kKblsG = ROMS_KBLS_G;
+// levels of k_kpp_int's Rig window / z_w loads in flight ahead of the level formed
+#ifndef ROMS_KPP_PFD
+#define ROMS_KPP_PFD 1
+#endif
+constexpr int kKppPfd = ROMS_KPP_PFD;
 
 // ---- pass 1: extended range ----
 #ifndef ROMS_KPP_EXT_WAVES
@@ -614,9 +619,13 @@ __global__ void __launch_bounds__(TY > 0 ? kCX * TY : 64, MW) k_kpp_int(Dev d, R
   // bottom-up stream: padding (lmd_vmix.F:359-370) and the in-place ascending
   // 1-2-1 filter Kv(k) = 0.5 Kv(k) + 0.25 Kv(k-1)[filtered] + 0.25 Kv(k+1)[raw] + bak
   double rv, rt, rs;  // raw level k (rs = rt unless LMD_DDMIX)
-  RL La, Ln;
+  // PD levels' loads in flight ahead of the one formed (a ring of RL)
+  constexpr int PD = kKppPfd;
+  RL La, Lr[PD];
   rload(1, La);
-  if (N - 1 >= 2) rload(2, Ln);
+#pragma unroll
+  for (int q = 0; q < PD; q++)
+    if (N - 1 >= 2 + q) rload(2 + q, Lr[q]);
   rcomp(La, rv, rt, rs);
   double zk = La.zw;  // z_w of level k
   double rvN = rv, rtN = rt, rsN = rs;  // raw level N-1 (known once reached)
@@ -626,8 +635,10 @@ __global__ void __launch_bounds__(TY > 0 ? kCX * TY : 64, MW) k_kpp_int(Dev d, R
     double nv, nt, ns;  // level k+1 before filtering
     double rvn = 0., rtn = 0., rsn = 0., zk1 = 0.;
     if (k + 1 <= N - 1) {
-      const RL cur = Ln;
-      if (k + 2 <= N - 1) rload(k + 2, Ln);
+      const RL cur = Lr[0];
+#pragma unroll
+      for (int q = 0; q + 1 < PD; q++) Lr[q] = Lr[q + 1];
+      if (k + 1 + PD <= N - 1) rload(k + 1 + PD, Lr[PD - 1]);
       rcomp(cur, rvn, rtn, rsn);
       zk1 = cur.zw;
       nv = rvn; nt = rtn; ns = rsn;
