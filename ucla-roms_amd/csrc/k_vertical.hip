@@ -431,7 +431,8 @@ constexpr int kOmR = kSegRows;   // levels per wave (N <= kSegRows * kSegMaxS)
 constexpr int kOmCW = kCX, kOmBlock = kSegMaxS * kOmCW;
 template <bool kHB, int CW = kOmCW, bool PAR = false>
 __global__ void __launch_bounds__(kSegMaxS * CW, 2) k_omega_seg(Dev d, Range R, double dtau, double hcff) {
-  const uint3 bI = xcd_tile();
+  // ROMS_GPU_OMEGA_ORD: the segment solvers' grouped block order (seg_tile)
+  const uint3 bI = d.p.omega_ord ? seg_tile(d.p.omega_ord, d.p.seg_xg) : xcd_tile();
   const Bounds& b = d.b;
   const Fields& F = d.f;
   const int N = b.N;

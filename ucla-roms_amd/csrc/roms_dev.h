@@ -77,6 +77,7 @@ struct Params {
   int uv1_lds;    // k_uv1_seg: Hz pairs kept in LDS from the spline phase, rufrc chained (ROMS_GPU_UV1_LDS=0: reloads)
   int omega_seg;  // omega: segment form k_omega_seg, one read of each input (ROMS_GPU_OMEGA_SEG=0: two-pass k_omega)
   int omega_cw;   // k_omega_seg columns per block: 64, 32 or 16 (ROMS_GPU_OMEGA_CW)
+  int omega_ord;  // k_omega_seg block order: 0 xcd_tile, 1..3 seg_tile's orders (ROMS_GPU_OMEGA_ORD)
   int omega_par;  // k_omega_seg: segment partial sums in parallel, one barrier (ROMS_GPU_OMEGA_PAR; not bitwise to the k-order chain)
   int p_in_rho;   // rho_eos's sweep also forms prsgrd's P (ROMS_GPU_P_IN_RHO=0: k_prsgrd_P)
   int omega_hb;   // the predictor's omega forms pre_step3d's Hz_bak/Hz_fwd (ROMS_GPU_OMEGA_HB=0: pre_step3d does)

@@ -911,6 +911,8 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     const char* e = getenv("ROMS_GPU_OMEGA_CW");
     const int v = e ? atoi(e) : (dims->N > 63 ? 16 : 64);
     P.omega_cw = v == 32 || v == 64 ? v : 16;
+    e = getenv("ROMS_GPU_OMEGA_ORD");
+    P.omega_ord = e && e[0] >= '1' && e[0] <= '3' ? e[0] - '0' : 0;
     e = getenv("ROMS_GPU_OMEGA_PAR");
     P.omega_par = e && e[0] == '1';
   }
