@@ -547,9 +547,11 @@ __global__ void __launch_bounds__(kSegBlock, ROMS_SEG_BUF_WAVES) k_step3d_t_segb
   T.solve(n, xL, xR);
   const double rm = BufF64(F.rmask).ld(vo, 0);
   const unsigned vs = act ? vo : kBufOff;
+  // straight-line stores (rows past n take kBufOff and are dropped): with a
+  // branch per row the compiler waited for every previous store before the
+  // next one (vmcnt(0) at each branch join, 14 store round trips per wave)
 #pragma unroll
-  for (int p = 0; p < KR; p++)
-    if (p < n) ST(Tn, T.D[p] * rm, vs, lev(c0 + p));
+  for (int p = 0; p < KR; p++) ST(Tn, T.D[p] * rm, p < n ? vs : kBufOff, lev(c0 + p));
 }
 
 void setup_column_kernels_t(size_t bytes) {
