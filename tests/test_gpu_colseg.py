@@ -222,7 +222,8 @@ def test_omega_blocks(case, monkeypatch):
     segment summing its own levels while the others do (PAR=1):
     - the chain keeps the reference's order: 6 whole steps (predictor omega
       with Hz_bak/Hz_fwd, corrector, closing omega) equal across block widths
-      bitwise; so do the PAR forms among themselves (same segment partition);
+      and block orders (ROMS_GPU_OMEGA_ORD) bitwise; so do the PAR forms
+      among themselves (same segment partition);
     - PAR reassociates the sums: one omega call within RTOL_ROUTINE of the
       oracle, and 6 whole steps within RMS_RUN of the chain form."""
     cfg = _omega_cfg(case)
@@ -236,10 +237,19 @@ def test_omega_blocks(case, monkeypatch):
             m.step(6)
             runs[par, cw] = {n: m.get(n) for n in names}
             m.close()
-    for par in ("0", "1"):
-        for cw in ("32", "16"):
-            for n in names:
-                assert np.array_equal(runs[par, "64"][n], runs[par, cw][n]), (par, cw, n)
+    # the segment solvers' grouped block order (ROMS_GPU_OMEGA_ORD=3) only
+    # changes which block runs which tile
+    monkeypatch.setenv("ROMS_GPU_OMEGA_PAR", "0")
+    monkeypatch.setenv("ROMS_GPU_OMEGA_CW", "16")
+    monkeypatch.setenv("ROMS_GPU_OMEGA_ORD", "3")
+    m = make_model(cfg, 1)
+    m.step(6)
+    runs["0", "16o3"] = {n: m.get(n) for n in names}
+    m.close()
+    monkeypatch.delenv("ROMS_GPU_OMEGA_ORD")
+    for par, cw in (("0", "32"), ("0", "16"), ("0", "16o3"), ("1", "32"), ("1", "16")):
+        for n in names:
+            assert np.array_equal(runs[par, "64"][n], runs[par, cw][n]), (par, cw, n)
     for n in names:
         a, b = runs["0", "64"][n], runs["1", "64"][n]
         rms = float(np.sqrt(np.mean((a - b) ** 2)))
