@@ -76,6 +76,12 @@ PRE_UV_SEG_PASSES = 14
 # the routine; here rho_eos's sweep stores it): not a model array, so it is
 # not counted -- the bytes it costs lower the fraction.
 PRSGRD_UV_PASSES = 10
+# k_uv1_segb is all of step3d_uv1 (14 passes)
+UV1_SEG_PASSES = 14
+# roofline.traffic is not measured in the bench run: it is read from the PMC
+# table tools/gpu.sh pmc wrote (a separate rocprofv3 --pmc pass per counter)
+PMC_SOURCE_C3 = "stored: profiles/pmc_traffic_c3.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE passes; tools/gpu.sh pmc)"
+PMC_SOURCE_C2 = "stored: profiles/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE passes; tools/gpu.sh pmc)"
 
 
 # set_HUV's Hz_u/Hz_v (set_depth.F:220,227) feed only extract_data.F; whole
@@ -229,7 +235,7 @@ def launch_ranks(args, argv):
 # one workload on this rank
 # ---------------------------------------------------------------------------
 def run_workload(kind, romsgpu, comm, rank, world, local_rank, steps, warmup, timing_steps, barrier, allmax,
-                 step_only=False):
+                 step_only=False, gather=None):
     npx, npe = proc_grid(world)
     c3 = kind == "c3"
     if c3:
@@ -255,10 +261,27 @@ def run_workload(kind, romsgpu, comm, rank, world, local_rank, steps, warmup, ti
     wall = time.perf_counter() - t0
     barrier()
     elapsed = allmax(max(wall, ev_ms / 1e3))
+    overlap = m.halo_overlap() if comm is not None else False
     if step_only:   # the whole-step time alone (the exchange-overlap A/B of a multi-rank run)
         m.close()
         return {"ms_per_step": 1e3 * elapsed / steps, "value": total_cells * steps / elapsed,
-                "steps": steps}
+                "steps": steps, "overlap": overlap}
+    halo_time = None
+    if comm is not None:
+        # the halo path per rank: HIP events around every exchange's pack,
+        # transport (IPC: signal + arrival wait, which also absorbs the other
+        # ranks' skew; RCCL: the send/recv group) and unpack over eager steps,
+        # where each exchange runs in place (timing any kernel turns the
+        # deferral off), so these are the costs the deferred order hides
+        mine = []
+        for ph in ("pack", "wait", "unpack"):
+            hms, hn = m.time_routine("k_halo_" + ph, timing_steps)
+            mine += [1e3 * hms * hn / timing_steps, float(hn) / timing_steps]
+        per = gather(mine) if gather is not None else [mine]
+        halo_time = {"source": "HIP events on the halo path, %d eager steps per phase, exchanges in place" % timing_steps,
+                     "exchanges_per_step": [r[1] for r in per]}
+        for q, ph in enumerate(("pack", "wait", "unpack")):
+            halo_time[ph + "_us_per_step"] = [r[2 * q] for r in per]
 
     # per-routine rooflines: HIP events around each routine's launches
     cells3 = Lr * Mr * Nz
@@ -297,30 +320,39 @@ def run_workload(kind, romsgpu, comm, rank, world, local_rank, steps, warmup, ti
                        "per_routine_frac": {r: routines[r]["frac"] for r in loop}}
     # the fused barotropic kernel alone: 35 2-D passes per fast step over its
     # launch time (one event interval per fast loop on a single rank)
-    # C3: the dominant kernel, pre_step3d's momentum segment solver, alone
-    if c3:
-        # the two largest kernels per step in the C3 kernel trace
-        # (profiles/r3_*_c3_per_step.txt): k_prsgrd_uv (2 launches) and k_pre_uv_seg
-        c3k = {}
-        for kname, npass in (("k_pre_uv_seg", PRE_UV_SEG_PASSES), ("k_prsgrd_uv", PRSGRD_UV_PASSES)):
-            kms, kn = m.time_routine(kname, timing_steps)
-            kb = 8.0 * npass * cells3
-            kg = kb / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
-            # the buffer-addressed form (k_pre_uv_segb, the default) under its own name in the PMC table
-            kt = pmc_kernel_traffic(kname + "b", c3=True)
-            kn_name = kname + "b" if kt is not None else kname
-            if kt is None:
-                kt = pmc_kernel_traffic(kname, c3=True)
-            c3k[kname] = {"bound": "hbm", "achieved": kg, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                          "frac": kg / HBM_PEAK_GBS, "traffic": kt, "kernel": kn_name,
-                          "bytes_per_launch": kb, "ms_per_launch": kms, "launches_per_step": kn / timing_steps,
-                          "ms_per_step": kms * kn / timing_steps, "passes": npass}
     fb_ms, fb_n = m.time_routine("k_s2d_fb", timing_steps)
     fb_bytes = 35.0 * 8 * Lr * Mr
     fb_gbs = fb_bytes / (fb_ms * 1e-3) / 1e9 if fb_ms > 0 else 0.0
     kernel_fb = {"kernel": "k_s2d_fb", "ms_per_launch": fb_ms, "launches_per_step": fb_n / timing_steps,
                  "ms_per_step": fb_ms * fb_n / timing_steps, "bytes_per_launch": fb_bytes,
                  "achieved_GBs": fb_gbs, "frac": fb_gbs / HBM_PEAK_GBS}
+    if c3:
+        # C3: every kernel with a kernel-level event timer and a fixed
+        # per-launch pass count (k_prsgrd_uv, k_pre_uv_seg, k_uv1_seg,
+        # k_s2d_fb -- the four largest per step in the committed C3 trace);
+        # the dominant kernel is the largest time per step among them, and
+        # trace_check names the committed trace's own maximum beside it
+        c3k = {}
+        for kname, npass in (("k_pre_uv_seg", PRE_UV_SEG_PASSES), ("k_prsgrd_uv", PRSGRD_UV_PASSES),
+                             ("k_uv1_seg", UV1_SEG_PASSES)):
+            kms, kn = m.time_routine(kname, timing_steps)
+            kb = 8.0 * npass * cells3
+            kg = kb / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
+            # the buffer-addressed forms (k_pre_uv_segb, k_uv1_segb) under their own names in the PMC table
+            kt = pmc_kernel_traffic(kname + "b", c3=True)
+            kn_name = kname + "b" if kt is not None else kname
+            if kt is None:
+                kt = pmc_kernel_traffic(kname, c3=True)
+            c3k[kname] = {"bound": "hbm", "achieved": kg, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": kg / HBM_PEAK_GBS, "traffic": kt, "traffic_source": PMC_SOURCE_C3,
+                          "kernel": kn_name, "bytes_per_launch": kb, "ms_per_launch": kms,
+                          "launches_per_step": kn / timing_steps, "ms_per_step": kms * kn / timing_steps,
+                          "passes": npass}
+        c3k["k_s2d_fb"] = {"bound": "hbm", "achieved": fb_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": fb_gbs / HBM_PEAK_GBS, "traffic": pmc_kernel_traffic("k_s2d_fb", c3=True),
+                           "traffic_source": PMC_SOURCE_C3, "kernel": "k_s2d_fb", "bytes_per_launch": fb_bytes,
+                           "ms_per_launch": fb_ms, "launches_per_step": fb_n / timing_steps,
+                           "ms_per_step": fb_ms * fb_n / timing_steps, "passes": "35 2-D"}
     transport = m.halo_transport() if comm is not None else "none (single rank)"
     # exchanges per step (the fast loop's zeta/ubar/vbar swap every K fast steps)
     exch, fast_k = m.halo_exchanges() if comm is not None else (0, 1)
@@ -336,18 +368,17 @@ def run_workload(kind, romsgpu, comm, rank, world, local_rank, steps, warmup, ti
         # (profiles/r2_*_c2_per_step.txt): the fused barotropic kernel
         roofline = {"bound": "hbm", "achieved": fb_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": fb_gbs / HBM_PEAK_GBS, "traffic": pmc_kernel_traffic("k_s2d_fb"),
+                    "traffic_source": PMC_SOURCE_C2,
                     "kernel": "k_s2d_fb", "bytes_per_launch": fb_bytes, "ms_per_launch": fb_ms,
                     # the 73 MB fast-time working set stays in the 256 MiB Infinity
                     # Cache across the 82 launches; c3.kernel_s2d_fb is the same
                     # kernel's HBM-resident figure (294 MB per launch)
                     "cache_resident": True}
     else:
-        # dominant kernel by time per step in the C3 kernel trace
-        # (profiles/r3_*_c3_per_step.txt): k_pre_uv_seg
-        # dominant kernel: the larger time per step of the two
         dom_k = max(c3k, key=lambda k: c3k[k]["ms_per_step"])
         roofline = dict(c3k[dom_k])
         roofline["other_kernels"] = {k: v for k, v in c3k.items() if k != dom_k}
+        roofline["trace_check"] = trace_top_kernel()
     return {
         "value": total_cells * steps / elapsed,
         "ms_per_step": ms_step,
@@ -357,7 +388,10 @@ def run_workload(kind, romsgpu, comm, rank, world, local_rank, steps, warmup, ti
                                "C2: Filament+S 512x512x50 per GPU, NT=2, dt=5s, ndtfast=60 (nfast=%d)" % nfast,
                    "grid_per_gpu": [Lr, Mr, Nz], "proc_grid": [npx, npe], "NT": NT, "dt": dt_step, "nfast": nfast,
                    "parallelism": "domain decomposition %dx%d" % (npx, npe), "halo_transport": transport,
-                   "halo_exchanges_per_step": exch, "fast_exchange_interval": fast_k},
+                   "halo_exchanges_per_step": exch, "fast_exchange_interval": fast_k,
+                   "exchange_order": ("deferred (3-D exchanges beside the next routine)" if overlap else
+                                      "in place" if comm is not None else "none (single rank)"),
+                   "halo_time_per_rank": halo_time},
         "scaling": "strong" if c3 else "weak",
         "steps": steps, "warmup": warmup,
         "roofline": roofline,
@@ -391,6 +425,19 @@ def pmc_kernel_traffic(kernel, c3=False):
         k = _pmc(c3).get("kernels", {}).get(kernel)
         return None if k is None else float(k["traffic_bytes"]) / float(k["dispatches"])
     except (KeyError, TypeError, ZeroDivisionError, ValueError):
+        return None
+
+
+def trace_top_kernel():
+    """The largest kernel per step in the committed C3 kernel trace of the
+    current tree (profiles/current_c3_per_step.txt, a copy of the newest
+    tools/prof_summary.py table), or None."""
+    f = os.path.join(ROOT, "profiles", "current_c3_per_step.txt")
+    try:
+        rows = [ln for ln in open(f).read().splitlines()[1:] if ln.strip() and not ln.startswith("busy")]
+        name = rows[0].rsplit(None, 4)[0]
+        return {"trace": os.path.relpath(f, ROOT), "top_kernel": name, "us_per_step": float(rows[0].split()[-3])}
+    except (OSError, IndexError, ValueError):
         return None
 
 
@@ -510,9 +557,18 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         return float(tt.item())
 
+    def gather(vec):   # every rank's vector, rank order
+        if dist is None:
+            return [list(vec)]
+        import torch
+        tt = torch.tensor(vec, dtype=torch.float64)
+        parts = [torch.empty_like(tt) for _ in range(world)]
+        dist.all_gather(parts, tt)
+        return [p.tolist() for p in parts]
+
     try:
         prim = run_workload(args.workload, romsgpu, comm, rank, world, local_rank, args.steps, args.warmup,
-                            args.timing_steps, barrier, allmax)
+                            args.timing_steps, barrier, allmax, gather=gather)
     except romsgpu.RomsGpuError as e:
         # the host channel carries no RCCL fallback: when the IPC transport
         # fails its set-up or self-test (a collective verdict, so every rank
@@ -523,22 +579,26 @@ def main():
         romsgpu.comm_destroy(comm)
         comm, bootstrap = rccl_comm(), "rccl (host-channel IPC self-test failed: %s)" % str(e)[:120]
         prim = run_workload(args.workload, romsgpu, comm, rank, world, local_rank, args.steps, args.warmup,
-                            args.timing_steps, barrier, allmax)
+                            args.timing_steps, barrier, allmax, gather=gather)
     prim["config"]["comm_bootstrap"] = bootstrap
     if comm is not None and world > 1 and os.environ.get("ROMS_GPU_XOVERLAP") is None:
-        # the deferred-exchange overlap (ROMS_GPU_XOVERLAP=1: each producer's
-        # 3-D exchange beside the next routine that reads none of its halo;
-        # off by default) A/B'd in the same job
-        os.environ["ROMS_GPU_XOVERLAP"] = "1"
+        # the deferred-exchange overlap (each producer's 3-D exchange beside
+        # the next routine that reads none of its halo; the library's default
+        # when every rank has its own GPU, in place when ranks share one,
+        # DESIGN.md section 5): the other order A/B'd in the same job
+        dflt = prim["config"]["exchange_order"].startswith("deferred")
+        os.environ["ROMS_GPU_XOVERLAP"] = "0" if dflt else "1"
         try:
-            on = run_workload(args.workload, romsgpu, comm, rank, world, local_rank, args.steps, args.warmup,
-                              args.timing_steps, barrier, allmax, step_only=True)
+            alt = run_workload(args.workload, romsgpu, comm, rank, world, local_rank, args.steps, args.warmup,
+                               args.timing_steps, barrier, allmax, step_only=True)
         finally:
             del os.environ["ROMS_GPU_XOVERLAP"]
+        on, off = (prim, alt) if dflt else (alt, prim)
         prim["config"]["exchange_overlap"] = {
-            "default": "off (every exchange in place; ROMS_GPU_XOVERLAP=1 defers them)",
-            "ms_per_step_off": prim["ms_per_step"], "ms_per_step_on": on["ms_per_step"],
-            "value_on": on["value"]}
+            "default": ("on (ranks on distinct GPUs; ROMS_GPU_XOVERLAP=0 keeps every exchange in place)" if dflt else
+                        "off (ranks share a GPU; ROMS_GPU_XOVERLAP=1 defers the 3-D exchanges)"),
+            "ms_per_step_off": off["ms_per_step"], "ms_per_step_on": on["ms_per_step"],
+            "value_on": on["value"], "value_off": off["value"]}
     out = {
         "metric": "grid-cell-updates/sec",
         "value": prim["value"],
@@ -565,7 +625,7 @@ def main():
         c3s = secondary == "c3"
         sec = run_workload(secondary, romsgpu, comm, rank, world, local_rank, min(args.steps, 10) if c3s else args.steps,
                            min(args.warmup, 2) if c3s else args.warmup, min(args.timing_steps, 2) if c3s else
-                           args.timing_steps, barrier, allmax)
+                           args.timing_steps, barrier, allmax, gather=gather)
         sec["metric"] = "grid-cell-updates/sec"
         sec["unit"] = "cell-updates/s"
         sec["data"] = ("synthetic (analytic closed basin, SURVEY.md 8(d) C3)" if c3s else

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define ROMS_GPU_ABI_VERSION 14
+#define ROMS_GPU_ABI_VERSION 15
 #define ROMS_MAX_FAST 288
 
 /* Subdomain geometry of this rank: param.F / dimensions.F / mpi_setup.F:39-210 */
@@ -287,6 +287,12 @@ int roms_gpu_halo_transport(void);
  * smallest subdomain of the mpi_setup.F split, the same on every rank;
  * rivers and pipes take every step).                                         */
 int roms_gpu_halo_exchanges(long *per_step, int *fast_interval);
+/* 1 if whole steps defer each producer's 3-D exchange onto the halo stream
+ * beside the next routine that reads none of its halo (the default with
+ * > 1 rank when every rank drives its own GPU; ROMS_GPU_XOVERLAP=1 forces
+ * it on, =0 off), 0 if every exchange runs in place, as the reference's
+ * exchange_xxx calls do (mpi_exchanges.F:672-800).                          */
+int roms_gpu_halo_overlap(void);
 /* Self-test of the allocation path: `chunks` arrays of n doubles filled
  * with ones and freed, then allocated again through the library's
  * zero-filling allocator; on the library's stream each is read at once
@@ -429,6 +435,9 @@ enum roms_routine {
   ROMS_R_K_UV1_SEG,        /* kernel level: step3d_uv1's momentum segment solver (N > 63) */
   ROMS_R_K_STEP3D_T_SEG,   /* kernel level: step3d_t's tracer segment solver (N > 63) */
   ROMS_R_K_PRSGRD_UV,      /* kernel level: prsgrd's ru/rv kernel (with the horizontal momentum r.h.s. in whole steps) */
+  ROMS_R_K_HALO_PACK,      /* halo path: the pack of every exchange (IPC: straight into the neighbours' buffers) */
+  ROMS_R_K_HALO_WAIT,      /* halo path: the transport (IPC: signal + arrival wait; RCCL: the send/recv group) */
+  ROMS_R_K_HALO_UNPACK,    /* halo path: the unpack of every exchange */
   ROMS_R_COUNT
 };
 int roms_gpu_time_routine(int routine, int nsteps, roms_tlev *t, double *avg_ms, long *launches);

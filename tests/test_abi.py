@@ -89,3 +89,25 @@ def test_fortran_module_abi_version_matches_header():
     vh = int(re.search(r"#define ROMS_GPU_ABI_VERSION (\d+)", h).group(1))
     vf = int(re.search(r"ROMS_GPU_ABI = (\d+)", f).group(1))
     assert vh == vf
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libromsgpu.so not built")
+def test_init_refuses_subdomain_beyond_buffer_offsets():
+    """The buffer-addressed kernels use 32-bit byte offsets below 2 GiB per
+    field (k_common.h BufF64): roms_gpu_init refuses a rank whose w-point
+    field reaches that (2048^2 x 100 on one rank: 3.4 GiB) with a clear error,
+    before touching the device, instead of dropping accesses."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "ucla-roms_amd"))
+    import romsgpu
+    L = romsgpu.load_library()
+    cfg = romsgpu.Cfg()
+    cfg.nfast, cfg.ndtfast, cfg.dt = 82, 60, 300.0
+    for (n, ok) in ((2048, False), (1024, True)):
+        dims = romsgpu.Dims(Lm=n, Mm=n, N=100, NT=2, LLm=n, MMm=n, np_xi=1, np_eta=1)
+        rc = L.roms_gpu_init(ctypes.byref(dims), ctypes.byref(cfg), 0, None)
+        err = L.roms_gpu_last_error().decode()
+        if ok:   # gets past the guard; without a GPU the device call then fails
+            assert "2 GiB" not in err, err
+        else:
+            assert rc == -1 and "2 GiB" in err, (rc, err)

@@ -108,6 +108,76 @@ def test_processes_deferred_exchanges_ipc_bitwise(kind):
     _ranks(kind, 2, 2, {"ROMS_GPU_XOVERLAP": "1", "ROMS_GPU_XDELAY_US": "300"})
 
 
+SKIP_SCRIPT = r"""
+import os, sys
+sys.path.insert(0, os.path.join(sys.argv[1], "ucla-roms_amd"))
+import numpy as np, romsgpu
+rank, chan, npx, npe = int(sys.argv[2]), sys.argv[3], int(sys.argv[4]), int(sys.argv[5])
+case = dict(case_id=1, LLm=36, MMm=28, N=20, NT=2, salinity=True, nonlin_eos=True, dt=60.0, ndtfast=30,
+            sizex=72e3, sizey=56e3, lmd=True, surf_flux=True)
+fields = ("zeta", "ubar", "vbar", "u", "v", "t", "FlxU", "FlxV", "We", "Wi", "Hz", "Akv", "Akt")
+m = romsgpu.Model.from_case(**case)
+m.step(4)
+ref = {f: m.get(f) for f in fields}
+m.close()
+ag = romsgpu.FileAllgather(chan, npx * npe, rank)
+h = romsgpu.comm_create_host(npx * npe, rank, ag)
+m = romsgpu.Model.from_case(np_xi=npx, np_eta=npe, comm=h, rank=rank, **case)
+assert m.halo_overlap(), "deferred exchanges expected on"
+m.step(4)
+m.sync()
+iSW, jSW, Lm, Mm = m.iSW, m.jSW, m.Lm, m.Mm
+bad = []
+for f in fields:
+    g = m.get(f)
+    w = ref[f][..., jSW:jSW + Mm + 4, iSW:iSW + Lm + 4]
+    if not np.array_equal(g[..., 2:-2, 2:-2], w[..., 2:-2, 2:-2]):
+        bad.append(f)
+m.close()
+romsgpu.comm_destroy(h)
+print("BAD", bad)
+"""
+
+
+def _skip_ranks(npx, npe, env):
+    """Every rank's BAD list (owned cells that differ from the single domain)."""
+    with tempfile.TemporaryDirectory() as td:
+        ps = [subprocess.Popen([sys.executable, "-c", SKIP_SCRIPT, ROOT, str(r), td, str(npx), str(npe)],
+                               env=dict(os.environ, **env), stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+              for r in range(npx * npe)]
+        outs = []
+        for p in ps:
+            try:
+                o, e = p.communicate(timeout=240)
+            except subprocess.TimeoutExpired:
+                for q in ps:
+                    q.kill()
+                raise
+            outs.append((p.returncode, o, e))
+    for rc, o, e in outs:
+        assert rc == 0 and "BAD" in o, (rc, o[-2000:], e[-3000:])
+    return [o.split("BAD", 1)[1].strip() for _, o, _ in outs]
+
+
+@pytest.mark.parametrize("bit,reader", [(1, "omega (predictor)"), (2, "pre_step3d"), (4, "rho_eos (corrector)"),
+                                        (8, "omega (corrector)"), (16, "step3d_uv1")])
+def test_processes_missing_join_is_detected(bit, reader):
+    """Each join of the deferred order guards a real read (ADVICE/VERDICT r5):
+    with one join left out (ROMS_GPU_XTEST_SKIPJOIN=bit) and every deferred
+    exchange's destination halo set to NaN before its held-back unpack
+    (ROMS_GPU_XDELAY_US), the routine after the missing join reads NaN and the
+    owned cells no longer equal the single domain -- for every one of the
+    five joins.  Across processes no host wait completes an earlier exchange
+    early (the in-process transport's do), and the NaN shows a stale read even
+    where stale and fresh halos agree.  The same run with every join kept is
+    bitwise."""
+    base = {"ROMS_GPU_XOVERLAP": "1", "ROMS_GPU_XDELAY_US": "2000", "GPU_MAX_HW_QUEUES": "16"}
+    bad = _skip_ranks(2, 1, dict(base, ROMS_GPU_XTEST_SKIPJOIN=str(bit)))
+    assert any(b != "[]" for b in bad), (reader, bad)
+    good = _skip_ranks(2, 1, base)
+    assert all(b == "[]" for b in good), good
+
+
 FATAL_SCRIPT = r"""
 import os, sys
 sys.path.insert(0, os.path.join(sys.argv[1], "ucla-roms_amd"))

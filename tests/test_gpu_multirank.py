@@ -381,20 +381,20 @@ def test_deferred_exchanges_off_equals_on():
             assert np.array_equal(on[r][4][f], off[r][4][f]), (r, f)
 
 
-@pytest.mark.parametrize("bit,reader", [(8, "omega (corrector)")])
-def test_deferred_exchange_missing_join_is_detected(bit, reader):
+@pytest.mark.parametrize("bit,kind,reader", [(1, "basin", "omega (predictor)"), (8, "basin_flux", "omega (corrector)"),
+                                             (16, "basin_flux", "step3d_uv1")])
+def test_deferred_exchange_missing_join_is_detected(bit, kind, reader):
     """The delay hook is a real check: with one join left out (test hook
     ROMS_GPU_XTEST_SKIPJOIN=bit) the routine after it reads a halo before the
-    late unpack and the decomposition no longer matches.  Only the joins of
-    the last exchange forked before their reader can be shown this way: the
-    in-process transport's host waits inside every exchange complete the
-    earlier ones (so bits 2 and 4 are covered by the bitwise runs above, not
-    here); the join before the predictor's omega (bit 1) guards a halo whose
-    stale and fresh values are equal (set_HUV recomputes the FlxU that
-    step3d_uv2 left there), and so, in this case, does the one before
-    step3d_uv1 (bit 16: the rank edge's Akv is the same in both lmd_vmix
-    calls of a step)."""
-    ok, out = _deferred("basin_flux", 2, 1, {"ROMS_GPU_XDELAY_US": "2000", "ROMS_GPU_XTEST_SKIPJOIN": str(bit)})
+    late unpack -- whose destination the hook first sets to NaN, so even a
+    stale value equal to the fresh one shows -- and the decomposition no
+    longer matches.  In process, the joins of the last exchange forked before
+    their reader show this way; the in-process transport's host wait inside
+    each exchange completes the earlier ones (bits 2 and 4, and bit 1 when
+    lmd_vmix's exchange is forked between set_HUV's and omega), so
+    tests/test_gpu_ipc.py::test_processes_missing_join_is_detected shows all
+    five joins across processes, where no host wait intervenes."""
+    ok, out = _deferred(kind, 2, 1, {"ROMS_GPU_XDELAY_US": "2000", "ROMS_GPU_XTEST_SKIPJOIN": str(bit)})
     assert not ok, out[-1500:]
-    ok, out = _deferred("basin_flux", 2, 1, {"ROMS_GPU_XDELAY_US": "2000"})
+    ok, out = _deferred(kind, 2, 1, {"ROMS_GPU_XDELAY_US": "2000"})
     assert ok, out[-1500:]

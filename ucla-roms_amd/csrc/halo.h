@@ -78,20 +78,23 @@ struct Halo {
   hipEvent_t xev[kRing] = {};
   long nfork = 0;   // exchanges forked onto cs since setup
   long njoin = 0;   // tickets < njoin are joined into the library stream
+  hipStream_t ls = nullptr;   // the library stream (the only stream whose joins advance njoin)
   HaloIpc ipc;
   int overlap = 0;  // 1: enabled (ROMS_GPU_S2D_OVERLAP=1; off by default, see halo_setup)
   int overlap3d = 0;  // rim-first overlap of the 3-D exchanges (launch_rim_first; ROMS_GPU_OVERLAP3D=1: on)
   // Deferred 3-D exchanges (enqueue_step): on multi-rank runs
   // a producer's trailing exchange runs on cs beside the next routine that
   // reads none of its halo; the step joins it before the first reader.
-  // xoverlap: enabled (ROMS_GPU_XOVERLAP=1 with a communicator of > 1 rank;
-  // off by default, see halo_setup); defer > 0: launch_exchange_list forks
-  // instead of exchanging on the caller's stream (set around one producer).
+  // xoverlap: enabled (the default with > 1 rank when no two ranks share a
+  // device; ROMS_GPU_XOVERLAP=1 forces it on, =0 off; see halo_setup);
+  // defer > 0: launch_exchange_list forks instead of exchanging on the
+  // caller's stream (set around one producer).
   int xoverlap = 0;
   int defer = 0;
-  // test hook (ROMS_GPU_XDELAY_US): a bounded spin of that many microseconds
-  // on cs before each forked exchange's unpack, so a reader the step forgot to
-  // join reads the stale halo (tests/test_gpu_multirank.py)
+  // test hook (ROMS_GPU_XDELAY_US): each forked exchange's destination halo
+  // is set to NaN, then a bounded spin of that many microseconds on cs holds
+  // back its unpack, so a reader the step forgot to join reads NaN
+  // (tests/test_gpu_multirank.py, tests/test_gpu_ipc.py)
   int xdelay_us = 0;
   long long xdelay_ticks = 0;
   // test hook (ROMS_GPU_XTEST_SKIPJOIN=bits): enqueue_step leaves out the

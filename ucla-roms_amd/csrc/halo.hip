@@ -27,7 +27,10 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <set>
 #include <vector>
+
+#include <unistd.h>
 
 #include "halo.h"
 #include "shim_state.h"
@@ -461,6 +464,32 @@ bool halo_failed(const Halo& H) {
   return H.ipc.ok && H.ipc.err_host && __atomic_load_n(H.ipc.err_host, __ATOMIC_ACQUIRE) != 0;
 }
 
+// every rank's (host, PCI location of its device) through the halo gather:
+// distinct = 1 when no two ranks share a device
+static int ranks_on_distinct_devices(const Halo& H, int& distinct) {
+  distinct = 0;
+  int dev = 0;
+  hipDeviceProp_t p{};
+  double key[2] = {-1.0, -1.0};
+  if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess)
+    key[0] = (double)p.pciDomainID * 65536.0 + (double)p.pciBusID * 256.0 + (double)p.pciDeviceID;
+  char host[256] = {0};
+  (void)gethostname(host, sizeof(host) - 1);
+  unsigned h = 2166136261u;   // FNV-1a of the host name
+  for (const char* c = host; *c; c++) h = (h ^ (unsigned char)*c) * 16777619u;
+  key[1] = (double)h;
+  const int nr = H.comm->nranks;
+  std::vector<double> all((size_t)2 * nr);
+  if (halo_allgather(H, H.cs, key, 2, all.data()) != 0) return -1;
+  std::set<std::pair<double, double>> seen;
+  for (int r = 0; r < nr; r++) {
+    if (all[2 * r] < 0.0) return 0;   // a rank could not tell its device: keep the in-place order
+    seen.insert({all[2 * r], all[2 * r + 1]});
+  }
+  distinct = (int)seen.size() == nr ? 1 : 0;
+  return 0;
+}
+
 int halo_setup(Halo& H, RomsComm* comm, const HaloPlan& plan, int maxlev, const HaloPlan& wide, int wide_maxlev,
                std::string& err) {
   H.comm = comm;
@@ -492,16 +521,18 @@ int halo_setup(Halo& H, RomsComm* comm, const HaloPlan& plan, int maxlev, const 
   H.nfork = H.njoin = 0;
   H.defer = 0;
   {
-    // deferred 3-D exchanges beside the next routine (enqueue_step): opt-in,
-    // ROMS_GPU_XOVERLAP=1.  Measured on one MI355X:
-    // one process exchanging with itself through IPC, C2, 7.12 vs 6.92-6.95
-    // ms per step; 2 and 4 ranks sharing the GPU, C3, 63-75 vs 57-58 ms --
-    // the forked pack / wait / unpack kernels and the graph's extra branches
-    // cost more than the exchange time they hide on one GPU.  Only an 8-GPU
-    // run can show the xGMI latency they would hide; bench.py --gpus N > 1
-    // reports both
+    // deferred 3-D exchanges beside the next routine (enqueue_step): on by
+    // default when every rank has a GPU of its own (decided at the end of
+    // this function), ROMS_GPU_XOVERLAP=1 / =0 forces either order.  Ranks
+    // sharing one MI355X measured slower deferred: one
+    // process exchanging with itself through IPC, C2, 7.12 vs 6.92-6.95 ms
+    // per step; 2 and 4 ranks sharing the GPU, C3, 63-75 vs 57-58 ms -- there
+    // the forked pack / wait / unpack kernels compete with the routine they
+    // would hide behind and there is no xGMI latency to hide.  bench.py
+    // --gpus N > 1 reports both orders
     const char* ex = getenv("ROMS_GPU_XOVERLAP");
-    H.xoverlap = ex && ex[0] == '1' && comm && comm->nranks > 1;
+    if (ex && (ex[0] == '0' || ex[0] == '1')) H.xoverlap = ex[0] == '1' && comm && comm->nranks > 1;
+    else H.xoverlap = -1;   // decided below, once every rank's device is known
     const char* es = getenv("ROMS_GPU_XTEST_SKIPJOIN");
     H.xskip = es ? atoi(es) : 0;
     const char* ed = getenv("ROMS_GPU_XDELAY_US");
@@ -553,6 +584,23 @@ int halo_setup(Halo& H, RomsComm* comm, const HaloPlan& plan, int maxlev, const 
             "(use roms_gpu_comm_create for RCCL)";
       return -5;
     }
+  }
+  if (H.xoverlap < 0) {
+    // default: deferred exchanges when every rank drives a GPU of its own
+    // (one process per GPU over xGMI: a deferred exchange's latency hides
+    // behind the next routine).  Ranks that share a device (a rehearsal with
+    // more ranks than GPUs) or threads of one process keep the in-place
+    // order: there the forked kernels compete with the routine they would
+    // hide behind, and measured slower.
+    int distinct = 0;
+    if (comm && comm->nranks > 1 && (comm->kind == 1 || comm->kind == 3)) {
+      const int r = ranks_on_distinct_devices(H, distinct);
+      if (r) {
+        err = "halo_setup: device-identity gather failed";
+        return -5;
+      }
+    }
+    H.xoverlap = distinct;
   }
   H.nexch = 0;   // the self-test's exchanges do not count
   return 0;
@@ -613,16 +661,40 @@ __global__ void k_halo_delay(long long ticks) {
   const long long t0 = wall_clock64();
   while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
 }
-void xdelay(const Halo& H, hipStream_t s) {
-  if (H.xdelay_us > 0 && s == H.cs) hipLaunchKernelGGL(k_halo_delay, dim3(1), dim3(64), 0, s, H.xdelay_ticks);
+// ... and before the delay every halo cell the unpack will fill is set to
+// NaN, so a routine that reads the halo before its join reads NaN -- even
+// where the stale and the fresh values agree -- and the run shows it
+__global__ void __launch_bounds__(256) k_halo_poison(HaloGeom g, ExchList L) {
+  const int h = g.act_dir[blockIdx.z];
+  if (!g.active[h]) return;
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= g.cnt[h]) return;
+  int lev = blockIdx.y;
+  const int q = list_slot(L, lev);
+  if (lev >= L.nlev[q]) return;
+  int i, j;
+  halo_dst(g, h, e, i, j);
+  L.p[q][(long)(i + 1) + (long)(j + 1) * g.nx2 + (long)lev * g.n2] = __builtin_nan("");
+}
+void xdelay(const Halo& H, hipStream_t s, const HaloGeom& g, const ExchList& L, const dim3& grid) {
+  if (H.xdelay_us > 0 && s == H.cs) {
+    hipLaunchKernelGGL(k_halo_poison, grid, dim3(256), 0, s, g, L);
+    hipLaunchKernelGGL(k_halo_delay, dim3(1), dim3(64), 0, s, H.xdelay_ticks);
+  }
 }
 void exchange_ipc(const Halo& H, hipStream_t s, const HaloGeom& g, const ExchList& L, const dim3& grid) {
   const IpcPtrs P = ipc_ptrs(H);
+  ktimer_mark(s, kTimedHaloPack, 0);
   hipLaunchKernelGGL(k_halo_pack_ipc, grid, dim3(256), 0, s, g, L, P, H.cap);
+  ktimer_mark(s, kTimedHaloPack, 1, 1);
   const int drop = H.ipc.drop_at >= 0 && H.ipc.nexch++ == H.ipc.drop_at;
+  ktimer_mark(s, kTimedHaloWait, 0);
   hipLaunchKernelGGL(k_halo_wait_ipc, dim3(1), dim3(64), 0, s, g, P, drop);
-  xdelay(H, s);
+  ktimer_mark(s, kTimedHaloWait, 1, 1);
+  xdelay(H, s, g, L, grid);
+  ktimer_mark(s, kTimedHaloUnpack, 0);
   hipLaunchKernelGGL(k_halo_unpack_ipc, grid, dim3(256), 0, s, g, L, P, H.cap);
+  ktimer_mark(s, kTimedHaloUnpack, 1, 1);
 }
 }  // namespace
 
@@ -643,9 +715,12 @@ void halo_exchange(const Halo& H, hipStream_t s, const ExchList& L) {
     exchange_ipc(H, s, g, L, grid);
     return;
   }
+  ktimer_mark(s, kTimedHaloPack, 0);
   hipLaunchKernelGGL(k_halo_pack, grid, dim3(256), 0, s, g, L, H.sbuf, H.cap);
+  ktimer_mark(s, kTimedHaloPack, 1, 1);
   RomsComm* c = H.comm;
   const int me = c->rank;
+  ktimer_mark(s, kTimedHaloWait, 0);
   if (c->kind == 1) {
     (void)ncclGroupStart();
     for (int d = 0; d < 8; d++)
@@ -677,8 +752,11 @@ void halo_exchange(const Halo& H, hipStream_t s, const ExchList& L) {
     (void)hipStreamSynchronize(s);
     G->barrier();
   }
-  xdelay(H, s);
+  ktimer_mark(s, kTimedHaloWait, 1, 1);
+  xdelay(H, s, g, L, grid);
+  ktimer_mark(s, kTimedHaloUnpack, 0);
   hipLaunchKernelGGL(k_halo_unpack, grid, dim3(256), 0, s, g, L, H.rbuf, H.cap);
+  ktimer_mark(s, kTimedHaloUnpack, 1, 1);
 }
 
 long halo_fork_exchange(Halo& H, hipStream_t s, const ExchList& L) {
@@ -694,7 +772,9 @@ long halo_fork_exchange(Halo& H, hipStream_t s, const ExchList& L) {
 void halo_join_to(Halo& H, hipStream_t s, long ticket) {
   if (ticket < H.njoin || ticket >= H.nfork) return;
   (void)hipStreamWaitEvent(s, H.xev[ticket % Halo::kRing], 0);
-  H.njoin = ticket + 1;
+  // njoin counts the library stream's joins only: a side stream that waits
+  // for an exchange does not make it joined for the library stream
+  if (s == H.ls || !H.ls) H.njoin = ticket + 1;
 }
 void halo_join(Halo& H, hipStream_t s) { halo_join_to(H, s, H.nfork - 1); }
 

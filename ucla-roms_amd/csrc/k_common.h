@@ -19,8 +19,9 @@ namespace roms {
 // (soffset), so a column walk keeps no 64-bit address per level in vector
 // registers -- the straight-line level loops of the column kernels otherwise
 // hold one address pair per level live across their passes (k_uv2_fused
-// spilled ~200 VGPRs that way).  Offsets must stay below 4 GiB from the base
-// (one 3-D field or one time slot: 855 MB at 1024^2 x 100).
+// spilled ~200 VGPRs that way).  Offsets must stay below 2 GiB from the base
+// (one 3-D field or one time slot: 855 MB at 1024^2 x 100); roms_gpu_init
+// refuses larger subdomains (buffer_span_ok, roms_dev.h).
 // With the array's extent given, an access beyond it is dropped by the
 // hardware (a store does nothing, a load returns 0): lanes that must not store
 // pass kBufOff instead of branching around the store, which keeps a level

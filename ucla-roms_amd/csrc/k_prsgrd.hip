@@ -13,6 +13,10 @@
 
 namespace roms {
 
+// k_prsgrd_strip.hip: rows jA..jB of the fused form in j-marching strips
+bool launch_prsgrd_strip(const Dev& d, hipStream_t s, int nrhs, int up, int imin, int imax, int jmin, int jmax,
+                         const UVBounds& ub, int& jA, int& jB);
+
 __device__ __forceinline__ double harm(double a, double b) {
   const double c = 2.0 * a * b;
   return c > 0.0 ? c / (a + b) : 0.0;
@@ -679,27 +683,40 @@ void launch_prsgrd(const Dev& d, hipStream_t s, const Tlev& t, int uv_up, bool p
   Range R1{0, b.Lm, 0, b.Mm};
   if (!p_ready) hipLaunchKernelGGL(k_prsgrd_P, grid_of(R1), dim3(kBX, kBY), 0, s, d, R1, split, d.p.tides);
   ktimer_mark(s, kTimedPrsgrdUv, 0);
-  if (uv_up >= 0 && d.p.ld16 && d.p.prs_ty != 8)
-    hipLaunchKernelGGL((k_prsgrd_uv<true, kBY, true>), grid3_of(R2, b.N), dim3(kBX, kBY), 0, s, d, R2, split, imin, imax,
-                       jmin, jmax, uv_bounds(b), uv_up, t.nrhs);
-  else if (!(uv_up >= 0) && d.p.ld16 && d.p.prs_ty != 8)
-    hipLaunchKernelGGL((k_prsgrd_uv<false, kBY, true>), grid3_of(R2, b.N), dim3(kBX, kBY), 0, s, d, R2, split, imin, imax,
-                       jmin, jmax, uv_bounds(b), 0, t.nrhs);
-  else if (uv_up >= 0 && d.p.prs_ty == 8)
-    hipLaunchKernelGGL((k_prsgrd_uv<true, 8>), grid3_ty(R2, b.N, 8), dim3(kBX, 8), 0, s, d, R2, split, imin, imax, jmin,
-                       jmax, uv_bounds(b), uv_up, t.nrhs);
-  else if (uv_up >= 0 && d.p.prs_buf)
-    hipLaunchKernelGGL((k_prsgrd_uv<true, kBY, false, true>), grid3_of(R2, b.N), dim3(kBX, kBY), 0, s, d, R2, split, imin,
-                       imax, jmin, jmax, uv_bounds(b), uv_up, t.nrhs);
-  else if (uv_up >= 0)
-    hipLaunchKernelGGL(k_prsgrd_uv<true>, grid3_of(R2, b.N), dim3(kBX, kBY), 0, s, d, R2, split, imin, imax, jmin, jmax,
-                       uv_bounds(b), uv_up, t.nrhs);
-  else if (d.p.prs_ty == 8)
-    hipLaunchKernelGGL((k_prsgrd_uv<false, 8>), grid3_ty(R2, b.N, 8), dim3(kBX, 8), 0, s, d, R2, split, imin, imax, jmin,
-                       jmax, uv_bounds(b), 0, t.nrhs);
-  else
-    hipLaunchKernelGGL(k_prsgrd_uv<false>, grid3_of(R2, b.N), dim3(kBX, kBY), 0, s, d, R2, split, imin, imax, jmin, jmax,
-                       uv_bounds(b), 0, t.nrhs);
+  auto tiles = [&](const Range& R) {   // k_prsgrd_uv over R (the variant Params selects)
+    if (uv_up >= 0 && d.p.ld16 && d.p.prs_ty != 8)
+      hipLaunchKernelGGL((k_prsgrd_uv<true, kBY, true>), grid3_of(R, b.N), dim3(kBX, kBY), 0, s, d, R, split, imin, imax,
+                         jmin, jmax, uv_bounds(b), uv_up, t.nrhs);
+    else if (!(uv_up >= 0) && d.p.ld16 && d.p.prs_ty != 8)
+      hipLaunchKernelGGL((k_prsgrd_uv<false, kBY, true>), grid3_of(R, b.N), dim3(kBX, kBY), 0, s, d, R, split, imin,
+                         imax, jmin, jmax, uv_bounds(b), 0, t.nrhs);
+    else if (uv_up >= 0 && d.p.prs_ty == 8)
+      hipLaunchKernelGGL((k_prsgrd_uv<true, 8>), grid3_ty(R, b.N, 8), dim3(kBX, 8), 0, s, d, R, split, imin, imax, jmin,
+                         jmax, uv_bounds(b), uv_up, t.nrhs);
+    else if (uv_up >= 0 && d.p.prs_buf)
+      hipLaunchKernelGGL((k_prsgrd_uv<true, kBY, false, true>), grid3_of(R, b.N), dim3(kBX, kBY), 0, s, d, R, split, imin,
+                         imax, jmin, jmax, uv_bounds(b), uv_up, t.nrhs);
+    else if (uv_up >= 0)
+      hipLaunchKernelGGL(k_prsgrd_uv<true>, grid3_of(R, b.N), dim3(kBX, kBY), 0, s, d, R, split, imin, imax, jmin, jmax,
+                         uv_bounds(b), uv_up, t.nrhs);
+    else if (d.p.prs_ty == 8)
+      hipLaunchKernelGGL((k_prsgrd_uv<false, 8>), grid3_ty(R, b.N, 8), dim3(kBX, 8), 0, s, d, R, split, imin, imax, jmin,
+                         jmax, uv_bounds(b), 0, t.nrhs);
+    else
+      hipLaunchKernelGGL(k_prsgrd_uv<false>, grid3_of(R, b.N), dim3(kBX, kBY), 0, s, d, R, split, imin, imax, jmin, jmax,
+                         uv_bounds(b), 0, t.nrhs);
+  };
+  // with the momentum r.h.s. (whole steps): rows jA..jB in j-marching strips
+  // (k_prsgrd_strip.hip), the bands of rows a closed-edge j-extrapolation
+  // reaches in k_prsgrd_uv tiles; ROMS_GPU_PRS_STRIP=0: tiles everywhere
+  int jA = 0, jB = -1;
+  if (uv_up >= 0 && d.p.prs_strip && d.p.uv_cor && d.p.uv_adv && !d.p.curvgrid &&
+      launch_prsgrd_strip(d, s, t.nrhs, uv_up, imin, imax, jmin, jmax, uv_bounds(b), jA, jB)) {
+    if (jA > R2.j0) tiles(Range{R2.i0, R2.i1, R2.j0, jA - 1});
+    if (jB < R2.j1) tiles(Range{R2.i0, R2.i1, jB + 1, R2.j1});
+  } else {
+    tiles(R2);
+  }
   ktimer_mark(s, kTimedPrsgrdUv, 1, 1);
 }
 // k_prsgrd_uv<true> adds the horizontal momentum r.h.s. of k_uv_horiz1 on

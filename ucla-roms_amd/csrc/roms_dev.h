@@ -70,6 +70,7 @@ struct Params {
   int prs_ty;     // tile rows of k_prsgrd_uv: 4 or 8 (ROMS_GPU_PRS_TY)
   int ld16;       // padded pitch: LDS windows read two doubles per lane (16-B loads; ROMS_GPU_LD16=0: 8-B)
   int prs_buf;    // k_prsgrd_uv windows through buffer loads (ROMS_GPU_PRS_BUF)
+  int prs_strip;  // prsgrd + momentum r.h.s. in j-marching strips (k_prsgrd_strip; ROMS_GPU_PRS_STRIP=0: tiles)
   int visc_stg;   // visc3d: raw u/v/Hz windows staged in LDS per level (default; ROMS_GPU_VISC_STG=0: per-point loads)
   int t3dmix_stg; // t3dmix (two tracers): Hz/T/S windows staged in LDS per level (default; ROMS_GPU_T3DMIX_STG=0: per-point loads)
   int kpp_ty;     // k_kpp_int: 4 (default) staged Rig windows on 64x4 blocks, 8 on 64x8, 43 64x4 at 3 waves/SIMD, 0 one row per block (ROMS_GPU_KPP_TY)
@@ -342,7 +343,15 @@ struct Tlev {
 constexpr int kTimedS2dFb = 13;   // ROMS_R_K_S2D_FB
 constexpr int kTimedPreUvSeg = 14, kTimedUv1Seg = 15, kTimedStep3dTSeg = 16;   // ROMS_R_K_*_SEG
 constexpr int kTimedPrsgrdUv = 17;   // ROMS_R_K_PRSGRD_UV
+constexpr int kTimedHaloPack = 18, kTimedHaloWait = 19, kTimedHaloUnpack = 20;   // ROMS_R_K_HALO_*
 void ktimer_mark(hipStream_t s, int kernel_id, int end, int count = 0);
+
+// The buffer-addressed kernels (BufF64, k_common.h) address one field with
+// 32-bit byte offsets that must stay below 2 GiB (kBufOff = 2^31 marks a lane
+// whose access the hardware drops): every field -- the largest is a w-point
+// field, n2*(N+1) doubles on the padded pitch -- must fit.  roms_gpu_init
+// refuses a subdomain that does not (1024^2 x 100 uses 0.85 GiB).
+inline bool buffer_span_ok(const Bounds& b) { return b.n3w * 8 < 2147483648L; }
 
 void launch_exchange(const Dev& d, hipStream_t s, double* a, int nlev);
 // several arrays in one launch (one reference exchange_xxx(A,B,C,D) call);

@@ -431,8 +431,8 @@ void enqueue_step(roms_tlev* t, bool rho_current, bool store_huv) {
     (void)hipEventRecord(g.pev[k], s2);
     (void)hipStreamWaitEvent(s, g.pev[k], 0);
   };
-  // Multi-rank runs (Halo::xoverlap, default with > 1 rank; not while one
-  // routine is timed): the trailing exchange of a producer in DEFER(...) runs
+  // Multi-rank runs (Halo::xoverlap: the default with > 1 rank when every
+  // rank drives its own GPU; not while one routine is timed): the trailing exchange of a producer in DEFER(...) runs
   // on the halo stream beside the routines that follow it, and XJOIN(t) makes
   // the library stream wait for it just before the first routine that reads
   // its halo (mpi_exchanges.F:672-800 posts and waits on every
@@ -442,7 +442,7 @@ void enqueue_step(roms_tlev* t, bool rho_current, bool store_huv) {
   // corrector's omega.  Same kernels on the same inputs, so the fields are
   // bitwise those of the serial order (tests/test_gpu_multirank.py, with a
   // delay hook that makes a missing join read stale halos).
-  const bool xo = d.halo != nullptr && g.halo.xoverlap && g.timed < 0;
+  const bool xo = d.halo != nullptr && g.halo.xoverlap > 0 && g.timed < 0;
   long xt = -1;   // ticket of the last deferred exchange
 #define DEFER(call)                          \
   do {                                       \
@@ -728,7 +728,6 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
       return -1;
     }
   }
-  CHECK_HIP(hipSetDevice(device));
   g.dims = *dims;
   g.cfg = *cfg;
   g.have_volume = false;
@@ -770,6 +769,13 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     g.hb = make_bounds(*dims, hx);
     g.d.p.s2d_k = k;
   }
+  if (!buffer_span_ok(g.d.b)) {
+    // checked before the device is touched (a host-only test calls this)
+    g.err = "roms_gpu_init: subdomain too large for one GPU rank: a w-point field (n2*(N+1)*8 B) reaches 2 GiB, "
+            "the limit of the kernels' 32-bit buffer offsets (k_common.h BufF64); split the grid over more ranks";
+    return -1;
+  }
+  CHECK_HIP(hipSetDevice(device));
   g.d.b.nTS = g.hb.nTS = cfg->salinity ? 2 : 1;
   Params& P = g.d.p;
   {
@@ -975,6 +981,13 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     P.prs_buf = !(e && e[0] == '0');
   }
   {
+    // prsgrd's ru/rv with the momentum r.h.s. in j-marching strips (one
+    // evaluation per face, neighbours through DPP lane shifts; bitwise equal
+    // to the k_prsgrd_uv tiles); ROMS_GPU_PRS_STRIP=0: tiles everywhere
+    const char* e = getenv("ROMS_GPU_PRS_STRIP");
+    P.prs_strip = !(e && e[0] == '0');
+  }
+  {
     const char* e = getenv("ROMS_GPU_TCHUNK");
     P.t_chunk = e ? atoi(e) : 0;
     if (P.t_chunk < 0) P.t_chunk = 0;
@@ -1108,6 +1121,7 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     }
     const int r = halo_setup(g.halo, (RomsComm*)comm, plan, 8 * (dims->N + 1), wide, kExchMax, g.err);
     if (r) return r;
+    g.halo.ls = g.s;
     g.d.halo = &g.halo;
   }
   {
@@ -1217,6 +1231,11 @@ ROUTINE(roms_gpu_set_depth, launch_set_depth(g.d, g.s, T))
 int roms_gpu_halo_transport(void) {
   REQUIRE_INIT_NOJOIN();
   return g.d.halo ? halo_transport(g.halo) : 0;
+}
+
+int roms_gpu_halo_overlap(void) {
+  REQUIRE_INIT_NOJOIN();
+  return g.d.halo && g.halo.xoverlap > 0 ? 1 : 0;
 }
 
 int roms_gpu_halo_exchanges(long* per_step, int* fast_interval) {

@@ -206,7 +206,8 @@ WRT_DEFAULT = 63
 ROUTINES = ("rho_eos", "set_HUV", "omega", "prsgrd", "pre_step3d", "set_HUV1", "step3d_uv1", "visc3d", "step2d",
             "step3d_uv2", "step3d_t", "t3dmix", "lmd_vmix",
             "k_s2d_fb",  # kernel level: the fused barotropic kernel alone
-            "k_pre_uv_seg", "k_uv1_seg", "k_step3d_t_seg", "k_prsgrd_uv")  # kernel level: the N > 63 column solvers
+            "k_pre_uv_seg", "k_uv1_seg", "k_step3d_t_seg", "k_prsgrd_uv",  # kernel level: the N > 63 column solvers
+            "k_halo_pack", "k_halo_wait", "k_halo_unpack")  # halo path: pack / transport / unpack of every exchange
 HALO_OPP = (1, 0, 3, 2, 7, 6, 5, 4)
 
 
@@ -532,6 +533,11 @@ class Model:
         """'ipc', 'rccl' (or single rank / in-process), or 'ipc-timeout'."""
         r = self.L.roms_gpu_halo_transport()
         return {1: "ipc", 0: "rccl", -1: "ipc-timeout"}.get(r, "error")
+
+    def halo_overlap(self):
+        """True when whole steps defer 3-D exchanges onto the halo stream
+        (roms_gpu_halo_overlap: the default with > 1 rank, one GPU each)."""
+        return bool(self.L.roms_gpu_halo_overlap())
 
     def halo_exchanges(self):
         """(exchanges in the last enqueued step, fast-loop exchange interval)
