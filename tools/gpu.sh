@@ -13,6 +13,7 @@
 #                             V = lib:<tag> (ucla-roms_amd/libromsgpu_<tag>.so from tools/build_variant.sh;
 #                             lib:cur the in-tree build) or env:VAR=1,VAR2=0 (environment switches)
 #   stall                     issue/wait PMC of the C2 kernels (tools/pmc_stall.sh)
+#   valu TAG                  VALU instruction mix per C3 kernel (tools/pmc_valu.py -> gpurun_out/pmc_valu_c3.json)
 #   final TAG                 the default bench line, C3/C2 kernel traces, PMC tables and a 2-rank
 #                             one-GPU rehearsal (both exchange orders): the round's profile set
 CMD=$1; TAG=$2; shift 2
@@ -86,6 +87,13 @@ ab)
   done ;;
 stall)
   bash $R/tools/pmc_stall.sh ;;
+valu)
+  # VALU instruction mix per kernel at C3 (one --pmc pass of 8 SQ counters)
+  cd /tmp && export TMPDIR=/tmp
+  export ROMS_GPU_NO_GRAPH=1
+  B="python $R/bench.py --no-cpu-baseline --no-secondary --workload c3 --timing-steps 1 --steps 2 --warmup 1"
+  timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 --output-format csv -d $O/pv_$TAG -o run -- $B > $O/pv_$TAG.log 2>&1 || exit 1
+  python3 $R/tools/pmc_valu.py $(find $O/pv_$TAG -name '*counter_collection.csv') --out $O/pmc_valu_c3.json || exit 1 ;;
 final)
   timeout -k 10 500 python bench.py > $O/bench_$TAG.json 2> $O/bench_$TAG.err || { echo BENCHFAIL; tail -20 $O/bench_$TAG.err; exit 1; }
   row $O/bench_$TAG.json bench

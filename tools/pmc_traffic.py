@@ -36,6 +36,8 @@ ROUTINE_OF = {
     # round 5: buffer-addressed segment solvers
     "k_pre_tracer_segb": "pre_step3d", "k_pre_uv_segb": "pre_step3d", "k_uv1_segb": "step3d_uv1",
     "k_step3d_t_segb": "step3d_t",
+    # round 6: prsgrd + momentum r.h.s. in j-marching strips
+    "k_prsgrd_strip": "prsgrd",
 }
 CALLS_PER_STEP = {"rho_eos": 2, "set_HUV": 1, "omega": 3, "prsgrd": 2, "pre_step3d": 1, "set_HUV1": 1,
                   "step3d_uv1": 1, "visc3d": 1, "step2d": None, "step3d_uv2": 1, "step3d_t": 1, "t3dmix": 1,

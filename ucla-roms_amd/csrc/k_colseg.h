@@ -117,9 +117,13 @@ struct SegXchg {
 // load); straight-line rows let it issue the loads of many rows back to back.
 // The live rows keep their expressions and order: results are unchanged.
 // Every segment of a launch has at least kSegNMin rows (seg_rows_ok, checked
-// on the host before a segment solver is chosen: N >= 50 at <= 13 rows per
-// segment gives 11), so rows q < kSegNMin are live in every wave and their
-// selects fold away at compile time; only the last rows pay for them.
+// on the host before a segment solver is chosen), so rows q < kSegNMin are
+// live in every wave and their selects fold away at compile time; only the
+// last rows pay for them.  With 16-column blocks the segment count is rounded
+// up to a multiple of four (four segments per wavefront, seg_count): N = 88..104
+// gives 8 segments of 11-13 rows; N = 64..87 would give 8 segments of 8-10
+// rows, fails the check and runs the sequential column solvers on global
+// scratch instead (ROMS_GPU_COLSEG=1 cannot force it).
 __device__ __forceinline__ bool seg_live(int q, int n) { return q < kSegNMin || q < n; }
 __device__ __forceinline__ bool seg_last(int q, int n) { return q >= kSegNMin - 1 && q == n - 1; }
 
