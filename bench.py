@@ -334,25 +334,23 @@ def run_workload(kind, romsgpu, comm, rank, world, local_rank, steps, warmup, ti
         # trace_check names the committed trace's own maximum beside it
         c3k = {}
         for kname, npass in (("k_pre_uv_seg", PRE_UV_SEG_PASSES), ("k_prsgrd_uv", PRSGRD_UV_PASSES),
-                             ("k_uv1_seg", UV1_SEG_PASSES)):
-            kms, kn = m.time_routine(kname, timing_steps)
-            kb = 8.0 * npass * cells3
+                             ("k_uv1_seg", UV1_SEG_PASSES), ("k_s2d_fb", None)):
+            if kname == "k_s2d_fb":
+                kms, kn, kb = fb_ms, fb_n, fb_bytes
+            else:
+                kms, kn = m.time_routine(kname, timing_steps)
+                kb = 8.0 * npass * cells3
             kg = kb / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
-            # the buffer-addressed forms (k_pre_uv_segb, k_uv1_segb) under their own names in the PMC table
-            kt = pmc_kernel_traffic(kname + "b", c3=True)
-            kn_name = kname + "b" if kt is not None else kname
-            if kt is None:
-                kt = pmc_kernel_traffic(kname, c3=True)
+            names = PMC_KERNELS[kname]
+            kt = pmc_group(names, _pmc(True), "traffic_bytes")
             c3k[kname] = {"bound": "hbm", "achieved": kg, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                           "frac": kg / HBM_PEAK_GBS, "traffic": kt, "traffic_source": PMC_SOURCE_C3,
-                          "kernel": kn_name, "bytes_per_launch": kb, "ms_per_launch": kms,
+                          "kernel": " + ".join(n for n in names if pmc_group([n], _pmc(True), "traffic_bytes")) or
+                                    kname,
+                          "bytes_per_launch": kb, "ms_per_launch": kms,
                           "launches_per_step": kn / timing_steps, "ms_per_step": kms * kn / timing_steps,
-                          "passes": npass}
-        c3k["k_s2d_fb"] = {"bound": "hbm", "achieved": fb_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                           "frac": fb_gbs / HBM_PEAK_GBS, "traffic": pmc_kernel_traffic("k_s2d_fb", c3=True),
-                           "traffic_source": PMC_SOURCE_C3, "kernel": "k_s2d_fb", "bytes_per_launch": fb_bytes,
-                           "ms_per_launch": fb_ms, "launches_per_step": fb_n / timing_steps,
-                           "ms_per_step": fb_ms * fb_n / timing_steps, "passes": "35 2-D"}
+                          "passes": npass if npass is not None else "35 2-D"}
+            c3k[kname].update(valu_issue(names, kms))
     transport = m.halo_transport() if comm is not None else "none (single rank)"
     # exchanges per step (the fast loop's zeta/ubar/vbar swap every K fast steps)
     exch, fast_k = m.halo_exchanges() if comm is not None else (0, 1)
@@ -426,6 +424,49 @@ def pmc_kernel_traffic(kernel, c3=False):
         return None if k is None else float(k["traffic_bytes"]) / float(k["dispatches"])
     except (KeyError, TypeError, ZeroDivisionError, ValueError):
         return None
+
+
+# the kernels each timed interval of the C3 candidates launches (PMC table names)
+PMC_KERNELS = {"k_prsgrd_uv": ["k_prsgrd_strip", "k_prsgrd_uv"], "k_pre_uv_seg": ["k_pre_uv_segb", "k_pre_uv_seg"],
+               "k_uv1_seg": ["k_uv1_segb", "k_uv1_seg"], "k_s2d_fb": ["k_s2d_fb"]}
+VALU_SOURCE = ("stored: profiles/pmc_valu_c3.json (rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_*_F64; "
+               "tools/gpu.sh valu)")
+SIMDS, CLK_GHZ = 1024, 2.4   # MI355X: 256 CUs x 4 SIMDs; peak engine clock
+
+
+def pmc_group(names, table, key):
+    """Per-launch sum of `key` over the kernels one timed interval launches:
+    the first name present sets the launch count (its dispatches), every
+    present kernel's total is divided by it; None if none is present."""
+    ks = table.get("kernels", {}) if table else {}
+    present = [n for n in names if n in ks]
+    if not present:
+        return None
+    try:
+        n0 = float(ks[present[0]]["dispatches"])
+        if key == "traffic_bytes":
+            return sum(float(ks[n]["traffic_bytes"]) for n in present) / n0
+        return sum(float(ks[n][key]) * float(ks[n]["dispatches"]) for n in present) / n0
+    except (KeyError, TypeError, ZeroDivisionError, ValueError):
+        return None
+
+
+def valu_issue(names, ms):
+    """roofline.valu_frac: the VALU issue time of one launch (a wave64 FP64
+    instruction holds a SIMD 4 cycles -- FP64 78.6 TF = 16 lanes per cycle per
+    SIMD -- every other VALU instruction 2) over the measured launch time."""
+    p = os.path.join(ROOT, "profiles", "pmc_valu_c3.json")
+    try:
+        t = json.load(open(p))
+    except (OSError, ValueError):
+        return {}
+    valu, f64 = pmc_group(names, t, "valu"), pmc_group(names, t, "valu_f64")
+    if valu is None or f64 is None or not ms or ms <= 0:
+        return {}
+    cyc = 4.0 * f64 + 2.0 * (valu - f64)
+    issue_ms = cyc / SIMDS / (CLK_GHZ * 1e9) * 1e3
+    return {"valu_frac": issue_ms / ms, "valu_issue_ms": issue_ms, "valu_insts": valu, "valu_f64_insts": f64,
+            "valu_source": VALU_SOURCE}
 
 
 def trace_top_kernel():

@@ -1145,8 +1145,9 @@ void launch_pre_step3d(const Dev& d, hipStream_t s, const Tlev& t, bool uv_done,
   hb_done = hb_done && d.p.hoist && b.NT <= 2;
   Range RI{b.istr, b.iend, b.jstr, b.jend};
   Range RH{b.istr - 1, b.iend, b.jstr - 1, b.jend};
-  // horizontal part on rows rh (the ring i = istr-1, j = jstr-1 included)
-  auto horiz = [&](const Range& rh) {
+  // horizontal part on rows rh (the ring i = istr-1, j = jstr-1 included):
+  // the rows strips cover (k_tracer_strip.hip), the rest on tiles
+  auto horiz_tiles = [&](const Range& rh) {
     if (d.p.hoist && d.p.h_jc > 0 && (b.NT == 1 || b.NT == 2)) {
       const dim3 g = grid3_jc(rh, b.N, d.p.h_jc), bs(kBX, kBY);
       const int jc = d.p.h_jc;
@@ -1175,6 +1176,16 @@ void launch_pre_step3d(const Dev& d, hipStream_t s, const Tlev& t, bool uv_done,
         hipLaunchKernelGGL((k_pre_tracer_h1<1, 4, false>), grid3_ty(rh, b.N, 4), dim3(kBX, 4), 0, s, d, rh, c, t.nstp, t.nnew, t.nrhs);
     } else {
       hipLaunchKernelGGL(k_pre_tracer_h, grid3_of(rh, b.N), dim3(kBX, kBY), 0, s, d, rh, c, t.nstp, t.nnew, t.nrhs);
+    }
+  };
+  auto horiz = [&](const Range& rh) {
+    int jA = 0, jB = -1;
+    if (d.p.hoist && d.p.h_jc == 0 &&
+        launch_tracer_strip(d, s, rh, 1, false, hb_done, t.nnew, t.nrhs, c.dtau, c.cf_stp, c.cf_bak, t.nstp, jA, jB)) {
+      if (jA > rh.j0) horiz_tiles(Range{rh.i0, rh.i1, rh.j0, jA - 1});
+      if (jB < rh.j1) horiz_tiles(Range{rh.i0, rh.i1, jB + 1, rh.j1});
+    } else {
+      horiz_tiles(rh);
     }
   };
   // column solves on rows ri

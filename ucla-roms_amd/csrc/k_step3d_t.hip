@@ -581,7 +581,7 @@ void launch_step3d_t(const Dev& d, hipStream_t s, const Tlev& t, bool exchange) 
     return;
   }
   // horizontal fluxes, then the column solves, on a sub-range of the interior
-  auto run = [&](const Range& r) {
+  auto h_tiles = [&](const Range& r) {
     if (d.p.hoist && b.NT == 2 && d.p.h_ty == 8)
       hipLaunchKernelGGL((k_step3d_t_h1<2, 8>), grid3_ty(r, b.N, 8), dim3(kBX, 8), 0, s, d, r, t.nnew, t.nrhs);
     else if (d.p.hoist && b.NT == 2)
@@ -590,6 +590,16 @@ void launch_step3d_t(const Dev& d, hipStream_t s, const Tlev& t, bool exchange) 
       hipLaunchKernelGGL((k_step3d_t_h1<1, 4>), grid3_ty(r, b.N, 4), dim3(kBX, 4), 0, s, d, r, t.nnew, t.nrhs);
     else
       hipLaunchKernelGGL(k_step3d_t_h, grid3_of(r, b.N), dim3(kBX, kBY), 0, s, d, r, t.nnew, t.nrhs, 1);
+  };
+  auto run = [&](const Range& r) {
+    // horizontal advection: the rows strips cover (k_tracer_strip.hip), the rest on tiles
+    int jA = 0, jB = -1;
+    if (d.p.hoist && launch_tracer_strip(d, s, r, 0, true, false, t.nnew, t.nrhs, 0.0, 0.0, 0.0, 0, jA, jB)) {
+      if (jA > r.j0) h_tiles(Range{r.i0, r.i1, r.j0, jA - 1});
+      if (jB < r.j1) h_tiles(Range{r.i0, r.i1, jB + 1, r.j1});
+    } else {
+      h_tiles(r);
+    }
     dim3 gt = gridc_of(r);
     gt.z = b.NT;
     if (d.p.colseg) {

@@ -828,7 +828,9 @@ __global__ void __launch_bounds__(256) k_rho_eos_linear(Dev d, Range R, int tidx
 }
 
 #ifndef ROMS_RHO_UNROLL
-#define ROMS_RHO_UNROLL 4
+// 1: 2 SGPR spills and 4 waves/SIMD instead of 13 spills at 3 (unroll 4);
+// rho_eos 1.446 vs 1.441 ms per C3 call, within noise (profiles/r6_e_tracer_strip_ab.txt)
+#define ROMS_RHO_UNROLL 1
 #endif
 #ifndef ROMS_RHO_PF
 #define ROMS_RHO_PF 4

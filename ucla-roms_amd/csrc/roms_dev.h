@@ -71,6 +71,7 @@ struct Params {
   int ld16;       // padded pitch: LDS windows read two doubles per lane (16-B loads; ROMS_GPU_LD16=0: 8-B)
   int prs_buf;    // k_prsgrd_uv windows through buffer loads (ROMS_GPU_PRS_BUF)
   int prs_strip;  // prsgrd + momentum r.h.s. in j-marching strips (k_prsgrd_strip; ROMS_GPU_PRS_STRIP=0: tiles)
+  int t_strip;    // horizontal tracer advection in j-marching strips (k_tracer_strip; ROMS_GPU_T_STRIP=0: tiles)
   int visc_stg;   // visc3d: raw u/v/Hz windows staged in LDS per level (default; ROMS_GPU_VISC_STG=0: per-point loads)
   int t3dmix_stg; // t3dmix (two tracers): Hz/T/S windows staged in LDS per level (default; ROMS_GPU_T3DMIX_STG=0: per-point loads)
   int kpp_ty;     // k_kpp_int: 4 (default) staged Rig windows on 64x4 blocks, 8 on 64x8, 43 64x4 at 3 waves/SIMD, 0 one row per block (ROMS_GPU_KPP_TY)
@@ -422,6 +423,10 @@ void launch_rho_eos(const Dev& d, hipStream_t s, const Tlev& t, int tidx);
 // passes uv_done to it)
 // p_ready: P is current from the last rho_eos (p_in_rho), k_prsgrd_P is skipped
 void launch_prsgrd(const Dev& d, hipStream_t s, const Tlev& t, int uv_up = -1, bool p_ready = false);
+// k_tracer_strip.hip: rows jA..jB of R's horizontal tracer advection in
+// j-marching strips (mode 0 step3d_t, 1 pre_step3d); false: not covered
+bool launch_tracer_strip(const Dev& d, hipStream_t s, const Range& R, int mode, bool up, bool hb_done, int nnew,
+                         int nrhs, double dtau, double cf_stp, double cf_bak, int nstp, int& jA, int& jB);
 bool p_in_rho(const Dev& d);   // every rho_eos also forms prsgrd's P (k_vertical.hip)
 void launch_prsgrd_P(const Dev& d, hipStream_t s);   // prsgrd's P alone (k_prsgrd_P)
 bool prsgrd_can_fuse_uv(const Dev& d);

@@ -988,6 +988,15 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     P.prs_strip = !(e && e[0] == '0');
   }
   {
+    // horizontal tracer advection of pre_step3d / step3d_t in j-marching
+    // strips (k_tracer_strip, bitwise equal to the k_*_h1 tiles): measured
+    // slower at C3 (pre_step3d 9.65 -> 10.56, step3d_t 4.75 -> 5.66 ms per
+    // call, profiles/r6_e_tracer_strip_ab.txt: too little arithmetic per row
+    // to cover each row's loads), so opt-in, ROMS_GPU_T_STRIP=1
+    const char* e = getenv("ROMS_GPU_T_STRIP");
+    P.t_strip = e && e[0] == '1';
+  }
+  {
     const char* e = getenv("ROMS_GPU_TCHUNK");
     P.t_chunk = e ? atoi(e) : 0;
     if (P.t_chunk < 0) P.t_chunk = 0;
