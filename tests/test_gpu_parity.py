@@ -512,8 +512,8 @@ def test_prsgrd_uv_tile_rows_bitwise(case, monkeypatch):
 
 @pytest.mark.parametrize("case", ["filament", "basin_odd", "basin_obc_odd"])
 def test_ld16_windows_bitwise(case, monkeypatch):
-    """LDS windows read two doubles per lane (ROMS_GPU_LD16, default with the
-    padded pitch: k_prsgrd_uv's raw and u/v windows) equal the 8-B form
+    """LDS windows read two doubles per lane (ROMS_GPU_LD16=1, opt-in, needs
+    the padded pitch: k_prsgrd_uv's raw and u/v windows) equal the 8-B form
     bitwise over 4 whole steps and one prsgrd routine call; odd Lm puts the
     last pair of a row half outside -1..Lm+2 (its upper double must read as 0)."""
     if case == "basin_odd":
