@@ -47,13 +47,10 @@ __device__ __forceinline__ double harm2(double a, double b) {   // k_prsgrd.hip 
 
 constexpr int kStripOwn = 60;   // owned columns per strip (lanes 2..61)
 #ifndef ROMS_PRS_STRIP_PF
-#define ROMS_PRS_STRIP_PF 1   // rows ahead whose inputs are loaded before this row's stores (0, 1, 2)
+#define ROMS_PRS_STRIP_PF 1   // 1: the next row's inputs are loaded before this row's stores
 #endif
 #ifndef ROMS_PRS_STRIP_J
 #define ROMS_PRS_STRIP_J 8    // rows per wavefront
-#endif
-#ifndef ROMS_PRS_STRIP_UNROLL
-#define ROMS_PRS_STRIP_UNROLL 8   // row loop unroll (8: straight-line rows, no register rotation)
 #endif
 #ifndef ROMS_PRS_STRIP_WAVES
 #define ROMS_PRS_STRIP_WAVES 1   // __launch_bounds__ minimum waves per SIMD
@@ -195,31 +192,23 @@ __global__ void __launch_bounds__(64, ROMS_PRS_STRIP_WAVES) k_prsgrd_strip(Dev d
   double HueeP = sec(FUm2, FUm1, FU0);
   double urP = dpp_shl(Um1);   // u(i+1, j-1)
 
-  // ---- the march: row j's new inputs are loaded one row ahead (PF = 1) or
-  // two (PF = 2: a ring of two rows' inputs) ----
-  struct RowIn {
-    double U, V, FV, FU, Z, R, Q, vm, HZ, PP, um, dn, dm, fo;
+  // ---- the march: row j's new inputs are loaded one row ahead (PF) ----
+  double nU = 0, nV = 0, nFV = 0, nFU = 0, nZ = 0, nR = 0, nQ = 0, nvm = 0, nHZ = 0, nPP = 0, num = 0, ndn = 0,
+         ndm = 0, nfo = 0;
+  auto load_row = [&](int jr) {   // inputs new at row jr
+    nU = L3(bU, jr + 2); nV = L3(bV, jr + 2); nFV = L3(bFV, jr + 2); nFU = L3(bFU, jr + 1);
+    nZ = L3(bZ, jr + 1); nR = L3(bR, jr + 1); if (SPLIT) nQ = L3(bQ, jr + 1); nvm = L2(bvm, jr + 1);
+    nHZ = L3(bHz, jr); nPP = L3(bP, jr); num = L2(bum, jr); ndn = L2(bdn, jr); ndm = L2(bdm, jr); nfo = L2(bfo, jr);
   };
-  auto load_row = [&](RowIn& q, int jr) {   // inputs new at row jr
-    q.U = L3(bU, jr + 2); q.V = L3(bV, jr + 2); q.FV = L3(bFV, jr + 2); q.FU = L3(bFU, jr + 1);
-    q.Z = L3(bZ, jr + 1); q.R = L3(bR, jr + 1); q.Q = SPLIT ? L3(bQ, jr + 1) : 0.0; q.vm = L2(bvm, jr + 1);
-    q.HZ = L3(bHz, jr); q.PP = L3(bP, jr); q.um = L2(bum, jr); q.dn = L2(bdn, jr); q.dm = L2(bdm, jr);
-    q.fo = L2(bfo, jr);
-  };
-  constexpr int PF = ROMS_PRS_STRIP_PF;
-  RowIn ring0{}, ring1{};
-  if (PF >= 1) load_row(ring0, j);
-  if (PF >= 2 && nrow > 1) load_row(ring1, j + 1);
-#pragma unroll ROMS_PRS_STRIP_UNROLL
+  if (ROMS_PRS_STRIP_PF) load_row(j);
+#pragma unroll
   for (int r = 0; r < J; r++) {
     if (r >= nrow) break;
     const int jr = ja + r;
-    RowIn& slot = (PF == 2 && (r & 1)) ? ring1 : ring0;
-    if (PF == 0) load_row(slot, jr);
-    const RowIn q = slot;
-    if (PF >= 1 && r + PF < nrow) load_row(slot, jr + PF);   // a later row's inputs, before this row's stores
-    const double U2 = q.U, V2 = q.V, FV2 = q.FV, FU1 = q.FU, Z1 = q.Z, R1 = q.R, Q1 = q.Q, vm1 = q.vm;
-    const double HZ0 = q.HZ, PP0 = q.PP, um0 = q.um, dn0 = q.dn, dm0 = q.dm, fo0 = q.fo;
+    if (!ROMS_PRS_STRIP_PF) load_row(jr);
+    const double U2 = nU, V2 = nV, FV2 = nFV, FU1 = nFU, Z1 = nZ, R1 = nR, Q1 = nQ, vm1 = nvm;
+    const double HZ0 = nHZ, PP0 = nPP, um0 = num, dn0 = ndn, dm0 = ndm, fo0 = nfo;
+    if (ROMS_PRS_STRIP_PF && r + 1 < nrow) load_row(jr + 1);   // the next row's inputs, before this row's stores
     // -- pressure gradient, XI: u-point at this lane (between i-1 and i),
     // harmonic means at rho points i (this lane) and i-1 (from the left) --
     const double Zl = dpp_shr(Z0), Rl = dpp_shr(R0), Ql = SPLIT ? dpp_shr(Q0) : 0.0;
