@@ -14,8 +14,8 @@
 #                             lib:cur the in-tree build) or env:VAR=1,VAR2=0 (environment switches)
 #   stall                     issue/wait PMC of the C2 kernels (tools/pmc_stall.sh)
 #   valu TAG                  VALU instruction mix per C3 kernel (tools/pmc_valu.py -> gpurun_out/pmc_valu_c3.json)
-#   final TAG                 the default bench line, C3/C2 kernel traces, PMC tables and a 2-rank
-#                             one-GPU rehearsal (both exchange orders): the round's profile set
+#   final TAG 1|2             1: the default bench line, C3/C2 kernel traces; 2: PMC traffic and VALU
+#                             tables and a 2-rank one-GPU rehearsal (both exchange orders)
 CMD=$1; TAG=$2; shift 2
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}; O=$R/gpurun_out; mkdir -p $O; cd $R
 PYT="python -u -m pytest -q --timeout 300 --timeout-method thread"
@@ -95,13 +95,21 @@ valu)
   timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 --output-format csv -d $O/pv_$TAG -o run -- $B > $O/pv_$TAG.log 2>&1 || exit 1
   python3 $R/tools/pmc_valu.py $(find $O/pv_$TAG -name '*counter_collection.csv') --out $O/pmc_valu_c3.json || exit 1 ;;
 final)
-  timeout -k 10 500 python bench.py > $O/bench_$TAG.json 2> $O/bench_$TAG.err || { echo BENCHFAIL; tail -20 $O/bench_$TAG.err; exit 1; }
-  row $O/bench_$TAG.json bench
-  bash $R/tools/gpu.sh trace ${TAG}_c3 c3 || exit 1
-  bash $R/tools/gpu.sh trace ${TAG}_c2 c2 || exit 1
-  bash $R/tools/gpu.sh pmc x || exit 1
-  cd $R
-  timeout -k 10 300 python bench.py --gpus 2 --steps 5 --warmup 1 --no-cpu-baseline --no-secondary > $O/bench_${TAG}_n2.json 2> $O/bench_${TAG}_n2.err || { tail -10 $O/bench_${TAG}_n2.err; exit 1; }
-  python3 -c "import json; d=json.load(open('$O/bench_${TAG}_n2.json')); print('n2', d['ms_per_step'], d['config'].get('exchange_overlap'))" ;;
+  # the round's profile set in two calls (each within gpurun's limit):
+  # final TAG 1 = bench line + C3/C2 kernel traces; final TAG 2 = PMC traffic
+  # and VALU tables + the 2-rank one-GPU rehearsal
+  PART=${1:-1}
+  if [ "$PART" = 1 ]; then
+    timeout -k 10 500 python bench.py > $O/bench_$TAG.json 2> $O/bench_$TAG.err || { echo BENCHFAIL; tail -20 $O/bench_$TAG.err; exit 1; }
+    row $O/bench_$TAG.json bench
+    bash $R/tools/gpu.sh trace ${TAG}_c3 c3 || exit 1
+    bash $R/tools/gpu.sh trace ${TAG}_c2 c2 || exit 1
+  else
+    bash $R/tools/gpu.sh pmc x || exit 1
+    bash $R/tools/gpu.sh valu $TAG || exit 1
+    cd $R
+    timeout -k 10 300 python bench.py --gpus 2 --steps 5 --warmup 1 --no-cpu-baseline --no-secondary > $O/bench_${TAG}_n2.json 2> $O/bench_${TAG}_n2.err || { tail -10 $O/bench_${TAG}_n2.err; exit 1; }
+    python3 -c "import json; d=json.load(open('$O/bench_${TAG}_n2.json')); print('n2', d['ms_per_step'], d['config'].get('exchange_overlap'))"
+  fi ;;
 *) echo "usage: bash tools/gpu.sh suite|tests|bench|trace|pmc|ab|stall|final TAG ..."; exit 2 ;;
 esac
