@@ -58,7 +58,7 @@ module roms_gpu_mod
   ! LMD switch bits of lmd_mixing (ROMS_LMD_*)
   integer(c_int), parameter :: ROMS_LMD_MIXING = 1, ROMS_LMD_KPP = 2, ROMS_LMD_BKPP = 4, ROMS_LMD_RIMIX = 8, &
                                ROMS_LMD_CONVEC = 16, ROMS_LMD_NONLOCAL = 32, ROMS_LMD_DDMIX = 64
-  integer(c_int), parameter :: ROMS_GPU_ABI = 15   ! ROMS_GPU_ABI_VERSION, include/roms_gpu.h
+  integer(c_int), parameter :: ROMS_GPU_ABI = 16   ! ROMS_GPU_ABI_VERSION, include/roms_gpu.h
   integer(c_int), parameter :: ROMS_FRC_SURFACE = 1, ROMS_FRC_BRY = 2
 
   ! field ids (enum roms_field) used by the drivers below

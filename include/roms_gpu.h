@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define ROMS_GPU_ABI_VERSION 15
+#define ROMS_GPU_ABI_VERSION 16
 #define ROMS_MAX_FAST 288
 
 /* Subdomain geometry of this rank: param.F / dimensions.F / mpi_setup.F:39-210 */
@@ -293,6 +293,11 @@ int roms_gpu_halo_exchanges(long *per_step, int *fast_interval);
  * it on, =0 off), 0 if every exchange runs in place, as the reference's
  * exchange_xxx calls do (mpi_exchanges.F:672-800).                          */
 int roms_gpu_halo_overlap(void);
+/* 1 if the fused fast step addresses its 2-D fields through one buffer
+ * window (the fields allocated side by side within 2 GiB; the default),
+ * 0 if through their pointers (ROMS_GPU_S2D_WIN=0, or a subdomain whose
+ * 2-D fields span more).  Same results either way.                         */
+int roms_gpu_s2d_window(void);
 /* Self-test of the allocation path: `chunks` arrays of n doubles filled
  * with ones and freed, then allocated again through the library's
  * zero-filling allocator; on the library's stream each is read at once

@@ -322,6 +322,36 @@ def test_s2d_edges_folded_bitwise(monkeypatch):
             assert np.array_equal(out[0][n], out[1][n]), (LLm, MMm, n)
 
 
+@pytest.mark.parametrize("case", ["basin_fold", "basin_edges", "basin_nofold", "filament"])
+def test_s2d_window_bitwise(case, monkeypatch):
+    """k_s2d_fb addresses its 25 2-D fields through one buffer window (one
+    descriptor, a 32-bit offset per field; roms_gpu_s2d_window) or through
+    their pointers (ROMS_GPU_S2D_WIN=0): the same loads and stores, bitwise
+    equal runs -- closed walls folded in, the separate edge launches
+    (ROMS_GPU_S2D_EDGES=1, with the zeta_new/Dnew scratch stores), a grid the
+    host cannot fold, and the periodic Filament with its halo images
+    (step2d_FB.F:77-570)."""
+    if case == "filament":
+        cfg = oracle.filament_cfg(LLm=48, MMm=32, N=16, np_xi=1, np_eta=1)
+    else:
+        cfg = basin_cfg(LLm=63 if case == "basin_nofold" else 40, MMm=27 if case == "basin_nofold" else 26, N=12,
+                        nonlin=True)
+    monkeypatch.setenv("ROMS_GPU_S2D_EDGES", "1" if case == "basin_edges" else "0")
+    out = []
+    for env in ("1", "0"):
+        monkeypatch.setenv("ROMS_GPU_S2D_WIN", env)
+        m = romsgpu.Model.from_case(cfg.case_id, cfg.LLm, cfg.MMm, cfg.N, cfg.NT, salinity=bool(cfg.salinity),
+                                    nonlin_eos=bool(cfg.nonlin_eos), dt=cfg.dt, ndtfast=cfg.ndtfast,
+                                    sizex=cfg.sizex, sizey=cfg.sizey)
+        assert m.s2d_window() == (env == "1")
+        m.step(4)
+        out.append({n: m.get(n) for n in ("zeta", "ubar", "vbar", "u", "v", "t", "DU_avg1", "DV_avg1", "Zt_avg1",
+                                          "DU_avg2", "rufrc")})
+        m.close()
+    for n in out[0]:
+        assert np.array_equal(out[0][n], out[1][n]), (case, n)
+
+
 @pytest.mark.parametrize("case", ["basin", "filament"])
 def test_prsgrd_uv_fused_bitwise(case, monkeypatch):
     """Whole steps run the horizontal momentum r.h.s. of pre_step3d /

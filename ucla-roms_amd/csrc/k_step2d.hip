@@ -251,10 +251,46 @@ __device__ __forceinline__ void gst(double* p, double v) {
   else
     *p = v;
 }
-template <bool kPipe, int kClosed, bool kWrap, int kWT = 1>
+// kWin: the 2-D fields through the buffer window d.w2 (S2dWin, roms_dev.h),
+// else through the pointers of Fields; the same loads and stores either way.
+template <bool kPipe, int kClosed, bool kWrap, int kWT = 1, bool kWin = false>
 __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int vwrap, int part) {
   constexpr int closed = kClosed;
   const uint3 bI = xcd_tile();
+  const Fields& Fp = d.f;
+  auto fp = [&](int f) -> double* {
+    switch (f) {
+      case kW_zeta: return Fp.zeta; case kW_ubar: return Fp.ubar; case kW_vbar: return Fp.vbar; case kW_h: return Fp.h;
+      case kW_dn_u: return Fp.dn_u; case kW_dm_v: return Fp.dm_v; case kW_pm: return Fp.pm; case kW_pn: return Fp.pn;
+      case kW_swflx: return Fp.swflx; case kW_rmask: return Fp.rmask; case kW_rhoS: return Fp.rhoS;
+      case kW_rhoA: return Fp.rhoA; case kW_umask: return Fp.umask; case kW_vmask: return Fp.vmask;
+      case kW_rufrc: return Fp.rufrc; case kW_rvfrc: return Fp.rvfrc; case kW_DU_avg1: return Fp.DU_avg1;
+      case kW_DV_avg1: return Fp.DV_avg1; case kW_DU_avg2: return Fp.DU_avg2; case kW_DV_avg2: return Fp.DV_avg2;
+      case kW_Zt_avg1: return Fp.Zt_avg1; case kW_DU_avg_bak: return Fp.DU_avg_bak;
+      case kW_DV_avg_bak: return Fp.DV_avg_bak; case kW_s0: return Fp.s0; default: return Fp.s1;
+    }
+  };
+  // element idx (+ a uniform slot offset sl) of field f; in the window the
+  // lane's part is the VGPR offset, the field's origin and the slot the SGPR one
+  const __amdgpu_buffer_rsrc_t wrs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(d.w2.base), (short)0, 0x7fffffff, 0x00020000);
+  auto LD = [&](int f, long idx, long sl = 0) -> double {
+    if constexpr (kWin)
+      return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+                                            wrs, (int)((unsigned)(idx + sl + d.w2.lead) * 8u),
+                                            (int)d.w2.off[f], 0));
+    else
+      return fp(f)[idx + sl];
+  };
+  auto ST = [&](int f, long idx, double v, long sl = 0) {
+    if constexpr (kWin)   // cache policy of gst<kWT>: 16 = sc1 (write-through), 2 = nt
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) int, v), wrs,
+                                            (int)((unsigned)(idx + sl + d.w2.lead) * 8u),
+                                            (int)d.w2.off[f],
+                                            kWT == 1 ? 16 : (kWT == 2 ? 2 : 0));
+    else
+      gst<kWT>(&fp(f)[idx + sl], v);
+  };
   // part 1: interior tiles only (their windows hold no halo cell), 2: the rim
   // tiles, 0: all (see the fast-loop overlap in launch_step2d)
   if (part) {
@@ -293,10 +329,10 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int vw
     g_z0[r] = g_z1[r] = g_z2[r] = g_h[r] = 0.0;
     if (q < kGN && inarr(i, j)) {
       const long ij = IJ(b, i, j), ft = FT(i, j);
-      g_z0[r] = F.zeta[ft + (long)(c.kstp - 1) * n2];
-      g_z1[r] = F.zeta[ft + (long)(c.kbak - 1) * n2];
-      g_z2[r] = F.zeta[ft + (long)(c.kold - 1) * n2];
-      g_h[r] = F.h[ij];
+      g_z0[r] = LD(kW_zeta, ft, (long)(c.kstp - 1) * n2);
+      g_z1[r] = LD(kW_zeta, ft, (long)(c.kbak - 1) * n2);
+      g_z2[r] = LD(kW_zeta, ft, (long)(c.kold - 1) * n2);
+      g_h[r] = LD(kW_h, ij);
     }
   }
   double f_a[3], f_b[3], f_c[3], f_d[3];  // 3 time levels of ubar/vbar and dn_u/dm_v at the thread's faces
@@ -308,16 +344,16 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int vw
       const int i = i0 - 1 + q % kUX, j = j0 - 1 + q / kUX;
       if (i >= -b.gx && inarr(i, j)) {   // DUon needs Drhs(i-1)
         const long ij = IJ(b, i, j), ft = FT(i, j);
-        f_a[r] = F.ubar[ft + (long)(c.kstp - 1) * n2]; f_b[r] = F.ubar[ft + (long)(c.kbak - 1) * n2];
-        f_c[r] = F.ubar[ft + (long)(c.kold - 1) * n2]; f_d[r] = F.dn_u[ij];
+        f_a[r] = LD(kW_ubar, ft, (long)(c.kstp - 1) * n2); f_b[r] = LD(kW_ubar, ft, (long)(c.kbak - 1) * n2);
+        f_c[r] = LD(kW_ubar, ft, (long)(c.kold - 1) * n2); f_d[r] = LD(kW_dn_u, ij);
       }
     } else if (q < kUN + kVN) {
       const int qq = q - kUN;
       const int i = i0 - 1 + qq % kFX, j = j0 - 1 + qq / kFX;
       if (j >= -b.gx && inarr(i, j)) {   // DVom needs Drhs(j-1)
         const long ij = IJ(b, i, j), ft = FT(i, j);
-        f_a[r] = F.vbar[ft + (long)(c.kstp - 1) * n2]; f_b[r] = F.vbar[ft + (long)(c.kbak - 1) * n2];
-        f_c[r] = F.vbar[ft + (long)(c.kold - 1) * n2]; f_d[r] = F.dm_v[ij];
+        f_a[r] = LD(kW_vbar, ft, (long)(c.kstp - 1) * n2); f_b[r] = LD(kW_vbar, ft, (long)(c.kbak - 1) * n2);
+        f_c[r] = LD(kW_vbar, ft, (long)(c.kold - 1) * n2); f_d[r] = LD(kW_dm_v, ij);
       }
     }
   }
@@ -332,9 +368,9 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int vw
     e_pp[r] = false;
     if (q < kFN && i >= za && i <= zb && j >= zc && j <= zd) {
       const long ij = IJ(b, i, j);
-      e_pm[r] = F.pm[ij];
-      e_pn[r] = F.pn[ij];
-      e_sw[r] = F.swflx[ij]; e_rm[r] = F.rmask[ij]; e_rS[r] = F.rhoS[ij]; e_rA[r] = F.rhoA[ij];
+      e_pm[r] = LD(kW_pm, ij);
+      e_pn[r] = LD(kW_pn, ij);
+      e_sw[r] = LD(kW_swflx, ij); e_rm[r] = LD(kW_rmask, ij); e_rS[r] = LD(kW_rhoS, ij); e_rA[r] = LD(kW_rhoA, ij);
       if (kPipe) { e_pp[r] = F.pipe_idx[ij] > 0; e_pf[r] = F.pipe_flx[ij]; }
     }
   }
@@ -347,16 +383,16 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int vw
   double x_rS0 = 0, x_rSx = 0, x_rSy = 0, x_DU2 = 0, x_DV2 = 0, x_Zt = 0;
   if (pint) {
     const long lk = (long)(c.kstp - 1) * n2;
-    x_rA0 = F.rhoA[pij]; x_rAx = F.rhoA[pij - 1]; x_rAy = F.rhoA[pij - sj];
-    x_dnu = F.dn_u[pij]; x_dmv = F.dm_v[pij];
-    x_rufrc = F.rufrc[pij]; x_rvfrc = F.rvfrc[pij];
-    x_ub = F.ubar[pij + lk]; x_vb = F.vbar[pij + lk];
-    x_pm0 = F.pm[pij]; x_pn0 = F.pn[pij]; x_pmx = F.pm[pij - 1]; x_pnx = F.pn[pij - 1];
-    x_pmy = F.pm[pij - sj]; x_pny = F.pn[pij - sj];
-    x_um = F.umask[pij]; x_vm = F.vmask[pij];
-    x_DU1 = F.DU_avg1[pij]; x_DV1 = F.DV_avg1[pij];
-    x_DU2 = F.DU_avg2[pij]; x_DV2 = F.DV_avg2[pij]; x_Zt = F.Zt_avg1[pij];
-    if (c.iif == 1) { x_rS0 = F.rhoS[pij]; x_rSx = F.rhoS[pij - 1]; x_rSy = F.rhoS[pij - sj]; }
+    x_rA0 = LD(kW_rhoA, pij); x_rAx = LD(kW_rhoA, pij - 1); x_rAy = LD(kW_rhoA, pij - sj);
+    x_dnu = LD(kW_dn_u, pij); x_dmv = LD(kW_dm_v, pij);
+    x_rufrc = LD(kW_rufrc, pij); x_rvfrc = LD(kW_rvfrc, pij);
+    x_ub = LD(kW_ubar, pij, lk); x_vb = LD(kW_vbar, pij, lk);
+    x_pm0 = LD(kW_pm, pij); x_pn0 = LD(kW_pn, pij); x_pmx = LD(kW_pm, pij - 1); x_pnx = LD(kW_pn, pij - 1);
+    x_pmy = LD(kW_pm, pij - sj); x_pny = LD(kW_pn, pij - sj);
+    x_um = LD(kW_umask, pij); x_vm = LD(kW_vmask, pij);
+    x_DU1 = LD(kW_DU_avg1, pij); x_DV1 = LD(kW_DV_avg1, pij);
+    x_DU2 = LD(kW_DU_avg2, pij); x_DV2 = LD(kW_DV_avg2, pij); x_Zt = LD(kW_Zt_avg1, pij);
+    if (c.iif == 1) { x_rS0 = LD(kW_rhoS, pij); x_rSx = LD(kW_rhoS, pij - 1); x_rSy = LD(kW_rhoS, pij - sj); }
   }
   // P0: time levels of zeta, h and Drhs = h + fwd*z(kstp) + fwd1*z(kbak) + fwd2*z(kold)
 #pragma unroll
@@ -431,12 +467,12 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int vw
       const int i = i0 - 1 + q % kFX, j = j0 - 1 + q / kFX;
       const long ij = IJ(b, i, j);
       if (j >= b.jstrV - 1 && j <= b.jend) {
-        if (b.west_edge && i == b.istr - 1 && in(b.istr, j)) { T.zn[q] = T.zn[L(b.istr, j)] * F.rmask[ij]; T.st[q] = 2; }
-        if (b.east_edge && i == b.iend + 1 && in(b.iend, j)) { T.zn[q] = T.zn[L(b.iend, j)] * F.rmask[ij]; T.st[q] = 2; }
+        if (b.west_edge && i == b.istr - 1 && in(b.istr, j)) { T.zn[q] = T.zn[L(b.istr, j)] * LD(kW_rmask, ij); T.st[q] = 2; }
+        if (b.east_edge && i == b.iend + 1 && in(b.iend, j)) { T.zn[q] = T.zn[L(b.iend, j)] * LD(kW_rmask, ij); T.st[q] = 2; }
       }
       if (i >= b.istrU - 1 && i <= b.iend) {
-        if (b.south_edge && j == b.jstr - 1 && in(i, b.jstr)) { T.zn[q] = T.zn[L(i, b.jstr)] * F.rmask[ij]; T.st[q] = 2; }
-        if (b.north_edge && j == b.jend + 1 && in(i, b.jend)) { T.zn[q] = T.zn[L(i, b.jend)] * F.rmask[ij]; T.st[q] = 2; }
+        if (b.south_edge && j == b.jstr - 1 && in(i, b.jstr)) { T.zn[q] = T.zn[L(i, b.jstr)] * LD(kW_rmask, ij); T.st[q] = 2; }
+        if (b.north_edge && j == b.jend + 1 && in(i, b.jend)) { T.zn[q] = T.zn[L(i, b.jend)] * LD(kW_rmask, ij); T.st[q] = 2; }
       }
     }
     __syncthreads();
@@ -455,8 +491,8 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int vw
     for (int q = tid; q < kFN && closed == 1; q += NT) {
       if (!T.st[q]) continue;
       const long o = IJ(b, i0 - 1 + q % kFX, j0 - 1 + q / kFX);
-      gst<kWT>(&F.s0[o], T.zn[q]);
-      if (T.st[q] == 1) gst<kWT>(&F.s1[o], T.Dn[q]);
+      ST(kW_s0, o, T.zn[q]);
+      if (T.st[q] == 1) ST(kW_s1, o, T.Dn[q]);
     }
   }
   // P3: zeta(knew), fast averages, pressure gradient, momentum
@@ -469,20 +505,20 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int vw
   double ubn = 0.0, vbn = 0.0;   // ubar/vbar(knew) this lane formed (closed == 2)
   if (pin) {
     const double z = T.zn[q];
-    gst<kWT>(&F.zeta[ij + (long)(c.knew - 1) * n2], z);
+    ST(kW_zeta, ij, z, (long)(c.knew - 1) * n2);
     const double du = DU(i, j), dv = DV(i, j);
     if (c.iif == 1) {
-      gst<kWT>(&F.DU_avg_bak[ij], (pint ? x_DU1 : F.DU_avg1[ij]) - 0.1024390243902439 * (pint ? x_DU2 : F.DU_avg2[ij]));
-      gst<kWT>(&F.DV_avg_bak[ij], (pint ? x_DV1 : F.DV_avg1[ij]) - 0.1024390243902439 * (pint ? x_DV2 : F.DV_avg2[ij]));
-      gst<kWT>(&F.Zt_avg1[ij], c.w1 * z);
-      gst<kWT>(&F.DU_avg1[ij], 0.0);
-      gst<kWT>(&F.DV_avg1[ij], 0.0);
-      gst<kWT>(&F.DU_avg2[ij], c.w2 * du);
-      gst<kWT>(&F.DV_avg2[ij], c.w2 * dv);
+      ST(kW_DU_avg_bak, ij, (pint ? x_DU1 : LD(kW_DU_avg1, ij)) - 0.1024390243902439 * (pint ? x_DU2 : LD(kW_DU_avg2, ij)));
+      ST(kW_DV_avg_bak, ij, (pint ? x_DV1 : LD(kW_DV_avg1, ij)) - 0.1024390243902439 * (pint ? x_DV2 : LD(kW_DV_avg2, ij)));
+      ST(kW_Zt_avg1, ij, c.w1 * z);
+      ST(kW_DU_avg1, ij, 0.0);
+      ST(kW_DV_avg1, ij, 0.0);
+      ST(kW_DU_avg2, ij, c.w2 * du);
+      ST(kW_DV_avg2, ij, c.w2 * dv);
     } else {
-      gst<kWT>(&F.Zt_avg1[ij], (pint ? x_Zt : F.Zt_avg1[ij]) + c.w1 * z);
-      gst<kWT>(&F.DU_avg2[ij], (pint ? x_DU2 : F.DU_avg2[ij]) + c.w2 * du);
-      gst<kWT>(&F.DV_avg2[ij], (pint ? x_DV2 : F.DV_avg2[ij]) + c.w2 * dv);
+      ST(kW_Zt_avg1, ij, (pint ? x_Zt : LD(kW_Zt_avg1, ij)) + c.w1 * z);
+      ST(kW_DU_avg2, ij, (pint ? x_DU2 : LD(kW_DU_avg2, ij)) + c.w2 * du);
+      ST(kW_DV_avg2, ij, (pint ? x_DV2 : LD(kW_DV_avg2, ij)) + c.w2 * dv);
     }
   }
   if (pint) {
@@ -502,8 +538,8 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int vw
     if (c.iif == 1) {
       rufrc = rufrc - rubar;
       rvfrc = rvfrc - rvbar;
-      gst<kWT>(&F.rufrc[ij], rufrc);
-      gst<kWT>(&F.rvfrc[ij], rvfrc);
+      ST(kW_rufrc, ij, rufrc);
+      ST(kW_rvfrc, ij, rvfrc);
       auto corr = [&](int qq, int gg, double rS, double rA, double& zwrk, double& rzeta, double& rzeta2,
                       double& rzetaSA) {
         const double zn = T.zn[qq], zk = T.z0[gg];
@@ -529,15 +565,15 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int vw
       const double Dstpm = T.z0[g - 1] + hxm;
       const double DUnew = ((Dstp0 + Dstpm) * x_ub + cff * (x_pm0 + x_pmx) * (x_pn0 + x_pnx) * (rubar + rufrc)) * x_um;
       ubn = DUnew / (T.Dn[q] + T.Dn[q - 1]);
-      gst<kWT>(&F.ubar[ij + (long)(c.knew - 1) * n2], ubn);
-      gst<kWT>(&F.DU_avg1[ij], (c.iif == 1 ? 0.0 : x_DU1) + cff1 * dn_u * (DUnew));
+      ST(kW_ubar, ij, ubn, (long)(c.knew - 1) * n2);
+      ST(kW_DU_avg1, ij, (c.iif == 1 ? 0.0 : x_DU1) + cff1 * dn_u * (DUnew));
     }
     if (j >= b.jstrV) {
       const double Dstpm = T.z0[g - kGX] + hym;
       const double DVnew = ((Dstp0 + Dstpm) * x_vb + cff * (x_pm0 + x_pmy) * (x_pn0 + x_pny) * (rvbar + rvfrc)) * x_vm;
       vbn = DVnew / (T.Dn[q] + T.Dn[q - kFX]);
-      gst<kWT>(&F.vbar[ij + (long)(c.knew - 1) * n2], vbn);
-      gst<kWT>(&F.DV_avg1[ij], (c.iif == 1 ? 0.0 : x_DV1) + cff1 * dm_v * (DVnew));
+      ST(kW_vbar, ij, vbn, (long)(c.knew - 1) * n2);
+      ST(kW_DV_avg1, ij, (c.iif == 1 ? 0.0 : x_DV1) + cff1 * dm_v * (DVnew));
     }
   }
   if (closed != 2) return;
@@ -553,11 +589,11 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int vw
     // phase 0: wall-normal components (u2dbc_im.F / v2dbc_im.F closed walls)
     if (pin && j >= js && j <= je && ((b.west_edge && i == is) || (b.east_edge && i == ie + 1))) {
       ubn = 0.0;
-      gst<kWT>(&F.ubar[ij + kn], ubn);
+      ST(kW_ubar, ij, ubn, kn);
     }
     if (pin && i >= is && i <= ie && ((b.south_edge && j == js) || (b.north_edge && j == je + 1))) {
       vbn = 0.0;
-      gst<kWT>(&F.vbar[ij + kn], vbn);
+      ST(kW_vbar, ij, vbn, kn);
     }
     sU[t] = ubn;
     sV[t] = vbn;
@@ -568,21 +604,21 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int vw
     {
       const int i0t = b.ew_periodic ? b.istrU : is, i1t = b.ew_periodic ? ie : b.iendR;
       if (b.south_edge && j == js - 1 && i >= i0t && i <= i1t) {
-        ubn = g2 * sU[t + kBX] * F.umask[ij];
-        gst<kWT>(&F.ubar[ij + kn], ubn);
+        ubn = g2 * sU[t + kBX] * LD(kW_umask, ij);
+        ST(kW_ubar, ij, ubn, kn);
       }
       if (b.north_edge && j == je + 1 && i >= i0t && i <= i1t) {
-        ubn = g2 * sU[t - kBX] * F.umask[ij];
-        gst<kWT>(&F.ubar[ij + kn], ubn);
+        ubn = g2 * sU[t - kBX] * LD(kW_umask, ij);
+        ST(kW_ubar, ij, ubn, kn);
       }
       const int j0t = b.ns_periodic ? b.jstrV : js, j1t = b.ns_periodic ? je : b.jendR;
       if (b.west_edge && i == is - 1 && j >= j0t && j <= j1t) {
-        vbn = g2 * sV[t + 1] * F.vmask[ij];
-        gst<kWT>(&F.vbar[ij + kn], vbn);
+        vbn = g2 * sV[t + 1] * LD(kW_vmask, ij);
+        ST(kW_vbar, ij, vbn, kn);
       }
       if (b.east_edge && i == ie + 1 && j >= j0t && j <= j1t) {
-        vbn = g2 * sV[t - 1] * F.vmask[ij];
-        gst<kWT>(&F.vbar[ij + kn], vbn);
+        vbn = g2 * sV[t - 1] * LD(kW_vmask, ij);
+        ST(kW_vbar, ij, vbn, kn);
       }
     }
     // phase 3: fast-time-averaged fluxes through the boundary faces; Dnew of
@@ -599,8 +635,8 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int vw
     if (b.east_edge && i == ie + 1 && j >= b.jstrV && j <= je) dv = true;
     if (b.south_edge && j == b.jstrV - 1 && i >= b.istrR && i <= b.iendR) dv = true;
     if (b.north_edge && j == je + 1 && i >= b.istrR && i <= b.iendR) dv = true;
-    if (du) gst<kWT>(&F.DU_avg1[ij], F.DU_avg1[ij] + cff1 * (Dn(q, g) + Dn(q - 1, g - 1)) * (ubn) * F.dn_u[ij]);
-    if (dv) gst<kWT>(&F.DV_avg1[ij], F.DV_avg1[ij] + cff1 * (Dn(q, g) + Dn(q - kFX, g - kGX)) * (vbn) * F.dm_v[ij]);
+    if (du) ST(kW_DU_avg1, ij, LD(kW_DU_avg1, ij) + cff1 * (Dn(q, g) + Dn(q - 1, g - 1)) * (ubn) * LD(kW_dn_u, ij));
+    if (dv) ST(kW_DV_avg1, ij, LD(kW_DV_avg1, ij) + cff1 * (Dn(q, g) + Dn(q - kFX, g - kGX)) * (vbn) * LD(kW_dm_v, ij));
     (void)sj;
   }
 }
@@ -978,6 +1014,12 @@ void launch_fast_step(const Dev& d, hipStream_t s, const FBCoef& c, const Tlev& 
     auto fb = [&](int part) {
       const dim3 gr = grid_of(RB), bl(kBX, kBY);
 #define S2D_FB(P, C, W) hipLaunchKernelGGL((k_s2d_fb<P, C, W>), gr, bl, 0, s, d, RB, c, vwrap, part)
+      // the window form when roms_gpu_init set one up (ROMS_GPU_S2D_WIN=0: pointers)
+#define S2D_FBW(C, W)                                                                                  \
+  do {                                                                                                 \
+    if (d.w2.base) hipLaunchKernelGGL((k_s2d_fb<false, C, W, 1, true>), gr, bl, 0, s, d, RB, c, vwrap, part); \
+    else S2D_FB(false, C, W);                                                                          \
+  } while (0)
       const bool wr = vwrap != 0;
       if (d.p.npip > 0) {
         if (cmode == 0) { if (wr) S2D_FB(true, 0, true); else S2D_FB(true, 0, false); }
@@ -990,10 +1032,11 @@ void launch_fast_step(const Dev& d, hipStream_t s, const FBCoef& c, const Tlev& 
         else if (cmode == 0 && wr && wt == 2) hipLaunchKernelGGL((k_s2d_fb<false, 0, true, 2>), gr, bl, 0, s, d, RB, c, vwrap, part);
         else if (cmode == 2 && !wr && wt == 0) hipLaunchKernelGGL((k_s2d_fb<false, 2, false, 0>), gr, bl, 0, s, d, RB, c, vwrap, part);
         else if (cmode == 2 && !wr && wt == 2) hipLaunchKernelGGL((k_s2d_fb<false, 2, false, 2>), gr, bl, 0, s, d, RB, c, vwrap, part);
-        else if (cmode == 0) { if (wr) S2D_FB(false, 0, true); else S2D_FB(false, 0, false); }
-        else if (cmode == 1) { if (wr) S2D_FB(false, 1, true); else S2D_FB(false, 1, false); }
-        else { if (wr) S2D_FB(false, 2, true); else S2D_FB(false, 2, false); }
+        else if (cmode == 0) { if (wr) S2D_FBW(0, true); else S2D_FBW(0, false); }
+        else if (cmode == 1) { if (wr) S2D_FBW(1, true); else S2D_FBW(1, false); }
+        else { if (wr) S2D_FBW(2, true); else S2D_FBW(2, false); }
       }
+#undef S2D_FBW
 #undef S2D_FB
     };
     // kernel-level timing: one interval per fast loop when nothing else runs

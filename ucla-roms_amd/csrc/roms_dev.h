@@ -153,12 +153,30 @@ struct Fields {
   double *iso_dTdz, *iso_FSC, *iso_dTdx, *iso_dTde, *iso_LapT;
 };
 
+// The fast step's 2-D fields addressed from one buffer window (k_s2d_fb):
+// one descriptor plus a 32-bit byte offset per field in place of a 64-bit
+// base each -- the fused fast step reads and writes 25 of them, and their
+// bases alone held more scalar registers than the kernel has.  roms_gpu_init
+// allocates these fields next to each other and fills the window when they
+// span less than 2 GiB (base = nullptr: the pointer form).
+enum S2dWinField : int {
+  kW_zeta, kW_ubar, kW_vbar, kW_h, kW_dn_u, kW_dm_v, kW_pm, kW_pn, kW_swflx, kW_rmask, kW_rhoS, kW_rhoA, kW_umask,
+  kW_vmask, kW_rufrc, kW_rvfrc, kW_DU_avg1, kW_DV_avg1, kW_DU_avg2, kW_DV_avg2, kW_Zt_avg1, kW_DU_avg_bak,
+  kW_DV_avg_bak, kW_s0, kW_s1, kWinN
+};
+struct S2dWin {
+  const double* base;   // nullptr: no window
+  int lead;             // element (i,j) of a field sits (IJ + lead) doubles past its window origin
+  unsigned off[kWinN];  // byte offset of each field's origin (its element IJ = -lead) from base
+};
+
 struct Halo;  // halo.h: multi-rank exchange state (host object; nullptr = single rank)
 struct Dev {
   Bounds b;
   Params p;
   Fields f;
   const Halo* halo;
+  S2dWin w2;
 };
 
 // ---- index helpers (device + host) ----

@@ -1060,7 +1060,9 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     g.guard = e && e[0] == '1';
   }
   const Bounds& b = g.d.b;
-  for (int id = 0; id < ROMS_NFIELDS; id++) {
+  // the 2-D fields first and next to each other (then the 2-D scratch), so
+  // that the fast step's fields share one buffer window (S2dWin below)
+  auto field = [&](int id) -> int {
     const long n = field_count(id, b);
     double* p = nullptr;
     CHECK_HIP(dev_alloc(p, n));
@@ -1069,19 +1071,48 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     g.f[id].hcount = field_count(id, g.hb);
     g.f[id].planar = planar_field(id);
     *field_slot(g.d.f, id) = p;
-  }
+    return 0;
+  };
+  auto planar2d = [&](int id) { return planar_field(id) && field_count(id, b) <= 4 * b.n2; };
+  for (int id = 0; id < ROMS_NFIELDS; id++)
+    if (planar2d(id) && field(id)) return -2;
   auto scratch = [&](double*& p, long n) -> int {
     CHECK_HIP(dev_alloc(p, n));
     g.scratch.push_back(p);
     return 0;
   };
   Fields& F = g.d.f;
-  if (scratch(F.P, b.n3) || scratch(F.rhos, b.n3) || scratch(F.c0, b.n3w) || scratch(F.c1, b.n3w) ||
-      scratch(F.c2, b.n3w) || scratch(F.c3, b.n3w))
-    return -2;
   double** s2[] = {&F.s0, &F.s1, &F.s2, &F.s3, &F.s4, &F.s5, &F.s6, &F.s7, &F.s8, &F.s9};
   for (double** q : s2)
     if (scratch(*q, b.n2)) return -2;
+  for (int id = 0; id < ROMS_NFIELDS; id++)
+    if (!planar2d(id) && field(id)) return -2;
+  if (scratch(F.P, b.n3) || scratch(F.rhos, b.n3) || scratch(F.c0, b.n3w) || scratch(F.c1, b.n3w) ||
+      scratch(F.c2, b.n3w) || scratch(F.c3, b.n3w))
+    return -2;
+  {
+    // the fast step's buffer window (k_s2d_fb): every field's origin IJ = -lead
+    // and its last element within 2 GiB of one base; else (or with
+    // ROMS_GPU_S2D_WIN=0) the kernel addresses them through their pointers
+    const char* e = getenv("ROMS_GPU_S2D_WIN");
+    g.d.w2 = S2dWin{};
+    const double* wp[kWinN] = {F.zeta,  F.ubar,  F.vbar,    F.h,       F.dn_u,    F.dm_v,       F.pm,
+                               F.pn,    F.swflx, F.rmask,   F.rhoS,    F.rhoA,    F.umask,      F.vmask,
+                               F.rufrc, F.rvfrc, F.DU_avg1, F.DV_avg1, F.DU_avg2, F.DV_avg2,    F.Zt_avg1,
+                               F.DU_avg_bak, F.DV_avg_bak, F.s0, F.s1};
+    const long lead = (long)b.gx * b.nx2 + b.gx + kRowAlign;   // below the lowest IJ the kernel forms
+    uintptr_t lo = UINTPTR_MAX, hi = 0;
+    for (int f = 0; f < kWinN; f++) {
+      const long cnt = f <= kW_vbar ? 4 * b.n2 : b.n2;
+      lo = std::min(lo, (uintptr_t)wp[f] - (uintptr_t)lead * 8u);
+      hi = std::max(hi, (uintptr_t)wp[f] + (uintptr_t)cnt * 8u);
+    }
+    if (!(e && e[0] == '0') && hi - lo < (uintptr_t)2147483648u - (1u << 20)) {
+      g.d.w2.base = (const double*)lo;
+      g.d.w2.lead = (int)lead;
+      for (int f = 0; f < kWinN; f++) g.d.w2.off[f] = (unsigned)((uintptr_t)wp[f] - (uintptr_t)lead * 8u - lo);
+    }
+  }
   if (col_global && scratch(F.colscr, 2L * (b.NT > 2 ? b.NT : 2) * b.n3w)) return -2;
   if (P.iso) {   // ADV_ISONEUTRAL fields (k_iso.hip), zero like the reference's allocations (eos_vars.F:50-52)
     double** r3[] = {&F.dRdx, &F.dRde, &F.diff3u, &F.diff3v, &F.iso_dTdx, &F.iso_dTde, &F.iso_LapT};
@@ -1245,6 +1276,11 @@ int roms_gpu_halo_transport(void) {
 int roms_gpu_halo_overlap(void) {
   REQUIRE_INIT_NOJOIN();
   return g.d.halo && g.halo.xoverlap > 0 ? 1 : 0;
+}
+
+int roms_gpu_s2d_window(void) {
+  REQUIRE_INIT_NOJOIN();
+  return g.d.w2.base ? 1 : 0;
 }
 
 int roms_gpu_halo_exchanges(long* per_step, int* fast_interval) {

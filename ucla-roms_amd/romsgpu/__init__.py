@@ -539,6 +539,11 @@ class Model:
         (roms_gpu_halo_overlap: the default with > 1 rank, one GPU each)."""
         return bool(self.L.roms_gpu_halo_overlap())
 
+    def s2d_window(self):
+        """True when the fused fast step reads its 2-D fields through one
+        buffer window (roms_gpu_s2d_window; ROMS_GPU_S2D_WIN=0: pointers)."""
+        return bool(self.L.roms_gpu_s2d_window())
+
     def halo_exchanges(self):
         """(exchanges in the last enqueued step, fast-loop exchange interval)
         -- roms_gpu_halo_exchanges."""
