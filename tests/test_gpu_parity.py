@@ -322,7 +322,7 @@ def test_s2d_edges_folded_bitwise(monkeypatch):
             assert np.array_equal(out[0][n], out[1][n]), (LLm, MMm, n)
 
 
-@pytest.mark.parametrize("case", ["basin_fold", "basin_edges", "basin_nofold", "filament"])
+@pytest.mark.parametrize("case", ["basin_fold", "basin_edges", "basin_nofold", "filament", "mask_edit"])
 def test_s2d_window_bitwise(case, monkeypatch):
     """k_s2d_fb addresses its 25 2-D fields through one buffer window (one
     descriptor, a 32-bit offset per field; roms_gpu_s2d_window) or through
@@ -330,7 +330,8 @@ def test_s2d_window_bitwise(case, monkeypatch):
     equal runs -- closed walls folded in, the separate edge launches
     (ROMS_GPU_S2D_EDGES=1, with the zeta_new/Dnew scratch stores), a grid the
     host cannot fold, and the periodic Filament with its halo images
-    (step2d_FB.F:77-570)."""
+    (step2d_FB.F:77-570); mask_edit writes land cells and non-binary mask
+    values between steps, which both forms must apply identically."""
     if case == "filament":
         cfg = oracle.filament_cfg(LLm=48, MMm=32, N=16, np_xi=1, np_eta=1)
     else:
@@ -345,6 +346,18 @@ def test_s2d_window_bitwise(case, monkeypatch):
                                     sizex=cfg.sizex, sizey=cfg.sizey)
         assert m.s2d_window() == (env == "1")
         m.step(4)
+        if case == "mask_edit":
+            rm, um, vm = m.get("rmask"), m.get("umask"), m.get("vmask")
+            rm[0, 10:14, 12:15] = 0.0
+            um[0, 10:14, 12:16] = 0.0
+            vm[0, 10:15, 12:15] = 0.0
+            rm[0, 20, 30] = 0.5
+            um[0, 21, 31] = 0.75
+            vm[0, 22, 32] = 0.25
+            m.put("rmask", rm)
+            m.put("umask", um)
+            m.put("vmask", vm)
+            m.step(3)
         out.append({n: m.get(n) for n in ("zeta", "ubar", "vbar", "u", "v", "t", "DU_avg1", "DV_avg1", "Zt_avg1",
                                           "DU_avg2", "rufrc")})
         m.close()
