@@ -262,6 +262,7 @@ def run_workload(kind, romsgpu, comm, rank, world, local_rank, steps, warmup, ti
     barrier()
     elapsed = allmax(max(wall, ev_ms / 1e3))
     overlap = m.halo_overlap() if comm is not None else False
+    s2d_window = m.s2d_window()
     if step_only:   # the whole-step time alone (the exchange-overlap A/B of a multi-rank run)
         m.close()
         return {"ms_per_step": 1e3 * elapsed / steps, "value": total_cells * steps / elapsed,
@@ -389,7 +390,8 @@ def run_workload(kind, romsgpu, comm, rank, world, local_rank, steps, warmup, ti
                    "halo_exchanges_per_step": exch, "fast_exchange_interval": fast_k,
                    "exchange_order": ("deferred (3-D exchanges beside the next routine)" if overlap else
                                       "in place" if comm is not None else "none (single rank)"),
-                   "halo_time_per_rank": halo_time},
+                   "halo_time_per_rank": halo_time,
+                   "s2d_window": s2d_window},
         "scaling": "strong" if c3 else "weak",
         "steps": steps, "warmup": warmup,
         "roofline": roofline,

@@ -77,7 +77,11 @@ struct Ctx {
   // NaN-filled guard bands before and after it, so an out-of-bounds read
   // turns into NaN instead of a value of whatever array lies next to it
   bool guard = false;
-  std::map<double*, double*> guard_base;
+  std::map<double*, double*> guard_base;   // array -> its allocation (nullptr: inside the 2-D arena)
+  // The 2-D fields and 2-D scratch come from one allocation (roms_gpu_init),
+  // so the fast step's fields always share one buffer window (S2dWin)
+  double* arena = nullptr;
+  long arena_n = 0, arena_used = 0;   // doubles
   double* small = nullptr;   // shim_scratch_small
   long small_n = 0;
   // Device row pitch (roms_dev.h): rows of nx2 = Lm+4 rounded up to 16
@@ -283,7 +287,16 @@ double* dev_base(double* p) {
   auto it = g.guard_base.find(p);
   return it == g.guard_base.end() ? p : it->second;
 }
-// zero-initialised device array of n doubles (guard bands when g.guard)
+// doubles one dev_alloc of n takes (guard bands, alignment lead, wide-halo
+// rows), rounded up to 256 B so that arena slices keep hipMalloc's alignment
+long dev_alloc_size(long n) {
+  const Bounds& b = g.d.b;
+  const long G = g.guard ? 4096 : 0;
+  const long pad = (g.off || b.gx) ? kRowAlign : 0;
+  return (n + 2 * G + pad + (long)b.gx * b.nx2 + 31) / 32 * 32;
+}
+// zero-initialised device array of n doubles (guard bands when g.guard),
+// sliced from g.arena while it has room, else its own hipMalloc
 hipError_t dev_alloc(double*& p, long n) {
   const long G = g.guard ? 4096 : 0;
   const Bounds& b = g.d.b;
@@ -294,14 +307,23 @@ hipError_t dev_alloc(double*& p, long n) {
   const long pre = (long)b.gx * b.nx2 + lead;
   const long pad = (g.off || b.gx) ? kRowAlign : 0;
   double* base = nullptr;
-  hipError_t e = hipMalloc(&base, (size_t)(n + 2 * G + pad + (long)b.gx * b.nx2) * sizeof(double));
+  const long sz = dev_alloc_size(n);
+  const bool sliced = g.arena && g.arena_used + sz <= g.arena_n;
+  hipError_t e = hipSuccess;
+  if (sliced) {
+    base = g.arena + g.arena_used;
+    g.arena_used += sz;
+  } else {
+    e = hipMalloc(&base, (size_t)(n + 2 * G + pad + (long)b.gx * b.nx2) * sizeof(double));
+  }
   if (e != hipSuccess) return e;
   if (G) {
     e = hipMemsetD32((hipDeviceptr_t)base, 0x7FF87FF8, (size_t)(n + 2 * G + pad + (long)b.gx * b.nx2) * 2);   // NaN bit pattern
     if (e != hipSuccess) return e;
   }
   p = base + G + pre;
-  if (G || pre) g.guard_base[p] = base;
+  if (sliced) g.guard_base[p] = nullptr;   // freed with the arena (hipFree(nullptr) is a no-op)
+  else if (G || pre) g.guard_base[p] = base;
   // The library's kernels run on a non-blocking stream, which does not wait
   // for work on the null stream: the zero fill must have landed before the
   // first kernel reads the array, or it may see what a previous model left in
@@ -327,6 +349,7 @@ void free_all() {
     if (g.f[id].d) { (void)hipFree(dev_base(g.f[id].d)); g.f[id] = FieldDesc{}; }
   for (double* p : g.scratch) (void)hipFree(dev_base(p));
   g.guard_base.clear();
+  if (g.arena) { (void)hipFree(g.arena); g.arena = nullptr; g.arena_n = g.arena_used = 0; }
   g.scratch.clear();
   if (g.d.f.pipe_idx) { (void)hipFree(g.d.f.pipe_idx); g.d.f.pipe_idx = nullptr; }
   if (g.d.f.riv_face) { (void)hipFree(g.d.f.riv_face); g.d.f.riv_face = nullptr; }
@@ -1074,6 +1097,18 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
     return 0;
   };
   auto planar2d = [&](int id) { return planar_field(id) && field_count(id, b) <= 4 * b.n2; };
+  {
+    // one allocation for them (dev_alloc slices it); a subdomain whose 2-D
+    // set passes 2 GiB allocates them one by one (and runs the pointer form)
+    long n = 10 * dev_alloc_size(b.n2);   // s0..s9
+    for (int id = 0; id < ROMS_NFIELDS; id++)
+      if (planar2d(id)) n += dev_alloc_size(field_count(id, b));
+    if (n * 8 < 2147483648L - (1L << 20)) {
+      CHECK_HIP(hipMalloc(&g.arena, (size_t)n * sizeof(double)));
+      g.arena_n = n;
+      g.arena_used = 0;
+    }
+  }
   for (int id = 0; id < ROMS_NFIELDS; id++)
     if (planar2d(id) && field(id)) return -2;
   auto scratch = [&](double*& p, long n) -> int {
@@ -1085,6 +1120,7 @@ int roms_gpu_init(const roms_dims* dims, const roms_cfg* cfg, int device, void* 
   double** s2[] = {&F.s0, &F.s1, &F.s2, &F.s3, &F.s4, &F.s5, &F.s6, &F.s7, &F.s8, &F.s9};
   for (double** q : s2)
     if (scratch(*q, b.n2)) return -2;
+  g.arena_n = g.arena_used;   // nothing else is sliced from it
   for (int id = 0; id < ROMS_NFIELDS; id++)
     if (!planar2d(id) && field(id)) return -2;
   if (scratch(F.P, b.n3) || scratch(F.rhos, b.n3) || scratch(F.c0, b.n3w) || scratch(F.c1, b.n3w) ||
