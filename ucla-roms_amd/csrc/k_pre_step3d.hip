@@ -771,7 +771,7 @@ __global__ void __launch_bounds__(kSegBlock, 2) k_pre_tracer_seg(Dev d, Range R,
 // entry with the spline inputs.  Same expressions and order: bitwise equal
 // to k_pre_tracer_seg. ----
 template <bool PF, bool UNI = true>
-__global__ void __launch_bounds__(kSegBlock, ROMS_SEG_BUF_WAVES) k_pre_tracer_segb(Dev d, Range R, PreCoef c, int nnew,
+__global__ void __launch_bounds__(kSegBlock, ROMS_PRE_T_SEG_WAVES) k_pre_tracer_segb(Dev d, Range R, PreCoef c, int nnew,
                                                                                    int nrhs) {
   const uint3 bI = seg_tile(d.p.seg_order, d.p.seg_xg);
   __shared__ SegXchg X;

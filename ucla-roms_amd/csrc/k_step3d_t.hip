@@ -381,7 +381,7 @@ __global__ void __launch_bounds__(kSegBlock, 2) k_step3d_t_seg(Dev d, Range R, i
 // reloaded for the diffusion phase instead of kept live across the spline
 // solve (30 VGPRs at its register peak).
 template <bool PF, bool RL = false, bool UNI = true>
-__global__ void __launch_bounds__(kSegBlock, ROMS_SEG_BUF_WAVES) k_step3d_t_segb(Dev d, Range R, int nnew, int nrhs) {
+__global__ void __launch_bounds__(kSegBlock, ROMS_T_SEG_WAVES) k_step3d_t_segb(Dev d, Range R, int nnew, int nrhs) {
   const uint3 bI = seg_tile(d.p.seg_order, d.p.seg_xg);
   __shared__ SegXchg X;
   constexpr int KR = kSegRows + 1;

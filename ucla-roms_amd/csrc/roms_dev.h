@@ -326,6 +326,12 @@ constexpr int kSegNMin = ROMS_SEG_NMIN;
 #ifndef ROMS_SEG_BUF_WAVES
 #define ROMS_SEG_BUF_WAVES 2
 #endif
+#ifndef ROMS_PRE_T_SEG_WAVES   // k_pre_tracer_segb alone (A/B builds)
+#define ROMS_PRE_T_SEG_WAVES ROMS_SEG_BUF_WAVES
+#endif
+#ifndef ROMS_T_SEG_WAVES       // k_step3d_t_segb alone (A/B builds)
+#define ROMS_T_SEG_WAVES ROMS_SEG_BUF_WAVES
+#endif
 // segments of an N-level column (one per wavefront at kSegCW = 64, seg_waves)
 // and whether each of them gets at least kSegNMin rows
 inline int seg_count(int N) {
