@@ -4,7 +4,7 @@ each run as a single-rank closed basin on one GPU: no exchange, so the
 figures bound what N GPUs can reach from kernel efficiency alone.  Prints one
 JSON line per size: ms per step (graph replay), the routine times, and the
 compute-only efficiency t(1024^2) / (N x t(size)).
-usage: python tools/subdomain_probe.py [STEPS]"""
+usage: python tools/subdomain_probe.py [STEPS [NGPU]] (NGPU: that size only)"""
 import json
 import os
 import sys
@@ -15,6 +15,8 @@ import romsgpu  # noqa: E402
 STEPS = int(sys.argv[1]) if len(sys.argv) > 1 else 6
 N, DT, DX, NDTFAST, NT = 100, 300.0, 2.0e3, 60, 2
 sizes = [(1024, 1024, 1), (512, 1024, 2), (512, 512, 4), (256, 512, 8)]
+if len(sys.argv) > 2:
+    sizes = [z for z in sizes if z[2] == int(sys.argv[2])]
 t1 = None
 for L, M, ngpu in sizes:
     m = romsgpu.Model.from_case(romsgpu.CASE_BASIN, L, M, N, NT, salinity=True, nonlin_eos=True,

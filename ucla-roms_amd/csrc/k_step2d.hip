@@ -251,12 +251,23 @@ __device__ __forceinline__ void gst(double* p, double v) {
   else
     *p = v;
 }
+#ifdef ROMS_S2D_PROBE
+// Timing probe (A/B builds only, tools/s2d_phase_probe.py): thread 0 of each
+// block stores the shader clock at the phase boundaries into
+// ptide[block*8 + phase] (ptide is unused without TIDES)
+#define S2D_T(ph) do { if (threadIdx.x == 0 && threadIdx.y == 0) { \
+    const unsigned long long t_ = __builtin_readcyclecounter(); \
+    d.f.ptide[(long)(blockIdx.x + gridDim.x * blockIdx.y) * 8 + (ph)] = (double)t_; } } while (0)
+#else
+#define S2D_T(ph) do { } while (0)
+#endif
 // kWin: the 2-D fields through the buffer window d.w2 (S2dWin, roms_dev.h),
 // else through the pointers of Fields; the same loads and stores either way.
 template <bool kPipe, int kClosed, bool kWrap, int kWT = 1, bool kWin = false>
 __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int vwrap, int part) {
   constexpr int closed = kClosed;
   const uint3 bI = xcd_tile();
+  S2D_T(0);
   const Fields& Fp = d.f;
   auto fp = [&](int f) -> double* {
     switch (f) {
@@ -370,9 +381,14 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int vw
       const long ij = IJ(b, i, j);
       e_pm[r] = LD(kW_pm, ij);
       e_pn[r] = LD(kW_pn, ij);
-      e_sw[r] = LD(kW_swflx, ij); e_rm[r] = LD(kW_rmask, ij); e_rS[r] = LD(kW_rhoS, ij); e_rA[r] = LD(kW_rhoA, ij);
+      e_sw[r] = LD(kW_swflx, ij); e_rS[r] = LD(kW_rhoS, ij); e_rA[r] = LD(kW_rhoA, ij);
       if (kPipe) { e_pp[r] = F.pipe_idx[ij] > 0; e_pf[r] = F.pipe_flx[ij]; }
     }
+    // rmask of every window cell: the zeta range's, and the closed-wall
+    // ghost cells' that zetabc multiplies by below (loaded with the rest, so
+    // zetabc issues no load and waits for no memory round trip of its own)
+    if (closed != 0 ? (q < kFN && inarr(i, j)) : (q < kFN && i >= za && i <= zb && j >= zc && j <= zd))
+      e_rm[r] = LD(kW_rmask, IJ(b, i, j));
   }
   const int pi = i0 + (int)threadIdx.x, pj = j0 + (int)threadIdx.y;
   const bool pact = pi >= R.i0 && pi <= R.i1 && pj <= R.j1;
@@ -394,6 +410,7 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int vw
     x_DU2 = LD(kW_DU_avg2, pij); x_DV2 = LD(kW_DV_avg2, pij); x_Zt = LD(kW_Zt_avg1, pij);
     if (c.iif == 1) { x_rS0 = LD(kW_rhoS, pij); x_rSx = LD(kW_rhoS, pij - 1); x_rSy = LD(kW_rhoS, pij - sj); }
   }
+  S2D_T(1);   // entry loads issued
   // P0: time levels of zeta, h and Drhs = h + fwd*z(kstp) + fwd1*z(kbak) + fwd2*z(kold)
 #pragma unroll
   for (int r = 0; r < 2; r++) {
@@ -403,6 +420,7 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int vw
     T.Dr[q] = g_h[r] + c.fwd * g_z0[r] + c.fwd1 * g_z1[r] + c.fwd2 * g_z2[r];
   }
   __syncthreads();
+  S2D_T(2);   // window in LDS
   // P1: barotropic fluxes DUon (u faces) and DVom (v faces), once each
 #pragma unroll
   for (int r = 0; r < 3; r++) {
@@ -429,6 +447,7 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int vw
   __syncthreads();
   auto DU = [&](int i, int j) { return T.DU[(i - (i0 - 1)) + (j - (j0 - 1)) * kUX]; };
   auto DV = [&](int i, int j) { return T.DV[(i - (i0 - 1)) + (j - (j0 - 1)) * kFX]; };
+  S2D_T(3);   // DU/DV
   // P2: free surface and the backward-averaged terms of the reference's
   // zeta range (istrU-1..iend, jstrV-1..jend) inside the window
 #pragma unroll
@@ -459,20 +478,30 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int vw
     T.rz2[q] = rzeta * zwrk;
   }
   __syncthreads();
-  if (closed != 0) {
+  S2D_T(4);   // zeta part
+  // blocks whose window (i0-1..i0+63, j0-1..j0+3) reaches a closed wall's
+  // ghost line: only they have zetabc cells (block-uniform, so the others
+  // skip its two barriers)
+  const bool wall_win = (b.west_edge && b.istr - 1 >= i0 - 1 && b.istr - 1 <= i0 + kBX - 1) ||
+                        (b.east_edge && b.iend + 1 >= i0 - 1 && b.iend + 1 <= i0 + kBX - 1) ||
+                        (b.south_edge && b.jstr - 1 >= j0 - 1 && b.jstr - 1 <= j0 + kBY - 1) ||
+                        (b.north_edge && b.jend + 1 >= j0 - 1 && b.jend + 1 <= j0 + kBY - 1);
+  if (closed != 0 && wall_win) {
     // zetabc_tile (zetabc.F), closed walls: edges, then corners
     auto L = [&](int i, int j) { return (i - (i0 - 1)) + (j - (j0 - 1)) * kFX; };
     auto in = [&](int i, int j) { return i >= i0 - 1 && i <= i0 + kBX - 1 && j >= j0 - 1 && j <= j0 + kBY - 1; };
-    for (int q = tid; q < kFN; q += NT) {
+#pragma unroll
+    for (int r = 0; r < 2; r++) {   // window cell q = tid + r*NT: its rmask is e_rm[r]
+      const int q = tid + r * NT;
+      if (q >= kFN) break;
       const int i = i0 - 1 + q % kFX, j = j0 - 1 + q / kFX;
-      const long ij = IJ(b, i, j);
       if (j >= b.jstrV - 1 && j <= b.jend) {
-        if (b.west_edge && i == b.istr - 1 && in(b.istr, j)) { T.zn[q] = T.zn[L(b.istr, j)] * LD(kW_rmask, ij); T.st[q] = 2; }
-        if (b.east_edge && i == b.iend + 1 && in(b.iend, j)) { T.zn[q] = T.zn[L(b.iend, j)] * LD(kW_rmask, ij); T.st[q] = 2; }
+        if (b.west_edge && i == b.istr - 1 && in(b.istr, j)) { T.zn[q] = T.zn[L(b.istr, j)] * e_rm[r]; T.st[q] = 2; }
+        if (b.east_edge && i == b.iend + 1 && in(b.iend, j)) { T.zn[q] = T.zn[L(b.iend, j)] * e_rm[r]; T.st[q] = 2; }
       }
       if (i >= b.istrU - 1 && i <= b.iend) {
-        if (b.south_edge && j == b.jstr - 1 && in(i, b.jstr)) { T.zn[q] = T.zn[L(i, b.jstr)] * LD(kW_rmask, ij); T.st[q] = 2; }
-        if (b.north_edge && j == b.jend + 1 && in(i, b.jend)) { T.zn[q] = T.zn[L(i, b.jend)] * LD(kW_rmask, ij); T.st[q] = 2; }
+        if (b.south_edge && j == b.jstr - 1 && in(i, b.jstr)) { T.zn[q] = T.zn[L(i, b.jstr)] * e_rm[r]; T.st[q] = 2; }
+        if (b.north_edge && j == b.jend + 1 && in(i, b.jend)) { T.zn[q] = T.zn[L(i, b.jend)] * e_rm[r]; T.st[q] = 2; }
       }
     }
     __syncthreads();
@@ -484,17 +513,20 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int vw
       if (b.north_edge && b.east_edge && in(ie + 1, je + 1) && in(ie, je + 1) && in(ie + 1, je)) { T.zn[L(ie + 1, je + 1)] = 0.5 * (T.zn[L(ie, je + 1)] + T.zn[L(ie + 1, je)]); T.st[L(ie + 1, je + 1)] = 2; }
     }
     __syncthreads();
+  }
+  if (closed == 1) {
     // the edge kernels read zeta_new / Dnew from global scratch: every block
     // stores the window cells it computed or set (identical values where
     // windows overlap); with the edges folded in (closed == 2) the block
     // reads them from its window instead
-    for (int q = tid; q < kFN && closed == 1; q += NT) {
+    for (int q = tid; q < kFN; q += NT) {
       if (!T.st[q]) continue;
       const long o = IJ(b, i0 - 1 + q % kFX, j0 - 1 + q / kFX);
       ST(kW_s0, o, T.zn[q]);
       if (T.st[q] == 1) ST(kW_s1, o, T.Dn[q]);
     }
   }
+  S2D_T(5);   // zetabc
   // P3: zeta(knew), fast averages, pressure gradient, momentum
   const int i = i0 + (int)threadIdx.x, j = j0 + (int)threadIdx.y;
   const bool pin = i >= R.i0 && i <= R.i1 && j <= R.j1;
@@ -576,7 +608,15 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int vw
       ST(kW_DV_avg1, ij, (c.iif == 1 ? 0.0 : x_DV1) + cff1 * dm_v * (DVnew));
     }
   }
-  if (closed != 2) return;
+  S2D_T(6);   // P3 stores issued
+  // the folded wall phases act on lanes of a wall's first or ghost row /
+  // column only (i = istr-1..istr, iend+1; j = jstr-1..jstr, jend+1):
+  // blocks whose tile holds none skip them and their barrier (block-uniform)
+  const bool wall_tile = (b.west_edge && b.istr >= i0 && b.istr - 1 <= i0 + kBX - 1) ||
+                         (b.east_edge && b.iend + 1 >= i0 && b.iend + 1 <= i0 + kBX - 1) ||
+                         (b.south_edge && b.jstr >= j0 && b.jstr - 1 <= j0 + kBY - 1) ||
+                         (b.north_edge && b.jend + 1 >= j0 && b.jend + 1 <= j0 + kBY - 1);
+  if (closed != 2 || !wall_tile) return;
   // ---- closed walls folded in (k_s2d_edges phases 0, 1, 3 with no open
   // edge; the host folds only when every edge cell and its interior
   // neighbour fall in one tile).  Same expressions as k_s2d_edges. ----
@@ -638,6 +678,7 @@ __global__ void __launch_bounds__(256) k_s2d_fb(Dev d, Range R, FBCoef c, int vw
     if (du) ST(kW_DU_avg1, ij, LD(kW_DU_avg1, ij) + cff1 * (Dn(q, g) + Dn(q - 1, g - 1)) * (ubn) * LD(kW_dn_u, ij));
     if (dv) ST(kW_DV_avg1, ij, LD(kW_DV_avg1, ij) + cff1 * (Dn(q, g) + Dn(q - kFX, g - kGX)) * (vbn) * LD(kW_dm_v, ij));
     (void)sj;
+    S2D_T(7);   // walls folded in
   }
 }
 
