@@ -143,6 +143,29 @@ constexpr int kSegLoadGroup = ROMS_SEG_LOAD_GROUP;
 #endif
 constexpr int kSegCoupleGroup = ROMS_SEG_COUPLE_GROUP;
 
+// 1/x in the elimination and coupling recurrences, the serial dependency
+// chain of every segment solve (one reciprocal per row): the hardware
+// reciprocal refined by two Newton steps -- 5 dependent FP64 operations
+// against the IEEE division's 10 -- agrees with 1/x to the last bit or one
+// ulp (the solvers already differ from the reference's sequential Thomas at
+// ~1e-15, k_colseg.h header); C3 pre_step3d, step3d_uv1 and step3d_t
+// 0.08-0.15 ms faster each (profiles/r6_rc_seg_rcp_ab.txt).
+// -DROMS_SEG_FASTRCP=0 builds the IEEE division.
+#ifndef ROMS_SEG_FASTRCP
+#define ROMS_SEG_FASTRCP 1
+#endif
+__device__ __forceinline__ double seg_rcp(double x) {
+#if ROMS_SEG_FASTRCP
+  double y = __builtin_amdgcn_rcp(x);
+  double e = __builtin_fma(-x, y, 1.0);
+  y = __builtin_fma(y, e, y);
+  e = __builtin_fma(-x, y, 1.0);
+  return __builtin_fma(y, e, y);
+#else
+  return 1.0 / x;
+#endif
+}
+
 template <int KR>
 struct SegTri {
   double C[KR], D[KR], E[KR];
@@ -155,7 +178,7 @@ struct SegTri {
     for (int q = 0; q < KR; q++) {
       double a, b, c, d;
       row(q, a, b, c, d);
-      const double rm = 1.0 / (b - a * Cp);
+      const double rm = seg_rcp(b - a * Cp);
       const double Cq = c * rm, Dq = (d - a * Dp) * rm, Eq = -a * Ep * rm;
       const bool live = seg_live(q, n);
       C[q] = live ? Cq : 0.0;
@@ -196,7 +219,7 @@ struct SegTri {
       if (t < S) {
         const double yf = X.v[0][t][l], af = X.v[1][t][l], bf = X.v[2][t][l];
         const double yL = X.v[3][t][l], aL = X.v[4][t][l], bL = X.v[5][t][l];
-        const double rden = 1.0 / (1.0 - af * Qp);
+        const double rden = seg_rcp(1.0 - af * Qp);
         const double Ut = (yf + af * Pp) * rden;
         const double Vt = bf * rden;
         Us = t == s ? Ut : Us;
