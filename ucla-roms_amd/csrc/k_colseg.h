@@ -166,6 +166,20 @@ __device__ __forceinline__ double seg_rcp(double x) {
 #endif
 }
 
+// the rows' diffusion coefficients 2 dt K / (Hz_k + Hz_k+1) (step3d_t_ISO.F
+// :1044-1065, step3d_uv1.F:146-170, pre_step3d4S.F:214-230,362-380): a times
+// seg_rcp(b), 6 instructions instead of the division's 10, within an ulp of
+// a / b; C3 pre_step3d, step3d_uv1 and step3d_t 0.05-0.07 ms faster each
+// (profiles/r6_rc_seg_rcp_ab.txt).  -DROMS_SEG_FASTDIV=0: a / b.
+#ifndef ROMS_SEG_FASTDIV
+#define ROMS_SEG_FASTDIV 1
+#endif
+#if ROMS_SEG_FASTDIV
+#define SEG_DIV(a, b) ((a) * seg_rcp(b))
+#else
+#define SEG_DIV(a, b) ((a) / (b))
+#endif
+
 template <int KR>
 struct SegTri {
   double C[KR], D[KR], E[KR];

@@ -737,7 +737,7 @@ __global__ void __launch_bounds__(kSegBlock, 2) k_pre_tracer_seg(Dev d, Range R,
     const long w = (long)min(max(r, 1), N - 1) * n2;
     const bool in = r > 0 && r < N;
     const int qa = q + 1 < KR + 1 ? q + 1 : KR;
-    const double f = 2.0 * c.dtau * Akt[w] / (hz[qa] + hz[q]);
+    const double f = SEG_DIV(2.0 * c.dtau * Akt[w], hz[qa] + hz[q]);
     const double wv = DC0 * Wi[w];
     fc = in ? f : 0.0;
     wc = in ? wv : 0.0;
@@ -839,7 +839,7 @@ __global__ void __launch_bounds__(kSegBlock, ROMS_PRE_T_SEG_WAVES) k_pre_tracer_
     const unsigned w = wlev(r);
     const bool in = r > 0 && r < N;
     const int qa = q + 1 < KR + 1 ? q + 1 : KR;
-    const double f = 2.0 * c.dtau * LD(Akt, vo, w) / (hz[qa] + hz[q]);
+    const double f = SEG_DIV(2.0 * c.dtau * LD(Akt, vo, w), hz[qa] + hz[q]);
     const double wv = DC0 * LD(Wi, vo, w);
     fc = in ? f : 0.0;
     wc = in ? wv : 0.0;
@@ -945,7 +945,7 @@ __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_pre_uv_seg(Dev d, R
     const long w = (long)min(max(r, 1), N - 1) * n2;
     const bool in = r > 0 && r < N;
     const int qa = q + 1 < KR + 1 ? q + 1 : KR;
-    const double f = 2.0 * c.dtau * (Akv[w] + Akv[w - s]) / (hf[qa] + hfm[qa] + hf[q] + hfm[q]);
+    const double f = SEG_DIV(2.0 * c.dtau * (Akv[w] + Akv[w - s]), hf[qa] + hfm[qa] + hf[q] + hfm[q]);
     const double wv = DC0 * 0.5 * (Wi[w] + Wi[w - s]);
     fc = in ? f : 0.0;
     wc = in ? wv : 0.0;
@@ -1063,7 +1063,7 @@ __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_pre_uv_segb(Dev d, 
     const unsigned w = (unsigned)min(max(r, 1), N - 1) * lv;
     const bool in = r > 0 && r < N;
     const int qa = q + 1 < KR + 1 ? q + 1 : KR;
-    const double f = 2.0 * c.dtau * (LD(Akv, vo, w) + LD(Akv, vm, w)) / (hf[qa] + hfm[qa] + hf[q] + hfm[q]);
+    const double f = SEG_DIV(2.0 * c.dtau * (LD(Akv, vo, w) + LD(Akv, vm, w)), hf[qa] + hfm[qa] + hf[q] + hfm[q]);
     const double wv = DC0 * 0.5 * (LD(Wi, vo, w) + LD(Wi, vm, w));
     fc = in ? f : 0.0;
     wc = in ? wv : 0.0;

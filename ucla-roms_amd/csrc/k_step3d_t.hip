@@ -338,7 +338,7 @@ __global__ void __launch_bounds__(kSegBlock, 2) k_step3d_t_seg(Dev d, Range R, i
     const long w = (long)min(max(r, 1), N - 1) * n2;
     const bool in = r > 0 && r < N;
     const int qa = q + 1 < KR + 1 ? q + 1 : KR;
-    const double f = 2.0 * dt * Akt[w] / (hz[q] + hz[qa]);
+    const double f = SEG_DIV(2.0 * dt * Akt[w], hz[q] + hz[qa]);
     const double c = DC0 * Wi[w];
     fc = in ? f : 0.0;
     wc = in ? c : 0.0;
@@ -524,7 +524,7 @@ __global__ void __launch_bounds__(kSegBlock, ROMS_T_SEG_WAVES) k_step3d_t_segb(D
     const unsigned w = wlev(r, 1, N - 1);
     const bool in = r > 0 && r < N;
     const int qa = q + 1 < KR + 1 ? q + 1 : KR;
-    const double f = 2.0 * dt * LD(Akt, vo, w) / (hz[q] + hz[qa]);
+    const double f = SEG_DIV(2.0 * dt * LD(Akt, vo, w), hz[q] + hz[qa]);
     const double c = DC0 * LD(Wi, vo, w);
     fc = in ? f : 0.0;
     wc = in ? c : 0.0;

@@ -340,7 +340,7 @@ __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_uv1_seg(Dev d, Rang
     const long w = (long)min(max(r, 1), N - 1) * n2;
     const bool in = r > 0 && r < N;
     const int qa = q + 1 < KR + 1 ? q + 1 : KR;
-    const double f = 2.0 * dt * (Akv[w] + Akv[w - s]) / (HZ(qa) + HZM(qa) + HZ(q) + HZM(q));
+    const double f = SEG_DIV(2.0 * dt * (Akv[w] + Akv[w - s]), HZ(qa) + HZM(qa) + HZ(q) + HZM(q));
     const double wv = DC0 * 0.5 * (Wi[w] + Wi[w - s]);
     fc = in ? f : 0.0;
     wc = in ? wv : 0.0;
@@ -470,7 +470,7 @@ __global__ void __launch_bounds__(kSegBlock * kSegJMax, 2) k_uv1_segb(Dev d, Ran
     const unsigned w = (unsigned)min(max(r, 1), N - 1) * lv;
     const bool in = r > 0 && r < N;
     const int qa = q + 1 < KR + 1 ? q + 1 : KR;
-    const double f = 2.0 * dt * (LD(Akv, vo, w) + LD(Akv, vm, w)) / (HZ(qa) + HZM(qa) + HZ(q) + HZM(q));
+    const double f = SEG_DIV(2.0 * dt * (LD(Akv, vo, w) + LD(Akv, vm, w)), HZ(qa) + HZM(qa) + HZ(q) + HZM(q));
     const double wv = DC0 * 0.5 * (LD(Wi, vo, w) + LD(Wi, vm, w));
     fc = in ? f : 0.0;
     wc = in ? wv : 0.0;
