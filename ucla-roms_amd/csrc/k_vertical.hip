@@ -835,8 +835,11 @@ __global__ void __launch_bounds__(256) k_rho_eos_linear(Dev d, Range R, int tidx
 #ifndef ROMS_RHO_PF
 #define ROMS_RHO_PF 4
 #endif
+#ifndef ROMS_RHO_MINW   // minimum waves per SIMD of k_rho_eos_split (VGPR cap; A/B builds)
+#define ROMS_RHO_MINW 1
+#endif
 template <bool kP>
-__global__ void __launch_bounds__(256) k_rho_eos_split(Dev d, Range R, int tidx) {
+__global__ void __launch_bounds__(256, ROMS_RHO_MINW) k_rho_eos_split(Dev d, Range R, int tidx) {
   ROMS_IJ_OR_RETURN(R)
   const Bounds& b = d.b;
   const Fields& F = d.f;
